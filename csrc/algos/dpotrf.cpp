@@ -1,0 +1,292 @@
+// Tiled Cholesky (lower) as a PTG taskpool: POTRF / TRSM / SYRK / GEMM.
+// The same DAG ships as a .jdf (algos/jdf/dpotrf_L.jdf, compiled by ptgpp); this
+// hand-built IR is what the compiler emits, kept here as the reference form.
+//
+//  POTRF(k)    k = 0..NT-1            : A(k,k)   T <- k==0 ? A(k,k) : T SYRK(k-1,k)
+//  TRSM(m,k)   k = 0..NT-2, m = k+1.. : A(m,k)   T <- T POTRF(k);  C <- k==0 ? A(m,k) : C GEMM(m,k,k-1)
+//  SYRK(k,m)   k = 0..NT-2, m = k+1.. : A(m,m)   A <- C TRSM(m,k); T <- k==0 ? A(m,m) : T SYRK(k-1,m)
+//  GEMM(m,n,k) k = 0..NT-3, m = k+2.., n = k+1..m-1 : A(m,n)
+//
+// GPU bodies enqueue descriptors into the device engine's per-round batch, so all
+// GEMM/SYRK tiles ready in a round run as ONE grouped MFMA launch; POTRF/TRSM and
+// the SYRK/GEMM feeding the next panel are routed to the high-priority stream.
+#include <cmath>
+#include <cstring>
+
+#include "../device/device.hpp"
+#include "linalg.hpp"
+
+namespace parsec {
+namespace algos {
+
+using namespace ptg;
+
+// ----------------------------------------------------------- IR helpers
+static LocalDef range_local(const std::string& n, Expr lo, Expr hi) {
+  LocalDef l;
+  l.name = n; l.is_range = true; l.is_param = true; l.lo = std::move(lo); l.hi = std::move(hi);
+  return l;
+}
+static Expr cst(int64_t v) { return [v](const Taskpool*, const int32_t*) { return v; }; }
+static Expr loc(int i) { return [i](const Taskpool*, const int32_t* L) { return (int64_t)L[i]; }; }
+static Expr locp(int i, int64_t d) { return [i, d](const Taskpool*, const int32_t* L) { return (int64_t)L[i] + d; }; }
+static CallArg val(Expr e) { CallArg a; a.value = std::move(e); return a; }
+static CallArg rng(Expr lo, Expr hi) { CallArg a; a.is_range = true; a.lo = std::move(lo); a.hi = std::move(hi); return a; }
+static DepTarget task(const std::string& tc, const std::string& flow, std::vector<CallArg> args) {
+  DepTarget t; t.kind = DEP_TASK; t.tc_name = tc; t.flow_name = flow; t.args = std::move(args); return t;
+}
+static DepTarget data(TiledMatrix* A, Expr m, Expr n) {
+  DepTarget t; t.kind = DEP_DATA; t.dc = [A](const Taskpool*) { return (DataCollection*)A; }; t.args = {val(std::move(m)), val(std::move(n))}; return t;
+}
+static Dep always(DepTarget t) { Dep d; d.then_t = std::move(t); return d; }
+static Dep cond(Guard g, DepTarget a, DepTarget b) { Dep d; d.guard = std::move(g); d.then_t = std::move(a); d.has_else = true; d.else_t = std::move(b); return d; }
+static Dep when(Guard g, DepTarget a) { Dep d; d.guard = std::move(g); d.then_t = std::move(a); return d; }
+
+static inline double* fptr(Task* t, int f) { return t->data[f].data_in ? static_cast<double*>(t->data[f].data_in->device_private) : nullptr; }
+
+// ------------------------------------------------------ CPU reference bodies
+static int cpu_potrf(double* A, int n, int lda) {
+  for (int j = 0; j < n; ++j) {
+    double d = A[j + (size_t)j * lda];
+    for (int k = 0; k < j; ++k) d -= A[j + (size_t)k * lda] * A[j + (size_t)k * lda];
+    if (d <= 0) return j + 1;
+    d = std::sqrt(d);
+    A[j + (size_t)j * lda] = d;
+    for (int i = j + 1; i < n; ++i) {
+      double s = A[i + (size_t)j * lda];
+      for (int k = 0; k < j; ++k) s -= A[i + (size_t)k * lda] * A[j + (size_t)k * lda];
+      A[i + (size_t)j * lda] = s / d;
+    }
+  }
+  return 0;
+}
+// B (m x n) := B L^-T
+static void cpu_trsm(const double* L, int ldl, double* B, int m, int n, int ldb) {
+  for (int j = 0; j < n; ++j) {
+    double d = L[j + (size_t)j * ldl];
+    for (int i = 0; i < m; ++i) B[i + (size_t)j * ldb] /= d;
+    for (int k = j + 1; k < n; ++k) {
+      double l = L[k + (size_t)j * ldl];
+      for (int i = 0; i < m; ++i) B[i + (size_t)k * ldb] -= B[i + (size_t)j * ldb] * l;
+    }
+  }
+}
+// C (m x n) += alpha A B^T (lower_only: i >= j)
+static void cpu_gemm_nt(double alpha, const double* A, int lda, const double* B, int ldb, double* C, int ldc, int m, int n, int k, bool lower) {
+  for (int j = 0; j < n; ++j)
+    for (int p = 0; p < k; ++p) {
+      double b = alpha * B[j + (size_t)p * ldb];
+      for (int i = lower ? j : 0; i < m; ++i) C[i + (size_t)j * ldc] += A[i + (size_t)p * lda] * b;
+    }
+}
+
+class DpotrfTaskpool : public PtgTaskpool {
+ public:
+  int* info_host = nullptr;
+  int* info_dev = nullptr;
+  int info_dev_index = -1;
+  std::atomic<int> info_cpu{0};
+  void on_complete_internal() override {
+    int v = info_cpu.load();
+    if (info_dev) {
+      int dv = 0;
+      device_memcpy(0, &dv, info_dev_index, info_dev, sizeof(int));
+      if (dv && (!v || dv < v)) v = dv;
+    }
+    if (info_host) *info_host = v;
+  }
+  ~DpotrfTaskpool() override {
+    if (info_dev) device_free(info_dev_index, info_dev);
+  }
+};
+
+ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
+  if (uplo != MATRIX_LOWER) fatal("dpotrf: only the lower factorization is implemented (uplo=%d)", uplo);
+  auto* tp = new DpotrfTaskpool();
+  tp->taskpool_name = "dpotrf_L";
+  tp->info_host = info_host;
+  if (info_host) *info_host = 0;
+  int gpu = first_gpu_device_index();
+  if (gpu >= 0) {
+    tp->info_dev = static_cast<int*>(device_alloc(gpu, sizeof(int)));
+    tp->info_dev_index = gpu;
+  }
+  const int64_t NT = A->nt;
+  const int64_t nb = A->nb;
+  auto nt1 = cst(NT - 1);
+  auto ntm2 = cst(NT - 2);
+  auto rows = [A](int64_t m) { return (int)A->tile_rows(m); };
+  auto cols = [A](int64_t n) { return (int)A->tile_cols(n); };
+  const int64_t ld = A->mb;
+  auto prio = [NT](int64_t v) { return (int64_t)((NT - v) * (NT - v) * (NT - v)); };
+  int* info_dev = tp->info_dev;
+  DpotrfTaskpool* self = tp;
+
+  // ---------------------------------------------------------------- POTRF(k)
+  {
+    TaskClassDef d;
+    d.name = "POTRF";
+    d.locals = {range_local("k", cst(0), nt1)};
+    d.affinity_dc = [A](const Taskpool*) { return (DataCollection*)A; };
+    d.affinity_args = {loc(0), loc(0)};
+    d.priority = [prio](const Taskpool*, const int32_t* L) { return prio(L[0]) + ((int64_t)1 << 30); };
+    d.flags = TC_HIGH_PRIORITY;
+    FlowDef T;
+    T.name = "T"; T.access = FLOW_RW;
+    T.in = {cond([](const Taskpool*, const int32_t* L) { return L[0] == 0; }, data(A, loc(0), loc(0)), task("SYRK", "T", {val(locp(0, -1)), val(loc(0))}))};
+    T.out = {always(task("TRSM", "T", {rng(locp(0, 1), nt1), val(loc(0))})), always(data(A, loc(0), loc(0)))};
+    d.flows = {T};
+    BodyDef g;
+    g.type = DEV_HIP;
+    g.gpu = [rows, ld, info_dev](GpuExecContext* c, Task* t) {
+      int k = t->locals[0];
+      c->batch->potrf.push_back(PotrfDesc{static_cast<double*>(c->ptr(0)), rows(k), (int)ld, info_dev});
+      return HOOK_DONE;
+    };
+    BodyDef cpu;
+    cpu.type = DEV_CPU;
+    cpu.cpu = [rows, ld, self](ExecutionStream*, Task* t) {
+      int k = t->locals[0];
+      int info = cpu_potrf(fptr(t, 0), rows(k), (int)ld);
+      if (info) { int exp = 0; self->info_cpu.compare_exchange_strong(exp, (int)(k * ld + info)); }
+      return HOOK_DONE;
+    };
+    d.bodies = {g, cpu};
+    d.flops = (double)nb * nb * nb / 3.0;
+    tp->add_task_class(std::move(d));
+  }
+  // ------------------------------------------------------------- TRSM(m,k)
+  {
+    TaskClassDef d;
+    d.name = "TRSM";
+    d.locals = {range_local("k", cst(0), ntm2), range_local("m", locp(0, 1), nt1)};
+    d.params = {"m", "k"};
+    d.affinity_dc = [A](const Taskpool*) { return (DataCollection*)A; };
+    d.affinity_args = {loc(1), loc(0)};
+    d.priority = [prio, NT](const Taskpool*, const int32_t* L) { int64_t k = L[0], m = L[1]; return prio(m) + 3 * ((2 * NT) - k - m - 1) * (m - k) + (m == k + 1 ? (int64_t)1 << 28 : 0); };
+    d.flags = TC_HIGH_PRIORITY;
+    FlowDef T;
+    T.name = "T"; T.access = FLOW_READ;
+    T.in = {always(task("POTRF", "T", {val(loc(0))}))};
+    FlowDef C;
+    C.name = "C"; C.access = FLOW_RW;
+    C.in = {cond([](const Taskpool*, const int32_t* L) { return L[0] == 0; }, data(A, loc(1), loc(0)), task("GEMM", "C", {val(loc(1)), val(loc(0)), val(locp(0, -1))}))};
+    C.out = {always(task("SYRK", "A", {val(loc(0)), val(loc(1))})),
+             always(task("GEMM", "A", {val(loc(1)), rng(locp(0, 1), locp(1, -1)), val(loc(0))})),
+             always(task("GEMM", "B", {rng(locp(1, 1), nt1), val(loc(1)), val(loc(0))})),
+             always(data(A, loc(1), loc(0)))};
+    d.flows = {T, C};
+    BodyDef g;
+    g.type = DEV_HIP;
+    g.gpu = [rows, cols, ld](GpuExecContext* c, Task* t) {
+      int k = t->locals[0], m = t->locals[1];
+      TrsmDesc td;
+      td.L = static_cast<double*>(c->ptr(0));
+      td.B = static_cast<double*>(c->ptr(1));
+      td.m = rows(m); td.n = cols(k); td.ldl = (int)ld; td.ldb = (int)ld; td.trans = 1;
+      c->batch->trsm.push_back(td);
+      return HOOK_DONE;
+    };
+    BodyDef cpu;
+    cpu.type = DEV_CPU;
+    cpu.cpu = [rows, cols, ld](ExecutionStream*, Task* t) {
+      int k = t->locals[0], m = t->locals[1];
+      cpu_trsm(fptr(t, 0), (int)ld, fptr(t, 1), rows(m), cols(k), (int)ld);
+      return HOOK_DONE;
+    };
+    d.bodies = {g, cpu};
+    d.flops = (double)nb * nb * nb;
+    tp->add_task_class(std::move(d));
+  }
+  // ------------------------------------------------------------- SYRK(k,m)
+  {
+    TaskClassDef d;
+    d.name = "SYRK";
+    d.locals = {range_local("k", cst(0), ntm2), range_local("m", locp(0, 1), nt1)};
+    d.params = {"k", "m"};
+    d.affinity_dc = [A](const Taskpool*) { return (DataCollection*)A; };
+    d.affinity_args = {loc(1), loc(1)};
+    d.priority = [prio](const Taskpool*, const int32_t* L) { int64_t k = L[0], m = L[1]; return prio(m) + 3 * (m - k) + (m == k + 1 ? (int64_t)1 << 28 : 0); };
+    FlowDef Af;
+    Af.name = "A"; Af.access = FLOW_READ;
+    Af.in = {always(task("TRSM", "C", {val(loc(1)), val(loc(0))}))};
+    FlowDef T;
+    T.name = "T"; T.access = FLOW_RW;
+    T.in = {cond([](const Taskpool*, const int32_t* L) { return L[0] == 0; }, data(A, loc(1), loc(1)), task("SYRK", "T", {val(locp(0, -1)), val(loc(1))}))};
+    T.out = {cond([](const Taskpool*, const int32_t* L) { return L[1] == L[0] + 1; }, task("POTRF", "T", {val(loc(1))}), task("SYRK", "T", {val(locp(0, 1)), val(loc(1))}))};
+    d.flows = {Af, T};
+    BodyDef g;
+    g.type = DEV_HIP;
+    g.gpu = [rows, cols, ld](GpuExecContext* c, Task* t) {
+      int k = t->locals[0], m = t->locals[1];
+      GemmDesc gd;
+      gd.A = static_cast<double*>(c->ptr(0)); gd.B = gd.A; gd.C = static_cast<double*>(c->ptr(1));
+      gd.m = rows(m); gd.n = rows(m); gd.k = cols(k);
+      gd.lda = gd.ldb = gd.ldc = (int)ld;
+      gd.alpha = -1.0; gd.beta = 1.0; gd.transA = 0; gd.transB = 1; gd.lower_only = 1; gd.pad = 0;
+      c->batch->gemm.push_back(gd);
+      return HOOK_DONE;
+    };
+    BodyDef cpu;
+    cpu.type = DEV_CPU;
+    cpu.cpu = [rows, cols, ld](ExecutionStream*, Task* t) {
+      int k = t->locals[0], m = t->locals[1];
+      cpu_gemm_nt(-1.0, fptr(t, 0), (int)ld, fptr(t, 0), (int)ld, fptr(t, 1), (int)ld, rows(m), rows(m), cols(k), true);
+      return HOOK_DONE;
+    };
+    d.bodies = {g, cpu};
+    d.flops = (double)nb * nb * nb;
+    tp->add_task_class(std::move(d));
+  }
+  // ----------------------------------------------------------- GEMM(m,n,k)
+  {
+    TaskClassDef d;
+    d.name = "GEMM";
+    d.locals = {range_local("k", cst(0), cst(NT - 3)), range_local("m", locp(0, 2), nt1), range_local("n", locp(0, 1), locp(1, -1))};
+    d.params = {"m", "n", "k"};
+    d.affinity_dc = [A](const Taskpool*) { return (DataCollection*)A; };
+    d.affinity_args = {loc(1), loc(2)};
+    d.priority = [prio, NT](const Taskpool*, const int32_t* L) {
+      int64_t k = L[0], m = L[1], n = L[2];
+      return prio(m) + 3 * ((2 * NT) - m - n - 3) * (m - n) + 6 * (m - k) + (n == k + 1 ? (int64_t)1 << 27 : 0);
+    };
+    FlowDef Af;
+    Af.name = "A"; Af.access = FLOW_READ;
+    Af.in = {always(task("TRSM", "C", {val(loc(1)), val(loc(0))}))};
+    FlowDef Bf;
+    Bf.name = "B"; Bf.access = FLOW_READ;
+    Bf.in = {always(task("TRSM", "C", {val(loc(2)), val(loc(0))}))};
+    FlowDef C;
+    C.name = "C"; C.access = FLOW_RW;
+    C.in = {cond([](const Taskpool*, const int32_t* L) { return L[0] == 0; }, data(A, loc(1), loc(2)), task("GEMM", "C", {val(loc(1)), val(loc(2)), val(locp(0, -1))}))};
+    C.out = {cond([](const Taskpool*, const int32_t* L) { return L[2] == L[0] + 1; }, task("TRSM", "C", {val(loc(1)), val(loc(2))}), task("GEMM", "C", {val(loc(1)), val(loc(2)), val(locp(0, 1))}))};
+    d.flows = {Af, Bf, C};
+    BodyDef g;
+    g.type = DEV_HIP;
+    g.gpu = [rows, cols, ld](GpuExecContext* c, Task* t) {
+      int k = t->locals[0], m = t->locals[1], n = t->locals[2];
+      GemmDesc gd;
+      gd.A = static_cast<double*>(c->ptr(0)); gd.B = static_cast<double*>(c->ptr(1)); gd.C = static_cast<double*>(c->ptr(2));
+      gd.m = rows(m); gd.n = rows(n); gd.k = cols(k);
+      gd.lda = gd.ldb = gd.ldc = (int)ld;
+      gd.alpha = -1.0; gd.beta = 1.0; gd.transA = 0; gd.transB = 1; gd.lower_only = 0; gd.pad = 0;
+      c->batch->gemm.push_back(gd);
+      return HOOK_DONE;
+    };
+    BodyDef cpu;
+    cpu.type = DEV_CPU;
+    cpu.cpu = [rows, cols, ld](ExecutionStream*, Task* t) {
+      int k = t->locals[0], m = t->locals[1], n = t->locals[2];
+      cpu_gemm_nt(-1.0, fptr(t, 0), (int)ld, fptr(t, 1), (int)ld, fptr(t, 2), (int)ld, rows(m), rows(n), cols(k), false);
+      return HOOK_DONE;
+    };
+    d.bodies = {g, cpu};
+    d.flops = 2.0 * nb * nb * nb;
+    tp->add_task_class(std::move(d));
+  }
+  tp->finalize();
+  return tp;
+}
+
+}  // namespace algos
+}  // namespace parsec

@@ -1,0 +1,29 @@
+// Dense tiled linear-algebra taskpools (the workloads named in BASELINE.json).
+// The reference keeps these in DPLASMA (CHANGELOG.md:82-84); they are part of
+// this framework so the benchmark runs end to end.
+#pragma once
+#include "../data/collections.hpp"
+#include "../ptg/ptg.hpp"
+
+namespace parsec {
+namespace algos {
+
+// Tiled Cholesky A = L L^T (lower) on a (Sym)BlockCyclic collection, PTG form.
+// `info_host` receives the LAPACK-style info after completion (0 = success).
+ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host);
+// Tiled GEMM C = alpha op(A) op(B) + beta C (PTG; B transposed if transB).
+ptg::PtgTaskpool* dgemm_new(double alpha, TiledMatrix* A, TiledMatrix* B, double beta, TiledMatrix* C, int transB);
+// Tiled QR A = QR (Householder, tile algorithm GEQRT/TSQRT/UNMQR/TSMQR). T holds
+// the block reflectors (ib x nb per tile).
+ptg::PtgTaskpool* dgeqrf_new(TiledMatrix* A, TiledMatrix* T, int ib);
+// Collection operators (reference data_dist/matrix/apply.jdf, map_operator.c, reduce*.jdf)
+using TileOp = std::function<void(TiledMatrix*, int64_t m, int64_t n, void* tile, void* arg)>;
+ptg::PtgTaskpool* apply_new(TiledMatrix* A, int uplo, TileOp op, void* arg);
+ptg::PtgTaskpool* map_operator_new(TiledMatrix* src, TiledMatrix* dst, TileOp op, void* arg);
+ptg::PtgTaskpool* reduce_col_new(TiledMatrix* A, TiledMatrix* res, std::function<void(const void* in, void* inout, int64_t rows, int64_t cols)> op);
+ptg::PtgTaskpool* reduce_row_new(TiledMatrix* A, TiledMatrix* res, std::function<void(const void* in, void* inout, int64_t rows, int64_t cols)> op);
+ptg::PtgTaskpool* broadcast_new(TiledMatrix* A, int64_t root_m, int64_t root_n, TiledMatrix* dst);
+ptg::PtgTaskpool* redistribute_new(TiledMatrix* src, TiledMatrix* dst, int64_t size_row, int64_t size_col, int64_t disi_src, int64_t disj_src, int64_t disi_dst, int64_t disj_dst);
+
+}  // namespace algos
+}  // namespace parsec

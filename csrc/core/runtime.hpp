@@ -1,0 +1,572 @@
+// Internal runtime model of parsec-amd: tasks, task classes, taskpools,
+// execution streams, virtual processes, context, and the plug-in interfaces
+// (scheduler, termination detection, devices) plus the data layer.
+//
+// Behavioural parity (reference, read-only):
+//   task/taskpool/task-class model     parsec/parsec_internal.h:119-161,381-425,503-515
+//   hook return codes                  parsec/runtime.h:139-147
+//   task status order                  parsec/parsec_internal.h:464-469
+//   action mask bits                   parsec/remote_dep.h:30-39
+//   scheduler module vtable            parsec/mca/sched/sched.h:325-332
+//   termdet module vtable              parsec/mca/termdet/termdet.h:305-320
+//   device module vtable               parsec/mca/device/device.h:115-148
+//   data / data copy coherency         parsec/data_internal.h:35-95, data.c:287-433
+// The layout is a fresh C++20 design: virtual interfaces instead of C
+// function-pointer tables, refcounted data copies instead of data repositories
+// on the hot path, and a device model where each GPU is an execution stream
+// with its own manager thread (see device/hip_device.cpp).
+#pragma once
+#include <array>
+#include <atomic>
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "base.hpp"
+#include "mca.hpp"
+
+namespace parsec {
+
+constexpr int kMaxLocals = 20;   // reference MAX_LOCAL_COUNT
+constexpr int kMaxFlows = 20;    // MAX_DEP_IN_COUNT + MAX_DEP_OUT_COUNT
+constexpr int kMaxDevices = 16;
+constexpr int kMaxThreadSlots = 512;
+
+enum HookReturn : int { HOOK_DONE = 0, HOOK_AGAIN = -1, HOOK_NEXT = -2, HOOK_DISABLE = -3, HOOK_ASYNC = -4, HOOK_ERROR = -5 };
+
+enum DeviceType : uint32_t {
+  DEV_NONE = 0x00, DEV_CPU = 0x01, DEV_RECURSIVE = 0x02, DEV_CUDA = 0x04, DEV_INTEL_PHI = 0x08,
+  DEV_OPENCL = 0x10, DEV_TEMPLATE = 0x20, DEV_HIP = 0x40, DEV_ALL = 0xff,
+};
+constexpr uint32_t DEV_GPU_MASK = DEV_CUDA | DEV_HIP;
+
+enum FlowAccess : uint8_t { FLOW_NONE = 0, FLOW_READ = 1, FLOW_WRITE = 2, FLOW_RW = 3, FLOW_CTL = 4 };
+
+enum TaskStatus : uint8_t { STATUS_NONE = 0, STATUS_PREPARE_INPUT, STATUS_EVAL, STATUS_HOOK, STATUS_PREPARE_OUTPUT, STATUS_COMPLETE };
+
+enum : uint32_t {
+  ACTION_DEPS_MASK = 0x00FFFFFFu,
+  ACTION_RELEASE_LOCAL_DEPS = 0x01000000u,
+  ACTION_RELEASE_LOCAL_REFS = 0x02000000u,
+  ACTION_GET_REPO_ENTRY = 0x04000000u,
+  ACTION_RESHAPE_ON_RELEASE = 0x08000000u,
+  ACTION_SEND_INIT_REMOTE_DEPS = 0x10000000u,
+  ACTION_SEND_REMOTE_DEPS = 0x20000000u,
+  ACTION_RECV_INIT_REMOTE_DEPS = 0x40000000u,
+  ACTION_RESHAPE_REMOTE_ON_RELEASE = 0x80000000u,
+  ACTION_RELEASE_REMOTE_DEPS = ACTION_SEND_INIT_REMOTE_DEPS | ACTION_SEND_REMOTE_DEPS,
+};
+
+struct Context;
+struct ExecutionStream;
+struct VirtualProcess;
+struct Taskpool;
+struct TaskClass;
+struct Task;
+struct Data;
+struct DataCopy;
+struct DataCollection;
+struct Arena;
+struct Device;
+struct Scheduler;
+struct TermdetModule;
+struct RemoteDeps;
+struct GpuTask;
+struct GpuExecContext;
+
+// ===================================================================== data
+enum Coherency : uint8_t { COHERENCY_INVALID = 0, COHERENCY_OWNED = 1, COHERENCY_EXCLUSIVE = 2, COHERENCY_SHARED = 4 };
+enum TransferStatus : uint8_t { TRANSFER_NOT = 0, TRANSFER_UNDER = 1, TRANSFER_COMPLETE = 2 };
+enum DataFlags : uint8_t { DATA_FLAG_ARENA = 0x1, DATA_FLAG_TRANSIT = 0x2, DATA_FLAG_PARSEC_MANAGED = 0x4, DATA_FLAG_PARSEC_OWNED = 0x8 };
+
+// Datatype: a typed, possibly strided layout. Replaces MPI datatypes of the
+// reference (datatype.h:14-130): contiguous, vector (count x blocklen, stride),
+// lower/upper triangles of a column-major tile, indexed.
+struct Datatype {
+  enum Kind : uint8_t { NONE = 0, CONTIGUOUS, VECTOR, LOWER, UPPER, INDEXED } kind = NONE;
+  uint32_t elem_size = 1;   // bytes per element
+  int64_t count = 0;        // CONTIGUOUS: elements; VECTOR: number of blocks; LOWER/UPPER: n (square)
+  int64_t blocklen = 0;     // VECTOR: elements per block
+  int64_t stride = 0;       // VECTOR / LOWER / UPPER: leading dimension in elements
+  bool diag = true;         // LOWER/UPPER: include the diagonal
+  std::vector<std::pair<int64_t, int64_t>> blocks;  // INDEXED: (offset elems, length elems)
+  int64_t packed_bytes() const;
+  int64_t extent_bytes() const;
+  void pack(const void* src, void* dst) const;    // gather layout -> contiguous
+  void unpack(const void* src, void* dst) const;  // scatter contiguous -> layout
+  bool operator==(const Datatype& o) const;
+  static Datatype contiguous(uint32_t esz, int64_t n) { Datatype d; d.kind = CONTIGUOUS; d.elem_size = esz; d.count = n; return d; }
+  static Datatype vector(uint32_t esz, int64_t count, int64_t blocklen, int64_t stride) { Datatype d; d.kind = VECTOR; d.elem_size = esz; d.count = count; d.blocklen = blocklen; d.stride = stride; return d; }
+  static Datatype lower(uint32_t esz, int64_t n, int64_t ld, bool diag = true) { Datatype d; d.kind = LOWER; d.elem_size = esz; d.count = n; d.stride = ld; d.diag = diag; return d; }
+  static Datatype upper(uint32_t esz, int64_t n, int64_t ld, bool diag = true) { Datatype d; d.kind = UPPER; d.elem_size = esz; d.count = n; d.stride = ld; d.diag = diag; return d; }
+};
+
+struct DataCopy : ListItem {  // ListItem: membership in a device LRU
+  std::atomic<int32_t> refcount{1};
+  Data* original = nullptr;
+  DataCopy* older = nullptr;
+  int8_t device_index = 0;
+  uint8_t flags = 0;
+  uint8_t coherency_state = COHERENCY_INVALID;
+  uint8_t transfer_status = TRANSFER_NOT;
+  std::atomic<int32_t> readers{0};
+  uint32_t version = 0;
+  void* device_private = nullptr;  // pointer to the bytes on device_index
+  Arena* arena = nullptr;          // set when allocated from an arena
+  Datatype dtt;
+  void* push_task = nullptr;       // GPU task currently staging this copy
+  void* dev_state = nullptr;       // device module private (events, LRU owner)
+  void* ptr() const { return device_private; }
+};
+
+struct Data {
+  std::atomic<int32_t> refcount{1};
+  SpinLock lock;
+  uint64_t key = 0;
+  DataCollection* dc = nullptr;
+  size_t nb_elts = 0;  // bytes
+  int8_t owner_device = -1;
+  int8_t preferred_device = -1;
+  std::atomic<DataCopy*> device_copies[kMaxDevices];
+  Data() { for (auto& c : device_copies) c.store(nullptr, std::memory_order_relaxed); }
+  DataCopy* copy(int dev) const { return device_copies[dev].load(std::memory_order_acquire); }
+  uint32_t newest_version() const;
+};
+
+Data* data_new();
+Data* data_create(Data** holder, DataCollection* dc, uint64_t key, void* ptr, size_t size, uint8_t flags = DATA_FLAG_PARSEC_MANAGED, int device = 0);
+void data_retain(Data* d);
+void data_release(Data* d);
+void data_destroy(Data* d);
+DataCopy* data_copy_new(Data* d, int device, void* ptr, uint8_t flags);
+void data_copy_retain(DataCopy* c);
+void data_copy_release(DataCopy* c);
+int data_copy_attach(Data* d, DataCopy* c, int device);
+int data_copy_detach(Data* d, DataCopy* c, int device);
+// Ownership / coherency protocol (reference data.c:287-433). Returns the copy
+// that must be transferred into `device` (nullptr if the local copy is current).
+DataCopy* data_start_transfer_ownership_to_copy(Data* d, int device, uint8_t access);
+void data_end_transfer_ownership_to_copy(Data* d, int device, uint8_t access);
+
+// Arena: freelist cached allocator of fixed-size typed buffers (reference arena.h:49-125).
+struct Arena {
+  size_t elem_size = 0;
+  size_t alignment = 64;
+  Datatype dtt;
+  int64_t max_used = INT64_MAX, max_cached = INT64_MAX;
+  std::atomic<int64_t> used{0}, released{0};
+  Lifo<PoolElt> freelist;
+  std::mutex chunks_m;
+  std::vector<void*> all_chunks;
+  Arena(size_t esz, size_t align, const Datatype& d);
+  ~Arena();
+  DataCopy* get_copy(Data* data, int device);   // host memory copy (device 0)
+  void* allocate();
+  void release_chunk(void* p);
+};
+
+struct ArenaDatatype {
+  std::shared_ptr<Arena> arena;
+  Datatype opaque_dtt;
+  int ht_index = 0;
+};
+void add2arena_rect(ArenaDatatype& adt, uint32_t esz, int64_t mb, int64_t nb, int64_t ld);
+void add2arena(ArenaDatatype& adt, const Datatype& dtt, size_t alignment = 64);
+
+// Data repository: entries keyed by producer task key, holding output copies
+// until `usage_limit` consumers have retrieved them (reference datarepo.h:74-150).
+struct DataRepoEntry {
+  uint64_t key = 0;
+  std::atomic<int32_t> usage_count{0};
+  std::atomic<int32_t> usage_limit{0};
+  std::atomic<int32_t> retained{0};
+  int nb_flows = 0;
+  DataCopy* data[kMaxFlows] = {};
+};
+class DataRepo {
+ public:
+  explicit DataRepo(int nb_flows) : nb_flows_(nb_flows) {}
+  ~DataRepo();
+  DataRepoEntry* lookup_and_create(uint64_t key);
+  DataRepoEntry* lookup(uint64_t key);
+  void entry_used_once(uint64_t key);
+  void entry_addto_usage_limit(uint64_t key, int32_t usage);
+  size_t size() { return map_.size(); }
+ private:
+  void maybe_free(uint64_t key, DataRepoEntry* e);
+  int nb_flows_;
+  ShardedMap<DataRepoEntry*> map_{6};
+};
+
+// ============================================================ collections
+// Data collection vtable (reference include/parsec/data_distribution.h:26-66).
+struct DataCollection {
+  uint32_t myrank = 0, nodes = 1;
+  uint64_t dc_id = 0;
+  std::string key_base = "dc";
+  Datatype default_dtt;
+  int memory_registration_status = 0;
+  virtual ~DataCollection() = default;
+  virtual uint32_t rank_of(const int64_t* idx, int n) const = 0;
+  virtual uint32_t rank_of_key(uint64_t key) const = 0;
+  virtual int32_t vpid_of(const int64_t* idx, int n) const { (void)idx; (void)n; return 0; }
+  virtual int32_t vpid_of_key(uint64_t key) const { (void)key; return 0; }
+  virtual Data* data_of(const int64_t* idx, int n) = 0;
+  virtual Data* data_of_key(uint64_t key) = 0;
+  virtual uint64_t data_key(const int64_t* idx, int n) const = 0;
+  virtual std::string key_to_string(uint64_t key) const { return key_base + "(" + std::to_string(key) + ")"; }
+  virtual int home_device() const { return 0; }  // device holding the collection's own storage
+  virtual int register_memory(Device* dev) { (void)dev; return 0; }
+  virtual int unregister_memory(Device* dev) { (void)dev; return 0; }
+  // convenience
+  uint32_t rank_of(std::initializer_list<int64_t> l) const { return rank_of(l.begin(), (int)l.size()); }
+  Data* data_of(std::initializer_list<int64_t> l) { return data_of(l.begin(), (int)l.size()); }
+};
+uint64_t dc_register_id(DataCollection* dc);
+void dc_unregister_id(uint64_t id);
+DataCollection* dc_lookup(uint64_t id);
+
+// ===================================================================== tasks
+struct TaskDataRef {
+  DataCopy* data_in = nullptr;
+  DataCopy* data_out = nullptr;
+  DataRepoEntry* source_repo_entry = nullptr;
+};
+
+enum TaskFlags : uint32_t { TASK_FLAG_REMOTE_SHADOW = 0x1, TASK_FLAG_STARTUP = 0x2, TASK_FLAG_INTERNAL = 0x4 };
+
+struct Task : PoolElt {
+  Taskpool* taskpool = nullptr;
+  const TaskClass* task_class = nullptr;
+  uint64_t key = 0;
+  int32_t priority = 0;
+  uint8_t status = STATUS_NONE;
+  int8_t chore_id = 0;
+  uint16_t nb_remote_targets = 0;
+  int32_t deps_remaining = 0;    // activations still expected (PTG counter mode)
+  uint32_t chore_mask = 0xffffffffu;
+  uint32_t flags = 0;
+  int32_t locals[kMaxLocals];
+  TaskDataRef data[kMaxFlows];
+  GpuTask* gpu = nullptr;        // GPU bookkeeping while owned by a device
+  int8_t selected_device = -1;
+  uint64_t sim_exec_date = 0;    // simulation mode (critical path)
+  uint64_t prof_event_id = 0;
+  void* user = nullptr;          // front-end private (DTD task, recursive parent, ...)
+  void* pending_events[4] = {};  // device events this task must wait on (stream-ordered release)
+  int nb_pending_events = 0;
+};
+
+struct Flow {
+  std::string name;
+  uint8_t access = FLOW_NONE;
+  uint8_t index = 0;  // slot in Task::data[]
+};
+
+using Hook = std::function<int(ExecutionStream*, Task*)>;
+using Evaluate = std::function<int(const Task*)>;  // HOOK_DONE -> runnable, HOOK_NEXT -> skip chore
+
+struct Chore {
+  uint32_t type = DEV_CPU;
+  Hook hook;                                              // CPU body
+  std::function<int(GpuExecContext*, Task*)> gpu_hook;    // GPU body (type & DEV_GPU_MASK)
+  Evaluate evaluate;
+  void* dyld_fn = nullptr;
+  std::string dyld;
+  double weight = 1.0;  // load-balancing ratio (reference BODY weight=)
+};
+
+enum TaskClassFlags : uint32_t { TC_HIGH_PRIORITY = 0x1, TC_IMMEDIATE = 0x2, TC_NO_PROFILE = 0x4, TC_COUNT_DEPS = 0x8 };
+
+// Visitor called for each successor/predecessor of a task.
+struct DepVisit {
+  const TaskClass* tc = nullptr;   // target task class (nullptr for collection / NEW / NULL)
+  const int32_t* locals = nullptr; // target locals
+  int nb_locals = 0;
+  int src_flow = -1;               // flow index in the visiting task
+  int dst_flow = -1;               // flow index in the target task
+  uint32_t rank = 0;               // target rank
+  int32_t priority = 0;
+  DataCollection* dc = nullptr;    // when the dep targets a collection
+  uint64_t dc_key = 0;
+  int datatype_index = 0;          // arena/datatype slot for the transported data
+};
+using DepVisitor = std::function<void(const DepVisit&)>;
+
+struct TaskClass {
+  std::string name;
+  uint16_t task_class_id = 0;
+  int nb_params = 0;
+  int nb_locals = 0;
+  std::vector<Flow> flows;
+  std::vector<Chore> chores;
+  uint32_t flags = 0;
+  std::vector<std::string> local_names;
+  double flops_per_task = 0;  // optional, used for device load / weights
+  virtual ~TaskClass() = default;
+  virtual uint64_t make_key(const Taskpool* tp, const int32_t* locals) const;
+  virtual std::string describe(const Task* t) const;
+  virtual int prepare_input(ExecutionStream* es, Task* t) const { (void)es; (void)t; return HOOK_DONE; }
+  virtual int prepare_output(ExecutionStream* es, Task* t) const { (void)es; (void)t; return HOOK_DONE; }
+  // Called once the body finished: release successors, write back data, free.
+  virtual int complete_execution(ExecutionStream* es, Task* t) const = 0;
+  virtual void release_task(ExecutionStream* es, Task* t) const;
+  virtual void iterate_successors(ExecutionStream* es, const Task* t, uint32_t action_mask, const DepVisitor& v) const { (void)es; (void)t; (void)action_mask; (void)v; }
+  virtual void iterate_predecessors(ExecutionStream* es, const Task* t, uint32_t action_mask, const DepVisitor& v) const { (void)es; (void)t; (void)action_mask; (void)v; }
+  virtual int64_t sim_cost(const Task* t) const { (void)t; return 1; }
+  // Device hints: data flows a GPU chore reads/writes, and flows whose result
+  // must be copied back to the host when the GPU body completes.
+  virtual uint32_t gpu_flow_mask(const Task* t) const;
+  virtual uint32_t gpu_pushout_mask(const Task* t, int device) const { (void)t; (void)device; return 0; }
+  int flow_index(const std::string& n) const { for (auto& f : flows) if (f.name == n) return f.index; return -1; }
+};
+
+// ================================================================ taskpool
+enum TermdetState : int { TERMDET_NOT_READY = 0, TERMDET_BUSY = 1, TERMDET_TERMINATED = 2 };
+
+struct Taskpool {
+  uint32_t taskpool_id = 0;
+  std::string taskpool_name = "taskpool";
+  int32_t priority = 0;
+  uint32_t devices_index_mask = 0xffffffffu;
+  Context* context = nullptr;
+  std::vector<TaskClass*> task_classes;
+  TermdetModule* tdm = nullptr;
+  // termdet bookkeeping (interpreted by the module)
+  std::atomic<int64_t> nb_tasks{0};
+  std::atomic<int64_t> nb_pending_actions{0};
+  std::atomic<int> termdet_state{TERMDET_NOT_READY};
+  void* termdet_private = nullptr;
+  std::function<int(Taskpool*)> on_complete;
+  std::function<int(Taskpool*)> on_enqueue;
+  std::string termdet_name;          // "" = context default
+  std::atomic<bool> completed{false};
+  std::vector<ArenaDatatype> arenas_datatypes;
+  // distributed
+  bool registered = false;
+  bool is_dtd = false;
+  // simulation
+  std::atomic<uint64_t> largest_simulation_date{0};
+  virtual ~Taskpool();
+  // Enumerate startup tasks into `ready` and set nb_tasks (reference startup_hook).
+  virtual void startup(Context* ctx, std::vector<Task*>& ready) = 0;
+  // Called when a remote activation for this taskpool arrives.
+  virtual void on_remote_activation(ExecutionStream* es, struct RemoteActivation& act) { (void)es; (void)act; }
+  virtual void on_complete_internal() {}
+  // Called by context_wait before waiting (DTD: closes insertion).
+  virtual void on_context_wait() {}
+  std::function<void()> destructor_hook;
+};
+
+// =============================================================== termdet
+struct TermdetModule {
+  virtual ~TermdetModule() = default;
+  virtual const char* name() const = 0;
+  virtual void monitor_taskpool(Taskpool* tp, std::function<void(Taskpool*)> on_terminated) = 0;
+  virtual void unmonitor_taskpool(Taskpool* tp) { (void)tp; }
+  virtual int taskpool_state(Taskpool* tp) { return tp->termdet_state.load(); }
+  virtual void taskpool_ready(Taskpool* tp) = 0;
+  virtual void taskpool_set_nb_tasks(Taskpool* tp, int64_t v) = 0;
+  virtual int64_t taskpool_addto_nb_tasks(Taskpool* tp, int64_t d) = 0;
+  virtual void taskpool_set_runtime_actions(Taskpool* tp, int64_t v) = 0;
+  virtual int64_t taskpool_addto_runtime_actions(Taskpool* tp, int64_t d) = 0;
+  // Message piggy-backing (fourcounter); bytes appended to activation messages.
+  virtual void outgoing_message_start(Taskpool* tp, int dst) { (void)tp; (void)dst; }
+  virtual size_t outgoing_message_pack(Taskpool* tp, int dst, uint8_t* buf, size_t cap) { (void)tp; (void)dst; (void)buf; (void)cap; return 0; }
+  virtual void incoming_message_start(Taskpool* tp, int src, const uint8_t* buf, size_t len) { (void)tp; (void)src; (void)buf; (void)len; }
+  virtual void incoming_message_end(Taskpool* tp) { (void)tp; }
+  virtual void user_trigger(Taskpool* tp) { (void)tp; }
+};
+TermdetModule* termdet_open_module(const std::string& name);
+std::vector<std::string> termdet_available();
+
+// ============================================================= scheduler
+struct Scheduler {
+  virtual ~Scheduler() = default;
+  virtual const char* name() const = 0;
+  virtual int install(Context* ctx) { (void)ctx; return 0; }
+  virtual int flow_init(ExecutionStream* es, Barrier* b) { (void)es; (void)b; return 0; }
+  // `tasks` is sorted by decreasing priority.
+  virtual int schedule(ExecutionStream* es, Task** tasks, int n, int32_t distance) = 0;
+  virtual Task* select(ExecutionStream* es, int32_t* distance) = 0;
+  virtual void display_stats(ExecutionStream* es) { (void)es; }
+  virtual void remove(Context* ctx) { (void)ctx; }
+  virtual int64_t pending_estimate(ExecutionStream* es) { (void)es; return -1; }
+};
+struct SchedulerComponent {
+  const char* name;
+  int priority;
+  const char* description;
+  std::function<Scheduler*()> factory;
+};
+const std::vector<SchedulerComponent>& scheduler_components();
+
+// ================================================= execution streams / VPs
+struct PinsChain;
+struct ProfilingStream;
+
+struct ExecutionStream {
+  int th_id = 0;          // global id in the context
+  int core_id = -1;
+  int socket_id = 0;
+  int slot = 0;           // mempool slot
+  VirtualProcess* vp = nullptr;
+  Context* ctx = nullptr;
+  Task* next_task = nullptr;
+  void* sched_obj = nullptr;
+  ProfilingStream* prof = nullptr;
+  uint32_t rand_seed = 1;
+  bool is_manager = false;  // GPU manager / comm thread (does not select tasks)
+  // statistics
+  uint64_t nb_executed = 0, nb_selected = 0, nb_stolen = 0;
+  std::vector<int> steal_order;  // other th_ids by distance (filled by vpmap)
+};
+
+struct VirtualProcess {
+  int vp_id = 0;
+  std::vector<ExecutionStream*> es;
+  void* sched_obj = nullptr;
+};
+
+// ================================================================ devices
+struct GpuExecContext;
+
+struct DeviceStats {
+  std::atomic<uint64_t> executed_tasks{0};
+  std::atomic<uint64_t> bytes_in{0}, bytes_out{0}, bytes_d2d{0};
+  std::atomic<uint64_t> data_faults{0};
+  std::atomic<uint64_t> kernel_launches{0}, batched_tasks{0};
+};
+
+struct Device {
+  std::string name;
+  uint32_t type = DEV_NONE;
+  int device_index = -1;
+  double gflops_fp64 = 1, gflops_fp32 = 1;
+  double gflops_weight = 1;  // relative weight computed at registration_complete
+  std::atomic<int64_t> load{0};
+  DeviceStats stats;
+  virtual ~Device() = default;
+  virtual int attach(Context* ctx) { (void)ctx; return 0; }
+  virtual int detach(Context* ctx) { (void)ctx; return 0; }
+  virtual int taskpool_register(Taskpool* tp) { (void)tp; return 0; }
+  virtual int taskpool_unregister(Taskpool* tp) { (void)tp; return 0; }
+  virtual int memory_register(DataCollection* dc, void* ptr, size_t len) { (void)dc; (void)ptr; (void)len; return 0; }
+  virtual int memory_unregister(DataCollection* dc, void* ptr) { (void)dc; (void)ptr; return 0; }
+  virtual void* find_function(const std::string& n) { (void)n; return nullptr; }
+  // Submit a task to the device (GPU: returns HOOK_ASYNC).
+  virtual int submit(ExecutionStream* es, Task* t, int chore) { (void)es; (void)t; (void)chore; return HOOK_NEXT; }
+  virtual void data_advise(Data* d, int advice) { (void)d; (void)advice; }
+  virtual void flush_data(Data* d) { (void)d; }
+  virtual bool is_gpu() const { return false; }
+  virtual void quiesce() {}
+};
+
+// Device registry (reference device.c): index 0 = CPU, 1 = recursive, >=2 GPUs.
+struct DeviceRegistry {
+  std::vector<Device*> devices;
+  bool frozen = false;
+  static DeviceRegistry& instance();
+  int add(Device* d);
+  Device* get(int i) { return i >= 0 && i < (int)devices.size() ? devices[i] : nullptr; }
+  int count() const { return (int)devices.size(); }
+  int nb_gpus() const;
+  void registration_complete();
+};
+int get_best_device(Task* t, double ratio);  // reference device.c:79-189
+
+// ================================================================ context
+struct CommEngine;
+struct RemoteDepEngine;
+struct Profiling;
+
+struct Context {
+  int nb_vp = 1;
+  int nb_cores = 1;          // compute threads (incl. master)
+  int my_rank = 0;
+  int nb_nodes = 1;
+  std::vector<VirtualProcess*> vps;
+  std::vector<ExecutionStream*> all_es;  // compute threads, th_id order
+  std::vector<ExecutionStream*> aux_es;  // managers / comm thread
+  Scheduler* scheduler = nullptr;
+  std::string scheduler_name;
+  std::string default_termdet = "local";
+  std::atomic<int32_t> active_taskpools{0};
+  std::atomic<bool> started{false};
+  std::atomic<bool> finalizing{false};
+  std::atomic<uint64_t> epoch{0};
+  std::mutex wake_m;
+  std::condition_variable wake_cv;
+  std::vector<std::thread> threads;
+  Barrier* barrier = nullptr;
+  std::unique_ptr<Mempool> task_mempool;
+  size_t task_size = sizeof(Task);
+  RemoteDepEngine* remote = nullptr;
+  CommEngine* comm = nullptr;
+  std::vector<std::function<void(void*)>> at_fini;
+  std::vector<void*> at_fini_data;
+  bool keep_highest_priority_task = true;
+  int comm_bcast_topology = 0;  // 0 star, 1 chain, 2 binomial
+  std::vector<int> core_bindings;
+  std::string grapher_file;     // DOT output
+  void* grapher = nullptr;
+  std::mutex tp_m;
+  std::vector<Taskpool*> taskpools_in_flight;
+  std::atomic<uint64_t> sim_date{0};
+  bool simulation = false;
+};
+
+// thread slot for mempools of non-runtime threads
+int thread_slot();
+ExecutionStream* my_execution_stream();
+void set_my_execution_stream(ExecutionStream* es);
+
+// ================================================= core engine functions
+Context* context_init(int nb_cores, std::vector<std::string>& args);
+int context_fini(Context** pctx);
+int context_add_taskpool(Context* ctx, Taskpool* tp);
+int context_start(Context* ctx);
+int context_test(Context* ctx);
+int context_wait(Context* ctx);
+void context_abort(Context* ctx, int status);
+
+Task* task_new(ExecutionStream* es, Taskpool* tp, const TaskClass* tc);
+void task_free(Task* t);
+// Push a set of ready tasks (sorted internally by priority).
+int schedule_tasks(ExecutionStream* es, Task** tasks, int n, int32_t distance);
+int schedule_task(ExecutionStream* es, Task* t, int32_t distance);
+int reschedule(ExecutionStream* es, Task* t);
+// Execute a task's body selecting among its chores (reference __parsec_execute).
+int execute_task(ExecutionStream* es, Task* t);
+int task_progress(ExecutionStream* es, Task* t, int32_t distance);
+int complete_task_execution(ExecutionStream* es, Task* t);
+void taskpool_task_done(Taskpool* tp, ExecutionStream* es);
+void worker_loop(ExecutionStream* es, bool master);
+
+// Taskpool registry (reference runtime.h:436-495).
+int taskpool_reserve_id(Taskpool* tp);
+int taskpool_register(Taskpool* tp);
+void taskpool_unregister(Taskpool* tp);
+Taskpool* taskpool_lookup(uint32_t id);
+void taskpool_sync_ids();
+int32_t taskpool_set_priority(Taskpool* tp, int32_t p);
+Taskpool* compose(Taskpool* start, Taskpool* next);
+void taskpool_free(Taskpool* tp);
+int taskpool_termination_detected(Taskpool* tp);
+
+// PINS events (reference mca/pins/pins.h:26-55)
+enum PinsEvent : int {
+  PINS_SELECT_BEGIN = 0, PINS_SELECT_END, PINS_PREPARE_INPUT_BEGIN, PINS_PREPARE_INPUT_END,
+  PINS_RELEASE_DEPS_BEGIN, PINS_RELEASE_DEPS_END, PINS_ACTIVATE_CB_BEGIN, PINS_ACTIVATE_CB_END,
+  PINS_DATA_FLUSH_BEGIN, PINS_DATA_FLUSH_END, PINS_EXEC_BEGIN, PINS_EXEC_END,
+  PINS_COMPLETE_EXEC_BEGIN, PINS_COMPLETE_EXEC_END, PINS_SCHEDULE_BEGIN, PINS_SCHEDULE_END,
+  PINS_THREAD_INIT, PINS_THREAD_FINI, PINS_NB_EVENTS
+};
+extern std::atomic<bool> g_pins_enabled;
+void pins_fire(ExecutionStream* es, int event, Task* t);
+#define PARSEC_PINS(es, ev, t) do { if (::parsec::g_pins_enabled.load(std::memory_order_relaxed)) ::parsec::pins_fire((es), (ev), (t)); } while (0)
+
+}  // namespace parsec

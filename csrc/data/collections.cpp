@@ -1,0 +1,274 @@
+#include "collections.hpp"
+
+#include <cstdlib>
+#include <cstring>
+
+#include "../device/device.hpp"
+
+namespace parsec {
+
+size_t matrix_type_size(int mtype) {
+  switch (mtype) {
+    case MATRIX_BYTE: return 1;
+    case MATRIX_INTEGER: return 4;
+    case MATRIX_FLOAT: return 4;
+    case MATRIX_DOUBLE: return 8;
+    case MATRIX_COMPLEX_FLOAT: return 8;
+    case MATRIX_COMPLEX_DOUBLE: return 16;
+  }
+  return 8;
+}
+
+// ============================================================ tiled matrix
+TiledMatrix::~TiledMatrix() {
+  for (Data*& d : tiles) if (d) { data_destroy(d); d = nullptr; }
+  if (owns_storage && mat) {
+    if (storage_device == 0) std::free(mat);
+    else device_free(storage_device, mat);
+  }
+  if (dc_id) dc_unregister_id(dc_id);
+}
+
+void TiledMatrix::init_base(int mt_, int myrank_, int nodes_, int64_t mb_, int64_t nb_, int64_t lm_, int64_t ln_, int64_t i_, int64_t j_, int64_t m_, int64_t n_) {
+  mtype = mt_;
+  elem_size = matrix_type_size(mt_);
+  myrank = (uint32_t)myrank_;
+  nodes = (uint32_t)nodes_;
+  mb = mb_; nb = nb_; lm = lm_; ln = ln_;
+  i = i_; j = j_; m = m_; n = n_;
+  lmt = (lm + mb - 1) / mb;
+  lnt = (ln + nb - 1) / nb;
+  mt = (i + m - 1) / mb - i / mb + 1;
+  nt = (j + n - 1) / nb - j / nb + 1;
+  if (m == 0) mt = 0;
+  if (n == 0) nt = 0;
+  bsiz = mb * nb;
+  default_dtt = Datatype::contiguous((uint32_t)elem_size, bsiz);
+  dc_register_id(this);
+}
+
+std::string TiledMatrix::key_to_string(uint64_t key) const {
+  return key_base + "(" + std::to_string(key % lmt) + ", " + std::to_string(key / lmt) + ")";
+}
+
+void TiledMatrix::allocate_storage(void* ptr) {
+  size_t bytes = (size_t)nb_local_tiles * (size_t)bsiz * elem_size;
+  if (ptr) { mat = ptr; owns_storage = false; }
+  else if (bytes) {
+    if (storage_device == 0) {
+      if (posix_memalign(&mat, 4096, bytes)) fatal("cannot allocate %zu bytes for a tiled matrix", bytes);
+      std::memset(mat, 0, bytes);
+    } else {
+      mat = device_alloc(storage_device, bytes);
+      if (!mat) fatal("cannot allocate %zu bytes on device %d", bytes, storage_device);
+    }
+    owns_storage = true;
+  }
+  tiles.assign((size_t)nb_local_tiles, nullptr);
+}
+
+void* TiledMatrix::tile_ptr(int64_t tm, int64_t tn) {
+  int64_t li = local_index(tm, tn);
+  if (li < 0 || !mat) return nullptr;
+  return static_cast<char*>(mat) + (size_t)li * (size_t)bsiz * elem_size;
+}
+
+Data* TiledMatrix::tile_data(int64_t tm, int64_t tn) {
+  int64_t li = local_index(tm, tn);
+  if (li < 0) return nullptr;
+  Data* d = __atomic_load_n(&tiles[li], __ATOMIC_ACQUIRE);
+  if (d) return d;
+  int64_t idx[2] = {tm, tn};
+  uint64_t key = data_key(idx, 2);
+  void* p = static_cast<char*>(mat) + (size_t)li * (size_t)bsiz * elem_size;
+  d = data_create(&tiles[li], this, key, p, (size_t)bsiz * elem_size, DATA_FLAG_PARSEC_MANAGED, storage_device);
+  d->copy(storage_device)->dtt = default_dtt;
+  return d;
+}
+
+// ============================================================ block cyclic
+void BlockCyclic::init(int mt_, int myrank_, int64_t mb_, int64_t nb_, int64_t lm_, int64_t ln_, int64_t i_, int64_t j_, int64_t m_, int64_t n_,
+                       int P_, int Q_, int kp_, int kq_, int ip_, int jq_) {
+  P = std::max(1, P_); Q = std::max(1, Q_);
+  kp = std::max(1, kp_); kq = std::max(1, kq_);
+  ip = ip_; jq = jq_;
+  init_base(mt_, myrank_, P * Q, mb_, nb_, lm_, ln_, i_, j_, m_, n_);
+  int myrow = (int)myrank / Q, mycol = (int)myrank % Q;
+  llm_tiles = 0;
+  for (int64_t g = 0; g < lmt; ++g) if ((g / kp + ip) % P == myrow) ++llm_tiles;
+  lln_tiles = 0;
+  for (int64_t g = 0; g < lnt; ++g) if ((g / kq + jq) % Q == mycol) ++lln_tiles;
+  nb_local_tiles = llm_tiles * lln_tiles;
+  key_base = "A";
+}
+
+uint32_t BlockCyclic::rank_of(const int64_t* idx, int n) const {
+  int64_t gm = idx[0] + i / mb;
+  int64_t gn = (n > 1 ? idx[1] : 0) + j / nb;
+  int64_t rr = (gm / kp + ip) % P;
+  int64_t cr = (gn / kq + jq) % Q;
+  return (uint32_t)(rr * Q + cr);
+}
+
+int32_t BlockCyclic::vpid_of(const int64_t* idx, int n) const {
+  if (nb_vp <= 1) return 0;
+  int64_t gm = idx[0] + i / mb, gn = (n > 1 ? idx[1] : 0) + j / nb;
+  return (int32_t)(((gm / (P * kp)) + (gn / (Q * kq))) % nb_vp);
+}
+
+int64_t BlockCyclic::local_index(int64_t tm, int64_t tn) const {
+  int64_t idx[2] = {tm, tn};
+  if (rank_of(idx, 2) != myrank) return -1;
+  int64_t gm = tm + i / mb, gn = tn + j / nb;
+  if (gm < 0 || gn < 0 || gm >= lmt || gn >= lnt) return -1;
+  // row position among this rank's tile rows (k-cyclic aware)
+  int64_t lmi = (gm / ((int64_t)P * kp)) * kp + gm % kp;
+  int64_t lni = (gn / ((int64_t)Q * kq)) * kq + gn % kq;
+  return lni * llm_tiles + lmi;
+}
+
+// ========================================================= symmetric BC
+void SymBlockCyclic::init_sym(int mt_, int myrank_, int64_t mb_, int64_t nb_, int64_t lm_, int64_t ln_, int64_t i_, int64_t j_, int64_t m_, int64_t n_, int P_, int Q_, int uplo_) {
+  init(mt_, myrank_, mb_, nb_, lm_, ln_, i_, j_, m_, n_, P_, Q_, 1, 1, 0, 0);
+  uplo = uplo_;
+  local_map.assign((size_t)(lmt * lnt), -1);
+  int64_t cnt = 0;
+  for (int64_t gn = 0; gn < lnt; ++gn)
+    for (int64_t gm = 0; gm < lmt; ++gm) {
+      bool in = uplo == MATRIX_LOWER ? gm >= gn : gm <= gn;
+      if (!in) continue;
+      int64_t idx[2] = {gm - i / mb, gn - j / nb};
+      if (BlockCyclic::rank_of(idx, 2) == myrank) local_map[gn * lmt + gm] = cnt++;
+    }
+  nb_local_tiles = cnt;
+}
+
+uint32_t SymBlockCyclic::rank_of(const int64_t* idx, int n) const {
+  int64_t gm = idx[0] + i / mb, gn = (n > 1 ? idx[1] : 0) + j / nb;
+  bool in = uplo == MATRIX_LOWER ? gm >= gn : gm <= gn;
+  if (!in) {  // mirror to the stored triangle
+    int64_t sw[2] = {idx[1], idx[0]};
+    return BlockCyclic::rank_of(sw, 2);
+  }
+  return BlockCyclic::rank_of(idx, n);
+}
+
+int64_t SymBlockCyclic::local_index(int64_t tm, int64_t tn) const {
+  int64_t gm = tm + i / mb, gn = tn + j / nb;
+  if (gm < 0 || gn < 0 || gm >= lmt || gn >= lnt) return -1;
+  return local_map[gn * lmt + gm];
+}
+
+// ================================================================= band
+void BandMatrix::init_band(BlockCyclic* b, BlockCyclic* off, int bs) {
+  band = b;
+  off_band = off;
+  band_size = bs;
+  mtype = off->mtype; elem_size = off->elem_size; myrank = off->myrank; nodes = off->nodes;
+  mb = off->mb; nb = off->nb; lm = off->lm; ln = off->ln; lmt = off->lmt; lnt = off->lnt;
+  m = off->m; n = off->n; mt = off->mt; nt = off->nt; bsiz = off->bsiz;
+  default_dtt = off->default_dtt;
+  key_base = "Band";
+  dc_register_id(this);
+}
+
+uint32_t BandMatrix::rank_of(const int64_t* idx, int n) const {
+  int64_t tm = idx[0], tn = n > 1 ? idx[1] : 0;
+  if (std::llabs(tm - tn) <= band_size) {
+    int64_t bidx[2] = {tm - tn + band_size, tn};
+    return band->rank_of(bidx, 2);
+  }
+  return off_band->rank_of(idx, n);
+}
+
+int32_t BandMatrix::vpid_of(const int64_t* idx, int n) const {
+  int64_t tm = idx[0], tn = n > 1 ? idx[1] : 0;
+  if (std::llabs(tm - tn) <= band_size) {
+    int64_t bidx[2] = {tm - tn + band_size, tn};
+    return band->vpid_of(bidx, 2);
+  }
+  return off_band->vpid_of(idx, n);
+}
+
+Data* BandMatrix::data_of(const int64_t* idx, int n) {
+  int64_t tm = idx[0], tn = n > 1 ? idx[1] : 0;
+  if (std::llabs(tm - tn) <= band_size) {
+    int64_t bidx[2] = {tm - tn + band_size, tn};
+    return band->data_of(bidx, 2);
+  }
+  return off_band->data_of(idx, n);
+}
+
+// ============================================================== tabular
+void TabularMatrix::init_tab(int mt_, int myrank_, int nodes_, int64_t mb_, int64_t nb_, int64_t lm_, int64_t ln_, const std::vector<int>& ranks) {
+  init_base(mt_, myrank_, nodes_, mb_, nb_, lm_, ln_, 0, 0, lm_, ln_);
+  table_rank = ranks;
+  if ((int64_t)table_rank.size() < lmt * lnt) table_rank.resize((size_t)(lmt * lnt), 0);
+  table_vp.assign(table_rank.size(), 0);
+  local_map.assign(table_rank.size(), -1);
+  int64_t cnt = 0;
+  for (size_t k = 0; k < table_rank.size(); ++k)
+    if ((uint32_t)table_rank[k] == myrank) local_map[k] = cnt++;
+  nb_local_tiles = cnt;
+  key_base = "Tab";
+}
+uint32_t TabularMatrix::rank_of(const int64_t* idx, int n) const { return (uint32_t)table_rank[(size_t)((n > 1 ? idx[1] : 0) * lmt + idx[0])]; }
+int32_t TabularMatrix::vpid_of(const int64_t* idx, int n) const { return table_vp[(size_t)((n > 1 ? idx[1] : 0) * lmt + idx[0])]; }
+int64_t TabularMatrix::local_index(int64_t tm, int64_t tn) const {
+  if (tm < 0 || tn < 0 || tm >= lmt || tn >= lnt) return -1;
+  return local_map[(size_t)(tn * lmt + tm)];
+}
+
+// ========================================================= vector cyclic
+void VectorCyclic::init_vec(int mt_, int myrank_, int nodes_, int64_t mb_, int64_t lm_, int dist_, int P_, int Q_) {
+  P = std::max(1, P_); Q = std::max(1, Q_);
+  dist = (Dist)dist_;
+  init_base(mt_, myrank_, nodes_, mb_, 1, lm_, 1, 0, 0, lm_, 1);
+  int64_t cnt = 0;
+  for (int64_t g = 0; g < lmt; ++g) { int64_t idx[1] = {g}; if (rank_of(idx, 1) == myrank) ++cnt; }
+  nb_local_tiles = cnt;
+  key_base = "V";
+}
+uint32_t VectorCyclic::rank_of(const int64_t* idx, int n) const {
+  (void)n;
+  int64_t g = idx[0];
+  switch (dist) {
+    case ROW: return (uint32_t)((g % P) * Q);          // first column of the grid
+    case COL: return (uint32_t)(g % Q);                 // first row
+    case DIAG: return (uint32_t)((g % P) * Q + (g % Q)); // diagonal processes
+  }
+  return 0;
+}
+int64_t VectorCyclic::local_index(int64_t tm, int64_t tn) const {
+  (void)tn;
+  int64_t idx[1] = {tm};
+  if (tm < 0 || tm >= lmt || rank_of(idx, 1) != myrank) return -1;
+  int64_t cnt = 0;
+  for (int64_t g = 0; g < tm; ++g) { int64_t id2[1] = {g}; if (rank_of(id2, 1) == myrank) ++cnt; }
+  return cnt;
+}
+
+// =================================================================== hash
+void HashCollection::set_entry(uint64_t key, uint32_t rank, int32_t vp, void* ptr, size_t size) {
+  Entry e;
+  e.rank = rank; e.vp = vp; e.ptr = ptr; e.size = size;
+  if (rank == myrank && ptr) e.data = data_create(nullptr, this, key, ptr, size);
+  map.insert(key, e);
+}
+uint32_t HashCollection::rank_of_key(uint64_t key) const {
+  Entry e;
+  return const_cast<ShardedMap<Entry>&>(map).find(key, e) ? e.rank : 0;
+}
+int32_t HashCollection::vpid_of_key(uint64_t key) const {
+  Entry e;
+  return const_cast<ShardedMap<Entry>&>(map).find(key, e) ? e.vp : 0;
+}
+Data* HashCollection::data_of_key(uint64_t key) {
+  Entry e;
+  return map.find(key, e) ? e.data : nullptr;
+}
+HashCollection::~HashCollection() {
+  map.for_each([](uint64_t, Entry& e) { if (e.data) data_destroy(e.data); e.data = nullptr; });
+}
+
+}  // namespace parsec

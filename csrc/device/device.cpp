@@ -1,0 +1,228 @@
+// Device registry, CPU and recursive devices, load-balanced device selection,
+// CPU-side staging of device-resident data.
+//
+// Parity: reference mca/device/device.c (registry :194-285, attach :843-904,
+// registration_complete -> relative weights :617-666, CPU weights :678-797,
+// parsec_get_best_device :79-189 with load_balance_skew).
+#include "device.hpp"
+
+#include <unistd.h>
+
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+
+#include "hip_device.hpp"
+
+namespace parsec {
+
+DeviceRegistry& DeviceRegistry::instance() {
+  static DeviceRegistry* r = new DeviceRegistry();
+  return *r;
+}
+
+int DeviceRegistry::add(Device* d) {
+  d->device_index = (int)devices.size();
+  devices.push_back(d);
+  return d->device_index;
+}
+
+int DeviceRegistry::nb_gpus() const {
+  int n = 0;
+  for (auto* d : devices) if (d && d->is_gpu()) ++n;
+  return n;
+}
+
+void DeviceRegistry::registration_complete() {
+  double maxg = 0;
+  for (auto* d : devices) if (d) maxg = std::max(maxg, d->gflops_fp64);
+  for (auto* d : devices) if (d) d->gflops_weight = d->gflops_fp64 > 0 ? maxg / d->gflops_fp64 : 1e9;
+  frozen = true;
+}
+
+struct CpuDevice : Device {
+  CpuDevice(int cores) {
+    name = "cpu";
+    type = DEV_CPU;
+    // 2 FMA pipes x 4 doubles (AVX2) x 2 flops x ~2.4 GHz per core
+    gflops_fp64 = std::max(1, cores) * 2.4 * 16.0;
+    gflops_fp32 = 2 * gflops_fp64;
+  }
+};
+
+struct RecursiveDevice : Device {
+  RecursiveDevice() { name = "recursive"; type = DEV_RECURSIVE; gflops_fp64 = 1; }
+};
+
+static double g_load_balance_skew = 20.0;
+
+void devices_init(Context* ctx) {
+  auto& reg = DeviceRegistry::instance();
+  auto& params = ParamRegistry::instance();
+  g_load_balance_skew = (double)params.reg_int("device", "", "load_balance_skew", "Allowed load imbalance (percent) before moving work off the data-owner device", 20);
+  if (reg.devices.empty()) {
+    double cpu_g = (double)params.reg_int("device", "cpu", "gflops", "Override the CPU device fp64 GFLOP/s estimate (0 = estimate)", 0);
+    auto* cpu = new CpuDevice(ctx->nb_cores);
+    if (cpu_g > 0) cpu->gflops_fp64 = cpu_g;
+    reg.add(cpu);
+    reg.add(new RecursiveDevice());
+    hip_devices_init(ctx);
+    reg.registration_complete();
+  }
+  for (auto* d : reg.devices) if (d) d->attach(ctx);
+  if (params.reg_int("device", "", "show_capabilities", "Print device capabilities at init", 0))
+    for (auto* d : reg.devices)
+      if (d) std::fprintf(stderr, "[parsec] device %d %s type=0x%x fp64=%.0f GF weight=%.3f\n", d->device_index, d->name.c_str(), d->type, d->gflops_fp64, d->gflops_weight);
+}
+
+void devices_start(Context* ctx) { hip_devices_start(ctx); }
+void devices_stop(Context* ctx) { hip_devices_stop(ctx); }
+
+void devices_fini(Context* ctx) {
+  auto& reg = DeviceRegistry::instance();
+  if (ParamRegistry::instance().reg_int("device", "", "show_statistics", "Print per-device statistics at fini", 0)) {
+    for (auto* d : reg.devices) {
+      if (!d) continue;
+      std::fprintf(stderr, "[parsec] device %d %-10s tasks=%llu launches=%llu batched=%llu in=%llu B out=%llu B d2d=%llu B faults=%llu\n", d->device_index, d->name.c_str(),
+                   (unsigned long long)d->stats.executed_tasks.load(), (unsigned long long)d->stats.kernel_launches.load(), (unsigned long long)d->stats.batched_tasks.load(),
+                   (unsigned long long)d->stats.bytes_in.load(), (unsigned long long)d->stats.bytes_out.load(), (unsigned long long)d->stats.bytes_d2d.load(),
+                   (unsigned long long)d->stats.data_faults.load());
+    }
+  }
+  for (auto* d : reg.devices) if (d) d->detach(ctx);
+}
+
+bool device_type_enabled(Taskpool* tp, uint32_t type) {
+  auto& reg = DeviceRegistry::instance();
+  for (auto* d : reg.devices) {
+    if (!d || !(d->type & type)) continue;
+    if (tp->devices_index_mask & (1u << d->device_index)) return true;
+  }
+  return false;
+}
+
+int get_best_device(Task* t, double ratio) {
+  auto& reg = DeviceRegistry::instance();
+  Taskpool* tp = t->taskpool;
+  const TaskClass* tc = t->task_class;
+  int dev = -1;
+  // 1) locality: a device that owns (or prefers) data we write, then data we read
+  for (int pass = 0; pass < 2 && dev < 0; ++pass) {
+    for (auto& f : tc->flows) {
+      if (f.access == FLOW_CTL || f.access == FLOW_NONE) continue;
+      bool w = f.access & FLOW_WRITE;
+      if ((pass == 0) != w) continue;
+      DataCopy* c = t->data[f.index].data_in;
+      if (!c || !c->original) continue;
+      Data* d = c->original;
+      int cand = d->preferred_device >= 2 ? d->preferred_device : d->owner_device;
+      if (cand >= 2 && cand < reg.count() && reg.devices[cand] && reg.devices[cand]->is_gpu() && (tp->devices_index_mask & (1u << cand))) {
+        dev = cand;
+        break;
+      }
+    }
+  }
+  // 2) load balance among enabled GPUs; keep the locality choice unless skewed
+  int best = -1;
+  double best_load = 0;
+  for (auto* d : reg.devices) {
+    if (!d || !d->is_gpu() || !(tp->devices_index_mask & (1u << d->device_index))) continue;
+    double l = (double)d->load.load(std::memory_order_relaxed) + ratio * d->gflops_weight;
+    if (best < 0 || l < best_load) { best = d->device_index; best_load = l; }
+  }
+  if (dev >= 0 && best >= 0 && dev != best) {
+    double ldev = (double)reg.devices[dev]->load.load() + ratio * reg.devices[dev]->gflops_weight;
+    if (ldev <= best_load * (1.0 + g_load_balance_skew / 100.0) + 1) return dev;
+    return best;
+  }
+  return dev >= 0 ? dev : best;
+}
+
+int gpu_chore_dispatch(ExecutionStream* es, Task* t, int chore) {
+  const Chore& ch = t->task_class->chores[chore];
+  int dev = t->selected_device >= 2 ? t->selected_device : get_best_device(t, ch.weight);
+  if (dev < 2) return HOOK_NEXT;
+  t->selected_device = (int8_t)dev;
+  return DeviceRegistry::instance().devices[dev]->submit(es, t, chore);
+}
+
+// ------------------------------------------------------------ host staging
+DataCopy* data_pull_to_host(Data* d) {
+  if (!d) return nullptr;
+  DataCopy* host = d->copy(0);
+  if (!host) {
+    void* p = nullptr;
+    if (posix_memalign(&p, 4096, std::max<size_t>(d->nb_elts, 64))) fatal("host allocation failed");
+    DataCopy* c = new DataCopy();
+    c->device_private = p;
+    c->flags = DATA_FLAG_PARSEC_OWNED;
+    c->coherency_state = COHERENCY_INVALID;
+    c->version = 0;
+    std::lock_guard<SpinLock> g(d->lock);
+    if (!d->copy(0)) data_copy_attach(d, c, 0);
+    else { std::free(p); delete c; }
+    host = d->copy(0);
+  }
+  DataCopy* src = data_start_transfer_ownership_to_copy(d, 0, FLOW_READ);
+  if (src && src != host) {
+    device_memcpy(0, host->device_private, src->device_index, src->device_private, d->nb_elts);
+    auto* dev = DeviceRegistry::instance().get(src->device_index);
+    if (dev) dev->stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
+  }
+  data_end_transfer_ownership_to_copy(d, 0, FLOW_READ);
+  return host;
+}
+
+void cpu_stage_in(ExecutionStream* es, Task* t) {
+  (void)es;
+  for (auto& f : t->task_class->flows) {
+    if (f.access == FLOW_CTL || f.access == FLOW_NONE) continue;
+    TaskDataRef& r = t->data[f.index];
+    DataCopy* c = r.data_in;
+    if (!c || !c->original) continue;
+    Data* d = c->original;
+    bool needs = c->device_index != 0;
+    if (!needs) {
+      // host copy present: is it current?
+      std::lock_guard<SpinLock> g(d->lock);
+      uint32_t newest = 0;
+      for (int i = 1; i < kMaxDevices; ++i) { DataCopy* o = d->copy(i); if (o && o->coherency_state != COHERENCY_INVALID) newest = std::max(newest, o->version); }
+      needs = newest > c->version && (f.access & FLOW_READ);
+    }
+    if (!needs) continue;
+    DataCopy* host = data_pull_to_host(d);
+    if (host != c) {
+      data_copy_retain(host);
+      data_copy_release(c);
+      r.data_in = host;
+    }
+  }
+}
+
+void cpu_write_epilog(Task* t) {
+  for (auto& f : t->task_class->flows) {
+    if (!(f.access & FLOW_WRITE)) continue;
+    DataCopy* c = t->data[f.index].data_in;
+    if (!c || !c->original || c->device_index != 0) continue;
+    Data* d = c->original;
+    std::lock_guard<SpinLock> g(d->lock);
+    uint32_t v = 0;
+    for (int i = 0; i < kMaxDevices; ++i) { DataCopy* o = d->copy(i); if (o && o->coherency_state != COHERENCY_INVALID) v = std::max(v, o->version); }
+    c->version = v + 1;
+    c->coherency_state = COHERENCY_OWNED;
+    d->owner_device = 0;
+  }
+}
+
+int device_hip_ordinal(int device_index) {
+  auto* d = DeviceRegistry::instance().get(device_index);
+  if (!d || !d->is_gpu()) return -1;
+  return static_cast<HipDevice*>(d)->ordinal;
+}
+
+int first_gpu_device_index() {
+  for (auto* d : DeviceRegistry::instance().devices) if (d && d->is_gpu()) return d->device_index;
+  return -1;
+}
+
+}  // namespace parsec

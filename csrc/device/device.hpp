@@ -1,0 +1,104 @@
+// Device framework: registry, CPU / recursive devices, the HIP device engine
+// entry points, and the GPU execution context handed to GPU chores.
+//
+// Parity: device registry with CPU=0, recursive=1, accelerators>=2 and relative
+// capability weights (reference mca/device/device.c:194-285,617-666,843-904),
+// parsec_get_best_device (device.c:79-189), GPU task staging / exec / pop
+// pipeline with event rings (device_cuda_module.c:1961-2763).
+// MI355X-first differences: one dedicated manager thread per GPU (no manager
+// election), kernel *batching* (all ready tile tasks of one kernel kind are
+// launched as ONE grouped kernel so small 512^2 tiles still fill 256 CUs),
+// HIP stream priorities for critical-path tasks, and collections that can live
+// in HBM permanently.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <vector>
+
+#include "../core/runtime.hpp"
+
+namespace parsec {
+
+void devices_init(Context* ctx);
+void devices_start(Context* ctx);
+void devices_stop(Context* ctx);
+void devices_fini(Context* ctx);
+bool device_type_enabled(Taskpool* tp, uint32_t type);
+int gpu_chore_dispatch(ExecutionStream* es, Task* t, int chore);
+
+// Raw device memory helpers (outside the engine's tile cache).
+void* device_alloc(int device_index, size_t bytes);
+void device_free(int device_index, void* p);
+int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t bytes);
+int device_hip_ordinal(int device_index);  // -1 if not a HIP device
+int first_gpu_device_index();
+// Bring the newest version of `d` to the host (device 0), synchronously.
+DataCopy* data_pull_to_host(Data* d);
+// Make sure every data_in of a CPU task is host-resident and current.
+void cpu_stage_in(ExecutionStream* es, Task* t);
+// After a CPU body wrote its flows: the host copies become the newest versions.
+void cpu_write_epilog(Task* t);
+
+// ------------------------------------------------------------------ batching
+// Kernel kinds that a GPU chore can enqueue into the manager's per-round batch.
+enum BatchKind : int { BATCH_GEMM = 0, BATCH_TRSM, BATCH_POTRF, BATCH_GEQRT, BATCH_TSQRT, BATCH_UNMQR, BATCH_TSMQR, BATCH_STENCIL, BATCH_NB_KINDS };
+
+struct GemmDesc {
+  const double* A;
+  const double* B;
+  double* C;
+  int m, n, k;
+  int lda, ldb, ldc;
+  double alpha, beta;
+  uint8_t transA, transB;  // 0 = N, 1 = T
+  uint8_t lower_only;      // 1: only C's lower triangle (SYRK)
+  uint8_t pad;
+};
+
+struct TrsmDesc {  // B := B * op(L)^-1 ; right side, lower, (trans), non-unit
+  const double* L;
+  double* B;
+  int m, n;  // B is m x n, L is n x n
+  int ldl, ldb;
+  uint8_t trans;  // 1: B * L^-T (the Cholesky panel)
+  uint8_t pad[7];
+};
+
+struct PotrfDesc {
+  double* A;
+  int n, lda;
+  int* info;  // device pointer (may be null)
+};
+
+struct KernelBatch {
+  std::vector<GemmDesc> gemm;
+  std::vector<TrsmDesc> trsm;
+  std::vector<PotrfDesc> potrf;
+  std::vector<std::function<void(hipStream_t)>> generic;  // other kernels, launched in order
+  bool empty() const { return gemm.empty() && trsm.empty() && potrf.empty() && generic.empty(); }
+  void clear() { gemm.clear(); trsm.clear(); potrf.clear(); generic.clear(); }
+};
+
+struct HipDevice;
+
+// Handed to a GPU chore body: the stream to launch on and device pointers of
+// the task's flows. Bodies may launch directly on `stream` or append to `batch`
+// (preferred for tile kernels).
+struct GpuExecContext {
+  HipDevice* dev = nullptr;
+  Device* device = nullptr;
+  hipStream_t stream = nullptr;
+  int stream_index = 0;
+  Task* task = nullptr;
+  KernelBatch* batch = nullptr;
+  void* flow_ptr[kMaxFlows] = {};
+  void* ptr(int flow) const { return flow_ptr[flow]; }
+  void* workspace(size_t bytes);  // per-stream scratch (valid until the task completes)
+};
+
+using GpuHook = std::function<int(GpuExecContext*, Task*)>;
+
+// Flush a batch on a stream (implemented next to the kernels).
+void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal);
+
+}  // namespace parsec

@@ -1,0 +1,688 @@
+#include "hip_device.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "../prof/profiling.hpp"
+
+namespace parsec {
+
+// ============================================================ zone allocator
+ZoneAllocator::ZoneAllocator(int ordinal, size_t max_bytes, size_t segment_bytes, size_t unit)
+    : ordinal_(ordinal), max_bytes_(max_bytes), seg_bytes_(segment_bytes), unit_(unit) {}
+
+ZoneAllocator::~ZoneAllocator() {
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(ordinal_);
+  for (auto& s : segs_) (void)hipFree(s.base);
+  (void)hipSetDevice(prev);
+}
+
+void* ZoneAllocator::alloc(size_t bytes) {
+  size_t sz = (bytes + unit_ - 1) / unit_ * unit_;
+  for (size_t si = 0; si < segs_.size(); ++si) {
+    auto& s = segs_[si];
+    for (auto it = s.free_.begin(); it != s.free_.end(); ++it) {
+      if (it->second < sz) continue;
+      size_t off = it->first, len = it->second;
+      s.free_.erase(it);
+      if (len > sz) s.free_[off + sz] = len - sz;
+      void* p = s.base + off;
+      live_[p] = {si, sz};
+      used_ += sz;
+      return p;
+    }
+  }
+  // new segment
+  size_t seg = std::max(seg_bytes_, sz);
+  if (reserved_ + seg > max_bytes_) {
+    if (reserved_ + sz > max_bytes_) return nullptr;
+    seg = std::max(sz, (max_bytes_ - reserved_) / unit_ * unit_);
+  }
+  void* base = nullptr;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(ordinal_);
+  hipError_t e = hipMalloc(&base, seg);
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess || !base) { (void)hipGetLastError(); return nullptr; }
+  reserved_ += seg;
+  segs_.push_back(Segment{static_cast<char*>(base), seg, {}});
+  auto& s = segs_.back();
+  if (seg > sz) s.free_[sz] = seg - sz;
+  live_[base] = {segs_.size() - 1, sz};
+  used_ += sz;
+  return base;
+}
+
+void ZoneAllocator::free(void* p) {
+  auto it = live_.find(p);
+  if (it == live_.end()) return;
+  auto [si, sz] = it->second;
+  live_.erase(it);
+  used_ -= sz;
+  auto& s = segs_[si];
+  size_t off = static_cast<char*>(p) - s.base;
+  auto nx = s.free_.lower_bound(off);
+  // coalesce with next
+  if (nx != s.free_.end() && nx->first == off + sz) { sz += nx->second; nx = s.free_.erase(nx); }
+  // coalesce with prev
+  if (nx != s.free_.begin()) {
+    auto pv = std::prev(nx);
+    if (pv->first + pv->second == off) { pv->second += sz; return; }
+  }
+  s.free_[off] = sz;
+}
+
+// ================================================================ helpers
+void* device_alloc(int device_index, size_t bytes) {
+  int ord = device_hip_ordinal(device_index);
+  if (ord < 0) return nullptr;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(ord);
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, bytes);
+  if (e == hipSuccess) (void)hipMemset(p, 0, bytes);
+  (void)hipSetDevice(prev);
+  return e == hipSuccess ? p : nullptr;
+}
+
+void device_free(int device_index, void* p) {
+  int ord = device_hip_ordinal(device_index);
+  if (ord < 0 || !p) return;
+  (void)hipFree(p);
+}
+
+int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t bytes) {
+  if (dst_dev == 0 && src_dev == 0) { std::memcpy(dst, src, bytes); return 0; }
+  hipMemcpyKind k = dst_dev == 0 ? hipMemcpyDeviceToHost : src_dev == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  hipError_t e = hipMemcpy(dst, src, bytes, k);
+  return e == hipSuccess ? 0 : -1;
+}
+
+void* GpuExecContext::workspace(size_t bytes) { return dev->workspace(stream_index, bytes); }
+
+// ================================================================ device
+static int g_nb_exec_streams = 4;
+
+int HipDevice::attach(Context* c) {
+  ctx = c;
+  return 0;
+}
+
+int HipDevice::detach(Context* c) {
+  (void)c;
+  shutdown();
+  return 0;
+}
+
+void HipDevice::start(Context* c) {
+  ctx = c;
+  if (manager.joinable()) return;
+  PARSEC_HIP_CHECK(hipSetDevice(ordinal));
+  int lo = 0, hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+  PARSEC_HIP_CHECK(hipStreamCreateWithFlags(&s_h2d, hipStreamNonBlocking));
+  PARSEC_HIP_CHECK(hipStreamCreateWithFlags(&s_d2h, hipStreamNonBlocking));
+  s_exec.resize(nb_exec_streams);
+  for (int i = 0; i < nb_exec_streams; ++i)
+    PARSEC_HIP_CHECK(hipStreamCreateWithPriority(&s_exec[i], hipStreamNonBlocking, i == 0 ? hi : lo));
+  executing.assign(nb_exec_streams, {});
+  batches.assign(nb_exec_streams, {});
+  round_tasks.assign(nb_exec_streams, {});
+  stream_workspace.assign(nb_exec_streams, nullptr);
+  stream_workspace_size.assign(nb_exec_streams, 0);
+  es = new ExecutionStream();
+  es->ctx = c;
+  es->vp = c->vps[0];
+  es->is_manager = true;
+  es->th_id = 1000 + device_index;
+  c->aux_es.push_back(es);
+  stop.store(false);
+  manager = std::thread([this] { manager_main(); });
+}
+
+void HipDevice::shutdown() {
+  if (!manager.joinable()) return;
+  stop.store(true);
+  in_cv.notify_all();
+  manager.join();
+  (void)hipSetDevice(ordinal);
+  for (auto e : event_pool) (void)hipEventDestroy(e);
+  event_pool.clear();
+  for (size_t i = 0; i < stream_workspace.size(); ++i) if (stream_workspace[i]) (void)hipFree(stream_workspace[i]);
+  stream_workspace.clear();
+  for (auto s : s_exec) (void)hipStreamDestroy(s);
+  s_exec.clear();
+  if (s_h2d) (void)hipStreamDestroy(s_h2d);
+  if (s_d2h) (void)hipStreamDestroy(s_d2h);
+  s_h2d = s_d2h = nullptr;
+  // drop cached copies
+  for (List* l : {&lru_clean, &lru_owned}) {
+    while (ListItem* it = l->pop_front()) {
+      DataCopy* c = static_cast<DataCopy*>(it);
+      if (Data* d = c->original) {
+        std::lock_guard<SpinLock> g(d->lock);
+        data_copy_detach(d, c, device_index);
+      }
+      if (zone) zone->free(c->device_private);
+      delete static_cast<DevCopyState*>(c->dev_state);
+      c->dev_state = nullptr;
+      c->original = nullptr;
+      data_copy_release(c);
+    }
+  }
+  zone.reset();
+}
+
+void HipDevice::quiesce() {
+  Backoff b;
+  while (inflight.load() > 0) b.idle();
+}
+
+hipEvent_t HipDevice::get_event() {
+  if (!event_pool.empty()) { hipEvent_t e = event_pool.back(); event_pool.pop_back(); return e; }
+  hipEvent_t e;
+  PARSEC_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return e;
+}
+void HipDevice::put_event(hipEvent_t e) { if (e) event_pool.push_back(e); }
+
+void* HipDevice::workspace(int stream, size_t bytes) {
+  if (stream < 0 || stream >= (int)stream_workspace.size()) stream = 0;
+  if (stream_workspace_size[stream] < bytes) {
+    // grow: the stream must be idle for the old buffer to be released safely
+    (void)hipStreamSynchronize(s_exec[stream]);
+    if (stream_workspace[stream]) (void)hipFree(stream_workspace[stream]);
+    size_t nb = std::max(bytes, (size_t)1 << 20);
+    PARSEC_HIP_CHECK(hipMalloc(&stream_workspace[stream], nb));
+    stream_workspace_size[stream] = nb;
+  }
+  return stream_workspace[stream];
+}
+
+int HipDevice::submit(ExecutionStream* submitter, Task* t, int chore) {
+  (void)submitter;
+  auto* g = new GpuTask();
+  g->task = t;
+  g->chore = chore;
+  g->load = t->task_class->chores[chore].weight * gflops_weight;
+  g->pushout = t->task_class->gpu_pushout_mask(t, device_index);
+  load.fetch_add((int64_t)g->load, std::memory_order_relaxed);
+  t->gpu = g;
+  inflight.fetch_add(1, std::memory_order_acq_rel);
+  {
+    std::lock_guard<std::mutex> lk(in_m);
+    incoming.push_back(g);
+    incoming_n.fetch_add(1, std::memory_order_release);
+  }
+  in_cv.notify_one();
+  return HOOK_ASYNC;
+}
+
+int HipDevice::memory_register(DataCollection* dc, void* ptr, size_t len) {
+  (void)dc;
+  if (!ptr || !len) return 0;
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, ptr) == hipSuccess && attr.type == hipMemoryTypeDevice) return 0;
+  (void)hipGetLastError();
+  if (hipHostRegister(ptr, len, hipHostRegisterDefault) != hipSuccess) { (void)hipGetLastError(); return -1; }
+  return 0;
+}
+
+int HipDevice::memory_unregister(DataCollection* dc, void* ptr) {
+  (void)dc;
+  if (ptr) { if (hipHostUnregister(ptr) != hipSuccess) (void)hipGetLastError(); }
+  return 0;
+}
+
+// --------------------------------------------------------------- LRU / mem
+void HipDevice::lru_remove(DataCopy* c) {
+  auto* st = static_cast<DevCopyState*>(c->dev_state);
+  if (!st || !st->in_lru) return;
+  (st->owned_lru ? lru_owned : lru_clean).remove(c);
+  st->in_lru = false;
+}
+
+void HipDevice::lru_touch(DataCopy* c) {
+  auto* st = static_cast<DevCopyState*>(c->dev_state);
+  if (!st || !st->cache_managed) return;
+  lru_remove(c);
+  if (c->readers.load() > 0) return;
+  Data* d = c->original;
+  bool dirty = false;
+  if (d) {
+    std::lock_guard<SpinLock> g(d->lock);
+    dirty = true;
+    for (int i = 0; i < kMaxDevices; ++i) {
+      if (i == device_index) continue;
+      DataCopy* o = d->copy(i);
+      if (o && o->coherency_state != COHERENCY_INVALID && o->version >= c->version) { dirty = false; break; }
+    }
+  }
+  st->owned_lru = dirty;
+  (dirty ? lru_owned : lru_clean).push_back(c);
+  st->in_lru = true;
+}
+
+bool HipDevice::evict(size_t bytes) {
+  size_t freed = 0;
+  auto drop = [&](DataCopy* c) -> bool {
+    Data* d = c->original;
+    if (!d) return false;
+    {
+      std::lock_guard<SpinLock> g(d->lock);
+      if (c->readers.load() > 0 || c->refcount.load() > 1) return false;
+      data_copy_detach(d, c, device_index);
+    }
+    freed += d->nb_elts;
+    zone->free(c->device_private);
+    c->device_private = nullptr;
+    delete static_cast<DevCopyState*>(c->dev_state);
+    c->dev_state = nullptr;
+    c->original = nullptr;
+    data_copy_release(c);
+    stats.data_faults.fetch_add(1, std::memory_order_relaxed);
+    return true;
+  };
+  for (ListItem* it = lru_clean.front(); it && it != lru_clean.end() && freed < bytes;) {
+    ListItem* nx = it->next;
+    DataCopy* c = static_cast<DataCopy*>(it);
+    lru_clean.remove(c);
+    static_cast<DevCopyState*>(c->dev_state)->in_lru = false;
+    if (!drop(c)) lru_touch(c);
+    it = nx;
+  }
+  // write back dirty copies (reference W2R task), then drop them
+  for (ListItem* it = lru_owned.front(); it && it != lru_owned.end() && freed < bytes;) {
+    ListItem* nx = it->next;
+    DataCopy* c = static_cast<DataCopy*>(it);
+    Data* d = c->original;
+    lru_owned.remove(c);
+    static_cast<DevCopyState*>(c->dev_state)->in_lru = false;
+    if (d && c->readers.load() == 0) {
+      DataCopy* host = d->copy(0);
+      if (!host) host = data_pull_to_host(d);  // allocates + copies synchronously
+      else {
+        PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, c->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_d2h));
+        PARSEC_HIP_CHECK(hipStreamSynchronize(s_d2h));
+        stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
+        std::lock_guard<SpinLock> g(d->lock);
+        host->version = c->version;
+        host->coherency_state = COHERENCY_SHARED;
+        d->owner_device = 0;
+      }
+      if (!drop(c)) lru_touch(c);
+    } else {
+      lru_touch(c);
+    }
+    it = nx;
+  }
+  return freed >= bytes;
+}
+
+void* HipDevice::cache_alloc(size_t bytes) {
+  if (!zone) {
+    size_t freeb = 0, total = 0;
+    (void)hipMemGetInfo(&freeb, &total);
+    double pct = (double)ParamRegistry::instance().reg_int("device", "hip", "memory_use", "Percent of free HBM the tile cache may use", 90);
+    size_t seg = ParamRegistry::instance().reg_sizet("device", "hip", "memory_block_size", "Tile-cache segment size (bytes)", (size_t)1 << 30);
+    size_t unit = ParamRegistry::instance().reg_sizet("device", "hip", "memory_unit", "Tile-cache allocation granule (bytes)", 4096);
+    size_t maxb = ParamRegistry::instance().reg_sizet("device", "hip", "memory_max", "Hard cap of the tile cache (bytes, 0 = percent rule)", 0);
+    zone_max = maxb ? maxb : (size_t)(freeb * pct / 100.0);
+    zone = std::make_unique<ZoneAllocator>(ordinal, zone_max, seg, unit);
+  }
+  void* p = zone->alloc(bytes);
+  if (!p && evict(bytes)) p = zone->alloc(bytes);
+  return p;
+}
+
+// --------------------------------------------------------------- staging
+// 0: ready now, 1: transfers in flight, -1: out of memory (retry later)
+int HipDevice::stage_in(GpuTask* g) {
+  Task* t = g->task;
+  const TaskClass* tc = t->task_class;
+  bool any = false;
+  for (auto& f : tc->flows) {
+    if (f.access == FLOW_CTL || f.access == FLOW_NONE) continue;
+    DataCopy* c = t->data[f.index].data_in;
+    if (!c || !c->original) continue;
+    g->flows |= 1u << f.index;
+    g->access[f.index] = f.access;
+  }
+  for (int fi = 0; fi < kMaxFlows; ++fi) {
+    if (!(g->flows & (1u << fi)) || g->dev_copy[fi]) continue;
+    DataCopy* c = t->data[fi].data_in;
+    Data* d = c->original;
+    DataCopy* local = d->copy(device_index);
+    if (!local) {
+      void* p = cache_alloc(d->nb_elts);
+      if (!p) return -1;
+      auto* nc = new DataCopy();
+      nc->device_private = p;
+      nc->flags = DATA_FLAG_PARSEC_OWNED;
+      nc->coherency_state = COHERENCY_INVALID;
+      nc->dtt = c->dtt;
+      nc->dev_state = new DevCopyState();
+      {
+        std::lock_guard<SpinLock> lk(d->lock);
+        local = d->copy(device_index);
+        if (!local) { data_copy_attach(d, nc, device_index); local = nc; }
+      }
+      if (local != nc) { zone->free(p); delete static_cast<DevCopyState*>(nc->dev_state); delete nc; }
+    }
+    if (!local->dev_state) {
+      auto* st = new DevCopyState();
+      st->cache_managed = false;  // collection storage in HBM: never evicted
+      local->dev_state = st;
+    }
+    lru_remove(local);
+    local->readers.fetch_add(1);
+    g->dev_copy[fi] = local;
+    if (local->transfer_status == TRANSFER_UNDER) { any = true; continue; }  // ordered behind the in-flight copy on s_h2d
+    DataCopy* src = data_start_transfer_ownership_to_copy(d, device_index, g->access[fi]);
+    if (src && src != local) {
+      hipMemcpyKind k = src->device_index == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+      if (k == hipMemcpyDeviceToDevice) {
+        int src_ord = device_hip_ordinal(src->device_index);
+        PARSEC_HIP_CHECK(hipMemcpyPeerAsync(local->device_private, ordinal, src->device_private, src_ord, d->nb_elts, s_h2d));
+        stats.bytes_d2d.fetch_add(d->nb_elts, std::memory_order_relaxed);
+      } else {
+        PARSEC_HIP_CHECK(hipMemcpyAsync(local->device_private, src->device_private, d->nb_elts, k, s_h2d));
+        stats.bytes_in.fetch_add(d->nb_elts, std::memory_order_relaxed);
+      }
+      local->transfer_status = TRANSFER_UNDER;
+      local->push_task = g;
+      g->issued_copy[fi] = true;
+      any = true;
+    }
+  }
+  if (!any) return 0;
+  g->ev_in = get_event();
+  PARSEC_HIP_CHECK(hipEventRecord(g->ev_in, s_h2d));
+  return 1;
+}
+
+void HipDevice::finish_stage_in(GpuTask* g) {
+  for (int fi = 0; fi < kMaxFlows; ++fi) {
+    if (!g->issued_copy[fi]) continue;
+    DataCopy* local = g->dev_copy[fi];
+    data_end_transfer_ownership_to_copy(local->original, device_index, g->access[fi]);
+    local->push_task = nullptr;
+  }
+  if (g->ev_in) { put_event(g->ev_in); g->ev_in = nullptr; }
+}
+
+// ------------------------------------------------------------- execution
+void HipDevice::execute_ready() {
+  if (ready.empty()) return;
+  std::stable_sort(ready.begin(), ready.end(), [](GpuTask* a, GpuTask* b) { return a->task->priority > b->task->priority; });
+  std::vector<GpuTask*> again;
+  for (GpuTask* g : ready) {
+    Task* t = g->task;
+    const Chore& ch = t->task_class->chores[g->chore];
+    int s;
+    if (nb_exec_streams == 1) s = 0;
+    else if (t->priority >= high_prio_threshold || (t->task_class->flags & TC_HIGH_PRIORITY)) s = 0;
+    else s = 1 + (int)(rr_stream++ % (uint32_t)(nb_exec_streams - 1));
+    GpuExecContext ctxg;
+    ctxg.dev = this;
+    ctxg.device = this;
+    ctxg.stream = s_exec[s];
+    ctxg.stream_index = s;
+    ctxg.task = t;
+    ctxg.batch = batching ? &batches[s] : nullptr;
+    for (int fi = 0; fi < kMaxFlows; ++fi) ctxg.flow_ptr[fi] = g->dev_copy[fi] ? g->dev_copy[fi]->device_private : nullptr;
+    KernelBatch local_batch;
+    if (!batching) ctxg.batch = &local_batch;
+    PARSEC_PINS(es, PINS_EXEC_BEGIN, t);
+    int rc = ch.gpu_hook ? ch.gpu_hook(&ctxg, t) : HOOK_NEXT;
+    PARSEC_PINS(es, PINS_EXEC_END, t);
+    if (!batching && !local_batch.empty()) {
+      launch_kernel_batch(local_batch, s_exec[s], ordinal);
+      stats.kernel_launches.fetch_add(1, std::memory_order_relaxed);
+    }
+    if (rc == HOOK_DONE) {
+      g->stream = s;
+      round_tasks[s].push_back(g);
+    } else if (rc == HOOK_AGAIN) {
+      again.push_back(g);
+    } else {
+      // give the task back to the runtime without this chore
+      for (int fi = 0; fi < kMaxFlows; ++fi)
+        if (g->dev_copy[fi]) { g->dev_copy[fi]->readers.fetch_sub(1); lru_touch(g->dev_copy[fi]); }
+      load.fetch_sub((int64_t)g->load, std::memory_order_relaxed);
+      t->gpu = nullptr;
+      t->chore_mask &= ~(1u << g->chore);
+      t->selected_device = -1;
+      delete g;
+      inflight.fetch_sub(1);
+      schedule_task(es, t, 1);
+    }
+  }
+  ready.swap(again);
+  for (int s = 0; s < nb_exec_streams; ++s) {
+    if (round_tasks[s].empty()) continue;
+    if (!batches[s].empty()) {
+      launch_kernel_batch(batches[s], s_exec[s], ordinal);
+      stats.kernel_launches.fetch_add(1, std::memory_order_relaxed);
+      batches[s].clear();
+    }
+    ExecGroup grp;
+    grp.ev = get_event();
+    PARSEC_HIP_CHECK(hipEventRecord(grp.ev, s_exec[s]));
+    grp.tasks.swap(round_tasks[s]);
+    grp.t_launch = now_ns();
+    stats.batched_tasks.fetch_add(grp.tasks.size(), std::memory_order_relaxed);
+    executing[s].push_back(std::move(grp));
+  }
+}
+
+void HipDevice::epilog(GpuTask* g) {
+  Task* t = g->task;
+  for (int fi = 0; fi < kMaxFlows; ++fi) {
+    DataCopy* local = g->dev_copy[fi];
+    if (!local) continue;
+    Data* d = local->original;
+    if (g->access[fi] & FLOW_WRITE) {
+      std::lock_guard<SpinLock> lk(d->lock);
+      uint32_t v = 0;
+      for (int i = 0; i < kMaxDevices; ++i) { DataCopy* o = d->copy(i); if (o && o->coherency_state != COHERENCY_INVALID) v = std::max(v, o->version); }
+      local->version = v + 1;
+      local->coherency_state = COHERENCY_OWNED;
+      d->owner_device = (int8_t)device_index;
+      if (t->data[fi].data_out != local) {
+        if (t->data[fi].data_out && t->data[fi].data_out != t->data[fi].data_in) data_copy_release(t->data[fi].data_out);
+        data_copy_retain(local);
+        t->data[fi].data_out = local;
+      }
+    }
+    local->readers.fetch_sub(1);
+  }
+}
+
+void HipDevice::complete(GpuTask* g) {
+  Task* t = g->task;
+  for (int fi = 0; fi < kMaxFlows; ++fi) if (g->dev_copy[fi]) lru_touch(g->dev_copy[fi]);
+  load.fetch_sub((int64_t)g->load, std::memory_order_relaxed);
+  stats.executed_tasks.fetch_add(1, std::memory_order_relaxed);
+  t->gpu = nullptr;
+  if (g->ev_out) put_event(g->ev_out);
+  delete g;
+  complete_task_execution(es, t);
+  inflight.fetch_sub(1, std::memory_order_acq_rel);
+}
+
+bool HipDevice::progress() {
+  bool did = false;
+  if (incoming_n.load(std::memory_order_acquire) > 0) {
+    std::vector<GpuTask*> in;
+    {
+      std::lock_guard<std::mutex> lk(in_m);
+      in.swap(incoming);
+      incoming_n.store(0);
+    }
+    for (GpuTask* g : in) { g->t_submit = now_ns(); pending.push_back(g); }
+    did = true;
+  }
+  // stage in
+  if (!pending.empty()) {
+    if (sort_pending && pending.size() > 1)
+      std::stable_sort(pending.begin(), pending.end(), [](GpuTask* a, GpuTask* b) { return a->task->priority > b->task->priority; });
+    std::vector<GpuTask*> keep;
+    for (GpuTask* g : pending) {
+      int rc = stage_in(g);
+      if (rc == 0) ready.push_back(g);
+      else if (rc == 1) staging.push_back(g);
+      else keep.push_back(g);
+    }
+    pending.swap(keep);
+    did = true;
+  }
+  // transfers done?
+  if (!staging.empty()) {
+    std::vector<GpuTask*> keep;
+    for (GpuTask* g : staging) {
+      if (g->ev_in && hipEventQuery(g->ev_in) == hipErrorNotReady) { keep.push_back(g); continue; }
+      finish_stage_in(g);
+      ready.push_back(g);
+      did = true;
+    }
+    staging.swap(keep);
+  }
+  if (!ready.empty()) { execute_ready(); did = true; }
+  // kernels done?
+  for (int s = 0; s < nb_exec_streams; ++s) {
+    auto& q = executing[s];
+    while (!q.empty()) {
+      ExecGroup& grp = q.front();
+      hipError_t e = hipEventQuery(grp.ev);
+      if (e == hipErrorNotReady) break;
+      if (e != hipSuccess) fatal("GPU kernel failure on device %d: %s", ordinal, hipGetErrorString(e));
+      put_event(grp.ev);
+      std::vector<GpuTask*> tasks;
+      tasks.swap(grp.tasks);
+      q.pop_front();
+      for (GpuTask* g : tasks) {
+        epilog(g);
+        if (g->pushout) {
+          for (int fi = 0; fi < kMaxFlows; ++fi) {
+            if (!(g->pushout & (1u << fi)) || !g->dev_copy[fi]) continue;
+            Data* d = g->dev_copy[fi]->original;
+            DataCopy* host = d->copy(0);
+            if (!host) { host = data_pull_to_host(d); continue; }
+            PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, g->dev_copy[fi]->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_d2h));
+            stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
+          }
+          g->ev_out = get_event();
+          PARSEC_HIP_CHECK(hipEventRecord(g->ev_out, s_d2h));
+          popping.push_back(g);
+        } else {
+          complete(g);
+        }
+      }
+      did = true;
+    }
+  }
+  while (!popping.empty()) {
+    GpuTask* g = popping.front();
+    if (hipEventQuery(g->ev_out) == hipErrorNotReady) break;
+    popping.pop_front();
+    for (int fi = 0; fi < kMaxFlows; ++fi) {
+      if (!(g->pushout & (1u << fi)) || !g->dev_copy[fi]) continue;
+      Data* d = g->dev_copy[fi]->original;
+      std::lock_guard<SpinLock> lk(d->lock);
+      if (DataCopy* host = d->copy(0)) { host->version = g->dev_copy[fi]->version; host->coherency_state = COHERENCY_SHARED; }
+    }
+    complete(g);
+    did = true;
+  }
+  return did;
+}
+
+void HipDevice::manager_main() {
+  (void)hipSetDevice(ordinal);
+  set_my_execution_stream(es);
+  es->slot = thread_slot();
+  profiling_thread_init(es);
+  Backoff backoff;
+  for (;;) {
+    bool did = progress();
+    if (did) { backoff.reset(); continue; }
+    if (inflight.load(std::memory_order_acquire) > 0) {
+      // work in flight on the GPU: poll tightly, yielding now and then
+      if (backoff.misses() < 2000) { PARSEC_CPU_RELAX(); backoff.idle(); }
+      else std::this_thread::yield();
+      continue;
+    }
+    if (stop.load()) break;
+    std::unique_lock<std::mutex> lk(in_m);
+    in_cv.wait_for(lk, std::chrono::milliseconds(2), [&] { return stop.load() || incoming_n.load() > 0; });
+    backoff.reset();
+  }
+  profiling_thread_fini(es);
+}
+
+// ================================================================ module
+static std::vector<HipDevice*> g_hip_devices;
+
+void hip_devices_init(Context* ctx) {
+  (void)ctx;
+  auto& params = ParamRegistry::instance();
+  int enabled = (int)params.reg_int("device", "hip", "enabled", "Enable the HIP device module (number of GPUs, -1 = all)", -1);
+  int64_t mask = params.reg_int("device", "hip", "mask", "Bit mask of HIP ordinals to use", -1);
+  g_nb_exec_streams = (int)params.reg_int("device", "hip", "max_streams", "Execution streams per GPU (stream 0 is high priority)", 4);
+  int batching = (int)params.reg_int("device", "hip", "batching", "Group ready tile kernels of one kind into one launch", 1);
+  int hp = (int)params.reg_int("device", "hip", "high_priority_threshold", "Task priority at or above which the high-priority stream is used", 1 << 27);
+  int sortp = (int)params.reg_int("device", "hip", "sort_pending_tasks", "Sort pending GPU tasks by priority", 1);
+  if (enabled == 0) return;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) { (void)hipGetLastError(); return; }
+  auto& reg = DeviceRegistry::instance();
+  for (int o = 0; o < count; ++o) {
+    if (mask >= 0 && !(mask & (1LL << o))) continue;
+    if (enabled > 0 && (int)g_hip_devices.size() >= enabled) break;
+    auto* d = new HipDevice();
+    d->ordinal = o;
+    (void)hipGetDeviceProperties(&d->props, o);
+    d->name = "hip" + std::to_string(o);
+    d->type = DEV_HIP;
+    // fp64 MFMA: 2048 flop / 64 cycles per SIMD -> 32 flop/clk/SIMD (measured 77.6 TF on MI355X)
+    double ghz = d->props.clockRate > 0 ? d->props.clockRate / 1e6 : 2.4;
+    d->gflops_fp64 = d->props.multiProcessorCount * 4 * 32.0 * ghz;
+    d->gflops_fp32 = 2 * d->gflops_fp64;
+    d->nb_exec_streams = std::max(1, g_nb_exec_streams);
+    d->batching = batching != 0;
+    d->high_prio_threshold = hp;
+    d->sort_pending = sortp != 0;
+    reg.add(d);
+    g_hip_devices.push_back(d);
+  }
+  // peer access between the GPUs this process drives (xGMI)
+  for (auto* a : g_hip_devices)
+    for (auto* b : g_hip_devices) {
+      if (a == b) continue;
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, a->ordinal, b->ordinal) == hipSuccess && can) {
+        (void)hipSetDevice(a->ordinal);
+        if (hipDeviceEnablePeerAccess(b->ordinal, 0) != hipSuccess) (void)hipGetLastError();
+      }
+    }
+  if (!g_hip_devices.empty()) (void)hipSetDevice(g_hip_devices[0]->ordinal);
+}
+
+void hip_devices_start(Context* ctx) {
+  for (auto* d : g_hip_devices) d->start(ctx);
+}
+
+void hip_devices_stop(Context* ctx) {
+  (void)ctx;
+  for (auto* d : g_hip_devices) d->quiesce();
+}
+
+}  // namespace parsec

@@ -1,0 +1,150 @@
+// HIP device module (native, gfx950). One manager thread per GPU owns the
+// device's streams: h2d, d2h and N exec streams (exec[0] is a high-priority
+// stream for critical-path tasks). Ready GPU tasks are staged in, their
+// bodies enqueue tile kernels into per-stream batches which are flushed as one
+// grouped launch per kind, and completion is detected by polling one event per
+// launch group.
+//
+// Parity: reference mca/device/cuda/device_cuda_module.c — module init with
+// streams/events (:326-547), zone memory + LRU reservation with eviction
+// (:613-743, :864-1168), stage_in/stage_out (:1180-1530), progress_stream /
+// push / pop / epilog (:1961-2453), kernel scheduler (:2537-2763), W2R flush
+// task (transfer_gpu.c:222-337), peer access (device_cuda_component.c:139-150).
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <deque>
+#include <map>
+#include <thread>
+
+#include "device.hpp"
+
+namespace parsec {
+
+// First-fit allocator over large hipMalloc segments (reference zone_malloc.c).
+class ZoneAllocator {
+ public:
+  ZoneAllocator(int ordinal, size_t max_bytes, size_t segment_bytes, size_t unit);
+  ~ZoneAllocator();
+  void* alloc(size_t bytes);
+  void free(void* p);
+  size_t used() const { return used_; }
+  size_t reserved() const { return reserved_; }
+  size_t max_bytes() const { return max_bytes_; }
+ private:
+  struct Segment {
+    char* base;
+    size_t size;
+    std::map<size_t, size_t> free_;  // offset -> size
+  };
+  int ordinal_;
+  size_t max_bytes_, seg_bytes_, unit_;
+  size_t used_ = 0, reserved_ = 0;
+  std::vector<Segment> segs_;
+  std::map<void*, std::pair<size_t, size_t>> live_;  // ptr -> (segment, size)
+};
+
+enum GpuTaskKind : int { GPU_TASK_KERNEL = 0x0, GPU_TASK_D2H_W2R = 0x1000, GPU_TASK_PREFETCH = 0x2000, GPU_TASK_WARMUP = 0x4000 };
+
+struct GpuTask {
+  Task* task = nullptr;
+  int chore = 0;
+  int kind = GPU_TASK_KERNEL;
+  uint32_t flows = 0;        // data flows handled by the engine
+  uint32_t pushout = 0;      // flows copied back to the host after execution
+  uint8_t access[kMaxFlows] = {};
+  DataCopy* dev_copy[kMaxFlows] = {};
+  bool issued_copy[kMaxFlows] = {};
+  hipEvent_t ev_in = nullptr;
+  hipEvent_t ev_out = nullptr;
+  int stream = -1;
+  double load = 0;
+  uint64_t t_submit = 0, t_exec = 0;
+};
+
+struct DevCopyState {  // DataCopy::dev_state for engine-managed copies
+  bool in_lru = false;
+  bool owned_lru = false;
+  bool cache_managed = true;  // allocated from the zone (evictable)
+};
+
+struct ExecGroup {
+  hipEvent_t ev = nullptr;
+  std::vector<GpuTask*> tasks;
+  uint64_t t_launch = 0;
+};
+
+struct HipDevice : Device {
+  int ordinal = 0;
+  hipDeviceProp_t props{};
+  int nb_exec_streams = 4;
+  hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+  std::vector<hipStream_t> s_exec;
+  std::unique_ptr<ZoneAllocator> zone;
+  size_t zone_max = 0;
+  // LRUs: clean copies (can be dropped) and owned copies (need write-back)
+  List lru_clean, lru_owned;
+  // incoming queue from submitters
+  std::mutex in_m;
+  std::condition_variable in_cv;
+  std::vector<GpuTask*> incoming;
+  std::atomic<int> incoming_n{0};
+  // manager-thread private state
+  std::vector<GpuTask*> pending, staging, ready;
+  std::vector<std::deque<ExecGroup>> executing;
+  std::deque<GpuTask*> popping;
+  std::vector<hipEvent_t> event_pool;
+  std::vector<KernelBatch> batches;
+  std::vector<std::vector<GpuTask*>> round_tasks;
+  std::vector<void*> stream_workspace;
+  std::vector<size_t> stream_workspace_size;
+  std::thread manager;
+  std::atomic<bool> stop{false};
+  std::atomic<int64_t> inflight{0};
+  ExecutionStream* es = nullptr;
+  Context* ctx = nullptr;
+  int high_prio_threshold = 1 << 30;
+  bool batching = true;
+  bool sort_pending = true;
+  int max_inflight_groups = 64;
+  uint32_t rr_stream = 0;
+  double us_busy = 0;
+
+  bool is_gpu() const override { return true; }
+  int attach(Context* c) override;
+  int detach(Context* c) override;
+  int submit(ExecutionStream* es, Task* t, int chore) override;
+  int memory_register(DataCollection* dc, void* ptr, size_t len) override;
+  int memory_unregister(DataCollection* dc, void* ptr) override;
+  void quiesce() override;
+  void start(Context* c);
+  void shutdown();
+
+  // manager internals
+  void manager_main();
+  bool progress();
+  int stage_in(GpuTask* g);
+  void finish_stage_in(GpuTask* g);
+  void execute_ready();
+  void complete(GpuTask* g);
+  void epilog(GpuTask* g);
+  void* cache_alloc(size_t bytes);
+  bool evict(size_t bytes);
+  hipEvent_t get_event();
+  void put_event(hipEvent_t e);
+  void lru_touch(DataCopy* c);
+  void lru_remove(DataCopy* c);
+  void* workspace(int stream, size_t bytes);
+};
+
+void hip_devices_init(Context* ctx);
+void hip_devices_start(Context* ctx);
+void hip_devices_stop(Context* ctx);
+
+#define PARSEC_HIP_CHECK(expr)                                                             \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess) ::parsec::fatal("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
+  } while (0)
+
+}  // namespace parsec

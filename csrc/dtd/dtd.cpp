@@ -1,0 +1,548 @@
+#include "dtd.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "../comm/comm.hpp"
+#include "../device/device.hpp"
+#include "../prof/profiling.hpp"
+
+namespace parsec {
+namespace dtd {
+
+static void task_retain(DtdTask* t) { t->refs.fetch_add(1, std::memory_order_relaxed); }
+static void task_unref(DtdTask* t);
+
+void tile_release(Tile* t) {
+  if (t->refcount.fetch_sub(1) == 1) {
+    if (t->is_new && t->data) data_destroy(t->data);
+    delete t;
+  }
+}
+
+// ================================================================ taskpool
+DtdTaskpool::DtdTaskpool() {
+  taskpool_name = "dtd";
+  is_dtd = true;
+  auto& reg = ParamRegistry::instance();
+  window = reg.reg_int("dtd", "", "window_size", "Tasks in flight before the inserting thread starts executing", 8000);
+  threshold = reg.reg_int("dtd", "", "threshold_size", "Tasks in flight at which the inserting thread resumes inserting", 4000);
+}
+
+DtdTaskpool::~DtdTaskpool() {
+  tiles.for_each([](uint64_t, Tile* t) {
+    if (t->writer) task_unref(t->writer);
+    for (auto& r : t->readers) task_unref(r.first);
+    t->writer = nullptr;
+    t->readers.clear();
+    tile_release(t);
+  });
+  tiles.clear();
+  remote_tasks.for_each([](uint64_t, DtdTask* t) { task_unref(t); });
+  remote_tasks.clear();
+  for (Tile* t : new_tiles) tile_release(t);
+  for (auto* c : classes) delete c;
+}
+
+void DtdTaskpool::arm_hold() {
+  bool exp = false;
+  if (hold.compare_exchange_strong(exp, true)) {
+    tdm->taskpool_addto_nb_tasks(this, 1);
+    tdm->taskpool_addto_runtime_actions(this, 1);
+  }
+}
+
+void DtdTaskpool::release_hold() {
+  bool exp = true;
+  if (hold.compare_exchange_strong(exp, false)) {
+    tdm->taskpool_addto_runtime_actions(this, -1);
+    tdm->taskpool_addto_nb_tasks(this, -1);
+  }
+}
+
+void DtdTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
+  (void)ctx; (void)ready;
+  hold.store(false);
+  tdm->taskpool_set_nb_tasks(this, 0);
+  arm_hold();
+}
+
+void DtdTaskpool::on_context_wait() {
+  wait();
+  release_hold();
+}
+
+DtdTaskClass* DtdTaskpool::create_task_class(const std::string& name, const std::vector<std::pair<int, int>>& params) {
+  std::lock_guard<std::mutex> g(classes_m);
+  auto it = classes_by_name.find(name);
+  if (it != classes_by_name.end()) return it->second;
+  auto* tc = new DtdTaskClass();
+  tc->owner = this;
+  tc->name = name;
+  tc->task_class_id = (uint16_t)classes.size();
+  tc->nb_params = 1;
+  tc->nb_locals = 1;
+  int nf = 0;
+  for (auto& p : params) {
+    tc->param_ops.push_back(p.first);
+    tc->param_sizes.push_back(p.second);
+    int op = p.first & OP_MASK;
+    if (op == INPUT || op == OUTPUT || op == INOUT || op == ATOMIC_WRITE) {
+      if (nf >= kMaxFlows) fatal("DTD task class %s has more than %d data arguments", name.c_str(), kMaxFlows);
+      uint8_t acc = op == INPUT ? FLOW_READ : op == OUTPUT ? FLOW_WRITE : FLOW_RW;
+      tc->flows.push_back(Flow{"f" + std::to_string(nf), acc, (uint8_t)nf});
+      ++nf;
+    }
+  }
+  classes.push_back(tc);
+  task_classes.push_back(tc);
+  classes_by_name[name] = tc;
+  return tc;
+}
+
+int DtdTaskpool::add_chore(DtdTaskClass* tc, uint32_t device_type, Hook cpu, std::function<int(GpuExecContext*, Task*)> gpu) {
+  Chore ch;
+  ch.type = device_type;
+  ch.hook = std::move(cpu);
+  ch.gpu_hook = std::move(gpu);
+  // GPU chores first so the device engine gets the first chance
+  if (device_type & DEV_GPU_MASK) tc->chores.insert(tc->chores.begin(), std::move(ch));
+  else tc->chores.push_back(std::move(ch));
+  return 0;
+}
+
+static uint64_t tile_key(DataCollection* dc, uint64_t key) { return ((dc ? dc->dc_id : 0) << 48) ^ (key & 0xFFFFFFFFFFFFULL); }
+
+Tile* DtdTaskpool::tile_of(DataCollection* dc, uint64_t key) {
+  uint64_t k = tile_key(dc, key);
+  return tiles.with(k, [&](auto& m) {
+    auto it = m.find(k);
+    if (it != m.end()) return it->second;
+    Tile* t = new Tile();
+    t->dc = dc;
+    t->key = key;
+    t->rank = (int)dc->rank_of_key(key);
+    t->data = dc->data_of_key(key);
+    if (!t->data) {
+      // remote tile: a local shadow Data receives the versions sent to us
+      t->data = data_new();
+      t->data->dc = dc;
+      t->data->key = key;
+      t->data->nb_elts = (size_t)std::max<int64_t>(dc->default_dtt.extent_bytes(), 0);
+      t->is_new = true;
+    }
+    m[k] = t;
+    return t;
+  });
+}
+
+Tile* DtdTaskpool::tile_new(size_t bytes, int rank) {
+  Tile* t = new Tile();
+  t->rank = rank;
+  t->is_new = true;
+  if (rank == (context ? context->my_rank : 0)) {
+    void* p = nullptr;
+    if (posix_memalign(&p, 64, std::max<size_t>(bytes, 64))) fatal("tile_new: out of memory");
+    std::memset(p, 0, bytes);
+    t->data = data_create(nullptr, nullptr, 0, p, bytes, DATA_FLAG_PARSEC_MANAGED | DATA_FLAG_PARSEC_OWNED, 0);
+  } else {
+    t->data = data_new();
+    t->data->nb_elts = bytes;
+  }
+  std::lock_guard<std::mutex> g(new_tiles_m);
+  new_tiles.push_back(t);
+  t->refcount.fetch_add(1);
+  return t;
+}
+
+// add a dependency pred -> succ unless pred already completed
+static bool add_edge(DtdTask* pred, DtdTask* succ, int src_flow, int dst_flow, bool data) {
+  std::lock_guard<SpinLock> g(pred->lock);
+  if (pred->completed) return false;
+  pred->succ.push_back(Edge{succ, dst_flow, src_flow, data});
+  succ->deps.fetch_add(1, std::memory_order_relaxed);
+  task_retain(succ);
+  return true;
+}
+
+DtdTask* DtdTaskpool::insert_task(DtdTaskClass* tc, int priority, const std::vector<Arg>& in_args) {
+  Context* ctx = context;
+  if (!ctx) fatal("insert_task on a DTD taskpool that is not attached to a context");
+  const int my = ctx->my_rank;
+  auto* t = new DtdTask();
+  t->taskpool = this;
+  t->task_class = tc;
+  t->priority = priority + this->priority;
+  t->seq = seq.fetch_add(1);
+  t->key = t->seq;
+  t->locals[0] = (int32_t)t->seq;
+  t->args = in_args;
+  // copy values into task-owned storage
+  size_t vbytes = 0;
+  for (auto& a : t->args) if ((a.op & OP_MASK) == VALUE) vbytes += (size_t)a.size;
+  t->values.resize(vbytes);
+  size_t off = 0;
+  int nf = 0;
+  int rank = -1;
+  for (auto& a : t->args) {
+    int op = a.op & OP_MASK;
+    if (op == VALUE) {
+      if (a.size > 0 && a.ptr) std::memcpy(t->values.data() + off, a.ptr, (size_t)a.size);
+      a.ptr = t->values.data() + off;
+      off += (size_t)a.size;
+    } else if ((op == INPUT || op == OUTPUT || op == INOUT || op == ATOMIC_WRITE)) {
+      a.flow = nf++;
+      if (a.tile) {
+        a.tile->refcount.fetch_add(1);
+        if ((a.op & AFFINITY) && rank < 0) rank = a.tile->rank;
+      }
+    }
+  }
+  t->nb_flows = nf;
+  if (rank < 0) for (auto& a : t->args) if (a.flow >= 0 && a.tile) { rank = a.tile->rank; break; }
+  if (rank < 0) rank = my;
+  t->rank = rank;
+  t->remote = rank != my;
+  if (!t->remote) tdm->taskpool_addto_nb_tasks(this, 1);
+  else {
+    task_retain(t);
+    remote_tasks.insert(t->seq, t);
+  }
+  // dependency tracking per tile
+  for (auto& a : t->args) {
+    if (a.flow < 0 || !a.tile || (a.op & DONT_TRACK)) continue;
+    Tile* tl = a.tile;
+    int op = a.op & OP_MASK;
+    std::lock_guard<SpinLock> g(tl->lock);
+    if (op == INPUT) {
+      if (tl->writer) add_edge(tl->writer, t, tl->writer_flow, a.flow, true);
+      task_retain(t);
+      tl->readers.emplace_back(t, a.flow);
+    } else {
+      if (tl->writer) add_edge(tl->writer, t, tl->writer_flow, a.flow, true);
+      for (auto& r : tl->readers) {
+        if (r.first != t) add_edge(r.first, t, r.second, a.flow, false);
+        task_unref(r.first);
+      }
+      tl->readers.clear();
+      if (tl->writer) task_unref(tl->writer);
+      task_retain(t);
+      tl->writer = t;
+      tl->writer_flow = a.flow;
+      tl->last_writer_rank = rank;
+      ++tl->version;
+    }
+  }
+  // activations that arrived before this (remote) task was discovered
+  if (t->remote) {
+    for (int f = 0; f < t->nb_flows; ++f) {
+      RemoteActivation* act = nullptr;
+      uint64_t k = (t->seq << 6) | (uint64_t)f;
+      if (early.find(k, act)) {
+        early.erase(k);
+        ExecutionStream* es = my_execution_stream();
+        on_remote_activation(es ? es : ctx->all_es[0], *act);
+        for (auto*& c : act->data) if (c) { data_copy_release(c); c = nullptr; }
+        delete act;
+      }
+    }
+  }
+  // drop the insertion guard
+  if (t->deps.fetch_sub(1) == 1 && !t->remote) {
+    ExecutionStream* es = my_execution_stream();
+    if (!es || es->ctx != ctx) es = ctx->all_es[0];
+    Task* tt = t;
+    ctx->scheduler->schedule(es, &tt, 1, 0);
+  }
+  // sliding window
+  if (!t->remote && nb_tasks.load(std::memory_order_relaxed) > window) execute_and_come_back(threshold);
+  return t;
+}
+
+void DtdTaskpool::execute_and_come_back(int64_t thr) {
+  Context* ctx = context;
+  ExecutionStream* prev = my_execution_stream();
+  ExecutionStream* es = prev && prev->ctx == ctx ? prev : ctx->all_es[0];
+  set_my_execution_stream(es);
+  if (!ctx->started.load()) context_start(ctx);
+  Backoff b;
+  while (nb_tasks.load() > thr) {
+    Task* t = es->next_task;
+    int32_t dist = 0;
+    if (t) es->next_task = nullptr;
+    else t = ctx->scheduler->select(es, &dist);
+    if (t) { b.reset(); task_progress(es, t, dist); }
+    else b.idle();
+  }
+  set_my_execution_stream(prev);
+}
+
+int DtdTaskpool::wait() {
+  if (!context) return -1;
+  int64_t base = hold.load() ? 1 : 0;
+  execute_and_come_back(base);
+  Backoff b;
+  while (nb_pending_actions.load() > base) b.idle();
+  return 0;
+}
+
+int DtdTaskpool::data_flush(Tile* tile) {
+  if (!tile || !tile->dc) return 0;
+  // A no-op CPU task reading the tile on its owner: the CPU staging of the
+  // engine brings the newest version home (GPU -> host, or remote -> owner).
+  if (tile->dc->home_device() != 0) return 0;
+  DtdTaskClass* tc = create_task_class("parsec_dtd_data_flush", {{INPUT | AFFINITY, (int)PASSED_BY_REF}});
+  if (tc->chores.empty()) add_chore(tc, DEV_CPU, [](ExecutionStream*, Task*) { return HOOK_DONE; }, nullptr);
+  Arg a;
+  a.op = INPUT | AFFINITY;
+  a.size = PASSED_BY_REF;
+  a.tile = tile;
+  insert_task(tc, INT32_MAX / 2, {a});
+  return 0;
+}
+
+int DtdTaskpool::data_flush_all(DataCollection* dc) {
+  std::vector<Tile*> ts;
+  tiles.for_each([&](uint64_t, Tile* t) { if (t->dc == dc) ts.push_back(t); });
+  std::sort(ts.begin(), ts.end(), [](Tile* a, Tile* b) { return a->key < b->key; });  // identical order on all ranks
+  for (Tile* t : ts) data_flush(t);
+  return 0;
+}
+
+// ============================================================ task class
+static DataCopy* newest_copy(Data* d) {
+  DataCopy* best = nullptr;
+  for (int i = 0; i < kMaxDevices; ++i) {
+    DataCopy* c = d->copy(i);
+    if (!c || c->coherency_state == COHERENCY_INVALID) continue;
+    if (!best || c->version > best->version || (c->version == best->version && i == d->owner_device)) best = c;
+  }
+  return best;
+}
+
+int DtdTaskClass::prepare_input(ExecutionStream* es, Task* tt) const {
+  (void)es;
+  auto* t = static_cast<DtdTask*>(tt);
+  for (auto& a : t->args) {
+    int op = a.op & OP_MASK;
+    if (op == SCRATCH) {
+      void* p = nullptr;
+      if (posix_memalign(&p, 64, std::max(64, a.size))) return HOOK_ERROR;
+      t->scratch.push_back(p);
+      a.ptr = p;
+    }
+    if (a.flow < 0 || !a.tile) continue;
+    TaskDataRef& r = t->data[a.flow];
+    if (r.data_in) continue;
+    Data* d = a.tile->data;
+    if (!d) continue;
+    DataCopy* c = newest_copy(d);
+    if (!c) continue;
+    data_copy_retain(c);
+    r.data_in = c;
+  }
+  return HOOK_DONE;
+}
+
+std::string DtdTaskClass::describe(const Task* t) const { return name + "[" + std::to_string(static_cast<const DtdTask*>(t)->seq) + "]"; }
+
+void DtdTaskClass::iterate_successors(ExecutionStream* es, const Task* tt, uint32_t mask, const DepVisitor& v) const {
+  (void)es;
+  auto* t = static_cast<const DtdTask*>(tt);
+  std::lock_guard<SpinLock> g(const_cast<DtdTask*>(t)->lock);
+  for (auto& e : t->succ) {
+    if (!(mask & (1u << e.src_flow))) continue;
+    DepVisit vis;
+    vis.tc = e.task->task_class;
+    vis.locals = e.task->locals;
+    vis.nb_locals = 1;
+    vis.src_flow = e.src_flow;
+    vis.dst_flow = e.dst_flow;
+    vis.rank = (uint32_t)e.task->rank;
+    v(vis);
+  }
+}
+
+// Called when `t` completed locally (local task) or its activation arrived (remote shadow).
+static void release_successors(ExecutionStream* es, DtdTask* t, uint32_t flow_mask, DataCopy* const* recv_data, std::vector<Task*>& ready, RemoteDepsMsg*& msg) {
+  std::vector<Edge> edges;
+  {
+    std::lock_guard<SpinLock> g(t->lock);
+    if (flow_mask == 0xffffffffu) {
+      t->completed = true;
+      edges.swap(t->succ);
+    } else {
+      // remote shadow: release only the edges of the activated flows
+      std::vector<Edge> keep;
+      for (auto& e : t->succ) (flow_mask & (1u << e.src_flow) ? edges : keep).push_back(e);
+      t->succ.swap(keep);
+      bool all = true;
+      for (int f = 0; f < t->nb_flows; ++f) if (!(flow_mask & (1u << f))) all = false;
+      if (all || t->succ.empty()) t->completed = true;
+    }
+  }
+  DtdTaskpool* tp = static_cast<DtdTaskpool*>(t->taskpool);
+  const int my = tp->context->my_rank;
+  for (auto& e : edges) {
+    DtdTask* s = e.task;
+    grapher_dep(es, t, s->task_class, s->locals, 1, e.src_flow, e.dst_flow);
+    if (s->remote) {
+      if (!t->remote) {
+        // local producer -> remote consumer: send once per (flow, rank)
+        int r = s->rank;
+        bool sent;
+        if (r < 32) { sent = t->sent_mask[e.src_flow] & (1u << r); t->sent_mask[e.src_flow] |= 1u << r; }
+        else {
+          uint64_t k = ((uint64_t)e.src_flow << 32) | (uint64_t)r;
+          sent = std::find(t->sent_ext.begin(), t->sent_ext.end(), k) != t->sent_ext.end();
+          if (!sent) t->sent_ext.push_back(k);
+        }
+        if (!sent) {
+          if (!msg) {
+            msg = new RemoteDepsMsg();
+            msg->outputs.resize(t->nb_flows);
+          }
+          auto& o = msg->outputs[e.src_flow];
+          DataCopy* dc = t->data[e.src_flow].data_out ? t->data[e.src_flow].data_out : t->data[e.src_flow].data_in;
+          if (e.data && dc) o.data = dc;
+          if (!e.data) o.ctl = o.data == nullptr;
+          if (std::find(o.ranks.begin(), o.ranks.end(), r) == o.ranks.end()) o.ranks.push_back(r);
+        }
+      }
+      // remote tasks do not run here: their deps counter is irrelevant
+    } else if (recv_data && e.data && recv_data[e.src_flow]) {
+      // remote producer -> local consumer: install the received version
+      (void)my;
+      if (s->data[e.dst_flow].data_in) data_copy_release(s->data[e.dst_flow].data_in);
+      data_copy_retain(recv_data[e.src_flow]);
+      s->data[e.dst_flow].data_in = recv_data[e.src_flow];
+    }
+    if (!s->remote && s->deps.fetch_sub(1) == 1) ready.push_back(s);
+    task_unref(s);
+  }
+}
+
+int DtdTaskClass::complete_execution(ExecutionStream* es, Task* tt) const {
+  auto* t = static_cast<DtdTask*>(tt);
+  std::vector<Task*> ready;
+  RemoteDepsMsg* msg = nullptr;
+  PARSEC_PINS(es, PINS_RELEASE_DEPS_BEGIN, t);
+  release_successors(es, t, 0xffffffffu, nullptr, ready, msg);
+  if (msg) {
+    msg->taskpool_id = t->taskpool->taskpool_id;
+    msg->task_class_id = task_class_id;
+    msg->dtd_task_id = t->seq;
+    msg->priority = t->priority;
+    remote_dep_activate(es, t->taskpool, *msg);
+    delete msg;
+  }
+  PARSEC_PINS(es, PINS_RELEASE_DEPS_END, t);
+  if (!ready.empty()) schedule_tasks(es, ready.data(), (int)ready.size(), 0);
+  release_task(es, t);
+  return 0;
+}
+
+void DtdTaskClass::release_task(ExecutionStream* es, Task* tt) const {
+  (void)es;
+  auto* t = static_cast<DtdTask*>(tt);
+  for (int f = 0; f < t->nb_flows; ++f) {
+    TaskDataRef& r = t->data[f];
+    if (r.data_out && r.data_out != r.data_in) data_copy_release(r.data_out);
+    if (r.data_in) data_copy_release(r.data_in);
+    r.data_in = r.data_out = nullptr;
+  }
+  for (void* p : t->scratch) std::free(p);
+  t->scratch.clear();
+  Taskpool* tp = t->taskpool;
+  bool remote = t->remote;
+  task_unref(t);
+  if (!remote) tp->tdm->taskpool_addto_nb_tasks(tp, -1);
+}
+
+static void task_unref(DtdTask* t) {
+  if (t->refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
+  for (auto& a : t->args) if (a.tile) tile_release(a.tile);
+  delete t;
+}
+
+void DtdTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& act) {
+  DtdTask* t = nullptr;
+  if (!remote_tasks.find(act.dtd_task_id, t)) {
+    // not discovered yet: park a copy of the activation per flow
+    for (int f = 0; f < kMaxFlows; ++f) {
+      if (!(act.output_mask & (1u << f))) continue;
+      auto* a = new RemoteActivation();
+      a->tp = this; a->taskpool_id = act.taskpool_id; a->dtd_task_id = act.dtd_task_id; a->src_rank = act.src_rank;
+      a->output_mask = 1u << f;
+      a->data[f] = act.data[f];
+      if (a->data[f]) data_copy_retain(a->data[f]);
+      early.insert((act.dtd_task_id << 6) | (uint64_t)f, a);
+    }
+    return;
+  }
+  // install received versions on the tiles the remote task wrote
+  for (auto& a : t->args) {
+    if (a.flow < 0 || !a.tile || !(act.output_mask & (1u << a.flow)) || !act.data[a.flow]) continue;
+    int op = a.op & OP_MASK;
+    if (op == INPUT) continue;
+    Data* d = a.tile->data;
+    DataCopy* c = act.data[a.flow];
+    if (!d || c->original == d) continue;
+    int home = a.tile->dc ? a.tile->dc->home_device() : 0;
+    DataCopy* hc = a.tile->is_new ? nullptr : d->copy(home);
+    if (hc) {
+      device_memcpy(hc->device_index, hc->device_private, c->device_index, c->device_private, std::min(d->nb_elts, c->original ? c->original->nb_elts : d->nb_elts));
+      std::lock_guard<SpinLock> g(d->lock);
+      hc->version = d->newest_version() + 1;
+      hc->coherency_state = COHERENCY_OWNED;
+      d->owner_device = (int8_t)hc->device_index;
+    } else {
+      // shadow Data: the received buffer becomes its current version
+      std::lock_guard<SpinLock> g(d->lock);
+      uint32_t v = d->newest_version() + 1;
+      for (int i = 0; i < kMaxDevices; ++i) { DataCopy* o = d->copy(i); if (o) o->coherency_state = COHERENCY_INVALID; }
+      DataCopy* nc = new DataCopy();
+      size_t n = c->original ? c->original->nb_elts : d->nb_elts;
+      void* p = nullptr;
+      if (posix_memalign(&p, 64, std::max<size_t>(n, 64))) fatal("oom");
+      device_memcpy(0, p, c->device_index, c->device_private, n);
+      nc->device_private = p;
+      nc->flags = DATA_FLAG_PARSEC_OWNED;
+      nc->coherency_state = COHERENCY_OWNED;
+      nc->version = v;
+      if (d->nb_elts == 0) d->nb_elts = n;
+      data_copy_attach(d, nc, 0);
+      d->owner_device = 0;
+    }
+  }
+  std::vector<Task*> ready;
+  RemoteDepsMsg* msg = nullptr;
+  release_successors(es, t, act.output_mask, act.data, ready, msg);
+  delete msg;  // remote shadows never forward
+  if (t->completed) {
+    if (remote_tasks.erase(t->seq)) task_unref(t);
+  }
+  if (!ready.empty()) schedule_tasks(es, ready.data(), (int)ready.size(), 1);
+}
+
+// ============================================================ accessors
+void* task_arg(const Task* tt, int i) {
+  auto* t = static_cast<const DtdTask*>(tt);
+  if (i < 0 || i >= (int)t->args.size()) return nullptr;
+  const Arg& a = t->args[i];
+  if (a.flow >= 0) {
+    DataCopy* c = t->data[a.flow].data_in;
+    return c ? c->device_private : nullptr;
+  }
+  return a.ptr;
+}
+int task_arg_flow(const Task* tt, int i) {
+  auto* t = static_cast<const DtdTask*>(tt);
+  return i >= 0 && i < (int)t->args.size() ? t->args[i].flow : -1;
+}
+int task_nb_args(const Task* tt) { return (int)static_cast<const DtdTask*>(tt)->args.size(); }
+DtdTaskpool* task_taskpool(const Task* t) { return static_cast<DtdTaskpool*>(t->taskpool); }
+
+}  // namespace dtd
+}  // namespace parsec

@@ -1,0 +1,368 @@
+#include "profiling.hpp"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <set>
+#include <sstream>
+
+namespace parsec {
+
+// ============================================================= profiling
+namespace {
+struct ProfState {
+  std::mutex m;
+  bool enabled = false;
+  std::string filename;
+  int rank = 0;
+  uint64_t t0 = 0;
+  std::vector<DictEntry> dict;
+  std::map<std::string, int> dict_index;
+  std::vector<ProfilingStream*> streams;
+  std::vector<std::pair<std::string, std::string>> infos;
+};
+ProfState& P() { static ProfState* s = new ProfState(); return *s; }
+}  // namespace
+
+bool profiling_enabled() { return P().enabled; }
+uint64_t profiling_now() { return now_ns() - P().t0; }
+
+void profiling_init(Context* ctx) {
+  auto& p = P();
+  std::string fn = ParamRegistry::instance().reg_string("profile", "", "filename", "Write a trace to <filename>-<rank>.prof", "");
+  std::lock_guard<std::mutex> g(p.m);
+  p.rank = ctx->my_rank;
+  if (p.t0 == 0) p.t0 = now_ns();
+  if (!fn.empty()) { p.enabled = true; p.filename = fn; }
+}
+
+void profiling_start() { P().t0 = now_ns(); }
+
+ProfilingStream* profiling_stream_create(const std::string& name) {
+  auto* s = new ProfilingStream();
+  s->name = name;
+  s->events.reserve(4096);
+  auto& p = P();
+  std::lock_guard<std::mutex> g(p.m);
+  s->thread_id = (int)p.streams.size();
+  p.streams.push_back(s);
+  return s;
+}
+
+void profiling_thread_init(ExecutionStream* es) {
+  if (!P().enabled || es->prof) return;
+  es->prof = profiling_stream_create((es->is_manager ? "manager " : "thread ") + std::to_string(es->th_id));
+}
+
+void profiling_thread_fini(ExecutionStream* es) { (void)es; }
+
+int profiling_add_dictionary_keyword(const std::string& name, const std::string& attributes, size_t info_length, const std::string& info_desc, int* bkey, int* ekey) {
+  auto& p = P();
+  std::lock_guard<std::mutex> g(p.m);
+  auto it = p.dict_index.find(name);
+  int id;
+  if (it != p.dict_index.end()) id = it->second;
+  else {
+    id = (int)p.dict.size();
+    p.dict.push_back(DictEntry{name, attributes, info_desc, info_length});
+    p.dict_index[name] = id;
+  }
+  if (bkey) *bkey = 2 * id;
+  if (ekey) *ekey = 2 * id + 1;
+  return 0;
+}
+
+int profiling_trace(ProfilingStream* s, int key, uint64_t event_id, uint32_t taskpool_id, const void* info, size_t info_len) {
+  if (!s) return -1;
+  ProfEvent e;
+  e.key = (uint16_t)key;
+  e.flags = info_len ? 1 : 0;
+  e.taskpool_id = taskpool_id;
+  e.event_id = event_id;
+  e.timestamp = profiling_now();
+  e.info_off = (uint32_t)s->info.size();
+  e.info_len = (uint32_t)info_len;
+  if (info_len) s->info.insert(s->info.end(), (const uint8_t*)info, (const uint8_t*)info + info_len);
+  s->events.push_back(e);
+  return 0;
+}
+
+void profiling_add_information(const std::string& key, const std::string& value) {
+  auto& p = P();
+  std::lock_guard<std::mutex> g(p.m);
+  p.infos.emplace_back(key, value);
+}
+
+static void wstr(std::ofstream& o, const std::string& s) {
+  uint32_t l = (uint32_t)s.size();
+  o.write((const char*)&l, 4);
+  o.write(s.data(), l);
+}
+
+int profiling_dump(const std::string& filename) {
+  auto& p = P();
+  std::lock_guard<std::mutex> g(p.m);
+  std::ofstream o(filename, std::ios::binary);
+  if (!o) return -1;
+  o.write("PAMDPRF1", 8);
+  uint32_t hdr[4] = {(uint32_t)p.rank, (uint32_t)p.dict.size(), (uint32_t)p.streams.size(), (uint32_t)p.infos.size()};
+  o.write((const char*)hdr, sizeof(hdr));
+  o.write((const char*)&p.t0, 8);
+  for (auto& kv : p.infos) { wstr(o, kv.first); wstr(o, kv.second); }
+  for (auto& d : p.dict) {
+    wstr(o, d.name); wstr(o, d.attributes); wstr(o, d.info_desc);
+    uint64_t il = d.info_length;
+    o.write((const char*)&il, 8);
+  }
+  for (auto* s : p.streams) {
+    wstr(o, s->name);
+    int32_t tid = s->thread_id;
+    o.write((const char*)&tid, 4);
+    uint64_t n = s->events.size();
+    o.write((const char*)&n, 8);
+    static_assert(sizeof(ProfEvent) == 32, "event layout");
+    o.write((const char*)s->events.data(), n * sizeof(ProfEvent));
+    uint64_t isz = s->info.size();
+    o.write((const char*)&isz, 8);
+    o.write((const char*)s->info.data(), isz);
+  }
+  return o ? 0 : -1;
+}
+
+void profiling_fini(Context* ctx) {
+  auto& p = P();
+  if (p.enabled && !p.filename.empty()) {
+    std::string fn = p.filename + "-" + std::to_string(ctx->my_rank) + ".prof";
+    if (profiling_dump(fn) != 0) warning("could not write trace %s", fn.c_str());
+  }
+  std::lock_guard<std::mutex> g(p.m);
+  for (auto* s : p.streams) delete s;
+  p.streams.clear();
+  for (auto* es : ctx->all_es) es->prof = nullptr;
+  for (auto* es : ctx->aux_es) es->prof = nullptr;
+}
+
+// ================================================================== PINS
+std::atomic<bool> g_pins_enabled{false};
+namespace {
+struct PinsState {
+  std::mutex m;
+  std::vector<PinsCallback> cbs[PINS_NB_EVENTS];
+  std::map<std::string, std::atomic<int64_t>*> counters;
+  std::set<std::string> active;
+};
+PinsState& PS() { static PinsState* s = new PinsState(); return *s; }
+
+std::atomic<int64_t>* counter(const std::string& n) {
+  auto& s = PS();
+  std::lock_guard<std::mutex> g(s.m);
+  auto it = s.counters.find(n);
+  if (it != s.counters.end()) return it->second;
+  auto* c = new std::atomic<int64_t>(0);
+  s.counters[n] = c;
+  return c;
+}
+
+// task_profiler: one begin/end key per task class
+struct TaskProfiler {
+  std::mutex m;
+  std::map<const TaskClass*, std::pair<int, int>> keys;
+  std::pair<int, int> key_of(const TaskClass* tc) {
+    std::lock_guard<std::mutex> g(m);
+    auto it = keys.find(tc);
+    if (it != keys.end()) return it->second;
+    int b, e;
+    profiling_add_dictionary_keyword(tc->name, "fill:#" + std::to_string(0x100000 + (tc->task_class_id * 2654435761u) % 0xEFFFFF), 16, "tp_id{uint32_t};tc_id{uint32_t};locals{int32_t[2]}", &b, &e);
+    keys[tc] = {b, e};
+    return {b, e};
+  }
+};
+TaskProfiler& TPf() { static TaskProfiler* t = new TaskProfiler(); return *t; }
+int g_key_release_b = -1, g_key_release_e = -1, g_key_select_b = -1, g_key_select_e = -1;
+}  // namespace
+
+void pins_fire(ExecutionStream* es, int event, Task* t) {
+  auto& s = PS();
+  for (auto& cb : s.cbs[event]) cb(es, event, t);
+}
+
+int pins_register_callback(int event, PinsCallback cb) {
+  auto& s = PS();
+  std::lock_guard<std::mutex> g(s.m);
+  s.cbs[event].push_back(std::move(cb));
+  g_pins_enabled.store(true);
+  return 0;
+}
+
+std::vector<std::string> pins_modules_available() { return {"task_profiler", "print_steals", "alperf", "iterators_checker"}; }
+
+std::vector<std::pair<std::string, int64_t>> pins_counters() {
+  auto& s = PS();
+  std::lock_guard<std::mutex> g(s.m);
+  std::vector<std::pair<std::string, int64_t>> out;
+  for (auto& kv : s.counters) out.emplace_back(kv.first, kv.second->load());
+  return out;
+}
+
+static void trace_task(ExecutionStream* es, Task* t, bool begin) {
+  if (!es || !es->prof || !t) return;
+  auto k = TPf().key_of(t->task_class);
+  struct { uint32_t tp, tc; int32_t l[2]; } info{t->taskpool->taskpool_id, t->task_class->task_class_id, {t->locals[0], t->task_class->nb_locals > 1 ? t->locals[1] : 0}};
+  profiling_trace(es->prof, begin ? k.first : k.second, t->key, t->taskpool->taskpool_id, &info, sizeof(info));
+}
+
+void pins_init(Context* ctx) {
+  (void)ctx;
+  std::string mods = ParamRegistry::instance().reg_string("mca", "", "pins", "Comma separated PINS modules: task_profiler,print_steals,alperf,iterators_checker", "");
+  auto& s = PS();
+  std::stringstream ss(mods);
+  std::string m;
+  while (std::getline(ss, m, ',')) {
+    if (m.empty() || s.active.count(m)) continue;
+    s.active.insert(m);
+    if (m == "task_profiler") {
+      profiling_add_dictionary_keyword("RELEASE_DEPS", "fill:#CCCCCC", 0, "", &g_key_release_b, &g_key_release_e);
+      profiling_add_dictionary_keyword("SELECT", "fill:#EEEEEE", 0, "", &g_key_select_b, &g_key_select_e);
+      pins_register_callback(PINS_EXEC_BEGIN, [](ExecutionStream* es, int, Task* t) { trace_task(es, t, true); });
+      pins_register_callback(PINS_EXEC_END, [](ExecutionStream* es, int, Task* t) { trace_task(es, t, false); });
+      pins_register_callback(PINS_COMPLETE_EXEC_BEGIN, [](ExecutionStream* es, int, Task* t) {
+        if (es && es->prof) profiling_trace(es->prof, g_key_release_b, t ? t->key : 0, t ? t->taskpool->taskpool_id : 0, nullptr, 0);
+      });
+      pins_register_callback(PINS_COMPLETE_EXEC_END, [](ExecutionStream* es, int, Task*) {
+        if (es && es->prof) profiling_trace(es->prof, g_key_release_e, 0, 0, nullptr, 0);
+      });
+    } else if (m == "print_steals") {
+      pins_register_callback(PINS_THREAD_FINI, [](ExecutionStream* es, int, Task*) {
+        counter("steals.thread" + std::to_string(es->th_id))->store((int64_t)es->nb_stolen);
+        std::fprintf(stderr, "[print_steals] thread %d selected %llu stolen %llu\n", es->th_id, (unsigned long long)es->nb_selected, (unsigned long long)es->nb_stolen);
+      });
+    } else if (m == "alperf") {
+      pins_register_callback(PINS_EXEC_END, [](ExecutionStream*, int, Task* t) {
+        if (!t) return;
+        counter("alperf.tp" + std::to_string(t->taskpool->taskpool_id) + "." + t->task_class->name)->fetch_add(1, std::memory_order_relaxed);
+      });
+    } else if (m == "iterators_checker") {
+      pins_register_callback(PINS_EXEC_BEGIN, [](ExecutionStream* es, int, Task* t) {
+        if (!t) return;
+        // every local successor must list this task among its predecessors
+        t->task_class->iterate_successors(es, t, ACTION_DEPS_MASK, [&](const DepVisit& v) {
+          if (!v.tc) return;
+          Task tmp;
+          tmp.taskpool = t->taskpool;
+          tmp.task_class = v.tc;
+          for (int i = 0; i < v.nb_locals && i < kMaxLocals; ++i) tmp.locals[i] = v.locals[i];
+          bool found = false;
+          v.tc->iterate_predecessors(es, &tmp, ACTION_DEPS_MASK, [&](const DepVisit& p) {
+            if (p.tc != t->task_class) return;
+            bool same = true;
+            for (int i = 0; i < t->task_class->nb_params; ++i) if (p.locals[i] != t->locals[i]) same = false;
+            if (same) found = true;
+          });
+          counter(found ? "iterators_checker.ok" : "iterators_checker.mismatch")->fetch_add(1);
+          if (!found) warning("iterators_checker: %s -> %s has no matching predecessor", t->task_class->describe(t).c_str(), v.tc->name.c_str());
+        });
+      });
+    } else {
+      warning("unknown PINS module '%s'", m.c_str());
+    }
+  }
+}
+
+void pins_fini(Context* ctx) { (void)ctx; }
+
+// ================================================================ grapher
+namespace {
+struct Grapher {
+  std::mutex m;
+  FILE* f = nullptr;
+};
+Grapher& G() { static Grapher* g = new Grapher(); return *g; }
+std::string node_name(const TaskClass* tc, const int32_t* locals, int n) {
+  std::string s = tc->name + "_";
+  for (int i = 0; i < n; ++i) { if (i) s += "_"; s += std::to_string(locals[i]); }
+  for (char& c : s) if (c == '-') c = 'm';
+  return s;
+}
+}  // namespace
+
+void grapher_init(Context* ctx) {
+  if (ctx->grapher_file.empty()) return;
+  auto& g = G();
+  std::lock_guard<std::mutex> lk(g.m);
+  std::string fn = ctx->grapher_file + "-" + std::to_string(ctx->my_rank) + ".dot";
+  g.f = std::fopen(fn.c_str(), "w");
+  if (g.f) std::fprintf(g.f, "digraph G {\n");
+}
+
+void grapher_task(ExecutionStream* es, Task* t) {
+  (void)es;
+  auto& g = G();
+  if (!g.f) return;
+  std::lock_guard<std::mutex> lk(g.m);
+  std::fprintf(g.f, "  %s [label=\"%s\" tooltip=\"tp %u\"];\n", node_name(t->task_class, t->locals, t->task_class->nb_params).c_str(),
+               t->task_class->describe(t).c_str(), t->taskpool->taskpool_id);
+}
+
+void grapher_dep(ExecutionStream* es, const Task* from, const TaskClass* to_tc, const int32_t* to_locals, int nb, int from_flow, int to_flow) {
+  (void)es;
+  auto& g = G();
+  if (!g.f) return;
+  std::lock_guard<std::mutex> lk(g.m);
+  const char* fl = from_flow >= 0 && from_flow < (int)from->task_class->flows.size() ? from->task_class->flows[from_flow].name.c_str() : "";
+  const char* tl = to_flow >= 0 && to_flow < (int)to_tc->flows.size() ? to_tc->flows[to_flow].name.c_str() : "";
+  std::fprintf(g.f, "  %s -> %s [label=\"%s=>%s\"];\n", node_name(from->task_class, from->locals, from->task_class->nb_params).c_str(), node_name(to_tc, to_locals, nb).c_str(), fl, tl);
+}
+
+void grapher_fini(Context* ctx) {
+  (void)ctx;
+  auto& g = G();
+  std::lock_guard<std::mutex> lk(g.m);
+  if (g.f) { std::fprintf(g.f, "}\n"); std::fclose(g.f); g.f = nullptr; }
+}
+
+// ============================================================ properties
+namespace {
+struct Props { std::mutex m; std::map<std::string, double> v; };
+Props& PR() { static Props* p = new Props(); return *p; }
+}  // namespace
+
+void properties_set(const std::string& name, double value) {
+  auto& p = PR();
+  std::lock_guard<std::mutex> g(p.m);
+  p.v[name] = value;
+}
+
+std::vector<std::pair<std::string, double>> properties_snapshot() {
+  auto& p = PR();
+  std::lock_guard<std::mutex> g(p.m);
+  std::vector<std::pair<std::string, double>> out(p.v.begin(), p.v.end());
+  for (auto& c : pins_counters()) out.emplace_back(c.first, (double)c.second);
+  return out;
+}
+
+// Publish properties in a POSIX shm region: an XML-ish header then the values
+// (reference dictionary.c exposes the same through shm for aggregator_visu).
+int properties_dump_shm(const std::string& shm_name) {
+  auto snap = properties_snapshot();
+  std::ostringstream os;
+  os << "<properties>\n";
+  for (auto& kv : snap) os << "  <p name=\"" << kv.first << "\" value=\"" << kv.second << "\"/>\n";
+  os << "</properties>\n";
+  std::string s = os.str();
+  int fd = shm_open(shm_name.c_str(), O_CREAT | O_RDWR, 0600);
+  if (fd < 0) return -1;
+  if (ftruncate(fd, (off_t)s.size() + 1) != 0) { close(fd); return -1; }
+  void* p = mmap(nullptr, s.size() + 1, PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) return -1;
+  std::memcpy(p, s.c_str(), s.size() + 1);
+  munmap(p, s.size() + 1);
+  return 0;
+}
+
+}  // namespace parsec

@@ -1,0 +1,79 @@
+// Tracing / instrumentation.
+//
+// Parity: PBP profiling (reference profiling.h, profiling.c:473-1485 — per-stream
+// event buffers, dictionary of begin/end keys with info convertors, one trace
+// file per rank), PINS callback chains on 16 events (mca/pins/pins.h:26-190) with
+// modules task_profiler / print_steals / alperf / iterators_checker, DOT grapher
+// (parsec_prof_grapher.c:86-266), properties dictionary (dictionary.h:14-60).
+// File format here is our own ("PAMDPRF1", see parsec_amd/profiling.py reader).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../core/runtime.hpp"
+
+namespace parsec {
+
+struct ProfEvent {
+  uint16_t key;       // dictionary key (begin = 2*k, end = 2*k+1)
+  uint16_t flags;     // bit0: has info
+  uint32_t taskpool_id;
+  uint64_t event_id;
+  uint64_t timestamp; // ns since profiling start
+  uint32_t info_off;  // offset in the stream's info blob
+  uint32_t info_len;
+};
+
+struct ProfilingStream {
+  std::string name;
+  int thread_id = 0;
+  std::vector<ProfEvent> events;
+  std::vector<uint8_t> info;
+  SpinLock lock;  // only for streams shared by several threads (devices)
+};
+
+struct DictEntry {
+  std::string name;
+  std::string attributes;  // e.g. "fill:#FF0000"
+  std::string info_desc;   // convertor, e.g. "size{int64_t};key{uint64_t}"
+  size_t info_length = 0;
+};
+
+// global enable (set when profile_filename is given)
+bool profiling_enabled();
+void profiling_init(Context* ctx);
+void profiling_fini(Context* ctx);
+void profiling_thread_init(ExecutionStream* es);
+void profiling_thread_fini(ExecutionStream* es);
+ProfilingStream* profiling_stream_create(const std::string& name);
+// returns the key pair (begin key = 2*id, end = 2*id+1)
+int profiling_add_dictionary_keyword(const std::string& name, const std::string& attributes, size_t info_length,
+                                     const std::string& info_desc, int* begin_key, int* end_key);
+int profiling_trace(ProfilingStream* s, int key, uint64_t event_id, uint32_t taskpool_id, const void* info, size_t info_len);
+uint64_t profiling_now();
+int profiling_dump(const std::string& filename);
+void profiling_add_information(const std::string& key, const std::string& value);
+void profiling_start();
+
+// PINS
+void pins_init(Context* ctx);
+void pins_fini(Context* ctx);
+using PinsCallback = std::function<void(ExecutionStream*, int event, Task*)>;
+int pins_register_callback(int event, PinsCallback cb);
+std::vector<std::string> pins_modules_available();
+// counters exposed by the alperf / print_steals modules
+std::vector<std::pair<std::string, int64_t>> pins_counters();
+
+// DOT grapher
+void grapher_init(Context* ctx);
+void grapher_task(ExecutionStream* es, Task* t);
+void grapher_dep(ExecutionStream* es, const Task* from, const TaskClass* to_tc, const int32_t* to_locals, int nb_locals, int from_flow, int to_flow);
+void grapher_fini(Context* ctx);
+
+// Properties dictionary (live counters readable by tools)
+void properties_set(const std::string& name, double value);
+std::vector<std::pair<std::string, double>> properties_snapshot();
+int properties_dump_shm(const std::string& shm_name);
+
+}  // namespace parsec

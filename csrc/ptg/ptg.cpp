@@ -1,0 +1,513 @@
+#include "ptg.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+#include "../comm/comm.hpp"
+#include "../device/device.hpp"
+#include "../prof/profiling.hpp"
+
+namespace parsec {
+namespace ptg {
+
+static inline int64_t ev(const Expr& e, const Taskpool* tp, const int32_t* L, int64_t d = 0) { return e ? e(tp, L) : d; }
+
+// Iterate the values of a range [lo..hi] with step (negative steps allowed).
+template <class F>
+static inline void for_range(int64_t lo, int64_t hi, int64_t step, F&& f) {
+  if (step == 0) step = 1;
+  if (step > 0) for (int64_t v = lo; v <= hi; v += step) f(v);
+  else for (int64_t v = lo; v >= hi; v += step) f(v);
+}
+
+// Expand call arguments (values and ranges) into concrete parameter tuples.
+template <class F>
+static void expand_args(const Taskpool* tp, const int32_t* L, const std::vector<CallArg>& args, size_t i, int32_t* out, F&& f) {
+  if (i == args.size()) { f(out); return; }
+  const CallArg& a = args[i];
+  if (!a.is_range) {
+    out[i] = (int32_t)ev(a.value, tp, L);
+    expand_args(tp, L, args, i + 1, out, f);
+    return;
+  }
+  for_range(ev(a.lo, tp, L), ev(a.hi, tp, L), ev(a.step, tp, L, 1), [&](int64_t v) {
+    out[i] = (int32_t)v;
+    expand_args(tp, L, args, i + 1, out, f);
+  });
+}
+
+static void collection_index(const Taskpool* tp, const int32_t* L, const std::vector<CallArg>& args, int64_t* idx) {
+  for (size_t i = 0; i < args.size(); ++i) idx[i] = ev(args[i].is_range ? args[i].lo : args[i].value, tp, L);
+}
+
+// ------------------------------------------------------------ execution space
+void for_each_task(const Taskpool* tp, const PtgTaskClass* tc, const std::function<void(const int32_t*)>& f) {
+  const auto& locals = tc->def.locals;
+  int32_t L[kMaxLocals] = {};
+  std::function<void(size_t)> rec = [&](size_t i) {
+    if (i == locals.size()) { f(L); return; }
+    const LocalDef& ld = locals[i];
+    if (!ld.is_range) {
+      L[i] = (int32_t)ev(ld.value, tp, L);
+      rec(i + 1);
+      return;
+    }
+    for_range(ev(ld.lo, tp, L), ev(ld.hi, tp, L), ev(ld.step, tp, L, 1), [&](int64_t v) {
+      L[i] = (int32_t)v;
+      rec(i + 1);
+    });
+  };
+  rec(0);
+}
+
+bool PtgTaskClass::complete_locals(const Taskpool* tp, int32_t* L, const int32_t* params) const {
+  const auto& locals = def.locals;
+  for (size_t i = 0; i < locals.size(); ++i) {
+    const LocalDef& ld = locals[i];
+    if (ld.is_param) {
+      int32_t v = params[local_param[i]];
+      if (ld.is_range) {
+        int64_t lo = ev(ld.lo, tp, L), hi = ev(ld.hi, tp, L), st = ev(ld.step, tp, L, 1);
+        if (st > 0 ? (v < lo || v > hi) : (v > lo || v < hi)) return false;
+        if (st != 1 && st != -1 && ((v - lo) % st) != 0) return false;
+      } else if (ld.value && v != (int32_t)ev(ld.value, tp, L)) {
+        return false;
+      }
+      L[i] = v;
+    } else {
+      L[i] = (int32_t)(ld.is_range ? ev(ld.lo, tp, L) : ev(ld.value, tp, L));
+    }
+  }
+  return true;
+}
+
+uint32_t PtgTaskClass::rank_of(const Taskpool* tp, const int32_t* L) const {
+  if (!def.affinity_dc) return tp->context ? (uint32_t)tp->context->my_rank : 0;
+  DataCollection* dc = def.affinity_dc(tp);
+  if (!dc) return 0;
+  int64_t idx[kMaxLocals];
+  for (size_t i = 0; i < def.affinity_args.size(); ++i) idx[i] = ev(def.affinity_args[i], tp, L);
+  return dc->rank_of(idx, (int)def.affinity_args.size());
+}
+
+int32_t PtgTaskClass::priority_of(const Taskpool* tp, const int32_t* L) const {
+  return (int32_t)(ev(def.priority, tp, L) + tp->priority);
+}
+
+uint64_t PtgTaskClass::make_key(const Taskpool* tp, const int32_t* L) const {
+  if (def.make_key_fn) return def.make_key_fn(tp, L);
+  auto* ptp = static_cast<const PtgTaskpool*>(tp);
+  (void)ptp;
+  return TaskClass::make_key(tp, L);
+}
+
+const DepTarget* PtgTaskClass::active_input(const Taskpool* tp, int flow, const int32_t* L) const {
+  for (const Dep& d : def.flows[flow].in) {
+    if (!d.guard || d.guard(tp, L)) return &d.then_t;
+    if (d.has_else) return &d.else_t;
+  }
+  return nullptr;
+}
+
+int PtgTaskClass::count_task_inputs(const Taskpool* tp, const int32_t* L) const {
+  int count = 0;
+  for (size_t f = 0; f < def.flows.size(); ++f) {
+    const DepTarget* t = active_input(tp, (int)f, L);
+    if (!t || t->kind != DEP_TASK) continue;
+    const PtgTaskClass* src = owner->classes[t->tc_id];
+    int32_t params[kMaxLocals];
+    expand_args(tp, L, t->args, 0, params, [&](const int32_t* P) {
+      int32_t SL[kMaxLocals];
+      if (src->complete_locals(tp, SL, P)) ++count;
+    });
+  }
+  return count;
+}
+
+int64_t PtgTaskClass::sim_cost(const Task* t) const { return def.sim_cost ? def.sim_cost(t->taskpool, t->locals) : 1; }
+
+// ------------------------------------------------------------- successors
+void PtgTaskClass::iterate_successors(ExecutionStream* es, const Task* t, uint32_t mask, const DepVisitor& v) const {
+  (void)es;
+  const Taskpool* tp = t->taskpool;
+  for (size_t f = 0; f < def.flows.size(); ++f) {
+    if (!(mask & (1u << f))) continue;
+    for (const Dep& d : def.flows[f].out) {
+      const DepTarget* tg = (!d.guard || d.guard(tp, t->locals)) ? &d.then_t : (d.has_else ? &d.else_t : nullptr);
+      if (!tg) continue;
+      if (tg->kind == DEP_TASK) {
+        const PtgTaskClass* dst = owner->classes[tg->tc_id];
+        int32_t params[kMaxLocals];
+        expand_args(tp, t->locals, tg->args, 0, params, [&](const int32_t* P) {
+          int32_t TL[kMaxLocals];
+          if (!dst->complete_locals(tp, TL, P)) return;
+          DepVisit vis;
+          vis.tc = dst; vis.locals = TL; vis.nb_locals = dst->nb_locals;
+          vis.src_flow = (int)f; vis.dst_flow = tg->dst_flow;
+          vis.rank = dst->rank_of(tp, TL);
+          vis.priority = dst->priority_of(tp, TL);
+          vis.datatype_index = tg->datatype_index;
+          v(vis);
+        });
+      } else if (tg->kind == DEP_DATA) {
+        DepVisit vis;
+        vis.src_flow = (int)f;
+        vis.dc = tg->dc(tp);
+        int64_t idx[kMaxLocals];
+        collection_index(tp, t->locals, tg->args, idx);
+        vis.dc_key = vis.dc->data_key(idx, (int)tg->args.size());
+        vis.rank = vis.dc->rank_of(idx, (int)tg->args.size());
+        v(vis);
+      }
+    }
+  }
+}
+
+void PtgTaskClass::iterate_predecessors(ExecutionStream* es, const Task* t, uint32_t mask, const DepVisitor& v) const {
+  (void)es;
+  const Taskpool* tp = t->taskpool;
+  for (size_t f = 0; f < def.flows.size(); ++f) {
+    if (!(mask & (1u << f))) continue;
+    const DepTarget* tg = active_input(tp, (int)f, t->locals);
+    if (!tg || tg->kind != DEP_TASK) continue;
+    const PtgTaskClass* src = owner->classes[tg->tc_id];
+    int32_t params[kMaxLocals];
+    expand_args(tp, t->locals, tg->args, 0, params, [&](const int32_t* P) {
+      int32_t SL[kMaxLocals];
+      if (!src->complete_locals(tp, SL, P)) return;
+      DepVisit vis;
+      vis.tc = src; vis.locals = SL; vis.nb_locals = src->nb_locals;
+      vis.src_flow = (int)f; vis.dst_flow = tg->dst_flow;
+      vis.rank = src->rank_of(tp, SL);
+      v(vis);
+    });
+  }
+}
+
+uint32_t PtgTaskClass::gpu_pushout_mask(const Task* t, int device) const {
+  uint32_t m = 0;
+  const Taskpool* tp = t->taskpool;
+  uint32_t my = tp->context ? (uint32_t)tp->context->my_rank : 0;
+  for (size_t f = 0; f < def.flows.size(); ++f) {
+    if (!(def.flows[f].access & FLOW_WRITE)) continue;
+    for (const Dep& d : def.flows[f].out) {
+      const DepTarget* tg = (!d.guard || d.guard(tp, t->locals)) ? &d.then_t : (d.has_else ? &d.else_t : nullptr);
+      if (!tg || tg->kind != DEP_DATA) continue;
+      DataCollection* dc = tg->dc(tp);
+      int64_t idx[kMaxLocals];
+      collection_index(tp, t->locals, tg->args, idx);
+      if (dc->home_device() != device && dc->rank_of(idx, (int)tg->args.size()) == my) m |= 1u << f;
+    }
+  }
+  return m;
+}
+
+// ------------------------------------------------------------- data lookup
+static DataCopy* newest_copy(Data* d) {
+  DataCopy* best = nullptr;
+  for (int i = 0; i < kMaxDevices; ++i) {
+    DataCopy* c = d->copy(i);
+    if (!c || c->coherency_state == COHERENCY_INVALID) continue;
+    if (!best || c->version > best->version || (c->version == best->version && i == d->owner_device)) best = c;
+  }
+  return best ? best : d->copy(std::max<int>(0, d->owner_device));
+}
+
+int PtgTaskClass::prepare_input(ExecutionStream* es, Task* t) const {
+  (void)es;
+  const Taskpool* tp = t->taskpool;
+  for (size_t f = 0; f < def.flows.size(); ++f) {
+    const FlowDef& fd = def.flows[f];
+    if (fd.access == FLOW_CTL) continue;
+    TaskDataRef& r = t->data[f];
+    if (r.data_in) continue;
+    const DepTarget* tg = active_input(tp, (int)f, t->locals);
+    if (!tg) continue;
+    switch (tg->kind) {
+      case DEP_DATA: {
+        DataCollection* dc = tg->dc(tp);
+        int64_t idx[kMaxLocals];
+        collection_index(tp, t->locals, tg->args, idx);
+        Data* d = dc->data_of(idx, (int)tg->args.size());
+        if (!d) fatal("%s: flow %s reads %s which is not local", describe(t).c_str(), fd.name.c_str(), dc->key_to_string(dc->data_key(idx, (int)tg->args.size())).c_str());
+        DataCopy* c = newest_copy(d);
+        data_copy_retain(c);
+        r.data_in = c;
+        break;
+      }
+      case DEP_NEW: {
+        auto& adts = t->taskpool->arenas_datatypes;
+        if (tg->datatype_index >= (int)adts.size() || !adts[tg->datatype_index].arena)
+          fatal("%s: NEW on flow %s needs arenas_datatypes[%d]", describe(t).c_str(), fd.name.c_str(), tg->datatype_index);
+        r.data_in = adts[tg->datatype_index].arena->get_copy(nullptr, 0);
+        if (!r.data_in) return HOOK_AGAIN;  // arena exhausted (max_used)
+        break;
+      }
+      default:
+        break;
+    }
+  }
+  return HOOK_DONE;
+}
+
+// Copy `src` into the collection's own copy of `home` (final write of a flow
+// into a collection position it did not come from).
+static void write_back(Data* home, DataCopy* src) {
+  if (!home || !src || src->original == home) return;
+  int hd = home->owner_device >= 0 ? home->owner_device : 0;
+  DataCopy* dst = home->copy(hd);
+  if (!dst) dst = home->copy(0);
+  if (!dst) return;
+  size_t n = std::min(home->nb_elts, src->original ? src->original->nb_elts : home->nb_elts);
+  device_memcpy(dst->device_index, dst->device_private, src->device_index, src->device_private, n);
+  std::lock_guard<SpinLock> g(home->lock);
+  dst->version = home->newest_version() + 1;
+}
+
+// --------------------------------------------------------- release (hot)
+int PtgTaskClass::complete_execution(ExecutionStream* es, Task* t) const {
+  PtgTaskpool* tp = owner;
+  const uint32_t my = (uint32_t)tp->context->my_rank;
+  std::vector<Task*> ready;
+  RemoteDepsMsg* msg = nullptr;
+  PARSEC_PINS(es, PINS_RELEASE_DEPS_BEGIN, t);
+  for (size_t f = 0; f < def.flows.size(); ++f) {
+    const FlowDef& fd = def.flows[f];
+    if (fd.out.empty()) continue;
+    DataCopy* data = fd.access == FLOW_CTL ? nullptr : (t->data[f].data_out ? t->data[f].data_out : t->data[f].data_in);
+    for (const Dep& d : fd.out) {
+      const DepTarget* tg = (!d.guard || d.guard(tp, t->locals)) ? &d.then_t : (d.has_else ? &d.else_t : nullptr);
+      if (!tg) continue;
+      if (tg->kind == DEP_TASK) {
+        PtgTaskClass* dst = tp->classes[tg->tc_id];
+        int32_t params[kMaxLocals];
+        expand_args(tp, t->locals, tg->args, 0, params, [&](const int32_t* P) {
+          int32_t TL[kMaxLocals];
+          if (!dst->complete_locals(tp, TL, P)) return;
+          uint32_t r = dst->rank_of(tp, TL);
+          grapher_dep(es, t, dst, TL, dst->nb_params, (int)f, tg->dst_flow);
+          if (r == my) {
+            tp->activate(es, dst, TL, tg->dst_flow, data, ready);
+          } else {
+            if (!msg) {
+              msg = new RemoteDepsMsg();
+              msg->outputs.resize(def.flows.size());
+            }
+            auto& o = msg->outputs[f];
+            o.data = data;
+            o.ctl = fd.access == FLOW_CTL || data == nullptr;
+            if (std::find(o.ranks.begin(), o.ranks.end(), (int)r) == o.ranks.end()) o.ranks.push_back((int)r);
+          }
+        });
+      } else if (tg->kind == DEP_DATA && data) {
+        DataCollection* dc = tg->dc(tp);
+        int64_t idx[kMaxLocals];
+        collection_index(tp, t->locals, tg->args, idx);
+        if (dc->rank_of(idx, (int)tg->args.size()) == my) write_back(dc->data_of(idx, (int)tg->args.size()), data);
+      }
+    }
+  }
+  if (msg) {
+    msg->taskpool_id = tp->taskpool_id;
+    msg->task_class_id = task_class_id;
+    msg->nb_locals = nb_locals;
+    std::memcpy(msg->locals, t->locals, sizeof(int32_t) * nb_locals);
+    msg->priority = t->priority;
+    remote_dep_activate(es, tp, *msg);
+    delete msg;
+  }
+  PARSEC_PINS(es, PINS_RELEASE_DEPS_END, t);
+  if (!ready.empty()) {
+    if (tp->context->simulation)
+      for (Task* n : ready) n->sim_exec_date = std::max(n->sim_exec_date, t->sim_exec_date + (uint64_t)sim_cost(t));
+    schedule_tasks(es, ready.data(), (int)ready.size(), 0);
+  }
+  release_task(es, t);
+  return 0;
+}
+
+// ================================================================ taskpool
+PtgTaskpool::PtgTaskpool() { taskpool_name = "ptg"; }
+
+PtgTaskpool::~PtgTaskpool() {
+  pending.for_each([](uint64_t, Task* t) {
+    for (int f = 0; f < kMaxFlows; ++f) if (t->data[f].data_in) data_copy_release(t->data[f].data_in);
+    task_free(t);
+  });
+  pending.clear();
+  for (auto* c : classes) delete c;
+}
+
+PtgTaskClass* PtgTaskpool::add_task_class(TaskClassDef def) {
+  auto* tc = new PtgTaskClass();
+  tc->owner = this;
+  tc->task_class_id = (uint16_t)classes.size();
+  tc->name = def.name;
+  tc->def = std::move(def);
+  classes.push_back(tc);
+  task_classes.push_back(tc);
+  finalized = false;
+  return tc;
+}
+
+void PtgTaskpool::finalize() {
+  for (auto* tc : classes) {
+    auto& d = tc->def;
+    if (d.locals.size() > (size_t)kMaxLocals) fatal("task class %s has too many locals", d.name.c_str());
+    if (d.flows.size() > (size_t)kMaxFlows) fatal("task class %s has too many flows", d.name.c_str());
+    tc->nb_locals = (int)d.locals.size();
+    tc->local_names.clear();
+    tc->param_local.clear();
+    tc->local_param.assign(d.locals.size(), -1);
+    for (size_t i = 0; i < d.locals.size(); ++i) tc->local_names.push_back(d.locals[i].name);
+    if (d.params.empty())
+      for (size_t i = 0; i < d.locals.size(); ++i) if (d.locals[i].is_param) d.params.push_back(d.locals[i].name);
+    for (auto& pn : d.params) {
+      int li = -1;
+      for (size_t i = 0; i < d.locals.size(); ++i) if (d.locals[i].name == pn) li = (int)i;
+      if (li < 0) fatal("task class %s: parameter %s has no definition", d.name.c_str(), pn.c_str());
+      d.locals[li].is_param = true;
+      tc->local_param[li] = (int)tc->param_local.size();
+      tc->param_local.push_back(li);
+    }
+    tc->nb_params = (int)tc->param_local.size();
+    tc->flows.clear();
+    for (size_t f = 0; f < d.flows.size(); ++f) tc->flows.push_back(Flow{d.flows[f].name, d.flows[f].access, (uint8_t)f});
+    tc->chores.clear();
+    for (auto& b : d.bodies) {
+      Chore ch;
+      ch.type = b.type;
+      ch.hook = b.cpu;
+      ch.gpu_hook = b.gpu;
+      ch.evaluate = b.evaluate;
+      ch.weight = b.weight;
+      ch.dyld = b.dyld;
+      tc->chores.push_back(std::move(ch));
+    }
+    tc->flags = d.flags;
+    tc->flops_per_task = d.flops;
+    auto resolve = [&](DepTarget& t) {
+      if (t.kind != DEP_TASK) return;
+      PtgTaskClass* dst = nullptr;
+      for (auto* c : classes) if (c->def.name == t.tc_name) dst = c;
+      if (!dst) fatal("%s: unknown task class %s", d.name.c_str(), t.tc_name.c_str());
+      t.tc_id = dst->task_class_id;
+      t.dst_flow = -1;
+      for (size_t g = 0; g < dst->def.flows.size(); ++g) if (dst->def.flows[g].name == t.flow_name) t.dst_flow = (int)g;
+      if (t.dst_flow < 0) fatal("%s: task class %s has no flow %s", d.name.c_str(), t.tc_name.c_str(), t.flow_name.c_str());
+    };
+    for (auto& fl : d.flows) {
+      for (auto& dep : fl.in) { resolve(dep.then_t); if (dep.has_else) resolve(dep.else_t); }
+      for (auto& dep : fl.out) { resolve(dep.then_t); if (dep.has_else) resolve(dep.else_t); }
+    }
+  }
+  finalized = true;
+}
+
+int64_t PtgTaskpool::global(const std::string& n) const {
+  for (size_t i = 0; i < global_names.size(); ++i) if (global_names[i] == n) return globals[i];
+  fatal("PTG taskpool %s has no global %s", taskpool_name.c_str(), n.c_str());
+}
+void PtgTaskpool::set_global(const std::string& n, int64_t v) {
+  for (size_t i = 0; i < global_names.size(); ++i) if (global_names[i] == n) { globals[i] = v; return; }
+  global_names.push_back(n);
+  globals.push_back(v);
+}
+
+void PtgTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
+  if (!finalized) finalize();
+  ExecutionStream* es = my_execution_stream();
+  uint32_t my = (uint32_t)ctx->my_rank;
+  int64_t nb_local = 0;
+  for (auto* tc : classes) {
+    if (tc->def.nb_local_tasks_fn) nb_local += tc->def.nb_local_tasks_fn(this);
+    if (tc->def.startup_fn) {
+      std::vector<std::vector<int32_t>> st;
+      tc->def.startup_fn(this, st);
+      for (auto& L : st) {
+        Task* t = task_new(es, this, tc);
+        std::copy(L.begin(), L.end(), t->locals);
+        t->key = tc->make_key(this, t->locals);
+        t->priority = tc->priority_of(this, t->locals);
+        t->flags |= TASK_FLAG_STARTUP;
+        ready.push_back(t);
+      }
+      if (tc->def.nb_local_tasks_fn) continue;
+    }
+    for_each_task(this, tc, [&](const int32_t* L) {
+      if (tc->rank_of(this, L) != my) return;
+      if (!tc->def.nb_local_tasks_fn) ++nb_local;
+      if (tc->def.startup_fn) return;
+      if (tc->count_task_inputs(this, L) != 0) return;
+      Task* t = task_new(es, this, tc);
+      std::memcpy(t->locals, L, sizeof(int32_t) * tc->nb_locals);
+      t->key = tc->make_key(this, L);
+      t->priority = tc->priority_of(this, L);
+      t->flags |= TASK_FLAG_STARTUP;
+      ready.push_back(t);
+    });
+  }
+  tdm->taskpool_set_nb_tasks(this, nb_local);
+}
+
+void PtgTaskpool::activate(ExecutionStream* es, PtgTaskClass* tc, const int32_t* L, int flow, DataCopy* data, std::vector<Task*>& ready) {
+  uint64_t key = tc->make_key(this, L);
+  Task* done = pending.with(key, [&](auto& m) -> Task* {
+    auto it = m.find(key);
+    Task* task;
+    if (it == m.end()) {
+      task = task_new(es, this, tc);
+      std::memcpy(task->locals, L, sizeof(int32_t) * tc->nb_locals);
+      task->key = key;
+      task->priority = tc->priority_of(this, L);
+      task->deps_remaining = tc->count_task_inputs(this, L);
+      m.emplace(key, task);
+    } else {
+      task = it->second;
+    }
+    if (data && flow >= 0) {
+      if (task->data[flow].data_in) data_copy_release(task->data[flow].data_in);
+      data_copy_retain(data);
+      task->data[flow].data_in = data;
+    }
+    if (--task->deps_remaining <= 0) {
+      m.erase(key);
+      return task;
+    }
+    return nullptr;
+  });
+  if (done) ready.push_back(done);
+}
+
+void PtgTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& act) {
+  if (act.task_class_id >= classes.size()) fatal("remote activation for unknown task class %u", act.task_class_id);
+  PtgTaskClass* tc = classes[act.task_class_id];
+  const uint32_t my = (uint32_t)context->my_rank;
+  std::vector<Task*> ready;
+  for (size_t f = 0; f < tc->def.flows.size(); ++f) {
+    if (!(act.output_mask & (1u << f))) continue;
+    DataCopy* data = act.data[f];
+    for (const Dep& d : tc->def.flows[f].out) {
+      const DepTarget* tg = (!d.guard || d.guard(this, act.locals)) ? &d.then_t : (d.has_else ? &d.else_t : nullptr);
+      if (!tg) continue;
+      if (tg->kind == DEP_TASK) {
+        PtgTaskClass* dst = classes[tg->tc_id];
+        int32_t params[kMaxLocals];
+        expand_args(this, act.locals, tg->args, 0, params, [&](const int32_t* P) {
+          int32_t TL[kMaxLocals];
+          if (!dst->complete_locals(this, TL, P)) return;
+          if (dst->rank_of(this, TL) == my) activate(es, dst, TL, tg->dst_flow, data, ready);
+        });
+      } else if (tg->kind == DEP_DATA && data) {
+        DataCollection* dc = tg->dc(this);
+        int64_t idx[kMaxLocals];
+        collection_index(this, act.locals, tg->args, idx);
+        if (dc->rank_of(idx, (int)tg->args.size()) == my) write_back(dc->data_of(idx, (int)tg->args.size()), data);
+      }
+    }
+  }
+  if (!ready.empty()) schedule_tasks(es, ready.data(), (int)ready.size(), 1);
+}
+
+}  // namespace ptg
+}  // namespace parsec

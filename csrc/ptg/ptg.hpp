@@ -1,0 +1,146 @@
+// PTG (Parameterized Task Graph) runtime.
+//
+// A PTG taskpool is a set of task classes, each with an execution space
+// (ordered locals, some of them ranged parameters), an affinity (collection +
+// indices -> owning rank), a priority expression, flows with guarded input and
+// output dependencies, and one or more bodies (CPU / GPU chores).
+// The `ptgpp` compiler (tools/ptgpp) translates `.jdf` files into C++ code that
+// builds these definitions with compiled lambdas; C++ users can also build them
+// directly (see csrc/algos/dpotrf.cpp).
+//
+// Parity (reference): task-class structure emitted by jdf2c (jdf2c.c:4038-4345),
+// iterate_successors / predecessors (jdf2c.c:7631-8060), startup tasks
+// (jdf2c.c:2989-3240), data_lookup / prepare_input (jdf2c.c:6431-6536),
+// release_deps (jdf2c.c:7175-7282), dependency counting with control gather
+// (parsec.c:1416-1500, 1554-1598), hash / index-array deps (parsec.c:1503-1551).
+// Design: dependency tracking creates the successor Task at its first
+// activation and stores the incoming data copies straight into it (refcounted),
+// so no per-producer data repository lookup happens on the hot path.
+#pragma once
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../core/runtime.hpp"
+
+namespace parsec {
+namespace ptg {
+
+using Expr = std::function<int64_t(const Taskpool*, const int32_t*)>;
+using Guard = std::function<bool(const Taskpool*, const int32_t*)>;
+
+struct LocalDef {
+  std::string name;
+  bool is_param = false;
+  bool is_range = false;
+  Expr value;           // !is_range
+  Expr lo, hi, step;    // is_range (step null = 1)
+};
+
+enum DepKind : uint8_t { DEP_NULL = 0, DEP_TASK, DEP_DATA, DEP_NEW };
+
+struct CallArg {
+  bool is_range = false;
+  Expr value;
+  Expr lo, hi, step;
+};
+
+struct DepTarget {
+  DepKind kind = DEP_NULL;
+  std::string tc_name;   // DEP_TASK (resolved to tc_id at finalize)
+  int tc_id = -1;
+  std::string flow_name; // DEP_TASK: flow in the target
+  int dst_flow = -1;
+  std::vector<CallArg> args;  // target parameters (TASK) or collection indices (DATA)
+  std::function<DataCollection*(const Taskpool*)> dc;  // DEP_DATA
+  int datatype_index = 0;     // arena / datatype slot (NEW, remote layout)
+  Expr displ_remote, count_remote;
+};
+
+struct Dep {
+  Guard guard;  // null: always active
+  DepTarget then_t;
+  bool has_else = false;
+  DepTarget else_t;
+};
+
+struct FlowDef {
+  std::string name;
+  uint8_t access = FLOW_READ;
+  std::vector<Dep> in, out;
+};
+
+struct BodyDef {
+  uint32_t type = DEV_CPU;
+  Hook cpu;
+  std::function<int(GpuExecContext*, Task*)> gpu;
+  Evaluate evaluate;
+  double weight = 1.0;
+  std::string dyld;
+};
+
+struct TaskClassDef {
+  std::string name;
+  std::vector<LocalDef> locals;
+  std::vector<std::string> params;  // header order TASK(p0, p1, ...); empty = param locals in order
+  std::function<DataCollection*(const Taskpool*)> affinity_dc;
+  std::vector<Expr> affinity_args;
+  Expr priority;
+  Expr sim_cost;
+  uint32_t flags = 0;  // TC_HIGH_PRIORITY, TC_IMMEDIATE, ...
+  std::vector<FlowDef> flows;
+  std::vector<BodyDef> bodies;
+  double flops = 0;
+  // user-defined overrides (reference udf.jdf properties)
+  std::function<uint64_t(const Taskpool*, const int32_t*)> make_key_fn;
+  std::function<int64_t(const Taskpool*)> nb_local_tasks_fn;
+  std::function<void(const Taskpool*, std::vector<std::vector<int32_t>>&)> startup_fn;  // returns startup locals
+};
+
+class PtgTaskpool;
+
+class PtgTaskClass : public TaskClass {
+ public:
+  PtgTaskpool* owner = nullptr;
+  TaskClassDef def;
+  std::vector<int> param_local;  // param i -> local index
+  std::vector<int> local_param;  // local i -> param index (-1 if derived)
+  uint64_t make_key(const Taskpool* tp, const int32_t* locals) const override;
+  int prepare_input(ExecutionStream* es, Task* t) const override;
+  int complete_execution(ExecutionStream* es, Task* t) const override;
+  void iterate_successors(ExecutionStream* es, const Task* t, uint32_t action_mask, const DepVisitor& v) const override;
+  void iterate_predecessors(ExecutionStream* es, const Task* t, uint32_t action_mask, const DepVisitor& v) const override;
+  int64_t sim_cost(const Task* t) const override;
+  uint32_t gpu_pushout_mask(const Task* t, int device) const override;
+  // helpers
+  bool complete_locals(const Taskpool* tp, int32_t* L, const int32_t* params) const;  // params -> locals, false if out of space
+  uint32_t rank_of(const Taskpool* tp, const int32_t* L) const;
+  int32_t priority_of(const Taskpool* tp, const int32_t* L) const;
+  int count_task_inputs(const Taskpool* tp, const int32_t* L) const;
+  const DepTarget* active_input(const Taskpool* tp, int flow, const int32_t* L) const;
+};
+
+class PtgTaskpool : public Taskpool {
+ public:
+  std::vector<PtgTaskClass*> classes;
+  ShardedMap<Task*> pending{10};
+  std::vector<int64_t> globals;      // generic storage for generated code
+  std::vector<std::string> global_names;
+  bool finalized = false;
+  PtgTaskpool();
+  ~PtgTaskpool() override;
+  PtgTaskClass* add_task_class(TaskClassDef def);
+  void finalize();  // resolve names, build flows/chores
+  void startup(Context* ctx, std::vector<Task*>& ready) override;
+  void on_remote_activation(ExecutionStream* es, RemoteActivation& act) override;
+  // Deliver data for flow `flow` of task (tc, L); appends to `ready` when complete.
+  void activate(ExecutionStream* es, PtgTaskClass* tc, const int32_t* L, int flow, DataCopy* data, std::vector<Task*>& ready);
+  int64_t global(const std::string& n) const;
+  void set_global(const std::string& n, int64_t v);
+};
+
+// Enumerate the execution space of `tc` (all locals), calling f(L).
+void for_each_task(const Taskpool* tp, const PtgTaskClass* tc, const std::function<void(const int32_t*)>& f);
+
+}  // namespace ptg
+}  // namespace parsec

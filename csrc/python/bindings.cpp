@@ -1,0 +1,511 @@
+// Python bindings (pybind11) for the parsec-amd runtime.
+// Blocking calls release the GIL; Python task bodies re-acquire it on the
+// worker thread that runs them.
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "../algos/linalg.hpp"
+#include "../comm/comm.hpp"
+#include "../core/runtime.hpp"
+#include "../data/collections.hpp"
+#include "../device/device.hpp"
+#include "../device/hip_device.hpp"
+#include "../dtd/dtd.hpp"
+#include "../prof/profiling.hpp"
+#include "../ptg/ptg.hpp"
+
+namespace py = pybind11;
+using namespace parsec;
+
+extern "C" int parsec_amd_dgemm_batch(const GemmDesc* descs, int n, void* stream);
+extern "C" int parsec_amd_dtrsm_batch(const TrsmDesc* descs, int n, void* stream);
+extern "C" int parsec_amd_dpotrf_tile(double* A, int n, int lda, int* info, void* stream);
+namespace parsec { void register_builtin_dtd_gpu_bodies(); std::function<int(GpuExecContext*, Task*)> builtin_dtd_gpu_body(const std::string& name); }
+
+namespace {
+
+struct PxContext {
+  Context* ctx = nullptr;
+  std::vector<py::object> keep;  // python objects referenced by running taskpools
+};
+
+static py::dtype dtype_of(int mtype) {
+  switch (mtype) {
+    case MATRIX_BYTE: return py::dtype::of<uint8_t>();
+    case MATRIX_INTEGER: return py::dtype::of<int32_t>();
+    case MATRIX_FLOAT: return py::dtype::of<float>();
+    case MATRIX_DOUBLE: return py::dtype::of<double>();
+    case MATRIX_COMPLEX_FLOAT: return py::dtype("complex64");
+    case MATRIX_COMPLEX_DOUBLE: return py::dtype("complex128");
+  }
+  return py::dtype::of<double>();
+}
+
+// numpy view of a host buffer laid out as an (mb x nb) column-major tile
+static py::array tile_view(void* p, int mtype, int64_t mb, int64_t nb, size_t esz) {
+  if (!p) return py::none();
+  std::vector<py::ssize_t> shape{(py::ssize_t)mb, (py::ssize_t)nb};
+  std::vector<py::ssize_t> strides{(py::ssize_t)esz, (py::ssize_t)(esz * mb)};
+  return py::array(dtype_of(mtype), shape, strides, p, py::capsule(p, [](void*) {}));
+}
+
+struct PyTask {
+  Task* t;
+};
+
+static py::object dtd_arg(Task* t, int i) {
+  auto* dt = static_cast<dtd::DtdTask*>(t);
+  if (i < 0 || i >= (int)dt->args.size()) throw py::index_error("argument index");
+  const dtd::Arg& a = dt->args[i];
+  int op = a.op & dtd::OP_MASK;
+  if (a.flow >= 0) {
+    DataCopy* c = t->data[a.flow].data_in;
+    if (!c) return py::none();
+    Data* d = c->original;
+    if (c->device_index != 0) return py::int_((uintptr_t)c->device_private);
+    if (d && d->dc) {
+      if (auto* tm = dynamic_cast<TiledMatrix*>(d->dc)) return tile_view(c->device_private, tm->mtype, tm->mb, tm->nb, tm->elem_size);
+    }
+    size_t n = d ? d->nb_elts : 0;
+    return py::array(py::dtype::of<uint8_t>(), {(py::ssize_t)n}, {1}, c->device_private, py::capsule(c->device_private, [](void*) {}));
+  }
+  if (op == dtd::VALUE) return py::bytes(static_cast<const char*>(a.ptr), (size_t)a.size);
+  if (op == dtd::SCRATCH) return py::array(py::dtype::of<uint8_t>(), {(py::ssize_t)a.size}, {1}, a.ptr, py::capsule(a.ptr, [](void*) {}));
+  if (op == dtd::REF) return py::int_((uintptr_t)a.ptr);
+  return py::none();
+}
+
+template <class M>
+static void bind_tiled_common(py::class_<M, TiledMatrix>& c) { (void)c; }
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "parsec-amd native runtime";
+
+  // ----------------------------------------------------------- constants
+  m.attr("HOOK_DONE") = (int)HOOK_DONE;
+  m.attr("HOOK_AGAIN") = (int)HOOK_AGAIN;
+  m.attr("HOOK_NEXT") = (int)HOOK_NEXT;
+  m.attr("HOOK_DISABLE") = (int)HOOK_DISABLE;
+  m.attr("HOOK_ASYNC") = (int)HOOK_ASYNC;
+  m.attr("HOOK_ERROR") = (int)HOOK_ERROR;
+  m.attr("DEV_CPU") = (int)DEV_CPU;
+  m.attr("DEV_RECURSIVE") = (int)DEV_RECURSIVE;
+  m.attr("DEV_HIP") = (int)DEV_HIP;
+  m.attr("DEV_ALL") = (int)DEV_ALL;
+  m.attr("INPUT") = (int)dtd::INPUT;
+  m.attr("OUTPUT") = (int)dtd::OUTPUT;
+  m.attr("INOUT") = (int)dtd::INOUT;
+  m.attr("ATOMIC_WRITE") = (int)dtd::ATOMIC_WRITE;
+  m.attr("SCRATCH") = (int)dtd::SCRATCH;
+  m.attr("VALUE") = (int)dtd::VALUE;
+  m.attr("REF") = (int)dtd::REF;
+  m.attr("AFFINITY") = (int)dtd::AFFINITY;
+  m.attr("DONT_TRACK") = (int)dtd::DONT_TRACK;
+  m.attr("PUSHOUT") = (int)dtd::PUSHOUT;
+  m.attr("PULLIN") = (int)dtd::PULLIN;
+  m.attr("PASSED_BY_REF") = (int)dtd::PASSED_BY_REF;
+  m.attr("MATRIX_BYTE") = (int)MATRIX_BYTE;
+  m.attr("MATRIX_INTEGER") = (int)MATRIX_INTEGER;
+  m.attr("MATRIX_FLOAT") = (int)MATRIX_FLOAT;
+  m.attr("MATRIX_DOUBLE") = (int)MATRIX_DOUBLE;
+  m.attr("MATRIX_COMPLEX_FLOAT") = (int)MATRIX_COMPLEX_FLOAT;
+  m.attr("MATRIX_COMPLEX_DOUBLE") = (int)MATRIX_COMPLEX_DOUBLE;
+  m.attr("MATRIX_FULL") = (int)MATRIX_FULL;
+  m.attr("MATRIX_LOWER") = (int)MATRIX_LOWER;
+  m.attr("MATRIX_UPPER") = (int)MATRIX_UPPER;
+
+  // --------------------------------------------------------------- params
+  m.def("mca_set", [](const std::string& n, const std::string& v) { ParamRegistry::instance().set_override(n, v); });
+  m.def("mca_unset", [](const std::string& n) { ParamRegistry::instance().clear_override(n); });
+  m.def("mca_get", [](const std::string& n) -> py::object {
+    std::string v;
+    if (ParamRegistry::instance().lookup(n, v)) return py::str(v);
+    return py::none();
+  });
+  m.def("mca_dump", []() {
+    py::list out;
+    for (auto& p : ParamRegistry::instance().dump()) out.append(py::make_tuple(p.full_name, p.value, p.source, p.help));
+    return out;
+  });
+  m.def("mca_parse_cmdline", [](std::vector<std::string> args) { return ParamRegistry::instance().parse_cmdline(args); });
+  m.def("schedulers", []() {
+    py::list out;
+    for (auto& c : scheduler_components()) out.append(py::make_tuple(c.name, c.priority, c.description));
+    return out;
+  });
+  m.def("termdet_modules", []() { return termdet_available(); });
+  m.def("pins_modules", []() { return pins_modules_available(); });
+
+  // -------------------------------------------------------------- context
+  py::class_<PxContext>(m, "Context")
+      .def(py::init([](int nb_cores, std::vector<std::string> args) {
+             auto* pc = new PxContext();
+             py::gil_scoped_release rel;
+             pc->ctx = context_init(nb_cores, args);
+             return pc;
+           }),
+           py::arg("nb_cores") = -1, py::arg("args") = std::vector<std::string>{})
+      .def("add_taskpool", [](PxContext& c, py::object tpo) {
+        Taskpool* tp = tpo.cast<Taskpool*>();
+        c.keep.push_back(tpo);
+        py::gil_scoped_release rel;
+        return context_add_taskpool(c.ctx, tp);
+      })
+      .def("start", [](PxContext& c) { py::gil_scoped_release rel; return context_start(c.ctx); })
+      .def("test", [](PxContext& c) { return context_test(c.ctx); })
+      .def("wait", [](PxContext& c) {
+        {
+          py::gil_scoped_release rel;
+          context_wait(c.ctx);
+        }
+        c.keep.clear();
+        return 0;
+      })
+      .def("fini", [](PxContext& c) {
+        if (!c.ctx) return 0;
+        {
+          py::gil_scoped_release rel;
+          context_fini(&c.ctx);
+        }
+        c.keep.clear();
+        return 0;
+      })
+      .def_property_readonly("nb_cores", [](PxContext& c) { return c.ctx->nb_cores; })
+      .def_property_readonly("nb_vp", [](PxContext& c) { return c.ctx->nb_vp; })
+      .def_property_readonly("rank", [](PxContext& c) { return c.ctx->my_rank; })
+      .def_property_readonly("nb_nodes", [](PxContext& c) { return c.ctx->nb_nodes; })
+      .def_property_readonly("scheduler", [](PxContext& c) { return c.ctx->scheduler_name; })
+      .def_property_readonly("active_taskpools", [](PxContext& c) { return c.ctx->active_taskpools.load(); })
+      .def_property_readonly("alive", [](PxContext& c) { return c.ctx != nullptr; });
+
+  // ------------------------------------------------------------- taskpools
+  py::class_<Taskpool>(m, "Taskpool")
+      .def_property("name", [](Taskpool& t) { return t.taskpool_name; }, [](Taskpool& t, const std::string& n) { t.taskpool_name = n; })
+      .def_property_readonly("taskpool_id", [](Taskpool& t) { return t.taskpool_id; })
+      .def_property("priority", [](Taskpool& t) { return t.priority; }, [](Taskpool& t, int p) { taskpool_set_priority(&t, p); })
+      .def_property("devices_mask", [](Taskpool& t) { return t.devices_index_mask; }, [](Taskpool& t, uint32_t m) { t.devices_index_mask = m; })
+      .def_property("termdet", [](Taskpool& t) { return t.termdet_name; }, [](Taskpool& t, const std::string& n) { t.termdet_name = n; })
+      .def_property_readonly("nb_tasks", [](Taskpool& t) { return t.nb_tasks.load(); })
+      .def_property_readonly("nb_pending_actions", [](Taskpool& t) { return t.nb_pending_actions.load(); })
+      .def_property_readonly("completed", [](Taskpool& t) { return t.completed.load(); })
+      .def_property_readonly("simulation_date", [](Taskpool& t) { return t.largest_simulation_date.load(); })
+      .def("set_complete_callback", [](Taskpool& t, py::function f) {
+        auto holder = std::make_shared<py::function>(f);
+        t.on_complete = [holder](Taskpool*) {
+          py::gil_scoped_acquire g;
+          py::object r = (*holder)();
+          return r.is_none() ? 0 : r.cast<int>();
+        };
+      })
+      .def("set_enqueue_callback", [](Taskpool& t, py::function f) {
+        auto holder = std::make_shared<py::function>(f);
+        t.on_enqueue = [holder](Taskpool*) {
+          py::gil_scoped_acquire g;
+          py::object r = (*holder)();
+          return r.is_none() ? 0 : r.cast<int>();
+        };
+      })
+      .def("task_classes", [](Taskpool& t) {
+        std::vector<std::string> out;
+        for (auto* tc : t.task_classes) out.push_back(tc->name);
+        return out;
+      });
+  m.def("taskpool_free", [](Taskpool* tp) { taskpool_free(tp); });
+  m.def("compose", [](Taskpool* a, Taskpool* b) { return compose(a, b); }, py::return_value_policy::reference);
+  m.def("taskpool_lookup", [](uint32_t id) { return taskpool_lookup(id); }, py::return_value_policy::reference);
+  m.def("taskpool_sync_ids", []() { taskpool_sync_ids(); });
+
+  py::class_<ptg::PtgTaskpool, Taskpool>(m, "PtgTaskpool")
+      .def("set_global", &ptg::PtgTaskpool::set_global)
+      .def("global_", &ptg::PtgTaskpool::global)
+      .def("nb_task_classes", [](ptg::PtgTaskpool& t) { return t.classes.size(); })
+      .def("count_tasks", [](ptg::PtgTaskpool& t, const std::string& name) {
+        if (!t.finalized) t.finalize();
+        int64_t n = 0;
+        for (auto* tc : t.classes)
+          if (tc->name == name) ptg::for_each_task(&t, tc, [&](const int32_t*) { ++n; });
+        return n;
+      });
+
+  // ------------------------------------------------------------------ DTD
+  py::class_<dtd::Tile>(m, "Tile")
+      .def_property_readonly("rank", [](dtd::Tile& t) { return t.rank; })
+      .def_property_readonly("key", [](dtd::Tile& t) { return t.key; })
+      .def("data", [](dtd::Tile& t) -> py::object {
+        if (!t.data) return py::none();
+        DataCopy* c = data_pull_to_host(t.data);
+        if (!c) return py::none();
+        if (t.dc) if (auto* tm = dynamic_cast<TiledMatrix*>(t.dc)) return tile_view(c->device_private, tm->mtype, tm->mb, tm->nb, tm->elem_size);
+        return py::array(py::dtype::of<uint8_t>(), {(py::ssize_t)t.data->nb_elts}, {1}, c->device_private, py::capsule(c->device_private, [](void*) {}));
+      });
+
+  py::class_<PyTask>(m, "Task")
+      .def("arg", [](PyTask& p, int i) { return dtd_arg(p.t, i); })
+      .def("value_int", [](PyTask& p, int i) { auto* a = static_cast<int32_t*>(dtd::task_arg(p.t, i)); return a ? (int64_t)*a : 0; })
+      .def("value_int64", [](PyTask& p, int i) { auto* a = static_cast<int64_t*>(dtd::task_arg(p.t, i)); return a ? *a : 0; })
+      .def("value_double", [](PyTask& p, int i) { auto* a = static_cast<double*>(dtd::task_arg(p.t, i)); return a ? *a : 0.0; })
+      .def("ptr", [](PyTask& p, int i) { return (uintptr_t)dtd::task_arg(p.t, i); })
+      .def_property_readonly("nb_args", [](PyTask& p) { return dtd::task_nb_args(p.t); })
+      .def_property_readonly("seq", [](PyTask& p) { return static_cast<dtd::DtdTask*>(p.t)->seq; })
+      .def_property_readonly("rank", [](PyTask& p) { return static_cast<dtd::DtdTask*>(p.t)->rank; })
+      .def_property_readonly("name", [](PyTask& p) { return p.t->task_class->name; })
+      .def_property_readonly("priority", [](PyTask& p) { return p.t->priority; })
+      .def("user_trigger_termination", [](PyTask& p) { p.t->taskpool->tdm->user_trigger(p.t->taskpool); });
+
+  py::class_<dtd::DtdTaskClass>(m, "DtdTaskClass")
+      .def_property_readonly("name", [](dtd::DtdTaskClass& c) { return c.name; })
+      .def_property_readonly("nb_flows", [](dtd::DtdTaskClass& c) { return c.flows.size(); });
+
+  py::class_<dtd::DtdTaskpool, Taskpool>(m, "DtdTaskpool")
+      .def(py::init([]() { return new dtd::DtdTaskpool(); }))
+      .def("task_class", [](dtd::DtdTaskpool& tp, const std::string& name, std::vector<std::pair<int, int>> params) { return tp.create_task_class(name, params); },
+           py::return_value_policy::reference)
+      .def("add_chore",
+           [](dtd::DtdTaskpool& tp, dtd::DtdTaskClass* tc, int device, py::object fn, const std::string& builtin) {
+             Hook cpu;
+             std::function<int(GpuExecContext*, Task*)> gpu;
+             if (!fn.is_none()) {
+               auto holder = std::make_shared<py::object>(fn);
+               cpu = [holder](ExecutionStream*, Task* t) {
+                 py::gil_scoped_acquire g;
+                 PyTask pt{t};
+                 py::object r = (*holder)(pt);
+                 return r.is_none() ? (int)HOOK_DONE : r.cast<int>();
+               };
+             }
+             if (!builtin.empty()) gpu = builtin_dtd_gpu_body(builtin);
+             return tp.add_chore(tc, (uint32_t)device, cpu, gpu);
+           },
+           py::arg("tc"), py::arg("device"), py::arg("fn") = py::none(), py::arg("builtin") = "")
+      .def("insert_task",
+           [](dtd::DtdTaskpool& tp, dtd::DtdTaskClass* tc, py::list args, int priority) {
+             std::vector<dtd::Arg> a;
+             std::vector<std::string> store;  // keep VALUE bytes alive during insertion
+             store.reserve(args.size());
+             for (auto item : args) {
+               py::tuple tup = item.cast<py::tuple>();
+               dtd::Arg x;
+               x.op = tup[1].cast<int>();
+               int op = x.op & dtd::OP_MASK;
+               py::object o = tup[0];
+               if (op == dtd::VALUE) {
+                 if (py::isinstance<py::bytes>(o)) store.push_back(o.cast<std::string>());
+                 else if (py::isinstance<py::float_>(o)) { double v = o.cast<double>(); store.emplace_back((const char*)&v, sizeof v); }
+                 else { int64_t v = o.cast<int64_t>(); int32_t v32 = (int32_t)v; if (tup.size() > 2 && tup[2].cast<int>() == 8) store.emplace_back((const char*)&v, 8); else store.emplace_back((const char*)&v32, 4); }
+                 x.ptr = store.back().data();
+                 x.size = (int)store.back().size();
+               } else if (op == dtd::SCRATCH) {
+                 x.size = o.cast<int>();
+               } else if (op == dtd::REF) {
+                 x.ptr = (void*)o.cast<uintptr_t>();
+               } else {
+                 x.tile = o.is_none() ? nullptr : o.cast<dtd::Tile*>();
+                 x.size = dtd::PASSED_BY_REF;
+               }
+               a.push_back(x);
+             }
+             py::gil_scoped_release rel;
+             tp.insert_task(tc, priority, a);
+           },
+           py::arg("tc"), py::arg("args"), py::arg("priority") = 0)
+      .def("tile_of", [](dtd::DtdTaskpool& tp, DataCollection* dc, uint64_t key) { return tp.tile_of(dc, key); }, py::return_value_policy::reference)
+      .def("tile_new", [](dtd::DtdTaskpool& tp, size_t bytes, int rank) { return tp.tile_new(bytes, rank); }, py::return_value_policy::reference)
+      .def("data_flush", [](dtd::DtdTaskpool& tp, dtd::Tile* t) { py::gil_scoped_release rel; return tp.data_flush(t); })
+      .def("data_flush_all", [](dtd::DtdTaskpool& tp, DataCollection* dc) { py::gil_scoped_release rel; return tp.data_flush_all(dc); })
+      .def("wait", [](dtd::DtdTaskpool& tp) { py::gil_scoped_release rel; return tp.wait(); })
+      .def_property("window", [](dtd::DtdTaskpool& tp) { return tp.window; }, [](dtd::DtdTaskpool& tp, int64_t w) { tp.window = w; })
+      .def_property("threshold", [](dtd::DtdTaskpool& tp) { return tp.threshold; }, [](dtd::DtdTaskpool& tp, int64_t w) { tp.threshold = w; });
+
+  // ----------------------------------------------------------- collections
+  py::class_<DataCollection>(m, "DataCollection")
+      .def_property_readonly("myrank", [](DataCollection& d) { return d.myrank; })
+      .def_property_readonly("nodes", [](DataCollection& d) { return d.nodes; })
+      .def_property_readonly("dc_id", [](DataCollection& d) { return d.dc_id; })
+      .def("rank_of", [](DataCollection& d, std::vector<int64_t> idx) { return d.rank_of(idx.data(), (int)idx.size()); })
+      .def("vpid_of", [](DataCollection& d, std::vector<int64_t> idx) { return d.vpid_of(idx.data(), (int)idx.size()); })
+      .def("data_key", [](DataCollection& d, std::vector<int64_t> idx) { return d.data_key(idx.data(), (int)idx.size()); })
+      .def("rank_of_key", &DataCollection::rank_of_key)
+      .def("key_to_string", &DataCollection::key_to_string);
+
+  py::class_<TiledMatrix, DataCollection>(m, "TiledMatrix")
+      .def_readonly("mb", &TiledMatrix::mb)
+      .def_readonly("nb", &TiledMatrix::nb)
+      .def_readonly("lm", &TiledMatrix::lm)
+      .def_readonly("ln", &TiledMatrix::ln)
+      .def_readonly("mt", &TiledMatrix::mt)
+      .def_readonly("nt", &TiledMatrix::nt)
+      .def_readonly("lmt", &TiledMatrix::lmt)
+      .def_readonly("lnt", &TiledMatrix::lnt)
+      .def_readonly("mtype", &TiledMatrix::mtype)
+      .def_readonly("nb_local_tiles", &TiledMatrix::nb_local_tiles)
+      .def_readonly("storage_device", &TiledMatrix::storage_device)
+      .def_property_readonly("storage_ptr", [](TiledMatrix& t) { return (uintptr_t)t.mat; })
+      .def_property_readonly("storage_bytes", [](TiledMatrix& t) { return (size_t)t.nb_local_tiles * (size_t)t.bsiz * t.elem_size; })
+      .def("local_index", &TiledMatrix::local_index)
+      .def("tile_ptr", [](TiledMatrix& t, int64_t a, int64_t b) { return (uintptr_t)t.tile_ptr(a, b); })
+      .def("tile", [](TiledMatrix& t, int64_t a, int64_t b) -> py::object {
+        Data* d = t.tile_data(a, b);
+        if (!d) return py::none();
+        DataCopy* c = t.storage_device == 0 ? d->copy(0) : data_pull_to_host(d);
+        if (t.storage_device == 0) {
+          // the user's host tile must show the newest version
+          c = data_pull_to_host(d);
+        }
+        return tile_view(c->device_private, t.mtype, t.mb, t.nb, t.elem_size);
+      })
+      .def("mark_host_modified", [](TiledMatrix& t, int64_t a, int64_t b) {
+        Data* d = t.tile_data(a, b);
+        if (!d) return;
+        DataCopy* c = d->copy(0);
+        if (!c) return;
+        std::lock_guard<SpinLock> g(d->lock);
+        c->version = d->newest_version() + 1;
+        c->coherency_state = COHERENCY_OWNED;
+        d->owner_device = 0;
+      })
+      .def("tile_rows", &TiledMatrix::tile_rows)
+      .def("tile_cols", &TiledMatrix::tile_cols);
+
+  py::class_<BlockCyclic, TiledMatrix>(m, "BlockCyclic")
+      .def(py::init([](int mtype, int myrank, int64_t mb, int64_t nb, int64_t lm, int64_t ln, int P, int Q, int kp, int kq, int ip, int jq, int device, uintptr_t ptr, int nb_vp) {
+             auto* bc = new BlockCyclic();
+             bc->storage_device = device;
+             bc->init(mtype, myrank, mb, nb, lm, ln, 0, 0, lm, ln, P, Q, kp, kq, ip, jq);
+             bc->nb_vp = nb_vp;
+             bc->allocate_storage((void*)ptr);
+             return bc;
+           }),
+           py::arg("mtype"), py::arg("myrank"), py::arg("mb"), py::arg("nb"), py::arg("lm"), py::arg("ln"), py::arg("P") = 1, py::arg("Q") = 1,
+           py::arg("kp") = 1, py::arg("kq") = 1, py::arg("ip") = 0, py::arg("jq") = 0, py::arg("device") = 0, py::arg("ptr") = 0, py::arg("nb_vp") = 1)
+      .def_readonly("P", &BlockCyclic::P)
+      .def_readonly("Q", &BlockCyclic::Q)
+      .def_readonly("llm_tiles", &BlockCyclic::llm_tiles)
+      .def_readonly("lln_tiles", &BlockCyclic::lln_tiles);
+
+  py::class_<SymBlockCyclic, BlockCyclic>(m, "SymBlockCyclic")
+      .def(py::init([](int mtype, int myrank, int64_t mb, int64_t nb, int64_t lm, int64_t ln, int P, int Q, int uplo, int device, uintptr_t ptr) {
+             auto* bc = new SymBlockCyclic();
+             bc->storage_device = device;
+             bc->init_sym(mtype, myrank, mb, nb, lm, ln, 0, 0, lm, ln, P, Q, uplo);
+             bc->allocate_storage((void*)ptr);
+             return bc;
+           }),
+           py::arg("mtype"), py::arg("myrank"), py::arg("mb"), py::arg("nb"), py::arg("lm"), py::arg("ln"), py::arg("P") = 1, py::arg("Q") = 1,
+           py::arg("uplo") = (int)MATRIX_LOWER, py::arg("device") = 0, py::arg("ptr") = 0);
+
+  py::class_<TabularMatrix, TiledMatrix>(m, "TabularMatrix")
+      .def(py::init([](int mtype, int myrank, int nodes, int64_t mb, int64_t nb, int64_t lm, int64_t ln, std::vector<int> ranks) {
+             auto* t = new TabularMatrix();
+             t->init_tab(mtype, myrank, nodes, mb, nb, lm, ln, ranks);
+             t->allocate_storage(nullptr);
+             return t;
+           }),
+           py::arg("mtype"), py::arg("myrank"), py::arg("nodes"), py::arg("mb"), py::arg("nb"), py::arg("lm"), py::arg("ln"), py::arg("ranks"));
+
+  py::class_<VectorCyclic, TiledMatrix>(m, "VectorCyclic")
+      .def(py::init([](int mtype, int myrank, int nodes, int64_t mb, int64_t lm, int dist, int P, int Q) {
+             auto* v = new VectorCyclic();
+             v->init_vec(mtype, myrank, nodes, mb, lm, dist, P, Q);
+             v->allocate_storage(nullptr);
+             return v;
+           }),
+           py::arg("mtype"), py::arg("myrank"), py::arg("nodes"), py::arg("mb"), py::arg("lm"), py::arg("dist") = 0, py::arg("P") = 1, py::arg("Q") = 1);
+
+  py::class_<BandMatrix, TiledMatrix>(m, "BandMatrix")
+      .def(py::init([](BlockCyclic* band, BlockCyclic* off, int bs) {
+             auto* b = new BandMatrix();
+             b->init_band(band, off, bs);
+             return b;
+           }),
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>());
+
+  py::class_<HashCollection, DataCollection>(m, "HashCollection")
+      .def(py::init([](int myrank, int nodes) {
+        auto* h = new HashCollection();
+        h->myrank = (uint32_t)myrank;
+        h->nodes = (uint32_t)nodes;
+        dc_register_id(h);
+        return h;
+      }))
+      .def("set_entry", [](HashCollection& h, uint64_t key, uint32_t rank, int32_t vp, uintptr_t ptr, size_t size) { h.set_entry(key, rank, vp, (void*)ptr, size); });
+
+  // ---------------------------------------------------------------- algos
+  m.def("dpotrf_new", [](TiledMatrix* A, int uplo) {
+        auto* info = new int(0);
+        auto* tp = algos::dpotrf_new(A, uplo, info);
+        tp->destructor_hook = [info]() { delete info; };
+        return py::make_tuple(py::cast(tp, py::return_value_policy::take_ownership), (uintptr_t)info);
+      });
+  m.def("read_int", [](uintptr_t p) { return *reinterpret_cast<int*>(p); });
+
+  // --------------------------------------------------------------- devices
+  m.def("devices", []() {
+    py::list out;
+    for (auto* d : DeviceRegistry::instance().devices) {
+      if (!d) continue;
+      py::dict e;
+      e["index"] = d->device_index;
+      e["name"] = d->name;
+      e["type"] = d->type;
+      e["gflops_fp64"] = d->gflops_fp64;
+      e["weight"] = d->gflops_weight;
+      e["executed_tasks"] = d->stats.executed_tasks.load();
+      e["kernel_launches"] = d->stats.kernel_launches.load();
+      e["batched_tasks"] = d->stats.batched_tasks.load();
+      e["bytes_in"] = d->stats.bytes_in.load();
+      e["bytes_out"] = d->stats.bytes_out.load();
+      e["bytes_d2d"] = d->stats.bytes_d2d.load();
+      e["data_faults"] = d->stats.data_faults.load();
+      out.append(e);
+    }
+    return out;
+  });
+  m.def("nb_gpus", []() { return DeviceRegistry::instance().nb_gpus(); });
+  m.def("first_gpu_device_index", &first_gpu_device_index);
+  m.def("device_alloc", [](int dev, size_t bytes) { return (uintptr_t)device_alloc(dev, bytes); });
+  m.def("device_free", [](int dev, uintptr_t p) { device_free(dev, (void*)p); });
+  m.def("device_memcpy", [](int dd, uintptr_t dst, int sd, uintptr_t src, size_t n) { return device_memcpy(dd, (void*)dst, sd, (const void*)src, n); });
+
+  // raw kernels (tests): descriptors built in python, device pointers as ints
+  m.def("kernel_dgemm", [](uintptr_t A, uintptr_t B, uintptr_t C, int mm, int nn, int kk, int lda, int ldb, int ldc, double alpha, double beta, int transB, int lower, uintptr_t stream) {
+    GemmDesc g{(const double*)A, (const double*)B, (double*)C, mm, nn, kk, lda, ldb, ldc, alpha, beta, 0, (uint8_t)transB, (uint8_t)lower, 0};
+    return parsec_amd_dgemm_batch(&g, 1, (void*)stream);
+  });
+  m.def("kernel_dgemm_batch", [](std::vector<std::tuple<uintptr_t, uintptr_t, uintptr_t, int, int, int, int, int, int, double, double, int, int>> ds, uintptr_t stream) {
+    std::vector<GemmDesc> v;
+    for (auto& d : ds) {
+      GemmDesc g{(const double*)std::get<0>(d), (const double*)std::get<1>(d), (double*)std::get<2>(d), std::get<3>(d), std::get<4>(d), std::get<5>(d), std::get<6>(d), std::get<7>(d), std::get<8>(d), std::get<9>(d), std::get<10>(d), 0, (uint8_t)std::get<11>(d), (uint8_t)std::get<12>(d), 0};
+      v.push_back(g);
+    }
+    return parsec_amd_dgemm_batch(v.data(), (int)v.size(), (void*)stream);
+  });
+  m.def("kernel_dtrsm", [](uintptr_t L, uintptr_t B, int mm, int nn, int ldl, int ldb, uintptr_t stream) {
+    TrsmDesc t;
+    t.L = (const double*)L; t.B = (double*)B; t.m = mm; t.n = nn; t.ldl = ldl; t.ldb = ldb; t.trans = 1;
+    return parsec_amd_dtrsm_batch(&t, 1, (void*)stream);
+  });
+  m.def("kernel_dpotrf", [](uintptr_t A, int n, int lda, uintptr_t info, uintptr_t stream) { return parsec_amd_dpotrf_tile((double*)A, n, lda, (int*)info, (void*)stream); });
+
+  // ------------------------------------------------------------- profiling
+  m.def("profiling_dump", [](const std::string& f) { return profiling_dump(f); });
+  m.def("profiling_enabled", &profiling_enabled);
+  m.def("pins_counters", []() { return pins_counters(); });
+  m.def("properties", []() { return properties_snapshot(); });
+  m.def("properties_set", &properties_set);
+  m.def("properties_dump_shm", &properties_dump_shm);
+  m.def("history", []() { return history_dump(); });
+
+  // ------------------------------------------------------------------ comm
+  m.def("comm_init", [](int rank, int size, const std::string& job, int gpu) { py::gil_scoped_release rel; return comm_init(rank, size, job, gpu); });
+  m.def("comm_fini", []() { py::gil_scoped_release rel; comm_fini(); });
+  m.def("comm_barrier", []() { py::gil_scoped_release rel; return comm_barrier(); });
+  m.def("comm_rank", &comm_rank);
+  m.def("comm_size", &comm_size);
+  m.def("comm_allreduce_max", [](uint32_t v) { py::gil_scoped_release rel; return comm_allreduce_max_u32(v); });
+}

@@ -1,0 +1,149 @@
+"""Native build driver: generates build/build.ninja and runs ninja.
+
+Outputs (in-tree so they travel with the repo snapshot to the GPU box):
+  parsec_amd/lib/libparsec_amd.so   runtime + gfx950 HIP kernels
+  parsec_amd/_C.<abi>.so            pybind11 bindings
+  parsec_amd/bin/ptgpp              .jdf -> C++ compiler
+  build/tests/*                     native unit tests
+
+Usage: python -m parsec_amd._build [--clean] [-j N]
+"""
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "parsec_amd")
+BUILD = os.path.join(ROOT, "build")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+
+CORE_SOURCES = [
+    "csrc/core/mca.cpp",
+    "csrc/core/context.cpp",
+    "csrc/core/scheduling.cpp",
+    "csrc/sched/schedulers.cpp",
+    "csrc/termdet/termdet.cpp",
+    "csrc/data/data.cpp",
+    "csrc/data/collections.cpp",
+    "csrc/device/device.cpp",
+    "csrc/device/hip_device.cpp",
+    "csrc/prof/profiling.cpp",
+    "csrc/comm/remote_dep.cpp",
+    "csrc/ptg/ptg.cpp",
+    "csrc/dtd/dtd.cpp",
+    "csrc/algos/dpotrf.cpp",
+    "csrc/algos/dtd_builtins.cpp",
+    "csrc/capi/capi.cpp",
+]
+HIP_SOURCES = [
+    "csrc/kernels/tile_kernels.hip",
+]
+PY_SOURCES = ["csrc/python/bindings.cpp"]
+PTGPP_SOURCES = []
+TEST_SOURCES = []
+
+
+def _exists(paths):
+    return [p for p in paths if os.path.exists(os.path.join(ROOT, p))]
+
+
+def _pybind_include():
+    import pybind11
+
+    return pybind11.get_include()
+
+
+def generate():
+    os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(os.path.join(PKG, "lib"), exist_ok=True)
+    os.makedirs(os.path.join(PKG, "bin"), exist_ok=True)
+    py_inc = sysconfig.get_paths()["include"]
+    ext = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    common = f"-std=c++20 -O3 -g -fPIC -Wall -Wno-unused-result -D__HIP_PLATFORM_AMD__ -I{ROCM}/include -I{ROOT}/csrc"
+    hipflags = f"-std=c++20 -O3 -fPIC --offload-arch={ARCH} -D__HIP_PLATFORM_AMD__ -I{ROOT}/csrc -Wno-unused-result"
+    lines = [
+        f"rocm = {ROCM}",
+        f"cxxflags = {common}",
+        f"hipflags = {hipflags}",
+        "rule cxx",
+        "  command = g++ $cxxflags -MMD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "  description = CXX $out",
+        "rule hipcc",
+        f"  command = {ROCM}/bin/hipcc $hipflags -MMD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "  description = HIPCC $out",
+        "rule solink",
+        "  command = g++ -shared -o $out $in $libs",
+        "  description = LINK $out",
+        "rule exelink",
+        "  command = g++ -o $out $in $libs",
+        "  description = LINK $out",
+        "rule pycxx",
+        f"  command = g++ $cxxflags -I{py_inc} -I{_pybind_include()} -fvisibility=hidden -MMD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "  description = PYCXX $out",
+    ]
+    objs = []
+    for src in _exists(CORE_SOURCES):
+        obj = os.path.join("obj", src.replace("/", "_") + ".o")
+        lines.append(f"build {obj}: cxx {os.path.join(ROOT, src)}")
+        objs.append(obj)
+    for src in _exists(HIP_SOURCES):
+        obj = os.path.join("obj", src.replace("/", "_") + ".o")
+        lines.append(f"build {obj}: hipcc {os.path.join(ROOT, src)}")
+        objs.append(obj)
+    lib = os.path.join(PKG, "lib", "libparsec_amd.so")
+    libs = f"-L{ROCM}/lib -lamdhip64 -lrccl -latomic -lpthread -lrt -Wl,-rpath,{ROCM}/lib"
+    lines.append(f"build {lib}: solink {' '.join(objs)}")
+    lines.append(f"  libs = {libs}")
+    pyobjs = []
+    for src in _exists(PY_SOURCES):
+        obj = os.path.join("obj", src.replace("/", "_") + ".o")
+        lines.append(f"build {obj}: pycxx {os.path.join(ROOT, src)}")
+        pyobjs.append(obj)
+    if pyobjs:
+        mod = os.path.join(PKG, "_C" + ext)
+        lines.append(f"build {mod}: solink {' '.join(pyobjs)} | {lib}")
+        lines.append(f"  libs = -L{PKG}/lib -lparsec_amd '-Wl,-rpath,$$ORIGIN/lib' {libs}")
+    ptg_objs = []
+    for src in _exists(PTGPP_SOURCES):
+        obj = os.path.join("obj", src.replace("/", "_") + ".o")
+        lines.append(f"build {obj}: cxx {os.path.join(ROOT, src)}")
+        ptg_objs.append(obj)
+    if ptg_objs:
+        lines.append(f"build {os.path.join(PKG, 'bin', 'ptgpp')}: exelink {' '.join(ptg_objs)}")
+        lines.append("  libs = ")
+    for src in _exists(TEST_SOURCES):
+        obj = os.path.join("obj", src.replace("/", "_") + ".o")
+        exe = os.path.join(BUILD, "tests", os.path.splitext(os.path.basename(src))[0])
+        lines.append(f"build {obj}: cxx {os.path.join(ROOT, src)}")
+        lines.append(f"build {exe}: exelink {obj} | {lib}")
+        lines.append(f"  libs = -L{PKG}/lib -lparsec_amd -Wl,-rpath,{PKG}/lib {libs}")
+    with open(os.path.join(BUILD, "build.ninja"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def build(jobs=None, verbose=False):
+    generate()
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    cmd = ["ninja", "-C", BUILD, f"-j{jobs}"]
+    if verbose:
+        cmd.append("-v")
+    r = subprocess.run(cmd)
+    if r.returncode != 0:
+        raise RuntimeError("native build failed")
+
+
+if __name__ == "__main__":
+    if "--clean" in sys.argv:
+        subprocess.run(["rm", "-rf", BUILD])
+    j = None
+    if "-j" in sys.argv:
+        j = int(sys.argv[sys.argv.index("-j") + 1])
+    build(j, verbose="-v" in sys.argv)
