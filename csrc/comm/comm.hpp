@@ -92,6 +92,7 @@ int comm_init(int rank, int size, const std::string& job_id, int gpu_ordinal);
 void comm_fini();
 
 TermdetModule* fourcounter_module();
+void fourcounter_register(CommEngine* ce);
 void termdet_user_trigger_broadcast(Taskpool* tp);
 
 }  // namespace parsec

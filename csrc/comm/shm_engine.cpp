@@ -1,0 +1,432 @@
+// Shared-memory active messages + RCCL pair communicators.
+//
+// Every rank owns one POSIX shm segment holding a header and one inbound SPSC
+// ring per peer (ring[src] is written only by rank src, read only by our comm
+// thread). Producers on the sending side serialize per destination; a full ring
+// never blocks a producer: the message goes to a per-destination backlog that
+// the comm thread flushes (the reference's funnelled MPI engine keeps a similar
+// per-peer FIFO, parsec_mpi_funnelled.c:1089-1139).
+//
+// RCCL: one 2-rank communicator + one HIP stream per DIRECTED rank pair. A
+// directed pair only ever carries sends from its rank 0 to its rank 1, issued in
+// the order GET requests arrive, and the receiver posts its receives in the order
+// it sent those GETs, so transfers are FIFO-matched and can never cross or
+// deadlock (unlike one shared communicator whose ordered stream would serialize
+// a send behind an unrelated receive).
+#include "shm_engine.hpp"
+
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstring>
+
+namespace parsec {
+
+namespace {
+constexpr uint64_t kMagic = 0x5041'4D44'5348'4D31ULL;  // "PAMDSHM1"
+struct MsgHdr {
+  uint32_t len;   // total bytes incl. header, multiple of 16; 0 = wrap marker
+  int16_t tag;
+  int16_t src;
+  uint32_t plen;  // user bytes
+  uint32_t magic;
+};
+static_assert(sizeof(MsgHdr) == 16, "hdr");
+inline uint64_t align16(uint64_t v) { return (v + 15) & ~uint64_t(15); }
+
+enum CollKind : uint8_t { COLL_ARRIVE = 0, COLL_RELEASE = 1 };
+struct CollMsg {
+  uint8_t kind;
+  uint8_t pad[7];
+  uint64_t epoch;
+  uint64_t value;
+};
+ShmEngine* g_engine = nullptr;
+}  // namespace
+
+ShmEngine* shm_engine() { return g_engine; }
+
+static std::string seg_name(const std::string& job, int r) {
+  std::string s = "/pamd_" + job + "_" + std::to_string(r);
+  for (auto& c : s) if (c != '/' && !isalnum((unsigned char)c) && c != '_') c = '_';
+  return s;
+}
+
+ShmEngine::ShmEngine(int rank_, int size_, const std::string& job, int gpu) : job_(job), gpu_(gpu) {
+  rank = rank_;
+  size = size_;
+  ring_bytes_ = ParamRegistry::instance().reg_sizet("comm", "shm", "ring_bytes", "Bytes of each inbound shared-memory ring", (size_t)8 << 20);
+  cbs_.resize(TAG_MAX);
+  for (int i = 0; i < size; ++i) out_.emplace_back(new Out());
+  maps_.assign(size, nullptr);
+  map_len_.assign(size, 0);
+}
+
+ShmEngine::~ShmEngine() {
+  stop_thread();
+  for (int r = 0; r < size; ++r)
+    if (maps_[r]) munmap(maps_[r], map_len_[r]);
+  shm_unlink(seg_name(job_, rank).c_str());
+}
+
+static size_t ring_stride(size_t ring_bytes) { return align16(sizeof(ShmRing) + ring_bytes + 64); }
+
+int ShmEngine::init() {
+  const size_t stride = ring_stride(ring_bytes_);
+  const size_t len = align16(sizeof(ShmHeader)) + stride * (size_t)size;
+  std::string me = seg_name(job_, rank);
+  shm_unlink(me.c_str());
+  int fd = shm_open(me.c_str(), O_CREAT | O_RDWR | O_EXCL, 0600);
+  if (fd < 0) { warning("shm_open(%s) failed", me.c_str()); return -1; }
+  if (ftruncate(fd, (off_t)len) != 0) { close(fd); return -1; }
+  void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) return -1;
+  std::memset(p, 0, align16(sizeof(ShmHeader)));
+  maps_[rank] = p;
+  map_len_[rank] = len;
+  me_ = static_cast<ShmHeader*>(p);
+  me_->rank = rank;
+  me_->size = size;
+  me_->ring_bytes = ring_bytes_;
+  for (int s = 0; s < size; ++s) {
+    auto* r = reinterpret_cast<ShmRing*>(static_cast<char*>(p) + align16(sizeof(ShmHeader)) + stride * s);
+    r->head.store(0);
+    r->tail.store(0);
+    r->cap = ring_bytes_;
+  }
+  me_->magic = kMagic;
+  me_->ready.store(1, std::memory_order_release);
+  // map every peer segment (wait for them to appear)
+  uint64_t t0 = now_ns();
+  for (int r = 0; r < size; ++r) {
+    if (r == rank) continue;
+    std::string nm = seg_name(job_, r);
+    for (;;) {
+      int pfd = shm_open(nm.c_str(), O_RDWR, 0600);
+      if (pfd >= 0) {
+        struct stat st;
+        if (fstat(pfd, &st) == 0 && (size_t)st.st_size >= len) {
+          void* q = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, pfd, 0);
+          close(pfd);
+          if (q != MAP_FAILED) {
+            auto* h = static_cast<ShmHeader*>(q);
+            while (h->ready.load(std::memory_order_acquire) == 0 || h->magic != kMagic) {
+              if (now_ns() - t0 > 120ull * 1000000000ull) { warning("rank %d never became ready", r); return -1; }
+              std::this_thread::sleep_for(std::chrono::milliseconds(1));
+            }
+            maps_[r] = q;
+            map_len_[r] = len;
+            break;
+          }
+        } else {
+          close(pfd);
+        }
+      }
+      if (now_ns() - t0 > 120ull * 1000000000ull) { warning("timed out waiting for rank %d shm segment", r); return -1; }
+      std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    }
+  }
+  // collective tag for barrier / allreduce
+  tag_register(TAG_BARRIER, [this](int src, int, const void* msg, size_t) {
+    (void)src;
+    CollMsg m;
+    std::memcpy(&m, msg, sizeof(m));
+    std::unique_lock<std::mutex> g(coll_m_);
+    if (m.kind == COLL_ARRIVE) {
+      coll_acc_ = std::max(coll_acc_, m.value);
+      if (++coll_arrived_ == size) {
+        CollMsg rel{COLL_RELEASE, {}, m.epoch, coll_acc_};
+        coll_arrived_ = 0;
+        coll_result_ = coll_acc_;
+        coll_acc_ = 0;
+        coll_done_epoch_ = m.epoch;
+        g.unlock();
+        for (int r = 1; r < size; ++r) send_am(TAG_BARRIER, r, &rel, sizeof(rel));
+        coll_cv_.notify_all();
+      }
+    } else {
+      coll_result_ = m.value;
+      coll_done_epoch_ = m.epoch;
+      coll_cv_.notify_all();
+    }
+  });
+  g_engine = this;
+  start_thread();
+  if (gpu_ >= 0 && ParamRegistry::instance().reg_int("comm", "", "rccl", "Use RCCL for device-resident data (GPU->GPU over xGMI)", 1)) {
+    std::atomic<int> rc{1};
+    std::atomic<bool> done{false};
+    post([&] { rc = init_rccl(); done = true; });
+    while (!done.load()) std::this_thread::sleep_for(std::chrono::microseconds(200));
+    rccl_ok_ = rc.load() == 0;
+    if (!rccl_ok_) warning("RCCL data plane unavailable (rc=%d): device tiles will be staged through host memory", rc.load());
+  }
+  sync();
+  return 0;
+}
+
+ShmRing* ShmEngine::in_ring(int src) {
+  const size_t stride = ring_stride(ring_bytes_);
+  return reinterpret_cast<ShmRing*>(static_cast<char*>(maps_[rank]) + align16(sizeof(ShmHeader)) + stride * src);
+}
+ShmRing* ShmEngine::out_ring(int dst) {
+  const size_t stride = ring_stride(ring_bytes_);
+  return reinterpret_cast<ShmRing*>(static_cast<char*>(maps_[dst]) + align16(sizeof(ShmHeader)) + stride * rank);
+}
+
+int ShmEngine::tag_register(int tag, AmCallback cb) {
+  if (tag < 0 || tag >= TAG_MAX) return -1;
+  cbs_[tag] = std::move(cb);
+  return 0;
+}
+int ShmEngine::tag_unregister(int tag) {
+  if (tag < 0 || tag >= TAG_MAX) return -1;
+  cbs_[tag] = nullptr;
+  return 0;
+}
+
+bool ShmEngine::ring_write(ShmRing* r, const void* hdr, size_t hlen, const void* payload, size_t plen, int tag, int src) {
+  const uint64_t total = align16(sizeof(MsgHdr) + hlen + plen);
+  const uint64_t cap = r->cap;
+  if (total > cap / 2) fatal("active message of %zu bytes exceeds the ring limit", (size_t)total);
+  uint64_t head = r->head.load(std::memory_order_relaxed);
+  uint64_t tail = r->tail.load(std::memory_order_acquire);
+  uint64_t pos = head % cap;
+  uint64_t need = total + ((pos + total > cap) ? cap - pos : 0);
+  if (cap - (head - tail) < need) return false;
+  if (pos + total > cap) {
+    MsgHdr w{0, 0, 0, 0, 0};
+    std::memcpy(r->data + pos, &w, sizeof(w));
+    head += cap - pos;
+    pos = 0;
+  }
+  MsgHdr h{(uint32_t)total, (int16_t)tag, (int16_t)src, (uint32_t)(hlen + plen), 0xA11C0DE5u};
+  std::memcpy(r->data + pos, &h, sizeof(h));
+  if (hlen) std::memcpy(r->data + pos + sizeof(h), hdr, hlen);
+  if (plen) std::memcpy(r->data + pos + sizeof(h) + hlen, payload, plen);
+  r->head.store(head + total, std::memory_order_release);
+  return true;
+}
+
+int ShmEngine::send_am(int tag, int dst, const void* buf, size_t len) { return send_am2(tag, dst, buf, len, nullptr, 0); }
+
+int ShmEngine::send_am2(int tag, int dst, const void* hdr, size_t hlen, const void* payload, size_t plen) {
+  if (dst == rank) {
+    // loopback: deliver on the comm thread to keep callback context uniform
+    std::vector<char> m(hlen + plen);
+    if (hlen) std::memcpy(m.data(), hdr, hlen);
+    if (plen) std::memcpy(m.data() + hlen, payload, plen);
+    post([this, tag, m = std::move(m)] { if (cbs_[tag]) cbs_[tag](rank, tag, m.data(), m.size()); });
+    return 0;
+  }
+  Out& o = *out_[dst];
+  std::lock_guard<std::mutex> g(o.m);
+  if (o.backlog.empty() && ring_write(out_ring(dst), hdr, hlen, payload, plen, tag, rank)) return 0;
+  std::vector<char> m(sizeof(int) + hlen + plen);
+  std::memcpy(m.data(), &tag, sizeof(int));
+  if (hlen) std::memcpy(m.data() + sizeof(int), hdr, hlen);
+  if (plen) std::memcpy(m.data() + sizeof(int) + hlen, payload, plen);
+  o.backlog.push_back(std::move(m));
+  return 0;
+}
+
+void ShmEngine::post(std::function<void()> fn) {
+  {
+    std::lock_guard<std::mutex> g(post_m_);
+    posted_.push_back(std::move(fn));
+  }
+  posted_n_.fetch_add(1, std::memory_order_release);
+}
+
+int ShmEngine::progress() {
+  int n = 0;
+  if (posted_n_.load(std::memory_order_acquire) > 0) {
+    std::vector<std::function<void()>> fns;
+    {
+      std::lock_guard<std::mutex> g(post_m_);
+      fns.swap(posted_);
+      posted_n_.store(0);
+    }
+    for (auto& f : fns) { f(); ++n; }
+  }
+  // flush backlogs
+  for (int d = 0; d < size; ++d) {
+    if (d == rank) continue;
+    Out& o = *out_[d];
+    if (o.backlog.empty()) continue;
+    std::lock_guard<std::mutex> g(o.m);
+    while (!o.backlog.empty()) {
+      auto& m = o.backlog.front();
+      int tag;
+      std::memcpy(&tag, m.data(), sizeof(int));
+      if (!ring_write(out_ring(d), m.data() + sizeof(int), m.size() - sizeof(int), nullptr, 0, tag, rank)) break;
+      o.backlog.pop_front();
+      ++n;
+    }
+  }
+  // inbound rings
+  for (int s = 0; s < size; ++s) {
+    if (s == rank) continue;
+    ShmRing* r = in_ring(s);
+    for (int k = 0; k < 64; ++k) {
+      uint64_t tail = r->tail.load(std::memory_order_relaxed);
+      uint64_t head = r->head.load(std::memory_order_acquire);
+      if (tail == head) break;
+      uint64_t pos = tail % r->cap;
+      MsgHdr h;
+      std::memcpy(&h, r->data + pos, sizeof(h));
+      if (h.len == 0) {  // wrap
+        r->tail.store(tail + (r->cap - pos), std::memory_order_release);
+        continue;
+      }
+      if (h.magic != 0xA11C0DE5u) fatal("corrupted shm message from rank %d", s);
+      const char* payload = r->data + pos + sizeof(h);
+      if (h.tag >= 0 && h.tag < TAG_MAX && cbs_[h.tag]) cbs_[h.tag](h.src, h.tag, payload, h.plen);
+      else warning("dropping active message with unregistered tag %d from %d", h.tag, s);
+      r->tail.store(tail + h.len, std::memory_order_release);
+      ++n;
+    }
+  }
+  // RCCL transfers
+  if (rccl_ok_) {
+    for (int p = 0; p < size; ++p) {
+      for (auto* q : {&send_q_[p], &recv_q_[p]}) {
+        while (!q->empty()) {
+          hipError_t e = hipEventQuery(q->front().ev);
+          if (e == hipErrorNotReady) break;
+          if (e != hipSuccess) fatal("RCCL transfer failed: %s", hipGetErrorString(e));
+          Xfer x = std::move(q->front());
+          q->pop_front();
+          ev_pool_.push_back(x.ev);
+          x.done();
+          ++n;
+        }
+      }
+    }
+  }
+  return n;
+}
+
+void ShmEngine::thread_main() {
+  thread_id_ = std::this_thread::get_id();
+  if (gpu_ >= 0) (void)hipSetDevice(gpu_);
+  Backoff b;
+  while (!stop_.load(std::memory_order_relaxed)) {
+    if (progress()) b.reset();
+    else if (b.misses() < 4096) { PARSEC_CPU_RELAX(); b.idle(); }
+    else std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+  // drain what is left
+  for (int i = 0; i < 1000 && progress(); ++i) {}
+}
+
+void ShmEngine::start_thread() {
+  if (thread_.joinable()) return;
+  stop_.store(false);
+  thread_ = std::thread([this] { thread_main(); });
+}
+
+void ShmEngine::stop_thread() {
+  if (!thread_.joinable()) return;
+  stop_.store(true);
+  thread_.join();
+}
+
+int ShmEngine::sync() { (void)allreduce_max(0); return 0; }
+
+uint64_t ShmEngine::allreduce_max(uint64_t v) {
+  std::unique_lock<std::mutex> g(coll_m_);
+  uint64_t epoch = ++coll_epoch_;
+  if (rank == 0) {
+    coll_acc_ = std::max(coll_acc_, v);
+    if (++coll_arrived_ == size) {
+      CollMsg rel{COLL_RELEASE, {}, epoch, coll_acc_};
+      coll_arrived_ = 0;
+      coll_result_ = coll_acc_;
+      coll_acc_ = 0;
+      coll_done_epoch_ = epoch;
+      g.unlock();
+      for (int r = 1; r < size; ++r) send_am(TAG_BARRIER, r, &rel, sizeof(rel));
+      g.lock();
+    }
+  } else {
+    CollMsg m{COLL_ARRIVE, {}, epoch, v};
+    g.unlock();
+    send_am(TAG_BARRIER, 0, &m, sizeof(m));
+    g.lock();
+  }
+  coll_cv_.wait(g, [&] { return coll_done_epoch_ >= epoch; });
+  return coll_result_;
+}
+
+// ------------------------------------------------------------------ RCCL
+int ShmEngine::init_rccl() {
+  if (hipSetDevice(gpu_) != hipSuccess) return -1;
+  send_comm_.assign(size, nullptr);
+  recv_comm_.assign(size, nullptr);
+  send_stream_.assign(size, nullptr);
+  recv_stream_.assign(size, nullptr);
+  send_q_.resize(size);
+  recv_q_.resize(size);
+  static_assert(sizeof(ncclUniqueId) <= 128, "id size");
+  for (int d = 0; d < size; ++d) {
+    if (d == rank) continue;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return -2;
+    std::memcpy(me_->nccl_ids[d], &id, sizeof(id));
+  }
+  me_->ids_ready.store(1, std::memory_order_release);
+  for (int r = 0; r < size; ++r) {
+    if (r == rank) continue;
+    auto* h = static_cast<ShmHeader*>(maps_[r]);
+    uint64_t t0 = now_ns();
+    while (h->ids_ready.load(std::memory_order_acquire) == 0) {
+      if (now_ns() - t0 > 120ull * 1000000000ull) return -3;
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+  }
+  // Ordered init over directed pairs (s -> d) in a global order: deadlock free.
+  for (int s = 0; s < size; ++s)
+    for (int d = 0; d < size; ++d) {
+      if (s == d || (s != rank && d != rank)) continue;
+      ncclUniqueId id;
+      auto* h = static_cast<ShmHeader*>(maps_[s]);
+      std::memcpy(&id, h->nccl_ids[d], sizeof(id));
+      ncclComm_t c;
+      ncclResult_t rc = ncclCommInitRank(&c, 2, id, s == rank ? 0 : 1);
+      if (rc != ncclSuccess) { warning("ncclCommInitRank(%d->%d) failed: %s", s, d, ncclGetErrorString(rc)); return -4; }
+      hipStream_t st;
+      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return -5;
+      if (s == rank) { send_comm_[d] = c; send_stream_[d] = st; }
+      else { recv_comm_[s] = c; recv_stream_[s] = st; }
+    }
+  return 0;
+}
+
+int ShmEngine::rccl_send(int peer, const void* buf, size_t bytes, std::function<void()> done) {
+  hipEvent_t ev;
+  if (!ev_pool_.empty()) { ev = ev_pool_.back(); ev_pool_.pop_back(); }
+  else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1;
+  ncclResult_t rc = ncclSend(buf, bytes, ncclChar, 1, (ncclComm_t)send_comm_[peer], send_stream_[peer]);
+  if (rc != ncclSuccess) fatal("ncclSend to %d failed: %s", peer, ncclGetErrorString(rc));
+  (void)hipEventRecord(ev, send_stream_[peer]);
+  send_q_[peer].push_back(Xfer{ev, std::move(done)});
+  return 0;
+}
+
+int ShmEngine::rccl_recv(int peer, void* buf, size_t bytes, std::function<void()> done) {
+  hipEvent_t ev;
+  if (!ev_pool_.empty()) { ev = ev_pool_.back(); ev_pool_.pop_back(); }
+  else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1;
+  ncclResult_t rc = ncclRecv(buf, bytes, ncclChar, 0, (ncclComm_t)recv_comm_[peer], recv_stream_[peer]);
+  if (rc != ncclSuccess) fatal("ncclRecv from %d failed: %s", peer, ncclGetErrorString(rc));
+  (void)hipEventRecord(ev, recv_stream_[peer]);
+  recv_q_[peer].push_back(Xfer{ev, std::move(done)});
+  return 0;
+}
+
+}  // namespace parsec

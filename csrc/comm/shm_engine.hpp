@@ -1,0 +1,103 @@
+// Shared-memory active-message transport + RCCL data plane (one node, one
+// process per GPU). See comm.hpp for the design rationale.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <deque>
+#include <thread>
+
+#include "comm.hpp"
+
+namespace parsec {
+
+// Single-producer / single-consumer byte ring living in POSIX shared memory.
+struct ShmRing {
+  alignas(64) std::atomic<uint64_t> head;  // producer position (bytes, monotonic)
+  alignas(64) std::atomic<uint64_t> tail;  // consumer position
+  alignas(64) uint64_t cap;
+  char data[1];  // cap bytes follow
+};
+
+struct ShmHeader {
+  uint64_t magic;
+  std::atomic<uint32_t> ready;
+  int32_t rank, size;
+  uint64_t ring_bytes;
+  // RCCL unique ids for the directed pair (this rank -> d), written by this rank
+  char nccl_ids[64][128];
+  std::atomic<uint32_t> ids_ready;
+};
+
+class ShmEngine : public CommEngine {
+ public:
+  ShmEngine(int rank, int size, const std::string& job, int gpu_ordinal);
+  ~ShmEngine() override;
+  int init();
+  int tag_register(int tag, AmCallback cb) override;
+  int tag_unregister(int tag) override;
+  int send_am(int tag, int dst, const void* buf, size_t len) override;
+  int send_am2(int tag, int dst, const void* hdr, size_t hlen, const void* payload, size_t plen);
+  int progress() override;
+  int sync() override;
+  uint64_t allreduce_max(uint64_t v) override;
+  void post(std::function<void()> fn);  // run on the comm thread
+  bool on_comm_thread() const { return std::this_thread::get_id() == thread_id_; }
+  size_t max_fragment() const { return ring_bytes_ / 4; }
+  // RCCL data plane (comm thread only)
+  bool rccl_ok() const { return rccl_ok_; }
+  int rccl_send(int peer, const void* buf, size_t bytes, std::function<void()> done);
+  int rccl_recv(int peer, void* buf, size_t bytes, std::function<void()> done);
+  int gpu_ordinal() const { return gpu_; }
+  void start_thread();
+  void stop_thread();
+
+ private:
+  struct Pending {
+    std::vector<char> msg;
+  };
+  struct Out {
+    std::mutex m;
+    std::deque<std::vector<char>> backlog;
+  };
+  struct Xfer {
+    hipEvent_t ev;
+    std::function<void()> done;
+  };
+  bool ring_write(ShmRing* r, const void* hdr, size_t hlen, const void* payload, size_t plen, int tag, int src);
+  ShmRing* in_ring(int src);
+  ShmRing* out_ring(int dst);
+  void thread_main();
+  int init_rccl();
+  std::string job_;
+  int gpu_;
+  size_t ring_bytes_;
+  std::vector<void*> maps_;     // mapped segment per rank
+  std::vector<size_t> map_len_;
+  ShmHeader* me_ = nullptr;
+  std::vector<AmCallback> cbs_;
+  std::vector<std::unique_ptr<Out>> out_;
+  std::mutex post_m_;
+  std::vector<std::function<void()>> posted_;
+  std::atomic<int> posted_n_{0};
+  std::thread thread_;
+  std::thread::id thread_id_;
+  std::atomic<bool> stop_{false};
+  // barrier / allreduce state
+  std::mutex coll_m_;
+  std::condition_variable coll_cv_;
+  uint64_t coll_epoch_ = 0;
+  uint64_t coll_done_epoch_ = 0;
+  uint64_t coll_result_ = 0;
+  int coll_arrived_ = 0;
+  uint64_t coll_acc_ = 0;
+  // RCCL
+  bool rccl_ok_ = false;
+  std::vector<void*> send_comm_, recv_comm_;  // ncclComm_t per peer
+  std::vector<hipStream_t> send_stream_, recv_stream_;
+  std::vector<std::deque<Xfer>> send_q_, recv_q_;
+  std::vector<hipEvent_t> ev_pool_;
+};
+
+ShmEngine* shm_engine();
+
+}  // namespace parsec

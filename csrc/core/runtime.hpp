@@ -119,6 +119,7 @@ struct DataCopy : ListItem {  // ListItem: membership in a device LRU
   Datatype dtt;
   void* push_task = nullptr;       // GPU task currently staging this copy
   void* dev_state = nullptr;       // device module private (events, LRU owner)
+  void (*release_fn)(DataCopy*) = nullptr;  // custom destruction (e.g. comm receive buffers)
   void* ptr() const { return device_private; }
 };
 

@@ -311,7 +311,6 @@ int context_add_taskpool(Context* ctx, Taskpool* tp) {
   tp->completed.store(false);
   taskpool_register(tp);
   std::string td = tp->termdet_name.empty() ? ctx->default_termdet : tp->termdet_name;
-  if (ctx->nb_nodes > 1 && td == "local") td = "fourcounter";
   tp->tdm = termdet_open_module(td);
   if (!tp->tdm) fatal("termination detection module '%s' not available", td.c_str());
   tp->tdm->monitor_taskpool(tp, [](Taskpool* p) { taskpool_termination_detected(p); });

@@ -185,6 +185,7 @@ void data_copy_retain(DataCopy* c) { c->refcount.fetch_add(1, std::memory_order_
 void data_copy_release(DataCopy* c) {
   if (!c) return;
   if (c->refcount.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
+  if (c->release_fn) { c->release_fn(c); return; }
   Data* d = c->original;
   if (c->flags & DATA_FLAG_ARENA) {
     if (d) {

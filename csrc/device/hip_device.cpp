@@ -377,9 +377,9 @@ int HipDevice::stage_in(GpuTask* g) {
       if (local != nc) { zone->free(p); delete static_cast<DevCopyState*>(nc->dev_state); delete nc; }
     }
     if (!local->dev_state) {
-      auto* st = new DevCopyState();
-      st->cache_managed = false;  // collection storage in HBM: never evicted
-      local->dev_state = st;
+      // collection storage in HBM / comm receive buffers: never evicted
+      static DevCopyState unmanaged{false, false, false};
+      local->dev_state = &unmanaged;
     }
     lru_remove(local);
     local->readers.fetch_add(1);

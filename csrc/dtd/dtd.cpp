@@ -64,7 +64,6 @@ void DtdTaskpool::release_hold() {
 void DtdTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
   (void)ctx; (void)ready;
   hold.store(false);
-  tdm->taskpool_set_nb_tasks(this, 0);
   arm_hold();
 }
 

@@ -447,7 +447,8 @@ void PtgTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
       ready.push_back(t);
     });
   }
-  tdm->taskpool_set_nb_tasks(this, nb_local);
+  // additive: remote activations may already have run (and completed) tasks
+  tdm->taskpool_addto_nb_tasks(this, nb_local);
 }
 
 void PtgTaskpool::activate(ExecutionStream* es, PtgTaskClass* tc, const int32_t* L, int flow, DataCopy* data, std::vector<Task*>& ready) {

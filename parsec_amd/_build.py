@@ -31,6 +31,8 @@ CORE_SOURCES = [
     "csrc/device/hip_device.cpp",
     "csrc/prof/profiling.cpp",
     "csrc/comm/remote_dep.cpp",
+    "csrc/comm/shm_engine.cpp",
+    "csrc/comm/fourcounter.cpp",
     "csrc/ptg/ptg.cpp",
     "csrc/dtd/dtd.cpp",
     "csrc/algos/dpotrf.cpp",

@@ -1,0 +1,49 @@
+"""Multi-process (one process per rank) runs of the distributed engine on CPU:
+shared-memory active messages, host-data fragments, broadcast trees,
+local / four-counter termination (reference tests: collections/*:mp, dsl/ptg :mp)."""
+import os
+import subprocess
+import sys
+import uuid
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+WORKER = os.path.join(HERE, "mp", "dist_dpotrf.py")
+
+
+def run_ranks(nranks, *args, timeout=120):
+    job = "pt" + uuid.uuid4().hex[:10]
+    env = dict(os.environ, PARSEC_MCA_device_hip_enabled="0")
+    procs = [subprocess.Popen([sys.executable, WORKER, str(r), str(nranks), job, *map(str, args)],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+             for r in range(nranks)]
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=timeout)
+            outs.append((p.returncode, out))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return outs
+
+
+@pytest.mark.parametrize("nranks,P,Q,topo,termdet", [
+    (2, 2, 1, "star", "local"),
+    (2, 1, 2, "star", "fourcounter"),
+    (4, 2, 2, "chain", "local"),
+    (4, 2, 2, "binomial", "fourcounter"),
+])
+def test_distributed_dpotrf(pa, nranks, P, Q, topo, termdet):
+    outs = run_ranks(nranks, 512, 64, P, Q, "lfq", topo, termdet)
+    for rc, out in outs:
+        assert rc == 0, out
+
+
+@pytest.mark.parametrize("sched", ["gd", "ll", "ap"])
+def test_distributed_other_schedulers(pa, sched):
+    outs = run_ranks(2, 384, 64, 2, 1, sched, "star", "local")
+    for rc, out in outs:
+        assert rc == 0, out
