@@ -163,7 +163,7 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
     d.params = {"m", "k"};
     d.affinity_dc = [A](const Taskpool*) { return (DataCollection*)A; };
     d.affinity_args = {loc(1), loc(0)};
-    d.priority = [prio, NT](const Taskpool*, const int32_t* L) { int64_t k = L[0], m = L[1]; return prio(m) + 3 * ((2 * NT) - k - m - 1) * (m - k) + (m == k + 1 ? (int64_t)1 << 28 : 0); };
+    d.priority = [prio, NT](const Taskpool*, const int32_t* L) { int64_t k = L[0], m = L[1]; return prio(m) + 3 * ((2 * NT) - k - m - 1) * (m - k) + (m == k + 1 ? (int64_t)1 << 29 : 0); };
     d.flags = TC_HIGH_PRIORITY;
     FlowDef T;
     T.name = "T"; T.access = FLOW_READ;
@@ -206,7 +206,7 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
     d.params = {"k", "m"};
     d.affinity_dc = [A](const Taskpool*) { return (DataCollection*)A; };
     d.affinity_args = {loc(1), loc(1)};
-    d.priority = [prio](const Taskpool*, const int32_t* L) { int64_t k = L[0], m = L[1]; return prio(m) + 3 * (m - k) + (m == k + 1 ? (int64_t)1 << 28 : 0); };
+    d.priority = [prio](const Taskpool*, const int32_t* L) { int64_t k = L[0], m = L[1]; return prio(m) + 3 * (m - k) + (m == k + 1 ? (int64_t)1 << 29 : 0); };
     FlowDef Af;
     Af.name = "A"; Af.access = FLOW_READ;
     Af.in = {always(task("TRSM", "C", {val(loc(1)), val(loc(0))}))};

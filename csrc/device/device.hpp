@@ -99,6 +99,7 @@ struct GpuExecContext {
 using GpuHook = std::function<int(GpuExecContext*, Task*)>;
 
 // Flush a batch on a stream (implemented next to the kernels).
-void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal);
+void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal, void* workspace);
+size_t kernel_batch_workspace_bytes(const KernelBatch& b);
 
 }  // namespace parsec

@@ -130,8 +130,26 @@ void HipDevice::start(Context* c) {
   PARSEC_HIP_CHECK(hipStreamCreateWithFlags(&s_h2d, hipStreamNonBlocking));
   PARSEC_HIP_CHECK(hipStreamCreateWithFlags(&s_d2h, hipStreamNonBlocking));
   s_exec.resize(nb_exec_streams);
-  for (int i = 0; i < nb_exec_streams; ++i)
-    PARSEC_HIP_CHECK(hipStreamCreateWithPriority(&s_exec[i], hipStreamNonBlocking, i == 0 ? hi : lo));
+  // Stream 0 carries the critical path (POTRF / next panel). With >= 3 streams it
+  // gets a few CUs of its own so its small latency-bound kernels never queue behind
+  // (or share CUs with) the bulk GEMM batches, which run on the remaining CUs.
+  const int ncu = props.multiProcessorCount > 0 ? props.multiProcessorCount : 256;
+  int reserve = nb_exec_streams >= 3 ? reserved_cus : 0;
+  if (reserve >= ncu) reserve = 0;
+  bool masked = false;
+  if (reserve > 0) {
+    std::vector<uint32_t> crit((ncu + 31) / 32, 0u), bulk((ncu + 31) / 32, 0u);
+    // spread the reserved CUs over the XCDs (CU ids are dealt round-robin to them)
+    for (int cu = 0; cu < ncu; ++cu) (cu < reserve ? crit : bulk)[cu / 32] |= 1u << (cu % 32);
+    masked = hipExtStreamCreateWithCUMask(&s_exec[0], (uint32_t)crit.size(), crit.data()) == hipSuccess;
+    for (int i = 1; masked && i < nb_exec_streams; ++i)
+      masked = hipExtStreamCreateWithCUMask(&s_exec[i], (uint32_t)bulk.size(), bulk.data()) == hipSuccess;
+    if (!masked) (void)hipGetLastError();
+  }
+  if (!masked)
+    for (int i = 0; i < nb_exec_streams; ++i)
+      PARSEC_HIP_CHECK(hipStreamCreateWithPriority(&s_exec[i], hipStreamNonBlocking, i <= 1 ? hi : lo));
+  cu_masked = masked;
   executing.assign(nb_exec_streams, {});
   batches.assign(nb_exec_streams, {});
   round_tasks.assign(nb_exec_streams, {});
@@ -427,9 +445,12 @@ void HipDevice::execute_ready() {
     Task* t = g->task;
     const Chore& ch = t->task_class->chores[g->chore];
     int s;
+    const bool hp = t->priority >= high_prio_threshold || (t->task_class->flags & TC_HIGH_PRIORITY);
     if (nb_exec_streams == 1) s = 0;
-    else if (t->priority >= high_prio_threshold || (t->task_class->flags & TC_HIGH_PRIORITY)) s = 0;
-    else s = 1 + (int)(rr_stream++ % (uint32_t)(nb_exec_streams - 1));
+    else if (nb_exec_streams == 2) s = hp ? 0 : 1;
+    else if (t->priority >= critical_threshold) s = 0;
+    else if (hp) s = 1;
+    else s = 2 + (int)(rr_stream++ % (uint32_t)(nb_exec_streams - 2));
     GpuExecContext ctxg;
     ctxg.dev = this;
     ctxg.device = this;
@@ -444,7 +465,7 @@ void HipDevice::execute_ready() {
     int rc = ch.gpu_hook ? ch.gpu_hook(&ctxg, t) : HOOK_NEXT;
     PARSEC_PINS(es, PINS_EXEC_END, t);
     if (!batching && !local_batch.empty()) {
-      launch_kernel_batch(local_batch, s_exec[s], ordinal);
+      launch_kernel_batch(local_batch, s_exec[s], ordinal, workspace(s, kernel_batch_workspace_bytes(local_batch) + 64));
       stats.kernel_launches.fetch_add(1, std::memory_order_relaxed);
     }
     if (rc == HOOK_DONE) {
@@ -469,7 +490,7 @@ void HipDevice::execute_ready() {
   for (int s = 0; s < nb_exec_streams; ++s) {
     if (round_tasks[s].empty()) continue;
     if (!batches[s].empty()) {
-      launch_kernel_batch(batches[s], s_exec[s], ordinal);
+      launch_kernel_batch(batches[s], s_exec[s], ordinal, workspace(s, kernel_batch_workspace_bytes(batches[s]) + 64));
       stats.kernel_launches.fetch_add(1, std::memory_order_relaxed);
       batches[s].clear();
     }
@@ -640,6 +661,8 @@ void hip_devices_init(Context* ctx) {
   int batching = (int)params.reg_int("device", "hip", "batching", "Group ready tile kernels of one kind into one launch", 1);
   int hp = (int)params.reg_int("device", "hip", "high_priority_threshold", "Task priority at or above which the high-priority stream is used", 1 << 27);
   int sortp = (int)params.reg_int("device", "hip", "sort_pending_tasks", "Sort pending GPU tasks by priority", 1);
+  int crit = (int)params.reg_int("device", "hip", "critical_threshold", "Task priority at or above which the CU-reserved critical stream is used", 1 << 29);
+  int rcus = (int)params.reg_int("device", "hip", "reserved_cus", "CUs reserved for the critical-path stream (0 = no CU masking; measured slower on MI355X)", 0);
   if (enabled == 0) return;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) { (void)hipGetLastError(); return; }
@@ -659,6 +682,8 @@ void hip_devices_init(Context* ctx) {
     d->nb_exec_streams = std::max(1, g_nb_exec_streams);
     d->batching = batching != 0;
     d->high_prio_threshold = hp;
+    d->critical_threshold = crit;
+    d->reserved_cus = rcus;
     d->sort_pending = sortp != 0;
     reg.add(d);
     g_hip_devices.push_back(d);

@@ -103,7 +103,10 @@ struct HipDevice : Device {
   std::atomic<int64_t> inflight{0};
   ExecutionStream* es = nullptr;
   Context* ctx = nullptr;
-  int high_prio_threshold = 1 << 30;
+  int high_prio_threshold = 1 << 27;
+  int critical_threshold = 1 << 29;
+  int reserved_cus = 0;
+  bool cu_masked = false;
   bool batching = true;
   bool sort_pending = true;
   int max_inflight_groups = 64;

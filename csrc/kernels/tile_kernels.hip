@@ -1,23 +1,28 @@
 // CDNA4 (gfx950) fp64 tile kernels for the dense linear-algebra taskpools.
 //
 //  * Grouped DGEMM / DSYRK (lower) on v_mfma_f64_16x16x4f64: ONE launch runs every
-//    ready GEMM-shaped tile task of a scheduling round, so 512^2 tiles (64 WG tiles
-//    each) still fill the 256 CUs. Workgroups are remapped so a task's tiles stay on
-//    one XCD (its operands stay in that XCD's 4 MiB L2).
-//  * The MFMA operand roles are swapped (A-operand <- B tile, B-operand <- A tile) so
-//    that the f64 accumulator layout (col = lane&15, row = (lane>>4)+4*r, measured on
-//    MI355X, profiles/probe_mfma_f64_and_vendor_baselines.log) maps lanes to
+//    ready GEMM-shaped tile task of a scheduling round, so 512^2 tiles still fill
+//    the 256 CUs. Two tilings: 128x128 (4 waves x 64x64, 16 accumulators per wave)
+//    for big batches and 64x64 for small ones. Workgroups are remapped so a task's
+//    tiles stay on one XCD (its operands stay in that XCD's 4 MiB L2).
+//  * MFMA operand roles are swapped (A-operand <- B tile, B-operand <- A tile) so
+//    the f64 accumulator layout (col = lane&15, row = (lane>>4)+4*r, measured on
+//    MI355X: profiles/probe_mfma_f64_and_vendor_baselines.log) maps lanes to
 //    consecutive ROWS of the column-major C tile: 128-byte coalesced epilogues.
-//  * TRSM (right, lower, trans: B := B L^-T) with the workgroup's row panel resident
-//    in LDS, 8-column blocks: triangular solve per row + rank-8 update.
-//  * POTRF of a tile: blocked (64) driver = diag-block factorization in LDS + TRSM of
-//    the panel + lower-only grouped GEMM update, all stream-ordered.
-// Reference behaviour these replace: cuBLAS/CBLAS calls in the reference DTD/PTG
-// tests (tests/dsl/dtd/dtd_test_simple_gemm.c:165-250) and DPLASMA's dpotrf tiles.
+//  * TRSM (B := B L^-T, right/lower/trans) = blocked MFMA solve with precomputed
+//    inverses of the 64x64 diagonal blocks: R_j = B_j - X_<j L_j,<j^T ; X_j = R_j invD_j^T.
+//    Each workgroup owns 16 rows and keeps its row panel in LDS with a stride of 16
+//    doubles, which makes every MFMA operand read bank-conflict free.
+//  * POTRF of a tile: per 64-column block, ONE wave factors the diagonal block
+//    (row per lane in registers, column broadcast through LDS, no block barriers)
+//    and inverts it, then the panel TRSM and the lower-only GEMM update run
+//    stream-ordered.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
+#include <mutex>
+#include <vector>
 
 #include "../device/device.hpp"
 
@@ -25,6 +30,7 @@ namespace parsec {
 namespace kern {
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
+typedef double double2_t __attribute__((ext_vector_type(2)));
 
 constexpr int kMaxGemmBatch = 40;
 
@@ -35,11 +41,12 @@ struct GemmBatchArgs {
   GemmDesc d[kMaxGemmBatch];
 };
 
-__device__ __forceinline__ int find_desc(const GemmBatchArgs& a, int t) {
+template <class Args>
+__device__ __forceinline__ int find_desc(const Args& a, const int* starts, int t) {
   int lo = 0, hi = a.count - 1;
   while (lo < hi) {
     int mid = (lo + hi + 1) >> 1;
-    if (a.tile_start[mid] <= t) lo = mid;
+    if (starts[mid] <= t) lo = mid;
     else hi = mid - 1;
   }
   return lo;
@@ -55,11 +62,11 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return base + i;
 }
 
-// BM x BN tile, BK deep, 256 threads = 4 waves as WM x WN.
+// ==================================================================== GEMM
 template <int BM, int BN, int BK, int WM, int WN, bool TRANSB>
-__global__ __launch_bounds__(256) void dgemm_batch_kernel(const GemmBatchArgs args) {
-  constexpr int WTM = BM / WM;  // rows per wave
-  constexpr int WTN = BN / WN;  // cols per wave
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void dgemm_batch_kernel(const GemmBatchArgs args) {
+  constexpr int WTM = BM / WM;
+  constexpr int WTN = BN / WN;
   constexpr int FM = WTM / 16;
   constexpr int FN = WTN / 16;
   constexpr int PADM = ((BM % 32) == 16) ? 0 : 16;
@@ -71,7 +78,7 @@ __global__ __launch_bounds__(256) void dgemm_batch_kernel(const GemmBatchArgs ar
 
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   if (tile >= args.total_tiles) return;
-  const int di = find_desc(args, tile);
+  const int di = find_desc(args, args.tile_start, tile);
   const GemmDesc& d = args.d[di];
   const int local = tile - args.tile_start[di];
   const int mt = (d.m + BM - 1) / BM;
@@ -87,6 +94,8 @@ __global__ __launch_bounds__(256) void dgemm_batch_kernel(const GemmBatchArgs ar
   const double* __restrict__ B = d.B;
   const int M = d.m, N = d.n, K = d.k;
   const int lda = d.lda, ldb = d.ldb;
+  // 16-byte loads when every row pair is aligned and fully inside the tile
+  const bool vec = ((lda | ldb) % 2 == 0) && ((((uintptr_t)A) | ((uintptr_t)B)) % 16 == 0) && (M % 2 == 0) && (TRANSB ? (N % 2 == 0) : (K % 2 == 0));
 
   double4_t acc[FN][FM];
 #pragma unroll
@@ -94,44 +103,66 @@ __global__ __launch_bounds__(256) void dgemm_batch_kernel(const GemmBatchArgs ar
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = (double4_t){0.0, 0.0, 0.0, 0.0};
 
-  // global -> register staging: A tile BM x BK (m contiguous), B tile (NT: n contiguous; NN: k contiguous)
-  constexpr int A_ELEMS = BM * BK;
-  constexpr int B_ELEMS = BN * BK;
-  constexpr int A_PER_T = A_ELEMS / 256;
-  constexpr int B_PER_T = B_ELEMS / 256;
-  double ra[A_PER_T], rb[B_PER_T];
+  constexpr int A_PAIRS = BM * BK / 2 / 256;  // double2 per thread
+  constexpr int B_PAIRS = BN * BK / 2 / 256;
+  static_assert(A_PAIRS >= 1 && B_PAIRS >= 1, "tile too small");
+  double2_t ra[A_PAIRS], rb[B_PAIRS];
 
   auto load_tile = [&](int k0) {
 #pragma unroll
-    for (int e = 0; e < A_PER_T; ++e) {
+    for (int e = 0; e < A_PAIRS; ++e) {
       int idx = tid + 256 * e;
-      int mm = idx % BM, kk = idx / BM;
+      int mm = (idx % (BM / 2)) * 2, kk = idx / (BM / 2);
       int gm = m0 + mm, gk = k0 + kk;
-      ra[e] = (gm < M && gk < K) ? A[(size_t)gk * lda + gm] : 0.0;
+      const double* p = A + (size_t)gk * lda + gm;
+      if (vec && gk < K && gm + 1 < M) ra[e] = *reinterpret_cast<const double2_t*>(p);
+      else {
+        ra[e].x = (gm < M && gk < K) ? p[0] : 0.0;
+        ra[e].y = (gm + 1 < M && gk < K) ? p[1] : 0.0;
+      }
     }
 #pragma unroll
-    for (int e = 0; e < B_PER_T; ++e) {
+    for (int e = 0; e < B_PAIRS; ++e) {
       int idx = tid + 256 * e;
-      int nn, kk;
-      if (TRANSB) { nn = idx % BN; kk = idx / BN; }
-      else { kk = idx % BK; nn = idx / BK; }
-      int gn = n0 + nn, gk = k0 + kk;
-      double v = 0.0;
-      if (gn < N && gk < K) v = TRANSB ? B[(size_t)gk * ldb + gn] : B[(size_t)gn * ldb + gk];
-      rb[e] = v;
+      if (TRANSB) {  // B is N x K (n contiguous)
+        int nn = (idx % (BN / 2)) * 2, kk = idx / (BN / 2);
+        int gn = n0 + nn, gk = k0 + kk;
+        const double* p = B + (size_t)gk * ldb + gn;
+        if (vec && gk < K && gn + 1 < N) rb[e] = *reinterpret_cast<const double2_t*>(p);
+        else {
+          rb[e].x = (gn < N && gk < K) ? p[0] : 0.0;
+          rb[e].y = (gn + 1 < N && gk < K) ? p[1] : 0.0;
+        }
+      } else {  // B is K x N (k contiguous)
+        int kk = (idx % (BK / 2)) * 2, nn = idx / (BK / 2);
+        int gn = n0 + nn, gk = k0 + kk;
+        const double* p = B + (size_t)gn * ldb + gk;
+        if (vec && gn < N && gk + 1 < K) rb[e] = *reinterpret_cast<const double2_t*>(p);
+        else {
+          rb[e].x = (gn < N && gk < K) ? p[0] : 0.0;
+          rb[e].y = (gn < N && gk + 1 < K) ? p[1] : 0.0;
+        }
+      }
     }
   };
   auto store_tile = [&](int buf) {
 #pragma unroll
-    for (int e = 0; e < A_PER_T; ++e) {
+    for (int e = 0; e < A_PAIRS; ++e) {
       int idx = tid + 256 * e;
-      As[buf][idx / BM][idx % BM] = ra[e];
+      int mm = (idx % (BM / 2)) * 2, kk = idx / (BM / 2);
+      *reinterpret_cast<double2_t*>(&As[buf][kk][mm]) = ra[e];
     }
 #pragma unroll
-    for (int e = 0; e < B_PER_T; ++e) {
+    for (int e = 0; e < B_PAIRS; ++e) {
       int idx = tid + 256 * e;
-      if (TRANSB) Bs[buf][idx / BN][idx % BN] = rb[e];
-      else Bs[buf][idx % BK][idx / BK] = rb[e];
+      if (TRANSB) {
+        int nn = (idx % (BN / 2)) * 2, kk = idx / (BN / 2);
+        *reinterpret_cast<double2_t*>(&Bs[buf][kk][nn]) = rb[e];
+      } else {
+        int kk = (idx % (BK / 2)) * 2, nn = idx / (BK / 2);
+        Bs[buf][kk][nn] = rb[e].x;
+        Bs[buf][kk + 1][nn] = rb[e].y;
+      }
     }
   };
 
@@ -155,13 +186,10 @@ __global__ __launch_bounds__(256) void dgemm_batch_kernel(const GemmBatchArgs ar
 #pragma unroll
         for (int j = 0; j < FM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(afr[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nkt) {
-      store_tile(cur ^ 1);
-    }
+    if (kt + 1 < nkt) store_tile(cur ^ 1);
     __syncthreads();
   }
 
-  // epilogue: lane holds C[m = base_m + fr][n = base_n + fk + 4r]
   double* __restrict__ C = d.C;
   const int ldc = d.ldc;
   const double alpha = d.alpha, beta = d.beta;
@@ -183,139 +211,181 @@ __global__ __launch_bounds__(256) void dgemm_batch_kernel(const GemmBatchArgs ar
     }
 }
 
-// ------------------------------------------------------------------- TRSM
-// B (m x n, ldb) := B * L^-T, L lower n x n (ldl). One workgroup owns TR rows and
-// keeps its row panel in LDS (row-major, stride n+1).
-constexpr int kMaxTrsmBatch = 64;
-struct TrsmBatchArgs {
+// ========================================================= diag blocks (1 wave)
+// Factor the w x w (w <= 64) lower block at T (ldt) in place and/or write its
+// inverse (64 x 64 col-major, identity padded) to invD. One wave, no block
+// barriers. Right-looking with a ROTATING register window: lane r owns row r; at
+// step j its a[0] is column j and a[1..] the trailing columns, so after the
+// update every slot shifts down by one. The outer loop is a real loop and every
+// register index is static (no scratch); each step is 63 independent FMAs fed by
+// broadcast LDS reads of the just-finished column. The inverse (lane c owns
+// column c of L^-1, forward substitution) uses the same window.
+constexpr int kDiagLd = 128;  // Ls column stride: reads of Ls[j][j+k] stay in bounds
+__device__ __forceinline__ void wave_potrf64(double* T, int ldt, int w, double* invD, int* info, int info_base, bool factor) {
+  __shared__ double Ls[64 * kDiagLd];  // Ls[c*kDiagLd + r] = L(r, c), zero above the diagonal / beyond 63
+  __shared__ double Xs[64][65];        // inverse staging: Xs[c][r] = inv(r, c)
+  const int r = threadIdx.x;
+  double a[64];
+#pragma unroll
+  for (int c = 0; c < 64; ++c) a[c] = (r < w && c < w) ? T[(size_t)c * ldt + r] : (r == c ? 1.0 : 0.0);
+#pragma unroll
+  for (int c = 0; c < 64; ++c) Ls[c * kDiagLd + 64 + r] = 0.0;
+  if (factor) {
+    int bad = 0;
+#pragma unroll 1
+    for (int j = 0; j < 64; ++j) {
+      double dj = __shfl(a[0], j, 64);
+      bad = (dj <= 0.0 && !bad && j < w) ? j + 1 : bad;
+      dj = dj <= 0.0 ? 1.0 : dj;
+      const double s = __builtin_sqrt(dj);
+      const double v = (r == j) ? s : (r > j ? a[0] / s : 0.0);
+      Ls[j * kDiagLd + r] = v;
+      if (r < w && j < w && r >= j) T[(size_t)j * ldt + r] = v;
+      __builtin_amdgcn_wave_barrier();
+      const double* colj = &Ls[j * kDiagLd + j];
+#pragma unroll
+      for (int k = 1; k < 64; ++k) a[k - 1] = a[k] - v * colj[k];
+      a[63] = 0.0;
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (bad && r == 0 && info) atomicCAS(info, 0, info_base + bad);
+  } else {
+#pragma unroll
+    for (int c = 0; c < 64; ++c) Ls[c * kDiagLd + r] = (r >= c) ? a[c] : 0.0;
+  }
+  if (!invD) return;
+  __builtin_amdgcn_wave_barrier();
+  // forward substitution L X = I, lane r owns column r of X (x[0] = current row)
+#pragma unroll
+  for (int i = 0; i < 64; ++i) a[i] = (i == r) ? 1.0 : 0.0;
+#pragma unroll 1
+  for (int i = 0; i < 64; ++i) {
+    const double* coli = &Ls[i * kDiagLd + i];
+    const double xi = a[0] / coli[0];
+    Xs[r][i] = xi;
+#pragma unroll
+    for (int k = 1; k < 64; ++k) a[k - 1] = a[k] - coli[k] * xi;
+    a[63] = 0.0;
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int c = 0; c < 64; ++c) invD[(size_t)c * 64 + r] = Xs[c][r];
+}
+
+__global__ __launch_bounds__(64) void dpotrf_diag_inv_kernel(double* A, int lda, int j, int jb, double* invD, int* info) {
+  wave_potrf64(A + (size_t)j * lda + j, lda, jb, invD, info, j, true);
+}
+
+// Inverses of the 64x64 diagonal blocks of L (n x n): block b -> invD + b*4096.
+__global__ __launch_bounds__(64) void dtrtri_diag_kernel(const double* L, int ldl, int n, double* invD) {
+  const int b = blockIdx.x;
+  const int c0 = b * 64;
+  wave_potrf64(const_cast<double*>(L) + (size_t)c0 * ldl + c0, ldl, min(64, n - c0), invD + (size_t)b * 4096, nullptr, 0, false);
+}
+
+// ==================================================================== TRSM
+constexpr int kMaxTrsmBatch = 48;
+struct TrsmInvArgs {
   int count;
   int block_start[kMaxTrsmBatch + 1];
   TrsmDesc d[kMaxTrsmBatch];
+  const double* invD[kMaxTrsmBatch];
 };
 
-template <int TR>
-__global__ __launch_bounds__(256) void dtrsm_rltn_kernel(const TrsmBatchArgs args) {
-  extern __shared__ double smem[];
+template <int BR>
+__global__ __launch_bounds__(256) void dtrsm_inv_kernel(const TrsmInvArgs args) {
+  extern __shared__ double P[];  // [ncols_padded][BR]
   const int b = blockIdx.x;
-  int lo = 0, hi = args.count - 1;
-  while (lo < hi) {
-    int mid = (lo + hi + 1) >> 1;
-    if (args.block_start[mid] <= b) lo = mid;
-    else hi = mid - 1;
-  }
-  const TrsmDesc& d = args.d[lo];
-  const int r0 = (b - args.block_start[lo]) * TR;
-  const int n = d.n;
-  const int ldp = n + 1;
-  double* P = smem;  // TR x ldp
-  const int tid = threadIdx.x;
-  const int rows = min(TR, d.m - r0);
-  // load panel (coalesced along rows for each column)
-  for (int idx = tid; idx < TR * n; idx += 256) {
-    int r = idx % TR, c = idx / TR;
-    P[r * ldp + c] = r < rows ? d.B[(size_t)c * d.ldb + r0 + r] : 0.0;
-  }
-  __syncthreads();
-  const double* L = d.L;
+  const int di = find_desc(args, args.block_start, b);
+  const TrsmDesc& d = args.d[di];
+  const double* __restrict__ invD = args.invD[di];
+  const int r0 = (b - args.block_start[di]) * BR;
+  const int n = d.n, m = d.m;
+  const int nblk = (n + 63) / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const double* __restrict__ L = d.L;
   const int ldl = d.ldl;
-  for (int cb = 0; cb < n; cb += 8) {
-    const int w = min(8, n - cb);
-    // 1) per-row triangular solve on the 8-column block
-    if (tid < TR) {
-      double x[8];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) x[c] = c < w ? P[tid * ldp + cb + c] : 0.0;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        if (c < w) {
-          x[c] /= L[(size_t)(cb + c) * ldl + cb + c];
-#pragma unroll
-          for (int c2 = c + 1; c2 < 8; ++c2)
-            if (c2 < w) x[c2] -= x[c] * L[(size_t)(cb + c) * ldl + cb + c2];
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 8; ++c) if (c < w) P[tid * ldp + cb + c] = x[c];
-    }
-    __syncthreads();
-    // 2) rank-w update of the remaining columns
-    for (int j = cb + w + tid; j < n; j += 256) {
-      double l[8];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) l[c] = c < w ? L[(size_t)(cb + c) * ldl + j] : 0.0;
-      for (int r = 0; r < TR; ++r) {
-        double acc = P[r * ldp + j];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) acc -= P[r * ldp + cb + c] * l[c];
-        P[r * ldp + j] = acc;
-      }
-    }
-    __syncthreads();
-  }
-  for (int idx = tid; idx < TR * n; idx += 256) {
-    int r = idx % TR, c = idx / TR;
-    if (r < rows) d.B[(size_t)c * d.ldb + r0 + r] = P[r * ldp + c];
-  }
-}
-
-// ------------------------------------------------------------------ POTRF
-// Factor the jb x jb diagonal block at A[j, j] in LDS (right-looking).
-__global__ __launch_bounds__(256) void dpotrf_diag_kernel(double* A, int lda, int j, int jb, int* info) {
-  __shared__ double T[64][65];
-  const int tid = threadIdx.x;
-  for (int idx = tid; idx < jb * jb; idx += 256) {
-    int r = idx % jb, c = idx / jb;
-    T[r][c] = (r >= c) ? A[(size_t)(j + c) * lda + j + r] : 0.0;
+  // load the row panel, column-major in LDS with stride BR
+  for (int idx = tid; idx < nblk * 64 * BR; idx += 256) {
+    int c = idx / BR, rr = idx % BR;
+    P[idx] = (c < n && r0 + rr < m) ? d.B[(size_t)c * d.ldb + r0 + rr] : 0.0;
   }
   __syncthreads();
-  for (int c = 0; c < jb; ++c) {
-    double dg = T[c][c];
-    if (dg <= 0.0) {
-      if (tid == 0 && info && *info == 0) *info = j + c + 1;
-      dg = 1.0;  // keep going to avoid NaN storms
+  for (int jb = 0; jb < nblk; ++jb) {
+    const int c0 = jb * 64;
+    const int cw = c0 + 16 * w + fr;  // L row this lane feeds as MFMA A-operand
+    double4_t acc = (double4_t){0.0, 0.0, 0.0, 0.0};
+    for (int k = 0; k < c0; k += 4) {
+      double a = (cw < n) ? L[(size_t)(k + fk) * ldl + cw] : 0.0;
+      double bb = P[(k + fk) * BR + fr];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
     }
-    double s = sqrt(dg);
+    // R[c][r] = B[r][c] - acc ; lane holds c = c0 + 16w + fk + 4i, r = fr
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int c = c0 + 16 * w + fk + 4 * i;
+      P[c * BR + fr] -= acc[i];
+    }
     __syncthreads();
-    if (tid == 0) T[c][c] = s;
-    for (int r = c + 1 + tid; r < jb; r += 256) T[r][c] /= s;
+    double4_t acc2 = (double4_t){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < 64; kk += 4) {
+      double a = invD[(size_t)jb * 4096 + (size_t)(kk + fk) * 64 + 16 * w + fr];
+      double bb = P[(c0 + kk + fk) * BR + fr];
+      acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc2, 0, 0, 0);
+    }
     __syncthreads();
-    // trailing update of the lower part
-    int rem = jb - c - 1;
-    for (int idx = tid; idx < rem * rem; idx += 256) {
-      int r = c + 1 + idx % rem, cc = c + 1 + idx / rem;
-      if (r >= cc) T[r][cc] -= T[r][c] * T[cc][c];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int c = c0 + 16 * w + fk + 4 * i;
+      P[c * BR + fr] = acc2[i];
     }
     __syncthreads();
   }
-  for (int idx = tid; idx < jb * jb; idx += 256) {
-    int r = idx % jb, c = idx / jb;
-    if (r >= c) A[(size_t)(j + c) * lda + j + r] = T[r][c];
+  for (int idx = tid; idx < n * BR; idx += 256) {
+    int c = idx / BR, rr = idx % BR;
+    if (r0 + rr < m) d.B[(size_t)c * d.ldb + r0 + rr] = P[idx];
   }
 }
 
 // ================================================================ launchers
+static int g_gemm_tile_policy = -1;  // -1 auto, 64, 128
+
 static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) {
-  // choose the transB variant per chunk (descriptors are grouped by it by the caller)
+  if (g_gemm_tile_policy < 0) {
+    const char* e = getenv("PARSEC_GEMM_TILE");
+    g_gemm_tile_policy = e ? atoi(e) : 0;
+  }
   GemmBatchArgs a;
   a.count = n;
+  int t128 = 0;
+  bool big = true;
+  for (int i = 0; i < n; ++i) {
+    t128 += ((descs[i].m + 127) / 128) * ((descs[i].n + 127) / 128);
+    if (descs[i].m < 128 || descs[i].n < 128) big = false;
+  }
+  int bm = (g_gemm_tile_policy == 128 || (g_gemm_tile_policy == 0 && big && t128 >= 384)) ? 128 : 64;
   int total = 0;
-  constexpr int BM = 64, BN = 64;
   for (int i = 0; i < n; ++i) {
     a.d[i] = descs[i];
     a.tile_start[i] = total;
-    total += ((descs[i].m + BM - 1) / BM) * ((descs[i].n + BN - 1) / BN);
+    total += ((descs[i].m + bm - 1) / bm) * ((descs[i].n + bm - 1) / bm);
   }
   a.tile_start[n] = total;
   a.total_tiles = total;
   if (total == 0) return;
-  if (descs[0].transB)
-    hipLaunchKernelGGL((dgemm_batch_kernel<64, 64, 16, 2, 2, true>), dim3(total), dim3(256), 0, stream, a);
-  else
-    hipLaunchKernelGGL((dgemm_batch_kernel<64, 64, 16, 2, 2, false>), dim3(total), dim3(256), 0, stream, a);
+  const bool tb = descs[0].transB;
+  if (bm == 128) {
+    if (tb) hipLaunchKernelGGL((dgemm_batch_kernel<128, 128, 16, 2, 2, true>), dim3(total), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((dgemm_batch_kernel<128, 128, 16, 2, 2, false>), dim3(total), dim3(256), 0, stream, a);
+  } else {
+    if (tb) hipLaunchKernelGGL((dgemm_batch_kernel<64, 64, 16, 2, 2, true>), dim3(total), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((dgemm_batch_kernel<64, 64, 16, 2, 2, false>), dim3(total), dim3(256), 0, stream, a);
+  }
 }
 
 void launch_gemm_batch(const GemmDesc* descs, int n, hipStream_t stream) {
-  // split by transB and into chunks that fit the kernel argument block
   std::vector<GemmDesc> nt, nn;
   for (int i = 0; i < n; ++i) (descs[i].transB ? nt : nn).push_back(descs[i]);
   for (auto* v : {&nt, &nn})
@@ -324,38 +394,75 @@ void launch_gemm_batch(const GemmDesc* descs, int n, hipStream_t stream) {
 
 static constexpr int kTrsmRows = 16;
 
-void launch_trsm_batch(const TrsmDesc* descs, int n, hipStream_t stream) {
+// invD[i] must already hold the inverted diagonal blocks of descs[i].L
+static void launch_trsm_inv(const TrsmDesc* descs, const double* const* invD, int n, hipStream_t stream) {
   for (int s0 = 0; s0 < n; s0 += kMaxTrsmBatch) {
     int cnt = std::min(kMaxTrsmBatch, n - s0);
-    TrsmBatchArgs a;
+    TrsmInvArgs a;
     a.count = cnt;
     int total = 0, maxn = 0;
     for (int i = 0; i < cnt; ++i) {
       a.d[i] = descs[s0 + i];
+      a.invD[i] = invD[s0 + i];
       a.block_start[i] = total;
       total += (a.d[i].m + kTrsmRows - 1) / kTrsmRows;
       maxn = std::max(maxn, a.d[i].n);
     }
     a.block_start[cnt] = total;
     if (total == 0) continue;
-    size_t lds = (size_t)kTrsmRows * (maxn + 1) * sizeof(double);
-    hipLaunchKernelGGL((dtrsm_rltn_kernel<kTrsmRows>), dim3(total), dim3(256), lds, stream, a);
+    size_t lds = (size_t)((maxn + 63) / 64) * 64 * kTrsmRows * sizeof(double);
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)dtrsm_inv_kernel<kTrsmRows>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    hipLaunchKernelGGL((dtrsm_inv_kernel<kTrsmRows>), dim3(total), dim3(256), lds, stream, a);
   }
 }
 
-// Blocked tile Cholesky (lower): diag block in LDS, panel TRSM, lower-only update.
-void launch_potrf(const PotrfDesc& p, hipStream_t stream) {
+size_t trsm_workspace_bytes(const TrsmDesc* descs, int n) {
+  size_t bytes = 0;
+  std::vector<const double*> seen;
+  for (int i = 0; i < n; ++i) {
+    if (std::find(seen.begin(), seen.end(), descs[i].L) != seen.end()) continue;
+    seen.push_back(descs[i].L);
+    bytes += (size_t)((descs[i].n + 63) / 64) * 4096 * sizeof(double);
+  }
+  return bytes;
+}
+
+void launch_trsm_batch(const TrsmDesc* descs, int n, hipStream_t stream, double* ws) {
+  if (n <= 0) return;
+  std::vector<const double*> seen;
+  std::vector<const double*> inv(n);
+  size_t off = 0;
+  for (int i = 0; i < n; ++i) {
+    auto it = std::find(seen.begin(), seen.end(), descs[i].L);
+    if (it != seen.end()) { inv[i] = inv[std::find_if(descs, descs + i, [&](const TrsmDesc& d) { return d.L == descs[i].L; }) - descs]; continue; }
+    seen.push_back(descs[i].L);
+    int nblk = (descs[i].n + 63) / 64;
+    double* blk = ws + off;
+    off += (size_t)nblk * 4096;
+    hipLaunchKernelGGL(dtrtri_diag_kernel, dim3(nblk), dim3(64), 0, stream, descs[i].L, descs[i].ldl, descs[i].n, blk);
+    inv[i] = blk;
+  }
+  launch_trsm_inv(descs, inv.data(), n, stream);
+}
+
+// Blocked tile Cholesky (lower). ws needs 4096 doubles.
+void launch_potrf(const PotrfDesc& p, hipStream_t stream, double* ws) {
   const int JB = 64;
   for (int j = 0; j < p.n; j += JB) {
     const int jb = std::min(JB, p.n - j);
-    hipLaunchKernelGGL(dpotrf_diag_kernel, dim3(1), dim3(256), 0, stream, p.A, p.lda, j, jb, p.info);
+    hipLaunchKernelGGL(dpotrf_diag_inv_kernel, dim3(1), dim3(64), 0, stream, p.A, p.lda, j, jb, ws, p.info);
     const int rest = p.n - j - jb;
     if (rest <= 0) break;
     TrsmDesc t;
     t.L = p.A + (size_t)j * p.lda + j;
     t.B = p.A + (size_t)j * p.lda + j + jb;
     t.m = rest; t.n = jb; t.ldl = p.lda; t.ldb = p.lda; t.trans = 1;
-    launch_trsm_batch(&t, 1, stream);
+    const double* inv = ws;
+    launch_trsm_inv(&t, &inv, 1, stream);
     GemmDesc g;
     g.A = t.B; g.B = t.B; g.C = p.A + (size_t)(j + jb) * p.lda + j + jb;
     g.m = rest; g.n = rest; g.k = jb; g.lda = p.lda; g.ldb = p.lda; g.ldc = p.lda;
@@ -366,11 +473,16 @@ void launch_potrf(const PotrfDesc& p, hipStream_t stream) {
 
 }  // namespace kern
 
-void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal) {
+size_t kernel_batch_workspace_bytes(const KernelBatch& b) {
+  size_t w = b.potrf.empty() ? 0 : 4096 * sizeof(double);
+  return std::max(w, kern::trsm_workspace_bytes(b.trsm.data(), (int)b.trsm.size()));
+}
+
+void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal, void* ws) {
   (void)device_ordinal;
   // critical-path kernels first: POTRF, then TRSM, then the GEMM/SYRK updates
-  for (auto& p : b.potrf) kern::launch_potrf(p, stream);
-  if (!b.trsm.empty()) kern::launch_trsm_batch(b.trsm.data(), (int)b.trsm.size(), stream);
+  for (auto& p : b.potrf) kern::launch_potrf(p, stream, static_cast<double*>(ws));
+  if (!b.trsm.empty()) kern::launch_trsm_batch(b.trsm.data(), (int)b.trsm.size(), stream, static_cast<double*>(ws));
   if (!b.gemm.empty()) kern::launch_gemm_batch(b.gemm.data(), (int)b.gemm.size(), stream);
   for (auto& g : b.generic) g(stream);
 }
@@ -378,18 +490,36 @@ void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal)
 }  // namespace parsec
 
 // ------------------------------------------------- C entry points (tests/bench)
+namespace {
+std::mutex g_ws_m;
+void* g_ws = nullptr;
+size_t g_ws_bytes = 0;
+void* test_ws(size_t bytes) {
+  std::lock_guard<std::mutex> g(g_ws_m);
+  if (g_ws_bytes < bytes) {
+    (void)hipDeviceSynchronize();
+    if (g_ws) (void)hipFree(g_ws);
+    (void)hipMalloc(&g_ws, bytes);
+    g_ws_bytes = bytes;
+  }
+  return g_ws;
+}
+}  // namespace
+
 extern "C" {
 int parsec_amd_dgemm_batch(const parsec::GemmDesc* descs, int n, void* stream) {
   parsec::kern::launch_gemm_batch(descs, n, (hipStream_t)stream);
   return (int)hipGetLastError();
 }
 int parsec_amd_dtrsm_batch(const parsec::TrsmDesc* descs, int n, void* stream) {
-  parsec::kern::launch_trsm_batch(descs, n, (hipStream_t)stream);
+  void* ws = test_ws(parsec::kern::trsm_workspace_bytes(descs, n) + 64);
+  parsec::kern::launch_trsm_batch(descs, n, (hipStream_t)stream, static_cast<double*>(ws));
   return (int)hipGetLastError();
 }
 int parsec_amd_dpotrf_tile(double* A, int n, int lda, int* info, void* stream) {
   parsec::PotrfDesc p{A, n, lda, info};
-  parsec::kern::launch_potrf(p, (hipStream_t)stream);
+  void* ws = test_ws(4096 * sizeof(double));
+  parsec::kern::launch_potrf(p, (hipStream_t)stream, static_cast<double*>(ws));
   return (int)hipGetLastError();
 }
 }
