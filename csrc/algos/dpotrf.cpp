@@ -12,6 +12,7 @@
 // the SYRK/GEMM feeding the next panel are routed to the high-priority stream.
 #include <cmath>
 #include <cstring>
+#include <memory>
 
 #include "../device/device.hpp"
 #include "linalg.hpp"
@@ -86,6 +87,11 @@ class DpotrfTaskpool : public PtgTaskpool {
   int* info_dev = nullptr;
   int info_dev_index = -1;
   std::atomic<int> info_cpu{0};
+  // 64x64 diagonal-block inverses kept by POTRF(k) on the GPU so the TRSM(m,k)
+  // panel solves skip their own inversion (valid when POTRF(k) ran on that GPU).
+  double* invbuf = nullptr;
+  size_t inv_stride = 0;
+  std::unique_ptr<std::atomic<uint8_t>[]> inv_ready;
   void on_complete_internal() override {
     int v = info_cpu.load();
     if (info_dev) {
@@ -97,6 +103,7 @@ class DpotrfTaskpool : public PtgTaskpool {
   }
   ~DpotrfTaskpool() override {
     if (info_dev) device_free(info_dev_index, info_dev);
+    if (invbuf) device_free(info_dev_index, invbuf);
   }
 };
 
@@ -110,6 +117,10 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
   if (gpu >= 0) {
     tp->info_dev = static_cast<int*>(device_alloc(gpu, sizeof(int)));
     tp->info_dev_index = gpu;
+    tp->inv_stride = (size_t)((A->nb + 63) / 64) * 4096;
+    tp->invbuf = static_cast<double*>(device_alloc(gpu, tp->inv_stride * A->nt * sizeof(double)));
+    tp->inv_ready.reset(new std::atomic<uint8_t>[A->nt]);
+    for (int64_t i = 0; i < A->nt; ++i) tp->inv_ready[i].store(0);
   }
   const int64_t NT = A->nt;
   const int64_t nb = A->nb;
@@ -138,9 +149,14 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
     d.flows = {T};
     BodyDef g;
     g.type = DEV_HIP;
-    g.gpu = [rows, ld, info_dev](GpuExecContext* c, Task* t) {
+    g.gpu = [rows, ld, info_dev, self](GpuExecContext* c, Task* t) {
       int k = t->locals[0];
-      c->batch->potrf.push_back(PotrfDesc{static_cast<double*>(c->ptr(0)), rows(k), (int)ld, info_dev});
+      PotrfDesc pd{static_cast<double*>(c->ptr(0)), rows(k), (int)ld, info_dev};
+      if (self->invbuf && c->device->device_index == self->info_dev_index) {
+        pd.invD_out = self->invbuf + self->inv_stride * k;
+        self->inv_ready[k].store(1, std::memory_order_release);
+      }
+      c->batch->potrf.push_back(pd);
       return HOOK_DONE;
     };
     BodyDef cpu;
@@ -178,9 +194,11 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
     d.flows = {T, C};
     BodyDef g;
     g.type = DEV_HIP;
-    g.gpu = [rows, cols, ld](GpuExecContext* c, Task* t) {
+    g.gpu = [rows, cols, ld, self](GpuExecContext* c, Task* t) {
       int k = t->locals[0], m = t->locals[1];
       TrsmDesc td;
+      if (self->invbuf && c->device->device_index == self->info_dev_index && self->inv_ready[k].load(std::memory_order_acquire))
+        td.invD = self->invbuf + self->inv_stride * k;
       td.L = static_cast<double*>(c->ptr(0));
       td.B = static_cast<double*>(c->ptr(1));
       td.m = rows(m); td.n = cols(k); td.ldl = (int)ld; td.ldb = (int)ld; td.trans = 1;

@@ -62,12 +62,14 @@ struct TrsmDesc {  // B := B * op(L)^-1 ; right side, lower, (trans), non-unit
   int ldl, ldb;
   uint8_t trans;  // 1: B * L^-T (the Cholesky panel)
   uint8_t pad[7];
+  const double* invD = nullptr;  // optional: inverses of L's 64x64 diagonal blocks (from POTRF)
 };
 
 struct PotrfDesc {
   double* A;
   int n, lda;
   int* info;  // device pointer (may be null)
+  double* invD_out = nullptr;  // optional: keep the 64x64 diagonal-block inverses (ceil(n/64) x 4096 doubles)
 };
 
 struct KernelBatch {

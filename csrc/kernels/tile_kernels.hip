@@ -211,76 +211,170 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
     }
 }
 
-// ========================================================= diag blocks (1 wave)
+// ========================================================= diag blocks (4 waves)
 // Factor the w x w (w <= 64) lower block at T (ldt) in place and/or write its
-// inverse (64 x 64 col-major, identity padded) to invD. One wave, no block
-// barriers. Right-looking with a ROTATING register window: lane r owns row r; at
-// step j its a[0] is column j and a[1..] the trailing columns, so after the
-// update every slot shifts down by one. The outer loop is a real loop and every
-// register index is static (no scratch); each step is 63 independent FMAs fed by
-// broadcast LDS reads of the just-finished column. The inverse (lane c owns
-// column c of L^-1, forward substitution) uses the same window.
-constexpr int kDiagLd = 128;  // Ls column stride: reads of Ls[j][j+k] stay in bounds
-__device__ __forceinline__ void wave_potrf64(double* T, int ldt, int w, double* invD, int* info, int info_base, bool factor) {
-  __shared__ double Ls[64 * kDiagLd];  // Ls[c*kDiagLd + r] = L(r, c), zero above the diagonal / beyond 63
-  __shared__ double Xs[64][65];        // inverse staging: Xs[c][r] = inv(r, c)
-  const int r = threadIdx.x;
-  double a[64];
-#pragma unroll
-  for (int c = 0; c < 64; ++c) a[c] = (r < w && c < w) ? T[(size_t)c * ldt + r] : (r == c ? 1.0 : 0.0);
-#pragma unroll
-  for (int c = 0; c < 64; ++c) Ls[c * kDiagLd + 64 + r] = 0.0;
-  if (factor) {
-    int bad = 0;
-#pragma unroll 1
-    for (int j = 0; j < 64; ++j) {
-      double dj = __shfl(a[0], j, 64);
-      bad = (dj <= 0.0 && !bad && j < w) ? j + 1 : bad;
-      dj = dj <= 0.0 ? 1.0 : dj;
-      const double s = __builtin_sqrt(dj);
-      const double v = (r == j) ? s : (r > j ? a[0] / s : 0.0);
-      Ls[j * kDiagLd + r] = v;
-      if (r < w && j < w && r >= j) T[(size_t)j * ldt + r] = v;
-      __builtin_amdgcn_wave_barrier();
-      const double* colj = &Ls[j * kDiagLd + j];
-#pragma unroll
-      for (int k = 1; k < 64; ++k) a[k - 1] = a[k] - v * colj[k];
-      a[63] = 0.0;
-      __builtin_amdgcn_wave_barrier();
-    }
-    if (bad && r == 0 && info) atomicCAS(info, 0, info_base + bad);
-  } else {
-#pragma unroll
-    for (int c = 0; c < 64; ++c) Ls[c * kDiagLd + r] = (r >= c) ? a[c] : 0.0;
-  }
-  if (!invD) return;
-  __builtin_amdgcn_wave_barrier();
-  // forward substitution L X = I, lane r owns column r of X (x[0] = current row)
-#pragma unroll
-  for (int i = 0; i < 64; ++i) a[i] = (i == r) ? 1.0 : 0.0;
-#pragma unroll 1
-  for (int i = 0; i < 64; ++i) {
-    const double* coli = &Ls[i * kDiagLd + i];
-    const double xi = a[0] / coli[0];
-    Xs[r][i] = xi;
-#pragma unroll
-    for (int k = 1; k < 64; ++k) a[k - 1] = a[k] - coli[k] * xi;
-    a[63] = 0.0;
-  }
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int c = 0; c < 64; ++c) invD[(size_t)c * 64 + r] = Xs[c][r];
+// inverse (64 x 64 col-major, identity padded) to invD. 256 threads; lane r of
+// wave v owns row r of columns 16v..16v+15 in registers. Blocked by 16-column
+// panels so the serial chain never leaves a wave:
+//   * panel p is factored entirely inside wave p: pivots and column entries are
+//     broadcast with v_readlane (no LDS round trip, no barrier), 1/sqrt is a
+//     hardware rsq refined by two Newton steps (no IEEE divide on the chain);
+//   * the panel goes to LDS (double-buffered, one barrier per panel) and waves
+//     v > p apply the rank-16 update to their columns.
+// The inverse is blocked the same way: each wave inverts its 16x16 diagonal
+// block, then wave j walks down its block column X_ij = -X_ii sum_k L_ik X_kj.
+__device__ __forceinline__ double readlane_d(double x, int lane) {
+  const long long b = __builtin_bit_cast(long long, x);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
 
-__global__ __launch_bounds__(64) void dpotrf_diag_inv_kernel(double* A, int lda, int j, int jb, double* invD, int* info) {
-  wave_potrf64(A + (size_t)j * lda + j, lda, jb, invD, info, j, true);
+__device__ __forceinline__ double rsqrt_nr(double d) {
+  double y = __builtin_amdgcn_rsq(d);
+  const double h = 0.5 * d;
+  y = y * __builtin_fma(-h * y, y, 1.5);
+  y = y * __builtin_fma(-h * y, y, 1.5);
+  return y;
+}
+
+__device__ __forceinline__ void block_potrf64(double* T, int ldt, int w, double* invD, int* info, int info_base, bool factor) {
+  __shared__ double Ls[64][65];      // Ls[c][r] = L(r, c)
+  __shared__ double Xs[64][65];      // Xs[c][r] = X(r, c), X = L^-1
+  __shared__ double Pn[2][16][65];   // panel broadcast buffers
+  __shared__ double Ts[4][16][17];   // per-wave scratch for the inverse
+  __shared__ double dinv[64];
+  __shared__ int bad_s;
+  const int r = threadIdx.x & 63;
+  const int v = threadIdx.x >> 6;
+  double a[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = 16 * v + i;
+    a[i] = (r < w && c < w) ? T[(size_t)c * ldt + r] : (r == c ? 1.0 : 0.0);
+  }
+  if (threadIdx.x == 0) bad_s = 0x7fffffff;
+  __syncthreads();
+  if (factor) {
+#pragma unroll 1
+    for (int p = 0; p < 4; ++p) {
+      double* pn = &Pn[p & 1][0][0];
+      if (v == p) {
+        int bad = 0x7fffffff;
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+          const int j = 16 * p + jj;
+          double d = readlane_d(a[jj], j);
+          if (d <= 0.0 && j < w && bad == 0x7fffffff) bad = j + 1;
+          d = d <= 0.0 ? 1.0 : d;
+          const double rs = rsqrt_nr(d);
+          const double lv = (r == j) ? d * rs : (r > j ? a[jj] * rs : 0.0);
+          a[jj] = lv;
+          if (r == j) dinv[j] = rs;
+#pragma unroll
+          for (int i = jj + 1; i < 16; ++i) a[i] -= lv * readlane_d(lv, 16 * p + i);
+        }
+        if (r == 0 && bad != 0x7fffffff) atomicMin(&bad_s, bad);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) pn[i * 65 + r] = a[i];
+      }
+      __syncthreads();
+      if (v > p) {
+        double lr[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) lr[t] = pn[t * 65 + r];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          double s = 0.0;
+#pragma unroll
+          for (int t = 0; t < 16; ++t) s = __builtin_fma(lr[t], pn[t * 65 + 16 * v + i], s);
+          a[i] -= s;
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && bad_s != 0x7fffffff && info) atomicCAS(info, 0, info_base + bad_s);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = 16 * v + i;
+      if (r < w && c < w && r >= c) T[(size_t)c * ldt + r] = a[i];
+    }
+  }
+  if (!invD) return;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = 16 * v + i;
+    Ls[c][r] = (r >= c) ? a[i] : 0.0;
+    Xs[c][r] = 0.0;
+    if (!factor && r == c) dinv[c] = 1.0 / a[i];
+  }
+  __syncthreads();
+  // (1) wave v inverts its 16x16 diagonal block; lane c < 16 owns column c
+  const int b0 = 16 * v;
+  if (r < 16) {
+    double x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      double s = (i == r) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < i; ++k) s = __builtin_fma(-Ls[b0 + k][b0 + i], x[k], s);
+      x[i] = s * dinv[b0 + i];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Xs[b0 + r][b0 + i] = x[i];
+  }
+  __syncthreads();
+  // (2) wave j computes block column j below the diagonal, top to bottom
+  {
+    const int j = v;
+    const int c = r & 15, rg = r >> 4;  // lane -> column c, rows rg + 4q
+#pragma unroll 1
+    for (int i = j + 1; i < 4; ++i) {
+      double tq[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int k = j; k < i; ++k) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          const double xv = Xs[16 * j + c][16 * k + t];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) tq[q] = __builtin_fma(Ls[16 * k + t][16 * i + rg + 4 * q], xv, tq[q]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Ts[j][rg + 4 * q][c] = tq[q];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): scratch visible to the wave
+      double oq[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const double tv = Ts[j][t][c];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) oq[q] = __builtin_fma(-Xs[16 * i + t][16 * i + rg + 4 * q], tv, oq[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Xs[16 * j + c][16 * i + rg + 4 * q] = oq[q];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = 16 * v + k;
+    invD[(size_t)c * 64 + r] = Xs[c][r];
+  }
+}
+
+constexpr int kDiagThreads = 256;
+
+__global__ __launch_bounds__(kDiagThreads) void dpotrf_diag_inv_kernel(double* A, int lda, int j, int jb, double* invD, int* info) {
+  block_potrf64(A + (size_t)j * lda + j, lda, jb, invD, info, j, true);
 }
 
 // Inverses of the 64x64 diagonal blocks of L (n x n): block b -> invD + b*4096.
-__global__ __launch_bounds__(64) void dtrtri_diag_kernel(const double* L, int ldl, int n, double* invD) {
+__global__ __launch_bounds__(kDiagThreads) void dtrtri_diag_kernel(const double* L, int ldl, int n, double* invD) {
   const int b = blockIdx.x;
   const int c0 = b * 64;
-  wave_potrf64(const_cast<double*>(L) + (size_t)c0 * ldl + c0, ldl, min(64, n - c0), invD + (size_t)b * 4096, nullptr, 0, false);
+  block_potrf64(const_cast<double*>(L) + (size_t)c0 * ldl + c0, ldl, min(64, n - c0), invD + (size_t)b * 4096, nullptr, 0, false);
 }
 
 // ==================================================================== TRSM
@@ -292,9 +386,16 @@ struct TrsmInvArgs {
   const double* invD[kMaxTrsmBatch];
 };
 
+// B := B L^-T by 64-column blocks: R_j = B_j - X_<j L_j,<j^T, X_j = R_j invD_j^T.
+// A workgroup owns BR = 16 rows of B (its row panel lives in LDS, stride 16:
+// conflict-free MFMA operand reads). 8 waves: wave (g, h) computes columns
+// 16g..16g+15 of the block over half h of the reduction, with four independent
+// MFMA accumulator chains; the two halves are summed through LDS.
+constexpr int kTrsmThreads = 512;
 template <int BR>
-__global__ __launch_bounds__(256) void dtrsm_inv_kernel(const TrsmInvArgs args) {
-  extern __shared__ double P[];  // [ncols_padded][BR]
+__global__ __launch_bounds__(kTrsmThreads) void dtrsm_inv_kernel(const TrsmInvArgs args) {
+  static_assert(BR == 16, "MFMA operand layout assumes 16-row panels");
+  extern __shared__ double P[];  // [ncols_padded][BR], then red[16][64]
   const int b = blockIdx.x;
   const int di = find_desc(args, args.block_start, b);
   const TrsmDesc& d = args.d[di];
@@ -302,48 +403,77 @@ __global__ __launch_bounds__(256) void dtrsm_inv_kernel(const TrsmInvArgs args) 
   const int r0 = (b - args.block_start[di]) * BR;
   const int n = d.n, m = d.m;
   const int nblk = (n + 63) / 64;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double* red = P + nblk * 64 * BR;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int g = wv & 3, h = wv >> 2;
   const int fr = lane & 15, fk = lane >> 4;
   const double* __restrict__ L = d.L;
-  const int ldl = d.ldl;
-  // load the row panel, column-major in LDS with stride BR
-  for (int idx = tid; idx < nblk * 64 * BR; idx += 256) {
+  const size_t ldl = d.ldl;
+  for (int idx = tid; idx < nblk * 64 * BR; idx += kTrsmThreads) {
     int c = idx / BR, rr = idx % BR;
     P[idx] = (c < n && r0 + rr < m) ? d.B[(size_t)c * d.ldb + r0 + rr] : 0.0;
   }
   __syncthreads();
   for (int jb = 0; jb < nblk; ++jb) {
     const int c0 = jb * 64;
-    const int cw = c0 + 16 * w + fr;  // L row this lane feeds as MFMA A-operand
-    double4_t acc = (double4_t){0.0, 0.0, 0.0, 0.0};
-    for (int k = 0; k < c0; k += 4) {
-      double a = (cw < n) ? L[(size_t)(k + fk) * ldl + cw] : 0.0;
-      double bb = P[(k + fk) * BR + fr];
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
-    }
-    // R[c][r] = B[r][c] - acc ; lane holds c = c0 + 16w + fk + 4i, r = fr
+    const int cw = c0 + 16 * g + fr;  // L row this lane feeds as the MFMA A-operand
+    const bool valid = cw < n;
+    const double* __restrict__ Lp = L + (valid ? cw : 0);
+    double4_t acc[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int c = c0 + 16 * w + fk + 4 * i;
-      P[c * BR + fr] -= acc[i];
+    for (int u = 0; u < 4; ++u) acc[u] = (double4_t){0.0, 0.0, 0.0, 0.0};
+    const int kh = c0 / 2;  // multiple of 32
+    const int kbeg = h * kh, kend = kbeg + kh;
+    for (int k = kbeg; k < kend; k += 16) {
+      double av[4], bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        av[u] = valid ? Lp[(size_t)(k + 4 * u + fk) * ldl] : 0.0;
+        bv[u] = P[(k + 4 * u + fk) * BR + fr];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc[u], 0, 0, 0);
+    }
+    double4_t s = acc[0] + acc[1] + acc[2] + acc[3];
+    if (h == 1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[(g * 4 + q) * 64 + lane] = s[q];
     }
     __syncthreads();
-    double4_t acc2 = (double4_t){0.0, 0.0, 0.0, 0.0};
+    if (h == 0) {
 #pragma unroll
-    for (int kk = 0; kk < 64; kk += 4) {
-      double a = invD[(size_t)jb * 4096 + (size_t)(kk + fk) * 64 + 16 * w + fr];
-      double bb = P[(c0 + kk + fk) * BR + fr];
-      acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc2, 0, 0, 0);
+      for (int q = 0; q < 4; ++q) {
+        const int c = c0 + 16 * g + fk + 4 * q;
+        P[c * BR + fr] -= s[q] + red[(g * 4 + q) * 64 + lane];
+      }
     }
     __syncthreads();
+    // X_j = R_j invD_j^T, reduction over kk split between the two halves
+    double4_t t0 = (double4_t){0.0, 0.0, 0.0, 0.0}, t1 = t0;
+    const double* __restrict__ Dj = invD + (size_t)jb * 4096 + 16 * g + fr;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int c = c0 + 16 * w + fk + 4 * i;
-      P[c * BR + fr] = acc2[i];
+    for (int kk = 32 * h; kk < 32 * h + 32; kk += 8) {
+      const double a0 = Dj[(kk + fk) * 64], a1 = Dj[(kk + 4 + fk) * 64];
+      const double b0 = P[(c0 + kk + fk) * BR + fr], b1 = P[(c0 + kk + 4 + fk) * BR + fr];
+      t0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, t0, 0, 0, 0);
+      t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, t1, 0, 0, 0);
+    }
+    double4_t t = t0 + t1;
+    if (h == 1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[(g * 4 + q) * 64 + lane] = t[q];
+    }
+    __syncthreads();
+    if (h == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = c0 + 16 * g + fk + 4 * q;
+        P[c * BR + fr] = t[q] + red[(g * 4 + q) * 64 + lane];
+      }
     }
     __syncthreads();
   }
-  for (int idx = tid; idx < n * BR; idx += 256) {
+  for (int idx = tid; idx < n * BR; idx += kTrsmThreads) {
     int c = idx / BR, rr = idx % BR;
     if (r0 + rr < m) d.B[(size_t)c * d.ldb + r0 + rr] = P[idx];
   }
@@ -393,9 +523,15 @@ void launch_gemm_batch(const GemmDesc* descs, int n, hipStream_t stream) {
 }
 
 static constexpr int kTrsmRows = 16;
+static constexpr int kTrsmMaxCols = 18 * 64;  // LDS bound: (18*64*16 + 1024) doubles < 160 KiB
 
 // invD[i] must already hold the inverted diagonal blocks of descs[i].L
 static void launch_trsm_inv(const TrsmDesc* descs, const double* const* invD, int n, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)dtrsm_inv_kernel<kTrsmRows>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
   for (int s0 = 0; s0 < n; s0 += kMaxTrsmBatch) {
     int cnt = std::min(kMaxTrsmBatch, n - s0);
     TrsmInvArgs a;
@@ -410,13 +546,9 @@ static void launch_trsm_inv(const TrsmDesc* descs, const double* const* invD, in
     }
     a.block_start[cnt] = total;
     if (total == 0) continue;
-    size_t lds = (size_t)((maxn + 63) / 64) * 64 * kTrsmRows * sizeof(double);
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)dtrsm_inv_kernel<kTrsmRows>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr = true;
-    }
-    hipLaunchKernelGGL((dtrsm_inv_kernel<kTrsmRows>), dim3(total), dim3(256), lds, stream, a);
+    if (maxn > kTrsmMaxCols) fatal("dtrsm tile kernel: n=%d exceeds the LDS-resident panel limit %d", maxn, kTrsmMaxCols);
+    size_t lds = ((size_t)((maxn + 63) / 64) * 64 * kTrsmRows + 1024) * sizeof(double);
+    hipLaunchKernelGGL((dtrsm_inv_kernel<kTrsmRows>), dim3(total), dim3(kTrsmThreads), lds, stream, a);
   }
 }
 
@@ -424,6 +556,7 @@ size_t trsm_workspace_bytes(const TrsmDesc* descs, int n) {
   size_t bytes = 0;
   std::vector<const double*> seen;
   for (int i = 0; i < n; ++i) {
+    if (descs[i].invD) continue;
     if (std::find(seen.begin(), seen.end(), descs[i].L) != seen.end()) continue;
     seen.push_back(descs[i].L);
     bytes += (size_t)((descs[i].n + 63) / 64) * 4096 * sizeof(double);
@@ -431,38 +564,43 @@ size_t trsm_workspace_bytes(const TrsmDesc* descs, int n) {
   return bytes;
 }
 
+// Diagonal-block inverses come from the descriptor (kept by POTRF) or are
+// computed once per distinct L into the workspace.
 void launch_trsm_batch(const TrsmDesc* descs, int n, hipStream_t stream, double* ws) {
   if (n <= 0) return;
-  std::vector<const double*> seen;
+  std::vector<std::pair<const double*, const double*>> seen;  // L -> inverse blocks
   std::vector<const double*> inv(n);
   size_t off = 0;
   for (int i = 0; i < n; ++i) {
-    auto it = std::find(seen.begin(), seen.end(), descs[i].L);
-    if (it != seen.end()) { inv[i] = inv[std::find_if(descs, descs + i, [&](const TrsmDesc& d) { return d.L == descs[i].L; }) - descs]; continue; }
-    seen.push_back(descs[i].L);
+    if (descs[i].invD) { inv[i] = descs[i].invD; continue; }
+    auto it = std::find_if(seen.begin(), seen.end(), [&](const auto& e) { return e.first == descs[i].L; });
+    if (it != seen.end()) { inv[i] = it->second; continue; }
     int nblk = (descs[i].n + 63) / 64;
     double* blk = ws + off;
     off += (size_t)nblk * 4096;
-    hipLaunchKernelGGL(dtrtri_diag_kernel, dim3(nblk), dim3(64), 0, stream, descs[i].L, descs[i].ldl, descs[i].n, blk);
+    hipLaunchKernelGGL(dtrtri_diag_kernel, dim3(nblk), dim3(kDiagThreads), 0, stream, descs[i].L, descs[i].ldl, descs[i].n, blk);
+    seen.emplace_back(descs[i].L, blk);
     inv[i] = blk;
   }
   launch_trsm_inv(descs, inv.data(), n, stream);
 }
 
-// Blocked tile Cholesky (lower). ws needs 4096 doubles.
+// Blocked tile Cholesky (lower). ws needs 4096 doubles unless p.invD_out keeps
+// every diagonal-block inverse (then the panel TRSMs can reuse them).
 void launch_potrf(const PotrfDesc& p, hipStream_t stream, double* ws) {
   const int JB = 64;
   for (int j = 0; j < p.n; j += JB) {
     const int jb = std::min(JB, p.n - j);
-    hipLaunchKernelGGL(dpotrf_diag_inv_kernel, dim3(1), dim3(64), 0, stream, p.A, p.lda, j, jb, ws, p.info);
+    double* inv = p.invD_out ? p.invD_out + (size_t)(j / JB) * 4096 : ws;
+    hipLaunchKernelGGL(dpotrf_diag_inv_kernel, dim3(1), dim3(kDiagThreads), 0, stream, p.A, p.lda, j, jb, inv, p.info);
     const int rest = p.n - j - jb;
     if (rest <= 0) break;
     TrsmDesc t;
     t.L = p.A + (size_t)j * p.lda + j;
     t.B = p.A + (size_t)j * p.lda + j + jb;
     t.m = rest; t.n = jb; t.ldl = p.lda; t.ldb = p.lda; t.trans = 1;
-    const double* inv = ws;
-    launch_trsm_inv(&t, &inv, 1, stream);
+    const double* cinv = inv;
+    launch_trsm_inv(&t, &cinv, 1, stream);
     GemmDesc g;
     g.A = t.B; g.B = t.B; g.C = p.A + (size_t)(j + jb) * p.lda + j + jb;
     g.m = rest; g.n = rest; g.k = jb; g.lda = p.lda; g.ldb = p.lda; g.ldc = p.lda;
