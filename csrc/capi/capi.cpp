@@ -1,0 +1,620 @@
+// C API (include/parsec.h) over the native runtime.
+//
+// Parity: reference parsec/runtime.h:155-628 (lifecycle, taskpool callbacks,
+// compose), data_distribution.h (C collection vtable with varargs callbacks),
+// two_dim_rectangle_cyclic.c (block-cyclic init / data_of), arena.c,
+// interfaces/dtd/insert_function.c:2978-3300 (variadic insert_task,
+// unpack_args), profiling.h (user dictionary / trace).
+#include <cstdarg>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <atomic>
+#include <thread>
+
+#include "../comm/comm.hpp"
+#include "../core/mca.hpp"
+#include "../core/runtime.hpp"
+#include "../data/collections.hpp"
+#include "../device/device.hpp"
+#include "../dtd/dtd.hpp"
+#include "../prof/profiling.hpp"
+// after the runtime headers: the C API defines PASSED_BY_REF & co. as macros
+#include "../../include/parsec.h"
+
+using namespace parsec;
+
+namespace {
+
+// ----------------------------------------------------------- datatypes
+std::mutex g_dt_m;
+std::vector<Datatype> g_types;  // handle -> layout
+
+void init_types_locked() {
+  if (!g_types.empty()) return;
+  const uint32_t sz[] = {0, 1, 2, 4, 8, 4, 8, 8, 16, 1};
+  for (uint32_t s : sz) g_types.push_back(Datatype::contiguous(s ? s : 1, s ? 1 : 0));
+}
+Datatype type_of(parsec_datatype_t h) {
+  std::lock_guard<std::mutex> g(g_dt_m);
+  init_types_locked();
+  if (h < 0 || h >= (int)g_types.size()) fatal("invalid parsec_datatype_t handle %d", h);
+  return g_types[h];
+}
+parsec_datatype_t new_type(const Datatype& d) {
+  std::lock_guard<std::mutex> g(g_dt_m);
+  init_types_locked();
+  g_types.push_back(d);
+  return (parsec_datatype_t)g_types.size() - 1;
+}
+
+// ------------------------------------------------ C collection adapter
+template <class R, class F>
+R call_varargs(F f, parsec_data_collection_t* dc, const int64_t* idx, int n) {
+  int a[8] = {};
+  for (int i = 0; i < n && i < 8; ++i) a[i] = (int)idx[i];
+  switch (n) {
+    case 0: return f(dc);
+    case 1: return f(dc, a[0]);
+    case 2: return f(dc, a[0], a[1]);
+    case 3: return f(dc, a[0], a[1], a[2]);
+    case 4: return f(dc, a[0], a[1], a[2], a[3]);
+    case 5: return f(dc, a[0], a[1], a[2], a[3], a[4]);
+    case 6: return f(dc, a[0], a[1], a[2], a[3], a[4], a[5]);
+    default: return f(dc, a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7]);
+  }
+}
+
+struct CCollection : DataCollection {
+  parsec_data_collection_t* c = nullptr;
+  uint32_t rank_of(const int64_t* idx, int n) const override {
+    if (c->rank_of) return call_varargs<uint32_t>(c->rank_of, c, idx, n);
+    if (c->rank_of_key) return c->rank_of_key(c, data_key(idx, n));
+    return myrank;
+  }
+  int32_t vpid_of(const int64_t* idx, int n) const override { return c->vpid_of ? call_varargs<int32_t>(c->vpid_of, c, idx, n) : 0; }
+  Data* data_of(const int64_t* idx, int n) override {
+    if (c->data_of) return call_varargs<Data*>(c->data_of, c, idx, n);
+    if (c->data_of_key) return c->data_of_key(c, data_key(idx, n));
+    return nullptr;
+  }
+  uint64_t data_key(const int64_t* idx, int n) const override {
+    if (c->data_key) return call_varargs<uint64_t>(c->data_key, c, idx, n);
+    uint64_t k = 0;
+    for (int i = 0; i < n; ++i) k = k * 1000003ULL + (uint64_t)idx[i];
+    return k;
+  }
+  uint32_t rank_of_key(uint64_t key) const override {
+    if (c->rank_of_key) return c->rank_of_key(c, key);
+    int64_t idx[1] = {(int64_t)key};
+    return c->rank_of ? call_varargs<uint32_t>(c->rank_of, c, idx, 1) : myrank;
+  }
+  int32_t vpid_of_key(uint64_t key) const override { return c->vpid_of_key ? c->vpid_of_key(c, key) : 0; }
+  Data* data_of_key(uint64_t key) override {
+    if (c->data_of_key) return c->data_of_key(c, key);
+    int64_t idx[1] = {(int64_t)key};
+    return c->data_of ? call_varargs<Data*>(c->data_of, c, idx, 1) : nullptr;
+  }
+};
+
+// Block-cyclic matrix behind parsec_matrix_block_cyclic_t: picks up the
+// user-provided `mat` pointer lazily (reference users assign it after init).
+struct CBlockCyclic : BlockCyclic {
+  parsec_matrix_block_cyclic_t* c = nullptr;
+  void sync() {
+    if (!mat && c->mat) allocate_storage(c->mat);
+  }
+  Data* data_of(const int64_t* idx, int n) override { sync(); return BlockCyclic::data_of(idx, n); }
+  Data* data_of_key(uint64_t key) override { sync(); return BlockCyclic::data_of_key(key); }
+};
+
+DataCollection* impl_of(parsec_data_collection_t* dc) {
+  if (!dc) return nullptr;
+  if (!dc->impl) fatal("data collection %p was not initialized (parsec_data_collection_init / parsec_matrix_block_cyclic_init)", (void*)dc);
+  return static_cast<DataCollection*>(dc->impl);
+}
+
+uint32_t bc_rank_of(parsec_data_collection_t* dc, ...) {
+  va_list ap;
+  va_start(ap, dc);
+  int64_t idx[2] = {va_arg(ap, int), va_arg(ap, int)};
+  va_end(ap);
+  return impl_of(dc)->rank_of(idx, 2);
+}
+int32_t bc_vpid_of(parsec_data_collection_t* dc, ...) {
+  va_list ap;
+  va_start(ap, dc);
+  int64_t idx[2] = {va_arg(ap, int), va_arg(ap, int)};
+  va_end(ap);
+  return impl_of(dc)->vpid_of(idx, 2);
+}
+parsec_data_t* bc_data_of(parsec_data_collection_t* dc, ...) {
+  va_list ap;
+  va_start(ap, dc);
+  int64_t idx[2] = {va_arg(ap, int), va_arg(ap, int)};
+  va_end(ap);
+  return impl_of(dc)->data_of(idx, 2);
+}
+parsec_data_key_t bc_data_key(parsec_data_collection_t* dc, ...) {
+  va_list ap;
+  va_start(ap, dc);
+  int64_t idx[2] = {va_arg(ap, int), va_arg(ap, int)};
+  va_end(ap);
+  return impl_of(dc)->data_key(idx, 2);
+}
+uint32_t bc_rank_of_key(parsec_data_collection_t* dc, parsec_data_key_t k) { return impl_of(dc)->rank_of_key(k); }
+int32_t bc_vpid_of_key(parsec_data_collection_t* dc, parsec_data_key_t k) { return impl_of(dc)->vpid_of_key(k); }
+parsec_data_t* bc_data_of_key(parsec_data_collection_t* dc, parsec_data_key_t k) { return impl_of(dc)->data_of_key(k); }
+
+// ----------------------------------------------------------------- DTD
+thread_local GpuExecContext* t_gpu_ctx = nullptr;
+std::mutex g_dtd_m;
+std::map<std::pair<dtd::DtdTaskpool*, std::string>, dtd::DtdTaskClass*> g_dtd_classes;
+
+dtd::DtdTaskpool* as_dtd(parsec_taskpool_t* tp) {
+  auto* d = dynamic_cast<dtd::DtdTaskpool*>(tp);
+  if (!d) fatal("taskpool %s is not a DTD taskpool", tp ? tp->taskpool_name.c_str() : "(null)");
+  return d;
+}
+
+struct PendingArgs {
+  std::vector<dtd::Arg> args;
+  std::vector<std::pair<int, int>> sig;
+};
+
+void parse_args(va_list ap, PendingArgs& pa) {
+  for (;;) {
+    int size = va_arg(ap, int);
+    if (size == PARSEC_DTD_ARG_END) break;
+    void* ptr = va_arg(ap, void*);
+    int flags = va_arg(ap, int);
+    dtd::Arg a;
+    a.op = flags;
+    const int op = flags & dtd::OP_MASK;
+    if (op == dtd::VALUE) {
+      a.ptr = ptr;
+      a.size = size;
+    } else if (op == dtd::SCRATCH) {
+      a.size = size;
+    } else if (op == dtd::REF) {
+      a.ptr = ptr;
+      a.size = size;
+    } else {
+      a.tile = reinterpret_cast<dtd::Tile*>(ptr);
+      a.size = (int)PASSED_BY_REF;
+    }
+    pa.args.push_back(a);
+    pa.sig.push_back({flags, a.size});
+    if ((int)pa.args.size() > PARSEC_DTD_MAX_PARAMS) fatal("parsec_dtd_insert_task: more than %d arguments", PARSEC_DTD_MAX_PARAMS);
+  }
+}
+
+// The reference keeps DTD tiles in the collection (parsec_dtd_tile_of takes no
+// taskpool); the runtime keeps them per taskpool, so the C API resolves against
+// the most recently created live DTD taskpool.
+std::atomic<dtd::DtdTaskpool*> g_last_dtd{nullptr};
+
+// user profiling stream (per thread)
+thread_local ProfilingStream* t_prof = nullptr;
+
+}  // namespace
+
+extern "C" {
+
+// ------------------------------------------------------------ datatypes
+int parsec_type_size(parsec_datatype_t type, int* size) {
+  *size = (int)type_of(type).packed_bytes();
+  return PARSEC_SUCCESS;
+}
+int parsec_type_extent(parsec_datatype_t type, ptrdiff_t* lb, ptrdiff_t* extent) {
+  if (lb) *lb = 0;
+  *extent = (ptrdiff_t)type_of(type).extent_bytes();
+  return PARSEC_SUCCESS;
+}
+int parsec_type_create_contiguous(int count, parsec_datatype_t oldtype, parsec_datatype_t* newtype) {
+  Datatype o = type_of(oldtype);
+  *newtype = new_type(Datatype::contiguous(o.elem_size, (int64_t)count * std::max<int64_t>(o.count, 1)));
+  return PARSEC_SUCCESS;
+}
+int parsec_type_create_vector(int count, int blocklength, int stride, parsec_datatype_t oldtype, parsec_datatype_t* newtype) {
+  Datatype o = type_of(oldtype);
+  *newtype = new_type(Datatype::vector(o.elem_size, count, blocklength, stride));
+  return PARSEC_SUCCESS;
+}
+int parsec_type_create_lower(int n, int ld, int diag, parsec_datatype_t oldtype, parsec_datatype_t* newtype) {
+  *newtype = new_type(Datatype::lower(type_of(oldtype).elem_size, n, ld, diag != 0));
+  return PARSEC_SUCCESS;
+}
+int parsec_type_create_upper(int n, int ld, int diag, parsec_datatype_t oldtype, parsec_datatype_t* newtype) {
+  *newtype = new_type(Datatype::upper(type_of(oldtype).elem_size, n, ld, diag != 0));
+  return PARSEC_SUCCESS;
+}
+int parsec_type_free(parsec_datatype_t* type) {
+  *type = PARSEC_DATATYPE_NULL;
+  return PARSEC_SUCCESS;
+}
+
+// -------------------------------------------------------------- context
+parsec_context_t* parsec_init(int nb_cores, int* pargc, char** pargv[]) {
+  std::vector<std::string> args;
+  if (pargc && pargv && *pargv)
+    for (int i = 1; i < *pargc; ++i) args.push_back((*pargv)[i]);
+  // multi-process launch (tools/parsec_run.py or torchrun-style environment)
+  const char* r = getenv("PARSEC_COMM_RANK");
+  const char* s = getenv("PARSEC_COMM_SIZE");
+  if (!r) r = getenv("RANK");
+  if (!s) s = getenv("WORLD_SIZE");
+  if (r && s && atoi(s) > 1 && comm_size() <= 1) {
+    const char* job = getenv("PARSEC_COMM_JOB");
+    std::string j = job ? job : (getenv("MASTER_PORT") ? getenv("MASTER_PORT") : "capi");
+    const char* g = getenv("PARSEC_COMM_GPU");
+    comm_init(atoi(r), atoi(s), j, g ? atoi(g) : -1);
+  }
+  Context* ctx = context_init(nb_cores, args);
+  if (pargc && pargv && *pargv) {  // hand back the arguments the runtime did not consume
+    int n = 1;
+    for (auto& a : args)
+      for (int i = 1; i < *pargc; ++i)
+        if (a == (*pargv)[i]) { (*pargv)[n++] = (*pargv)[i]; break; }
+    *pargc = n;
+  }
+  return ctx;
+}
+int parsec_fini(parsec_context_t** pcontext) {
+  int rc = context_fini(pcontext);
+  if (comm_size() > 1) comm_fini();
+  return rc;
+}
+void parsec_abort(parsec_context_t* context, int status) { context_abort(context, status); }
+int parsec_context_add_taskpool(parsec_context_t* context, parsec_taskpool_t* tp) { return context_add_taskpool(context, tp); }
+int parsec_context_start(parsec_context_t* context) { return context_start(context); }
+int parsec_context_test(parsec_context_t* context) { return context_test(context); }
+int parsec_context_wait(parsec_context_t* context) { return context_wait(context); }
+int parsec_context_rank(const parsec_context_t* context) { return context->my_rank; }
+int parsec_context_nb_nodes(const parsec_context_t* context) { return context->nb_nodes; }
+int parsec_context_nb_cores(const parsec_context_t* context) { return context->nb_cores; }
+int parsec_comm_barrier(void) { return comm_size() > 1 ? comm_barrier() : 0; }
+
+// ------------------------------------------------------------- taskpool
+int parsec_taskpool_set_complete_callback(parsec_taskpool_t* tp, parsec_event_cb_t cb, void* cb_data) {
+  tp->on_complete = [cb, cb_data](Taskpool* t) { return cb(t, cb_data); };
+  return PARSEC_SUCCESS;
+}
+int parsec_taskpool_set_enqueue_callback(parsec_taskpool_t* tp, parsec_event_cb_t cb, void* cb_data) {
+  tp->on_enqueue = [cb, cb_data](Taskpool* t) { return cb(t, cb_data); };
+  return PARSEC_SUCCESS;
+}
+int32_t parsec_taskpool_set_priority(parsec_taskpool_t* tp, int32_t p) { return taskpool_set_priority(tp, p); }
+int parsec_taskpool_wait(parsec_taskpool_t* tp) {
+  if (auto* d = dynamic_cast<dtd::DtdTaskpool*>(tp)) return d->wait();
+  Context* ctx = tp->context;
+  if (!ctx) return PARSEC_ERROR;
+  if (!ctx->started.load()) context_start(ctx);
+  ExecutionStream* prev = my_execution_stream();
+  ExecutionStream* es = prev && prev->ctx == ctx ? prev : ctx->all_es[0];
+  set_my_execution_stream(es);
+  Backoff b;
+  while (!tp->completed.load()) {
+    Task* t = es->next_task;
+    int32_t dist = 0;
+    if (t) es->next_task = nullptr;
+    else t = ctx->scheduler->select(es, &dist);
+    if (t) { b.reset(); task_progress(es, t, dist); }
+    else b.idle();
+  }
+  set_my_execution_stream(prev);
+  return PARSEC_SUCCESS;
+}
+void parsec_taskpool_free(parsec_taskpool_t* tp) { taskpool_free(tp); }
+uint32_t parsec_taskpool_id(const parsec_taskpool_t* tp) { return tp->taskpool_id; }
+parsec_taskpool_t* parsec_taskpool_lookup(uint32_t id) { return taskpool_lookup(id); }
+parsec_taskpool_t* parsec_compose(parsec_taskpool_t* start, parsec_taskpool_t* next) { return compose(start, next); }
+void parsec_taskpool_set_devices_mask(parsec_taskpool_t* tp, uint32_t mask) { tp->devices_index_mask = mask; }
+
+int parsec_task_nb_locals(const parsec_task_t* task) { return task->task_class->nb_locals; }
+int32_t parsec_task_local(const parsec_task_t* task, int i) { return task->locals[i]; }
+const char* parsec_task_class_name(const parsec_task_t* task) { return task->task_class->name.c_str(); }
+parsec_taskpool_t* parsec_task_taskpool(const parsec_task_t* task) { return task->taskpool; }
+int parsec_execution_stream_id(const parsec_execution_stream_t* es) { return es->th_id; }
+
+// ------------------------------------------------------------ MCA params
+int parsec_mca_param_set_string(const char* name, const char* value) {
+  ParamRegistry::instance().set_override(name, value);
+  return PARSEC_SUCCESS;
+}
+int parsec_mca_param_set_int(const char* name, int64_t value) {
+  ParamRegistry::instance().set_override(name, std::to_string(value));
+  return PARSEC_SUCCESS;
+}
+int parsec_mca_param_get_int(const char* name, int64_t* value) {
+  std::string v;
+  if (!ParamRegistry::instance().lookup(name, v)) return PARSEC_ERR_NOT_FOUND;
+  *value = strtoll(v.c_str(), nullptr, 0);
+  return PARSEC_SUCCESS;
+}
+
+// ------------------------------------------------------ data collections
+void parsec_data_collection_init(parsec_data_collection_t* dc, int nodes, int myrank) {
+  std::memset(dc, 0, sizeof(*dc));
+  dc->nodes = (uint32_t)nodes;
+  dc->myrank = (uint32_t)myrank;
+  dc->nb_indices = 2;
+  auto* impl = new CCollection();
+  impl->c = dc;
+  impl->nodes = (uint32_t)nodes;
+  impl->myrank = (uint32_t)myrank;
+  dc->impl = impl;
+}
+void parsec_data_collection_destroy(parsec_data_collection_t* dc) {
+  if (dc->impl) delete static_cast<DataCollection*>(dc->impl);
+  dc->impl = nullptr;
+  free(dc->key_base);
+  dc->key_base = nullptr;
+}
+void parsec_data_collection_set_key(parsec_data_collection_t* dc, const char* name) {
+  free(dc->key_base);
+  dc->key_base = strdup(name);
+  impl_of(dc)->key_base = name;
+}
+parsec_data_t* parsec_data_create(parsec_data_t** holder, parsec_data_collection_t* desc, parsec_data_key_t key, void* ptr, size_t size) {
+  return data_create(holder, impl_of(desc), key, ptr, size);
+}
+void parsec_data_destroy(parsec_data_t* data) { data_destroy(data); }
+parsec_data_copy_t* parsec_data_get_copy(parsec_data_t* data, int device) { return data ? data->copy(device) : nullptr; }
+void* parsec_data_copy_get_ptr(parsec_data_copy_t* copy) { return copy ? copy->device_private : nullptr; }
+void* parsec_data_get_ptr(parsec_data_t* data, int device) {
+  DataCopy* c = data ? data->copy(device) : nullptr;
+  return c ? c->device_private : nullptr;
+}
+void* parsec_data_pull_to_host(parsec_data_t* data) {
+  DataCopy* c = data_pull_to_host(data);
+  return c ? c->device_private : nullptr;
+}
+void* parsec_data_allocate(size_t size) {
+  void* p = nullptr;
+  if (posix_memalign(&p, 4096, size ? size : 1)) return nullptr;
+  return p;
+}
+void parsec_data_free(void* ptr) { free(ptr); }
+
+// --------------------------------------------------------- tiled matrices
+size_t parsec_matrix_type_size(parsec_matrix_type_t mtype) { return matrix_type_size((int)mtype); }
+
+void parsec_matrix_block_cyclic_init(parsec_matrix_block_cyclic_t* dc, parsec_matrix_type_t mtype, parsec_matrix_storage_t storage, int myrank, int mb, int nb, int lm, int ln,
+                                     int i, int j, int m, int n, int p, int q, int kp, int kq, int ip, int jq) {
+  std::memset(dc, 0, sizeof(*dc));
+  auto* bc = new CBlockCyclic();
+  bc->c = dc;
+  bc->init((int)mtype, myrank, mb, nb, lm, ln, i, j, m, n, p, q, kp, kq, ip, jq);
+  parsec_data_collection_t* d = &dc->super.super;
+  d->myrank = bc->myrank;
+  d->nodes = bc->nodes;
+  d->rank_of = bc_rank_of;
+  d->vpid_of = bc_vpid_of;
+  d->data_of = bc_data_of;
+  d->data_key = bc_data_key;
+  d->rank_of_key = bc_rank_of_key;
+  d->vpid_of_key = bc_vpid_of_key;
+  d->data_of_key = bc_data_of_key;
+  d->nb_indices = 2;
+  d->impl = static_cast<DataCollection*>(bc);
+  parsec_tiled_matrix_t* t = &dc->super;
+  t->mtype = mtype;
+  t->storage = storage;
+  t->mb = mb; t->nb = nb; t->bsiz = (int)bc->bsiz;
+  t->lm = lm; t->ln = ln; t->lmt = (int)bc->lmt; t->lnt = (int)bc->lnt;
+  t->i = i; t->j = j; t->m = (int)bc->m; t->n = (int)bc->n; t->mt = (int)bc->mt; t->nt = (int)bc->nt;
+  t->llm = (int)(bc->llm_tiles * mb); t->lln = (int)(bc->lln_tiles * nb);
+  t->nb_local_tiles = (int)bc->nb_local_tiles;
+  dc->grid.rank = myrank;
+  dc->grid.rows = p; dc->grid.cols = q;
+  dc->grid.krows = kp; dc->grid.kcols = kq;
+  dc->grid.ip = ip; dc->grid.jq = jq;
+  dc->grid.rrank = q > 0 ? myrank / q : 0;
+  dc->grid.crank = q > 0 ? myrank % q : 0;
+}
+void parsec_tiled_matrix_destroy(parsec_tiled_matrix_t* tdesc) { parsec_data_collection_destroy(&tdesc->super); }
+parsec_data_key_t parsec_tiled_matrix_data_key(parsec_tiled_matrix_t* tdesc, int m, int n) {
+  int64_t idx[2] = {m, n};
+  return impl_of(&tdesc->super)->data_key(idx, 2);
+}
+int parsec_tiled_matrix_set_storage_device(parsec_tiled_matrix_t* tdesc, int device_index) {
+  auto* tm = dynamic_cast<TiledMatrix*>(impl_of(&tdesc->super));
+  if (!tm || tm->mat) return PARSEC_ERROR;
+  tm->storage_device = device_index;
+  tm->allocate_storage(nullptr);
+  return PARSEC_SUCCESS;
+}
+
+// --------------------------------------------------------------- arenas
+int parsec_arena_datatype_construct(parsec_arena_datatype_t* adt, size_t elem_size, size_t alignment, parsec_datatype_t opaque_dtt) {
+  Datatype d = opaque_dtt == PARSEC_DATATYPE_NULL ? Datatype::contiguous(1, (int64_t)elem_size) : type_of(opaque_dtt);
+  adt->opaque_dtt = d;
+  adt->arena = std::make_shared<Arena>(std::max<size_t>(elem_size, 1), alignment ? alignment : 64, d);
+  return PARSEC_SUCCESS;
+}
+parsec_arena_datatype_t* parsec_arena_datatype_new(size_t elem_size, size_t alignment, parsec_datatype_t opaque_dtt) {
+  auto* a = new ArenaDatatype();
+  parsec_arena_datatype_construct(a, elem_size, alignment, opaque_dtt);
+  return a;
+}
+void parsec_arena_datatype_free(parsec_arena_datatype_t* adt) { delete adt; }
+int parsec_add2arena_rect(parsec_arena_datatype_t* adt, parsec_datatype_t oldtype, int tile_mb, int tile_nb, int resized) {
+  (void)resized;
+  add2arena_rect(*adt, type_of(oldtype).elem_size, tile_mb, tile_nb, tile_mb);
+  return PARSEC_SUCCESS;
+}
+int parsec_add2arena(parsec_arena_datatype_t* adt, parsec_datatype_t oldtype, parsec_matrix_uplo_t uplo, int diag, int m, int n, int ld, size_t alignment, int resized) {
+  (void)resized;
+  const uint32_t esz = type_of(oldtype).elem_size;
+  Datatype d;
+  if (uplo == PARSEC_MATRIX_LOWER) d = Datatype::lower(esz, m, ld, diag != 0);
+  else if (uplo == PARSEC_MATRIX_UPPER) d = Datatype::upper(esz, m, ld, diag != 0);
+  else d = ld == m ? Datatype::contiguous(esz, (int64_t)m * n) : Datatype::vector(esz, n, m, ld);
+  add2arena(*adt, d, alignment ? alignment : 64);
+  // the arena element is always the full m x ld tile so NEW copies can hold any layout
+  adt->arena = std::make_shared<Arena>((size_t)ld * n * esz, alignment ? alignment : 64, d);
+  return PARSEC_SUCCESS;
+}
+void parsec_del2arena(parsec_arena_datatype_t* adt) { adt->arena.reset(); }
+int parsec_taskpool_set_arena_datatype(parsec_taskpool_t* tp, int idx, size_t elem_size, size_t alignment, parsec_datatype_t opaque_dtt) {
+  if (idx < 0) return PARSEC_ERROR;
+  if ((int)tp->arenas_datatypes.size() <= idx) tp->arenas_datatypes.resize(idx + 1);
+  return parsec_arena_datatype_construct(&tp->arenas_datatypes[idx], elem_size, alignment, opaque_dtt);
+}
+
+// ------------------------------------------------------------------ DTD
+parsec_taskpool_t* parsec_dtd_taskpool_new(void) {
+  auto* tp = new dtd::DtdTaskpool();
+  g_last_dtd.store(tp);
+  tp->destructor_hook = [tp] {
+    dtd::DtdTaskpool* e = tp;
+    g_last_dtd.compare_exchange_strong(e, nullptr);
+    std::lock_guard<std::mutex> g(g_dtd_m);
+    for (auto it = g_dtd_classes.begin(); it != g_dtd_classes.end();) it = it->first.first == tp ? g_dtd_classes.erase(it) : std::next(it);
+  };
+  return tp;
+}
+int parsec_dtd_taskpool_wait(parsec_taskpool_t* tp) { return as_dtd(tp)->wait(); }
+void parsec_dtd_set_window(parsec_taskpool_t* tp, int64_t window, int64_t threshold) {
+  auto* d = as_dtd(tp);
+  d->window = window;
+  d->threshold = threshold;
+}
+
+void parsec_dtd_insert_task(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, int priority, int device_type, const char* name, ...) {
+  auto* d = as_dtd(tp);
+  PendingArgs pa;
+  va_list ap;
+  va_start(ap, name);
+  parse_args(ap, pa);
+  va_end(ap);
+  char key[64];
+  snprintf(key, sizeof key, "@%p", (void*)fpointer);
+  std::string cname = std::string(name ? name : "dtd_task") + key;
+  dtd::DtdTaskClass* tc;
+  {
+    std::lock_guard<std::mutex> g(g_dtd_m);
+    auto it = g_dtd_classes.find({d, cname});
+    if (it == g_dtd_classes.end()) {
+      tc = d->create_task_class(cname, pa.sig);
+      tc->name = name ? name : "dtd_task";
+      if (device_type & PARSEC_DEV_HIP) {
+        auto* gfn = reinterpret_cast<parsec_dtd_gpu_funcptr_t*>(fpointer);
+        d->add_chore(tc, DEV_HIP, nullptr, [gfn](GpuExecContext* c, Task* t) {
+          t_gpu_ctx = c;
+          int rc = gfn((void*)c->stream, t);
+          t_gpu_ctx = nullptr;
+          return rc;
+        });
+      }
+      if ((device_type & PARSEC_DEV_CPU) || device_type == 0 || !(device_type & PARSEC_DEV_HIP))
+        d->add_chore(tc, DEV_CPU, [fpointer](ExecutionStream* es, Task* t) { return fpointer(es, t); }, nullptr);
+      g_dtd_classes[{d, cname}] = tc;
+    } else {
+      tc = it->second;
+    }
+  }
+  d->insert_task(tc, priority, pa.args);
+}
+
+parsec_dtd_task_class_t* parsec_dtd_create_task_class(parsec_taskpool_t* tp, const char* name, ...) {
+  auto* d = as_dtd(tp);
+  std::vector<std::pair<int, int>> sig;
+  va_list ap;
+  va_start(ap, name);
+  for (;;) {
+    int size = va_arg(ap, int);
+    if (size == PARSEC_DTD_ARG_END) break;
+    int flags = va_arg(ap, int);
+    sig.push_back({flags, size});
+  }
+  va_end(ap);
+  return reinterpret_cast<parsec_dtd_task_class_t*>(d->create_task_class(name, sig));
+}
+int parsec_dtd_task_class_add_chore(parsec_taskpool_t* tp, parsec_dtd_task_class_t* tcp, int device_type, void* function) {
+  auto* d = as_dtd(tp);
+  auto* tc = reinterpret_cast<dtd::DtdTaskClass*>(tcp);
+  if (device_type == PARSEC_DEV_HIP) {
+    auto* gfn = reinterpret_cast<parsec_dtd_gpu_funcptr_t*>(function);
+    return d->add_chore(tc, DEV_HIP, nullptr, [gfn](GpuExecContext* c, Task* t) {
+      t_gpu_ctx = c;
+      int rc = gfn((void*)c->stream, t);
+      t_gpu_ctx = nullptr;
+      return rc;
+    });
+  }
+  auto* fn = reinterpret_cast<parsec_dtd_funcptr_t*>(function);
+  return d->add_chore(tc, (uint32_t)device_type, [fn](ExecutionStream* es, Task* t) { return fn(es, t); }, nullptr);
+}
+void parsec_dtd_insert_task_with_task_class(parsec_taskpool_t* tp, parsec_dtd_task_class_t* tcp, int priority, int device_type, ...) {
+  (void)device_type;
+  auto* d = as_dtd(tp);
+  PendingArgs pa;
+  va_list ap;
+  va_start(ap, device_type);
+  parse_args(ap, pa);
+  va_end(ap);
+  d->insert_task(reinterpret_cast<dtd::DtdTaskClass*>(tcp), priority, pa.args);
+}
+parsec_dtd_tile_t* parsec_dtd_tile_of(parsec_data_collection_t* dc, parsec_data_key_t key) {
+  // tiles are per-taskpool in the runtime; the C API keeps the reference's
+  // collection-scoped call by resolving against the most recent DTD taskpool
+  DataCollection* impl = impl_of(dc);
+  dtd::DtdTaskpool* tp = g_last_dtd.load();
+  if (!tp) fatal("parsec_dtd_tile_of: no DTD taskpool is active (add one to a context first)");
+  return reinterpret_cast<parsec_dtd_tile_t*>(tp->tile_of(impl, key));
+}
+parsec_dtd_tile_t* parsec_dtd_tile_new(parsec_taskpool_t* tp, int rank, size_t size) {
+  return reinterpret_cast<parsec_dtd_tile_t*>(as_dtd(tp)->tile_new(size, rank));
+}
+void parsec_dtd_data_collection_init(parsec_data_collection_t* dc) { (void)dc; }
+void parsec_dtd_data_collection_fini(parsec_data_collection_t* dc) { (void)dc; }
+int parsec_dtd_data_flush(parsec_taskpool_t* tp, parsec_dtd_tile_t* tile) { return as_dtd(tp)->data_flush(reinterpret_cast<dtd::Tile*>(tile)); }
+int parsec_dtd_data_flush_all(parsec_taskpool_t* tp, parsec_data_collection_t* dc) { return as_dtd(tp)->data_flush_all(impl_of(dc)); }
+
+void parsec_dtd_unpack_args(parsec_task_t* this_task, ...) {
+  va_list ap;
+  va_start(ap, this_task);
+  const int n = dtd::task_nb_args(this_task);
+  const auto* tc = static_cast<const dtd::DtdTaskClass*>(this_task->task_class);
+  for (int i = 0; i < n; ++i) {
+    void* out = va_arg(ap, void*);
+    const int op = tc->param_ops[i] & dtd::OP_MASK;
+    void* p = dtd::task_arg(this_task, i);
+    if (op == dtd::VALUE) std::memcpy(out, p, (size_t)tc->param_sizes[i]);
+    else *static_cast<void**>(out) = p;
+  }
+  va_end(ap);
+}
+void* parsec_dtd_get_dev_ptr(parsec_task_t* this_task, int i) {
+  const int f = dtd::task_arg_flow(this_task, i);
+  if (f < 0) return nullptr;
+  if (t_gpu_ctx) return t_gpu_ctx->ptr(f);
+  return dtd::task_arg(this_task, i);
+}
+
+// ------------------------------------------------------------ profiling
+int parsec_profiling_init(const char* basename) {
+  ParamRegistry::instance().set_override("profile_filename", basename ? basename : "parsec");
+  return PARSEC_SUCCESS;
+}
+int parsec_profiling_fini(void) { return PARSEC_SUCCESS; }
+int parsec_profiling_add_dictionary_keyword(const char* name, const char* attributes, size_t info_length, const char* convertor_code, int* key_start, int* key_end) {
+  return profiling_add_dictionary_keyword(name, attributes ? attributes : "", info_length, convertor_code ? convertor_code : "", key_start, key_end);
+}
+int parsec_profiling_trace(int key, uint64_t event_id, uint32_t taskpool_id, const void* info) {
+  if (!t_prof) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "user thread %zu", std::hash<std::thread::id>()(std::this_thread::get_id()) % 100000);
+    t_prof = profiling_stream_create(nm);
+  }
+  return profiling_trace(t_prof, key, event_id, taskpool_id, info, 0);
+}
+int parsec_profiling_dump(void) {
+  std::string f;
+  ParamRegistry::instance().lookup("profile_filename", f);
+  return profiling_dump(f.empty() ? "parsec" : f);
+}
+
+}  // extern "C"

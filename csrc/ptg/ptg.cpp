@@ -47,6 +47,14 @@ void for_each_task(const Taskpool* tp, const PtgTaskClass* tc, const std::functi
   std::function<void(size_t)> rec = [&](size_t i) {
     if (i == locals.size()) { f(L); return; }
     const LocalDef& ld = locals[i];
+    if (ld.has_index) {
+      for_range(ev(ld.lo, tp, L), ev(ld.hi, tp, L), ev(ld.step, tp, L, 1), [&](int64_t ix) {
+        L[ld.index_slot] = (int32_t)ix;
+        L[i] = (int32_t)ev(ld.value, tp, L);
+        rec(i + 1);
+      });
+      return;
+    }
     if (!ld.is_range) {
       L[i] = (int32_t)ev(ld.value, tp, L);
       rec(i + 1);
@@ -60,11 +68,51 @@ void for_each_task(const Taskpool* tp, const PtgTaskClass* tc, const std::functi
   rec(0);
 }
 
+static void expand_iters(const Taskpool* tp, int32_t* X, const std::vector<IterDef>& its, size_t i, const std::function<void()>& f) {
+  if (i == its.size()) { f(); return; }
+  const IterDef& it = its[i];
+  for_range(ev(it.lo, tp, X), ev(it.hi, tp, X), ev(it.step, tp, X, 1), [&](int64_t v) {
+    X[it.slot] = (int32_t)v;
+    expand_iters(tp, X, its, i + 1, f);
+  });
+}
+
+void for_each_dep_instance(const Taskpool* tp, const int32_t* L, const Dep& d, const std::function<void(const int32_t*, const DepTarget*)>& f) {
+  auto pick = [&](const int32_t* X) -> const DepTarget* {
+    if (!d.guard || d.guard(tp, X)) return &d.then_t;
+    return d.has_else ? &d.else_t : nullptr;
+  };
+  if (d.iters.empty() && d.then_t.iters.empty() && d.else_t.iters.empty()) {
+    if (const DepTarget* tg = pick(L)) f(L, tg);
+    return;
+  }
+  int32_t X[kMaxLocals];
+  std::memcpy(X, L, sizeof(X));
+  expand_iters(tp, X, d.iters, 0, [&] {
+    const DepTarget* tg = pick(X);
+    if (!tg) return;
+    expand_iters(tp, X, tg->iters, 0, [&] { f(X, tg); });
+  });
+}
+
 bool PtgTaskClass::complete_locals(const Taskpool* tp, int32_t* L, const int32_t* params) const {
   const auto& locals = def.locals;
   for (size_t i = 0; i < locals.size(); ++i) {
     const LocalDef& ld = locals[i];
-    if (ld.is_param) {
+    if (ld.is_param && ld.has_index) {
+      const int32_t v = params[local_param[i]];
+      bool found = false;
+      for_range(ev(ld.lo, tp, L), ev(ld.hi, tp, L), ev(ld.step, tp, L, 1), [&](int64_t ix) {
+        if (found) return;
+        L[ld.index_slot] = (int32_t)ix;
+        if ((int32_t)ev(ld.value, tp, L) == v) found = true;
+      });
+      if (!found) return false;
+      L[i] = v;
+    } else if (ld.has_index) {
+      L[ld.index_slot] = (int32_t)ev(ld.lo, tp, L);
+      L[i] = (int32_t)ev(ld.value, tp, L);
+    } else if (ld.is_param) {
       int32_t v = params[local_param[i]];
       if (ld.is_range) {
         int64_t lo = ev(ld.lo, tp, L), hi = ev(ld.hi, tp, L), st = ev(ld.step, tp, L, 1);
@@ -96,29 +144,42 @@ int32_t PtgTaskClass::priority_of(const Taskpool* tp, const int32_t* L) const {
 
 uint64_t PtgTaskClass::make_key(const Taskpool* tp, const int32_t* L) const {
   if (def.make_key_fn) return def.make_key_fn(tp, L);
-  auto* ptp = static_cast<const PtgTaskpool*>(tp);
-  (void)ptp;
-  return TaskClass::make_key(tp, L);
+  // parameters are not necessarily the leading locals: hash them in header order
+  uint64_t k = 0;
+  for (int i = 0; i < nb_params; ++i) k = k * 0x9E3779B97F4A7C15ULL + (uint64_t)(uint32_t)L[param_local[i]] + 0x632BE59BD9B4E019ULL;
+  return (k & 0x00FFFFFFFFFFFFFFULL) | ((uint64_t)task_class_id << 56);
 }
 
 const DepTarget* PtgTaskClass::active_input(const Taskpool* tp, int flow, const int32_t* L) const {
   for (const Dep& d : def.flows[flow].in) {
+    if (!d.iters.empty() || !d.then_t.iters.empty()) continue;  // iterated inputs only make sense for CTL gathers
     if (!d.guard || d.guard(tp, L)) return &d.then_t;
     if (d.has_else) return &d.else_t;
   }
   return nullptr;
 }
 
+// Data flows: the first active input dependency. CTL flows: every active
+// instance of every input dependency (control gather, reference ctlgat.jdf).
+void PtgTaskClass::for_each_input(const Taskpool* tp, int flow, const int32_t* L, const std::function<void(const int32_t*, const DepTarget*)>& f) const {
+  if (def.flows[flow].access != FLOW_CTL) {
+    if (const DepTarget* t = active_input(tp, flow, L)) f(L, t);
+    return;
+  }
+  for (const Dep& d : def.flows[flow].in) for_each_dep_instance(tp, L, d, f);
+}
+
 int PtgTaskClass::count_task_inputs(const Taskpool* tp, const int32_t* L) const {
   int count = 0;
   for (size_t f = 0; f < def.flows.size(); ++f) {
-    const DepTarget* t = active_input(tp, (int)f, L);
-    if (!t || t->kind != DEP_TASK) continue;
-    const PtgTaskClass* src = owner->classes[t->tc_id];
-    int32_t params[kMaxLocals];
-    expand_args(tp, L, t->args, 0, params, [&](const int32_t* P) {
-      int32_t SL[kMaxLocals];
-      if (src->complete_locals(tp, SL, P)) ++count;
+    for_each_input(tp, (int)f, L, [&](const int32_t* X, const DepTarget* t) {
+      if (t->kind != DEP_TASK) return;
+      const PtgTaskClass* src = owner->classes[t->tc_id];
+      int32_t params[kMaxLocals];
+      expand_args(tp, X, t->args, 0, params, [&](const int32_t* P) {
+        int32_t SL[kMaxLocals];
+        if (src->complete_locals(tp, SL, P)) ++count;
+      });
     });
   }
   return count;
@@ -132,13 +193,11 @@ void PtgTaskClass::iterate_successors(ExecutionStream* es, const Task* t, uint32
   const Taskpool* tp = t->taskpool;
   for (size_t f = 0; f < def.flows.size(); ++f) {
     if (!(mask & (1u << f))) continue;
-    for (const Dep& d : def.flows[f].out) {
-      const DepTarget* tg = (!d.guard || d.guard(tp, t->locals)) ? &d.then_t : (d.has_else ? &d.else_t : nullptr);
-      if (!tg) continue;
+    for (const Dep& d : def.flows[f].out) for_each_dep_instance(tp, t->locals, d, [&](const int32_t* X, const DepTarget* tg) {
       if (tg->kind == DEP_TASK) {
         const PtgTaskClass* dst = owner->classes[tg->tc_id];
         int32_t params[kMaxLocals];
-        expand_args(tp, t->locals, tg->args, 0, params, [&](const int32_t* P) {
+        expand_args(tp, X, tg->args, 0, params, [&](const int32_t* P) {
           int32_t TL[kMaxLocals];
           if (!dst->complete_locals(tp, TL, P)) return;
           DepVisit vis;
@@ -154,12 +213,12 @@ void PtgTaskClass::iterate_successors(ExecutionStream* es, const Task* t, uint32
         vis.src_flow = (int)f;
         vis.dc = tg->dc(tp);
         int64_t idx[kMaxLocals];
-        collection_index(tp, t->locals, tg->args, idx);
+        collection_index(tp, X, tg->args, idx);
         vis.dc_key = vis.dc->data_key(idx, (int)tg->args.size());
         vis.rank = vis.dc->rank_of(idx, (int)tg->args.size());
         v(vis);
       }
-    }
+    });
   }
 }
 
@@ -168,18 +227,19 @@ void PtgTaskClass::iterate_predecessors(ExecutionStream* es, const Task* t, uint
   const Taskpool* tp = t->taskpool;
   for (size_t f = 0; f < def.flows.size(); ++f) {
     if (!(mask & (1u << f))) continue;
-    const DepTarget* tg = active_input(tp, (int)f, t->locals);
-    if (!tg || tg->kind != DEP_TASK) continue;
-    const PtgTaskClass* src = owner->classes[tg->tc_id];
-    int32_t params[kMaxLocals];
-    expand_args(tp, t->locals, tg->args, 0, params, [&](const int32_t* P) {
-      int32_t SL[kMaxLocals];
-      if (!src->complete_locals(tp, SL, P)) return;
-      DepVisit vis;
-      vis.tc = src; vis.locals = SL; vis.nb_locals = src->nb_locals;
-      vis.src_flow = (int)f; vis.dst_flow = tg->dst_flow;
-      vis.rank = src->rank_of(tp, SL);
-      v(vis);
+    for_each_input(tp, (int)f, t->locals, [&](const int32_t* X, const DepTarget* tg) {
+      if (tg->kind != DEP_TASK) return;
+      const PtgTaskClass* src = owner->classes[tg->tc_id];
+      int32_t params[kMaxLocals];
+      expand_args(tp, X, tg->args, 0, params, [&](const int32_t* P) {
+        int32_t SL[kMaxLocals];
+        if (!src->complete_locals(tp, SL, P)) return;
+        DepVisit vis;
+        vis.tc = src; vis.locals = SL; vis.nb_locals = src->nb_locals;
+        vis.src_flow = (int)f; vis.dst_flow = tg->dst_flow;
+        vis.rank = src->rank_of(tp, SL);
+        v(vis);
+      });
     });
   }
 }
@@ -190,14 +250,13 @@ uint32_t PtgTaskClass::gpu_pushout_mask(const Task* t, int device) const {
   uint32_t my = tp->context ? (uint32_t)tp->context->my_rank : 0;
   for (size_t f = 0; f < def.flows.size(); ++f) {
     if (!(def.flows[f].access & FLOW_WRITE)) continue;
-    for (const Dep& d : def.flows[f].out) {
-      const DepTarget* tg = (!d.guard || d.guard(tp, t->locals)) ? &d.then_t : (d.has_else ? &d.else_t : nullptr);
-      if (!tg || tg->kind != DEP_DATA) continue;
+    for (const Dep& d : def.flows[f].out) for_each_dep_instance(tp, t->locals, d, [&](const int32_t* X, const DepTarget* tg) {
+      if (tg->kind != DEP_DATA) return;
       DataCollection* dc = tg->dc(tp);
       int64_t idx[kMaxLocals];
-      collection_index(tp, t->locals, tg->args, idx);
+      collection_index(tp, X, tg->args, idx);
       if (dc->home_device() != device && dc->rank_of(idx, (int)tg->args.size()) == my) m |= 1u << f;
-    }
+    });
   }
   return m;
 }
@@ -275,13 +334,13 @@ int PtgTaskClass::complete_execution(ExecutionStream* es, Task* t) const {
     const FlowDef& fd = def.flows[f];
     if (fd.out.empty()) continue;
     DataCopy* data = fd.access == FLOW_CTL ? nullptr : (t->data[f].data_out ? t->data[f].data_out : t->data[f].data_in);
-    for (const Dep& d : fd.out) {
-      const DepTarget* tg = (!d.guard || d.guard(tp, t->locals)) ? &d.then_t : (d.has_else ? &d.else_t : nullptr);
-      if (!tg) continue;
+    for (const Dep& d : fd.out) for_each_dep_instance(tp, t->locals, d, [&](const int32_t* X, const DepTarget* tg) {
       if (tg->kind == DEP_TASK) {
         PtgTaskClass* dst = tp->classes[tg->tc_id];
+        if (!data && fd.access != FLOW_CTL && !warned_null_forward.exchange(true))
+          warning("%s: A NULL is forwarded on flow %s to %s", describe(t).c_str(), fd.name.c_str(), dst->name.c_str());
         int32_t params[kMaxLocals];
-        expand_args(tp, t->locals, tg->args, 0, params, [&](const int32_t* P) {
+        expand_args(tp, X, tg->args, 0, params, [&](const int32_t* P) {
           int32_t TL[kMaxLocals];
           if (!dst->complete_locals(tp, TL, P)) return;
           uint32_t r = dst->rank_of(tp, TL);
@@ -302,10 +361,10 @@ int PtgTaskClass::complete_execution(ExecutionStream* es, Task* t) const {
       } else if (tg->kind == DEP_DATA && data) {
         DataCollection* dc = tg->dc(tp);
         int64_t idx[kMaxLocals];
-        collection_index(tp, t->locals, tg->args, idx);
+        collection_index(tp, X, tg->args, idx);
         if (dc->rank_of(idx, (int)tg->args.size()) == my) write_back(dc->data_of(idx, (int)tg->args.size()), data);
       }
-    }
+    });
   }
   if (msg) {
     msg->taskpool_id = tp->taskpool_id;
@@ -453,6 +512,8 @@ void PtgTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
 
 void PtgTaskpool::activate(ExecutionStream* es, PtgTaskClass* tc, const int32_t* L, int flow, DataCopy* data, std::vector<Task*>& ready) {
   uint64_t key = tc->make_key(this, L);
+  PARSEC_DEBUG(kVerbNoisier, "ptg", "activate %s(%d,%d,%d,%d) flow %d key %llx", tc->name.c_str(), L[0], tc->nb_locals > 1 ? L[1] : 0, tc->nb_locals > 2 ? L[2] : 0,
+               tc->nb_locals > 3 ? L[3] : 0, flow, (unsigned long long)key);
   Task* done = pending.with(key, [&](auto& m) -> Task* {
     auto it = m.find(key);
     Task* task;
@@ -471,6 +532,7 @@ void PtgTaskpool::activate(ExecutionStream* es, PtgTaskClass* tc, const int32_t*
       data_copy_retain(data);
       task->data[flow].data_in = data;
     }
+    PARSEC_DEBUG(kVerbNoisier, "ptg", "  %s deps_remaining %d -> %d", tc->name.c_str(), task->deps_remaining, task->deps_remaining - 1);
     if (--task->deps_remaining <= 0) {
       m.erase(key);
       return task;
@@ -488,13 +550,11 @@ void PtgTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& ac
   for (size_t f = 0; f < tc->def.flows.size(); ++f) {
     if (!(act.output_mask & (1u << f))) continue;
     DataCopy* data = act.data[f];
-    for (const Dep& d : tc->def.flows[f].out) {
-      const DepTarget* tg = (!d.guard || d.guard(this, act.locals)) ? &d.then_t : (d.has_else ? &d.else_t : nullptr);
-      if (!tg) continue;
+    for (const Dep& d : tc->def.flows[f].out) for_each_dep_instance(this, act.locals, d, [&](const int32_t* X, const DepTarget* tg) {
       if (tg->kind == DEP_TASK) {
         PtgTaskClass* dst = classes[tg->tc_id];
         int32_t params[kMaxLocals];
-        expand_args(this, act.locals, tg->args, 0, params, [&](const int32_t* P) {
+        expand_args(this, X, tg->args, 0, params, [&](const int32_t* P) {
           int32_t TL[kMaxLocals];
           if (!dst->complete_locals(this, TL, P)) return;
           if (dst->rank_of(this, TL) == my) activate(es, dst, TL, tg->dst_flow, data, ready);
@@ -502,10 +562,10 @@ void PtgTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& ac
       } else if (tg->kind == DEP_DATA && data) {
         DataCollection* dc = tg->dc(this);
         int64_t idx[kMaxLocals];
-        collection_index(this, act.locals, tg->args, idx);
+        collection_index(this, X, tg->args, idx);
         if (dc->rank_of(idx, (int)tg->args.size()) == my) write_back(dc->data_of(idx, (int)tg->args.size()), data);
       }
-    }
+    });
   }
   if (!ready.empty()) schedule_tasks(es, ready.data(), (int)ready.size(), 1);
 }

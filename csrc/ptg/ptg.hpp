@@ -35,6 +35,20 @@ struct LocalDef {
   bool is_range = false;
   Expr value;           // !is_range
   Expr lo, hi, step;    // is_range (step null = 1)
+  // Index-mapped definition `x = [ i = lo .. hi .. step ] value`: the local takes
+  // value(i) for every i of the index range; `i` lives in locals[index_slot]
+  // (a scratch slot past the declared locals). Reference local_indices.jdf.
+  bool has_index = false;
+  int index_slot = -1;
+};
+
+// Dependency iterator `[ i = lo .. hi .. step ]` in front of a dependency: the
+// guard and the target arguments are evaluated once per iterator value, with
+// the value stored in locals[slot] (reference local_indices.jdf:26-33).
+struct IterDef {
+  std::string name;
+  Expr lo, hi, step;
+  int slot = -1;
 };
 
 enum DepKind : uint8_t { DEP_NULL = 0, DEP_TASK, DEP_DATA, DEP_NEW };
@@ -55,6 +69,7 @@ struct DepTarget {
   std::function<DataCollection*(const Taskpool*)> dc;  // DEP_DATA
   int datatype_index = 0;     // arena / datatype slot (NEW, remote layout)
   Expr displ_remote, count_remote;
+  std::vector<IterDef> iters;  // iterators local to this branch (`? [ j = .. ] T(..) : ..`)
 };
 
 struct Dep {
@@ -62,6 +77,7 @@ struct Dep {
   DepTarget then_t;
   bool has_else = false;
   DepTarget else_t;
+  std::vector<IterDef> iters;  // optional dependency iterators (outermost first)
 };
 
 struct FlowDef {
@@ -118,7 +134,13 @@ class PtgTaskClass : public TaskClass {
   int32_t priority_of(const Taskpool* tp, const int32_t* L) const;
   int count_task_inputs(const Taskpool* tp, const int32_t* L) const;
   const DepTarget* active_input(const Taskpool* tp, int flow, const int32_t* L) const;
+  // Every active input instance of `flow` (one for data flows, all for CTL gathers).
+  void for_each_input(const Taskpool* tp, int flow, const int32_t* L, const std::function<void(const int32_t* Lx, const DepTarget*)>& f) const;
+  mutable std::atomic<bool> warned_null_forward{false};
 };
+
+// Call f(Lx, target) for every active instance of `d` (expanding iterators).
+void for_each_dep_instance(const Taskpool* tp, const int32_t* L, const Dep& d, const std::function<void(const int32_t* Lx, const DepTarget*)>& f);
 
 class PtgTaskpool : public Taskpool {
  public:

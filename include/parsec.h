@@ -1,0 +1,281 @@
+/*
+ * parsec_amd public C API.
+ *
+ * The runtime API a PaRSEC application programs against: context lifecycle,
+ * taskpools (PTG taskpools come from parsec-ptgpp generated code, DTD taskpools
+ * from parsec_dtd_taskpool_new), data collections with user callbacks, tiled
+ * block-cyclic matrices, arenas / datatypes and the DTD insertion interface.
+ * Parity: reference parsec/runtime.h:155-628 (context / taskpool API and hook
+ * return codes :139-147), include/parsec/data_distribution.h (collection
+ * vtable), data_dist/matrix/two_dim_rectangle_cyclic.h:73-83, arena.h:49-125,
+ * interfaces/dtd/insert_function.h (DTD surface, Appendix B of SURVEY.md).
+ *
+ * Handles are opaque in C. In C++ they alias the runtime classes
+ * (parsec::Context, parsec::Taskpool, ...), so a generated
+ * parsec_<name>_taskpool_t* converts to parsec_taskpool_t* implicitly.
+ */
+#ifndef PARSEC_AMD_PARSEC_H
+#define PARSEC_AMD_PARSEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#define PARSEC_VERSION_MAJOR 4
+#define PARSEC_VERSION_MINOR 0
+
+/* hook return codes (reference runtime.h:139-147) */
+#define PARSEC_HOOK_RETURN_DONE 0
+#define PARSEC_HOOK_RETURN_AGAIN (-1)
+#define PARSEC_HOOK_RETURN_NEXT (-2)
+#define PARSEC_HOOK_RETURN_DISABLE (-3)
+#define PARSEC_HOOK_RETURN_ASYNC (-4)
+#define PARSEC_HOOK_RETURN_ERROR (-5)
+
+#define PARSEC_SUCCESS 0
+#define PARSEC_ERROR (-1)
+#define PARSEC_ERR_NOT_FOUND (-13)
+
+/* device types (reference mca/device/device.h) */
+#define PARSEC_DEV_NONE 0x00
+#define PARSEC_DEV_CPU 0x01
+#define PARSEC_DEV_RECURSIVE 0x02
+#define PARSEC_DEV_HIP 0x40
+#define PARSEC_DEV_ALL 0xff
+
+#ifdef __cplusplus
+namespace parsec {
+struct Context;
+struct Taskpool;
+struct Task;
+struct ExecutionStream;
+struct Data;
+struct DataCopy;
+struct ArenaDatatype;
+}  // namespace parsec
+typedef parsec::Context parsec_context_t;
+typedef parsec::Taskpool parsec_taskpool_t;
+typedef parsec::Task parsec_task_t;
+typedef parsec::ExecutionStream parsec_execution_stream_t;
+typedef parsec::Data parsec_data_t;
+typedef parsec::DataCopy parsec_data_copy_t;
+typedef parsec::ArenaDatatype parsec_arena_datatype_t;
+extern "C" {
+#else
+typedef struct parsec_context_s parsec_context_t;
+typedef struct parsec_taskpool_s parsec_taskpool_t;
+typedef struct parsec_task_s parsec_task_t;
+typedef struct parsec_execution_stream_s parsec_execution_stream_t;
+typedef struct parsec_data_s parsec_data_t;
+typedef struct parsec_data_copy_s parsec_data_copy_t;
+typedef struct parsec_arena_datatype_s parsec_arena_datatype_t;
+#endif
+
+typedef uint64_t parsec_data_key_t;
+
+/* ------------------------------------------------------------ datatypes */
+/* Datatypes are integer handles: the predefined element types below, or
+ * derived layouts created with parsec_type_create_* (reference datatype.h). */
+typedef int parsec_datatype_t;
+#define parsec_datatype_null_t 0
+#define parsec_datatype_int8_t 1
+#define parsec_datatype_int16_t 2
+#define parsec_datatype_int32_t 3
+#define parsec_datatype_int64_t 4
+#define parsec_datatype_float_t 5
+#define parsec_datatype_double_t 6
+#define parsec_datatype_complex_t 7
+#define parsec_datatype_double_complex_t 8
+#define parsec_datatype_uint8_t 9
+#define parsec_datatype_int_t parsec_datatype_int32_t
+#define parsec_datatype_long_t parsec_datatype_int64_t
+#define parsec_datatype_byte_t parsec_datatype_uint8_t
+#define PARSEC_DATATYPE_NULL parsec_datatype_null_t
+
+int parsec_type_size(parsec_datatype_t type, int* size);
+int parsec_type_extent(parsec_datatype_t type, ptrdiff_t* lb, ptrdiff_t* extent);
+int parsec_type_create_contiguous(int count, parsec_datatype_t oldtype, parsec_datatype_t* newtype);
+int parsec_type_create_vector(int count, int blocklength, int stride, parsec_datatype_t oldtype, parsec_datatype_t* newtype);
+int parsec_type_create_lower(int n, int ld, int diag, parsec_datatype_t oldtype, parsec_datatype_t* newtype);
+int parsec_type_create_upper(int n, int ld, int diag, parsec_datatype_t oldtype, parsec_datatype_t* newtype);
+int parsec_type_free(parsec_datatype_t* type);
+
+/* --------------------------------------------------------------- context */
+parsec_context_t* parsec_init(int nb_cores, int* pargc, char** pargv[]);
+int parsec_fini(parsec_context_t** pcontext);
+void parsec_abort(parsec_context_t* context, int status);
+int parsec_context_add_taskpool(parsec_context_t* context, parsec_taskpool_t* tp);
+int parsec_context_start(parsec_context_t* context);
+int parsec_context_test(parsec_context_t* context);
+int parsec_context_wait(parsec_context_t* context);
+int parsec_context_rank(const parsec_context_t* context);
+int parsec_context_nb_nodes(const parsec_context_t* context);
+int parsec_context_nb_cores(const parsec_context_t* context);
+int parsec_comm_barrier(void);
+
+/* -------------------------------------------------------------- taskpool */
+typedef int (*parsec_event_cb_t)(parsec_taskpool_t* tp, void* cb_data);
+int parsec_taskpool_set_complete_callback(parsec_taskpool_t* tp, parsec_event_cb_t cb, void* cb_data);
+int parsec_taskpool_set_enqueue_callback(parsec_taskpool_t* tp, parsec_event_cb_t cb, void* cb_data);
+int32_t parsec_taskpool_set_priority(parsec_taskpool_t* tp, int32_t new_priority);
+int parsec_taskpool_wait(parsec_taskpool_t* tp);
+void parsec_taskpool_free(parsec_taskpool_t* tp);
+uint32_t parsec_taskpool_id(const parsec_taskpool_t* tp);
+parsec_taskpool_t* parsec_taskpool_lookup(uint32_t taskpool_id);
+parsec_taskpool_t* parsec_compose(parsec_taskpool_t* start, parsec_taskpool_t* next);
+/* restrict the devices a taskpool may use (bit i = device index i) */
+void parsec_taskpool_set_devices_mask(parsec_taskpool_t* tp, uint32_t mask);
+
+/* task inspection (inside bodies) */
+int parsec_task_nb_locals(const parsec_task_t* task);
+int32_t parsec_task_local(const parsec_task_t* task, int i);
+const char* parsec_task_class_name(const parsec_task_t* task);
+parsec_taskpool_t* parsec_task_taskpool(const parsec_task_t* task);
+int parsec_execution_stream_id(const parsec_execution_stream_t* es);
+
+/* --------------------------------------------------------- MCA params */
+int parsec_mca_param_set_string(const char* name, const char* value);
+int parsec_mca_param_set_int(const char* name, int64_t value);
+int parsec_mca_param_get_int(const char* name, int64_t* value);
+
+/* ---------------------------------------------------- data collections */
+typedef struct parsec_data_collection_s parsec_data_collection_t;
+/* user callbacks take the collection followed by the indices as ints; the
+ * runtime passes `nb_indices` of them (reference data_distribution.h:26-66) */
+struct parsec_data_collection_s {
+  uint32_t myrank;
+  uint32_t nodes;
+  uint32_t (*rank_of)(parsec_data_collection_t* dc, ...);
+  int32_t (*vpid_of)(parsec_data_collection_t* dc, ...);
+  parsec_data_t* (*data_of)(parsec_data_collection_t* dc, ...);
+  parsec_data_key_t (*data_key)(parsec_data_collection_t* dc, ...);
+  uint32_t (*rank_of_key)(parsec_data_collection_t* dc, parsec_data_key_t key);
+  int32_t (*vpid_of_key)(parsec_data_collection_t* dc, parsec_data_key_t key);
+  parsec_data_t* (*data_of_key)(parsec_data_collection_t* dc, parsec_data_key_t key);
+  int nb_indices;          /* max indices passed to the varargs callbacks (default 2) */
+  parsec_datatype_t default_dtt;
+  char* key_base;
+  void* impl;              /* runtime-side collection object */
+};
+
+void parsec_data_collection_init(parsec_data_collection_t* dc, int nodes, int myrank);
+void parsec_data_collection_destroy(parsec_data_collection_t* dc);
+void parsec_data_collection_set_key(parsec_data_collection_t* dc, const char* name);
+
+parsec_data_t* parsec_data_create(parsec_data_t** holder, parsec_data_collection_t* desc, parsec_data_key_t key, void* ptr, size_t size);
+void parsec_data_destroy(parsec_data_t* data);
+parsec_data_copy_t* parsec_data_get_copy(parsec_data_t* data, int device);
+void* parsec_data_copy_get_ptr(parsec_data_copy_t* copy);
+void* parsec_data_get_ptr(parsec_data_t* data, int device);
+/* Bring the newest version of `data` back to host memory and return it. */
+void* parsec_data_pull_to_host(parsec_data_t* data);
+#define PARSEC_DATA_COPY_GET_PTR(c) parsec_data_copy_get_ptr(c)
+
+void* parsec_data_allocate(size_t size);
+void parsec_data_free(void* ptr);
+
+/* ---------------------------------------------------- tiled matrices */
+typedef enum { PARSEC_MATRIX_BYTE = 0, PARSEC_MATRIX_INTEGER, PARSEC_MATRIX_FLOAT, PARSEC_MATRIX_DOUBLE, PARSEC_MATRIX_COMPLEX_FLOAT, PARSEC_MATRIX_COMPLEX_DOUBLE } parsec_matrix_type_t;
+typedef enum { PARSEC_MATRIX_LAPACK = 0, PARSEC_MATRIX_TILE = 1 } parsec_matrix_storage_t;
+typedef enum { PARSEC_MATRIX_FULL = 0, PARSEC_MATRIX_LOWER = 1, PARSEC_MATRIX_UPPER = 2 } parsec_matrix_uplo_t;
+
+typedef struct parsec_tiled_matrix_s {
+  parsec_data_collection_t super;
+  parsec_matrix_type_t mtype;
+  parsec_matrix_storage_t storage;
+  int mb, nb, bsiz;        /* tile size, elements per tile */
+  int lm, ln, lmt, lnt;    /* whole matrix */
+  int i, j, m, n, mt, nt;  /* submatrix */
+  int llm, lln;            /* local rows / columns */
+  int nb_local_tiles;
+} parsec_tiled_matrix_t;
+
+typedef struct parsec_grid_2Dcyclic_s {
+  int rank, rows, cols, krows, kcols, ip, jq, rrank, crank;
+} parsec_grid_2Dcyclic_t;
+
+typedef struct parsec_matrix_block_cyclic_s {
+  parsec_tiled_matrix_t super;
+  parsec_grid_2Dcyclic_t grid;
+  void* mat; /* local tile storage (set by the user or parsec_data_allocate) */
+} parsec_matrix_block_cyclic_t;
+
+void parsec_matrix_block_cyclic_init(parsec_matrix_block_cyclic_t* dc, parsec_matrix_type_t mtype, parsec_matrix_storage_t storage, int myrank, int mb, int nb, int lm, int ln,
+                                     int i, int j, int m, int n, int p, int q, int kp, int kq, int ip, int jq);
+void parsec_tiled_matrix_destroy(parsec_tiled_matrix_t* tdesc);
+parsec_data_key_t parsec_tiled_matrix_data_key(parsec_tiled_matrix_t* tdesc, int m, int n);
+size_t parsec_matrix_type_size(parsec_matrix_type_t mtype);
+/* place the local storage in HBM of a GPU device (device index >= 2) */
+int parsec_tiled_matrix_set_storage_device(parsec_tiled_matrix_t* tdesc, int device_index);
+
+/* ---------------------------------------------------------------- arenas */
+#define PARSEC_ARENA_ALIGNMENT_64b 8
+#define PARSEC_ARENA_ALIGNMENT_INT sizeof(int)
+#define PARSEC_ARENA_ALIGNMENT_PTR sizeof(void*)
+#define PARSEC_ARENA_ALIGNMENT_SSE 16
+#define PARSEC_ARENA_ALIGNMENT_CL1 64
+
+int parsec_arena_datatype_construct(parsec_arena_datatype_t* adt, size_t elem_size, size_t alignment, parsec_datatype_t opaque_dtt);
+parsec_arena_datatype_t* parsec_arena_datatype_new(size_t elem_size, size_t alignment, parsec_datatype_t opaque_dtt);
+void parsec_arena_datatype_free(parsec_arena_datatype_t* adt);
+int parsec_add2arena_rect(parsec_arena_datatype_t* adt, parsec_datatype_t oldtype, int tile_mb, int tile_nb, int resized);
+int parsec_add2arena(parsec_arena_datatype_t* adt, parsec_datatype_t oldtype, parsec_matrix_uplo_t uplo, int diag, int m, int n, int ld, size_t alignment, int resized);
+void parsec_del2arena(parsec_arena_datatype_t* adt);
+/* Set arena slot `idx` of a taskpool (generated PARSEC_<name>_<TYPE>_ADT_IDX). */
+int parsec_taskpool_set_arena_datatype(parsec_taskpool_t* tp, int idx, size_t elem_size, size_t alignment, parsec_datatype_t opaque_dtt);
+
+/* ------------------------------------------------------------------ DTD */
+#define PARSEC_INPUT 0x100000
+#define PARSEC_OUTPUT 0x200000
+#define PARSEC_INOUT 0x300000
+#define PARSEC_ATOMIC_WRITE 0x400000
+#define PARSEC_SCRATCH 0x500000
+#define PARSEC_VALUE 0x600000
+#define PARSEC_REF 0x700000
+#define PARSEC_GET_OP_TYPE 0xf00000
+#define PARSEC_AFFINITY (1 << 16)
+#define PARSEC_DONT_TRACK (1 << 17)
+#define PARSEC_PUSHOUT (1 << 18)
+#define PARSEC_PULLIN (1 << 19)
+#define PARSEC_GET_OTHER_FLAG_INFO 0xf0000
+#define PARSEC_GET_REGION_INFO 0xffff
+#define PASSED_BY_REF (-2)
+#define PARSEC_DTD_ARG_END (-1)
+#define PARSEC_DTD_EMPTY_FLAG 0
+#define PARSEC_DTD_MAX_PARAMS 64
+
+typedef struct parsec_dtd_tile_s parsec_dtd_tile_t;
+typedef struct parsec_dtd_task_class_s parsec_dtd_task_class_t;
+typedef int(parsec_dtd_funcptr_t)(parsec_execution_stream_t* es, parsec_task_t* this_task);
+/* GPU chore: launches on `stream` (a hipStream_t); device pointers via parsec_dtd_get_dev_ptr */
+typedef int(parsec_dtd_gpu_funcptr_t)(void* stream, parsec_task_t* this_task);
+
+parsec_taskpool_t* parsec_dtd_taskpool_new(void);
+int parsec_dtd_taskpool_wait(parsec_taskpool_t* tp);
+void parsec_dtd_insert_task(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, int priority, int device_type, const char* name_of_kernel, ...);
+parsec_dtd_task_class_t* parsec_dtd_create_task_class(parsec_taskpool_t* tp, const char* name, ...);
+int parsec_dtd_task_class_add_chore(parsec_taskpool_t* tp, parsec_dtd_task_class_t* tc, int device_type, void* function);
+void parsec_dtd_insert_task_with_task_class(parsec_taskpool_t* tp, parsec_dtd_task_class_t* tc, int priority, int device_type, ...);
+parsec_dtd_tile_t* parsec_dtd_tile_of(parsec_data_collection_t* dc, parsec_data_key_t key);
+parsec_dtd_tile_t* parsec_dtd_tile_new(parsec_taskpool_t* tp, int rank, size_t size);
+void parsec_dtd_data_collection_init(parsec_data_collection_t* dc);
+void parsec_dtd_data_collection_fini(parsec_data_collection_t* dc);
+int parsec_dtd_data_flush(parsec_taskpool_t* tp, parsec_dtd_tile_t* tile);
+int parsec_dtd_data_flush_all(parsec_taskpool_t* tp, parsec_data_collection_t* dc);
+void parsec_dtd_unpack_args(parsec_task_t* this_task, ...);
+void* parsec_dtd_get_dev_ptr(parsec_task_t* this_task, int i);
+void parsec_dtd_set_window(parsec_taskpool_t* tp, int64_t window, int64_t threshold);
+#define PARSEC_DTD_TILE_OF(DC, I, J) parsec_dtd_tile_of((parsec_data_collection_t*)(DC), (DC)->super.super.data_key((parsec_data_collection_t*)(DC), (I), (J)))
+#define PARSEC_DTD_TILE_OF_KEY(DC, KEY) parsec_dtd_tile_of((parsec_data_collection_t*)(DC), (KEY))
+
+/* -------------------------------------------------------------- profiling */
+int parsec_profiling_init(const char* basename);
+int parsec_profiling_fini(void);
+int parsec_profiling_add_dictionary_keyword(const char* name, const char* attributes, size_t info_length, const char* convertor_code, int* key_start, int* key_end);
+int parsec_profiling_trace(int key, uint64_t event_id, uint32_t taskpool_id, const void* info);
+int parsec_profiling_dump(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PARSEC_AMD_PARSEC_H */

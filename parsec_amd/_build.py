@@ -3,7 +3,7 @@
 Outputs (in-tree so they travel with the repo snapshot to the GPU box):
   parsec_amd/lib/libparsec_amd.so   runtime + gfx950 HIP kernels
   parsec_amd/_C.<abi>.so            pybind11 bindings
-  parsec_amd/bin/ptgpp              .jdf -> C++ compiler
+  parsec_amd/bin/parsec-ptgpp       .jdf -> C++ compiler
   build/tests/*                     native unit tests
 
 Usage: python -m parsec_amd._build [--clean] [-j N]
@@ -43,7 +43,7 @@ HIP_SOURCES = [
     "csrc/kernels/tile_kernels.hip",
 ]
 PY_SOURCES = ["csrc/python/bindings.cpp"]
-PTGPP_SOURCES = []
+PTGPP_SOURCES = ["tools/ptgpp/ptgpp.cpp"]
 TEST_SOURCES = []
 
 
@@ -63,7 +63,7 @@ def generate():
     os.makedirs(os.path.join(PKG, "bin"), exist_ok=True)
     py_inc = sysconfig.get_paths()["include"]
     ext = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    common = f"-std=c++20 -O3 -g -fPIC -Wall -Wno-unused-result -D__HIP_PLATFORM_AMD__ -I{ROCM}/include -I{ROOT}/csrc"
+    common = f"-std=c++20 -O3 -g -fPIC -Wall -Wno-unused-result -D__HIP_PLATFORM_AMD__ -I{ROCM}/include -I{ROOT}/csrc -I{ROOT}/include"
     hipflags = f"-std=c++20 -O3 -fPIC --offload-arch={ARCH} -D__HIP_PLATFORM_AMD__ -I{ROOT}/csrc -Wno-unused-result"
     lines = [
         f"rocm = {ROCM}",
@@ -119,7 +119,7 @@ def generate():
         lines.append(f"build {obj}: cxx {os.path.join(ROOT, src)}")
         ptg_objs.append(obj)
     if ptg_objs:
-        lines.append(f"build {os.path.join(PKG, 'bin', 'ptgpp')}: exelink {' '.join(ptg_objs)}")
+        lines.append(f"build {os.path.join(PKG, 'bin', 'parsec-ptgpp')}: exelink {' '.join(ptg_objs)}")
         lines.append("  libs = ")
     for src in _exists(TEST_SOURCES):
         obj = os.path.join("obj", src.replace("/", "_") + ".o")

@@ -1,0 +1,72 @@
+"""Driver for the PTG compiler: .jdf -> C++ (parsec-ptgpp) -> program / library.
+
+    from parsec_amd import ptgpp
+    exe = ptgpp.build_program("chain.jdf", "/tmp/out")     # main() in the JDF epilogue
+    ptgpp.compile_jdf("chain.jdf", "/tmp/out")              # just the generated .cpp/.h
+
+CPU-only JDFs are compiled with g++; JDFs with BODY [type=HIP] (or hip=True)
+with hipcc for gfx950. Mirrors the reference's CMake helper
+target_ptg_sources (cmake_modules/ParsecCompilePTG.cmake:142-150).
+"""
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "parsec_amd")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+PTGPP = os.path.join(PKG, "bin", "parsec-ptgpp")
+
+
+class CompileError(RuntimeError):
+    pass
+
+
+def run_ptgpp(jdf, out_base=None, function_base=None, check_only=False):
+    """Run parsec-ptgpp; returns CompletedProcess (stdout/stderr captured)."""
+    if not os.path.exists(PTGPP):
+        raise CompileError("parsec-ptgpp is not built (python -m parsec_amd._build)")
+    cmd = [PTGPP, "-i", jdf]
+    if out_base:
+        cmd += ["-o", out_base]
+    if function_base:
+        cmd += ["-f", function_base]
+    if check_only:
+        cmd.append("-E")
+    return subprocess.run(cmd, capture_output=True, text=True)
+
+
+def compile_jdf(jdf, outdir, name=None):
+    os.makedirs(outdir, exist_ok=True)
+    name = name or os.path.splitext(os.path.basename(jdf))[0]
+    base = os.path.join(outdir, name)
+    r = run_ptgpp(jdf, base, name)
+    if r.returncode != 0:
+        raise CompileError(r.stderr)
+    return base + ".cpp", base + ".h"
+
+
+def _has_hip_body(jdf):
+    with open(jdf) as f:
+        src = f.read()
+    return "type=HIP" in src.replace(" ", "")
+
+
+def compile_flags(hip=False):
+    inc = [f"-I{ROOT}/include", f"-I{ROOT}/csrc", f"-I{ROCM}/include", "-D__HIP_PLATFORM_AMD__"]
+    libs = [f"-L{PKG}/lib", "-lparsec_amd", f"-Wl,-rpath,{PKG}/lib", f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib", "-lpthread"]
+    if hip:
+        return [f"{ROCM}/bin/hipcc", "-std=c++20", "-O2", f"--offload-arch={ARCH}"] + inc, libs
+    return ["g++", "-std=c++20", "-O2"] + inc, libs
+
+
+def build_program(jdf, outdir, extra_sources=(), hip=None, name=None):
+    cpp, _ = compile_jdf(jdf, outdir, name)
+    hip = _has_hip_body(jdf) if hip is None else hip
+    cc, libs = compile_flags(hip)
+    exe = os.path.splitext(cpp)[0]
+    cmd = cc + [f"-I{outdir}", cpp] + list(extra_sources) + ["-o", exe] + libs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise CompileError(" ".join(cmd) + "\n" + r.stderr[-6000:])
+    return exe
