@@ -1,0 +1,50 @@
+"""C API (include/parsec.h) tests: a C99 DTD program and a compiled JDF,
+single process and multi-process through parsec_amd.launch (the `:mp`
+variants of the reference's tests, tests/dsl/dtd/Testings.cmake:15-28)."""
+import os
+import subprocess
+
+import pytest
+
+from parsec_amd import launch, ptgpp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+@pytest.fixture(scope="module")
+def dtd_capi(tmp_path_factory, pa):
+    out = tmp_path_factory.mktemp("capi") / "dtd_capi"
+    cmd = ["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-O1", f"-I{ROOT}/include", os.path.join(HERE, "capi", "dtd_capi.c"), "-o", str(out),
+           f"-L{ROOT}/parsec_amd/lib", "-lparsec_amd", f"-Wl,-rpath,{ROOT}/parsec_amd/lib", "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return str(out)
+
+
+def test_dtd_c_program(dtd_capi):
+    r = subprocess.run([dtd_capi], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok" in r.stdout
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_dtd_c_program_multiprocess(dtd_capi, nranks):
+    rc, outs = launch.launch(nranks, [dtd_capi], timeout=120, capture=True)
+    assert rc == 0, outs
+    assert sum("ok" in o for o, _ in outs) == nranks
+
+
+@pytest.fixture(scope="module")
+def bcast_gather(tmp_path_factory, pa):
+    return ptgpp.build_program(os.path.join(HERE, "jdf", "bcast_gather.jdf"), str(tmp_path_factory.mktemp("jdfmp")))
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_jdf_multiprocess(bcast_gather, nranks):
+    """PTG broadcast of a NEW buffer to remote LEAF tasks and a remote CTL gather."""
+    rc, outs = launch.launch(nranks, [bcast_gather], timeout=120, capture=True)
+    assert rc == 0, outs
+    sinks = sum(int(o.split("sink")[1].split()[0]) for o, _ in outs)
+    leaves = sum(int(o.split("leaves")[1].split()[0]) for o, _ in outs)
+    assert sinks == 1 and leaves == 37
