@@ -31,6 +31,11 @@ def grid_of(n):
     return max(p, n // p), min(p, n // p)  # P >= Q
 
 
+def _stage(msg):
+    if os.environ.get("PARSEC_BENCH_VERBOSE"):
+        print(f"[bench rank {os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -62,6 +67,7 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    _stage("process group up")
     import parsec_amd as pa
 
     pa.require_native()
@@ -74,7 +80,9 @@ def main():
         rc = pa.comm_init(rank, world, job, -1 if args.share_gpu else local)
         if rc != 0:
             raise RuntimeError(f"comm_init failed rc={rc}")
+    _stage("comm up")
     ctx = pa.init(args.cores)
+    _stage("context up")
     gpu = pa.first_gpu_device_index()
     if gpu < 0:
         raise RuntimeError("no GPU device registered in the runtime")
@@ -109,7 +117,9 @@ def main():
         tp, info = pa.dpotrf_new(A, pa.MATRIX_LOWER)
         ctx.add_taskpool(tp)
         ctx.start()
+        _stage("taskpool started")
         ctx.wait()
+        _stage("taskpool done")
         return pa.read_int(info)
 
     def barrier():

@@ -16,34 +16,14 @@
 
 #include "../device/device.hpp"
 #include "linalg.hpp"
+#include "ptg_ir.hpp"
 
 namespace parsec {
 namespace algos {
 
 using namespace ptg;
 
-// ----------------------------------------------------------- IR helpers
-static LocalDef range_local(const std::string& n, Expr lo, Expr hi) {
-  LocalDef l;
-  l.name = n; l.is_range = true; l.is_param = true; l.lo = std::move(lo); l.hi = std::move(hi);
-  return l;
-}
-static Expr cst(int64_t v) { return [v](const Taskpool*, const int32_t*) { return v; }; }
-static Expr loc(int i) { return [i](const Taskpool*, const int32_t* L) { return (int64_t)L[i]; }; }
-static Expr locp(int i, int64_t d) { return [i, d](const Taskpool*, const int32_t* L) { return (int64_t)L[i] + d; }; }
-static CallArg val(Expr e) { CallArg a; a.value = std::move(e); return a; }
-static CallArg rng(Expr lo, Expr hi) { CallArg a; a.is_range = true; a.lo = std::move(lo); a.hi = std::move(hi); return a; }
-static DepTarget task(const std::string& tc, const std::string& flow, std::vector<CallArg> args) {
-  DepTarget t; t.kind = DEP_TASK; t.tc_name = tc; t.flow_name = flow; t.args = std::move(args); return t;
-}
-static DepTarget data(TiledMatrix* A, Expr m, Expr n) {
-  DepTarget t; t.kind = DEP_DATA; t.dc = [A](const Taskpool*) { return (DataCollection*)A; }; t.args = {val(std::move(m)), val(std::move(n))}; return t;
-}
-static Dep always(DepTarget t) { Dep d; d.then_t = std::move(t); return d; }
-static Dep cond(Guard g, DepTarget a, DepTarget b) { Dep d; d.guard = std::move(g); d.then_t = std::move(a); d.has_else = true; d.else_t = std::move(b); return d; }
-static Dep when(Guard g, DepTarget a) { Dep d; d.guard = std::move(g); d.then_t = std::move(a); return d; }
-
-static inline double* fptr(Task* t, int f) { return t->data[f].data_in ? static_cast<double*>(t->data[f].data_in->device_private) : nullptr; }
+using namespace ir;
 
 // ------------------------------------------------------ CPU reference bodies
 static int cpu_potrf(double* A, int n, int lda) {

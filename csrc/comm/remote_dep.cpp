@@ -244,6 +244,8 @@ void on_activate(int src, int, const void* msg, size_t len) {
   ActHdr h;
   std::memcpy(&h, msg, sizeof(h));
   Taskpool* tp = taskpool_lookup(h.tp_id);
+  PARSEC_DEBUG(kVerbDebug, "comm", "ACTIVATE from %d tp %u tc %u mask %x%s", src, h.tp_id, (unsigned)h.tc_id, (unsigned)h.output_mask,
+               (!tp || !tp->context || tp->completed.load()) ? " (parked)" : "");
   if (!tp || !tp->context || tp->completed.load()) {
     std::lock_guard<std::mutex> g(g_m);
     g_parked[h.tp_id].emplace_back(src, std::vector<char>((const char*)msg, (const char*)msg + len));
@@ -317,12 +319,14 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
     }
   }
   GetMsg gm{r->hdr.send_id, r->id, get_mask, g_ce->rank};
+  PARSEC_DEBUG(kVerbDebug, "comm", "request data from %d (recv %llu mask %x)", src, (unsigned long long)r->id, get_mask);
   g_ce->send_am(TAG_GET_DATA, src, &gm, sizeof(gm));
 }
 
 void on_get(int src, int, const void* msg, size_t) {
   GetMsg g;
   std::memcpy(&g, msg, sizeof(g));
+  PARSEC_DEBUG(kVerbDebug, "comm", "GET from %d send %llu mask %x", src, (unsigned long long)g.send_id, (unsigned)g.flow_mask);
   SendState* s = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_m);
@@ -383,6 +387,7 @@ void on_fragment(int src, int, const void* msg, size_t len) {
 
 void deliver(RecvState* r) {
   Taskpool* tp = r->tp;
+  PARSEC_DEBUG(kVerbDebug, "comm", "deliver from %d tp %u tc %u", r->src, r->hdr.tp_id, (unsigned)r->hdr.tc_id);
   RemoteActivation act;
   act.tp = tp;
   act.taskpool_id = r->hdr.tp_id;

@@ -72,13 +72,44 @@ struct PotrfDesc {
   double* invD_out = nullptr;  // optional: keep the 64x64 diagonal-block inverses (ceil(n/64) x 4096 doubles)
 };
 
+// Householder QR of a tile (GEQRT: A2 == nullptr) or of a triangle on top of a
+// tile (TSQRT: [R = A1 (upper); A2]), compact WY with a full n x n upper T.
+struct QrPanelDesc {
+  double* A1;
+  int lda1;
+  double* A2;      // TSQRT only
+  int lda2;
+  double* T;       // n x n, written upper triangular with zeros below
+  int ldt;
+  double* Vcopy;   // GEQRT only (optional): clean unit-lower V (m1 x min(m1,n), ld m1)
+  int m1;          // GEQRT: rows of the tile (min(m1, n) reflectors)
+  int m2, n;       // TSQRT: rows of A2; columns
+};
+
+// Apply Q^T of a QR panel: UNMQR (A1 == nullptr: C = A2 := Q^T C with C and the
+// unit-lower V both m2 rows, n reflectors) or TSMQR ([A1; A2] := Q^T [A1; A2]
+// with V = [I; V2], V2 m2 x n, A1 n x ncols).
+struct QrApplyDesc {
+  const double* V;
+  int ldv;
+  const double* T;
+  int ldt;
+  double* A1;
+  int lda1;
+  double* A2;
+  int lda2;
+  int m2, n, ncols;
+};
+
 struct KernelBatch {
   std::vector<GemmDesc> gemm;
   std::vector<TrsmDesc> trsm;
   std::vector<PotrfDesc> potrf;
+  std::vector<QrPanelDesc> qr_panel;
+  std::vector<QrApplyDesc> qr_apply;
   std::vector<std::function<void(hipStream_t)>> generic;  // other kernels, launched in order
-  bool empty() const { return gemm.empty() && trsm.empty() && potrf.empty() && generic.empty(); }
-  void clear() { gemm.clear(); trsm.clear(); potrf.clear(); generic.clear(); }
+  bool empty() const { return gemm.empty() && trsm.empty() && potrf.empty() && qr_panel.empty() && qr_apply.empty() && generic.empty(); }
+  void clear() { gemm.clear(); trsm.clear(); potrf.clear(); qr_panel.clear(); qr_apply.clear(); generic.clear(); }
 };
 
 struct HipDevice;

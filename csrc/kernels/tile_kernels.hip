@@ -63,7 +63,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 }
 
 // ==================================================================== GEMM
-template <int BM, int BN, int BK, int WM, int WN, bool TRANSB>
+template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void dgemm_batch_kernel(const GemmBatchArgs args) {
   constexpr int WTM = BM / WM;
   constexpr int WTN = BN / WN;
@@ -95,7 +95,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
   const int M = d.m, N = d.n, K = d.k;
   const int lda = d.lda, ldb = d.ldb;
   // 16-byte loads when every row pair is aligned and fully inside the tile
-  const bool vec = ((lda | ldb) % 2 == 0) && ((((uintptr_t)A) | ((uintptr_t)B)) % 16 == 0) && (M % 2 == 0) && (TRANSB ? (N % 2 == 0) : (K % 2 == 0));
+  const bool vec = ((lda | ldb) % 2 == 0) && ((((uintptr_t)A) | ((uintptr_t)B)) % 16 == 0) && (TRANSA ? (K % 2 == 0) : (M % 2 == 0)) &&
+                   (TRANSB ? (N % 2 == 0) : (K % 2 == 0));
 
   double4_t acc[FN][FM];
 #pragma unroll
@@ -112,13 +113,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
 #pragma unroll
     for (int e = 0; e < A_PAIRS; ++e) {
       int idx = tid + 256 * e;
-      int mm = (idx % (BM / 2)) * 2, kk = idx / (BM / 2);
-      int gm = m0 + mm, gk = k0 + kk;
-      const double* p = A + (size_t)gk * lda + gm;
-      if (vec && gk < K && gm + 1 < M) ra[e] = *reinterpret_cast<const double2_t*>(p);
-      else {
-        ra[e].x = (gm < M && gk < K) ? p[0] : 0.0;
-        ra[e].y = (gm + 1 < M && gk < K) ? p[1] : 0.0;
+      if (TRANSA) {  // A is K x M (k contiguous): op(A)(m, k) = A[k + m*lda]
+        int kk = (idx % (BK / 2)) * 2, mm = idx / (BK / 2);
+        int gm = m0 + mm, gk = k0 + kk;
+        const double* p = A + (size_t)gm * lda + gk;
+        if (vec && gm < M && gk + 1 < K) ra[e] = *reinterpret_cast<const double2_t*>(p);
+        else {
+          ra[e].x = (gm < M && gk < K) ? p[0] : 0.0;
+          ra[e].y = (gm < M && gk + 1 < K) ? p[1] : 0.0;
+        }
+      } else {
+        int mm = (idx % (BM / 2)) * 2, kk = idx / (BM / 2);
+        int gm = m0 + mm, gk = k0 + kk;
+        const double* p = A + (size_t)gk * lda + gm;
+        if (vec && gk < K && gm + 1 < M) ra[e] = *reinterpret_cast<const double2_t*>(p);
+        else {
+          ra[e].x = (gm < M && gk < K) ? p[0] : 0.0;
+          ra[e].y = (gm + 1 < M && gk < K) ? p[1] : 0.0;
+        }
       }
     }
 #pragma unroll
@@ -149,8 +161,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
 #pragma unroll
     for (int e = 0; e < A_PAIRS; ++e) {
       int idx = tid + 256 * e;
-      int mm = (idx % (BM / 2)) * 2, kk = idx / (BM / 2);
-      *reinterpret_cast<double2_t*>(&As[buf][kk][mm]) = ra[e];
+      if (TRANSA) {
+        int kk = (idx % (BK / 2)) * 2, mm = idx / (BK / 2);
+        As[buf][kk][mm] = ra[e].x;
+        As[buf][kk + 1][mm] = ra[e].y;
+      } else {
+        int mm = (idx % (BM / 2)) * 2, kk = idx / (BM / 2);
+        *reinterpret_cast<double2_t*>(&As[buf][kk][mm]) = ra[e];
+      }
     }
 #pragma unroll
     for (int e = 0; e < B_PAIRS; ++e) {
@@ -505,21 +523,32 @@ static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) 
   a.tile_start[n] = total;
   a.total_tiles = total;
   if (total == 0) return;
-  const bool tb = descs[0].transB;
+  const int mode = (descs[0].transA ? 2 : 0) | (descs[0].transB ? 1 : 0);
+#define PARSEC_GEMM_LAUNCH(BMV, TA, TB) hipLaunchKernelGGL((dgemm_batch_kernel<BMV, BMV, 16, 2, 2, TA, TB>), dim3(total), dim3(256), 0, stream, a)
   if (bm == 128) {
-    if (tb) hipLaunchKernelGGL((dgemm_batch_kernel<128, 128, 16, 2, 2, true>), dim3(total), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((dgemm_batch_kernel<128, 128, 16, 2, 2, false>), dim3(total), dim3(256), 0, stream, a);
+    switch (mode) {
+      case 0: PARSEC_GEMM_LAUNCH(128, false, false); break;
+      case 1: PARSEC_GEMM_LAUNCH(128, false, true); break;
+      case 2: PARSEC_GEMM_LAUNCH(128, true, false); break;
+      default: PARSEC_GEMM_LAUNCH(128, true, true); break;
+    }
   } else {
-    if (tb) hipLaunchKernelGGL((dgemm_batch_kernel<64, 64, 16, 2, 2, true>), dim3(total), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((dgemm_batch_kernel<64, 64, 16, 2, 2, false>), dim3(total), dim3(256), 0, stream, a);
+    switch (mode) {
+      case 0: PARSEC_GEMM_LAUNCH(64, false, false); break;
+      case 1: PARSEC_GEMM_LAUNCH(64, false, true); break;
+      case 2: PARSEC_GEMM_LAUNCH(64, true, false); break;
+      default: PARSEC_GEMM_LAUNCH(64, true, true); break;
+    }
   }
+#undef PARSEC_GEMM_LAUNCH
 }
 
+// Group descriptors by (transA, transB): one grouped launch per combination.
 void launch_gemm_batch(const GemmDesc* descs, int n, hipStream_t stream) {
-  std::vector<GemmDesc> nt, nn;
-  for (int i = 0; i < n; ++i) (descs[i].transB ? nt : nn).push_back(descs[i]);
-  for (auto* v : {&nt, &nn})
-    for (size_t s = 0; s < v->size(); s += kMaxGemmBatch) launch_gemm_chunk(v->data() + s, (int)std::min<size_t>(kMaxGemmBatch, v->size() - s), stream);
+  std::vector<GemmDesc> g[4];
+  for (int i = 0; i < n; ++i) g[(descs[i].transA ? 2 : 0) | (descs[i].transB ? 1 : 0)].push_back(descs[i]);
+  for (auto& v : g)
+    for (size_t s = 0; s < v.size(); s += kMaxGemmBatch) launch_gemm_chunk(v.data() + s, (int)std::min<size_t>(kMaxGemmBatch, v.size() - s), stream);
 }
 
 static constexpr int kTrsmRows = 16;
@@ -611,16 +640,25 @@ void launch_potrf(const PotrfDesc& p, hipStream_t stream, double* ws) {
 
 }  // namespace kern
 
+namespace kern {
+void launch_qr_panel(const QrPanelDesc* descs, int n, hipStream_t stream);
+void launch_qr_apply(const QrApplyDesc* descs, int n, hipStream_t stream, double* ws);
+size_t qr_apply_workspace_bytes(const QrApplyDesc* descs, int n);
+}  // namespace kern
+
 size_t kernel_batch_workspace_bytes(const KernelBatch& b) {
   size_t w = b.potrf.empty() ? 0 : 4096 * sizeof(double);
-  return std::max(w, kern::trsm_workspace_bytes(b.trsm.data(), (int)b.trsm.size()));
+  w = std::max(w, kern::trsm_workspace_bytes(b.trsm.data(), (int)b.trsm.size()));
+  return std::max(w, kern::qr_apply_workspace_bytes(b.qr_apply.data(), (int)b.qr_apply.size()));
 }
 
 void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal, void* ws) {
   (void)device_ordinal;
   // critical-path kernels first: POTRF, then TRSM, then the GEMM/SYRK updates
   for (auto& p : b.potrf) kern::launch_potrf(p, stream, static_cast<double*>(ws));
+  if (!b.qr_panel.empty()) kern::launch_qr_panel(b.qr_panel.data(), (int)b.qr_panel.size(), stream);
   if (!b.trsm.empty()) kern::launch_trsm_batch(b.trsm.data(), (int)b.trsm.size(), stream, static_cast<double*>(ws));
+  if (!b.qr_apply.empty()) kern::launch_qr_apply(b.qr_apply.data(), (int)b.qr_apply.size(), stream, static_cast<double*>(ws));
   if (!b.gemm.empty()) kern::launch_gemm_batch(b.gemm.data(), (int)b.gemm.size(), stream);
   for (auto& g : b.generic) g(stream);
 }

@@ -450,6 +450,8 @@ PYBIND11_MODULE(_C, m) {
         tp->destructor_hook = [info]() { delete info; };
         return py::make_tuple(py::cast(tp, py::return_value_policy::take_ownership), (uintptr_t)info);
       });
+  m.def("dgeqrf_new", [](TiledMatrix* A, TiledMatrix* T, int ib) { return algos::dgeqrf_new(A, T, ib); }, py::arg("A"), py::arg("T"), py::arg("ib") = 0,
+        py::return_value_policy::take_ownership);
   m.def("read_int", [](uintptr_t p) { return *reinterpret_cast<int*>(p); });
 
   // --------------------------------------------------------------- devices
