@@ -137,6 +137,7 @@ def main():
         info = step()
     barrier()
     dt = time.perf_counter() - t0
+    _stage("timed region done")
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device="cpu" if args.share_gpu else "cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -176,11 +177,15 @@ def main():
             dist.all_reduce(te, op=dist.ReduceOp.MAX)
             err = float(te.item())
         check = err
+        _stage("check done")
 
     devs = pa.devices()
+    _stage("fini context")
     ctx.fini()
+    _stage("context finalized")
     if world > 1:
         pa.comm_fini()
+        _stage("comm finalized")
     if rank == 0:
         out = {
             "metric": "GFLOP/s (whole node) tiled DPOTRF 2D block-cyclic at 1/2/4/8 MI355X",

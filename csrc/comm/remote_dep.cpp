@@ -516,6 +516,7 @@ void remote_dep_fini(Context* ctx) {
   if (g_ce) {
     // nothing must be in flight when the context goes away
     g_ce->sync();
+    PARSEC_DEBUG(kVerbDebug, "fini", "comm barrier passed");
     g_ce->post([] { set_my_execution_stream(nullptr); });
   }
   g_comm_es = nullptr;

@@ -237,9 +237,13 @@ int context_fini(Context** pctx) {
   Context* ctx = *pctx;
   if (!ctx) return 0;
   if (ctx->active_taskpools.load() > 0) context_wait(ctx);
+  PARSEC_DEBUG(kVerbDebug, "fini", "at_fini hooks (%zu)", ctx->at_fini.size());
   for (size_t i = 0; i < ctx->at_fini.size(); ++i) ctx->at_fini[i](ctx->at_fini_data[i]);
+  PARSEC_DEBUG(kVerbDebug, "fini", "remote deps");
   remote_dep_fini(ctx);
+  PARSEC_DEBUG(kVerbDebug, "fini", "devices stop");
   devices_stop(ctx);
+  PARSEC_DEBUG(kVerbDebug, "fini", "joining workers");
   {
     std::lock_guard<std::mutex> g(ctx->wake_m);
     ctx->finalizing.store(true);
@@ -247,6 +251,7 @@ int context_fini(Context** pctx) {
   ctx->wake_cv.notify_all();
   for (auto& t : ctx->threads) t.join();
   ctx->threads.clear();
+  PARSEC_DEBUG(kVerbDebug, "fini", "workers joined");
   ExecutionStream* master = ctx->all_es[0];
   PARSEC_PINS(master, PINS_THREAD_FINI, nullptr);
   if (ParamRegistry::instance().reg_int("runtime", "", "show_stats", "Display scheduler statistics at fini", 0))
@@ -255,7 +260,9 @@ int context_fini(Context** pctx) {
   grapher_fini(ctx);
   pins_fini(ctx);
   profiling_fini(ctx);
+  PARSEC_DEBUG(kVerbDebug, "fini", "devices fini");
   devices_fini(ctx);
+  PARSEC_DEBUG(kVerbDebug, "fini", "scheduler remove");
   ctx->scheduler->remove(ctx);
   delete ctx->scheduler;
   for (auto* vp : ctx->vps) {
@@ -266,6 +273,7 @@ int context_fini(Context** pctx) {
   set_my_execution_stream(nullptr);
   delete ctx;
   *pctx = nullptr;
+  PARSEC_DEBUG(kVerbDebug, "fini", "context released");
   return 0;
 }
 

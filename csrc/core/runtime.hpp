@@ -219,6 +219,9 @@ struct DataCollection {
   virtual Data* data_of_key(uint64_t key) = 0;
   virtual uint64_t data_key(const int64_t* idx, int n) const = 0;
   virtual std::string key_to_string(uint64_t key) const { return key_base + "(" + std::to_string(key) + ")"; }
+  // Bytes of the datum behind `key` (used for remote shadows; collections with
+  // heterogeneous tile sizes override it).
+  virtual size_t data_size_of_key(uint64_t key) const { (void)key; return (size_t)std::max<int64_t>(default_dtt.extent_bytes(), 0); }
   virtual int home_device() const { return 0; }  // device holding the collection's own storage
   virtual int register_memory(Device* dev) { (void)dev; return 0; }
   virtual int unregister_memory(Device* dev) { (void)dev; return 0; }

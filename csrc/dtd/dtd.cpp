@@ -128,7 +128,7 @@ Tile* DtdTaskpool::tile_of(DataCollection* dc, uint64_t key) {
       t->data = data_new();
       t->data->dc = dc;
       t->data->key = key;
-      t->data->nb_elts = (size_t)std::max<int64_t>(dc->default_dtt.extent_bytes(), 0);
+      t->data->nb_elts = dc->data_size_of_key(key);
       t->is_new = true;
     }
     m[k] = t;
@@ -155,10 +155,86 @@ Tile* DtdTaskpool::tile_new(size_t bytes, int rank) {
   return t;
 }
 
-// add a dependency pred -> succ unless pred already completed
+// Private copy of `src` for a pending remote transfer (host or device memory).
+static void snapshot_release(DataCopy* c) {
+  if (c->device_index == 0) std::free(c->device_private);
+  else device_free(c->device_index, c->device_private);
+  Data* d = c->original;
+  if (d) {
+    d->lock.lock();
+    data_copy_detach(d, c, c->device_index);
+    d->lock.unlock();
+  }
+  delete c;
+  if (d) data_release(d);
+}
+
+static DataCopy* snapshot_copy(DataCopy* src) {
+  const size_t n = src->original ? src->original->nb_elts : 0;
+  void* p = nullptr;
+  int dev = src->device_index;
+  if (dev != 0) p = device_alloc(dev, std::max<size_t>(n, 64));
+  if (!p) {
+    dev = 0;
+    if (posix_memalign(&p, 64, std::max<size_t>(n, 64))) fatal("DTD: out of memory for a send snapshot");
+  }
+  if (n) device_memcpy(dev, p, src->device_index, src->device_private, n);
+  Data* d = data_new();
+  d->nb_elts = n;
+  d->owner_device = (int8_t)dev;
+  DataCopy* c = new DataCopy();
+  c->device_private = p;
+  c->device_index = (int8_t)dev;
+  c->coherency_state = COHERENCY_OWNED;
+  c->version = src->version;
+  c->dtt = src->dtt;
+  c->release_fn = snapshot_release;
+  data_copy_attach(d, c, dev);
+  return c;
+}
+
+static DataCopy* newest_copy(Data* d);
+
+// A remote consumer was inserted after its local producer `w` completed: send
+// the producer's version of flow `flow` (still the tile's current data -- no
+// later writer can have been inserted before the consumer) unless that rank
+// already received it.
+static void send_late(DtdTask* w, int flow, int rank) {
+  auto* tp = static_cast<DtdTaskpool*>(w->taskpool);
+  {
+    std::lock_guard<SpinLock> g(w->lock);
+    bool sent;
+    if (rank < 32) { sent = w->sent_mask[flow] & (1u << rank); w->sent_mask[flow] |= 1u << rank; }
+    else {
+      uint64_t k = ((uint64_t)flow << 32) | (uint64_t)rank;
+      sent = std::find(w->sent_ext.begin(), w->sent_ext.end(), k) != w->sent_ext.end();
+      if (!sent) w->sent_ext.push_back(k);
+    }
+    if (sent) return;
+  }
+  Tile* tile = nullptr;
+  for (auto& a : w->args) if (a.flow == flow) tile = a.tile;
+  DataCopy* src = tile && tile->data ? newest_copy(tile->data) : nullptr;
+  RemoteDepsMsg msg;
+  msg.outputs.resize(w->nb_flows);
+  auto& o = msg.outputs[flow];
+  o.data = src ? snapshot_copy(src) : nullptr;
+  o.ctl = o.data == nullptr;
+  o.ranks.push_back(rank);
+  msg.taskpool_id = tp->taskpool_id;
+  msg.task_class_id = w->task_class->task_class_id;
+  msg.dtd_task_id = w->seq;
+  msg.priority = w->priority;
+  ExecutionStream* es = my_execution_stream();
+  remote_dep_activate(es ? es : tp->context->all_es[0], tp, msg);
+  if (o.data) data_copy_release(o.data);
+}
+
+// add a dependency pred -> succ unless pred's output is already available:
+// a local pred that completed, or a remote shadow whose flow already arrived
 static bool add_edge(DtdTask* pred, DtdTask* succ, int src_flow, int dst_flow, bool data) {
   std::lock_guard<SpinLock> g(pred->lock);
-  if (pred->completed) return false;
+  if (pred->remote ? (pred->activated & (1u << src_flow)) != 0 : pred->completed) return false;
   pred->succ.push_back(Edge{succ, dst_flow, src_flow, data});
   succ->deps.fetch_add(1, std::memory_order_relaxed);
   task_retain(succ);
@@ -208,20 +284,35 @@ DtdTask* DtdTaskpool::insert_task(DtdTaskClass* tc, int priority, const std::vec
     task_retain(t);
     remote_tasks.insert(t->seq, t);
   }
-  // dependency tracking per tile
+  // dependency tracking per tile. Tasks of different ranks never share memory
+  // (each rank works on its own copy of a tile), so only same-rank WAR / WAW
+  // edges exist; cross-rank edges carry data (writer -> reader / updater).
+  std::vector<std::pair<DtdTask*, int>> late;  // completed local writer -> remote consumer
   for (auto& a : t->args) {
     if (a.flow < 0 || !a.tile || (a.op & DONT_TRACK)) continue;
     Tile* tl = a.tile;
     int op = a.op & OP_MASK;
+    if (op != INPUT) t->written |= 1u << a.flow;
     std::lock_guard<SpinLock> g(tl->lock);
+    DtdTask* w = tl->writer;
+    const bool needs_data = op == INPUT || op == INOUT || op == ATOMIC_WRITE;
+    if (w) {
+      const bool same = w->rank == t->rank;
+      if (same) {
+        if (!(w->remote && t->remote)) add_edge(w, t, tl->writer_flow, a.flow, true);
+      } else if (needs_data) {
+        if (!add_edge(w, t, tl->writer_flow, a.flow, true) && !w->remote && t->remote) {
+          task_retain(w);
+          late.emplace_back(w, tl->writer_flow);
+        }
+      }
+    }
     if (op == INPUT) {
-      if (tl->writer) add_edge(tl->writer, t, tl->writer_flow, a.flow, true);
       task_retain(t);
       tl->readers.emplace_back(t, a.flow);
     } else {
-      if (tl->writer) add_edge(tl->writer, t, tl->writer_flow, a.flow, true);
       for (auto& r : tl->readers) {
-        if (r.first != t) add_edge(r.first, t, r.second, a.flow, false);
+        if (r.first != t && r.first->rank == t->rank && !(r.first->remote && t->remote)) add_edge(r.first, t, r.second, a.flow, false);
         task_unref(r.first);
       }
       tl->readers.clear();
@@ -232,6 +323,10 @@ DtdTask* DtdTaskpool::insert_task(DtdTaskClass* tc, int priority, const std::vec
       tl->last_writer_rank = rank;
       ++tl->version;
     }
+  }
+  for (auto& lw : late) {
+    send_late(lw.first, lw.second, t->rank);
+    task_unref(lw.first);
   }
   // activations that arrived before this (remote) task was discovered
   if (t->remote) {
@@ -282,7 +377,14 @@ int DtdTaskpool::wait() {
   int64_t base = hold.load() ? 1 : 0;
   execute_and_come_back(base);
   Backoff b;
-  while (nb_pending_actions.load() > base) b.idle();
+  uint64_t t0 = now_ns();
+  while (nb_pending_actions.load() > base) {
+    b.idle();
+    if (now_ns() - t0 > 2000000000ull) {
+      PARSEC_DEBUG(kVerbDebug, "dtd", "wait: %lld tasks, %lld pending actions (base %lld)", (long long)nb_tasks.load(), (long long)nb_pending_actions.load(), (long long)base);
+      t0 = now_ns();
+    }
+  }
   return 0;
 }
 
@@ -373,12 +475,10 @@ static void release_successors(ExecutionStream* es, DtdTask* t, uint32_t flow_ma
       edges.swap(t->succ);
     } else {
       // remote shadow: release only the edges of the activated flows
+      t->activated |= flow_mask;
       std::vector<Edge> keep;
       for (auto& e : t->succ) (flow_mask & (1u << e.src_flow) ? edges : keep).push_back(e);
       t->succ.swap(keep);
-      bool all = true;
-      for (int f = 0; f < t->nb_flows; ++f) if (!(flow_mask & (1u << f))) all = false;
-      if (all || t->succ.empty()) t->completed = true;
     }
   }
   DtdTaskpool* tp = static_cast<DtdTaskpool*>(t->taskpool);
@@ -404,7 +504,9 @@ static void release_successors(ExecutionStream* es, DtdTask* t, uint32_t flow_ma
           }
           auto& o = msg->outputs[e.src_flow];
           DataCopy* dc = t->data[e.src_flow].data_out ? t->data[e.src_flow].data_out : t->data[e.src_flow].data_in;
-          if (e.data && dc) o.data = dc;
+          // snapshot: a later same-rank writer may update the tile in place
+          // while the transfer is still pending
+          if (e.data && dc && !o.data) o.data = snapshot_copy(dc);
           if (!e.data) o.ctl = o.data == nullptr;
           if (std::find(o.ranks.begin(), o.ranks.end(), r) == o.ranks.end()) o.ranks.push_back(r);
         }
@@ -434,6 +536,7 @@ int DtdTaskClass::complete_execution(ExecutionStream* es, Task* tt) const {
     msg->dtd_task_id = t->seq;
     msg->priority = t->priority;
     remote_dep_activate(es, t->taskpool, *msg);
+    for (auto& o : msg->outputs) if (o.data) data_copy_release(o.data);  // remote_dep holds its own refs
     delete msg;
   }
   PARSEC_PINS(es, PINS_RELEASE_DEPS_END, t);
@@ -519,7 +622,7 @@ void DtdTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& ac
   RemoteDepsMsg* msg = nullptr;
   release_successors(es, t, act.output_mask, act.data, ready, msg);
   delete msg;  // remote shadows never forward
-  if (t->completed) {
+  if (t->written && (t->activated & t->written) == t->written) {
     if (remote_tasks.erase(t->seq)) task_unref(t);
   }
   if (!ready.empty()) schedule_tasks(es, ready.data(), (int)ready.size(), 1);

@@ -79,6 +79,8 @@ struct DtdTask : Task {
   uint64_t seq = 0;
   uint32_t sent_mask[kMaxFlows] = {};  // per flow: bitmap of ranks already activated (first 32 ranks)
   std::vector<uint64_t> sent_ext;      // beyond 32 ranks
+  uint32_t activated = 0;    // remote shadow: flows whose output version has arrived
+  uint32_t written = 0;      // flows this task writes (OUTPUT / INOUT / ATOMIC_WRITE)
 };
 
 class DtdTaskClass : public TaskClass {

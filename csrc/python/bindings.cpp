@@ -9,6 +9,7 @@
 #include <cstring>
 
 #include "../algos/linalg.hpp"
+#include "../algos/stencil3d.hpp"
 #include "../comm/comm.hpp"
 #include "../core/runtime.hpp"
 #include "../data/collections.hpp"
@@ -452,6 +453,34 @@ PYBIND11_MODULE(_C, m) {
       });
   m.def("dgeqrf_new", [](TiledMatrix* A, TiledMatrix* T, int ib) { return algos::dgeqrf_new(A, T, ib); }, py::arg("A"), py::arg("T"), py::arg("ib") = 0,
         py::return_value_policy::take_ownership);
+  py::class_<algos::StencilGrid, DataCollection>(m, "StencilGrid")
+      .def(py::init([](int myrank, int nodes, int64_t nx, int64_t ny, int64_t nz, int bx, int by, int bz, int device) {
+             auto* g = new algos::StencilGrid();
+             g->init(myrank, nodes, nx, ny, nz, bx, by, bz, device);
+             return g;
+           }),
+           py::arg("myrank"), py::arg("nodes"), py::arg("nx"), py::arg("ny"), py::arg("nz"), py::arg("bx"), py::arg("by"), py::arg("bz"), py::arg("device") = 0)
+      .def_readonly("nblocks", &algos::StencilGrid::nblocks)
+      .def("block_rank", &algos::StencilGrid::block_rank)
+      .def("block_dims", [](algos::StencilGrid& g, int64_t b) { int x, y, z; g.block_dims(b, &x, &y, &z); return py::make_tuple(x, y, z); })
+      .def("block", [](algos::StencilGrid& g, int64_t b, int parity) -> py::object {
+        // host copy of block b's solution buffer (local blocks only), shape (ez, ey, ex)
+        Data* d = g.data_of_key(g.key(0, parity, b, 0));
+        if (!d) return py::none();
+        DataCopy* c = data_pull_to_host(d);
+        int x, y, z;
+        g.block_dims(b, &x, &y, &z);
+        std::vector<py::ssize_t> shape{z, y, x}, strides{(py::ssize_t)(8 * x * y), (py::ssize_t)(8 * x), 8};
+        return py::array(py::dtype::of<double>(), shape, strides, c->device_private, py::capsule(c->device_private, [](void*) {}));
+      });
+  m.def("stencil3d_run", [](PxContext& c, algos::StencilGrid* g, int iters, double c0, double c1, bool gpu) {
+        algos::Stencil3DResult r;
+        {
+          py::gil_scoped_release rel;
+          r = algos::stencil3d_run(c.ctx, g, iters, c0, c1, gpu);
+        }
+        return py::make_tuple(r.seconds, r.points, r.final_parity);
+      }, py::arg("ctx"), py::arg("grid"), py::arg("iters"), py::arg("c0") = 0.4, py::arg("c1") = 0.1, py::arg("gpu") = true);
   m.def("read_int", [](uintptr_t p) { return *reinterpret_cast<int*>(p); });
 
   // --------------------------------------------------------------- devices

@@ -37,12 +37,14 @@ CORE_SOURCES = [
     "csrc/dtd/dtd.cpp",
     "csrc/algos/dpotrf.cpp",
     "csrc/algos/dgeqrf.cpp",
+    "csrc/algos/stencil3d.cpp",
     "csrc/algos/dtd_builtins.cpp",
     "csrc/capi/capi.cpp",
 ]
 HIP_SOURCES = [
     "csrc/kernels/tile_kernels.hip",
     "csrc/kernels/qr_kernels.hip",
+    "csrc/kernels/stencil_kernels.hip",
 ]
 PY_SOURCES = ["csrc/python/bindings.cpp"]
 PTGPP_SOURCES = ["tools/ptgpp/ptgpp.cpp"]
