@@ -5,6 +5,8 @@
 #include "../data/collections.hpp"
 #include "../ptg/ptg.hpp"
 
+#include <functional>
+
 namespace parsec {
 namespace algos {
 
@@ -16,14 +18,24 @@ ptg::PtgTaskpool* dgemm_new(double alpha, TiledMatrix* A, TiledMatrix* B, double
 // Tiled QR A = QR (Householder, tile algorithm GEQRT/TSQRT/UNMQR/TSMQR). T holds
 // the block reflectors (ib x nb per tile).
 ptg::PtgTaskpool* dgeqrf_new(TiledMatrix* A, TiledMatrix* T, int ib);
-// Collection operators (reference data_dist/matrix/apply.jdf, map_operator.c, reduce*.jdf)
+// Collection operators (reference data_dist/matrix/apply.jdf, map_operator.c,
+// reduce_col/row.jdf, broadcast.jdf, redistribute/*; see collection_ops.cpp).
 using TileOp = std::function<void(TiledMatrix*, int64_t m, int64_t n, void* tile, void* arg)>;
+using MapOp = std::function<void(const void* src, void* dst, int64_t m, int64_t n, int64_t rows, int64_t cols)>;
+// inout = op(in, inout); `first` is true for the first tile of a chain (inout
+// then holds the initial value of the result tile).
+using ReduceOp = std::function<void(const void* in, void* inout, int64_t rows, int64_t cols, bool first)>;
 ptg::PtgTaskpool* apply_new(TiledMatrix* A, int uplo, TileOp op, void* arg);
-ptg::PtgTaskpool* map_operator_new(TiledMatrix* src, TiledMatrix* dst, TileOp op, void* arg);
-ptg::PtgTaskpool* reduce_col_new(TiledMatrix* A, TiledMatrix* res, std::function<void(const void* in, void* inout, int64_t rows, int64_t cols)> op);
-ptg::PtgTaskpool* reduce_row_new(TiledMatrix* A, TiledMatrix* res, std::function<void(const void* in, void* inout, int64_t rows, int64_t cols)> op);
+ptg::PtgTaskpool* map_operator_new(TiledMatrix* src, TiledMatrix* dst, MapOp op);
+ptg::PtgTaskpool* reduce_col_new(TiledMatrix* A, TiledMatrix* res, ReduceOp op);
+ptg::PtgTaskpool* reduce_row_new(TiledMatrix* A, TiledMatrix* res, ReduceOp op);
 ptg::PtgTaskpool* broadcast_new(TiledMatrix* A, int64_t root_m, int64_t root_n, TiledMatrix* dst);
-ptg::PtgTaskpool* redistribute_new(TiledMatrix* src, TiledMatrix* dst, int64_t size_row, int64_t size_col, int64_t disi_src, int64_t disj_src, int64_t disi_dst, int64_t disj_dst);
+// Copy the size_row x size_col window at (disi_src, disj_src) of src to
+// (disi_dst, disj_dst) of dst (any tile sizes / distributions). Blocking (DTD).
+int redistribute(Context* ctx, TiledMatrix* src, TiledMatrix* dst, int64_t size_row, int64_t size_col, int64_t disi_src, int64_t disj_src, int64_t disi_dst,
+                 int64_t disj_dst);
+// Tiled C = alpha A B + beta C inserted as DTD tasks (blocking).
+int dtd_dgemm(Context* ctx, double alpha, TiledMatrix* A, TiledMatrix* B, double beta, TiledMatrix* C, bool use_gpu);
 
 }  // namespace algos
 }  // namespace parsec

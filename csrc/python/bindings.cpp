@@ -481,6 +481,64 @@ PYBIND11_MODULE(_C, m) {
         }
         return py::make_tuple(r.seconds, r.points, r.final_parity);
       }, py::arg("ctx"), py::arg("grid"), py::arg("iters"), py::arg("c0") = 0.4, py::arg("c1") = 0.1, py::arg("gpu") = true);
+  // ------------------------------------------------ collection operators
+  m.def("apply_new", [](TiledMatrix* A, int uplo, py::function fn) {
+        auto* keep = new py::function(fn);
+        auto* tp = algos::apply_new(A, uplo, [keep](TiledMatrix* M, int64_t mm, int64_t nn, void* tile, void*) {
+          py::gil_scoped_acquire g;
+          (*keep)(mm, nn, tile_view(tile, M->mtype, M->mb, M->nb, M->elem_size));
+        }, nullptr);
+        tp->destructor_hook = [keep] { py::gil_scoped_acquire g; delete keep; };
+        return (Taskpool*)tp;
+      }, py::return_value_policy::take_ownership);
+  m.def("map_new", [](TiledMatrix* src, TiledMatrix* dst, py::function fn) {
+        auto* keep = new py::function(fn);
+        auto* tp = algos::map_operator_new(src, dst, [keep, src, dst](const void* s, void* d, int64_t mm, int64_t nn, int64_t, int64_t) {
+          py::gil_scoped_acquire g;
+          (*keep)(tile_view(const_cast<void*>(s), src->mtype, src->mb, src->nb, src->elem_size), tile_view(d, dst->mtype, dst->mb, dst->nb, dst->elem_size), mm, nn);
+        });
+        tp->destructor_hook = [keep] { py::gil_scoped_acquire g; delete keep; };
+        return (Taskpool*)tp;
+      }, py::return_value_policy::take_ownership);
+  auto reduce_binding = [](bool by_col) {
+    return [by_col](TiledMatrix* A, TiledMatrix* res, py::object fn) {
+      algos::ReduceOp op;
+      py::function* keep = nullptr;
+      if (py::isinstance<py::str>(fn) && fn.cast<std::string>() == "sum") {
+        const int64_t ld = A->mb;
+        op = [ld](const void* in, void* io, int64_t rows, int64_t cols, bool first) {
+          const double* a = static_cast<const double*>(in);
+          double* r = static_cast<double*>(io);
+          for (int64_t c = 0; c < cols; ++c)
+            for (int64_t i = 0; i < rows; ++i) r[i + c * ld] = (first ? 0.0 : r[i + c * ld]) + a[i + c * ld];
+        };
+      } else {
+        keep = new py::function(fn.cast<py::function>());
+        op = [keep, A](const void* in, void* io, int64_t, int64_t, bool first) {
+          py::gil_scoped_acquire g;
+          (*keep)(tile_view(const_cast<void*>(in), A->mtype, A->mb, A->nb, A->elem_size), tile_view(io, A->mtype, A->mb, A->nb, A->elem_size), first);
+        };
+      }
+      auto* tp = by_col ? algos::reduce_col_new(A, res, op) : algos::reduce_row_new(A, res, op);
+      if (keep) tp->destructor_hook = [keep] { py::gil_scoped_acquire g; delete keep; };
+      return (Taskpool*)tp;
+    };
+  };
+  m.def("reduce_col_new", reduce_binding(true), py::return_value_policy::take_ownership);
+  m.def("reduce_row_new", reduce_binding(false), py::return_value_policy::take_ownership);
+  m.def("broadcast_new", [](TiledMatrix* A, int64_t rm, int64_t rn, TiledMatrix* dst) { return (Taskpool*)algos::broadcast_new(A, rm, rn, dst); },
+        py::return_value_policy::take_ownership);
+  m.def("redistribute", [](PxContext& c, TiledMatrix* src, TiledMatrix* dst, int64_t size_row, int64_t size_col, int64_t disi_src, int64_t disj_src, int64_t disi_dst,
+                           int64_t disj_dst) {
+        py::gil_scoped_release rel;
+        return algos::redistribute(c.ctx, src, dst, size_row, size_col, disi_src, disj_src, disi_dst, disj_dst);
+      });
+  m.def("dgemm_new", [](double alpha, TiledMatrix* A, TiledMatrix* B, double beta, TiledMatrix* C, int transB) { return (Taskpool*)algos::dgemm_new(alpha, A, B, beta, C, transB); },
+        py::arg("alpha"), py::arg("A"), py::arg("B"), py::arg("beta"), py::arg("C"), py::arg("transB") = 0, py::return_value_policy::take_ownership);
+  m.def("dtd_dgemm", [](PxContext& c, double alpha, TiledMatrix* A, TiledMatrix* B, double beta, TiledMatrix* C, bool gpu) {
+        py::gil_scoped_release rel;
+        return algos::dtd_dgemm(c.ctx, alpha, A, B, beta, C, gpu);
+      }, py::arg("ctx"), py::arg("alpha"), py::arg("A"), py::arg("B"), py::arg("beta"), py::arg("C"), py::arg("gpu") = false);
   m.def("read_int", [](uintptr_t p) { return *reinterpret_cast<int*>(p); });
 
   // --------------------------------------------------------------- devices

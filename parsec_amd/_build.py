@@ -38,6 +38,7 @@ CORE_SOURCES = [
     "csrc/algos/dpotrf.cpp",
     "csrc/algos/dgeqrf.cpp",
     "csrc/algos/stencil3d.cpp",
+    "csrc/algos/collection_ops.cpp",
     "csrc/algos/dtd_builtins.cpp",
     "csrc/capi/capi.cpp",
 ]
