@@ -10,6 +10,7 @@
 
 #include "../algos/linalg.hpp"
 #include "../algos/stencil3d.hpp"
+#include "../core/recursive.hpp"
 #include "../comm/comm.hpp"
 #include "../core/runtime.hpp"
 #include "../data/collections.hpp"
@@ -257,7 +258,9 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("rank", [](PyTask& p) { return static_cast<dtd::DtdTask*>(p.t)->rank; })
       .def_property_readonly("name", [](PyTask& p) { return p.t->task_class->name; })
       .def_property_readonly("priority", [](PyTask& p) { return p.t->priority; })
-      .def("user_trigger_termination", [](PyTask& p) { p.t->taskpool->tdm->user_trigger(p.t->taskpool); });
+      .def("user_trigger_termination", [](PyTask& p) { p.t->taskpool->tdm->user_trigger(p.t->taskpool); })
+      .def("recursive_call", [](PyTask& p, Taskpool* inner) { return recursive_call(my_execution_stream(), p.t, inner); },
+           "run `inner` as this task's body; return the result (HOOK_ASYNC) from the body");
 
   py::class_<dtd::DtdTaskClass>(m, "DtdTaskClass")
       .def_property_readonly("name", [](dtd::DtdTaskClass& c) { return c.name; })
@@ -320,6 +323,7 @@ PYBIND11_MODULE(_C, m) {
       .def("data_flush", [](dtd::DtdTaskpool& tp, dtd::Tile* t) { py::gil_scoped_release rel; return tp.data_flush(t); })
       .def("data_flush_all", [](dtd::DtdTaskpool& tp, DataCollection* dc) { py::gil_scoped_release rel; return tp.data_flush_all(dc); })
       .def("wait", [](dtd::DtdTaskpool& tp) { py::gil_scoped_release rel; return tp.wait(); })
+      .def("close", [](dtd::DtdTaskpool& tp) { tp.release_hold(); }, "no more insertions: the taskpool may terminate once its tasks ran")
       .def_property("window", [](dtd::DtdTaskpool& tp) { return tp.window; }, [](dtd::DtdTaskpool& tp, int64_t w) { tp.window = w; })
       .def_property("threshold", [](dtd::DtdTaskpool& tp) { return tp.threshold; }, [](dtd::DtdTaskpool& tp, int64_t w) { tp.threshold = w; });
 

@@ -23,6 +23,7 @@ CORE_SOURCES = [
     "csrc/core/mca.cpp",
     "csrc/core/context.cpp",
     "csrc/core/scheduling.cpp",
+    "csrc/core/recursive.cpp",
     "csrc/sched/schedulers.cpp",
     "csrc/termdet/termdet.cpp",
     "csrc/data/data.cpp",

@@ -307,3 +307,45 @@ def test_properties_dictionary(pa):
     pa.properties_set("test.flops", 12.5)
     props = dict(pa.properties())
     assert props["test.flops"] == 12.5
+
+
+# ------------------------------------------------------------ recursive
+def test_recursive_task(pa):
+    """A DTD task body runs an inner DTD taskpool (recursive_call -> HOOK_ASYNC);
+    its successor only runs once the inner taskpool terminated
+    (reference recursive.h:20-76)."""
+    ctx = _ctx(pa, 4)
+    A = _vector_tiles(pa, 2)
+    tp = pa.dtd_taskpool(ctx)
+    ctx.start()
+    inner_runs = []
+    keep = []
+
+    def inner_body(task):
+        inner_runs.append(1)
+        return 0
+
+    def parent(task):
+        inner = pa.DtdTaskpool()
+        keep.append(inner)
+        rc = task.recursive_call(inner)
+        t = inner.tile_of(A, A.data_key([1, 0]))
+        for _ in range(10):
+            pa.insert_task(inner, inner_body, [(t, pa.INOUT)], name="inner_body")
+        inner.data_flush_all(A)
+        inner.close()
+        return rc
+
+    seen = []
+
+    def after(task):
+        seen.append(len(inner_runs))
+        return 0
+
+    t0 = tp.tile_of(A, A.data_key([0, 0]))
+    pa.insert_task(tp, parent, [(t0, pa.INOUT)], name="parent")
+    pa.insert_task(tp, after, [(t0, pa.INPUT)], name="after")
+    tp.data_flush_all(A)
+    ctx.wait()
+    assert seen == [10]
+    ctx.fini()
