@@ -127,6 +127,12 @@ def generate():
     if ptg_objs:
         lines.append(f"build {os.path.join(PKG, 'bin', 'parsec-ptgpp')}: exelink {' '.join(ptg_objs)}")
         lines.append("  libs = ")
+    # GPU bandwidth shmoo (host code only, links the HIP runtime)
+    bw = "tools/bandwidth/bandwidth.cpp"
+    if os.path.exists(os.path.join(ROOT, bw)):
+        lines.append(f"build obj/tools_bandwidth.o: cxx {os.path.join(ROOT, bw)}")
+        lines.append(f"build {os.path.join(PKG, 'bin', 'parsec-bandwidth')}: exelink obj/tools_bandwidth.o")
+        lines.append(f"  libs = -L{ROCM}/lib -lamdhip64 -Wl,-rpath,{ROCM}/lib")
     for src in _exists(TEST_SOURCES):
         obj = os.path.join("obj", src.replace("/", "_") + ".o")
         exe = os.path.join(BUILD, "tests", os.path.splitext(os.path.basename(src))[0])
