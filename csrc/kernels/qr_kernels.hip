@@ -23,12 +23,14 @@ namespace kern {
 void launch_gemm_batch(const GemmDesc* descs, int n, hipStream_t stream);  // tile_kernels.hip
 
 constexpr int kQrThreads = 256;
-constexpr int kMaxQrBatch = 64;
+constexpr int kMaxQrBatch = 32;
 
 struct QrPanelArgs {
   int count;
   QrPanelDesc d[kMaxQrBatch];
 };
+// kernel arguments are passed by value and must fit the 4 KiB kernarg segment
+static_assert(sizeof(QrPanelArgs) <= 4096, "QrPanelArgs exceeds the kernel argument limit");
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -148,6 +150,7 @@ struct Axpy2DArgs {
   int count;
   Axpy2D d[kMaxQrBatch];
 };
+static_assert(sizeof(Axpy2DArgs) <= 4096, "Axpy2DArgs exceeds the kernel argument limit");
 __global__ __launch_bounds__(256) void axpy2d_kernel(const Axpy2DArgs a) {
   const Axpy2D& d = a.d[blockIdx.y];
   const int64_t total = (int64_t)d.rows * d.cols;

@@ -40,6 +40,7 @@ struct GemmBatchArgs {
   int tile_start[kMaxGemmBatch + 1];
   GemmDesc d[kMaxGemmBatch];
 };
+static_assert(sizeof(GemmBatchArgs) <= 4096, "GemmBatchArgs exceeds the kernel argument limit");
 
 template <class Args>
 __device__ __forceinline__ int find_desc(const Args& a, const int* starts, int t) {
@@ -403,6 +404,7 @@ struct TrsmInvArgs {
   TrsmDesc d[kMaxTrsmBatch];
   const double* invD[kMaxTrsmBatch];
 };
+static_assert(sizeof(TrsmInvArgs) <= 4096, "TrsmInvArgs exceeds the kernel argument limit");
 
 // B := B L^-T by 64-column blocks: R_j = B_j - X_<j L_j,<j^T, X_j = R_j invD_j^T.
 // A workgroup owns BR = 16 rows of B (its row panel lives in LDS, stride 16:

@@ -306,7 +306,36 @@ int PtgTaskClass::prepare_input(ExecutionStream* es, Task* t) const {
         break;
     }
   }
+  reshape_inputs(t);
   return HOOK_DONE;
+}
+
+// Local reshape (reference parsec_reshape.c:29-771): an input dependency that
+// names an arena datatype other than DEFAULT receives a private copy holding
+// only the elements of that layout (e.g. [type = LOWER]: the lower triangle,
+// zeros elsewhere) when the incoming copy has a different layout. Host copies
+// only; device-resident inputs are passed unchanged.
+void PtgTaskClass::reshape_inputs(Task* t) const {
+  auto& adts = t->taskpool->arenas_datatypes;
+  for (size_t f = 0; f < def.flows.size(); ++f) {
+    TaskDataRef& r = t->data[f];
+    DataCopy* c = r.data_in;
+    if (!c || c->device_index != 0 || def.flows[f].access == FLOW_CTL) continue;
+    const DepTarget* tg = active_input(t->taskpool, (int)f, t->locals);
+    if (!tg || tg->datatype_index <= 0 || tg->datatype_index >= (int)adts.size()) continue;
+    const ArenaDatatype& adt = adts[tg->datatype_index];
+    const Datatype& want = adt.opaque_dtt;
+    if (!adt.arena || want.kind == Datatype::NONE || want == c->dtt) continue;
+    DataCopy* nc = adt.arena->get_copy(nullptr, 0);
+    if (!nc) continue;
+    std::memset(nc->device_private, 0, adt.arena->elem_size);
+    std::vector<uint8_t> tmp((size_t)want.packed_bytes());
+    want.pack(c->device_private, tmp.data());
+    want.unpack(tmp.data(), nc->device_private);
+    nc->dtt = want;
+    data_copy_release(c);
+    r.data_in = nc;
+  }
 }
 
 // Copy `src` into the collection's own copy of `home` (final write of a flow

@@ -137,6 +137,7 @@ class PtgTaskClass : public TaskClass {
   // Every active input instance of `flow` (one for data flows, all for CTL gathers).
   void for_each_input(const Taskpool* tp, int flow, const int32_t* L, const std::function<void(const int32_t* Lx, const DepTarget*)>& f) const;
   mutable std::atomic<bool> warned_null_forward{false};
+  void reshape_inputs(Task* t) const;
 };
 
 // Call f(Lx, target) for every active instance of `d` (expanding iterators).

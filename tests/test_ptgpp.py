@@ -26,6 +26,7 @@ def _run(exe, timeout=60, env=None):
     ("chain", "chain value 10"),
     ("bcast_gather", "leaves 37 sink 1 bad 0"),
     ("local_indices", "runs 16 48 32 1"),
+    ("reshape", "reshape ok 5 bad 0 full 1"),
 ])
 def test_jdf_program(tmp_path, name, expect):
     exe = ptgpp.build_program(os.path.join(JDF, name + ".jdf"), str(tmp_path))
