@@ -138,7 +138,11 @@ int execute_task(ExecutionStream* es, Task* t) {
       rc = ch.hook(es, t);
       PARSEC_PINS(es, PINS_EXEC_END, t);
       if (rc == HOOK_DONE) {
-        DeviceRegistry::instance().devices[0]->stats.executed_tasks.fetch_add(1, std::memory_order_relaxed);
+        Device* dev = DeviceRegistry::instance().devices[0];
+        if (ch.type == DEV_TEMPLATE)
+          for (Device* d : DeviceRegistry::instance().devices)
+            if (d && d->type == DEV_TEMPLATE) dev = d;
+        dev->stats.executed_tasks.fetch_add(1, std::memory_order_relaxed);
         ++es->nb_executed;
         if (gpus) cpu_write_epilog(t);
       }

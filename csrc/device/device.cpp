@@ -54,6 +54,16 @@ struct RecursiveDevice : Device {
   RecursiveDevice() { name = "recursive"; type = DEV_RECURSIVE; gflops_fp64 = 1; }
 };
 
+// Device template (reference mca/device/template): a pseudo-accelerator whose
+// chores (type DEV_TEMPLATE) run on the worker threads, with no-op memory
+// registration. It exercises chore selection, device masks and per-device
+// statistics without GPU hardware (--mca device_template_enabled 1).
+struct TemplateDevice : Device {
+  TemplateDevice() { name = "template"; type = DEV_TEMPLATE; gflops_fp64 = 1; }
+  int memory_register(DataCollection*, void*, size_t) override { return 0; }
+  int memory_unregister(DataCollection*, void*) override { return 0; }
+};
+
 static double g_load_balance_skew = 20.0;
 
 void devices_init(Context* ctx) {
@@ -68,6 +78,15 @@ void devices_init(Context* ctx) {
     reg.add(new RecursiveDevice());
     hip_devices_init(ctx);
     reg.registration_complete();
+  }
+  // the template device can be enabled by a later context of the same process
+  if (params.reg_int("device", "template", "enabled", "Register the template pseudo-device (framework testing)", 0)) {
+    bool have = false;
+    for (auto* d : reg.devices) if (d && d->type == DEV_TEMPLATE) have = true;
+    if (!have) {
+      reg.add(new TemplateDevice());
+      reg.registration_complete();
+    }
   }
   for (auto* d : reg.devices) if (d) d->attach(ctx);
   if (params.reg_int("device", "", "show_capabilities", "Print device capabilities at init", 0))

@@ -99,6 +99,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("DEV_CPU") = (int)DEV_CPU;
   m.attr("DEV_RECURSIVE") = (int)DEV_RECURSIVE;
   m.attr("DEV_HIP") = (int)DEV_HIP;
+  m.attr("DEV_TEMPLATE") = (int)DEV_TEMPLATE;
   m.attr("DEV_ALL") = (int)DEV_ALL;
   m.attr("INPUT") = (int)dtd::INPUT;
   m.attr("OUTPUT") = (int)dtd::OUTPUT;

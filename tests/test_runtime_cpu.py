@@ -349,3 +349,30 @@ def test_recursive_task(pa):
     ctx.wait()
     assert seen == [10]
     ctx.fini()
+
+
+def test_template_device(pa):
+    """Device template (reference mca/device/template): chores typed
+    DEV_TEMPLATE run on the pseudo-device once it is enabled; the CPU chore
+    is the fallback."""
+    pa.mca_set("device_template_enabled", "1")
+    try:
+        ctx = pa.init(2)
+    finally:
+        pa.mca_unset("device_template_enabled")
+    A = _vector_tiles(pa, 1)
+    tp = pa.dtd_taskpool(ctx)
+    ctx.start()
+    ran = []
+    tc = tp.task_class("templ", [(pa.INOUT, pa.PASSED_BY_REF)])
+    tp.add_chore(tc, pa.DEV_TEMPLATE, lambda task: (ran.append("template"), 0)[1])
+    tp.add_chore(tc, pa.DEV_CPU, lambda task: (ran.append("cpu"), 0)[1])
+    t = tp.tile_of(A, 0)
+    for _ in range(5):
+        tp.insert_task(tc, [(t, pa.INOUT)], 0)
+    tp.data_flush_all(A)
+    ctx.wait()
+    devs = {d["name"]: d for d in pa.devices()}
+    ctx.fini()
+    assert ran == ["template"] * 5
+    assert devs["template"]["executed_tasks"] >= 5
