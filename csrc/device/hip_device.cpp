@@ -184,7 +184,8 @@ void HipDevice::shutdown() {
   for (List* l : {&lru_clean, &lru_owned}) {
     while (ListItem* it = l->pop_front()) {
       DataCopy* c = static_cast<DataCopy*>(it);
-      if (Data* d = c->original) {
+      Data* d = c->original;
+      if (d) {
         std::lock_guard<SpinLock> g(d->lock);
         data_copy_detach(d, c, device_index);
       }
@@ -193,6 +194,7 @@ void HipDevice::shutdown() {
       c->dev_state = nullptr;
       c->original = nullptr;
       data_copy_release(c);
+      if (d) data_release(d);
     }
   }
   zone.reset();
@@ -305,6 +307,7 @@ bool HipDevice::evict(size_t bytes) {
     c->dev_state = nullptr;
     c->original = nullptr;
     data_copy_release(c);
+    data_release(d);
     stats.data_faults.fetch_add(1, std::memory_order_relaxed);
     return true;
   };
@@ -390,7 +393,11 @@ int HipDevice::stage_in(GpuTask* g) {
       {
         std::lock_guard<SpinLock> lk(d->lock);
         local = d->copy(device_index);
-        if (!local) { data_copy_attach(d, nc, device_index); local = nc; }
+        if (!local) {
+          data_copy_attach(d, nc, device_index);
+          data_retain(d);  // an engine-managed copy keeps its Data alive (NEW / arena data may lose its host copy first)
+          local = nc;
+        }
       }
       if (local != nc) { zone->free(p); delete static_cast<DevCopyState*>(nc->dev_state); delete nc; }
     }
@@ -529,6 +536,7 @@ void HipDevice::epilog(GpuTask* g) {
 
 void HipDevice::complete(GpuTask* g) {
   Task* t = g->task;
+  PARSEC_DEBUG(kVerbNoisier, "hip", "completed %s", t->task_class->describe(t).c_str());
   for (int fi = 0; fi < kMaxFlows; ++fi) if (g->dev_copy[fi]) lru_touch(g->dev_copy[fi]);
   load.fetch_sub((int64_t)g->load, std::memory_order_relaxed);
   stats.executed_tasks.fetch_add(1, std::memory_order_relaxed);

@@ -26,6 +26,9 @@ using namespace parsec;
 extern "C" int parsec_amd_dgemm_batch(const GemmDesc* descs, int n, void* stream);
 extern "C" int parsec_amd_dtrsm_batch(const TrsmDesc* descs, int n, void* stream);
 extern "C" int parsec_amd_dpotrf_tile(double* A, int n, int lda, int* info, void* stream);
+extern "C" int parsec_amd_qr_panel(const parsec::QrPanelDesc* d, int n, void* stream);
+extern "C" int parsec_amd_qr_apply(const parsec::QrApplyDesc* d, int n, void* ws, void* stream);
+extern "C" size_t parsec_amd_qr_apply_ws(const parsec::QrApplyDesc* d, int n);
 namespace parsec { void register_builtin_dtd_gpu_bodies(); std::function<int(GpuExecContext*, Task*)> builtin_dtd_gpu_body(const std::string& name); }
 
 namespace {
@@ -591,6 +594,18 @@ PYBIND11_MODULE(_C, m) {
     TrsmDesc t;
     t.L = (const double*)L; t.B = (double*)B; t.m = mm; t.n = nn; t.ldl = ldl; t.ldb = ldb; t.trans = 1;
     return parsec_amd_dtrsm_batch(&t, 1, (void*)stream);
+  });
+  m.def("kernel_qr_panel", [](uintptr_t A1, int lda1, uintptr_t A2, int lda2, uintptr_t T, int ldt, uintptr_t V, int m1, int m2, int n, uintptr_t stream) {
+    QrPanelDesc q{};
+    q.A1 = (double*)A1; q.lda1 = lda1; q.A2 = (double*)A2; q.lda2 = lda2; q.T = (double*)T; q.ldt = ldt; q.Vcopy = (double*)V;
+    q.m1 = m1; q.m2 = m2; q.n = n;
+    return parsec_amd_qr_panel(&q, 1, (void*)stream);
+  });
+  m.def("kernel_qr_apply", [](uintptr_t V, int ldv, uintptr_t T, int ldt, uintptr_t A1, int lda1, uintptr_t A2, int lda2, int m2, int n, int ncols, uintptr_t ws, uintptr_t stream) {
+    QrApplyDesc q{};
+    q.V = (const double*)V; q.ldv = ldv; q.T = (const double*)T; q.ldt = ldt; q.A1 = (double*)A1; q.lda1 = lda1; q.A2 = (double*)A2; q.lda2 = lda2;
+    q.m2 = m2; q.n = n; q.ncols = ncols;
+    return parsec_amd_qr_apply(&q, 1, (void*)ws, (void*)stream);
   });
   m.def("kernel_dpotrf", [](uintptr_t A, int n, int lda, uintptr_t info, uintptr_t stream) { return parsec_amd_dpotrf_tile((double*)A, n, lda, (int*)info, (void*)stream); });
 

@@ -1,4 +1,5 @@
 """Numerics of the hand-written CDNA4 fp64 tile kernels vs fp64 torch references."""
+import numpy as np
 import pytest
 
 torch = pytest.importorskip("torch")
@@ -69,3 +70,82 @@ def test_dpotrf_tile(pa, dev, n):
     L = torch.tril(A)
     err = (L @ L.t() - S).norm() / S.norm()
     assert err.item() < 1e-13
+
+
+# --------------------------------------------------------------- QR kernels
+def _house_qr_ref(A):
+    """numpy reference of the compact-WY QR: R (upper), V (unit lower), T."""
+    import numpy as np
+
+    A = A.copy()
+    m, n = A.shape
+    k = min(m, n)
+    V = np.zeros((m, k))
+    T = np.zeros((k, k))
+    for j in range(k):
+        x = A[j:, j]
+        alpha, sigma = x[0], float(x[1:] @ x[1:])
+        if sigma == 0.0:
+            tau, beta, v = 0.0, alpha, np.zeros_like(x)
+            v[0] = 1.0
+        else:
+            beta = -np.copysign(np.sqrt(alpha * alpha + sigma), alpha)
+            tau = (beta - alpha) / beta
+            v = x / (alpha - beta)
+            v[0] = 1.0
+        A[j:, j:] -= tau * np.outer(v, v @ A[j:, j:])
+        V[j:, j] = v
+        T[:j, j] = -tau * T[:j, :j] @ (V[:, :j].T @ V[:, j])
+        T[j, j] = tau
+    return np.triu(A)[:k], V, T
+
+
+def _cm(x, dev):
+    """column-major device copy of a (rows, cols) array: returns the (cols, rows) tensor"""
+    return torch.as_tensor(np.ascontiguousarray(np.asarray(x).T), dtype=torch.float64).to(dev)
+
+
+def _np(t):
+    return t.cpu().numpy().T
+
+
+@pytest.mark.parametrize("m,n", [(256, 256), (300, 200), (128, 256)])
+def test_qr_panel_geqrt(pa, dev, m, n):
+    A = np.random.default_rng(0).standard_normal((m, n))
+    k = min(m, n)
+    Ad = _cm(A, dev)
+    Td = torch.zeros((k, k), dtype=torch.float64, device=dev)
+    Vd = torch.zeros((k, m), dtype=torch.float64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    assert pa.kernel_qr_panel(Ad.data_ptr(), m, 0, 0, Td.data_ptr(), k, Vd.data_ptr(), m, 0, n, s) == 0
+    torch.cuda.synchronize()
+    R_ref, V_ref, T_ref = _house_qr_ref(A)
+    assert np.allclose(np.triu(_np(Ad))[:k], R_ref, atol=1e-10)
+    assert np.allclose(_np(Vd), V_ref, atol=1e-10)
+    assert np.allclose(_np(Td), T_ref, atol=1e-10)
+
+
+@pytest.mark.parametrize("m2,n", [(256, 256), (100, 64)])
+def test_qr_panel_tsqrt_and_tsmqr(pa, dev, m2, n):
+    rng = np.random.default_rng(1)
+    R = np.triu(rng.standard_normal((n, n)))
+    A2 = rng.standard_normal((m2, n))
+    Rd, A2d = _cm(R, dev), _cm(A2, dev)
+    Td = torch.zeros((n, n), dtype=torch.float64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    assert pa.kernel_qr_panel(Rd.data_ptr(), n, A2d.data_ptr(), m2, Td.data_ptr(), n, 0, 0, m2, n, s) == 0
+    torch.cuda.synchronize()
+    R_ref, V_ref, T_ref = _house_qr_ref(np.vstack([R, A2]))
+    assert np.allclose(np.triu(_np(Rd)), R_ref, atol=1e-10)
+    assert np.allclose(_np(A2d), V_ref[n:], atol=1e-10)
+    assert np.allclose(_np(Td), T_ref, atol=1e-10)
+    # TSMQR: [B1; B2] := Q^T [B1; B2]
+    nc = 96
+    B1, B2 = rng.standard_normal((n, nc)), rng.standard_normal((m2, nc))
+    B1d, B2d = _cm(B1, dev), _cm(B2, dev)
+    ws = torch.empty(2 * n * nc, dtype=torch.float64, device=dev)
+    assert pa.kernel_qr_apply(A2d.data_ptr(), m2, Td.data_ptr(), n, B1d.data_ptr(), n, B2d.data_ptr(), m2, m2, n, nc, ws.data_ptr(), s) == 0
+    torch.cuda.synchronize()
+    X = np.vstack([B1, B2])
+    ref = X - V_ref @ (T_ref.T @ (V_ref.T @ X))
+    assert np.allclose(np.vstack([_np(B1d), _np(B2d)]), ref, atol=1e-10)
