@@ -77,7 +77,7 @@ def main():
     if world > 1:
         # unique per launch: the launcher pid is shared by all ranks of one job
         job = "_".join([os.environ.get("MASTER_PORT", "0"), os.environ.get("TORCHELASTIC_RUN_ID", "bench"), str(os.getppid())])
-        rc = pa.comm_init(rank, world, job, -1 if args.share_gpu else local)
+        rc = pa.comm_init(rank, world, job, local)
         if rc != 0:
             raise RuntimeError(f"comm_init failed rc={rc}")
     _stage("comm up")

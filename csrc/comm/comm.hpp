@@ -8,10 +8,11 @@
 // MI355X-native design (one process per GPU on one node, no MPI):
 //  * control plane: lock-free SPSC shared-memory rings, one per ordered rank pair,
 //    progressed by one comm thread per rank;
-//  * data plane: device tiles travel GPU->GPU with RCCL send/recv over xGMI, on a
-//    dedicated communicator + HIP stream per directed rank pair (FIFO-matched by
-//    the GET order, so sends/recvs can never cross); host tiles travel through the
-//    shm rings in fragments.
+//  * data plane: device tiles travel GPU->GPU over xGMI -- by default the receiver
+//    maps the sender's allocation through HIP IPC and pulls the tile with an async
+//    D2D copy (one IPC_DONE ack releases the sender's copy); optionally with RCCL
+//    send/recv on a communicator + HIP stream per directed rank pair; host tiles
+//    travel through the shm rings in fragments.
 #pragma once
 #include <cstdint>
 #include <functional>
@@ -25,6 +26,7 @@ namespace parsec {
 enum CommTag : int {
   TAG_GET_INTERNAL = 0, TAG_PUT_INTERNAL = 1, TAG_REMOTE_DEP_ACTIVATE = 2, TAG_GET_DATA = 3, TAG_PUT_END = 4,
   TAG_TERMDET_FOURCOUNTER = 5, TAG_TERMDET_USER_TRIGGER = 6, TAG_DATA_FRAGMENT = 7, TAG_BARRIER = 8, TAG_ALLREDUCE = 9,
+  TAG_DATA_IPC = 10, TAG_IPC_DONE = 11,
   TAG_USER = 16, TAG_MAX = 32,
 };
 

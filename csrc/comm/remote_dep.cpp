@@ -74,6 +74,22 @@ struct FragHdr {
   uint64_t total;
 };
 
+struct IpcMsg {
+  uint64_t recv_id;
+  uint64_t send_id;
+  uint32_t flow;
+  uint32_t pad;
+  uint64_t offset;
+  uint64_t bytes;
+  char handle[64];
+};
+
+struct IpcDone {
+  uint64_t send_id;
+  uint32_t flow;
+  uint32_t pad;
+};
+
 struct SendState {
   uint64_t id;
   Taskpool* tp;
@@ -281,7 +297,7 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
       off += (d.bytes + 7) / 8 * 8;
       r->data[f] = c;
     } else if (d.kind == FK_HOST || d.kind == FK_DEVICE) {
-      bool dev = d.kind == FK_DEVICE && g_ce->rccl_ok();
+      bool dev = d.kind == FK_DEVICE && g_ce->device_direct();
       r->data[f] = new_recv_copy(d.bytes, dev);
       get_mask |= 1u << f;
       ++r->remaining;
@@ -301,7 +317,7 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
   for (int f = 0; f < nflows; ++f) {
     if (!(get_mask & (1u << f))) continue;
     DataCopy* c = r->data[f];
-    if (c->device_index != 0) {
+    if (c->device_index != 0 && g_ce->rccl_ok()) {
       uint64_t rid = r->id;
       g_ce->rccl_recv(src, c->device_private, r->fd[f].bytes, [rid, f] {
         RecvState* rs = nullptr;
@@ -342,6 +358,18 @@ void on_get(int src, int, const void* msg, size_t) {
       g_ce->rccl_send(g.requester, c->device_private, bytes, [s] { release_send(s); });
       continue;
     }
+    if (c->device_index != 0 && g_ce->ipc_ok()) {
+      IpcMsg m{};
+      m.recv_id = g.recv_id;
+      m.send_id = g.send_id;
+      m.flow = (uint32_t)f;
+      m.bytes = bytes;
+      if (g_ce->ipc_export(c->device_private, m.handle, &m.offset) == 0) {
+        // the receiver pulls the bytes; its IPC_DONE releases this copy
+        g_ce->send_am(TAG_DATA_IPC, g.requester, &m, sizeof(m));
+        continue;
+      }
+    }
     const char* src_ptr = static_cast<const char*>(c->device_private);
     std::vector<char> staged;
     if (c->device_index != 0) {
@@ -358,6 +386,53 @@ void on_get(int src, int, const void* msg, size_t) {
     }
     release_send(s);
   }
+}
+
+// Receiver: map the sender's allocation and pull the tile (comm thread).
+void on_data_ipc(int src, int, const void* msg, size_t) {
+  IpcMsg m;
+  std::memcpy(&m, msg, sizeof(m));
+  RecvState* r = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_m);
+    auto it = g_recvs.find(m.recv_id);
+    if (it == g_recvs.end()) fatal("IPC data for unknown receive");
+    r = it->second;
+  }
+  char* base = static_cast<char*>(g_ce->ipc_open(src, m.handle));
+  DataCopy* c = r->data[m.flow];
+  const uint64_t rid = m.recv_id, sid = m.send_id;
+  const uint32_t f = m.flow;
+  const uint64_t bytes = m.bytes;
+  g_ce->ipc_copy(c->device_private, base + m.offset, bytes, [rid, sid, f, src, bytes] {
+    IpcDone d{sid, f, 0};
+    g_ce->send_am(TAG_IPC_DONE, src, &d, sizeof(d));
+    RecvState* rs = nullptr;
+    {
+      std::lock_guard<std::mutex> g(g_m);
+      auto it = g_recvs.find(rid);
+      if (it == g_recvs.end()) return;
+      rs = it->second;
+      rs->got[f] = bytes;
+      if (--rs->remaining > 0) return;
+      g_recvs.erase(it);
+    }
+    deliver(rs);
+  });
+}
+
+// Sender: the receiver finished pulling one flow.
+void on_ipc_done(int, int, const void* msg, size_t) {
+  IpcDone d;
+  std::memcpy(&d, msg, sizeof(d));
+  SendState* s = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_m);
+    auto it = g_sends.find(d.send_id);
+    if (it == g_sends.end()) fatal("IPC_DONE for unknown send %llu", (unsigned long long)d.send_id);
+    s = it->second;
+  }
+  release_send(s);
 }
 
 void on_fragment(int src, int, const void* msg, size_t len) {
@@ -473,6 +548,8 @@ int comm_init(int rank, int size, const std::string& job_id, int gpu_ordinal) {
   e->tag_register(TAG_REMOTE_DEP_ACTIVATE, on_activate);
   e->tag_register(TAG_GET_DATA, on_get);
   e->tag_register(TAG_DATA_FRAGMENT, on_fragment);
+  e->tag_register(TAG_DATA_IPC, on_data_ipc);
+  e->tag_register(TAG_IPC_DONE, on_ipc_done);
   e->tag_register(TAG_TERMDET_USER_TRIGGER, on_user_trigger);
   fourcounter_register(e);
   if (e->init() != 0) {

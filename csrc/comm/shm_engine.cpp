@@ -24,6 +24,12 @@
 
 #include <cstring>
 
+#define PARSEC_HIP_CHECK_COMM(x)                                                    \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) fatal("%s failed: %s", #x, hipGetErrorString(e_));      \
+  } while (0)
+
 namespace parsec {
 
 namespace {
@@ -68,6 +74,9 @@ ShmEngine::ShmEngine(int rank_, int size_, const std::string& job, int gpu) : jo
 
 ShmEngine::~ShmEngine() {
   stop_thread();
+  for (auto& kv : ipc_opened_) (void)hipIpcCloseMemHandle(kv.second);
+  ipc_opened_.clear();
+  if (ipc_stream_) (void)hipStreamDestroy(ipc_stream_);
   for (int r = 0; r < size; ++r)
     if (maps_[r]) munmap(maps_[r], map_len_[r]);
   shm_unlink(seg_name(job_, rank).c_str());
@@ -157,13 +166,23 @@ int ShmEngine::init() {
   });
   g_engine = this;
   start_thread();
-  if (gpu_ >= 0 && ParamRegistry::instance().reg_int("comm", "", "rccl", "Use RCCL for device-resident data (GPU->GPU over xGMI)", 1)) {
+  // device data plane: ipc (default) | rccl | host
+  const std::string plane = ParamRegistry::instance().reg_string("comm", "", "device_plane", "Data plane for device-resident tiles: ipc, rccl or host", "ipc");
+  if (gpu_ >= 0 && plane == "rccl") {
     std::atomic<int> rc{1};
     std::atomic<bool> done{false};
     post([&] { rc = init_rccl(); done = true; });
     while (!done.load()) std::this_thread::sleep_for(std::chrono::microseconds(200));
     rccl_ok_ = rc.load() == 0;
-    if (!rccl_ok_) warning("RCCL data plane unavailable (rc=%d): device tiles will be staged through host memory", rc.load());
+    if (rccl_ok_) plane_ = PLANE_RCCL;
+    else warning("RCCL data plane unavailable (rc=%d): device tiles will be staged through host memory", rc.load());
+  } else if (gpu_ >= 0 && plane == "ipc") {
+    std::atomic<int> rc{1};
+    std::atomic<bool> done{false};
+    post([&] { rc = init_ipc(); done = true; });
+    while (!done.load()) std::this_thread::sleep_for(std::chrono::microseconds(200));
+    if (rc.load() == 0) plane_ = PLANE_IPC;
+    else warning("IPC data plane unavailable (rc=%d): device tiles will be staged through host memory", rc.load());
   }
   sync();
   return 0;
@@ -291,6 +310,17 @@ int ShmEngine::progress() {
       ++n;
     }
   }
+  // IPC copies
+  while (!ipc_q_.empty()) {
+    hipError_t e = hipEventQuery(ipc_q_.front().ev);
+    if (e == hipErrorNotReady) break;
+    if (e != hipSuccess) fatal("IPC copy failed: %s", hipGetErrorString(e));
+    Xfer x = std::move(ipc_q_.front());
+    ipc_q_.pop_front();
+    ev_pool_.push_back(x.ev);
+    x.done();
+    ++n;
+  }
   // RCCL transfers
   if (rccl_ok_) {
     for (int p = 0; p < size; ++p) {
@@ -361,6 +391,57 @@ uint64_t ShmEngine::allreduce_max(uint64_t v) {
   }
   coll_cv_.wait(g, [&] { return coll_done_epoch_ >= epoch; });
   return coll_result_;
+}
+
+// ------------------------------------------------------------------- IPC
+int ShmEngine::init_ipc() {
+  if (hipSetDevice(gpu_) != hipSuccess) return -1;
+  if (hipStreamCreateWithFlags(&ipc_stream_, hipStreamNonBlocking) != hipSuccess) return -2;
+  return 0;
+}
+
+int ShmEngine::ipc_export(const void* ptr, void* handle64, uint64_t* offset) {
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess || !base) return -1;
+  auto key = std::make_pair((uintptr_t)base, size);
+  auto it = ipc_exported_.find(key);
+  if (it == ipc_exported_.end()) {
+    hipIpcMemHandle_t h;
+    hipError_t e = hipIpcGetMemHandle(&h, (void*)base);
+    if (e != hipSuccess) { warning("hipIpcGetMemHandle failed: %s", hipGetErrorString(e)); return -2; }
+    std::array<char, 64> a{};
+    static_assert(sizeof(h) <= 64, "ipc handle size");
+    std::memcpy(a.data(), &h, sizeof(h));
+    it = ipc_exported_.emplace(key, a).first;
+  }
+  std::memcpy(handle64, it->second.data(), 64);
+  *offset = (uint64_t)((uintptr_t)ptr - (uintptr_t)base);
+  return 0;
+}
+
+void* ShmEngine::ipc_open(int src, const void* handle64) {
+  std::string k((const char*)handle64, 64);
+  auto key = std::make_pair(src, k);
+  auto it = ipc_opened_.find(key);
+  if (it != ipc_opened_.end()) return it->second;
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle64, sizeof(h));
+  void* p = nullptr;
+  hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+  if (e != hipSuccess) fatal("hipIpcOpenMemHandle (from rank %d) failed: %s", src, hipGetErrorString(e));
+  ipc_opened_[key] = p;
+  return p;
+}
+
+int ShmEngine::ipc_copy(void* dst, const void* src, size_t bytes, std::function<void()> done) {
+  hipEvent_t ev;
+  if (!ev_pool_.empty()) { ev = ev_pool_.back(); ev_pool_.pop_back(); }
+  else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1;
+  PARSEC_HIP_CHECK_COMM(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, ipc_stream_));
+  (void)hipEventRecord(ev, ipc_stream_);
+  ipc_q_.push_back(Xfer{ev, std::move(done)});
+  return 0;
 }
 
 // ------------------------------------------------------------------ RCCL

@@ -3,7 +3,9 @@
 #pragma once
 #include <hip/hip_runtime_api.h>
 
+#include <array>
 #include <deque>
+#include <map>
 #include <thread>
 
 #include "comm.hpp"
@@ -43,7 +45,18 @@ class ShmEngine : public CommEngine {
   void post(std::function<void()> fn);  // run on the comm thread
   bool on_comm_thread() const { return std::this_thread::get_id() == thread_id_; }
   size_t max_fragment() const { return ring_bytes_ / 4; }
-  // RCCL data plane (comm thread only)
+  // Device data planes (comm thread only). IPC: the sender exports the tile's
+  // allocation (hipIpcGetMemHandle), the receiver maps it once and pulls the
+  // bytes with an async D2D copy (xGMI between GPUs). RCCL: pair communicators.
+  enum DevicePlane { PLANE_HOST = 0, PLANE_IPC = 1, PLANE_RCCL = 2 };
+  int device_plane() const { return plane_; }
+  bool device_direct() const { return plane_ != PLANE_HOST; }
+  bool ipc_ok() const { return plane_ == PLANE_IPC; }
+  // IPC: export (handle + offset of `ptr` inside its allocation), open a peer's
+  // handle (cached), and enqueue a device copy with a completion callback.
+  int ipc_export(const void* ptr, void* handle64, uint64_t* offset);
+  void* ipc_open(int src, const void* handle64);
+  int ipc_copy(void* dst, const void* src, size_t bytes, std::function<void()> done);
   bool rccl_ok() const { return rccl_ok_; }
   int rccl_send(int peer, const void* buf, size_t bytes, std::function<void()> done);
   int rccl_recv(int peer, void* buf, size_t bytes, std::function<void()> done);
@@ -90,6 +103,13 @@ class ShmEngine : public CommEngine {
   uint64_t coll_result_ = 0;
   int coll_arrived_ = 0;
   uint64_t coll_acc_ = 0;
+  // IPC
+  int plane_ = PLANE_HOST;
+  hipStream_t ipc_stream_ = nullptr;
+  std::deque<Xfer> ipc_q_;
+  std::map<std::pair<uintptr_t, size_t>, std::array<char, 64>> ipc_exported_;  // (base, size) -> handle
+  std::map<std::pair<int, std::string>, void*> ipc_opened_;                    // (src, handle) -> base
+  int init_ipc();
   // RCCL
   bool rccl_ok_ = false;
   std::vector<void*> send_comm_, recv_comm_;  // ncclComm_t per peer
