@@ -13,6 +13,9 @@
 #include <cmath>
 #include <cstring>
 #include <memory>
+#include <vector>
+
+#include "../core/mca.hpp"
 
 #include "../device/device.hpp"
 #include "linalg.hpp"
@@ -51,6 +54,24 @@ static void cpu_trsm(const double* L, int ldl, double* B, int m, int n, int ldb)
       for (int i = 0; i < m; ++i) B[i + (size_t)k * ldb] -= B[i + (size_t)j * ldb] * l;
     }
   }
+}
+// B (m x n) := B W (W n x n), row by row through a scratch row
+static void cpu_gemm_right_inplace(double* B, int m, int n, int ldb, const double* W, int ldw) {
+  std::vector<double> row(n);
+  for (int i = 0; i < m; ++i) {
+    for (int p = 0; p < n; ++p) row[p] = B[i + (size_t)p * ldb];
+    for (int j = 0; j < n; ++j) {
+      double s = 0;
+      for (int p = 0; p <= j; ++p) s += row[p] * W[p + (size_t)j * ldw];  // W is upper triangular
+      B[i + (size_t)j * ldb] = s;
+    }
+  }
+}
+// W (n x n, ld n) := L^-T
+static void cpu_inverse_t(const double* L, int ldl, double* W, int n) {
+  for (int j = 0; j < n; ++j)
+    for (int i = 0; i < n; ++i) W[i + (size_t)j * n] = i == j ? 1.0 : 0.0;
+  cpu_trsm(L, ldl, W, n, n, n);
 }
 // C (m x n) += alpha A B^T (lower_only: i >= j)
 static void cpu_gemm_nt(double alpha, const double* A, int lda, const double* B, int ldb, double* C, int ldc, int m, int n, int k, bool lower) {
@@ -104,6 +125,15 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
   }
   const int64_t NT = A->nt;
   const int64_t nb = A->nb;
+  // Panel solves through W = L(k,k)^-T: POTRF(k) also writes W (a NEW tile sent
+  // to the TRSMs of its column instead of L), and every TRSM(m,k) becomes one
+  // GEMM, A(m,k) := A(m,k) W, batched with the other panel tiles.
+  const bool use_w = ParamRegistry::instance().reg_int("dpotrf", "", "trsm_inverse",
+      "Panel TRSM as a GEMM with the explicit inverse L^-T computed by POTRF (1) or a blocked solve (0)", 1) != 0 && NT > 1;
+  if (use_w) {
+    tp->arenas_datatypes.resize(1);
+    add2arena_rect(tp->arenas_datatypes[0], sizeof(double), nb, nb, nb);
+  }
   auto nt1 = cst(NT - 1);
   auto ntm2 = cst(NT - 2);
   auto rows = [A](int64_t m) { return (int)A->tile_rows(m); };
@@ -125,13 +155,22 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
     FlowDef T;
     T.name = "T"; T.access = FLOW_RW;
     T.in = {cond([](const Taskpool*, const int32_t* L) { return L[0] == 0; }, data(A, loc(0), loc(0)), task("SYRK", "T", {val(locp(0, -1)), val(loc(0))}))};
-    T.out = {always(task("TRSM", "T", {rng(locp(0, 1), nt1), val(loc(0))})), always(data(A, loc(0), loc(0)))};
+    if (use_w) T.out = {always(data(A, loc(0), loc(0)))};
+    else T.out = {always(task("TRSM", "T", {rng(locp(0, 1), nt1), val(loc(0))})), always(data(A, loc(0), loc(0)))};
     d.flows = {T};
+    if (use_w) {
+      FlowDef W;
+      W.name = "W"; W.access = FLOW_WRITE;
+      W.in = {always(newbuf(0))};
+      W.out = {when([NT](const Taskpool*, const int32_t* L) { return L[0] < NT - 1; }, task("TRSM", "W", {rng(locp(0, 1), nt1), val(loc(0))}))};
+      d.flows.push_back(W);
+    }
     BodyDef g;
     g.type = DEV_HIP;
-    g.gpu = [rows, ld, info_dev, self](GpuExecContext* c, Task* t) {
+    g.gpu = [rows, ld, info_dev, self, use_w, NT](GpuExecContext* c, Task* t) {
       int k = t->locals[0];
       PotrfDesc pd{static_cast<double*>(c->ptr(0)), rows(k), (int)ld, info_dev};
+      if (use_w && k < NT - 1) { pd.W_out = static_cast<double*>(c->ptr(1)); pd.ldw = rows(k); }
       if (self->invbuf && c->device->device_index == self->info_dev_index) {
         pd.invD_out = self->invbuf + self->inv_stride * k;
         self->inv_ready[k].store(1, std::memory_order_release);
@@ -141,10 +180,11 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
     };
     BodyDef cpu;
     cpu.type = DEV_CPU;
-    cpu.cpu = [rows, ld, self](ExecutionStream*, Task* t) {
+    cpu.cpu = [rows, ld, self, use_w, NT](ExecutionStream*, Task* t) {
       int k = t->locals[0];
       int info = cpu_potrf(fptr(t, 0), rows(k), (int)ld);
       if (info) { int exp = 0; self->info_cpu.compare_exchange_strong(exp, (int)(k * ld + info)); }
+      if (use_w && k < NT - 1) cpu_inverse_t(fptr(t, 0), (int)ld, fptr(t, 1), rows(k));
       return HOOK_DONE;
     };
     d.bodies = {g, cpu};
@@ -162,8 +202,8 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
     d.priority = [prio, NT](const Taskpool*, const int32_t* L) { int64_t k = L[0], m = L[1]; return prio(m) + 3 * ((2 * NT) - k - m - 1) * (m - k) + (m == k + 1 ? (int64_t)1 << 29 : 0); };
     d.flags = TC_HIGH_PRIORITY;
     FlowDef T;
-    T.name = "T"; T.access = FLOW_READ;
-    T.in = {always(task("POTRF", "T", {val(loc(0))}))};
+    T.name = use_w ? "W" : "T"; T.access = FLOW_READ;
+    T.in = {always(task("POTRF", use_w ? "W" : "T", {val(loc(0))}))};
     FlowDef C;
     C.name = "C"; C.access = FLOW_RW;
     C.in = {cond([](const Taskpool*, const int32_t* L) { return L[0] == 0; }, data(A, loc(1), loc(0)), task("GEMM", "C", {val(loc(1)), val(loc(0)), val(locp(0, -1))}))};
@@ -174,8 +214,13 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
     d.flows = {T, C};
     BodyDef g;
     g.type = DEV_HIP;
-    g.gpu = [rows, cols, ld, self](GpuExecContext* c, Task* t) {
+    g.gpu = [rows, cols, ld, self, use_w](GpuExecContext* c, Task* t) {
       int k = t->locals[0], m = t->locals[1];
+      if (use_w) {
+        TrsmGemmDesc w{static_cast<double*>(c->ptr(1)), static_cast<const double*>(c->ptr(0)), rows(m), cols(k), (int)ld, cols(k)};
+        c->batch->trsm_w.push_back(w);
+        return HOOK_DONE;
+      }
       TrsmDesc td;
       if (self->invbuf && c->device->device_index == self->info_dev_index && self->inv_ready[k].load(std::memory_order_acquire))
         td.invD = self->invbuf + self->inv_stride * k;
@@ -187,9 +232,10 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
     };
     BodyDef cpu;
     cpu.type = DEV_CPU;
-    cpu.cpu = [rows, cols, ld](ExecutionStream*, Task* t) {
+    cpu.cpu = [rows, cols, ld, use_w](ExecutionStream*, Task* t) {
       int k = t->locals[0], m = t->locals[1];
-      cpu_trsm(fptr(t, 0), (int)ld, fptr(t, 1), rows(m), cols(k), (int)ld);
+      if (use_w) cpu_gemm_right_inplace(fptr(t, 1), rows(m), cols(k), (int)ld, fptr(t, 0), cols(k));
+      else cpu_trsm(fptr(t, 0), (int)ld, fptr(t, 1), rows(m), cols(k), (int)ld);
       return HOOK_DONE;
     };
     d.bodies = {g, cpu};

@@ -404,7 +404,7 @@ void on_data_ipc(int src, int, const void* msg, size_t) {
   const uint64_t rid = m.recv_id, sid = m.send_id;
   const uint32_t f = m.flow;
   const uint64_t bytes = m.bytes;
-  g_ce->ipc_copy(c->device_private, base + m.offset, bytes, [rid, sid, f, src, bytes] {
+  g_ce->ipc_copy(src, c->device_private, base + m.offset, bytes, [rid, sid, f, src, bytes] {
     IpcDone d{sid, f, 0};
     g_ce->send_am(TAG_IPC_DONE, src, &d, sizeof(d));
     RecvState* rs = nullptr;

@@ -76,7 +76,7 @@ ShmEngine::~ShmEngine() {
   stop_thread();
   for (auto& kv : ipc_opened_) (void)hipIpcCloseMemHandle(kv.second);
   ipc_opened_.clear();
-  if (ipc_stream_) (void)hipStreamDestroy(ipc_stream_);
+  for (auto st : ipc_stream_) if (st) (void)hipStreamDestroy(st);
   for (int r = 0; r < size; ++r)
     if (maps_[r]) munmap(maps_[r], map_len_[r]);
   shm_unlink(seg_name(job_, rank).c_str());
@@ -310,16 +310,18 @@ int ShmEngine::progress() {
       ++n;
     }
   }
-  // IPC copies
-  while (!ipc_q_.empty()) {
-    hipError_t e = hipEventQuery(ipc_q_.front().ev);
-    if (e == hipErrorNotReady) break;
-    if (e != hipSuccess) fatal("IPC copy failed: %s", hipGetErrorString(e));
-    Xfer x = std::move(ipc_q_.front());
-    ipc_q_.pop_front();
-    ev_pool_.push_back(x.ev);
-    x.done();
-    ++n;
+  // IPC copies (per source rank, completed in stream order)
+  for (auto& q : ipc_q_) {
+    while (!q.empty()) {
+      hipError_t e = hipEventQuery(q.front().ev);
+      if (e == hipErrorNotReady) break;
+      if (e != hipSuccess) fatal("IPC copy failed: %s", hipGetErrorString(e));
+      Xfer x = std::move(q.front());
+      q.pop_front();
+      ev_pool_.push_back(x.ev);
+      x.done();
+      ++n;
+    }
   }
   // RCCL transfers
   if (rccl_ok_) {
@@ -396,7 +398,15 @@ uint64_t ShmEngine::allreduce_max(uint64_t v) {
 // ------------------------------------------------------------------- IPC
 int ShmEngine::init_ipc() {
   if (hipSetDevice(gpu_) != hipSuccess) return -1;
-  if (hipStreamCreateWithFlags(&ipc_stream_, hipStreamNonBlocking) != hipSuccess) return -2;
+  ipc_stream_.assign(size, nullptr);
+  ipc_q_.resize(size);
+  int lo = 0, hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+  for (int r = 0; r < size; ++r) {
+    if (r == rank) continue;
+    // high priority: a pulled tile usually feeds the critical path (panel broadcast)
+    if (hipStreamCreateWithPriority(&ipc_stream_[r], hipStreamNonBlocking, hi) != hipSuccess) return -2;
+  }
   return 0;
 }
 
@@ -434,13 +444,15 @@ void* ShmEngine::ipc_open(int src, const void* handle64) {
   return p;
 }
 
-int ShmEngine::ipc_copy(void* dst, const void* src, size_t bytes, std::function<void()> done) {
+int ShmEngine::ipc_copy(int src_rank, void* dst, const void* src, size_t bytes, std::function<void()> done) {
+  if (src_rank < 0 || src_rank >= size || !ipc_stream_[src_rank]) return -1;
+  hipStream_t st = ipc_stream_[src_rank];
   hipEvent_t ev;
   if (!ev_pool_.empty()) { ev = ev_pool_.back(); ev_pool_.pop_back(); }
   else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1;
-  PARSEC_HIP_CHECK_COMM(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, ipc_stream_));
-  (void)hipEventRecord(ev, ipc_stream_);
-  ipc_q_.push_back(Xfer{ev, std::move(done)});
+  PARSEC_HIP_CHECK_COMM(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st));
+  (void)hipEventRecord(ev, st);
+  ipc_q_[src_rank].push_back(Xfer{ev, std::move(done)});
   return 0;
 }
 

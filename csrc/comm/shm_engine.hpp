@@ -56,7 +56,9 @@ class ShmEngine : public CommEngine {
   // handle (cached), and enqueue a device copy with a completion callback.
   int ipc_export(const void* ptr, void* handle64, uint64_t* offset);
   void* ipc_open(int src, const void* handle64);
-  int ipc_copy(void* dst, const void* src, size_t bytes, std::function<void()> done);
+  // one copy stream per source rank: pulls from different peers use different
+  // xGMI links concurrently instead of queueing behind each other
+  int ipc_copy(int src_rank, void* dst, const void* src, size_t bytes, std::function<void()> done);
   bool rccl_ok() const { return rccl_ok_; }
   int rccl_send(int peer, const void* buf, size_t bytes, std::function<void()> done);
   int rccl_recv(int peer, void* buf, size_t bytes, std::function<void()> done);
@@ -105,8 +107,8 @@ class ShmEngine : public CommEngine {
   uint64_t coll_acc_ = 0;
   // IPC
   int plane_ = PLANE_HOST;
-  hipStream_t ipc_stream_ = nullptr;
-  std::deque<Xfer> ipc_q_;
+  std::vector<hipStream_t> ipc_stream_;
+  std::vector<std::deque<Xfer>> ipc_q_;
   std::map<std::pair<uintptr_t, size_t>, std::array<char, 64>> ipc_exported_;  // (base, size) -> handle
   std::map<std::pair<int, std::string>, void*> ipc_opened_;                    // (src, handle) -> base
   int init_ipc();

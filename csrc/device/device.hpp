@@ -70,6 +70,17 @@ struct PotrfDesc {
   int n, lda;
   int* info;  // device pointer (may be null)
   double* invD_out = nullptr;  // optional: keep the 64x64 diagonal-block inverses (ceil(n/64) x 4096 doubles)
+  double* W_out = nullptr;     // optional: also write W = L^-T (n x n, upper triangular, ld ldw)
+  int ldw = 0;
+};
+
+// Panel solve through the explicit inverse: B := B * W with W = L^-T from POTRF
+// (one grouped MFMA GEMM instead of a sequential blocked solve per tile).
+struct TrsmGemmDesc {
+  double* B;
+  const double* W;
+  int m, n;  // B is m x n, W is n x n
+  int ldb, ldw;
 };
 
 // Householder QR of a tile (GEQRT: A2 == nullptr) or of a triangle on top of a
@@ -105,11 +116,12 @@ struct KernelBatch {
   std::vector<GemmDesc> gemm;
   std::vector<TrsmDesc> trsm;
   std::vector<PotrfDesc> potrf;
+  std::vector<TrsmGemmDesc> trsm_w;
   std::vector<QrPanelDesc> qr_panel;
   std::vector<QrApplyDesc> qr_apply;
   std::vector<std::function<void(hipStream_t)>> generic;  // other kernels, launched in order
-  bool empty() const { return gemm.empty() && trsm.empty() && potrf.empty() && qr_panel.empty() && qr_apply.empty() && generic.empty(); }
-  void clear() { gemm.clear(); trsm.clear(); potrf.clear(); qr_panel.clear(); qr_apply.clear(); generic.clear(); }
+  bool empty() const { return gemm.empty() && trsm.empty() && potrf.empty() && trsm_w.empty() && qr_panel.empty() && qr_apply.empty() && generic.empty(); }
+  void clear() { gemm.clear(); trsm.clear(); potrf.clear(); trsm_w.clear(); qr_panel.clear(); qr_apply.clear(); generic.clear(); }
 };
 
 struct HipDevice;

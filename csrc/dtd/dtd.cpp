@@ -17,6 +17,7 @@ static void task_unref(DtdTask* t);
 void tile_release(Tile* t) {
   if (t->refcount.fetch_sub(1) == 1) {
     if (t->is_new && t->data) data_destroy(t->data);
+    else if (t->data_ref && t->data) data_release(t->data);
     delete t;
   }
 }
@@ -131,6 +132,24 @@ Tile* DtdTaskpool::tile_of(DataCollection* dc, uint64_t key) {
       t->data->nb_elts = dc->data_size_of_key(key);
       t->is_new = true;
     }
+    m[k] = t;
+    return t;
+  });
+}
+
+Tile* DtdTaskpool::tile_of_data(Data* d) {
+  // keyed by the Data address (top bit set: disjoint from collection keys)
+  const uint64_t k = (1ull << 63) | (uint64_t)(uintptr_t)d;
+  return tiles.with(k, [&](auto& m) {
+    auto it = m.find(k);
+    if (it != m.end()) return it->second;
+    Tile* t = new Tile();
+    t->dc = nullptr;
+    t->key = k;
+    t->rank = context ? context->my_rank : 0;
+    data_retain(d);
+    t->data = d;
+    t->data_ref = true;  // the tile holds a reference on its Data
     m[k] = t;
     return t;
   });

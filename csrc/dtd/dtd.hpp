@@ -39,6 +39,7 @@ struct Tile {
   uint64_t key = 0;
   int rank = 0;
   bool is_new = false;  // parsec_dtd_tile_new
+  bool data_ref = false;  // holds a reference on an existing Data (tile_of_data)
   SpinLock lock;
   DtdTask* writer = nullptr;
   int writer_flow = -1;
@@ -121,6 +122,7 @@ class DtdTaskpool : public Taskpool {
   DtdTask* insert_task(DtdTaskClass* tc, int priority, const std::vector<Arg>& args);
   Tile* tile_of(DataCollection* dc, uint64_t key);
   Tile* tile_new(size_t bytes, int rank);
+  Tile* tile_of_data(Data* d);  // local tile tracking an existing Data (ptg_to_dtd)
   int data_flush(Tile* tile);
   int data_flush_all(DataCollection* dc);
   int wait();

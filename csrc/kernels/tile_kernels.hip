@@ -64,8 +64,14 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 }
 
 // ==================================================================== GEMM
-template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void dgemm_batch_kernel(const GemmBatchArgs args) {
+// FULL: every descriptor of the launch is a whole number of BM x BN x BK tiles
+// with 16-byte aligned operands (the host checks), so the k loop carries no
+// bounds checks and no divergent control flow around its loads.
+// NBUF = 2: double-buffered LDS, one barrier per k-tile; NBUF = 1: one LDS
+// buffer (half the LDS, two barriers per k-tile) for deeper BK.
+template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF = 2>
+__global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2))) void dgemm_batch_kernel(const GemmBatchArgs args) {
+  constexpr int NT = WM * WN * 64;
   constexpr int WTM = BM / WM;
   constexpr int WTN = BN / WN;
   constexpr int FM = WTM / 16;
@@ -74,8 +80,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
   constexpr int PADN = ((BN % 32) == 16) ? 0 : 16;
   constexpr int LDA_S = BM + PADM;
   constexpr int LDB_S = BN + PADN;
-  __shared__ double As[2][BK][LDA_S];
-  __shared__ double Bs[2][BK][LDB_S];
+  __shared__ double As[NBUF][BK][LDA_S];
+  __shared__ double Bs[NBUF][BK][LDB_S];
 
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   if (tile >= args.total_tiles) return;
@@ -96,7 +102,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
   const int M = d.m, N = d.n, K = d.k;
   const int lda = d.lda, ldb = d.ldb;
   // 16-byte loads when every row pair is aligned and fully inside the tile
-  const bool vec = ((lda | ldb) % 2 == 0) && ((((uintptr_t)A) | ((uintptr_t)B)) % 16 == 0) && (TRANSA ? (K % 2 == 0) : (M % 2 == 0)) &&
+  const bool vec = FULL || ((lda | ldb) % 2 == 0) && ((((uintptr_t)A) | ((uintptr_t)B)) % 16 == 0) && (TRANSA ? (K % 2 == 0) : (M % 2 == 0)) &&
                    (TRANSB ? (N % 2 == 0) : (K % 2 == 0));
 
   double4_t acc[FN][FM];
@@ -105,20 +111,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
 #pragma unroll
     for (int j = 0; j < FM; ++j) acc[i][j] = (double4_t){0.0, 0.0, 0.0, 0.0};
 
-  constexpr int A_PAIRS = BM * BK / 2 / 256;  // double2 per thread
-  constexpr int B_PAIRS = BN * BK / 2 / 256;
+  constexpr int A_PAIRS = BM * BK / 2 / NT;  // double2 per thread
+  constexpr int B_PAIRS = BN * BK / 2 / NT;
   static_assert(A_PAIRS >= 1 && B_PAIRS >= 1, "tile too small");
   double2_t ra[A_PAIRS], rb[B_PAIRS];
 
   auto load_tile = [&](int k0) {
 #pragma unroll
     for (int e = 0; e < A_PAIRS; ++e) {
-      int idx = tid + 256 * e;
+      int idx = tid + NT * e;
       if (TRANSA) {  // A is K x M (k contiguous): op(A)(m, k) = A[k + m*lda]
         int kk = (idx % (BK / 2)) * 2, mm = idx / (BK / 2);
         int gm = m0 + mm, gk = k0 + kk;
         const double* p = A + (size_t)gm * lda + gk;
-        if (vec && gm < M && gk + 1 < K) ra[e] = *reinterpret_cast<const double2_t*>(p);
+        if (FULL) ra[e] = *reinterpret_cast<const double2_t*>(p);
+        else if (vec && gm < M && gk + 1 < K) ra[e] = *reinterpret_cast<const double2_t*>(p);
         else {
           ra[e].x = (gm < M && gk < K) ? p[0] : 0.0;
           ra[e].y = (gm < M && gk + 1 < K) ? p[1] : 0.0;
@@ -127,7 +134,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
         int mm = (idx % (BM / 2)) * 2, kk = idx / (BM / 2);
         int gm = m0 + mm, gk = k0 + kk;
         const double* p = A + (size_t)gk * lda + gm;
-        if (vec && gk < K && gm + 1 < M) ra[e] = *reinterpret_cast<const double2_t*>(p);
+        if (FULL) ra[e] = *reinterpret_cast<const double2_t*>(p);
+        else if (vec && gk < K && gm + 1 < M) ra[e] = *reinterpret_cast<const double2_t*>(p);
         else {
           ra[e].x = (gm < M && gk < K) ? p[0] : 0.0;
           ra[e].y = (gm + 1 < M && gk < K) ? p[1] : 0.0;
@@ -136,12 +144,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
     }
 #pragma unroll
     for (int e = 0; e < B_PAIRS; ++e) {
-      int idx = tid + 256 * e;
+      int idx = tid + NT * e;
       if (TRANSB) {  // B is N x K (n contiguous)
         int nn = (idx % (BN / 2)) * 2, kk = idx / (BN / 2);
         int gn = n0 + nn, gk = k0 + kk;
         const double* p = B + (size_t)gk * ldb + gn;
-        if (vec && gk < K && gn + 1 < N) rb[e] = *reinterpret_cast<const double2_t*>(p);
+        if (FULL) rb[e] = *reinterpret_cast<const double2_t*>(p);
+        else if (vec && gk < K && gn + 1 < N) rb[e] = *reinterpret_cast<const double2_t*>(p);
         else {
           rb[e].x = (gn < N && gk < K) ? p[0] : 0.0;
           rb[e].y = (gn + 1 < N && gk < K) ? p[1] : 0.0;
@@ -150,7 +159,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
         int kk = (idx % (BK / 2)) * 2, nn = idx / (BK / 2);
         int gn = n0 + nn, gk = k0 + kk;
         const double* p = B + (size_t)gn * ldb + gk;
-        if (vec && gn < N && gk + 1 < K) rb[e] = *reinterpret_cast<const double2_t*>(p);
+        if (FULL) rb[e] = *reinterpret_cast<const double2_t*>(p);
+        else if (vec && gn < N && gk + 1 < K) rb[e] = *reinterpret_cast<const double2_t*>(p);
         else {
           rb[e].x = (gn < N && gk < K) ? p[0] : 0.0;
           rb[e].y = (gn < N && gk + 1 < K) ? p[1] : 0.0;
@@ -161,7 +171,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int e = 0; e < A_PAIRS; ++e) {
-      int idx = tid + 256 * e;
+      int idx = tid + NT * e;
       if (TRANSA) {
         int kk = (idx % (BK / 2)) * 2, mm = idx / (BK / 2);
         As[buf][kk][mm] = ra[e].x;
@@ -173,7 +183,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
     }
 #pragma unroll
     for (int e = 0; e < B_PAIRS; ++e) {
-      int idx = tid + 256 * e;
+      int idx = tid + NT * e;
       if (TRANSB) {
         int nn = (idx % (BN / 2)) * 2, kk = idx / (BN / 2);
         *reinterpret_cast<double2_t*>(&Bs[buf][kk][nn]) = rb[e];
@@ -186,12 +196,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
   };
 
   const int nkt = (K + BK - 1) / BK;
+  const int fr = lane & 15, fk = lane >> 4;
+  // Full tiles with |alpha| = 1: the accumulators start from (beta/alpha) C (exact),
+  // loaded behind the first A/B tile so the C read latency overlaps the prologue
+  // and the epilogue is a pure store (no read-modify-write tail when a batch's
+  // workgroups all finish together).
+  const bool preload = FULL && (d.alpha == 1.0 || d.alpha == -1.0);
+  double* __restrict__ C = d.C;
+  const int ldc = d.ldc;
   load_tile(0);
+  if (preload && d.beta != 0.0) {
+    const double cs = d.beta / d.alpha;
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const double* p = C + (size_t)(n0 + wn * WTN + i * 16 + fk) * ldc + (m0 + wm * WTM + j * 16 + fr);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = cs * p[(size_t)4 * r * ldc];
+      }
+  }
   store_tile(0);
   __syncthreads();
-  const int fr = lane & 15, fk = lane >> 4;
   for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
+    const int cur = NBUF == 2 ? (kt & 1) : 0;
     if (kt + 1 < nkt) load_tile((kt + 1) * BK);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
@@ -205,13 +233,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
 #pragma unroll
         for (int j = 0; j < FM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(afr[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nkt) store_tile(cur ^ 1);
-    __syncthreads();
+    if (NBUF == 2) {
+      if (kt + 1 < nkt) store_tile(cur ^ 1);
+      __syncthreads();
+    } else if (kt + 1 < nkt) {
+      __syncthreads();
+      store_tile(0);
+      __syncthreads();
+    }
   }
 
-  double* __restrict__ C = d.C;
-  const int ldc = d.ldc;
-  const double alpha = d.alpha, beta = d.beta;
+  const double alpha = d.alpha, beta = preload ? 0.0 : d.beta;
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -220,7 +252,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int gn = n0 + wn * WTN + i * 16 + fk + 4 * r;
-        if (gm < M && gn < N && (!d.lower_only || gm >= gn)) {
+        if ((FULL || (gm < M && gn < N)) && (!d.lower_only || gm >= gn)) {
           double* p = C + (size_t)gn * ldc + gm;
           double v = alpha * acc[i][j][r];
           if (beta != 0.0) v += beta * *p;
@@ -500,12 +532,52 @@ __global__ __launch_bounds__(kTrsmThreads) void dtrsm_inv_kernel(const TrsmInvAr
 }
 
 // ================================================================ launchers
-static int g_gemm_tile_policy = -1;  // -1 auto, 64, 128
+static int g_gemm_tile_policy = -1;  // -1 unset, 0 auto, 64, 128
+static int g_gemm_variant = -1;      // big-tile kernel shape (PARSEC_GEMM_VARIANT)
+static int g_gemm_full = -1;         // PARSEC_GEMM_FULL=0 disables the unchecked fast path
+static int g_gemm_big_tiles = 384;   // PARSEC_GEMM_BIG_TILES: 128x128 tiles in a launch to pick the big kernel
+
+template <int BM, int BN, int BK, int WM, int WN, int NBUF>
+static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hipStream_t stream) {
+  int total = 0;
+  bool full = g_gemm_full != 0;
+  for (int i = 0; i < n; ++i) {
+    const GemmDesc& g = descs[i];
+    full = full && g.m % BM == 0 && g.n % BN == 0 && g.k % BK == 0 && (g.lda | g.ldb) % 2 == 0 &&
+           ((uintptr_t)g.A | (uintptr_t)g.B) % 16 == 0;
+    a.d[i] = g;
+    a.tile_start[i] = total;
+    total += ((g.m + BM - 1) / BM) * ((g.n + BN - 1) / BN);
+  }
+  a.tile_start[n] = total;
+  a.total_tiles = total;
+  if (total == 0) return;
+  const int mode = (descs[0].transA ? 2 : 0) | (descs[0].transB ? 1 : 0);
+  const dim3 grid(total), block(WM * WN * 64);
+#define PARSEC_GEMM_LAUNCH(TA, TB)                                                                                    \
+  do {                                                                                                                \
+    if (full) hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF>), grid, block, 0, stream, a); \
+    else hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, false, NBUF>), grid, block, 0, stream, a);    \
+  } while (0)
+  switch (mode) {
+    case 0: PARSEC_GEMM_LAUNCH(false, false); break;
+    case 1: PARSEC_GEMM_LAUNCH(false, true); break;
+    case 2: PARSEC_GEMM_LAUNCH(true, false); break;
+    default: PARSEC_GEMM_LAUNCH(true, true); break;
+  }
+#undef PARSEC_GEMM_LAUNCH
+}
 
 static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) {
   if (g_gemm_tile_policy < 0) {
     const char* e = getenv("PARSEC_GEMM_TILE");
     g_gemm_tile_policy = e ? atoi(e) : 0;
+    e = getenv("PARSEC_GEMM_VARIANT");
+    g_gemm_variant = e ? atoi(e) : 0;
+    e = getenv("PARSEC_GEMM_FULL");
+    g_gemm_full = e ? atoi(e) : 1;
+    e = getenv("PARSEC_GEMM_BIG_TILES");
+    if (e) g_gemm_big_tiles = atoi(e);
   }
   GemmBatchArgs a;
   a.count = n;
@@ -515,34 +587,15 @@ static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) 
     t128 += ((descs[i].m + 127) / 128) * ((descs[i].n + 127) / 128);
     if (descs[i].m < 128 || descs[i].n < 128) big = false;
   }
-  int bm = (g_gemm_tile_policy == 128 || (g_gemm_tile_policy == 0 && big && t128 >= 384)) ? 128 : 64;
-  int total = 0;
-  for (int i = 0; i < n; ++i) {
-    a.d[i] = descs[i];
-    a.tile_start[i] = total;
-    total += ((descs[i].m + bm - 1) / bm) * ((descs[i].n + bm - 1) / bm);
+  const bool use_big = g_gemm_tile_policy == 128 || (g_gemm_tile_policy == 0 && big && t128 >= g_gemm_big_tiles);
+  if (!use_big) { launch_gemm_shape<64, 64, 16, 2, 2, 2>(a, descs, n, stream); return; }
+  switch (g_gemm_variant) {
+    case 1: launch_gemm_shape<128, 128, 32, 2, 2, 1>(a, descs, n, stream); break;
+    case 2: launch_gemm_shape<256, 128, 16, 4, 2, 2>(a, descs, n, stream); break;
+    case 3: launch_gemm_shape<128, 128, 32, 2, 2, 2>(a, descs, n, stream); break;
+    case 4: launch_gemm_shape<256, 128, 32, 4, 2, 1>(a, descs, n, stream); break;
+    default: launch_gemm_shape<128, 128, 16, 2, 2, 2>(a, descs, n, stream); break;
   }
-  a.tile_start[n] = total;
-  a.total_tiles = total;
-  if (total == 0) return;
-  const int mode = (descs[0].transA ? 2 : 0) | (descs[0].transB ? 1 : 0);
-#define PARSEC_GEMM_LAUNCH(BMV, TA, TB) hipLaunchKernelGGL((dgemm_batch_kernel<BMV, BMV, 16, 2, 2, TA, TB>), dim3(total), dim3(256), 0, stream, a)
-  if (bm == 128) {
-    switch (mode) {
-      case 0: PARSEC_GEMM_LAUNCH(128, false, false); break;
-      case 1: PARSEC_GEMM_LAUNCH(128, false, true); break;
-      case 2: PARSEC_GEMM_LAUNCH(128, true, false); break;
-      default: PARSEC_GEMM_LAUNCH(128, true, true); break;
-    }
-  } else {
-    switch (mode) {
-      case 0: PARSEC_GEMM_LAUNCH(64, false, false); break;
-      case 1: PARSEC_GEMM_LAUNCH(64, false, true); break;
-      case 2: PARSEC_GEMM_LAUNCH(64, true, false); break;
-      default: PARSEC_GEMM_LAUNCH(64, true, true); break;
-    }
-  }
-#undef PARSEC_GEMM_LAUNCH
 }
 
 // Group descriptors by (transA, transB): one grouped launch per combination.
@@ -557,7 +610,7 @@ static constexpr int kTrsmRows = 16;
 static constexpr int kTrsmMaxCols = 18 * 64;  // LDS bound: (18*64*16 + 1024) doubles < 160 KiB
 
 // invD[i] must already hold the inverted diagonal blocks of descs[i].L
-static void launch_trsm_inv(const TrsmDesc* descs, const double* const* invD, int n, hipStream_t stream) {
+void launch_trsm_inv(const TrsmDesc* descs, const double* const* invD, int n, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)dtrsm_inv_kernel<kTrsmRows>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -616,13 +669,46 @@ void launch_trsm_batch(const TrsmDesc* descs, int n, hipStream_t stream, double*
   launch_trsm_inv(descs, inv.data(), n, stream);
 }
 
+__global__ void set_identity_kernel(double* W, int n, int ldw) {
+  const int j = blockIdx.y;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) W[(size_t)j * ldw + i] = i == j ? 1.0 : 0.0;
+}
+
+constexpr int kMaxCopyBatch = 64;
+struct CopyBatchArgs {
+  int count;
+  int rows[kMaxCopyBatch], cols[kMaxCopyBatch], ld_src[kMaxCopyBatch];
+  const double* src[kMaxCopyBatch];
+  double* dst[kMaxCopyBatch];  // packed (ld = rows)
+};
+static_assert(sizeof(CopyBatchArgs) <= 4096, "CopyBatchArgs exceeds the kernel argument limit");
+
+// blockIdx.y = tile, blockIdx.x strides over columns; one wave-row per column.
+__global__ __launch_bounds__(256) void copy_tiles_kernel(const CopyBatchArgs a) {
+  const int t = blockIdx.y;
+  const int rows = a.rows[t], cols = a.cols[t], lds = a.ld_src[t];
+  const double* __restrict__ s = a.src[t];
+  double* __restrict__ d = a.dst[t];
+  for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cols; c += gridDim.x * 4)
+    for (int r = threadIdx.x & 63; r < rows; r += 64) d[(size_t)c * rows + r] = s[(size_t)c * lds + r];
+}
+
+size_t potrf_workspace_bytes(const PotrfDesc& p) {
+  if (p.W_out && !p.invD_out) return (size_t)((p.n + 63) / 64) * 4096 * sizeof(double);
+  return 4096 * sizeof(double);
+}
+
 // Blocked tile Cholesky (lower). ws needs 4096 doubles unless p.invD_out keeps
-// every diagonal-block inverse (then the panel TRSMs can reuse them).
+// every diagonal-block inverse (then the panel TRSMs can reuse them); with W_out
+// and no invD_out it needs every block inverse (potrf_workspace_bytes).
+void launch_trsm_inv(const TrsmDesc* descs, const double* const* invD, int n, hipStream_t stream);
 void launch_potrf(const PotrfDesc& p, hipStream_t stream, double* ws) {
   const int JB = 64;
+  const bool keep_all = p.invD_out || p.W_out;
+  double* inv_base = p.invD_out ? p.invD_out : ws;
   for (int j = 0; j < p.n; j += JB) {
     const int jb = std::min(JB, p.n - j);
-    double* inv = p.invD_out ? p.invD_out + (size_t)(j / JB) * 4096 : ws;
+    double* inv = keep_all ? inv_base + (size_t)(j / JB) * 4096 : ws;
     hipLaunchKernelGGL(dpotrf_diag_inv_kernel, dim3(1), dim3(kDiagThreads), 0, stream, p.A, p.lda, j, jb, inv, p.info);
     const int rest = p.n - j - jb;
     if (rest <= 0) break;
@@ -638,18 +724,64 @@ void launch_potrf(const PotrfDesc& p, hipStream_t stream, double* ws) {
     g.alpha = -1.0; g.beta = 1.0; g.transA = 0; g.transB = 1; g.lower_only = 1; g.pad = 0;
     launch_gemm_batch(&g, 1, stream);
   }
+  if (p.W_out) {
+    // W = I L^-T with the diagonal-block inverses just computed
+    hipLaunchKernelGGL(set_identity_kernel, dim3((p.n + 255) / 256, p.n), dim3(256), 0, stream, p.W_out, p.n, p.ldw);
+    TrsmDesc t;
+    t.L = p.A; t.B = p.W_out; t.m = p.n; t.n = p.n; t.ldl = p.lda; t.ldb = p.ldw; t.trans = 1;
+    const double* cinv = inv_base;
+    launch_trsm_inv(&t, &cinv, 1, stream);
+  }
+}
+
+size_t trsm_w_workspace_bytes(const TrsmGemmDesc* d, int n) {
+  size_t b = 0;
+  for (int i = 0; i < n; ++i) b += ((size_t)d[i].m * d[i].n * sizeof(double) + 255) / 256 * 256;
+  return b;
+}
+
+// B := B W for every descriptor: copy the B tiles into the workspace, then one
+// grouped GEMM writes B from (copy x W).
+void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, double* ws) {
+  for (int s0 = 0; s0 < n; s0 += kMaxCopyBatch) {
+    const int cnt = std::min(kMaxCopyBatch, n - s0);
+    CopyBatchArgs ca;
+    ca.count = cnt;
+    std::vector<GemmDesc> g(cnt);
+    char* p = reinterpret_cast<char*>(ws);
+    int maxc = 1;
+    for (int i = 0; i < cnt; ++i) {
+      const TrsmGemmDesc& t = d[s0 + i];
+      ca.rows[i] = t.m; ca.cols[i] = t.n; ca.ld_src[i] = t.ldb;
+      ca.src[i] = t.B; ca.dst[i] = reinterpret_cast<double*>(p);
+      maxc = std::max(maxc, t.n);
+      GemmDesc& e = g[i];
+      e.A = ca.dst[i]; e.B = t.W; e.C = t.B;
+      e.m = t.m; e.n = t.n; e.k = t.n;
+      e.lda = t.m; e.ldb = t.ldw; e.ldc = t.ldb;
+      e.alpha = 1.0; e.beta = 0.0; e.transA = 0; e.transB = 0; e.lower_only = 0; e.pad = 0;
+      p += ((size_t)t.m * t.n * sizeof(double) + 255) / 256 * 256;
+    }
+    hipLaunchKernelGGL(copy_tiles_kernel, dim3(std::min(256, (maxc + 3) / 4), cnt), dim3(256), 0, stream, ca);
+    launch_gemm_batch(g.data(), cnt, stream);
+  }
 }
 
 }  // namespace kern
 
 namespace kern {
+size_t potrf_workspace_bytes(const PotrfDesc& p);
+size_t trsm_w_workspace_bytes(const TrsmGemmDesc* d, int n);
+void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, double* ws);
 void launch_qr_panel(const QrPanelDesc* descs, int n, hipStream_t stream);
 void launch_qr_apply(const QrApplyDesc* descs, int n, hipStream_t stream, double* ws);
 size_t qr_apply_workspace_bytes(const QrApplyDesc* descs, int n);
 }  // namespace kern
 
 size_t kernel_batch_workspace_bytes(const KernelBatch& b) {
-  size_t w = b.potrf.empty() ? 0 : 4096 * sizeof(double);
+  size_t w = 0;
+  for (auto& p : b.potrf) w = std::max(w, kern::potrf_workspace_bytes(p));
+  if (!b.trsm_w.empty()) w = std::max(w, kern::trsm_w_workspace_bytes(b.trsm_w.data(), (int)b.trsm_w.size()));
   w = std::max(w, kern::trsm_workspace_bytes(b.trsm.data(), (int)b.trsm.size()));
   return std::max(w, kern::qr_apply_workspace_bytes(b.qr_apply.data(), (int)b.qr_apply.size()));
 }
@@ -660,6 +792,7 @@ void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal,
   for (auto& p : b.potrf) kern::launch_potrf(p, stream, static_cast<double*>(ws));
   if (!b.qr_panel.empty()) kern::launch_qr_panel(b.qr_panel.data(), (int)b.qr_panel.size(), stream);
   if (!b.trsm.empty()) kern::launch_trsm_batch(b.trsm.data(), (int)b.trsm.size(), stream, static_cast<double*>(ws));
+  if (!b.trsm_w.empty()) kern::launch_trsm_w_batch(b.trsm_w.data(), (int)b.trsm_w.size(), stream, static_cast<double*>(ws));
   if (!b.qr_apply.empty()) kern::launch_qr_apply(b.qr_apply.data(), (int)b.qr_apply.size(), stream, static_cast<double*>(ws));
   if (!b.gemm.empty()) kern::launch_gemm_batch(b.gemm.data(), (int)b.gemm.size(), stream);
   for (auto& g : b.generic) g(stream);
