@@ -328,6 +328,7 @@ int context_add_taskpool(Context* ctx, Taskpool* tp) {
   remote_dep_new_taskpool(ctx, tp);
   std::vector<Task*> ready;
   tp->startup(ctx, ready);
+  if (ptg_to_dtd_enabled()) ptg_to_dtd_taskpool_init(ctx, tp);
   if (!ready.empty()) {
     ExecutionStream* es = my_execution_stream();
     if (!es || es->ctx != ctx) es = ctx->all_es[0];

@@ -199,13 +199,14 @@ int pins_register_callback(int event, PinsCallback cb) {
   return 0;
 }
 
-std::vector<std::string> pins_modules_available() { return {"task_profiler", "print_steals", "alperf", "iterators_checker"}; }
+std::vector<std::string> pins_modules_available() { return {"task_profiler", "print_steals", "alperf", "iterators_checker", "ptg_to_dtd"}; }
 
 std::vector<std::pair<std::string, int64_t>> pins_counters() {
   auto& s = PS();
   std::lock_guard<std::mutex> g(s.m);
   std::vector<std::pair<std::string, int64_t>> out;
   for (auto& kv : s.counters) out.emplace_back(kv.first, kv.second->load());
+  if (ptg_to_dtd_redirected() > 0) out.emplace_back("ptg_to_dtd.redirected", ptg_to_dtd_redirected());
   return out;
 }
 
@@ -218,7 +219,7 @@ static void trace_task(ExecutionStream* es, Task* t, bool begin) {
 
 void pins_init(Context* ctx) {
   (void)ctx;
-  std::string mods = ParamRegistry::instance().reg_string("mca", "", "pins", "Comma separated PINS modules: task_profiler,print_steals,alperf,iterators_checker", "");
+  std::string mods = ParamRegistry::instance().reg_string("mca", "", "pins", "Comma separated PINS modules: task_profiler,print_steals,alperf,iterators_checker,ptg_to_dtd", "");
   auto& s = PS();
   std::stringstream ss(mods);
   std::string m;
@@ -267,13 +268,18 @@ void pins_init(Context* ctx) {
           if (!found) warning("iterators_checker: %s -> %s has no matching predecessor", t->task_class->describe(t).c_str(), v.tc->name.c_str());
         });
       });
+    } else if (m == "ptg_to_dtd") {
+      ptg_to_dtd_enable(true);
     } else {
       warning("unknown PINS module '%s'", m.c_str());
     }
   }
 }
 
-void pins_fini(Context* ctx) { (void)ctx; }
+void pins_fini(Context* ctx) {
+  (void)ctx;
+  ptg_to_dtd_enable(false);
+}
 
 // ================================================================ grapher
 namespace {

@@ -65,6 +65,12 @@ std::vector<std::string> pins_modules_available();
 // counters exposed by the alperf / print_steals modules
 std::vector<std::pair<std::string, int64_t>> pins_counters();
 
+// ptg_to_dtd PINS module (ptg_to_dtd.cpp)
+void ptg_to_dtd_enable(bool on);
+bool ptg_to_dtd_enabled();
+int64_t ptg_to_dtd_redirected();
+void ptg_to_dtd_taskpool_init(Context* ctx, Taskpool* tp);
+
 // DOT grapher
 void grapher_init(Context* ctx);
 void grapher_task(ExecutionStream* es, Task* t);

@@ -31,6 +31,7 @@ CORE_SOURCES = [
     "csrc/device/device.cpp",
     "csrc/device/hip_device.cpp",
     "csrc/prof/profiling.cpp",
+    "csrc/prof/ptg_to_dtd.cpp",
     "csrc/comm/remote_dep.cpp",
     "csrc/comm/shm_engine.cpp",
     "csrc/comm/fourcounter.cpp",

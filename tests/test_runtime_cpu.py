@@ -303,6 +303,31 @@ def test_pins_alperf_counts(pa):
     assert hits and hits[0] == 25
 
 
+def test_pins_ptg_to_dtd(pa):
+    """--mca mca_pins ptg_to_dtd: every ready PTG task is re-inserted as a DTD
+    task (tiles from its resolved data, access from its flows) and completes
+    the PTG task when it runs (reference mca/pins/ptg_to_dtd). A tiled Cholesky
+    must still factor correctly, with every task redirected."""
+    pa.mca_set("mca_pins", "ptg_to_dtd")
+    try:
+        ctx = _ctx(pa, 4)
+    finally:
+        pa.mca_unset("mca_pins")
+    N, nb = 128, 16
+    A, S = _spd_matrix(pa, N, nb, 7)
+    tp, info = pa.dpotrf_new(A, pa.MATRIX_LOWER)
+    ctx.add_taskpool(tp)
+    ctx.start()
+    ctx.wait()
+    counters = dict(pa.pins_counters())
+    assert pa.read_int(info) == 0
+    L = _lower_of(A, N, nb)
+    ctx.fini()
+    assert np.linalg.norm(L @ L.T - S) / np.linalg.norm(S) < 1e-13
+    NT = N // nb
+    assert counters.get("ptg_to_dtd.redirected", 0) >= NT * (NT + 1) * (NT + 2) // 6
+
+
 def test_properties_dictionary(pa):
     pa.properties_set("test.flops", 12.5)
     props = dict(pa.properties())
