@@ -55,23 +55,25 @@ static void cpu_trsm(const double* L, int ldl, double* B, int m, int n, int ldb)
     }
   }
 }
-// B (m x n) := B W (W n x n), row by row through a scratch row
+// B (m x n) := B W^T (W n x n lower triangular), row by row through a scratch row
 static void cpu_gemm_right_inplace(double* B, int m, int n, int ldb, const double* W, int ldw) {
   std::vector<double> row(n);
   for (int i = 0; i < m; ++i) {
     for (int p = 0; p < n; ++p) row[p] = B[i + (size_t)p * ldb];
     for (int j = 0; j < n; ++j) {
       double s = 0;
-      for (int p = 0; p <= j; ++p) s += row[p] * W[p + (size_t)j * ldw];  // W is upper triangular
+      for (int p = 0; p <= j; ++p) s += row[p] * W[j + (size_t)p * ldw];
       B[i + (size_t)j * ldb] = s;
     }
   }
 }
-// W (n x n, ld n) := L^-T
-static void cpu_inverse_t(const double* L, int ldl, double* W, int n) {
+// W (n x n, ld n) := L^-1 (lower, zero above the diagonal)
+static void cpu_inverse(const double* L, int ldl, double* W, int n) {
+  std::vector<double> T((size_t)n * n, 0.0);  // T = I L^-T = (L^-1)^T
+  for (int j = 0; j < n; ++j) T[j + (size_t)j * n] = 1.0;
+  cpu_trsm(L, ldl, T.data(), n, n, n);
   for (int j = 0; j < n; ++j)
-    for (int i = 0; i < n; ++i) W[i + (size_t)j * n] = i == j ? 1.0 : 0.0;
-  cpu_trsm(L, ldl, W, n, n, n);
+    for (int i = 0; i < n; ++i) W[i + (size_t)j * n] = i >= j ? T[j + (size_t)i * n] : 0.0;
 }
 // C (m x n) += alpha A B^T (lower_only: i >= j)
 static void cpu_gemm_nt(double alpha, const double* A, int lda, const double* B, int ldb, double* C, int ldc, int m, int n, int k, bool lower) {
@@ -125,9 +127,9 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
   }
   const int64_t NT = A->nt;
   const int64_t nb = A->nb;
-  // Panel solves through W = L(k,k)^-T: POTRF(k) also writes W (a NEW tile sent
+  // Panel solves through W = L(k,k)^-1: POTRF(k) also writes W (a NEW tile sent
   // to the TRSMs of its column instead of L), and every TRSM(m,k) becomes one
-  // GEMM, A(m,k) := A(m,k) W, batched with the other panel tiles.
+  // GEMM, A(m,k) := A(m,k) W^T, batched with the other panel tiles.
   const bool use_w = ParamRegistry::instance().reg_int("dpotrf", "", "trsm_inverse",
       "Panel TRSM as a GEMM with the explicit inverse L^-T computed by POTRF (1) or a blocked solve (0)", 1) != 0 && NT > 1;
   if (use_w) {
@@ -184,7 +186,7 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
       int k = t->locals[0];
       int info = cpu_potrf(fptr(t, 0), rows(k), (int)ld);
       if (info) { int exp = 0; self->info_cpu.compare_exchange_strong(exp, (int)(k * ld + info)); }
-      if (use_w && k < NT - 1) cpu_inverse_t(fptr(t, 0), (int)ld, fptr(t, 1), rows(k));
+      if (use_w && k < NT - 1) cpu_inverse(fptr(t, 0), (int)ld, fptr(t, 1), rows(k));
       return HOOK_DONE;
     };
     d.bodies = {g, cpu};

@@ -513,6 +513,7 @@ struct Context {
   std::vector<std::function<void(void*)>> at_fini;
   std::vector<void*> at_fini_data;
   bool keep_highest_priority_task = true;
+  bool manager_inline_gpu = true;  // GPU managers dispatch GPU-bound successors themselves
   int comm_bcast_topology = 0;  // 0 star, 1 chain, 2 binomial
   std::vector<int> core_bindings;
   std::string grapher_file;     // DOT output

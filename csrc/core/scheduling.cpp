@@ -102,6 +102,26 @@ int schedule_tasks(ExecutionStream* es, Task** tasks, int n, int32_t distance) {
     es = my_execution_stream();
     if (!es) es = tasks[0]->taskpool->context->all_es[0];
   }
+  if (es->is_manager && es->ctx->manager_inline_gpu && !es->ctx->simulation) {
+    // A GPU manager releasing successors whose first usable chore is a GPU chore
+    // prepares and submits them itself: the task reaches a device queue without
+    // a round trip through a compute thread's scheduler queue.
+    int kept = 0;
+    for (int i = 0; i < n; ++i) {
+      Task* t = tasks[i];
+      const TaskClass* tc = t->task_class;
+      bool gpu_first = false;
+      for (int c = 0; c < (int)tc->chores.size(); ++c) {
+        if (!(t->chore_mask & (1u << c)) || !device_type_enabled(t->taskpool, tc->chores[c].type)) continue;
+        gpu_first = (tc->chores[c].type & DEV_GPU_MASK) && !tc->chores[c].evaluate;
+        break;
+      }
+      if (gpu_first) task_progress(es, t, 0);
+      else tasks[kept++] = t;
+    }
+    n = kept;
+    if (n == 0) return 0;
+  }
   if (es->is_manager) {
     // Managers never run CPU work: hand the tasks to a compute thread's queues.
     Context* ctx = es->ctx;

@@ -70,16 +70,16 @@ struct PotrfDesc {
   int n, lda;
   int* info;  // device pointer (may be null)
   double* invD_out = nullptr;  // optional: keep the 64x64 diagonal-block inverses (ceil(n/64) x 4096 doubles)
-  double* W_out = nullptr;     // optional: also write W = L^-T (n x n, upper triangular, ld ldw)
+  double* W_out = nullptr;     // optional: also write W = L^-1 (n x n, lower triangular, zero above, ld ldw)
   int ldw = 0;
 };
 
-// Panel solve through the explicit inverse: B := B * W with W = L^-T from POTRF
-// (one grouped MFMA GEMM instead of a sequential blocked solve per tile).
+// Panel solve through the explicit inverse: B := B * W^T with W = L^-1 from
+// POTRF (one grouped MFMA GEMM instead of a sequential blocked solve per tile).
 struct TrsmGemmDesc {
   double* B;
   const double* W;
-  int m, n;  // B is m x n, W is n x n
+  int m, n;  // B is m x n, W is n x n lower triangular
   int ldb, ldw;
 };
 

@@ -457,7 +457,21 @@ void HipDevice::execute_ready() {
     else if (nb_exec_streams == 2) s = hp ? 0 : 1;
     else if (t->priority >= critical_threshold) s = 0;
     else if (hp) s = 1;
-    else s = 2 + (int)(rr_stream++ % (uint32_t)(nb_exec_streams - 2));
+    else {
+      // Bulk work: pick a bulk stream with fewer than max_inflight_groups launched
+      // groups; when every bulk stream is that far ahead, hold the task so the
+      // next round launches it in a larger batch (the streams are busy anyway).
+      const int nbulk = nb_exec_streams - 2;
+      s = -1;
+      for (int i = 0; i < nbulk && s < 0; ++i)  // join a batch already open this round
+        if (!round_tasks[2 + i].empty()) s = 2 + i;
+      for (int i = 0; i < nbulk && s < 0; ++i) {
+        const int c = 2 + (int)((rr_stream + i) % (uint32_t)nbulk);
+        if (max_inflight_groups <= 0 || (int)executing[c].size() < max_inflight_groups) s = c;
+      }
+      if (s < 0) { again.push_back(g); continue; }
+      if (round_tasks[s].empty()) ++rr_stream;
+    }
     GpuExecContext ctxg;
     ctxg.dev = this;
     ctxg.device = this;
@@ -671,6 +685,7 @@ void hip_devices_init(Context* ctx) {
   int sortp = (int)params.reg_int("device", "hip", "sort_pending_tasks", "Sort pending GPU tasks by priority", 1);
   int crit = (int)params.reg_int("device", "hip", "critical_threshold", "Task priority at or above which the CU-reserved critical stream is used", 1 << 29);
   int rcus = (int)params.reg_int("device", "hip", "reserved_cus", "CUs reserved for the critical-path stream (0 = no CU masking; measured slower on MI355X)", 0);
+  int maxg = (int)params.reg_int("device", "hip", "max_inflight_batches", "Launched kernel groups per bulk stream before new bulk tasks wait for a larger batch (0 = no limit)", 2);
   if (enabled == 0) return;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) { (void)hipGetLastError(); return; }
@@ -692,6 +707,7 @@ void hip_devices_init(Context* ctx) {
     d->high_prio_threshold = hp;
     d->critical_threshold = crit;
     d->reserved_cus = rcus;
+    d->max_inflight_groups = maxg;
     d->sort_pending = sortp != 0;
     reg.add(d);
     g_hip_devices.push_back(d);

@@ -109,8 +109,8 @@ struct HipDevice : Device {
   bool cu_masked = false;
   bool batching = true;
   bool sort_pending = true;
-  int max_inflight_groups = 64;
   uint32_t rr_stream = 0;
+  int max_inflight_groups = 2;  // bulk streams: launched groups in flight before new bulk work waits (0 = no limit)
   double us_busy = 0;
 
   bool is_gpu() const override { return true; }

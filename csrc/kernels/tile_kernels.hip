@@ -292,8 +292,13 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 __device__ __forceinline__ void block_potrf64(double* T, int ldt, int w, double* invD, int* info, int info_base, bool factor) {
   __shared__ double Ls[64][65];      // Ls[c][r] = L(r, c)
   __shared__ double Xs[64][65];      // Xs[c][r] = X(r, c), X = L^-1
-  __shared__ double Pn[2][16][65];   // panel broadcast buffers
-  __shared__ double Ts[4][16][17];   // per-wave scratch for the inverse
+  // The panel broadcast buffers (factor phase) and the per-wave scratch of the
+  // inverse phase share one LDS array: the kernel then fits (83 KB) next to a
+  // resident 128x128 GEMM workgroup (74 KB), so the critical-path factorization
+  // is not held back until a CU drains completely.
+  __shared__ double PnTs[2 * 16 * 65];
+  double(*Pn)[16][65] = reinterpret_cast<double(*)[16][65]>(PnTs);  // panel broadcast buffers
+  double(*Ts)[16][17] = reinterpret_cast<double(*)[16][17]>(PnTs);  // per-wave scratch for the inverse
   __shared__ double dinv[64];
   __shared__ int bad_s;
   const int r = threadIdx.x & 63;
@@ -674,28 +679,81 @@ __global__ void set_identity_kernel(double* W, int n, int ldw) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) W[(size_t)j * ldw + i] = i == j ? 1.0 : 0.0;
 }
 
-constexpr int kMaxCopyBatch = 64;
+constexpr int kMaxCopyBatch = 48;
 struct CopyBatchArgs {
   int count;
-  int rows[kMaxCopyBatch], cols[kMaxCopyBatch], ld_src[kMaxCopyBatch];
+  int rows[kMaxCopyBatch], cols[kMaxCopyBatch], ld_src[kMaxCopyBatch], ld_dst[kMaxCopyBatch];
   const double* src[kMaxCopyBatch];
-  double* dst[kMaxCopyBatch];  // packed (ld = rows)
+  double* dst[kMaxCopyBatch];
 };
 static_assert(sizeof(CopyBatchArgs) <= 4096, "CopyBatchArgs exceeds the kernel argument limit");
 
 // blockIdx.y = tile, blockIdx.x strides over columns; one wave-row per column.
 __global__ __launch_bounds__(256) void copy_tiles_kernel(const CopyBatchArgs a) {
   const int t = blockIdx.y;
-  const int rows = a.rows[t], cols = a.cols[t], lds = a.ld_src[t];
+  const int rows = a.rows[t], cols = a.cols[t], lds = a.ld_src[t], ldd = a.ld_dst[t];
   const double* __restrict__ s = a.src[t];
   double* __restrict__ d = a.dst[t];
   for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cols; c += gridDim.x * 4)
-    for (int r = threadIdx.x & 63; r < rows; r += 64) d[(size_t)c * rows + r] = s[(size_t)c * lds + r];
+    for (int r = threadIdx.x & 63; r < rows; r += 64) d[(size_t)c * ldd + r] = s[(size_t)c * lds + r];
 }
 
 size_t potrf_workspace_bytes(const PotrfDesc& p) {
-  if (p.W_out && !p.invD_out) return (size_t)((p.n + 63) / 64) * 4096 * sizeof(double);
-  return 4096 * sizeof(double);
+  if (!p.W_out) return 4096 * sizeof(double);
+  const size_t inv = p.invD_out ? 0 : (size_t)((p.n + 63) / 64) * 4096;
+  const size_t tmp = (size_t)p.n * p.n / 2 + 4096;  // doubling products, <= n^2/4 (+ a partial group)
+  return (inv + tmp) * sizeof(double);
+}
+
+// X = L^-1 (n x n lower, ld ldx, zero above the diagonal) from the inverses of
+// L's 64x64 diagonal blocks by recursive doubling: groups of g blocks pair up,
+// inv([A 0; B C]) = [inv(A) 0; -inv(C) B inv(A)  inv(C)], each level two
+// grouped MFMA GEMMs over all pairs (log2(n/64) levels, no sequential solve).
+void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, double* ws);
+static void launch_lower_inverse(const double* L, int lda, int n, const double* invD, double* X, int ldx, double* tmp, hipStream_t stream) {
+  const int nblk = (n + 63) / 64;
+  (void)hipMemset2DAsync(X, (size_t)ldx * sizeof(double), 0, (size_t)n * sizeof(double), n, stream);
+  for (int b0 = 0; b0 < nblk; b0 += kMaxCopyBatch) {
+    CopyBatchArgs ca;
+    ca.count = std::min(kMaxCopyBatch, nblk - b0);
+    for (int i = 0; i < ca.count; ++i) {
+      const int b = b0 + i, w = std::min(64, n - 64 * b);
+      ca.rows[i] = w; ca.cols[i] = w; ca.ld_src[i] = 64; ca.ld_dst[i] = ldx;
+      ca.src[i] = invD + (size_t)b * 4096;
+      ca.dst[i] = X + (size_t)64 * b * ldx + 64 * b;
+    }
+    hipLaunchKernelGGL(copy_tiles_kernel, dim3(16, ca.count), dim3(256), 0, stream, ca);
+  }
+  std::vector<GemmDesc> g1, g2;
+  for (int g = 1; g < nblk; g *= 2) {
+    g1.clear();
+    g2.clear();
+    size_t off = 0;
+    for (int a0 = 0; a0 + g < nblk; a0 += 2 * g) {
+      const int ra = 64 * a0, rc = 64 * (a0 + g);
+      const int sa = std::min(64 * g, n - ra), sc = std::min(64 * g, n - rc);
+      double* T = tmp + off;
+      off += (size_t)sc * sa;
+      GemmDesc e{};
+      // T = L[C rows, A cols] * X_A
+      e.A = L + (size_t)ra * lda + rc; e.lda = lda;
+      e.B = X + (size_t)ra * ldx + ra; e.ldb = ldx;
+      e.C = T; e.ldc = sc;
+      e.m = sc; e.n = sa; e.k = sa;
+      e.alpha = 1.0; e.beta = 0.0;
+      g1.push_back(e);
+      // X[C rows, A cols] = -X_C * T
+      GemmDesc f{};
+      f.A = X + (size_t)rc * ldx + rc; f.lda = ldx;
+      f.B = T; f.ldb = sc;
+      f.C = X + (size_t)ra * ldx + rc; f.ldc = ldx;
+      f.m = sc; f.n = sa; f.k = sc;
+      f.alpha = -1.0; f.beta = 0.0;
+      g2.push_back(f);
+    }
+    launch_gemm_batch(g1.data(), (int)g1.size(), stream);
+    launch_gemm_batch(g2.data(), (int)g2.size(), stream);
+  }
 }
 
 // Blocked tile Cholesky (lower). ws needs 4096 doubles unless p.invD_out keeps
@@ -725,12 +783,9 @@ void launch_potrf(const PotrfDesc& p, hipStream_t stream, double* ws) {
     launch_gemm_batch(&g, 1, stream);
   }
   if (p.W_out) {
-    // W = I L^-T with the diagonal-block inverses just computed
-    hipLaunchKernelGGL(set_identity_kernel, dim3((p.n + 255) / 256, p.n), dim3(256), 0, stream, p.W_out, p.n, p.ldw);
-    TrsmDesc t;
-    t.L = p.A; t.B = p.W_out; t.m = p.n; t.n = p.n; t.ldl = p.lda; t.ldb = p.ldw; t.trans = 1;
-    const double* cinv = inv_base;
-    launch_trsm_inv(&t, &cinv, 1, stream);
+    // W = L^-1 from the diagonal-block inverses just computed
+    double* tmp = ws + (p.invD_out ? 0 : (size_t)((p.n + 63) / 64) * 4096);
+    launch_lower_inverse(p.A, p.lda, p.n, inv_base, p.W_out, p.ldw, tmp, stream);
   }
 }
 
@@ -752,14 +807,14 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
     int maxc = 1;
     for (int i = 0; i < cnt; ++i) {
       const TrsmGemmDesc& t = d[s0 + i];
-      ca.rows[i] = t.m; ca.cols[i] = t.n; ca.ld_src[i] = t.ldb;
+      ca.rows[i] = t.m; ca.cols[i] = t.n; ca.ld_src[i] = t.ldb; ca.ld_dst[i] = t.m;
       ca.src[i] = t.B; ca.dst[i] = reinterpret_cast<double*>(p);
       maxc = std::max(maxc, t.n);
       GemmDesc& e = g[i];
       e.A = ca.dst[i]; e.B = t.W; e.C = t.B;
       e.m = t.m; e.n = t.n; e.k = t.n;
       e.lda = t.m; e.ldb = t.ldw; e.ldc = t.ldb;
-      e.alpha = 1.0; e.beta = 0.0; e.transA = 0; e.transB = 0; e.lower_only = 0; e.pad = 0;
+      e.alpha = 1.0; e.beta = 0.0; e.transA = 0; e.transB = 1; e.lower_only = 0; e.pad = 0;  // copy x (L^-1)^T
       p += ((size_t)t.m * t.n * sizeof(double) + 255) / 256 * 256;
     }
     hipLaunchKernelGGL(copy_tiles_kernel, dim3(std::min(256, (maxc + 3) / 4), cnt), dim3(256), 0, stream, ca);
@@ -831,6 +886,21 @@ int parsec_amd_dpotrf_tile(double* A, int n, int lda, int* info, void* stream) {
   parsec::PotrfDesc p{A, n, lda, info};
   void* ws = test_ws(4096 * sizeof(double));
   parsec::kern::launch_potrf(p, (hipStream_t)stream, static_cast<double*>(ws));
+  return (int)hipGetLastError();
+}
+// Tile Cholesky that also writes W = L^-1 (ld ldw)
+int parsec_amd_dpotrf_tile_w(double* A, int n, int lda, int* info, double* W, int ldw, void* stream) {
+  parsec::PotrfDesc p{A, n, lda, info};
+  p.W_out = W;
+  p.ldw = ldw;
+  void* ws = test_ws(parsec::kern::potrf_workspace_bytes(p));
+  parsec::kern::launch_potrf(p, (hipStream_t)stream, static_cast<double*>(ws));
+  return (int)hipGetLastError();
+}
+// B := B W^T for a batch (the DPOTRF panel solve through the inverse)
+int parsec_amd_trsm_w_batch(const parsec::TrsmGemmDesc* d, int n, void* stream) {
+  void* ws = test_ws(parsec::kern::trsm_w_workspace_bytes(d, n) + 64);
+  parsec::kern::launch_trsm_w_batch(d, n, (hipStream_t)stream, static_cast<double*>(ws));
   return (int)hipGetLastError();
 }
 }

@@ -26,6 +26,8 @@ using namespace parsec;
 extern "C" int parsec_amd_dgemm_batch(const GemmDesc* descs, int n, void* stream);
 extern "C" int parsec_amd_dtrsm_batch(const TrsmDesc* descs, int n, void* stream);
 extern "C" int parsec_amd_dpotrf_tile(double* A, int n, int lda, int* info, void* stream);
+extern "C" int parsec_amd_dpotrf_tile_w(double* A, int n, int lda, int* info, double* W, int ldw, void* stream);
+extern "C" int parsec_amd_trsm_w_batch(const parsec::TrsmGemmDesc* d, int n, void* stream);
 extern "C" int parsec_amd_qr_panel(const parsec::QrPanelDesc* d, int n, void* stream);
 extern "C" int parsec_amd_qr_apply(const parsec::QrApplyDesc* d, int n, void* ws, void* stream);
 extern "C" size_t parsec_amd_qr_apply_ws(const parsec::QrApplyDesc* d, int n);
@@ -608,6 +610,14 @@ PYBIND11_MODULE(_C, m) {
     return parsec_amd_qr_apply(&q, 1, (void*)ws, (void*)stream);
   });
   m.def("kernel_dpotrf", [](uintptr_t A, int n, int lda, uintptr_t info, uintptr_t stream) { return parsec_amd_dpotrf_tile((double*)A, n, lda, (int*)info, (void*)stream); });
+  m.def("kernel_dpotrf_w", [](uintptr_t A, int n, int lda, uintptr_t info, uintptr_t W, int ldw, uintptr_t stream) {
+    return parsec_amd_dpotrf_tile_w((double*)A, n, lda, (int*)info, (double*)W, ldw, (void*)stream);
+  });
+  m.def("kernel_trsm_w_batch", [](std::vector<std::tuple<uintptr_t, uintptr_t, int, int, int, int>> ds, uintptr_t stream) {
+    std::vector<TrsmGemmDesc> v;
+    for (auto& d : ds) v.push_back(TrsmGemmDesc{(double*)std::get<0>(d), (const double*)std::get<1>(d), std::get<2>(d), std::get<3>(d), std::get<4>(d), std::get<5>(d)});
+    return parsec_amd_trsm_w_batch(v.data(), (int)v.size(), (void*)stream);
+  });
 
   // ------------------------------------------------------------- profiling
   m.def("profiling_dump", [](const std::string& f) { return profiling_dump(f); });

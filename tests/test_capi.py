@@ -48,3 +48,39 @@ def test_jdf_multiprocess(bcast_gather, nranks):
     sinks = sum(int(o.split("sink")[1].split()[0]) for o, _ in outs)
     leaves = sum(int(o.split("leaves")[1].split()[0]) for o, _ in outs)
     assert sinks == 1 and leaves == 37
+
+
+@pytest.fixture(scope="module")
+def apps(tmp_path_factory, pa):
+    out = str(tmp_path_factory.mktemp("jdfapps"))
+    return {n: ptgpp.build_program(os.path.join(HERE, "jdf", n + ".jdf"), out) for n in ("tree_reduce", "pingpong", "all2all")}
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_tree_reduce_multiprocess(apps, nranks):
+    """Binary reduction tree of NEW buffers whose interior edges cross ranks
+    (reference tests/apps/haar_tree, generalized_reduction)."""
+    rc, outs = launch.launch(nranks, [apps["tree_reduce"], "6"], timeout=120, capture=True)
+    assert rc == 0, outs
+    assert "root 2080" in outs[0][0]
+    assert sum(int(o.split("nodes")[1].split()[0]) for o, _ in outs) == 63
+
+
+def test_pingpong_two_ranks(apps):
+    """Round trips of a 256 KiB tile between two ranks, payload checked at every hop
+    (reference tests/apps/pingpong rtt.jdf / bandwidth.jdf)."""
+    rc, outs = launch.launch(2, [apps["pingpong"], "20", "32768"], timeout=120, capture=True)
+    assert rc == 0, outs
+    assert "rtt_us" in outs[0][0]
+    hops = sum(int(o.split("hops")[1].split()[0]) for o, _ in outs)
+    assert hops == 41
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_all2all_multiprocess(apps, nranks):
+    """Every rank sends a distinct NEW buffer to every rank; each DONE gathers
+    one CTL per sender (reference tests/apps/all2all)."""
+    rc, outs = launch.launch(nranks, [apps["all2all"]], timeout=120, capture=True)
+    assert rc == 0, outs
+    assert sum(int(o.split("recv")[1].split()[0]) for o, _ in outs) == nranks * nranks
+    assert all("bad 0" in o for o, _ in outs)

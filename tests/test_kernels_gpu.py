@@ -72,6 +72,53 @@ def test_dpotrf_tile(pa, dev, n):
     assert err.item() < 1e-13
 
 
+def _colmajor(rows, cols=None):
+    cols = rows if cols is None else cols
+    return torch.empty((cols, rows), dtype=torch.float64, device="cuda").t()  # rows x cols, column-major (ld = rows)
+
+
+@pytest.mark.parametrize("n", [1024, 512, 320, 200])
+def test_dpotrf_tile_inverse(pa, dev, n):
+    """POTRF that also writes W = L^-1 by recursive doubling of the 64x64
+    diagonal-block inverses (two grouped GEMMs per level); checked against the
+    fp64 torch Cholesky: W L = I, W lower triangular."""
+    R = torch.randn((n, n), dtype=torch.float64, device=dev)
+    S = R @ R.t() + n * torch.eye(n, dtype=torch.float64, device=dev)
+    A = S.t().contiguous().t().clone()
+    W = _colmajor(n)
+    W.fill_(7.0)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    pa.kernel_dpotrf_w(A.data_ptr(), n, n, info.data_ptr(), W.data_ptr(), n, _stream())
+    torch.cuda.synchronize()
+    assert info.item() == 0
+    L = torch.tril(A)
+    assert ((L @ L.t() - S).norm() / S.norm()).item() < 1e-13
+    eye = torch.eye(n, dtype=torch.float64, device=dev)
+    assert (W @ L - eye).abs().max().item() < 1e-12
+    assert torch.triu(W, 1).abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("m,n,tasks", [(1024, 1024, 3), (512, 512, 5), (300, 200, 2)])
+def test_trsm_through_inverse(pa, dev, m, n, tasks):
+    """Panel solve B := B L^-T as copy + grouped GEMM with W = L^-1 (the
+    DPOTRF TRSM path) vs torch.linalg.solve_triangular in fp64."""
+    R = torch.randn((n, n), dtype=torch.float64, device=dev)
+    L = torch.linalg.cholesky(R @ R.t() + n * torch.eye(n, dtype=torch.float64, device=dev))
+    Wt = torch.linalg.inv(L)
+    W = _colmajor(n)
+    W.copy_(Wt)
+    Bs = [_colmajor(m, n) for _ in range(tasks)]
+    refs = []
+    for B in Bs:
+        B.copy_(torch.randn((m, n), dtype=torch.float64, device=dev))
+        refs.append(torch.linalg.solve_triangular(L, B.t(), upper=False).t())  # X L^T = B
+    descs = [(B.data_ptr(), W.data_ptr(), m, n, m, n) for B in Bs]
+    pa.kernel_trsm_w_batch(descs, _stream())
+    torch.cuda.synchronize()
+    for B, ref in zip(Bs, refs):
+        assert ((B - ref).abs().max() / ref.abs().max()).item() < 1e-12
+
+
 # --------------------------------------------------------------- QR kernels
 def _house_qr_ref(A):
     """numpy reference of the compact-WY QR: R (upper), V (unit lower), T."""
