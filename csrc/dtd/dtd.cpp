@@ -296,6 +296,30 @@ DtdTask* DtdTaskpool::insert_task(DtdTaskClass* tc, int priority, const std::vec
   t->nb_flows = nf;
   if (rank < 0) for (auto& a : t->args) if (a.flow >= 0 && a.tile) { rank = a.tile->rank; break; }
   if (rank < 0) rank = my;
+  // A tile read on another rank before any task wrote it: its owner's initial
+  // data is version 0. Every rank inserts (in the same stream position) a no-op
+  // INOUT task on the owner, which then sends that version like any writer.
+  if (ctx->nb_nodes > 1) {
+    for (auto& a : t->args) {
+      const int op = a.op & OP_MASK;
+      if (a.flow < 0 || !a.tile || (a.op & DONT_TRACK) || op == OUTPUT) continue;
+      Tile* tl = a.tile;
+      bool first_use;
+      {
+        std::lock_guard<SpinLock> g(tl->lock);
+        first_use = !tl->writer && tl->version == 0 && tl->rank != rank && tl->dc;
+      }
+      if (!first_use) continue;
+      static const Hook noop = [](ExecutionStream*, Task*) { return HOOK_DONE; };
+      DtdTaskClass* itc = create_task_class("dtd_tile_initial_version", {{INOUT | AFFINITY, (int)PASSED_BY_REF}});
+      if (itc->chores.empty()) add_chore(itc, DEV_CPU, noop, nullptr);
+      Arg ia;
+      ia.op = INOUT | AFFINITY;
+      ia.size = PASSED_BY_REF;
+      ia.tile = tl;
+      insert_task(itc, priority, {ia});
+    }
+  }
   t->rank = rank;
   t->remote = rank != my;
   if (!t->remote) tdm->taskpool_addto_nb_tasks(this, 1);

@@ -70,7 +70,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // NBUF = 2: double-buffered LDS, one barrier per k-tile; NBUF = 1: one LDS
 // buffer (half the LDS, two barriers per k-tile) for deeper BK.
 template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF = 2>
-__global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2))) void dgemm_batch_kernel(const GemmBatchArgs args) {
+__global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(WM * WN / 2))) void dgemm_batch_kernel(const GemmBatchArgs args) {
   constexpr int NT = WM * WN * 64;
   constexpr int WTM = BM / WM;
   constexpr int WTN = BN / WN;
@@ -599,7 +599,13 @@ static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) 
     case 2: launch_gemm_shape<256, 128, 16, 4, 2, 2>(a, descs, n, stream); break;
     case 3: launch_gemm_shape<128, 128, 32, 2, 2, 2>(a, descs, n, stream); break;
     case 4: launch_gemm_shape<256, 128, 32, 4, 2, 1>(a, descs, n, stream); break;
-    default: launch_gemm_shape<128, 128, 16, 2, 2, 2>(a, descs, n, stream); break;
+    case 6: launch_gemm_shape<128, 128, 16, 4, 2, 2>(a, descs, n, stream); break;
+    case 7: launch_gemm_shape<128, 128, 32, 2, 4, 1>(a, descs, n, stream); break;
+    case 8: launch_gemm_shape<128, 128, 16, 2, 2, 2>(a, descs, n, stream); break;
+    // default: 8 waves (2 x 4) of 64x32 per 128x128 tile, 126 VGPRs -> 4 waves per
+    // SIMD with two workgroups per CU (measured: DPOTRF 64k +4 %, 16k +7 % over
+    // the 4-wave 64x64-per-wave kernel, profiles/r1_gemm_variants_v8.log)
+    default: launch_gemm_shape<128, 128, 16, 2, 4, 2>(a, descs, n, stream); break;
   }
 }
 

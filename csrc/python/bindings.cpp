@@ -74,8 +74,10 @@ static py::object dtd_arg(Task* t, int i) {
     if (!c) return py::none();
     Data* d = c->original;
     if (c->device_index != 0) return py::int_((uintptr_t)c->device_private);
-    if (d && d->dc) {
-      if (auto* tm = dynamic_cast<TiledMatrix*>(d->dc)) return tile_view(c->device_private, tm->mtype, tm->mb, tm->nb, tm->elem_size);
+    // received remote copies carry a bare Data: type them through the tile's collection
+    DataCollection* dcc = (d && d->dc) ? d->dc : (a.tile ? a.tile->dc : nullptr);
+    if (dcc) {
+      if (auto* tm = dynamic_cast<TiledMatrix*>(dcc)) return tile_view(c->device_private, tm->mtype, tm->mb, tm->nb, tm->elem_size);
     }
     size_t n = d ? d->nb_elts : 0;
     return py::array(py::dtype::of<uint8_t>(), {(py::ssize_t)n}, {1}, c->device_private, py::capsule(c->device_private, [](void*) {}));

@@ -12,10 +12,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 WORKER = os.path.join(HERE, "mp", "dist_dpotrf.py")
 
 
-def run_ranks(nranks, *args, timeout=120):
+def run_ranks(nranks, *args, timeout=120, worker=WORKER):
     job = "pt" + uuid.uuid4().hex[:10]
     env = dict(os.environ, PARSEC_MCA_device_hip_enabled="0")
-    procs = [subprocess.Popen([sys.executable, WORKER, str(r), str(nranks), job, *map(str, args)],
+    procs = [subprocess.Popen([sys.executable, worker, str(r), str(nranks), job, *map(str, args)],
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
              for r in range(nranks)]
     outs = []
@@ -45,5 +45,16 @@ def test_distributed_dpotrf(pa, nranks, P, Q, topo, termdet):
 @pytest.mark.parametrize("sched", ["gd", "ll", "ap"])
 def test_distributed_other_schedulers(pa, sched):
     outs = run_ranks(2, 384, 64, 2, 1, sched, "star", "local")
+    for rc, out in outs:
+        assert rc == 0, out
+
+
+@pytest.mark.parametrize("case", ["broadcast", "reduce", "allreduce", "pingpong", "war"])
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_distributed_dtd_patterns(pa, case, nranks):
+    """Distributed DTD: one writer read on every rank, reduction into rank 0,
+    all-reduce, a tile bouncing between ranks, readers-before-writer across
+    ranks (reference tests/dsl/dtd broadcast / reduce / allreduce / pingpong / war)."""
+    outs = run_ranks(nranks, case, worker=os.path.join(HERE, "mp", "dist_dtd.py"))
     for rc, out in outs:
         assert rc == 0, out
