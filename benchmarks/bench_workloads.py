@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""The other BASELINE.json workloads, one JSON line each (rank 0):
+
+  qr       tiled Householder QR (PTG DGEQRF: GEQRT/UNMQR/TSQRT/TSMQR), matrix and
+           T factors resident in HBM, GFLOP/s with 4/3 N^3 (config 4)
+  stencil  DTD 3D 7-point Jacobi stencil, halo faces between blocks (and ranks),
+           GPU bodies, Gpoint-updates/s and GFLOP/s at 8 flop/point (config 5)
+  dtd_gemm DTD tiled DGEMM C += A B on 4 x 4 tiles, CPU bodies in one process
+           (config 1, the plumbing check), GFLOP/s
+
+Multi-GPU: launch like bench.py (torch.distributed.run, one rank per GPU).
+
+    python benchmarks/bench_workloads.py qr --n 16384 --nb 512
+    python benchmarks/bench_workloads.py stencil --n 512 --b 128 --iters 20
+    python benchmarks/bench_workloads.py dtd_gemm --n 2048
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+def _comm(pa, world, rank, local, gpu=True):
+    if world > 1:
+        job = "_".join([os.environ.get("MASTER_PORT", "0"), os.environ.get("TORCHELASTIC_RUN_ID", "wl"), str(os.getppid())])
+        if pa.comm_init(rank, world, job, local if gpu else -1) != 0:
+            raise RuntimeError("comm_init failed")
+
+
+def bench_qr(args):
+    import torch
+    import torch.distributed as dist
+
+    world, rank, local = _dist()
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import parsec_amd as pa
+
+    pa.require_native()
+    pa.mca_set("device_hip_mask", str(1 << local))
+    _comm(pa, world, rank, local)
+    ctx = pa.init(args.cores)
+    gpu = pa.first_gpu_device_index()
+    N, nb = args.n, args.nb
+    P = world  # 1D row-cyclic distribution over ranks (process grid P x 1)
+    NT = (N + nb - 1) // nb
+    lm = sum(1 for g in range(NT) if g % P == rank)
+    storeA = torch.empty((NT, lm, nb, nb), dtype=torch.float64, device="cuda")
+    storeT = torch.zeros((NT, lm, nb, nb), dtype=torch.float64, device="cuda")
+    A = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=1, device=gpu, ptr=storeA.data_ptr())
+    T = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=1, device=gpu, ptr=storeT.data_ptr())
+    g = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    storeA.copy_(torch.rand(storeA.shape, dtype=torch.float64, device="cuda", generator=g) - 0.5)
+    backup = storeA.clone()
+
+    def step():
+        storeA.copy_(backup)
+        storeT.zero_()
+        torch.cuda.synchronize()
+        tp = pa.dgeqrf_new(A, T, args.ib)
+        ctx.add_taskpool(tp)
+        ctx.start()
+        ctx.wait()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        barrier()
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    dt = (time.perf_counter() - t0) / args.steps
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ctx.fini()
+    if world > 1:
+        pa.comm_fini()
+    out = {"metric": "GFLOP/s tiled DGEQRF (PTG, HBM-resident)", "value": round(4.0 / 3.0 * N ** 3 / dt / 1e9, 1), "unit": "GFLOP/s",
+           "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
+           "dtype": "fp64", "data": "synthetic uniform(-0.5, 0.5)", "config": {"model": "tiled DGEQRF", "N": N, "nb": nb, "ib": args.ib,
+                                                                             "parallelism": f"1D row-cyclic P{P}x1"}}
+    if world > 1:
+        dist.destroy_process_group()
+    return out, rank
+
+
+def bench_stencil(args):
+    world, rank, local = _dist()
+    import torch
+
+    torch.cuda.set_device(local)
+    import parsec_amd as pa
+
+    pa.require_native()
+    pa.mca_set("device_hip_mask", str(1 << local))
+    _comm(pa, world, rank, local)
+    ctx = pa.init(args.cores)
+    G = pa.StencilGrid(rank, world, args.n, args.n, args.n, args.b, args.b, args.b)
+    pa.stencil3d_run(ctx, G, 2, 0.4, 0.1, True)  # warmup: tiles to HBM, kernels loaded
+    secs, pts, _ = pa.stencil3d_run(ctx, G, args.iters, 0.4, 0.1, True)
+    if world > 1:
+        secs = pa.comm_allreduce_max_f64(secs) if hasattr(pa, "comm_allreduce_max_f64") else secs
+    ctx.fini()
+    if world > 1:
+        pa.comm_fini()
+    gpts = pts / secs / 1e9
+    out = {"metric": "Gpoint-updates/s DTD 3D 7-point stencil", "value": round(gpts, 2), "unit": "Gpoints/s", "gflops": round(8 * gpts, 1),
+           "n_gpus": world, "steps": args.iters, "ms_per_step": round(secs / args.iters * 1e3, 3), "higher_is_better": True, "dtype": "fp64",
+           "data": "synthetic smooth field", "config": {"model": "DTD stencil3d", "grid": [args.n] * 3, "block": args.b, "ranks": world}}
+    return out, rank
+
+
+def bench_dtd_gemm(args):
+    import numpy as np
+
+    import parsec_amd as pa
+
+    pa.mca_set("device_hip_enabled", "0")
+    ctx = pa.init(args.cores)
+    N, nt = args.n, 4
+    nb = N // nt
+    mats = [pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb, nb, N, N) for _ in range(3)]
+    rng = np.random.default_rng(0)
+    for M in mats:
+        for m in range(nt):
+            for n in range(nt):
+                M.tile(m, n)[:, :] = rng.standard_normal((nb, nb))
+    pa.dtd_dgemm(ctx, 1.0, mats[0], mats[1], 1.0, mats[2], False)  # warmup
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pa.dtd_dgemm(ctx, 1.0, mats[0], mats[1], 1.0, mats[2], False)
+    dt = (time.perf_counter() - t0) / args.steps
+    ctx.fini()
+    out = {"metric": "GFLOP/s DTD tiled DGEMM (CPU bodies, 1 process)", "value": round(2.0 * N ** 3 / dt / 1e9, 2), "unit": "GFLOP/s",
+           "n_gpus": 0, "steps": args.steps, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "fp64",
+           "config": {"model": "DTD dgemm", "N": N, "tiles": "4x4", "cores": args.cores}}
+    return out, 0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("workload", choices=["qr", "stencil", "dtd_gemm"])
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--nb", type=int, default=512)
+    ap.add_argument("--ib", type=int, default=32)
+    ap.add_argument("--b", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--cores", type=int, default=4)
+    args = ap.parse_args()
+    if args.n is None:
+        args.n = {"qr": 16384, "stencil": 512, "dtd_gemm": 2048}[args.workload]
+    fn = {"qr": bench_qr, "stencil": bench_stencil, "dtd_gemm": bench_dtd_gemm}[args.workload]
+    out, rank = fn(args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -139,6 +139,194 @@ __global__ __launch_bounds__(kQrThreads) void qr_panel_kernel(const QrPanelArgs 
     }
 }
 
+// ------------------------------------------------------------ blocked panel
+// Sub-panel of at most kSubJB columns, factored with the whole column block in
+// registers: 512 threads, thread t owns virtual rows t + 512 q (q < R). Virtual
+// rows [0, nR) are rows of A1 (GEQRT: the tile from row j0 down; TSQRT: the
+// jb x jb block of R), rows [nR, nR + m2) are rows of A2 (TSQRT). Per column:
+// one scalar and one 32-wide block reduction (norm; V^T [A | V] for the
+// trailing update and the compact-WY T column), everything else in registers.
+constexpr int kSubJB = 32;
+constexpr int kSubThreads = 512;
+
+struct QrSubDesc {
+  double* A1;
+  int lda1;
+  int nR;          // virtual rows taken from A1
+  double* A2;      // TS only
+  int lda2, m2;
+  int jb;          // columns (<= kSubJB)
+  int ts;          // 1: TSQRT (only the pivot row of R participates)
+  double* T;       // jb x jb (ldt), written upper with zeros below
+  int ldt;
+  double* Vc;      // GEQRT: clean unit-lower V (nR x jb, ldvc), may be null
+  int ldvc;
+};
+constexpr int kMaxSubBatch = 48;
+struct QrSubArgs {
+  int count;
+  QrSubDesc d[kMaxSubBatch];
+};
+static_assert(sizeof(QrSubArgs) <= 4096, "QrSubArgs exceeds the kernel argument limit");
+
+template <int R>
+__global__ __launch_bounds__(kSubThreads) void qr_subpanel_kernel(const QrSubArgs args) {
+  const QrSubDesc& d = args.d[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  constexpr int NW = kSubThreads / 64;
+  __shared__ double red[NW][kSubJB];
+  __shared__ double svec[kSubJB];
+  __shared__ double Tl[kSubJB][kSubJB + 1];
+  __shared__ double s_tau, s_scale, s_alpha;
+  const int nR = d.nR, m = d.nR + (d.ts ? d.m2 : 0), jb = d.jb;
+  double a[R][kSubJB];
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const int r = tid + kSubThreads * q;
+#pragma unroll
+    for (int c = 0; c < kSubJB; ++c) {
+      double x = 0.0;
+      if (r < m && c < jb) x = r < nR ? d.A1[(size_t)c * d.lda1 + r] : d.A2[(size_t)c * d.lda2 + (r - nR)];
+      a[q][c] = x;
+    }
+  }
+  for (int j = 0; j < jb; ++j) {
+    // participation of virtual row r in step j
+    auto part = [&](int r) { return r == j || (r > j && r < m && (!d.ts || r >= nR)); };
+    // ---- sigma = sum of squares below the pivot
+    double sq = 0.0;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int r = tid + kSubThreads * q;
+      double x = 0.0;
+#pragma unroll
+      for (int c = 0; c < kSubJB; ++c) if (c == j) x = a[q][c];
+      if (r != j && part(r)) sq += x * x;
+    }
+    sq = wave_sum(sq);
+    if (lane == 0) red[wv][0] = sq;
+    if (tid == j) {  // the pivot row lives in thread j (q = 0)
+#pragma unroll
+      for (int c = 0; c < kSubJB; ++c) if (c == j) s_alpha = a[0][c];
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double sigma = 0.0;
+      for (int w = 0; w < NW; ++w) sigma += red[w][0];
+      const double alpha = s_alpha;
+      if (sigma == 0.0) {
+        s_tau = 0.0;
+        s_scale = 0.0;
+      } else {
+        const double norm = sqrt(alpha * alpha + sigma);
+        const double beta = alpha >= 0.0 ? -norm : norm;
+        s_tau = (beta - alpha) / beta;
+        s_scale = 1.0 / (alpha - beta);
+        svec[0] = beta;
+      }
+    }
+    __syncthreads();
+    const double tau = s_tau, scale = s_scale;
+    // ---- v (stored in place below the pivot), pivot := beta
+    double v[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int r = tid + kSubThreads * q;
+      v[q] = 0.0;
+      if (r == j) {
+        v[q] = 1.0;
+        if (tau != 0.0) {
+#pragma unroll
+          for (int c = 0; c < kSubJB; ++c) if (c == j) a[q][c] = svec[0];
+        }
+      } else if (part(r)) {
+#pragma unroll
+        for (int c = 0; c < kSubJB; ++c)
+          if (c == j) { a[q][c] *= scale; v[q] = a[q][c]; }
+      }
+    }
+    // ---- s_c = sum_r v_r A(r, c): trailing w (c > j) and z for T (c < j)
+    double p[kSubJB];
+#pragma unroll
+    for (int c = 0; c < kSubJB; ++c) p[c] = 0.0;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int r = tid + kSubThreads * q;
+      const bool pivot_ts = d.ts && r == j;  // TS: R's row j left of the pivot is not V
+#pragma unroll
+      for (int c = 0; c < kSubJB; ++c) {
+        const double x = (pivot_ts && c < j) ? 0.0 : a[q][c];
+        p[c] = __builtin_fma(v[q], x, p[c]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < kSubJB; ++c) p[c] = wave_sum(p[c]);
+    if (lane == 0) {
+#pragma unroll
+      for (int c = 0; c < kSubJB; ++c) red[wv][c] = p[c];
+    }
+    __syncthreads();
+    if (tid < kSubJB) {
+      double t = 0.0;
+      for (int w = 0; w < NW; ++w) t += red[w][tid];
+      svec[tid] = t;
+    }
+    __syncthreads();
+    // ---- trailing update inside the sub-panel
+    if (tau != 0.0) {
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const double tv = tau * v[q];
+#pragma unroll
+        for (int c = 0; c < kSubJB; ++c)
+          if (c > j) a[q][c] = __builtin_fma(-tv, svec[c], a[q][c]);
+      }
+    }
+    // ---- T(0:j, j) = -tau T(0:j, 0:j) z ; T(j, j) = tau
+    if (tid < j) {
+      double t = 0.0;
+      for (int l = tid; l < j; ++l) t += Tl[tid][l] * svec[l];
+      Tl[tid][j] = -tau * t;
+    }
+    if (tid == j) Tl[j][j] = tau;
+    __syncthreads();
+  }
+  // ---- write back the sub-panel, T (upper, zeros below) and the clean V
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const int r = tid + kSubThreads * q;
+    if (r >= m) continue;
+#pragma unroll
+    for (int c = 0; c < kSubJB; ++c) {
+      if (c >= jb) continue;
+      if (r < nR) d.A1[(size_t)c * d.lda1 + r] = a[q][c];
+      else d.A2[(size_t)c * d.lda2 + (r - nR)] = a[q][c];
+      if (d.Vc && r < nR) d.Vc[(size_t)c * d.ldvc + r] = r > c ? a[q][c] : (r == c ? 1.0 : 0.0);
+    }
+  }
+  for (int idx = tid; idx < jb * jb; idx += kSubThreads) {
+    const int i = idx % jb, j = idx / jb;
+    d.T[(size_t)j * d.ldt + i] = i <= j ? Tl[i][j] : 0.0;
+  }
+}
+
+static void launch_subpanels(const std::vector<QrSubDesc>& v, hipStream_t stream) {
+  for (size_t s0 = 0; s0 < v.size(); s0 += kMaxSubBatch) {
+    QrSubArgs a;
+    a.count = (int)std::min<size_t>(kMaxSubBatch, v.size() - s0);
+    int rows = 0;
+    for (int i = 0; i < a.count; ++i) {
+      a.d[i] = v[s0 + i];
+      rows = std::max(rows, a.d[i].nR + (a.d[i].ts ? a.d[i].m2 : 0));
+    }
+    const int R = (rows + kSubThreads - 1) / kSubThreads;
+    if (R <= 1) hipLaunchKernelGGL(qr_subpanel_kernel<1>, dim3(a.count), dim3(kSubThreads), 0, stream, a);
+    else if (R == 2) hipLaunchKernelGGL(qr_subpanel_kernel<2>, dim3(a.count), dim3(kSubThreads), 0, stream, a);
+    else if (R == 3) hipLaunchKernelGGL(qr_subpanel_kernel<3>, dim3(a.count), dim3(kSubThreads), 0, stream, a);
+    else hipLaunchKernelGGL(qr_subpanel_kernel<4>, dim3(a.count), dim3(kSubThreads), 0, stream, a);
+  }
+}
+
 // dst(:, :) (+)= alpha * src  over rows x cols, batched
 struct Axpy2D {
   const double* src;
@@ -183,6 +371,124 @@ void launch_qr_panel(const QrPanelDesc* descs, int n, hipStream_t stream) {
     for (int i = 0; i < a.count; ++i) { a.d[i] = descs[s + i]; maxn = std::max(maxn, a.d[i].n); }
     maxn = std::max(maxn, 1);
     hipLaunchKernelGGL(qr_panel_kernel, dim3(a.count), dim3(kQrThreads), (size_t)maxn * sizeof(double), stream, a);
+  }
+}
+
+// Workspace of the blocked panel: per task the apply scratch (2 jb x n), the
+// T-update products (2 n x jb) and, for a GEQRT without Vcopy, a clean V (m1 x n).
+size_t qr_panel_workspace_bytes(const QrPanelDesc* descs, int n) {
+  size_t b = 0;
+  for (int i = 0; i < n; ++i) {
+    const QrPanelDesc& d = descs[i];
+    b += (size_t)4 * kSubJB * d.n + 64;
+    if (!d.A2 && !d.Vcopy) b += (size_t)d.m1 * d.n;
+  }
+  return b * sizeof(double);
+}
+
+void launch_qr_apply(const QrApplyDesc* descs, int n, hipStream_t stream, double* ws);
+
+// Blocked GEQRT / TSQRT (DPLASMA-style inner blocking, ib = 32): per column block
+// j0 of every task of the batch, (1) factor the sub-panel in registers, (2) apply
+// its block reflector to the trailing columns with the grouped MFMA GEMMs, (3)
+// extend the tile's compact-WY T: T(0:j0, j0:j0+jb) = -T11 (V1^T V2) T22.
+void launch_qr_panel_blocked(const QrPanelDesc* descs, int n, hipStream_t stream, double* ws) {
+  if (n <= 0) return;
+  struct Task {
+    QrPanelDesc d;
+    bool ts;
+    int kr;
+    double* Vc;   // GEQRT clean V (m1 x kr, ld m1)
+    double* app;  // apply scratch
+    double* X;    // j0 x jb products
+    double* Y;
+  };
+  std::vector<Task> tk(n);
+  // [ apply scratch of all tasks | per task: X, Y, (clean V) ]
+  size_t app_total = 0;
+  for (int i = 0; i < n; ++i) app_total += (size_t)2 * kSubJB * descs[i].n;
+  double* app_ws = ws;
+  double* p = ws + app_total;
+  int steps = 0;
+  std::vector<Axpy2D> zero;
+  for (int i = 0; i < n; ++i) {
+    Task& t = tk[i];
+    t.d = descs[i];
+    t.ts = t.d.A2 != nullptr;
+    t.kr = t.ts ? t.d.n : std::min(t.d.m1, t.d.n);
+    t.app = nullptr;
+    t.X = p; p += (size_t)kSubJB * t.d.n;
+    t.Y = p; p += (size_t)kSubJB * t.d.n + 64;
+    t.Vc = nullptr;
+    if (!t.ts) {
+      if (t.d.Vcopy) t.Vc = t.d.Vcopy;
+      else { t.Vc = p; p += (size_t)t.d.m1 * t.d.n; }
+      zero.push_back(Axpy2D{t.Vc, t.Vc, t.d.m1, t.d.m1, t.d.m1, t.kr, 0.0, 0.0});
+    }
+    zero.push_back(Axpy2D{t.d.T, t.d.T, t.d.ldt, t.d.ldt, t.d.n, t.d.n, 0.0, 0.0});
+    steps = std::max(steps, (t.kr + kSubJB - 1) / kSubJB);
+  }
+  launch_axpy(zero, stream);
+  std::vector<QrSubDesc> sub;
+  std::vector<QrApplyDesc> app;
+  std::vector<GemmDesc> gx, gy, gt;
+  for (int st = 0; st < steps; ++st) {
+    const int j0 = st * kSubJB;
+    sub.clear(); app.clear(); gx.clear(); gy.clear(); gt.clear();
+    for (Task& t : tk) {
+      if (j0 >= t.kr) continue;
+      const QrPanelDesc& d = t.d;
+      const int jb = std::min(kSubJB, t.kr - j0);
+      double* Tjj = d.T + (size_t)j0 * d.ldt + j0;
+      QrSubDesc q{};
+      q.jb = jb; q.T = Tjj; q.ldt = d.ldt; q.lda1 = d.lda1;
+      q.A1 = d.A1 + (size_t)j0 * d.lda1 + j0;
+      if (t.ts) {
+        q.ts = 1; q.nR = jb; q.A2 = d.A2 + (size_t)j0 * d.lda2; q.lda2 = d.lda2; q.m2 = d.m2;
+      } else {
+        q.ts = 0; q.nR = d.m1 - j0; q.Vc = t.Vc + (size_t)j0 * d.m1 + j0; q.ldvc = d.m1;
+      }
+      sub.push_back(q);
+      const int rest = d.n - j0 - jb;
+      if (rest > 0) {
+        QrApplyDesc a{};
+        a.T = Tjj; a.ldt = d.ldt; a.n = jb; a.ncols = rest;
+        if (t.ts) {
+          a.V = d.A2 + (size_t)j0 * d.lda2; a.ldv = d.lda2;
+          a.A1 = d.A1 + (size_t)(j0 + jb) * d.lda1 + j0; a.lda1 = d.lda1;
+          a.A2 = d.A2 + (size_t)(j0 + jb) * d.lda2; a.lda2 = d.lda2; a.m2 = d.m2;
+        } else {
+          a.V = t.Vc + (size_t)j0 * d.m1 + j0; a.ldv = d.m1;
+          a.A1 = nullptr;
+          a.A2 = d.A1 + (size_t)(j0 + jb) * d.lda1 + j0; a.lda2 = d.lda1; a.m2 = d.m1 - j0;
+        }
+        app.push_back(a);
+      }
+      if (j0 > 0) {
+        // X = V(:, 0:j0)^T V(:, j0:j0+jb), Y = T11 X, T12 = -Y T22
+        GemmDesc g{};
+        g.m = j0; g.n = jb; g.transA = 1;
+        if (t.ts) { g.A = d.A2; g.lda = d.lda2; g.B = d.A2 + (size_t)j0 * d.lda2; g.ldb = d.lda2; g.k = d.m2; }
+        else { g.A = t.Vc + j0; g.lda = d.m1; g.B = t.Vc + (size_t)j0 * d.m1 + j0; g.ldb = d.m1; g.k = d.m1 - j0; }
+        g.C = t.X; g.ldc = j0; g.alpha = 1.0; g.beta = 0.0;
+        gx.push_back(g);
+        GemmDesc h{};
+        h.A = d.T; h.lda = d.ldt; h.B = t.X; h.ldb = j0; h.C = t.Y; h.ldc = j0;
+        h.m = j0; h.n = jb; h.k = j0; h.alpha = 1.0; h.beta = 0.0;
+        gy.push_back(h);
+        GemmDesc f{};
+        f.A = t.Y; f.lda = j0; f.B = Tjj; f.ldb = d.ldt; f.C = d.T + (size_t)j0 * d.ldt; f.ldc = d.ldt;
+        f.m = j0; f.n = jb; f.k = jb; f.alpha = -1.0; f.beta = 0.0;
+        gt.push_back(f);
+      }
+    }
+    launch_subpanels(sub, stream);
+    if (!app.empty()) launch_qr_apply(app.data(), (int)app.size(), stream, app_ws);  // 2 jb x ncols per task
+    if (!gx.empty()) {
+      launch_gemm_batch(gx.data(), (int)gx.size(), stream);
+      launch_gemm_batch(gy.data(), (int)gy.size(), stream);
+      launch_gemm_batch(gt.data(), (int)gt.size(), stream);
+    }
   }
 }
 
@@ -234,7 +540,22 @@ void launch_qr_apply(const QrApplyDesc* descs, int n, hipStream_t stream, double
 }  // namespace parsec
 
 extern "C" {
+// Blocked panel (the engine's path); scratch from a cached test buffer.
 int parsec_amd_qr_panel(const parsec::QrPanelDesc* d, int n, void* stream) {
+  static void* ws = nullptr;
+  static size_t ws_bytes = 0;
+  const size_t need = parsec::kern::qr_panel_workspace_bytes(d, n);
+  if (need > ws_bytes) {
+    (void)hipDeviceSynchronize();
+    if (ws) (void)hipFree(ws);
+    if (hipMalloc(&ws, need) != hipSuccess) return -1;
+    ws_bytes = need;
+  }
+  parsec::kern::launch_qr_panel_blocked(d, n, (hipStream_t)stream, static_cast<double*>(ws));
+  return (int)hipGetLastError();
+}
+// One-level panel (one workgroup walks every column): reference path.
+int parsec_amd_qr_panel_unblocked(const parsec::QrPanelDesc* d, int n, void* stream) {
   parsec::kern::launch_qr_panel(d, n, (hipStream_t)stream);
   return (int)hipGetLastError();
 }

@@ -595,16 +595,12 @@ static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) 
   const bool use_big = g_gemm_tile_policy == 128 || (g_gemm_tile_policy == 0 && big && t128 >= g_gemm_big_tiles);
   if (!use_big) { launch_gemm_shape<64, 64, 16, 2, 2, 2>(a, descs, n, stream); return; }
   switch (g_gemm_variant) {
-    case 1: launch_gemm_shape<128, 128, 32, 2, 2, 1>(a, descs, n, stream); break;
-    case 2: launch_gemm_shape<256, 128, 16, 4, 2, 2>(a, descs, n, stream); break;
-    case 3: launch_gemm_shape<128, 128, 32, 2, 2, 2>(a, descs, n, stream); break;
-    case 4: launch_gemm_shape<256, 128, 32, 4, 2, 1>(a, descs, n, stream); break;
     case 6: launch_gemm_shape<128, 128, 16, 4, 2, 2>(a, descs, n, stream); break;
-    case 7: launch_gemm_shape<128, 128, 32, 2, 4, 1>(a, descs, n, stream); break;
     case 8: launch_gemm_shape<128, 128, 16, 2, 2, 2>(a, descs, n, stream); break;
     // default: 8 waves (2 x 4) of 64x32 per 128x128 tile, 126 VGPRs -> 4 waves per
     // SIMD with two workgroups per CU (measured: DPOTRF 64k +4 %, 16k +7 % over
-    // the 4-wave 64x64-per-wave kernel, profiles/r1_gemm_variants_v8.log)
+    // the 4-wave 64x64-per-wave kernel = variant 8; profiles/r1_gemm_variants_v8.log;
+    // BK=32 single-buffer and 256x128 tiles measured no better: r1_gemm_variants_v4.log)
     default: launch_gemm_shape<128, 128, 16, 2, 4, 2>(a, descs, n, stream); break;
   }
 }
@@ -835,6 +831,8 @@ size_t potrf_workspace_bytes(const PotrfDesc& p);
 size_t trsm_w_workspace_bytes(const TrsmGemmDesc* d, int n);
 void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, double* ws);
 void launch_qr_panel(const QrPanelDesc* descs, int n, hipStream_t stream);
+void launch_qr_panel_blocked(const QrPanelDesc* descs, int n, hipStream_t stream, double* ws);
+size_t qr_panel_workspace_bytes(const QrPanelDesc* descs, int n);
 void launch_qr_apply(const QrApplyDesc* descs, int n, hipStream_t stream, double* ws);
 size_t qr_apply_workspace_bytes(const QrApplyDesc* descs, int n);
 }  // namespace kern
@@ -843,6 +841,7 @@ size_t kernel_batch_workspace_bytes(const KernelBatch& b) {
   size_t w = 0;
   for (auto& p : b.potrf) w = std::max(w, kern::potrf_workspace_bytes(p));
   if (!b.trsm_w.empty()) w = std::max(w, kern::trsm_w_workspace_bytes(b.trsm_w.data(), (int)b.trsm_w.size()));
+  if (!b.qr_panel.empty()) w = std::max(w, kern::qr_panel_workspace_bytes(b.qr_panel.data(), (int)b.qr_panel.size()));
   w = std::max(w, kern::trsm_workspace_bytes(b.trsm.data(), (int)b.trsm.size()));
   return std::max(w, kern::qr_apply_workspace_bytes(b.qr_apply.data(), (int)b.qr_apply.size()));
 }
@@ -851,7 +850,7 @@ void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal,
   (void)device_ordinal;
   // critical-path kernels first: POTRF, then TRSM, then the GEMM/SYRK updates
   for (auto& p : b.potrf) kern::launch_potrf(p, stream, static_cast<double*>(ws));
-  if (!b.qr_panel.empty()) kern::launch_qr_panel(b.qr_panel.data(), (int)b.qr_panel.size(), stream);
+  if (!b.qr_panel.empty()) kern::launch_qr_panel_blocked(b.qr_panel.data(), (int)b.qr_panel.size(), stream, static_cast<double*>(ws));
   if (!b.trsm.empty()) kern::launch_trsm_batch(b.trsm.data(), (int)b.trsm.size(), stream, static_cast<double*>(ws));
   if (!b.trsm_w.empty()) kern::launch_trsm_w_batch(b.trsm_w.data(), (int)b.trsm_w.size(), stream, static_cast<double*>(ws));
   if (!b.qr_apply.empty()) kern::launch_qr_apply(b.qr_apply.data(), (int)b.qr_apply.size(), stream, static_cast<double*>(ws));
