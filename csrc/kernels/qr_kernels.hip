@@ -259,12 +259,21 @@ __global__ __launch_bounds__(kSubThreads) void qr_subpanel_kernel(const QrSubArg
         p[c] = __builtin_fma(v[q], x, p[c]);
       }
     }
+    // transposing butterfly: each exchange halves the values a lane keeps, so
+    // 32 partial sums reduce over the wave in 32 shuffles (not 32 x 6); lane
+    // pair (2c', 2c'+1) ends with column c = (lane >> 1) & 31
 #pragma unroll
-    for (int c = 0; c < kSubJB; ++c) p[c] = wave_sum(p[c]);
-    if (lane == 0) {
+    for (int h = kSubJB / 2, bit = 32; h >= 1; h >>= 1, bit >>= 1) {
+      const bool up = lane & bit;
 #pragma unroll
-      for (int c = 0; c < kSubJB; ++c) red[wv][c] = p[c];
+      for (int i = 0; i < h; ++i) {
+        const double send = up ? p[i] : p[i + h];
+        const double keep = up ? p[i + h] : p[i];
+        p[i] = keep + __shfl_xor(send, bit, 64);
+      }
     }
+    p[0] += __shfl_xor(p[0], 1, 64);
+    if (!(lane & 1)) red[wv][(lane >> 1) & 31] = p[0];
     __syncthreads();
     if (tid < kSubJB) {
       double t = 0.0;
