@@ -115,7 +115,8 @@ def bench_stencil(args):
     pa.mca_set("device_hip_mask", str(1 << local))
     _comm(pa, world, rank, local)
     ctx = pa.init(args.cores)
-    G = pa.StencilGrid(rank, world, args.n, args.n, args.n, args.b, args.b, args.b)
+    # grid resident in HBM (the home device of every block and face buffer)
+    G = pa.StencilGrid(rank, world, args.n, args.n, args.n, args.b, args.b, args.b, device=pa.first_gpu_device_index())
     pa.stencil3d_run(ctx, G, 2, 0.4, 0.1, True)  # warmup: tiles to HBM, kernels loaded
     secs, pts, _ = pa.stencil3d_run(ctx, G, args.iters, 0.4, 0.1, True)
     if world > 1:

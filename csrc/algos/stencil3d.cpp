@@ -26,15 +26,7 @@
 
 namespace parsec {
 namespace kern {
-struct StencilArgs {
-  const double* u;
-  double* out;
-  const double* fin[6];
-  double* fout[6];
-  int bx, by, bz;
-  double c0, c1;
-};
-void launch_stencil7(const StencilArgs& a, hipStream_t stream);
+using StencilArgs = StencilDesc;
 }  // namespace kern
 
 namespace algos {
@@ -243,7 +235,7 @@ Stencil3DResult stencil3d_run(Context* ctx, StencilGrid* G, int iters, double c0
           a.out = out;
           a.bx = p.ex; a.by = p.ey; a.bz = p.ez;
           a.c0 = p.c0; a.c1 = p.c1;
-          c->batch->generic.push_back([a](hipStream_t s) { kern::launch_stencil7(a, s); });
+          c->batch->stencil.push_back(a);  // grouped with the round's other block updates
           return HOOK_DONE;
         });
       tp->add_chore(tc, DEV_CPU, [vidx](ExecutionStream*, Task* t) {

@@ -112,16 +112,27 @@ struct QrApplyDesc {
   int m2, n, ncols;
 };
 
+// One block update of the DTD 3D 7-point stencil (stencil_kernels.hip).
+struct StencilDesc {
+  const double* u;
+  double* out;
+  const double* fin[6];  // -x +x -y +y -z +z neighbour planes (nullptr: boundary)
+  double* fout[6];       // this block's boundary planes (nullptr: not needed)
+  int bx, by, bz;
+  double c0, c1;
+};
+
 struct KernelBatch {
   std::vector<GemmDesc> gemm;
   std::vector<TrsmDesc> trsm;
   std::vector<PotrfDesc> potrf;
   std::vector<TrsmGemmDesc> trsm_w;
+  std::vector<StencilDesc> stencil;
   std::vector<QrPanelDesc> qr_panel;
   std::vector<QrApplyDesc> qr_apply;
   std::vector<std::function<void(hipStream_t)>> generic;  // other kernels, launched in order
-  bool empty() const { return gemm.empty() && trsm.empty() && potrf.empty() && trsm_w.empty() && qr_panel.empty() && qr_apply.empty() && generic.empty(); }
-  void clear() { gemm.clear(); trsm.clear(); potrf.clear(); trsm_w.clear(); qr_panel.clear(); qr_apply.clear(); generic.clear(); }
+  bool empty() const { return gemm.empty() && trsm.empty() && potrf.empty() && trsm_w.empty() && stencil.empty() && qr_panel.empty() && qr_apply.empty() && generic.empty(); }
+  void clear() { gemm.clear(); trsm.clear(); potrf.clear(); trsm_w.clear(); stencil.clear(); qr_panel.clear(); qr_apply.clear(); generic.clear(); }
 };
 
 struct HipDevice;

@@ -10,31 +10,36 @@
 // fill 256 CUs from one block), the k-1 / k / k+1 values kept in registers.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "../device/device.hpp"
 
 namespace parsec {
 namespace kern {
 
-struct StencilArgs {
-  const double* u;
-  double* out;
-  const double* fin[6];  // -x +x -y +y -z +z (nullptr: boundary)
-  double* fout[6];
-  int bx, by, bz;
-  double c0, c1;
-};
+using StencilArgs = StencilDesc;
 
 constexpr int kStencilKc = 16;
+constexpr int kMaxStencilBatch = 24;
 
-__global__ __launch_bounds__(256) void stencil7_kernel(const StencilArgs a) {
-  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+struct StencilBatchArgs {
+  int count;
+  int start[kMaxStencilBatch + 1];  // first workgroup of each block update
+  StencilDesc d[kMaxStencilBatch];
+};
+static_assert(sizeof(StencilBatchArgs) <= 4096, "StencilBatchArgs exceeds the kernel argument limit");
+
+// 64 x 4 (i, j) columns of kStencilKc planes per workgroup
+__device__ __forceinline__ void stencil7_tile(const StencilArgs& a, int tx, int ty, int tz) {
+  const int i = tx * 64 + (threadIdx.x & 63);
+  const int j = ty * 4 + (threadIdx.x >> 6);
   if (i >= a.bx || j >= a.by) return;
+  const int blockIdx_z = tz;
   const int bx = a.bx, by = a.by, bz = a.bz;
   const size_t plane = (size_t)bx * by;
   const double* __restrict__ u = a.u;
   auto at = [&](int k) { return u[(size_t)k * plane + (size_t)j * bx + i]; };
-  const int k0 = blockIdx.z * kStencilKc, k1 = min(bz, k0 + kStencilKc);
+  const int k0 = blockIdx_z * kStencilKc, k1 = min(bz, k0 + kStencilKc);
   double zm = k0 > 0 ? at(k0 - 1) : (a.fin[4] ? a.fin[4][(size_t)j * bx + i] : 0.0);
   double c = at(k0);
   for (int k = k0; k < k1; ++k) {
@@ -57,9 +62,44 @@ __global__ __launch_bounds__(256) void stencil7_kernel(const StencilArgs a) {
   }
 }
 
+__global__ __launch_bounds__(256) void stencil7_kernel(const StencilArgs a) { stencil7_tile(a, blockIdx.x, blockIdx.y, blockIdx.z); }
+
+// Every block update of a scheduling round in ONE launch (1D grid over all of
+// their workgroups; a binary search maps the workgroup to its block).
+__global__ __launch_bounds__(256) void stencil7_batch_kernel(const StencilBatchArgs args) {
+  const int w = blockIdx.x;
+  int lo = 0, hi = args.count - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (args.start[mid] <= w) lo = mid;
+    else hi = mid - 1;
+  }
+  const StencilArgs& a = args.d[lo];
+  const int local = w - args.start[lo];
+  const int nx = (a.bx + 63) / 64, ny = (a.by + 3) / 4;
+  stencil7_tile(a, local % nx, (local / nx) % ny, local / (nx * ny));
+}
+
+static int stencil_wgs(const StencilArgs& a) { return ((a.bx + 63) / 64) * ((a.by + 3) / 4) * ((a.bz + kStencilKc - 1) / kStencilKc); }
+
 void launch_stencil7(const StencilArgs& a, hipStream_t stream) {
   dim3 grid((a.bx + 63) / 64, (a.by + 3) / 4, (a.bz + kStencilKc - 1) / kStencilKc);
   hipLaunchKernelGGL(stencil7_kernel, grid, dim3(256), 0, stream, a);
+}
+
+void launch_stencil7_batch(const StencilDesc* d, int n, hipStream_t stream) {
+  for (int s0 = 0; s0 < n; s0 += kMaxStencilBatch) {
+    StencilBatchArgs a;
+    a.count = std::min(kMaxStencilBatch, n - s0);
+    int total = 0;
+    for (int i = 0; i < a.count; ++i) {
+      a.d[i] = d[s0 + i];
+      a.start[i] = total;
+      total += stencil_wgs(a.d[i]);
+    }
+    a.start[a.count] = total;
+    if (total > 0) hipLaunchKernelGGL(stencil7_batch_kernel, dim3(total), dim3(256), 0, stream, a);
+  }
 }
 
 }  // namespace kern

@@ -831,6 +831,7 @@ size_t potrf_workspace_bytes(const PotrfDesc& p);
 size_t trsm_w_workspace_bytes(const TrsmGemmDesc* d, int n);
 void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, double* ws);
 void launch_qr_panel(const QrPanelDesc* descs, int n, hipStream_t stream);
+void launch_stencil7_batch(const StencilDesc* d, int n, hipStream_t stream);
 void launch_qr_panel_blocked(const QrPanelDesc* descs, int n, hipStream_t stream, double* ws);
 size_t qr_panel_workspace_bytes(const QrPanelDesc* descs, int n);
 void launch_qr_apply(const QrApplyDesc* descs, int n, hipStream_t stream, double* ws);
@@ -855,6 +856,7 @@ void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal,
   if (!b.trsm_w.empty()) kern::launch_trsm_w_batch(b.trsm_w.data(), (int)b.trsm_w.size(), stream, static_cast<double*>(ws));
   if (!b.qr_apply.empty()) kern::launch_qr_apply(b.qr_apply.data(), (int)b.qr_apply.size(), stream, static_cast<double*>(ws));
   if (!b.gemm.empty()) kern::launch_gemm_batch(b.gemm.data(), (int)b.gemm.size(), stream);
+  if (!b.stencil.empty()) kern::launch_stencil7_batch(b.stencil.data(), (int)b.stencil.size(), stream);
   for (auto& g : b.generic) g(stream);
 }
 
