@@ -69,8 +69,8 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // bounds checks and no divergent control flow around its loads.
 // NBUF = 2: double-buffered LDS, one barrier per k-tile; NBUF = 1: one LDS
 // buffer (half the LDS, two barriers per k-tile) for deeper BK.
-template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF = 2>
-__global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(WM * WN / 2))) void dgemm_batch_kernel(const GemmBatchArgs args) {
+template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF = 2, int OCC = WM * WN / 2>
+__global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OCC))) void dgemm_batch_kernel(const GemmBatchArgs args) {
   constexpr int NT = WM * WN * 64;
   constexpr int WTM = BM / WM;
   constexpr int WTN = BN / WN;
@@ -542,7 +542,7 @@ static int g_gemm_variant = -1;      // big-tile kernel shape (PARSEC_GEMM_VARIA
 static int g_gemm_full = -1;         // PARSEC_GEMM_FULL=0 disables the unchecked fast path
 static int g_gemm_big_tiles = 384;   // PARSEC_GEMM_BIG_TILES: 128x128 tiles in a launch to pick the big kernel
 
-template <int BM, int BN, int BK, int WM, int WN, int NBUF>
+template <int BM, int BN, int BK, int WM, int WN, int NBUF, int OCC = WM * WN / 2>
 static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hipStream_t stream) {
   int total = 0;
   bool full = g_gemm_full != 0;
@@ -561,8 +561,8 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
   const dim3 grid(total), block(WM * WN * 64);
 #define PARSEC_GEMM_LAUNCH(TA, TB)                                                                                    \
   do {                                                                                                                \
-    if (full) hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF>), grid, block, 0, stream, a); \
-    else hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, false, NBUF>), grid, block, 0, stream, a);    \
+    if (full) hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, OCC>), grid, block, 0, stream, a); \
+    else hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, false, NBUF, OCC>), grid, block, 0, stream, a);    \
   } while (0)
   switch (mode) {
     case 0: PARSEC_GEMM_LAUNCH(false, false); break;
@@ -600,7 +600,8 @@ static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) 
     // default: 8 waves (2 x 4) of 64x32 per 128x128 tile, 126 VGPRs -> 4 waves per
     // SIMD with two workgroups per CU (measured: DPOTRF 64k +4 %, 16k +7 % over
     // the 4-wave 64x64-per-wave kernel = variant 8; profiles/r1_gemm_variants_v8.log;
-    // BK=32 single-buffer and 256x128 tiles measured no better: r1_gemm_variants_v4.log)
+    // BK=32 single-buffer and 256x128 tiles (8 or 16 waves) measured no better:
+    // r1_gemm_variants_v4.log, r1_gemm_variants_v13.log)
     default: launch_gemm_shape<128, 128, 16, 2, 4, 2>(a, descs, n, stream); break;
   }
 }

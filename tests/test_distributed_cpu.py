@@ -35,6 +35,7 @@ def run_ranks(nranks, *args, timeout=120, worker=WORKER):
     (2, 1, 2, "star", "fourcounter"),
     (4, 2, 2, "chain", "local"),
     (4, 2, 2, "binomial", "fourcounter"),
+    (8, 4, 2, "binomial", "fourcounter"),  # the process grid bench.py uses on 8 GPUs
 ])
 def test_distributed_dpotrf(pa, nranks, P, Q, topo, termdet):
     outs = run_ranks(nranks, 512, 64, P, Q, "lfq", topo, termdet)
