@@ -524,7 +524,7 @@ void PtgTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
     }
     for_each_task(this, tc, [&](const int32_t* L) {
       if (tc->rank_of(this, L) != my) return;
-      if (!tc->def.nb_local_tasks_fn) ++nb_local;
+      if (!tc->def.nb_local_tasks_fn && !dynamic_termdet) ++nb_local;
       if (tc->def.startup_fn) return;
       if (tc->count_task_inputs(this, L) != 0) return;
       Task* t = task_new(es, this, tc);
@@ -535,6 +535,7 @@ void PtgTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
       ready.push_back(t);
     });
   }
+  if (dynamic_termdet) nb_local = (int64_t)ready.size();  // the rest is counted on first activation
   // additive: remote activations may already have run (and completed) tasks
   tdm->taskpool_addto_nb_tasks(this, nb_local);
 }
@@ -552,6 +553,7 @@ void PtgTaskpool::activate(ExecutionStream* es, PtgTaskClass* tc, const int32_t*
       task->key = key;
       task->priority = tc->priority_of(this, L);
       task->deps_remaining = tc->count_task_inputs(this, L);
+      if (dynamic_termdet) tdm->taskpool_addto_nb_tasks(this, 1);
       m.emplace(key, task);
     } else {
       task = it->second;

@@ -148,6 +148,13 @@ class PtgTaskpool : public Taskpool {
   std::vector<PtgTaskClass*> classes;
   ShardedMap<Task*> pending{10};
   std::vector<int64_t> globals;      // generic storage for generated code
+  // ptgpp --dynamic-termdet: tasks are counted as they are discovered (startup
+  // tasks, then each first activation) instead of enumerating the whole local
+  // task space at startup (reference jdf2c.c dynamic termination detection).
+  bool dynamic_termdet = false;
+  // ptgpp --dep-management: both modes map to the sharded hash table of pending
+  // tasks (dense index arrays bring nothing on top of it here)
+  std::string dep_management = "dynamic-hash-table";
   std::vector<std::string> global_names;
   bool finalized = false;
   PtgTaskpool();

@@ -22,8 +22,9 @@ class CompileError(RuntimeError):
     pass
 
 
-def run_ptgpp(jdf, out_base=None, function_base=None, check_only=False):
-    """Run parsec-ptgpp; returns CompletedProcess (stdout/stderr captured)."""
+def run_ptgpp(jdf, out_base=None, function_base=None, check_only=False, flags=()):
+    """Run parsec-ptgpp; returns CompletedProcess (stdout/stderr captured).
+    ``flags``: extra compiler options (--dynamic-termdet, --dep-management X, --noline, -W...)."""
     if not os.path.exists(PTGPP):
         raise CompileError("parsec-ptgpp is not built (python -m parsec_amd._build)")
     cmd = [PTGPP, "-i", jdf]
@@ -33,14 +34,15 @@ def run_ptgpp(jdf, out_base=None, function_base=None, check_only=False):
         cmd += ["-f", function_base]
     if check_only:
         cmd.append("-E")
+    cmd += list(flags)
     return subprocess.run(cmd, capture_output=True, text=True)
 
 
-def compile_jdf(jdf, outdir, name=None):
+def compile_jdf(jdf, outdir, name=None, flags=()):
     os.makedirs(outdir, exist_ok=True)
     name = name or os.path.splitext(os.path.basename(jdf))[0]
     base = os.path.join(outdir, name)
-    r = run_ptgpp(jdf, base, name)
+    r = run_ptgpp(jdf, base, name, flags=flags)
     if r.returncode != 0:
         raise CompileError(r.stderr)
     return base + ".cpp", base + ".h"
@@ -60,8 +62,8 @@ def compile_flags(hip=False):
     return ["g++", "-std=c++20", "-O2"] + inc, libs
 
 
-def build_program(jdf, outdir, extra_sources=(), hip=None, name=None):
-    cpp, _ = compile_jdf(jdf, outdir, name)
+def build_program(jdf, outdir, extra_sources=(), hip=None, name=None, flags=()):
+    cpp, _ = compile_jdf(jdf, outdir, name, flags=flags)
     hip = _has_hip_body(jdf) if hip is None else hip
     cc, libs = compile_flags(hip)
     exe = os.path.splitext(cpp)[0]

@@ -84,3 +84,13 @@ def test_all2all_multiprocess(apps, nranks):
     assert rc == 0, outs
     assert sum(int(o.split("recv")[1].split()[0]) for o, _ in outs) == nranks * nranks
     assert all("bad 0" in o for o, _ in outs)
+
+
+def test_dynamic_termdet_multiprocess(tmp_path):
+    """ptgpp --dynamic-termdet across 3 ranks: remote first activations count the
+    tasks they create; termination still waits for the last remote NODE."""
+    exe = ptgpp.build_program(os.path.join(HERE, "jdf", "tree_reduce.jdf"), str(tmp_path), flags=["--dynamic-termdet"])
+    rc, outs = launch.launch(3, [exe, "6"], timeout=120, capture=True)
+    assert rc == 0, outs
+    assert "root 2080" in outs[0][0]
+    assert sum(int(o.split("nodes")[1].split()[0]) for o, _ in outs) == 63

@@ -84,3 +84,34 @@ def test_generated_header_api(tmp_path):
     # hidden global with a default is not a parameter of _new
     assert "parsec_bcast_gather_new(parsec_matrix_block_cyclic_t* descA, int NB)" in hdr
     assert "#define PARSEC_bcast_gather_DEFAULT_ADT_IDX 0" in hdr
+
+
+def test_compiler_flags(tmp_path):
+    """--noline drops #line directives, --dep-management is recorded in the
+    generated constructor, a bad mode is rejected (reference main.c:177-197)."""
+    src = os.path.join(JDF, "chain.jdf")
+    cpp, _ = ptgpp.compile_jdf(src, str(tmp_path / "a"), flags=["--noline", "--dep-management", "index-array", "-Wremote"])
+    text = open(cpp).read()
+    assert "#line" not in text
+    assert 'dep_management = "index-array"' in text
+    cpp2, _ = ptgpp.compile_jdf(src, str(tmp_path / "b"))
+    assert "#line" in open(cpp2).read()
+    r = ptgpp.run_ptgpp(src, str(tmp_path / "c"), flags=["--dep-management", "bogus"])
+    assert r.returncode != 0
+
+
+@pytest.mark.parametrize("name,args,expect", [
+    ("tree_reduce", ["6"], "root 2080 nodes 63 bad 0"),
+    ("chain", [], "chain value 10"),
+    ("bcast_gather", [], "leaves 37 sink 1 bad 0"),
+])
+def test_dynamic_termdet(tmp_path, name, args, expect):
+    """--dynamic-termdet: tasks are counted as they are discovered instead of
+    enumerating the local task space at startup; the DAG must still terminate
+    exactly when its last task completes."""
+    exe = ptgpp.build_program(os.path.join(JDF, name + ".jdf"), str(tmp_path), flags=["--dynamic-termdet"])
+    cpp = exe + ".cpp"
+    assert "dynamic_termdet = true" in open(cpp).read()
+    r = subprocess.run([exe] + args, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert expect in r.stdout

@@ -40,6 +40,9 @@ constexpr int kMaxOutFlows = 10;   // reference MAX_DEP_OUT_COUNT
 constexpr int kMaxFlows = 20;
 
 std::string g_file;
+bool g_noline = false;               // --noline: no #line directives
+bool g_dynamic_termdet = false;      // --dynamic-termdet
+std::string g_dep_management = "dynamic-hash-table";  // --dep-management
 int g_errors = 0;
 
 [[noreturn]] void die(int line, const std::string& msg) {
@@ -887,7 +890,7 @@ struct Gen {
       else c << "  [[maybe_unused]] void* " << fl.name << " = parsec::ptg::flow_ptr(this_task, " << k << ");\n";
     }
     if (gpu) c << "  [[maybe_unused]] parsec::ptg::GpuBody parsec_body{__ctx->stream, __ctx};\n";
-    c << "#line " << b.line + 1 << " \"" << g_file << "\"\n";
+    if (!g_noline) c << "#line " << b.line + 1 << " \"" << g_file << "\"\n";
     c << "  {" << b.code << "}\n";
     c << "  return PARSEC_HOOK_RETURN_DONE;\n}\n\n";
   }
@@ -925,7 +928,10 @@ struct Gen {
 
     c << "// Generated by parsec-ptgpp from " << g_file << ". Do not edit.\n";
     c << "#include \"parsec_amd/ptg_gen.hpp\"\n";
-    if (!j.prologue.empty()) c << "#line " << j.prologue_line << " \"" << g_file << "\"\n" << j.prologue << "\n";
+    if (!j.prologue.empty()) {
+      if (!g_noline) c << "#line " << j.prologue_line << " \"" << g_file << "\"\n";
+      c << j.prologue << "\n";
+    }
     c << "#include \"" << base_name(base) << ".h\"\n\n";
     // bodies
     for (auto& f : j.functions)
@@ -1012,8 +1018,13 @@ struct Gen {
     for (auto& kv : j.options)
       if (kv.first == "nb_local_tasks_fn")
         c << "  (void)__has_nb_local;\n  if (!__tp->classes.empty()) __tp->classes[0]->def.nb_local_tasks_fn = [](const parsec::Taskpool* tp) { return (int64_t)" << kv.second << "(tp); };\n";
+    if (g_dynamic_termdet) c << "  __tp->dynamic_termdet = true;\n";
+    c << "  __tp->dep_management = \"" << g_dep_management << "\";\n";
     c << "  __tp->finalize();\n  return __tp;\n}\n";
-    if (!j.epilogue.empty()) c << "#line " << j.epilogue_line << " \"" << g_file << "\"\n" << j.epilogue << "\n";
+    if (!j.epilogue.empty()) {
+      if (!g_noline) c << "#line " << j.epilogue_line << " \"" << g_file << "\"\n";
+      c << j.epilogue << "\n";
+    }
   }
   static std::string base_name(const std::string& p) {
     size_t s = p.find_last_of('/');
@@ -1032,8 +1043,19 @@ int main(int argc, char** argv) {
     else if ((a == "-o" || a == "--output") && i + 1 < argc) out = argv[++i];
     else if ((a == "-f" || a == "--function-name") && i + 1 < argc) fn = argv[++i];
     else if (a == "-E") check_only = true;
-    else if (a == "-h" || a == "--help") {
-      printf("usage: parsec-ptgpp -i file.jdf [-o output_base] [-f function_base] [-E]\n");
+    else if (a == "--noline") g_noline = true;
+    else if (a == "--dynamic-termdet") g_dynamic_termdet = true;
+    else if (a == "--dep-management" && i + 1 < argc) {
+      g_dep_management = argv[++i];
+      if (g_dep_management != "index-array" && g_dep_management != "dynamic-hash-table") {
+        fprintf(stderr, "parsec-ptgpp: --dep-management takes index-array or dynamic-hash-table\n");
+        return 2;
+      }
+    } else if (a.rfind("-W", 0) == 0) {
+      // warning controls (-Wremote, -Wno-masks, ...): accepted, diagnostics are always on
+    } else if (a == "-h" || a == "--help") {
+      printf("usage: parsec-ptgpp -i file.jdf [-o output_base] [-f function_base] [-E] [--noline]\n"
+             "                    [--dynamic-termdet] [--dep-management index-array|dynamic-hash-table] [-W...]\n");
       return 0;
     } else if (in.empty() && a[0] != '-') in = a;
     else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
