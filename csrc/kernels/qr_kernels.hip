@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "../device/device.hpp"
@@ -21,6 +22,8 @@ namespace parsec {
 namespace kern {
 
 void launch_gemm_batch(const GemmDesc* descs, int n, hipStream_t stream);  // tile_kernels.hip
+
+typedef double double4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kQrThreads = 256;
 constexpr int kMaxQrBatch = 32;
@@ -397,12 +400,577 @@ size_t qr_panel_workspace_bytes(const QrPanelDesc* descs, int n) {
 
 void launch_qr_apply(const QrApplyDesc* descs, int n, hipStream_t stream, double* ws);
 
+// ===================================================== column-per-lane panel
+// Fast path for panels of at most 8 x kP2MaxRPT virtual rows (TSQRT with
+// m2 <= 512, GEQRT with m1 <= 544). Two launches per 32-column sub-step for the
+// whole batch:
+//  (1) qr_sub2_kernel: one 256-thread workgroup per task factors the sub-panel.
+//      Lane l owns column (l & 31) for the rows g + 8 i of row group
+//      g = 2 * wave + (l >> 5), so the 32-wide reduction V^T A of a column step
+//      is a per-thread dot product + one xor-32 shuffle + a 4-way LDS sum, and
+//      selecting column j is a lane predicate (no register-array selects). The
+//      reflector v is broadcast through LDS. 3 barriers per column; the
+//      compact-WY T column of step j is formed one step late, off the barrier
+//      chain of the reductions.
+//  (2) qr_subapply_kernel: grouped work items over all tasks:
+//      - trailing column blocks (32 columns): W = C1 + V^T C2 (MFMA), W2 = T^T W,
+//        C1 -= W2, C2 -= V W2 (MFMA, transposed so lanes walk rows: coalesced),
+//      - X blocks of this step: X_lb = V_lb^T V_s (MFMA) for the T extension,
+//      - the T extension of the PREVIOUS step (its X was produced by the
+//        previous launch): T(ib, s-1) = -(sum_lb T(ib, lb) X_lb) T(s-1, s-1).
+//      The last step's T extension runs in one extra launch.
+constexpr int kP2MaxRPT = 68;  // 8 row groups x 68 = 544 = 32 (R block) + 512
+constexpr int kMaxSub2Batch = 40;
+
+struct QrSub2Desc {
+  double* A1;   // GEQRT: sub-panel top-left (row j0, col j0); TS: the jb x jb R block
+  int lda1;
+  int nR;       // GEQRT: rows of the sub-panel (m1 - j0)
+  double* A2;   // TS only: A2 columns j0..j0+jb
+  int lda2, m2;
+  int jb, ts;
+  double* Tjj;  // T block of this step (jb x jb), zeros written below it down to row kr
+  int ldt, tzero;
+  double* Vc;   // GEQRT: clean V block (row j0, col j0); rows [-vzero, 0) are zeroed
+  int ldvc, vzero;
+};
+struct QrSub2Args {
+  int count;
+  QrSub2Desc d[kMaxSub2Batch];
+};
+static_assert(sizeof(QrSub2Args) <= 4096, "QrSub2Args exceeds the kernel argument limit");
+
+template <int RPT>
+__global__ __launch_bounds__(256) void qr_sub2_kernel(const QrSub2Args args) {
+  // Loops over a thread's rows run in chunks of 8 with ONE uniform test per
+  // chunk (skip chunks entirely above the pivot); inside a chunk there are no
+  // branches, so LDS reads issue back to back. vb holds zeros for rows that do
+  // not take part in a step, which keeps the dot products and updates unmasked.
+  constexpr int NCH = (RPT + 7) / 8;
+  const QrSub2Desc& d = args.d[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c = lane & 31, g = 2 * w + (lane >> 5);
+  const bool ts = d.ts != 0;
+  const int jb = d.jb;
+  __shared__ double vb[8][8 * NCH];
+  __shared__ double red1[4];
+  __shared__ double red2[4][32];
+  __shared__ double Tl[32][33];
+  __shared__ double zb[32], taus[32];
+  __shared__ double s_alpha;
+  for (int idx = tid; idx < 32 * 33; idx += 256) (&Tl[0][0])[idx] = 0.0;
+  if (tid < 32) zb[tid] = 0.0;
+  double a[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int vr = g + 8 * i;
+    double x = 0.0;
+    if (c < jb) {
+      if (ts) {
+        if (i < 4) {
+          if (vr <= c) x = d.A1[(size_t)c * d.lda1 + vr];  // upper R only (GEQRT's V lies below)
+        } else if (vr - 32 < d.m2) {
+          x = d.A2[(size_t)c * d.lda2 + (vr - 32)];
+        }
+      } else if (vr < d.nR) {
+        x = d.A1[(size_t)c * d.lda1 + vr];
+      }
+    }
+    a[i] = x;
+  }
+  __syncthreads();
+  // T column jp = -tau_jp T(0:jp, 0:jp) z, formed one step late by wave 3; Tl and
+  // zb start zeroed and fill monotonically, so a full 32-term dot needs no mask
+  auto t_column = [&](int jp) {
+    if (w != 3 || lane >= 32) return;
+    double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+    for (int l = 0; l < 32; l += 2) {
+      t0 = __builtin_fma(Tl[lane][l], zb[l], t0);
+      t1 = __builtin_fma(Tl[lane][l + 1], zb[l + 1], t1);
+    }
+    if (lane < jp) Tl[lane][jp] = -taus[jp] * (t0 + t1);
+    else if (lane == jp) Tl[jp][jp] = taus[jp];
+  };
+  for (int j = 0; j < jb; ++j) {
+    const int jq = j >> 3;
+    // ---- 1: sigma (squares below the pivot) and alpha, column-j lanes only
+    if (c == j) {
+      double sq = 0.0, al = 0.0;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const int i0 = 8 * k;
+        if (i0 + 8 <= jq) continue;
+        if (i0 > jq && !(ts && i0 < 4)) {
+#pragma unroll
+          for (int i = i0; i < i0 + 8 && i < RPT; ++i) sq = __builtin_fma(a[i], a[i], sq);
+        } else {
+#pragma unroll
+          for (int i = i0; i < i0 + 8 && i < RPT; ++i) {
+            const int vr = g + 8 * i;
+            const bool below = ts ? (i >= 4) : (vr > j);
+            sq = below ? __builtin_fma(a[i], a[i], sq) : sq;
+            al = vr == j ? a[i] : al;
+          }
+        }
+      }
+      sq += __shfl_xor(sq, 32, 64);
+      if (lane == c) red1[w] = sq;
+      if (g == (j & 7)) s_alpha = al;
+    }
+    __syncthreads();  // A
+    if (j > 0) t_column(j - 1);
+    const double sigma = red1[0] + red1[1] + red1[2] + red1[3];
+    const double alpha = s_alpha;
+    double tau = 0.0, scale = 0.0, beta = alpha;
+    if (sigma != 0.0) {
+      const double norm = sqrt(alpha * alpha + sigma);
+      beta = alpha >= 0.0 ? -norm : norm;
+      tau = (beta - alpha) / beta;
+      scale = 1.0 / (alpha - beta);
+    }
+    // ---- 2: v (stored in place below the pivot), pivot := beta, v -> LDS
+    if (c == j) {
+      const double pivv = tau != 0.0 ? beta : alpha;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const int i0 = 8 * k;
+        if (i0 + 8 <= jq) continue;
+        if (i0 > jq && !(ts && i0 < 4)) {
+#pragma unroll
+          for (int i = i0; i < i0 + 8 && i < RPT; ++i) {
+            a[i] *= scale;
+            vb[g][i] = a[i];
+          }
+        } else {
+#pragma unroll
+          for (int i = i0; i < i0 + 8 && i < RPT; ++i) {
+            const int vr = g + 8 * i;
+            const bool below = ts ? (i >= 4) : (vr > j);
+            const bool piv = vr == j;
+            const double sc = a[i] * scale;
+            vb[g][i] = below ? sc : (piv ? 1.0 : 0.0);
+            a[i] = below ? sc : (piv ? pivv : a[i]);
+          }
+        }
+      }
+    }
+    __syncthreads();  // B
+    // ---- 3: p_c = sum_r v_r A(r, c) (c > j: trailing w; c < j: z for T)
+    double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int i0 = 8 * k;
+      if (i0 + 8 <= jq) continue;
+#pragma unroll
+      for (int i = i0; i < i0 + 8 && i < RPT; i += 2) {
+        p0 = __builtin_fma(vb[g][i], a[i], p0);
+        if (i + 1 < RPT) p1 = __builtin_fma(vb[g][i + 1], a[i + 1], p1);
+      }
+    }
+    double p = p0 + p1;
+    p += __shfl_xor(p, 32, 64);
+    if (lane < 32) red2[w][c] = p;
+    __syncthreads();  // C
+    const double pc = red2[0][c] + red2[1][c] + red2[2][c] + red2[3][c];
+    // ---- 4: trailing update inside the sub-panel, z and tau for T
+    if (c > j && tau != 0.0) {
+      const double tp = -tau * pc;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const int i0 = 8 * k;
+        if (i0 + 8 <= jq) continue;
+#pragma unroll
+        for (int i = i0; i < i0 + 8 && i < RPT; ++i) a[i] = __builtin_fma(tp, vb[g][i], a[i]);
+      }
+    }
+    if (tid < j) zb[tid] = pc;  // tid < 32: c == tid
+    if (tid == 0) taus[j] = tau;
+  }
+  __syncthreads();
+  t_column(jb - 1);
+  __syncthreads();
+  // ---- write back the sub-panel, the clean V, T (+ zeros below) and zeros above V
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int vr = g + 8 * i;
+    if (c >= jb) continue;
+    if (ts) {
+      if (i < 4) {
+        if (vr <= c) d.A1[(size_t)c * d.lda1 + vr] = a[i];
+      } else if (vr - 32 < d.m2) {
+        d.A2[(size_t)c * d.lda2 + (vr - 32)] = a[i];
+      }
+    } else if (vr < d.nR) {
+      d.A1[(size_t)c * d.lda1 + vr] = a[i];
+      if (d.Vc) d.Vc[(size_t)c * d.ldvc + vr] = vr > c ? a[i] : (vr == c ? 1.0 : 0.0);
+    }
+  }
+  for (int idx = tid; idx < jb * (jb + d.tzero); idx += 256) {
+    const int col = idx / (jb + d.tzero), r = idx % (jb + d.tzero);
+    d.Tjj[(size_t)col * d.ldt + r] = (r < jb && r <= col) ? Tl[r][col] : 0.0;
+  }
+  if (d.Vc)
+    for (int idx = tid; idx < jb * d.vzero; idx += 256) {
+      const int col = idx / d.vzero, r = idx % d.vzero;
+      d.Vc[(size_t)col * d.ldvc + r - d.vzero] = 0.0;
+    }
+}
+
+struct QrSubApplyTask {
+  const double* Vd;  // dense reflector rows of this step (rd x jb, ldv); TS: A2 cols; GEQRT: clean V from row j0
+  int ldv, rd, jb;
+  double* C2;        // trailing dense part (rd x rest, ldc2)
+  int ldc2, rest;
+  double* C1;        // TS: jb x rest block of A1 (identity part of V), else null
+  int ldc1;
+  const double* T22; // this step's T block (jb x jb, upper)
+  int ldt;
+  const double* Vold;  // X blocks: Vold(:, 32 lb : 32 lb + 32) (same rows and ld as Vd), lb < nx
+  double* Xout;        // nx blocks of 32 x 32 (column-major, ld 32)
+  int nx;
+  const double* Xprev; // T extension of the previous step sp: ne = sp blocks of X
+  double* T;           // the tile's T (ldt)
+  int ne, sp, jbp;     // previous step index and width
+};
+constexpr int kMaxSubApplyBatch = 24;
+struct QrSubApplyArgs {
+  int count;
+  int start[kMaxSubApplyBatch + 1];  // first item of each task
+  int ntr[kMaxSubApplyBatch];        // trailing column blocks per task
+  QrSubApplyTask t[kMaxSubApplyBatch];
+};
+static_assert(sizeof(QrSubApplyArgs) <= 4096, "QrSubApplyArgs exceeds the kernel argument limit");
+
+// D(16x16) = A^T B over rows [rb, re): A (16 cols, lda), B (16 cols, ldb).
+// Lanes: m = lane & 15 is A's column, n = lane & 15 B's column, and MFMA u of
+// a 16-row step takes rows 4 (lane >> 4) + u, so each lane reads 4 consecutive
+// doubles per operand. 64 rows per group, the next group prefetched.
+__device__ __forceinline__ double4_t mfma_atb(const double* __restrict__ A, int lda, int acols, const double* __restrict__ B, int ldb, int bcols,
+                                              int rb, int re, int lane) {
+  double4_t acc = {0.0, 0.0, 0.0, 0.0};
+  const int col = lane & 15, kq = 4 * (lane >> 4);
+  const bool av = col < acols, bv = col < bcols;
+  const double* ap = A + (size_t)(av ? col : 0) * lda;
+  const double* bp = B + (size_t)(bv ? col : 0) * ldb;
+  double xa[16], ya[16];
+  auto load = [&](int r0, double* x, double* y) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = r0 + 16 * s + kq + u;
+        const bool ok = r < re;
+        x[4 * s + u] = (av && ok) ? ap[r] : 0.0;
+        y[4 * s + u] = (bv && ok) ? bp[r] : 0.0;
+      }
+  };
+  if (rb < re) load(rb, xa, ya);
+  for (int r0 = rb; r0 < re; r0 += 64) {
+    double xn[16], yn[16];
+    const bool more = r0 + 64 < re;
+    if (more) load(r0 + 64, xn, yn);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[q], ya[q], acc, 0, 0, 0);
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) { xa[q] = xn[q]; ya[q] = yn[q]; }
+    }
+  }
+  return acc;
+}
+
+constexpr int kSubApplyThreads = 512;
+
+__global__ __launch_bounds__(kSubApplyThreads) void qr_subapply_kernel(const QrSubApplyArgs args) {
+  int ti = 0;
+  while (ti + 1 < args.count && (int)blockIdx.x >= args.start[ti + 1]) ++ti;
+  const QrSubApplyTask& t = args.t[ti];
+  int item = blockIdx.x - args.start[ti];
+  constexpr int NT = kSubApplyThreads;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // wave w: 16 x 16 quadrant (iq, cq) of a 32 x 32 A^T B product, half kh of the rows
+  const int qd = w & 3, iq = qd & 1, cq = qd >> 1, kh = w >> 2;
+  const int half = ((t.rd + 31) / 32) * 16;
+  const int rb = kh * half, re = min(t.rd, rb + half);
+  __shared__ double S0[32][33], S1[32][33], S2[32][33], S3[32][33];
+  if (item < args.ntr[ti]) {
+    // ------------------------------------------------ trailing column block
+    const int c0 = item * 32, cw = min(32, t.rest - c0);
+    double4_t acc = mfma_atb(t.Vd + (size_t)(16 * iq) * t.ldv, t.ldv, t.jb - 16 * iq, t.C2 + (size_t)(c0 + 16 * cq) * t.ldc2, t.ldc2, cw - 16 * cq,
+                             rb, re, lane);
+    double(*Sk)[33] = kh ? S3 : S0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Sk[16 * iq + (lane >> 4) + 4 * q][16 * cq + (lane & 15)] = acc[q];  // W (i, col)
+    for (int idx = tid; idx < 1024; idx += NT) {
+      const int cc = idx >> 5, r = idx & 31;
+      S1[r][cc] = (r < t.jb && cc < t.jb && r <= cc) ? t.T22[(size_t)cc * t.ldt + r] : 0.0;  // T (r, cc)
+    }
+    __syncthreads();
+    for (int idx = tid; idx < 1024; idx += NT) {
+      const int cc = idx >> 5, r = idx & 31;
+      double x = S0[r][cc] + S3[r][cc];
+      if (t.C1 && r < t.jb && cc < cw) x += t.C1[(size_t)(c0 + cc) * t.ldc1 + r];
+      S0[r][cc] = x;
+    }
+    __syncthreads();
+    // W2 = T^T W: W2(i, col) = sum_{l <= i} T(l, i) W(l, col)
+    for (int idx = tid; idx < 1024; idx += NT) {
+      const int cc = idx & 31, i = idx >> 5;
+      double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+      for (int l = 0; l < 32; l += 2) {
+        s0 = __builtin_fma(S1[l][i], S0[l][cc], s0);
+        s1 = __builtin_fma(S1[l + 1][i], S0[l + 1][cc], s1);
+      }
+      S2[i][cc] = (i < t.jb && cc < cw) ? s0 + s1 : 0.0;
+    }
+    __syncthreads();
+    if (t.C1)
+      for (int idx = tid; idx < 1024; idx += NT) {
+        const int cc = idx >> 5, r = idx & 31;
+        if (r < t.jb && cc < cw) t.C1[(size_t)(c0 + cc) * t.ldc1 + r] -= S2[r][cc];
+      }
+    // C2 -= V W2, computed transposed: D(m = col, n = row) = C2^T - W2^T V^T,
+    // two 16 x 16 tiles per pass so their loads are in flight together
+    const int fr = lane & 15, fk = lane >> 4;
+    double wa[2][8];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) wa[ct][kk] = -S2[4 * kk + fk][16 * ct + fr];
+    const int nrt = (t.rd + 15) / 16;
+    const int ntiles = 2 * nrt;
+    const int nw = NT / 64;
+    for (int tb = w; tb < ntiles; tb += 2 * nw) {
+      double4_t accs[2];
+      double vv[2][8];
+      int rows[2], cts[2];
+      bool act[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int tile = tb + h * nw;
+        cts[h] = tile & 1;
+        rows[h] = (tile >> 1) * 16 + fr;
+        act[h] = tile < ntiles && 16 * cts[h] < cw;
+        const bool rok = act[h] && rows[h] < t.rd;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int cc = 16 * cts[h] + fk + 4 * q;
+          accs[h][q] = (rok && cc < cw) ? t.C2[(size_t)(c0 + cc) * t.ldc2 + rows[h]] : 0.0;
+        }
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+          const int i = 4 * kk + fk;
+          vv[h][kk] = (rok && i < t.jb) ? t.Vd[(size_t)i * t.ldv + rows[h]] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (!act[h]) continue;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+          accs[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(cts[h] ? wa[1][kk] : wa[0][kk], vv[h][kk], accs[h], 0, 0, 0);
+        if (rows[h] < t.rd) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int cc = 16 * cts[h] + fk + 4 * q;
+            if (cc < cw) t.C2[(size_t)(c0 + cc) * t.ldc2 + rows[h]] = accs[h][q];
+          }
+        }
+      }
+    }
+    return;
+  }
+  item -= args.ntr[ti];
+  if (item < t.nx) {
+    // ------------------------------------- X_lb = Vold(:, lb block)^T Vd
+    double4_t acc = mfma_atb(t.Vold + (size_t)(32 * item + 16 * iq) * t.ldv, t.ldv, 16, t.Vd + (size_t)(16 * cq) * t.ldv, t.ldv, t.jb - 16 * cq, rb,
+                             re, lane);
+    if (kh) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) S3[16 * iq + (lane >> 4) + 4 * q][16 * cq + (lane & 15)] = acc[q];
+    }
+    __syncthreads();
+    if (!kh) {
+      double* X = t.Xout + (size_t)item * 1024;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 16 * iq + (lane >> 4) + 4 * q, cc = 16 * cq + (lane & 15);
+        X[cc * 32 + i] = acc[q] + S3[i][cc];
+      }
+    }
+    return;
+  }
+  item -= t.nx;
+  // ------------------ T extension of step sp: T(ib, sp) = -(sum_lb T(ib, lb) X_lb) T(sp, sp)
+  const int ib = item, sp = t.sp;
+  const int col = tid & 31, i0 = tid >> 5;  // rows i0 and i0 + 16
+  double y0 = 0.0, y1 = 0.0;
+  for (int lb = ib; lb < sp; ++lb) {
+    for (int idx = tid; idx < 1024; idx += NT) {
+      const int cc = idx >> 5, r = idx & 31;
+      S0[r][cc] = t.T[(size_t)(32 * lb + cc) * t.ldt + 32 * ib + r];  // T(ib, lb) block (r, cc)
+      S1[r][cc] = t.Xprev[(size_t)lb * 1024 + cc * 32 + r];           // X_lb (r, cc)
+    }
+    __syncthreads();
+#pragma unroll
+    for (int l = 0; l < 32; ++l) {
+      const double x = S1[l][col];
+      y0 = __builtin_fma(S0[i0][l], x, y0);
+      y1 = __builtin_fma(S0[i0 + 16][l], x, y1);
+    }
+    __syncthreads();
+  }
+  S2[i0][col] = y0;
+  S2[i0 + 16][col] = y1;
+  for (int idx = tid; idx < 1024; idx += NT) {
+    const int cc = idx >> 5, r = idx & 31;
+    S1[r][cc] = (r < t.jbp && cc < t.jbp && r <= cc) ? t.T[(size_t)(32 * sp + cc) * t.ldt + 32 * sp + r] : 0.0;
+  }
+  __syncthreads();
+  if (col < t.jbp) {
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int l = 0; l < 32; ++l) {
+      const double tv = S1[l][col];  // zero for l > col
+      s0 = __builtin_fma(S2[i0][l], tv, s0);
+      s1 = __builtin_fma(S2[i0 + 16][l], tv, s1);
+    }
+    t.T[(size_t)(32 * sp + col) * t.ldt + 32 * ib + i0] = -s0;
+    t.T[(size_t)(32 * sp + col) * t.ldt + 32 * ib + i0 + 16] = -s1;
+  }
+}
+
+static void launch_sub2(const std::vector<QrSub2Desc>& v, int rpt, hipStream_t stream) {
+  for (size_t s0 = 0; s0 < v.size(); s0 += kMaxSub2Batch) {
+    QrSub2Args a;
+    a.count = (int)std::min<size_t>(kMaxSub2Batch, v.size() - s0);
+    for (int i = 0; i < a.count; ++i) a.d[i] = v[s0 + i];
+    const dim3 grid(a.count), block(256);
+    if (rpt <= 8) hipLaunchKernelGGL(qr_sub2_kernel<8>, grid, block, 0, stream, a);
+    else if (rpt <= 16) hipLaunchKernelGGL(qr_sub2_kernel<16>, grid, block, 0, stream, a);
+    else if (rpt <= 36) hipLaunchKernelGGL(qr_sub2_kernel<36>, grid, block, 0, stream, a);
+    else hipLaunchKernelGGL(qr_sub2_kernel<kP2MaxRPT>, grid, block, 0, stream, a);
+  }
+}
+
+static void launch_subapply(const std::vector<QrSubApplyTask>& v, hipStream_t stream) {
+  for (size_t s0 = 0; s0 < v.size(); s0 += kMaxSubApplyBatch) {
+    QrSubApplyArgs a;
+    a.count = (int)std::min<size_t>(kMaxSubApplyBatch, v.size() - s0);
+    int items = 0;
+    for (int i = 0; i < a.count; ++i) {
+      const QrSubApplyTask& t = v[s0 + i];
+      a.t[i] = t;
+      a.start[i] = items;
+      a.ntr[i] = t.rest > 0 ? (t.rest + 31) / 32 : 0;
+      items += a.ntr[i] + t.nx + t.ne;
+    }
+    a.start[a.count] = items;
+    if (items > 0) hipLaunchKernelGGL(qr_subapply_kernel, dim3(items), dim3(kSubApplyThreads), 0, stream, a);
+  }
+}
+
+// Returns false (nothing launched) when a task exceeds the register-resident row budget.
+static bool launch_qr_panel_fast(const QrPanelDesc* descs, int n, hipStream_t stream, double* ws) {
+  struct Task {
+    QrPanelDesc d;
+    bool ts;
+    int kr, rows;
+    double* Vc;
+    double* X[2];
+  };
+  std::vector<Task> tk(n);
+  int rpt = 1, steps = 0;
+  for (int i = 0; i < n; ++i) {
+    Task& t = tk[i];
+    t.d = descs[i];
+    t.ts = t.d.A2 != nullptr;
+    t.kr = t.ts ? t.d.n : std::min(t.d.m1, t.d.n);
+    t.rows = t.ts ? 32 + t.d.m2 : t.d.m1;
+    rpt = std::max(rpt, (t.rows + 7) / 8);
+    steps = std::max(steps, (t.kr + kSubJB - 1) / kSubJB);
+  }
+  if (rpt > kP2MaxRPT) return false;
+  double* p = ws;
+  for (Task& t : tk) {
+    t.X[0] = p; p += (size_t)kSubJB * t.d.n;
+    t.X[1] = p; p += (size_t)kSubJB * t.d.n + 64;
+    t.Vc = nullptr;
+    if (!t.ts) {
+      if (t.d.Vcopy) t.Vc = t.d.Vcopy;
+      else { t.Vc = p; p += (size_t)t.d.m1 * t.d.n; }
+    }
+  }
+  std::vector<QrSub2Desc> sub;
+  std::vector<QrSubApplyTask> app;
+  for (int st = 0; st <= steps; ++st) {
+    const int j0 = st * kSubJB;
+    sub.clear();
+    app.clear();
+    for (Task& t : tk) {
+      const QrPanelDesc& d = t.d;
+      const bool active = j0 < t.kr;
+      const int jb = active ? std::min(kSubJB, t.kr - j0) : 0;
+      if (active) {
+        QrSub2Desc q{};
+        q.jb = jb; q.ts = t.ts ? 1 : 0; q.ldt = d.ldt;
+        q.Tjj = d.T + (size_t)j0 * d.ldt + j0;
+        q.tzero = t.kr - j0 - jb;
+        q.A1 = d.A1 + (size_t)j0 * d.lda1 + j0; q.lda1 = d.lda1;
+        if (t.ts) {
+          q.A2 = d.A2 + (size_t)j0 * d.lda2; q.lda2 = d.lda2; q.m2 = d.m2;
+        } else {
+          q.nR = d.m1 - j0;
+          q.Vc = t.Vc + (size_t)j0 * d.m1 + j0; q.ldvc = d.m1; q.vzero = j0;
+        }
+        sub.push_back(q);
+      }
+      QrSubApplyTask a{};
+      a.ldt = d.ldt;
+      a.T = d.T;
+      if (active) {
+        a.jb = jb;
+        a.T22 = d.T + (size_t)j0 * d.ldt + j0;
+        a.rest = d.n - j0 - jb;
+        if (t.ts) {
+          a.Vd = d.A2 + (size_t)j0 * d.lda2; a.ldv = d.lda2; a.rd = d.m2;
+          a.C2 = d.A2 + (size_t)(j0 + jb) * d.lda2; a.ldc2 = d.lda2;
+          a.C1 = d.A1 + (size_t)(j0 + jb) * d.lda1 + j0; a.ldc1 = d.lda1;
+          a.Vold = d.A2;
+        } else {
+          a.Vd = t.Vc + (size_t)j0 * d.m1 + j0; a.ldv = d.m1; a.rd = d.m1 - j0;
+          a.C2 = d.A1 + (size_t)(j0 + jb) * d.lda1 + j0; a.ldc2 = d.lda1;
+          a.Vold = t.Vc + j0;
+        }
+        a.nx = st;  // X_lb for lb < st
+        a.Xout = t.X[st & 1];
+      }
+      // T extension of the previous step (its X blocks were written by the previous launch)
+      const int sp = st - 1;
+      if (sp >= 1 && sp * kSubJB < t.kr) {
+        a.sp = sp;
+        a.ne = sp;
+        a.jbp = std::min(kSubJB, t.kr - sp * kSubJB);
+        a.Xprev = t.X[sp & 1];
+      }
+      if (a.rest > 0 || a.nx > 0 || a.ne > 0) app.push_back(a);
+    }
+    if (!sub.empty()) launch_sub2(sub, rpt, stream);
+    if (!app.empty()) launch_subapply(app, stream);
+  }
+  return true;
+}
+
 // Blocked GEQRT / TSQRT (DPLASMA-style inner blocking, ib = 32): per column block
 // j0 of every task of the batch, (1) factor the sub-panel in registers, (2) apply
 // its block reflector to the trailing columns with the grouped MFMA GEMMs, (3)
 // extend the tile's compact-WY T: T(0:j0, j0:j0+jb) = -T11 (V1^T V2) T22.
 void launch_qr_panel_blocked(const QrPanelDesc* descs, int n, hipStream_t stream, double* ws) {
   if (n <= 0) return;
+  static const bool legacy = getenv("PARSEC_QR_LEGACY_PANEL") != nullptr;
+  if (!legacy && launch_qr_panel_fast(descs, n, stream, ws)) return;
   struct Task {
     QrPanelDesc d;
     bool ts;

@@ -1,0 +1,9 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out/prof
+timeout -k 10 120 python scripts/qr_kbench.py 512 > gpurun_out/qr_kbench.log 2>&1 && cat gpurun_out/qr_kbench.log && \
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && \
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/qrk -o run -- python3 scripts/qr_kbench.py 512 > gpurun_out/prof/qrk.log 2>&1
+rc=$?
+find gpurun_out/prof/qrk -name "*kernel_stats.csv" | head -1 | xargs cut -d, -f1-4 | cut -c1-160
+exit $rc

@@ -156,7 +156,7 @@ def _np(t):
     return t.cpu().numpy().T
 
 
-@pytest.mark.parametrize("m,n", [(256, 256), (300, 200), (128, 256)])
+@pytest.mark.parametrize("m,n", [(256, 256), (300, 200), (128, 256), (512, 512), (544, 480), (232, 232), (20, 40)])
 def test_qr_panel_geqrt(pa, dev, m, n):
     A = np.random.default_rng(0).standard_normal((m, n))
     k = min(m, n)
@@ -172,7 +172,7 @@ def test_qr_panel_geqrt(pa, dev, m, n):
     assert np.allclose(_np(Td), T_ref, atol=1e-10)
 
 
-@pytest.mark.parametrize("m2,n", [(256, 256), (100, 64)])
+@pytest.mark.parametrize("m2,n", [(256, 256), (100, 64), (512, 512), (232, 232), (512, 200)])
 def test_qr_panel_tsqrt_and_tsmqr(pa, dev, m2, n):
     rng = np.random.default_rng(1)
     R = np.triu(rng.standard_normal((n, n)))
