@@ -129,7 +129,11 @@ void HipDevice::start(Context* c) {
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
   PARSEC_HIP_CHECK(hipStreamCreateWithFlags(&s_h2d, hipStreamNonBlocking));
   PARSEC_HIP_CHECK(hipStreamCreateWithFlags(&s_d2h, hipStreamNonBlocking));
-  s_exec.resize(nb_exec_streams);
+  // streams [0, nb_exec_streams): critical / high-priority / bulk; then
+  // extra_crit_streams more critical streams, so independent critical-path
+  // batches (e.g. the panels of different QR steps) are not serialised
+  const int total_streams = nb_exec_streams + (nb_exec_streams >= 3 ? extra_crit_streams : 0);
+  s_exec.resize(total_streams);
   // Stream 0 carries the critical path (POTRF / next panel). With >= 3 streams it
   // gets a few CUs of its own so its small latency-bound kernels never queue behind
   // (or share CUs with) the bulk GEMM batches, which run on the remaining CUs.
@@ -149,12 +153,13 @@ void HipDevice::start(Context* c) {
   if (!masked)
     for (int i = 0; i < nb_exec_streams; ++i)
       PARSEC_HIP_CHECK(hipStreamCreateWithPriority(&s_exec[i], hipStreamNonBlocking, i <= 1 ? hi : lo));
+  for (int i = nb_exec_streams; i < total_streams; ++i) PARSEC_HIP_CHECK(hipStreamCreateWithPriority(&s_exec[i], hipStreamNonBlocking, hi));
   cu_masked = masked;
-  executing.assign(nb_exec_streams, {});
-  batches.assign(nb_exec_streams, {});
-  round_tasks.assign(nb_exec_streams, {});
-  stream_workspace.assign(nb_exec_streams, nullptr);
-  stream_workspace_size.assign(nb_exec_streams, 0);
+  executing.assign(total_streams, {});
+  batches.assign(total_streams, {});
+  round_tasks.assign(total_streams, {});
+  stream_workspace.assign(total_streams, nullptr);
+  stream_workspace_size.assign(total_streams, 0);
   es = new ExecutionStream();
   es->ctx = c;
   es->vp = c->vps[0];
@@ -455,7 +460,18 @@ void HipDevice::execute_ready() {
     const bool hp = t->priority >= high_prio_threshold || (t->task_class->flags & TC_HIGH_PRIORITY);
     if (nb_exec_streams == 1) s = 0;
     else if (nb_exec_streams == 2) s = hp ? 0 : 1;
-    else if (t->priority >= critical_threshold) s = 0;
+    else if (t->priority >= critical_threshold) {
+      // one critical stream per round (its tasks batch together): stream 0 unless it
+      // has work in flight and an extra critical stream is idle
+      s = -1;
+      for (size_t c = 0; c < round_tasks.size() && s < 0; ++c)
+        if ((c == 0 || c >= (size_t)nb_exec_streams) && !round_tasks[c].empty()) s = (int)c;
+      if (s < 0) {
+        s = 0;
+        for (size_t c = nb_exec_streams; c < executing.size() && !executing[0].empty(); ++c)
+          if (executing[c].size() < executing[s].size()) s = (int)c;
+      }
+    }
     else if (hp) s = 1;
     else {
       // Bulk work: pick a bulk stream with fewer than max_inflight_groups launched
@@ -508,7 +524,7 @@ void HipDevice::execute_ready() {
     }
   }
   ready.swap(again);
-  for (int s = 0; s < nb_exec_streams; ++s) {
+  for (int s = 0; s < (int)round_tasks.size(); ++s) {
     if (round_tasks[s].empty()) continue;
     if (!batches[s].empty()) {
       launch_kernel_batch(batches[s], s_exec[s], ordinal, workspace(s, kernel_batch_workspace_bytes(batches[s]) + 64));
@@ -600,7 +616,7 @@ bool HipDevice::progress() {
   }
   if (!ready.empty()) { execute_ready(); did = true; }
   // kernels done?
-  for (int s = 0; s < nb_exec_streams; ++s) {
+  for (int s = 0; s < (int)executing.size(); ++s) {
     auto& q = executing[s];
     while (!q.empty()) {
       ExecGroup& grp = q.front();
@@ -685,6 +701,7 @@ void hip_devices_init(Context* ctx) {
   int sortp = (int)params.reg_int("device", "hip", "sort_pending_tasks", "Sort pending GPU tasks by priority", 1);
   int crit = (int)params.reg_int("device", "hip", "critical_threshold", "Task priority at or above which the CU-reserved critical stream is used", 1 << 29);
   int rcus = (int)params.reg_int("device", "hip", "reserved_cus", "CUs reserved for the critical-path stream (0 = no CU masking; measured slower on MI355X)", 0);
+  int xcrit = (int)params.reg_int("device", "hip", "critical_streams", "Additional critical-path streams used when the critical stream is busy", 7);
   int maxg = (int)params.reg_int("device", "hip", "max_inflight_batches", "Launched kernel groups per bulk stream before new bulk tasks wait for a larger batch (0 = no limit)", 2);
   if (enabled == 0) return;
   int count = 0;
@@ -708,6 +725,7 @@ void hip_devices_init(Context* ctx) {
     d->critical_threshold = crit;
     d->reserved_cus = rcus;
     d->max_inflight_groups = maxg;
+    d->extra_crit_streams = std::max(0, xcrit);
     d->sort_pending = sortp != 0;
     reg.add(d);
     g_hip_devices.push_back(d);
