@@ -433,6 +433,7 @@ struct QrSub2Desc {
   int ldt, tzero;
   double* Vc;   // GEQRT: clean V block (row j0, col j0); rows [-vzero, 0) are zeroed
   int ldvc, vzero;
+  unsigned long long* prof;  // optional per-wave phase cycle counters (8 x 4 waves), PARSEC_QR_PROFILE
 };
 struct QrSub2Args {
   int count;
@@ -440,34 +441,39 @@ struct QrSub2Args {
 };
 static_assert(sizeof(QrSub2Args) <= 4096, "QrSub2Args exceeds the kernel argument limit");
 
-template <int RPT>
-__global__ __launch_bounds__(256) void qr_sub2_kernel(const QrSub2Args args) {
-  // Loops over a thread's rows run in chunks of 8 with ONE uniform test per
-  // chunk (skip chunks entirely above the pivot); inside a chunk there are no
-  // branches, so LDS reads issue back to back. vb holds zeros for rows that do
-  // not take part in a step, which keeps the dot products and updates unmasked.
+template <int RPT, int NW>
+__global__ __launch_bounds__(64 * NW) void qr_sub2_kernel(const QrSub2Args args) {
+  constexpr int G = 2 * NW, RB = 32 / G, NTH = 64 * NW;
+  // Two barriers per column. Loops over a thread's rows run in chunks of 8 with
+  // ONE uniform test per chunk (chunks entirely above the pivot are skipped).
+  // Scaling is lazy: column j keeps the raw values u (v = scale_j u below the
+  // pivot, v_j = 1), so the reflector goes to LDS in the same pass that forms
+  // sigma (before the norm is known) and the trailing dot is
+  //   p_c = A(j, c) + scale_j * sum_{r > j} u_r A(r, c);
+  // V columns are scaled only when written back (and z_c = scale_c * p_c).
   constexpr int NCH = (RPT + 7) / 8;
   const QrSub2Desc& d = args.d[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c = lane & 31, g = 2 * w + (lane >> 5);
   const bool ts = d.ts != 0;
   const int jb = d.jb;
-  __shared__ double vb[8][8 * NCH];
-  __shared__ double red1[4];
-  __shared__ double red2[4][32];
+  __shared__ __attribute__((aligned(16))) double vb[2][G][8 * NCH];  // raw reflector, by parity of j
+  __shared__ double prow[2][32];                                      // pivot row A(j, :)
+  __shared__ double red1[NW];
+  __shared__ double red2[NW][32];
   __shared__ double Tl[32][33];
-  __shared__ double zb[32], taus[32];
+  __shared__ double zb[32], taus[32], scs[32], betas[32];
   __shared__ double s_alpha;
-  for (int idx = tid; idx < 32 * 33; idx += 256) (&Tl[0][0])[idx] = 0.0;
+  for (int idx = tid; idx < 32 * 33; idx += NTH) (&Tl[0][0])[idx] = 0.0;
   if (tid < 32) zb[tid] = 0.0;
   double a[RPT];
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
-    const int vr = g + 8 * i;
+    const int vr = g + G * i;
     double x = 0.0;
     if (c < jb) {
       if (ts) {
-        if (i < 4) {
+        if (i < RB) {
           if (vr <= c) x = d.A1[(size_t)c * d.lda1 + vr];  // upper R only (GEQRT's V lies below)
         } else if (vr - 32 < d.m2) {
           x = d.A2[(size_t)c * d.lda2 + (vr - 32)];
@@ -479,48 +485,77 @@ __global__ __launch_bounds__(256) void qr_sub2_kernel(const QrSub2Args args) {
     a[i] = x;
   }
   __syncthreads();
-  // T column jp = -tau_jp T(0:jp, 0:jp) z, formed one step late by wave 3; Tl and
-  // zb start zeroed and fill monotonically, so a full 32-term dot needs no mask
+  // T column jp = -tau_jp T(0:jp, 0:jp) z, one step late, spread over all waves:
+  // wave w forms rows 8w..8w+7; lane = (row, eighth of the 32-term dot)
   auto t_column = [&](int jp) {
-    if (w != 3 || lane >= 32) return;
-    double t0 = 0.0, t1 = 0.0;
+    constexpr int RPW = 32 / NW, LPR = 64 / RPW, TPL = 32 / LPR;  // rows per wave, lanes per row, terms per lane
+    const int i = RPW * w + (lane % RPW), l0 = TPL * (lane / RPW);
+    double t = 0.0;
 #pragma unroll
-    for (int l = 0; l < 32; l += 2) {
-      t0 = __builtin_fma(Tl[lane][l], zb[l], t0);
-      t1 = __builtin_fma(Tl[lane][l + 1], zb[l + 1], t1);
+    for (int l = 0; l < TPL; ++l) t = __builtin_fma(Tl[i][l0 + l], zb[l0 + l], t);
+#pragma unroll
+    for (int o = RPW; o < 64; o <<= 1) t += __shfl_xor(t, o, 64);
+    if (lane < RPW) {
+      if (i < jp) Tl[i][jp] = -taus[jp] * t;
+      else if (i == jp) Tl[jp][jp] = taus[jp];
     }
-    if (lane < jp) Tl[lane][jp] = -taus[jp] * (t0 + t1);
-    else if (lane == jp) Tl[jp][jp] = taus[jp];
+  };
+  unsigned long long pc_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tmark = __builtin_amdgcn_s_memtime();
+  auto mark = [&](int ph) {
+    if (d.prof) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      pc_acc[ph] += t - tmark;
+      tmark = t;
+    }
   };
   for (int j = 0; j < jb; ++j) {
-    const int jq = j >> 3;
-    // ---- 1: sigma (squares below the pivot) and alpha, column-j lanes only
-    if (c == j) {
-      double sq = 0.0, al = 0.0;
+    const int jq = j / G, jg = j % G, par = j & 1;
+    // ---- 1: column-j lanes: sigma, raw reflector -> LDS; g == j%8 lanes: pivot row -> LDS
+    {
+      double s0 = 0.0, s1 = 0.0, pr = 0.0;
 #pragma unroll
       for (int k = 0; k < NCH; ++k) {
         const int i0 = 8 * k;
         if (i0 + 8 <= jq) continue;
-        if (i0 > jq && !(ts && i0 < 4)) {
+        if (i0 > jq && !(ts && i0 < RB)) {
+          if (c == j) {
 #pragma unroll
-          for (int i = i0; i < i0 + 8 && i < RPT; ++i) sq = __builtin_fma(a[i], a[i], sq);
+            for (int i = i0; i < i0 + 8 && i < RPT; i += 2) {
+              s0 = __builtin_fma(a[i], a[i], s0);
+              double2 v2;
+              v2.x = a[i];
+              v2.y = i + 1 < RPT ? a[i + 1] : 0.0;
+              if (i + 1 < RPT) s1 = __builtin_fma(a[i + 1], a[i + 1], s1);
+              *reinterpret_cast<double2*>(&vb[par][g][i]) = v2;
+            }
+          }
         } else {
 #pragma unroll
           for (int i = i0; i < i0 + 8 && i < RPT; ++i) {
-            const int vr = g + 8 * i;
-            const bool below = ts ? (i >= 4) : (vr > j);
-            sq = below ? __builtin_fma(a[i], a[i], sq) : sq;
-            al = vr == j ? a[i] : al;
+            const int vr = g + G * i;
+            const bool below = ts ? (i >= RB) : (vr > j);
+            const double u = below ? a[i] : 0.0;
+            s0 = __builtin_fma(u, u, s0);
+            pr = vr == j ? a[i] : pr;
+            if (c == j) vb[par][g][i] = u;
           }
         }
       }
-      sq += __shfl_xor(sq, 32, 64);
-      if (lane == c) red1[w] = sq;
-      if (g == (j & 7)) s_alpha = al;
+      if (c == j) {
+        double sq = s0 + s1;
+        sq += __shfl_xor(sq, 32, 64);
+        if (lane == c) red1[w] = sq;
+        if (g == jg) s_alpha = pr;
+      }
+      if (g == jg) prow[par][c] = pr;
     }
+    mark(0);
     __syncthreads();  // A
-    if (j > 0) t_column(j - 1);
-    const double sigma = red1[0] + red1[1] + red1[2] + red1[3];
+    mark(1);
+    double sigma = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) sigma += red1[q];
     const double alpha = s_alpha;
     double tau = 0.0, scale = 0.0, beta = alpha;
     if (sigma != 0.0) {
@@ -529,34 +564,10 @@ __global__ __launch_bounds__(256) void qr_sub2_kernel(const QrSub2Args args) {
       tau = (beta - alpha) / beta;
       scale = 1.0 / (alpha - beta);
     }
-    // ---- 2: v (stored in place below the pivot), pivot := beta, v -> LDS
-    if (c == j) {
-      const double pivv = tau != 0.0 ? beta : alpha;
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) {
-        const int i0 = 8 * k;
-        if (i0 + 8 <= jq) continue;
-        if (i0 > jq && !(ts && i0 < 4)) {
-#pragma unroll
-          for (int i = i0; i < i0 + 8 && i < RPT; ++i) {
-            a[i] *= scale;
-            vb[g][i] = a[i];
-          }
-        } else {
-#pragma unroll
-          for (int i = i0; i < i0 + 8 && i < RPT; ++i) {
-            const int vr = g + 8 * i;
-            const bool below = ts ? (i >= 4) : (vr > j);
-            const bool piv = vr == j;
-            const double sc = a[i] * scale;
-            vb[g][i] = below ? sc : (piv ? 1.0 : 0.0);
-            a[i] = below ? sc : (piv ? pivv : a[i]);
-          }
-        }
-      }
-    }
-    __syncthreads();  // B
-    // ---- 3: p_c = sum_r v_r A(r, c) (c > j: trailing w; c < j: z for T)
+    mark(2);
+    if (j > 0) t_column(j - 1);
+    mark(3);
+    // ---- 2: dot of the raw reflector with every column
     double p0 = 0.0, p1 = 0.0;
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
@@ -564,54 +575,87 @@ __global__ __launch_bounds__(256) void qr_sub2_kernel(const QrSub2Args args) {
       if (i0 + 8 <= jq) continue;
 #pragma unroll
       for (int i = i0; i < i0 + 8 && i < RPT; i += 2) {
-        p0 = __builtin_fma(vb[g][i], a[i], p0);
-        if (i + 1 < RPT) p1 = __builtin_fma(vb[g][i + 1], a[i + 1], p1);
+        if (i + 1 < RPT) {
+          const double2 v2 = *reinterpret_cast<const double2*>(&vb[par][g][i]);
+          p0 = __builtin_fma(v2.x, a[i], p0);
+          p1 = __builtin_fma(v2.y, a[i + 1], p1);
+        } else {
+          p0 = __builtin_fma(vb[par][g][i], a[i], p0);
+        }
       }
     }
     double p = p0 + p1;
     p += __shfl_xor(p, 32, 64);
     if (lane < 32) red2[w][c] = p;
-    __syncthreads();  // C
-    const double pc = red2[0][c] + red2[1][c] + red2[2][c] + red2[3][c];
-    // ---- 4: trailing update inside the sub-panel, z and tau for T
+    mark(4);
+    __syncthreads();  // B
+    mark(5);
+    double rs = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) rs += red2[q][c];
+    const double pc = prow[par][c] + scale * rs;
+    // ---- 3: trailing update inside the sub-panel (rows > j via the raw reflector, row j directly)
     if (c > j && tau != 0.0) {
-      const double tp = -tau * pc;
+      const double tp = tau * pc, coef = -tp * scale;
 #pragma unroll
       for (int k = 0; k < NCH; ++k) {
         const int i0 = 8 * k;
         if (i0 + 8 <= jq) continue;
+        const bool has_pivot = i0 <= jq;
 #pragma unroll
-        for (int i = i0; i < i0 + 8 && i < RPT; ++i) a[i] = __builtin_fma(tp, vb[g][i], a[i]);
+        for (int i = i0; i < i0 + 8 && i < RPT; i += 2) {
+          if (i + 1 < RPT) {
+            const double2 v2 = *reinterpret_cast<const double2*>(&vb[par][g][i]);
+            a[i] = __builtin_fma(coef, v2.x, a[i]);
+            a[i + 1] = __builtin_fma(coef, v2.y, a[i + 1]);
+          } else {
+            a[i] = __builtin_fma(coef, vb[par][g][i], a[i]);
+          }
+          if (has_pivot) {
+            if (g + G * i == j) a[i] -= tp;
+            if (i + 1 < RPT && g + G * (i + 1) == j) a[i + 1] -= tp;
+          }
+        }
       }
     }
-    if (tid < j) zb[tid] = pc;  // tid < 32: c == tid
-    if (tid == 0) taus[j] = tau;
+    if (tid < j) zb[tid] = scs[tid] * pc;  // tid < 32: c == tid; z_c = V_c^T v_j
+    if (tid == 0) {
+      taus[j] = tau;
+      scs[j] = scale;
+      betas[j] = beta;
+    }
+    mark(6);
   }
+  if (d.prof && lane == 0)
+    for (int q = 0; q < 8; ++q) atomicAdd(&d.prof[(w & 3) * 8 + q], pc_acc[q]);
   __syncthreads();
   t_column(jb - 1);
   __syncthreads();
-  // ---- write back the sub-panel, the clean V, T (+ zeros below) and zeros above V
+  // ---- write back: V columns scaled below the diagonal, beta on it; T (+ zeros below); zeros above V
+  const double sc_c = c < jb ? scs[c] : 0.0;
+  const double be_c = c < jb ? betas[c] : 0.0;
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
-    const int vr = g + 8 * i;
+    const int vr = g + G * i;
     if (c >= jb) continue;
+    const double x = vr == c ? be_c : (vr > c ? a[i] * sc_c : a[i]);
     if (ts) {
-      if (i < 4) {
-        if (vr <= c) d.A1[(size_t)c * d.lda1 + vr] = a[i];
+      if (i < RB) {
+        if (vr <= c) d.A1[(size_t)c * d.lda1 + vr] = x;
       } else if (vr - 32 < d.m2) {
-        d.A2[(size_t)c * d.lda2 + (vr - 32)] = a[i];
+        d.A2[(size_t)c * d.lda2 + (vr - 32)] = a[i] * sc_c;
       }
     } else if (vr < d.nR) {
-      d.A1[(size_t)c * d.lda1 + vr] = a[i];
-      if (d.Vc) d.Vc[(size_t)c * d.ldvc + vr] = vr > c ? a[i] : (vr == c ? 1.0 : 0.0);
+      d.A1[(size_t)c * d.lda1 + vr] = x;
+      if (d.Vc) d.Vc[(size_t)c * d.ldvc + vr] = vr > c ? x : (vr == c ? 1.0 : 0.0);
     }
   }
-  for (int idx = tid; idx < jb * (jb + d.tzero); idx += 256) {
+  for (int idx = tid; idx < jb * (jb + d.tzero); idx += NTH) {
     const int col = idx / (jb + d.tzero), r = idx % (jb + d.tzero);
     d.Tjj[(size_t)col * d.ldt + r] = (r < jb && r <= col) ? Tl[r][col] : 0.0;
   }
   if (d.Vc)
-    for (int idx = tid; idx < jb * d.vzero; idx += 256) {
+    for (int idx = tid; idx < jb * d.vzero; idx += NTH) {
       const int col = idx / d.vzero, r = idx % d.vzero;
       d.Vc[(size_t)col * d.ldvc + r - d.vzero] = 0.0;
     }
@@ -842,16 +886,29 @@ __global__ __launch_bounds__(kSubApplyThreads) void qr_subapply_kernel(const QrS
   }
 }
 
-static void launch_sub2(const std::vector<QrSub2Desc>& v, int rpt, hipStream_t stream) {
+static void launch_sub2(const std::vector<QrSub2Desc>& v, int rows, hipStream_t stream) {
+  // 8 waves (16 row groups) for tall sub-panels, 4 waves otherwise
+  static const int nw_env = getenv("PARSEC_QR_PANEL_WAVES") ? atoi(getenv("PARSEC_QR_PANEL_WAVES")) : 8;
+  const int nw = nw_env == 4 ? 4 : 8;
   for (size_t s0 = 0; s0 < v.size(); s0 += kMaxSub2Batch) {
     QrSub2Args a;
     a.count = (int)std::min<size_t>(kMaxSub2Batch, v.size() - s0);
     for (int i = 0; i < a.count; ++i) a.d[i] = v[s0 + i];
-    const dim3 grid(a.count), block(256);
-    if (rpt <= 8) hipLaunchKernelGGL(qr_sub2_kernel<8>, grid, block, 0, stream, a);
-    else if (rpt <= 16) hipLaunchKernelGGL(qr_sub2_kernel<16>, grid, block, 0, stream, a);
-    else if (rpt <= 36) hipLaunchKernelGGL(qr_sub2_kernel<36>, grid, block, 0, stream, a);
-    else hipLaunchKernelGGL(qr_sub2_kernel<kP2MaxRPT>, grid, block, 0, stream, a);
+    const dim3 grid(a.count);
+    if (nw == 8) {
+      const int rpt = (rows + 15) / 16;
+      const dim3 block(512);
+      if (rpt <= 8) hipLaunchKernelGGL((qr_sub2_kernel<8, 8>), grid, block, 0, stream, a);
+      else if (rpt <= 16) hipLaunchKernelGGL((qr_sub2_kernel<16, 8>), grid, block, 0, stream, a);
+      else hipLaunchKernelGGL((qr_sub2_kernel<36, 8>), grid, block, 0, stream, a);
+    } else {
+      const int rpt = (rows + 7) / 8;
+      const dim3 block(256);
+      if (rpt <= 8) hipLaunchKernelGGL((qr_sub2_kernel<8, 4>), grid, block, 0, stream, a);
+      else if (rpt <= 16) hipLaunchKernelGGL((qr_sub2_kernel<16, 4>), grid, block, 0, stream, a);
+      else if (rpt <= 36) hipLaunchKernelGGL((qr_sub2_kernel<36, 4>), grid, block, 0, stream, a);
+      else hipLaunchKernelGGL((qr_sub2_kernel<kP2MaxRPT, 4>), grid, block, 0, stream, a);
+    }
   }
 }
 
@@ -873,6 +930,8 @@ static void launch_subapply(const std::vector<QrSubApplyTask>& v, hipStream_t st
 }
 
 // Returns false (nothing launched) when a task exceeds the register-resident row budget.
+static unsigned long long* g_qr_prof = nullptr;  // PARSEC_QR_PROFILE phase counters
+
 static bool launch_qr_panel_fast(const QrPanelDesc* descs, int n, hipStream_t stream, double* ws) {
   struct Task {
     QrPanelDesc d;
@@ -882,7 +941,7 @@ static bool launch_qr_panel_fast(const QrPanelDesc* descs, int n, hipStream_t st
     double* X[2];
   };
   std::vector<Task> tk(n);
-  int rpt = 1, steps = 0;
+  int rpt = 1, steps = 0, rows_max = 1;
   for (int i = 0; i < n; ++i) {
     Task& t = tk[i];
     t.d = descs[i];
@@ -890,6 +949,7 @@ static bool launch_qr_panel_fast(const QrPanelDesc* descs, int n, hipStream_t st
     t.kr = t.ts ? t.d.n : std::min(t.d.m1, t.d.n);
     t.rows = t.ts ? 32 + t.d.m2 : t.d.m1;
     rpt = std::max(rpt, (t.rows + 7) / 8);
+    rows_max = std::max(rows_max, t.rows);
     steps = std::max(steps, (t.kr + kSubJB - 1) / kSubJB);
   }
   if (rpt > kP2MaxRPT) return false;
@@ -905,6 +965,12 @@ static bool launch_qr_panel_fast(const QrPanelDesc* descs, int n, hipStream_t st
   }
   std::vector<QrSub2Desc> sub;
   std::vector<QrSubApplyTask> app;
+  static const bool profiling = getenv("PARSEC_QR_PROFILE") != nullptr;
+  if (profiling && !g_qr_prof) {
+    if (hipMalloc(&g_qr_prof, 32 * sizeof(unsigned long long)) != hipSuccess) g_qr_prof = nullptr;
+    else (void)hipMemset(g_qr_prof, 0, 32 * sizeof(unsigned long long));
+  }
+  unsigned long long* prof = g_qr_prof;
   for (int st = 0; st <= steps; ++st) {
     const int j0 = st * kSubJB;
     sub.clear();
@@ -925,6 +991,7 @@ static bool launch_qr_panel_fast(const QrPanelDesc* descs, int n, hipStream_t st
           q.nR = d.m1 - j0;
           q.Vc = t.Vc + (size_t)j0 * d.m1 + j0; q.ldvc = d.m1; q.vzero = j0;
         }
+        q.prof = prof;
         sub.push_back(q);
       }
       QrSubApplyTask a{};
@@ -957,7 +1024,7 @@ static bool launch_qr_panel_fast(const QrPanelDesc* descs, int n, hipStream_t st
       }
       if (a.rest > 0 || a.nx > 0 || a.ne > 0) app.push_back(a);
     }
-    if (!sub.empty()) launch_sub2(sub, rpt, stream);
+    if (!sub.empty()) launch_sub2(sub, rows_max, stream);
     if (!app.empty()) launch_subapply(app, stream);
   }
   return true;
@@ -1117,6 +1184,15 @@ void launch_qr_apply(const QrApplyDesc* descs, int n, hipStream_t stream, double
 }  // namespace parsec
 
 extern "C" {
+// PARSEC_QR_PROFILE: accumulated sub-panel phase cycles per wave (4 x 8), then reset.
+int parsec_amd_qr_profile(unsigned long long* out) {
+  unsigned long long* p = parsec::kern::g_qr_prof;
+  if (!p) return -1;
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpy(out, p, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+  (void)hipMemset(p, 0, 32 * sizeof(unsigned long long));
+  return 0;
+}
 // Blocked panel (the engine's path); scratch from a cached test buffer.
 int parsec_amd_qr_panel(const parsec::QrPanelDesc* d, int n, void* stream) {
   static void* ws = nullptr;

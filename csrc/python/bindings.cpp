@@ -29,6 +29,7 @@ extern "C" int parsec_amd_dpotrf_tile(double* A, int n, int lda, int* info, void
 extern "C" int parsec_amd_dpotrf_tile_w(double* A, int n, int lda, int* info, double* W, int ldw, void* stream);
 extern "C" int parsec_amd_trsm_w_batch(const parsec::TrsmGemmDesc* d, int n, void* stream);
 extern "C" int parsec_amd_qr_panel(const parsec::QrPanelDesc* d, int n, void* stream);
+extern "C" int parsec_amd_qr_profile(unsigned long long* out);
 extern "C" int parsec_amd_qr_apply(const parsec::QrApplyDesc* d, int n, void* ws, void* stream);
 extern "C" size_t parsec_amd_qr_apply_ws(const parsec::QrApplyDesc* d, int n);
 namespace parsec { void register_builtin_dtd_gpu_bodies(); std::function<int(GpuExecContext*, Task*)> builtin_dtd_gpu_body(const std::string& name); }
@@ -604,6 +605,11 @@ PYBIND11_MODULE(_C, m) {
     q.A1 = (double*)A1; q.lda1 = lda1; q.A2 = (double*)A2; q.lda2 = lda2; q.T = (double*)T; q.ldt = ldt; q.Vcopy = (double*)V;
     q.m1 = m1; q.m2 = m2; q.n = n;
     return parsec_amd_qr_panel(&q, 1, (void*)stream);
+  });
+  m.def("kernel_qr_profile", []() {
+    std::vector<unsigned long long> v(32, 0);
+    if (parsec_amd_qr_profile(v.data()) != 0) v.clear();
+    return v;
   });
   m.def("kernel_qr_apply", [](uintptr_t V, int ldv, uintptr_t T, int ldt, uintptr_t A1, int lda1, uintptr_t A2, int lda2, int m2, int n, int ncols, uintptr_t ws, uintptr_t stream) {
     QrApplyDesc q{};
