@@ -352,12 +352,12 @@ struct Axpy2DArgs {
 };
 static_assert(sizeof(Axpy2DArgs) <= 4096, "Axpy2DArgs exceeds the kernel argument limit");
 __global__ __launch_bounds__(256) void axpy2d_kernel(const Axpy2DArgs a) {
+  // blockIdx.x strides over columns, threads over rows (32-bit indexing, coalesced)
   const Axpy2D& d = a.d[blockIdx.y];
-  const int64_t total = (int64_t)d.rows * d.cols;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int r = (int)(i % d.rows), c = (int)(i / d.rows);
-    double* p = d.dst + (size_t)c * d.ldd + r;
-    *p = (d.beta == 0.0 ? 0.0 : d.beta * *p) + d.alpha * d.src[(size_t)c * d.lds + r];
+  for (int c = blockIdx.x; c < d.cols; c += gridDim.x) {
+    const double* __restrict__ src = d.src + (size_t)c * d.lds;
+    double* __restrict__ dst = d.dst + (size_t)c * d.ldd;
+    for (int r = threadIdx.x; r < d.rows; r += 256) dst[r] = (d.beta == 0.0 ? 0.0 : d.beta * dst[r]) + d.alpha * src[r];
   }
 }
 
@@ -366,7 +366,7 @@ static void launch_axpy(const std::vector<Axpy2D>& v, hipStream_t stream) {
     Axpy2DArgs a;
     a.count = (int)std::min<size_t>(kMaxQrBatch, v.size() - s);
     for (int i = 0; i < a.count; ++i) a.d[i] = v[s + i];
-    hipLaunchKernelGGL(axpy2d_kernel, dim3(64, a.count), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(axpy2d_kernel, dim3(128, a.count), dim3(256), 0, stream, a);
   }
 }
 
