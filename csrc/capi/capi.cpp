@@ -426,6 +426,15 @@ int parsec_tiled_matrix_set_storage_device(parsec_tiled_matrix_t* tdesc, int dev
   return PARSEC_SUCCESS;
 }
 
+int parsec_tiled_matrix_data_write(parsec_tiled_matrix_t* tdesc, const char* filename) {
+  auto* tm = dynamic_cast<TiledMatrix*>(impl_of(&tdesc->super));
+  return tm && tm->data_write(filename) == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+int parsec_tiled_matrix_data_read(parsec_tiled_matrix_t* tdesc, const char* filename) {
+  auto* tm = dynamic_cast<TiledMatrix*>(impl_of(&tdesc->super));
+  return tm && tm->data_read(filename) == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+
 // --------------------------------------------------------------- arenas
 int parsec_arena_datatype_construct(parsec_arena_datatype_t* adt, size_t elem_size, size_t alignment, parsec_datatype_t opaque_dtt) {
   Datatype d = opaque_dtt == PARSEC_DATATYPE_NULL ? Datatype::contiguous(1, (int64_t)elem_size) : type_of(opaque_dtt);

@@ -59,6 +59,15 @@ class FourCounter : public TermdetModule {
     std::lock_guard<std::mutex> g(reg_m_);
     by_id_.erase(tp->taskpool_id);
   }
+  void release_taskpool(Taskpool* tp) override {
+    {
+      std::lock_guard<std::mutex> g(reg_m_);
+      auto it = by_id_.find(tp->taskpool_id);
+      if (it != by_id_.end() && it->second == tp) by_id_.erase(it);
+    }
+    delete st(tp);
+    tp->termdet_private = nullptr;
+  }
   void taskpool_ready(Taskpool* tp) override {
     int exp = TERMDET_NOT_READY;
     tp->termdet_state.compare_exchange_strong(exp, TERMDET_BUSY);

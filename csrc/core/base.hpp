@@ -138,20 +138,37 @@ class Lifo {
 };
 
 // Locked dequeue (reference class/dequeue.h) used as the per-VP system queue.
+// The unlocked emptiness fast path reads an atomic element count (maintained
+// under the lock), never the list links: no data race with concurrent pushes.
 template <class T>
 class Dequeue {
  public:
-  void push_back(T* t) { std::lock_guard<SpinLock> g(lock_); list_.push_back(t); }
-  void push_front(T* t) { std::lock_guard<SpinLock> g(lock_); list_.push_front(t); }
-  T* pop_front() { if (list_.empty()) return nullptr; std::lock_guard<SpinLock> g(lock_); return static_cast<T*>(list_.pop_front()); }
-  T* pop_back() { if (list_.empty()) return nullptr; std::lock_guard<SpinLock> g(lock_); return static_cast<T*>(list_.pop_back()); }
-  bool empty() const { return list_.empty(); }
-  size_t size() const { return list_.size(); }
+  void push_back(T* t) { std::lock_guard<SpinLock> g(lock_); list_.push_back(t); sync_count(); }
+  void push_front(T* t) { std::lock_guard<SpinLock> g(lock_); list_.push_front(t); sync_count(); }
+  T* pop_front() {
+    if (empty()) return nullptr;
+    std::lock_guard<SpinLock> g(lock_);
+    T* t = static_cast<T*>(list_.pop_front());
+    sync_count();
+    return t;
+  }
+  T* pop_back() {
+    if (empty()) return nullptr;
+    std::lock_guard<SpinLock> g(lock_);
+    T* t = static_cast<T*>(list_.pop_back());
+    sync_count();
+    return t;
+  }
+  bool empty() const { return count_.load(std::memory_order_acquire) == 0; }
+  size_t size() const { return count_.load(std::memory_order_relaxed); }
   SpinLock& lock() { return lock_; }
+  // direct list access: hold lock() and call sync_count() after modifying the list
   List& raw() { return list_; }
+  void sync_count() { count_.store(list_.size(), std::memory_order_release); }
  private:
   SpinLock lock_;
   List list_;
+  std::atomic<size_t> count_{0};
 };
 
 // ---------------------------------------------------------------- barrier

@@ -145,6 +145,8 @@ Context* context_init(int nb_cores, std::vector<std::string>& args) {
   if (nb_cores <= 0) nb_cores = 1;
   ctx->nb_cores = nb_cores;
   ctx->keep_highest_priority_task = reg.reg_int("runtime", "", "keep_highest_priority_task", "Keep the highest priority ready task on the releasing thread", 1) != 0;
+  ctx->paranoid = reg.reg_int("debug", "", "paranoid", "Check task lifecycle invariants (scheduled twice, completed twice, scheduled after release, PTG dependency underflow)", 0) != 0;
+  g_paranoid = ctx->paranoid;
   ctx->manager_inline_gpu = reg.reg_int("device", "", "manager_inline_dispatch", "GPU managers prepare and submit successors whose first chore is a GPU chore (no hop through a compute thread)", 1) != 0;
   std::string bcast = reg.reg_string("runtime", "comm", "coll_bcast", "Broadcast topology for remote activations: star|chain|binomial", "star");
   ctx->comm_bcast_topology = bcast == "chain" ? 1 : bcast == "binomial" ? 2 : 0;
@@ -266,6 +268,9 @@ int context_fini(Context** pctx) {
   PARSEC_DEBUG(kVerbDebug, "fini", "scheduler remove");
   ctx->scheduler->remove(ctx);
   delete ctx->scheduler;
+  // manager / comm pseudo execution streams (their threads are stopped by now)
+  for (auto* es : ctx->aux_es) delete es;
+  ctx->aux_es.clear();
   for (auto* vp : ctx->vps) {
     for (auto* es : vp->es) delete es;
     delete vp;

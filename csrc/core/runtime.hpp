@@ -240,7 +240,9 @@ struct TaskDataRef {
   DataRepoEntry* source_repo_entry = nullptr;
 };
 
-enum TaskFlags : uint32_t { TASK_FLAG_REMOTE_SHADOW = 0x1, TASK_FLAG_STARTUP = 0x2, TASK_FLAG_INTERNAL = 0x4 };
+enum TaskFlags : uint32_t { TASK_FLAG_REMOTE_SHADOW = 0x1, TASK_FLAG_STARTUP = 0x2, TASK_FLAG_INTERNAL = 0x4, TASK_FLAG_QUEUED = 0x8 };
+// Freed-task marker written by task_free when debug_paranoid is set (use-after-release detection).
+constexpr uint8_t STATUS_FREED = 0xFF;
 
 struct Task : PoolElt {
   Taskpool* taskpool = nullptr;
@@ -371,6 +373,8 @@ struct TermdetModule {
   virtual const char* name() const = 0;
   virtual void monitor_taskpool(Taskpool* tp, std::function<void(Taskpool*)> on_terminated) = 0;
   virtual void unmonitor_taskpool(Taskpool* tp) { (void)tp; }
+  // free the module's per-taskpool state (called when the taskpool is destroyed)
+  virtual void release_taskpool(Taskpool* tp) { (void)tp; }
   virtual int taskpool_state(Taskpool* tp) { return tp->termdet_state.load(); }
   virtual void taskpool_ready(Taskpool* tp) = 0;
   virtual void taskpool_set_nb_tasks(Taskpool* tp, int64_t v) = 0;
@@ -513,6 +517,7 @@ struct Context {
   std::vector<std::function<void(void*)>> at_fini;
   std::vector<void*> at_fini_data;
   bool keep_highest_priority_task = true;
+  bool paranoid = false;      // debug_paranoid: task lifecycle invariants (double schedule / completion, use after release)
   bool manager_inline_gpu = true;  // GPU managers dispatch GPU-bound successors themselves
   int comm_bcast_topology = 0;  // 0 star, 1 chain, 2 binomial
   std::vector<int> core_bindings;
@@ -540,6 +545,7 @@ void context_abort(Context* ctx, int status);
 
 Task* task_new(ExecutionStream* es, Taskpool* tp, const TaskClass* tc);
 void task_free(Task* t);
+extern bool g_paranoid;  // debug_paranoid (set at init)
 // Push a set of ready tasks (sorted internally by priority).
 int schedule_tasks(ExecutionStream* es, Task** tasks, int n, int32_t distance);
 int schedule_task(ExecutionStream* es, Task* t, int32_t distance);

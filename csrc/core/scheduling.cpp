@@ -30,9 +30,26 @@ Task* task_new(ExecutionStream* es, Taskpool* tp, const TaskClass* tc) {
   return t;
 }
 
+bool g_paranoid = false;
+
+// Paranoid-mode lifecycle checks (reference PARSEC_DEBUG_PARANOID, parsec.c:1619-1657, 1821-1830).
+static void paranoid_on_schedule(Task* t) {
+  if (t->status == STATUS_FREED) fatal("paranoid: a released task (class %p) was scheduled", (const void*)t->task_class);
+  const std::string who = t->task_class ? t->task_class->describe(t) : std::string("?");
+  if (t->status == STATUS_COMPLETE) fatal("paranoid: task %s scheduled after its completion", who.c_str());
+  if (t->flags & TASK_FLAG_QUEUED) fatal("paranoid: task %s scheduled twice", who.c_str());
+  t->flags |= TASK_FLAG_QUEUED;
+}
+
 void task_free(Task* t) {
   PoolCache* owner = t->owner;
-  t->~Task();
+  if (g_paranoid) {
+    if (t->status == STATUS_FREED) fatal("paranoid: task released twice");
+    t->~Task();
+    t->status = STATUS_FREED;
+  } else {
+    t->~Task();
+  }
   PoolElt* e = static_cast<PoolElt*>(static_cast<void*>(t));
   e->owner = owner;
   Mempool::release(e);
@@ -98,6 +115,8 @@ static int schedule_sorted(ExecutionStream* es, Task** tasks, int n, int32_t dis
 
 int schedule_tasks(ExecutionStream* es, Task** tasks, int n, int32_t distance) {
   if (n <= 0) return 0;
+  if (g_paranoid)
+    for (int i = 0; i < n; ++i) paranoid_on_schedule(tasks[i]);
   if (!es) {
     es = my_execution_stream();
     if (!es) es = tasks[0]->taskpool->context->all_es[0];
@@ -177,6 +196,7 @@ int execute_task(ExecutionStream* es, Task* t) {
 
 int complete_task_execution(ExecutionStream* es, Task* t) {
   PARSEC_PINS(es, PINS_COMPLETE_EXEC_BEGIN, t);
+  if (g_paranoid && t->status == STATUS_COMPLETE) fatal("paranoid: task %s completed twice", t->task_class->describe(t).c_str());
   t->status = STATUS_PREPARE_OUTPUT;
   const TaskClass* tc = t->task_class;
   tc->prepare_output(es, t);
@@ -194,6 +214,10 @@ int complete_task_execution(ExecutionStream* es, Task* t) {
 
 int task_progress(ExecutionStream* es, Task* t, int32_t distance) {
   (void)distance;
+  if (g_paranoid) {
+    if (t->status == STATUS_FREED) fatal("paranoid: a released task was selected for execution");
+    t->flags &= ~TASK_FLAG_QUEUED;
+  }
   if (t->status < STATUS_PREPARE_INPUT) {
     t->status = STATUS_PREPARE_INPUT;
     PARSEC_PINS(es, PINS_PREPARE_INPUT_BEGIN, t);
@@ -305,6 +329,7 @@ int32_t taskpool_set_priority(Taskpool* tp, int32_t p) {
 
 Taskpool::~Taskpool() {
   if (registered) taskpool_unregister(this);
+  if (tdm && termdet_private) tdm->release_taskpool(this);
 }
 
 void taskpool_free(Taskpool* tp) {
@@ -333,11 +358,15 @@ int taskpool_termination_detected(Taskpool* tp) {
 int context_add_taskpool(Context* ctx, Taskpool* tp) {
   tp->context = ctx;
   tp->completed.store(false);
-  taskpool_register(tp);
+  // termination detection is set up BEFORE the taskpool is published to the
+  // communication thread (taskpool_register): an early remote activation must
+  // find tdm and its counters in place (race found by the TSan build)
+  taskpool_reserve_id(tp);
   std::string td = tp->termdet_name.empty() ? ctx->default_termdet : tp->termdet_name;
   tp->tdm = termdet_open_module(td);
   if (!tp->tdm) fatal("termination detection module '%s' not available", td.c_str());
   tp->tdm->monitor_taskpool(tp, [](Taskpool* p) { taskpool_termination_detected(p); });
+  taskpool_register(tp);
   ctx->active_taskpools.fetch_add(1, std::memory_order_acq_rel);
   {
     std::lock_guard<std::mutex> g(ctx->tp_m);

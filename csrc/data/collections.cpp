@@ -1,7 +1,9 @@
 #include "collections.hpp"
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "../device/device.hpp"
 
@@ -84,6 +86,72 @@ Data* TiledMatrix::tile_data(int64_t tm, int64_t tn) {
   d = data_create(&tiles[li], this, key, p, (size_t)bsiz * elem_size, DATA_FLAG_PARSEC_MANAGED, storage_device);
   d->copy(storage_device)->dtt = default_dtt;
   return d;
+}
+
+// ======================================================== file dump / load
+// Reference parsec_tiled_matrix_data_write / _read (data_dist/matrix/matrix.h:133-135):
+// every LOCAL tile, raw (bsiz elements), in column-major tile order. One file
+// per process; the file names the distribution it was written with so a read
+// into a different tiling is refused.
+namespace {
+struct MatFileHeader {
+  char magic[8];
+  int32_t mtype, elem_size;
+  int64_t mb, nb, m, n, ntiles;
+};
+constexpr char kMatMagic[8] = {'P', 'A', 'M', 'D', 'T', 'M', 'X', '1'};
+}  // namespace
+
+int TiledMatrix::data_write(const std::string& filename) {
+  FILE* f = std::fopen(filename.c_str(), "wb");
+  if (!f) return -1;
+  MatFileHeader h{};
+  std::memcpy(h.magic, kMatMagic, 8);
+  h.mtype = mtype; h.elem_size = (int32_t)elem_size;
+  h.mb = mb; h.nb = nb; h.m = m; h.n = n;
+  for (int64_t tn = 0; tn < nt; ++tn)
+    for (int64_t tm = 0; tm < mt; ++tm) h.ntiles += local_index(tm, tn) >= 0 ? 1 : 0;
+  int rc = std::fwrite(&h, sizeof(h), 1, f) == 1 ? 0 : -2;
+  const size_t bytes = (size_t)bsiz * elem_size;
+  for (int64_t tn = 0; tn < nt && rc == 0; ++tn)
+    for (int64_t tm = 0; tm < mt && rc == 0; ++tm) {
+      if (local_index(tm, tn) < 0) continue;
+      DataCopy* c = data_pull_to_host(tile_data(tm, tn));  // newest version, wherever it lives
+      const int64_t idx[2] = {tm, tn};
+      if (std::fwrite(idx, sizeof(idx), 1, f) != 1 || std::fwrite(c->device_private, 1, bytes, f) != bytes) rc = -2;
+    }
+  if (std::fclose(f) != 0 && rc == 0) rc = -2;
+  return rc;
+}
+
+int TiledMatrix::data_read(const std::string& filename) {
+  FILE* f = std::fopen(filename.c_str(), "rb");
+  if (!f) return -1;
+  MatFileHeader h{};
+  int rc = 0;
+  if (std::fread(&h, sizeof(h), 1, f) != 1 || std::memcmp(h.magic, kMatMagic, 8) != 0) rc = -3;
+  else if (h.mtype != mtype || h.elem_size != (int32_t)elem_size || h.mb != mb || h.nb != nb || h.m != m || h.n != n) rc = -4;
+  const size_t bytes = (size_t)bsiz * elem_size;
+  std::vector<char> buf(bytes);
+  for (int64_t t = 0; t < h.ntiles && rc == 0; ++t) {
+    int64_t idx[2];
+    if (std::fread(idx, sizeof(idx), 1, f) != 1 || std::fread(buf.data(), 1, bytes, f) != bytes) { rc = -2; break; }
+    Data* d = tile_data(idx[0], idx[1]);
+    if (!d) { rc = -5; break; }  // tile not local here: written with another distribution
+    DataCopy* home = d->copy(storage_device);
+    if (storage_device == 0) std::memcpy(home->device_private, buf.data(), bytes);
+    else if (device_memcpy(storage_device, home->device_private, 0, buf.data(), bytes) != 0) { rc = -2; break; }
+    // the loaded copy becomes the only valid version
+    std::lock_guard<SpinLock> g(d->lock);
+    uint32_t newest = 0;
+    for (int i = 0; i < kMaxDevices; ++i) if (DataCopy* o = d->copy(i)) newest = std::max(newest, o->version);
+    for (int i = 0; i < kMaxDevices; ++i) if (DataCopy* o = d->copy(i); o && o != home) o->coherency_state = COHERENCY_INVALID;
+    home->version = newest + 1;
+    home->coherency_state = COHERENCY_OWNED;
+    d->owner_device = (int8_t)storage_device;
+  }
+  std::fclose(f);
+  return rc;
 }
 
 // ============================================================ block cyclic

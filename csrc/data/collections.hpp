@@ -54,6 +54,9 @@ struct TiledMatrix : DataCollection {
   int64_t tile_rows(int64_t m) const { return std::min<int64_t>(mb, this->m - m * mb); }
   int64_t tile_cols(int64_t n) const { return std::min<int64_t>(nb, this->n - n * nb); }
   void init_base(int mtype, int myrank, int nodes, int64_t mb, int64_t nb, int64_t lm, int64_t ln, int64_t i, int64_t j, int64_t m, int64_t n);
+  // dump / load the local tiles (newest versions) to / from a file; 0 on success
+  int data_write(const std::string& filename);
+  int data_read(const std::string& filename);
 };
 
 // 2D block-cyclic on a P x Q grid, optional k-cyclic repetition (kp, kq) and

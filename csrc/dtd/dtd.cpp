@@ -323,10 +323,7 @@ DtdTask* DtdTaskpool::insert_task(DtdTaskClass* tc, int priority, const std::vec
   t->rank = rank;
   t->remote = rank != my;
   if (!t->remote) tdm->taskpool_addto_nb_tasks(this, 1);
-  else {
-    task_retain(t);
-    remote_tasks.insert(t->seq, t);
-  }
+  else task_retain(t);  // the reference remote_tasks will hold (published below)
   // dependency tracking per tile. Tasks of different ranks never share memory
   // (each rank works on its own copy of a tile), so only same-rank WAR / WAW
   // edges exist; cross-rank edges carry data (writer -> reader / updater).
@@ -371,18 +368,28 @@ DtdTask* DtdTaskpool::insert_task(DtdTaskClass* tc, int priority, const std::vec
     send_late(lw.first, lw.second, t->rank);
     task_unref(lw.first);
   }
-  // activations that arrived before this (remote) task was discovered
+  // Publish the shadow only now that its fields and tile edges are complete,
+  // and collect the activations parked before it was discovered, atomically
+  // with respect to the communication thread's lookup-or-park (shadow_m).
   if (t->remote) {
-    for (int f = 0; f < t->nb_flows; ++f) {
-      RemoteActivation* act = nullptr;
-      uint64_t k = (t->seq << 6) | (uint64_t)f;
-      if (early.find(k, act)) {
-        early.erase(k);
-        ExecutionStream* es = my_execution_stream();
-        on_remote_activation(es ? es : ctx->all_es[0], *act);
-        for (auto*& c : act->data) if (c) { data_copy_release(c); c = nullptr; }
-        delete act;
+    std::vector<RemoteActivation*> parked;
+    {
+      std::lock_guard<std::mutex> g(shadow_m);
+      remote_tasks.insert(t->seq, t);
+      for (int f = 0; f < t->nb_flows; ++f) {
+        RemoteActivation* act = nullptr;
+        uint64_t k = (t->seq << 6) | (uint64_t)f;
+        if (early.find(k, act)) {
+          early.erase(k);
+          parked.push_back(act);
+        }
       }
+    }
+    for (RemoteActivation* act : parked) {
+      ExecutionStream* es = my_execution_stream();
+      on_remote_activation(es ? es : ctx->all_es[0], *act);
+      for (auto*& c : act->data) if (c) { data_copy_release(c); c = nullptr; }
+      delete act;
     }
   }
   // drop the insertion guard
@@ -394,6 +401,13 @@ DtdTask* DtdTaskpool::insert_task(DtdTaskClass* tc, int priority, const std::vec
   }
   // sliding window
   if (!t->remote && nb_tasks.load(std::memory_order_relaxed) > window) execute_and_come_back(threshold);
+  if (t->remote) {
+    // a remote shadow never completes here: drop the insertion reference; the
+    // shadow lives on through remote_tasks and the edges that reference it
+    // (leak found by the ASan build)
+    task_unref(t);
+    return nullptr;
+  }
   return t;
 }
 
@@ -613,6 +627,7 @@ static void task_unref(DtdTask* t) {
 
 void DtdTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& act) {
   DtdTask* t = nullptr;
+  std::unique_lock<std::mutex> lk(shadow_m);
   if (!remote_tasks.find(act.dtd_task_id, t)) {
     // not discovered yet: park a copy of the activation per flow
     for (int f = 0; f < kMaxFlows; ++f) {
@@ -626,6 +641,7 @@ void DtdTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& ac
     }
     return;
   }
+  lk.unlock();
   // install received versions on the tiles the remote task wrote
   for (auto& a : t->args) {
     if (a.flow < 0 || !a.tile || !(act.output_mask & (1u << a.flow)) || !act.data[a.flow]) continue;

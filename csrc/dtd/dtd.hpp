@@ -11,6 +11,7 @@
 // (every rank inserts the whole stream; owner computes; activation once per
 // (flow, rank), :1568-1577, remote_dep_mpi.c:858-898).
 #pragma once
+#include <mutex>
 #include <map>
 #include <string>
 #include <vector>
@@ -103,6 +104,7 @@ class DtdTaskpool : public Taskpool {
   std::vector<DtdTaskClass*> classes;
   ShardedMap<Tile*> tiles{8};
   ShardedMap<DtdTask*> remote_tasks{8};   // seq -> remote shadow awaiting activation
+  std::mutex shadow_m;  // lookup-or-park of remote activations vs publication of a shadow
   ShardedMap<RemoteActivation*> early{6}; // activations that arrived before the insert
   std::atomic<uint64_t> seq{0};
   int64_t window = 8000, threshold = 4000;

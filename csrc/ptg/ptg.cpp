@@ -565,6 +565,12 @@ void PtgTaskpool::activate(ExecutionStream* es, PtgTaskClass* tc, const int32_t*
     }
     PARSEC_DEBUG(kVerbNoisier, "ptg", "  %s deps_remaining %d -> %d", tc->name.c_str(), task->deps_remaining, task->deps_remaining - 1);
     if (--task->deps_remaining <= 0) {
+      if (g_paranoid) {
+        if (task->deps_remaining < 0)
+          fatal("paranoid: %s activated more times than it has inputs (%d extra)", tc->describe(task).c_str(), -task->deps_remaining);
+        std::lock_guard<std::mutex> lk(paranoid_m);
+        if (!paranoid_fired.insert(key).second) fatal("paranoid: %s became ready twice (double activation)", tc->describe(task).c_str());
+      }
       m.erase(key);
       return task;
     }

@@ -17,6 +17,8 @@
 // activation and stores the incoming data copies straight into it (refcounted),
 // so no per-producer data repository lookup happens on the hot path.
 #pragma once
+#include <mutex>
+#include <unordered_set>
 #include <functional>
 #include <string>
 #include <vector>
@@ -147,6 +149,9 @@ class PtgTaskpool : public Taskpool {
  public:
   std::vector<PtgTaskClass*> classes;
   ShardedMap<Task*> pending{10};
+  // debug_paranoid: keys of tasks that already became ready (double-activation check)
+  std::mutex paranoid_m;
+  std::unordered_set<uint64_t> paranoid_fired;
   std::vector<int64_t> globals;      // generic storage for generated code
   // ptgpp --dynamic-termdet: tasks are counted as they are discovered (startup
   // tasks, then each first activation) instead of enumerating the whole local

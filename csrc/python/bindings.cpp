@@ -362,6 +362,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("storage_ptr", [](TiledMatrix& t) { return (uintptr_t)t.mat; })
       .def_property_readonly("storage_bytes", [](TiledMatrix& t) { return (size_t)t.nb_local_tiles * (size_t)t.bsiz * t.elem_size; })
       .def("local_index", &TiledMatrix::local_index)
+      .def("data_write", [](TiledMatrix& t, const std::string& f) { py::gil_scoped_release rel; return t.data_write(f); })
+      .def("data_read", [](TiledMatrix& t, const std::string& f) { py::gil_scoped_release rel; return t.data_read(f); })
       .def("tile_ptr", [](TiledMatrix& t, int64_t a, int64_t b) { return (uintptr_t)t.tile_ptr(a, b); })
       .def("tile", [](TiledMatrix& t, int64_t a, int64_t b) -> py::object {
         // column-major numpy view of the newest host copy of a local tile

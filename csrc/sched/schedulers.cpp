@@ -110,23 +110,25 @@ class HBBuffer {
 // Priority heap of tasks with split-and-steal (reference maxheap.c:156).
 class MaxHeap {
  public:
-  void insert(Task* t) { std::lock_guard<SpinLock> g(lock_); v_.push_back(t); std::push_heap(v_.begin(), v_.end(), cmp); }
+  void insert(Task* t) { std::lock_guard<SpinLock> g(lock_); v_.push_back(t); std::push_heap(v_.begin(), v_.end(), cmp); sync(); }
   void insert_many(Task** t, int n) {
     std::lock_guard<SpinLock> g(lock_);
     for (int i = 0; i < n; ++i) { v_.push_back(t[i]); std::push_heap(v_.begin(), v_.end(), cmp); }
+    sync();
   }
   Task* pop() {
-    if (v_.empty()) return nullptr;
+    if (count_.load(std::memory_order_acquire) == 0) return nullptr;  // unlocked fast path: atomic count only
     std::lock_guard<SpinLock> g(lock_);
     if (v_.empty()) return nullptr;
     std::pop_heap(v_.begin(), v_.end(), cmp);
     Task* t = v_.back();
     v_.pop_back();
+    sync();
     return t;
   }
   // Steal: take the top and half of the remaining elements into `out`.
   Task* split_and_steal(MaxHeap& thief) {
-    if (v_.empty()) return nullptr;
+    if (count_.load(std::memory_order_acquire) == 0) return nullptr;
     std::vector<Task*> moved;
     Task* top = nullptr;
     {
@@ -141,12 +143,15 @@ class MaxHeap {
       moved.assign(v_.end() - half, v_.end());
       v_.resize(v_.size() - half);
       std::make_heap(v_.begin(), v_.end(), cmp);
+      sync();
     }
     if (!moved.empty()) thief.insert_many(moved.data(), (int)moved.size());
     return top;
   }
-  size_t size() const { return v_.size(); }
+  size_t size() const { return count_.load(std::memory_order_relaxed); }
  private:
+  void sync() { count_.store(v_.size(), std::memory_order_release); }
+  std::atomic<size_t> count_{0};
   static bool cmp(Task* a, Task* b) { return a->priority < b->priority; }
   SpinLock lock_;
   std::vector<Task*> v_;
@@ -158,23 +163,26 @@ class SortedQueue {
   void push_sorted(Task** t, int n) {
     std::lock_guard<SpinLock> g(lock_);
     for (int i = 0; i < n; ++i) q_.push({t[i]->priority, seq_++, t[i]});
+    count_.store(q_.size(), std::memory_order_release);
   }
   Task* pop_best() {
-    if (q_.empty()) return nullptr;
+    if (empty()) return nullptr;  // unlocked fast path reads the atomic count only
     std::lock_guard<SpinLock> g(lock_);
     if (q_.empty()) return nullptr;
     Task* t = q_.top().t;
     q_.pop();
+    count_.store(q_.size(), std::memory_order_release);
     return t;
   }
-  bool empty() const { return q_.empty(); }
-  size_t size() const { return q_.size(); }
+  bool empty() const { return count_.load(std::memory_order_acquire) == 0; }
+  size_t size() const { return count_.load(std::memory_order_relaxed); }
  private:
   struct E { int32_t prio; uint64_t seq; Task* t; };
   struct C { bool operator()(const E& a, const E& b) const { return a.prio != b.prio ? a.prio < b.prio : a.seq > b.seq; } };
   SpinLock lock_;
   std::priority_queue<E, std::vector<E>, C> q_;
   uint64_t seq_ = 0;
+  std::atomic<size_t> count_{0};
 };
 
 // Common helpers ----------------------------------------------------------
@@ -350,16 +358,18 @@ class VpListScheduler : public Scheduler {
       if (mode_ == IP) key = -key;
       q->items.push({key, q->seq++, tasks[i]});
     }
+    q->count.store(q->items.size(), std::memory_order_release);
     return 0;
   }
   Task* select(ExecutionStream* es, int32_t* distance) override {
     *distance = 0;
     Q* q = static_cast<Q*>(es->vp->sched_obj);
-    if (q->items.empty()) return nullptr;
+    if (q->count.load(std::memory_order_acquire) == 0) return nullptr;  // unlocked fast path: atomic count only
     std::lock_guard<SpinLock> g(q->lock);
     if (q->items.empty()) return nullptr;
     Task* t = q->items.top().t;
     q->items.pop();
+    q->count.store(q->items.size(), std::memory_order_release);
     return t;
   }
   void remove(Context* ctx) override {
@@ -372,6 +382,7 @@ class VpListScheduler : public Scheduler {
     SpinLock lock;
     std::priority_queue<E, std::vector<E>, C> items;
     uint64_t seq = 0;
+    std::atomic<size_t> count{0};
     std::minstd_rand rng{42};
   };
   Mode mode_;
@@ -437,6 +448,7 @@ class GdScheduler : public Scheduler {
       if (!head || tasks[i]->priority >= head->priority) l.push_front(tasks[i]);
       else l.push_back(tasks[i]);
     }
+    q->sync_count();
     return 0;
   }
   Task* select(ExecutionStream* es, int32_t* distance) override {

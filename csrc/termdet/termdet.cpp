@@ -37,6 +37,10 @@ class LocalTermdet : public TermdetModule {
     // keep the callback object alive until the taskpool dies; it is tiny.
     (void)tp;
   }
+  void release_taskpool(Taskpool* tp) override {
+    delete static_cast<TermdetCallback*>(tp->termdet_private);
+    tp->termdet_private = nullptr;
+  }
   void taskpool_ready(Taskpool* tp) override {
     int exp = TERMDET_NOT_READY;
     tp->termdet_state.compare_exchange_strong(exp, TERMDET_BUSY);
@@ -75,6 +79,12 @@ class UserTriggerTermdet : public TermdetModule {
     tp->nb_pending_actions.store(0);
     tp->termdet_state.store(TERMDET_NOT_READY);
     tp->termdet_private = new TermdetCallback{std::move(cb)};
+    triggered_.erase(tp);
+  }
+  void release_taskpool(Taskpool* tp) override {
+    delete static_cast<TermdetCallback*>(tp->termdet_private);
+    tp->termdet_private = nullptr;
+    std::lock_guard<std::mutex> g(m_);
     triggered_.erase(tp);
   }
   void taskpool_ready(Taskpool* tp) override {

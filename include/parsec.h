@@ -206,6 +206,9 @@ parsec_data_key_t parsec_tiled_matrix_data_key(parsec_tiled_matrix_t* tdesc, int
 size_t parsec_matrix_type_size(parsec_matrix_type_t mtype);
 /* place the local storage in HBM of a GPU device (device index >= 2) */
 int parsec_tiled_matrix_set_storage_device(parsec_tiled_matrix_t* tdesc, int device_index);
+/* dump / load the local tiles of a matrix to / from a file (one file per process) */
+int parsec_tiled_matrix_data_write(parsec_tiled_matrix_t* tdesc, const char* filename);
+int parsec_tiled_matrix_data_read(parsec_tiled_matrix_t* tdesc, const char* filename);
 
 /* ---------------------------------------------------------------- arenas */
 #define PARSEC_ARENA_ALIGNMENT_64b 8

@@ -6,7 +6,12 @@ Outputs (in-tree so they travel with the repo snapshot to the GPU box):
   parsec_amd/bin/parsec-ptgpp       .jdf -> C++ compiler
   build/tests/*                     native unit tests
 
-Usage: python -m parsec_amd._build [--clean] [-j N]
+Usage: python -m parsec_amd._build [--clean] [-j N] [--sanitize address|thread|leak]
+
+--sanitize KIND (reference CMake PARSEC_DEBUG_MEM_ADDR / _LEAK / _RACE,
+CMakeLists.txt:195-200): host code of the runtime rebuilt with -fsanitize=KIND
+into build-KIND/ (libparsec_amd.so, the container test and the C DTD program);
+the gfx950 kernel objects of the main build are linked in uninstrumented.
 """
 import os
 import subprocess
@@ -144,6 +149,77 @@ def generate():
         f.write("\n".join(lines) + "\n")
 
 
+SANITIZERS = ("address", "thread", "leak")
+
+
+def sanitize_dir(kind):
+    return os.path.join(ROOT, "build-" + kind)
+
+
+def generate_sanitized(kind):
+    """build-KIND/build.ninja: instrumented host runtime + test executables."""
+    if kind not in SANITIZERS:
+        raise ValueError(f"unknown sanitizer {kind!r}")
+    out = sanitize_dir(kind)
+    os.makedirs(os.path.join(out, "obj"), exist_ok=True)
+    flags = (f"-std=c++20 -O1 -g -fno-omit-frame-pointer -fPIC -fsanitize={kind} -D__HIP_PLATFORM_AMD__ "
+             f"-I{ROCM}/include -I{ROOT}/csrc -I{ROOT}/include -Wno-unused-result")
+    libs = f"-fsanitize={kind} -L{ROCM}/lib -lamdhip64 -lrccl -latomic -lpthread -lrt -Wl,-rpath,{ROCM}/lib"
+    lines = [
+        "rule cxx",
+        f"  command = g++ {flags} -MMD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "  description = CXX[" + kind + "] $out",
+        "rule cc",
+        f"  command = gcc -std=c99 -O1 -g -fno-omit-frame-pointer -fsanitize={kind} -I{ROOT}/include -c $in -o $out",
+        "  description = CC[" + kind + "] $out",
+        "rule solink",
+        "  command = g++ -shared -o $out $in $libs",
+        "  description = LINK $out",
+        "rule exelink",
+        "  command = g++ -o $out $in $libs",
+        "  description = LINK $out",
+    ]
+    objs = []
+    for src in _exists(CORE_SOURCES):
+        obj = os.path.join(out, "obj", src.replace("/", "_") + ".o")
+        lines.append(f"build {obj}: cxx {os.path.join(ROOT, src)}")
+        objs.append(obj)
+    # device kernels: the main build's objects (host stubs only, not instrumented)
+    for src in _exists(HIP_SOURCES):
+        objs.append(os.path.join(BUILD, "obj", src.replace("/", "_") + ".o"))
+    lib = os.path.join(out, "libparsec_amd.so")
+    lines.append(f"build {lib}: solink {' '.join(objs)}")
+    lines.append(f"  libs = {libs}")
+    for src in _exists(TEST_SOURCES):
+        obj = os.path.join(out, "obj", src.replace("/", "_") + ".o")
+        exe = os.path.join(out, os.path.splitext(os.path.basename(src))[0])
+        lines.append(f"build {obj}: cxx {os.path.join(ROOT, src)}")
+        lines.append(f"build {exe}: exelink {obj} | {lib}")
+        lines.append(f"  libs = -L{out} -lparsec_amd -Wl,-rpath,{out} {libs}")
+    capi = "tests/capi/dtd_capi.c"
+    if os.path.exists(os.path.join(ROOT, capi)):
+        lines.append(f"build {os.path.join(out, 'obj', 'dtd_capi.o')}: cc {os.path.join(ROOT, capi)}")
+        lines.append(f"build {os.path.join(out, 'dtd_capi')}: exelink {os.path.join(out, 'obj', 'dtd_capi.o')} | {lib}")
+        lines.append(f"  libs = -L{out} -lparsec_amd -Wl,-rpath,{out} {libs}")
+    with open(os.path.join(out, "build.ninja"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return out
+
+
+def build_sanitized(kind, jobs=None):
+    """Build the instrumented runtime (needs the main build's kernel objects)."""
+    need = [os.path.join(BUILD, "obj", s.replace("/", "_") + ".o") for s in _exists(HIP_SOURCES)]
+    if not all(os.path.exists(p) for p in need):
+        build(jobs)
+    out = generate_sanitized(kind)
+    r = subprocess.run(["ninja", "-C", out, f"-j{jobs or min(8, os.cpu_count() or 4)}"])
+    if r.returncode != 0:
+        raise RuntimeError(f"sanitized ({kind}) build failed")
+    return out
+
+
 def build(jobs=None, verbose=False):
     generate()
     jobs = jobs or min(8, os.cpu_count() or 4)
@@ -161,4 +237,7 @@ if __name__ == "__main__":
     j = None
     if "-j" in sys.argv:
         j = int(sys.argv[sys.argv.index("-j") + 1])
-    build(j, verbose="-v" in sys.argv)
+    if "--sanitize" in sys.argv:
+        build_sanitized(sys.argv[sys.argv.index("--sanitize") + 1], j)
+    else:
+        build(j, verbose="-v" in sys.argv)

@@ -27,18 +27,36 @@ def launch(nprocs, cmd, gpus=0, timeout=None, env=None, capture=False):
             e["PARSEC_COMM_GPU"] = str(r % gpus)
         kw = dict(stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) if capture else {}
         procs.append(subprocess.Popen(cmd, env=e, **kw))
-    deadline = time.time() + timeout if timeout else None
-    outs = []
+    # drain every rank's pipes concurrently: a rank blocked on a full pipe
+    # would otherwise stall the ranks waiting for it (collective deadlock)
+    results = [None] * len(procs)
+
+    def _wait(i, p):
+        try:
+            results[i] = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            results[i] = "timeout"
+
+    import threading
+
+    th = [threading.Thread(target=_wait, args=(i, p), daemon=True) for i, p in enumerate(procs)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if any(r == "timeout" for r in results):
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+        for q in procs:
+            try:
+                q.communicate(timeout=10)
+            except Exception:
+                pass
+        raise subprocess.TimeoutExpired(cmd, timeout)
+    outs = [r if r is not None else (None, None) for r in results]
     rc = 0
     for p in procs:
-        left = max(1.0, deadline - time.time()) if deadline else None
-        try:
-            o, er = p.communicate(timeout=left)
-        except subprocess.TimeoutExpired:
-            for q in procs:
-                q.kill()
-            raise
-        outs.append((o, er))
         if p.returncode and not rc:
             rc = p.returncode
     return (rc, outs) if capture else rc

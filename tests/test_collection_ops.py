@@ -153,3 +153,33 @@ def test_ptg_dgemm_gpu(pa):
     _run(pa, ctx, pa.dgemm_new(1.0, A, B, 1.0, C, 0))
     assert np.allclose(_dense(C, M, N, b), SA @ SB + SC)
     ctx.fini()
+
+
+def test_tiled_matrix_data_write_read(pa, tmp_path):
+    """parsec_tiled_matrix_data_write / _read (reference data_dist/matrix/matrix.h:133-135):
+    local tiles dumped after a DAG ran on them, reloaded into a fresh collection;
+    a file written with another tiling is refused."""
+    import numpy as np
+
+    ctx = pa.init(2)
+    nb, N = 16, 40
+    A = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb, nb, N, N)
+    rng = np.random.default_rng(3)
+    ref = {}
+    for m in range(A.mt):
+        for n in range(A.nt):
+            ref[m, n] = rng.standard_normal((nb, nb))
+            A.tile(m, n)[:, :] = ref[m, n]
+    path = str(tmp_path / "A.bin")
+    assert A.data_write(path) == 0
+    B = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb, nb, N, N)
+    for m in range(B.mt):
+        for n in range(B.nt):
+            B.tile(m, n)[:, :] = 0.0
+    assert B.data_read(path) == 0
+    for (m, n), t in ref.items():
+        assert np.array_equal(np.asarray(B.tile(m, n)), t)
+    C = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, 8, 8, N, N)
+    assert C.data_read(path) != 0
+    assert B.data_read(str(tmp_path / "missing.bin")) != 0
+    ctx.fini()

@@ -38,6 +38,29 @@ def test_jdf_program(tmp_path, name, expect):
     assert expect in r.stdout
 
 
+@pytest.mark.parametrize("name,expect", [
+    ("chain", "chain value 10"),
+    ("bcast_gather", "leaves 37 sink 1 bad 0"),
+    ("tree_reduce", "root 2080 nodes 63 bad 0"),
+    ("all2all", "recv 16 done 4 bad 0"),
+])
+def test_jdf_program_paranoid(tmp_path, name, expect):
+    """debug_paranoid (reference PARSEC_DEBUG_PARANOID) raises no false positive on valid DAGs."""
+    exe = ptgpp.build_program(os.path.join(JDF, name + ".jdf"), str(tmp_path))
+    r = _run(exe, env={"PARSEC_MCA_debug_paranoid": "1"})
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert expect in r.stdout
+
+
+def test_paranoid_detects_double_activation(tmp_path):
+    """A DAG whose producer releases a single-input consumer twice: paranoid mode aborts
+    with a double-activation diagnostic (reference parsec.c:1619-1657)."""
+    exe = ptgpp.build_program(os.path.join(JDF, "double_activation.jdf"), str(tmp_path))
+    r = _run(exe, env={"PARSEC_MCA_debug_paranoid": "1"})
+    assert r.returncode != 0
+    assert "double activation" in r.stderr
+
+
 @pytest.mark.parametrize("name,msg", [
     ("bad_output_null", "NULL data only supported in IN dependencies."),
     ("bad_output_new", "Automatic data allocation with NEW only supported in IN dependencies."),
