@@ -101,8 +101,16 @@ struct CCollection : DataCollection {
 // user-provided `mat` pointer lazily (reference users assign it after init).
 struct CBlockCyclic : BlockCyclic {
   parsec_matrix_block_cyclic_t* c = nullptr;
+  std::mutex sync_m;
+  std::atomic<bool> synced{false};
+  // called from every worker thread's data_of: the first caller installs the
+  // storage (tiles table included) under the lock, the others wait for it
   void sync() {
+    if (synced.load(std::memory_order_acquire)) return;
+    std::lock_guard<std::mutex> g(sync_m);
+    if (synced.load(std::memory_order_relaxed)) return;
     if (!mat && c->mat) allocate_storage(c->mat);
+    if (mat) synced.store(true, std::memory_order_release);
   }
   Data* data_of(const int64_t* idx, int n) override { sync(); return BlockCyclic::data_of(idx, n); }
   Data* data_of_key(uint64_t key) override { sync(); return BlockCyclic::data_of_key(key); }
