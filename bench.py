@@ -36,6 +36,60 @@ def _stage(msg):
         print(f"[bench rank {os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
 
 
+def residual_probe(torch, dist, world, A, store, backup, nb, N, rank, share_gpu):
+    """||A x - L L^T x||_2 / (||A||_F ||x||_2) from the local tiles of A (backup,
+    lower half) and L (store); the three partial vectors and ||A||_F^2 are summed
+    over ranks (two all-reduces)."""
+    dev = store.device
+    g = torch.Generator(device=dev).manual_seed(4242)
+    x = torch.rand(N, dtype=torch.float64, device=dev, generator=g) - 0.5
+    tiles, btiles = store.view(-1, nb, nb), backup.view(-1, nb, nb)
+    NT = A.nt
+    loc = [(m, n, A.local_index(m, n)) for n in range(NT) for m in range(n, NT)]
+    loc = [(m, n, li) for (m, n, li) in loc if li >= 0]
+
+    def blk(t, m, n):  # column-major tile -> (rows x cols) matrix view
+        r, c = min(nb, N - m * nb), min(nb, N - n * nb)
+        return t.t()[:r, :c]
+
+    def allsum(v):
+        if world > 1:
+            if share_gpu:
+                c = v.cpu()
+                dist.all_reduce(c)
+                v.copy_(c)
+            else:
+                dist.all_reduce(v)
+        return v
+
+    ax = torch.zeros(N, dtype=torch.float64, device=dev)
+    ltx = torch.zeros(N, dtype=torch.float64, device=dev)
+    fro = torch.zeros(1, dtype=torch.float64, device=dev)
+    for m, n, li in loc:
+        a = blk(btiles[li], m, n)
+        l = blk(tiles[li], m, n)
+        sm, sn = slice(m * nb, m * nb + a.shape[0]), slice(n * nb, n * nb + a.shape[1])
+        if m == n:
+            a = torch.tril(a) + torch.tril(a, -1).t()
+            l = torch.tril(l)
+            fro += (a * a).sum()
+        else:
+            ax[sn] += a.t() @ x[sm]
+            fro += 2 * (a * a).sum()
+        ax[sm] += a @ x[sn]
+        ltx[sn] += l.t() @ x[sm]
+    allsum(ltx)
+    llx = torch.zeros(N, dtype=torch.float64, device=dev)
+    for m, n, li in loc:
+        l = blk(tiles[li], m, n)
+        if m == n:
+            l = torch.tril(l)
+        llx[m * nb:m * nb + l.shape[0]] += l @ ltx[n * nb:n * nb + l.shape[1]]
+    v = torch.cat([ax - llx, fro])
+    allsum(v)
+    return float(torch.linalg.norm(v[:N]) / (torch.sqrt(v[N]) * torch.linalg.norm(x)))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -133,9 +187,12 @@ def main():
             raise RuntimeError("dpotrf reported a non-SPD matrix")
     barrier()
     t0 = time.perf_counter()
+    bad = 0
     for _ in range(args.steps):
-        info = step()
+        bad = bad or step()  # LAPACK info of every timed factorization (host int, no sync)
     barrier()
+    if bad:
+        raise RuntimeError(f"dpotrf info={bad} in a timed step")
     dt = time.perf_counter() - t0
     _stage("timed region done")
     if world > 1:
@@ -145,6 +202,14 @@ def main():
     ms = dt / args.steps * 1e3
     flops = N ** 3 / 3 + N ** 2 / 2 + N / 6
     gflops = flops / (ms * 1e-3) / 1e9
+
+    # Backward error of the LAST timed factorization over the whole matrix (outside
+    # the timed region): r = ||A x - L (L^T x)|| / (||A||_F ||x||) for a random x,
+    # each rank contributing its local tiles, partial vectors summed over ranks.
+    resid = residual_probe(torch, dist, world, A, store, backup, nb, N, rank, args.share_gpu)
+    _stage(f"residual {resid:.3e}")
+    if not resid < 1e-12:
+        raise RuntimeError(f"DPOTRF residual {resid:.3e} too large")
 
     check = None
     if args.check:
@@ -199,7 +264,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp64",
-            "data": "synthetic random SPD (diagonally dominant), HBM-resident tiles",
+            "data": "synthetic random symmetric + N*I (DPLASMA plgsy convention), HBM-resident tiles",
+            "residual": float(f"{resid:.3e}"),
             "config": {"model": "tiled DPOTRF lower (PTG)", "N": N, "nb": nb, "global_batch": 1, "seq_len": N,
                        "parallelism": f"2D block-cyclic P{P}xQ{Q}, 1 process/GPU", "threads_per_rank": args.cores},
         }

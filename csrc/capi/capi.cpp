@@ -429,6 +429,8 @@ parsec_data_key_t parsec_tiled_matrix_data_key(parsec_tiled_matrix_t* tdesc, int
 int parsec_tiled_matrix_set_storage_device(parsec_tiled_matrix_t* tdesc, int device_index) {
   auto* tm = dynamic_cast<TiledMatrix*>(impl_of(&tdesc->super));
   if (!tm || tm->mat) return PARSEC_ERROR;
+  // a user pointer assigned after init but not yet picked up also owns the storage
+  if (auto* cb = dynamic_cast<CBlockCyclic*>(tm); cb && cb->c && cb->c->mat) return PARSEC_ERROR;
   tm->storage_device = device_index;
   tm->allocate_storage(nullptr);
   return PARSEC_SUCCESS;

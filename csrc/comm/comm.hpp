@@ -87,6 +87,7 @@ int remote_dep_activate(ExecutionStream* es, Taskpool* tp, RemoteDepsMsg& msg);
 CommEngine* comm_engine();
 uint32_t comm_allreduce_max_u32(uint32_t v);
 int comm_barrier();
+const char* comm_device_plane_name();  // "ipc" | "rccl" | "host" | "none"
 int comm_rank();
 int comm_size();
 // Bring up the engine explicitly (Python / launcher); returns 0 on success.

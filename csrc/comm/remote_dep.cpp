@@ -31,6 +31,14 @@ int comm_rank() { return g_ce ? g_ce->rank : 0; }
 int comm_size() { return g_ce ? g_ce->size : 1; }
 uint32_t comm_allreduce_max_u32(uint32_t v) { return g_ce ? (uint32_t)g_ce->allreduce_max(v) : v; }
 int comm_barrier() { return g_ce ? g_ce->sync() : 0; }
+const char* comm_device_plane_name() {
+  if (!g_ce) return "none";
+  switch (g_ce->device_plane()) {
+    case ShmEngine::PLANE_IPC: return "ipc";
+    case ShmEngine::PLANE_RCCL: return "rccl";
+    default: return "host";
+  }
+}
 
 // ------------------------------------------------------------- wire format
 namespace {
@@ -174,6 +182,9 @@ DataCopy* new_recv_copy(size_t bytes, bool device) {
       auto& v = pool.free[bytes];
       if (!v.empty()) { p = v.back(); v.pop_back(); }
     }
+    // carved from the GPU's tile-cache zone (no hipMalloc / memset on the comm
+    // thread); recycled by size through the pool, returned at remote_dep_fini
+    if (!p) p = device_cache_alloc(g_gpu_index, bytes);
     if (!p) p = device_alloc(g_gpu_index, bytes);
     dev = p ? g_gpu_index : 0;
   }
@@ -590,6 +601,15 @@ void remote_dep_init(Context* ctx) {
 }
 
 void remote_dep_fini(Context* ctx) {
+  {
+    // the zone goes away with the devices: hand the cached receive buffers back
+    auto& p = dev_pool();
+    std::lock_guard<std::mutex> g(p.m);
+    for (auto& [sz, v] : p.free)
+      for (void* b : v)
+        if (!device_cache_free(g_gpu_index, b)) device_free(g_gpu_index, b);
+    p.free.clear();
+  }
   if (g_ce) {
     // nothing must be in flight when the context goes away
     g_ce->sync();

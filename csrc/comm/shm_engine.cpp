@@ -14,6 +14,7 @@
 // deadlock (unlike one shared communicator whose ordered stream would serialize
 // a send behind an unrelated receive).
 #include "shm_engine.hpp"
+#include "../device/device.hpp"
 
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
@@ -165,6 +166,10 @@ int ShmEngine::init() {
     }
   });
   g_engine = this;
+  // the comm thread (and the runtime threads created later from this thread)
+  // run on the NUMA node of this rank's GPU
+  if (gpu_ >= 0 && ParamRegistry::instance().reg_int("runtime", "", "bind_gpu_numa", "Restrict runtime threads to the NUMA node of the (first) GPU", 1))
+    bind_thread_to_gpu_numa(gpu_);
   start_thread();
   // device data plane: ipc (default) | rccl | host
   const std::string plane = ParamRegistry::instance().reg_string("comm", "", "device_plane", "Data plane for device-resident tiles: ipc, rccl or host", "ipc");

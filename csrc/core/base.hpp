@@ -110,14 +110,17 @@ class Lifo {
   void push(T* it) noexcept {
     Head old, nw;
     load(old);
-    do { static_cast<ListItem*>(it)->next = old.ptr; nw.ptr = it; nw.gen = old.gen + 1; } while (!cas(old, nw));
+    // `next` is accessed atomically: a concurrent pop may read it from an item
+    // that was popped and is being pushed again (the generation makes that CAS
+    // fail, but the read itself must not be a data race)
+    do { __atomic_store_n(&static_cast<ListItem*>(it)->next, old.ptr, __ATOMIC_RELAXED); nw.ptr = it; nw.gen = old.gen + 1; } while (!cas(old, nw));
   }
   T* pop() noexcept {
     Head old, nw;
     load(old);
     do {
       if (!old.ptr) return nullptr;
-      nw.ptr = old.ptr->next; nw.gen = old.gen + 1;
+      nw.ptr = __atomic_load_n(&old.ptr->next, __ATOMIC_RELAXED); nw.gen = old.gen + 1;
     } while (!cas(old, nw));
     return static_cast<T*>(old.ptr);
   }

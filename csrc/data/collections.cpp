@@ -116,8 +116,11 @@ int TiledMatrix::data_write(const std::string& filename) {
   for (int64_t tn = 0; tn < nt && rc == 0; ++tn)
     for (int64_t tm = 0; tm < mt && rc == 0; ++tm) {
       if (local_index(tm, tn) < 0) continue;
-      DataCopy* c = data_pull_to_host(tile_data(tm, tn));  // newest version, wherever it lives
       const int64_t idx[2] = {tm, tn};
+      // virtual data_of: subclasses with lazily attached storage install it first
+      Data* d = data_of(idx, 2);
+      if (!d) { rc = -5; break; }
+      DataCopy* c = data_pull_to_host(d);  // newest version, wherever it lives
       if (std::fwrite(idx, sizeof(idx), 1, f) != 1 || std::fwrite(c->device_private, 1, bytes, f) != bytes) rc = -2;
     }
   if (std::fclose(f) != 0 && rc == 0) rc = -2;
@@ -133,10 +136,13 @@ int TiledMatrix::data_read(const std::string& filename) {
   else if (h.mtype != mtype || h.elem_size != (int32_t)elem_size || h.mb != mb || h.nb != nb || h.m != m || h.n != n) rc = -4;
   const size_t bytes = (size_t)bsiz * elem_size;
   std::vector<char> buf(bytes);
+  // a file written on another process grid holds a different tile set: refuse it
+  if (rc == 0 && h.ntiles != nb_local_tiles) rc = -5;
   for (int64_t t = 0; t < h.ntiles && rc == 0; ++t) {
     int64_t idx[2];
     if (std::fread(idx, sizeof(idx), 1, f) != 1 || std::fread(buf.data(), 1, bytes, f) != bytes) { rc = -2; break; }
-    Data* d = tile_data(idx[0], idx[1]);
+    if (local_index(idx[0], idx[1]) < 0) { rc = -5; break; }  // tile not local here: written with another distribution
+    Data* d = data_of(idx, 2);
     if (!d) { rc = -5; break; }  // tile not local here: written with another distribution
     DataCopy* home = d->copy(storage_device);
     if (storage_device == 0) std::memcpy(home->device_private, buf.data(), bytes);

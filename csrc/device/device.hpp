@@ -29,6 +29,15 @@ int gpu_chore_dispatch(ExecutionStream* es, Task* t, int chore);
 // Raw device memory helpers (outside the engine's tile cache).
 void* device_alloc(int device_index, size_t bytes);
 void device_free(int device_index, void* p);
+// Thread-safe allocation from a GPU's tile-cache zone (no eviction, no memset):
+// communication receive buffers. nullptr when the zone is full / no such GPU.
+void* device_cache_alloc(int device_index, size_t bytes);
+// Returns false when `p` does not belong to the zone (then use device_free).
+bool device_cache_free(int device_index, void* p);
+// Restrict the calling thread (and the threads it creates later) to the CPUs of
+// the NUMA node closest to HIP device `ordinal` (intersected with the current
+// affinity). Returns the node, or -1 when unknown / nothing to do.
+int bind_thread_to_gpu_numa(int ordinal);
 int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t bytes);
 int device_hip_ordinal(int device_index);  // -1 if not a HIP device
 int first_gpu_device_index();

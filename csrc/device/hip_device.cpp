@@ -2,9 +2,12 @@
 
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 
 #include "../prof/profiling.hpp"
 
@@ -59,9 +62,9 @@ void* ZoneAllocator::alloc(size_t bytes) {
   return base;
 }
 
-void ZoneAllocator::free(void* p) {
+bool ZoneAllocator::free(void* p) {
   auto it = live_.find(p);
-  if (it == live_.end()) return;
+  if (it == live_.end()) return false;
   auto [si, sz] = it->second;
   live_.erase(it);
   used_ -= sz;
@@ -73,9 +76,10 @@ void ZoneAllocator::free(void* p) {
   // coalesce with prev
   if (nx != s.free_.begin()) {
     auto pv = std::prev(nx);
-    if (pv->first + pv->second == off) { pv->second += sz; return; }
+    if (pv->first + pv->second == off) { pv->second += sz; return true; }
   }
   s.free_[off] = sz;
+  return true;
 }
 
 // ================================================================ helpers
@@ -96,6 +100,72 @@ void device_free(int device_index, void* p) {
   int ord = device_hip_ordinal(device_index);
   if (ord < 0 || !p) return;
   (void)hipFree(p);
+}
+
+void* device_cache_alloc(int device_index, size_t bytes) {
+  auto* d = dynamic_cast<HipDevice*>(DeviceRegistry::instance().get(device_index));
+  if (!d) return nullptr;
+  std::lock_guard<std::mutex> g(d->zone_m);
+  d->ensure_zone();
+  return d->zone->alloc(bytes);
+}
+
+bool device_cache_free(int device_index, void* p) {
+  auto* d = dynamic_cast<HipDevice*>(DeviceRegistry::instance().get(device_index));
+  if (!d || !p) return false;
+  std::lock_guard<std::mutex> g(d->zone_m);
+  return d->zone && d->zone->free(p);
+}
+
+// GPU -> PCI bus id -> /sys/bus/pci/devices/<id>/numa_node -> node cpulist
+// (reference bindthread.c:35-110 + parsec_hwloc.c distances; no hwloc here).
+static std::vector<int> parse_cpulist(const std::string& s) {
+  std::vector<int> v;
+  size_t i = 0;
+  while (i < s.size()) {
+    size_t j = s.find(',', i);
+    std::string part = s.substr(i, j == std::string::npos ? std::string::npos : j - i);
+    size_t dash = part.find('-');
+    try {
+      if (dash == std::string::npos) { if (!part.empty()) v.push_back(std::stoi(part)); }
+      else for (int c = std::stoi(part.substr(0, dash)); c <= std::stoi(part.substr(dash + 1)); ++c) v.push_back(c);
+    } catch (...) {}
+    if (j == std::string::npos) break;
+    i = j + 1;
+  }
+  return v;
+}
+
+int gpu_numa_node(int ordinal) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), ordinal) != hipSuccess) { (void)hipGetLastError(); return -1; }
+  std::string id(bus);
+  for (auto& ch : id) ch = (char)std::tolower((unsigned char)ch);
+  std::ifstream f("/sys/bus/pci/devices/" + id + "/numa_node");
+  int node = -1;
+  if (!(f >> node)) return -1;
+  return node;
+}
+
+int bind_thread_to_gpu_numa(int ordinal) {
+  const int node = gpu_numa_node(ordinal);
+  if (node < 0) return -1;
+  std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+  std::string list;
+  if (!std::getline(f, list)) return -1;
+  cpu_set_t cur, want;
+  CPU_ZERO(&cur);
+  CPU_ZERO(&want);
+  if (sched_getaffinity(0, sizeof(cur), &cur) != 0) return -1;
+  int n = 0;
+  for (int c : parse_cpulist(list))
+    if (c >= 0 && c < CPU_SETSIZE && CPU_ISSET(c, &cur)) { CPU_SET(c, &want); ++n; }
+  // keep at least a few CPUs: a cgroup share that barely meets the node would
+  // starve the worker + manager + comm threads
+  if (n < 4 || CPU_EQUAL(&cur, &want)) return -1;
+  if (sched_setaffinity(0, sizeof(want), &want) != 0) return -1;
+  PARSEC_DEBUG(kVerbInfo, "hip", "threads bound to NUMA node %d of GPU %d (%d cpus)", node, ordinal, n);
+  return node;
 }
 
 int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t bytes) {
@@ -194,7 +264,7 @@ void HipDevice::shutdown() {
         std::lock_guard<SpinLock> g(d->lock);
         data_copy_detach(d, c, device_index);
       }
-      if (zone) zone->free(c->device_private);
+      zone_free(c->device_private);
       delete static_cast<DevCopyState*>(c->dev_state);
       c->dev_state = nullptr;
       c->original = nullptr;
@@ -202,7 +272,10 @@ void HipDevice::shutdown() {
       if (d) data_release(d);
     }
   }
-  zone.reset();
+  {
+    std::lock_guard<std::mutex> g(zone_m);
+    zone.reset();
+  }
 }
 
 void HipDevice::quiesce() {
@@ -306,7 +379,7 @@ bool HipDevice::evict(size_t bytes) {
       data_copy_detach(d, c, device_index);
     }
     freed += d->nb_elts;
-    zone->free(c->device_private);
+    zone_free(c->device_private);
     c->device_private = nullptr;
     delete static_cast<DevCopyState*>(c->dev_state);
     c->dev_state = nullptr;
@@ -352,7 +425,7 @@ bool HipDevice::evict(size_t bytes) {
   return freed >= bytes;
 }
 
-void* HipDevice::cache_alloc(size_t bytes) {
+void HipDevice::ensure_zone() {
   if (!zone) {
     size_t freeb = 0, total = 0;
     (void)hipMemGetInfo(&freeb, &total);
@@ -363,9 +436,25 @@ void* HipDevice::cache_alloc(size_t bytes) {
     zone_max = maxb ? maxb : (size_t)(freeb * pct / 100.0);
     zone = std::make_unique<ZoneAllocator>(ordinal, zone_max, seg, unit);
   }
-  void* p = zone->alloc(bytes);
-  if (!p && evict(bytes)) p = zone->alloc(bytes);
+}
+
+void* HipDevice::cache_alloc(size_t bytes) {
+  void* p;
+  {
+    std::lock_guard<std::mutex> g(zone_m);
+    ensure_zone();
+    p = zone->alloc(bytes);
+  }
+  if (!p && evict(bytes)) {
+    std::lock_guard<std::mutex> g(zone_m);
+    p = zone->alloc(bytes);
+  }
   return p;
+}
+
+void HipDevice::zone_free(void* p) {
+  std::lock_guard<std::mutex> g(zone_m);
+  if (zone) zone->free(p);
 }
 
 // --------------------------------------------------------------- staging
@@ -404,7 +493,7 @@ int HipDevice::stage_in(GpuTask* g) {
           local = nc;
         }
       }
-      if (local != nc) { zone->free(p); delete static_cast<DevCopyState*>(nc->dev_state); delete nc; }
+      if (local != nc) { zone_free(p); delete static_cast<DevCopyState*>(nc->dev_state); delete nc; }
     }
     if (!local->dev_state) {
       // collection storage in HBM / comm receive buffers: never evicted
@@ -740,7 +829,13 @@ void hip_devices_init(Context* ctx) {
         if (hipDeviceEnablePeerAccess(b->ordinal, 0) != hipSuccess) (void)hipGetLastError();
       }
     }
-  if (!g_hip_devices.empty()) (void)hipSetDevice(g_hip_devices[0]->ordinal);
+  if (!g_hip_devices.empty()) {
+    (void)hipSetDevice(g_hip_devices[0]->ordinal);
+    // workers, GPU manager and comm threads are created after this point and
+    // inherit the calling thread's affinity
+    if (params.reg_int("runtime", "", "bind_gpu_numa", "Restrict runtime threads to the NUMA node of the (first) GPU", 1))
+      bind_thread_to_gpu_numa(g_hip_devices[0]->ordinal);
+  }
 }
 
 void hip_devices_start(Context* ctx) {

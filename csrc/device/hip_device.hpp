@@ -27,7 +27,7 @@ class ZoneAllocator {
   ZoneAllocator(int ordinal, size_t max_bytes, size_t segment_bytes, size_t unit);
   ~ZoneAllocator();
   void* alloc(size_t bytes);
-  void free(void* p);
+  bool free(void* p);  // false: not a live allocation of this zone
   size_t used() const { return used_; }
   size_t reserved() const { return reserved_; }
   size_t max_bytes() const { return max_bytes_; }
@@ -81,6 +81,7 @@ struct HipDevice : Device {
   hipStream_t s_h2d = nullptr, s_d2h = nullptr;
   std::vector<hipStream_t> s_exec;
   std::unique_ptr<ZoneAllocator> zone;
+  std::mutex zone_m;  // the comm thread allocates receive buffers from the zone too
   size_t zone_max = 0;
   // LRUs: clean copies (can be dropped) and owned copies (need write-back)
   List lru_clean, lru_owned;
@@ -133,6 +134,8 @@ struct HipDevice : Device {
   void complete(GpuTask* g);
   void epilog(GpuTask* g);
   void* cache_alloc(size_t bytes);
+  void ensure_zone();  // zone_m held
+  void zone_free(void* p);
   bool evict(size_t bytes);
   hipEvent_t get_event();
   void put_event(hipEvent_t e);

@@ -641,8 +641,16 @@ void DtdTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& ac
     }
     return;
   }
+  // keep the shadow alive past the unlock: a concurrent activation of another
+  // flow (or insert_task replaying parked ones) may complete it and drop the
+  // remote_tasks reference while this thread still installs data
+  t->refs.fetch_add(1, std::memory_order_acq_rel);
   lk.unlock();
-  // install received versions on the tiles the remote task wrote
+  // install received versions on the tiles the remote task wrote; local
+  // consumers then work on the tile's own copy (not the receive buffer), so a
+  // local task that is the tile's last writer leaves its result in the tile
+  DataCopy* inst[kMaxFlows];
+  for (int f = 0; f < kMaxFlows; ++f) inst[f] = act.data[f];
   for (auto& a : t->args) {
     if (a.flow < 0 || !a.tile || !(act.output_mask & (1u << a.flow)) || !act.data[a.flow]) continue;
     int op = a.op & OP_MASK;
@@ -658,6 +666,7 @@ void DtdTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& ac
       hc->version = d->newest_version() + 1;
       hc->coherency_state = COHERENCY_OWNED;
       d->owner_device = (int8_t)hc->device_index;
+      inst[a.flow] = hc;
     } else {
       // shadow Data: the received buffer becomes its current version
       std::lock_guard<SpinLock> g(d->lock);
@@ -675,16 +684,21 @@ void DtdTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& ac
       if (d->nb_elts == 0) d->nb_elts = n;
       data_copy_attach(d, nc, 0);
       d->owner_device = 0;
+      inst[a.flow] = nc;
     }
   }
   std::vector<Task*> ready;
   RemoteDepsMsg* msg = nullptr;
-  release_successors(es, t, act.output_mask, act.data, ready, msg);
+  release_successors(es, t, act.output_mask, inst, ready, msg);
   delete msg;  // remote shadows never forward
-  if (t->written && (t->activated & t->written) == t->written) {
-    if (remote_tasks.erase(t->seq)) task_unref(t);
+  bool all_written;
+  {
+    std::lock_guard<SpinLock> g(t->lock);
+    all_written = t->written && (t->activated & t->written) == t->written;
   }
+  if (all_written && remote_tasks.erase(t->seq)) task_unref(t);
   if (!ready.empty()) schedule_tasks(es, ready.data(), (int)ready.size(), 1);
+  task_unref(t);  // this activation's guard
 }
 
 // ============================================================ accessors

@@ -357,7 +357,9 @@ __global__ __launch_bounds__(256) void axpy2d_kernel(const Axpy2DArgs a) {
   for (int c = blockIdx.x; c < d.cols; c += gridDim.x) {
     const double* __restrict__ src = d.src + (size_t)c * d.lds;
     double* __restrict__ dst = d.dst + (size_t)c * d.ldd;
-    for (int r = threadIdx.x; r < d.rows; r += 256) dst[r] = (d.beta == 0.0 ? 0.0 : d.beta * dst[r]) + d.alpha * src[r];
+    // BLAS convention: a zero coefficient does not read its operand, so a 'zero'
+    // descriptor (alpha = beta = 0) clears NaN/Inf garbage of fresh workspaces
+    for (int r = threadIdx.x; r < d.rows; r += 256) dst[r] = (d.beta == 0.0 ? 0.0 : d.beta * dst[r]) + (d.alpha == 0.0 ? 0.0 : d.alpha * src[r]);
   }
 }
 

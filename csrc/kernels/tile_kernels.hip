@@ -573,7 +573,7 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
 #undef PARSEC_GEMM_LAUNCH
 }
 
-static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) {
+static void gemm_policy_init() {
   if (g_gemm_tile_policy < 0) {
     const char* e = getenv("PARSEC_GEMM_TILE");
     g_gemm_tile_policy = e ? atoi(e) : 0;
@@ -584,6 +584,18 @@ static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) 
     e = getenv("PARSEC_GEMM_BIG_TILES");
     if (e) g_gemm_big_tiles = atoi(e);
   }
+}
+
+// Tile-size policy of the grouped GEMM (0 = auto, 64, 128); returns the previous one.
+int gemm_tile_policy(int p) {
+  gemm_policy_init();
+  const int prev = g_gemm_tile_policy;
+  if (p >= 0) g_gemm_tile_policy = p;
+  return prev;
+}
+
+static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) {
+  gemm_policy_init();
   GemmBatchArgs a;
   a.count = n;
   int t128 = 0;
@@ -881,6 +893,7 @@ void* test_ws(size_t bytes) {
 }  // namespace
 
 extern "C" {
+int parsec_amd_gemm_tile_policy(int p) { return parsec::kern::gemm_tile_policy(p); }
 int parsec_amd_dgemm_batch(const parsec::GemmDesc* descs, int n, void* stream) {
   parsec::kern::launch_gemm_batch(descs, n, (hipStream_t)stream);
   return (int)hipGetLastError();

@@ -391,7 +391,20 @@ int PtgTaskClass::complete_execution(ExecutionStream* es, Task* t) const {
         DataCollection* dc = tg->dc(tp);
         int64_t idx[kMaxLocals];
         collection_index(tp, X, tg->args, idx);
-        if (dc->rank_of(idx, (int)tg->args.size()) == my) write_back(dc->data_of(idx, (int)tg->args.size()), data);
+        const uint32_t r = dc->rank_of(idx, (int)tg->args.size());
+        if (r == my) {
+          write_back(dc->data_of(idx, (int)tg->args.size()), data);
+        } else {
+          // final version of a tile owned by another rank (e.g. the R of a QR
+          // TS chain): ship it; the owner writes it back in on_remote_activation
+          if (!msg) {
+            msg = new RemoteDepsMsg();
+            msg->outputs.resize(def.flows.size());
+          }
+          auto& o = msg->outputs[f];
+          o.data = data;
+          if (std::find(o.ranks.begin(), o.ranks.end(), (int)r) == o.ranks.end()) o.ranks.push_back((int)r);
+        }
       }
     });
   }
@@ -474,6 +487,10 @@ void PtgTaskpool::finalize() {
     }
     tc->flags = d.flags;
     tc->flops_per_task = d.flops;
+    tc->writes_collections = false;
+    for (auto& fl : d.flows)
+      for (auto& dep : fl.out)
+        if (dep.then_t.kind == DEP_DATA || (dep.has_else && dep.else_t.kind == DEP_DATA)) tc->writes_collections = true;
     auto resolve = [&](DepTarget& t) {
       if (t.kind != DEP_TASK) return;
       PtgTaskClass* dst = nullptr;
@@ -536,6 +553,30 @@ void PtgTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
     });
   }
   if (dynamic_termdet) nb_local = (int64_t)ready.size();  // the rest is counted on first activation
+  // Final versions of local tiles written by tasks of OTHER ranks (e.g. R(k,k)
+  // at the end of a QR TS chain) arrive as remote activations that no local task
+  // waits for: count them as pending runtime actions so this rank does not
+  // terminate (and the user read the tile) before they landed.
+  if (ctx->nb_nodes > 1) {
+    int64_t expected = 0;
+    for (auto* tc : classes) {
+      if (!tc->writes_collections) continue;
+      for_each_task(this, tc, [&](const int32_t* L) {
+        if (tc->rank_of(this, L) == my) return;
+        for (size_t f = 0; f < tc->def.flows.size(); ++f) {
+          if (tc->def.flows[f].access == FLOW_CTL) continue;
+          for (const Dep& d : tc->def.flows[f].out) for_each_dep_instance(this, L, d, [&](const int32_t* X, const DepTarget* tg) {
+            if (tg->kind != DEP_DATA) return;
+            int64_t idx[kMaxLocals];
+            collection_index(this, X, tg->args, idx);
+            if (tg->dc(this)->rank_of(idx, (int)tg->args.size()) == my) ++expected;
+          });
+        }
+      });
+    }
+    remote_writebacks_expected = expected;
+    if (expected) tdm->taskpool_addto_runtime_actions(this, expected);
+  }
   // additive: remote activations may already have run (and completed) tasks
   tdm->taskpool_addto_nb_tasks(this, nb_local);
 }
@@ -600,7 +641,10 @@ void PtgTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& ac
         DataCollection* dc = tg->dc(this);
         int64_t idx[kMaxLocals];
         collection_index(this, X, tg->args, idx);
-        if (dc->rank_of(idx, (int)tg->args.size()) == my) write_back(dc->data_of(idx, (int)tg->args.size()), data);
+        if (dc->rank_of(idx, (int)tg->args.size()) == my) {
+          write_back(dc->data_of(idx, (int)tg->args.size()), data);
+          tdm->taskpool_addto_runtime_actions(this, -1);  // counted at startup
+        }
       }
     });
   }

@@ -139,6 +139,7 @@ class PtgTaskClass : public TaskClass {
   // Every active input instance of `flow` (one for data flows, all for CTL gathers).
   void for_each_input(const Taskpool* tp, int flow, const int32_t* L, const std::function<void(const int32_t* Lx, const DepTarget*)>& f) const;
   mutable std::atomic<bool> warned_null_forward{false};
+  bool writes_collections = false;  // some output dependency targets a data collection
   void reshape_inputs(Task* t) const;
 };
 
@@ -161,6 +162,7 @@ class PtgTaskpool : public Taskpool {
   // tasks (dense index arrays bring nothing on top of it here)
   std::string dep_management = "dynamic-hash-table";
   std::vector<std::string> global_names;
+  int64_t remote_writebacks_expected = 0;  // final tile versions other ranks send here
   bool finalized = false;
   PtgTaskpool();
   ~PtgTaskpool() override;

@@ -24,6 +24,7 @@ namespace py = pybind11;
 using namespace parsec;
 
 extern "C" int parsec_amd_dgemm_batch(const GemmDesc* descs, int n, void* stream);
+extern "C" int parsec_amd_gemm_tile_policy(int p);
 extern "C" int parsec_amd_dtrsm_batch(const TrsmDesc* descs, int n, void* stream);
 extern "C" int parsec_amd_dpotrf_tile(double* A, int n, int lda, int* info, void* stream);
 extern "C" int parsec_amd_dpotrf_tile_w(double* A, int n, int lda, int* info, double* W, int ldw, void* stream);
@@ -597,6 +598,7 @@ PYBIND11_MODULE(_C, m) {
     }
     return parsec_amd_dgemm_batch(v.data(), (int)v.size(), (void*)stream);
   });
+  m.def("kernel_gemm_tile_policy", [](int p) { return parsec_amd_gemm_tile_policy(p); });
   m.def("kernel_dtrsm", [](uintptr_t L, uintptr_t B, int mm, int nn, int ldl, int ldb, uintptr_t stream) {
     TrsmDesc t;
     t.L = (const double*)L; t.B = (double*)B; t.m = mm; t.n = nn; t.ldl = ldl; t.ldb = ldb; t.trans = 1;
@@ -644,5 +646,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("comm_barrier", []() { py::gil_scoped_release rel; return comm_barrier(); });
   m.def("comm_rank", &comm_rank);
   m.def("comm_size", &comm_size);
+  m.def("comm_device_plane", []() { return std::string(comm_device_plane_name()); });
   m.def("comm_allreduce_max", [](uint32_t v) { py::gil_scoped_release rel; return comm_allreduce_max_u32(v); });
 }

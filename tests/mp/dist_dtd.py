@@ -71,6 +71,22 @@ def main():
             pa.insert_task(tp, copy_from, [(T[0], pa.INPUT), (T[r], pa.INOUT | pa.AFFINITY), (100.0, pa.VALUE)])
         pa.insert_task(tp, setv(-5.0), [(T[0], pa.INOUT | pa.AFFINITY)])
         expect = -5.0 if rank == 0 else 101.0
+    elif case == "multiflow":
+        # a remote writer with two written flows (T0 and T1 on rank 1), read on
+        # rank 0 right away: both flows of the shadow are activated on rank 0
+        # while later insertions race with the arrivals (dtd.cpp)
+        def w2(task):
+            task.arg(0)[:] += 1
+            task.arg(1)[:] += 2
+            return 0
+
+        t0, t1 = 1.0, 2.0
+        for _ in range(12):
+            pa.insert_task(tp, w2, [(T[0], pa.INOUT), (T[1], pa.INOUT | pa.AFFINITY)])
+            pa.insert_task(tp, add_into, [(T[0], pa.INOUT | pa.AFFINITY), (T[1], pa.INPUT)])
+            t0, t1 = t0 + 1, t1 + 2
+            t0 += t1
+        expect = t0 if rank == 0 else (t1 if rank == 1 else rank + 1.0)
     else:
         raise SystemExit(f"unknown case {case}")
     tp.data_flush_all(A)

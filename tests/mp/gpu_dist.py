@@ -1,0 +1,160 @@
+"""Worker: one rank of a multi-process GPU run where every rank drives GPU 0 and
+remote tiles move through the device data plane (HIP IPC: the receiver maps the
+sender's HBM allocation and pulls with an async D2D copy). Used by
+tests/test_multirank_gpu.py; each rank validates what it owns.
+
+argv: case rank size job [case args...]
+  dpotrf N nb P Q        HBM-resident 2D block-cyclic Cholesky, local tiles vs torch
+  dgeqrf N nb P outdir   1D row-cyclic QR, writes this rank's tiles of R
+  stencil nx ny nz b iters   DTD 7-point stencil on GPU bodies, local blocks vs numpy
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+
+def _spd(N, torch, dev):
+    g = torch.Generator().manual_seed(2024)
+    R = torch.randn((N, N), dtype=torch.float64, generator=g).to(dev)
+    return R @ R.t() / N + torch.eye(N, dtype=torch.float64, device=dev)  # not diagonally dominant
+
+
+def _setup(pa, rank, size, job):
+    pa.mca_set("device_hip_mask", "1")
+    assert pa.comm_init(rank, size, job, 0) == 0
+    return pa.init(2)
+
+
+def case_dpotrf(pa, torch, rank, size, job, N, nb, P, Q):
+    ctx = _setup(pa, rank, size, job)
+    gpu = pa.first_gpu_device_index()
+    NT = (N + nb - 1) // nb
+    llm = sum(1 for g in range(NT) if g % P == rank // Q)
+    lln = sum(1 for g in range(NT) if g % Q == rank % Q)
+    store = torch.zeros((lln, llm, nb, nb), dtype=torch.float64, device="cuda")
+    A = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=Q, device=gpu, ptr=store.data_ptr())
+    S = _spd(N, torch, "cuda")
+    tiles = store.view(-1, nb, nb)
+    for n in range(NT):
+        for m in range(n, NT):
+            li = A.local_index(m, n)
+            if li >= 0:
+                tiles[li].copy_(S[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb].t())
+    torch.cuda.synchronize()
+    tp, info = pa.dpotrf_new(A, pa.MATRIX_LOWER)
+    ctx.add_taskpool(tp)
+    ctx.start()
+    ctx.wait()
+    Lref = torch.linalg.cholesky(S)
+    err = 0.0
+    for n in range(NT):
+        for m in range(n, NT):
+            li = A.local_index(m, n)
+            if li < 0:
+                continue
+            got, ref = tiles[li].t(), Lref[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb]
+            if m == n:
+                got, ref = torch.tril(got), torch.tril(ref)
+            err = max(err, float((got - ref).abs().max()))
+    stats = [d for d in pa.devices() if d["type"] == pa.DEV_HIP][0]
+    plane = pa.comm_device_plane()
+    ctx.fini()
+    pa.comm_fini()
+    err /= float(Lref.abs().max())
+    want = os.environ.get("EXPECT_PLANE")
+    if want and plane != want:
+        print(f"rank {rank}: device plane {plane}, expected {want}", flush=True)
+        return False
+    print(f"rank {rank} dpotrf err {err:.3e} info {pa.read_int(info)} gpu_tasks {stats['executed_tasks']} plane {plane}", flush=True)
+    return err < 1e-12 and pa.read_int(info) == 0 and stats["executed_tasks"] > 0
+
+
+def case_dgeqrf(pa, torch, rank, size, job, N, nb, P, outdir):
+    ctx = _setup(pa, rank, size, job)
+    gpu = pa.first_gpu_device_index()
+    NT = (N + nb - 1) // nb
+    lm = sum(1 for g in range(NT) if g % P == rank)
+    storeA = torch.zeros((NT, lm, nb, nb), dtype=torch.float64, device="cuda")
+    storeT = torch.zeros((NT, lm, nb, nb), dtype=torch.float64, device="cuda")
+    A = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=1, device=gpu, ptr=storeA.data_ptr())
+    T = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=1, device=gpu, ptr=storeT.data_ptr())
+    g = torch.Generator().manual_seed(77)
+    Afull = (torch.rand((N, N), dtype=torch.float64, generator=g) - 0.5).cuda()
+    tiles = storeA.view(-1, nb, nb)
+    for n in range(NT):
+        for m in range(NT):
+            li = A.local_index(m, n)
+            if li >= 0:
+                tiles[li].copy_(Afull[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb].t())
+    torch.cuda.synchronize()
+    tp = pa.dgeqrf_new(A, T, 32)
+    ctx.add_taskpool(tp)
+    ctx.start()
+    ctx.wait()
+    # this rank's tiles of R (upper triangle of the tiles with m <= n), zeros elsewhere
+    Rrows = torch.zeros((N, N), dtype=torch.float64, device="cuda")
+    for m in range(NT):
+        for n in range(m, NT):
+            li = A.local_index(m, n)
+            if li >= 0:
+                t = tiles[li].t()
+                Rrows[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb] = torch.triu(t) if m == n else t
+    part = Rrows.cpu().numpy()
+    ctx.fini()
+    pa.comm_fini()
+    np.save(os.path.join(outdir, f"R{rank}.npy"), part)
+    print(f"rank {rank} dgeqrf done", flush=True)
+    return True
+
+
+def case_stencil(pa, torch, rank, size, job, nx, ny, nz, b, iters):
+    ctx = _setup(pa, rank, size, job)
+    G = pa.StencilGrid(rank, size, nx, ny, nz, b, b, b, device=pa.first_gpu_device_index())
+    _, _, par = pa.stencil3d_run(ctx, G, iters, 0.4, 0.1, True)
+    f = lambda v, n: (v + 1) / (n + 1) * (1 - (v + 1) / (n + 1))  # noqa: E731
+    U = 64.0 * f(np.arange(nz), nz)[:, None, None] * f(np.arange(ny), ny)[None, :, None] * f(np.arange(nx), nx)[None, None, :]
+    for _ in range(iters):
+        Pd = np.pad(U, 1)
+        U = 0.4 * U + 0.1 * (Pd[1:-1, 1:-1, :-2] + Pd[1:-1, 1:-1, 2:] + Pd[1:-1, :-2, 1:-1] + Pd[1:-1, 2:, 1:-1] + Pd[:-2, 1:-1, 1:-1] + Pd[2:, 1:-1, 1:-1])
+    nbx, nby = (nx + b - 1) // b, (ny + b - 1) // b
+    err, mine = 0.0, 0
+    for blk in range(G.nblocks):
+        if G.block_rank(blk) != rank:
+            continue
+        mine += 1
+        ib, jb, kb = blk % nbx, (blk // nbx) % nby, blk // (nbx * nby)
+        got = G.block(blk, par)
+        ref = U[kb * b:kb * b + got.shape[0], jb * b:jb * b + got.shape[1], ib * b:ib * b + got.shape[2]]
+        err = max(err, float(np.abs(got - ref).max()))
+    ctx.fini()
+    pa.comm_fini()
+    print(f"rank {rank} stencil blocks {mine} err {err:.3e}", flush=True)
+    return err < 1e-12 and mine > 0
+
+
+def main():
+    case, rank, size, job = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    rest = sys.argv[5:]
+    import torch
+
+    torch.cuda.set_device(0)
+    import parsec_amd as pa
+
+    pa.require_native()
+    if case == "dpotrf":
+        ok = case_dpotrf(pa, torch, rank, size, job, *map(int, rest))
+    elif case == "dgeqrf":
+        ok = case_dgeqrf(pa, torch, rank, size, job, int(rest[0]), int(rest[1]), int(rest[2]), rest[3])
+    elif case == "stencil":
+        ok = case_stencil(pa, torch, rank, size, job, *map(int, rest))
+    else:
+        raise SystemExit(f"unknown case {case}")
+    sys.exit(0 if ok else 1)
+
+
+if __name__ == "__main__":
+    main()

@@ -22,6 +22,19 @@ def dtd_capi(tmp_path_factory, pa):
     return str(out)
 
 
+def test_checkpoint_user_storage_after_init(tmp_path, pa):
+    """data_write / data_read with dc.mat assigned after init (lazy pickup)."""
+    exe = tmp_path / "ckpt"
+    cmd = ["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-O1", f"-I{ROOT}/include", os.path.join(HERE, "capi", "checkpoint_capi.c"), "-o", str(exe),
+           f"-L{ROOT}/parsec_amd/lib", "-lparsec_amd", f"-Wl,-rpath,{ROOT}/parsec_amd/lib", "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(exe), str(tmp_path / "A.ckpt")], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok" in r.stdout
+
+
 def test_dtd_c_program(dtd_capi):
     r = subprocess.run([dtd_capi], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr

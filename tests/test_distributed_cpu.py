@@ -50,7 +50,7 @@ def test_distributed_other_schedulers(pa, sched):
         assert rc == 0, out
 
 
-@pytest.mark.parametrize("case", ["broadcast", "reduce", "allreduce", "pingpong", "war"])
+@pytest.mark.parametrize("case", ["broadcast", "reduce", "allreduce", "pingpong", "war", "multiflow"])
 @pytest.mark.parametrize("nranks", [2, 3])
 def test_distributed_dtd_patterns(pa, case, nranks):
     """Distributed DTD: one writer read on every rank, reduction into rank 0,
@@ -59,3 +59,31 @@ def test_distributed_dtd_patterns(pa, case, nranks):
     outs = run_ranks(nranks, case, worker=os.path.join(HERE, "mp", "dist_dtd.py"))
     for rc, out in outs:
         assert rc == 0, out
+
+
+def test_launcher_kills_survivors_on_failure():
+    """mpiexec semantics: one rank failing ends the whole job."""
+    import time
+
+    from parsec_amd import launch
+
+    prog = "import os, sys, time; r = int(os.environ['PARSEC_COMM_RANK']); sys.exit(3) if r == 1 else time.sleep(60)"
+    t0 = time.monotonic()
+    rc = launch.launch(3, [sys.executable, "-c", prog], timeout=50)
+    assert rc == 3
+    assert time.monotonic() - t0 < 20
+
+
+@pytest.mark.parametrize("nranks,P,Q,M,N", [(2, 2, 1, 96, 96), (3, 3, 1, 112, 80), (4, 2, 2, 96, 128)])
+def test_distributed_dgeqrf(pa, tmp_path, nranks, P, Q, M, N):
+    """QR over P x Q ranks: the TS chains write R(k,k) / A(k,n) from remote ranks,
+    so the final versions must travel back to the owning rank."""
+    import numpy as np
+
+    outs = run_ranks(nranks, M, N, 16, P, Q, str(tmp_path), worker=os.path.join(HERE, "mp", "dist_qr.py"))
+    for rc, out in outs:
+        assert rc == 0, out
+    R = sum(np.load(tmp_path / f"R{r}.npy") for r in range(nranks))
+    S = np.random.default_rng(5).standard_normal((M, N))
+    G = S.T @ S
+    assert np.linalg.norm(R.T @ R - G) / np.linalg.norm(G) < 1e-13

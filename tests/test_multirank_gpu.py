@@ -1,0 +1,93 @@
+"""Multi-rank runs of the distributed device data plane on one MI355X: 2, 4 and
+8 processes (one per "GPU" of a P x Q grid) all drive GPU 0, and every remote
+tile moves HBM -> HBM through HIP IPC (the receiver maps the sender's
+allocation and pulls it on a per-peer stream; IPC_DONE releases the source).
+Reference: collections/*:mp and dsl/* :mp tests run with mpiexec -n 2|4|8
+(tests/collections/Testings.cmake:5-6, remote_dep.c:454-591)."""
+import os
+import subprocess
+import sys
+import tempfile
+import uuid
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+WORKER = os.path.join(HERE, "mp", "gpu_dist.py")
+
+
+def _gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _run(case, nranks, *args, timeout=100, env_extra=None):
+    job = "g" + uuid.uuid4().hex[:10]
+    env = dict(os.environ, PYTHONUNBUFFERED="1", **(env_extra or {}))
+    procs = [subprocess.Popen([sys.executable, WORKER, case, str(r), str(nranks), job, *map(str, args)],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, start_new_session=True)
+             for r in range(nranks)]
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=timeout)
+            outs.append((p.returncode, out))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for rc, out in outs:
+        print(out.strip().splitlines()[-1] if out.strip() else "")
+    return outs
+
+
+@pytest.mark.parametrize("nranks,P,Q", [(2, 2, 1), (4, 2, 2), (8, 4, 2)])
+def test_dpotrf_multirank_ipc(pa, nranks, P, Q):
+    """N=8192, nb=512 Cholesky over P x Q ranks (the 8-rank grid is the one
+    bench.py uses on 8 GPUs), every rank checking its tiles of L."""
+    _gpu()
+    for rc, out in _run("dpotrf", nranks, 8192, 512, P, Q, env_extra={"EXPECT_PLANE": "ipc"}):
+        assert rc == 0, out
+
+
+def test_dpotrf_rccl_plane_request(pa):
+    """comm_device_plane=rccl with two ranks on ONE GPU: RCCL refuses two ranks of
+    a communicator on the same device, so the engine must report that and fall
+    back to the host-staged plane with a correct result (the RCCL plane is for
+    ranks on distinct GPUs; IPC is the default either way)."""
+    _gpu()
+    outs = _run("dpotrf", 2, 2048, 256, 2, 1, env_extra={"PARSEC_MCA_comm_device_plane": "rccl"})
+    for rc, out in outs:
+        assert rc == 0, out
+    planes = {o.strip().splitlines()[-1].split("plane")[-1].strip() for _, o in outs}
+    print("rccl request ->", planes)
+    assert planes <= {"rccl", "host"}
+
+
+def test_dgeqrf_two_ranks_ipc(pa):
+    """1D row-cyclic QR over 2 ranks: R assembled from both ranks satisfies R^T R = A^T A
+    (the R(k,k) of each TS chain is written back from the remote rank)."""
+    _gpu()
+    import torch
+
+    N, nb = 2048, 256
+    with tempfile.TemporaryDirectory() as d:
+        for rc, out in _run("dgeqrf", 2, N, nb, 2, d):
+            assert rc == 0, out
+        R = sum(np.load(os.path.join(d, f"R{r}.npy")) for r in range(2))
+    g = torch.Generator().manual_seed(77)
+    A = (torch.rand((N, N), dtype=torch.float64, generator=g) - 0.5).numpy()
+    AtA = A.T @ A
+    assert np.linalg.norm(R.T @ R - AtA) / np.linalg.norm(AtA) < 1e-12
+
+
+def test_stencil_four_ranks_ipc(pa):
+    """DTD 3D stencil over 4 ranks with GPU bodies: halo faces cross ranks
+    through the device plane."""
+    _gpu()
+    for rc, out in _run("stencil", 4, 48, 40, 36, 16, 6):
+        assert rc == 0, out
