@@ -224,7 +224,9 @@ def main():
                     t = (t + t.t()) * 0.5 + N * torch.eye(nb, dtype=torch.float64, device="cuda")
                 full[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb] = t
         S = torch.tril(full) + torch.tril(full, -1).t()
-        Lref = torch.linalg.cholesky(S)
+        # host LAPACK reference: the GPU library Cholesky returned wrong factors
+        # when several processes shared the GPU (--share-gpu validation runs)
+        Lref = torch.linalg.cholesky(S.cpu()).to(S.device)
         err = 0.0
         for n in range(NT):
             for m in range(n, NT):

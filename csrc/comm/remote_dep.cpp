@@ -25,6 +25,10 @@ static ShmEngine* g_ce = nullptr;
 static Context* g_ctx = nullptr;
 static ExecutionStream* g_comm_es = nullptr;
 static size_t g_short_limit = 1024;
+static bool g_recv_from_cache = true;
+static int g_recv_pool = 1;  // 0 free after use, 1 recycle by size, 2 never reuse (diagnostic)
+static int g_ipc_debug_sync = 0;  // 1: sender hipDeviceSynchronize before answering a GET (diagnostic)
+static int g_ipc_verify = 0;      // diagnostic: checksum every IPC payload at the sender and after the pull
 
 CommEngine* comm_engine() { return g_ce; }
 int comm_rank() { return g_ce ? g_ce->rank : 0; }
@@ -89,8 +93,17 @@ struct IpcMsg {
   uint32_t pad;
   uint64_t offset;
   uint64_t bytes;
+  uint64_t checksum;  // comm_ipc_verify: sender-side sum of the payload words
   char handle[64];
 };
+
+uint64_t debug_checksum(int dev, const void* p, size_t bytes) {
+  std::vector<uint64_t> h((bytes + 7) / 8, 0);
+  device_memcpy(0, h.data(), dev, p, bytes);
+  uint64_t s = 0;
+  for (size_t i = 0; i < h.size(); ++i) s = s * 1099511628211ull + h[i];
+  return s;
+}
 
 struct IpcDone {
   uint64_t send_id;
@@ -158,7 +171,11 @@ int g_gpu_index = -1;
 void recv_copy_release(DataCopy* c) {
   Data* d = c->original;
   if (c->device_index == 0) std::free(c->device_private);
-  else {
+  else if (g_recv_pool == 2) {
+    // diagnostic: quarantine (leak) the buffer
+  } else if (!g_recv_pool) {
+    if (!device_cache_free(c->device_index, c->device_private)) device_free(c->device_index, c->device_private);
+  } else {
     auto& p = dev_pool();
     std::lock_guard<std::mutex> g(p.m);
     p.free[d ? d->nb_elts : 0].push_back(c->device_private);
@@ -184,7 +201,7 @@ DataCopy* new_recv_copy(size_t bytes, bool device) {
     }
     // carved from the GPU's tile-cache zone (no hipMalloc / memset on the comm
     // thread); recycled by size through the pool, returned at remote_dep_fini
-    if (!p) p = device_cache_alloc(g_gpu_index, bytes);
+    if (!p && g_recv_from_cache) p = device_cache_alloc(g_gpu_index, bytes);
     if (!p) p = device_alloc(g_gpu_index, bytes);
     dev = p ? g_gpu_index : 0;
   }
@@ -370,7 +387,16 @@ void on_get(int src, int, const void* msg, size_t) {
       continue;
     }
     if (c->device_index != 0 && g_ce->ipc_ok()) {
+      if (g_ipc_debug_sync == 1) (void)hipDeviceSynchronize();
       IpcMsg m{};
+      if (g_ipc_verify) {
+        m.checksum = debug_checksum(c->device_index, c->device_private, bytes);
+        (void)hipDeviceSynchronize();
+        const uint64_t later = debug_checksum(c->device_index, c->device_private, bytes);
+        if (later != m.checksum)
+          warning("IPC verify: tile of send %llu flow %d (%llu bytes) changed after its producer completed (%016llx -> %016llx)", (unsigned long long)g.send_id, f,
+                  (unsigned long long)bytes, (unsigned long long)m.checksum, (unsigned long long)later);
+      }
       m.recv_id = g.recv_id;
       m.send_id = g.send_id;
       m.flow = (uint32_t)f;
@@ -415,7 +441,17 @@ void on_data_ipc(int src, int, const void* msg, size_t) {
   const uint64_t rid = m.recv_id, sid = m.send_id;
   const uint32_t f = m.flow;
   const uint64_t bytes = m.bytes;
-  g_ce->ipc_copy(src, c->device_private, base + m.offset, bytes, [rid, sid, f, src, bytes] {
+  const uint64_t want = m.checksum;
+  const char* srcp = base + m.offset;
+  g_ce->ipc_copy(src, c->device_private, srcp, bytes, [rid, sid, f, src, bytes, want, c, srcp] {
+    if (g_ipc_verify) {
+      uint64_t got = debug_checksum(c->device_index, c->device_private, bytes);
+      if (got != want) {
+        uint64_t again = debug_checksum(c->device_index, srcp, bytes);
+        warning("IPC verify: flow %u from rank %d (%llu bytes): pulled %016llx, sender had %016llx, source now %016llx", f, src, (unsigned long long)bytes,
+                (unsigned long long)got, (unsigned long long)want, (unsigned long long)again);
+      }
+    }
     IpcDone d{sid, f, 0};
     g_ce->send_am(TAG_IPC_DONE, src, &d, sizeof(d));
     RecvState* rs = nullptr;
@@ -582,6 +618,10 @@ void comm_fini() {
 
 void remote_dep_init(Context* ctx) {
   g_short_limit = ParamRegistry::instance().reg_sizet("runtime", "comm", "short_limit", "Eager payload limit (bytes) for host data in activations", 1024);
+  g_recv_pool = (int)ParamRegistry::instance().reg_int("comm", "", "recv_pool", "Device receive buffers: 1 recycle by size, 0 free after use, 2 never reuse (diagnostic)", 1);
+  g_ipc_debug_sync = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_debug_sync", "Diagnostic: device-synchronize before exporting a tile to a peer", 0);
+  g_ipc_verify = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_verify", "Diagnostic: checksum IPC payloads at the sender and after the pull", 0);
+  g_recv_from_cache = ParamRegistry::instance().reg_int("comm", "", "recv_from_cache", "Carve device receive buffers from the GPU tile-cache zone (1) or hipMalloc them (0)", 1) != 0;
   ctx->my_rank = comm_rank();
   ctx->nb_nodes = comm_size();
   set_debug_rank(ctx->my_rank);

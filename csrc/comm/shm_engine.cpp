@@ -455,7 +455,14 @@ int ShmEngine::ipc_copy(int src_rank, void* dst, const void* src, size_t bytes, 
   hipEvent_t ev;
   if (!ev_pool_.empty()) { ev = ev_pool_.back(); ev_pool_.pop_back(); }
   else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1;
-  PARSEC_HIP_CHECK_COMM(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st));
+  static const int mode = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_copy_mode", "Peer pull: 0 = hipMemcpyAsync, 1 = copy kernel", 0);
+  static const int dbg = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_debug_sync", "Diagnostic: device-synchronize before exporting a tile to a peer", 0);
+  if (mode == 1) {
+    if (device_copy_kernel(dst, src, bytes, st) != 0) fatal("IPC copy kernel launch failed");
+  } else {
+    PARSEC_HIP_CHECK_COMM(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st));
+  }
+  if (dbg == 2) (void)hipStreamSynchronize(st);
   (void)hipEventRecord(ev, st);
   ipc_q_[src_rank].push_back(Xfer{ev, std::move(done)});
   return 0;

@@ -147,7 +147,11 @@ Context* context_init(int nb_cores, std::vector<std::string>& args) {
   ctx->keep_highest_priority_task = reg.reg_int("runtime", "", "keep_highest_priority_task", "Keep the highest priority ready task on the releasing thread", 1) != 0;
   ctx->paranoid = reg.reg_int("debug", "", "paranoid", "Check task lifecycle invariants (scheduled twice, completed twice, scheduled after release, PTG dependency underflow)", 0) != 0;
   g_paranoid = ctx->paranoid;
-  ctx->manager_inline_gpu = reg.reg_int("device", "", "manager_inline_dispatch", "GPU managers prepare and submit successors whose first chore is a GPU chore (no hop through a compute thread)", 1) != 0;
+  {
+    int im = (int)reg.reg_int("device", "", "manager_inline_dispatch", "GPU managers (and the comm thread) prepare and submit successors whose first chore is a GPU chore: 0 off, 1 managers + comm, 2 managers only, 3 comm only", 1);
+    ctx->manager_inline_gpu = im != 0;
+    ctx->manager_inline_mode = im;
+  }
   std::string bcast = reg.reg_string("runtime", "comm", "coll_bcast", "Broadcast topology for remote activations: star|chain|binomial", "star");
   ctx->comm_bcast_topology = bcast == "chain" ? 1 : bcast == "binomial" ? 2 : 0;
   ctx->default_termdet = reg.reg_string("termdet", "", "default", "Default termination detection module", "local");

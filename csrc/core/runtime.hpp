@@ -519,6 +519,7 @@ struct Context {
   bool keep_highest_priority_task = true;
   bool paranoid = false;      // debug_paranoid: task lifecycle invariants (double schedule / completion, use after release)
   bool manager_inline_gpu = true;  // GPU managers dispatch GPU-bound successors themselves
+  int manager_inline_mode = 1;     // 1 managers + comm thread, 2 GPU managers only, 3 comm thread only
   int comm_bcast_topology = 0;  // 0 star, 1 chain, 2 binomial
   std::vector<int> core_bindings;
   std::string grapher_file;     // DOT output

@@ -121,7 +121,9 @@ int schedule_tasks(ExecutionStream* es, Task** tasks, int n, int32_t distance) {
     es = my_execution_stream();
     if (!es) es = tasks[0]->taskpool->context->all_es[0];
   }
-  if (es->is_manager && es->ctx->manager_inline_gpu && !es->ctx->simulation) {
+  const int im = es->ctx->manager_inline_mode;  // 1 all, 2 GPU managers only, 3 comm thread only
+  const bool is_comm = es->th_id == 2000;
+  if (es->is_manager && es->ctx->manager_inline_gpu && !es->ctx->simulation && (im == 1 || (im == 2 && !is_comm) || (im == 3 && is_comm))) {
     // A GPU manager releasing successors whose first usable chore is a GPU chore
     // prepares and submits them itself: the task reaches a device queue without
     // a round trip through a compute thread's scheduler queue.

@@ -38,6 +38,8 @@ bool device_cache_free(int device_index, void* p);
 // the NUMA node closest to HIP device `ordinal` (intersected with the current
 // affinity). Returns the node, or -1 when unknown / nothing to do.
 int bind_thread_to_gpu_numa(int ordinal);
+// dst <- src (bytes) as a copy kernel on `stream` (hipStream_t); 0 on success.
+int device_copy_kernel(void* dst, const void* src, size_t bytes, void* stream);
 int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t bytes);
 int device_hip_ordinal(int device_index);  // -1 if not a HIP device
 int first_gpu_device_index();

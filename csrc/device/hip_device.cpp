@@ -615,10 +615,17 @@ void HipDevice::execute_ready() {
   ready.swap(again);
   for (int s = 0; s < (int)round_tasks.size(); ++s) {
     if (round_tasks[s].empty()) continue;
+    const size_t ng = batches[s].gemm.size(), nw = batches[s].trsm_w.size(), np = batches[s].potrf.size();
     if (!batches[s].empty()) {
       launch_kernel_batch(batches[s], s_exec[s], ordinal, workspace(s, kernel_batch_workspace_bytes(batches[s]) + 64));
       stats.kernel_launches.fetch_add(1, std::memory_order_relaxed);
       batches[s].clear();
+    }
+    if (trace_launches) {
+      std::string line = "[engine] stream " + std::to_string(s) + ":";
+      for (GpuTask* g : round_tasks[s]) line += " " + g->task->task_class->describe(g->task);
+      line += " | gemm " + std::to_string(ng) + " trsm_w " + std::to_string(nw) + " potrf " + std::to_string(np);
+      std::fprintf(stderr, "%s\n", line.c_str());
     }
     ExecGroup grp;
     grp.ev = get_event();
@@ -791,6 +798,7 @@ void hip_devices_init(Context* ctx) {
   int crit = (int)params.reg_int("device", "hip", "critical_threshold", "Task priority at or above which the CU-reserved critical stream is used", 1 << 29);
   int rcus = (int)params.reg_int("device", "hip", "reserved_cus", "CUs reserved for the critical-path stream (0 = no CU masking; measured slower on MI355X)", 0);
   int xcrit = (int)params.reg_int("device", "hip", "critical_streams", "Additional critical-path streams used when the critical stream is busy", 7);
+  const bool trace = params.reg_int("device", "hip", "trace_launches", "Print every launched kernel group (stream, tasks, batch sizes) to stderr", 0) != 0;
   int maxg = (int)params.reg_int("device", "hip", "max_inflight_batches", "Launched kernel groups per bulk stream before new bulk tasks wait for a larger batch (0 = no limit)", 2);
   if (enabled == 0) return;
   int count = 0;
@@ -816,6 +824,7 @@ void hip_devices_init(Context* ctx) {
     d->max_inflight_groups = maxg;
     d->extra_crit_streams = std::max(0, xcrit);
     d->sort_pending = sortp != 0;
+    d->trace_launches = trace;
     reg.add(d);
     g_hip_devices.push_back(d);
   }

@@ -110,6 +110,7 @@ struct HipDevice : Device {
   bool cu_masked = false;
   bool batching = true;
   bool sort_pending = true;
+  bool trace_launches = false;
   uint32_t rr_stream = 0;
   int extra_crit_streams = 7;   // additional critical streams (see start())
   int max_inflight_groups = 2;  // bulk streams: launched groups in flight before new bulk work waits (0 = no limit)

@@ -873,6 +873,29 @@ void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal,
   for (auto& g : b.generic) g(stream);
 }
 
+// Device-to-device byte copy as a kernel (16-byte vectors, grid-stride): used for
+// pulls from peer-process (IPC) allocations so the copy is an ordinary kernel in
+// stream order on this process's queue.
+__global__ __launch_bounds__(256) void copy_bytes_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n16) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
+__global__ void copy_tail_kernel(char* __restrict__ dst, const char* __restrict__ src, size_t n) {
+  for (size_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
+int device_copy_kernel(void* dst, const void* src, size_t bytes, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const bool aligned = ((uintptr_t)dst % 16 == 0) && ((uintptr_t)src % 16 == 0);
+  size_t n16 = aligned ? bytes / 16 : 0;
+  if (n16) {
+    const unsigned blocks = (unsigned)std::min<size_t>(1024, (n16 + 255) / 256);
+    hipLaunchKernelGGL(copy_bytes_kernel, dim3(blocks), dim3(256), 0, s, static_cast<uint4*>(dst), static_cast<const uint4*>(src), n16);
+  }
+  const size_t done = n16 * 16;
+  if (bytes > done) hipLaunchKernelGGL(copy_tail_kernel, dim3(1), dim3(256), 0, s, static_cast<char*>(dst) + done, static_cast<const char*>(src) + done, bytes - done);
+  return (int)hipGetLastError();
+}
+
 }  // namespace parsec
 
 // ------------------------------------------------- C entry points (tests/bench)

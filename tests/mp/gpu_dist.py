@@ -39,38 +39,58 @@ def case_dpotrf(pa, torch, rank, size, job, N, nb, P, Q):
     A = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=Q, device=gpu, ptr=store.data_ptr())
     S = _spd(N, torch, "cuda")
     tiles = store.view(-1, nb, nb)
-    for n in range(NT):
-        for m in range(n, NT):
-            li = A.local_index(m, n)
-            if li >= 0:
-                tiles[li].copy_(S[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb].t())
-    torch.cuda.synchronize()
-    tp, info = pa.dpotrf_new(A, pa.MATRIX_LOWER)
-    ctx.add_taskpool(tp)
-    ctx.start()
-    ctx.wait()
-    Lref = torch.linalg.cholesky(S)
-    err = 0.0
-    for n in range(NT):
-        for m in range(n, NT):
-            li = A.local_index(m, n)
-            if li < 0:
-                continue
-            got, ref = tiles[li].t(), Lref[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb]
-            if m == n:
-                got, ref = torch.tril(got), torch.tril(ref)
-            err = max(err, float((got - ref).abs().max()))
+    # reference factor on the host (LAPACK): the GPU library Cholesky is not used
+    # as the oracle (it was observed to return a wrong factor when several
+    # processes share the GPU)
+    Lref = torch.linalg.cholesky(S.cpu()).to(S.device)
+    if os.environ.get("CHECK_TORCH_GPU"):
+        Lg = torch.linalg.cholesky(S)
+        print(f"rank {rank} torch GPU cholesky vs host: {float((Lg - Lref).abs().max()):.3e}", flush=True)
+    repeat = int(os.environ.get("REPEAT", "1"))
+    worst, nbad, info_v = 0.0, 0, 0
+    for rep in range(repeat):
+        for n in range(NT):
+            for m in range(n, NT):
+                li = A.local_index(m, n)
+                if li >= 0:
+                    tiles[li].copy_(S[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb].t())
+        torch.cuda.synchronize()
+        if size > 1:
+            pa.comm_barrier()
+        tp, info = pa.dpotrf_new(A, pa.MATRIX_LOWER)
+        ctx.add_taskpool(tp)
+        ctx.start()
+        ctx.wait()
+        info_v = info_v or pa.read_int(info)
+        err = 0.0
+        bad = []
+        for n in range(NT):
+            for m in range(n, NT):
+                li = A.local_index(m, n)
+                if li < 0:
+                    continue
+                got, ref = tiles[li].t(), Lref[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb]
+                if m == n:
+                    got, ref = torch.tril(got), torch.tril(ref)
+                e = float((got - ref).abs().max())
+                if e > 1e-10:
+                    bad.append((m, n, f"{e:.1e}"))
+                err = max(err, e)
+        if bad:
+            nbad += 1
+            print(f"rank {rank} rep {rep} bad tiles {bad[:12]} ({len(bad)} total)", flush=True)
+        worst = max(worst, err)
     stats = [d for d in pa.devices() if d["type"] == pa.DEV_HIP][0]
     plane = pa.comm_device_plane()
     ctx.fini()
     pa.comm_fini()
-    err /= float(Lref.abs().max())
+    worst /= float(Lref.abs().max())
     want = os.environ.get("EXPECT_PLANE")
     if want and plane != want:
         print(f"rank {rank}: device plane {plane}, expected {want}", flush=True)
         return False
-    print(f"rank {rank} dpotrf err {err:.3e} info {pa.read_int(info)} gpu_tasks {stats['executed_tasks']} plane {plane}", flush=True)
-    return err < 1e-12 and pa.read_int(info) == 0 and stats["executed_tasks"] > 0
+    print(f"rank {rank} dpotrf err {worst:.3e} info {info_v} gpu_tasks {stats['executed_tasks']} plane {plane} bad_reps {nbad}/{repeat}", flush=True)
+    return worst < 1e-12 and info_v == 0 and stats["executed_tasks"] > 0
 
 
 def case_dgeqrf(pa, torch, rank, size, job, N, nb, P, outdir):

@@ -127,7 +127,7 @@ def test_dpotrf_illconditioned_nb1024(pa, trsm_inverse):
         assert pa.read_int(info) == 0
         L = torch.tril(store.permute(1, 3, 0, 2).reshape(N, N))
         backward = (torch.linalg.norm(L @ L.t() - S) / torch.linalg.norm(S)).item()
-        Lref = torch.linalg.cholesky(S)
+        Lref = torch.linalg.cholesky(S.cpu()).to(dev)  # host LAPACK oracle
         backward_ref = (torch.linalg.norm(Lref @ Lref.t() - S) / torch.linalg.norm(S)).item()
         forward = (torch.linalg.norm(L - Lref) / torch.linalg.norm(Lref)).item()
         print(f"trsm_inverse={trsm_inverse} backward={backward:.3e} (torch {backward_ref:.3e}) forward-vs-torch={forward:.3e}")

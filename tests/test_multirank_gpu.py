@@ -3,7 +3,13 @@
 tile moves HBM -> HBM through HIP IPC (the receiver maps the sender's
 allocation and pulls it on a per-peer stream; IPC_DONE releases the source).
 Reference: collections/*:mp and dsl/* :mp tests run with mpiexec -n 2|4|8
-(tests/collections/Testings.cmake:5-6, remote_dep.c:454-591)."""
+(tests/collections/Testings.cmake:5-6, remote_dep.c:454-591).
+
+Oracle note: every rank checks its tiles against a HOST (LAPACK) Cholesky.
+torch.linalg.cholesky on the GPU was measured to return factors off by ~2e-3 in
+about half of the processes when 2-4 processes share one MI355X
+(scripts/gpu_r2_diag.sh history, profiles/r2_multirank_oracle.log); the
+runtime's own factor matched the host reference to 1e-15 in all of them."""
 import os
 import subprocess
 import sys
@@ -63,7 +69,7 @@ def test_dpotrf_rccl_plane_request(pa):
     outs = _run("dpotrf", 2, 2048, 256, 2, 1, env_extra={"PARSEC_MCA_comm_device_plane": "rccl"})
     for rc, out in outs:
         assert rc == 0, out
-    planes = {o.strip().splitlines()[-1].split("plane")[-1].strip() for _, o in outs}
+    planes = {o.strip().splitlines()[-1].split(" plane ")[-1].split()[0] for _, o in outs}
     print("rccl request ->", planes)
     assert planes <= {"rccl", "host"}
 
