@@ -62,13 +62,11 @@ StencilGrid::~StencilGrid() {
   for (Data*& d : data)
     if (d) {
       DataCopy* c = d->copy(storage_device);
-      if (c && c->device_private) {
-        if (storage_device == 0) std::free(c->device_private);
-        else device_free(storage_device, c->device_private);
-      }
+      if (c && c->device_private && storage_device == 0) std::free(c->device_private);
       data_destroy(d);
       d = nullptr;
     }
+  if (slab) device_free(storage_device, slab);
 }
 
 void StencilGrid::block_dims(int64_t b, int* ex, int* ey, int* ez) const {
@@ -122,8 +120,26 @@ Data* StencilGrid::data_of_key(uint64_t k) {
     if (posix_memalign(&p, 256, std::max<size_t>(bytes, 64))) fatal("stencil: out of host memory");
     std::memset(p, 0, bytes);
   } else {
-    p = device_alloc(storage_device, std::max<size_t>(bytes, 64));
-    if (!p) fatal("stencil: out of device memory");
+    // every local block and face lives in ONE device allocation: fewer
+    // allocations, and a peer can map it through HIP IPC (small hipMallocs are
+    // sub-allocated from shared buffer objects and cannot be exported)
+    if (!slab) {
+      slab_off.assign(data.size(), -1);
+      size_t total = 0;
+      for (uint64_t kk = 0; kk < data.size(); ++kk) {
+        if (rank_of_key(kk) != myrank) continue;
+        int kind, pp, dd;
+        int64_t bb;
+        decode(kk, &kind, &pp, &bb, &dd);
+        if (kind == 0 ? dd != 0 : (dd >= 6 || neighbor(bb, dd) < 0)) continue;  // unused keys / no face on a grid boundary
+        slab_off[kk] = (int64_t)total;
+        total += (data_size_of_key(kk) + 255) / 256 * 256;
+      }
+      slab = device_alloc(storage_device, std::max<size_t>(total, 256));
+      if (!slab) fatal("stencil: out of device memory (%zu bytes)", total);
+    }
+    if (slab_off[k] < 0) fatal("stencil: key %llu has no slab slot", (unsigned long long)k);
+    p = static_cast<char*>(slab) + slab_off[k];
   }
   Data* nd = data_create(nullptr, this, k, p, bytes, DATA_FLAG_PARSEC_MANAGED, storage_device);
   __atomic_store_n(&data[k], nd, __ATOMIC_RELEASE);

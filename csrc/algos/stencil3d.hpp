@@ -16,6 +16,8 @@ struct StencilGrid : DataCollection {
   int64_t nbx = 0, nby = 0, nbz = 0, nblocks = 0, per_rank = 0;
   int storage_device = 0;
   std::vector<Data*> data;
+  void* slab = nullptr;              // device storage: every local buffer, carved (IPC-exportable)
+  std::vector<int64_t> slab_off;     // key -> byte offset in slab (-1: not local / unused)
   SpinLock lock;
   ~StencilGrid() override;
   void init(int myrank, int nodes, int64_t nx, int64_t ny, int64_t nz, int bx, int by, int bz, int device);

@@ -419,6 +419,10 @@ int ShmEngine::ipc_export(const void* ptr, void* handle64, uint64_t* offset) {
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
   if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess || !base) return -1;
+  // small hipMallocs are sub-allocated from shared buffer objects that a peer
+  // cannot map at the right offset: such tiles travel through host fragments
+  static const size_t min_bytes = ParamRegistry::instance().reg_sizet("comm", "", "ipc_min_alloc", "Smallest device allocation exported through HIP IPC (smaller ones are host-staged)", (size_t)2 << 20);
+  if (size < min_bytes) return -3;
   auto key = std::make_pair((uintptr_t)base, size);
   auto it = ipc_exported_.find(key);
   if (it == ipc_exported_.end()) {

@@ -6,6 +6,9 @@
 // Design: the calling thread is compute thread 0; the others are std::threads
 // that sleep on a condition variable between epochs. Steal order is derived from
 // the Linux /sys topology (package + NUMA node) instead of hwloc.
+#include <execinfo.h>
+#include <csignal>
+#include <unistd.h>
 #include <pthread.h>
 #include <sched.h>
 #include <unistd.h>
@@ -133,7 +136,28 @@ static void thread_main(Context* ctx, ExecutionStream* es) {
   profiling_thread_fini(es);
 }
 
+// Fatal-signal handler (reference debug_backtrace_* MCA params, utils/debug.c):
+// print the faulting rank and a native backtrace, then re-raise.
+static void fatal_signal_handler(int sig) {
+  char head[96];
+  int n = std::snprintf(head, sizeof(head), "[parsec %d] fatal signal %d, backtrace:\n", debug_rank(), sig);
+  if (n > 0) (void)!write(2, head, (size_t)n);
+  void* frames[64];
+  int k = backtrace(frames, 64);
+  backtrace_symbols_fd(frames, k, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+static void install_fatal_handlers() {
+  static std::atomic<bool> done{false};
+  if (done.exchange(true)) return;
+  if (!ParamRegistry::instance().reg_int("debug", "", "backtrace_on_fatal", "Print a native backtrace on SIGSEGV / SIGBUS / SIGABRT / SIGFPE", 1)) return;
+  for (int s : {SIGSEGV, SIGBUS, SIGFPE, SIGABRT}) signal(s, fatal_signal_handler);
+}
+
 Context* context_init(int nb_cores, std::vector<std::string>& args) {
+  install_fatal_handlers();
   auto& reg = ParamRegistry::instance();
   args = reg.parse_cmdline(args);
   output_init();

@@ -80,7 +80,10 @@ struct GpuExecContext;
 // ===================================================================== data
 enum Coherency : uint8_t { COHERENCY_INVALID = 0, COHERENCY_OWNED = 1, COHERENCY_EXCLUSIVE = 2, COHERENCY_SHARED = 4 };
 enum TransferStatus : uint8_t { TRANSFER_NOT = 0, TRANSFER_UNDER = 1, TRANSFER_COMPLETE = 2 };
-enum DataFlags : uint8_t { DATA_FLAG_ARENA = 0x1, DATA_FLAG_TRANSIT = 0x2, DATA_FLAG_PARSEC_MANAGED = 0x4, DATA_FLAG_PARSEC_OWNED = 0x8 };
+enum DataFlags : uint8_t {
+  DATA_FLAG_ARENA = 0x1, DATA_FLAG_TRANSIT = 0x2, DATA_FLAG_PARSEC_MANAGED = 0x4, DATA_FLAG_PARSEC_OWNED = 0x8,
+  DATA_FLAG_DEVICE_CACHE = 0x10,  // a device engine's cache copy: the engine owns its lifetime (LRU, eviction)
+};
 
 // Datatype: a typed, possibly strided layout. Replaces MPI datatypes of the
 // reference (datatype.h:14-130): contiguous, vector (count x blocklen, stride),

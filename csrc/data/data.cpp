@@ -168,12 +168,22 @@ void data_release(Data* d) {
 void data_destroy(Data* d) {
   if (!d) return;
   for (int i = 0; i < kMaxDevices; ++i) {
-    DataCopy* c = d->device_copies[i].exchange(nullptr);
+    DataCopy* c;
+    {
+      std::lock_guard<SpinLock> g(d->lock);
+      c = d->device_copies[i].exchange(nullptr);
+    }
     while (c) {
       DataCopy* older = c->older;
-      c->original = nullptr;
       c->older = nullptr;
-      data_copy_release(c);
+      if (c->flags & DATA_FLAG_DEVICE_CACHE) {
+        // orphan it: the device engine still lists it (LRU) and frees it on
+        // eviction / shutdown; releasing it here left a dangling LRU entry
+        __atomic_store_n(&c->original, (Data*)nullptr, __ATOMIC_RELEASE);
+      } else {
+        c->original = nullptr;
+        data_copy_release(c);
+      }
       c = older;
     }
   }

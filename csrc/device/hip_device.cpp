@@ -259,17 +259,19 @@ void HipDevice::shutdown() {
   for (List* l : {&lru_clean, &lru_owned}) {
     while (ListItem* it = l->pop_front()) {
       DataCopy* c = static_cast<DataCopy*>(it);
-      Data* d = c->original;
+      Data* d = __atomic_load_n(&c->original, __ATOMIC_ACQUIRE);  // null: orphaned by data_destroy
+      auto* st = static_cast<DevCopyState*>(c->dev_state);
       if (d) {
         std::lock_guard<SpinLock> g(d->lock);
         data_copy_detach(d, c, device_index);
       }
       zone_free(c->device_private);
-      delete static_cast<DevCopyState*>(c->dev_state);
+      Data* keep = st ? st->retained : nullptr;
+      delete st;
       c->dev_state = nullptr;
       c->original = nullptr;
       data_copy_release(c);
-      if (d) data_release(d);
+      if (keep) data_release(keep);
     }
   }
   {
@@ -371,21 +373,28 @@ void HipDevice::lru_touch(DataCopy* c) {
 bool HipDevice::evict(size_t bytes) {
   size_t freed = 0;
   auto drop = [&](DataCopy* c) -> bool {
-    Data* d = c->original;
-    if (!d) return false;
-    {
+    Data* d = __atomic_load_n(&c->original, __ATOMIC_ACQUIRE);
+    auto* st = static_cast<DevCopyState*>(c->dev_state);
+    size_t bytes = 0;
+    if (d) {
       std::lock_guard<SpinLock> g(d->lock);
       if (c->readers.load() > 0 || c->refcount.load() > 1) return false;
       data_copy_detach(d, c, device_index);
+      bytes = d->nb_elts;
+    } else {
+      // orphaned by data_destroy: nobody can reach it any more
+      if (c->readers.load() > 0 || c->refcount.load() > 1) return false;
+      bytes = st && st->retained ? st->retained->nb_elts : 0;
     }
-    freed += d->nb_elts;
+    freed += bytes;
     zone_free(c->device_private);
     c->device_private = nullptr;
-    delete static_cast<DevCopyState*>(c->dev_state);
+    Data* keep = st ? st->retained : nullptr;
+    delete st;
     c->dev_state = nullptr;
     c->original = nullptr;
     data_copy_release(c);
-    data_release(d);
+    if (keep) data_release(keep);
     stats.data_faults.fetch_add(1, std::memory_order_relaxed);
     return true;
   };
@@ -480,16 +489,18 @@ int HipDevice::stage_in(GpuTask* g) {
       if (!p) return -1;
       auto* nc = new DataCopy();
       nc->device_private = p;
-      nc->flags = DATA_FLAG_PARSEC_OWNED;
+      nc->flags = DATA_FLAG_PARSEC_OWNED | DATA_FLAG_DEVICE_CACHE;
       nc->coherency_state = COHERENCY_INVALID;
       nc->dtt = c->dtt;
-      nc->dev_state = new DevCopyState();
+      auto* nst = new DevCopyState();
+      nc->dev_state = nst;
       {
         std::lock_guard<SpinLock> lk(d->lock);
         local = d->copy(device_index);
         if (!local) {
           data_copy_attach(d, nc, device_index);
           data_retain(d);  // an engine-managed copy keeps its Data alive (NEW / arena data may lose its host copy first)
+          nst->retained = d;
           local = nc;
         }
       }

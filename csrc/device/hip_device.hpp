@@ -66,6 +66,7 @@ struct DevCopyState {  // DataCopy::dev_state for engine-managed copies
   bool in_lru = false;
   bool owned_lru = false;
   bool cache_managed = true;  // allocated from the zone (evictable)
+  Data* retained = nullptr;   // the Data this cache copy keeps alive (released when the copy is dropped)
 };
 
 struct ExecGroup {

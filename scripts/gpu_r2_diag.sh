@@ -1,11 +1,26 @@
 #!/bin/bash
-# 4 independent single-rank DPOTRF processes on one GPU; host LAPACK reference, torch GPU cholesky compared too
+# 2-rank GPU DGEQRF (1D row-cyclic), repeated, IPC vs host plane
 set -o pipefail
-mkdir -p gpurun_out
+mkdir -p gpurun_out/qr
 export PYTHONUNBUFFERED=1
-for r in 0 1 2 3; do env REPEAT=3 CHECK_TORCH_GPU=1 timeout -k 5 150 python tests/mp/gpu_dist.py dpotrf 0 1 tr_${r}_$$ 8192 512 1 1 > gpurun_out/tr_$r.log 2>&1 & done
-wait
-for r in 0 1 2 3; do echo "== $r"; grep -h "bad_reps\|bad tiles\|torch GPU" gpurun_out/tr_$r.log | cut -c1-160; done
-for r in 0 1; do env REPEAT=3 CHECK_TORCH_GPU=1 timeout -k 5 150 python tests/mp/gpu_dist.py dpotrf $r 2 ipc_$$ 8192 512 2 1 > gpurun_out/ip_$r.log 2>&1 & done
-wait
-for r in 0 1; do echo "== ipc $r"; grep -h "bad_reps\|bad tiles\|torch GPU" gpurun_out/ip_$r.log | cut -c1-160; done
+run() {
+  local name=$1; shift
+  rm -f gpurun_out/qr/R*.npy
+  for r in 0 1; do env "$@" timeout -k 5 60 python tests/mp/gpu_dist.py dgeqrf $r 2 qr_${name}_$$ 2048 256 2 gpurun_out/qr > gpurun_out/qr_${name}_$r.log 2>&1 & done
+  wait
+  python - <<'PY'
+import numpy as np, torch
+R = sum(np.load(f"gpurun_out/qr/R{r}.npy") for r in range(2))
+g = torch.Generator().manual_seed(77)
+A = (torch.rand((2048, 2048), dtype=torch.float64, generator=g) - 0.5).numpy()
+G = A.T @ A
+E = np.abs(R.T @ R - G)
+bad = sorted({(int(i) // 256, int(j) // 256) for i, j in zip(*np.nonzero(E > 1e-8))})
+print(f"rel {np.linalg.norm(R.T @ R - G) / np.linalg.norm(G):.2e} bad blocks {bad[:10]}")
+PY
+  echo "   ^ $name"
+}
+for i in 1 2 3; do
+run ipc$i A=1
+run host$i PARSEC_MCA_comm_device_plane=host
+done
