@@ -804,6 +804,265 @@ void launch_potrf(const PotrfDesc& p, hipStream_t stream, double* ws) {
   }
 }
 
+// ============================================ fused tile POTRF (one launch)
+// The whole tile factorization (+ optional W = L^-1) in ONE cooperative launch
+// of G workgroups (256 threads): per 64-column block j
+//   1. WG 0 factors the diagonal block and inverts it (block_potrf64)
+//   2. the panel below is solved against the inverse, 16-row chunks over all WGs
+//   3. the trailing lower triangle gets the rank-64 update, 64x64 blocks over WGs
+// separated by grid barriers; then W by recursive doubling of the diagonal
+// inverses (two block-GEMM phases per level). On the DPOTRF critical path this
+// replaces ~3 launches per 64 columns (each waiting for a free CU behind the
+// bulk GEMMs) by one launch. Block products run on v_mfma_f64_16x16x4f64 with
+// operands read straight from L2 (a wave owns a 32x32 quadrant of a 64x64 block).
+struct PotrfCoopArgs {
+  double* A;
+  int lda, n;
+  double* W;        // optional (ldw)
+  int ldw;
+  double* invD;     // nblk x 4096 diagonal-block inverses
+  double* T;        // n x n scratch (ld n) for the doubling (W only)
+  int* info;        // optional
+  unsigned* bar;    // grid-barrier counter, zero at launch
+  int* fault;       // set when a barrier times out (never expected)
+  long long* timing;  // optional: wall clock (100 MHz) after every grid barrier (WG 0)
+};
+
+constexpr int kCoopThreads = 256;
+
+__device__ __forceinline__ bool coop_sync(const PotrfCoopArgs& a, unsigned& phase) {
+  __threadfence();
+  __syncthreads();
+  bool ok = true;
+  if (threadIdx.x == 0) {
+    atomicAdd(a.bar, 1u);
+    const unsigned target = (phase + 1) * gridDim.x;
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(a.bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock64() - t0 > 400000000ll) {  // 4 s at 100 MHz: give up, flag the fault
+        atomicExch(a.fault, 1);
+        ok = false;
+        break;
+      }
+    }
+  }
+  if (a.timing && blockIdx.x == 0 && threadIdx.x == 0 && phase < 96) a.timing[phase] = wall_clock64();
+  ++phase;
+  __syncthreads();
+  __threadfence();
+  return ok;
+}
+
+// acc += Am(64 x 64) * Bn(64 x 64)^T restricted to this wave's 32x32 quadrant.
+// Am(m, k) = am_t ? Am[m * lda + k] : Am[k * lda + m]; same for Bn. Both
+// operands are staged through LDS first (every load of the block issued at once:
+// one memory latency per product instead of one per k-step), then 16 k-steps of
+// v_mfma_f64_16x16x4f64 read them back. Ends with a barrier: the caller may
+// overwrite the operands afterwards.
+constexpr int kBlkLd = 72;  // 64 + 8 doubles of padding
+__device__ __forceinline__ void blk_mma(double4_t (&acc)[2][2], double (*As)[kBlkLd], double (*Bs)[kBlkLd], const double* __restrict__ Am, int lda, bool am_t,
+                                        const double* __restrict__ Bn, int ldb, bool bn_t) {
+  const int tid = threadIdx.x;
+  // stage: 2048 double2 pairs per operand, 8 per thread
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int p = tid + kCoopThreads * e;
+    const int hi = p >> 5, lo = (p & 31) * 2;  // (major index, pair along the contiguous one)
+    if (!am_t) *reinterpret_cast<double2_t*>(&As[hi][lo]) = *reinterpret_cast<const double2_t*>(Am + (size_t)hi * lda + lo);  // k = hi, m = lo..
+    else {
+      const double2_t v = *reinterpret_cast<const double2_t*>(Am + (size_t)hi * lda + lo);  // m = hi, k = lo..
+      As[lo][hi] = v.x;
+      As[lo + 1][hi] = v.y;
+    }
+    if (!bn_t) *reinterpret_cast<double2_t*>(&Bs[hi][lo]) = *reinterpret_cast<const double2_t*>(Bn + (size_t)hi * ldb + lo);
+    else {
+      const double2_t v = *reinterpret_cast<const double2_t*>(Bn + (size_t)hi * ldb + lo);
+      Bs[lo][hi] = v.x;
+      Bs[lo + 1][hi] = v.y;
+    }
+  }
+  __syncthreads();
+  const int lane = tid & 63, w = tid >> 6;
+  const int qm = (w & 1) * 32, qn = (w >> 1) * 32;
+  const int r = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < 64; kk += 4) {
+    double y[2], x[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) y[j] = As[kk + kq][qm + j * 16 + r];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) x[i] = Bs[kk + kq][qn + i * 16 + r];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[i], y[j], acc[i][j], 0, 0, 0);
+  }
+  __syncthreads();
+}
+
+// C(64x64, ldc) = beta * C + alpha * acc (this wave's quadrant); lower: only m >= n
+__device__ __forceinline__ void blk_store(const double4_t (&acc)[2][2], double* __restrict__ C, int ldc, double alpha, double beta, bool lower) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qm = (w & 1) * 32, qn = (w >> 1) * 32;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = qm + j * 16 + (lane & 15), nn = qn + i * 16 + (lane >> 4) + 4 * q;
+        if (lower && m < nn) continue;
+        double* p = C + (size_t)nn * ldc + m;
+        *p = (beta == 0.0 ? 0.0 : beta * *p) + alpha * acc[i][j][q];
+      }
+}
+
+__device__ __forceinline__ void acc_zero(double4_t (&acc)[2][2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (double4_t){0.0, 0.0, 0.0, 0.0};
+}
+
+__global__ __launch_bounds__(kCoopThreads) void dpotrf_tile_coop_kernel(const PotrfCoopArgs a) {
+  __shared__ double As[64][kBlkLd];
+  __shared__ double Bs[64][kBlkLd];
+  const int n = a.n, lda = a.lda, nblk = n / 64;
+  const int G = gridDim.x, wg = blockIdx.x;
+  unsigned phase = 0;
+  double* __restrict__ A = a.A;
+  for (int j = 0; j < nblk; ++j) {
+    double* Djj = A + (size_t)(64 * j) * lda + 64 * j;
+    double* invj = a.invD + (size_t)j * 4096;
+    if (wg == 0) block_potrf64(Djj, lda, 64, invj, a.info, 64 * j, true);
+    if (!coop_sync(a, phase)) return;
+    const int r0 = 64 * (j + 1), rem = n - r0;
+    if (rem <= 0) break;
+    // panel: rows r0.., 64 rows per work item (one 64x64 block product each)
+    const int pblk = rem / 64;
+    for (int t = wg; t < pblk; t += G) {
+      double* B = A + (size_t)(64 * j) * lda + r0 + 64 * t;  // block (j + 1 + t, j)
+      double4_t acc[2][2];
+      acc_zero(acc);
+      blk_mma(acc, As, Bs, B, lda, false, invj, 64, false);  // B(m,k) * X(n,k) -> B X^T (ends with a barrier)
+      blk_store(acc, B, lda, 1.0, 0.0, false);
+    }
+    if (!coop_sync(a, phase)) return;
+    // trailing lower update: blocks (r, c), j < c <= r
+    const int Tn = nblk - j - 1, nt = Tn * (Tn + 1) / 2;
+    for (int t = wg; t < nt; t += G) {
+      // t -> (rr, cc) with cc <= rr (row-major over the lower triangle)
+      int rr = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+      while ((rr + 1) * (rr + 2) / 2 <= t) ++rr;
+      while (rr * (rr + 1) / 2 > t) --rr;
+      const int cc = t - rr * (rr + 1) / 2;
+      const int br = j + 1 + rr, bc = j + 1 + cc;
+      const double* Lr = A + (size_t)(64 * j) * lda + 64 * br;
+      const double* Lc = A + (size_t)(64 * j) * lda + 64 * bc;
+      double* C = A + (size_t)(64 * bc) * lda + 64 * br;
+      double4_t acc[2][2];
+      acc_zero(acc);
+      blk_mma(acc, As, Bs, Lr, lda, false, Lc, lda, false);
+      blk_store(acc, C, lda, -1.0, 1.0, br == bc);
+    }
+    if (!coop_sync(a, phase)) return;
+  }
+  if (!a.W) return;
+  // ---- W = L^-1: diagonal blocks from invD, zeros above, doubling below
+  double* __restrict__ W = a.W;
+  const int ldw = a.ldw;
+  for (int t = wg; t < nblk * nblk; t += G) {
+    const int bi = t % nblk, bj = t / nblk;  // block (bi, bj)
+    if (bi > bj) continue;                   // strictly-lower blocks come from the doubling
+    for (int e = threadIdx.x; e < 4096; e += kCoopThreads) {
+      const int rr = e & 63, cc = e >> 6;
+      W[(size_t)(64 * bj + cc) * ldw + 64 * bi + rr] = bi == bj ? a.invD[(size_t)bi * 4096 + (size_t)cc * 64 + rr] : 0.0;
+    }
+  }
+  if (!coop_sync(a, phase)) return;
+  double* __restrict__ Tm = a.T;
+  for (int g = 1; g < nblk; g *= 2) {
+    // T(c, a) = sum_{k = a}^{a0 + g - 1} L(c, k) X(k, a) for c in C, a in A
+    const int pairs = (nblk + 2 * g - 1) / (2 * g);
+    int items = 0;
+    for (int p = 0; p < pairs; ++p) {
+      const int a0 = 2 * g * p, c0 = a0 + g, c1 = min(a0 + 2 * g, nblk);
+      if (c0 >= nblk) continue;
+      const int nc = c1 - c0;
+      for (int it = 0; it < nc * g; ++it, ++items) {
+        if (items % G != wg) continue;
+        const int c = c0 + it % nc, ab = a0 + it / nc;
+        double4_t acc[2][2];
+        acc_zero(acc);
+        for (int kb = ab; kb < c0; ++kb)
+          blk_mma(acc, As, Bs, A + (size_t)(64 * kb) * lda + 64 * c, lda, false, W + (size_t)(64 * ab) * ldw + 64 * kb, ldw, true);
+        blk_store(acc, Tm + (size_t)(64 * ab) * n + 64 * c, n, 1.0, 0.0, false);
+      }
+    }
+    if (!coop_sync(a, phase)) return;
+    // X(c, a) = - sum_{k = c0}^{c} X(c, k) T(k, a)
+    items = 0;
+    for (int p = 0; p < pairs; ++p) {
+      const int a0 = 2 * g * p, c0 = a0 + g, c1 = min(a0 + 2 * g, nblk);
+      if (c0 >= nblk) continue;
+      const int nc = c1 - c0;
+      for (int it = 0; it < nc * g; ++it, ++items) {
+        if (items % G != wg) continue;
+        const int c = c0 + it % nc, ab = a0 + it / nc;
+        double4_t acc[2][2];
+        acc_zero(acc);
+        for (int kb = c0; kb <= c; ++kb)
+          blk_mma(acc, As, Bs, W + (size_t)(64 * kb) * ldw + 64 * c, ldw, false, Tm + (size_t)(64 * ab) * n + 64 * kb, n, true);
+        blk_store(acc, W + (size_t)(64 * ab) * ldw + 64 * c, ldw, -1.0, 0.0, false);
+      }
+    }
+    if (!coop_sync(a, phase)) return;
+  }
+}
+
+static int g_potrf_fused = -1;  // PARSEC_POTRF_FUSED=0 restores the multi-launch tile POTRF
+
+constexpr size_t kCoopHeader = 1024;  // barrier counter, fault flag, 96 timing slots
+static int g_potrf_timing = -1;       // PARSEC_POTRF_TIMING=1: record the barrier clocks
+
+size_t potrf_fused_workspace_bytes(const PotrfDesc& p) {
+  const size_t nblk = (size_t)p.n / 64;
+  return (nblk * 4096 + (p.W_out ? (size_t)p.n * p.n : 0)) * sizeof(double) + kCoopHeader;
+}
+
+bool potrf_fused_eligible(const PotrfDesc& p) {
+  if (g_potrf_fused < 0) {
+    const char* e = getenv("PARSEC_POTRF_FUSED");
+    g_potrf_fused = e ? atoi(e) : 0;
+  }
+  return g_potrf_fused != 0 && p.n % 64 == 0 && p.n >= 128 && p.n <= 2048;
+}
+
+// ws layout: [barrier counter (256 B)] [invD (unless kept by the caller)] [T]
+void launch_potrf_fused(const PotrfDesc& p, hipStream_t stream, double* ws) {
+  PotrfCoopArgs a{};
+  a.A = p.A; a.lda = p.lda; a.n = p.n; a.W = p.W_out; a.ldw = p.ldw; a.info = p.info;
+  char* base = reinterpret_cast<char*>(ws);
+  a.bar = reinterpret_cast<unsigned*>(base);
+  a.fault = reinterpret_cast<int*>(base + 64);
+  if (g_potrf_timing < 0) {
+    const char* e = getenv("PARSEC_POTRF_TIMING");
+    g_potrf_timing = e ? atoi(e) : 0;
+  }
+  a.timing = g_potrf_timing ? reinterpret_cast<long long*>(base + 128) : nullptr;
+  double* d = reinterpret_cast<double*>(base + kCoopHeader);
+  const int nblk = p.n / 64;
+  a.invD = p.invD_out ? p.invD_out : d;
+  if (!p.invD_out) d += (size_t)nblk * 4096;
+  a.T = d;
+  (void)hipMemsetAsync(base, 0, kCoopHeader, stream);
+  // enough workgroups for the widest phase, few enough to be co-resident next to
+  // the bulk GEMMs (one 84 KB-LDS workgroup per CU)
+  const int G = 32;
+  hipLaunchKernelGGL(dpotrf_tile_coop_kernel, dim3(G), dim3(kCoopThreads), 0, stream, a);
+}
+
 size_t trsm_w_workspace_bytes(const TrsmGemmDesc* d, int n) {
   size_t b = 0;
   for (int i = 0; i < n; ++i) b += ((size_t)d[i].m * d[i].n * sizeof(double) + 255) / 256 * 256;
@@ -841,6 +1100,9 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
 
 namespace kern {
 size_t potrf_workspace_bytes(const PotrfDesc& p);
+size_t potrf_fused_workspace_bytes(const PotrfDesc& p);
+bool potrf_fused_eligible(const PotrfDesc& p);
+void launch_potrf_fused(const PotrfDesc& p, hipStream_t stream, double* ws);
 size_t trsm_w_workspace_bytes(const TrsmGemmDesc* d, int n);
 void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, double* ws);
 void launch_qr_panel(const QrPanelDesc* descs, int n, hipStream_t stream);
@@ -853,7 +1115,7 @@ size_t qr_apply_workspace_bytes(const QrApplyDesc* descs, int n);
 
 size_t kernel_batch_workspace_bytes(const KernelBatch& b) {
   size_t w = 0;
-  for (auto& p : b.potrf) w = std::max(w, kern::potrf_workspace_bytes(p));
+  for (auto& p : b.potrf) w = std::max(w, kern::potrf_fused_eligible(p) ? kern::potrf_fused_workspace_bytes(p) : kern::potrf_workspace_bytes(p));
   if (!b.trsm_w.empty()) w = std::max(w, kern::trsm_w_workspace_bytes(b.trsm_w.data(), (int)b.trsm_w.size()));
   if (!b.qr_panel.empty()) w = std::max(w, kern::qr_panel_workspace_bytes(b.qr_panel.data(), (int)b.qr_panel.size()));
   w = std::max(w, kern::trsm_workspace_bytes(b.trsm.data(), (int)b.trsm.size()));
@@ -863,7 +1125,10 @@ size_t kernel_batch_workspace_bytes(const KernelBatch& b) {
 void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal, void* ws) {
   (void)device_ordinal;
   // critical-path kernels first: POTRF, then TRSM, then the GEMM/SYRK updates
-  for (auto& p : b.potrf) kern::launch_potrf(p, stream, static_cast<double*>(ws));
+  for (auto& p : b.potrf) {
+    if (kern::potrf_fused_eligible(p)) kern::launch_potrf_fused(p, stream, static_cast<double*>(ws));
+    else kern::launch_potrf(p, stream, static_cast<double*>(ws));
+  }
   if (!b.qr_panel.empty()) kern::launch_qr_panel_blocked(b.qr_panel.data(), (int)b.qr_panel.size(), stream, static_cast<double*>(ws));
   if (!b.trsm.empty()) kern::launch_trsm_batch(b.trsm.data(), (int)b.trsm.size(), stream, static_cast<double*>(ws));
   if (!b.trsm_w.empty()) kern::launch_trsm_w_batch(b.trsm_w.data(), (int)b.trsm_w.size(), stream, static_cast<double*>(ws));
@@ -917,6 +1182,12 @@ void* test_ws(size_t bytes) {
 
 extern "C" {
 int parsec_amd_gemm_tile_policy(int p) { return parsec::kern::gemm_tile_policy(p); }
+// barrier clocks of the last fused tile POTRF run through the test entry points
+int parsec_amd_potrf_timing(long long* out, int n) {
+  std::lock_guard<std::mutex> g(g_ws_m);
+  if (!g_ws || n > 96) return -1;
+  return (int)hipMemcpy(out, static_cast<char*>(g_ws) + 128, sizeof(long long) * n, hipMemcpyDeviceToHost);
+}
 int parsec_amd_dgemm_batch(const parsec::GemmDesc* descs, int n, void* stream) {
   parsec::kern::launch_gemm_batch(descs, n, (hipStream_t)stream);
   return (int)hipGetLastError();
@@ -928,6 +1199,11 @@ int parsec_amd_dtrsm_batch(const parsec::TrsmDesc* descs, int n, void* stream) {
 }
 int parsec_amd_dpotrf_tile(double* A, int n, int lda, int* info, void* stream) {
   parsec::PotrfDesc p{A, n, lda, info};
+  if (parsec::kern::potrf_fused_eligible(p)) {
+    void* ws = test_ws(parsec::kern::potrf_fused_workspace_bytes(p));
+    parsec::kern::launch_potrf_fused(p, (hipStream_t)stream, static_cast<double*>(ws));
+    return (int)hipGetLastError();
+  }
   void* ws = test_ws(4096 * sizeof(double));
   parsec::kern::launch_potrf(p, (hipStream_t)stream, static_cast<double*>(ws));
   return (int)hipGetLastError();
@@ -937,6 +1213,11 @@ int parsec_amd_dpotrf_tile_w(double* A, int n, int lda, int* info, double* W, in
   parsec::PotrfDesc p{A, n, lda, info};
   p.W_out = W;
   p.ldw = ldw;
+  if (parsec::kern::potrf_fused_eligible(p)) {
+    void* ws = test_ws(parsec::kern::potrf_fused_workspace_bytes(p));
+    parsec::kern::launch_potrf_fused(p, (hipStream_t)stream, static_cast<double*>(ws));
+    return (int)hipGetLastError();
+  }
   void* ws = test_ws(parsec::kern::potrf_workspace_bytes(p));
   parsec::kern::launch_potrf(p, (hipStream_t)stream, static_cast<double*>(ws));
   return (int)hipGetLastError();

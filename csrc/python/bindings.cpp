@@ -25,6 +25,7 @@ using namespace parsec;
 
 extern "C" int parsec_amd_dgemm_batch(const GemmDesc* descs, int n, void* stream);
 extern "C" int parsec_amd_gemm_tile_policy(int p);
+extern "C" int parsec_amd_potrf_timing(long long* out, int n);
 extern "C" int parsec_amd_dtrsm_batch(const TrsmDesc* descs, int n, void* stream);
 extern "C" int parsec_amd_dpotrf_tile(double* A, int n, int lda, int* info, void* stream);
 extern "C" int parsec_amd_dpotrf_tile_w(double* A, int n, int lda, int* info, double* W, int ldw, void* stream);
@@ -599,6 +600,11 @@ PYBIND11_MODULE(_C, m) {
     return parsec_amd_dgemm_batch(v.data(), (int)v.size(), (void*)stream);
   });
   m.def("kernel_gemm_tile_policy", [](int p) { return parsec_amd_gemm_tile_policy(p); });
+  m.def("kernel_potrf_timing", [](int n) {
+    std::vector<long long> v(n, 0);
+    if (parsec_amd_potrf_timing(v.data(), n) != 0) v.clear();
+    return v;
+  });
   m.def("kernel_dtrsm", [](uintptr_t L, uintptr_t B, int mm, int nn, int ldl, int ldb, uintptr_t stream) {
     TrsmDesc t;
     t.L = (const double*)L; t.B = (double*)B; t.m = mm; t.n = nn; t.ldl = ldl; t.ldb = ldb; t.trans = 1;
