@@ -256,6 +256,7 @@ struct Task : PoolElt {
   int8_t chore_id = 0;
   uint16_t nb_remote_targets = 0;
   int32_t deps_remaining = 0;    // activations still expected (PTG counter mode)
+  uint32_t deps_mask = 0;        // flows satisfied so far (PTG mask mode)
   uint32_t chore_mask = 0xffffffffu;
   uint32_t flags = 0;
   int32_t locals[kMaxLocals];
@@ -288,7 +289,8 @@ struct Chore {
   double weight = 1.0;  // load-balancing ratio (reference BODY weight=)
 };
 
-enum TaskClassFlags : uint32_t { TC_HIGH_PRIORITY = 0x1, TC_IMMEDIATE = 0x2, TC_NO_PROFILE = 0x4, TC_COUNT_DEPS = 0x8 };
+enum TaskClassFlags : uint32_t { TC_HIGH_PRIORITY = 0x1, TC_IMMEDIATE = 0x2, TC_NO_PROFILE = 0x4, TC_COUNT_DEPS = 0x8,
+  TC_INTERNAL = 0x10 /* runtime-internal tasks (startup generators): not counted in device stats */ };
 
 // Visitor called for each successor/predecessor of a task.
 struct DepVisit {

@@ -166,7 +166,7 @@ int execute_task(ExecutionStream* es, Task* t) {
   for (int i = 0; i < (int)tc->chores.size(); ++i) {
     if (!(t->chore_mask & (1u << i))) continue;
     const Chore& ch = tc->chores[i];
-    if (!device_type_enabled(tp, ch.type)) { t->chore_mask &= ~(1u << i); continue; }
+    if (!(tc->flags & TC_INTERNAL) && !device_type_enabled(tp, ch.type)) { t->chore_mask &= ~(1u << i); continue; }
     if (ch.evaluate && ch.evaluate(t) == HOOK_NEXT) continue;
     t->chore_id = (int8_t)i;
     t->status = STATUS_HOOK;
@@ -178,7 +178,7 @@ int execute_task(ExecutionStream* es, Task* t) {
       PARSEC_PINS(es, PINS_EXEC_BEGIN, t);
       rc = ch.hook(es, t);
       PARSEC_PINS(es, PINS_EXEC_END, t);
-      if (rc == HOOK_DONE) {
+      if (rc == HOOK_DONE && !(tc->flags & TC_INTERNAL)) {
         Device* dev = DeviceRegistry::instance().devices[0];
         if (ch.type == DEV_TEMPLATE)
           for (Device* d : DeviceRegistry::instance().devices)

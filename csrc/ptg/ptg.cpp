@@ -4,11 +4,15 @@
 #include <cstring>
 
 #include "../comm/comm.hpp"
+#include "../core/mca.hpp"
 #include "../device/device.hpp"
 #include "../prof/profiling.hpp"
 
 namespace parsec {
 namespace ptg {
+
+// index-array slot of a task that already became ready
+static Task* const kReadyMark = reinterpret_cast<Task*>(uintptr_t(1));
 
 static inline int64_t ev(const Expr& e, const Taskpool* tp, const int32_t* L, int64_t d = 0) { return e ? e(tp, L) : d; }
 
@@ -66,6 +70,73 @@ void for_each_task(const Taskpool* tp, const PtgTaskClass* tc, const std::functi
     });
   };
   rec(0);
+}
+
+// Odometer with dependent ranges: a level's bounds are evaluated from the
+// levels above it when the level is (re)entered; an empty range backtracks.
+void SpaceCursor::assign(size_t j) {
+  const LocalDef& ld = tc_->def.locals[j];
+  if (ld.has_index) {
+    L_[ld.index_slot] = (int32_t)cur_[j];
+    L_[j] = (int32_t)ev(ld.value, tp_, L_);
+  } else {
+    L_[j] = (int32_t)cur_[j];
+  }
+}
+
+int SpaceCursor::bump(int j) {
+  const auto& locals = tc_->def.locals;
+  for (; j >= 0; --j) {
+    if (!locals[j].has_index && !locals[j].is_range) continue;
+    const int64_t nv = cur_[j] + step_[j];
+    if (step_[j] > 0 ? nv <= hi_[j] : nv >= hi_[j]) {
+      cur_[j] = nv;
+      assign((size_t)j);
+      return j;
+    }
+  }
+  return -1;
+}
+
+bool SpaceCursor::settle(size_t from) {
+  const auto& locals = tc_->def.locals;
+  size_t j = from;
+  while (j < locals.size()) {
+    const LocalDef& ld = locals[j];
+    if (!ld.has_index && !ld.is_range) {
+      L_[j] = (int32_t)ev(ld.value, tp_, L_);
+      ++j;
+      continue;
+    }
+    const int64_t lo = ev(ld.lo, tp_, L_), hi = ev(ld.hi, tp_, L_);
+    int64_t st = ev(ld.step, tp_, L_, 1);
+    if (st == 0) st = 1;
+    if (st > 0 ? lo <= hi : lo >= hi) {
+      cur_[j] = lo;
+      hi_[j] = hi;
+      step_[j] = st;
+      assign(j);
+      ++j;
+      continue;
+    }
+    const int b = bump((int)j - 1);  // empty range: advance an outer level
+    if (b < 0) return false;
+    j = (size_t)b + 1;
+  }
+  return true;
+}
+
+bool SpaceCursor::next(int32_t* L) {
+  if (done_) return false;
+  if (!started_) {
+    started_ = true;
+    if (!settle(0)) { done_ = true; return false; }
+  } else {
+    const int b = bump((int)tc_->def.locals.size() - 1);
+    if (b < 0 || !settle((size_t)b + 1)) { done_ = true; return false; }
+  }
+  std::memcpy(L, L_, sizeof(int32_t) * kMaxLocals);
+  return true;
 }
 
 static void expand_iters(const Taskpool* tp, int32_t* X, const std::vector<IterDef>& its, size_t i, const std::function<void()>& f) {
@@ -169,20 +240,76 @@ void PtgTaskClass::for_each_input(const Taskpool* tp, int flow, const int32_t* L
   for (const Dep& d : def.flows[flow].in) for_each_dep_instance(tp, L, d, f);
 }
 
+int PtgTaskClass::flow_task_inputs(const Taskpool* tp, int f, const int32_t* L) const {
+  int count = 0;
+  for_each_input(tp, f, L, [&](const int32_t* X, const DepTarget* t) {
+    if (t->kind != DEP_TASK) return;
+    const PtgTaskClass* src = owner->classes[t->tc_id];
+    int32_t params[kMaxLocals];
+    expand_args(tp, X, t->args, 0, params, [&](const int32_t* P) {
+      int32_t SL[kMaxLocals];
+      if (src->complete_locals(tp, SL, P)) ++count;
+    });
+  });
+  return count;
+}
+
 int PtgTaskClass::count_task_inputs(const Taskpool* tp, const int32_t* L) const {
   int count = 0;
-  for (size_t f = 0; f < def.flows.size(); ++f) {
-    for_each_input(tp, (int)f, L, [&](const int32_t* X, const DepTarget* t) {
-      if (t->kind != DEP_TASK) return;
-      const PtgTaskClass* src = owner->classes[t->tc_id];
-      int32_t params[kMaxLocals];
-      expand_args(tp, X, t->args, 0, params, [&](const int32_t* P) {
-        int32_t SL[kMaxLocals];
-        if (src->complete_locals(tp, SL, P)) ++count;
-      });
-    });
-  }
+  for (size_t f = 0; f < def.flows.size(); ++f) count += flow_task_inputs(tp, (int)f, L);
   return count;
+}
+
+// Flows of the goal that no predecessor task will activate for this instance:
+// memory / NULL / NEW inputs, CTL flows whose every guard is false, inputs
+// naming a task outside its execution space (reference parsec.c:1317-1390).
+uint32_t PtgTaskClass::direct_mask(const Taskpool* tp, const int32_t* L) const {
+  uint32_t m = 0;
+  for (size_t f = 0; f < def.flows.size(); ++f)
+    if ((deps_goal & (1u << f)) && flow_task_inputs(tp, (int)f, L) == 0) m |= 1u << f;
+  return m;
+}
+
+void PtgTaskClass::build_index_store(const Taskpool* tp) {
+  IndexStore& st = istore;
+  st.ok = false;
+  if (def.startup_fn || def.nb_local_tasks_fn || def.make_key_fn || nb_params == 0) return;
+  const uint32_t my = tp->context ? (uint32_t)tp->context->my_rank : 0;
+  std::vector<int64_t> mn(nb_params, INT64_MAX), mx(nb_params, INT64_MIN);
+  int64_t n = 0;
+  for_each_task(tp, this, [&](const int32_t* L) {
+    if (rank_of(tp, L) != my) return;
+    ++n;
+    for (int i = 0; i < nb_params; ++i) {
+      mn[i] = std::min<int64_t>(mn[i], L[param_local[i]]);
+      mx[i] = std::max<int64_t>(mx[i], L[param_local[i]]);
+    }
+  });
+  if (n == 0) return;  // nothing local: activations of this class never arrive here
+  int64_t total = 1;
+  st.lo = mn;
+  st.ext.resize(nb_params);
+  for (int i = 0; i < nb_params; ++i) {
+    st.ext[i] = mx[i] - mn[i] + 1;
+    total *= st.ext[i];
+    if (total > (int64_t)1 << 26) return;  // > 64M slots: keep the hash table
+  }
+  st.slots.assign((size_t)total, nullptr);
+  st.locks.reset(new std::mutex[256]);
+  st.ok = true;
+}
+
+bool PtgTaskClass::is_startup_instance(const Taskpool* tp, const int32_t* L) const {
+  if (count_task_inputs(tp, L) != 0) return false;
+  for (size_t f = 0; f < def.flows.size(); ++f) {
+    if (def.flows[f].access == FLOW_CTL || def.flows[f].in.empty()) continue;
+    bool any = false;
+    for_each_input(tp, (int)f, L, [&](const int32_t*, const DepTarget*) { any = true; });
+    // a data flow whose every input guard is false waits for a run-time
+    // decision (data-dependent guards): it is not a startup task
+    if (!any) return false;
+  }
+  return true;
 }
 
 int64_t PtgTaskClass::sim_cost(const Task* t) const { return def.sim_cost ? def.sim_cost(t->taskpool, t->locals) : 1; }
@@ -436,7 +563,16 @@ PtgTaskpool::~PtgTaskpool() {
     task_free(t);
   });
   pending.clear();
-  for (auto* c : classes) delete c;
+  for (auto* c : classes) {
+    for (Task*& t : c->istore.slots)
+      if (t && t != kReadyMark) {
+        for (int f = 0; f < kMaxFlows; ++f) if (t->data[f].data_in) data_copy_release(t->data[f].data_in);
+        task_free(t);
+        t = nullptr;
+      }
+    delete c;
+  }
+  for (auto* g : startup_gens) delete g;
 }
 
 PtgTaskClass* PtgTaskpool::add_task_class(TaskClassDef def) {
@@ -452,6 +588,10 @@ PtgTaskClass* PtgTaskpool::add_task_class(TaskClassDef def) {
 }
 
 void PtgTaskpool::finalize() {
+  if (!options_resolved) {
+    options_resolved = true;
+    resolve_runtime_options();
+  }
   for (auto* tc : classes) {
     auto& d = tc->def;
     if (d.locals.size() > (size_t)kMaxLocals) fatal("task class %s has too many locals", d.name.c_str());
@@ -487,6 +627,23 @@ void PtgTaskpool::finalize() {
     }
     tc->flags = d.flags;
     tc->flops_per_task = d.flops;
+    tc->has_ctl_gather = false;
+    tc->deps_goal = 0;
+    for (size_t f = 0; f < d.flows.size(); ++f) {
+      if (!d.flows[f].in.empty()) tc->deps_goal |= 1u << f;
+      if (d.flows[f].access != FLOW_CTL) continue;
+      for (auto& dep : d.flows[f].in) {
+        bool ranged = !dep.iters.empty() || !dep.then_t.iters.empty();
+        for (auto& a : dep.then_t.args) ranged = ranged || a.is_range;
+        if (dep.has_else) for (auto& a : dep.else_t.args) ranged = ranged || a.is_range;
+        if (ranged) tc->has_ctl_gather = true;
+      }
+    }
+    const bool want_mask = d.deps_mode == 1 || (d.deps_mode < 0 && deps_mask_default);
+    tc->use_mask = want_mask && !tc->has_ctl_gather;
+    if (want_mask && tc->has_ctl_gather && d.deps_mode == 1)
+      warning("In task %s, mask_deps was requested, but this method cannot be provided: it uses control gather, which must be counted."
+              " Falling back to the counting method for dependency managing.", d.name.c_str());
     tc->writes_collections = false;
     for (auto& fl : d.flows)
       for (auto& dep : fl.out)
@@ -509,6 +666,19 @@ void PtgTaskpool::finalize() {
   finalized = true;
 }
 
+void PtgTaskpool::resolve_runtime_options() {
+  auto& R = ParamRegistry::instance();
+  const std::string dm = R.reg_string("ptg", "", "dep_management",
+      "Pending-task storage of PTG taskpools: index-array | dynamic-hash-table (empty = as compiled by ptgpp)", "");
+  if (dm == "index-array" || dm == "dynamic-hash-table") dep_management = dm;
+  else if (!dm.empty()) warning("ptg_dep_management: unknown mode '%s' ignored", dm.c_str());
+  const int64_t mask = R.reg_int("ptg", "", "deps_mask",
+      "PTG dependency tracking: 1 = per-flow bit masks, 0 = counters, -1 = as compiled (class mask_deps / count_deps win)", -1);
+  if (mask >= 0) deps_mask_default = mask != 0;
+  startup_chunk = R.reg_int("ptg", "", "startup_chunk", "Startup tasks generated per step of a class's startup generator (reference parsec_task_startup_chunk; 0 = all at once)", 256);
+  startup_iter = R.reg_int("ptg", "", "startup_iter", "Execution-space tuples visited per startup task generated before a generator yields (reference parsec_task_startup_iter)", 64);
+}
+
 int64_t PtgTaskpool::global(const std::string& n) const {
   for (size_t i = 0; i < global_names.size(); ++i) if (global_names[i] == n) return globals[i];
   fatal("PTG taskpool %s has no global %s", taskpool_name.c_str(), n.c_str());
@@ -519,13 +689,90 @@ void PtgTaskpool::set_global(const std::string& n, int64_t v) {
   globals.push_back(v);
 }
 
+// ------------------------------------------------------------ startup
+struct PtgTaskpool::StartupGen {
+  PtgTaskClass* tc;
+  SpaceCursor cur;
+  StartupGen(const Taskpool* tp, PtgTaskClass* c) : tc(c), cur(tp, c) {}
+};
+
+namespace {
+// The task class of startup generators: one CPU chore that resumes the
+// enumeration of a class's execution space, schedules the startup tasks it
+// finds and asks to be rescheduled until the space is exhausted. A generator
+// holds one runtime action of its taskpool, so termination waits for it.
+struct StartupGenClass : TaskClass {
+  StartupGenClass() {
+    name = "ptg_startup";
+    flags = TC_INTERNAL | TC_NO_PROFILE;
+    Chore ch;
+    ch.type = DEV_CPU;
+    ch.hook = [](ExecutionStream* es, Task* t) {
+      auto* tp = static_cast<PtgTaskpool*>(t->taskpool);
+      return tp->startup_step(es, static_cast<PtgTaskpool::StartupGen*>(t->user));
+    };
+    chores.push_back(std::move(ch));
+  }
+  int complete_execution(ExecutionStream* es, Task* t) const override {
+    (void)es;
+    Taskpool* tp = t->taskpool;
+    task_free(t);
+    tp->tdm->taskpool_addto_runtime_actions(tp, -1);
+    return 0;
+  }
+};
+const StartupGenClass& startup_gen_class() {
+  static StartupGenClass c;
+  return c;
+}
+}  // namespace
+
+// Emit up to max_tasks startup tasks of g's class visiting at most max_visits
+// tuples; true when the execution space is exhausted.
+bool PtgTaskpool::startup_emit(ExecutionStream* es, StartupGen* g, int64_t max_tasks, int64_t max_visits, std::vector<Task*>& out) {
+  PtgTaskClass* tc = g->tc;
+  const uint32_t my = (uint32_t)context->my_rank;
+  int32_t L[kMaxLocals];
+  int64_t made = 0, visits = 0;
+  while (made < max_tasks && visits < max_visits) {
+    if (!g->cur.next(L)) return true;
+    ++visits;
+    if (tc->rank_of(this, L) != my || !tc->is_startup_instance(this, L)) continue;
+    Task* t = task_new(es, this, tc);
+    std::memcpy(t->locals, L, sizeof(int32_t) * tc->nb_locals);
+    t->key = tc->make_key(this, L);
+    t->priority = tc->priority_of(this, L);
+    t->flags |= TASK_FLAG_STARTUP;
+    out.push_back(t);
+    ++made;
+  }
+  return false;
+}
+
+int PtgTaskpool::startup_step(ExecutionStream* es, StartupGen* g) {
+  std::vector<Task*> out;
+  const int64_t chunk = std::max<int64_t>(startup_chunk, 1);
+  const bool done = startup_emit(es, g, chunk, chunk * std::max<int64_t>(startup_iter, 1), out);
+  if (dynamic_termdet && !out.empty()) tdm->taskpool_addto_nb_tasks(this, (int64_t)out.size());
+  if (!out.empty()) schedule_tasks(es, out.data(), (int)out.size(), 0);
+  return done ? HOOK_DONE : HOOK_AGAIN;
+}
+
 void PtgTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
   if (!finalized) finalize();
   ExecutionStream* es = my_execution_stream();
   uint32_t my = (uint32_t)ctx->my_rank;
-  int64_t nb_local = 0;
+  int64_t nb_local = nb_local_tasks_fn ? nb_local_tasks_fn(this) : 0;
+  const bool enumerate_count = !nb_local_tasks_fn && !dynamic_termdet;
+  const bool chunked = startup_chunk > 0 && !ctx->simulation;
+  int64_t nb_startup = 0;
   for (auto* tc : classes) {
-    if (tc->def.nb_local_tasks_fn) nb_local += tc->def.nb_local_tasks_fn(this);
+    if (use_index_store()) std::call_once(tc->istore_once, [&] { tc->build_index_store(this); });
+    if (tc->def.nb_local_tasks_fn && !nb_local_tasks_fn) nb_local += tc->def.nb_local_tasks_fn(this);
+    if (enumerate_count && !tc->def.nb_local_tasks_fn)
+      for_each_task(this, tc, [&](const int32_t* L) {
+        if (tc->rank_of(this, L) == my) ++nb_local;
+      });
     if (tc->def.startup_fn) {
       std::vector<std::vector<int32_t>> st;
       tc->def.startup_fn(this, st);
@@ -536,23 +783,28 @@ void PtgTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
         t->priority = tc->priority_of(this, t->locals);
         t->flags |= TASK_FLAG_STARTUP;
         ready.push_back(t);
+        ++nb_startup;
       }
-      if (tc->def.nb_local_tasks_fn) continue;
+      continue;
     }
-    for_each_task(this, tc, [&](const int32_t* L) {
-      if (tc->rank_of(this, L) != my) return;
-      if (!tc->def.nb_local_tasks_fn && !dynamic_termdet) ++nb_local;
-      if (tc->def.startup_fn) return;
-      if (tc->count_task_inputs(this, L) != 0) return;
-      Task* t = task_new(es, this, tc);
-      std::memcpy(t->locals, L, sizeof(int32_t) * tc->nb_locals);
-      t->key = tc->make_key(this, L);
-      t->priority = tc->priority_of(this, L);
-      t->flags |= TASK_FLAG_STARTUP;
-      ready.push_back(t);
-    });
+    // the first chunk is produced here; a generator task continues the rest
+    auto* g = new StartupGen(this, tc);
+    const size_t before = ready.size();
+    const bool done = chunked ? startup_emit(es, g, startup_chunk, startup_chunk * std::max<int64_t>(startup_iter, 1), ready)
+                              : startup_emit(es, g, INT64_MAX, INT64_MAX, ready);
+    nb_startup += (int64_t)(ready.size() - before);
+    if (done) {
+      delete g;
+      continue;
+    }
+    startup_gens.push_back(g);
+    Task* gt = task_new(es, this, &startup_gen_class());
+    gt->user = g;
+    gt->priority = INT32_MAX / 2;
+    tdm->taskpool_addto_runtime_actions(this, 1);
+    ready.push_back(gt);
   }
-  if (dynamic_termdet) nb_local = (int64_t)ready.size();  // the rest is counted on first activation
+  if (dynamic_termdet) nb_local = nb_startup;  // the rest is counted on first activation / by the generators
   // Final versions of local tiles written by tasks of OTHER ranks (e.g. R(k,k)
   // at the end of a QR TS chain) arrive as remote activations that no local task
   // waits for: count them as pending runtime actions so this rank does not
@@ -581,41 +833,87 @@ void PtgTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
   tdm->taskpool_addto_nb_tasks(this, nb_local);
 }
 
+// Run f(slot) under the lock that owns the pending-task slot of (tc, L); f
+// reads/writes the Task* (nullptr = no pending task; set nullptr to remove).
+template <class F>
+Task* PtgTaskpool::with_pending(PtgTaskClass* tc, const int32_t* L, uint64_t key, F&& f) {
+  if (use_index_store()) {
+    std::call_once(tc->istore_once, [&] { tc->build_index_store(this); });
+    auto& st = tc->istore;
+    if (st.ok) {
+      int32_t P[kMaxLocals];
+      for (int i = 0; i < tc->nb_params; ++i) P[i] = L[tc->param_local[i]];
+      const int64_t ix = st.index(P);
+      if (ix >= 0) {
+        std::lock_guard<std::mutex> g(st.locks[(size_t)ix & 255]);
+        return f(st.slots[(size_t)ix]);
+      }
+    }
+  }
+  return pending.with(key, [&](auto& m) -> Task* {
+    auto it = m.find(key);
+    Task* slot = it == m.end() ? nullptr : it->second;
+    Task* r = f(slot);
+    if (slot == kReadyMark) slot = nullptr;  // the hash table forgets completed keys
+    if (slot && it == m.end()) m.emplace(key, slot);
+    else if (!slot && it != m.end()) m.erase(it);
+    return r;
+  });
+}
+
 void PtgTaskpool::activate(ExecutionStream* es, PtgTaskClass* tc, const int32_t* L, int flow, DataCopy* data, std::vector<Task*>& ready) {
   uint64_t key = tc->make_key(this, L);
   PARSEC_DEBUG(kVerbNoisier, "ptg", "activate %s(%d,%d,%d,%d) flow %d key %llx", tc->name.c_str(), L[0], tc->nb_locals > 1 ? L[1] : 0, tc->nb_locals > 2 ? L[2] : 0,
                tc->nb_locals > 3 ? L[3] : 0, flow, (unsigned long long)key);
-  Task* done = pending.with(key, [&](auto& m) -> Task* {
-    auto it = m.find(key);
-    Task* task;
-    if (it == m.end()) {
+  Task* done = with_pending(tc, L, key, [&](Task*& slot) -> Task* {
+    Task* task = slot;
+    if (task == kReadyMark) {
+      // index-array slots remember that the task already became ready (the
+      // reference's persistent dependency words): an extra activation is a DAG
+      // error, fatal in mask mode / paranoid, otherwise reported and dropped
+      if (tc->use_mask || g_paranoid)
+        fatal("%s: flow %s activated after the task became ready (double activation of an already satisfied dependency)",
+              tc->name.c_str(), flow >= 0 ? tc->def.flows[flow].name.c_str() : "?");
+      if (!tc->warned_extra_activation.exchange(true))
+        warning("%s: extra activation of flow %s after the task became ready ignored", tc->name.c_str(), flow >= 0 ? tc->def.flows[flow].name.c_str() : "?");
+      return nullptr;
+    }
+    if (!task) {
       task = task_new(es, this, tc);
       std::memcpy(task->locals, L, sizeof(int32_t) * tc->nb_locals);
       task->key = key;
       task->priority = tc->priority_of(this, L);
-      task->deps_remaining = tc->count_task_inputs(this, L);
+      if (tc->use_mask) task->deps_mask = tc->direct_mask(this, L);
+      else task->deps_remaining = tc->count_task_inputs(this, L);
       if (dynamic_termdet) tdm->taskpool_addto_nb_tasks(this, 1);
-      m.emplace(key, task);
-    } else {
-      task = it->second;
+      slot = task;
     }
     if (data && flow >= 0) {
       if (task->data[flow].data_in) data_copy_release(task->data[flow].data_in);
       data_copy_retain(data);
       task->data[flow].data_in = data;
     }
-    PARSEC_DEBUG(kVerbNoisier, "ptg", "  %s deps_remaining %d -> %d", tc->name.c_str(), task->deps_remaining, task->deps_remaining - 1);
-    if (--task->deps_remaining <= 0) {
-      if (g_paranoid) {
-        if (task->deps_remaining < 0)
-          fatal("paranoid: %s activated more times than it has inputs (%d extra)", tc->describe(task).c_str(), -task->deps_remaining);
-        std::lock_guard<std::mutex> lk(paranoid_m);
-        if (!paranoid_fired.insert(key).second) fatal("paranoid: %s became ready twice (double activation)", tc->describe(task).c_str());
-      }
-      m.erase(key);
-      return task;
+    bool ready_now;
+    if (tc->use_mask && flow >= 0) {
+      const uint32_t bit = 1u << flow;
+      if (task->deps_mask & bit)
+        fatal("%s: flow %s activated by a second predecessor (mask dependency already satisfied 0x%x)", tc->describe(task).c_str(),
+              tc->def.flows[flow].name.c_str(), task->deps_mask);
+      task->deps_mask |= bit;
+      ready_now = (task->deps_mask & tc->deps_goal) == tc->deps_goal;
+    } else {
+      PARSEC_DEBUG(kVerbNoisier, "ptg", "  %s deps_remaining %d -> %d", tc->name.c_str(), task->deps_remaining, task->deps_remaining - 1);
+      ready_now = --task->deps_remaining <= 0;
+      if (ready_now && g_paranoid && task->deps_remaining < 0)
+        fatal("paranoid: %s activated more times than it has inputs (%d extra)", tc->describe(task).c_str(), -task->deps_remaining);
     }
-    return nullptr;
+    if (!ready_now) return nullptr;
+    if (g_paranoid) {
+      std::lock_guard<std::mutex> lk(paranoid_m);
+      if (!paranoid_fired.insert(key).second) fatal("paranoid: %s became ready twice (double activation)", tc->describe(task).c_str());
+    }
+    slot = use_index_store() ? kReadyMark : nullptr;
+    return task;
   });
   if (done) ready.push_back(done);
 }

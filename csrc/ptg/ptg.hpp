@@ -113,6 +113,9 @@ struct TaskClassDef {
   std::function<uint64_t(const Taskpool*, const int32_t*)> make_key_fn;
   std::function<int64_t(const Taskpool*)> nb_local_tasks_fn;
   std::function<void(const Taskpool*, std::vector<std::vector<int32_t>>&)> startup_fn;  // returns startup locals
+  // dependency tracking: -1 = taskpool default, 0 = counter, 1 = mask
+  // (reference class properties count_deps / mask_deps, jdf2c.c:4171-4206)
+  int deps_mode = -1;
 };
 
 class PtgTaskpool;
@@ -135,12 +138,52 @@ class PtgTaskClass : public TaskClass {
   uint32_t rank_of(const Taskpool* tp, const int32_t* L) const;
   int32_t priority_of(const Taskpool* tp, const int32_t* L) const;
   int count_task_inputs(const Taskpool* tp, const int32_t* L) const;
+  // No task input is active AND every data flow that declares inputs has one
+  // active (memory / NULL / NEW) input: the startup rule of the reference
+  // compiler (jdf2c.c:2775-2815 has_ready_input_dependency, 2870-2965).
+  bool is_startup_instance(const Taskpool* tp, const int32_t* L) const;
   const DepTarget* active_input(const Taskpool* tp, int flow, const int32_t* L) const;
   // Every active input instance of `flow` (one for data flows, all for CTL gathers).
   void for_each_input(const Taskpool* tp, int flow, const int32_t* L, const std::function<void(const int32_t* Lx, const DepTarget*)>& f) const;
   mutable std::atomic<bool> warned_null_forward{false};
+  mutable std::atomic<bool> warned_extra_activation{false};
   bool writes_collections = false;  // some output dependency targets a data collection
   void reshape_inputs(Task* t) const;
+
+  // ---- dependency tracking (reference parsec.c:1317-1390, 1554-1664)
+  // Counter mode: Task::deps_remaining = number of task inputs, decremented per
+  // activation. Mask mode: one bit per flow with input dependencies
+  // (deps_goal); the flows satisfied without a predecessor task are ORed in at
+  // the first activation and every activation sets its flow's bit; a second
+  // activation of the same flow is an error. Control gathers need counting.
+  bool use_mask = false;
+  bool has_ctl_gather = false;
+  uint32_t deps_goal = 0;
+  int flow_task_inputs(const Taskpool* tp, int flow, const int32_t* L) const;
+  uint32_t direct_mask(const Taskpool* tp, const int32_t* L) const;
+
+  // ---- index-array storage of pending tasks (reference parsec.c:1503-1522
+  // default_find_deps): a dense slot per parameter tuple of the local task
+  // space, bounds from enumerating it; classes whose space is not enumerable
+  // (user startup/count functions) or too large keep the hash table.
+  struct IndexStore {
+    std::vector<int64_t> lo, ext;
+    std::vector<Task*> slots;
+    std::unique_ptr<std::mutex[]> locks;
+    bool ok = false;
+    int64_t index(const int32_t* params) const {
+      int64_t ix = 0;
+      for (size_t i = 0; i < lo.size(); ++i) {
+        const int64_t v = params[i] - lo[i];
+        if (v < 0 || v >= ext[i]) return -1;
+        ix = ix * ext[i] + v;
+      }
+      return ix;
+    }
+  };
+  IndexStore istore;
+  std::once_flag istore_once;
+  void build_index_store(const Taskpool* tp);
 };
 
 // Call f(Lx, target) for every active instance of `d` (expanding iterators).
@@ -158,26 +201,61 @@ class PtgTaskpool : public Taskpool {
   // tasks, then each first activation) instead of enumerating the whole local
   // task space at startup (reference jdf2c.c dynamic termination detection).
   bool dynamic_termdet = false;
-  // ptgpp --dep-management: both modes map to the sharded hash table of pending
-  // tasks (dense index arrays bring nothing on top of it here)
+  // ptgpp --dep-management: "index-array" (dense per-class slot arrays, the
+  // reference default) or "dynamic-hash-table" (sharded hash of pending tasks);
+  // MCA ptg_dep_management overrides the compiled choice.
   std::string dep_management = "dynamic-hash-table";
+  bool deps_mask_default = false;  // ptgpp --deps-mask / MCA ptg_deps_mask
+  // user %option nb_local_tasks_fn: total number of local tasks of the taskpool
+  std::function<int64_t(const Taskpool*)> nb_local_tasks_fn;
+  // Resumable chunked startup (reference jdf2c.c:3183-3192, parsec.c:74-75):
+  // startup tasks are produced by one generator task per class, each call
+  // emitting a chunk that doubles from startup_iter up to startup_chunk.
+  int64_t startup_chunk = 256, startup_iter = 64;
+  struct StartupGen;
+  std::vector<StartupGen*> startup_gens;
+  int startup_step(ExecutionStream* es, StartupGen* g);
+  bool startup_emit(ExecutionStream* es, StartupGen* g, int64_t max_tasks, int64_t max_visits, std::vector<Task*>& out);
   std::vector<std::string> global_names;
   int64_t remote_writebacks_expected = 0;  // final tile versions other ranks send here
   bool finalized = false;
+  bool options_resolved = false;
   PtgTaskpool();
   ~PtgTaskpool() override;
   PtgTaskClass* add_task_class(TaskClassDef def);
   void finalize();  // resolve names, build flows/chores
+  void resolve_runtime_options();  // MCA overrides of the compiled dependency / startup modes
   void startup(Context* ctx, std::vector<Task*>& ready) override;
   void on_remote_activation(ExecutionStream* es, RemoteActivation& act) override;
   // Deliver data for flow `flow` of task (tc, L); appends to `ready` when complete.
   void activate(ExecutionStream* es, PtgTaskClass* tc, const int32_t* L, int flow, DataCopy* data, std::vector<Task*>& ready);
   int64_t global(const std::string& n) const;
   void set_global(const std::string& n, int64_t v);
+ private:
+  bool use_index_store() const { return dep_management == "index-array"; }
+  template <class F>
+  Task* with_pending(PtgTaskClass* tc, const int32_t* L, uint64_t key, F&& f);
 };
 
 // Enumerate the execution space of `tc` (all locals), calling f(L).
 void for_each_task(const Taskpool* tp, const PtgTaskClass* tc, const std::function<void(const int32_t*)>& f);
+
+// Resumable odometer over the execution space of a class (same order as
+// for_each_task): next() fills L with the next tuple, false when exhausted.
+class SpaceCursor {
+ public:
+  SpaceCursor(const Taskpool* tp, const PtgTaskClass* tc) : tp_(tp), tc_(tc) {}
+  bool next(int32_t* L);
+ private:
+  bool settle(size_t from);
+  int bump(int j);
+  void assign(size_t j);
+  const Taskpool* tp_;
+  const PtgTaskClass* tc_;
+  int32_t L_[kMaxLocals] = {};
+  int64_t cur_[kMaxLocals] = {}, hi_[kMaxLocals] = {}, step_[kMaxLocals] = {};
+  bool started_ = false, done_ = false;
+};
 
 }  // namespace ptg
 }  // namespace parsec

@@ -72,6 +72,13 @@ typedef struct parsec_arena_datatype_s parsec_arena_datatype_t;
 
 typedef uint64_t parsec_data_key_t;
 
+/* Compile-time limits of the PTG runtime (reference parsec_config.h / jdf2c
+ * checks): locals per task class, flows per class, dependencies per flow. */
+#define MAX_LOCAL_COUNT 20
+#define MAX_PARAM_COUNT 20
+#define MAX_DEP_IN_COUNT 10
+#define MAX_DEP_OUT_COUNT 10
+
 /* ------------------------------------------------------------ datatypes */
 /* Datatypes are integer handles: the predefined element types below, or
  * derived layouts created with parsec_type_create_* (reference datatype.h). */

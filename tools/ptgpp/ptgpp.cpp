@@ -35,6 +35,7 @@
 namespace {
 
 constexpr int kMaxLocals = 20;     // runtime kMaxLocals (reference MAX_LOCAL_COUNT)
+constexpr int kMaxDepsPerFlow = 10;  // reference MAX_DEP_IN_COUNT / MAX_DEP_OUT_COUNT (per flow)
 constexpr int kMaxInFlows = 10;    // reference MAX_DEP_IN_COUNT
 constexpr int kMaxOutFlows = 10;   // reference MAX_DEP_OUT_COUNT
 constexpr int kMaxFlows = 20;
@@ -42,7 +43,8 @@ constexpr int kMaxFlows = 20;
 std::string g_file;
 bool g_noline = false;               // --noline: no #line directives
 bool g_dynamic_termdet = false;      // --dynamic-termdet
-std::string g_dep_management = "dynamic-hash-table";  // --dep-management
+std::string g_dep_management = "index-array";  // --dep-management (reference default)
+bool g_deps_mask = false;            // --deps-mask: mask dependency tracking by default
 int g_errors = 0;
 
 [[noreturn]] void die(int line, const std::string& msg) {
@@ -382,6 +384,8 @@ class Parser {
     const Tok& t = cur();
     if (t.k == T_NUM || t.k == T_STR) { next(); return t.s; }
     if (t.k == T_CODE) { std::string c = code_expr(t.s); next(); return c; }
+    // inline_c %{ ... %}: inline C returning the value (reference parsec.l inline_c)
+    if (t.k == T_IDENT && t.s == "inline_c" && peek(1).k == T_CODE) { next(); std::string c = code_expr(cur().s); next(); return c; }
     if (t.k == T_IDENT) { std::string s = t.s; next(); return s; }
     if (is_op("(")) {
       next();
@@ -576,7 +580,8 @@ class Parser {
         if (t.k == T_OP && (t.s == "(" || t.s == "[")) ++depth;
         else if (t.k == T_OP && (t.s == ")" || t.s == "]")) { if (--depth < 0) { ok = false; break; } }
         else if (depth == 0 && t.k == T_OP && t.s == "?") break;
-        else if (depth == 0 && ((t.k == T_OP && (t.s == "->" || t.s == "<-" || t.s == ";")) || t.k == T_BODY || (t.k == T_IDENT && (t.s == "BODY" || t.s == "READ" || t.s == "WRITE" || t.s == "RW" || t.s == "CTL")))) {
+        else if (depth == 0 && ((t.k == T_OP && (t.s == "->" || t.s == "<-" || t.s == ";")) || t.k == T_BODY ||
+                                   (t.k == T_IDENT && (t.s == "BODY" || t.s == "READ" || t.s == "WRITE" || t.s == "RW" || t.s == "CTL" || t.s == "RO" || t.s == "WO")))) {
           // '->' inside an expression is member access: only stop when it starts a new dependency line
           if (t.s == "->" && k > i_ && t_[k - 1].line == t.line) continue;
           ok = false;
@@ -607,6 +612,8 @@ class Parser {
     Flow f;
     f.line = cur().line;
     f.access = expect_ident();
+    if (f.access == "RO") f.access = "READ";    // reference parsec.l aliases
+    if (f.access == "WO") f.access = "WRITE";
     f.name = expect_ident();
     f.props = properties();
     while (is_op("<-") || is_op("->")) f.deps.push_back(dep());
@@ -663,7 +670,7 @@ class Parser {
       }
       next();
     }
-    while (is_id("READ") || is_id("WRITE") || is_id("RW") || is_id("CTL")) f.flows.push_back(flow());
+    while (is_id("READ") || is_id("WRITE") || is_id("RW") || is_id("CTL") || is_id("RO") || is_id("WO")) f.flows.push_back(flow());
     if (is_op(";")) { next(); f.priority = expr(true); }
     while (is_id("BODY")) {
       Body b;
@@ -684,6 +691,41 @@ class Parser {
   std::vector<Tok> t_;
   size_t i_ = 0;
 };
+
+// ------------------------------------------------------- implicit globals
+// A data reference (dependency target or affinity) that names no declared
+// global is declared implicitly as a data collection, `parsec_data_collection_t*`
+// (reference parsec.y:120-164 jdf_find_or_create_data); like the reference, the
+// implicit globals go in front of the declared ones, newest first.
+void declare_implicit_globals(Jdf& j) {
+  std::set<std::string> known, fns;
+  for (auto& g : j.globals) known.insert(g.name);
+  for (auto& f : j.functions) fns.insert(f.name);
+  std::vector<Global> implicit;
+  auto use = [&](const std::string& name, int line) {
+    if (name.empty() || known.count(name) || fns.count(name)) return;
+    known.insert(name);
+    Global g;
+    g.name = name;
+    g.line = line;
+    Prop p;
+    p.key = "type";
+    p.val = "parsec_data_collection_t*";
+    p.is_str = true;
+    g.props.push_back(p);
+    implicit.push_back(g);
+  };
+  for (auto& f : j.functions) {
+    use(f.aff_name, f.line);
+    for (auto& fl : f.flows)
+      for (auto& d : fl.deps) {
+        if (d.then_t.kind == TG_DATA) use(d.then_t.name, d.line);
+        if (d.has_else && d.else_t.kind == TG_DATA) use(d.else_t.name, d.line);
+      }
+  }
+  std::reverse(implicit.begin(), implicit.end());
+  j.globals.insert(j.globals.begin(), implicit.begin(), implicit.end());
+}
 
 // ---------------------------------------------------------------- checks
 void sanity(const Jdf& j) {
@@ -718,13 +760,20 @@ void sanity(const Jdf& j) {
             bool has = false;
             for (auto& g : it->second->flows) if (g.name == t->flow) has = true;
             if (!has) error_at(d.line, "task class " + t->name + " has no flow " + t->flow);
-            if (t->args.size() != it->second->params.size()) error_at(d.line, "call to " + t->name + " with " + std::to_string(t->args.size()) + " arguments, expected " + std::to_string(it->second->params.size()));
+            // the reference compiler does not check call arity; warn (missing parameters are passed as 0)
+            if (t->args.size() != it->second->params.size())
+              warn_at(d.line, "call to " + t->name + " with " + std::to_string(t->args.size()) + " arguments, expected " + std::to_string(it->second->params.size()));
           }
           if (t->kind == TG_DATA && !gnames.count(t->name)) error_at(d.line, "data reference " + t->name + " is not a global");
         }
       }
       if (hin) ++nin;
       if (hout) ++nout;
+      // per-flow dependency limits (reference parsec_flow_t dep_in[MAX_DEP_IN_COUNT] / dep_out[MAX_DEP_OUT_COUNT])
+      int din = 0, dout = 0;
+      for (auto& d : fl.deps) (d.out ? dout : din) += d.has_else ? 2 : 1;
+      if (din > kMaxDepsPerFlow) error_at(fl.line, "flow " + fl.name + " of " + f.name + " has too many input dependencies (" + std::to_string(din) + " > " + std::to_string(kMaxDepsPerFlow) + ")");
+      if (dout > kMaxDepsPerFlow) error_at(fl.line, "flow " + fl.name + " of " + f.name + " has too many output dependencies (" + std::to_string(dout) + " > " + std::to_string(kMaxDepsPerFlow) + ")");
       if (fl.access == "CTL") {
         for (auto& d : fl.deps)
           if ((d.then_t.kind == TG_DATA) || (d.has_else && d.else_t.kind == TG_DATA)) error_at(d.line, "CTL flow " + fl.name + " cannot reference data");
@@ -810,7 +859,9 @@ struct Gen {
     return o;
   }
 
-  std::string callargs(const Function& f, const std::vector<CallArg>& args, const Scope& sc) const {
+  std::string callargs(const Function& f, const std::vector<CallArg>& args_in, const Scope& sc, size_t want = 0) const {
+    std::vector<CallArg> args = args_in;
+    while (args.size() < want) { CallArg z; z.e = "0"; args.push_back(z); }  // arity mismatch (warned)
     std::string s = "{";
     for (size_t i = 0; i < args.size(); ++i) {
       const CallArg& a = args[i];
@@ -841,7 +892,7 @@ struct Gen {
       case TG_NEW: o << "__t.kind = parsec::ptg::DEP_NEW; "; break;
       case TG_TASK:
         o << "__t.kind = parsec::ptg::DEP_TASK; __t.tc_name = \"" << t.name << "\"; __t.flow_name = \"" << t.flow << "\"; ";
-        o << "__t.args = " << callargs(f, t.args, sc) << "; ";
+        o << "__t.args = " << callargs(f, t.args, sc, nparams(t.name)) << "; ";
         break;
       case TG_DATA:
         o << "__t.kind = parsec::ptg::DEP_DATA; __t.dc = [=](const parsec::Taskpool*) { return parsec::ptg::to_dc(__tp->_g_" << t.name << "); }; ";
@@ -856,6 +907,10 @@ struct Gen {
     if (const Prop* d = find_prop(dprops, "count_remote")) o << "__t.count_remote = " << lam(f, prop_expr(*d), sc) << "; ";
     o << "return __t; }()";
     return o.str();
+  }
+  size_t nparams(const std::string& tc) const {
+    for (auto& g : j.functions) if (g.name == tc) return g.params.size();
+    return 0;
   }
   static std::string prop_expr(const Prop& p) {
     if (p.val.rfind("%{", 0) == 0) return "([&]() -> int64_t {" + p.val.substr(2) + "})()";
@@ -993,6 +1048,9 @@ struct Gen {
       if (const Prop* p = find_prop(f.props, "startup_fn")) c << "    d.startup_fn = [](const parsec::Taskpool* tp, std::vector<std::vector<int32_t>>& out) { " << p->val << "(tp, out); };\n";
       if (const Prop* p = find_prop(f.props, "nb_local_tasks_fn")) c << "    d.nb_local_tasks_fn = [](const parsec::Taskpool* tp) { return (int64_t)" << p->val << "(tp); };\n";
       if (const Prop* p = find_prop(f.props, "flops")) c << "    d.flops = (double)(" << p->val << ");\n";
+      auto prop_on = [&](const char* k) { const Prop* p = find_prop(f.props, k); return p && (p->val == "on" || p->val == "true" || p->val == "1"); };
+      if (prop_on("count_deps")) c << "    d.deps_mode = 0;\n";
+      else if (prop_on("mask_deps")) c << "    d.deps_mode = 1;\n";
       for (auto& fl : f.flows) {
         c << "    { parsec::ptg::FlowDef fl; fl.name = \"" << fl.name << "\"; fl.access = parsec::FLOW_" << fl.access << ";\n";
         for (auto& d : fl.deps) c << "      fl." << (d.out ? "out" : "in") << ".push_back(" << dep(f, fl, d) << ");\n";
@@ -1017,8 +1075,9 @@ struct Gen {
     }
     for (auto& kv : j.options)
       if (kv.first == "nb_local_tasks_fn")
-        c << "  (void)__has_nb_local;\n  if (!__tp->classes.empty()) __tp->classes[0]->def.nb_local_tasks_fn = [](const parsec::Taskpool* tp) { return (int64_t)" << kv.second << "(tp); };\n";
+        c << "  (void)__has_nb_local;\n  __tp->nb_local_tasks_fn = [](const parsec::Taskpool* tp) { return (int64_t)" << kv.second << "(tp); };\n";
     if (g_dynamic_termdet) c << "  __tp->dynamic_termdet = true;\n";
+    if (g_deps_mask) c << "  __tp->deps_mask_default = true;\n";
     c << "  __tp->dep_management = \"" << g_dep_management << "\";\n";
     c << "  __tp->finalize();\n  return __tp;\n}\n";
     if (!j.epilogue.empty()) {
@@ -1045,6 +1104,7 @@ int main(int argc, char** argv) {
     else if (a == "-E") check_only = true;
     else if (a == "--noline") g_noline = true;
     else if (a == "--dynamic-termdet") g_dynamic_termdet = true;
+    else if (a == "--deps-mask") g_deps_mask = true;
     else if (a == "--dep-management" && i + 1 < argc) {
       g_dep_management = argv[++i];
       if (g_dep_management != "index-array" && g_dep_management != "dynamic-hash-table") {
@@ -1055,7 +1115,7 @@ int main(int argc, char** argv) {
       // warning controls (-Wremote, -Wno-masks, ...): accepted, diagnostics are always on
     } else if (a == "-h" || a == "--help") {
       printf("usage: parsec-ptgpp -i file.jdf [-o output_base] [-f function_base] [-E] [--noline]\n"
-             "                    [--dynamic-termdet] [--dep-management index-array|dynamic-hash-table] [-W...]\n");
+             "                    [--dynamic-termdet] [--deps-mask] [--dep-management index-array|dynamic-hash-table] [-W...]\n");
       return 0;
     } else if (in.empty() && a[0] != '-') in = a;
     else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
@@ -1079,6 +1139,7 @@ int main(int argc, char** argv) {
   Tokenizer tz(src);
   Parser p(tz.run());
   Jdf j = p.parse();
+  declare_implicit_globals(j);
   sanity(j);
   if (g_errors) {
     fprintf(stderr, "parsec-ptgpp: %d error(s)\n", g_errors);
