@@ -180,31 +180,6 @@ struct ArenaDatatype {
 void add2arena_rect(ArenaDatatype& adt, uint32_t esz, int64_t mb, int64_t nb, int64_t ld);
 void add2arena(ArenaDatatype& adt, const Datatype& dtt, size_t alignment = 64);
 
-// Data repository: entries keyed by producer task key, holding output copies
-// until `usage_limit` consumers have retrieved them (reference datarepo.h:74-150).
-struct DataRepoEntry {
-  uint64_t key = 0;
-  std::atomic<int32_t> usage_count{0};
-  std::atomic<int32_t> usage_limit{0};
-  std::atomic<int32_t> retained{0};
-  int nb_flows = 0;
-  DataCopy* data[kMaxFlows] = {};
-};
-class DataRepo {
- public:
-  explicit DataRepo(int nb_flows) : nb_flows_(nb_flows) {}
-  ~DataRepo();
-  DataRepoEntry* lookup_and_create(uint64_t key);
-  DataRepoEntry* lookup(uint64_t key);
-  void entry_used_once(uint64_t key);
-  void entry_addto_usage_limit(uint64_t key, int32_t usage);
-  size_t size() { return map_.size(); }
- private:
-  void maybe_free(uint64_t key, DataRepoEntry* e);
-  int nb_flows_;
-  ShardedMap<DataRepoEntry*> map_{6};
-};
-
 // ============================================================ collections
 // Data collection vtable (reference include/parsec/data_distribution.h:26-66).
 struct DataCollection {
@@ -240,7 +215,6 @@ DataCollection* dc_lookup(uint64_t id);
 struct TaskDataRef {
   DataCopy* data_in = nullptr;
   DataCopy* data_out = nullptr;
-  DataRepoEntry* source_repo_entry = nullptr;
 };
 
 enum TaskFlags : uint32_t { TASK_FLAG_REMOTE_SHADOW = 0x1, TASK_FLAG_STARTUP = 0x2, TASK_FLAG_INTERNAL = 0x4, TASK_FLAG_QUEUED = 0x8 };

@@ -327,61 +327,6 @@ void add2arena(ArenaDatatype& adt, const Datatype& dtt, size_t alignment) {
   adt.arena = std::make_shared<Arena>((size_t)std::max<int64_t>(dtt.extent_bytes(), 8), alignment, dtt);
 }
 
-// ============================================================== data repo
-DataRepo::~DataRepo() {
-  map_.for_each([](uint64_t, DataRepoEntry* e) {
-    for (auto* c : e->data) if (c) data_copy_release(c);
-    delete e;
-  });
-}
-
-DataRepoEntry* DataRepo::lookup_and_create(uint64_t key) {
-  return map_.with(key, [&](auto& m) {
-    auto it = m.find(key);
-    if (it != m.end()) return it->second;
-    auto* e = new DataRepoEntry();
-    e->key = key;
-    e->nb_flows = nb_flows_;
-    m[key] = e;
-    return e;
-  });
-}
-
-DataRepoEntry* DataRepo::lookup(uint64_t key) {
-  DataRepoEntry* e = nullptr;
-  map_.find(key, e);
-  return e;
-}
-
-void DataRepo::maybe_free(uint64_t key, DataRepoEntry* e) {
-  bool del = map_.with(key, [&](auto& m) {
-    if (e->usage_count.load() >= e->usage_limit.load() && e->retained.load() == 0 && e->usage_limit.load() >= 0) {
-      m.erase(key);
-      return true;
-    }
-    return false;
-  });
-  if (del) {
-    for (auto*& c : e->data) { if (c) data_copy_release(c); c = nullptr; }
-    delete e;
-  }
-}
-
-void DataRepo::entry_used_once(uint64_t key) {
-  DataRepoEntry* e = lookup(key);
-  if (!e) return;
-  e->usage_count.fetch_add(1);
-  maybe_free(key, e);
-}
-
-void DataRepo::entry_addto_usage_limit(uint64_t key, int32_t usage) {
-  DataRepoEntry* e = lookup(key);
-  if (!e) return;
-  e->usage_limit.fetch_add(usage);
-  e->retained.store(0);
-  maybe_free(key, e);
-}
-
 // ========================================================= dc id registry
 static std::mutex g_dc_m;
 static std::map<uint64_t, DataCollection*> g_dcs;

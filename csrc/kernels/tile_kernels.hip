@@ -37,6 +37,11 @@ constexpr int kMaxGemmBatch = 40;
 struct GemmBatchArgs {
   int count;
   int total_tiles;
+  // split-K tail: workgroups [main_tiles, grid) each take 1/ksplit of the K range
+  // of one of the last (total_tiles - main_tiles) tiles and add alpha * partial
+  // into C with f64 atomics (beta == 1 for every descriptor of such a launch)
+  int main_tiles;
+  int ksplit;
   int tile_start[kMaxGemmBatch + 1];
   GemmDesc d[kMaxGemmBatch];
 };
@@ -83,7 +88,18 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
   __shared__ double As[NBUF][BK][LDA_S];
   __shared__ double Bs[NBUF][BK][LDB_S];
 
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  // Workgroups [0, main_tiles) own whole tiles (XCD-aware order); the ones
+  // dispatched last split the K range of the tail tiles (wave quantisation:
+  // a 606-tile launch on 512 slots would otherwise run a 94-tile second round)
+  int tile, ks = 0, nsplit = 1;
+  if ((int)blockIdx.x < args.main_tiles) {
+    tile = xcd_remap(blockIdx.x, args.main_tiles);
+  } else {
+    const int u = blockIdx.x - args.main_tiles;
+    nsplit = args.ksplit;
+    tile = args.main_tiles + u / nsplit;
+    ks = u % nsplit;
+  }
   if (tile >= args.total_tiles) return;
   const int di = find_desc(args, args.tile_start, tile);
   const GemmDesc& d = args.d[di];
@@ -97,10 +113,15 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
-  const double* __restrict__ A = d.A;
-  const double* __restrict__ B = d.B;
-  const int M = d.m, N = d.n, K = d.k;
+  const int M = d.m, N = d.n;
   const int lda = d.lda, ldb = d.ldb;
+  // K range of this workgroup (whole K unless split); chunks are BK multiples
+  const int kchunk = nsplit > 1 ? (((d.k + nsplit - 1) / nsplit + BK - 1) / BK) * BK : d.k;
+  const int kbeg = ks * kchunk;
+  if (kbeg >= d.k) return;
+  const int K = min(d.k, kbeg + kchunk) - kbeg;
+  const double* __restrict__ A = d.A + (TRANSA ? (size_t)kbeg : (size_t)kbeg * lda);
+  const double* __restrict__ B = d.B + (TRANSB ? (size_t)kbeg * ldb : (size_t)kbeg);
   // 16-byte loads when every row pair is aligned and fully inside the tile
   const bool vec = FULL || ((lda | ldb) % 2 == 0) && ((((uintptr_t)A) | ((uintptr_t)B)) % 16 == 0) && (TRANSA ? (K % 2 == 0) : (M % 2 == 0)) &&
                    (TRANSB ? (N % 2 == 0) : (K % 2 == 0));
@@ -201,7 +222,8 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
   // loaded behind the first A/B tile so the C read latency overlaps the prologue
   // and the epilogue is a pure store (no read-modify-write tail when a batch's
   // workgroups all finish together).
-  const bool preload = FULL && (d.alpha == 1.0 || d.alpha == -1.0);
+  const bool split = nsplit > 1;
+  const bool preload = FULL && !split && (d.alpha == 1.0 || d.alpha == -1.0);
   double* __restrict__ C = d.C;
   const int ldc = d.ldc;
   load_tile(0);
@@ -255,6 +277,10 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
         if ((FULL || (gm < M && gn < N)) && (!d.lower_only || gm >= gn)) {
           double* p = C + (size_t)gn * ldc + gm;
           double v = alpha * acc[i][j][r];
+          if (split) {
+            unsafeAtomicAdd(p, v);  // no-return global f64 add, performed at the memory side
+            continue;
+          }
           if (beta != 0.0) v += beta * *p;
           *p = v;
         }
@@ -541,6 +567,8 @@ static int g_gemm_tile_policy = -1;  // -1 unset, 0 auto, 64, 128
 static int g_gemm_variant = -1;      // big-tile kernel shape (PARSEC_GEMM_VARIANT)
 static int g_gemm_full = -1;         // PARSEC_GEMM_FULL=0 disables the unchecked fast path
 static int g_gemm_big_tiles = 384;   // PARSEC_GEMM_BIG_TILES: 128x128 tiles in a launch to pick the big kernel
+static int g_gemm_splitk = -1;       // PARSEC_GEMM_SPLITK=0 disables the split-K tail of the 128x128 kernel
+static int g_gemm_slots = 512;       // resident 128x128 workgroups (2 per CU): one round of the big kernel
 
 template <int BM, int BN, int BK, int WM, int WN, int NBUF, int OCC = WM * WN / 2>
 static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hipStream_t stream) {
@@ -556,9 +584,31 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
   }
   a.tile_start[n] = total;
   a.total_tiles = total;
+  a.main_tiles = total;
+  a.ksplit = 1;
   if (total == 0) return;
+  int grid_size = total;
+  if (BM == 128 && g_gemm_splitk != 0 && total > g_gemm_slots) {
+    // the last partial round of workgroups: split its tiles' K range so it
+    // finishes in 1/s of a tile time; needs beta == 1 (partials are added into C)
+    // and >= 256 of K per chunk (fewer flops per added byte would be bound by
+    // the chip's f64 atomic rate)
+    const int tail = total % g_gemm_slots;
+    int kmin = 1 << 30;
+    bool ok = tail > 0 && 2 * tail <= g_gemm_slots;
+    for (int i = 0; ok && i < n; ++i) {
+      ok = descs[i].beta == 1.0;
+      kmin = std::min(kmin, descs[i].k);
+    }
+    const int s = ok ? std::min({g_gemm_slots / std::max(tail, 1), kmin / 256, 8}) : 1;
+    if (s >= 2) {
+      a.main_tiles = total - tail;
+      a.ksplit = s;
+      grid_size = a.main_tiles + tail * s;
+    }
+  }
   const int mode = (descs[0].transA ? 2 : 0) | (descs[0].transB ? 1 : 0);
-  const dim3 grid(total), block(WM * WN * 64);
+  const dim3 grid(grid_size), block(WM * WN * 64);
 #define PARSEC_GEMM_LAUNCH(TA, TB)                                                                                    \
   do {                                                                                                                \
     if (full) hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, OCC>), grid, block, 0, stream, a); \
@@ -583,7 +633,22 @@ static void gemm_policy_init() {
     g_gemm_full = e ? atoi(e) : 1;
     e = getenv("PARSEC_GEMM_BIG_TILES");
     if (e) g_gemm_big_tiles = atoi(e);
+    e = getenv("PARSEC_GEMM_SPLITK");
+    g_gemm_splitk = e ? atoi(e) : 0;  // enabled once validated on the box (tests/test_headline_gpu.py)
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+      g_gemm_slots = 2 * ncu;
+    e = getenv("PARSEC_GEMM_SLOTS");
+    if (e) g_gemm_slots = std::max(1, atoi(e));
   }
+}
+
+// Split-K tail of the 128x128 kernel on (1) / off (0), < 0 queries; returns the previous setting.
+int gemm_splitk(int on) {
+  gemm_policy_init();
+  const int prev = g_gemm_splitk;
+  if (on >= 0) g_gemm_splitk = on;
+  return prev;
 }
 
 // Tile-size policy of the grouped GEMM (0 = auto, 64, 128); returns the previous one.
@@ -1182,6 +1247,7 @@ void* test_ws(size_t bytes) {
 
 extern "C" {
 int parsec_amd_gemm_tile_policy(int p) { return parsec::kern::gemm_tile_policy(p); }
+int parsec_amd_gemm_splitk(int on) { return parsec::kern::gemm_splitk(on); }
 // barrier clocks of the last fused tile POTRF run through the test entry points
 int parsec_amd_potrf_timing(long long* out, int n) {
   std::lock_guard<std::mutex> g(g_ws_m);

@@ -1,6 +1,7 @@
 #include "ptg.hpp"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 
 #include "../comm/comm.hpp"
@@ -467,21 +468,34 @@ void PtgTaskClass::reshape_inputs(Task* t) const {
 
 // Copy `src` into the collection's own copy of `home` (final write of a flow
 // into a collection position it did not come from).
+static int g_trace_writeback = -1;
 static void write_back(Data* home, DataCopy* src) {
+  if (g_trace_writeback < 0) g_trace_writeback = (int)ParamRegistry::instance().reg_int("ptg", "", "trace_writeback", "Log every final write of a flow into a collection tile (debug)", 0);
+  if (g_trace_writeback)
+    std::fprintf(stderr, "[writeback] home key %llu owner_dev %d src %p dev %d orig==home %d home copies:%s%s\n", (unsigned long long)(home ? home->key : 0),
+                 home ? home->owner_device : -9, src ? src->device_private : nullptr, src ? src->device_index : -9, (int)(home && src && src->original == home),
+                 home && home->copy(0) ? " host" : "", home && home->copy(home->owner_device > 0 ? home->owner_device : 1) ? " dev" : "");
   if (!home || !src || src->original == home) return;
   int hd = home->owner_device >= 0 ? home->owner_device : 0;
   DataCopy* dst = home->copy(hd);
   if (!dst) dst = home->copy(0);
   if (!dst) return;
   size_t n = std::min(home->nb_elts, src->original ? src->original->nb_elts : home->nb_elts);
+  if (g_trace_writeback) std::fprintf(stderr, "[writeback]   -> dst %p dev %d bytes %zu\n", dst->device_private, dst->device_index, n);
   device_memcpy(dst->device_index, dst->device_private, src->device_index, src->device_private, n);
   std::lock_guard<SpinLock> g(home->lock);
   dst->version = home->newest_version() + 1;
 }
 
 // --------------------------------------------------------- release (hot)
+// Simulation mode: completion date of the task whose successors are being
+// activated; every activation (not only the last one) raises the successor's
+// start date, so a task starts after its slowest predecessor (reference PARSEC_SIM).
+static thread_local uint64_t t_sim_release_date = 0;
+
 int PtgTaskClass::complete_execution(ExecutionStream* es, Task* t) const {
   PtgTaskpool* tp = owner;
+  t_sim_release_date = tp->context->simulation ? t->sim_exec_date + (uint64_t)sim_cost(t) : 0;
   const uint32_t my = (uint32_t)tp->context->my_rank;
   std::vector<Task*> ready;
   RemoteDepsMsg* msg = nullptr;
@@ -545,11 +559,8 @@ int PtgTaskClass::complete_execution(ExecutionStream* es, Task* t) const {
     delete msg;
   }
   PARSEC_PINS(es, PINS_RELEASE_DEPS_END, t);
-  if (!ready.empty()) {
-    if (tp->context->simulation)
-      for (Task* n : ready) n->sim_exec_date = std::max(n->sim_exec_date, t->sim_exec_date + (uint64_t)sim_cost(t));
-    schedule_tasks(es, ready.data(), (int)ready.size(), 0);
-  }
+  t_sim_release_date = 0;
+  if (!ready.empty()) schedule_tasks(es, ready.data(), (int)ready.size(), 0);
   release_task(es, t);
   return 0;
 }
@@ -888,6 +899,7 @@ void PtgTaskpool::activate(ExecutionStream* es, PtgTaskClass* tc, const int32_t*
       if (dynamic_termdet) tdm->taskpool_addto_nb_tasks(this, 1);
       slot = task;
     }
+    if (t_sim_release_date > task->sim_exec_date) task->sim_exec_date = t_sim_release_date;
     if (data && flow >= 0) {
       if (task->data[flow].data_in) data_copy_release(task->data[flow].data_in);
       data_copy_retain(data);

@@ -25,6 +25,7 @@ using namespace parsec;
 
 extern "C" int parsec_amd_dgemm_batch(const GemmDesc* descs, int n, void* stream);
 extern "C" int parsec_amd_gemm_tile_policy(int p);
+extern "C" int parsec_amd_gemm_splitk(int on);
 extern "C" int parsec_amd_potrf_timing(long long* out, int n);
 extern "C" int parsec_amd_dtrsm_batch(const TrsmDesc* descs, int n, void* stream);
 extern "C" int parsec_amd_dpotrf_tile(double* A, int n, int lda, int* info, void* stream);
@@ -600,6 +601,7 @@ PYBIND11_MODULE(_C, m) {
     return parsec_amd_dgemm_batch(v.data(), (int)v.size(), (void*)stream);
   });
   m.def("kernel_gemm_tile_policy", [](int p) { return parsec_amd_gemm_tile_policy(p); });
+  m.def("kernel_gemm_splitk", [](int on) { return parsec_amd_gemm_splitk(on); }, "split-K tail of the 128x128 grouped DGEMM: 1 on, 0 off, -1 query; returns the previous setting");
   m.def("kernel_potrf_timing", [](int n) {
     std::vector<long long> v(n, 0);
     if (parsec_amd_potrf_timing(v.data(), n) != 0) v.clear();

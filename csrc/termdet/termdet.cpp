@@ -78,7 +78,9 @@ class UserTriggerTermdet : public TermdetModule {
     tp->nb_tasks.store(0);
     tp->nb_pending_actions.store(0);
     tp->termdet_state.store(TERMDET_NOT_READY);
+    delete static_cast<TermdetCallback*>(tp->termdet_private);  // re-monitoring replaces the callback
     tp->termdet_private = new TermdetCallback{std::move(cb)};
+    std::lock_guard<std::mutex> g(m_);
     triggered_.erase(tp);
   }
   void release_taskpool(Taskpool* tp) override {

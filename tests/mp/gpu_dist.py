@@ -103,32 +103,55 @@ def case_dgeqrf(pa, torch, rank, size, job, N, nb, P, outdir):
     A = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=1, device=gpu, ptr=storeA.data_ptr())
     T = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=1, device=gpu, ptr=storeT.data_ptr())
     g = torch.Generator().manual_seed(77)
-    Afull = (torch.rand((N, N), dtype=torch.float64, generator=g) - 0.5).cuda()
+    Ahost = torch.rand((N, N), dtype=torch.float64, generator=g) - 0.5
+    Afull = Ahost.cuda()
+    # host reference R (rows sign-normalised against ours below)
+    Rref = np.linalg.qr(Ahost.numpy(), mode="r")
     tiles = storeA.view(-1, nb, nb)
-    for n in range(NT):
+    repeat = int(os.environ.get("REPEAT", "1"))
+    nbad = 0
+    for rep in range(repeat):
+        for n in range(NT):
+            for m in range(NT):
+                li = A.local_index(m, n)
+                if li >= 0:
+                    tiles[li].copy_(Afull[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb].t())
+        storeT.zero_()
+        torch.cuda.synchronize()
+        if size > 1:
+            pa.comm_barrier()
+        tp = pa.dgeqrf_new(A, T, 32)
+        ctx.add_taskpool(tp)
+        ctx.start()
+        ctx.wait()
+        # this rank's tiles of R (upper triangle of the tiles with m <= n), zeros elsewhere
+        Rrows = torch.zeros((N, N), dtype=torch.float64, device="cuda")
         for m in range(NT):
-            li = A.local_index(m, n)
-            if li >= 0:
-                tiles[li].copy_(Afull[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb].t())
-    torch.cuda.synchronize()
-    tp = pa.dgeqrf_new(A, T, 32)
-    ctx.add_taskpool(tp)
-    ctx.start()
-    ctx.wait()
-    # this rank's tiles of R (upper triangle of the tiles with m <= n), zeros elsewhere
-    Rrows = torch.zeros((N, N), dtype=torch.float64, device="cuda")
-    for m in range(NT):
-        for n in range(m, NT):
-            li = A.local_index(m, n)
-            if li >= 0:
-                t = tiles[li].t()
-                Rrows[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb] = torch.triu(t) if m == n else t
-    part = Rrows.cpu().numpy()
+            for n in range(m, NT):
+                li = A.local_index(m, n)
+                if li >= 0:
+                    t = tiles[li].t()
+                    Rrows[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb] = torch.triu(t) if m == n else t
+        part = Rrows.cpu().numpy()
+        bad = []
+        for m in range(NT):
+            if A.local_index(m, m) < 0:
+                continue
+            rows = slice(m * nb, (m + 1) * nb)
+            sg = np.sign(np.diag(part[rows, rows])) * np.sign(np.diag(Rref[rows, rows]))
+            for n in range(m, NT):
+                cols = slice(n * nb, (n + 1) * nb)
+                e = np.abs(sg[:, None] * part[rows, cols] - Rref[rows, cols]).max() / np.abs(Rref).max()
+                if e > 1e-10:
+                    bad.append((m, n, f"{e:.1e}"))
+        if bad:
+            nbad += 1
+            print(f"rank {rank} rep {rep} bad R tiles {bad[:16]} ({len(bad)} total)", flush=True)
     ctx.fini()
     pa.comm_fini()
     np.save(os.path.join(outdir, f"R{rank}.npy"), part)
-    print(f"rank {rank} dgeqrf done", flush=True)
-    return True
+    print(f"rank {rank} dgeqrf done bad_reps {nbad}/{repeat}", flush=True)
+    return nbad == 0
 
 
 def case_stencil(pa, torch, rank, size, job, nx, ny, nz, b, iters):

@@ -80,6 +80,35 @@ def test_dgemm_batch_128_mixed_syrk_gemm(pa):
             assert ((C - ref).abs().max() / ref.abs().max()).item() < 1e-14
 
 
+@pytest.mark.parametrize("syrk", [False, True])
+def test_dgemm_batch_split_k_tail(pa, syrk):
+    """9 descriptors of 1024^3 = 576 128-tiles on 512 resident slots: the 64 tiles
+    of the second round are split 4 ways along K and accumulated into C with f64
+    atomics (beta = 1); every element must match the fp64 reference."""
+    dev = _dev()
+    g = torch.Generator(device=dev).manual_seed(21)
+    n, cnt = 1024, 9
+    As = [_cm(n, n, dev, g) for _ in range(cnt)]
+    Bs = As if syrk else [_cm(n, n, dev, g) for _ in range(cnt)]
+    Cs = [_cm(n, n, dev, g) for _ in range(cnt)]
+    C0 = [C.clone() for C in Cs]
+    refs = [C - A @ B.t() for A, B, C in zip(As, Bs, Cs)]
+    descs = [(A.data_ptr(), B.data_ptr(), C.data_ptr(), n, n, n, n, n, n, -1.0, 1.0, 1, int(syrk)) for A, B, C in zip(As, Bs, Cs)]
+    prev = pa.kernel_gemm_splitk(1)
+    try:
+        assert pa.kernel_dgemm_batch(descs, _stream()) == 0
+        torch.cuda.synchronize()
+    finally:
+        pa.kernel_gemm_splitk(prev)
+    low = torch.tril(torch.ones(n, n, dtype=torch.bool, device=dev))
+    for C, ref, c0 in zip(Cs, refs, C0):
+        if syrk:
+            assert ((C[low] - ref[low]).abs().max() / ref[low].abs().max()).item() < 1e-14
+            assert torch.equal(C[~low], c0[~low])
+        else:
+            assert ((C - ref).abs().max() / ref.abs().max()).item() < 1e-14
+
+
 def test_dgemm_batch_big_tiles_forced_edge(pa):
     """128x128 kernel on ragged shapes (non-FULL path with bounds checks)."""
     dev = _dev()

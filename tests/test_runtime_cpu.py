@@ -401,3 +401,110 @@ def test_template_device(pa):
     ctx.fini()
     assert ran == ["template"] * 5
     assert devs["template"]["executed_tasks"] >= 5
+
+
+# ----------------------------------------------------------- simulation
+@pytest.mark.parametrize("NT", [1, 4, 6])
+def test_simulation_critical_path(pa, NT):
+    """runtime_simulation=1 (reference PARSEC_SIM): every task costs 1 and starts
+    after its slowest predecessor, so the taskpool's simulation date is the
+    critical path of tiled Cholesky, POTRF(0) -> TRSM(1,0) -> SYRK(1,1) -> POTRF(1)
+    ... = 3 (NT - 1) + 1 tasks, whatever the thread count or the schedule."""
+    pa.mca_set("runtime_simulation", "1")
+    try:
+        ctx = _ctx(pa, 4)
+    finally:
+        pa.mca_unset("runtime_simulation")
+    nb = 8
+    A, S = _spd_matrix(pa, NT * nb, nb, 3)
+    tp, info = pa.dpotrf_new(A, pa.MATRIX_LOWER)
+    ctx.add_taskpool(tp)
+    ctx.start()
+    ctx.wait()
+    date = tp.simulation_date
+    ctx.fini()
+    assert pa.read_int(info) == 0
+    assert date == 3 * (NT - 1) + 1
+
+
+# --------------------------------------------------------- user_trigger
+def test_user_trigger_termdet(pa):
+    """termdet user_trigger (reference mca/termdet/user_trigger): the taskpool
+    stays alive after all of its tasks completed, until a task declares
+    termination; pending runtime actions still delay it."""
+    import time
+
+    ctx = _ctx(pa, 2)
+    tp = pa._C.DtdTaskpool()
+    tp.termdet = "user_trigger"
+    ctx.add_taskpool(tp)
+    ctx.start()
+    A = _vector_tiles(pa, 1)
+    t = tp.tile_of(A, A.data_key([0, 0]))
+    ran = []
+
+    def body(task):
+        ran.append(task.seq)
+        return 0
+
+    for _ in range(10):
+        pa.insert_task(tp, body, [(t, pa.INOUT | pa.AFFINITY)])
+    deadline = time.time() + 10
+    while len(ran) < 10 and time.time() < deadline:
+        time.sleep(0.01)
+    time.sleep(0.05)
+    assert len(ran) == 10
+    assert not tp.completed  # every task done, termination not declared yet
+
+    def trigger(task):
+        task.user_trigger_termination()
+        return 0
+
+    pa.insert_task(tp, trigger, [(t, pa.INOUT | pa.AFFINITY)])
+    tp.data_flush_all(A)
+    ctx.wait()
+    assert tp.completed
+    ctx.fini()
+
+
+# ------------------------------------------------- PINS: checkers / steals
+def test_pins_iterators_checker(pa):
+    """iterators_checker (reference mca/pins/iterators_checker): for every executed
+    task, each successor named by iterate_successors lists the task among its
+    predecessors; a tiled Cholesky has no mismatch."""
+    pa.mca_set("mca_pins", "iterators_checker")
+    try:
+        ctx = _ctx(pa, 3)
+    finally:
+        pa.mca_unset("mca_pins")
+    NT, nb = 5, 8
+    A, S = _spd_matrix(pa, NT * nb, nb, 11)
+    tp, info = pa.dpotrf_new(A, pa.MATRIX_LOWER)
+    ctx.add_taskpool(tp)
+    ctx.start()
+    ctx.wait()
+    counters = dict(pa.pins_counters())
+    ctx.fini()
+    assert pa.read_int(info) == 0
+    assert counters.get("iterators_checker.ok", 0) > NT * NT
+    assert counters.get("iterators_checker.mismatch", 0) == 0
+
+
+def test_pins_print_steals(pa):
+    """print_steals (reference mca/pins/print_steals): per-thread selected / stolen
+    counts are reported when the threads finish."""
+    pa.mca_set("mca_pins", "print_steals")
+    try:
+        ctx = _ctx(pa, 4)
+    finally:
+        pa.mca_unset("mca_pins")
+    A = _vector_tiles(pa, 64)
+    tp = pa.dtd_taskpool(ctx)
+    ctx.start()
+    for i in range(64):
+        pa.insert_task(tp, lambda task: 0, [(tp.tile_of(A, A.data_key([i, 0])), pa.INOUT | pa.AFFINITY)])
+    tp.data_flush_all(A)
+    ctx.wait()
+    ctx.fini()
+    steals = {k: v for k, v in pa.pins_counters() if k.startswith("steals.thread")}
+    assert len(steals) >= 1 and all(v >= 0 for v in steals.values())
