@@ -100,6 +100,8 @@ def main():
     ap.add_argument("--cores", type=int, default=int(os.environ.get("PARSEC_BENCH_CORES", "4")))
     ap.add_argument("--check", action="store_true", help="verify the factorization (small N only)")
     ap.add_argument("--mca", nargs=2, action="append", default=[])
+    ap.add_argument("--taskpool", choices=["ir", "jdf"], default="ir",
+                    help="ir: DAG built in C++ (csrc/algos/dpotrf.cpp); jdf: the same DAG compiled by parsec-ptgpp from csrc/algos/jdf/dpotrf_L.jdf")
     ap.add_argument("--share-gpu", action="store_true",
                     help="validation mode: every rank uses GPU 0 (torch gloo, shm data plane instead of RCCL)")
     args = ap.parse_args()
@@ -168,7 +170,7 @@ def main():
     def step():
         store.copy_(backup)
         torch.cuda.synchronize()
-        tp, info = pa.dpotrf_new(A, pa.MATRIX_LOWER)
+        tp, info = pa.dpotrf_jdf_new(A) if args.taskpool == "jdf" else pa.dpotrf_new(A, pa.MATRIX_LOWER)
         ctx.add_taskpool(tp)
         ctx.start()
         _stage("taskpool started")
@@ -268,7 +270,7 @@ def main():
             "dtype": "fp64",
             "data": "synthetic random symmetric + N*I (DPLASMA plgsy convention), HBM-resident tiles",
             "residual": float(f"{resid:.3e}"),
-            "config": {"model": "tiled DPOTRF lower (PTG)", "N": N, "nb": nb, "global_batch": 1, "seq_len": N,
+            "config": {"model": "tiled DPOTRF lower (PTG)" if args.taskpool == "ir" else "tiled DPOTRF lower (PTG, ptgpp-compiled dpotrf_L.jdf)", "N": N, "nb": nb, "global_batch": 1, "seq_len": N,
                        "parallelism": f"2D block-cyclic P{P}xQ{Q}, 1 process/GPU", "threads_per_rank": args.cores},
         }
         if check is not None:

@@ -13,6 +13,9 @@ namespace algos {
 // Tiled Cholesky A = L L^T (lower) on a (Sym)BlockCyclic collection, PTG form.
 // `info_host` receives the LAPACK-style info after completion (0 = success).
 ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host);
+// The same factorization from the JDF source algos/jdf/dpotrf_L.jdf, compiled by
+// parsec-ptgpp at build time (lower only, W = L^-1 panel solves).
+ptg::PtgTaskpool* dpotrf_jdf_new(TiledMatrix* A, int* info_host);
 // Tiled GEMM C = alpha op(A) op(B) + beta C (PTG; B transposed if transB).
 ptg::PtgTaskpool* dgemm_new(double alpha, TiledMatrix* A, TiledMatrix* B, double beta, TiledMatrix* C, int transB);
 // Tiled QR A = QR (Householder, tile algorithm GEQRT/TSQRT/UNMQR/TSMQR). T holds

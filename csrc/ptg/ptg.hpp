@@ -220,6 +220,12 @@ class PtgTaskpool : public Taskpool {
   int64_t remote_writebacks_expected = 0;  // final tile versions other ranks send here
   bool finalized = false;
   bool options_resolved = false;
+  // called once the taskpool completed (wrappers of generated taskpools read
+  // back results here, e.g. the LAPACK info of a factorization)
+  std::function<void()> complete_hook;
+  void on_complete_internal() override {
+    if (complete_hook) complete_hook();
+  }
   PtgTaskpool();
   ~PtgTaskpool() override;
   PtgTaskClass* add_task_class(TaskClassDef def);

@@ -469,6 +469,13 @@ PYBIND11_MODULE(_C, m) {
         tp->destructor_hook = [info]() { delete info; };
         return py::make_tuple(py::cast(tp, py::return_value_policy::take_ownership), (uintptr_t)info);
       });
+  m.def("dpotrf_jdf_new", [](TiledMatrix* A) {
+        auto* info = new int(0);
+        auto* tp = algos::dpotrf_jdf_new(A, info);
+        auto prev = tp->destructor_hook;
+        tp->destructor_hook = [info, prev]() { if (prev) prev(); delete info; };
+        return py::make_tuple(py::cast(tp, py::return_value_policy::take_ownership), (uintptr_t)info);
+      }, "tiled Cholesky (lower) from the ptgpp-compiled algos/jdf/dpotrf_L.jdf; returns (taskpool, info address)");
   m.def("dgeqrf_new", [](TiledMatrix* A, TiledMatrix* T, int ib) { return algos::dgeqrf_new(A, T, ib); }, py::arg("A"), py::arg("T"), py::arg("ib") = 0,
         py::return_value_policy::take_ownership);
   py::class_<algos::StencilGrid, DataCollection>(m, "StencilGrid")

@@ -48,6 +48,7 @@ CORE_SOURCES = [
     "csrc/algos/collection_ops.cpp",
     "csrc/algos/dtd_builtins.cpp",
     "csrc/capi/capi.cpp",
+    "csrc/algos/dpotrf_jdf.cpp",
 ]
 HIP_SOURCES = [
     "csrc/kernels/tile_kernels.hip",
@@ -56,6 +57,11 @@ HIP_SOURCES = [
 ]
 PY_SOURCES = ["csrc/python/bindings.cpp"]
 PTGPP_SOURCES = ["tools/ptgpp/ptgpp.cpp"]
+# Taskpools written in the JDF language: compiled by parsec-ptgpp into build/gen
+# and linked into the runtime library (reference: DPLASMA ships its *.jdf the same way)
+JDF_SOURCES = ["csrc/algos/jdf/dpotrf_L.jdf"]
+# runtime sources that include generated JDF headers
+JDF_USERS = ["csrc/algos/dpotrf_jdf.cpp"]
 TEST_SOURCES = ["tests/native/test_containers.cpp"]
 
 
@@ -103,10 +109,32 @@ def generate():
         "  deps = gcc",
         "  description = PYCXX $out",
     ]
-    objs = []
+    lines += [
+        "rule ptgpp",
+        f"  command = {PKG}/bin/parsec-ptgpp -i $in -o $base -f $fname",
+        "  description = PTGPP $in",
+    ]
+    ptgpp_exe = os.path.join(PKG, "bin", "parsec-ptgpp")
+    gen = os.path.join(BUILD, "gen")
+    gen_headers, objs = [], []
+    for src in _exists(JDF_SOURCES):
+        name = os.path.splitext(os.path.basename(src))[0]
+        base = os.path.join(gen, name)
+        lines.append(f"build {base}.cpp {base}.h: ptgpp {os.path.join(ROOT, src)} | {ptgpp_exe}")
+        lines.append(f"  base = {base}")
+        lines.append(f"  fname = {name}")
+        obj = os.path.join("obj", "gen_" + name + ".o")
+        lines.append(f"build {obj}: cxx {base}.cpp")
+        lines.append(f"  cxxflags = {common} -I{gen} -Wno-unused-variable -Wno-unused-but-set-variable")
+        objs.append(obj)
+        gen_headers.append(base + ".h")
     for src in _exists(CORE_SOURCES):
         obj = os.path.join("obj", src.replace("/", "_") + ".o")
-        lines.append(f"build {obj}: cxx {os.path.join(ROOT, src)}")
+        if src in JDF_USERS:
+            lines.append(f"build {obj}: cxx {os.path.join(ROOT, src)} || {' '.join(gen_headers)}")
+            lines.append(f"  cxxflags = {common} -I{gen}")
+        else:
+            lines.append(f"build {obj}: cxx {os.path.join(ROOT, src)}")
         objs.append(obj)
     for src in _exists(HIP_SOURCES):
         obj = os.path.join("obj", src.replace("/", "_") + ".o")
@@ -167,7 +195,7 @@ def generate_sanitized(kind):
     libs = f"-fsanitize={kind} -L{ROCM}/lib -lamdhip64 -lrccl -latomic -lpthread -lrt -Wl,-rpath,{ROCM}/lib"
     lines = [
         "rule cxx",
-        f"  command = g++ {flags} -MMD -MF $out.d -c $in -o $out",
+        f"  command = g++ {flags} $flags_extra -MMD -MF $out.d -c $in -o $out",
         "  depfile = $out.d",
         "  deps = gcc",
         "  description = CXX[" + kind + "] $out",
@@ -182,9 +210,18 @@ def generate_sanitized(kind):
         "  description = LINK $out",
     ]
     objs = []
+    gen = os.path.join(BUILD, "gen")  # generated by the main build (run it first)
+    for src in _exists(JDF_SOURCES):
+        name = os.path.splitext(os.path.basename(src))[0]
+        obj = os.path.join(out, "obj", "gen_" + name + ".o")
+        lines.append(f"build {obj}: cxx {os.path.join(gen, name + '.cpp')}")
+        lines.append(f"  flags_extra = -I{gen}")
+        objs.append(obj)
     for src in _exists(CORE_SOURCES):
         obj = os.path.join(out, "obj", src.replace("/", "_") + ".o")
         lines.append(f"build {obj}: cxx {os.path.join(ROOT, src)}")
+        if src in JDF_USERS:
+            lines.append(f"  flags_extra = -I{gen}")
         objs.append(obj)
     # device kernels: the main build's objects (host stubs only, not instrumented)
     for src in _exists(HIP_SOURCES):
@@ -211,6 +248,7 @@ def generate_sanitized(kind):
 def build_sanitized(kind, jobs=None):
     """Build the instrumented runtime (needs the main build's kernel objects)."""
     need = [os.path.join(BUILD, "obj", s.replace("/", "_") + ".o") for s in _exists(HIP_SOURCES)]
+    need += [os.path.join(BUILD, "gen", os.path.splitext(os.path.basename(s))[0] + ".cpp") for s in _exists(JDF_SOURCES)]
     if not all(os.path.exists(p) for p in need):
         build(jobs)
     out = generate_sanitized(kind)

@@ -24,7 +24,10 @@ def main(rank, size, job, N, nb, P, Q, sched="lfq", topo="star", termdet="local"
             if A.rank_of([m, n]) == rank:
                 A.tile(m, n)[:, :] = S[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb]
                 A.mark_host_modified(m, n)
-    tp, info = pa.dpotrf_new(A, pa.MATRIX_LOWER)
+    if os.environ.get("DPOTRF_TASKPOOL") == "jdf":
+        tp, info = pa.dpotrf_jdf_new(A)  # ptgpp-compiled algos/jdf/dpotrf_L.jdf
+    else:
+        tp, info = pa.dpotrf_new(A, pa.MATRIX_LOWER)
     tp.termdet = termdet
     ctx.add_taskpool(tp)
     ctx.start()

@@ -12,9 +12,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 WORKER = os.path.join(HERE, "mp", "dist_dpotrf.py")
 
 
-def run_ranks(nranks, *args, timeout=120, worker=WORKER):
+def run_ranks(nranks, *args, timeout=120, worker=WORKER, env_extra=None):
     job = "pt" + uuid.uuid4().hex[:10]
-    env = dict(os.environ, PARSEC_MCA_device_hip_enabled="0")
+    env = dict(os.environ, PARSEC_MCA_device_hip_enabled="0", **(env_extra or {}))
     procs = [subprocess.Popen([sys.executable, worker, str(r), str(nranks), job, *map(str, args)],
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
              for r in range(nranks)]
@@ -39,6 +39,19 @@ def run_ranks(nranks, *args, timeout=120, worker=WORKER):
 ])
 def test_distributed_dpotrf(pa, nranks, P, Q, topo, termdet):
     outs = run_ranks(nranks, 512, 64, P, Q, "lfq", topo, termdet)
+    for rc, out in outs:
+        assert rc == 0, out
+
+
+@pytest.mark.parametrize("nranks,P,Q,mode", [
+    (2, 2, 1, {}),
+    (4, 2, 2, {"PARSEC_MCA_ptg_deps_mask": "1"}),
+    (3, 3, 1, {"PARSEC_MCA_ptg_dep_management": "dynamic-hash-table"}),
+])
+def test_distributed_dpotrf_jdf(pa, nranks, P, Q, mode):
+    """The ptgpp-compiled dpotrf_L.jdf over several ranks (remote activations
+    into index-array / hash storage, counter / mask tracking)."""
+    outs = run_ranks(nranks, 384, 64, P, Q, "lfq", "star", "local", env_extra=dict(mode, DPOTRF_TASKPOOL="jdf"))
     for rc, out in outs:
         assert rc == 0, out
 

@@ -167,3 +167,34 @@ def test_dpotrf_illconditioned_nb1024(pa, trsm_inverse):
     finally:
         ctx.fini()
         pa.mca_unset("dpotrf_trsm_inverse")
+
+
+@pytest.mark.parametrize("N,nb", [(4096, 512), (8192, 1024)])
+def test_dpotrf_jdf_gpu(pa, N, nb):
+    """The ptgpp-compiled dpotrf_L.jdf with its BODY [type = HIP] chores on the
+    MI355X (same batched kernels as the C++ IR taskpool), host LAPACK oracle."""
+    dev = _dev()
+    NT = N // nb
+    S = _illcond_spd(N, 1e6, dev, seed=8)
+    ctx = pa.init(3)
+    try:
+        gpu = pa.first_gpu_device_index()
+        store = torch.empty((NT, NT, nb, nb), dtype=torch.float64, device=dev)
+        store.copy_(S.reshape(NT, nb, NT, nb).permute(2, 0, 3, 1))
+        A = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb, nb, N, N, device=gpu, ptr=store.data_ptr())
+        torch.cuda.synchronize()
+        tp, info = pa.dpotrf_jdf_new(A)
+        ctx.add_taskpool(tp)
+        ctx.start()
+        ctx.wait()
+        assert pa.read_int(info) == 0
+        stats = [d for d in pa.devices() if d["type"] == pa.DEV_HIP][0]
+        assert stats["executed_tasks"] > 0
+        L = torch.tril(store.permute(1, 3, 0, 2).reshape(N, N))
+        backward = (torch.linalg.norm(L @ L.t() - S) / torch.linalg.norm(S)).item()
+        Lref = torch.linalg.cholesky(S.cpu()).to(dev)
+        backward_ref = (torch.linalg.norm(Lref @ Lref.t() - S) / torch.linalg.norm(S)).item()
+        print(f"jdf N={N} nb={nb} backward={backward:.3e} (torch {backward_ref:.3e})")
+        assert backward < max(20 * backward_ref, 1e-15)
+    finally:
+        ctx.fini()

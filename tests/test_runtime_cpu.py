@@ -508,3 +508,36 @@ def test_pins_print_steals(pa):
     ctx.fini()
     steals = {k: v for k, v in pa.pins_counters() if k.startswith("steals.thread")}
     assert len(steals) >= 1 and all(v >= 0 for v in steals.values())
+
+
+# ------------------------------------------------ JDF-compiled DPOTRF (CPU)
+@pytest.mark.parametrize("NT,nb", [(1, 16), (6, 16), (9, 8)])
+def test_dpotrf_jdf_cpu(pa, NT, nb):
+    """algos/jdf/dpotrf_L.jdf, compiled by parsec-ptgpp into the runtime at build
+    time, factors like the hand-built IR (CPU bodies; W = L^-1 panel solves)."""
+    ctx = _ctx(pa, 4)
+    N = NT * nb
+    A, S = _spd_matrix(pa, N, nb, 5)
+    tp, info = pa.dpotrf_jdf_new(A)
+    assert tp.name == "dpotrf_L.jdf"
+    ctx.add_taskpool(tp)
+    ctx.start()
+    ctx.wait()
+    L = _lower_of(A, N, nb)
+    ctx.fini()
+    assert pa.read_int(info) == 0
+    assert np.linalg.norm(L @ L.T - S) / np.linalg.norm(S) < 1e-14
+
+
+def test_dpotrf_jdf_reports_info(pa):
+    """A matrix that is not positive definite: info = global index of the failing pivot."""
+    ctx = _ctx(pa, 2)
+    N, nb = 48, 16
+    A, S = _spd_matrix(pa, N, nb, 9)
+    A.tile(1, 1)[5, 5] = -1e6  # pivot 16 + 5 goes negative
+    tp, info = pa.dpotrf_jdf_new(A)
+    ctx.add_taskpool(tp)
+    ctx.start()
+    ctx.wait()
+    ctx.fini()
+    assert pa.read_int(info) == 16 + 6
