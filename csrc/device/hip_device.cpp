@@ -168,10 +168,36 @@ int bind_thread_to_gpu_numa(int ordinal) {
   return node;
 }
 
+// Blocking copy: returns once the bytes landed. hipMemcpy alone is NOT enough:
+// a device-to-device hipMemcpy may return before the copy ran (CUDA/HIP
+// semantics), and callers release or recycle the source right after (e.g. a
+// remote write-back from a pooled receive buffer, which the next receive then
+// overwrote: intermittent stale tiles in the 2-rank GPU QR). Each calling thread
+// copies on its own non-blocking stream and waits for it.
 int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t bytes) {
   if (dst_dev == 0 && src_dev == 0) { std::memcpy(dst, src, bytes); return 0; }
   hipMemcpyKind k = dst_dev == 0 ? hipMemcpyDeviceToHost : src_dev == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
-  hipError_t e = hipMemcpy(dst, src, bytes, k);
+  const int dev = dst_dev != 0 ? dst_dev : src_dev;
+  const int ord = device_hip_ordinal(dev);
+  thread_local hipStream_t s = nullptr;
+  thread_local int s_ord = -1;
+  if (ord >= 0 && (s == nullptr || s_ord != ord)) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(ord);
+    if (s) (void)hipStreamDestroy(s);
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+    s_ord = ord;
+    (void)hipSetDevice(cur);
+  }
+  hipError_t e;
+  if (s) {
+    e = hipMemcpyAsync(dst, src, bytes, k, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+  } else {
+    e = hipMemcpy(dst, src, bytes, k);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+  }
   return e == hipSuccess ? 0 : -1;
 }
 
