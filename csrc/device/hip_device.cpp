@@ -697,7 +697,36 @@ void HipDevice::epilog(GpuTask* g) {
   }
 }
 
-void HipDevice::complete(GpuTask* g) {
+namespace {
+// Internal task that releases a completed GPU task on a compute thread: the
+// dependency release of a finished batch (hundreds of activations when a panel
+// completes) then runs on every compute thread in parallel, by priority,
+// instead of serially on the manager between two launches.
+struct GpuCompleteClass : TaskClass {
+  GpuCompleteClass() {
+    name = "gpu_complete";
+    flags = TC_INTERNAL | TC_NO_PROFILE;
+    Chore ch;
+    ch.type = DEV_CPU;
+    ch.hook = [](ExecutionStream* es, Task* w) {
+      complete_task_execution(es, static_cast<Task*>(w->user));
+      return (int)HOOK_DONE;
+    };
+    chores.push_back(std::move(ch));
+  }
+  int complete_execution(ExecutionStream* es, Task* w) const override {
+    (void)es;
+    task_free(w);
+    return 0;
+  }
+};
+const GpuCompleteClass& gpu_complete_class() {
+  static GpuCompleteClass c;
+  return c;
+}
+}  // namespace
+
+void HipDevice::complete(GpuTask* g, bool small_group) {
   Task* t = g->task;
   PARSEC_DEBUG(kVerbNoisier, "hip", "completed %s", t->task_class->describe(t).c_str());
   for (int fi = 0; fi < kMaxFlows; ++fi) if (g->dev_copy[fi]) lru_touch(g->dev_copy[fi]);
@@ -706,8 +735,32 @@ void HipDevice::complete(GpuTask* g) {
   t->gpu = nullptr;
   if (g->ev_out) put_event(g->ev_out);
   delete g;
-  complete_task_execution(es, t);
+  // critical-path work (and tiny groups) is released here: its successors are
+  // few and the manager dispatches them to the GPU at once
+  const bool inline_release = small_group || t->priority >= critical_threshold;
+  if (complete_on_workers && !inline_release && ctx && !ctx->simulation && !ctx->all_es.empty()) {
+    Task* w = task_new(es, t->taskpool, &gpu_complete_class());
+    w->user = t;
+    w->priority = t->priority;
+    completions.push_back(w);
+  } else {
+    complete_task_execution(es, t);
+  }
   inflight.fetch_sub(1, std::memory_order_acq_rel);
+}
+
+void HipDevice::flush_completions() {
+  if (completions.empty()) return;
+  // straight to the compute threads' queues (schedule_tasks from a manager
+  // would try to dispatch GPU work inline)
+  std::stable_sort(completions.begin(), completions.end(), [](Task* a, Task* b) { return a->priority > b->priority; });
+  const int nes = (int)ctx->all_es.size();
+  std::vector<std::vector<Task*>> per(nes);
+  for (size_t i = 0; i < completions.size(); ++i) per[(rr_complete + i) % nes].push_back(completions[i]);
+  rr_complete += (uint32_t)completions.size();
+  for (int i = 0; i < nes; ++i)
+    if (!per[i].empty()) ctx->scheduler->schedule(ctx->all_es[i], per[i].data(), (int)per[i].size(), 0);
+  completions.clear();
 }
 
 bool HipDevice::progress() {
@@ -775,9 +828,10 @@ bool HipDevice::progress() {
           PARSEC_HIP_CHECK(hipEventRecord(g->ev_out, s_d2h));
           popping.push_back(g);
         } else {
-          complete(g);
+          complete(g, tasks.size() <= 2);
         }
       }
+      flush_completions();
       did = true;
     }
   }
@@ -791,9 +845,10 @@ bool HipDevice::progress() {
       std::lock_guard<SpinLock> lk(d->lock);
       if (DataCopy* host = d->copy(0)) { host->version = g->dev_copy[fi]->version; host->coherency_state = COHERENCY_SHARED; }
     }
-    complete(g);
+    complete(g, false);
     did = true;
   }
+  flush_completions();
   return did;
 }
 
@@ -836,6 +891,7 @@ void hip_devices_init(Context* ctx) {
   int rcus = (int)params.reg_int("device", "hip", "reserved_cus", "CUs reserved for the critical-path stream (0 = no CU masking; measured slower on MI355X)", 0);
   int xcrit = (int)params.reg_int("device", "hip", "critical_streams", "Additional critical-path streams used when the critical stream is busy", 7);
   const bool trace = params.reg_int("device", "hip", "trace_launches", "Print every launched kernel group (stream, tasks, batch sizes) to stderr", 0) != 0;
+  const bool cow = params.reg_int("device", "hip", "complete_on_workers", "Release completed GPU tasks (successor activation) on the compute threads instead of the manager (measured no faster on DPOTRF; breaks the multi-rank DTD stencil: off)", 0) != 0;
   int maxg = (int)params.reg_int("device", "hip", "max_inflight_batches", "Launched kernel groups per bulk stream before new bulk tasks wait for a larger batch (0 = no limit)", 2);
   if (enabled == 0) return;
   int count = 0;
@@ -861,6 +917,7 @@ void hip_devices_init(Context* ctx) {
     d->max_inflight_groups = maxg;
     d->extra_crit_streams = std::max(0, xcrit);
     d->sort_pending = sortp != 0;
+    d->complete_on_workers = cow;
     d->trace_launches = trace;
     reg.add(d);
     g_hip_devices.push_back(d);

@@ -111,6 +111,12 @@ struct HipDevice : Device {
   bool cu_masked = false;
   bool batching = true;
   bool sort_pending = true;
+  // completed GPU tasks are released (successor activation) by the compute
+  // threads instead of the manager, which keeps launching critical work
+  bool complete_on_workers = false;
+  std::vector<Task*> completions;  // release tasks gathered during one progress pass
+  uint32_t rr_complete = 0;
+  void flush_completions();
   bool trace_launches = false;
   uint32_t rr_stream = 0;
   int extra_crit_streams = 7;   // additional critical streams (see start())
@@ -133,7 +139,7 @@ struct HipDevice : Device {
   int stage_in(GpuTask* g);
   void finish_stage_in(GpuTask* g);
   void execute_ready();
-  void complete(GpuTask* g);
+  void complete(GpuTask* g, bool small_group);
   void epilog(GpuTask* g);
   void* cache_alloc(size_t bytes);
   void ensure_zone();  // zone_m held

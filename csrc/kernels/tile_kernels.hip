@@ -569,6 +569,7 @@ static int g_gemm_full = -1;         // PARSEC_GEMM_FULL=0 disables the unchecke
 static int g_gemm_big_tiles = 384;   // PARSEC_GEMM_BIG_TILES: 128x128 tiles in a launch to pick the big kernel
 static int g_gemm_splitk = -1;       // PARSEC_GEMM_SPLITK=0 disables the split-K tail of the 128x128 kernel
 static int g_gemm_slots = 512;       // resident 128x128 workgroups (2 per CU): one round of the big kernel
+static int g_gemm_chunk_fill = -1;   // PARSEC_GEMM_CHUNK_FILL=0: fixed 40-descriptor launches
 
 template <int BM, int BN, int BK, int WM, int WN, int NBUF, int OCC = WM * WN / 2>
 static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hipStream_t stream) {
@@ -634,10 +635,12 @@ static void gemm_policy_init() {
     e = getenv("PARSEC_GEMM_BIG_TILES");
     if (e) g_gemm_big_tiles = atoi(e);
     e = getenv("PARSEC_GEMM_SPLITK");
-    g_gemm_splitk = e ? atoi(e) : 0;  // enabled once validated on the box (tests/test_headline_gpu.py)
+    g_gemm_splitk = e ? atoi(e) : 1;  // validated: tests/test_headline_gpu.py, profiles/r2_bench_ab_fill_splitk.log
     int dev = 0, ncu = 0;
     if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
       g_gemm_slots = 2 * ncu;
+    e = getenv("PARSEC_GEMM_CHUNK_FILL");
+    g_gemm_chunk_fill = e ? atoi(e) : 1;
     e = getenv("PARSEC_GEMM_SLOTS");
     if (e) g_gemm_slots = std::max(1, atoi(e));
   }
@@ -683,12 +686,36 @@ static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) 
   }
 }
 
+// Descriptors per launch (<= kMaxGemmBatch, the kernel-argument limit): the cut
+// that fills whole rounds of resident 128x128 workgroups best. 40 tiles of
+// 512^2 are 640 128-tiles = 1.25 rounds of 512 slots (62 % of the second round
+// idle); 32 of them are exactly one round.
+static int gemm_chunk_size(const GemmDesc* d, int n) {
+  const int cap = std::min(n, kMaxGemmBatch);
+  if (g_gemm_chunk_fill == 0) return cap;
+  int best = cap, tiles = 0;
+  double best_fill = -1.0;
+  for (int c = 1; c <= cap; ++c) {
+    tiles += ((d[c - 1].m + 127) / 128) * ((d[c - 1].n + 127) / 128);
+    if (tiles < g_gemm_slots) continue;
+    const int rounds = (tiles + g_gemm_slots - 1) / g_gemm_slots;
+    const double fill = (double)tiles / ((double)rounds * g_gemm_slots);
+    if (fill >= best_fill - 1e-9) { best_fill = fill; best = c; }  // ties: the larger cut
+  }
+  return best_fill >= 0.0 ? best : cap;
+}
+
 // Group descriptors by (transA, transB): one grouped launch per combination.
 void launch_gemm_batch(const GemmDesc* descs, int n, hipStream_t stream) {
+  gemm_policy_init();
   std::vector<GemmDesc> g[4];
   for (int i = 0; i < n; ++i) g[(descs[i].transA ? 2 : 0) | (descs[i].transB ? 1 : 0)].push_back(descs[i]);
   for (auto& v : g)
-    for (size_t s = 0; s < v.size(); s += kMaxGemmBatch) launch_gemm_chunk(v.data() + s, (int)std::min<size_t>(kMaxGemmBatch, v.size() - s), stream);
+    for (size_t s = 0; s < v.size();) {
+      const int c = gemm_chunk_size(v.data() + s, (int)(v.size() - s));
+      launch_gemm_chunk(v.data() + s, c, stream);
+      s += (size_t)c;
+    }
 }
 
 static constexpr int kTrsmRows = 16;

@@ -603,6 +603,7 @@ void PtgTaskpool::finalize() {
     options_resolved = true;
     resolve_runtime_options();
   }
+  index_store_mode = dep_management == "index-array";
   for (auto* tc : classes) {
     auto& d = tc->def;
     if (d.locals.size() > (size_t)kMaxLocals) fatal("task class %s has too many locals", d.name.c_str());

@@ -204,7 +204,7 @@ class PtgTaskpool : public Taskpool {
   // ptgpp --dep-management: "index-array" (dense per-class slot arrays, the
   // reference default) or "dynamic-hash-table" (sharded hash of pending tasks);
   // MCA ptg_dep_management overrides the compiled choice.
-  std::string dep_management = "dynamic-hash-table";
+  std::string dep_management = "index-array";
   bool deps_mask_default = false;  // ptgpp --deps-mask / MCA ptg_deps_mask
   // user %option nb_local_tasks_fn: total number of local tasks of the taskpool
   std::function<int64_t(const Taskpool*)> nb_local_tasks_fn;
@@ -238,7 +238,8 @@ class PtgTaskpool : public Taskpool {
   int64_t global(const std::string& n) const;
   void set_global(const std::string& n, int64_t v);
  private:
-  bool use_index_store() const { return dep_management == "index-array"; }
+  bool use_index_store() const { return index_store_mode; }
+  bool index_store_mode = false;  // dep_management == "index-array", resolved by finalize()
   template <class F>
   Task* with_pending(PtgTaskClass* tc, const int32_t* L, uint64_t key, F&& f);
 };
