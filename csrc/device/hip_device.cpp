@@ -173,10 +173,12 @@ int bind_thread_to_gpu_numa(int ordinal) {
 // semantics), and callers release or recycle the source right after (e.g. a
 // remote write-back from a pooled receive buffer, which the next receive then
 // overwrote: intermittent stale tiles in the 2-rank GPU QR). Each calling thread
-// copies on its own non-blocking stream and waits for it.
+// copies on its own (blocking) stream and waits for it.
 int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t bytes) {
   if (dst_dev == 0 && src_dev == 0) { std::memcpy(dst, src, bytes); return 0; }
   hipMemcpyKind k = dst_dev == 0 ? hipMemcpyDeviceToHost : src_dev == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  static const bool legacy = getenv("PARSEC_MEMCPY_LEGACY") != nullptr;  // A/B switch (debug)
+  if (legacy) return hipMemcpy(dst, src, bytes, k) == hipSuccess ? 0 : -1;
   const int dev = dst_dev != 0 ? dst_dev : src_dev;
   const int ord = device_hip_ordinal(dev);
   thread_local hipStream_t s = nullptr;
@@ -186,7 +188,9 @@ int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t b
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(ord);
     if (s) (void)hipStreamDestroy(s);
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+    // a BLOCKING stream: like hipMemcpy, the copy is ordered after earlier work
+    // of the null stream (initialisation kernels / memsets launched there)
+    if (hipStreamCreateWithFlags(&s, hipStreamDefault) != hipSuccess) s = nullptr;
     s_ord = ord;
     (void)hipSetDevice(cur);
   }
