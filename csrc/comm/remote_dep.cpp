@@ -137,6 +137,31 @@ std::unordered_map<uint64_t, RecvState*> g_recvs;
 std::map<uint32_t, std::vector<std::pair<int, std::vector<char>>>> g_parked;  // tp_id -> (src, msg)
 std::atomic<uint64_t> g_next_id{1};
 
+// ---- communication events in the trace (profile_filename set): one span per
+// (flow, payload) on each side, with peer and byte count (reference
+// remote_dep.h:374-415 MPI_DATA_PLD_SND / RCV, checked by check-comms.py)
+ProfilingStream* g_comm_prof = nullptr;
+int k_snd_b = -1, k_snd_e = -1, k_rcv_b = -1, k_rcv_e = -1, k_act_b = -1, k_act_e = -1;
+enum : int32_t { PLANE_HOST = 0, PLANE_IPC = 1, PLANE_RCCL = 2 };
+struct CommInfo {
+  int32_t peer, flow;
+  int64_t bytes;
+  int32_t plane, pad;
+};
+void comm_trace_init() {
+  if (!profiling_enabled() || g_comm_prof) return;
+  const char* desc = "peer{int32_t};flow{int32_t};bytes{int64_t};plane{int32_t};pad{int32_t}";
+  profiling_add_dictionary_keyword("COMM_DATA_SND", "fill:#0077FF", sizeof(CommInfo), desc, &k_snd_b, &k_snd_e);
+  profiling_add_dictionary_keyword("COMM_DATA_RCV", "fill:#00BB44", sizeof(CommInfo), desc, &k_rcv_b, &k_rcv_e);
+  profiling_add_dictionary_keyword("COMM_ACTIVATE", "fill:#AA00AA", sizeof(CommInfo), desc, &k_act_b, &k_act_e);
+  g_comm_prof = profiling_stream_create("comm");
+}
+inline void comm_trace(int key, uint64_t id, uint32_t tp, const CommInfo* info) {
+  (void)tp;  // begin / end must match on (key, taskpool 0, event id): ends do not know the taskpool
+  if (g_comm_prof) profiling_trace_at(g_comm_prof, key, id, 0, profiling_now(), info, info ? sizeof(CommInfo) : 0);
+}
+inline uint64_t flow_event(uint64_t id, int f) { return id * 32 + (uint64_t)f; }
+
 // position-based broadcast trees over [root] + ranks
 std::vector<int> tree_children(int topo, int pos, int n) {
   std::vector<int> c;
@@ -279,7 +304,15 @@ void send_activations(Taskpool* tp, const ActHdr& base, int my_pos_root_rank, co
     size_t tdn = tp->tdm->outgoing_message_pack(tp, dst, td, sizeof(td));
     h.termdet_bytes = (uint32_t)tdn;
     if (tdn) put(td, tdn);
-    g_ce->send_am2(TAG_REMOTE_DEP_ACTIVATE, dst, &h, sizeof(h), body.data(), body.size());
+    if (g_comm_prof) {
+      CommInfo ci{dst, -1, (int64_t)(sizeof(h) + body.size()), PLANE_HOST, 0};
+      const uint64_t ev = g_next_id.fetch_add(1);
+      comm_trace(k_act_b, ev, h.tp_id, &ci);
+      g_ce->send_am2(TAG_REMOTE_DEP_ACTIVATE, dst, &h, sizeof(h), body.data(), body.size());
+      comm_trace(k_act_e, ev, h.tp_id, nullptr);
+    } else {
+      g_ce->send_am2(TAG_REMOTE_DEP_ACTIVATE, dst, &h, sizeof(h), body.data(), body.size());
+    }
   }
   release_send(s);  // drop the construction guard
 }
@@ -349,6 +382,7 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
       uint64_t rid = r->id;
       g_ce->rccl_recv(src, c->device_private, r->fd[f].bytes, [rid, f] {
         RecvState* rs = nullptr;
+        comm_trace(k_rcv_e, flow_event(rid, f), 0, nullptr);
         {
           std::lock_guard<std::mutex> g(g_m);
           auto it = g_recvs.find(rid);
@@ -362,6 +396,14 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
       });
     }
   }
+  if (g_comm_prof)
+    for (int f = 0; f < nflows; ++f) {
+      if (!(get_mask & (1u << f))) continue;
+      DataCopy* c = r->data[f];
+      const int32_t plane = c->device_index != 0 && g_ce->rccl_ok() ? PLANE_RCCL : (c->device_index != 0 && g_ce->ipc_ok() ? PLANE_IPC : PLANE_HOST);
+      CommInfo ci{src, f, (int64_t)r->fd[f].bytes, plane, 0};
+      comm_trace(k_rcv_b, flow_event(r->id, f), r->hdr.tp_id, &ci);
+    }
   GetMsg gm{r->hdr.send_id, r->id, get_mask, g_ce->rank};
   PARSEC_DEBUG(kVerbDebug, "comm", "request data from %d (recv %llu mask %x)", src, (unsigned long long)r->id, get_mask);
   g_ce->send_am(TAG_GET_DATA, src, &gm, sizeof(gm));
@@ -382,8 +424,15 @@ void on_get(int src, int, const void* msg, size_t) {
     if (!(g.flow_mask & (1u << f))) continue;
     DataCopy* c = s->data[f];
     size_t bytes = c->original ? c->original->nb_elts : 0;
+    const uint32_t tpid = s->tp ? s->tp->taskpool_id : 0;
     if (c->device_index != 0 && g_ce->rccl_ok()) {
-      g_ce->rccl_send(g.requester, c->device_private, bytes, [s] { release_send(s); });
+      CommInfo ci{g.requester, f, (int64_t)bytes, PLANE_RCCL, 0};
+      comm_trace(k_snd_b, flow_event(g.send_id, f), tpid, &ci);
+      const uint64_t ev = flow_event(g.send_id, f);
+      g_ce->rccl_send(g.requester, c->device_private, bytes, [s, ev, tpid] {
+        comm_trace(k_snd_e, ev, tpid, nullptr);
+        release_send(s);
+      });
       continue;
     }
     if (c->device_index != 0 && g_ce->ipc_ok()) {
@@ -403,6 +452,8 @@ void on_get(int src, int, const void* msg, size_t) {
       m.bytes = bytes;
       if (g_ce->ipc_export(c->device_private, m.handle, &m.offset) == 0) {
         // the receiver pulls the bytes; its IPC_DONE releases this copy
+        CommInfo ci{g.requester, f, (int64_t)bytes, PLANE_IPC, 0};
+        comm_trace(k_snd_b, flow_event(g.send_id, f), tpid, &ci);
         g_ce->send_am(TAG_DATA_IPC, g.requester, &m, sizeof(m));
         continue;
       }
@@ -414,6 +465,8 @@ void on_get(int src, int, const void* msg, size_t) {
       device_memcpy(0, staged.data(), c->device_index, c->device_private, bytes);
       src_ptr = staged.data();
     }
+    CommInfo ci{g.requester, f, (int64_t)bytes, PLANE_HOST, 0};
+    comm_trace(k_snd_b, flow_event(g.send_id, f), tpid, &ci);
     size_t frag = g_ce->max_fragment() - sizeof(FragHdr) - 64;
     for (size_t off = 0; off < bytes || (bytes == 0 && off == 0); off += frag) {
       FragHdr fh{g.recv_id, (uint32_t)f, 0, off, bytes};
@@ -421,6 +474,7 @@ void on_get(int src, int, const void* msg, size_t) {
       g_ce->send_am2(TAG_DATA_FRAGMENT, g.requester, &fh, sizeof(fh), src_ptr + off, n);
       if (bytes == 0) break;
     }
+    comm_trace(k_snd_e, flow_event(g.send_id, f), tpid, nullptr);
     release_send(s);
   }
 }
@@ -452,6 +506,7 @@ void on_data_ipc(int src, int, const void* msg, size_t) {
                 (unsigned long long)got, (unsigned long long)want, (unsigned long long)again);
       }
     }
+    comm_trace(k_rcv_e, flow_event(rid, f), 0, nullptr);
     IpcDone d{sid, f, 0};
     g_ce->send_am(TAG_IPC_DONE, src, &d, sizeof(d));
     RecvState* rs = nullptr;
@@ -472,6 +527,7 @@ void on_data_ipc(int src, int, const void* msg, size_t) {
 void on_ipc_done(int, int, const void* msg, size_t) {
   IpcDone d;
   std::memcpy(&d, msg, sizeof(d));
+  comm_trace(k_snd_e, flow_event(d.send_id, (int)d.flow), 0, nullptr);
   SendState* s = nullptr;
   {
     std::lock_guard<std::mutex> g(g_m);
@@ -499,6 +555,7 @@ void on_fragment(int src, int, const void* msg, size_t len) {
   else device_memcpy(c->device_index, static_cast<char*>(c->device_private) + fh.offset, 0, (const char*)msg + sizeof(FragHdr), n);
   r->got[fh.flow] += n;
   if (r->got[fh.flow] < fh.total) return;
+  comm_trace(k_rcv_e, flow_event(fh.recv_id, (int)fh.flow), 0, nullptr);
   {
     std::lock_guard<std::mutex> g(g_m);
     if (--r->remaining > 0) return;
@@ -626,6 +683,7 @@ void remote_dep_init(Context* ctx) {
   ctx->nb_nodes = comm_size();
   set_debug_rank(ctx->my_rank);
   g_ctx = ctx;
+  if (ctx->nb_nodes > 1) comm_trace_init();
   if (g_ce) {
     ctx->comm = g_ce;
     auto* es = new ExecutionStream();
@@ -641,6 +699,7 @@ void remote_dep_init(Context* ctx) {
 }
 
 void remote_dep_fini(Context* ctx) {
+  g_comm_prof = nullptr;  // owned by the profiling module (freed at profiling_fini)
   {
     // the zone goes away with the devices: hand the cached receive buffers back
     auto& p = dev_pool();

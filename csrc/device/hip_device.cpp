@@ -323,6 +323,29 @@ hipEvent_t HipDevice::get_event() {
 }
 void HipDevice::put_event(hipEvent_t e) { if (e) event_pool.push_back(e); }
 
+hipEvent_t HipDevice::get_timing_event() {
+  if (!timing_pool.empty()) { hipEvent_t e = timing_pool.back(); timing_pool.pop_back(); return e; }
+  hipEvent_t e;
+  PARSEC_HIP_CHECK(hipEventCreate(&e));
+  return e;
+}
+
+void HipDevice::trace_group(int s, const ExecGroup& g) {
+  float b = 0.f, e = 0.f;
+  if (hipEventElapsedTime(&b, trace_ref, g.ts_begin) != hipSuccess || hipEventElapsedTime(&e, trace_ref, g.ts_end) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  if ((size_t)s >= trace_streams.size()) trace_streams.resize(s + 1, nullptr);
+  if (!trace_streams[s]) trace_streams[s] = profiling_stream_create(name + " stream " + std::to_string(s));
+  struct { int32_t ntasks, stream; uint32_t tc; int32_t l0; } info{(int32_t)g.tasks.size(), s, g.tasks.empty() ? 0u : g.tasks[0]->task->task_class->task_class_id,
+                                                                   g.tasks.empty() ? 0 : g.tasks[0]->task->locals[0]};
+  const uint32_t tp = g.tasks.empty() ? 0 : g.tasks[0]->task->taskpool->taskpool_id;
+  const uint64_t id = (uint64_t)(uintptr_t)g.ev;
+  profiling_trace_at(trace_streams[s], trace_key_b, id, tp, trace_ref_ns + (uint64_t)((double)b * 1e6), &info, sizeof(info));
+  profiling_trace_at(trace_streams[s], trace_key_e, id, tp, trace_ref_ns + (uint64_t)((double)e * 1e6), nullptr, 0);
+}
+
 void* HipDevice::workspace(int stream, size_t bytes) {
   if (stream < 0 || stream >= (int)stream_workspace.size()) stream = 0;
   if (stream_workspace_size[stream] < bytes) {
@@ -657,6 +680,11 @@ void HipDevice::execute_ready() {
   for (int s = 0; s < (int)round_tasks.size(); ++s) {
     if (round_tasks[s].empty()) continue;
     const size_t ng = batches[s].gemm.size(), nw = batches[s].trsm_w.size(), np = batches[s].potrf.size();
+    hipEvent_t tb = nullptr;
+    if (gpu_trace) {
+      tb = get_timing_event();
+      PARSEC_HIP_CHECK(hipEventRecord(tb, s_exec[s]));
+    }
     if (!batches[s].empty()) {
       launch_kernel_batch(batches[s], s_exec[s], ordinal, workspace(s, kernel_batch_workspace_bytes(batches[s]) + 64));
       stats.kernel_launches.fetch_add(1, std::memory_order_relaxed);
@@ -669,6 +697,11 @@ void HipDevice::execute_ready() {
       std::fprintf(stderr, "%s\n", line.c_str());
     }
     ExecGroup grp;
+    if (tb) {  // end timing event first: complete whenever grp.ev is
+      grp.ts_begin = tb;
+      grp.ts_end = get_timing_event();
+      PARSEC_HIP_CHECK(hipEventRecord(grp.ts_end, s_exec[s]));
+    }
     grp.ev = get_event();
     PARSEC_HIP_CHECK(hipEventRecord(grp.ev, s_exec[s]));
     grp.tasks.swap(round_tasks[s]);
@@ -813,6 +846,11 @@ bool HipDevice::progress() {
       hipError_t e = hipEventQuery(grp.ev);
       if (e == hipErrorNotReady) break;
       if (e != hipSuccess) fatal("GPU kernel failure on device %d: %s", ordinal, hipGetErrorString(e));
+      if (grp.ts_begin) {
+        trace_group(s, grp);
+        timing_pool.push_back(grp.ts_begin);
+        timing_pool.push_back(grp.ts_end);
+      }
       put_event(grp.ev);
       std::vector<GpuTask*> tasks;
       tasks.swap(grp.tasks);
@@ -861,6 +899,15 @@ void HipDevice::manager_main() {
   set_my_execution_stream(es);
   es->slot = thread_slot();
   profiling_thread_init(es);
+  if (profiling_enabled() && !trace_ref) {
+    // GPU spans: one reference event, host time taken once it completed
+    profiling_add_dictionary_keyword("GPU_EXEC", "fill:#FF8800", 16, "ntasks{int32_t};stream{int32_t};tc_id{uint32_t};l0{int32_t}", &trace_key_b, &trace_key_e);
+    PARSEC_HIP_CHECK(hipEventCreate(&trace_ref));
+    PARSEC_HIP_CHECK(hipEventRecord(trace_ref, s_exec[0]));
+    PARSEC_HIP_CHECK(hipEventSynchronize(trace_ref));
+    trace_ref_ns = profiling_now();
+    gpu_trace = true;
+  }
   Backoff backoff;
   for (;;) {
     bool did = progress();

@@ -73,6 +73,8 @@ struct ExecGroup {
   hipEvent_t ev = nullptr;
   std::vector<GpuTask*> tasks;
   uint64_t t_launch = 0;
+  // profiling: timing events around the group's kernels (GPU-side span)
+  hipEvent_t ts_begin = nullptr, ts_end = nullptr;
 };
 
 struct HipDevice : Device {
@@ -117,6 +119,17 @@ struct HipDevice : Device {
   std::vector<Task*> completions;  // release tasks gathered during one progress pass
   uint32_t rr_complete = 0;
   void flush_completions();
+  // ---- GPU-side tracing (profile_filename set): HIP timing events around each
+  // launched group, converted to the profiling clock through a reference event
+  // recorded (and waited for) when the manager starts
+  bool gpu_trace = false;
+  hipEvent_t trace_ref = nullptr;
+  uint64_t trace_ref_ns = 0;
+  int trace_key_b = -1, trace_key_e = -1;
+  std::vector<struct ProfilingStream*> trace_streams;
+  std::vector<hipEvent_t> timing_pool;
+  hipEvent_t get_timing_event();
+  void trace_group(int stream, const ExecGroup& g);
   bool trace_launches = false;
   uint32_t rr_stream = 0;
   int extra_crit_streams = 7;   // additional critical streams (see start())

@@ -2,12 +2,16 @@
 
 #include <fcntl.h>
 #include <sys/mman.h>
+#include <sys/resource.h>
 #include <unistd.h>
 
 #include <cstdio>
 #include <cstring>
+#include <condition_variable>
+#include <deque>
 #include <fstream>
 #include <map>
+#include <thread>
 #include <set>
 #include <sstream>
 
@@ -15,18 +19,99 @@ namespace parsec {
 
 // ============================================================= profiling
 namespace {
+struct SpillJob {
+  ProfilingStream* s;
+  std::vector<ProfEvent> events;
+  std::vector<uint8_t> info;
+};
 struct ProfState {
   std::mutex m;
   bool enabled = false;
   std::string filename;
   int rank = 0;
   uint64_t t0 = 0;
+  size_t buffer_events = 65536;
   std::vector<DictEntry> dict;
   std::map<std::string, int> dict_index;
   std::vector<ProfilingStream*> streams;
   std::vector<std::pair<std::string, std::string>> infos;
+  // writer thread
+  std::mutex wm;
+  std::condition_variable wcv;
+  std::deque<SpillJob> jobs;
+  std::thread writer;
+  bool writer_stop = false;
+  size_t jobs_pending = 0;
+  std::condition_variable wdone;
 };
 ProfState& P() { static ProfState* s = new ProfState(); return *s; }
+
+void append_file(const std::string& path, const void* data, size_t n) {
+  if (!n) return;
+  FILE* f = std::fopen(path.c_str(), "ab");
+  if (!f) { warning("profiling: cannot append to %s", path.c_str()); return; }
+  std::fwrite(data, 1, n, f);
+  std::fclose(f);
+}
+
+void writer_main() {
+  auto& p = P();
+  for (;;) {
+    SpillJob j;
+    {
+      std::unique_lock<std::mutex> lk(p.wm);
+      p.wcv.wait(lk, [&] { return p.writer_stop || !p.jobs.empty(); });
+      if (p.jobs.empty()) return;
+      j = std::move(p.jobs.front());
+      p.jobs.pop_front();
+    }
+    append_file(j.s->spill_ev, j.events.data(), j.events.size() * sizeof(ProfEvent));
+    append_file(j.s->spill_info, j.info.data(), j.info.size());
+    {
+      std::lock_guard<std::mutex> lk(p.wm);
+      --p.jobs_pending;
+    }
+    p.wdone.notify_all();
+  }
+}
+
+// hand the full buffer of `s` to the writer (caller owns s: its thread or lock)
+void spill(ProfilingStream* s) {
+  auto& p = P();
+  SpillJob j;
+  j.s = s;
+  j.events.swap(s->events);
+  j.info.swap(s->info);
+  s->spilled_events += j.events.size();
+  s->info_base += j.info.size();
+  s->events.reserve(p.buffer_events);
+  {
+    std::lock_guard<std::mutex> lk(p.wm);
+    if (!p.writer.joinable()) p.writer = std::thread(writer_main);
+    p.jobs.push_back(std::move(j));
+    ++p.jobs_pending;
+  }
+  p.wcv.notify_one();
+}
+
+void writer_drain() {
+  auto& p = P();
+  std::unique_lock<std::mutex> lk(p.wm);
+  p.wdone.wait(lk, [&] { return p.jobs_pending == 0; });
+}
+
+std::vector<uint8_t> read_all(const std::string& path) {
+  std::vector<uint8_t> out;
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return out;
+  std::fseek(f, 0, SEEK_END);
+  long n = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  out.resize(n > 0 ? (size_t)n : 0);
+  if (n > 0 && std::fread(out.data(), 1, (size_t)n, f) != (size_t)n) out.clear();
+  std::fclose(f);
+  return out;
+}
 }  // namespace
 
 bool profiling_enabled() { return P().enabled; }
@@ -35,7 +120,10 @@ uint64_t profiling_now() { return now_ns() - P().t0; }
 void profiling_init(Context* ctx) {
   auto& p = P();
   std::string fn = ParamRegistry::instance().reg_string("profile", "", "filename", "Write a trace to <filename>-<rank>.prof", "");
+  const int64_t be = ParamRegistry::instance().reg_int("profile", "", "buffer_events",
+      "Events buffered per stream before the writer thread spills them to disk", 65536);
   std::lock_guard<std::mutex> g(p.m);
+  p.buffer_events = (size_t)std::max<int64_t>(be, 16);
   p.rank = ctx->my_rank;
   if (p.t0 == 0) p.t0 = now_ns();
   if (!fn.empty()) { p.enabled = true; p.filename = fn; }
@@ -46,10 +134,15 @@ void profiling_start() { P().t0 = now_ns(); }
 ProfilingStream* profiling_stream_create(const std::string& name) {
   auto* s = new ProfilingStream();
   s->name = name;
-  s->events.reserve(4096);
   auto& p = P();
   std::lock_guard<std::mutex> g(p.m);
+  s->events.reserve(std::min<size_t>(p.buffer_events, 4096));
   s->thread_id = (int)p.streams.size();
+  const std::string base = (p.filename.empty() ? std::string("parsec_prof") : p.filename) + "-pid" + std::to_string((long)getpid()) + ".s" + std::to_string(s->thread_id);
+  s->spill_ev = base + ".ev.tmp";
+  s->spill_info = base + ".info.tmp";
+  std::remove(s->spill_ev.c_str());
+  std::remove(s->spill_info.c_str());
   p.streams.push_back(s);
   return s;
 }
@@ -77,19 +170,47 @@ int profiling_add_dictionary_keyword(const std::string& name, const std::string&
   return 0;
 }
 
-int profiling_trace(ProfilingStream* s, int key, uint64_t event_id, uint32_t taskpool_id, const void* info, size_t info_len) {
-  if (!s) return -1;
+static void trace_into(ProfilingStream* s, int key, uint64_t event_id, uint32_t taskpool_id, uint64_t ts, const void* info, size_t info_len) {
   ProfEvent e;
   e.key = (uint16_t)key;
   e.flags = info_len ? 1 : 0;
   e.taskpool_id = taskpool_id;
   e.event_id = event_id;
-  e.timestamp = profiling_now();
-  e.info_off = (uint32_t)s->info.size();
+  e.timestamp = ts;
+  e.info_off = (uint32_t)(s->info_base + s->info.size());
   e.info_len = (uint32_t)info_len;
   if (info_len) s->info.insert(s->info.end(), (const uint8_t*)info, (const uint8_t*)info + info_len);
   s->events.push_back(e);
+  if (s->events.size() >= P().buffer_events) spill(s);
+}
+
+int profiling_trace(ProfilingStream* s, int key, uint64_t event_id, uint32_t taskpool_id, const void* info, size_t info_len) {
+  if (!s) return -1;
+  trace_into(s, key, event_id, taskpool_id, profiling_now(), info, info_len);
   return 0;
+}
+
+int profiling_trace_at(ProfilingStream* s, int key, uint64_t event_id, uint32_t taskpool_id, uint64_t timestamp, const void* info, size_t info_len) {
+  if (!s) return -1;
+  std::lock_guard<SpinLock> g(s->lock);
+  trace_into(s, key, event_id, taskpool_id, timestamp, info, info_len);
+  return 0;
+}
+
+std::vector<std::pair<std::string, double>> profiling_rusage() {
+  std::vector<std::pair<std::string, double>> out;
+  struct rusage ru {};
+  if (getrusage(RUSAGE_SELF, &ru) != 0) return out;
+  out.emplace_back("ru_utime_s", ru.ru_utime.tv_sec + ru.ru_utime.tv_usec * 1e-6);
+  out.emplace_back("ru_stime_s", ru.ru_stime.tv_sec + ru.ru_stime.tv_usec * 1e-6);
+  out.emplace_back("ru_maxrss_kb", (double)ru.ru_maxrss);
+  out.emplace_back("ru_minflt", (double)ru.ru_minflt);
+  out.emplace_back("ru_majflt", (double)ru.ru_majflt);
+  out.emplace_back("ru_nvcsw", (double)ru.ru_nvcsw);
+  out.emplace_back("ru_nivcsw", (double)ru.ru_nivcsw);
+  out.emplace_back("ru_inblock", (double)ru.ru_inblock);
+  out.emplace_back("ru_oublock", (double)ru.ru_oublock);
+  return out;
 }
 
 void profiling_add_information(const std::string& key, const std::string& value) {
@@ -123,25 +244,49 @@ int profiling_dump(const std::string& filename) {
     wstr(o, s->name);
     int32_t tid = s->thread_id;
     o.write((const char*)&tid, 4);
-    uint64_t n = s->events.size();
+    // spilled chunks (in order) + the in-memory tail
+    std::vector<uint8_t> sev = read_all(s->spill_ev), sinfo = read_all(s->spill_info);
+    uint64_t n = sev.size() / sizeof(ProfEvent) + s->events.size();
     o.write((const char*)&n, 8);
     static_assert(sizeof(ProfEvent) == 32, "event layout");
-    o.write((const char*)s->events.data(), n * sizeof(ProfEvent));
-    uint64_t isz = s->info.size();
+    o.write((const char*)sev.data(), sev.size());
+    o.write((const char*)s->events.data(), s->events.size() * sizeof(ProfEvent));
+    uint64_t isz = sinfo.size() + s->info.size();
     o.write((const char*)&isz, 8);
-    o.write((const char*)s->info.data(), isz);
+    o.write((const char*)sinfo.data(), sinfo.size());
+    o.write((const char*)s->info.data(), s->info.size());
   }
   return o ? 0 : -1;
 }
 
 void profiling_fini(Context* ctx) {
   auto& p = P();
+  const auto ru = profiling_rusage();
+  if (ParamRegistry::instance().reg_int("runtime", "", "report_rusage", "Print the process resource usage (getrusage) at fini", 0)) {
+    std::string line;
+    for (auto& kv : ru) line += " " + kv.first + "=" + std::to_string(kv.second);
+    std::fprintf(stderr, "[parsec %d] rusage:%s\n", ctx->my_rank, line.c_str());
+  }
+  writer_drain();
+  p.rank = ctx->my_rank;  // known only once the communication engine attached
   if (p.enabled && !p.filename.empty()) {
+    for (auto& kv : ru) profiling_add_information(kv.first, std::to_string(kv.second));
     std::string fn = p.filename + "-" + std::to_string(ctx->my_rank) + ".prof";
     if (profiling_dump(fn) != 0) warning("could not write trace %s", fn.c_str());
   }
+  {
+    std::lock_guard<std::mutex> lk(p.wm);
+    p.writer_stop = true;
+  }
+  p.wcv.notify_all();
+  if (p.writer.joinable()) p.writer.join();
+  p.writer_stop = false;
   std::lock_guard<std::mutex> g(p.m);
-  for (auto* s : p.streams) delete s;
+  for (auto* s : p.streams) {
+    std::remove(s->spill_ev.c_str());
+    std::remove(s->spill_info.c_str());
+    delete s;
+  }
   p.streams.clear();
   for (auto* es : ctx->all_es) es->prof = nullptr;
   for (auto* es : ctx->aux_es) es->prof = nullptr;

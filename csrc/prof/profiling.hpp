@@ -25,11 +25,19 @@ struct ProfEvent {
   uint32_t info_len;
 };
 
+// One event buffer per thread (or per device stream). When `events` reaches
+// the buffer size (MCA profile_buffer_events) it is handed to the writer
+// thread, which appends it to this stream's spill files; memory stays bounded
+// and the file is assembled at fini (reference profiling.c:384-432 buffers
+// flushed by a helper thread).
 struct ProfilingStream {
   std::string name;
   int thread_id = 0;
   std::vector<ProfEvent> events;
   std::vector<uint8_t> info;
+  uint64_t info_base = 0;       // info bytes already spilled (info_off is stream-global)
+  uint64_t spilled_events = 0;  // events already handed to the writer
+  std::string spill_ev, spill_info;  // spill file paths
   SpinLock lock;  // only for streams shared by several threads (devices)
 };
 
@@ -51,6 +59,14 @@ ProfilingStream* profiling_stream_create(const std::string& name);
 int profiling_add_dictionary_keyword(const std::string& name, const std::string& attributes, size_t info_length,
                                      const std::string& info_desc, int* begin_key, int* end_key);
 int profiling_trace(ProfilingStream* s, int key, uint64_t event_id, uint32_t taskpool_id, const void* info, size_t info_len);
+// Same with an explicit timestamp (ns on the profiling clock), e.g. GPU spans
+// converted from HIP events; `s` may be shared (its lock is taken).
+int profiling_trace_at(ProfilingStream* s, int key, uint64_t event_id, uint32_t taskpool_id, uint64_t timestamp, const void* info, size_t info_len);
+ProfilingStream* profiling_stream_create(const std::string& name);
+// Process resource usage (getrusage) as "name=value" pairs; also recorded in the
+// trace header at fini and printed when runtime_report_rusage is set
+// (reference parsec.c:107-145).
+std::vector<std::pair<std::string, double>> profiling_rusage();
 uint64_t profiling_now();
 int profiling_dump(const std::string& filename);
 void profiling_add_information(const std::string& key, const std::string& value);

@@ -56,3 +56,58 @@ def test_trace_roundtrip(pa, tmp_path):
     profiling.dot_merge([str(tmp_path / d) for d in dots], str(tmp_path / "merged.dot"))
     text = open(tmp_path / "merged.dot").read()
     assert text.startswith("digraph") and text.count("traced_work") >= 40
+
+
+def test_trace_streaming_writer(pa, tmp_path):
+    """profile_buffer_events=16: every stream's buffer is handed to the writer
+    thread many times during the run (bounded memory, reference profiling.c
+    helper-thread flush); the assembled trace still holds every event, the spill
+    files are gone, and the header carries the process rusage."""
+    base = str(tmp_path / "spill")
+    pa.mca_set("profile_filename", base)
+    pa.mca_set("profile_buffer_events", "16")
+    pa.mca_set("mca_pins", "task_profiler")
+    try:
+        ctx = pa.init(2)
+    finally:
+        for k in ("profile_filename", "profile_buffer_events", "mca_pins"):
+            pa.mca_unset(k)
+    A = pa.BlockCyclic(pa.MATRIX_INTEGER, 0, 1, 1, 8, 1)
+    tp = pa.dtd_taskpool(ctx)
+    ctx.start()
+    for i in range(300):
+        pa.insert_task(tp, lambda task: 0, [(tp.tile_of(A, A.data_key([i % 8, 0])), pa.INOUT)], name="spilled_work")
+    tp.data_flush_all(A)
+    ctx.wait()
+    ctx.fini()
+    tr = profiling.read_trace(base + "-0.prof")
+    assert profiling.summary([tr])["spilled_work"]["count"] == 300
+    assert not [p for p in os.listdir(tmp_path) if p.endswith(".tmp")]
+    infos = dict(tr.infos)
+    assert float(infos["ru_utime_s"]) >= 0 and float(infos["ru_maxrss_kb"]) > 0
+
+
+def test_comm_trace_payload_sizes(pa, tmp_path):
+    """Distributed run with a trace per rank: every payload has a COMM_DATA_SND
+    span at its sender and a COMM_DATA_RCV span at its receiver with the same
+    byte count (the check of the reference's tests/profiling/check-comms.py)."""
+    import subprocess
+    import sys
+    import uuid
+
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp", "dist_dpotrf.py")
+    base = str(tmp_path / "comm")
+    job = "pc" + uuid.uuid4().hex[:10]
+    env = dict(os.environ, PARSEC_MCA_device_hip_enabled="0", PARSEC_MCA_profile_filename=base)
+    procs = [subprocess.Popen([sys.executable, worker, str(r), "2", job, "256", "32", "2", "1"], stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True, env=env) for r in range(2)]
+    for p in procs:
+        out, _ = p.communicate(timeout=120)
+        assert p.returncode == 0, out
+    traces = [profiling.read_trace(f"{base}-{r}.prof") for r in range(2)]
+    rows = profiling.intervals(traces)
+    snd = [(r["rank"], r["peer"], r["bytes"]) for r in rows if r["type"] == "COMM_DATA_SND"]
+    rcv = [(r["peer"], r["rank"], r["bytes"]) for r in rows if r["type"] == "COMM_DATA_RCV"]
+    assert snd and sorted(snd) == sorted(rcv)
+    assert all(b == 32 * 32 * 8 for *_, b in snd)
+    assert any(r["type"] == "COMM_ACTIVATE" for r in rows)
