@@ -426,7 +426,13 @@ struct DeviceStats {
   std::atomic<uint64_t> bytes_in{0}, bytes_out{0}, bytes_d2d{0};
   std::atomic<uint64_t> data_faults{0};
   std::atomic<uint64_t> kernel_launches{0}, batched_tasks{0};
+  std::atomic<uint64_t> w2r_tasks{0}, prefetches{0};
 };
+
+// data_advise (reference device.c parsec_advise_data_on_device, PARSEC_DEV_DATA_ADVICE_*)
+enum DataAdvice : int { DATA_ADVICE_PREFETCH = 1, DATA_ADVICE_PREFERRED_DEVICE = 2, DATA_ADVICE_WARMUP = 3 };
+// Route `advice` for data `d` to device `device_index` (returns -1 for an unknown device).
+int data_advise_on_device(Data* d, int device_index, int advice);
 
 struct Device {
   std::string name;

@@ -244,4 +244,12 @@ int first_gpu_device_index() {
   return -1;
 }
 
+int data_advise_on_device(Data* d, int device_index, int advice) {
+  auto& reg = DeviceRegistry::instance();
+  if (!d || device_index < 0 || device_index >= reg.count() || !reg.devices[device_index]) return -1;
+  if (advice == DATA_ADVICE_PREFERRED_DEVICE) d->preferred_device = (int8_t)device_index;
+  reg.devices[device_index]->data_advise(d, advice);
+  return 0;
+}
+
 }  // namespace parsec

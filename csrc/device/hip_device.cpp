@@ -459,32 +459,161 @@ bool HipDevice::evict(size_t bytes) {
     if (!drop(c)) lru_touch(c);
     it = nx;
   }
-  // write back dirty copies (reference W2R task), then drop them
-  for (ListItem* it = lru_owned.front(); it && it != lru_owned.end() && freed < bytes;) {
+  // not enough clean memory: write dirty copies back asynchronously (W2R); the
+  // allocation is retried once they completed and became clean
+  if (freed < bytes) start_w2r(bytes - freed);
+  return freed >= bytes;
+}
+
+bool HipDevice::start_w2r(size_t bytes) {
+  if (w2r_bytes_inflight >= bytes) return false;  // enough already on its way
+  W2RJob job;
+  size_t queued = 0;
+  for (ListItem* it = lru_owned.front(); it && it != lru_owned.end() && w2r_bytes_inflight + queued < bytes;) {
     ListItem* nx = it->next;
     DataCopy* c = static_cast<DataCopy*>(it);
     Data* d = c->original;
-    lru_owned.remove(c);
-    static_cast<DevCopyState*>(c->dev_state)->in_lru = false;
-    if (d && c->readers.load() == 0) {
-      DataCopy* host = d->copy(0);
-      if (!host) host = data_pull_to_host(d);  // allocates + copies synchronously
-      else {
-        PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, c->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_d2h));
-        PARSEC_HIP_CHECK(hipStreamSynchronize(s_d2h));
-        stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
-        std::lock_guard<SpinLock> g(d->lock);
-        host->version = c->version;
-        host->coherency_state = COHERENCY_SHARED;
-        d->owner_device = 0;
-      }
-      if (!drop(c)) lru_touch(c);
-    } else {
+    auto* st = static_cast<DevCopyState*>(c->dev_state);
+    if (!d || c->readers.load() > 0 || st->w2r) { it = nx; continue; }
+    DataCopy* host = d->copy(0);
+    if (!host) {
+      // no host buffer to write into (NEW / arena data): allocate + copy now
+      lru_remove(c);
+      host = data_pull_to_host(d);
       lru_touch(c);
+      it = nx;
+      continue;
     }
+    lru_remove(c);
+    st->w2r = true;
+    c->readers.fetch_add(1);  // pinned: not dropped while the copy is in flight
+    PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, c->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_d2h));
+    stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
+    job.copies.push_back(c);
+    job.versions.push_back(c->version);
+    queued += d->nb_elts;
     it = nx;
   }
-  return freed >= bytes;
+  if (job.copies.empty()) return false;
+  job.ev = get_event();
+  PARSEC_HIP_CHECK(hipEventRecord(job.ev, s_d2h));
+  w2r_bytes_inflight += queued;
+  stats.w2r_tasks.fetch_add(1, std::memory_order_relaxed);
+  w2r_jobs.push_back(std::move(job));
+  return true;
+}
+
+bool HipDevice::progress_w2r() {
+  bool did = false;
+  while (!w2r_jobs.empty()) {
+    W2RJob& j = w2r_jobs.front();
+    if (hipEventQuery(j.ev) == hipErrorNotReady) break;
+    for (size_t i = 0; i < j.copies.size(); ++i) {
+      DataCopy* c = j.copies[i];
+      Data* d = c->original;
+      auto* st = static_cast<DevCopyState*>(c->dev_state);
+      if (d) {
+        std::lock_guard<SpinLock> g(d->lock);
+        DataCopy* host = d->copy(0);
+        w2r_bytes_inflight -= std::min(w2r_bytes_inflight, (size_t)d->nb_elts);
+        // a writer may not have touched it meanwhile (writers wait for w2r)
+        if (host && c->version == j.versions[i]) {
+          host->version = c->version;
+          host->coherency_state = COHERENCY_SHARED;
+        }
+      }
+      st->w2r = false;
+      c->readers.fetch_sub(1);
+      lru_touch(c);  // clean now: lands on the clean LRU
+    }
+    put_event(j.ev);
+    w2r_jobs.pop_front();
+    did = true;
+  }
+  return did;
+}
+
+void HipDevice::data_advise(Data* d, int advice) {
+  if (!d) return;
+  if (advice == DATA_ADVICE_PREFERRED_DEVICE) {
+    d->preferred_device = (int8_t)device_index;
+  } else if (advice == DATA_ADVICE_PREFETCH) {
+    data_retain(d);  // kept alive until the prefetch completed
+    {
+      std::lock_guard<std::mutex> lk(advise_m);
+      prefetch_requests.push_back(d);
+    }
+    in_cv.notify_one();
+  }
+  // DATA_ADVICE_WARMUP: nothing to do, the LRU order is already by last use
+}
+
+bool HipDevice::progress_prefetch() {
+  bool did = false;
+  std::vector<Data*> reqs;
+  {
+    std::lock_guard<std::mutex> lk(advise_m);
+    reqs.swap(prefetch_requests);
+  }
+  for (Data* d : reqs) {
+    did = true;
+    DataCopy* local = d->copy(device_index);
+    if (!local) {
+      DataCopy* any = nullptr;
+      for (int i = 0; i < kMaxDevices && !any; ++i) any = d->copy(i);
+      void* p = any ? cache_alloc(d->nb_elts) : nullptr;
+      if (!p) { data_release(d); continue; }  // no memory now: a prefetch is only a hint
+      auto* nc = new DataCopy();
+      nc->device_private = p;
+      nc->flags = DATA_FLAG_PARSEC_OWNED | DATA_FLAG_DEVICE_CACHE;
+      nc->coherency_state = COHERENCY_INVALID;
+      nc->dtt = any->dtt;
+      auto* nst = new DevCopyState();
+      nc->dev_state = nst;
+      {
+        std::lock_guard<SpinLock> lk(d->lock);
+        local = d->copy(device_index);
+        if (!local) {
+          data_copy_attach(d, nc, device_index);
+          data_retain(d);
+          nst->retained = d;
+          local = nc;
+        }
+      }
+      if (local != nc) { zone_free(p); delete nst; delete nc; }
+    }
+    if (local->transfer_status == TRANSFER_UNDER) { data_release(d); continue; }
+    DataCopy* src = data_start_transfer_ownership_to_copy(d, device_index, FLOW_READ);
+    if (!src || src == local) {
+      data_end_transfer_ownership_to_copy(d, device_index, FLOW_READ);
+      data_release(d);
+      continue;
+    }
+    if (src->device_index == 0) PARSEC_HIP_CHECK(hipMemcpyAsync(local->device_private, src->device_private, d->nb_elts, hipMemcpyHostToDevice, s_h2d));
+    else PARSEC_HIP_CHECK(hipMemcpyPeerAsync(local->device_private, ordinal, src->device_private, device_hip_ordinal(src->device_index), d->nb_elts, s_h2d));
+    stats.bytes_in.fetch_add(d->nb_elts, std::memory_order_relaxed);
+    stats.prefetches.fetch_add(1, std::memory_order_relaxed);
+    local->transfer_status = TRANSFER_UNDER;
+    local->readers.fetch_add(1);
+    PrefetchJob j;
+    j.ev = get_event();
+    PARSEC_HIP_CHECK(hipEventRecord(j.ev, s_h2d));
+    j.local = local;
+    j.d = d;
+    prefetch_jobs.push_back(j);
+  }
+  while (!prefetch_jobs.empty()) {
+    PrefetchJob& j = prefetch_jobs.front();
+    if (hipEventQuery(j.ev) == hipErrorNotReady) break;
+    data_end_transfer_ownership_to_copy(j.d, device_index, FLOW_READ);
+    j.local->readers.fetch_sub(1);
+    lru_touch(j.local);
+    put_event(j.ev);
+    data_release(j.d);
+    prefetch_jobs.pop_front();
+    did = true;
+  }
+  return did;
 }
 
 void HipDevice::ensure_zone() {
@@ -564,6 +693,7 @@ int HipDevice::stage_in(GpuTask* g) {
       static DevCopyState unmanaged{false, false, false};
       local->dev_state = &unmanaged;
     }
+    if (auto* lst = static_cast<DevCopyState*>(local->dev_state); lst->w2r && (g->access[fi] & FLOW_WRITE)) return -1;  // retry after the write-back
     lru_remove(local);
     local->readers.fetch_add(1);
     g->dev_copy[fi] = local;
@@ -812,6 +942,8 @@ bool HipDevice::progress() {
     for (GpuTask* g : in) { g->t_submit = now_ns(); pending.push_back(g); }
     did = true;
   }
+  if (!w2r_jobs.empty() && progress_w2r()) did = true;
+  if ((!prefetch_jobs.empty() || !prefetch_requests.empty()) && progress_prefetch()) did = true;
   // stage in
   if (!pending.empty()) {
     if (sort_pending && pending.size() > 1)

@@ -67,6 +67,22 @@ struct DevCopyState {  // DataCopy::dev_state for engine-managed copies
   bool owned_lru = false;
   bool cache_managed = true;  // allocated from the zone (evictable)
   Data* retained = nullptr;   // the Data this cache copy keeps alive (released when the copy is dropped)
+  bool w2r = false;           // write-back to the host in flight (readers may use it, writers wait)
+};
+
+// Asynchronous write-back of dirty cache copies (reference W2R task,
+// transfer_gpu.c:221-337): D2H copies on the d2h stream, completed by the
+// manager's progress loop; the copies then become clean and evictable.
+struct W2RJob {
+  hipEvent_t ev = nullptr;
+  std::vector<DataCopy*> copies;
+  std::vector<uint32_t> versions;
+};
+// Prefetch of one tile to the device (data_advise PREFETCH), no task attached.
+struct PrefetchJob {
+  hipEvent_t ev = nullptr;
+  DataCopy* local = nullptr;
+  Data* d = nullptr;
 };
 
 struct ExecGroup {
@@ -119,6 +135,16 @@ struct HipDevice : Device {
   std::vector<Task*> completions;  // release tasks gathered during one progress pass
   uint32_t rr_complete = 0;
   void flush_completions();
+  std::deque<W2RJob> w2r_jobs;
+  size_t w2r_bytes_inflight = 0;
+  bool start_w2r(size_t bytes);
+  bool progress_w2r();
+  // data_advise: PREFETCH requests are queued by any thread, served by the manager
+  std::mutex advise_m;
+  std::vector<Data*> prefetch_requests;
+  std::deque<PrefetchJob> prefetch_jobs;
+  void data_advise(Data* d, int advice) override;
+  bool progress_prefetch();
   // ---- GPU-side tracing (profile_filename set): HIP timing events around each
   // launched group, converted to the profiling clock through a reference event
   // recorded (and waited for) when the manager starts

@@ -567,6 +567,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("read_int", [](uintptr_t p) { return *reinterpret_cast<int*>(p); });
 
   // --------------------------------------------------------------- devices
+  m.attr("DATA_ADVICE_PREFETCH") = (int)DATA_ADVICE_PREFETCH;
+  m.attr("DATA_ADVICE_PREFERRED_DEVICE") = (int)DATA_ADVICE_PREFERRED_DEVICE;
+  m.attr("DATA_ADVICE_WARMUP") = (int)DATA_ADVICE_WARMUP;
+  m.def("data_advise", [](TiledMatrix* A, int64_t m, int64_t n, int device, int advice) {
+        const int64_t idx[2] = {m, n};
+        return data_advise_on_device(A->data_of(idx, 2), device, advice);
+      }, "advise the runtime about tile (m, n): DATA_ADVICE_PREFETCH copies it to the device ahead of use, "
+         "DATA_ADVICE_PREFERRED_DEVICE steers tasks writing it to that device (reference parsec_advise_data_on_device)");
   m.def("devices", []() {
     py::list out;
     for (auto* d : DeviceRegistry::instance().devices) {
@@ -584,6 +592,8 @@ PYBIND11_MODULE(_C, m) {
       e["bytes_out"] = d->stats.bytes_out.load();
       e["bytes_d2d"] = d->stats.bytes_d2d.load();
       e["data_faults"] = d->stats.data_faults.load();
+      e["w2r_tasks"] = d->stats.w2r_tasks.load();
+      e["prefetches"] = d->stats.prefetches.load();
       out.append(e);
     }
     return out;
