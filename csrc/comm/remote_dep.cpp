@@ -180,7 +180,12 @@ void release_send(SendState* s) {
     std::lock_guard<std::mutex> g(g_m);
     g_sends.erase(s->id);
   }
-  for (auto*& c : s->data) if (c) { data_copy_release(c); c = nullptr; }
+  for (auto*& c : s->data)
+    if (c) {
+      if (c->device_index != 0) c->readers.fetch_sub(1);
+      data_copy_release(c);
+      c = nullptr;
+    }
   if (s->tp && s->tp->tdm) s->tp->tdm->taskpool_addto_runtime_actions(s->tp, -1);
   delete s;
 }
@@ -270,7 +275,11 @@ void send_activations(Taskpool* tp, const ActHdr& base, int my_pos_root_rank, co
   s->id = g_next_id.fetch_add(1);
   s->tp = tp;
   for (int f = 0; f < nflows; ++f)
-    if (data[f]) { data_copy_retain(data[f]); s->data[f] = data[f]; }
+    if (data[f]) {
+      data_copy_retain(data[f]);
+      if (data[f]->device_index != 0) data[f]->readers.fetch_add(1);  // pinned: a GPU cache must not evict it before the peer read it
+      s->data[f] = data[f];
+    }
   {
     std::lock_guard<std::mutex> g(g_m);
     g_sends[s->id] = s;

@@ -423,12 +423,39 @@ void HipDevice::lru_touch(DataCopy* c) {
   st->in_lru = true;
 }
 
+// A clean cache copy still referenced by tasks that are not ready yet (their
+// data_in): its memory is reclaimed, the object stays with them (device_private
+// null, detached) and they stage the data in again from its valid version.
+static void evicted_copy_release(DataCopy* c) {
+  Data* d = c->original;
+  delete c;
+  if (d) data_release(d);
+}
+
 bool HipDevice::evict(size_t bytes) {
   size_t freed = 0;
   auto drop = [&](DataCopy* c) -> bool {
     Data* d = __atomic_load_n(&c->original, __ATOMIC_ACQUIRE);
     auto* st = static_cast<DevCopyState*>(c->dev_state);
     size_t bytes = 0;
+    if (d && c->refcount.load() > 1) {
+      std::lock_guard<SpinLock> g(d->lock);
+      if (c->readers.load() > 0 || st->w2r) return false;
+      bool clean = false;  // another valid copy at least as new
+      for (int i = 0; i < kMaxDevices && !clean; ++i)
+        if (DataCopy* o = d->copy(i); o && o != c && o->coherency_state != COHERENCY_INVALID && o->version >= c->version) clean = true;
+      if (!clean) return false;
+      data_copy_detach(d, c, device_index);
+      c->coherency_state = COHERENCY_INVALID;
+      zone_free(c->device_private);
+      c->device_private = nullptr;
+      delete st;
+      c->dev_state = nullptr;
+      c->release_fn = evicted_copy_release;  // drops the Data reference the cache copy held
+      freed += d->nb_elts;
+      stats.data_faults.fetch_add(1, std::memory_order_relaxed);
+      return true;
+    }
     if (d) {
       std::lock_guard<SpinLock> g(d->lock);
       if (c->readers.load() > 0 || c->refcount.load() > 1) return false;
@@ -660,6 +687,58 @@ int HipDevice::stage_in(GpuTask* g) {
     if (!c || !c->original) continue;
     g->flows |= 1u << f.index;
     g->access[f.index] = f.access;
+  }
+  // Pass 1: all or nothing. Every flow gets its device copy (allocating may
+  // evict or start write-backs) before any of them is pinned; when memory runs
+  // out the copies created here are dropped again, so a waiting task pins
+  // nothing and can never starve the others (deadlock under a small cache).
+  {
+    std::vector<DataCopy*> fresh;
+    auto rollback = [&] {
+      for (DataCopy* nc : fresh) {
+        Data* d = nc->original;
+        auto* st = static_cast<DevCopyState*>(nc->dev_state);
+        {
+          std::lock_guard<SpinLock> lk(d->lock);
+          data_copy_detach(d, nc, device_index);
+        }
+        zone_free(nc->device_private);
+        nc->device_private = nullptr;
+        Data* keep = st->retained;
+        delete st;
+        nc->dev_state = nullptr;
+        nc->original = nullptr;
+        data_copy_release(nc);
+        if (keep) data_release(keep);
+      }
+    };
+    for (int fi = 0; fi < kMaxFlows; ++fi) {
+      if (!(g->flows & (1u << fi)) || g->dev_copy[fi]) continue;
+      DataCopy* c = t->data[fi].data_in;
+      Data* d = c->original;
+      DataCopy* local = d->copy(device_index);
+      if (local) {
+        auto* lst = static_cast<DevCopyState*>(local->dev_state);
+        if (lst && lst->w2r && (g->access[fi] & FLOW_WRITE)) { rollback(); return -1; }  // retry after the write-back
+        continue;
+      }
+      void* p = cache_alloc(d->nb_elts);
+      if (!p) { rollback(); return -1; }
+      auto* nc = new DataCopy();
+      nc->device_private = p;
+      nc->flags = DATA_FLAG_PARSEC_OWNED | DATA_FLAG_DEVICE_CACHE;
+      nc->coherency_state = COHERENCY_INVALID;
+      nc->dtt = c->dtt;
+      auto* nst = new DevCopyState();
+      nc->dev_state = nst;
+      {
+        std::lock_guard<SpinLock> lk(d->lock);
+        data_copy_attach(d, nc, device_index);
+        data_retain(d);  // an engine-managed copy keeps its Data alive (NEW / arena data may lose its host copy first)
+        nst->retained = d;
+      }
+      fresh.push_back(nc);
+    }
   }
   for (int fi = 0; fi < kMaxFlows; ++fi) {
     if (!(g->flows & (1u << fi)) || g->dev_copy[fi]) continue;
