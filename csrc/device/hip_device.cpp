@@ -1135,6 +1135,10 @@ void HipDevice::manager_main() {
     backoff.reset();
   }
   profiling_thread_fini(es);
+  // trace streams belong to this context's profiling session (freed at its fini)
+  gpu_trace = false;
+  trace_streams.clear();
+  if (trace_ref) { (void)hipEventDestroy(trace_ref); trace_ref = nullptr; }
 }
 
 // ================================================================ module
