@@ -466,6 +466,41 @@ void PtgTaskClass::reshape_inputs(Task* t) const {
   }
 }
 
+DataCopy* PtgTaskClass::remote_reshape(const Taskpool* tp, const int32_t* PL, const DepTarget& out, const PtgTaskClass* dst, int dst_flow, const int32_t* DL,
+                                       DataCopy* data) const {
+  if (!data || data->device_index != 0) return nullptr;  // host payloads (device ones pass unchanged)
+  const DepTarget* in = dst->active_input(tp, dst_flow, DL);
+  const bool in_shape = in && in->remote_datatype_index >= 0;
+  if (!out.has_remote_shape() && !in_shape) return nullptr;
+  auto& adts = tp->arenas_datatypes;
+  auto dtt_of = [&](int idx) -> const ArenaDatatype* { return idx >= 0 && idx < (int)adts.size() && adts[idx].arena ? &adts[idx] : nullptr; };
+  const int oi = out.remote_datatype_index >= 0 ? out.remote_datatype_index : out.datatype_index;
+  const ArenaDatatype* oadt = dtt_of(oi);
+  const ArenaDatatype* iadt = in_shape ? dtt_of(in->remote_datatype_index) : nullptr;
+  if (!oadt && !iadt) return nullptr;
+  const Datatype& odt = oadt ? oadt->opaque_dtt : iadt->opaque_dtt;
+  const Datatype& idt = iadt ? iadt->opaque_dtt : odt;
+  const int64_t displ = out.displ_remote ? out.displ_remote(tp, PL) : 0;
+  const int64_t count = out.count_remote ? std::max<int64_t>(out.count_remote(tp, PL), 1) : 1;
+  const size_t src_bytes = data->original ? data->original->nb_elts : 0;
+  if (displ < 0 || (src_bytes && (size_t)(displ + count * odt.extent_bytes()) > src_bytes))
+    fatal("%s: displ_remote %lld + %lld x %lld bytes exceeds the %zu-byte payload", name.c_str(), (long long)displ, (long long)count,
+          (long long)odt.extent_bytes(), src_bytes);
+  const ArenaDatatype* dadt = iadt ? iadt : oadt;
+  DataCopy* nc = dadt->arena->get_copy(nullptr, 0);
+  if (!nc) return nullptr;
+  std::memset(nc->device_private, 0, dadt->arena->elem_size);
+  std::vector<uint8_t> packed((size_t)(odt.packed_bytes() * count));
+  for (int64_t i = 0; i < count; ++i)
+    odt.pack(static_cast<const uint8_t*>(data->device_private) + displ + i * odt.extent_bytes(), packed.data() + i * odt.packed_bytes());
+  if ((size_t)idt.packed_bytes() * (size_t)count > packed.size() && count == 1) packed.resize((size_t)idt.packed_bytes(), 0);
+  const int64_t ni = std::max<int64_t>(1, (int64_t)packed.size() / std::max<int64_t>(1, idt.packed_bytes()));
+  for (int64_t i = 0; i < ni && (size_t)((i + 1) * idt.extent_bytes()) <= dadt->arena->elem_size; ++i)
+    idt.unpack(packed.data() + i * idt.packed_bytes(), static_cast<uint8_t*>(nc->device_private) + i * idt.extent_bytes());
+  nc->dtt = idt;
+  return nc;
+}
+
 // Copy `src` into the collection's own copy of `home` (final write of a flow
 // into a collection position it did not come from).
 static int g_trace_writeback = -1;
@@ -946,7 +981,13 @@ void PtgTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& ac
         expand_args(this, X, tg->args, 0, params, [&](const int32_t* P) {
           int32_t TL[kMaxLocals];
           if (!dst->complete_locals(this, TL, P)) return;
-          if (dst->rank_of(this, TL) == my) activate(es, dst, TL, tg->dst_flow, data, ready);
+          if (dst->rank_of(this, TL) != my) return;
+          if (DataCopy* shaped = tc->remote_reshape(this, act.locals, *tg, dst, tg->dst_flow, TL, data)) {
+            activate(es, dst, TL, tg->dst_flow, shaped, ready);
+            data_copy_release(shaped);  // activate retained it
+          } else {
+            activate(es, dst, TL, tg->dst_flow, data, ready);
+          }
         });
       } else if (tg->kind == DEP_DATA && data) {
         DataCollection* dc = tg->dc(this);

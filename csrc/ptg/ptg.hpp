@@ -69,8 +69,13 @@ struct DepTarget {
   int dst_flow = -1;
   std::vector<CallArg> args;  // target parameters (TASK) or collection indices (DATA)
   std::function<DataCollection*(const Taskpool*)> dc;  // DEP_DATA
-  int datatype_index = 0;     // arena / datatype slot (NEW, remote layout)
+  int datatype_index = 0;     // arena / datatype slot ([type = ...]: NEW, local reshape)
+  // [type_remote / displ_remote / count_remote] (reference remote_dep_mpi.c:594-731):
+  // what a successor on ANOTHER rank receives: count_remote elements of
+  // type_remote starting displ_remote bytes into the producer's copy. -1: as `type`.
+  int remote_datatype_index = -1;
   Expr displ_remote, count_remote;
+  bool has_remote_shape() const { return remote_datatype_index >= 0 || (bool)displ_remote || (bool)count_remote; }
   std::vector<IterDef> iters;  // iterators local to this branch (`? [ j = .. ] T(..) : ..`)
 };
 
@@ -149,6 +154,11 @@ class PtgTaskClass : public TaskClass {
   mutable std::atomic<bool> warned_extra_activation{false};
   bool writes_collections = false;  // some output dependency targets a data collection
   void reshape_inputs(Task* t) const;
+  // Remote reshape at the receiver: the layout an output dependency ships to a
+  // successor on this rank (type_remote at displ_remote, count_remote times),
+  // unpacked into the successor input's type_remote layout. nullptr: unchanged.
+  DataCopy* remote_reshape(const Taskpool* tp, const int32_t* producer_locals, const DepTarget& out, const PtgTaskClass* dst, int dst_flow,
+                           const int32_t* dst_locals, DataCopy* data) const;
 
   // ---- dependency tracking (reference parsec.c:1317-1390, 1554-1664)
   // Counter mode: Task::deps_remaining = number of task inputs, decremented per

@@ -37,6 +37,7 @@ def _run(exe, timeout=60, env=None):
     ("startup", "startup seeds 17990/17990 rows 300 sum_ok 1 bad 0"),
     ("udf", "udf chain 40 free 17 keys_used 1 bad 0"),
     ("merge_sort", "merge_sort L=5 B=97 merges 31 bad 0"),
+    ("stencil_1d", "stencil_1d rank 0 tiles 6 err 0.000e+00"),
 ])
 def test_jdf_program(tmp_path, name, expect):
     exe = ptgpp.build_program(os.path.join(JDF, name + ".jdf"), str(tmp_path))
@@ -282,3 +283,18 @@ def test_reference_jdf_corpus(tmp_path):
         elif r.returncode != 0:
             failures.append(f"{rel}: {r.stderr[-400:]}")
     assert not failures, "\n".join(failures)
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 4])
+def test_stencil_1d_remote_reshape(tmp_path, nranks):
+    """Neighbours on other ranks receive only the halo columns of a tile
+    ([type_remote = HALO displ_remote = ...], reference stencil_1D.jdf:83-92);
+    neighbours on the same rank read the whole tile; every rank checks its
+    tiles against the serial stencil."""
+    from parsec_amd.launch import launch
+
+    exe = ptgpp.build_program(os.path.join(JDF, "stencil_1d.jdf"), str(tmp_path))
+    rc, outs = launch(nranks, [exe, "6", "9"], timeout=120, capture=True)
+    text = "".join(o or "" for o, _ in outs)
+    assert rc == 0, text + "".join(e or "" for _, e in outs)
+    assert text.count("err 0.000e+00") == nranks

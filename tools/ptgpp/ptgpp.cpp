@@ -900,9 +900,9 @@ struct Gen {
         break;
     }
     const Prop* ty = find_prop(dprops, "type");
-    if (!ty) ty = find_prop(dprops, "type_remote");
     if (!ty) ty = find_prop(fprops, "type");
     if (ty) o << "__t.datatype_index = " << adt_index(ty->val) << "; ";
+    if (const Prop* tr = find_prop(dprops, "type_remote")) o << "__t.remote_datatype_index = " << adt_index(tr->val) << "; ";
     if (const Prop* d = find_prop(dprops, "displ_remote")) o << "__t.displ_remote = " << lam(f, prop_expr(*d), sc) << "; ";
     if (const Prop* d = find_prop(dprops, "count_remote")) o << "__t.count_remote = " << lam(f, prop_expr(*d), sc) << "; ";
     o << "return __t; }()";
