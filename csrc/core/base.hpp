@@ -270,6 +270,38 @@ class ShardedMap {
   size_t mask_;
 };
 
+// ---------------------------------------------------------------- rw lock
+// Writer-preferring reader/writer spin lock in one 32-bit word (reference
+// class/parsec_rwlock.c, the atomic variant): bit 31 = writer holds it,
+// bit 30 = writer waiting (new readers back off), low bits = reader count.
+class RwLock {
+ public:
+  void rdlock() noexcept {
+    for (;;) {
+      uint32_t v = w_.load(std::memory_order_relaxed);
+      if (!(v & (kWriter | kWaiting)) && w_.compare_exchange_weak(v, v + 1, std::memory_order_acquire)) return;
+      PARSEC_CPU_RELAX();
+    }
+  }
+  void rdunlock() noexcept { w_.fetch_sub(1, std::memory_order_release); }
+  void wrlock() noexcept {
+    for (;;) {
+      uint32_t v = w_.load(std::memory_order_relaxed);
+      if ((v & ~kWaiting) == 0) {
+        if (w_.compare_exchange_weak(v, kWriter, std::memory_order_acquire)) return;
+      } else if (!(v & kWaiting)) {
+        w_.compare_exchange_weak(v, v | kWaiting, std::memory_order_relaxed);
+      }
+      PARSEC_CPU_RELAX();
+    }
+  }
+  void wrunlock() noexcept { w_.store(0, std::memory_order_release); }
+  uint32_t readers() const noexcept { return w_.load(std::memory_order_relaxed) & ~(kWriter | kWaiting); }
+ private:
+  static constexpr uint32_t kWriter = 1u << 31, kWaiting = 1u << 30;
+  std::atomic<uint32_t> w_{0};
+};
+
 // ---------------------------------------------------------------- misc
 inline uint64_t now_ns() {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();

@@ -107,6 +107,7 @@ struct Datatype {
   static Datatype upper(uint32_t esz, int64_t n, int64_t ld, bool diag = true) { Datatype d; d.kind = UPPER; d.elem_size = esz; d.count = n; d.stride = ld; d.diag = diag; return d; }
 };
 
+class DatacopyFuture;
 struct DataCopy : ListItem {  // ListItem: membership in a device LRU
   std::atomic<int32_t> refcount{1};
   Data* original = nullptr;
@@ -123,6 +124,11 @@ struct DataCopy : ListItem {  // ListItem: membership in a device LRU
   void* push_task = nullptr;       // GPU task currently staging this copy
   void* dev_state = nullptr;       // device module private (events, LRU owner)
   void (*release_fn)(DataCopy*) = nullptr;  // custom destruction (e.g. comm receive buffers)
+  // reshaped views of this copy shared by the successors that read it with
+  // the same datatype (one future per version; see ptg.cpp reshape_inputs)
+  std::shared_ptr<DatacopyFuture> reshape_future;
+  uint32_t reshape_version = 0;
+  const void* reshape_owner = nullptr;  // taskpool whose arenas produced the views
   void* ptr() const { return device_private; }
 };
 

@@ -5,6 +5,7 @@
 #include <cstring>
 
 #include "../comm/comm.hpp"
+#include "../core/future.hpp"
 #include "../core/mca.hpp"
 #include "../device/device.hpp"
 #include "../prof/profiling.hpp"
@@ -439,10 +440,71 @@ int PtgTaskClass::prepare_input(ExecutionStream* es, Task* t) const {
 }
 
 // Local reshape (reference parsec_reshape.c:29-771): an input dependency that
-// names an arena datatype other than DEFAULT receives a private copy holding
-// only the elements of that layout (e.g. [type = LOWER]: the lower triangle,
-// zeros elsewhere) when the incoming copy has a different layout. Host copies
-// only; device-resident inputs are passed unchanged.
+// names an arena datatype other than DEFAULT receives a copy holding only the
+// elements of that layout (e.g. [type = LOWER]: the lower triangle, zeros
+// elsewhere) when the incoming copy has a different layout. Read-only inputs
+// share the reshaped copy through a DatacopyFuture kept on the source copy
+// (one per source version, one nested future per target datatype): the first
+// successor produces it, the others wait for and retain it, like the
+// reference's reshape promises. Writable inputs get a private copy. Host
+// copies only; device-resident inputs are passed unchanged.
+static SpinLock g_reshape_locks[64];
+
+static DataCopy* reshape_produce(const ArenaDatatype* adt, const DataCopy* c) {
+  const Datatype& want = adt->opaque_dtt;
+  DataCopy* nc = adt->arena->get_copy(nullptr, 0);
+  if (!nc) return nullptr;
+  std::memset(nc->device_private, 0, adt->arena->elem_size);
+  std::vector<uint8_t> tmp((size_t)want.packed_bytes());
+  want.pack(c->device_private, tmp.data());
+  want.unpack(tmp.data(), nc->device_private);
+  nc->dtt = want;
+  return nc;
+}
+
+static SpinLock& reshape_lock(const DataCopy* c) { return g_reshape_locks[(reinterpret_cast<uintptr_t>(c) >> 6) & 63]; }
+
+static std::shared_ptr<DatacopyFuture> reshape_future_of(PtgTaskpool* tp, DataCopy* c) {
+  std::lock_guard<SpinLock> g(reshape_lock(c));
+  if (!c->reshape_future || c->reshape_version != c->version || c->reshape_owner != tp) {
+    if (c->reshape_owner != tp) {
+      std::lock_guard<std::mutex> g2(tp->reshape_m);
+      data_copy_retain(c);
+      tp->reshape_sources.push_back(c);
+    }
+    c->reshape_owner = tp;
+    // a new version invalidates the views of the old one (holders keep
+    // their own references to the copies they already got)
+    c->reshape_future = std::make_shared<DatacopyFuture>(
+        c, nullptr,
+        [](void* in, const void* spec) -> void* { return reshape_produce(static_cast<const ArenaDatatype*>(spec), static_cast<DataCopy*>(in)); },
+        [](const void* a, const void* b) { return static_cast<const ArenaDatatype*>(a)->opaque_dtt == static_cast<const ArenaDatatype*>(b)->opaque_dtt; },
+        [](void* v) { data_copy_release(static_cast<DataCopy*>(v)); });
+    c->reshape_version = c->version;
+  }
+  return c->reshape_future;
+}
+
+void PtgTaskpool::drop_reshape_views() {
+  std::vector<DataCopy*> srcs;
+  {
+    std::lock_guard<std::mutex> g(reshape_m);
+    srcs.swap(reshape_sources);
+  }
+  for (DataCopy* c : srcs) {
+    std::shared_ptr<DatacopyFuture> old;
+    {
+      std::lock_guard<SpinLock> g(reshape_lock(c));
+      if (c->reshape_owner == this) {
+        old.swap(c->reshape_future);
+        c->reshape_owner = nullptr;
+      }
+    }
+    old.reset();  // releases the views (their holders keep their own references)
+    data_copy_release(c);
+  }
+}
+
 void PtgTaskClass::reshape_inputs(Task* t) const {
   auto& adts = t->taskpool->arenas_datatypes;
   for (size_t f = 0; f < def.flows.size(); ++f) {
@@ -452,15 +514,16 @@ void PtgTaskClass::reshape_inputs(Task* t) const {
     const DepTarget* tg = active_input(t->taskpool, (int)f, t->locals);
     if (!tg || tg->datatype_index <= 0 || tg->datatype_index >= (int)adts.size()) continue;
     const ArenaDatatype& adt = adts[tg->datatype_index];
-    const Datatype& want = adt.opaque_dtt;
-    if (!adt.arena || want.kind == Datatype::NONE || want == c->dtt) continue;
-    DataCopy* nc = adt.arena->get_copy(nullptr, 0);
+    if (!adt.arena || adt.opaque_dtt.kind == Datatype::NONE || adt.opaque_dtt == c->dtt) continue;
+    DataCopy* nc = nullptr;
+    if (def.flows[f].access == FLOW_READ) {
+      std::shared_ptr<DatacopyFuture> fut = reshape_future_of(static_cast<PtgTaskpool*>(t->taskpool), c);
+      nc = static_cast<DataCopy*>(fut->get_or_trigger(&adt));
+      if (nc) data_copy_retain(nc);
+    } else {
+      nc = reshape_produce(&adt, c);
+    }
     if (!nc) continue;
-    std::memset(nc->device_private, 0, adt.arena->elem_size);
-    std::vector<uint8_t> tmp((size_t)want.packed_bytes());
-    want.pack(c->device_private, tmp.data());
-    want.unpack(tmp.data(), nc->device_private);
-    nc->dtt = want;
     data_copy_release(c);
     r.data_in = nc;
   }
@@ -604,6 +667,7 @@ int PtgTaskClass::complete_execution(ExecutionStream* es, Task* t) const {
 PtgTaskpool::PtgTaskpool() { taskpool_name = "ptg"; }
 
 PtgTaskpool::~PtgTaskpool() {
+  drop_reshape_views();
   pending.for_each([](uint64_t, Task* t) {
     for (int f = 0; f < kMaxFlows; ++f) if (t->data[f].data_in) data_copy_release(t->data[f].data_in);
     task_free(t);

@@ -234,8 +234,14 @@ class PtgTaskpool : public Taskpool {
   // back results here, e.g. the LAPACK info of a factorization)
   std::function<void()> complete_hook;
   void on_complete_internal() override {
+    drop_reshape_views();
     if (complete_hook) complete_hook();
   }
+  // source copies holding shared reshaped views made from this taskpool's
+  // arenas (retained; views dropped when the taskpool completes or dies)
+  std::mutex reshape_m;
+  std::vector<DataCopy*> reshape_sources;
+  void drop_reshape_views();
   PtgTaskpool();
   ~PtgTaskpool() override;
   PtgTaskClass* add_task_class(TaskClassDef def);

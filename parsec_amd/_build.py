@@ -62,7 +62,7 @@ PTGPP_SOURCES = ["tools/ptgpp/ptgpp.cpp"]
 JDF_SOURCES = ["csrc/algos/jdf/dpotrf_L.jdf"]
 # runtime sources that include generated JDF headers
 JDF_USERS = ["csrc/algos/dpotrf_jdf.cpp"]
-TEST_SOURCES = ["tests/native/test_containers.cpp"]
+TEST_SOURCES = ["tests/native/test_containers.cpp", "tests/native/test_futures.cpp"]
 
 
 def _exists(paths):

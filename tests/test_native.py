@@ -1,5 +1,5 @@
 """Runs the native C++ unit-test programs built by parsec_amd._build
-(build/tests/*): lock-free containers, mempool, sharded hash map, barrier."""
+(build/tests/*): lock-free containers, mempool, sharded hash map, barrier, futures, rwlock."""
 import os
 import subprocess
 
@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "build", "tests")
 
 
-@pytest.mark.parametrize("prog", ["test_containers"])
+@pytest.mark.parametrize("prog", ["test_containers", "test_futures"])
 def test_native_program(pa, prog):
     exe = os.path.join(BIN, prog)
     if not os.path.exists(exe):

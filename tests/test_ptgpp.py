@@ -26,7 +26,7 @@ def _run(exe, timeout=60, env=None):
     ("chain", "chain value 10"),
     ("bcast_gather", "leaves 37 sink 1 bad 0"),
     ("local_indices", "runs 16 48 32 1"),
-    ("reshape", "reshape ok 5 bad 0 full 1"),
+    ("reshape", "reshape ok 15 bad 0 full 1 upper 5 shared 1"),
     ("tree_reduce", "root 2080 nodes 63 bad 0"),
     ("pingpong", "hops 101 bad 0"),
     ("all2all", "recv 16 done 4 bad 0"),
