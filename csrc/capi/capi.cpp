@@ -215,8 +215,45 @@ int parsec_type_size(parsec_datatype_t type, int* size) {
   return PARSEC_SUCCESS;
 }
 int parsec_type_extent(parsec_datatype_t type, ptrdiff_t* lb, ptrdiff_t* extent) {
-  if (lb) *lb = 0;
-  *extent = (ptrdiff_t)type_of(type).extent_bytes();
+  Datatype t = type_of(type);
+  if (lb) *lb = (ptrdiff_t)t.lb;
+  *extent = (ptrdiff_t)t.extent_bytes();
+  return PARSEC_SUCCESS;
+}
+int parsec_type_create_hvector(int count, int blocklength, ptrdiff_t stride_bytes, parsec_datatype_t oldtype, parsec_datatype_t* newtype) {
+  *newtype = new_type(Datatype::hvector(type_of(oldtype), count, blocklength, stride_bytes));
+  return PARSEC_SUCCESS;
+}
+int parsec_type_create_indexed(int count, const int blocklengths[], const int displacements[], parsec_datatype_t oldtype, parsec_datatype_t* newtype) {
+  Datatype o = type_of(oldtype);
+  if (o.kind == Datatype::CONTIGUOUS && o.count == 1) {  // element type: keep the typed INDEXED form
+    Datatype d; d.kind = Datatype::INDEXED; d.elem_size = o.elem_size;
+    for (int i = 0; i < count; ++i) d.blocks.emplace_back(displacements[i], blocklengths[i]);
+    *newtype = new_type(d);
+    return PARSEC_SUCCESS;
+  }
+  std::vector<int64_t> c(count), dl(count);
+  for (int i = 0; i < count; ++i) { c[i] = blocklengths[i]; dl[i] = (int64_t)displacements[i] * o.extent_bytes(); }
+  *newtype = new_type(Datatype::structure(c, dl, std::vector<Datatype>(count, o)));
+  return PARSEC_SUCCESS;
+}
+int parsec_type_create_struct(int count, const int blocklengths[], const ptrdiff_t displacements[], const parsec_datatype_t types[], parsec_datatype_t* newtype) {
+  std::vector<int64_t> c(count), dl(count);
+  std::vector<Datatype> ts;
+  for (int i = 0; i < count; ++i) { c[i] = blocklengths[i]; dl[i] = displacements[i]; ts.push_back(type_of(types[i])); }
+  *newtype = new_type(Datatype::structure(c, dl, ts));
+  return PARSEC_SUCCESS;
+}
+int parsec_type_create_resized(parsec_datatype_t oldtype, ptrdiff_t lb, ptrdiff_t extent, parsec_datatype_t* newtype) {
+  *newtype = new_type(Datatype::resized(type_of(oldtype), lb, extent));
+  return PARSEC_SUCCESS;
+}
+int parsec_type_pack(parsec_datatype_t type, const void* src, void* dst) {
+  type_of(type).pack(src, dst);
+  return PARSEC_SUCCESS;
+}
+int parsec_type_unpack(parsec_datatype_t type, const void* src, void* dst) {
+  type_of(type).unpack(src, dst);
   return PARSEC_SUCCESS;
 }
 int parsec_type_create_contiguous(int count, parsec_datatype_t oldtype, parsec_datatype_t* newtype) {
@@ -464,12 +501,13 @@ int parsec_add2arena_rect(parsec_arena_datatype_t* adt, parsec_datatype_t oldtyp
   return PARSEC_SUCCESS;
 }
 int parsec_add2arena(parsec_arena_datatype_t* adt, parsec_datatype_t oldtype, parsec_matrix_uplo_t uplo, int diag, int m, int n, int ld, size_t alignment, int resized) {
-  (void)resized;
   const uint32_t esz = type_of(oldtype).elem_size;
   Datatype d;
   if (uplo == PARSEC_MATRIX_LOWER) d = Datatype::lower(esz, m, ld, diag != 0);
   else if (uplo == PARSEC_MATRIX_UPPER) d = Datatype::upper(esz, m, ld, diag != 0);
   else d = ld == m ? Datatype::contiguous(esz, (int64_t)m * n) : Datatype::vector(esz, n, m, ld);
+  // resized >= 0: the type's extent becomes `resized` elements (reference matrixtypes.c:53-55)
+  if (resized >= 0) d = Datatype::resized(d, 0, (int64_t)resized * esz);
   add2arena(*adt, d, alignment ? alignment : 64);
   // the arena element is always the full m x ld tile so NEW copies can hold any layout
   adt->arena = std::make_shared<Arena>((size_t)ld * n * esz, alignment ? alignment : 64, d);

@@ -87,17 +87,25 @@ enum DataFlags : uint8_t {
 
 // Datatype: a typed, possibly strided layout. Replaces MPI datatypes of the
 // reference (datatype.h:14-130): contiguous, vector (count x blocklen, stride),
-// lower/upper triangles of a column-major tile, indexed.
+// lower/upper triangles of a column-major tile, indexed, and BYTES -- a list of
+// (byte offset, byte length) runs that hvector / hindexed / struct layouts
+// flatten into. `extent_override` / `lb` implement resized types: the layout
+// is unchanged, only the stride between consecutive items (count > 1) moves.
 struct Datatype {
-  enum Kind : uint8_t { NONE = 0, CONTIGUOUS, VECTOR, LOWER, UPPER, INDEXED } kind = NONE;
-  uint32_t elem_size = 1;   // bytes per element
+  enum Kind : uint8_t { NONE = 0, CONTIGUOUS, VECTOR, LOWER, UPPER, INDEXED, BYTES } kind = NONE;
+  uint32_t elem_size = 1;   // bytes per element (BYTES: 1)
   int64_t count = 0;        // CONTIGUOUS: elements; VECTOR: number of blocks; LOWER/UPPER: n (square)
   int64_t blocklen = 0;     // VECTOR: elements per block
   int64_t stride = 0;       // VECTOR / LOWER / UPPER: leading dimension in elements
   bool diag = true;         // LOWER/UPPER: include the diagonal
-  std::vector<std::pair<int64_t, int64_t>> blocks;  // INDEXED: (offset elems, length elems)
+  std::vector<std::pair<int64_t, int64_t>> blocks;  // INDEXED: (offset elems, length elems); BYTES: (offset bytes, length bytes)
+  int64_t lb = 0;                // resized lower bound (bytes)
+  int64_t extent_override = -1;  // resized extent (bytes), -1 = natural
   int64_t packed_bytes() const;
   int64_t extent_bytes() const;
+  int64_t natural_extent_bytes() const;
+  // every layout as byte runs in packing order
+  std::vector<std::pair<int64_t, int64_t>> byte_runs() const;
   void pack(const void* src, void* dst) const;    // gather layout -> contiguous
   void unpack(const void* src, void* dst) const;  // scatter contiguous -> layout
   bool operator==(const Datatype& o) const;
@@ -105,6 +113,12 @@ struct Datatype {
   static Datatype vector(uint32_t esz, int64_t count, int64_t blocklen, int64_t stride) { Datatype d; d.kind = VECTOR; d.elem_size = esz; d.count = count; d.blocklen = blocklen; d.stride = stride; return d; }
   static Datatype lower(uint32_t esz, int64_t n, int64_t ld, bool diag = true) { Datatype d; d.kind = LOWER; d.elem_size = esz; d.count = n; d.stride = ld; d.diag = diag; return d; }
   static Datatype upper(uint32_t esz, int64_t n, int64_t ld, bool diag = true) { Datatype d; d.kind = UPPER; d.elem_size = esz; d.count = n; d.stride = ld; d.diag = diag; return d; }
+  static Datatype bytes(std::vector<std::pair<int64_t, int64_t>> runs) { Datatype d; d.kind = BYTES; d.elem_size = 1; d.blocks = std::move(runs); return d; }
+  // count blocks of `blocklen` items of `old`, block starts `stride_bytes` apart
+  static Datatype hvector(const Datatype& old, int64_t count, int64_t blocklen, int64_t stride_bytes);
+  // struct: block i = counts[i] items of types[i] at byte displacement displs[i]
+  static Datatype structure(const std::vector<int64_t>& counts, const std::vector<int64_t>& displs, const std::vector<Datatype>& types);
+  static Datatype resized(const Datatype& old, int64_t lb, int64_t extent) { Datatype d = old; d.lb = lb; d.extent_override = extent; return d; }
 };
 
 class DatacopyFuture;

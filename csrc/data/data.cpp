@@ -28,7 +28,8 @@ int64_t Datatype::packed_bytes() const {
       int64_t e = diag ? n * (n + 1) / 2 : n * (n - 1) / 2;
       return e * elem_size;
     }
-    case INDEXED: {
+    case INDEXED:
+    case BYTES: {
       int64_t s = 0;
       for (auto& b : blocks) s += b.second;
       return s * elem_size;
@@ -37,14 +38,15 @@ int64_t Datatype::packed_bytes() const {
   return 0;
 }
 
-int64_t Datatype::extent_bytes() const {
+int64_t Datatype::natural_extent_bytes() const {
   switch (kind) {
     case NONE: return 0;
     case CONTIGUOUS: return count * elem_size;
     case VECTOR: return count > 0 ? ((count - 1) * stride + blocklen) * elem_size : 0;
     case LOWER:
     case UPPER: return count * stride * elem_size;
-    case INDEXED: {
+    case INDEXED:
+    case BYTES: {
       int64_t e = 0;
       for (auto& b : blocks) e = std::max(e, b.first + b.second);
       return e * elem_size;
@@ -53,34 +55,61 @@ int64_t Datatype::extent_bytes() const {
   return 0;
 }
 
+int64_t Datatype::extent_bytes() const { return extent_override >= 0 ? extent_override : natural_extent_bytes(); }
+
+std::vector<std::pair<int64_t, int64_t>> Datatype::byte_runs() const {
+  std::vector<std::pair<int64_t, int64_t>> r;
+  const int64_t es = elem_size;
+  auto add = [&](int64_t off_elems, int64_t n_elems) {
+    if (n_elems <= 0) return;
+    // merge with the previous run when contiguous (vector of full columns, ...)
+    if (!r.empty() && r.back().first + r.back().second == off_elems * es) r.back().second += n_elems * es;
+    else r.emplace_back(off_elems * es, n_elems * es);
+  };
+  switch (kind) {
+    case NONE: break;
+    case CONTIGUOUS: add(0, count); break;
+    case VECTOR: for (int64_t b = 0; b < count; ++b) add(b * stride, blocklen); break;
+    case LOWER:  // column-major: column j rows j(+1)..n-1
+      for (int64_t j = 0; j < count; ++j) { int64_t r0 = diag ? j : j + 1; add(j * stride + r0, count - r0); }
+      break;
+    case UPPER:  // column j rows 0..j(-1)
+      for (int64_t j = 0; j < count; ++j) add(j * stride, diag ? j + 1 : j);
+      break;
+    case INDEXED: for (auto& b : blocks) add(b.first, b.second); break;
+    case BYTES: for (auto& b : blocks) { if (b.second > 0) { if (!r.empty() && r.back().first + r.back().second == b.first) r.back().second += b.second; else r.push_back(b); } } break;
+  }
+  return r;
+}
+
+Datatype Datatype::hvector(const Datatype& old, int64_t count, int64_t blocklen, int64_t stride_bytes) {
+  std::vector<std::pair<int64_t, int64_t>> runs;
+  const auto base = old.byte_runs();
+  const int64_t ext = old.extent_bytes();
+  for (int64_t b = 0; b < count; ++b)
+    for (int64_t i = 0; i < blocklen; ++i)
+      for (auto& x : base) runs.emplace_back(b * stride_bytes + i * ext + x.first, x.second);
+  return bytes(std::move(runs));
+}
+
+Datatype Datatype::structure(const std::vector<int64_t>& counts, const std::vector<int64_t>& displs, const std::vector<Datatype>& types) {
+  std::vector<std::pair<int64_t, int64_t>> runs;
+  for (size_t k = 0; k < counts.size() && k < displs.size() && k < types.size(); ++k) {
+    const auto base = types[k].byte_runs();
+    const int64_t ext = types[k].extent_bytes();
+    for (int64_t i = 0; i < counts[k]; ++i)
+      for (auto& x : base) runs.emplace_back(displs[k] + i * ext + x.first, x.second);
+  }
+  return bytes(std::move(runs));
+}
+
 template <bool PACK>
 static void xfer(const Datatype& d, const char* src, char* dst) {
-  const int64_t es = d.elem_size;
   int64_t pos = 0;  // packed offset in bytes
-  auto move = [&](int64_t layout_off_elems, int64_t n_elems) {
-    if (n_elems <= 0) return;
-    if (PACK) std::memcpy(dst + pos, src + layout_off_elems * es, n_elems * es);
-    else std::memcpy(dst + layout_off_elems * es, src + pos, n_elems * es);
-    pos += n_elems * es;
-  };
-  switch (d.kind) {
-    case Datatype::NONE: break;
-    case Datatype::CONTIGUOUS: move(0, d.count); break;
-    case Datatype::VECTOR:
-      for (int64_t b = 0; b < d.count; ++b) move(b * d.stride, d.blocklen);
-      break;
-    case Datatype::LOWER:  // column-major: column j rows j(+1)..n-1
-      for (int64_t j = 0; j < d.count; ++j) {
-        int64_t r0 = d.diag ? j : j + 1;
-        move(j * d.stride + r0, d.count - r0);
-      }
-      break;
-    case Datatype::UPPER:  // column j rows 0..j(-1)
-      for (int64_t j = 0; j < d.count; ++j) move(j * d.stride, d.diag ? j + 1 : j);
-      break;
-    case Datatype::INDEXED:
-      for (auto& b : d.blocks) move(b.first, b.second);
-      break;
+  for (auto& run : d.byte_runs()) {
+    if (PACK) std::memcpy(dst + pos, src + run.first, run.second);
+    else std::memcpy(dst + run.first, src + pos, run.second);
+    pos += run.second;
   }
 }
 
@@ -88,7 +117,8 @@ void Datatype::pack(const void* src, void* dst) const { xfer<true>(*this, (const
 void Datatype::unpack(const void* src, void* dst) const { xfer<false>(*this, (const char*)src, (char*)dst); }
 
 bool Datatype::operator==(const Datatype& o) const {
-  return kind == o.kind && elem_size == o.elem_size && count == o.count && blocklen == o.blocklen && stride == o.stride && diag == o.diag && blocks == o.blocks;
+  return kind == o.kind && elem_size == o.elem_size && count == o.count && blocklen == o.blocklen && stride == o.stride && diag == o.diag && blocks == o.blocks &&
+         lb == o.lb && extent_override == o.extent_override;
 }
 
 // =================================================================== data

@@ -104,6 +104,14 @@ int parsec_type_create_contiguous(int count, parsec_datatype_t oldtype, parsec_d
 int parsec_type_create_vector(int count, int blocklength, int stride, parsec_datatype_t oldtype, parsec_datatype_t* newtype);
 int parsec_type_create_lower(int n, int ld, int diag, parsec_datatype_t oldtype, parsec_datatype_t* newtype);
 int parsec_type_create_upper(int n, int ld, int diag, parsec_datatype_t oldtype, parsec_datatype_t* newtype);
+int parsec_type_create_hvector(int count, int blocklength, ptrdiff_t stride_bytes, parsec_datatype_t oldtype, parsec_datatype_t* newtype);
+int parsec_type_create_indexed(int count, const int blocklengths[], const int displacements[], parsec_datatype_t oldtype, parsec_datatype_t* newtype);
+int parsec_type_create_struct(int count, const int blocklengths[], const ptrdiff_t displacements[], const parsec_datatype_t types[], parsec_datatype_t* newtype);
+int parsec_type_create_resized(parsec_datatype_t oldtype, ptrdiff_t lb, ptrdiff_t extent, parsec_datatype_t* newtype);
+/* gather a layout into a contiguous buffer / scatter it back (the role
+ * MPI_Pack / MPI_Unpack play for the reference's MPI datatypes) */
+int parsec_type_pack(parsec_datatype_t type, const void* src, void* dst);
+int parsec_type_unpack(parsec_datatype_t type, const void* src, void* dst);
 int parsec_type_free(parsec_datatype_t* type);
 
 /* --------------------------------------------------------------- context */

@@ -35,6 +35,18 @@ def test_checkpoint_user_storage_after_init(tmp_path, pa):
     assert "ok" in r.stdout
 
 
+def test_datatypes_c_program(tmp_path, pa):
+    """Derived datatypes: vector / hvector / indexed / struct / resized / lower (reference datatype.h)."""
+    exe = tmp_path / "dtt"
+    cmd = ["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-O1", f"-I{ROOT}/include", os.path.join(HERE, "capi", "datatype_capi.c"), "-o", str(exe),
+           f"-L{ROOT}/parsec_amd/lib", "-lparsec_amd", f"-Wl,-rpath,{ROOT}/parsec_amd/lib", "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "datatype ok" in r.stdout
+
+
 def test_dtd_c_program(dtd_capi):
     r = subprocess.run([dtd_capi], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
