@@ -170,30 +170,34 @@ struct PendingArgs {
   std::vector<std::pair<int, int>> sig;
 };
 
+void parse_one(int size, void* ptr, int flags, PendingArgs& pa) {
+  dtd::Arg a;
+  a.op = flags;
+  const int op = flags & dtd::OP_MASK;
+  if (op == dtd::VALUE) {
+    a.ptr = ptr;
+    a.size = size;
+  } else if (op == dtd::SCRATCH) {
+    a.size = size;
+  } else if (op == dtd::REF) {
+    a.ptr = ptr;
+    a.size = size;
+  } else {
+    a.tile = reinterpret_cast<dtd::Tile*>(ptr);
+    a.size = (int)PASSED_BY_REF;
+  }
+  pa.args.push_back(a);
+  pa.sig.push_back({flags, a.size});
+  if ((int)pa.args.size() > PARSEC_DTD_MAX_PARAMS) fatal("parsec_dtd_insert_task: more than %d arguments", PARSEC_DTD_MAX_PARAMS);
+}
+
 void parse_args(va_list ap, PendingArgs& pa) {
   for (;;) {
     int size = va_arg(ap, int);
     if (size == PARSEC_DTD_ARG_END) break;
     void* ptr = va_arg(ap, void*);
     int flags = va_arg(ap, int);
-    dtd::Arg a;
-    a.op = flags;
-    const int op = flags & dtd::OP_MASK;
-    if (op == dtd::VALUE) {
-      a.ptr = ptr;
-      a.size = size;
-    } else if (op == dtd::SCRATCH) {
-      a.size = size;
-    } else if (op == dtd::REF) {
-      a.ptr = ptr;
-      a.size = size;
-    } else {
-      a.tile = reinterpret_cast<dtd::Tile*>(ptr);
-      a.size = (int)PASSED_BY_REF;
-    }
-    pa.args.push_back(a);
-    pa.sig.push_back({flags, a.size});
-    if ((int)pa.args.size() > PARSEC_DTD_MAX_PARAMS) fatal("parsec_dtd_insert_task: more than %d arguments", PARSEC_DTD_MAX_PARAMS);
+    parse_one(size, ptr, flags, pa);
   }
 }
 
@@ -321,13 +325,64 @@ int parsec_context_nb_cores(const parsec_context_t* context) { return context->n
 int parsec_comm_barrier(void) { return comm_size() > 1 ? comm_barrier() : 0; }
 
 // ------------------------------------------------------------- taskpool
+// the raw (cb, data) pairs, for the get_*_callback queries
+static std::mutex g_cb_m;
+static std::map<std::pair<const Taskpool*, int>, std::pair<parsec_event_cb_t, void*>> g_cbs;
 int parsec_taskpool_set_complete_callback(parsec_taskpool_t* tp, parsec_event_cb_t cb, void* cb_data) {
   tp->on_complete = [cb, cb_data](Taskpool* t) { return cb(t, cb_data); };
+  std::lock_guard<std::mutex> g(g_cb_m);
+  g_cbs[{tp, 0}] = {cb, cb_data};
   return PARSEC_SUCCESS;
 }
 int parsec_taskpool_set_enqueue_callback(parsec_taskpool_t* tp, parsec_event_cb_t cb, void* cb_data) {
   tp->on_enqueue = [cb, cb_data](Taskpool* t) { return cb(t, cb_data); };
+  std::lock_guard<std::mutex> g(g_cb_m);
+  g_cbs[{tp, 1}] = {cb, cb_data};
   return PARSEC_SUCCESS;
+}
+static void get_cb(const parsec_taskpool_t* tp, int which, parsec_event_cb_t* cb, void** cb_data, int* ierr) {
+  std::lock_guard<std::mutex> g(g_cb_m);
+  auto it = g_cbs.find({tp, which});
+  *cb = it == g_cbs.end() ? nullptr : it->second.first;
+  *cb_data = it == g_cbs.end() ? nullptr : it->second.second;
+  if (ierr) *ierr = PARSEC_SUCCESS;
+}
+void parsec_taskpool_get_complete_callback_f08(const parsec_taskpool_t* tp, parsec_event_cb_t* cb, void** cb_data, int* ierr) { get_cb(tp, 0, cb, cb_data, ierr); }
+void parsec_taskpool_get_enqueue_callback_f08(const parsec_taskpool_t* tp, parsec_event_cb_t* cb, void** cb_data, int* ierr) { get_cb(tp, 1, cb, cb_data, ierr); }
+
+// ------------------------------------------------------- Fortran / version
+int parsec_version(int* major, int* minor, int* release) {
+  if (major) *major = 2;
+  if (minor) *minor = 0;
+  if (release) *release = 0;
+  return PARSEC_SUCCESS;
+}
+int parsec_version_ex(size_t len, char* out) {
+  if (!out || !len) return PARSEC_ERROR;
+  std::snprintf(out, len, "parsec-amd 2.0.0 (gfx950 HIP engine)");
+  return PARSEC_SUCCESS;
+}
+void parsec_init_f08(int nbcores, parsec_context_t** context, int* ierr) {
+  *context = parsec_init(nbcores, nullptr, nullptr);
+  if (ierr) *ierr = *context ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+void parsec_fini_f08(parsec_context_t** context, int* ierr) {
+  int rc = parsec_fini(context);
+  if (ierr) *ierr = rc;
+}
+void parsec_profiling_init_f08(const char* basename, int len, int* ierr) {
+  std::string b(basename, (size_t)std::max(len, 0));
+  int rc = parsec_profiling_init(b.c_str());
+  if (ierr) *ierr = rc;
+}
+void parsec_profile_add_dictionary_keyword_f08(const char* name, int name_len, const char* attributes, int attr_len, int info_length, int* key_start, int* key_end, int* ierr) {
+  std::string n(name, (size_t)std::max(name_len, 0)), a(attributes, (size_t)std::max(attr_len, 0));
+  int rc = parsec_profiling_add_dictionary_keyword(n.c_str(), a.c_str(), (size_t)std::max(info_length, 0), "", key_start, key_end);
+  if (ierr) *ierr = rc >= 0 ? PARSEC_SUCCESS : rc;
+}
+void parsec_profiling_trace_f08(int key, int64_t event_id, int taskpool_id, int* ierr) {
+  int rc = parsec_profiling_trace(key, (uint64_t)event_id, (uint32_t)taskpool_id, nullptr);
+  if (ierr) *ierr = rc >= 0 ? PARSEC_SUCCESS : rc;
 }
 int32_t parsec_taskpool_set_priority(parsec_taskpool_t* tp, int32_t p) { return taskpool_set_priority(tp, p); }
 int parsec_taskpool_wait(parsec_taskpool_t* tp) {
@@ -539,13 +594,8 @@ void parsec_dtd_set_window(parsec_taskpool_t* tp, int64_t window, int64_t thresh
   d->threshold = threshold;
 }
 
-void parsec_dtd_insert_task(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, int priority, int device_type, const char* name, ...) {
+static void dtd_insert(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, int priority, int device_type, const char* name, PendingArgs& pa) {
   auto* d = as_dtd(tp);
-  PendingArgs pa;
-  va_list ap;
-  va_start(ap, name);
-  parse_args(ap, pa);
-  va_end(ap);
   char key[64];
   snprintf(key, sizeof key, "@%p", (void*)fpointer);
   std::string cname = std::string(name ? name : "dtd_task") + key;
@@ -574,6 +624,27 @@ void parsec_dtd_insert_task(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointe
   }
   d->insert_task(tc, priority, pa.args);
 }
+
+void parsec_dtd_insert_task(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, int priority, int device_type, const char* name, ...) {
+  PendingArgs pa;
+  va_list ap;
+  va_start(ap, name);
+  parse_args(ap, pa);
+  va_end(ap);
+  dtd_insert(tp, fpointer, priority, device_type, name, pa);
+}
+
+// Array form of parsec_dtd_insert_task for callers without C varargs
+// (Fortran bindings): argument i is (sizes[i], ptrs[i], flags[i]).
+void parsec_dtd_insert_task_array(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, int priority, int device_type, const char* name, int nargs,
+                                  const int* sizes, void* const* ptrs, const int* flags) {
+  PendingArgs pa;
+  for (int i = 0; i < nargs; ++i) parse_one(sizes[i], ptrs[i], flags[i], pa);
+  dtd_insert(tp, fpointer, priority, device_type, name, pa);
+}
+
+// Pointer to argument i of a running DTD task (value, scratch or tile data).
+void* parsec_dtd_task_arg(parsec_task_t* this_task, int i) { return dtd::task_arg(this_task, i); }
 
 parsec_dtd_task_class_t* parsec_dtd_create_task_class(parsec_taskpool_t* tp, const char* name, ...) {
   auto* d = as_dtd(tp);
@@ -657,6 +728,7 @@ int parsec_profiling_init(const char* basename) {
   return PARSEC_SUCCESS;
 }
 int parsec_profiling_fini(void) { return PARSEC_SUCCESS; }
+int parsec_profiling_reset(void) { return profiling_reset(); }
 int parsec_profiling_add_dictionary_keyword(const char* name, const char* attributes, size_t info_length, const char* convertor_code, int* key_start, int* key_end) {
   return profiling_add_dictionary_keyword(name, attributes ? attributes : "", info_length, convertor_code ? convertor_code : "", key_start, key_end);
 }

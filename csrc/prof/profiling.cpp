@@ -225,6 +225,29 @@ static void wstr(std::ofstream& o, const std::string& s) {
   o.write(s.data(), l);
 }
 
+// Drop every event recorded so far and restart the clock (reference
+// parsec_profiling_reset, profiling.c): waits for pending spills, truncates
+// the spill files, clears the in-memory tails. Keys and streams are kept.
+int profiling_reset() {
+  auto& p = P();
+  {
+    std::unique_lock<std::mutex> lk(p.wm);
+    p.wdone.wait(lk, [&] { return p.jobs_pending == 0; });
+  }
+  std::lock_guard<std::mutex> g(p.m);
+  for (auto* s : p.streams) {
+    std::lock_guard<SpinLock> sg(s->lock);
+    s->events.clear();
+    s->info.clear();
+    s->info_base = 0;
+    s->spilled_events = 0;
+    std::remove(s->spill_ev.c_str());
+    std::remove(s->spill_info.c_str());
+  }
+  p.t0 = now_ns();
+  return 0;
+}
+
 int profiling_dump(const std::string& filename) {
   auto& p = P();
   std::lock_guard<std::mutex> g(p.m);

@@ -69,6 +69,7 @@ ProfilingStream* profiling_stream_create(const std::string& name);
 std::vector<std::pair<std::string, double>> profiling_rusage();
 uint64_t profiling_now();
 int profiling_dump(const std::string& filename);
+int profiling_reset();
 void profiling_add_information(const std::string& key, const std::string& value);
 void profiling_start();
 

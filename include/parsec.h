@@ -280,6 +280,10 @@ void parsec_dtd_data_collection_fini(parsec_data_collection_t* dc);
 int parsec_dtd_data_flush(parsec_taskpool_t* tp, parsec_dtd_tile_t* tile);
 int parsec_dtd_data_flush_all(parsec_taskpool_t* tp, parsec_data_collection_t* dc);
 void parsec_dtd_unpack_args(parsec_task_t* this_task, ...);
+/* varargs-free forms (used by the Fortran bindings) */
+void parsec_dtd_insert_task_array(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, int priority, int device_type, const char* name_of_kernel, int nargs,
+                                  const int* sizes, void* const* ptrs, const int* flags);
+void* parsec_dtd_task_arg(parsec_task_t* this_task, int i);
 void* parsec_dtd_get_dev_ptr(parsec_task_t* this_task, int i);
 void parsec_dtd_set_window(parsec_taskpool_t* tp, int64_t window, int64_t threshold);
 #define PARSEC_DTD_TILE_OF(DC, I, J) parsec_dtd_tile_of((parsec_data_collection_t*)(DC), (DC)->super.super.data_key((parsec_data_collection_t*)(DC), (I), (J)))
@@ -291,6 +295,22 @@ int parsec_profiling_fini(void);
 int parsec_profiling_add_dictionary_keyword(const char* name, const char* attributes, size_t info_length, const char* convertor_code, int* key_start, int* key_end);
 int parsec_profiling_trace(int key, uint64_t event_id, uint32_t taskpool_id, const void* info);
 int parsec_profiling_dump(void);
+int parsec_profiling_reset(void);
+
+/* ---------------------------------------------------------------- version */
+int parsec_version(int* version_major, int* version_minor, int* version_release);
+int parsec_version_ex(size_t len, char* version_string);
+
+/* ------------------------------------------------- Fortran entry points
+ * (reference parsec/fortran/parsecf.c, parsec_profilef.c): no argc/argv,
+ * Fortran strings arrive with their length. */
+void parsec_init_f08(int nbcores, parsec_context_t** context, int* ierr);
+void parsec_fini_f08(parsec_context_t** context, int* ierr);
+void parsec_taskpool_get_complete_callback_f08(const parsec_taskpool_t* tp, parsec_event_cb_t* cb, void** cb_data, int* ierr);
+void parsec_taskpool_get_enqueue_callback_f08(const parsec_taskpool_t* tp, parsec_event_cb_t* cb, void** cb_data, int* ierr);
+void parsec_profiling_init_f08(const char* basename, int len, int* ierr);
+void parsec_profile_add_dictionary_keyword_f08(const char* name, int name_len, const char* attributes, int attr_len, int info_length, int* key_start, int* key_end, int* ierr);
+void parsec_profiling_trace_f08(int key, int64_t event_id, int taskpool_id, int* ierr);
 
 #ifdef __cplusplus
 }

@@ -62,6 +62,8 @@ PTGPP_SOURCES = ["tools/ptgpp/ptgpp.cpp"]
 JDF_SOURCES = ["csrc/algos/jdf/dpotrf_L.jdf"]
 # runtime sources that include generated JDF headers
 JDF_USERS = ["csrc/algos/dpotrf_jdf.cpp"]
+FORTRAN_SOURCES = ["csrc/fortran/parsecf.F90", "csrc/fortran/parsec_profilef.F90"]
+FLANG = os.path.join(ROCM, "lib", "llvm", "bin", "flang")
 TEST_SOURCES = ["tests/native/test_containers.cpp", "tests/native/test_futures.cpp"]
 
 
@@ -167,6 +169,23 @@ def generate():
         lines.append(f"build obj/tools_bandwidth.o: cxx {os.path.join(ROOT, bw)}")
         lines.append(f"build {os.path.join(PKG, 'bin', 'parsec-bandwidth')}: exelink obj/tools_bandwidth.o")
         lines.append(f"  libs = -L{ROCM}/lib -lamdhip64 -Wl,-rpath,{ROCM}/lib")
+    # Fortran 2008 modules (parsec_f08, parsec_profile_f08) with ROCm's flang:
+    # objects in parsec_amd/lib, .mod files in parsec_amd/include/fortran
+    if os.path.exists(FLANG) and _exists(FORTRAN_SOURCES):
+        moddir = os.path.join(PKG, "include", "fortran")
+        os.makedirs(moddir, exist_ok=True)
+        lines.append("rule fc")
+        lines.append(f"  command = {FLANG} -O2 -fPIC -module-dir {moddir} -c $in -o $out")
+        lines.append("  description = FC $out")
+        fobjs = []
+        for src in _exists(FORTRAN_SOURCES):
+            fo = os.path.join(PKG, "lib", os.path.splitext(os.path.basename(src))[0] + ".o")
+            lines.append(f"build {fo}: fc {os.path.join(ROOT, src)}")
+            fobjs.append(fo)
+        lines.append("rule ar")
+        lines.append("  command = rm -f $out && ar rcs $out $in")
+        lines.append("  description = AR $out")
+        lines.append(f"build {os.path.join(PKG, 'lib', 'libparsec_amd_f08.a')}: ar {' '.join(fobjs)}")
     for src in _exists(TEST_SOURCES):
         obj = os.path.join("obj", src.replace("/", "_") + ".o")
         exe = os.path.join(BUILD, "tests", os.path.splitext(os.path.basename(src))[0])
