@@ -298,3 +298,25 @@ def test_stencil_1d_remote_reshape(tmp_path, nranks):
     text = "".join(o or "" for o, _ in outs)
     assert rc == 0, text + "".join(e or "" for _, e in outs)
     assert text.count("err 0.000e+00") == nranks
+
+
+SCHEDULERS = ["lfq", "pbq", "ltq", "lhq", "ap", "spq", "gd", "ll", "llp", "rnd", "ip"]
+
+
+@pytest.fixture(scope="module")
+def ep_exe(tmp_path_factory):
+    return ptgpp.build_program(os.path.join(JDF, "ep.jdf"), str(tmp_path_factory.mktemp("ep")))
+
+
+@pytest.mark.parametrize("sched", SCHEDULERS)
+def test_empty_task_benchmark(ep_exe, sched):
+    """Empty-task scheduling cost under every scheduler (reference
+    tests/runtime/scheduling/main.c:88-130 + ep.jdf): all chains complete and
+    a per-task time is reported."""
+    r = subprocess.run([ep_exe, "64", "32", "2", "--", "--mca", "mca_sched", sched], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = [x for x in r.stdout.splitlines() if x.startswith("ep ")][-1]
+    assert "tasks 2049" in line and "ran_ok 1" in line
+    us = float(line.split("us_per_task ")[1].split()[0])
+    assert 0 < us < 1000
