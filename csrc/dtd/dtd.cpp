@@ -282,6 +282,13 @@ DtdTask* DtdTaskpool::insert_task(DtdTaskClass* tc, int priority, const std::vec
   for (auto& a : t->args) {
     int op = a.op & OP_MASK;
     if (op == VALUE) {
+      // VALUE | AFFINITY: the int value names the rank that runs the task
+      // (reference dtd_test_task_placement.c; out-of-range ranks -> rank 0)
+      if ((a.op & AFFINITY) && rank < 0 && a.ptr && a.size == (int)sizeof(int32_t)) {
+        int32_t r;
+        std::memcpy(&r, a.ptr, sizeof r);
+        rank = r >= 0 && r < ctx->nb_nodes ? r : 0;
+      }
       if (a.size > 0 && a.ptr) std::memcpy(t->values.data() + off, a.ptr, (size_t)a.size);
       a.ptr = t->values.data() + off;
       off += (size_t)a.size;

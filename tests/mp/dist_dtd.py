@@ -87,6 +87,35 @@ def main():
             t0, t1 = t0 + 1, t1 + 2
             t0 += t1
         expect = t0 if rank == 0 else (t1 if rank == 1 else rank + 1.0)
+    elif case == "placement":
+        # VALUE | AFFINITY places a task on the rank it names; out-of-range
+        # ranks fall back to rank 0 (reference dtd_test_task_placement.c)
+        ran = []
+
+        def placed(task):
+            ran.append(task.value_int(0))
+            return 0
+
+        for r in range(size + 1):
+            pa.insert_task(tp, placed, [(r, pa.VALUE | pa.AFFINITY)])
+        tp.wait()
+        bad = [r for r in ran if (r if r < size else 0) != rank]
+        mine[:] = len(ran) if not bad else -1
+        expect = 2.0 if rank == 0 else 1.0
+    elif case == "null_tile":
+        # NULL passed as a tile: the task runs on the inserting rank with a
+        # null argument (reference dtd_test_null_as_tile.c)
+        ran = []
+
+        def nulltask(task):
+            ran.append(task.arg(0) is None)
+            return 0
+
+        for _ in range(5):
+            pa.insert_task(tp, nulltask, [(None, pa.INOUT)])
+        tp.wait()
+        mine[:] = sum(ran)
+        expect = 5.0
     else:
         raise SystemExit(f"unknown case {case}")
     tp.data_flush_all(A)

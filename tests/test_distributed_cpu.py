@@ -63,7 +63,7 @@ def test_distributed_other_schedulers(pa, sched):
         assert rc == 0, out
 
 
-@pytest.mark.parametrize("case", ["broadcast", "reduce", "allreduce", "pingpong", "war", "multiflow"])
+@pytest.mark.parametrize("case", ["broadcast", "reduce", "allreduce", "pingpong", "war", "multiflow", "placement", "null_tile"])
 @pytest.mark.parametrize("nranks", [2, 3])
 def test_distributed_dtd_patterns(pa, case, nranks):
     """Distributed DTD: one writer read on every rank, reduction into rank 0,
