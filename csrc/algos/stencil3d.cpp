@@ -27,6 +27,7 @@
 namespace parsec {
 namespace kern {
 using StencilArgs = StencilDesc;
+void launch_stencil_init(const StencilInitDesc& d, hipStream_t stream);
 }  // namespace kern
 
 namespace algos {
@@ -292,6 +293,21 @@ Stencil3DResult stencil3d_run(Context* ctx, StencilGrid* G, int iters, double c0
     if (tc->chores.empty()) {
       const int vidx = 1 + __builtin_popcount(mask);
       const int64_t nx = G->nx, ny = G->ny, nz = G->nz;
+      // HBM-resident grid: the initial condition is computed on the device
+      // (no host round trip of the whole field before the first sweep)
+      if (use_gpu && G->storage_device > 0)
+        tp->add_chore(tc, DEV_HIP, nullptr, [vidx, nx, ny, nz](GpuExecContext* c, Task* t) {
+          const InitParams& ip = *static_cast<const InitParams*>(task_arg(t, vidx));
+          StencilInitDesc d{};
+          d.u = static_cast<double*>(c->ptr(task_arg_flow(t, 0)));
+          int a = 1;
+          for (int dd = 0; dd < 6; ++dd) d.fout[dd] = (ip.p.mask >> dd & 1) ? static_cast<double*>(c->ptr(task_arg_flow(t, a++))) : nullptr;
+          d.bx = ip.p.ex; d.by = ip.p.ey; d.bz = ip.p.ez;
+          d.ox = ip.ox; d.oy = ip.oy; d.oz = ip.oz;
+          d.nx = nx; d.ny = ny; d.nz = nz;
+          c->batch->generic.push_back([d](hipStream_t s) { kern::launch_stencil_init(d, s); });
+          return HOOK_DONE;
+        });
       tp->add_chore(tc, DEV_CPU, [vidx, nx, ny, nz](ExecutionStream*, Task* t) {
         const InitParams& ip = *static_cast<const InitParams*>(task_arg(t, vidx));
         double* u = static_cast<double*>(task_arg(t, 0));

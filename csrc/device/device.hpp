@@ -133,6 +133,14 @@ struct StencilDesc {
   double c0, c1;
 };
 
+// Initial condition of one stencil block (stencil_init_kernel).
+struct StencilInitDesc {
+  double* u;
+  double* fout[6];
+  int bx, by, bz;
+  int64_t ox, oy, oz, nx, ny, nz;
+};
+
 struct KernelBatch {
   std::vector<GemmDesc> gemm;
   std::vector<TrsmDesc> trsm;

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "../device/device.hpp"
 
@@ -64,6 +65,116 @@ __device__ __forceinline__ void stencil7_tile(const StencilArgs& a, int tx, int 
 
 __global__ __launch_bounds__(256) void stencil7_kernel(const StencilArgs a) { stencil7_tile(a, blockIdx.x, blockIdx.y, blockIdx.z); }
 
+// Vectorised variant (even bx, 16-byte aligned buffers): a wave owns one
+// 128-point row segment, each lane two consecutive points loaded as one
+// 16-byte double2 (1 KiB per wave access, fully coalesced); the x neighbours
+// come from the adjacent lanes through cross-lane shuffles, so a plane step
+// issues 3 vector loads (next plane, row above, row below) per 128 points
+// instead of 5 scalar loads per 64. 4 waves = 4 rows, kStencilKc2 planes per
+// workgroup marched with the k-1 / k / k+1 values kept in registers.
+constexpr int kStencilKc2 = 32;
+
+__device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+__device__ __forceinline__ void st2(double* p, double2 v) { *reinterpret_cast<double2*>(p) = v; }
+
+__device__ __forceinline__ void stencil7v_tile(const StencilArgs& a, int tx, int ty, int tz) {
+  const int lane = threadIdx.x & 63;
+  const int i = tx * 128 + lane * 2;
+  const int j = ty * 4 + (threadIdx.x >> 6);
+  const int bx = a.bx, by = a.by, bz = a.bz;
+  const bool in = j < by && i < bx;  // bx even: i + 1 < bx as well
+  const size_t plane = (size_t)bx * by;
+  const size_t row = (size_t)j * bx + i;
+  const double* __restrict__ u = a.u;
+  const int k0 = tz * kStencilKc2, k1 = min(bz, k0 + kStencilKc2);
+  const double2 zero = make_double2(0.0, 0.0);
+  double2 zm = zero, c = zero;
+  if (in) {
+    zm = k0 > 0 ? ld2(u + (size_t)(k0 - 1) * plane + row) : (a.fin[4] ? ld2(a.fin[4] + row) : zero);
+    c = ld2(u + (size_t)k0 * plane + row);
+  }
+  for (int k = k0; k < k1; ++k) {
+    const size_t idx = (size_t)k * plane + row;
+    double2 zp = zero, ym = zero, yp = zero;
+    if (in) {
+      zp = k + 1 < bz ? ld2(u + idx + plane) : (a.fin[5] ? ld2(a.fin[5] + row) : zero);
+      ym = j > 0 ? ld2(u + idx - bx) : (a.fin[2] ? ld2(a.fin[2] + (size_t)k * bx + i) : zero);
+      yp = j + 1 < by ? ld2(u + idx + bx) : (a.fin[3] ? ld2(a.fin[3] + (size_t)k * bx + i) : zero);
+    }
+    // every lane takes part in the shuffles; edge lanes then fetch their
+    // outer neighbour from memory (next segment or the face buffer)
+    double left = __shfl_up(c.y, 1);
+    double right = __shfl_down(c.x, 1);
+    if (in) {
+      if (lane == 0) left = i > 0 ? u[idx - 1] : (a.fin[0] ? a.fin[0][(size_t)k * by + j] : 0.0);
+      if (lane == 63 || i + 2 >= bx) right = i + 2 < bx ? u[idx + 2] : (a.fin[1] ? a.fin[1][(size_t)k * by + j] : 0.0);
+      double2 v;
+      v.x = a.c0 * c.x + a.c1 * (left + c.y + ym.x + yp.x + zm.x + zp.x);
+      v.y = a.c0 * c.y + a.c1 * (c.x + right + ym.y + yp.y + zm.y + zp.y);
+      st2(a.out + idx, v);
+      if (i == 0 && a.fout[0]) a.fout[0][(size_t)k * by + j] = v.x;
+      if (i + 2 == bx && a.fout[1]) a.fout[1][(size_t)k * by + j] = v.y;
+      if (j == 0 && a.fout[2]) st2(a.fout[2] + (size_t)k * bx + i, v);
+      if (j == by - 1 && a.fout[3]) st2(a.fout[3] + (size_t)k * bx + i, v);
+      if (k == 0 && a.fout[4]) st2(a.fout[4] + row, v);
+      if (k == bz - 1 && a.fout[5]) st2(a.fout[5] + row, v);
+    }
+    zm = c;
+    c = zp;
+  }
+}
+
+static int stencil_wgs_v(const StencilArgs& a) { return ((a.bx + 127) / 128) * ((a.by + 3) / 4) * ((a.bz + kStencilKc2 - 1) / kStencilKc2); }
+
+static bool stencil_vec_ok(const StencilArgs& a) {
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (a.bx % 2 || !al(a.u) || !al(a.out)) return false;
+  for (int d = 2; d < 6; ++d)
+    if (!al(a.fin[d]) || !al(a.fout[d])) return false;
+  return true;
+}
+
+__global__ __launch_bounds__(256) void stencil7v_batch_kernel(const StencilBatchArgs args) {
+  const int w = blockIdx.x;
+  int lo = 0, hi = args.count - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (args.start[mid] <= w) lo = mid;
+    else hi = mid - 1;
+  }
+  const StencilArgs& a = args.d[lo];
+  const int local = w - args.start[lo];
+  const int nx = (a.bx + 127) / 128, ny = (a.by + 3) / 4;
+  stencil7v_tile(a, local % nx, (local / nx) % ny, local / (nx * ny));
+}
+
+// Initial condition of a block (the same smooth bump as the host
+// stencil3d_initial) and its boundary planes, written on the device so an
+// HBM-resident grid never goes through the host.
+__global__ __launch_bounds__(256) void stencil_init_kernel(const StencilInitDesc d) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= d.bx || j >= d.by) return;
+  const double fx = (double)(d.ox + i + 1) / (double)(d.nx + 1), fy = (double)(d.oy + j + 1) / (double)(d.ny + 1);
+  const double gxy = fx * (1.0 - fx) * fy * (1.0 - fy) * 64.0;
+  for (int k = 0; k < d.bz; ++k) {
+    const double fz = (double)(d.oz + k + 1) / (double)(d.nz + 1);
+    const double v = gxy * (fz * (1.0 - fz));
+    d.u[(size_t)k * d.bx * d.by + (size_t)j * d.bx + i] = v;
+    if (i == 0 && d.fout[0]) d.fout[0][(size_t)k * d.by + j] = v;
+    if (i == d.bx - 1 && d.fout[1]) d.fout[1][(size_t)k * d.by + j] = v;
+    if (j == 0 && d.fout[2]) d.fout[2][(size_t)k * d.bx + i] = v;
+    if (j == d.by - 1 && d.fout[3]) d.fout[3][(size_t)k * d.bx + i] = v;
+    if (k == 0 && d.fout[4]) d.fout[4][(size_t)j * d.bx + i] = v;
+    if (k == d.bz - 1 && d.fout[5]) d.fout[5][(size_t)j * d.bx + i] = v;
+  }
+}
+
+void launch_stencil_init(const StencilInitDesc& d, hipStream_t stream) {
+  dim3 grid((d.bx + 63) / 64, (d.by + 3) / 4);
+  hipLaunchKernelGGL(stencil_init_kernel, grid, dim3(256), 0, stream, d);
+}
+
 // Every block update of a scheduling round in ONE launch (1D grid over all of
 // their workgroups; a binary search maps the workgroup to its block).
 __global__ __launch_bounds__(256) void stencil7_batch_kernel(const StencilBatchArgs args) {
@@ -87,18 +198,28 @@ void launch_stencil7(const StencilArgs& a, hipStream_t stream) {
   hipLaunchKernelGGL(stencil7_kernel, grid, dim3(256), 0, stream, a);
 }
 
+static int g_stencil_vec = -1;  // PARSEC_STENCIL_VEC=0 forces the scalar kernel
+
 void launch_stencil7_batch(const StencilDesc* d, int n, hipStream_t stream) {
+  if (g_stencil_vec < 0) {
+    const char* e = std::getenv("PARSEC_STENCIL_VEC");
+    g_stencil_vec = e ? std::atoi(e) : 1;
+  }
   for (int s0 = 0; s0 < n; s0 += kMaxStencilBatch) {
     StencilBatchArgs a;
     a.count = std::min(kMaxStencilBatch, n - s0);
+    bool vec = g_stencil_vec != 0;
+    for (int i = 0; i < a.count; ++i) vec = vec && stencil_vec_ok(d[s0 + i]);
     int total = 0;
     for (int i = 0; i < a.count; ++i) {
       a.d[i] = d[s0 + i];
       a.start[i] = total;
-      total += stencil_wgs(a.d[i]);
+      total += vec ? stencil_wgs_v(a.d[i]) : stencil_wgs(a.d[i]);
     }
     a.start[a.count] = total;
-    if (total > 0) hipLaunchKernelGGL(stencil7_batch_kernel, dim3(total), dim3(256), 0, stream, a);
+    if (total <= 0) continue;
+    if (vec) hipLaunchKernelGGL(stencil7v_batch_kernel, dim3(total), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL(stencil7_batch_kernel, dim3(total), dim3(256), 0, stream, a);
   }
 }
 

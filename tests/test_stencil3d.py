@@ -59,7 +59,7 @@ def test_stencil_distributed(pa, nranks):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,b,iters", [(96, 32, 6), (130, 64, 4)])
+@pytest.mark.parametrize("n,b,iters", [(96, 32, 6), (130, 64, 4), (99, 33, 3), (300, 256, 3)])
 def test_stencil_gpu(pa, n, b, iters):
     ctx = pa.init(4)
     dev = pa.first_gpu_device_index()
