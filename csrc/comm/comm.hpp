@@ -26,7 +26,7 @@ namespace parsec {
 enum CommTag : int {
   TAG_GET_INTERNAL = 0, TAG_PUT_INTERNAL = 1, TAG_REMOTE_DEP_ACTIVATE = 2, TAG_GET_DATA = 3, TAG_PUT_END = 4,
   TAG_TERMDET_FOURCOUNTER = 5, TAG_TERMDET_USER_TRIGGER = 6, TAG_DATA_FRAGMENT = 7, TAG_BARRIER = 8, TAG_ALLREDUCE = 9,
-  TAG_DATA_IPC = 10, TAG_IPC_DONE = 11,
+  TAG_DATA_IPC = 10, TAG_IPC_DONE = 11, TAG_AGGREGATE = 12,
   TAG_USER = 16, TAG_MAX = 32,
 };
 
@@ -76,6 +76,10 @@ struct RemoteDepsMsg {
   int32_t priority = 0;
 };
 
+// send-side counters of the communication engine: direct ring writes,
+// backlogged messages, aggregates sent and the messages they carried, the
+// largest per-peer backlog
+std::vector<std::pair<std::string, uint64_t>> comm_stats();
 void remote_dep_init(Context* ctx);
 void remote_dep_fini(Context* ctx);
 void remote_dep_on(Context* ctx);

@@ -317,10 +317,10 @@ void send_activations(Taskpool* tp, const ActHdr& base, int my_pos_root_rank, co
       CommInfo ci{dst, -1, (int64_t)(sizeof(h) + body.size()), PLANE_HOST, 0};
       const uint64_t ev = g_next_id.fetch_add(1);
       comm_trace(k_act_b, ev, h.tp_id, &ci);
-      g_ce->send_am2(TAG_REMOTE_DEP_ACTIVATE, dst, &h, sizeof(h), body.data(), body.size());
+      g_ce->send_am_prio(TAG_REMOTE_DEP_ACTIVATE, dst, &h, sizeof(h), body.data(), body.size(), h.priority);
       comm_trace(k_act_e, ev, h.tp_id, nullptr);
     } else {
-      g_ce->send_am2(TAG_REMOTE_DEP_ACTIVATE, dst, &h, sizeof(h), body.data(), body.size());
+      g_ce->send_am_prio(TAG_REMOTE_DEP_ACTIVATE, dst, &h, sizeof(h), body.data(), body.size(), h.priority);
     }
   }
   release_send(s);  // drop the construction guard
@@ -672,6 +672,18 @@ int comm_init(int rank, int size, const std::string& job_id, int gpu_ordinal) {
   }
   set_debug_rank(rank);
   return 0;
+}
+
+std::vector<std::pair<std::string, uint64_t>> comm_stats() {
+  std::vector<std::pair<std::string, uint64_t>> r;
+  if (!g_ce) return r;
+  auto& st = g_ce->stats;
+  r.emplace_back("direct", st.direct.load());
+  r.emplace_back("backlogged", st.backlogged.load());
+  r.emplace_back("aggregates", st.aggregates.load());
+  r.emplace_back("aggregated_msgs", st.aggregated_msgs.load());
+  r.emplace_back("max_waiting", st.max_waiting.load());
+  return r;
 }
 
 void comm_fini() {

@@ -68,6 +68,23 @@ ShmEngine::ShmEngine(int rank_, int size_, const std::string& job, int gpu) : jo
   size = size_;
   ring_bytes_ = ParamRegistry::instance().reg_sizet("comm", "shm", "ring_bytes", "Bytes of each inbound shared-memory ring", (size_t)8 << 20);
   cbs_.resize(TAG_MAX);
+  aggregate_ = ParamRegistry::instance().reg_int("runtime", "comm", "aggregate", "Pack activations waiting for the same peer into one message (reference runtime_comm_aggregate)", 1) != 0;
+  // an aggregate: [u32 count] then per message [i32 tag][u32 len][bytes, 8-aligned]
+  cbs_[TAG_AGGREGATE] = [this](int src, int, const void* msg, size_t len) {
+    const char* p = static_cast<const char*>(msg);
+    uint32_t count;
+    std::memcpy(&count, p, 4);
+    size_t off = 8;
+    for (uint32_t i = 0; i < count && off + 8 <= len; ++i) {
+      int32_t tag;
+      uint32_t n;
+      std::memcpy(&tag, p + off, 4);
+      std::memcpy(&n, p + off + 4, 4);
+      off += 8;
+      if (tag >= 0 && tag < TAG_MAX && cbs_[tag]) cbs_[tag](src, tag, p + off, n);
+      off += (n + 7) & ~(size_t)7;
+    }
+  };
   for (int i = 0; i < size; ++i) out_.emplace_back(new Out());
   maps_.assign(size, nullptr);
   map_len_.assign(size, 0);
@@ -249,13 +266,109 @@ int ShmEngine::send_am2(int tag, int dst, const void* hdr, size_t hlen, const vo
   }
   Out& o = *out_[dst];
   std::lock_guard<std::mutex> g(o.m);
-  if (o.backlog.empty() && ring_write(out_ring(dst), hdr, hlen, payload, plen, tag, rank)) return 0;
+  if (o.backlog.empty() && ring_write(out_ring(dst), hdr, hlen, payload, plen, tag, rank)) {
+    stats.direct.fetch_add(1, std::memory_order_relaxed);
+    return 0;
+  }
   std::vector<char> m(sizeof(int) + hlen + plen);
   std::memcpy(m.data(), &tag, sizeof(int));
   if (hlen) std::memcpy(m.data() + sizeof(int), hdr, hlen);
   if (plen) std::memcpy(m.data() + sizeof(int) + hlen, payload, plen);
   o.backlog.push_back(std::move(m));
+  note_waiting(o, 1);
   return 0;
+}
+
+void ShmEngine::note_waiting(Out& o, int delta) {
+  const int w = o.waiting.fetch_add(delta, std::memory_order_relaxed) + delta;
+  if (delta > 0) {
+    stats.backlogged.fetch_add(1, std::memory_order_relaxed);
+    uint64_t m = stats.max_waiting.load(std::memory_order_relaxed);
+    while ((uint64_t)w > m && !stats.max_waiting.compare_exchange_weak(m, (uint64_t)w, std::memory_order_relaxed)) {}
+  }
+}
+
+int ShmEngine::send_am_prio(int tag, int dst, const void* hdr, size_t hlen, const void* payload, size_t plen, int32_t priority) {
+  if (dst == rank) return send_am2(tag, dst, hdr, hlen, payload, plen);
+  Out& o = *out_[dst];
+  std::lock_guard<std::mutex> g(o.m);
+  // straight into the ring when nothing of this class waits for the peer
+  if (o.prio.empty() && ring_write(out_ring(dst), hdr, hlen, payload, plen, tag, rank)) {
+    stats.direct.fetch_add(1, std::memory_order_relaxed);
+    return 0;
+  }
+  PrioMsg pm{priority, o.seq++, std::vector<char>(sizeof(int) + hlen + plen)};
+  std::memcpy(pm.bytes.data(), &tag, sizeof(int));
+  if (hlen) std::memcpy(pm.bytes.data() + sizeof(int), hdr, hlen);
+  if (plen) std::memcpy(pm.bytes.data() + sizeof(int) + hlen, payload, plen);
+  o.prio.push_back(std::move(pm));
+  std::push_heap(o.prio.begin(), o.prio.end());
+  note_waiting(o, 1);
+  return 0;
+}
+
+// Drain what waits for `d` (lock held): FIFO first, then activations by
+// priority, several per ring message when aggregation is on.
+int ShmEngine::drain_peer(int d, Out& o) {
+  int n = 0;
+  ShmRing* ring = out_ring(d);
+  while (!o.backlog.empty()) {
+    auto& m = o.backlog.front();
+    int tag;
+    std::memcpy(&tag, m.data(), sizeof(int));
+    if (!ring_write(ring, m.data() + sizeof(int), m.size() - sizeof(int), nullptr, 0, tag, rank)) return n;
+    o.backlog.pop_front();
+    note_waiting(o, -1);
+    ++n;
+  }
+  const size_t limit = ring_bytes_ / 4;
+  while (!o.prio.empty()) {
+    if (!aggregate_ || o.prio.size() == 1) {
+      const auto& m = o.prio.front();
+      int tag;
+      std::memcpy(&tag, m.bytes.data(), sizeof(int));
+      if (!ring_write(ring, m.bytes.data() + sizeof(int), m.bytes.size() - sizeof(int), nullptr, 0, tag, rank)) return n;
+      std::pop_heap(o.prio.begin(), o.prio.end());
+      o.prio.pop_back();
+      note_waiting(o, -1);
+      ++n;
+      continue;
+    }
+    // take messages in priority order while the aggregate stays under the limit
+    std::vector<PrioMsg> take;
+    size_t bytes = 8;
+    while (!o.prio.empty()) {
+      const size_t add = 8 + ((o.prio.front().bytes.size() - sizeof(int) + 7) & ~(size_t)7);
+      if (!take.empty() && bytes + add > limit) break;
+      std::pop_heap(o.prio.begin(), o.prio.end());
+      take.push_back(std::move(o.prio.back()));
+      o.prio.pop_back();
+      bytes += add;
+    }
+    std::vector<char> agg(bytes, 0);
+    const uint32_t count = (uint32_t)take.size();
+    std::memcpy(agg.data(), &count, 4);
+    size_t off = 8;
+    for (auto& m : take) {
+      const uint32_t len = (uint32_t)(m.bytes.size() - sizeof(int));
+      std::memcpy(agg.data() + off, m.bytes.data(), 4);  // tag
+      std::memcpy(agg.data() + off + 4, &len, 4);
+      std::memcpy(agg.data() + off + 8, m.bytes.data() + sizeof(int), len);
+      off += 8 + ((len + 7) & ~(size_t)7);
+    }
+    if (!ring_write(ring, agg.data(), agg.size(), nullptr, 0, TAG_AGGREGATE, rank)) {
+      for (auto& m : take) {  // put them back, order is restored by the heap
+        o.prio.push_back(std::move(m));
+        std::push_heap(o.prio.begin(), o.prio.end());
+      }
+      return n;
+    }
+    note_waiting(o, -(int)count);
+    stats.aggregates.fetch_add(1, std::memory_order_relaxed);
+    stats.aggregated_msgs.fetch_add(count, std::memory_order_relaxed);
+    n += (int)count;
+  }
+  return n;
 }
 
 void ShmEngine::post(std::function<void()> fn) {
@@ -281,16 +394,9 @@ int ShmEngine::progress() {
   for (int d = 0; d < size; ++d) {
     if (d == rank) continue;
     Out& o = *out_[d];
-    if (o.backlog.empty()) continue;
+    if (o.waiting.load(std::memory_order_relaxed) == 0) continue;
     std::lock_guard<std::mutex> g(o.m);
-    while (!o.backlog.empty()) {
-      auto& m = o.backlog.front();
-      int tag;
-      std::memcpy(&tag, m.data(), sizeof(int));
-      if (!ring_write(out_ring(d), m.data() + sizeof(int), m.size() - sizeof(int), nullptr, 0, tag, rank)) break;
-      o.backlog.pop_front();
-      ++n;
-    }
+    n += drain_peer(d, o);
   }
   // inbound rings
   for (int s = 0; s < size; ++s) {

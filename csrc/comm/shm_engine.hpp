@@ -39,6 +39,12 @@ class ShmEngine : public CommEngine {
   int tag_unregister(int tag) override;
   int send_am(int tag, int dst, const void* buf, size_t len) override;
   int send_am2(int tag, int dst, const void* hdr, size_t hlen, const void* payload, size_t plen);
+  // activation-class message: may be reordered by priority and aggregated
+  int send_am_prio(int tag, int dst, const void* hdr, size_t hlen, const void* payload, size_t plen, int32_t priority);
+  struct Stats {
+    std::atomic<uint64_t> direct{0}, backlogged{0}, aggregates{0}, aggregated_msgs{0};
+    std::atomic<uint64_t> max_waiting{0};
+  } stats;
   int progress() override;
   int sync() override;
   uint64_t allreduce_max(uint64_t v) override;
@@ -70,15 +76,32 @@ class ShmEngine : public CommEngine {
   struct Pending {
     std::vector<char> msg;
   };
+  // Per-peer send state. Messages that do not fit the peer's ring wait in
+  // `backlog` (FIFO: data / control) or in `prio` (activations, highest task
+  // priority first; reference remote_dep_mpi.c:1089-1139 per-peer ordered
+  // command queues). When several activations wait they leave in one
+  // TAG_AGGREGATE message (reference runtime_comm_aggregate).
+  struct PrioMsg {
+    int32_t prio;
+    uint64_t seq;
+    std::vector<char> bytes;  // [int tag][hdr][payload]
+    bool operator<(const PrioMsg& o) const { return prio != o.prio ? prio < o.prio : seq > o.seq; }
+  };
   struct Out {
     std::mutex m;
     std::deque<std::vector<char>> backlog;
+    std::vector<PrioMsg> prio;  // std heap
+    uint64_t seq = 0;
+    std::atomic<int> waiting{0};  // backlog + prio sizes (read without the lock)
   };
   struct Xfer {
     hipEvent_t ev;
     std::function<void()> done;
   };
   bool ring_write(ShmRing* r, const void* hdr, size_t hlen, const void* payload, size_t plen, int tag, int src);
+  int drain_peer(int d, Out& o);
+  void note_waiting(Out& o, int delta);
+  bool aggregate_ = true;
   ShmRing* in_ring(int src);
   ShmRing* out_ring(int dst);
   void thread_main();

@@ -668,6 +668,7 @@ PYBIND11_MODULE(_C, m) {
   // ------------------------------------------------------------------ comm
   m.def("comm_init", [](int rank, int size, const std::string& job, int gpu) { py::gil_scoped_release rel; return comm_init(rank, size, job, gpu); });
   m.def("comm_fini", []() { py::gil_scoped_release rel; comm_fini(); });
+  m.def("comm_stats", []() { py::dict d; for (auto& kv : comm_stats()) d[py::str(kv.first)] = kv.second; return d; });
   m.def("comm_barrier", []() { py::gil_scoped_release rel; return comm_barrier(); });
   m.def("comm_rank", &comm_rank);
   m.def("comm_size", &comm_size);

@@ -43,6 +43,9 @@ def main(rank, size, job, N, nb, P, Q, sched="lfq", topo="star", termdet="local"
                 if m == n:
                     t, ref = np.tril(t), np.tril(ref)
                 err = max(err, float(np.abs(t - ref).max()))
+    if os.environ.get("DIST_PRINT_COMM_STATS"):
+        st = pa.comm_stats()
+        print("comm_stats " + " ".join(f"{k}={v}" for k, v in sorted(st.items())), flush=True)
     ctx.fini()
     pa.comm_fini()
     return err, pa.read_int(info)

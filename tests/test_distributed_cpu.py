@@ -56,6 +56,28 @@ def test_distributed_dpotrf_jdf(pa, nranks, P, Q, mode):
         assert rc == 0, out
 
 
+@pytest.mark.parametrize("aggregate", ["1", "0"])
+def test_distributed_backpressure_aggregation(pa, aggregate):
+    """Tiny shared-memory rings force activations into the per-peer priority
+    backlog; with runtime_comm_aggregate they leave packed in one message
+    (reference remote_dep_mpi.c:1089-1139, runtime_comm_aggregate). The
+    factorization stays exact either way."""
+    outs = run_ranks(4, 256, 8, 2, 2, "lfq", "star", "local",
+                     env_extra={"PARSEC_MCA_comm_shm_ring_bytes": "8192", "PARSEC_MCA_runtime_comm_aggregate": aggregate,
+                                "DIST_PRINT_COMM_STATS": "1"})
+    stats = []
+    for rc, out in outs:
+        assert rc == 0, out
+        line = [x for x in out.splitlines() if x.startswith("comm_stats")][0]
+        stats.append(dict(kv.split("=") for kv in line.split()[1:]))
+    assert sum(int(s["backlogged"]) for s in stats) > 0
+    if aggregate == "1":
+        assert sum(int(s["aggregates"]) for s in stats) > 0
+        assert all(int(s["aggregated_msgs"]) >= 2 * int(s["aggregates"]) for s in stats)
+    else:
+        assert sum(int(s["aggregates"]) for s in stats) == 0
+
+
 @pytest.mark.parametrize("sched", ["gd", "ll", "ap"])
 def test_distributed_other_schedulers(pa, sched):
     outs = run_ranks(2, 384, 64, 2, 1, sched, "star", "local")
