@@ -350,6 +350,18 @@ static void get_cb(const parsec_taskpool_t* tp, int which, parsec_event_cb_t* cb
 void parsec_taskpool_get_complete_callback_f08(const parsec_taskpool_t* tp, parsec_event_cb_t* cb, void** cb_data, int* ierr) { get_cb(tp, 0, cb, cb_data, ierr); }
 void parsec_taskpool_get_enqueue_callback_f08(const parsec_taskpool_t* tp, parsec_event_cb_t* cb, void** cb_data, int* ierr) { get_cb(tp, 1, cb, cb_data, ierr); }
 
+void parsec_grid_2Dcyclic_init(parsec_grid_2Dcyclic_t* g, int rank, int P, int Q, int kp, int kq, int ip, int jq) {
+  g->rank = rank;
+  g->rows = P > 0 ? P : 1;
+  g->cols = Q > 0 ? Q : 1;
+  g->krows = kp > 0 ? kp : 1;
+  g->kcols = kq > 0 ? kq : 1;
+  g->ip = ip;
+  g->jq = jq;
+  g->rrank = rank / g->cols;
+  g->crank = rank % g->cols;
+}
+
 // ------------------------------------------------------- Fortran / version
 int parsec_version(int* major, int* minor, int* release) {
   if (major) *major = 2;
@@ -506,12 +518,7 @@ void parsec_matrix_block_cyclic_init(parsec_matrix_block_cyclic_t* dc, parsec_ma
   t->i = i; t->j = j; t->m = (int)bc->m; t->n = (int)bc->n; t->mt = (int)bc->mt; t->nt = (int)bc->nt;
   t->llm = (int)(bc->llm_tiles * mb); t->lln = (int)(bc->lln_tiles * nb);
   t->nb_local_tiles = (int)bc->nb_local_tiles;
-  dc->grid.rank = myrank;
-  dc->grid.rows = p; dc->grid.cols = q;
-  dc->grid.krows = kp; dc->grid.kcols = kq;
-  dc->grid.ip = ip; dc->grid.jq = jq;
-  dc->grid.rrank = q > 0 ? myrank / q : 0;
-  dc->grid.crank = q > 0 ? myrank % q : 0;
+  parsec_grid_2Dcyclic_init(&dc->grid, myrank, p, q, kp, kq, ip, jq);
 }
 void parsec_tiled_matrix_destroy(parsec_tiled_matrix_t* tdesc) { parsec_data_collection_destroy(&tdesc->super); }
 parsec_data_key_t parsec_tiled_matrix_data_key(parsec_tiled_matrix_t* tdesc, int m, int n) {

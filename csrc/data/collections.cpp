@@ -23,7 +23,7 @@ size_t matrix_type_size(int mtype) {
 
 // ============================================================ tiled matrix
 TiledMatrix::~TiledMatrix() {
-  for (Data*& d : tiles) if (d) { data_destroy(d); d = nullptr; }
+  for (Data*& d : tiles) if (d) { data_destroy(d); d = nullptr; }  // views keep `tiles` empty (SubTileMatrix owns its aliasing Data)
   if (owns_storage && mat) {
     if (storage_device == 0) std::free(mat);
     else device_free(storage_device, mat);
@@ -158,6 +158,106 @@ int TiledMatrix::data_read(const std::string& filename) {
   }
   std::fclose(f);
   return rc;
+}
+
+// ================================================================== views
+void KViewMatrix::init_view(BlockCyclic* o, int kp_, int kq_) {
+  if (o->kp != 1 || o->kq != 1) fatal("kview: the origin must not be k-cyclic already");
+  origin = o;
+  kp = std::max(1, kp_);
+  kq = std::max(1, kq_);
+  init_base(o->mtype, (int)o->myrank, (int)o->nodes, o->mb, o->nb, o->lm, o->ln, o->i, o->j, o->m, o->n);
+  storage_device = o->storage_device;
+  nb_local_tiles = o->nb_local_tiles;
+  is_view = true;
+  key_base = o->key_base + "_kview";
+}
+
+// index permutation inside groups of p*k tiles; indices that fall beyond the
+// last (partial) group are permuted again until they are valid
+static int64_t kview_perm(int64_t x, int64_t p, int64_t k, int64_t count) {
+  if (p <= 1 || k <= 1) return x;
+  do {
+    const int64_t grp = x - x % (p * k);
+    x = grp + (x % k) * p + (x / k) % p;
+  } while (x >= count);
+  return x;
+}
+int64_t KViewMatrix::map_m(int64_t m_) const { return kview_perm(m_, origin->P, kp, mt); }
+int64_t KViewMatrix::map_n(int64_t n_) const { return kview_perm(n_, origin->Q, kq, nt); }
+uint32_t KViewMatrix::rank_of(const int64_t* idx, int n_) const {
+  const int64_t o[2] = {map_m(idx[0]), n_ > 1 ? map_n(idx[1]) : 0};
+  return origin->rank_of(o, 2);
+}
+int32_t KViewMatrix::vpid_of(const int64_t* idx, int n_) const {
+  const int64_t o[2] = {map_m(idx[0]), n_ > 1 ? map_n(idx[1]) : 0};
+  return origin->vpid_of(o, 2);
+}
+int64_t KViewMatrix::local_index(int64_t m_, int64_t n_) const { return origin->local_index(map_m(m_), map_n(n_)); }
+uint64_t KViewMatrix::data_key(const int64_t* idx, int n_) const {
+  const int64_t o[2] = {map_m(idx[0]), n_ > 1 ? map_n(idx[1]) : 0};
+  return origin->data_key(o, 2);
+}
+Data* KViewMatrix::data_of(const int64_t* idx, int n_) {
+  const int64_t o[2] = {map_m(idx[0]), n_ > 1 ? map_n(idx[1]) : 0};
+  return origin->data_of(o, 2);
+}
+
+void SubMatrixView::init_view(TiledMatrix* o, int64_t i_, int64_t j_, int64_t m_, int64_t n_) {
+  if (i_ < 0 || i_ % o->mb || j_ < 0 || j_ % o->nb) fatal("submatrix: (i, j) = (%lld, %lld) must be tile aligned", (long long)i_, (long long)j_);
+  if (m_ < 0 || n_ < 0 || i_ + m_ > o->m || j_ + n_ > o->n) fatal("submatrix: %lld x %lld at (%lld, %lld) exceeds the matrix", (long long)m_, (long long)n_, (long long)i_, (long long)j_);
+  origin = o;
+  toff_m = i_ / o->mb;
+  toff_n = j_ / o->nb;
+  init_base(o->mtype, (int)o->myrank, (int)o->nodes, o->mb, o->nb, o->lm, o->ln, o->i + i_, o->j + j_, m_, n_);
+  storage_device = o->storage_device;
+  is_view = true;
+  key_base = o->key_base;
+  for (int64_t b = 0; b < nt; ++b)
+    for (int64_t a = 0; a < mt; ++a) nb_local_tiles += local_index(a, b) >= 0 ? 1 : 0;
+}
+uint32_t SubMatrixView::rank_of(const int64_t* idx, int n_) const {
+  const int64_t o[2] = {idx[0] + toff_m, (n_ > 1 ? idx[1] : 0) + toff_n};
+  return origin->rank_of(o, 2);
+}
+int32_t SubMatrixView::vpid_of(const int64_t* idx, int n_) const {
+  const int64_t o[2] = {idx[0] + toff_m, (n_ > 1 ? idx[1] : 0) + toff_n};
+  return origin->vpid_of(o, 2);
+}
+int64_t SubMatrixView::local_index(int64_t m_, int64_t n_) const { return origin->local_index(m_ + toff_m, n_ + toff_n); }
+uint64_t SubMatrixView::data_key(const int64_t* idx, int n_) const {
+  const int64_t o[2] = {idx[0] + toff_m, (n_ > 1 ? idx[1] : 0) + toff_n};
+  return origin->data_key(o, 2);
+}
+Data* SubMatrixView::data_of(const int64_t* idx, int n_) {
+  const int64_t o[2] = {idx[0] + toff_m, (n_ > 1 ? idx[1] : 0) + toff_n};
+  return origin->data_of(o, 2);
+}
+
+void SubTileMatrix::init_subtile(TiledMatrix* parent, int64_t tm, int64_t tn, int64_t smb, int64_t snb) {
+  const int64_t idx[2] = {tm, tn};
+  Data* d = parent->data_of(idx, 2);
+  if (!d) fatal("subtile: tile (%lld, %lld) is not local", (long long)tm, (long long)tn);
+  DataCopy* c = data_pull_to_host(d);  // newest version, on the host
+  base = static_cast<char*>(c->device_private);
+  plda = parent->mb;
+  const int64_t rows = parent->tile_rows(tm), cols = parent->tile_cols(tn);
+  init_base(parent->mtype, (int)parent->myrank, 1, smb, snb, rows, cols, 0, 0, rows, cols);
+  nb_local_tiles = mt * nt;
+  tiles.assign((size_t)nb_local_tiles, nullptr);
+  key_base = parent->key_base + "_sub";
+}
+Data* SubTileMatrix::data_of(const int64_t* idx, int n_) {
+  const int64_t sm = idx[0], sn = n_ > 1 ? idx[1] : 0;
+  const int64_t li = local_index(sm, sn);
+  if (li < 0) return nullptr;
+  Data* d = __atomic_load_n(&tiles[li], __ATOMIC_ACQUIRE);
+  if (d) return d;
+  const int64_t key_idx[2] = {sm, sn};
+  // a strided view into the parent tile: the host copy aliases it (not owned)
+  d = data_create(&tiles[li], this, data_key(key_idx, 2), sub_ptr(sm, sn), (size_t)mb * nb * elem_size, DATA_FLAG_PARSEC_MANAGED, 0);
+  d->copy(0)->dtt = Datatype::vector((uint32_t)elem_size, tile_cols(sn), tile_rows(sm), plda);
+  return d;
 }
 
 // ============================================================ block cyclic

@@ -42,10 +42,12 @@ struct TiledMatrix : DataCollection {
   // local tile index or -1 when not local
   virtual int64_t local_index(int64_t m, int64_t n) const = 0;
   void* tile_ptr(int64_t m, int64_t n);
+  bool is_view = false;  // views own neither storage nor Data objects
   Data* tile_data(int64_t m, int64_t n);
   uint64_t data_key(const int64_t* idx, int n) const override { return (uint64_t)((idx[0] + i / mb) + (n > 1 ? (idx[1] + j / nb) : 0) * lmt); }
   Data* data_of(const int64_t* idx, int n) override { return tile_data(idx[0], n > 1 ? idx[1] : 0); }
-  Data* data_of_key(uint64_t key) override { return tile_data((int64_t)(key % lmt) - i / mb, (int64_t)(key / lmt) - j / nb); }
+  // through the virtual data_of, so subclasses with their own storage (views, band, sub-tiles) resolve keys the same way
+  Data* data_of_key(uint64_t key) override { const int64_t idx[2] = {(int64_t)(key % lmt) - i / mb, (int64_t)(key / lmt) - j / nb}; return data_of(idx, 2); }
   uint32_t rank_of_key(uint64_t key) const override { int64_t idx[2] = {(int64_t)(key % lmt) - i / mb, (int64_t)(key / lmt) - j / nb}; return rank_of(idx, 2); }
   int32_t vpid_of_key(uint64_t key) const override { int64_t idx[2] = {(int64_t)(key % lmt) - i / mb, (int64_t)(key / lmt) - j / nb}; return vpid_of(idx, 2); }
   std::string key_to_string(uint64_t key) const override;
@@ -70,6 +72,60 @@ struct BlockCyclic : TiledMatrix {
   uint32_t rank_of(const int64_t* idx, int n) const override;
   int32_t vpid_of(const int64_t* idx, int n) const override;
   int64_t local_index(int64_t m, int64_t n) const override;
+};
+
+// ---- views over an existing tiled matrix (no storage of their own)
+//
+// k-cyclic view of a plain 2D block-cyclic matrix (reference
+// parsec_matrix_block_cyclic_kview, two_dim_rectangle_cyclic.c:419-560): view
+// tile (m, n) is origin tile (perm_P(m), perm_Q(n)), where perm reorders each
+// group of P*k consecutive tile rows so that k consecutive view rows land on
+// the same process row. Data, keys and ranks are the origin's.
+struct KViewMatrix : TiledMatrix {
+  BlockCyclic* origin = nullptr;
+  int kp = 1, kq = 1;
+  void init_view(BlockCyclic* origin, int kp, int kq);
+  int64_t map_m(int64_t m) const;
+  int64_t map_n(int64_t n) const;
+  uint32_t rank_of(const int64_t* idx, int n) const override;
+  int32_t vpid_of(const int64_t* idx, int n) const override;
+  int64_t local_index(int64_t m, int64_t n) const override;
+  uint64_t data_key(const int64_t* idx, int n) const override;
+  Data* data_of(const int64_t* idx, int n) override;
+  Data* data_of_key(uint64_t key) override { return origin->data_of_key(key); }
+  uint32_t rank_of_key(uint64_t key) const override { return origin->rank_of_key(key); }
+  int32_t vpid_of_key(uint64_t key) const override { return origin->vpid_of_key(key); }
+};
+
+// Submatrix view (reference parsec_tiled_matrix_submatrix, matrix.c:158-215):
+// the tile-aligned block starting at element (i, j) of size m x n; view tile
+// (a, b) is origin tile (a + i/mb, b + j/nb).
+struct SubMatrixView : TiledMatrix {
+  TiledMatrix* origin = nullptr;
+  int64_t toff_m = 0, toff_n = 0;
+  void init_view(TiledMatrix* origin, int64_t i, int64_t j, int64_t m, int64_t n);
+  uint32_t rank_of(const int64_t* idx, int n) const override;
+  int32_t vpid_of(const int64_t* idx, int n) const override;
+  int64_t local_index(int64_t m, int64_t n) const override;
+  uint64_t data_key(const int64_t* idx, int n) const override;
+  Data* data_of(const int64_t* idx, int n) override;
+  Data* data_of_key(uint64_t key) override { return origin->data_of_key(key); }
+  uint32_t rank_of_key(uint64_t key) const override { return origin->rank_of_key(key); }
+  int32_t vpid_of_key(uint64_t key) const override { return origin->vpid_of_key(key); }
+};
+
+// One tile of a matrix seen as a tiled matrix of smaller smb x snb tiles
+// (reference subtile_desc_create, subtile.c): single-rank, host-resident
+// view; every sub-tile aliases the parent tile's storage in LAPACK layout
+// (leading dimension = the parent's mb), so bodies index it with ld = plda.
+struct SubTileMatrix : TiledMatrix {
+  char* base = nullptr;  // parent tile storage
+  int64_t plda = 0;      // parent leading dimension (elements)
+  void init_subtile(TiledMatrix* parent, int64_t tm, int64_t tn, int64_t smb, int64_t snb);
+  uint32_t rank_of(const int64_t*, int) const override { return myrank; }
+  int64_t local_index(int64_t m, int64_t n) const override { return m >= 0 && n >= 0 && m < mt && n < nt ? m + n * mt : -1; }
+  Data* data_of(const int64_t* idx, int n) override;
+  void* sub_ptr(int64_t m, int64_t n) const { return base + ((size_t)n * nb * plda + (size_t)m * mb) * elem_size; }
 };
 
 // Symmetric: only the `uplo` triangle of tiles exists.

@@ -81,6 +81,11 @@ static py::object dtd_arg(Task* t, int i) {
     // received remote copies carry a bare Data: type them through the tile's collection
     DataCollection* dcc = (d && d->dc) ? d->dc : (a.tile ? a.tile->dc : nullptr);
     if (dcc) {
+      if (auto* st = dynamic_cast<SubTileMatrix*>(dcc)) {  // strided view: ld = the parent tile's
+        const size_t es = st->elem_size;
+        return py::array(py::dtype(st->mtype == MATRIX_INTEGER ? "int32" : (st->mtype == MATRIX_FLOAT ? "float32" : "float64")), {(py::ssize_t)st->mb, (py::ssize_t)st->nb},
+                         {(py::ssize_t)es, (py::ssize_t)(es * st->plda)}, c->device_private, py::capsule(c->device_private, [](void*) {}));
+      }
       if (auto* tm = dynamic_cast<TiledMatrix*>(dcc)) return tile_view(c->device_private, tm->mtype, tm->mb, tm->nb, tm->elem_size);
     }
     size_t n = d ? d->nb_elts : 0;
@@ -370,24 +375,23 @@ PYBIND11_MODULE(_C, m) {
       .def("tile_ptr", [](TiledMatrix& t, int64_t a, int64_t b) { return (uintptr_t)t.tile_ptr(a, b); })
       .def("tile", [](TiledMatrix& t, int64_t a, int64_t b) -> py::object {
         // column-major numpy view of the newest host copy of a local tile
-        Data* d = t.tile_data(a, b);
+        // (virtual data_of: views resolve to their origin's tiles)
+        const int64_t idx[2] = {a, b};
+        Data* d = t.data_of(idx, 2);
         if (!d) return py::none();
         DataCopy* c = data_pull_to_host(d);
         if (!c) return py::none();
-        return tile_view(c->device_private, t.mtype, t.mb, t.nb, t.elem_size);
-      })
-      .def("tile", [](TiledMatrix& t, int64_t a, int64_t b) -> py::object {
-        Data* d = t.tile_data(a, b);
-        if (!d) return py::none();
-        DataCopy* c = t.storage_device == 0 ? d->copy(0) : data_pull_to_host(d);
-        if (t.storage_device == 0) {
-          // the user's host tile must show the newest version
-          c = data_pull_to_host(d);
+        if (auto* st = dynamic_cast<SubTileMatrix*>(&t)) {  // strided view into the parent tile
+          const size_t es = st->elem_size;
+          return py::array(py::dtype(st->mtype == MATRIX_INTEGER ? "int32" : (st->mtype == MATRIX_FLOAT ? "float32" : "float64")),
+                           {(py::ssize_t)st->tile_rows(a), (py::ssize_t)st->tile_cols(b)}, {(py::ssize_t)es, (py::ssize_t)(es * st->plda)},
+                           c->device_private, py::capsule(c->device_private, [](void*) {}));
         }
         return tile_view(c->device_private, t.mtype, t.mb, t.nb, t.elem_size);
       })
       .def("mark_host_modified", [](TiledMatrix& t, int64_t a, int64_t b) {
-        Data* d = t.tile_data(a, b);
+        const int64_t idx[2] = {a, b};
+        Data* d = t.data_of(idx, 2);
         if (!d) return;
         DataCopy* c = d->copy(0);
         if (!c) return;
@@ -414,6 +418,19 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("Q", &BlockCyclic::Q)
       .def_readonly("llm_tiles", &BlockCyclic::llm_tiles)
       .def_readonly("lln_tiles", &BlockCyclic::lln_tiles);
+
+  // views (reference parsec_matrix_block_cyclic_kview, parsec_tiled_matrix_submatrix, subtile_desc_create)
+  py::class_<KViewMatrix, TiledMatrix>(m, "KViewMatrix")
+      .def(py::init([](BlockCyclic* o, int kp, int kq) { auto* v = new KViewMatrix(); v->init_view(o, kp, kq); return v; }), py::keep_alive<1, 2>(),
+           py::arg("origin"), py::arg("kp"), py::arg("kq"))
+      .def("origin_index", [](KViewMatrix& v, int64_t a, int64_t b) { return std::make_pair(v.map_m(a), v.map_n(b)); });
+  py::class_<SubMatrixView, TiledMatrix>(m, "SubMatrixView")
+      .def(py::init([](TiledMatrix* o, int64_t i, int64_t j, int64_t mm, int64_t nn) { auto* v = new SubMatrixView(); v->init_view(o, i, j, mm, nn); return v; }),
+           py::keep_alive<1, 2>(), py::arg("origin"), py::arg("i"), py::arg("j"), py::arg("m"), py::arg("n"));
+  py::class_<SubTileMatrix, TiledMatrix>(m, "SubTileMatrix")
+      .def(py::init([](TiledMatrix* p, int64_t tm, int64_t tn, int64_t smb, int64_t snb) { auto* v = new SubTileMatrix(); v->init_subtile(p, tm, tn, smb, snb); return v; }),
+           py::keep_alive<1, 2>(), py::arg("parent"), py::arg("tm"), py::arg("tn"), py::arg("smb"), py::arg("snb"))
+      .def_readonly("plda", &SubTileMatrix::plda);
 
   py::class_<SymBlockCyclic, BlockCyclic>(m, "SymBlockCyclic")
       .def(py::init([](int mtype, int myrank, int64_t mb, int64_t nb, int64_t lm, int64_t ln, int P, int Q, int uplo, int device, uintptr_t ptr) {

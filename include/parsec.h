@@ -208,6 +208,10 @@ typedef struct parsec_grid_2Dcyclic_s {
   int rank, rows, cols, krows, kcols, ip, jq, rrank, crank;
 } parsec_grid_2Dcyclic_t;
 
+/* process-grid coordinates of `rank` on a P x Q grid with k-cyclicity and
+ * displacement (reference data_dist/matrix/grid_2Dcyclic.h:55) */
+void parsec_grid_2Dcyclic_init(parsec_grid_2Dcyclic_t* grid, int rank, int P, int Q, int kp, int kq, int ip, int jq);
+
 typedef struct parsec_matrix_block_cyclic_s {
   parsec_tiled_matrix_t super;
   parsec_grid_2Dcyclic_t grid;
