@@ -273,8 +273,27 @@ struct Flow {
 using Hook = std::function<int(ExecutionStream*, Task*)>;
 using Evaluate = std::function<int(const Task*)>;  // HOOK_DONE -> runnable, HOOK_NEXT -> skip chore
 
+// User data movement for a GPU chore (reference BODY stage_in= / stage_out=,
+// device_gpu.h:61,85): called on the engine's transfer stream with the flows
+// to move; src / dst are the copies (host <-> device), dc the per-flow
+// collection (BODY F.dc=), bytes the device buffer size (BODY F.size=).
+struct GpuStageContext {
+  Task* task = nullptr;
+  uint32_t flow_mask = 0;
+  void* stream = nullptr;  // hipStream_t
+  int device_index = 0;
+  DataCopy* src[kMaxFlows] = {};
+  DataCopy* dst[kMaxFlows] = {};
+  DataCollection* dc[kMaxFlows] = {};
+  size_t bytes[kMaxFlows] = {};
+};
+using GpuStageFn = std::function<int(GpuStageContext&)>;
+
 struct Chore {
   uint32_t type = DEV_CPU;
+  GpuStageFn stage_in, stage_out;                                      // custom transfers (nullptr = plain copies)
+  std::vector<std::function<size_t(const Task*)>> flow_size;           // per flow index: device buffer bytes
+  std::vector<std::function<DataCollection*(const Task*)>> flow_dc;    // per flow index: collection for the stage hooks
   Hook hook;                                              // CPU body
   std::function<int(GpuExecContext*, Task*)> gpu_hook;    // GPU body (type & DEV_GPU_MASK)
   Evaluate evaluate;

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../core/runtime.hpp"
+#include "../core/info.hpp"
 
 namespace parsec {
 
@@ -169,6 +170,9 @@ struct GpuExecContext {
   void* flow_ptr[kMaxFlows] = {};
   void* ptr(int flow) const { return flow_ptr[flow]; }
   void* workspace(size_t bytes);  // per-stream scratch (valid until the task completes)
+  // per-stream info slot `id` of gpu_stream_infos(), built on first use on
+  // this stream (e.g. a library handle bound to `stream`)
+  void* info(int id);
 };
 
 using GpuHook = std::function<int(GpuExecContext*, Task*)>;

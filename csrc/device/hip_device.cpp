@@ -207,6 +207,16 @@ int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t b
 
 void* GpuExecContext::workspace(size_t bytes) { return dev->workspace(stream_index, bytes); }
 
+InfoRegistry& gpu_stream_infos() {
+  static InfoRegistry* r = new InfoRegistry();
+  return *r;
+}
+
+void* GpuExecContext::info(int id) {
+  if (stream_index < 0 || stream_index >= (int)dev->stream_infos.size()) return nullptr;
+  return dev->stream_infos[stream_index]->get(id);
+}
+
 // ================================================================ device
 static int g_nb_exec_streams = 4;
 
@@ -260,6 +270,8 @@ void HipDevice::start(Context* c) {
   round_tasks.assign(total_streams, {});
   stream_workspace.assign(total_streams, nullptr);
   stream_workspace_size.assign(total_streams, 0);
+  stream_infos.clear();
+  for (int i = 0; i < total_streams; ++i) stream_infos.emplace_back(new InfoArray(&gpu_stream_infos(), (void*)s_exec[i]));
   es = new ExecutionStream();
   es->ctx = c;
   es->vp = c->vps[0];
@@ -280,6 +292,7 @@ void HipDevice::shutdown() {
   event_pool.clear();
   for (size_t i = 0; i < stream_workspace.size(); ++i) if (stream_workspace[i]) (void)hipFree(stream_workspace[i]);
   stream_workspace.clear();
+  stream_infos.clear();  // per-stream objects die before their streams
   for (auto s : s_exec) (void)hipStreamDestroy(s);
   s_exec.clear();
   if (s_h2d) (void)hipStreamDestroy(s_h2d);
@@ -501,7 +514,7 @@ bool HipDevice::start_w2r(size_t bytes) {
     DataCopy* c = static_cast<DataCopy*>(it);
     Data* d = c->original;
     auto* st = static_cast<DevCopyState*>(c->dev_state);
-    if (!d || c->readers.load() > 0 || st->w2r) { it = nx; continue; }
+    if (!d || c->readers.load() > 0 || st->w2r || st->custom) { it = nx; continue; }  // custom layouts: written back by their chore
     DataCopy* host = d->copy(0);
     if (!host) {
       // no host buffer to write into (NEW / arena data): allocate + copy now
@@ -680,6 +693,14 @@ void HipDevice::zone_free(void* p) {
 int HipDevice::stage_in(GpuTask* g) {
   Task* t = g->task;
   const TaskClass* tc = t->task_class;
+  const Chore& ch = tc->chores[g->chore];
+  // device buffer size of flow fi: the chore's F.size when given
+  auto dev_bytes = [&](int fi, const Data* d) -> size_t {
+    if (fi < (int)ch.flow_size.size() && ch.flow_size[fi]) return ch.flow_size[fi](t);
+    return d->nb_elts;
+  };
+  const bool custom_in = (bool)ch.stage_in;
+  GpuStageContext sctx;
   bool any = false;
   for (auto& f : tc->flows) {
     if (f.access == FLOW_CTL || f.access == FLOW_NONE) continue;
@@ -722,7 +743,7 @@ int HipDevice::stage_in(GpuTask* g) {
         if (lst && lst->w2r && (g->access[fi] & FLOW_WRITE)) { rollback(); return -1; }  // retry after the write-back
         continue;
       }
-      void* p = cache_alloc(d->nb_elts);
+      void* p = cache_alloc(dev_bytes(fi, d));
       if (!p) { rollback(); return -1; }
       auto* nc = new DataCopy();
       nc->device_private = p;
@@ -730,6 +751,7 @@ int HipDevice::stage_in(GpuTask* g) {
       nc->coherency_state = COHERENCY_INVALID;
       nc->dtt = c->dtt;
       auto* nst = new DevCopyState();
+      nst->custom = custom_in;
       nc->dev_state = nst;
       {
         std::lock_guard<SpinLock> lk(d->lock);
@@ -746,7 +768,7 @@ int HipDevice::stage_in(GpuTask* g) {
     Data* d = c->original;
     DataCopy* local = d->copy(device_index);
     if (!local) {
-      void* p = cache_alloc(d->nb_elts);
+      void* p = cache_alloc(dev_bytes(fi, d));
       if (!p) return -1;
       auto* nc = new DataCopy();
       nc->device_private = p;
@@ -754,6 +776,7 @@ int HipDevice::stage_in(GpuTask* g) {
       nc->coherency_state = COHERENCY_INVALID;
       nc->dtt = c->dtt;
       auto* nst = new DevCopyState();
+      nst->custom = custom_in;
       nc->dev_state = nst;
       {
         std::lock_guard<SpinLock> lk(d->lock);
@@ -778,7 +801,19 @@ int HipDevice::stage_in(GpuTask* g) {
     g->dev_copy[fi] = local;
     if (local->transfer_status == TRANSFER_UNDER) { any = true; continue; }  // ordered behind the in-flight copy on s_h2d
     DataCopy* src = data_start_transfer_ownership_to_copy(d, device_index, g->access[fi]);
-    if (src && src != local) {
+    if (src && src != local && custom_in && src->device_index == 0) {
+      // the chore moves this flow itself (one stage_in call for all of them below)
+      sctx.flow_mask |= 1u << fi;
+      sctx.src[fi] = src;
+      sctx.dst[fi] = local;
+      sctx.dc[fi] = fi < (int)ch.flow_dc.size() && ch.flow_dc[fi] ? ch.flow_dc[fi](t) : d->dc;
+      sctx.bytes[fi] = dev_bytes(fi, d);
+      stats.bytes_in.fetch_add(sctx.bytes[fi], std::memory_order_relaxed);
+      local->transfer_status = TRANSFER_UNDER;
+      local->push_task = g;
+      g->issued_copy[fi] = true;
+      any = true;
+    } else if (src && src != local) {
       hipMemcpyKind k = src->device_index == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
       if (k == hipMemcpyDeviceToDevice) {
         int src_ord = device_hip_ordinal(src->device_index);
@@ -793,6 +828,12 @@ int HipDevice::stage_in(GpuTask* g) {
       g->issued_copy[fi] = true;
       any = true;
     }
+  }
+  if (sctx.flow_mask) {
+    sctx.task = t;
+    sctx.stream = s_h2d;
+    sctx.device_index = device_index;
+    if (ch.stage_in(sctx) != 0) fatal("%s: user stage_in failed", t->task_class->name.c_str());
   }
   if (!any) return 0;
   g->ev_in = get_event();
@@ -1068,14 +1109,34 @@ bool HipDevice::progress() {
       q.pop_front();
       for (GpuTask* g : tasks) {
         epilog(g);
+        const Chore& gch = g->task->task_class->chores[g->chore];
+        if (gch.stage_in || gch.stage_out)  // custom layouts go home through the chore, right after the task
+          for (int fi = 0; fi < kMaxFlows; ++fi)
+            if (g->dev_copy[fi] && (g->access[fi] & FLOW_WRITE)) g->pushout |= 1u << fi;
         if (g->pushout) {
+          GpuStageContext octx;
           for (int fi = 0; fi < kMaxFlows; ++fi) {
             if (!(g->pushout & (1u << fi)) || !g->dev_copy[fi]) continue;
             Data* d = g->dev_copy[fi]->original;
             DataCopy* host = d->copy(0);
             if (!host) { host = data_pull_to_host(d); continue; }
+            if (gch.stage_out) {
+              octx.flow_mask |= 1u << fi;
+              octx.src[fi] = g->dev_copy[fi];
+              octx.dst[fi] = host;
+              octx.dc[fi] = fi < (int)gch.flow_dc.size() && gch.flow_dc[fi] ? gch.flow_dc[fi](g->task) : d->dc;
+              octx.bytes[fi] = fi < (int)gch.flow_size.size() && gch.flow_size[fi] ? gch.flow_size[fi](g->task) : d->nb_elts;
+              stats.bytes_out.fetch_add(octx.bytes[fi], std::memory_order_relaxed);
+              continue;
+            }
             PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, g->dev_copy[fi]->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_d2h));
             stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
+          }
+          if (octx.flow_mask) {
+            octx.task = g->task;
+            octx.stream = s_d2h;
+            octx.device_index = device_index;
+            if (gch.stage_out(octx) != 0) fatal("%s: user stage_out failed", g->task->task_class->name.c_str());
           }
           g->ev_out = get_event();
           PARSEC_HIP_CHECK(hipEventRecord(g->ev_out, s_d2h));

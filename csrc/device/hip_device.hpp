@@ -18,6 +18,7 @@
 #include <thread>
 
 #include "device.hpp"
+#include "../core/info.hpp"
 
 namespace parsec {
 
@@ -68,6 +69,8 @@ struct DevCopyState {  // DataCopy::dev_state for engine-managed copies
   bool cache_managed = true;  // allocated from the zone (evictable)
   Data* retained = nullptr;   // the Data this cache copy keeps alive (released when the copy is dropped)
   bool w2r = false;           // write-back to the host in flight (readers may use it, writers wait)
+  bool custom = false;        // staged by a chore's stage_in (its layout may differ from the host copy's):
+                              // written back by that chore's stage_out, never by the generic W2R
 };
 
 // Asynchronous write-back of dirty cache copies (reference W2R task,
@@ -99,6 +102,7 @@ struct HipDevice : Device {
   int nb_exec_streams = 4;
   hipStream_t s_h2d = nullptr, s_d2h = nullptr;
   std::vector<hipStream_t> s_exec;
+  std::vector<std::unique_ptr<InfoArray>> stream_infos;  // one per s_exec stream (gpu_stream_infos())
   std::unique_ptr<ZoneAllocator> zone;
   std::mutex zone_m;  // the comm thread allocates receive buffers from the zone too
   size_t zone_max = 0;

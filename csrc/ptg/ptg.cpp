@@ -734,6 +734,10 @@ void PtgTaskpool::finalize() {
       ch.evaluate = b.evaluate;
       ch.weight = b.weight;
       ch.dyld = b.dyld;
+      ch.stage_in = b.stage_in;
+      ch.stage_out = b.stage_out;
+      ch.flow_size = b.flow_size;
+      ch.flow_dc = b.flow_dc;
       tc->chores.push_back(std::move(ch));
     }
     tc->flags = d.flags;

@@ -100,6 +100,10 @@ struct BodyDef {
   Evaluate evaluate;
   double weight = 1.0;
   std::string dyld;
+  // BODY stage_in= / stage_out= / F.size= / F.dc= (reference jdf2c.c:6583-6830)
+  GpuStageFn stage_in, stage_out;
+  std::vector<std::function<size_t(const Task*)>> flow_size;
+  std::vector<std::function<DataCollection*(const Task*)>> flow_dc;
 };
 
 struct TaskClassDef {

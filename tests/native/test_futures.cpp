@@ -1,13 +1,15 @@
-// Futures and the reader/writer lock (reference tests/class/future.c,
-// future_datacopy.c, rwlock.c -- same intent, written for core/future.hpp
+// Futures, the reader/writer lock and the info registry (reference tests/class/future.c,
+// future_datacopy.c, rwlock.c, info -- same intent, written for core/future.hpp
 // and core/base.hpp). Exit code 0 = pass; one line per test.
 #include <atomic>
 #include <cstdio>
+#include <memory>
 #include <thread>
 #include <vector>
 
 #include "core/base.hpp"
 #include "core/future.hpp"
+#include "core/info.hpp"
 
 using namespace parsec;
 
@@ -127,11 +129,45 @@ static void test_rwlock(int nthreads, int iters) {
   std::printf("rwlock threads=%d iters=%d ok\n", nthreads, iters);
 }
 
+// info registry: lazily built per-object slots, one construction per object
+// even under concurrent first use, destructors at object death, lookup by name
+// (reference tests/class/info: parsec_info_register / get / test_and_set)
+static void test_info(int nthreads) {
+  InfoRegistry reg;
+  std::atomic<int> built{0}, destroyed{0};
+  const int id = reg.register_info("handle", [&](void* owner) -> void* { built++; return new long((long)(intptr_t)owner); },
+                                   [&](void* v) { destroyed++; delete static_cast<long*>(v); });
+  CHECK(reg.lookup("handle") == id && reg.lookup("nope") == -1, "info lookup");
+  {
+    std::vector<std::unique_ptr<InfoArray>> objs;
+    for (int o = 0; o < 4; ++o) objs.emplace_back(new InfoArray(&reg, (void*)(intptr_t)(100 + o)));
+    std::atomic<int> bad{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t)
+      th.emplace_back([&] {
+        for (int r = 0; r < 1000; ++r) {
+          const int o = r % 4;
+          long* v = static_cast<long*>(objs[o]->get(id));
+          if (!v || *v != 100 + o) bad++;
+        }
+      });
+    for (auto& x : th) x.join();
+    CHECK(bad.load() == 0, "info get returned %d wrong values", bad.load());
+    CHECK(built.load() >= 4, "info built %d", built.load());
+    CHECK(objs[0]->get(id + 7) == nullptr, "unknown id");
+  }
+  CHECK(built.load() == destroyed.load(), "info: %d built, %d destroyed", built.load(), destroyed.load());
+  reg.unregister_info(id);
+  CHECK(reg.lookup("handle") == -1, "info unregister");
+  std::printf("info threads=%d ok\n", nthreads);
+}
+
 int main() {
   const int nt = std::max(2u, std::min(8u, std::thread::hardware_concurrency())) & ~1u;
   test_base_and_countable(nt, 100);
   test_datacopy(nt, 2000);
   test_rwlock(nt, 200000);
+  test_info(nt);
   if (g_fail) { std::printf("%d failure(s)\n", g_fail); return 1; }
   std::printf("all future/rwlock tests passed\n");
   return 0;

@@ -320,3 +320,30 @@ def test_empty_task_benchmark(ep_exe, sched):
     assert "tasks 2049" in line and "ran_ok 1" in line
     us = float(line.split("us_per_task ")[1].split()[0])
     assert 0 < us < 1000
+
+
+@pytest.mark.gpu
+def test_stage_custom_hip_body(tmp_path):
+    """BODY [type=HIP stage_in= stage_out= B.size= B.dc=] (reference
+    tests/dsl/ptg/cuda/stage_custom.jdf): the device copy has a padded leading
+    dimension, moved by the user's pitched 2D copies in both directions."""
+    exe = ptgpp.build_program(os.path.join(JDF, "stage_custom.jdf"), str(tmp_path))
+    r = _run(exe, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "stage_custom tiles 6 stage_in 6 stage_out 6 bad_dc 0 bad 0 handles_ok 1" in r.stdout
+
+
+@pytest.mark.parametrize("props,msg", [
+    ("[type=HIP B.colour=%{ return 1; %}]", "unknown BODY flow property B.colour"),
+    ("[type=HIP Z.size=%{ return 8; %}]", "no flow named Z"),
+    ("[stage_in=f]", "only meaningful on a BODY [type=HIP]"),
+])
+def test_stage_properties_diagnostics(tmp_path, props, msg):
+    src = ("descB [ type = \"parsec_matrix_block_cyclic_t*\" ]\n"
+           "T(m)\n  m = 0 .. 1\n: descB(m, 0)\nRW B <- descB(m, 0)\n     -> descB(m, 0)\n"
+           f"BODY {props}\n{{\n}}\nEND\n")
+    p = tmp_path / "bad.jdf"
+    p.write_text(src)
+    r = subprocess.run([ptgpp.PTGPP, "-i", str(p), "-o", str(tmp_path / "bad")], capture_output=True, text=True)
+    assert r.returncode != 0
+    assert msg in r.stderr + r.stdout

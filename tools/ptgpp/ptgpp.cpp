@@ -828,6 +828,11 @@ struct Gen {
     for (auto& g : j.globals) s += "[[maybe_unused]] auto& " + g.name + " = __tp->_g_" + g.name + "; ";
     return s;
   }
+  std::string bind_globals_const() const {
+    std::string s;
+    for (auto& g : j.globals) s += "[[maybe_unused]] const auto& " + g.name + " = __tp->_g_" + g.name + "; ";
+    return s;
+  }
   std::string bind_locals(const Function& f, const char* arr) const {
     std::string s;
     for (size_t i = 0; i < f.locals.size(); ++i) s += "[[maybe_unused]] const int32_t " + f.locals[i].name + " = " + arr + "[" + std::to_string(i) + "]; ";
@@ -1069,6 +1074,34 @@ struct Gen {
         if (const Prop* w = find_prop(bd.props, "weight")) c << "b.weight = (double)(" << w->val << "); ";
         if (const Prop* e = find_prop(bd.props, "evaluate")) c << "b.evaluate = [](const parsec::Task* t) { return " << e->val << "(t); }; ";
         if (const Prop* dy = find_prop(bd.props, "dyld")) c << "b.dyld = \"" << esc(dy->val) << "\"; ";
+        // user data movement and per-flow device size / collection
+        for (const char* k : {"stage_in", "stage_out"})
+          if (const Prop* sp = find_prop(bd.props, k)) {
+            if (type != "HIP") die(sp->line, std::string(k) + " is only meaningful on a BODY [type=HIP]");
+            c << "b." << k << " = [](parsec::GpuStageContext& __c) { return (int)" << sp->val << "(__c); }; ";
+          }
+        for (const Prop& fp : bd.props) {
+          const size_t dot = fp.key.find('.');
+          if (dot == std::string::npos) continue;
+          const std::string flow = fp.key.substr(0, dot), what = fp.key.substr(dot + 1);
+          int fidx = -1;
+          for (size_t k = 0; k < f.flows.size(); ++k) if (f.flows[k].name == flow) fidx = (int)k;
+          if (fidx < 0) die(fp.line, "BODY property " + fp.key + ": no flow named " + flow + " in " + f.name);
+          const bool code = fp.val.compare(0, 2, "%{") == 0;
+          const std::string body = code ? fp.val.substr(2) : "return (" + fp.val + ");";
+          const std::string prologue = "[[maybe_unused]] auto* __tp = static_cast<const parsec_" + fname + "_taskpool_t*>(this_task->taskpool); " +
+                                       bind_globals_const() + bind_locals(f, "this_task->locals");
+          if (what == "size") {
+            c << "if (b.flow_size.size() <= " << fidx << ") b.flow_size.resize(" << fidx + 1 << "); ";
+            c << "b.flow_size[" << fidx << "] = [](const parsec::Task* this_task) -> size_t { " << prologue << " " << body << " }; ";
+          } else if (what == "dc") {
+            c << "if (b.flow_dc.size() <= " << fidx << ") b.flow_dc.resize(" << fidx + 1 << "); ";
+            c << "b.flow_dc[" << fidx << "] = [](const parsec::Task* this_task) -> parsec::DataCollection* { " << prologue
+              << " return parsec::ptg::to_dc([&]() { " << body << " }()); }; ";
+          } else {
+            die(fp.line, "unknown BODY flow property " + fp.key + " (size, dc)");
+          }
+        }
         c << "d.bodies.push_back(std::move(b)); }\n";
       }
       c << "    __tp->add_task_class(std::move(d));\n  }\n";
