@@ -199,7 +199,9 @@ class Barrier {
 struct PoolElt : ListItem {
   struct PoolCache* owner = nullptr;
 };
-struct PoolCache {
+// one cache line per thread's cache: packed caches put several threads'
+// freelist heads on one line and every allocation bounced it between cores
+struct alignas(kCacheLine) PoolCache {
   MpscLifo<PoolElt> freelist;
   size_t allocated = 0;
 };

@@ -434,7 +434,7 @@ const std::vector<SchedulerComponent>& scheduler_components();
 struct PinsChain;
 struct ProfilingStream;
 
-struct ExecutionStream {
+struct alignas(64) ExecutionStream {  // one thread writes it per task: keep it off its neighbours' lines
   int th_id = 0;          // global id in the context
   int core_id = -1;
   int socket_id = 0;
@@ -448,6 +448,7 @@ struct ExecutionStream {
   bool is_manager = false;  // GPU manager / comm thread (does not select tasks)
   // statistics
   uint64_t nb_executed = 0, nb_selected = 0, nb_stolen = 0;
+  uint32_t cpu_exec_pending = 0;  // executed CPU tasks not yet added to the CPU device's shared counter
   std::vector<int> steal_order;  // other th_ids by distance (filled by vpmap)
 };
 

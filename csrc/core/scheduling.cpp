@@ -183,7 +183,13 @@ int execute_task(ExecutionStream* es, Task* t) {
         if (ch.type == DEV_TEMPLATE)
           for (Device* d : DeviceRegistry::instance().devices)
             if (d && d->type == DEV_TEMPLATE) dev = d;
-        dev->stats.executed_tasks.fetch_add(1, std::memory_order_relaxed);
+        // the shared device counter is updated in batches (a per-task atomic
+        // on one line is the hottest contention point of empty-task DAGs)
+        if (dev->type == DEV_CPU) {
+          if (++es->cpu_exec_pending >= 64) { dev->stats.executed_tasks.fetch_add(es->cpu_exec_pending, std::memory_order_relaxed); es->cpu_exec_pending = 0; }
+        } else {
+          dev->stats.executed_tasks.fetch_add(1, std::memory_order_relaxed);
+        }
         ++es->nb_executed;
         if (gpus) cpu_write_epilog(t);
       }
@@ -246,6 +252,12 @@ int task_progress(ExecutionStream* es, Task* t, int32_t distance) {
   return 0;
 }
 
+static void flush_exec_counter(ExecutionStream* es) {
+  if (!es->cpu_exec_pending) return;
+  DeviceRegistry::instance().devices[0]->stats.executed_tasks.fetch_add(es->cpu_exec_pending, std::memory_order_relaxed);
+  es->cpu_exec_pending = 0;
+}
+
 void worker_loop(ExecutionStream* es, bool master) {
   Context* ctx = es->ctx;
   Scheduler* s = ctx->scheduler;
@@ -272,9 +284,11 @@ void worker_loop(ExecutionStream* es, bool master) {
       if (dist > 0) ++es->nb_stolen;
       task_progress(es, t, dist);
     } else {
+      flush_exec_counter(es);
       backoff.idle();
     }
   }
+  flush_exec_counter(es);
   // drain the bypass slot so a later epoch does not lose it
   if (es->next_task) {
     Task* t = es->next_task;

@@ -15,6 +15,8 @@ namespace ptg {
 
 // index-array slot of a task that already became ready
 static Task* const kReadyMark = reinterpret_cast<Task*>(uintptr_t(1));
+// an index-array slot being updated (the slot word is its own lock)
+static Task* const kBusyMark = reinterpret_cast<Task*>(uintptr_t(3));
 
 static inline int64_t ev(const Expr& e, const Taskpool* tp, const int32_t* L, int64_t d = 0) { return e ? e(tp, L) : d; }
 
@@ -297,7 +299,6 @@ void PtgTaskClass::build_index_store(const Taskpool* tp) {
     if (total > (int64_t)1 << 26) return;  // > 64M slots: keep the hash table
   }
   st.slots.assign((size_t)total, nullptr);
-  st.locks.reset(new std::mutex[256]);
   st.ok = true;
 }
 
@@ -960,8 +961,18 @@ Task* PtgTaskpool::with_pending(PtgTaskClass* tc, const int32_t* L, uint64_t key
       for (int i = 0; i < tc->nb_params; ++i) P[i] = L[tc->param_local[i]];
       const int64_t ix = st.index(P);
       if (ix >= 0) {
-        std::lock_guard<std::mutex> g(st.locks[(size_t)ix & 255]);
-        return f(st.slots[(size_t)ix]);
+        // per-slot lock: swap the busy mark in, work on the previous value,
+        // publish the new one (only activations of the same task contend)
+        Task** sp = &st.slots[(size_t)ix];
+        Task* slot;
+        for (;;) {
+          slot = __atomic_exchange_n(sp, kBusyMark, __ATOMIC_ACQUIRE);
+          if (slot != kBusyMark) break;
+          while (__atomic_load_n(sp, __ATOMIC_RELAXED) == kBusyMark) PARSEC_CPU_RELAX();
+        }
+        Task* r = f(slot);
+        __atomic_store_n(sp, slot, __ATOMIC_RELEASE);
+        return r;
       }
     }
   }

@@ -183,7 +183,8 @@ class PtgTaskClass : public TaskClass {
   struct IndexStore {
     std::vector<int64_t> lo, ext;
     std::vector<Task*> slots;
-    std::unique_ptr<std::mutex[]> locks;
+    // slots are updated under a per-slot lock held in the slot word itself
+    // (ptg.cpp with_pending)
     bool ok = false;
     int64_t index(const int32_t* params) const {
       int64_t ix = 0;
