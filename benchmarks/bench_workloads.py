@@ -92,6 +92,21 @@ def bench_qr(args):
         tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+    check = None
+    if args.check and world == 1:
+        # R of the last timed factorization against the input, outside the
+        # timed region: ||R^T R - A^T A||_F / ||A^T A||_F (Q orthogonal =>
+        # A^T A = R^T Q^T Q R = R^T R)
+        torch.cuda.synchronize()
+        Afull = backup.permute(1, 3, 0, 2).reshape(N, N)
+        R = torch.triu(storeA.permute(1, 3, 0, 2).reshape(N, N))
+        AtA = Afull.t() @ Afull
+        del Afull
+        RtR = R.t() @ R
+        del R
+        check = float(torch.linalg.norm(RtR - AtA) / torch.linalg.norm(AtA))
+        del RtR, AtA
+        torch.cuda.empty_cache()
     ctx.fini()
     if world > 1:
         pa.comm_fini()
@@ -99,6 +114,8 @@ def bench_qr(args):
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
            "dtype": "fp64", "data": "synthetic uniform(-0.5, 0.5)", "config": {"model": "tiled DGEQRF", "N": N, "nb": nb, "ib": args.ib,
                                                                              "parallelism": f"1D row-cyclic P{P}x1"}}
+    if check is not None:
+        out["residual_RtR_vs_AtA"] = check
     if world > 1:
         dist.destroy_process_group()
     return out, rank
@@ -169,6 +186,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cores", type=int, default=4)
+    ap.add_argument("--check", action="store_true", help="qr: verify R (||R^T R - A^T A|| / ||A^T A||) after the timed steps")
     args = ap.parse_args()
     if args.n is None:
         args.n = {"qr": 16384, "stencil": 512, "dtd_gemm": 2048}[args.workload]
