@@ -179,8 +179,12 @@ void outputv(int level, const char* sub, const char* fmt, va_list ap) {
   if (level > debug_verbosity()) return;
   char buf[2048];
   vsnprintf(buf, sizeof(buf), fmt, ap);
+  // debug lines carry a monotonic timestamp (ms) so protocol gaps can be read off a log
+  static const auto t0 = std::chrono::steady_clock::now();
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   std::lock_guard<std::mutex> g(g_out_mutex);
-  std::fprintf(stderr, "[parsec %d%s%s] %s\n", g_rank.load(), sub && *sub ? " " : "", sub ? sub : "", buf);
+  if (level >= kVerbDebug) std::fprintf(stderr, "[parsec %d%s%s %.3f] %s\n", g_rank.load(), sub && *sub ? " " : "", sub ? sub : "", ms, buf);
+  else std::fprintf(stderr, "[parsec %d%s%s] %s\n", g_rank.load(), sub && *sub ? " " : "", sub ? sub : "", buf);
 }
 
 void output(int level, const char* sub, const char* fmt, ...) {
