@@ -76,7 +76,15 @@ constexpr int kStencilKc2 = 32;
 
 __device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
 __device__ __forceinline__ void st2(double* p, double2 v) { *reinterpret_cast<double2*>(p) = v; }
+// the new block is read back only in the next sweep (the grid is far larger
+// than L2 + MALL): stream it past the caches
+__device__ __forceinline__ void st2_nt(double* p, double2 v) {
+  __builtin_nontemporal_store(v.x, p);
+  __builtin_nontemporal_store(v.y, p + 1);
+}
+static int g_stencil_nt = -1;  // PARSEC_STENCIL_NT=0: plain stores for the block output
 
+template <bool NT>
 __device__ __forceinline__ void stencil7v_tile(const StencilArgs& a, int tx, int ty, int tz) {
   const int lane = threadIdx.x & 63;
   const int i = tx * 128 + lane * 2;
@@ -111,7 +119,8 @@ __device__ __forceinline__ void stencil7v_tile(const StencilArgs& a, int tx, int
       double2 v;
       v.x = a.c0 * c.x + a.c1 * (left + c.y + ym.x + yp.x + zm.x + zp.x);
       v.y = a.c0 * c.y + a.c1 * (c.x + right + ym.y + yp.y + zm.y + zp.y);
-      st2(a.out + idx, v);
+      if (NT) st2_nt(a.out + idx, v);
+      else st2(a.out + idx, v);
       if (i == 0 && a.fout[0]) a.fout[0][(size_t)k * by + j] = v.x;
       if (i + 2 == bx && a.fout[1]) a.fout[1][(size_t)k * by + j] = v.y;
       if (j == 0 && a.fout[2]) st2(a.fout[2] + (size_t)k * bx + i, v);
@@ -134,6 +143,7 @@ static bool stencil_vec_ok(const StencilArgs& a) {
   return true;
 }
 
+template <bool NT>
 __global__ __launch_bounds__(256) void stencil7v_batch_kernel(const StencilBatchArgs args) {
   const int w = blockIdx.x;
   int lo = 0, hi = args.count - 1;
@@ -145,7 +155,7 @@ __global__ __launch_bounds__(256) void stencil7v_batch_kernel(const StencilBatch
   const StencilArgs& a = args.d[lo];
   const int local = w - args.start[lo];
   const int nx = (a.bx + 127) / 128, ny = (a.by + 3) / 4;
-  stencil7v_tile(a, local % nx, (local / nx) % ny, local / (nx * ny));
+  stencil7v_tile<NT>(a, local % nx, (local / nx) % ny, local / (nx * ny));
 }
 
 // Initial condition of a block (the same smooth bump as the host
@@ -204,6 +214,8 @@ void launch_stencil7_batch(const StencilDesc* d, int n, hipStream_t stream) {
   if (g_stencil_vec < 0) {
     const char* e = std::getenv("PARSEC_STENCIL_VEC");
     g_stencil_vec = e ? std::atoi(e) : 1;
+    const char* n = std::getenv("PARSEC_STENCIL_NT");
+    g_stencil_nt = n ? std::atoi(n) : 1;
   }
   for (int s0 = 0; s0 < n; s0 += kMaxStencilBatch) {
     StencilBatchArgs a;
@@ -218,7 +230,8 @@ void launch_stencil7_batch(const StencilDesc* d, int n, hipStream_t stream) {
     }
     a.start[a.count] = total;
     if (total <= 0) continue;
-    if (vec) hipLaunchKernelGGL(stencil7v_batch_kernel, dim3(total), dim3(256), 0, stream, a);
+    if (vec && g_stencil_nt) hipLaunchKernelGGL(stencil7v_batch_kernel<true>, dim3(total), dim3(256), 0, stream, a);
+    else if (vec) hipLaunchKernelGGL(stencil7v_batch_kernel<false>, dim3(total), dim3(256), 0, stream, a);
     else hipLaunchKernelGGL(stencil7_batch_kernel, dim3(total), dim3(256), 0, stream, a);
   }
 }
