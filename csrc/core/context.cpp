@@ -1,3 +1,4 @@
+#include <array>
 // Context bring-up / tear-down, virtual-process map, thread binding.
 //
 // Parity: parsec_init/parsec_fini (reference parsec.c:384-924, 1158-1301),
@@ -40,11 +41,21 @@ ExecutionStream* my_execution_stream() { return t_es; }
 void set_my_execution_stream(ExecutionStream* es) { t_es = es; }
 
 // ----------------------------------------------------------- topology
+// hwloc-equivalent view of one allowed CPU (reference parsec_hwloc.c): the
+// package, NUMA node and the caches it shares (id = lowest CPU sharing it)
 struct CpuTopo {
   int cpu;
   int package;
   int numa;
+  int l2 = -1, l3 = -1;
 };
+
+static int first_cpu_of_list(const std::string& path) {
+  std::ifstream in(path);
+  std::string s;
+  if (!(in >> s)) return -1;
+  return std::atoi(s.c_str());  // "a-b,c..." -> a
+}
 
 static int read_int_file(const std::string& p, int dflt) {
   std::ifstream in(p);
@@ -71,9 +82,35 @@ static std::vector<CpuTopo> allowed_cpus() {
       std::ifstream probe("/sys/devices/system/cpu/cpu" + std::to_string(c) + "/node" + std::to_string(n) + "/cpumap");
       if (probe) { t.numa = n; break; }
     }
+    for (int k = 0; k < 8; ++k) {
+      const std::string base = "/sys/devices/system/cpu/cpu" + std::to_string(c) + "/cache/index" + std::to_string(k) + "/";
+      const int level = read_int_file(base + "level", -1);
+      if (level < 0) break;
+      if (level == 2) t.l2 = first_cpu_of_list(base + "shared_cpu_list");
+      if (level == 3) t.l3 = first_cpu_of_list(base + "shared_cpu_list");
+    }
     out.push_back(t);
   }
   return out;
+}
+
+std::vector<std::array<int, 5>> topology_cpus() {
+  std::vector<std::array<int, 5>> r;
+  for (auto& c : allowed_cpus()) r.push_back({c.cpu, c.package, c.numa, c.l2, c.l3});
+  return r;
+}
+
+std::vector<std::vector<int>> topology_numa_distances() {
+  std::vector<std::vector<int>> r;
+  for (int n = 0; n < 64; ++n) {
+    std::ifstream in("/sys/devices/system/node/node" + std::to_string(n) + "/distance");
+    if (!in) break;
+    std::vector<int> row;
+    int v;
+    while (in >> v) row.push_back(v);
+    r.push_back(row);
+  }
+  return r;
 }
 
 static void bind_current_thread(int cpu) {
@@ -202,6 +239,8 @@ Context* context_init(int nb_cores, std::vector<std::string>& args) {
         const CpuTopo& ct = cpus[tid % cpus.size()];
         es->core_id = ct.cpu;
         es->socket_id = ct.package * 64 + ct.numa;
+        es->l2_id = ct.l2;
+        es->l3_id = ct.l3;
       }
       vp->es.push_back(es);
       ctx->all_es.push_back(es);
@@ -209,19 +248,31 @@ Context* context_init(int nb_cores, std::vector<std::string>& args) {
     ctx->vps.push_back(vp);
   }
   std::sort(ctx->all_es.begin(), ctx->all_es.end(), [](auto* a, auto* b) { return a->th_id < b->th_id; });
-  // steal order: same VP only (no stealing across VPs), closest socket first.
+  // steal order: same VP only (no stealing across VPs), closest first in the
+  // cache hierarchy: shared L2, shared L3, same NUMA node, same package, other
   for (auto* vp : ctx->vps)
     for (auto* es : vp->es) {
       std::vector<std::pair<int, int>> d;
-      for (auto* o : vp->es)
-        if (o != es) d.push_back({o->socket_id == es->socket_id ? 0 : 1, o->th_id});
-      std::stable_sort(d.begin(), d.end());
-      // rotate within equal distances so threads do not all hit the same victim first
-      for (auto& p : d) es->steal_order.push_back(p.second);
-      if (!es->steal_order.empty()) {
-        size_t rot = (size_t)es->th_id % es->steal_order.size();
-        std::rotate(es->steal_order.begin(), es->steal_order.begin() + rot, es->steal_order.end());
+      for (auto* o : vp->es) {
+        if (o == es) continue;
+        int dist = 4;
+        if (o->l2_id >= 0 && o->l2_id == es->l2_id) dist = 0;
+        else if (o->l3_id >= 0 && o->l3_id == es->l3_id) dist = 1;
+        else if (o->socket_id == es->socket_id) dist = 2;
+        else if (o->socket_id / 64 == es->socket_id / 64) dist = 3;
+        d.push_back({dist, o->th_id});
       }
+      std::stable_sort(d.begin(), d.end());
+      // rotate within each equal-distance group so threads do not all hit the
+      // same victim first (the groups themselves stay in distance order)
+      for (size_t b = 0; b < d.size();) {
+        size_t e = b;
+        while (e < d.size() && d[e].first == d[b].first) ++e;
+        const size_t n = e - b;
+        if (n > 1) std::rotate(d.begin() + b, d.begin() + b + (size_t)es->th_id % n, d.begin() + e);
+        b = e;
+      }
+      for (auto& p : d) es->steal_order.push_back(p.second);
     }
 
   // task mempool: large enough for every front-end's task type.

@@ -448,7 +448,8 @@ struct alignas(64) ExecutionStream {  // one thread writes it per task: keep it 
   bool is_manager = false;  // GPU manager / comm thread (does not select tasks)
   // statistics
   uint64_t nb_executed = 0, nb_selected = 0, nb_stolen = 0;
-  uint32_t cpu_exec_pending = 0;  // executed CPU tasks not yet added to the CPU device's shared counter
+  uint32_t cpu_exec_pending = 0;
+  int l2_id = -1, l3_id = -1;  // caches this thread's core shares (lowest CPU id sharing them)  // executed CPU tasks not yet added to the CPU device's shared counter
   std::vector<int> steal_order;  // other th_ids by distance (filled by vpmap)
 };
 
@@ -558,6 +559,9 @@ struct Context {
 // thread slot for mempools of non-runtime threads
 int thread_slot();
 ExecutionStream* my_execution_stream();
+// hwloc-style topology of the allowed CPUs: {cpu, package, numa, l2 id, l3 id}, NUMA distance matrix
+std::vector<std::array<int, 5>> topology_cpus();
+std::vector<std::vector<int>> topology_numa_distances();
 void set_my_execution_stream(ExecutionStream* es);
 
 // ================================================= core engine functions

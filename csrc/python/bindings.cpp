@@ -685,6 +685,18 @@ PYBIND11_MODULE(_C, m) {
   // ------------------------------------------------------------------ comm
   m.def("comm_init", [](int rank, int size, const std::string& job, int gpu) { py::gil_scoped_release rel; return comm_init(rank, size, job, gpu); });
   m.def("comm_fini", []() { py::gil_scoped_release rel; comm_fini(); });
+  m.def("topology", []() {
+    py::dict d;
+    py::list cpus;
+    for (auto& c : topology_cpus()) {
+      py::dict e;
+      e["cpu"] = c[0]; e["package"] = c[1]; e["numa"] = c[2]; e["l2"] = c[3]; e["l3"] = c[4];
+      cpus.append(e);
+    }
+    d["cpus"] = cpus;
+    d["numa_distances"] = topology_numa_distances();
+    return d;
+  }, "hwloc-style view of the allowed CPUs (package, NUMA node, shared L2 / L3) and NUMA distances");
   m.def("comm_stats", []() { py::dict d; for (auto& kv : comm_stats()) d[py::str(kv.first)] = kv.second; return d; });
   m.def("comm_barrier", []() { py::gil_scoped_release rel; return comm_barrier(); });
   m.def("comm_rank", &comm_rank);

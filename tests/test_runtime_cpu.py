@@ -541,3 +541,19 @@ def test_dpotrf_jdf_reports_info(pa):
     ctx.wait()
     ctx.fini()
     assert pa.read_int(info) == 16 + 6
+
+
+def test_topology_cache_levels(pa):
+    """hwloc-equivalent topology (reference parsec_hwloc.c): every allowed CPU
+    reports its package, NUMA node and shared L2 / L3 (lowest sharing CPU id),
+    plus the NUMA distance matrix; used to order work stealing."""
+    t = pa.topology()
+    cpus = t["cpus"]
+    assert cpus and all({"cpu", "package", "numa", "l2", "l3"} <= set(c) for c in cpus)
+    for c in cpus:
+        assert c["l2"] <= c["cpu"] or c["l2"] == -1
+        assert c["l3"] <= c["cpu"] or c["l3"] == -1
+    d = t["numa_distances"]
+    assert all(len(row) == len(d) for row in d)
+    if d:
+        assert all(d[i][i] == min(d[i]) for i in range(len(d)))
