@@ -111,3 +111,41 @@ def test_comm_trace_payload_sizes(pa, tmp_path):
     assert snd and sorted(snd) == sorted(rcv)
     assert all(b == 32 * 32 * 8 for *_, b in snd)
     assert any(r["type"] == "COMM_ACTIVATE" for r in rows)
+
+
+def test_dagtools_on_recorded_cholesky_dag(pa, tmp_path):
+    """DAG tools (reference tools/dagenum.c, grapher.c): the DOT written by the
+    grapher for a tiled Cholesky has every task, is acyclic, and its critical
+    path is POTRF -> TRSM -> SYRK per panel (3 NT - 2 tasks)."""
+    from parsec_amd import dagtools
+
+    NT, nb = 5, 4
+    pa.mca_set("parsec_dot", str(tmp_path / "chol"))
+    pa.mca_set("device_hip_enabled", "0")
+    try:
+        ctx = pa.init(2)
+    finally:
+        pa.mca_unset("parsec_dot")
+        pa.mca_unset("device_hip_enabled")
+    N = NT * nb
+    A = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb, nb, N, N)
+    S = np.random.default_rng(3).standard_normal((N, N))
+    S = S @ S.T + N * np.eye(N)
+    for m in range(NT):
+        for n in range(NT):
+            A.tile(m, n)[:, :] = S[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb]
+            A.mark_host_modified(m, n)
+    tp, info = pa.dpotrf_new(A, pa.MATRIX_LOWER)
+    ctx.add_taskpool(tp)
+    ctx.start()
+    ctx.wait()
+    ctx.fini()
+    dots = [str(tmp_path / p) for p in os.listdir(tmp_path) if p.startswith("chol")]
+    g = dagtools.read_dot(dots)
+    st = g.stats()
+    assert st["nodes"] == NT * (NT + 1) * (NT + 2) // 6
+    assert st["acyclic"] and st["roots"] == 1
+    assert st["critical_path"] == 3 * NT - 2
+    assert dagtools.main(["stats"] + dots) == 0
+    classes = {g.class_of(x) for x in g.nodes}
+    assert len(classes) >= 3
