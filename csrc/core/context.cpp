@@ -296,6 +296,7 @@ Context* context_init(int nb_cores, std::vector<std::string>& args) {
   pins_init(ctx);
   devices_init(ctx);
   remote_dep_init(ctx);
+  properties_publisher_start(ctx);
 
   // threads
   ctx->barrier = new Barrier(nb_cores);
@@ -341,6 +342,7 @@ int context_fini(Context** pctx) {
   profiling_thread_fini(master);
   grapher_fini(ctx);
   pins_fini(ctx);
+  properties_publisher_stop();
   profiling_fini(ctx);
   PARSEC_DEBUG(kVerbDebug, "fini", "devices fini");
   devices_fini(ctx);

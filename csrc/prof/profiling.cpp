@@ -15,6 +15,9 @@
 #include <set>
 #include <sstream>
 
+#include "../comm/comm.hpp"
+#include "../device/device.hpp"
+
 namespace parsec {
 
 // ============================================================= profiling
@@ -519,12 +522,89 @@ std::vector<std::pair<std::string, double>> properties_snapshot() {
   return out;
 }
 
+// Runtime counters published next to the user properties: per-device
+// executed tasks / kernel launches, threads and active taskpools,
+// communication counters (reference dictionary.c namespaces
+// PARSEC::<dev>::..., PARSEC::<thread>::...).
+static std::vector<std::pair<std::string, double>> runtime_properties(Context* ctx) {
+  std::vector<std::pair<std::string, double>> r;
+  auto& reg = DeviceRegistry::instance();
+  for (Device* d : reg.devices) {
+    if (!d) continue;
+    r.emplace_back("device." + d->name + ".executed_tasks", (double)d->stats.executed_tasks.load());
+    r.emplace_back("device." + d->name + ".kernel_launches", (double)d->stats.kernel_launches.load());
+  }
+  if (ctx) {
+    r.emplace_back("runtime.threads", (double)ctx->all_es.size());
+    r.emplace_back("runtime.active_taskpools", (double)ctx->active_taskpools.load());
+  }
+  for (auto& kv : comm_stats()) r.emplace_back("comm." + kv.first, (double)kv.second);
+  return r;
+}
+
+namespace {
+struct Publisher {
+  std::thread th;
+  std::mutex m;
+  std::condition_variable cv;
+  bool stop = false;
+  std::string name;
+  Context* ctx = nullptr;
+};
+Publisher& PUB() { static Publisher* p = new Publisher(); return *p; }
+}  // namespace
+
+static int properties_write_shm(const std::string& shm_name, const std::vector<std::pair<std::string, double>>& snap, uint64_t seq);
+
+// Live publication (reference aggregator_visu reads the dictionary from shm
+// while the application runs): MCA profile_properties_shm=<name> refreshes
+// /dev/shm/<name> every profile_properties_period_ms.
+void properties_publisher_start(Context* ctx) {
+  auto& pr = ParamRegistry::instance();
+  std::string name = pr.reg_string("profile", "properties", "shm", "Publish runtime counters + properties in this POSIX shm segment while running", "");
+  const int64_t period = pr.reg_int("profile", "properties", "period_ms", "Refresh period of the published properties (ms)", 100);
+  if (name.empty()) return;
+  if (name[0] != '/') name = "/" + name;
+  auto& p = PUB();
+  if (p.th.joinable()) return;
+  p.stop = false;
+  p.name = name;
+  p.ctx = ctx;
+  p.th = std::thread([&p, period] {
+    uint64_t seq = 0;
+    std::unique_lock<std::mutex> lk(p.m);
+    for (;;) {
+      auto snap = properties_snapshot();
+      for (auto& kv : runtime_properties(p.ctx)) snap.push_back(kv);
+      properties_write_shm(p.name, snap, ++seq);
+      if (p.cv.wait_for(lk, std::chrono::milliseconds(std::max<int64_t>(period, 1)), [&] { return p.stop; })) break;
+    }
+  });
+}
+
+void properties_publisher_stop() {
+  auto& p = PUB();
+  if (!p.th.joinable()) return;
+  {
+    std::lock_guard<std::mutex> g(p.m);
+    p.stop = true;
+  }
+  p.cv.notify_all();
+  p.th.join();
+  // final values stay readable after the run; the segment is the user's to remove
+  auto snap = properties_snapshot();
+  for (auto& kv : runtime_properties(p.ctx)) snap.push_back(kv);
+  properties_write_shm(p.name, snap, ~0ull);
+  p.ctx = nullptr;
+}
+
+int properties_dump_shm(const std::string& shm_name) { return properties_write_shm(shm_name, properties_snapshot(), 0); }
+
 // Publish properties in a POSIX shm region: an XML-ish header then the values
 // (reference dictionary.c exposes the same through shm for aggregator_visu).
-int properties_dump_shm(const std::string& shm_name) {
-  auto snap = properties_snapshot();
+static int properties_write_shm(const std::string& shm_name, const std::vector<std::pair<std::string, double>>& snap, uint64_t seq) {
   std::ostringstream os;
-  os << "<properties>\n";
+  os << "<properties seq=\"" << seq << "\">\n";
   for (auto& kv : snap) os << "  <p name=\"" << kv.first << "\" value=\"" << kv.second << "\"/>\n";
   os << "</properties>\n";
   std::string s = os.str();

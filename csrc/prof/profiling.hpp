@@ -96,6 +96,8 @@ void grapher_fini(Context* ctx);
 
 // Properties dictionary (live counters readable by tools)
 void properties_set(const std::string& name, double value);
+void properties_publisher_start(Context* ctx);
+void properties_publisher_stop();
 std::vector<std::pair<std::string, double>> properties_snapshot();
 int properties_dump_shm(const std::string& shm_name);
 

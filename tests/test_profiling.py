@@ -149,3 +149,48 @@ def test_dagtools_on_recorded_cholesky_dag(pa, tmp_path):
     assert dagtools.main(["stats"] + dots) == 0
     classes = {g.class_of(x) for x in g.nodes}
     assert len(classes) >= 3
+
+
+def test_live_properties_publisher(pa, tmp_path):
+    """Live properties (reference tools/aggregator_visu over the shm dictionary):
+    with profile_properties_shm the runtime refreshes the segment while it runs;
+    parsec_amd.aggregator reads the device counters and user properties."""
+    import uuid
+
+    from parsec_amd import aggregator
+
+    name = "pamd_props_" + uuid.uuid4().hex[:8]
+    pa.mca_set("profile_properties_shm", name)
+    pa.mca_set("profile_properties_period_ms", "10")
+    try:
+        ctx = pa.init(2)
+    finally:
+        pa.mca_unset("profile_properties_shm")
+        pa.mca_unset("profile_properties_period_ms")
+    try:
+        pa.properties_set("app.iteration", 7.0)
+        A = pa.BlockCyclic(pa.MATRIX_INTEGER, 0, 1, 1, 4, 1)
+        tp = pa.dtd_taskpool(ctx)
+        ctx.start()
+        for i in range(64):
+            pa.insert_task(tp, lambda task: 0, [(tp.tile_of(A, A.data_key([i % 4, 0])), pa.INOUT)], name="props_work")
+        tp.data_flush_all(A)
+        ctx.wait()
+        import time
+
+        time.sleep(0.05)
+        seq, vals = aggregator.read(name)
+        assert seq >= 1
+        assert vals.get("app.iteration") == 7.0
+        assert any(k.startswith("device.") and k.endswith(".executed_tasks") for k in vals)
+        assert "runtime.threads" in vals
+        ctx.fini()
+        seq2, vals2 = aggregator.read(name)  # final snapshot written at fini
+        cpu = [v for k, v in vals2.items() if k.endswith(".executed_tasks")]
+        assert max(cpu) >= 64
+        assert aggregator.main([name, "--count", "1", "--interval", "0"]) == 0
+    finally:
+        try:
+            os.unlink(os.path.join("/dev/shm", name))
+        except OSError:
+            pass
