@@ -457,10 +457,18 @@ int ShmEngine::progress() {
 void ShmEngine::thread_main() {
   thread_id_ = std::this_thread::get_id();
   if (gpu_ >= 0) (void)hipSetDevice(gpu_);
-  Backoff b;
+  // Every message hop of the remote-dependency protocol waits for this loop
+  // to notice it: spin while traffic is recent (no sleeping backoff: a 1-50 us
+  // nap per poll added up to ~4 naps per remote edge), yield for a while
+  // after that, and only sleep once the engine has been quiet for 2 ms.
+  uint64_t last = now_ns();
+  uint32_t spins = 0;
   while (!stop_.load(std::memory_order_relaxed)) {
-    if (progress()) b.reset();
-    else if (b.misses() < 4096) { PARSEC_CPU_RELAX(); b.idle(); }
+    if (progress()) { last = now_ns(); continue; }
+    if ((++spins & 63) != 0) { PARSEC_CPU_RELAX(); continue; }
+    const uint64_t quiet = now_ns() - last;
+    if (quiet < 200000) PARSEC_CPU_RELAX();
+    else if (quiet < 2000000) std::this_thread::yield();
     else std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
   // drain what is left

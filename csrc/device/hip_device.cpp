@@ -1181,13 +1181,17 @@ void HipDevice::manager_main() {
     gpu_trace = true;
   }
   Backoff backoff;
+  uint32_t poll_spins = 0;
   for (;;) {
     bool did = progress();
     if (did) { backoff.reset(); continue; }
     if (inflight.load(std::memory_order_acquire) > 0) {
-      // work in flight on the GPU: poll tightly, yielding now and then
-      if (backoff.misses() < 2000) { PARSEC_CPU_RELAX(); backoff.idle(); }
-      else std::this_thread::yield();
+      // work in flight on the GPU: poll tightly (never sleep: a completion
+      // noticed late is dead time on the critical path -- a 1-50 us backoff
+      // sleep here left ~50 us gaps between dependent kernels), yielding the
+      // core now and then
+      for (int i = 0; i < 8; ++i) PARSEC_CPU_RELAX();
+      if ((++poll_spins & 4095) == 0) std::this_thread::yield();
       continue;
     }
     if (stop.load()) break;
