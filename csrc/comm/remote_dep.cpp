@@ -27,7 +27,8 @@ static ExecutionStream* g_comm_es = nullptr;
 static size_t g_short_limit = 1024;
 static bool g_recv_from_cache = true;
 static int g_recv_pool = 1;  // 0 free after use, 1 recycle by size, 2 never reuse (diagnostic)
-static int g_ipc_debug_sync = 0;  // 1: sender hipDeviceSynchronize before answering a GET (diagnostic)
+static int g_ipc_debug_sync = 0;
+static int g_eager_ipc = 1;  // comm_eager_ipc: IPC descriptors ride in the activation (no GET round trip)  // 1: sender hipDeviceSynchronize before answering a GET (diagnostic)
 static int g_ipc_verify = 0;      // diagnostic: checksum every IPC payload at the sender and after the pull
 
 CommEngine* comm_engine() { return g_ce; }
@@ -46,7 +47,9 @@ const char* comm_device_plane_name() {
 
 // ------------------------------------------------------------- wire format
 namespace {
-enum FlowKind : uint8_t { FK_CTL = 0, FK_HOST = 1, FK_DEVICE = 2, FK_EAGER = 3 };
+// FK_IPC: a device flow whose IPC descriptor rides in the activation itself
+// (the receiver pulls at once: no GET round trip; its IPC_DONE releases)
+enum FlowKind : uint8_t { FK_CTL = 0, FK_HOST = 1, FK_DEVICE = 2, FK_EAGER = 3, FK_IPC = 4 };
 
 struct ActHdr {
   uint32_t tp_id;
@@ -104,6 +107,11 @@ uint64_t debug_checksum(int dev, const void* p, size_t bytes) {
   for (size_t i = 0; i < h.size(); ++i) s = s * 1099511628211ull + h[i];
   return s;
 }
+
+struct IpcDesc {
+  uint64_t offset;
+  char handle[64];
+};
 
 struct IpcDone {
   uint64_t send_id;
@@ -254,6 +262,7 @@ DataCopy* new_recv_copy(size_t bytes, bool device) {
 
 void deliver(RecvState* r);
 void start_recv(int src, const char* msg, size_t len, Taskpool* tp);
+void pull_ipc(int src, RecvState* r, uint32_t f, const char* handle, uint64_t offset, uint64_t sid, uint64_t want);
 
 // Build and send activations to the direct children of this rank for every flow.
 void send_activations(Taskpool* tp, const ActHdr& base, int my_pos_root_rank, const std::vector<FlowDesc>& fd_in,
@@ -285,6 +294,14 @@ void send_activations(Taskpool* tp, const ActHdr& base, int my_pos_root_rank, co
     g_sends[s->id] = s;
   }
   tp->tdm->taskpool_addto_runtime_actions(tp, 1);
+  // device flows on the IPC plane: export once, every destination pulls
+  std::vector<FlowDesc> fd_eff(fd_in.begin(), fd_in.end());
+  IpcDesc ipc[kMaxFlows];
+  if (g_eager_ipc && g_ce->ipc_ok() && !g_ce->rccl_ok())
+    for (int f = 0; f < nflows; ++f)
+      if ((base.output_mask & (1u << f)) && fd_eff[f].kind == FK_DEVICE && data[f] && data[f]->device_index != 0 &&
+          g_ce->ipc_export(data[f]->device_private, ipc[f].handle, &ipc[f].offset) == 0)
+        fd_eff[f].kind = FK_IPC;
   for (auto& [dst, mask] : dest_flows) {
     ActHdr h = base;
     h.send_id = s->id;
@@ -295,13 +312,16 @@ void send_activations(Taskpool* tp, const ActHdr& base, int my_pos_root_rank, co
     int gets = 0;
     for (int f = 0; f < nflows; ++f) {
       if (!(mask & (1u << f))) continue;
-      FlowDesc d = fd_in[f];
+      FlowDesc d = fd_eff[f];
       d.nranks = (uint16_t)ranks[f].size();
       put(&d, sizeof(d));
       put(ranks[f].data(), ranks[f].size() * sizeof(int));
       if (d.kind == FK_EAGER) {
         put(data[f]->device_private, d.bytes);
         while (body.size() % 8) body.push_back(0);
+      } else if (d.kind == FK_IPC) {
+        put(&ipc[f], sizeof(IpcDesc));
+        ++gets;  // released by this destination's IPC_DONE
       } else if (d.kind != FK_CTL) {
         ++gets;
       }
@@ -351,7 +371,8 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
   for (int f = 0; f < kMaxFlows; ++f) if (r->hdr.output_mask & (1u << f)) nflows = f + 1;
   r->fd.resize(nflows);
   r->ranks.resize(nflows);
-  uint32_t get_mask = 0;
+  uint32_t get_mask = 0, ipc_mask = 0;
+  IpcDesc ipc[kMaxFlows];
   for (int f = 0; f < nflows; ++f) {
     if (!(r->hdr.output_mask & (1u << f))) continue;
     FlowDesc d;
@@ -371,6 +392,12 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
       r->data[f] = new_recv_copy(d.bytes, dev);
       get_mask |= 1u << f;
       ++r->remaining;
+    } else if (d.kind == FK_IPC) {
+      std::memcpy(&ipc[f], msg + off, sizeof(IpcDesc));
+      off += sizeof(IpcDesc);
+      r->data[f] = new_recv_copy(d.bytes, true);
+      ipc_mask |= 1u << f;
+      ++r->remaining;
     }
   }
   if (r->hdr.extra_bytes) { r->extra.assign(msg + off, msg + off + r->hdr.extra_bytes); off += r->hdr.extra_bytes; }
@@ -378,10 +405,26 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
   off += r->hdr.termdet_bytes;
   (void)len;
   tp->tdm->taskpool_addto_runtime_actions(tp, 1);
-  if (!get_mask) { deliver(r); return; }
+  if (!get_mask && !ipc_mask) { deliver(r); return; }
   {
     std::lock_guard<std::mutex> g(g_m);
     g_recvs[r->id] = r;
+  }
+  // flows whose IPC descriptor came with the activation: pull right away
+  // (the last completion may deliver r: nothing below touches r after it
+  // unless GETs are still outstanding, which keep r alive)
+  if (ipc_mask) {
+    if (g_comm_prof)
+      for (int f = 0; f < nflows; ++f)
+        if (ipc_mask & (1u << f)) {
+          CommInfo ci{src, f, (int64_t)r->fd[f].bytes, PLANE_IPC, 0};
+          comm_trace(k_rcv_b, flow_event(r->id, f), r->hdr.tp_id, &ci);
+        }
+    const uint64_t sid = r->hdr.send_id;
+    const uint32_t gm_left = get_mask;
+    for (int f = 0; f < nflows; ++f)
+      if (ipc_mask & (1u << f)) pull_ipc(src, r, (uint32_t)f, ipc[f].handle, ipc[f].offset, sid, 0);
+    if (!gm_left) return;
   }
   // post the device receives before asking, in flow order (FIFO-matched by RCCL)
   for (int f = 0; f < nflows; ++f) {
@@ -488,26 +531,16 @@ void on_get(int src, int, const void* msg, size_t) {
   }
 }
 
-// Receiver: map the sender's allocation and pull the tile (comm thread).
-void on_data_ipc(int src, int, const void* msg, size_t) {
-  IpcMsg m;
-  std::memcpy(&m, msg, sizeof(m));
-  RecvState* r = nullptr;
-  {
-    std::lock_guard<std::mutex> g(g_m);
-    auto it = g_recvs.find(m.recv_id);
-    if (it == g_recvs.end()) fatal("IPC data for unknown receive");
-    r = it->second;
-  }
-  char* base = static_cast<char*>(g_ce->ipc_open(src, m.handle));
-  DataCopy* c = r->data[m.flow];
-  const uint64_t rid = m.recv_id, sid = m.send_id;
-  const uint32_t f = m.flow;
-  const uint64_t bytes = m.bytes;
-  const uint64_t want = m.checksum;
-  const char* srcp = base + m.offset;
+// Receiver: map the sender's allocation and pull flow f of receive r (comm
+// thread); the completion sends IPC_DONE and delivers when it was the last flow.
+void pull_ipc(int src, RecvState* r, uint32_t f, const char* handle, uint64_t offset, uint64_t sid, uint64_t want) {
+  char* base = static_cast<char*>(g_ce->ipc_open(src, handle));
+  DataCopy* c = r->data[f];
+  const uint64_t rid = r->id;
+  const uint64_t bytes = r->fd[f].bytes;
+  const char* srcp = base + offset;
   g_ce->ipc_copy(src, c->device_private, srcp, bytes, [rid, sid, f, src, bytes, want, c, srcp] {
-    if (g_ipc_verify) {
+    if (g_ipc_verify && want) {
       uint64_t got = debug_checksum(c->device_index, c->device_private, bytes);
       if (got != want) {
         uint64_t again = debug_checksum(c->device_index, srcp, bytes);
@@ -530,6 +563,20 @@ void on_data_ipc(int src, int, const void* msg, size_t) {
     }
     deliver(rs);
   });
+}
+
+void on_data_ipc(int src, int, const void* msg, size_t) {
+  IpcMsg m;
+  std::memcpy(&m, msg, sizeof(m));
+  RecvState* r = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_m);
+    auto it = g_recvs.find(m.recv_id);
+    if (it == g_recvs.end()) fatal("IPC data for unknown receive");
+    r = it->second;
+  }
+  if (r->fd[m.flow].bytes != m.bytes) fatal("IPC data: %llu bytes announced, %llu expected", (unsigned long long)m.bytes, (unsigned long long)r->fd[m.flow].bytes);
+  pull_ipc(src, r, m.flow, m.handle, m.offset, m.send_id, m.checksum);
 }
 
 // Sender: the receiver finished pulling one flow.
@@ -699,6 +746,7 @@ void remote_dep_init(Context* ctx) {
   g_recv_pool = (int)ParamRegistry::instance().reg_int("comm", "", "recv_pool", "Device receive buffers: 1 recycle by size, 0 free after use, 2 never reuse (diagnostic)", 1);
   g_ipc_debug_sync = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_debug_sync", "Diagnostic: device-synchronize before exporting a tile to a peer", 0);
   g_ipc_verify = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_verify", "Diagnostic: checksum IPC payloads at the sender and after the pull", 0);
+  g_eager_ipc = (int)ParamRegistry::instance().reg_int("comm", "", "eager_ipc", "Send the IPC descriptor of device flows with the activation (receiver pulls without a GET round trip)", 1);
   g_recv_from_cache = ParamRegistry::instance().reg_int("comm", "", "recv_from_cache", "Carve device receive buffers from the GPU tile-cache zone (1) or hipMalloc them (0)", 1) != 0;
   ctx->my_rank = comm_rank();
   ctx->nb_nodes = comm_size();
