@@ -54,13 +54,24 @@ def bench_qr(args):
     ctx = pa.init(args.cores)
     gpu = pa.first_gpu_device_index()
     N, nb = args.n, args.nb
-    P = world  # 1D row-cyclic distribution over ranks (process grid P x 1)
+    # process grid: --qr-grid 1d = P x 1 row-cyclic (the TS chain of a panel
+    # crosses every rank), 2d = the most square P x Q (P >= Q), which halves the
+    # ranks a panel chain crosses at 8 GPUs and spreads the trailing update
+    if args.qr_grid == "2d":
+        P = int(world ** 0.5)
+        while world % P:
+            P -= 1
+        P, Q = max(P, world // P), min(P, world // P)
+    else:
+        P, Q = world, 1
     NT = (N + nb - 1) // nb
-    lm = sum(1 for g in range(NT) if g % P == rank)
-    storeA = torch.empty((NT, lm, nb, nb), dtype=torch.float64, device="cuda")
-    storeT = torch.zeros((NT, lm, nb, nb), dtype=torch.float64, device="cuda")
-    A = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=1, device=gpu, ptr=storeA.data_ptr())
-    T = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=1, device=gpu, ptr=storeT.data_ptr())
+    myrow, mycol = rank // Q, rank % Q
+    lm = sum(1 for g in range(NT) if g % P == myrow)
+    ln = sum(1 for g in range(NT) if g % Q == mycol)
+    storeA = torch.empty((ln, lm, nb, nb), dtype=torch.float64, device="cuda")
+    storeT = torch.zeros((ln, lm, nb, nb), dtype=torch.float64, device="cuda")
+    A = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=Q, device=gpu, ptr=storeA.data_ptr())
+    T = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=Q, device=gpu, ptr=storeT.data_ptr())
     g = torch.Generator(device="cuda").manual_seed(1234 + rank)
     storeA.copy_(torch.rand(storeA.shape, dtype=torch.float64, device="cuda", generator=g) - 0.5)
     backup = storeA.clone()
@@ -113,7 +124,7 @@ def bench_qr(args):
     out = {"metric": "GFLOP/s tiled DGEQRF (PTG, HBM-resident)", "value": round(4.0 / 3.0 * N ** 3 / dt / 1e9, 1), "unit": "GFLOP/s",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
            "dtype": "fp64", "data": "synthetic uniform(-0.5, 0.5)", "config": {"model": "tiled DGEQRF", "N": N, "nb": nb, "ib": args.ib,
-                                                                             "parallelism": f"1D row-cyclic P{P}x1"}}
+                                                                             "parallelism": f"2D block-cyclic P{P}xQ{Q}" if Q > 1 else f"1D row-cyclic P{P}x1"}}
     if check is not None:
         out["residual_RtR_vs_AtA"] = check
     if world > 1:
@@ -186,6 +197,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cores", type=int, default=4)
+    ap.add_argument("--qr-grid", choices=["1d", "2d"], default="2d", help="qr: process grid over the ranks")
     ap.add_argument("--check", action="store_true", help="qr: verify R (||R^T R - A^T A|| / ||A^T A||) after the timed steps")
     args = ap.parse_args()
     if args.n is None:
