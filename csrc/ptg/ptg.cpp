@@ -1,5 +1,7 @@
 #include "ptg.hpp"
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -664,6 +666,25 @@ int PtgTaskClass::complete_execution(ExecutionStream* es, Task* t) const {
   return 0;
 }
 
+// Symbol lookup for BODY dyld=: the process first, then the libraries named
+// by MCA device_dyld_libs (colon separated, e.g. librocblas.so).
+void* dyld_lookup(const std::string& sym) {
+  if (void* p = dlsym(RTLD_DEFAULT, sym.c_str())) return p;
+  const std::string libs = ParamRegistry::instance().reg_string("device", "", "dyld_libs", "Libraries searched for BODY dyld= symbols (colon separated)",
+                                                                "librocblas.so:libhipblas.so:libm.so.6");
+  size_t b = 0;
+  while (b <= libs.size()) {
+    size_t e = libs.find(':', b);
+    if (e == std::string::npos) e = libs.size();
+    const std::string lib = libs.substr(b, e - b);
+    if (!lib.empty())
+      if (void* h = dlopen(lib.c_str(), RTLD_LAZY | RTLD_GLOBAL))
+        if (void* p = dlsym(h, sym.c_str())) return p;
+    b = e + 1;
+  }
+  return nullptr;
+}
+
 // ================================================================ taskpool
 PtgTaskpool::PtgTaskpool() { taskpool_name = "ptg"; }
 
@@ -735,6 +756,16 @@ void PtgTaskpool::finalize() {
       ch.evaluate = b.evaluate;
       ch.weight = b.weight;
       ch.dyld = b.dyld;
+      if (!ch.dyld.empty()) {
+        // BODY dyld=<symbol> (reference device.c:800-841): resolve the library
+        // function the body calls through parsec_body.dyld_fn; a chore whose
+        // symbol cannot be found is skipped (the next BODY runs instead)
+        ch.dyld_fn = dyld_lookup(ch.dyld);
+        if (!ch.dyld_fn) {
+          warning("%s: dyld symbol '%s' not found; this BODY is disabled", d.name.c_str(), ch.dyld.c_str());
+          ch.evaluate = [](const Task*) { return (int)HOOK_NEXT; };
+        }
+      }
       ch.stage_in = b.stage_in;
       ch.stage_out = b.stage_out;
       ch.flow_size = b.flow_size;

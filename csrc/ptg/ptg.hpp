@@ -265,6 +265,9 @@ class PtgTaskpool : public Taskpool {
   Task* with_pending(PtgTaskClass* tc, const int32_t* L, uint64_t key, F&& f);
 };
 
+// Address of a BODY dyld= symbol (process, then MCA device_dyld_libs); nullptr if absent.
+void* dyld_lookup(const std::string& sym);
+
 // Enumerate the execution space of `tc` (all locals), calling f(L).
 void for_each_task(const Taskpool* tp, const PtgTaskClass* tc, const std::function<void(const int32_t*)>& f);
 

@@ -143,7 +143,7 @@ def generate():
         lines.append(f"build {obj}: hipcc {os.path.join(ROOT, src)}")
         objs.append(obj)
     lib = os.path.join(PKG, "lib", "libparsec_amd.so")
-    libs = f"-L{ROCM}/lib -lamdhip64 -lrccl -latomic -lpthread -lrt -Wl,-rpath,{ROCM}/lib"
+    libs = f"-L{ROCM}/lib -lamdhip64 -lrccl -latomic -lpthread -lrt -ldl -Wl,-rpath,{ROCM}/lib"
     lines.append(f"build {lib}: solink {' '.join(objs)}")
     lines.append(f"  libs = {libs}")
     pyobjs = []

@@ -949,7 +949,13 @@ struct Gen {
       if (gpu) c << "  [[maybe_unused]] void* " << fl.name << " = __ctx->ptr(" << k << ");\n";
       else c << "  [[maybe_unused]] void* " << fl.name << " = parsec::ptg::flow_ptr(this_task, " << k << ");\n";
     }
-    if (gpu) c << "  [[maybe_unused]] parsec::ptg::GpuBody parsec_body{__ctx->stream, __ctx};\n";
+    // parsec_body: stream / context of a GPU body, and the resolved BODY dyld=
+    // symbol typed by dyldtype= (reference jdf2c.c parsec_body.dyld_fn)
+    const Prop* dyt = find_prop(b.props, "dyldtype");
+    const std::string fnty = dyt ? dyt->val : "void*";
+    const std::string dyld_expr = "(" + fnty + ")this_task->task_class->chores[this_task->chore_id].dyld_fn";
+    if (gpu) c << "  [[maybe_unused]] struct { hipStream_t stream; parsec::GpuExecContext* ctx; " << fnty << " dyld_fn; } parsec_body{__ctx->stream, __ctx, " << dyld_expr << "};\n";
+    else c << "  [[maybe_unused]] struct { " << fnty << " dyld_fn; } parsec_body{" << dyld_expr << "};\n";
     if (!g_noline) c << "#line " << b.line + 1 << " \"" << g_file << "\"\n";
     c << "  {" << b.code << "}\n";
     c << "  return PARSEC_HOOK_RETURN_DONE;\n}\n\n";
