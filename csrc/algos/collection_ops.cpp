@@ -250,13 +250,7 @@ int redistribute(Context* ctx, TiledMatrix* src, TiledMatrix* dst, int64_t size_
 
 // ------------------------------------------------------------------ dgemm
 static void cpu_gemm(int m, int n, int k, double alpha, const double* A, int lda, const double* B, int ldb, bool transB, double beta, double* C, int ldc) {
-  for (int j = 0; j < n; ++j) {
-    for (int i = 0; i < m; ++i) C[i + (size_t)j * ldc] *= beta;
-    for (int p = 0; p < k; ++p) {
-      const double b = alpha * (transB ? B[j + (size_t)p * ldb] : B[p + (size_t)j * ldb]);
-      for (int i = 0; i < m; ++i) C[i + (size_t)j * ldc] += A[i + (size_t)p * lda] * b;
-    }
-  }
+  host_dgemm(m, n, k, alpha, A, lda, B, ldb, transB, beta, C, ldc);
 }
 
 ptg::PtgTaskpool* dgemm_new(double alpha, TiledMatrix* A, TiledMatrix* B, double beta, TiledMatrix* C, int transB) {

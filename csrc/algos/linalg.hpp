@@ -38,6 +38,8 @@ ptg::PtgTaskpool* broadcast_new(TiledMatrix* A, int64_t root_m, int64_t root_n, 
 int redistribute(Context* ctx, TiledMatrix* src, TiledMatrix* dst, int64_t size_row, int64_t size_col, int64_t disi_src, int64_t disj_src, int64_t disi_dst,
                  int64_t disj_dst);
 // Tiled C = alpha A B + beta C inserted as DTD tasks (blocking).
+// Host DGEMM for CPU bodies (packed panels, AVX2/FMA micro-kernel; host_gemm.cpp)
+void host_dgemm(int m, int n, int k, double alpha, const double* A, int lda, const double* B, int ldb, bool transB, double beta, double* C, int ldc);
 int dtd_dgemm(Context* ctx, double alpha, TiledMatrix* A, TiledMatrix* B, double beta, TiledMatrix* C, bool use_gpu);
 
 }  // namespace algos

@@ -46,6 +46,7 @@ CORE_SOURCES = [
     "csrc/algos/dgeqrf.cpp",
     "csrc/algos/stencil3d.cpp",
     "csrc/algos/collection_ops.cpp",
+    "csrc/algos/host_gemm.cpp",
     "csrc/algos/dtd_builtins.cpp",
     "csrc/capi/capi.cpp",
     "csrc/algos/dpotrf_jdf.cpp",
