@@ -28,7 +28,7 @@ static size_t g_short_limit = 1024;
 static bool g_recv_from_cache = true;
 static int g_recv_pool = 1;  // 0 free after use, 1 recycle by size, 2 never reuse (diagnostic)
 static int g_ipc_debug_sync = 0;
-static int g_eager_ipc = 1;  // comm_eager_ipc: IPC descriptors ride in the activation (no GET round trip)  // 1: sender hipDeviceSynchronize before answering a GET (diagnostic)
+static int g_eager_ipc = 0;  // comm_eager_ipc: IPC descriptors ride in the activation (no GET round trip)  // 1: sender hipDeviceSynchronize before answering a GET (diagnostic)
 static int g_ipc_verify = 0;      // diagnostic: checksum every IPC payload at the sender and after the pull
 
 CommEngine* comm_engine() { return g_ce; }
@@ -422,8 +422,17 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
         }
     const uint64_t sid = r->hdr.send_id;
     const uint32_t gm_left = get_mask;
+    // the pulls run on the comm thread (copy queues are its own); a replayed
+    // parked activation arrives here on the thread that added the taskpool
     for (int f = 0; f < nflows; ++f)
-      if (ipc_mask & (1u << f)) pull_ipc(src, r, (uint32_t)f, ipc[f].handle, ipc[f].offset, sid, 0);
+      if (ipc_mask & (1u << f)) {
+        if (g_ce->on_comm_thread()) {
+          pull_ipc(src, r, (uint32_t)f, ipc[f].handle, ipc[f].offset, sid, 0);
+        } else {
+          IpcDesc d = ipc[f];
+          g_ce->post([src, r, f, d, sid] { pull_ipc(src, r, (uint32_t)f, d.handle, d.offset, sid, 0); });
+        }
+      }
     if (!gm_left) return;
   }
   // post the device receives before asking, in flow order (FIFO-matched by RCCL)
@@ -746,7 +755,7 @@ void remote_dep_init(Context* ctx) {
   g_recv_pool = (int)ParamRegistry::instance().reg_int("comm", "", "recv_pool", "Device receive buffers: 1 recycle by size, 0 free after use, 2 never reuse (diagnostic)", 1);
   g_ipc_debug_sync = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_debug_sync", "Diagnostic: device-synchronize before exporting a tile to a peer", 0);
   g_ipc_verify = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_verify", "Diagnostic: checksum IPC payloads at the sender and after the pull", 0);
-  g_eager_ipc = (int)ParamRegistry::instance().reg_int("comm", "", "eager_ipc", "Send the IPC descriptor of device flows with the activation (receiver pulls without a GET round trip)", 1);
+  g_eager_ipc = (int)ParamRegistry::instance().reg_int("comm", "", "eager_ipc", "Send the IPC descriptor of device flows with the activation (receiver pulls without a GET round trip; off: A/B on shared-GPU ranks inconclusive, profiles/r2_eager_ipc_ab.log)", 0);
   g_recv_from_cache = ParamRegistry::instance().reg_int("comm", "", "recv_from_cache", "Carve device receive buffers from the GPU tile-cache zone (1) or hipMalloc them (0)", 1) != 0;
   ctx->my_rank = comm_rank();
   ctx->nb_nodes = comm_size();

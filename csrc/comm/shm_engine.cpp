@@ -537,6 +537,8 @@ int ShmEngine::ipc_export(const void* ptr, void* handle64, uint64_t* offset) {
   // cannot map at the right offset: such tiles travel through host fragments
   static const size_t min_bytes = ParamRegistry::instance().reg_sizet("comm", "", "ipc_min_alloc", "Smallest device allocation exported through HIP IPC (smaller ones are host-staged)", (size_t)2 << 20);
   if (size < min_bytes) return -3;
+  // called by workers (activations with eager IPC descriptors) and the comm thread
+  std::lock_guard<std::mutex> g(ipc_m_);
   auto key = std::make_pair((uintptr_t)base, size);
   auto it = ipc_exported_.find(key);
   if (it == ipc_exported_.end()) {
@@ -554,6 +556,7 @@ int ShmEngine::ipc_export(const void* ptr, void* handle64, uint64_t* offset) {
 }
 
 void* ShmEngine::ipc_open(int src, const void* handle64) {
+  std::lock_guard<std::mutex> g(ipc_m_);
   std::string k((const char*)handle64, 64);
   auto key = std::make_pair(src, k);
   auto it = ipc_opened_.find(key);

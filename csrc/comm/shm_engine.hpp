@@ -133,6 +133,7 @@ class ShmEngine : public CommEngine {
   std::vector<hipStream_t> ipc_stream_;
   std::vector<std::deque<Xfer>> ipc_q_;
   std::map<std::pair<uintptr_t, size_t>, std::array<char, 64>> ipc_exported_;  // (base, size) -> handle
+  std::mutex ipc_m_;  // ipc_exported_ / ipc_opened_ (exports happen on worker threads too)
   std::map<std::pair<int, std::string>, void*> ipc_opened_;                    // (src, handle) -> base
   int init_ipc();
   // RCCL
