@@ -27,8 +27,8 @@ static ExecutionStream* g_comm_es = nullptr;
 static size_t g_short_limit = 1024;
 static bool g_recv_from_cache = true;
 static int g_recv_pool = 1;  // 0 free after use, 1 recycle by size, 2 never reuse (diagnostic)
-static int g_ipc_debug_sync = 0;
-static int g_eager_ipc = 0;  // comm_eager_ipc: IPC descriptors ride in the activation (no GET round trip)  // 1: sender hipDeviceSynchronize before answering a GET (diagnostic)
+static int g_ipc_debug_sync = 0;  // 1: sender hipDeviceSynchronize before answering a GET (diagnostic)
+static int g_eager_ipc = 0;  // comm_eager_ipc: IPC descriptors ride in the activation (no GET round trip)
 static int g_ipc_verify = 0;      // diagnostic: checksum every IPC payload at the sender and after the pull
 
 CommEngine* comm_engine() { return g_ce; }
