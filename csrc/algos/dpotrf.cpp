@@ -77,6 +77,10 @@ static void cpu_inverse(const double* L, int ldl, double* W, int n) {
 }
 // C (m x n) += alpha A B^T (lower_only: i >= j)
 static void cpu_gemm_nt(double alpha, const double* A, int lda, const double* B, int ldb, double* C, int ldc, int m, int n, int k, bool lower) {
+  if (!lower) {  // full tile update: the packed host GEMM
+    host_dgemm(m, n, k, alpha, A, lda, B, ldb, true, 1.0, C, ldc);
+    return;
+  }
   for (int j = 0; j < n; ++j)
     for (int p = 0; p < k; ++p) {
       double b = alpha * B[j + (size_t)p * ldb];
