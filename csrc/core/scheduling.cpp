@@ -150,6 +150,25 @@ int schedule_tasks(ExecutionStream* es, Task** tasks, int n, int32_t distance) {
     es = ctx->all_es[rr.fetch_add(1, std::memory_order_relaxed) % ctx->all_es.size()];
     distance = std::max(distance, 1);
   }
+  // TC_IMMEDIATE classes (reference PARSEC_IMMEDIATE_TASK): run on the
+  // releasing compute thread right away instead of going through a queue
+  // (bounded nesting: deeper releases are queued normally)
+  static thread_local int t_immediate_depth = 0;
+  if (!es->is_manager && my_execution_stream() == es && t_immediate_depth < 8) {
+    int kept = 0;
+    for (int i = 0; i < n; ++i) {
+      Task* t = tasks[i];
+      if (t->task_class->flags & TC_IMMEDIATE) {
+        ++t_immediate_depth;
+        task_progress(es, t, 0);
+        --t_immediate_depth;
+      } else {
+        tasks[kept++] = t;
+      }
+    }
+    n = kept;
+    if (n == 0) return 0;
+  }
   if (n > 1) std::stable_sort(tasks, tasks + n, [](const Task* a, const Task* b) { return a->priority > b->priority; });
   return schedule_sorted(es, tasks, n, distance);
 }

@@ -708,6 +708,15 @@ void DtdTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& ac
   task_unref(t);  // this activation's guard
 }
 
+uint32_t DtdTaskClass::gpu_pushout_mask(const Task* tt, int device) const {
+  (void)device;
+  auto* t = static_cast<const DtdTask*>(tt);
+  uint32_t m = 0;
+  for (const Arg& a : t->args)
+    if (a.flow >= 0 && (a.op & PUSHOUT) && (a.op & OP_MASK) != INPUT) m |= 1u << a.flow;
+  return m;
+}
+
 // ============================================================ accessors
 void* task_arg(const Task* tt, int i) {
   auto* t = static_cast<const DtdTask*>(tt);

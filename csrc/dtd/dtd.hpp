@@ -95,6 +95,8 @@ class DtdTaskClass : public TaskClass {
   void release_task(ExecutionStream* es, Task* t) const override;
   std::string describe(const Task* t) const override;
   void iterate_successors(ExecutionStream* es, const Task* t, uint32_t mask, const DepVisitor& v) const override;
+  // flows inserted with PUSHOUT: copied back to the host when a GPU chore ran
+  uint32_t gpu_pushout_mask(const Task* t, int device) const override;
 };
 
 class DtdTaskpool : public Taskpool {

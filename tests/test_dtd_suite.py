@@ -203,3 +203,33 @@ def test_explicit_task_class(pa):
     assert int(A.tile(0, 0)[0, 0]) == 55
     assert tc.name == "axpy" and tc.nb_flows == 1
     ctx.fini()
+
+
+@pytest.mark.gpu
+def test_pushout_flow_returns_home_after_gpu_task(pa):
+    """DTD PUSHOUT (reference PARSEC_PUSHOUT): a flow written by a GPU chore is
+    copied back to the host when the task completes (device bytes_out grows by
+    the tile size before any flush), without the flag it stays on the GPU."""
+    ctx = pa.init(2)
+    if pa.first_gpu_device_index() < 0:
+        pytest.skip("no GPU")
+    A = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, 256, 256, 512, 256)
+    tp = pa.dtd_taskpool(ctx)
+    ctx.start()
+    gpu = [d for d in pa.devices() if d["type"] == pa.DEV_HIP][0]
+    bytes_tile = 256 * 256 * 8
+    t0 = tp.tile_of(A, A.data_key([0, 0]))
+    t1 = tp.tile_of(A, A.data_key([1, 0]))
+    out0 = gpu["bytes_out"]
+    pa.insert_task(tp, None, [(t0, pa.INOUT), (bytes_tile, pa.VALUE, 8), (0, pa.VALUE)], name="memset_plain", gpu="memset")
+    tp.wait()
+    out1 = [d for d in pa.devices() if d["type"] == pa.DEV_HIP][0]["bytes_out"]
+    pa.insert_task(tp, None, [(t1, pa.INOUT | pa.PUSHOUT), (bytes_tile, pa.VALUE, 8), (0, pa.VALUE)], name="memset_push", gpu="memset")
+    tp.wait()
+    out2 = [d for d in pa.devices() if d["type"] == pa.DEV_HIP][0]["bytes_out"]
+    tp.data_flush_all(A)
+    ctx.wait()
+    assert out1 - out0 < bytes_tile
+    assert out2 - out1 >= bytes_tile
+    assert float(abs(A.tile(1, 0)).max()) == 0.0
+    ctx.fini()

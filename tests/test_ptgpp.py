@@ -39,6 +39,7 @@ def _run(exe, timeout=60, env=None):
     ("merge_sort", "merge_sort L=5 B=97 merges 31 bad 0"),
     ("stencil_1d", "stencil_1d rank 0 tiles 6 err 0.000e+00"),
     ("dyld", "dyld lib 6 fallback 6 bad 0"),
+    ("immediate", "immediate ran 64 same_thread 64"),
 ])
 def test_jdf_program(tmp_path, name, expect):
     exe = ptgpp.build_program(os.path.join(JDF, name + ".jdf"), str(tmp_path))
