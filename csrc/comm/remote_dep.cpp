@@ -797,9 +797,23 @@ void remote_dep_fini(Context* ctx) {
   if (g_ctx == ctx) g_ctx = nullptr;
 }
 
-void remote_dep_on(Context* ctx) { (void)ctx; }
-void remote_dep_off(Context* ctx) { (void)ctx; }
-void remote_dep_progress_inline(Context* ctx) { (void)ctx; }
+// The context runs taskpools between on and off (reference remote_dep_on /
+// remote_dep_off around the comm thread's active phase): the comm thread polls
+// for latency while on and naps while off.
+void remote_dep_on(Context* ctx) {
+  (void)ctx;
+  if (g_ce) g_ce->set_active(true);
+}
+void remote_dep_off(Context* ctx) {
+  (void)ctx;
+  if (g_ce) g_ce->set_active(false);
+}
+// Progress from the calling thread when no comm thread runs (never concurrent
+// with it: progress() is single-threaded).
+void remote_dep_progress_inline(Context* ctx) {
+  (void)ctx;
+  if (g_ce && !g_ce->thread_running()) g_ce->progress();
+}
 
 void remote_dep_new_taskpool(Context* ctx, Taskpool* tp) {
   (void)ctx;

@@ -467,6 +467,7 @@ void ShmEngine::thread_main() {
     if (progress()) { last = now_ns(); continue; }
     if ((++spins & 63) != 0) { PARSEC_CPU_RELAX(); continue; }
     const uint64_t quiet = now_ns() - last;
+    if (!active_.load(std::memory_order_relaxed) && quiet > 200000) { std::this_thread::sleep_for(std::chrono::microseconds(50)); continue; }
     if (quiet < 200000) PARSEC_CPU_RELAX();
     else if (quiet < 2000000) std::this_thread::yield();
     else std::this_thread::sleep_for(std::chrono::microseconds(20));

@@ -50,6 +50,10 @@ class ShmEngine : public CommEngine {
   uint64_t allreduce_max(uint64_t v) override;
   void post(std::function<void()> fn);  // run on the comm thread
   bool on_comm_thread() const { return std::this_thread::get_id() == thread_id_; }
+  // remote_dep_on / off: a context is running taskpools (poll for latency) or
+  // idle (the comm thread only naps between polls)
+  void set_active(bool on) { active_.store(on, std::memory_order_relaxed); }
+  bool thread_running() const { return thread_.joinable(); }
   size_t max_fragment() const { return ring_bytes_ / 4; }
   // Device data planes (comm thread only). IPC: the sender exports the tile's
   // allocation (hipIpcGetMemHandle), the receiver maps it once and pulls the
@@ -119,6 +123,7 @@ class ShmEngine : public CommEngine {
   std::atomic<int> posted_n_{0};
   std::thread thread_;
   std::thread::id thread_id_;
+  std::atomic<bool> active_{true};
   std::atomic<bool> stop_{false};
   // barrier / allreduce state
   std::mutex coll_m_;
