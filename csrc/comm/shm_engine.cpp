@@ -463,7 +463,10 @@ void ShmEngine::thread_main() {
   // after that, and only sleep once the engine has been quiet for 2 ms.
   uint64_t last = now_ns();
   uint32_t spins = 0;
+  // test hook: a slow receiver (every pass naps), so senders build backlogs
+  const int64_t debug_delay = ParamRegistry::instance().reg_int("comm", "shm", "debug_delay_us", "Diagnostic: nap this long after every progress pass of the comm thread", 0);
   while (!stop_.load(std::memory_order_relaxed)) {
+    if (debug_delay > 0) std::this_thread::sleep_for(std::chrono::microseconds(debug_delay));
     if (progress()) { last = now_ns(); continue; }
     if ((++spins & 63) != 0) { PARSEC_CPU_RELAX(); continue; }
     const uint64_t quiet = now_ns() - last;

@@ -58,12 +58,13 @@ def test_distributed_dpotrf_jdf(pa, nranks, P, Q, mode):
 
 @pytest.mark.parametrize("aggregate", ["1", "0"])
 def test_distributed_backpressure_aggregation(pa, aggregate):
-    """Tiny shared-memory rings force activations into the per-peer priority
-    backlog; with runtime_comm_aggregate they leave packed in one message
+    """Tiny shared-memory rings and a slow receiver (comm_shm_debug_delay_us)
+    force activations into the per-peer priority backlog; with runtime_comm_aggregate they leave packed in one message
     (reference remote_dep_mpi.c:1089-1139, runtime_comm_aggregate). The
     factorization stays exact either way."""
     outs = run_ranks(4, 256, 8, 2, 2, "lfq", "star", "local",
                      env_extra={"PARSEC_MCA_comm_shm_ring_bytes": "8192", "PARSEC_MCA_runtime_comm_aggregate": aggregate,
+                                "PARSEC_MCA_comm_shm_debug_delay_us": "300",
                                 "DIST_PRINT_COMM_STATS": "1"})
     stats = []
     for rc, out in outs:
