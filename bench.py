@@ -3,7 +3,8 @@
 resident in HBM, one process per MI355X, PTG taskpool, batched MFMA tile kernels.
 
 Metric (BASELINE.json): GFLOP/s (whole node) tiled DPOTRF 2D block-cyclic at
-1/2/4/8 MI355X. Default config = BASELINE config 3 (N=65536, nb=1024), the
+1/2/4/8 MI355X. The taskpool is the one parsec-ptgpp compiles from
+csrc/algos/jdf/dpotrf_L.jdf. Default config = BASELINE config 3 (N=65536, nb=1024), the
 same problem at every GPU count (strong scaling). `--n 16384 --nb 512`
 reproduces config 2 (1 GPU).
 
@@ -100,8 +101,8 @@ def main():
     ap.add_argument("--cores", type=int, default=int(os.environ.get("PARSEC_BENCH_CORES", "4")))
     ap.add_argument("--check", action="store_true", help="verify the factorization (small N only)")
     ap.add_argument("--mca", nargs=2, action="append", default=[])
-    ap.add_argument("--taskpool", choices=["ir", "jdf"], default="ir",
-                    help="ir: DAG built in C++ (csrc/algos/dpotrf.cpp); jdf: the same DAG compiled by parsec-ptgpp from csrc/algos/jdf/dpotrf_L.jdf")
+    ap.add_argument("--taskpool", choices=["ir", "jdf"], default="jdf",
+                    help="jdf (default): the DAG compiled by parsec-ptgpp from csrc/algos/jdf/dpotrf_L.jdf; ir: the same DAG built by hand in C++ (csrc/algos/dpotrf.cpp, a test fixture)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="validation mode: every rank uses GPU 0 (torch gloo, shm data plane instead of RCCL)")
     args = ap.parse_args()
@@ -270,7 +271,7 @@ def main():
             "dtype": "fp64",
             "data": "synthetic random symmetric + N*I (DPLASMA plgsy convention), HBM-resident tiles",
             "residual": float(f"{resid:.3e}"),
-            "config": {"model": "tiled DPOTRF lower (PTG)" if args.taskpool == "ir" else "tiled DPOTRF lower (PTG, ptgpp-compiled dpotrf_L.jdf)", "N": N, "nb": nb, "global_batch": 1, "seq_len": N,
+            "config": {"model": "tiled DPOTRF lower (PTG, ptgpp-compiled dpotrf_L.jdf)" if args.taskpool == "jdf" else "tiled DPOTRF lower (PTG, hand-built C++ DAG)", "N": N, "nb": nb, "global_batch": 1, "seq_len": N,
                        "parallelism": f"2D block-cyclic P{P}xQ{Q}, 1 process/GPU", "threads_per_rank": args.cores},
         }
         if check is not None:

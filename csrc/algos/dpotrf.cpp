@@ -102,15 +102,16 @@ class DpotrfTaskpool : public PtgTaskpool {
   void on_complete_internal() override {
     int v = info_cpu.load();
     if (info_dev) {
-      int dv = 0;
-      device_memcpy(0, &dv, info_dev_index, info_dev, sizeof(int));
+      const int dv = device_status_release(info_dev_index, info_dev);
+      info_dev = nullptr;
       if (dv && (!v || dv < v)) v = dv;
     }
     if (info_host) *info_host = v;
   }
   ~DpotrfTaskpool() override {
-    if (info_dev) device_free(info_dev_index, info_dev);
-    if (invbuf) device_free(info_dev_index, invbuf);
+    if (info_dev) device_status_release(info_dev_index, info_dev);
+    // the inverse blocks live in the tile-cache zone (no hipMalloc / hipFree per taskpool)
+    if (invbuf && !device_cache_free(info_dev_index, invbuf)) device_free(info_dev_index, invbuf);
   }
 };
 
@@ -122,10 +123,12 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
   if (info_host) *info_host = 0;
   int gpu = first_gpu_device_index();
   if (gpu >= 0) {
-    tp->info_dev = static_cast<int*>(device_alloc(gpu, sizeof(int)));
+    tp->info_dev = device_status_acquire(gpu);
     tp->info_dev_index = gpu;
     tp->inv_stride = (size_t)((A->nb + 63) / 64) * 4096;
-    tp->invbuf = static_cast<double*>(device_alloc(gpu, tp->inv_stride * A->nt * sizeof(double)));
+    const size_t inv_bytes = tp->inv_stride * A->nt * sizeof(double);
+    tp->invbuf = static_cast<double*>(device_cache_alloc(gpu, inv_bytes));
+    if (!tp->invbuf) tp->invbuf = static_cast<double*>(device_alloc(gpu, inv_bytes));
     tp->inv_ready.reset(new std::atomic<uint8_t>[A->nt]);
     for (int64_t i = 0; i < A->nt; ++i) tp->inv_ready[i].store(0);
   }

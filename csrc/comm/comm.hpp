@@ -41,6 +41,9 @@ struct CommEngine {
   virtual int progress() = 0;  // returns number of events handled
   virtual int sync() = 0;      // barrier
   virtual uint64_t allreduce_max(uint64_t v) = 0;
+  // Unmap every peer memory region opened by this engine (before the peers
+  // free them: a region still mapped elsewhere makes its owner's free block)
+  virtual void release_peer_mappings() {}
 };
 
 // Received data for one flow of a remote activation.

@@ -791,6 +791,11 @@ void remote_dep_fini(Context* ctx) {
     // nothing must be in flight when the context goes away
     g_ce->sync();
     PARSEC_DEBUG(kVerbDebug, "fini", "comm barrier passed");
+    // every rank unmaps its peers' tile memory before ANY rank frees its own
+    // (devices_fini): freeing a region another process still maps stalled the
+    // owner's hipFree for seconds (2-rank GPU runs, round 2)
+    g_ce->release_peer_mappings();
+    g_ce->sync();
     g_ce->post([] { set_my_execution_stream(nullptr); });
   }
   g_comm_es = nullptr;

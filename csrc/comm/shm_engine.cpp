@@ -94,7 +94,7 @@ ShmEngine::~ShmEngine() {
   stop_thread();
   for (auto& kv : ipc_opened_) (void)hipIpcCloseMemHandle(kv.second);
   ipc_opened_.clear();
-  for (auto st : ipc_stream_) if (st) (void)hipStreamDestroy(st);
+  ipc_stream_.clear();  // the shared copy stream outlives the engine
   for (int r = 0; r < size; ++r)
     if (maps_[r]) munmap(maps_[r], map_len_[r]);
   shm_unlink(seg_name(job_, rank).c_str());
@@ -292,8 +292,15 @@ int ShmEngine::send_am_prio(int tag, int dst, const void* hdr, size_t hlen, cons
   if (dst == rank) return send_am2(tag, dst, hdr, hlen, payload, plen);
   Out& o = *out_[dst];
   std::lock_guard<std::mutex> g(o.m);
-  // straight into the ring when nothing of this class waits for the peer
-  if (o.prio.empty() && ring_write(out_ring(dst), hdr, hlen, payload, plen, tag, rank)) {
+  // straight into the ring only when NOTHING waits for the peer: an activation
+  // never overtakes a control message (GET / fragment / termdet / barrier) that
+  // was backlogged before it. The converse can happen and is allowed: drain_peer
+  // sends the FIFO backlog before queued activations, so a later control message
+  // may overtake a queued activation. Every protocol tolerates that: GETs and
+  // fragments answer activations already delivered, the four-counter waves
+  // re-check counters until they balance, and the fini barrier runs after the
+  // last activation was delivered.
+  if (o.prio.empty() && o.backlog.empty() && ring_write(out_ring(dst), hdr, hlen, payload, plen, tag, rank)) {
     stats.direct.fetch_add(1, std::memory_order_relaxed);
     return 0;
   }
@@ -523,13 +530,12 @@ int ShmEngine::init_ipc() {
   if (hipSetDevice(gpu_) != hipSuccess) return -1;
   ipc_stream_.assign(size, nullptr);
   ipc_q_.resize(size);
-  int lo = 0, hi = 0;
-  (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-  for (int r = 0; r < size; ++r) {
-    if (r == rank) continue;
-    // high priority: a pulled tile usually feeds the critical path (panel broadcast)
-    if (hipStreamCreateWithPriority(&ipc_stream_[r], hipStreamNonBlocking, hi) != hipSuccess) return -2;
-  }
+  // every pull rides the GPU's one (high-priority) copy stream, shared with the
+  // device engine's transfers: no per-peer streams beyond the 4 hardware queues
+  hipStream_t st = gpu_copy_stream(gpu_);
+  if (!st) return -2;
+  for (int r = 0; r < size; ++r)
+    if (r != rank) ipc_stream_[r] = st;
   return 0;
 }
 
@@ -572,6 +578,12 @@ void* ShmEngine::ipc_open(int src, const void* handle64) {
   if (e != hipSuccess) fatal("hipIpcOpenMemHandle (from rank %d) failed: %s", src, hipGetErrorString(e));
   ipc_opened_[key] = p;
   return p;
+}
+
+void ShmEngine::release_peer_mappings() {
+  std::lock_guard<std::mutex> g(ipc_m_);
+  for (auto& kv : ipc_opened_) (void)hipIpcCloseMemHandle(kv.second);
+  ipc_opened_.clear();
 }
 
 int ShmEngine::ipc_copy(int src_rank, void* dst, const void* src, size_t bytes, std::function<void()> done) {

@@ -48,6 +48,7 @@ class ShmEngine : public CommEngine {
   int progress() override;
   int sync() override;
   uint64_t allreduce_max(uint64_t v) override;
+  void release_peer_mappings() override;
   void post(std::function<void()> fn);  // run on the comm thread
   bool on_comm_thread() const { return std::this_thread::get_id() == thread_id_; }
   // remote_dep_on / off: a context is running taskpools (poll for latency) or

@@ -143,6 +143,9 @@ struct DataCopy : ListItem {  // ListItem: membership in a device LRU
   std::shared_ptr<DatacopyFuture> reshape_future;
   uint32_t reshape_version = 0;
   const void* reshape_owner = nullptr;  // taskpool whose arenas produced the views
+  // set once a view exists: CPU-only runs bump `version` of such copies when a
+  // task writes them in place, so a later reshaped read gets a fresh view
+  std::atomic<bool> has_reshape_view{false};
   void* ptr() const { return device_private; }
 };
 

@@ -210,7 +210,17 @@ int execute_task(ExecutionStream* es, Task* t) {
           dev->stats.executed_tasks.fetch_add(1, std::memory_order_relaxed);
         }
         ++es->nb_executed;
-        if (gpus) cpu_write_epilog(t);
+        if (gpus) {
+          cpu_write_epilog(t);
+        } else {
+          // CPU-only: versions only matter to cached reshape views (ptg.cpp
+          // reshape_future_of); an in-place write makes them stale
+          for (auto& f : tc->flows) {
+            if (!(f.access & FLOW_WRITE)) continue;
+            DataCopy* c = t->data[f.index].data_in;
+            if (c && c->has_reshape_view.load(std::memory_order_acquire)) __atomic_add_fetch(&c->version, 1, __ATOMIC_ACQ_REL);
+          }
+        }
       }
     }
     if (rc == HOOK_NEXT) { t->chore_mask &= ~(1u << i); continue; }

@@ -30,6 +30,12 @@ int gpu_chore_dispatch(ExecutionStream* es, Task* t, int chore);
 // Raw device memory helpers (outside the engine's tile cache).
 void* device_alloc(int device_index, size_t bytes);
 void device_free(int device_index, void* p);
+// Device-resident status words (LAPACK info of a factorization taskpool): a
+// per-GPU pool allocated once, so building a taskpool costs no hipMalloc /
+// hipMemset / hipFree (each of which synchronises the device). A slot is zero
+// when acquired; release reads its final value (one 4-byte copy) and zeroes it.
+int* device_status_acquire(int device_index);
+int device_status_release(int device_index, int* slot);
 // Thread-safe allocation from a GPU's tile-cache zone (no eviction, no memset):
 // communication receive buffers. nullptr when the zone is full / no such GPU.
 void* device_cache_alloc(int device_index, size_t bytes);
@@ -42,6 +48,8 @@ int bind_thread_to_gpu_numa(int ordinal);
 // dst <- src (bytes) as a copy kernel on `stream` (hipStream_t); 0 on success.
 int device_copy_kernel(void* dst, const void* src, size_t bytes, void* stream);
 int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t bytes);
+// The process-wide copy stream of HIP device `ordinal` (created on first use).
+hipStream_t gpu_copy_stream(int ordinal);
 int device_hip_ordinal(int device_index);  // -1 if not a HIP device
 int first_gpu_device_index();
 // Bring the newest version of `d` to the host (device 0), synchronously.
@@ -151,6 +159,7 @@ struct KernelBatch {
   std::vector<QrPanelDesc> qr_panel;
   std::vector<QrApplyDesc> qr_apply;
   std::vector<std::function<void(hipStream_t)>> generic;  // other kernels, launched in order
+  bool critical = false;  // launched on the critical stream: waves at raised issue priority
   bool empty() const { return gemm.empty() && trsm.empty() && potrf.empty() && trsm_w.empty() && stencil.empty() && qr_panel.empty() && qr_apply.empty() && generic.empty(); }
   void clear() { gemm.clear(); trsm.clear(); potrf.clear(); trsm_w.clear(); stencil.clear(); qr_panel.clear(); qr_apply.clear(); generic.clear(); }
 };

@@ -102,6 +102,45 @@ void device_free(int device_index, void* p) {
   (void)hipFree(p);
 }
 
+namespace {
+struct StatusPool {
+  std::mutex m;
+  int* base = nullptr;
+  std::vector<int> free_slots;
+};
+constexpr int kStatusSlots = 4096;
+StatusPool g_status_pool[kMaxDevices];
+}  // namespace
+
+int* device_status_acquire(int device_index) {
+  if (device_index < 0 || device_index >= kMaxDevices) return nullptr;
+  StatusPool& sp = g_status_pool[device_index];
+  std::lock_guard<std::mutex> g(sp.m);
+  if (!sp.base) {
+    sp.base = static_cast<int*>(device_alloc(device_index, kStatusSlots * sizeof(int)));  // zeroed, once per process
+    if (!sp.base) return nullptr;
+    for (int i = kStatusSlots - 1; i >= 0; --i) sp.free_slots.push_back(i);
+  }
+  if (sp.free_slots.empty()) return nullptr;
+  const int i = sp.free_slots.back();
+  sp.free_slots.pop_back();
+  return sp.base + i;
+}
+
+int device_status_release(int device_index, int* slot) {
+  if (!slot || device_index < 0 || device_index >= kMaxDevices) return 0;
+  StatusPool& sp = g_status_pool[device_index];
+  int v = 0;
+  device_memcpy(0, &v, device_index, slot, sizeof(int));
+  if (v != 0) {
+    const int zero = 0;
+    device_memcpy(device_index, slot, 0, &zero, sizeof(int));
+  }
+  std::lock_guard<std::mutex> g(sp.m);
+  sp.free_slots.push_back((int)(slot - sp.base));
+  return v;
+}
+
 void* device_cache_alloc(int device_index, size_t bytes) {
   auto* d = dynamic_cast<HipDevice*>(DeviceRegistry::instance().get(device_index));
   if (!d) return nullptr;
@@ -168,40 +207,70 @@ int bind_thread_to_gpu_numa(int ordinal) {
   return node;
 }
 
+// One copy stream per GPU and process (GPU_MAX_HW_QUEUES is 4: a process owns
+// at most 4 hardware queues, so the runtime keeps its stream count to that):
+// critical + 2 bulk execution streams per device and THIS stream, shared by every
+// transfer of the runtime -- the engine's stage-in / write-back / prefetch, the
+// comm engine's IPC pulls and the blocking device_memcpy helper (SDMA engines do
+// the copies either way). Created on first use (the comm engine may need it
+// before the device engine starts) and kept for the life of the process.
+static std::mutex g_copy_stream_m;
+static hipStream_t g_copy_stream[64] = {};
+
+hipStream_t gpu_copy_stream(int ordinal) {
+  if (ordinal < 0 || ordinal >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(g_copy_stream_m);
+  if (!g_copy_stream[ordinal]) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(ordinal);
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    // high priority: stage-ins and pulled tiles usually feed the critical path
+    if (hipStreamCreateWithPriority(&g_copy_stream[ordinal], hipStreamNonBlocking, hi) != hipSuccess) {
+      (void)hipGetLastError();
+      g_copy_stream[ordinal] = nullptr;
+    }
+    (void)hipSetDevice(cur);
+  }
+  return g_copy_stream[ordinal];
+}
+
 // Blocking copy: returns once the bytes landed. hipMemcpy alone is NOT enough:
 // a device-to-device hipMemcpy may return before the copy ran (CUDA/HIP
 // semantics), and callers release or recycle the source right after (e.g. a
 // remote write-back from a pooled receive buffer, which the next receive then
-// overwrote: intermittent stale tiles in the 2-rank GPU QR). Each calling thread
-// copies on its own (blocking) stream and waits for it.
+// overwrote: intermittent stale tiles in the 2-rank GPU QR). The copy goes on the
+// device's copy stream, ordered after earlier work of the null stream (like
+// hipMemcpy: initialisation kernels / memsets launched there), and the caller
+// waits for an event behind it (not for the whole stream's later work).
 int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t bytes) {
   if (dst_dev == 0 && src_dev == 0) { std::memcpy(dst, src, bytes); return 0; }
   hipMemcpyKind k = dst_dev == 0 ? hipMemcpyDeviceToHost : src_dev == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
-  static const bool legacy = getenv("PARSEC_MEMCPY_LEGACY") != nullptr;  // A/B switch (debug)
-  if (legacy) return hipMemcpy(dst, src, bytes, k) == hipSuccess ? 0 : -1;
   const int dev = dst_dev != 0 ? dst_dev : src_dev;
   const int ord = device_hip_ordinal(dev);
-  thread_local hipStream_t s = nullptr;
-  thread_local int s_ord = -1;
-  if (ord >= 0 && (s == nullptr || s_ord != ord)) {
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    (void)hipSetDevice(ord);
-    if (s) (void)hipStreamDestroy(s);
-    // a BLOCKING stream: like hipMemcpy, the copy is ordered after earlier work
-    // of the null stream (initialisation kernels / memsets launched there)
-    if (hipStreamCreateWithFlags(&s, hipStreamDefault) != hipSuccess) s = nullptr;
-    s_ord = ord;
-    (void)hipSetDevice(cur);
-  }
-  hipError_t e;
-  if (s) {
-    e = hipMemcpyAsync(dst, src, bytes, k, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-  } else {
-    e = hipMemcpy(dst, src, bytes, k);
+  hipStream_t s = ord >= 0 ? gpu_copy_stream(ord) : nullptr;
+  if (!s) {
+    hipError_t e = hipMemcpy(dst, src, bytes, k);
     if (e == hipSuccess) e = hipDeviceSynchronize();
+    return e == hipSuccess ? 0 : -1;
   }
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (cur != ord) (void)hipSetDevice(ord);
+  thread_local hipEvent_t evs[64][2] = {};  // per calling thread and GPU (events belong to a device)
+  hipEvent_t& ev_null = evs[ord & 63][0];
+  hipEvent_t& ev_done = evs[ord & 63][1];
+  if (!ev_null) {
+    (void)hipEventCreateWithFlags(&ev_null, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&ev_done, hipEventDisableTiming);
+  }
+  hipError_t e = hipEventRecord(ev_null, nullptr);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, ev_null, 0);
+  if (e == hipSuccess) e = hipMemcpyAsync(dst, src, bytes, k, s);
+  if (e == hipSuccess) e = hipEventRecord(ev_done, s);
+  if (e == hipSuccess) e = hipEventSynchronize(ev_done);
+  if (cur != ord) (void)hipSetDevice(cur);
   return e == hipSuccess ? 0 : -1;
 }
 
@@ -218,7 +287,7 @@ void* GpuExecContext::info(int id) {
 }
 
 // ================================================================ device
-static int g_nb_exec_streams = 4;
+static int g_nb_exec_streams = 3;
 
 int HipDevice::attach(Context* c) {
   ctx = c;
@@ -237,33 +306,45 @@ void HipDevice::start(Context* c) {
   PARSEC_HIP_CHECK(hipSetDevice(ordinal));
   int lo = 0, hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-  PARSEC_HIP_CHECK(hipStreamCreateWithFlags(&s_h2d, hipStreamNonBlocking));
-  PARSEC_HIP_CHECK(hipStreamCreateWithFlags(&s_d2h, hipStreamNonBlocking));
-  // streams [0, nb_exec_streams): critical / high-priority / bulk; then
-  // extra_crit_streams more critical streams, so independent critical-path
-  // batches (e.g. the panels of different QR steps) are not serialised
-  const int total_streams = nb_exec_streams + (nb_exec_streams >= 3 ? extra_crit_streams : 0);
-  s_exec.resize(total_streams);
-  // Stream 0 carries the critical path (POTRF / next panel). With >= 3 streams it
-  // gets a few CUs of its own so its small latency-bound kernels never queue behind
-  // (or share CUs with) the bulk GEMM batches, which run on the remaining CUs.
+  s_copy = gpu_copy_stream(ordinal);
+  if (!s_copy) fatal("hip%d: cannot create the copy stream", ordinal);
+  const int total_streams = std::max(1, nb_exec_streams);
+  s_exec.assign(total_streams, nullptr);
+  // Stream 0 carries the critical path at high priority. A critical kernel that
+  // shares a CU with bulk GEMM workgroups gets a third of its MFMA pipe and waits
+  // behind their LDS / VALU traffic: a 20 us tile-POTRF step ran 50-200 us beside
+  // the 16k bulk updates (profiles/r3_contended_potrf_steps.txt). With
+  // reserved_cus > 0 the CUs are partitioned: the critical stream runs on the
+  // reserved ones only and the bulk streams on the rest (CU masks).
   const int ncu = props.multiProcessorCount > 0 ? props.multiProcessorCount : 256;
-  int reserve = nb_exec_streams >= 3 ? reserved_cus : 0;
+  int reserve = total_streams >= 2 ? reserved_cus : 0;
   if (reserve >= ncu) reserve = 0;
   bool masked = false;
   if (reserve > 0) {
-    std::vector<uint32_t> crit((ncu + 31) / 32, 0u), bulk((ncu + 31) / 32, 0u);
-    // spread the reserved CUs over the XCDs (CU ids are dealt round-robin to them)
-    for (int cu = 0; cu < ncu; ++cu) (cu < reserve ? crit : bulk)[cu / 32] |= 1u << (cu % 32);
+    std::vector<uint32_t> bulk((ncu + 31) / 32, ~0u), crit((ncu + 31) / 32, 0u);
+    if (ncu % 32) bulk.back() = (1u << (ncu % 32)) - 1;
+    // reserved CU ids: 0, stride, 2 stride, ... (wrapping to the next offset):
+    // the stride decides how they spread over the XCDs (reserved_cus_stride)
+    const int stride = std::max(1, reserved_stride);
+    for (int i = 0; i < reserve; ++i) {
+      const int cu = (i * stride) % ncu + (i * stride) / ncu;
+      if (cu >= ncu) continue;
+      bulk[cu / 32] &= ~(1u << (cu % 32));
+      crit[cu / 32] |= 1u << (cu % 32);
+    }
     masked = hipExtStreamCreateWithCUMask(&s_exec[0], (uint32_t)crit.size(), crit.data()) == hipSuccess;
-    for (int i = 1; masked && i < nb_exec_streams; ++i)
+    for (int i = 1; masked && i < total_streams; ++i)
       masked = hipExtStreamCreateWithCUMask(&s_exec[i], (uint32_t)bulk.size(), bulk.data()) == hipSuccess;
-    if (!masked) (void)hipGetLastError();
+    if (!masked) {
+      (void)hipGetLastError();
+      for (int i = 0; i < total_streams; ++i)
+        if (s_exec[i]) { (void)hipStreamDestroy(s_exec[i]); s_exec[i] = nullptr; }
+    }
   }
-  if (!masked)
-    for (int i = 0; i < nb_exec_streams; ++i)
-      PARSEC_HIP_CHECK(hipStreamCreateWithPriority(&s_exec[i], hipStreamNonBlocking, i <= 1 ? hi : lo));
-  for (int i = nb_exec_streams; i < total_streams; ++i) PARSEC_HIP_CHECK(hipStreamCreateWithPriority(&s_exec[i], hipStreamNonBlocking, hi));
+  if (!masked) {
+    PARSEC_HIP_CHECK(hipStreamCreateWithPriority(&s_exec[0], hipStreamNonBlocking, hi));
+    for (int i = 1; i < total_streams; ++i) PARSEC_HIP_CHECK(hipStreamCreateWithPriority(&s_exec[i], hipStreamNonBlocking, lo));
+  }
   cu_masked = masked;
   executing.assign(total_streams, {});
   batches.assign(total_streams, {});
@@ -295,9 +376,7 @@ void HipDevice::shutdown() {
   stream_infos.clear();  // per-stream objects die before their streams
   for (auto s : s_exec) (void)hipStreamDestroy(s);
   s_exec.clear();
-  if (s_h2d) (void)hipStreamDestroy(s_h2d);
-  if (s_d2h) (void)hipStreamDestroy(s_d2h);
-  s_h2d = s_d2h = nullptr;
+  s_copy = nullptr;  // the process-wide copy stream outlives the engine
   // drop cached copies
   for (List* l : {&lru_clean, &lru_owned}) {
     while (ListItem* it = l->pop_front()) {
@@ -527,16 +606,17 @@ bool HipDevice::start_w2r(size_t bytes) {
     lru_remove(c);
     st->w2r = true;
     c->readers.fetch_add(1);  // pinned: not dropped while the copy is in flight
-    PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, c->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_d2h));
+    PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, c->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_copy));
     stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
     job.copies.push_back(c);
     job.versions.push_back(c->version);
+    job.bytes.push_back(d->nb_elts);
     queued += d->nb_elts;
     it = nx;
   }
   if (job.copies.empty()) return false;
   job.ev = get_event();
-  PARSEC_HIP_CHECK(hipEventRecord(job.ev, s_d2h));
+  PARSEC_HIP_CHECK(hipEventRecord(job.ev, s_copy));
   w2r_bytes_inflight += queued;
   stats.w2r_tasks.fetch_add(1, std::memory_order_relaxed);
   w2r_jobs.push_back(std::move(job));
@@ -552,10 +632,10 @@ bool HipDevice::progress_w2r() {
       DataCopy* c = j.copies[i];
       Data* d = c->original;
       auto* st = static_cast<DevCopyState*>(c->dev_state);
+      w2r_bytes_inflight -= std::min(w2r_bytes_inflight, j.bytes[i]);
       if (d) {
         std::lock_guard<SpinLock> g(d->lock);
         DataCopy* host = d->copy(0);
-        w2r_bytes_inflight -= std::min(w2r_bytes_inflight, (size_t)d->nb_elts);
         // a writer may not have touched it meanwhile (writers wait for w2r)
         if (host && c->version == j.versions[i]) {
           host->version = c->version;
@@ -629,15 +709,15 @@ bool HipDevice::progress_prefetch() {
       data_release(d);
       continue;
     }
-    if (src->device_index == 0) PARSEC_HIP_CHECK(hipMemcpyAsync(local->device_private, src->device_private, d->nb_elts, hipMemcpyHostToDevice, s_h2d));
-    else PARSEC_HIP_CHECK(hipMemcpyPeerAsync(local->device_private, ordinal, src->device_private, device_hip_ordinal(src->device_index), d->nb_elts, s_h2d));
+    if (src->device_index == 0) PARSEC_HIP_CHECK(hipMemcpyAsync(local->device_private, src->device_private, d->nb_elts, hipMemcpyHostToDevice, s_copy));
+    else PARSEC_HIP_CHECK(hipMemcpyPeerAsync(local->device_private, ordinal, src->device_private, device_hip_ordinal(src->device_index), d->nb_elts, s_copy));
     stats.bytes_in.fetch_add(d->nb_elts, std::memory_order_relaxed);
     stats.prefetches.fetch_add(1, std::memory_order_relaxed);
     local->transfer_status = TRANSFER_UNDER;
     local->readers.fetch_add(1);
     PrefetchJob j;
     j.ev = get_event();
-    PARSEC_HIP_CHECK(hipEventRecord(j.ev, s_h2d));
+    PARSEC_HIP_CHECK(hipEventRecord(j.ev, s_copy));
     j.local = local;
     j.d = d;
     prefetch_jobs.push_back(j);
@@ -799,7 +879,7 @@ int HipDevice::stage_in(GpuTask* g) {
     lru_remove(local);
     local->readers.fetch_add(1);
     g->dev_copy[fi] = local;
-    if (local->transfer_status == TRANSFER_UNDER) { any = true; continue; }  // ordered behind the in-flight copy on s_h2d
+    if (local->transfer_status == TRANSFER_UNDER) { any = true; continue; }  // ordered behind the in-flight copy on s_copy
     DataCopy* src = data_start_transfer_ownership_to_copy(d, device_index, g->access[fi]);
     if (src && src != local && custom_in && src->device_index == 0) {
       // the chore moves this flow itself (one stage_in call for all of them below)
@@ -817,10 +897,10 @@ int HipDevice::stage_in(GpuTask* g) {
       hipMemcpyKind k = src->device_index == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
       if (k == hipMemcpyDeviceToDevice) {
         int src_ord = device_hip_ordinal(src->device_index);
-        PARSEC_HIP_CHECK(hipMemcpyPeerAsync(local->device_private, ordinal, src->device_private, src_ord, d->nb_elts, s_h2d));
+        PARSEC_HIP_CHECK(hipMemcpyPeerAsync(local->device_private, ordinal, src->device_private, src_ord, d->nb_elts, s_copy));
         stats.bytes_d2d.fetch_add(d->nb_elts, std::memory_order_relaxed);
       } else {
-        PARSEC_HIP_CHECK(hipMemcpyAsync(local->device_private, src->device_private, d->nb_elts, k, s_h2d));
+        PARSEC_HIP_CHECK(hipMemcpyAsync(local->device_private, src->device_private, d->nb_elts, k, s_copy));
         stats.bytes_in.fetch_add(d->nb_elts, std::memory_order_relaxed);
       }
       local->transfer_status = TRANSFER_UNDER;
@@ -831,13 +911,13 @@ int HipDevice::stage_in(GpuTask* g) {
   }
   if (sctx.flow_mask) {
     sctx.task = t;
-    sctx.stream = s_h2d;
+    sctx.stream = s_copy;
     sctx.device_index = device_index;
     if (ch.stage_in(sctx) != 0) fatal("%s: user stage_in failed", t->task_class->name.c_str());
   }
   if (!any) return 0;
   g->ev_in = get_event();
-  PARSEC_HIP_CHECK(hipEventRecord(g->ev_in, s_h2d));
+  PARSEC_HIP_CHECK(hipEventRecord(g->ev_in, s_copy));
   return 1;
 }
 
@@ -861,31 +941,32 @@ void HipDevice::execute_ready() {
     const Chore& ch = t->task_class->chores[g->chore];
     int s;
     const bool hp = t->priority >= high_prio_threshold || (t->task_class->flags & TC_HIGH_PRIORITY);
-    if (nb_exec_streams == 1) s = 0;
-    else if (nb_exec_streams == 2) s = hp ? 0 : 1;
-    else if (t->priority >= critical_threshold) {
-      // one critical stream per round (its tasks batch together): stream 0 unless it
-      // has work in flight and an extra critical stream is idle
+    // critical path (POTRF and what feeds the next one): the critical stream.
+    // Other high-priority work goes to the least loaded bulk stream at once; with
+    // a CU partition (reserved_cus) it would crowd the few critical CUs, and
+    // without one it would queue behind the critical kernels.
+    const bool crit = t->priority >= critical_threshold;
+    if (nb_exec_streams == 1 || (crit && (cu_masked || nb_exec_streams == 2)) || (!cu_masked && nb_exec_streams >= 3 && hp)) {
+      s = 0;
+    } else if (hp || crit) {
       s = -1;
-      for (size_t c = 0; c < round_tasks.size() && s < 0; ++c)
-        if ((c == 0 || c >= (size_t)nb_exec_streams) && !round_tasks[c].empty()) s = (int)c;
+      for (int i = 1; i < nb_exec_streams && s < 0; ++i)  // join a batch already open this round
+        if (!round_tasks[i].empty()) s = i;
       if (s < 0) {
-        s = 0;
-        for (size_t c = nb_exec_streams; c < executing.size() && !executing[0].empty(); ++c)
-          if (executing[c].size() < executing[s].size()) s = (int)c;
+        s = 1;
+        for (int i = 2; i < nb_exec_streams; ++i)
+          if (executing[i].size() < executing[s].size()) s = i;
       }
-    }
-    else if (hp) s = 1;
-    else {
+    } else {
       // Bulk work: pick a bulk stream with fewer than max_inflight_groups launched
       // groups; when every bulk stream is that far ahead, hold the task so the
       // next round launches it in a larger batch (the streams are busy anyway).
-      const int nbulk = nb_exec_streams - 2;
+      const int nbulk = nb_exec_streams - 1;
       s = -1;
       for (int i = 0; i < nbulk && s < 0; ++i)  // join a batch already open this round
-        if (!round_tasks[2 + i].empty()) s = 2 + i;
+        if (!round_tasks[1 + i].empty()) s = 1 + i;
       for (int i = 0; i < nbulk && s < 0; ++i) {
-        const int c = 2 + (int)((rr_stream + i) % (uint32_t)nbulk);
+        const int c = 1 + (int)((rr_stream + i) % (uint32_t)nbulk);
         if (max_inflight_groups <= 0 || (int)executing[c].size() < max_inflight_groups) s = c;
       }
       if (s < 0) { again.push_back(g); continue; }
@@ -936,6 +1017,7 @@ void HipDevice::execute_ready() {
       PARSEC_HIP_CHECK(hipEventRecord(tb, s_exec[s]));
     }
     if (!batches[s].empty()) {
+      batches[s].critical = s == 0 && nb_exec_streams >= 2 && wave_priority;
       launch_kernel_batch(batches[s], s_exec[s], ordinal, workspace(s, kernel_batch_workspace_bytes(batches[s]) + 64));
       stats.kernel_launches.fetch_add(1, std::memory_order_relaxed);
       batches[s].clear();
@@ -1129,17 +1211,17 @@ bool HipDevice::progress() {
               stats.bytes_out.fetch_add(octx.bytes[fi], std::memory_order_relaxed);
               continue;
             }
-            PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, g->dev_copy[fi]->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_d2h));
+            PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, g->dev_copy[fi]->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_copy));
             stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
           }
           if (octx.flow_mask) {
             octx.task = g->task;
-            octx.stream = s_d2h;
+            octx.stream = s_copy;
             octx.device_index = device_index;
             if (gch.stage_out(octx) != 0) fatal("%s: user stage_out failed", g->task->task_class->name.c_str());
           }
           g->ev_out = get_event();
-          PARSEC_HIP_CHECK(hipEventRecord(g->ev_out, s_d2h));
+          PARSEC_HIP_CHECK(hipEventRecord(g->ev_out, s_copy));
           popping.push_back(g);
         } else {
           complete(g, tasks.size() <= 2);
@@ -1214,13 +1296,14 @@ void hip_devices_init(Context* ctx) {
   auto& params = ParamRegistry::instance();
   int enabled = (int)params.reg_int("device", "hip", "enabled", "Enable the HIP device module (number of GPUs, -1 = all)", -1);
   int64_t mask = params.reg_int("device", "hip", "mask", "Bit mask of HIP ordinals to use", -1);
-  g_nb_exec_streams = (int)params.reg_int("device", "hip", "max_streams", "Execution streams per GPU (stream 0 is high priority)", 4);
+  g_nb_exec_streams = (int)params.reg_int("device", "hip", "max_streams", "Execution streams per GPU: stream 0 (high priority) takes critical-path and high-priority tasks, the others the bulk (with the copy stream: 4 hardware queues)", 3);
   int batching = (int)params.reg_int("device", "hip", "batching", "Group ready tile kernels of one kind into one launch", 1);
   int hp = (int)params.reg_int("device", "hip", "high_priority_threshold", "Task priority at or above which the high-priority stream is used", 1 << 27);
   int sortp = (int)params.reg_int("device", "hip", "sort_pending_tasks", "Sort pending GPU tasks by priority", 1);
-  int crit = (int)params.reg_int("device", "hip", "critical_threshold", "Task priority at or above which the CU-reserved critical stream is used", 1 << 29);
-  int rcus = (int)params.reg_int("device", "hip", "reserved_cus", "CUs reserved for the critical-path stream (0 = no CU masking; measured slower on MI355X)", 0);
-  int xcrit = (int)params.reg_int("device", "hip", "critical_streams", "Additional critical-path streams used when the critical stream is busy", 7);
+  int crit = (int)params.reg_int("device", "hip", "critical_threshold", "Task priority at or above which a completed GPU task is released by the manager itself (critical path)", 1 << 29);
+  int rcus = (int)params.reg_int("device", "hip", "reserved_cus", "CUs the bulk streams leave free for the critical stream (CU mask on the bulk streams; 0 = none)", 0);
+  int rstride = (int)params.reg_int("device", "hip", "reserved_cus_stride", "Spacing of the reserved CU ids in the CU mask", 1);
+  const bool wprio = params.reg_int("device", "hip", "wave_priority", "Kernels of the critical stream raise their waves' issue priority (s_setprio) over co-resident bulk waves", 1) != 0;
   const bool trace = params.reg_int("device", "hip", "trace_launches", "Print every launched kernel group (stream, tasks, batch sizes) to stderr", 0) != 0;
   const bool cow = params.reg_int("device", "hip", "complete_on_workers", "Release completed GPU tasks (successor activation) on the compute threads instead of the manager (measured no faster on DPOTRF; breaks the multi-rank DTD stencil: off)", 0) != 0;
   int maxg = (int)params.reg_int("device", "hip", "max_inflight_batches", "Launched kernel groups per bulk stream before new bulk tasks wait for a larger batch (0 = no limit)", 2);
@@ -1245,8 +1328,9 @@ void hip_devices_init(Context* ctx) {
     d->high_prio_threshold = hp;
     d->critical_threshold = crit;
     d->reserved_cus = rcus;
+    d->reserved_stride = rstride;
+    d->wave_priority = wprio;
     d->max_inflight_groups = maxg;
-    d->extra_crit_streams = std::max(0, xcrit);
     d->sort_pending = sortp != 0;
     d->complete_on_workers = cow;
     d->trace_launches = trace;

@@ -1,6 +1,9 @@
 // HIP device module (native, gfx950). One manager thread per GPU owns the
-// device's streams: h2d, d2h and N exec streams (exec[0] is a high-priority
-// stream for critical-path tasks). Ready GPU tasks are staged in, their
+// device's execution streams: exec[0] is the high-priority stream of the
+// critical path (POTRF / panel tasks), exec[1..] carry the bulk updates; every
+// transfer goes through the process-wide copy stream of the GPU
+// (gpu_copy_stream): 4 streams in all, one per hardware queue
+// (GPU_MAX_HW_QUEUES = 4). Ready GPU tasks are staged in, their
 // bodies enqueue tile kernels into per-stream batches which are flushed as one
 // grouped launch per kind, and completion is detected by polling one event per
 // launch group.
@@ -80,6 +83,7 @@ struct W2RJob {
   hipEvent_t ev = nullptr;
   std::vector<DataCopy*> copies;
   std::vector<uint32_t> versions;
+  std::vector<size_t> bytes;  // per copy: subtracted from w2r_bytes_inflight even if the copy was orphaned meanwhile
 };
 // Prefetch of one tile to the device (data_advise PREFETCH), no task attached.
 struct PrefetchJob {
@@ -99,8 +103,8 @@ struct ExecGroup {
 struct HipDevice : Device {
   int ordinal = 0;
   hipDeviceProp_t props{};
-  int nb_exec_streams = 4;
-  hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+  int nb_exec_streams = 3;
+  hipStream_t s_copy = nullptr;  // gpu_copy_stream(ordinal): stage-in, write-back, prefetch
   std::vector<hipStream_t> s_exec;
   std::vector<std::unique_ptr<InfoArray>> stream_infos;  // one per s_exec stream (gpu_stream_infos())
   std::unique_ptr<ZoneAllocator> zone;
@@ -130,6 +134,8 @@ struct HipDevice : Device {
   int high_prio_threshold = 1 << 27;
   int critical_threshold = 1 << 29;
   int reserved_cus = 0;
+  int reserved_stride = 1;
+  bool wave_priority = true;
   bool cu_masked = false;
   bool batching = true;
   bool sort_pending = true;
@@ -162,7 +168,6 @@ struct HipDevice : Device {
   void trace_group(int stream, const ExecGroup& g);
   bool trace_launches = false;
   uint32_t rr_stream = 0;
-  int extra_crit_streams = 7;   // additional critical streams (see start())
   int max_inflight_groups = 2;  // bulk streams: launched groups in flight before new bulk work waits (0 = no limit)
   double us_busy = 0;
 

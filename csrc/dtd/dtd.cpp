@@ -177,7 +177,7 @@ Tile* DtdTaskpool::tile_new(size_t bytes, int rank) {
 // Private copy of `src` for a pending remote transfer (host or device memory).
 static void snapshot_release(DataCopy* c) {
   if (c->device_index == 0) std::free(c->device_private);
-  else device_free(c->device_index, c->device_private);
+  else if (!device_cache_free(c->device_index, c->device_private)) device_free(c->device_index, c->device_private);
   Data* d = c->original;
   if (d) {
     d->lock.lock();
@@ -192,7 +192,9 @@ static DataCopy* snapshot_copy(DataCopy* src) {
   const size_t n = src->original ? src->original->nb_elts : 0;
   void* p = nullptr;
   int dev = src->device_index;
-  if (dev != 0) p = device_alloc(dev, std::max<size_t>(n, 64));
+  // from the GPU's tile-cache zone: no hipMalloc (device-synchronising) per send
+  if (dev != 0) p = device_cache_alloc(dev, std::max<size_t>(n, 64));
+  if (dev != 0 && !p) p = device_alloc(dev, std::max<size_t>(n, 64));
   if (!p) {
     dev = 0;
     if (posix_memalign(&p, 64, std::max<size_t>(n, 64))) fatal("DTD: out of memory for a send snapshot");

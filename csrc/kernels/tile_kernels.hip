@@ -36,6 +36,7 @@ constexpr int kMaxGemmBatch = 40;
 
 struct GemmBatchArgs {
   int count;
+  int prio;  // critical-path launch: raise the waves' issue priority (s_setprio)
   int total_tiles;
   // split-K tail: workgroups [main_tiles, grid) each take 1/ksplit of the K range
   // of one of the last (total_tiles - main_tiles) tiles and add alpha * partial
@@ -46,6 +47,14 @@ struct GemmBatchArgs {
   GemmDesc d[kMaxGemmBatch];
 };
 static_assert(sizeof(GemmBatchArgs) <= 4096, "GemmBatchArgs exceeds the kernel argument limit");
+
+// Issue priority of the waves of the kernels launched by this thread right now:
+// launch_kernel_batch sets it for the critical stream's batch. A critical kernel
+// sharing a CU with bulk GEMM waves otherwise gets a third of the SIMD's MFMA
+// pipe and waits behind their instructions (s_setprio: the SIMD arbitrates by
+// priority, then age).
+static thread_local int t_launch_prio = 0;
+#define PARSEC_WAVE_PRIO(p) do { if (p) __builtin_amdgcn_s_setprio(2); } while (0)
 
 template <class Args>
 __device__ __forceinline__ int find_desc(const Args& a, const int* starts, int t) {
@@ -87,6 +96,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
   constexpr int LDB_S = BN + PADN;
   __shared__ double As[NBUF][BK][LDA_S];
   __shared__ double Bs[NBUF][BK][LDB_S];
+  PARSEC_WAVE_PRIO(args.prio);
 
   // Workgroups [0, main_tiles) own whole tiles (XCD-aware order); the ones
   // dispatched last split the K range of the tail tiles (wave quantisation:
@@ -463,6 +473,7 @@ __global__ __launch_bounds__(kDiagThreads) void dtrtri_diag_kernel(const double*
 constexpr int kMaxTrsmBatch = 48;
 struct TrsmInvArgs {
   int count;
+  int prio;
   int block_start[kMaxTrsmBatch + 1];
   TrsmDesc d[kMaxTrsmBatch];
   const double* invD[kMaxTrsmBatch];
@@ -479,6 +490,7 @@ template <int BR>
 __global__ __launch_bounds__(kTrsmThreads) void dtrsm_inv_kernel(const TrsmInvArgs args) {
   static_assert(BR == 16, "MFMA operand layout assumes 16-row panels");
   extern __shared__ double P[];  // [ncols_padded][BR], then red[16][64]
+  PARSEC_WAVE_PRIO(args.prio);
   const int b = blockIdx.x;
   const int di = find_desc(args, args.block_start, b);
   const TrsmDesc& d = args.d[di];
@@ -573,6 +585,7 @@ static int g_gemm_chunk_fill = -1;   // PARSEC_GEMM_CHUNK_FILL=0: fixed 40-descr
 
 template <int BM, int BN, int BK, int WM, int WN, int NBUF, int OCC = WM * WN / 2>
 static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hipStream_t stream) {
+  a.prio = t_launch_prio;
   int total = 0;
   bool full = g_gemm_full != 0;
   for (int i = 0; i < n; ++i) {
@@ -732,6 +745,7 @@ void launch_trsm_inv(const TrsmDesc* descs, const double* const* invD, int n, hi
     int cnt = std::min(kMaxTrsmBatch, n - s0);
     TrsmInvArgs a;
     a.count = cnt;
+    a.prio = t_launch_prio;
     int total = 0, maxn = 0;
     for (int i = 0; i < cnt; ++i) {
       a.d[i] = descs[s0 + i];
@@ -789,6 +803,7 @@ __global__ void set_identity_kernel(double* W, int n, int ldw) {
 constexpr int kMaxCopyBatch = 48;
 struct CopyBatchArgs {
   int count;
+  int prio;
   int rows[kMaxCopyBatch], cols[kMaxCopyBatch], ld_src[kMaxCopyBatch], ld_dst[kMaxCopyBatch];
   const double* src[kMaxCopyBatch];
   double* dst[kMaxCopyBatch];
@@ -797,6 +812,7 @@ static_assert(sizeof(CopyBatchArgs) <= 4096, "CopyBatchArgs exceeds the kernel a
 
 // blockIdx.y = tile, blockIdx.x strides over columns; one wave-row per column.
 __global__ __launch_bounds__(256) void copy_tiles_kernel(const CopyBatchArgs a) {
+  PARSEC_WAVE_PRIO(a.prio);
   const int t = blockIdx.y;
   const int rows = a.rows[t], cols = a.cols[t], lds = a.ld_src[t], ldd = a.ld_dst[t];
   const double* __restrict__ s = a.src[t];
@@ -823,6 +839,7 @@ static void launch_lower_inverse(const double* L, int lda, int n, const double* 
   for (int b0 = 0; b0 < nblk; b0 += kMaxCopyBatch) {
     CopyBatchArgs ca;
     ca.count = std::min(kMaxCopyBatch, nblk - b0);
+    ca.prio = t_launch_prio;
     for (int i = 0; i < ca.count; ++i) {
       const int b = b0 + i, w = std::min(64, n - 64 * b);
       ca.rows[i] = w; ca.cols[i] = w; ca.ld_src[i] = 64; ca.ld_dst[i] = ldx;
@@ -896,118 +913,45 @@ void launch_potrf(const PotrfDesc& p, hipStream_t stream, double* ws) {
   }
 }
 
-// ============================================ fused tile POTRF (one launch)
-// The whole tile factorization (+ optional W = L^-1) in ONE cooperative launch
-// of G workgroups (256 threads): per 64-column block j
-//   1. WG 0 factors the diagonal block and inverts it (block_potrf64)
-//   2. the panel below is solved against the inverse, 16-row chunks over all WGs
-//   3. the trailing lower triangle gets the rank-64 update, 64x64 blocks over WGs
-// separated by grid barriers; then W by recursive doubling of the diagonal
-// inverses (two block-GEMM phases per level). On the DPOTRF critical path this
-// replaces ~3 launches per 64 columns (each waiting for a free CU behind the
-// bulk GEMMs) by one launch. Block products run on v_mfma_f64_16x16x4f64 with
-// operands read straight from L2 (a wave owns a 32x32 quadrant of a 64x64 block).
-struct PotrfCoopArgs {
-  double* A;
-  int lda, n;
-  double* W;        // optional (ldw)
-  int ldw;
-  double* invD;     // nblk x 4096 diagonal-block inverses
-  double* T;        // n x n scratch (ld n) for the doubling (W only)
-  int* info;        // optional
-  unsigned* bar;    // grid-barrier counter, zero at launch
-  int* fault;       // set when a barrier times out (never expected)
-  long long* timing;  // optional: wall clock (100 MHz) after every grid barrier (WG 0)
-};
+// ====================================== tile POTRF (+W) in n/64 + 1 launches
+// Right-looking blocked Cholesky of an n x n tile (n % 64 == 0) by 64-column
+// steps, ONE launch per step: the launch of step j holds every work item that
+// depends only on step j-1's results, each item a 256-thread workgroup that
+// recomputes the panel blocks it needs instead of waiting for another workgroup
+// (no grid barrier, no inter-workgroup hand-off: the kernel boundary is the only
+// synchronisation, 1.5 us on MI355X against ~5-20 us for an in-kernel barrier
+// with the cross-XCD L2 write-backs it needs). With D_j = L_jj, iD_j = D_j^-1
+// (64 x 64, kept in invD) and P_x = A_xj iD_j^T (= L_xj):
+//   DIAG   (j+1)        D = A_{j+1,j+1} - P_{j+1} P_{j+1}^T, factor D, invert it
+//   TRAIL  (r, c)       A_rc -= P_r P_c^T               j < c <= r, (r,c) != (j+1,j+1)
+//   LW     (r)          A_{r,j-1} := P_r of step j-1     (written one step late: step
+//                                                       j no longer reads column j-1)
+// and, when W = L^-1 is wanted, a right-looking forward substitution L X = I
+// carried along in the W buffer (R = the right-hand sides, X_jc = iD_j R_jc):
+//   RUPD   (r, c)       R_rc -= P_r X_jc                 r > j >= c (X_jj = iD_j)
+//   XW     (c)          W_{j-1,c} := iD_{j-1} R_{j-1,c}  (row j-1 is final)
+// The first launch factors D_0 and zeroes W, the last one writes the final panel
+// and X rows. Every item runs 2-3 64^3 block products on v_mfma_f64_16x16x4f64
+// (4 waves, a 32 x 32 quadrant each) from LDS; DIAG adds the 64 x 64 factor +
+// inverse of diag_factor_inv. Critical path per step: one launch boundary + DIAG.
+constexpr int kPL = 80;  // LDS ld of a staged 64x64 block: 160 dwords = 32 mod 64, conflict-free MFMA operand reads
+typedef double Blk[64][kPL];  // operand form: S[k][m] = op(m, k)
 
-constexpr int kCoopThreads = 256;
-
-__device__ __forceinline__ bool coop_sync(const PotrfCoopArgs& a, unsigned& phase) {
-  __threadfence();
-  __syncthreads();
-  bool ok = true;
-  if (threadIdx.x == 0) {
-    atomicAdd(a.bar, 1u);
-    const unsigned target = (phase + 1) * gridDim.x;
-    const long long t0 = wall_clock64();
-    while (__hip_atomic_load(a.bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(2);
-      if (wall_clock64() - t0 > 400000000ll) {  // 4 s at 100 MHz: give up, flag the fault
-        atomicExch(a.fault, 1);
-        ok = false;
-        break;
-      }
-    }
-  }
-  if (a.timing && blockIdx.x == 0 && threadIdx.x == 0 && phase < 96) a.timing[phase] = wall_clock64();
-  ++phase;
-  __syncthreads();
-  __threadfence();
-  return ok;
-}
-
-// acc += Am(64 x 64) * Bn(64 x 64)^T restricted to this wave's 32x32 quadrant.
-// Am(m, k) = am_t ? Am[m * lda + k] : Am[k * lda + m]; same for Bn. Both
-// operands are staged through LDS first (every load of the block issued at once:
-// one memory latency per product instead of one per k-step), then 16 k-steps of
-// v_mfma_f64_16x16x4f64 read them back. Ends with a barrier: the caller may
-// overwrite the operands afterwards.
-constexpr int kBlkLd = 72;  // 64 + 8 doubles of padding
-__device__ __forceinline__ void blk_mma(double4_t (&acc)[2][2], double (*As)[kBlkLd], double (*Bs)[kBlkLd], const double* __restrict__ Am, int lda, bool am_t,
-                                        const double* __restrict__ Bn, int ldb, bool bn_t) {
+// S[k][m] = G(m, k) (col-major, ld) or, transposed, S[k][m] = G(k, m)
+__device__ __forceinline__ void stage_blk(Blk& S, const double* __restrict__ G, int ld, bool t) {
   const int tid = threadIdx.x;
-  // stage: 2048 double2 pairs per operand, 8 per thread
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const int p = tid + kCoopThreads * e;
-    const int hi = p >> 5, lo = (p & 31) * 2;  // (major index, pair along the contiguous one)
-    if (!am_t) *reinterpret_cast<double2_t*>(&As[hi][lo]) = *reinterpret_cast<const double2_t*>(Am + (size_t)hi * lda + lo);  // k = hi, m = lo..
-    else {
-      const double2_t v = *reinterpret_cast<const double2_t*>(Am + (size_t)hi * lda + lo);  // m = hi, k = lo..
-      As[lo][hi] = v.x;
-      As[lo + 1][hi] = v.y;
-    }
-    if (!bn_t) *reinterpret_cast<double2_t*>(&Bs[hi][lo]) = *reinterpret_cast<const double2_t*>(Bn + (size_t)hi * ldb + lo);
-    else {
-      const double2_t v = *reinterpret_cast<const double2_t*>(Bn + (size_t)hi * ldb + lo);
-      Bs[lo][hi] = v.x;
-      Bs[lo + 1][hi] = v.y;
+    const int p = tid + 256 * e;
+    const int hi = p >> 5, lo = (p & 31) * 2;
+    const double2_t v = *reinterpret_cast<const double2_t*>(G + (size_t)hi * ld + lo);
+    if (!t) {
+      *reinterpret_cast<double2_t*>(&S[hi][lo]) = v;
+    } else {
+      S[lo][hi] = v.x;
+      S[lo + 1][hi] = v.y;
     }
   }
-  __syncthreads();
-  const int lane = tid & 63, w = tid >> 6;
-  const int qm = (w & 1) * 32, qn = (w >> 1) * 32;
-  const int r = lane & 15, kq = lane >> 4;
-#pragma unroll
-  for (int kk = 0; kk < 64; kk += 4) {
-    double y[2], x[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) y[j] = As[kk + kq][qm + j * 16 + r];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) x[i] = Bs[kk + kq][qn + i * 16 + r];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[i], y[j], acc[i][j], 0, 0, 0);
-  }
-  __syncthreads();
-}
-
-// C(64x64, ldc) = beta * C + alpha * acc (this wave's quadrant); lower: only m >= n
-__device__ __forceinline__ void blk_store(const double4_t (&acc)[2][2], double* __restrict__ C, int ldc, double alpha, double beta, bool lower) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int qm = (w & 1) * 32, qn = (w >> 1) * 32;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = qm + j * 16 + (lane & 15), nn = qn + i * 16 + (lane >> 4) + 4 * q;
-        if (lower && m < nn) continue;
-        double* p = C + (size_t)nn * ldc + m;
-        *p = (beta == 0.0 ? 0.0 : beta * *p) + alpha * acc[i][j][q];
-      }
 }
 
 __device__ __forceinline__ void acc_zero(double4_t (&acc)[2][2]) {
@@ -1017,142 +961,498 @@ __device__ __forceinline__ void acc_zero(double4_t (&acc)[2][2]) {
     for (int j = 0; j < 2; ++j) acc[i][j] = (double4_t){0.0, 0.0, 0.0, 0.0};
 }
 
-__global__ __launch_bounds__(kCoopThreads) void dpotrf_tile_coop_kernel(const PotrfCoopArgs a) {
-  __shared__ double As[64][kBlkLd];
-  __shared__ double Bs[64][kBlkLd];
-  const int n = a.n, lda = a.lda, nblk = n / 64;
-  const int G = gridDim.x, wg = blockIdx.x;
-  unsigned phase = 0;
+// acc (this wave's quadrant of C) += sign * sum_k S_a[k][m] S_b[k][n]
+__device__ __forceinline__ void mma_blk(double4_t (&acc)[2][2], const Blk& Sa, const Blk& Sb, double sign) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qm = (w & 1) * 32, qn = (w >> 1) * 32;
+  const int r = lane & 15, kq = lane >> 4;
+#pragma unroll 4
+  for (int kk = 0; kk < 64; kk += 4) {
+    double y[2], x[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) y[j] = Sa[kk + kq][qm + j * 16 + r];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) x[i] = sign * Sb[kk + kq][qn + i * 16 + r];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[i], y[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// (m, n) of accumulator element q of tile (i, j) for this lane
+#define PARSEC_ACC_MN(i, j, q)                                     \
+  const int m = qm + (j) * 16 + (lane & 15);                       \
+  const int n = qn + (i) * 16 + (lane >> 4) + 4 * (q)
+
+// acc -> LDS: S[n][m] = C(m, n) (operand form of C as an NT operand) or, with
+// t, S[m][n] = C(m, n) (C as the B operand of an NN product)
+__device__ __forceinline__ void acc_to_blk(const double4_t (&acc)[2][2], Blk& S, bool t) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qm = (w & 1) * 32, qn = (w >> 1) * 32;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        PARSEC_ACC_MN(i, j, q);
+        if (t) S[m][n] = acc[i][j][q];
+        else S[n][m] = acc[i][j][q];
+      }
+}
+
+// acc = C (global, col-major ldc) or 0
+__device__ __forceinline__ void acc_load(double4_t (&acc)[2][2], const double* __restrict__ C, int ldc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qm = (w & 1) * 32, qn = (w >> 1) * 32;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        PARSEC_ACC_MN(i, j, q);
+        acc[i][j][q] = C ? C[(size_t)n * ldc + m] : 0.0;
+      }
+}
+
+__device__ __forceinline__ void acc_store(const double4_t (&acc)[2][2], double* __restrict__ C, int ldc, bool lower) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qm = (w & 1) * 32, qn = (w >> 1) * 32;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        PARSEC_ACC_MN(i, j, q);
+        if (lower && m < n) continue;
+        C[(size_t)n * ldc + m] = acc[i][j][q];
+      }
+}
+#undef PARSEC_ACC_MN
+
+// 16 x 16 x kn MFMA product into one accumulator tile: acc(m, n) += sign *
+// sum_k Sa[k][m] Sb[k][n] (LDS, leading dimensions lda_s / ldb_s, k from k0).
+// Lane layout of acc: m = lane & 15, n = (lane >> 4) + 4 q.
+__device__ __forceinline__ void mfma16(double4_t& acc, const double* Sa, int lda_s, const double* Sb, int ldb_s, int k0, int kn, double sign) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < kn; kk += 4) {
+    const double y = Sa[(k0 + kk + kq) * lda_s + r];
+    const double x = sign * Sb[(k0 + kk + kq) * ldb_s + r];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
+  }
+}
+
+// Factor the 64 x 64 SPD block held in LDS (Dl[c][r] = D(r, c), ld kPL) in
+// place and invert the factor: L (lower part) -> T (global, ldt), X = L^-1 ->
+// invD (64 x 64, col-major). Four iterations over 16-column panels with a
+// one-panel lookahead; in iteration q
+//   wave q      applies panel q-1's rank-16 update to its own column block q
+//               (v_mfma_f64_16x16x4f64 from LDS), factors panel q (rows in
+//               lanes; the next pivot column through v_readlane, the other
+//               columns through an LDS broadcast: the only serial chain), stores
+//               it and inverts its 16 x 16 diagonal block X_qq (forward
+//               substitution, lane = column);
+//   the others  apply panel q-1's update to the tiles right of column block q,
+//               and wave j < q-1 computes X_{q-1,j} = -X_{q-1,q-1} sum_k L_{q-1,k} X_kj;
+// then the three X_3j tiles. Only the panel chain and one column update per
+// panel are serial; the rest of the update and the inverse run beside them.
+// `pool` (kDiagPoolDoubles, not overlapping Dl) holds X block-packed (the 10
+// lower 16 x 16 blocks, row-major), the diagonal blocks of X col-major, per-wave
+// scratch and the broadcast buffers.
+constexpr int kDiagPoolDoubles = 2560 + 1024 + 1024 + 64 + 128 + 1;
+__device__ __forceinline__ int xblk(int i, int j) { return (i * (i + 1) / 2 + j) * 256; }  // block (i >= j) of X
+// Diagnostics (PARSEC_POTRF_STAMPS=1): wall clock (100 MHz) at the phase
+// boundaries of the last diagonal factorization, read by parsec_amd_potrf_stamps
+__device__ long long g_potrf_stamps[16];
+static int g_potrf_stamp_mode = -1;
+#define PARSEC_STAMP(k) do { if (stamp && threadIdx.x == 0) g_potrf_stamps[k] = wall_clock64(); } while (0)
+
+// X_ij (tile of the inverse, i > j) by wave-local MFMA: T = sum_k L_ik X_kj,
+// X_ij = -X_ii T (Xc block i as the A operand)
+__device__ __forceinline__ void inv_tile(const double* Dl, double* Xb, const double* Xc, double* Tw, int i, int j) {
+  const int lane = threadIdx.x & 63;
+  double4_t t = (double4_t){0.0, 0.0, 0.0, 0.0};
+  for (int k = j; k < i; ++k)  // Sa[kk][m] = L(16i + m, 16k + kk); Sb[kk][n] = X(16k + kk, 16j + n)
+    mfma16(t, Dl + 16 * k * kPL + 16 * i, kPL, Xb + xblk(k, j), 16, 0, 16, 1.0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Tw[((lane >> 4) + 4 * q) + 16 * (lane & 15)] = t[q];  // row-major T: B operand Sb[k][n] = T(k, n)
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS writes are visible to it
+  double4_t x = (double4_t){0.0, 0.0, 0.0, 0.0};
+  mfma16(x, Xc + 256 * i, 16, Tw, 16, 0, 16, -1.0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Xb[xblk(i, j) + (lane & 15) * 16 + (lane >> 4) + 4 * q] = x[q];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+}
+
+__device__ __forceinline__ void diag_factor_inv(double* __restrict__ Dl, double* __restrict__ pool, double* __restrict__ T, int ldt, double* __restrict__ invD, int* info, int info_base, bool stamp) {
+  PARSEC_STAMP(1);
+  double* Xb = pool;                    // X, block-packed: Xb[xblk(i, j) + m * 16 + n] = X(16i + m, 16j + n)
+  double* Xc = pool + 2560;             // 4 diagonal blocks, col-major 16 x 16: Xc[b*256 + k*16 + m] = X(16b+m, 16b+k)
+  double* Tw = Xc + 1024;               // per-wave 16 x 16 scratch (row-major)
+  double* dinv = Tw + 1024;             // 1 / L(i, i)
+  double* colb = dinv + 64;             // column broadcast buffers of the panel wave (2 x 64)
+  int* bad_s = reinterpret_cast<int*>(colb + 128);
+  const int lane = threadIdx.x & 63;
+  const int v = threadIdx.x >> 6;
+  const int r = lane;
+  if (threadIdx.x == 0) *bad_s = 0x7fffffff;
+  __syncthreads();
+  PARSEC_STAMP(2);
+  // rank-16 update of tile (R, C) by panel p
+  auto upd_tile = [&](int R, int C, int p) {
+    double4_t acc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = Dl[(16 * C + (lane >> 4) + 4 * q) * kPL + 16 * R + (lane & 15)];
+    mfma16(acc, Dl + 16 * R, kPL, Dl + 16 * C, kPL, 16 * p, 16, -1.0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Dl[(16 * C + (lane >> 4) + 4 * q) * kPL + 16 * R + (lane & 15)] = acc[q];
+  };
+  // unrolled: every v_readlane below gets a constant lane index
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (v == p) {
+      if (p >= 1) {  // lookahead: panel p-1's update of this wave's own column block
+        for (int R = p; R < 4; ++R) upd_tile(R, p, p - 1);
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+      }
+      double a[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) a[i] = Dl[(16 * p + i) * kPL + r];
+      int bad = 0x7fffffff;
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) {
+        const int j = 16 * p + jj;
+        double d = readlane_d(a[jj], j);
+        if (d <= 0.0 && bad == 0x7fffffff) bad = j + 1;
+        d = d <= 0.0 ? 1.0 : d;
+        const double rs = rsqrt_nr(d);
+        const double lv = (r == j) ? d * rs : (r > j ? a[jj] * rs : 0.0);
+        a[jj] = lv;
+        if (r == j) dinv[j] = rs;
+        // next pivot column first (the chain, one v_readlane), the other
+        // columns off it: the column goes through LDS and comes back as
+        // broadcast reads (no SGPR pressure, all reads in flight at once)
+        if (jj + 1 < 16) a[jj + 1] -= lv * readlane_d(lv, j + 1);
+        if (jj + 2 < 16) {
+          colb[(jj & 1) * 64 + r] = lv;
+#pragma unroll
+          for (int i = jj + 2; i < 16; ++i) a[i] -= lv * colb[(jj & 1) * 64 + 16 * p + i];
+        }
+      }
+      if (r == 0 && bad != 0x7fffffff) atomicMin(bad_s, bad);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        Dl[(16 * p + i) * kPL + r] = a[i];
+        if (r >= 16 * p + i) T[(size_t)(16 * p + i) * ldt + r] = a[i];  // L is final: straight out
+      }
+      if (stamp && lane == 0) g_potrf_stamps[3 + 2 * p] = wall_clock64();
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // this wave's panel / dinv stores are visible to it
+      // X_pp: lane c < 16 owns column c; s_i -= L(i, k) x_k as soon as x_k is known
+      if (lane < 16) {
+        const int b0 = 16 * p;
+        double sv[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sv[i] = (i == lane) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          sv[k] *= dinv[b0 + k];
+#pragma unroll
+          for (int i = k + 1; i < 16; ++i) sv[i] = __builtin_fma(-Dl[(b0 + k) * kPL + b0 + i], sv[k], sv[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          Xb[xblk(p, p) + i * 16 + lane] = sv[i];
+          Xc[p * 256 + lane * 16 + i] = sv[i];
+        }
+      }
+    } else if (p >= 1) {
+      // panel p-1's update of the tiles right of column block p: (R, C), p < C <= R,
+      // dealt to the three other waves
+      const int nt = (3 - p) * (4 - p) / 2;
+      const int me = (v - p + 3) & 3;  // 0..2 among the other waves
+      for (int t = me; t < nt; t += 3) {
+        int R = p + 1, u = t;
+        while (u > R - (p + 1)) { u -= R - p; ++R; }
+        upd_tile(R, p + 1 + u, p - 1);
+      }
+      // row p-1 of the inverse (its diagonal block is done): wave j < p-1 takes X_{p-1,j}
+      if (p >= 2 && v < p - 1) inv_tile(Dl, Xb, Xc, Tw + 256 * v, p - 1, v);
+    }
+    __syncthreads();
+    PARSEC_STAMP(4 + 2 * p);
+  }
+  if (threadIdx.x == 0 && *bad_s != 0x7fffffff && info) atomicCAS(info, 0, info_base + *bad_s);
+  // row 3 of the inverse
+  if (v < 3) inv_tile(Dl, Xb, Xc, Tw + 256 * v, 3, v);
+  __syncthreads();
+  PARSEC_STAMP(11);
+  PARSEC_STAMP(12);
+  // invD col-major: invD[c * 64 + r] = X(r, c), zero above the diagonal
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = 16 * v + k;
+    invD[(size_t)c * 64 + r] = r >= c ? Xb[xblk(r >> 4, v) + (r & 15) * 16 + k] : 0.0;
+  }
+  PARSEC_STAMP(13);
+}
+
+struct PotrfStepArgs {
+  double* A;
+  double* W;        // optional: W = L^-1 (ldw); also holds the right-hand sides R
+  double* invD;     // nb x 4096: iD_j
+  int* info;
+  int lda, ldw, nb; // nb = n / 64 blocks
+  int stamp;        // record phase clocks of the DIAG item (diagnostics)
+  int j;            // step (-1: first launch, nb - 1: last launch)
+  // item ranges: [0, n_diag) DIAG, then TRAIL, RUPD, LW, XW, ZERO
+  int n_diag, n_trail, n_rupd, n_lw, n_xw, n_zero;
+};
+
+// Prefetch of a 64 x 64 block into registers (8 x 16 B per thread), so its
+// global latency overlaps the MFMA work on the LDS buffers, then the LDS store.
+struct BlkRegs {
+  double2_t v[8];
+};
+__device__ __forceinline__ void blk_fetch(BlkRegs& R, const double* __restrict__ G, int ld) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int p = tid + 256 * e;
+    R.v[e] = *reinterpret_cast<const double2_t*>(G + (size_t)(p >> 5) * ld + (p & 31) * 2);
+  }
+}
+__device__ __forceinline__ void blk_put(Blk& S, const BlkRegs& R, bool t) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int p = tid + 256 * e;
+    const int hi = p >> 5, lo = (p & 31) * 2;
+    if (!t) {
+      *reinterpret_cast<double2_t*>(&S[hi][lo]) = R.v[e];
+    } else {
+      S[lo][hi] = R.v[e].x;
+      S[lo + 1][hi] = R.v[e].y;
+    }
+  }
+}
+
+// Two 64 x 64 staging blocks (80 KB) in all: a step workgroup then fits on a CU
+// next to ONE resident 128 x 128 GEMM workgroup (74 KB of LDS), so critical-path
+// work starts as soon as a bulk workgroup retires instead of waiting for a CU to
+// drain completely (the 120 KB version waited 1.2 ms per tile POTRF at 16k).
+__global__ __launch_bounds__(256) void dpotrf_step_kernel(const PotrfStepArgs a) {
+  __shared__ double pool[2 * 64 * kPL];
+  static_assert(kDiagPoolDoubles <= 64 * kPL, "diag_factor_inv scratch exceeds one staging block");
+  __builtin_amdgcn_s_setprio(2);  // the tile POTRF is the critical path
+  Blk& S0 = *reinterpret_cast<Blk*>(pool);
+  Blk& S1 = *reinterpret_cast<Blk*>(pool + 64 * kPL);
+  const int nb = a.nb, j = a.j, lda = a.lda, ldw = a.ldw;
   double* __restrict__ A = a.A;
-  for (int j = 0; j < nblk; ++j) {
-    double* Djj = A + (size_t)(64 * j) * lda + 64 * j;
-    double* invj = a.invD + (size_t)j * 4096;
-    if (wg == 0) block_potrf64(Djj, lda, 64, invj, a.info, 64 * j, true);
-    if (!coop_sync(a, phase)) return;
-    const int r0 = 64 * (j + 1), rem = n - r0;
-    if (rem <= 0) break;
-    // panel: rows r0.., 64 rows per work item (one 64x64 block product each)
-    const int pblk = rem / 64;
-    for (int t = wg; t < pblk; t += G) {
-      double* B = A + (size_t)(64 * j) * lda + r0 + 64 * t;  // block (j + 1 + t, j)
-      double4_t acc[2][2];
-      acc_zero(acc);
-      blk_mma(acc, As, Bs, B, lda, false, invj, 64, false);  // B(m,k) * X(n,k) -> B X^T (ends with a barrier)
-      blk_store(acc, B, lda, 1.0, 0.0, false);
+  auto blkA = [&](int r, int c) { return A + (size_t)(64 * c) * lda + 64 * r; };
+  auto blkW = [&](int r, int c) { return a.W + (size_t)(64 * c) * ldw + 64 * r; };
+  const double* iD = a.invD + (size_t)(j < 0 ? 0 : j) * 4096;
+  int it = blockIdx.x;
+  double4_t acc[2][2];
+  // ---------------------------------------------------------------- DIAG
+  if (it < a.n_diag) {
+    const bool stamp = a.stamp != 0;
+    PARSEC_STAMP(0);
+    const int d = j + 1;  // block to factor (0 in the first launch)
+    if (j < 0) {          // first launch: D_0 = A_00
+      stage_blk(S1, blkA(0, 0), lda, false);  // S1[c][r] = D(r, c)
+      __syncthreads();
+    } else {
+      acc_load(acc, blkA(d, d), lda);
+      stage_blk(S0, blkA(d, j), lda, false);
+      stage_blk(S1, iD, 64, false);
+      __syncthreads();
+      double4_t p[2][2];
+      acc_zero(p);
+      mma_blk(p, S0, S1, 1.0);  // P = A_dj iD^T
+      __syncthreads();
+      acc_to_blk(p, S0, false);  // S0 = P (operand form)
+      __syncthreads();
+      mma_blk(acc, S0, S0, -1.0);  // D = A_dd - P P^T
+      acc_to_blk(acc, S1, false);  // S1[c][r] = D(r, c) (S1 = iD no longer read)
+      __syncthreads();
     }
-    if (!coop_sync(a, phase)) return;
-    // trailing lower update: blocks (r, c), j < c <= r
-    const int Tn = nblk - j - 1, nt = Tn * (Tn + 1) / 2;
-    for (int t = wg; t < nt; t += G) {
-      // t -> (rr, cc) with cc <= rr (row-major over the lower triangle)
-      int rr = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-      while ((rr + 1) * (rr + 2) / 2 <= t) ++rr;
-      while (rr * (rr + 1) / 2 > t) --rr;
-      const int cc = t - rr * (rr + 1) / 2;
-      const int br = j + 1 + rr, bc = j + 1 + cc;
-      const double* Lr = A + (size_t)(64 * j) * lda + 64 * br;
-      const double* Lc = A + (size_t)(64 * j) * lda + 64 * bc;
-      double* C = A + (size_t)(64 * bc) * lda + 64 * br;
-      double4_t acc[2][2];
-      acc_zero(acc);
-      blk_mma(acc, As, Bs, Lr, lda, false, Lc, lda, false);
-      blk_store(acc, C, lda, -1.0, 1.0, br == bc);
-    }
-    if (!coop_sync(a, phase)) return;
+    diag_factor_inv(&S1[0][0], &S0[0][0], blkA(d, d), lda, a.invD + (size_t)d * 4096, a.info, 64 * d, stamp);
+    return;
   }
-  if (!a.W) return;
-  // ---- W = L^-1: diagonal blocks from invD, zeros above, doubling below
-  double* __restrict__ W = a.W;
-  const int ldw = a.ldw;
-  for (int t = wg; t < nblk * nblk; t += G) {
-    const int bi = t % nblk, bj = t / nblk;  // block (bi, bj)
-    if (bi > bj) continue;                   // strictly-lower blocks come from the doubling
-    for (int e = threadIdx.x; e < 4096; e += kCoopThreads) {
-      const int rr = e & 63, cc = e >> 6;
-      W[(size_t)(64 * bj + cc) * ldw + 64 * bi + rr] = bi == bj ? a.invD[(size_t)bi * 4096 + (size_t)cc * 64 + rr] : 0.0;
+  it -= a.n_diag;
+  // --------------------------------------------------------------- TRAIL
+  if (it < a.n_trail) {
+    // lower triangle of the (nb-1-j)^2 trailing blocks in row-major order, minus (0,0)
+    const int t = it + 1;
+    int rr = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while ((rr + 1) * (rr + 2) / 2 <= t) ++rr;
+    while (rr * (rr + 1) / 2 > t) --rr;
+    const int cc = t - rr * (rr + 1) / 2;
+    const int r = j + 1 + rr, c = j + 1 + cc;
+    BlkRegs rc;
+    if (r != c) blk_fetch(rc, blkA(c, j), lda);
+    acc_load(acc, blkA(r, c), lda);
+    stage_blk(S0, blkA(r, j), lda, false);
+    stage_blk(S1, iD, 64, false);
+    __syncthreads();
+    double4_t pr[2][2], pc[2][2];
+    acc_zero(pr);
+    mma_blk(pr, S0, S1, 1.0);  // P_r
+    __syncthreads();
+    if (r != c) {
+      blk_put(S0, rc, false);
+      __syncthreads();
+      acc_zero(pc);
+      mma_blk(pc, S0, S1, 1.0);  // P_c
+      __syncthreads();
+      acc_to_blk(pc, S1, false);
     }
+    acc_to_blk(pr, S0, false);
+    __syncthreads();
+    mma_blk(acc, S0, r != c ? S1 : S0, -1.0);  // A_rc -= P_r P_c^T
+    acc_store(acc, blkA(r, c), lda, r == c);
+    return;
   }
-  if (!coop_sync(a, phase)) return;
-  double* __restrict__ Tm = a.T;
-  for (int g = 1; g < nblk; g *= 2) {
-    // T(c, a) = sum_{k = a}^{a0 + g - 1} L(c, k) X(k, a) for c in C, a in A
-    const int pairs = (nblk + 2 * g - 1) / (2 * g);
-    int items = 0;
-    for (int p = 0; p < pairs; ++p) {
-      const int a0 = 2 * g * p, c0 = a0 + g, c1 = min(a0 + 2 * g, nblk);
-      if (c0 >= nblk) continue;
-      const int nc = c1 - c0;
-      for (int it = 0; it < nc * g; ++it, ++items) {
-        if (items % G != wg) continue;
-        const int c = c0 + it % nc, ab = a0 + it / nc;
-        double4_t acc[2][2];
-        acc_zero(acc);
-        for (int kb = ab; kb < c0; ++kb)
-          blk_mma(acc, As, Bs, A + (size_t)(64 * kb) * lda + 64 * c, lda, false, W + (size_t)(64 * ab) * ldw + 64 * kb, ldw, true);
-        blk_store(acc, Tm + (size_t)(64 * ab) * n + 64 * c, n, 1.0, 0.0, false);
-      }
+  it -= a.n_trail;
+  // ---------------------------------------------------------------- RUPD
+  if (it < a.n_rupd) {
+    const int rows = nb - 1 - j;
+    const int r = j + 1 + it % rows, c = it / rows;  // c in [0, j]
+    BlkRegs rx;
+    if (c != j) blk_fetch(rx, blkW(j, c), ldw);
+    acc_load(acc, blkW(r, c), ldw);
+    stage_blk(S0, blkA(r, j), lda, false);
+    stage_blk(S1, iD, 64, false);
+    __syncthreads();
+    double4_t pr[2][2], x[2][2];
+    acc_zero(pr);
+    mma_blk(pr, S0, S1, 1.0);  // P_r
+    __syncthreads();
+    if (c == j) {
+      stage_blk(S1, iD, 64, true);  // X_jj = iD as the NN B operand: S1[k][n] = iD(k, n)
+    } else {
+      blk_put(S0, rx, true);  // R_jc as the NN B operand
+      __syncthreads();
+      acc_zero(x);
+      mma_blk(x, S1, S0, 1.0);  // X_jc = iD R_jc  (S1[k][m] = iD(m, k))
+      __syncthreads();
+      acc_to_blk(x, S1, true);
     }
-    if (!coop_sync(a, phase)) return;
-    // X(c, a) = - sum_{k = c0}^{c} X(c, k) T(k, a)
-    items = 0;
-    for (int p = 0; p < pairs; ++p) {
-      const int a0 = 2 * g * p, c0 = a0 + g, c1 = min(a0 + 2 * g, nblk);
-      if (c0 >= nblk) continue;
-      const int nc = c1 - c0;
-      for (int it = 0; it < nc * g; ++it, ++items) {
-        if (items % G != wg) continue;
-        const int c = c0 + it % nc, ab = a0 + it / nc;
-        double4_t acc[2][2];
-        acc_zero(acc);
-        for (int kb = c0; kb <= c; ++kb)
-          blk_mma(acc, As, Bs, W + (size_t)(64 * kb) * ldw + 64 * c, ldw, false, Tm + (size_t)(64 * ab) * n + 64 * kb, n, true);
-        blk_store(acc, W + (size_t)(64 * ab) * ldw + 64 * c, ldw, -1.0, 0.0, false);
-      }
+    acc_to_blk(pr, S0, false);
+    __syncthreads();
+    mma_blk(acc, S0, S1, -1.0);  // R_rc -= P_r X_jc
+    acc_store(acc, blkW(r, c), ldw, false);
+    return;
+  }
+  it -= a.n_rupd;
+  // ------------------------------------------------------------------ LW
+  if (it < a.n_lw) {
+    const int p = j - 1, r = p + 1 + it;  // the panel of step j - 1
+    stage_blk(S0, blkA(r, p), lda, false);
+    stage_blk(S1, a.invD + (size_t)p * 4096, 64, false);
+    __syncthreads();
+    acc_zero(acc);
+    mma_blk(acc, S0, S1, 1.0);
+    __syncthreads();  // every wave has read S0 (a copy of the block being overwritten)
+    acc_store(acc, blkA(r, p), lda, false);
+    return;
+  }
+  it -= a.n_lw;
+  // ------------------------------------------------------------------ XW
+  if (it < a.n_xw) {
+    // rows [j - 1, ...] that became final: the last launch finishes two rows
+    int row = j - 1, c = it;
+    if (c >= row + 1) { c -= row + 1; ++row; }
+    const double* iDr = a.invD + (size_t)row * 4096;
+    if (c == row) {  // diagonal block: iD itself
+      double* Wd = blkW(row, row);
+      for (int e = threadIdx.x; e < 4096; e += 256) Wd[(size_t)(e >> 6) * ldw + (e & 63)] = iDr[e];
+      return;
     }
-    if (!coop_sync(a, phase)) return;
+    stage_blk(S1, iDr, 64, false);
+    stage_blk(S0, blkW(row, c), ldw, true);
+    __syncthreads();
+    acc_zero(acc);
+    mma_blk(acc, S1, S0, 1.0);
+    __syncthreads();
+    acc_store(acc, blkW(row, c), ldw, false);
+    return;
+  }
+  it -= a.n_xw;
+  // ---------------------------------------------------------------- ZERO
+  if (it < a.n_zero) {
+    const size_t nn = (size_t)64 * nb;
+    for (size_t c = (size_t)it; c < nn; c += (size_t)a.n_zero)
+      for (size_t r = threadIdx.x * 2; r < nn; r += 512) *reinterpret_cast<double2_t*>(a.W + c * ldw + r) = (double2_t){0.0, 0.0};
   }
 }
 
-static int g_potrf_fused = -1;  // PARSEC_POTRF_FUSED=0 restores the multi-launch tile POTRF
+static int g_potrf_steps = -1;  // PARSEC_POTRF_STEPS=0 restores the 3-launches-per-64-columns tile POTRF
 
-constexpr size_t kCoopHeader = 1024;  // barrier counter, fault flag, 96 timing slots
-static int g_potrf_timing = -1;       // PARSEC_POTRF_TIMING=1: record the barrier clocks
-
-size_t potrf_fused_workspace_bytes(const PotrfDesc& p) {
-  const size_t nblk = (size_t)p.n / 64;
-  return (nblk * 4096 + (p.W_out ? (size_t)p.n * p.n : 0)) * sizeof(double) + kCoopHeader;
+int potrf_steps_mode(int on) {
+  const int prev = g_potrf_steps;
+  if (on >= 0) g_potrf_steps = on;
+  return prev;
 }
 
-bool potrf_fused_eligible(const PotrfDesc& p) {
-  if (g_potrf_fused < 0) {
-    const char* e = getenv("PARSEC_POTRF_FUSED");
-    g_potrf_fused = e ? atoi(e) : 0;
+bool potrf_steps_eligible(const PotrfDesc& p) {
+  if (g_potrf_steps < 0) {
+    const char* e = getenv("PARSEC_POTRF_STEPS");
+    g_potrf_steps = e ? atoi(e) : 1;
   }
-  return g_potrf_fused != 0 && p.n % 64 == 0 && p.n >= 128 && p.n <= 2048;
+  return g_potrf_steps != 0 && p.n % 64 == 0 && p.n >= 64 && p.lda % 2 == 0 && ((uintptr_t)p.A % 16) == 0 &&
+         (!p.W_out || (p.ldw % 2 == 0 && ((uintptr_t)p.W_out % 16) == 0));
 }
 
-// ws layout: [barrier counter (256 B)] [invD (unless kept by the caller)] [T]
-void launch_potrf_fused(const PotrfDesc& p, hipStream_t stream, double* ws) {
-  PotrfCoopArgs a{};
-  a.A = p.A; a.lda = p.lda; a.n = p.n; a.W = p.W_out; a.ldw = p.ldw; a.info = p.info;
-  char* base = reinterpret_cast<char*>(ws);
-  a.bar = reinterpret_cast<unsigned*>(base);
-  a.fault = reinterpret_cast<int*>(base + 64);
-  if (g_potrf_timing < 0) {
-    const char* e = getenv("PARSEC_POTRF_TIMING");
-    g_potrf_timing = e ? atoi(e) : 0;
+size_t potrf_steps_workspace_bytes(const PotrfDesc& p) { return p.invD_out ? 0 : (size_t)(p.n / 64) * 4096 * sizeof(double); }
+
+void launch_potrf_steps(const PotrfDesc& p, hipStream_t stream, double* ws) {
+  PotrfStepArgs a{};
+  a.A = p.A; a.lda = p.lda; a.W = p.W_out; a.ldw = p.ldw; a.info = p.info;
+  a.invD = p.invD_out ? p.invD_out : ws;
+  if (g_potrf_stamp_mode < 0) {
+    const char* e = getenv("PARSEC_POTRF_STAMPS");
+    g_potrf_stamp_mode = e ? atoi(e) : 0;
   }
-  a.timing = g_potrf_timing ? reinterpret_cast<long long*>(base + 128) : nullptr;
-  double* d = reinterpret_cast<double*>(base + kCoopHeader);
-  const int nblk = p.n / 64;
-  a.invD = p.invD_out ? p.invD_out : d;
-  if (!p.invD_out) d += (size_t)nblk * 4096;
-  a.T = d;
-  (void)hipMemsetAsync(base, 0, kCoopHeader, stream);
-  // enough workgroups for the widest phase, few enough to be co-resident next to
-  // the bulk GEMMs (one 84 KB-LDS workgroup per CU)
-  const int G = 32;
-  hipLaunchKernelGGL(dpotrf_tile_coop_kernel, dim3(G), dim3(kCoopThreads), 0, stream, a);
+  a.stamp = g_potrf_stamp_mode;
+  const int nb = p.n / 64;
+  a.nb = nb;
+  const bool w = p.W_out != nullptr;
+  auto launch = [&](int j) {
+    a.j = j;
+    const int rows = nb - 1 - j;  // blocks below the diagonal of step j
+    if (j < 0) {
+      a.n_diag = 1; a.n_trail = 0; a.n_rupd = 0; a.n_lw = 0; a.n_xw = 0;
+      a.n_zero = w ? std::min(4 * nb, 256) : 0;
+    } else if (j < nb - 1) {
+      a.n_diag = 1;
+      a.n_trail = rows * (rows + 1) / 2 - 1;
+      a.n_rupd = w ? rows * (j + 1) : 0;
+      a.n_lw = j >= 1 ? nb - j : 0;
+      a.n_xw = (w && j >= 1) ? j : 0;
+      a.n_zero = 0;
+    } else {  // last launch: the final panel and the last two X rows
+      a.n_diag = 0; a.n_trail = 0; a.n_rupd = 0;
+      a.n_lw = nb >= 2 ? 1 : 0;
+      a.n_xw = w ? (nb >= 2 ? (nb - 1) + nb : 1) : 0;
+      a.n_zero = 0;
+    }
+    if (j == nb - 1 && nb == 1) {  // a single block: X row 0 only
+      a.n_lw = 0;
+    }
+    const int grid = a.n_diag + a.n_trail + a.n_rupd + a.n_lw + a.n_xw + a.n_zero;
+    if (grid > 0) hipLaunchKernelGGL(dpotrf_step_kernel, dim3(grid), dim3(256), 0, stream, a);
+  };
+  launch(-1);
+  for (int j = 0; j < nb - 1; ++j) launch(j);
+  launch(nb - 1);
 }
 
 size_t trsm_w_workspace_bytes(const TrsmGemmDesc* d, int n) {
@@ -1168,6 +1468,7 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
     const int cnt = std::min(kMaxCopyBatch, n - s0);
     CopyBatchArgs ca;
     ca.count = cnt;
+    ca.prio = t_launch_prio;
     std::vector<GemmDesc> g(cnt);
     char* p = reinterpret_cast<char*>(ws);
     int maxc = 1;
@@ -1192,9 +1493,10 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
 
 namespace kern {
 size_t potrf_workspace_bytes(const PotrfDesc& p);
-size_t potrf_fused_workspace_bytes(const PotrfDesc& p);
-bool potrf_fused_eligible(const PotrfDesc& p);
-void launch_potrf_fused(const PotrfDesc& p, hipStream_t stream, double* ws);
+size_t potrf_steps_workspace_bytes(const PotrfDesc& p);
+bool potrf_steps_eligible(const PotrfDesc& p);
+int potrf_steps_mode(int on);
+void launch_potrf_steps(const PotrfDesc& p, hipStream_t stream, double* ws);
 size_t trsm_w_workspace_bytes(const TrsmGemmDesc* d, int n);
 void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, double* ws);
 void launch_qr_panel(const QrPanelDesc* descs, int n, hipStream_t stream);
@@ -1207,7 +1509,7 @@ size_t qr_apply_workspace_bytes(const QrApplyDesc* descs, int n);
 
 size_t kernel_batch_workspace_bytes(const KernelBatch& b) {
   size_t w = 0;
-  for (auto& p : b.potrf) w = std::max(w, kern::potrf_fused_eligible(p) ? kern::potrf_fused_workspace_bytes(p) : kern::potrf_workspace_bytes(p));
+  for (auto& p : b.potrf) w = std::max(w, kern::potrf_steps_eligible(p) ? kern::potrf_steps_workspace_bytes(p) : kern::potrf_workspace_bytes(p));
   if (!b.trsm_w.empty()) w = std::max(w, kern::trsm_w_workspace_bytes(b.trsm_w.data(), (int)b.trsm_w.size()));
   if (!b.qr_panel.empty()) w = std::max(w, kern::qr_panel_workspace_bytes(b.qr_panel.data(), (int)b.qr_panel.size()));
   w = std::max(w, kern::trsm_workspace_bytes(b.trsm.data(), (int)b.trsm.size()));
@@ -1216,9 +1518,14 @@ size_t kernel_batch_workspace_bytes(const KernelBatch& b) {
 
 void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal, void* ws) {
   (void)device_ordinal;
+  struct PrioScope {
+    int prev;
+    explicit PrioScope(bool on) : prev(kern::t_launch_prio) { kern::t_launch_prio = on ? 1 : 0; }
+    ~PrioScope() { kern::t_launch_prio = prev; }
+  } prio_scope(b.critical);
   // critical-path kernels first: POTRF, then TRSM, then the GEMM/SYRK updates
   for (auto& p : b.potrf) {
-    if (kern::potrf_fused_eligible(p)) kern::launch_potrf_fused(p, stream, static_cast<double*>(ws));
+    if (kern::potrf_steps_eligible(p)) kern::launch_potrf_steps(p, stream, static_cast<double*>(ws));
     else kern::launch_potrf(p, stream, static_cast<double*>(ws));
   }
   if (!b.qr_panel.empty()) kern::launch_qr_panel_blocked(b.qr_panel.data(), (int)b.qr_panel.size(), stream, static_cast<double*>(ws));
@@ -1275,12 +1582,6 @@ void* test_ws(size_t bytes) {
 extern "C" {
 int parsec_amd_gemm_tile_policy(int p) { return parsec::kern::gemm_tile_policy(p); }
 int parsec_amd_gemm_splitk(int on) { return parsec::kern::gemm_splitk(on); }
-// barrier clocks of the last fused tile POTRF run through the test entry points
-int parsec_amd_potrf_timing(long long* out, int n) {
-  std::lock_guard<std::mutex> g(g_ws_m);
-  if (!g_ws || n > 96) return -1;
-  return (int)hipMemcpy(out, static_cast<char*>(g_ws) + 128, sizeof(long long) * n, hipMemcpyDeviceToHost);
-}
 int parsec_amd_dgemm_batch(const parsec::GemmDesc* descs, int n, void* stream) {
   parsec::kern::launch_gemm_batch(descs, n, (hipStream_t)stream);
   return (int)hipGetLastError();
@@ -1292,9 +1593,9 @@ int parsec_amd_dtrsm_batch(const parsec::TrsmDesc* descs, int n, void* stream) {
 }
 int parsec_amd_dpotrf_tile(double* A, int n, int lda, int* info, void* stream) {
   parsec::PotrfDesc p{A, n, lda, info};
-  if (parsec::kern::potrf_fused_eligible(p)) {
-    void* ws = test_ws(parsec::kern::potrf_fused_workspace_bytes(p));
-    parsec::kern::launch_potrf_fused(p, (hipStream_t)stream, static_cast<double*>(ws));
+  if (parsec::kern::potrf_steps_eligible(p)) {
+    void* ws = test_ws(parsec::kern::potrf_steps_workspace_bytes(p) + 64);
+    parsec::kern::launch_potrf_steps(p, (hipStream_t)stream, static_cast<double*>(ws));
     return (int)hipGetLastError();
   }
   void* ws = test_ws(4096 * sizeof(double));
@@ -1306,14 +1607,25 @@ int parsec_amd_dpotrf_tile_w(double* A, int n, int lda, int* info, double* W, in
   parsec::PotrfDesc p{A, n, lda, info};
   p.W_out = W;
   p.ldw = ldw;
-  if (parsec::kern::potrf_fused_eligible(p)) {
-    void* ws = test_ws(parsec::kern::potrf_fused_workspace_bytes(p));
-    parsec::kern::launch_potrf_fused(p, (hipStream_t)stream, static_cast<double*>(ws));
+  if (parsec::kern::potrf_steps_eligible(p)) {
+    void* ws = test_ws(parsec::kern::potrf_steps_workspace_bytes(p) + 64);
+    parsec::kern::launch_potrf_steps(p, (hipStream_t)stream, static_cast<double*>(ws));
     return (int)hipGetLastError();
   }
   void* ws = test_ws(parsec::kern::potrf_workspace_bytes(p));
   parsec::kern::launch_potrf(p, (hipStream_t)stream, static_cast<double*>(ws));
   return (int)hipGetLastError();
+}
+// Phase clocks of the last stamped diagonal factorization (PARSEC_POTRF_STAMPS=1)
+int parsec_amd_potrf_stamps(long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(parsec::kern::g_potrf_stamps), sizeof(long long) * 16, 0, hipMemcpyDeviceToHost);
+}
+// Select the tile POTRF: 1 = n/64 + 1 fused step launches (default), 0 = the
+// 3-launches-per-64-columns path; < 0 queries. Returns the previous setting.
+int parsec_amd_potrf_steps(int on) {
+  parsec::kern::potrf_steps_eligible(parsec::PotrfDesc{nullptr, 0, 0, nullptr});
+  const int prev = parsec::kern::potrf_steps_mode(on);
+  return prev;
 }
 // B := B W^T for a batch (the DPOTRF panel solve through the inverse)
 int parsec_amd_trsm_w_batch(const parsec::TrsmGemmDesc* d, int n, void* stream) {

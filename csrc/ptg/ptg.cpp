@@ -304,15 +304,28 @@ void PtgTaskClass::build_index_store(const Taskpool* tp) {
   st.ok = true;
 }
 
+// One pass per flow: the guards of each input are evaluated exactly once, so a
+// data-dependent guard (reference tests/dsl/ptg/choice/choice.jdf) that flips
+// while a chunked startup scan runs cannot make the instance look like a
+// startup task in one evaluation and like an activated task in another.
 bool PtgTaskClass::is_startup_instance(const Taskpool* tp, const int32_t* L) const {
-  if (count_task_inputs(tp, L) != 0) return false;
   for (size_t f = 0; f < def.flows.size(); ++f) {
-    if (def.flows[f].access == FLOW_CTL || def.flows[f].in.empty()) continue;
-    bool any = false;
-    for_each_input(tp, (int)f, L, [&](const int32_t*, const DepTarget*) { any = true; });
+    const bool data_flow = def.flows[f].access != FLOW_CTL && !def.flows[f].in.empty();
+    bool any = false, from_task = false;
+    for_each_input(tp, (int)f, L, [&](const int32_t* X, const DepTarget* t) {
+      any = true;
+      if (t->kind != DEP_TASK || from_task) return;
+      const PtgTaskClass* src = owner->classes[t->tc_id];
+      int32_t params[kMaxLocals];
+      expand_args(tp, X, t->args, 0, params, [&](const int32_t* P) {
+        int32_t SL[kMaxLocals];
+        if (!from_task && src->complete_locals(tp, SL, P)) from_task = true;
+      });
+    });
+    if (from_task) return false;
     // a data flow whose every input guard is false waits for a run-time
     // decision (data-dependent guards): it is not a startup task
-    if (!any) return false;
+    if (data_flow && !any) return false;
   }
   return true;
 }
@@ -484,6 +497,7 @@ static std::shared_ptr<DatacopyFuture> reshape_future_of(PtgTaskpool* tp, DataCo
         [](const void* a, const void* b) { return static_cast<const ArenaDatatype*>(a)->opaque_dtt == static_cast<const ArenaDatatype*>(b)->opaque_dtt; },
         [](void* v) { data_copy_release(static_cast<DataCopy*>(v)); });
     c->reshape_version = c->version;
+    c->has_reshape_view.store(true, std::memory_order_release);
   }
   return c->reshape_future;
 }
@@ -600,6 +614,9 @@ int PtgTaskClass::complete_execution(ExecutionStream* es, Task* t) const {
   const uint32_t my = (uint32_t)tp->context->my_rank;
   std::vector<Task*> ready;
   RemoteDepsMsg* msg = nullptr;
+  // write-backs per destination rank carried by this message: the owner retires
+  // exactly the sender's count (its own guard evaluation may differ)
+  std::vector<std::pair<int32_t, int32_t>> wb_counts;
   PARSEC_PINS(es, PINS_RELEASE_DEPS_BEGIN, t);
   for (size_t f = 0; f < def.flows.size(); ++f) {
     const FlowDef& fd = def.flows[f];
@@ -629,23 +646,29 @@ int PtgTaskClass::complete_execution(ExecutionStream* es, Task* t) const {
             if (std::find(o.ranks.begin(), o.ranks.end(), (int)r) == o.ranks.end()) o.ranks.push_back((int)r);
           }
         });
-      } else if (tg->kind == DEP_DATA && data) {
+      } else if (tg->kind == DEP_DATA) {
         DataCollection* dc = tg->dc(tp);
         int64_t idx[kMaxLocals];
         collection_index(tp, X, tg->args, idx);
         const uint32_t r = dc->rank_of(idx, (int)tg->args.size());
         if (r == my) {
-          write_back(dc->data_of(idx, (int)tg->args.size()), data);
-        } else {
+          if (data) write_back(dc->data_of(idx, (int)tg->args.size()), data);
+        } else if (fd.access != FLOW_CTL) {
           // final version of a tile owned by another rank (e.g. the R of a QR
-          // TS chain): ship it; the owner writes it back in on_remote_activation
+          // TS chain): ship it; the owner writes it back in on_remote_activation.
+          // A NULL flow still sends a (data-less) notice: the owner counted this
+          // write-back at startup and must retire it either way.
           if (!msg) {
             msg = new RemoteDepsMsg();
             msg->outputs.resize(def.flows.size());
           }
           auto& o = msg->outputs[f];
           o.data = data;
+          if (!data) o.ctl = true;
           if (std::find(o.ranks.begin(), o.ranks.end(), (int)r) == o.ranks.end()) o.ranks.push_back((int)r);
+          auto it = std::find_if(wb_counts.begin(), wb_counts.end(), [&](const std::pair<int32_t, int32_t>& e) { return e.first == (int32_t)r; });
+          if (it == wb_counts.end()) wb_counts.emplace_back((int32_t)r, 1);
+          else ++it->second;
         }
       }
     });
@@ -656,6 +679,12 @@ int PtgTaskClass::complete_execution(ExecutionStream* es, Task* t) const {
     msg->nb_locals = nb_locals;
     std::memcpy(msg->locals, t->locals, sizeof(int32_t) * nb_locals);
     msg->priority = t->priority;
+    if (!wb_counts.empty()) {
+      const uint32_t n = (uint32_t)wb_counts.size();
+      msg->extra.resize(sizeof(n) + n * 2 * sizeof(int32_t));
+      std::memcpy(msg->extra.data(), &n, sizeof(n));
+      std::memcpy(msg->extra.data() + sizeof(n), wb_counts.data(), n * 2 * sizeof(int32_t));
+    }
     remote_dep_activate(es, tp, *msg);
     delete msg;
   }
@@ -704,7 +733,7 @@ PtgTaskpool::~PtgTaskpool() {
       }
     delete c;
   }
-  for (auto* g : startup_gens) delete g;
+  delete_startup_gens();
 }
 
 PtgTaskClass* PtgTaskpool::add_task_class(TaskClassDef def) {
@@ -843,6 +872,12 @@ struct PtgTaskpool::StartupGen {
   StartupGen(const Taskpool* tp, PtgTaskClass* c) : tc(c), cur(tp, c) {}
 };
 
+// (after the definition: deleting the incomplete type would skip ~SpaceCursor)
+void PtgTaskpool::delete_startup_gens() {
+  for (auto* g : startup_gens) delete g;
+  startup_gens.clear();
+}
+
 namespace {
 // The task class of startup generators: one CPU chore that resumes the
 // enumeration of a class's execution space, schedules the startup tasks it
@@ -956,7 +991,12 @@ void PtgTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
   // at the end of a QR TS chain) arrive as remote activations that no local task
   // waits for: count them as pending runtime actions so this rank does not
   // terminate (and the user read the tile) before they landed.
-  if (ctx->nb_nodes > 1) {
+  // The four-counter termination detection already covers messages in flight
+  // (a rank with an undelivered write-back is not idle), so only the local
+  // module needs the count. Guards of DEP_DATA outputs must then be functions of
+  // the task locals and taskpool globals: they are evaluated here, at startup,
+  // on the owner, and at completion on the sender.
+  if (counts_remote_writebacks()) {
     int64_t expected = 0;
     for (auto* tc : classes) {
       if (!tc->writes_collections) continue;
@@ -1103,12 +1143,23 @@ void PtgTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& ac
         DataCollection* dc = tg->dc(this);
         int64_t idx[kMaxLocals];
         collection_index(this, X, tg->args, idx);
-        if (dc->rank_of(idx, (int)tg->args.size()) == my) {
-          write_back(dc->data_of(idx, (int)tg->args.size()), data);
-          tdm->taskpool_addto_runtime_actions(this, -1);  // counted at startup
-        }
+        if (dc->rank_of(idx, (int)tg->args.size()) == my) write_back(dc->data_of(idx, (int)tg->args.size()), data);
       }
     });
+  }
+  // retire the write-backs this message carries for this rank (counted at startup)
+  if (act.extra.size() >= sizeof(uint32_t) && counts_remote_writebacks()) {
+    uint32_t n = 0;
+    std::memcpy(&n, act.extra.data(), sizeof(n));
+    if (act.extra.size() < sizeof(n) + (size_t)n * 2 * sizeof(int32_t)) fatal("malformed write-back notice (%zu bytes for %u entries)", act.extra.size(), n);
+    for (uint32_t i = 0; i < n; ++i) {
+      int32_t e[2];
+      std::memcpy(e, act.extra.data() + sizeof(n) + (size_t)i * sizeof(e), sizeof(e));
+      if (e[0] == (int32_t)my && e[1] > 0) {
+        remote_writebacks_received += e[1];
+        tdm->taskpool_addto_runtime_actions(this, -e[1]);
+      }
+    }
   }
   if (!ready.empty()) schedule_tasks(es, ready.data(), (int)ready.size(), 1);
 }

@@ -17,6 +17,7 @@
 // activation and stores the incoming data copies straight into it (refcounted),
 // so no per-producer data repository lookup happens on the hot path.
 #pragma once
+#include <cstring>
 #include <mutex>
 #include <unordered_set>
 #include <functional>
@@ -228,11 +229,19 @@ class PtgTaskpool : public Taskpool {
   // emitting a chunk that doubles from startup_iter up to startup_chunk.
   int64_t startup_chunk = 256, startup_iter = 64;
   struct StartupGen;
+  void delete_startup_gens();
   std::vector<StartupGen*> startup_gens;
   int startup_step(ExecutionStream* es, StartupGen* g);
   bool startup_emit(ExecutionStream* es, StartupGen* g, int64_t max_tasks, int64_t max_visits, std::vector<Task*>& out);
   std::vector<std::string> global_names;
   int64_t remote_writebacks_expected = 0;  // final tile versions other ranks send here
+  int64_t remote_writebacks_received = 0;
+  // expected write-backs are held as runtime actions (not with fourcounter,
+  // which already waits for messages in flight); decided from state that is in
+  // place before the taskpool is published to the comm thread
+  bool counts_remote_writebacks() const {
+    return context && context->nb_nodes > 1 && tdm && std::strcmp(tdm->name(), "fourcounter") != 0;
+  }
   bool finalized = false;
   bool options_resolved = false;
   // called once the taskpool completed (wrappers of generated taskpools read

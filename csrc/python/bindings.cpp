@@ -26,7 +26,8 @@ using namespace parsec;
 extern "C" int parsec_amd_dgemm_batch(const GemmDesc* descs, int n, void* stream);
 extern "C" int parsec_amd_gemm_tile_policy(int p);
 extern "C" int parsec_amd_gemm_splitk(int on);
-extern "C" int parsec_amd_potrf_timing(long long* out, int n);
+extern "C" int parsec_amd_potrf_steps(int on);
+extern "C" int parsec_amd_potrf_stamps(long long* out);
 extern "C" int parsec_amd_dtrsm_batch(const TrsmDesc* descs, int n, void* stream);
 extern "C" int parsec_amd_dpotrf_tile(double* A, int n, int lda, int* info, void* stream);
 extern "C" int parsec_amd_dpotrf_tile_w(double* A, int n, int lda, int* info, double* W, int ldw, void* stream);
@@ -636,11 +637,12 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("kernel_gemm_tile_policy", [](int p) { return parsec_amd_gemm_tile_policy(p); });
   m.def("kernel_gemm_splitk", [](int on) { return parsec_amd_gemm_splitk(on); }, "split-K tail of the 128x128 grouped DGEMM: 1 on, 0 off, -1 query; returns the previous setting");
-  m.def("kernel_potrf_timing", [](int n) {
-    std::vector<long long> v(n, 0);
-    if (parsec_amd_potrf_timing(v.data(), n) != 0) v.clear();
+  m.def("kernel_potrf_stamps", []() {
+    std::vector<long long> v(16, 0);
+    if (parsec_amd_potrf_stamps(v.data()) != 0) v.clear();
     return v;
   });
+  m.def("kernel_potrf_steps", [](int on) { return parsec_amd_potrf_steps(on); }, "tile POTRF: 1 = n/64 + 1 fused step launches, 0 = 3 launches per 64 columns, -1 query; returns the previous setting");
   m.def("kernel_dtrsm", [](uintptr_t L, uintptr_t B, int mm, int nn, int ldl, int ldb, uintptr_t stream) {
     TrsmDesc t;
     t.L = (const double*)L; t.B = (double*)B; t.m = mm; t.n = nn; t.ldl = ldl; t.ldb = ldb; t.trans = 1;

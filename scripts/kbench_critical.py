@@ -41,12 +41,18 @@ def main():
         C = torch.randn((n, n), dtype=torch.float64, device=dev)
         t_sy = timeit(lambda: pa.kernel_dgemm(B.data_ptr(), B.data_ptr(), C.data_ptr(), n, n, n, n, n, n, -1.0, 1.0, 1, 1, s))
         t_ge = timeit(lambda: pa.kernel_dgemm(B.data_ptr(), A.data_ptr(), C.data_ptr(), n, n, n, n, n, n, -1.0, 1.0, 1, 0, s))
-        if os.environ.get("PARSEC_POTRF_TIMING"):
+        if os.environ.get("PARSEC_POTRF_STAMPS"):
             A.copy_(S)
             pa.kernel_dpotrf_w(A.data_ptr(), n, n, info.data_ptr(), W.data_ptr(), n, s)
             torch.cuda.synchronize()
-            tm = [t for t in pa.kernel_potrf_timing(96) if t]
-            print(f"n={n} fused phases (us): " + " ".join(f"{(b - a) / 100:.1f}" for a, b in zip(tm, tm[1:])), flush=True)
+            st = pa.kernel_potrf_stamps()
+            names = ["start", "enter", "zeroed", "p0 panel", "p0 rest", "p1 panel", "p1 rest", "p2 panel", "p2 rest", "p3 panel", "p3 rest", "row3 inv", "-", "end"]
+            print(f"n={n} last DIAG phases (us): " + " ".join(f"{names[i]} {(st[i] - st[i - 1]) / 100:.2f}" for i in range(1, 14)), flush=True)
+        prev = pa.kernel_potrf_steps(0)
+        t_pw0 = timeit(lambda: (A.copy_(S), pa.kernel_dpotrf_w(A.data_ptr(), n, n, info.data_ptr(), W.data_ptr(), n, s)))
+        t_p0 = timeit(lambda: (A.copy_(S), pa.kernel_dpotrf(A.data_ptr(), n, n, info.data_ptr(), s)))
+        pa.kernel_potrf_steps(prev)
+        print(f"n={n}: 3-launch path: potrf+W {t_pw0 - t_cp:.1f} us, potrf {t_p0 - t_cp:.1f} us", flush=True)
         print(f"n={n}: potrf+W {t_pw - t_cp:.1f} us, potrf {t_p - t_cp:.1f} us, trsm-as-gemm {t_tw:.1f} us, trsm-blocked {t_tb:.1f} us, "
               f"syrk {t_sy:.1f} us, gemm {t_ge:.1f} us (copy {t_cp:.1f})", flush=True)
 

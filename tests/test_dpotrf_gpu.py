@@ -1,4 +1,5 @@
-"""PTG Cholesky through the GPU engine (HBM-resident and host-resident tiles)."""
+"""PTG Cholesky (the ptgpp-compiled dpotrf_L.jdf taskpool) through the GPU engine
+(HBM-resident and host-resident tiles)."""
 import pytest
 
 torch = pytest.importorskip("torch")
@@ -24,7 +25,7 @@ def test_dpotrf_hbm_resident(pa, N, nb):
         S = _spd(N, "cuda")
         store.copy_(S.reshape(NT, nb, NT, nb).permute(2, 0, 3, 1))
         torch.cuda.synchronize()
-        tp, info = pa.dpotrf_new(A, pa.MATRIX_LOWER)
+        tp, info = pa.dpotrf_jdf_new(A)
         ctx.add_taskpool(tp)
         ctx.start()
         ctx.wait()
@@ -52,7 +53,7 @@ def test_dpotrf_host_resident_staged(pa):
         for m in range(A.mt):
             for n in range(A.nt):
                 A.tile(m, n)[:, :] = S[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb]
-        tp, info = pa.dpotrf_new(A, pa.MATRIX_LOWER)
+        tp, info = pa.dpotrf_jdf_new(A)
         ctx.add_taskpool(tp)
         ctx.start()
         ctx.wait()

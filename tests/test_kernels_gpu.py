@@ -72,6 +72,41 @@ def test_dpotrf_tile(pa, dev, n):
     assert err.item() < 1e-13
 
 
+@pytest.mark.parametrize("steps", [1, 0])
+@pytest.mark.parametrize("n", [128, 512, 1024])
+def test_dpotrf_tile_paths_and_info(pa, dev, n, steps):
+    """Both tile POTRF implementations (n/64 + 1 fused step launches, and 3
+    launches per 64 columns) factor and invert the same SPD tile, and report the
+    LAPACK info (first non-positive pivot, 1-based) of a tile that is not SPD."""
+    prev = pa.kernel_potrf_steps(steps)
+    try:
+        R = torch.randn((n, n), dtype=torch.float64, device=dev)
+        S = R @ R.t() / n + torch.eye(n, dtype=torch.float64, device=dev)
+        A = S.t().contiguous().t().clone()
+        W = _colmajor(n)
+        W.fill_(3.0)
+        info = torch.zeros(1, dtype=torch.int32, device=dev)
+        pa.kernel_dpotrf_w(A.data_ptr(), n, n, info.data_ptr(), W.data_ptr(), n, _stream())
+        torch.cuda.synchronize()
+        assert info.item() == 0
+        Lref = torch.linalg.cholesky(S.cpu()).to(dev)
+        L = torch.tril(A)
+        assert ((L - Lref).abs().max() / Lref.abs().max()).item() < 1e-12
+        eye = torch.eye(n, dtype=torch.float64, device=dev)
+        assert (W @ Lref - eye).abs().max().item() < 1e-10
+        assert torch.triu(W, 1).abs().max().item() == 0.0
+        # not SPD: a negative pivot at row 100 (1-based 101) after the leading 100 x 100
+        B = S.clone()
+        B[100, 100] = -1.0
+        A2 = B.t().contiguous().t().clone()
+        info.zero_()
+        pa.kernel_dpotrf(A2.data_ptr(), n, n, info.data_ptr(), _stream())
+        torch.cuda.synchronize()
+        assert info.item() == 101
+    finally:
+        pa.kernel_potrf_steps(prev)
+
+
 def _colmajor(rows, cols=None):
     cols = rows if cols is None else cols
     return torch.empty((cols, rows), dtype=torch.float64, device="cuda").t()  # rows x cols, column-major (ld = rows)

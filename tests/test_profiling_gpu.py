@@ -30,7 +30,7 @@ def test_gpu_exec_spans(pa, tmp_path):
     store.copy_(S.reshape(NT, nb, NT, nb).permute(2, 0, 3, 1))
     A = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb, nb, N, N, device=pa.first_gpu_device_index(), ptr=store.data_ptr())
     torch.cuda.synchronize()
-    tp, info = pa.dpotrf_new(A, pa.MATRIX_LOWER)
+    tp, info = pa.dpotrf_jdf_new(A)
     ctx.add_taskpool(tp)
     ctx.start()
     ctx.wait()

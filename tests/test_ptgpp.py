@@ -26,7 +26,7 @@ def _run(exe, timeout=60, env=None):
     ("chain", "chain value 10"),
     ("bcast_gather", "leaves 37 sink 1 bad 0"),
     ("local_indices", "runs 16 48 32 1"),
-    ("reshape", "reshape ok 15 bad 0 full 1 upper 5 shared 1"),
+    ("reshape", "reshape ok 15 bad 0 full 1 upper 5 shared 1 rewritten 5"),
     ("tree_reduce", "root 2080 nodes 63 bad 0"),
     ("pingpong", "hops 101 bad 0"),
     ("all2all", "recv 16 done 4 bad 0"),
@@ -184,6 +184,18 @@ def test_dependency_modes(built, name, mode):
     r = _run(built[name], env=_MODES[mode])
     assert r.returncode == 0, r.stdout + r.stderr
     assert _PROGRAMS[name] in r.stdout
+
+
+def test_choice_chunked_startup_repeated(built):
+    """The reference choice.jdf guards (GEN(k) has no active input until GEN(k-1)
+    decided) under one-task startup chunks: the startup scan runs concurrently
+    with the decisions and evaluates each guard once, so an undecided GEN(k) is
+    never emitted as a startup task (it would run twice). Repeated runs make the
+    interleaving likely."""
+    for _ in range(25):
+        r = _run(built["choice"], env=_MODES["chunk1"])
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert "bad 0" in r.stdout
 
 
 def test_mask_mode_detects_double_activation(tmp_path):
