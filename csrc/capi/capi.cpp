@@ -754,3 +754,184 @@ int parsec_profiling_dump(void) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------ communication engine (C)
+// The reference's parsec_comm_engine_t vtable (parsec_comm_engine.h:161-182)
+// over the runtime's CommEngine. User tags t map to the engine's TAG_USER + t;
+// a mem_reg handle points to a MemReg (get_mem_handle_size() bytes, copyable
+// into messages: a peer's handle is read in place).
+namespace {
+std::mutex g_ce_m;
+struct CeTagSlot {
+  parsec_ce_am_callback_t cb = nullptr;
+  void* cb_data = nullptr;
+};
+CeTagSlot g_ce_tags[TAG_MAX - TAG_USER];
+
+int ce_engine_tag(parsec_ce_tag_t tag) { return tag < (parsec_ce_tag_t)(TAG_MAX - TAG_USER) ? TAG_USER + (int)tag : -1; }
+
+int ce_tag_register(parsec_ce_tag_t tag, parsec_ce_am_callback_t cb, void* cb_data, size_t msg_length) {
+  (void)msg_length;
+  CommEngine* ce = comm_engine();
+  const int t = ce_engine_tag(tag);
+  if (!ce || t < 0) return PARSEC_ERROR;
+  {
+    std::lock_guard<std::mutex> g(g_ce_m);
+    g_ce_tags[t - TAG_USER] = CeTagSlot{cb, cb_data};
+  }
+  return ce->tag_register(t, [tag](int src, int, const void* msg, size_t len) {
+    CeTagSlot s = g_ce_tags[tag];
+    if (s.cb) s.cb(&parsec_ce, tag, const_cast<void*>(msg), len, src, s.cb_data);
+  }) == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+int ce_tag_unregister(parsec_ce_tag_t tag) {
+  CommEngine* ce = comm_engine();
+  const int t = ce_engine_tag(tag);
+  if (!ce || t < 0) return PARSEC_ERROR;
+  return ce->tag_unregister(t) == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+int ce_register_common(void* mem, size_t bytes, int device, parsec_datatype_t dtt, int count, parsec_ce_mem_reg_handle_t* lreg, size_t* lreg_size) {
+  CommEngine* ce = comm_engine();
+  if (!ce || !lreg) return PARSEC_ERROR;
+  auto* r = new MemReg();
+  if (ce->mem_register(mem, bytes, device, dtt, count, r) != 0) { delete r; return PARSEC_ERROR; }
+  *lreg = r;
+  if (lreg_size) *lreg_size = sizeof(MemReg);
+  return PARSEC_SUCCESS;
+}
+int ce_mem_register(void* mem, parsec_mem_type_t mem_type, size_t count, parsec_datatype_t datatype, size_t mem_size, parsec_ce_mem_reg_handle_t* lreg,
+                    size_t* lreg_size) {
+  size_t bytes = mem_size;
+  parsec_datatype_t dtt = datatype;
+  int cnt = (int)count;
+  if (mem_type == PARSEC_MEM_TYPE_NONCONTIGUOUS) {
+    bytes = (size_t)type_of(datatype).packed_bytes() * count;  // a byte range of the packed size
+  } else {
+    dtt = new_type(Datatype::contiguous(1, (int64_t)mem_size));  // so mem_retrieve + parsec_type_size give the bytes
+    cnt = 1;
+  }
+  return ce_register_common(mem, bytes, 0, dtt, cnt, lreg, lreg_size);
+}
+int ce_mem_unregister(parsec_ce_mem_reg_handle_t* lreg) {
+  CommEngine* ce = comm_engine();
+  if (!ce || !lreg || !*lreg) return PARSEC_ERROR;
+  auto* r = static_cast<MemReg*>(*lreg);
+  const int rc = ce->mem_unregister(r);
+  // handles made by mem_register are heap objects; one read in place from a
+  // message (a peer's) is not ours to free
+  delete r;
+  *lreg = nullptr;
+  return rc == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+int ce_get_mem_handle_size(void) { return (int)sizeof(MemReg); }
+int ce_mem_retrieve(parsec_ce_mem_reg_handle_t lreg, void** mem, parsec_datatype_t* datatype, int* count) {
+  CommEngine* ce = comm_engine();
+  if (!ce || !lreg) return PARSEC_ERROR;
+  MemReg r;
+  std::memcpy(&r, lreg, sizeof(r));
+  int64_t dtt = 0;
+  int cnt = 0;
+  if (ce->mem_retrieve(r, mem, nullptr, &dtt, &cnt) != 0) return PARSEC_ERROR;
+  if (datatype) *datatype = (parsec_datatype_t)dtt;
+  if (count) *count = cnt;
+  return PARSEC_SUCCESS;
+}
+int ce_onesided(bool is_get, parsec_comm_engine_t* ce_c, parsec_ce_mem_reg_handle_t lreg, ptrdiff_t ldispl, parsec_ce_mem_reg_handle_t rreg, ptrdiff_t rdispl,
+                size_t size, int remote, parsec_ce_onesided_callback_t l_cb, void* l_cb_data, parsec_ce_tag_t r_tag, void* r_cb_data, size_t r_cb_data_size) {
+  CommEngine* ce = comm_engine();
+  if (!ce || !lreg || !rreg) return PARSEC_ERROR;
+  MemReg l, r;
+  std::memcpy(&l, lreg, sizeof(l));
+  std::memcpy(&r, rreg, sizeof(r));
+  // the callback gets the caller's handles back (valid until it unregisters them)
+  OneSidedCallback cb = [ce_c, l_cb, l_cb_data, lreg](const MemReg&, ptrdiff_t ld, const MemReg& rr, ptrdiff_t rd, size_t sz, int rem) {
+    if (!l_cb) return;
+    MemReg rcopy = rr;
+    l_cb(ce_c, lreg, ld, &rcopy, rd, sz, rem, l_cb_data);
+  };
+  const int t = ce_engine_tag(r_tag);
+  const int rc = is_get ? ce->get(l, ldispl, r, rdispl, size, remote, std::move(cb), t, r_cb_data, r_cb_data_size)
+                        : ce->put(l, ldispl, r, rdispl, size, remote, std::move(cb), t, r_cb_data, r_cb_data_size);
+  return rc == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+int ce_put(parsec_comm_engine_t* ce, parsec_ce_mem_reg_handle_t lreg, ptrdiff_t ldispl, parsec_ce_mem_reg_handle_t rreg, ptrdiff_t rdispl, size_t size, int remote,
+           parsec_ce_onesided_callback_t l_cb, void* l_cb_data, parsec_ce_tag_t r_tag, void* r_cb_data, size_t r_cb_data_size) {
+  return ce_onesided(false, ce, lreg, ldispl, rreg, rdispl, size, remote, l_cb, l_cb_data, r_tag, r_cb_data, r_cb_data_size);
+}
+int ce_get(parsec_comm_engine_t* ce, parsec_ce_mem_reg_handle_t lreg, ptrdiff_t ldispl, parsec_ce_mem_reg_handle_t rreg, ptrdiff_t rdispl, size_t size, int remote,
+           parsec_ce_onesided_callback_t l_cb, void* l_cb_data, parsec_ce_tag_t r_tag, void* r_cb_data, size_t r_cb_data_size) {
+  return ce_onesided(true, ce, lreg, ldispl, rreg, rdispl, size, remote, l_cb, l_cb_data, r_tag, r_cb_data, r_cb_data_size);
+}
+int ce_send_am(parsec_comm_engine_t*, parsec_ce_tag_t tag, int remote, void* addr, size_t size) {
+  CommEngine* ce = comm_engine();
+  const int t = ce_engine_tag(tag);
+  if (!ce || t < 0) return PARSEC_ERROR;
+  return ce->send_am(t, remote, addr, size) == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+int ce_progress(parsec_comm_engine_t*) {
+  // the communication thread progresses the engine; a caller spinning on
+  // progress() only has to yield
+  std::this_thread::yield();
+  return 0;
+}
+int ce_enable(parsec_comm_engine_t*) { return PARSEC_SUCCESS; }
+int ce_disable(parsec_comm_engine_t*) { return PARSEC_SUCCESS; }
+int ce_pack(parsec_comm_engine_t*, void* inbuf, int incount, parsec_datatype_t type, void* outbuf, int outsize, int* position) {
+  CommEngine* ce = comm_engine();
+  return ce && ce->pack(inbuf, incount, type_of(type), outbuf, outsize, position) == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+int ce_pack_size(parsec_comm_engine_t*, int incount, parsec_datatype_t type, int* size) {
+  CommEngine* ce = comm_engine();
+  return ce && ce->pack_size(incount, type_of(type), size) == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+int ce_unpack(parsec_comm_engine_t*, void* inbuf, int insize, int* position, void* outbuf, int outcount, parsec_datatype_t type) {
+  CommEngine* ce = comm_engine();
+  return ce && ce->unpack(inbuf, insize, position, outbuf, outcount, type_of(type)) == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+int ce_sync(parsec_comm_engine_t*) {
+  CommEngine* ce = comm_engine();
+  return ce && ce->sync() == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+int ce_can_serve(parsec_comm_engine_t*) {
+  CommEngine* ce = comm_engine();
+  return ce && ce->can_serve() ? 1 : 0;
+}
+}  // namespace
+
+extern "C" {
+parsec_comm_engine_t parsec_ce = {0, 1, {2, 0}, ce_tag_register, ce_tag_unregister, ce_mem_register, ce_mem_unregister, ce_get_mem_handle_size, ce_mem_retrieve,
+                                  ce_put, ce_get, ce_send_am, ce_progress, ce_enable, ce_disable, ce_pack, ce_pack_size, ce_unpack, ce_sync, ce_can_serve};
+
+parsec_comm_engine_t* parsec_comm_engine_init(parsec_context_t* context) {
+  (void)context;
+  if (comm_size() <= 1) {
+    const char* r = getenv("PARSEC_COMM_RANK");
+    const char* s = getenv("PARSEC_COMM_SIZE");
+    if (!r) r = getenv("RANK");
+    if (!s) s = getenv("WORLD_SIZE");
+    if (r && s && atoi(s) > 1) {
+      const char* job = getenv("PARSEC_COMM_JOB");
+      std::string j = job ? job : (getenv("MASTER_PORT") ? getenv("MASTER_PORT") : "capi");
+      const char* g = getenv("PARSEC_COMM_GPU");
+      if (comm_init(atoi(r), atoi(s), j, g ? atoi(g) : -1) != 0) return nullptr;
+    }
+  }
+  parsec_ce.rank = comm_rank();
+  parsec_ce.size = comm_size();
+  return &parsec_ce;
+}
+
+int parsec_comm_engine_fini(parsec_comm_engine_t* ce) {
+  (void)ce;
+  return PARSEC_SUCCESS;  // the engine lives until parsec_fini / process exit
+}
+
+int parsec_ce_mem_register_device(void* mem, size_t bytes, int device, parsec_ce_mem_reg_handle_t* lreg, size_t* lreg_size) {
+  return ce_register_common(mem, bytes, device, new_type(Datatype::contiguous(1, (int64_t)bytes)), 1, lreg, lreg_size);
+}
+
+int parsec_ce_gpu_device_index(void) {
+  const int g = first_gpu_device_index();
+  return g >= 0 ? g : 2;
+}
+}

@@ -32,6 +32,16 @@ enum CommTag : int {
 
 using AmCallback = std::function<void(int src, int tag, const void* msg, size_t len)>;
 
+// Registration of a memory region for one-sided access (reference
+// parsec_comm_engine.h:72-103 mem_reg_handle): opaque bytes that travel inside
+// active messages; only the engine interprets them.
+struct MemReg {
+  alignas(8) unsigned char b[128];
+};
+// Completion of a one-sided transfer on the calling side (reference
+// parsec_ce_onesided_callback_t): local and remote registrations, offsets, bytes.
+using OneSidedCallback = std::function<void(const MemReg& lreg, ptrdiff_t ldispl, const MemReg& rreg, ptrdiff_t rdispl, size_t size, int remote)>;
+
 struct CommEngine {
   int rank = 0, size = 1;
   virtual ~CommEngine() = default;
@@ -44,6 +54,34 @@ struct CommEngine {
   // Unmap every peer memory region opened by this engine (before the peers
   // free them: a region still mapped elsewhere makes its owner's free block)
   virtual void release_peer_mappings() {}
+
+  // ---- one-sided API (reference parsec_comm_engine.h:72-144). `device` is the
+  // runtime device index of the memory (0: host). A region is described by the
+  // MemReg its owner fills in; user data (datatype handle, count) rides along
+  // for mem_retrieve. get() pulls `size` bytes (0: the whole remote region past
+  // rdispl) of the remote region into the local one, put() pushes local bytes
+  // into the remote region. l_cb runs on the comm thread once the transfer is
+  // complete on this side; the remote side then receives an active message on
+  // `r_tag` carrying r_cb_data (r_tag < 0: no notification). Returns 0 or < 0.
+  virtual int mem_register(void* mem, size_t bytes, int device, int64_t user_dtt, int user_count, MemReg* reg) { (void)mem; (void)bytes; (void)device; (void)user_dtt; (void)user_count; (void)reg; return -1; }
+  virtual int mem_unregister(MemReg* reg) { (void)reg; return -1; }
+  // owner side: the region behind a registration made by this rank
+  virtual int mem_retrieve(const MemReg& reg, void** mem, size_t* bytes, int64_t* user_dtt, int* user_count) { (void)reg; (void)mem; (void)bytes; (void)user_dtt; (void)user_count; return -1; }
+  virtual int get(const MemReg& lreg, ptrdiff_t ldispl, const MemReg& rreg, ptrdiff_t rdispl, size_t size, int remote, OneSidedCallback l_cb, int r_tag,
+                  const void* r_cb_data, size_t r_cb_size) { (void)lreg; (void)ldispl; (void)rreg; (void)rdispl; (void)size; (void)remote; (void)l_cb; (void)r_tag; (void)r_cb_data; (void)r_cb_size; return -1; }
+  virtual int put(const MemReg& lreg, ptrdiff_t ldispl, const MemReg& rreg, ptrdiff_t rdispl, size_t size, int remote, OneSidedCallback l_cb, int r_tag,
+                  const void* r_cb_data, size_t r_cb_size) { (void)lreg; (void)ldispl; (void)rreg; (void)rdispl; (void)size; (void)remote; (void)l_cb; (void)r_tag; (void)r_cb_data; (void)r_cb_size; return -1; }
+  // Pack `incount` elements of `type` from inbuf into outbuf at *position
+  // (advanced), and the inverse; pack_size gives the packed bytes (reference
+  // parsec_ce_pack_fn_t / unpack / pack_size, MPI_Pack semantics).
+  virtual int pack(const void* inbuf, int incount, const Datatype& type, void* outbuf, int outsize, int* position);
+  virtual int unpack(const void* inbuf, int insize, int* position, void* outbuf, int outcount, const Datatype& type);
+  virtual int pack_size(int incount, const Datatype& type, int* size);
+  // Local reshape (reference parsec_ce_reshape_fn_t): dst (layout dst_type) <-
+  // src (layout src_type), through the packed form.
+  virtual int reshape(void* dst, const Datatype& dst_type, const void* src, const Datatype& src_type);
+  // the engine is up and serving requests (reference can_serve)
+  virtual bool can_serve() const { return size > 1; }
 };
 
 // Received data for one flow of a remote activation.

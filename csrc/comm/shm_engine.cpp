@@ -182,6 +182,7 @@ int ShmEngine::init() {
       coll_cv_.notify_all();
     }
   });
+  init_onesided();
   g_engine = this;
   // the comm thread (and the runtime threads created later from this thread)
   // run on the NUMA node of this rank's GPU

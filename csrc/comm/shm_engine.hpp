@@ -49,6 +49,18 @@ class ShmEngine : public CommEngine {
   int sync() override;
   uint64_t allreduce_max(uint64_t v) override;
   void release_peer_mappings() override;
+  // one-sided API (shm_onesided.cpp): device regions move GPU <-> GPU over xGMI
+  // through the IPC mapping of the owner's allocation (one async copy on the GPU's
+  // copy stream); host regions move in ring fragments handled by the owner's
+  // comm thread (TAG_GET_INTERNAL request, TAG_PUT_INTERNAL fragments).
+  int mem_register(void* mem, size_t bytes, int device, int64_t user_dtt, int user_count, MemReg* reg) override;
+  int mem_unregister(MemReg* reg) override;
+  int mem_retrieve(const MemReg& reg, void** mem, size_t* bytes, int64_t* user_dtt, int* user_count) override;
+  int get(const MemReg& lreg, ptrdiff_t ldispl, const MemReg& rreg, ptrdiff_t rdispl, size_t size, int remote, OneSidedCallback l_cb, int r_tag,
+          const void* r_cb_data, size_t r_cb_size) override;
+  int put(const MemReg& lreg, ptrdiff_t ldispl, const MemReg& rreg, ptrdiff_t rdispl, size_t size, int remote, OneSidedCallback l_cb, int r_tag,
+          const void* r_cb_data, size_t r_cb_size) override;
+  bool can_serve() const override { return me_ != nullptr; }
   void post(std::function<void()> fn);  // run on the comm thread
   bool on_comm_thread() const { return std::this_thread::get_id() == thread_id_; }
   // remote_dep_on / off: a context is running taskpools (poll for latency) or
@@ -142,6 +154,34 @@ class ShmEngine : public CommEngine {
   std::mutex ipc_m_;  // ipc_exported_ / ipc_opened_ (exports happen on worker threads too)
   std::map<std::pair<int, std::string>, void*> ipc_opened_;                    // (src, handle) -> base
   int init_ipc();
+  // one-sided: this rank's registrations and the gets waiting for fragments
+  struct Region {
+    void* ptr;
+    size_t bytes;
+    int device;
+    int64_t user_dtt;
+    int user_count;
+  };
+  struct PendingGet {
+    MemReg lreg, rreg;
+    ptrdiff_t ldispl, rdispl;
+    size_t size, received;
+    char* dst;
+    int dst_device;
+    std::vector<char> staging;  // device destination: fragments land here first
+    OneSidedCallback l_cb;
+    int r_tag;
+    std::vector<char> r_cb_data;
+  };
+  std::mutex reg_m_;
+  std::map<uint32_t, Region> regions_;
+  uint32_t next_region_ = 1;
+  std::map<uint64_t, PendingGet> gets_;  // comm thread only
+  uint64_t next_get_ = 1;
+  void init_onesided();
+  void notify_remote(int remote, int r_tag, const std::vector<char>& data);
+  void send_region_fragments(int dst, uint32_t kind, uint32_t region, uint64_t req, const char* src, size_t size, uint64_t dst_off, int r_tag,
+                             const std::vector<char>& r_cb_data);
   // RCCL
   bool rccl_ok_ = false;
   std::vector<void*> send_comm_, recv_comm_;  // ncclComm_t per peer

@@ -301,6 +301,61 @@ int parsec_profiling_trace(int key, uint64_t event_id, uint32_t taskpool_id, con
 int parsec_profiling_dump(void);
 int parsec_profiling_reset(void);
 
+/* --------------------------------------------------- communication engine
+ * (reference parsec/parsec_comm_engine.h:22-186). Active messages on user tags
+ * 0..15, and one-sided get / put on registered memory: host regions travel in
+ * shared-memory ring fragments served by the owner's comm thread, GPU regions
+ * (parsec_ce_mem_register_device) GPU to GPU over xGMI through HIP IPC.
+ * Callbacks run on the communication thread; r_tag of get / put is an AM tag
+ * of the remote side (its callback receives r_cb_data once the transfer is
+ * complete), not a function address. progress() is a no-op while the
+ * communication thread runs. */
+typedef uint64_t parsec_ce_tag_t;
+typedef void* parsec_ce_mem_reg_handle_t;
+typedef enum { PARSEC_MEM_TYPE_CONTIGUOUS = 0, PARSEC_MEM_TYPE_NONCONTIGUOUS = 1 } parsec_mem_type_t;
+typedef struct parsec_comm_engine_s parsec_comm_engine_t;
+typedef int (*parsec_ce_am_callback_t)(parsec_comm_engine_t* ce, parsec_ce_tag_t tag, void* msg, size_t msg_size, int src, void* cb_data);
+typedef int (*parsec_ce_onesided_callback_t)(parsec_comm_engine_t* ce, parsec_ce_mem_reg_handle_t lreg, ptrdiff_t ldispl, parsec_ce_mem_reg_handle_t rreg,
+                                             ptrdiff_t rdispl, size_t size, int remote, void* cb_data);
+typedef int (*parsec_ce_onesided_fn_t)(parsec_comm_engine_t* ce, parsec_ce_mem_reg_handle_t lreg, ptrdiff_t ldispl, parsec_ce_mem_reg_handle_t rreg,
+                                       ptrdiff_t rdispl, size_t size, int remote, parsec_ce_onesided_callback_t l_cb, void* l_cb_data, parsec_ce_tag_t r_tag,
+                                       void* r_cb_data, size_t r_cb_data_size);
+typedef struct {
+    int sided;                            /* 2: one-sided emulated over active messages */
+    int supports_noncontiguous_datatype;  /* 0: registrations are byte ranges */
+} parsec_ce_capabilities_t;
+struct parsec_comm_engine_s {
+    int rank, size;
+    parsec_ce_capabilities_t capabilites; /* (sic) the reference's spelling */
+    int (*tag_register)(parsec_ce_tag_t tag, parsec_ce_am_callback_t cb, void* cb_data, size_t msg_length);
+    int (*tag_unregister)(parsec_ce_tag_t tag);
+    int (*mem_register)(void* mem, parsec_mem_type_t mem_type, size_t count, parsec_datatype_t datatype, size_t mem_size,
+                        parsec_ce_mem_reg_handle_t* lreg, size_t* lreg_size);
+    int (*mem_unregister)(parsec_ce_mem_reg_handle_t* lreg);
+    int (*get_mem_handle_size)(void);
+    int (*mem_retrieve)(parsec_ce_mem_reg_handle_t lreg, void** mem, parsec_datatype_t* datatype, int* count);
+    parsec_ce_onesided_fn_t put;
+    parsec_ce_onesided_fn_t get;
+    int (*send_am)(parsec_comm_engine_t* ce, parsec_ce_tag_t tag, int remote, void* addr, size_t size);
+    int (*progress)(parsec_comm_engine_t* ce);
+    int (*enable)(parsec_comm_engine_t* ce);
+    int (*disable)(parsec_comm_engine_t* ce);
+    int (*pack)(parsec_comm_engine_t* ce, void* inbuf, int incount, parsec_datatype_t type, void* outbuf, int outsize, int* position);
+    int (*pack_size)(parsec_comm_engine_t* ce, int incount, parsec_datatype_t type, int* size);
+    int (*unpack)(parsec_comm_engine_t* ce, void* inbuf, int insize, int* position, void* outbuf, int outcount, parsec_datatype_t type);
+    int (*sync)(parsec_comm_engine_t* ce);
+    int (*can_serve)(parsec_comm_engine_t* ce);
+};
+extern parsec_comm_engine_t parsec_ce;
+/* joins the multi-process job from PARSEC_COMM_RANK / _SIZE / _JOB when no
+ * context did (the reference's test calls it without parsec_init) */
+parsec_comm_engine_t* parsec_comm_engine_init(parsec_context_t* context);
+int parsec_comm_engine_fini(parsec_comm_engine_t* ce);
+/* register `bytes` of memory of runtime device `device` (0: host) */
+int parsec_ce_mem_register_device(void* mem, size_t bytes, int device, parsec_ce_mem_reg_handle_t* lreg, size_t* lreg_size);
+/* runtime device index of this process's GPU (2, the first accelerator, when no context registered devices) */
+int parsec_ce_gpu_device_index(void);
+
 /* ---------------------------------------------------------------- version */
 int parsec_version(int* version_major, int* version_minor, int* version_release);
 int parsec_version_ex(size_t len, char* version_string);

@@ -39,6 +39,7 @@ CORE_SOURCES = [
     "csrc/prof/ptg_to_dtd.cpp",
     "csrc/comm/remote_dep.cpp",
     "csrc/comm/shm_engine.cpp",
+    "csrc/comm/shm_onesided.cpp",
     "csrc/comm/fourcounter.cpp",
     "csrc/ptg/ptg.cpp",
     "csrc/dtd/dtd.cpp",

@@ -1,0 +1,265 @@
+/* The communication engine API from C: port of the reference's
+ * tests/dsl/dtd/dtd_test_ce.c (active messages both ways, a GET 1 <- 0 and a
+ * PUT 0 -> 1 on registered memory, completion notifications through AM tags),
+ * plus pack / unpack. Two ranks (parsec_amd.launch -n 2). With "gpu" as the
+ * first argument the registered buffers live in GPU memory (hipMalloc) and the
+ * one-sided transfers go GPU to GPU through HIP IPC; PARSEC_COMM_GPU selects
+ * the device. Differences from the reference: r_tag of get / put is an AM tag
+ * (the reference's MPI engine takes a callback address); values are checked. */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef CE_WITH_HIP
+#include <hip/hip_runtime_api.h>
+#endif
+
+#include "parsec.h"
+
+#define AM_FROM_0_TAG 2
+#define AM_FROM_1_TAG 3
+#define NOTIFY_GET_TAG 4
+#define NOTIFY_PUT_TAG 5
+#define MEM_HANDLE_FROM_1_TAG 6
+#define GET_END_ACK_TAG 7
+#define PUT_END_ACK_TAG 8
+#define N 4096 /* ints per buffer: 16 KB, several ring fragments at most */
+
+static volatile int counter = 0;
+static int my_rank, use_gpu = 0, bad = 0;
+
+static void* buf_alloc(size_t bytes) {
+#ifdef CE_WITH_HIP
+    if (use_gpu) {
+        void* p = NULL;
+        if (hipMalloc(&p, bytes < (4u << 20) ? (4u << 20) : bytes) != hipSuccess) return NULL; /* >= 2 MB: IPC-exportable */
+        return p;
+    }
+#endif
+    return malloc(bytes);
+}
+static void buf_free(void* p) {
+#ifdef CE_WITH_HIP
+    if (use_gpu) { hipFree(p); return; }
+#endif
+    free(p);
+}
+static void buf_write(void* dst, const int* src, size_t n) {
+#ifdef CE_WITH_HIP
+    if (use_gpu) { hipMemcpy(dst, src, n * sizeof(int), hipMemcpyHostToDevice); return; }
+#endif
+    memcpy(dst, src, n * sizeof(int));
+}
+static void buf_read(int* dst, const void* src, size_t n) {
+#ifdef CE_WITH_HIP
+    if (use_gpu) { hipMemcpy(dst, src, n * sizeof(int), hipMemcpyDeviceToHost); return; }
+#endif
+    memcpy(dst, src, n * sizeof(int));
+}
+static int reg(void* mem, size_t bytes, parsec_ce_mem_reg_handle_t* h, size_t* hs) {
+    if (use_gpu) return parsec_ce_mem_register_device(mem, bytes, parsec_ce_gpu_device_index(), h, hs);
+    return parsec_ce.mem_register(mem, PARSEC_MEM_TYPE_CONTIGUOUS, 1, PARSEC_DATATYPE_NULL, bytes, h, hs);
+}
+static int check(const void* mem, int mult, const char* what) {
+    int* h = malloc(N * sizeof(int));
+    buf_read(h, mem, N);
+    int ok = 1;
+    for (int i = 0; i < N; i++) if (h[i] != i * mult) { ok = 0; break; }
+    printf("[%d] %s %s\n", my_rank, what, ok ? "ok" : "WRONG");
+    free(h);
+    if (!ok) bad++;
+    return ok;
+}
+
+static int am_ints(parsec_comm_engine_t* ce, parsec_ce_tag_t tag, void* msg, size_t size, int src, void* cb_data) {
+    (void)ce; (void)tag; (void)src; (void)cb_data;
+    const int* v = (const int*)msg;
+    if (size != 3 * sizeof(int) || v[0] != 10 || v[1] != 11 || v[2] != 12) bad++;
+    counter++;
+    return 1;
+}
+static int am_floats(parsec_comm_engine_t* ce, parsec_ce_tag_t tag, void* msg, size_t size, int src, void* cb_data) {
+    (void)ce; (void)tag; (void)src; (void)cb_data;
+    const float* v = (const float*)msg;
+    if (size != 2 * sizeof(float) || v[0] != 9.5f || v[1] != 19.5f) bad++;
+    counter++;
+    return 1;
+}
+
+/* ---- GET: 1 pulls from 0 */
+static int get_end(parsec_comm_engine_t* ce, parsec_ce_mem_reg_handle_t lreg, ptrdiff_t ldispl, parsec_ce_mem_reg_handle_t rreg, ptrdiff_t rdispl,
+                   size_t size, int remote, void* cb_data) {
+    (void)ldispl; (void)rreg; (void)rdispl; (void)remote; (void)cb_data;
+    void* mem;
+    parsec_datatype_t dtt;
+    int count, bytes;
+    ce->mem_retrieve(lreg, &mem, &dtt, &count);
+    parsec_type_size(dtt, &bytes);
+    if (size != N * sizeof(int) || bytes != (int)size) bad++;
+    check(mem, 1, "GET");
+    ce->mem_unregister(&lreg);
+    buf_free(mem);
+    counter++;
+    return 1;
+}
+static int notify_get(parsec_comm_engine_t* ce, parsec_ce_tag_t tag, void* msg, size_t size, int src, void* cb_data) {
+    (void)tag; (void)size; (void)cb_data;
+    /* msg = rank 0's handle; register a receive buffer and pull */
+    void* rbuf = buf_alloc(N * sizeof(int));
+    parsec_ce_mem_reg_handle_t mine;
+    size_t hs;
+    reg(rbuf, N * sizeof(int), &mine, &hs);
+    ce->get(ce, mine, 0, (parsec_ce_mem_reg_handle_t)msg, 0, 0, src, get_end, NULL, GET_END_ACK_TAG, msg, (size_t)ce->get_mem_handle_size());
+    counter++;
+    return 1;
+}
+static int get_end_ack(parsec_comm_engine_t* ce, parsec_ce_tag_t tag, void* msg, size_t size, int src, void* cb_data) {
+    (void)tag; (void)size; (void)src; (void)cb_data;
+    /* back on rank 0 with its own handle: release the source buffer */
+    void* mem;
+    ce->mem_retrieve((parsec_ce_mem_reg_handle_t)msg, &mem, NULL, NULL);
+    buf_free(mem);
+    counter++;
+    return 1;
+}
+
+/* ---- PUT: 0 pushes into 1 */
+static parsec_ce_mem_reg_handle_t put_src_handle; /* rank 0 */
+static int notify_put(parsec_comm_engine_t* ce, parsec_ce_tag_t tag, void* msg, size_t size, int src, void* cb_data) {
+    (void)tag; (void)size; (void)cb_data;
+    const int hs0 = ce->get_mem_handle_size();
+    void* rbuf = buf_alloc(N * sizeof(int));
+    parsec_ce_mem_reg_handle_t mine;
+    size_t hs;
+    reg(rbuf, N * sizeof(int), &mine, &hs);
+    char* reply = malloc(2 * (size_t)hs0);
+    memcpy(reply, msg, (size_t)hs0);                  /* 0's handle */
+    memcpy(reply + hs0, mine, (size_t)hs0);           /* 1's handle */
+    ce->send_am(ce, MEM_HANDLE_FROM_1_TAG, src, reply, 2 * (size_t)hs0);
+    free(reply);
+    counter++;
+    return 1;
+}
+static int put_end(parsec_comm_engine_t* ce, parsec_ce_mem_reg_handle_t lreg, ptrdiff_t ldispl, parsec_ce_mem_reg_handle_t rreg, ptrdiff_t rdispl,
+                   size_t size, int remote, void* cb_data) {
+    (void)ldispl; (void)rreg; (void)rdispl; (void)remote; (void)cb_data;
+    if (size != N * sizeof(int)) bad++;
+    void* mem;
+    ce->mem_retrieve(lreg, &mem, NULL, NULL);
+    ce->mem_unregister(&put_src_handle);
+    buf_free(mem);
+    counter++;
+    return 1;
+}
+static int handles_from_1(parsec_comm_engine_t* ce, parsec_ce_tag_t tag, void* msg, size_t size, int src, void* cb_data) {
+    (void)tag; (void)size; (void)cb_data;
+    const int hs = ce->get_mem_handle_size();
+    parsec_ce_mem_reg_handle_t theirs = (char*)msg + hs;
+    ce->put(ce, put_src_handle, 0, theirs, 0, 0, src, put_end, NULL, PUT_END_ACK_TAG, theirs, (size_t)hs);
+    counter++;
+    return 1;
+}
+static int put_end_ack(parsec_comm_engine_t* ce, parsec_ce_tag_t tag, void* msg, size_t size, int src, void* cb_data) {
+    (void)tag; (void)size; (void)src; (void)cb_data;
+    void* mem;
+    parsec_ce_mem_reg_handle_t h = (parsec_ce_mem_reg_handle_t)msg;
+    ce->mem_retrieve(h, &mem, NULL, NULL);
+    check(mem, 2, "PUT");
+    buf_free(mem);
+    counter++;
+    return 1;
+}
+
+static void wait_for(int n) {
+    while (counter < n) parsec_ce.progress(&parsec_ce);
+}
+
+int main(int argc, char** argv) {
+    use_gpu = argc > 1 && strcmp(argv[1], "gpu") == 0;
+    parsec_comm_engine_t* ce = parsec_comm_engine_init(NULL);
+    if (!ce || ce->size != 2) {
+        printf("needs 2 ranks\n");
+        return 1;
+    }
+    my_rank = ce->rank;
+    ce->tag_register(AM_FROM_0_TAG, am_ints, ce, 4096);
+    ce->tag_register(AM_FROM_1_TAG, am_floats, ce, 4096);
+    ce->tag_register(NOTIFY_GET_TAG, notify_get, ce, 4096);
+    ce->tag_register(NOTIFY_PUT_TAG, notify_put, ce, 4096);
+    ce->tag_register(MEM_HANDLE_FROM_1_TAG, handles_from_1, ce, 4096);
+    ce->tag_register(GET_END_ACK_TAG, get_end_ack, ce, 4096);
+    ce->tag_register(PUT_END_ACK_TAG, put_end_ack, ce, 4096);
+    ce->sync(ce); /* every tag registered everywhere */
+
+    /* active messages: 0 -> 1 twice, 1 -> 0 twice */
+    if (my_rank == 0) {
+        int v[3] = {10, 11, 12};
+        ce->send_am(ce, AM_FROM_0_TAG, 1, v, sizeof(v));
+        ce->send_am(ce, AM_FROM_0_TAG, 1, v, sizeof(v));
+    } else {
+        float f[2] = {9.5f, 19.5f};
+        ce->send_am(ce, AM_FROM_1_TAG, 0, f, sizeof(f));
+        ce->send_am(ce, AM_FROM_1_TAG, 0, f, sizeof(f));
+    }
+    wait_for(2);
+    ce->sync(ce);
+    counter = 0;
+
+    /* GET: 0 registers, tells 1; 1 pulls (get_end) and acknowledges (get_end_ack on 0) */
+    if (my_rank == 0) {
+        int* h = malloc(N * sizeof(int));
+        for (int i = 0; i < N; i++) h[i] = i;
+        void* sbuf = buf_alloc(N * sizeof(int));
+        buf_write(sbuf, h, N);
+        free(h);
+        parsec_ce_mem_reg_handle_t mine;
+        size_t hs;
+        reg(sbuf, N * sizeof(int), &mine, &hs);
+        ce->send_am(ce, NOTIFY_GET_TAG, 1, mine, hs);
+        wait_for(1);
+        ce->mem_unregister(&mine);
+    } else {
+        wait_for(2);
+    }
+    ce->sync(ce);
+    counter = 0;
+
+    /* PUT: 0 tells 1, 1 answers with both handles, 0 pushes (put_end), 1 checks (put_end_ack) */
+    if (my_rank == 0) {
+        int* h = malloc(N * sizeof(int));
+        for (int i = 0; i < N; i++) h[i] = 2 * i;
+        void* sbuf = buf_alloc(N * sizeof(int));
+        buf_write(sbuf, h, N);
+        free(h);
+        size_t hs;
+        reg(sbuf, N * sizeof(int), &put_src_handle, &hs);
+        ce->send_am(ce, NOTIFY_PUT_TAG, 1, put_src_handle, hs);
+        wait_for(2);
+    } else {
+        wait_for(2);
+    }
+    ce->sync(ce);
+
+    /* pack / unpack: the lower triangle of a 4 x 4 column-major matrix */
+    {
+        parsec_datatype_t lower, dbl;
+        parsec_type_create_contiguous(1, parsec_datatype_double_t, &dbl);
+        parsec_type_create_lower(4, 4, 1, parsec_datatype_double_t, &lower);
+        double a[16], b[16] = {0};
+        for (int i = 0; i < 16; i++) a[i] = i + 1;
+        int psize = 0, pos = 0, upos = 0;
+        ce->pack_size(ce, 1, lower, &psize);
+        char* packed = malloc((size_t)psize);
+        if (psize != 10 * (int)sizeof(double) || ce->pack(ce, a, 1, lower, packed, psize, &pos) != 0 || pos != psize) bad++;
+        if (ce->unpack(ce, packed, psize, &upos, b, 1, lower) != 0 || upos != psize) bad++;
+        for (int c = 0; c < 4; c++)
+            for (int r = 0; r < 4; r++)
+                if (b[r + 4 * c] != (r >= c ? a[r + 4 * c] : 0.0)) bad++;
+        free(packed);
+        (void)dbl;
+    }
+    printf("[%d] ce %s (can_serve %d)\n", my_rank, bad ? "FAILED" : "ok", ce->can_serve(ce));
+    ce->sync(ce);
+    parsec_comm_engine_fini(ce);
+    return bad ? 1 : 0;
+}

@@ -119,3 +119,27 @@ def test_dynamic_termdet_multiprocess(tmp_path):
     assert rc == 0, outs
     assert "root 2080" in outs[0][0]
     assert sum(int(o.split("nodes")[1].split()[0]) for o, _ in outs) == 63
+
+
+def _build_ce(tmp_path, gpu=False):
+    exe = tmp_path / ("ce_capi_gpu" if gpu else "ce_capi")
+    cmd = ["gcc", "-std=c99", "-Wall", "-Wextra", "-O1", f"-I{ROOT}/include", os.path.join(HERE, "capi", "ce_capi.c"), "-o", str(exe),
+           f"-L{ROOT}/parsec_amd/lib", "-lparsec_amd", f"-Wl,-rpath,{ROOT}/parsec_amd/lib", "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+    if gpu:
+        cmd[1:1] = ["-DCE_WITH_HIP", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
+    else:
+        cmd.insert(1, "-Werror")
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return str(exe)
+
+
+def test_comm_engine_c_program(tmp_path, pa):
+    """The communication-engine vtable from C (port of the reference's
+    tests/dsl/dtd/dtd_test_ce.c): active messages both ways, a GET and a PUT on
+    registered host memory with AM completion notices, pack / unpack."""
+    exe = _build_ce(tmp_path)
+    rc, outs = launch.launch(2, [exe], timeout=120, capture=True)
+    assert rc == 0, outs
+    text = "".join(o for o, _ in outs)
+    assert text.count("ce ok") == 2 and "[1] GET ok" in text and "[1] PUT ok" in text, text

@@ -97,3 +97,25 @@ def test_stencil_four_ranks_ipc(pa):
     _gpu()
     for rc, out in _run("stencil", 4, 48, 40, 36, 16, 6):
         assert rc == 0, out
+
+
+def test_comm_engine_c_program_gpu_memory(tmp_path, pa):
+    """CE get / put between GPU buffers of two processes (both on GPU 0): the
+    registrations export the allocations through HIP IPC and every transfer is
+    one device copy on the copy stream (ports dtd_test_ce.c to device memory)."""
+    import subprocess
+
+    from parsec_amd import launch
+
+    _gpu()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "ce_capi_gpu")
+    cmd = ["gcc", "-std=c99", "-O1", "-DCE_WITH_HIP", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", f"-I{root}/include",
+           os.path.join(root, "tests", "capi", "ce_capi.c"), "-o", exe, f"-L{root}/parsec_amd/lib", "-lparsec_amd",
+           f"-Wl,-rpath,{root}/parsec_amd/lib", "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    rc, outs = launch.launch(2, [exe, "gpu"], timeout=120, capture=True, env={"PARSEC_COMM_GPU": "0"})
+    assert rc == 0, outs
+    text = "".join(o for o, _ in outs)
+    assert text.count("ce ok") == 2 and "[1] GET ok" in text and "[1] PUT ok" in text, text
