@@ -282,6 +282,8 @@ def main():
         if gpu_stats:
             out["gpu_kernel_launches"] = gpu_stats[0]["kernel_launches"]
             out["gpu_tasks"] = gpu_stats[0]["executed_tasks"]
+            if os.environ.get("PARSEC_BENCH_VERBOSE"):
+                out["manager_ms"] = {k: round(gpu_stats[0][k], 2) for k in ("ms_complete", "ms_complete_max", "ms_launch")}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -767,6 +767,7 @@ struct CeTagSlot {
   void* cb_data = nullptr;
 };
 CeTagSlot g_ce_tags[TAG_MAX - TAG_USER];
+bool g_ce_owns_engine = false;  // parsec_comm_engine_init started the engine
 
 int ce_engine_tag(parsec_ce_tag_t tag) { return tag < (parsec_ce_tag_t)(TAG_MAX - TAG_USER) ? TAG_USER + (int)tag : -1; }
 
@@ -914,6 +915,7 @@ parsec_comm_engine_t* parsec_comm_engine_init(parsec_context_t* context) {
       std::string j = job ? job : (getenv("MASTER_PORT") ? getenv("MASTER_PORT") : "capi");
       const char* g = getenv("PARSEC_COMM_GPU");
       if (comm_init(atoi(r), atoi(s), j, g ? atoi(g) : -1) != 0) return nullptr;
+      g_ce_owns_engine = true;
     }
   }
   parsec_ce.rank = comm_rank();
@@ -923,7 +925,13 @@ parsec_comm_engine_t* parsec_comm_engine_init(parsec_context_t* context) {
 
 int parsec_comm_engine_fini(parsec_comm_engine_t* ce) {
   (void)ce;
-  return PARSEC_SUCCESS;  // the engine lives until parsec_fini / process exit
+  // an engine brought up here (no parsec_init) goes away here: barrier, then
+  // its shared-memory segments are unlinked; a context's engine lives until parsec_fini
+  if (g_ce_owns_engine) {
+    comm_fini();
+    g_ce_owns_engine = false;
+  }
+  return PARSEC_SUCCESS;
 }
 
 int parsec_ce_mem_register_device(void* mem, size_t bytes, int device, parsec_ce_mem_reg_handle_t* lreg, size_t* lreg_size) {

@@ -471,6 +471,9 @@ struct DeviceStats {
   std::atomic<uint64_t> data_faults{0};
   std::atomic<uint64_t> kernel_launches{0}, batched_tasks{0};
   std::atomic<uint64_t> w2r_tasks{0}, prefetches{0};
+  // GPU manager thread: time (ns) spent retiring completed kernel groups
+  // (epilog + dependency release) and the longest single retirement pass
+  std::atomic<uint64_t> ns_complete{0}, ns_complete_max{0}, ns_launch{0};
 };
 
 // data_advise (reference device.c parsec_advise_data_on_device, PARSEC_DEV_DATA_ADVICE_*)

@@ -946,7 +946,7 @@ void HipDevice::execute_ready() {
     // a CU partition (reserved_cus) it would crowd the few critical CUs, and
     // without one it would queue behind the critical kernels.
     const bool crit = t->priority >= critical_threshold;
-    if (nb_exec_streams == 1 || (crit && (cu_masked || nb_exec_streams == 2)) || (!cu_masked && nb_exec_streams >= 3 && hp)) {
+    if (nb_exec_streams == 1 || crit || (hp && hp_on_critical && !cu_masked)) {
       s = 0;
     } else if (hp || crit) {
       s = -1;
@@ -1171,8 +1171,15 @@ bool HipDevice::progress() {
     }
     staging.swap(keep);
   }
-  if (!ready.empty()) { execute_ready(); did = true; }
+  if (!ready.empty()) {
+    const uint64_t t0 = now_ns();
+    execute_ready();
+    stats.ns_launch.fetch_add(now_ns() - t0, std::memory_order_relaxed);
+    did = true;
+  }
   // kernels done?
+  const uint64_t tc0 = now_ns();
+  bool retired = false;
   for (int s = 0; s < (int)executing.size(); ++s) {
     auto& q = executing[s];
     while (!q.empty()) {
@@ -1229,7 +1236,13 @@ bool HipDevice::progress() {
       }
       flush_completions();
       did = true;
+      retired = true;
     }
+  }
+  if (retired) {
+    const uint64_t dt = now_ns() - tc0;
+    stats.ns_complete.fetch_add(dt, std::memory_order_relaxed);
+    if (dt > stats.ns_complete_max.load(std::memory_order_relaxed)) stats.ns_complete_max.store(dt, std::memory_order_relaxed);
   }
   while (!popping.empty()) {
     GpuTask* g = popping.front();
@@ -1303,6 +1316,7 @@ void hip_devices_init(Context* ctx) {
   int crit = (int)params.reg_int("device", "hip", "critical_threshold", "Task priority at or above which a completed GPU task is released by the manager itself (critical path)", 1 << 29);
   int rcus = (int)params.reg_int("device", "hip", "reserved_cus", "CUs the bulk streams leave free for the critical stream (CU mask on the bulk streams; 0 = none)", 0);
   int rstride = (int)params.reg_int("device", "hip", "reserved_cus_stride", "Spacing of the reserved CU ids in the CU mask", 1);
+  const bool hp_crit = params.reg_int("device", "hip", "hp_on_critical_stream", "High-priority tasks below the critical threshold share the critical stream (1) or go to the least loaded bulk stream (0)", 0) != 0;
   const bool wprio = params.reg_int("device", "hip", "wave_priority", "Kernels of the critical stream raise their waves' issue priority (s_setprio) over co-resident bulk waves", 1) != 0;
   const bool trace = params.reg_int("device", "hip", "trace_launches", "Print every launched kernel group (stream, tasks, batch sizes) to stderr", 0) != 0;
   const bool cow = params.reg_int("device", "hip", "complete_on_workers", "Release completed GPU tasks (successor activation) on the compute threads instead of the manager (measured no faster on DPOTRF; breaks the multi-rank DTD stencil: off)", 0) != 0;
@@ -1330,6 +1344,7 @@ void hip_devices_init(Context* ctx) {
     d->reserved_cus = rcus;
     d->reserved_stride = rstride;
     d->wave_priority = wprio;
+    d->hp_on_critical = hp_crit;
     d->max_inflight_groups = maxg;
     d->sort_pending = sortp != 0;
     d->complete_on_workers = cow;

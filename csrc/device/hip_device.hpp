@@ -136,6 +136,7 @@ struct HipDevice : Device {
   int reserved_cus = 0;
   int reserved_stride = 1;
   bool wave_priority = true;
+  bool hp_on_critical = false;
   bool cu_masked = false;
   bool batching = true;
   bool sort_pending = true;

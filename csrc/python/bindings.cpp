@@ -604,6 +604,9 @@ PYBIND11_MODULE(_C, m) {
       e["gflops_fp64"] = d->gflops_fp64;
       e["weight"] = d->gflops_weight;
       e["executed_tasks"] = d->stats.executed_tasks.load();
+      e["ms_complete"] = d->stats.ns_complete.load() / 1e6;
+      e["ms_complete_max"] = d->stats.ns_complete_max.load() / 1e6;
+      e["ms_launch"] = d->stats.ns_launch.load() / 1e6;
       e["kernel_launches"] = d->stats.kernel_launches.load();
       e["batched_tasks"] = d->stats.batched_tasks.load();
       e["bytes_in"] = d->stats.bytes_in.load();

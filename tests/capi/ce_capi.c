@@ -27,6 +27,8 @@
 
 static volatile int counter = 0;
 static int my_rank, use_gpu = 0, bad = 0;
+/* callbacks run on the communication thread, concurrently with main(): counter
+ * is reset before each barrier, never after it */
 
 static void* buf_alloc(size_t bytes) {
 #ifdef CE_WITH_HIP
@@ -202,8 +204,8 @@ int main(int argc, char** argv) {
         ce->send_am(ce, AM_FROM_1_TAG, 0, f, sizeof(f));
     }
     wait_for(2);
+    counter = 0; /* before the barrier: the peer's next messages may arrive right after it */
     ce->sync(ce);
-    counter = 0;
 
     /* GET: 0 registers, tells 1; 1 pulls (get_end) and acknowledges (get_end_ack on 0) */
     if (my_rank == 0) {
@@ -221,8 +223,8 @@ int main(int argc, char** argv) {
     } else {
         wait_for(2);
     }
-    ce->sync(ce);
     counter = 0;
+    ce->sync(ce);
 
     /* PUT: 0 tells 1, 1 answers with both handles, 0 pushes (put_end), 1 checks (put_end_ack) */
     if (my_rank == 0) {
