@@ -149,7 +149,7 @@ std::atomic<uint64_t> g_next_id{1};
 // (flow, payload) on each side, with peer and byte count (reference
 // remote_dep.h:374-415 MPI_DATA_PLD_SND / RCV, checked by check-comms.py)
 ProfilingStream* g_comm_prof = nullptr;
-int k_snd_b = -1, k_snd_e = -1, k_rcv_b = -1, k_rcv_e = -1, k_act_b = -1, k_act_e = -1;
+int k_snd_b = -1, k_snd_e = -1, k_rcv_b = -1, k_rcv_e = -1, k_act_b = -1, k_act_e = -1, k_pull_b = -1, k_pull_e = -1;
 enum : int32_t { PLANE_HOST = 0, PLANE_IPC = 1, PLANE_RCCL = 2 };
 struct CommInfo {
   int32_t peer, flow;
@@ -162,6 +162,8 @@ void comm_trace_init() {
   profiling_add_dictionary_keyword("COMM_DATA_SND", "fill:#0077FF", sizeof(CommInfo), desc, &k_snd_b, &k_snd_e);
   profiling_add_dictionary_keyword("COMM_DATA_RCV", "fill:#00BB44", sizeof(CommInfo), desc, &k_rcv_b, &k_rcv_e);
   profiling_add_dictionary_keyword("COMM_ACTIVATE", "fill:#AA00AA", sizeof(CommInfo), desc, &k_act_b, &k_act_e);
+  // the device copy of an IPC pull alone: issued on the copy stream -> landed
+  profiling_add_dictionary_keyword("COMM_IPC_PULL", "fill:#FFAA00", sizeof(CommInfo), desc, &k_pull_b, &k_pull_e);
   g_comm_prof = profiling_stream_create("comm");
 }
 inline void comm_trace(int key, uint64_t id, uint32_t tp, const CommInfo* info) {
@@ -548,7 +550,12 @@ void pull_ipc(int src, RecvState* r, uint32_t f, const char* handle, uint64_t of
   const uint64_t rid = r->id;
   const uint64_t bytes = r->fd[f].bytes;
   const char* srcp = base + offset;
+  if (g_comm_prof) {
+    CommInfo ci{src, (int32_t)f, (int64_t)bytes, 1, 0};
+    comm_trace(k_pull_b, flow_event(rid, f), r->hdr.tp_id, &ci);
+  }
   g_ce->ipc_copy(src, c->device_private, srcp, bytes, [rid, sid, f, src, bytes, want, c, srcp] {
+    comm_trace(k_pull_e, flow_event(rid, f), 0, nullptr);
     if (g_ipc_verify && want) {
       uint64_t got = debug_checksum(c->device_index, c->device_private, bytes);
       if (got != want) {
@@ -645,7 +652,11 @@ void deliver(RecvState* r) {
   // forward down the broadcast trees first (children fetch from us)
   send_activations(tp, r->hdr, r->hdr.root, r->fd, r->ranks, r->data, r->extra);
   ExecutionStream* es = g_comm_es ? g_comm_es : (tp->context ? tp->context->all_es[0] : nullptr);
+  // reference remote_dep_mpi.c:1838,1887: the activation callback of a received
+  // remote dependency, bracketed for PINS modules (task_profiler traces it)
+  PARSEC_PINS(es, PINS_ACTIVATE_CB_BEGIN, nullptr);
   tp->on_remote_activation(es, act);
+  PARSEC_PINS(es, PINS_ACTIVATE_CB_END, nullptr);
   tp->tdm->incoming_message_end(tp);
   for (auto*& c : r->data) if (c) { data_copy_release(c); c = nullptr; }
   tp->tdm->taskpool_addto_runtime_actions(tp, -1);
@@ -771,6 +782,7 @@ void remote_dep_init(Context* ctx) {
     es->th_id = 2000;
     es->slot = -1;
     ctx->aux_es.push_back(es);
+    es->prof = g_comm_prof;  // PINS events of the comm thread (ACTIVATE_CB) land in its trace stream
     g_comm_es = es;
     g_ce->post([es] { es->slot = thread_slot(); set_my_execution_stream(es); });
   }

@@ -9,6 +9,8 @@
 #include <cstring>
 #include <fstream>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "../prof/profiling.hpp"
 
 namespace parsec {
@@ -438,6 +440,40 @@ void HipDevice::trace_group(int s, const ExecGroup& g) {
   profiling_trace_at(trace_streams[s], trace_key_e, id, tp, trace_ref_ns + (uint64_t)((double)e * 1e6), nullptr, 0);
 }
 
+hipEvent_t HipDevice::copy_span_begin() {
+  if (!gpu_trace) return nullptr;
+  hipEvent_t b = get_timing_event();
+  PARSEC_HIP_CHECK(hipEventRecord(b, s_copy));
+  return b;
+}
+
+void HipDevice::copy_span_end(hipEvent_t b, int key, uint64_t bytes, int src_dev, int dst_dev) {
+  if (!b) return;
+  hipEvent_t e = get_timing_event();
+  PARSEC_HIP_CHECK(hipEventRecord(e, s_copy));
+  copy_spans.push_back(CopySpan{b, e, key, bytes, src_dev, dst_dev});
+}
+
+void HipDevice::progress_copy_spans() {
+  while (!copy_spans.empty()) {
+    CopySpan& c = copy_spans.front();
+    if (hipEventQuery(c.e) == hipErrorNotReady) break;
+    float tb = 0.f, te = 0.f;
+    if (hipEventElapsedTime(&tb, trace_ref, c.b) == hipSuccess && hipEventElapsedTime(&te, trace_ref, c.e) == hipSuccess) {
+      if (!trace_copy_stream) trace_copy_stream = profiling_stream_create(name + " copy");
+      struct { uint64_t bytes; int32_t src, dst; } info{c.bytes, c.src_dev, c.dst_dev};
+      const uint64_t id = (uint64_t)(uintptr_t)c.e;
+      profiling_trace_at(trace_copy_stream, c.key, id, 0, trace_ref_ns + (uint64_t)((double)tb * 1e6), &info, sizeof(info));
+      profiling_trace_at(trace_copy_stream, c.key + 1, id, 0, trace_ref_ns + (uint64_t)((double)te * 1e6), nullptr, 0);
+    } else {
+      (void)hipGetLastError();
+    }
+    timing_pool.push_back(c.b);
+    timing_pool.push_back(c.e);
+    copy_spans.pop_front();
+  }
+}
+
 void* HipDevice::workspace(int stream, size_t bytes) {
   if (stream < 0 || stream >= (int)stream_workspace.size()) stream = 0;
   if (stream_workspace_size[stream] < bytes) {
@@ -606,7 +642,9 @@ bool HipDevice::start_w2r(size_t bytes) {
     lru_remove(c);
     st->w2r = true;
     c->readers.fetch_add(1);  // pinned: not dropped while the copy is in flight
+    hipEvent_t sb = copy_span_begin();
     PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, c->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_copy));
+    copy_span_end(sb, trace_key_out, d->nb_elts, device_index, 0);
     stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
     job.copies.push_back(c);
     job.versions.push_back(c->version);
@@ -709,8 +747,10 @@ bool HipDevice::progress_prefetch() {
       data_release(d);
       continue;
     }
+    hipEvent_t sb = copy_span_begin();
     if (src->device_index == 0) PARSEC_HIP_CHECK(hipMemcpyAsync(local->device_private, src->device_private, d->nb_elts, hipMemcpyHostToDevice, s_copy));
     else PARSEC_HIP_CHECK(hipMemcpyPeerAsync(local->device_private, ordinal, src->device_private, device_hip_ordinal(src->device_index), d->nb_elts, s_copy));
+    copy_span_end(sb, trace_key_pf, d->nb_elts, src->device_index, device_index);
     stats.bytes_in.fetch_add(d->nb_elts, std::memory_order_relaxed);
     stats.prefetches.fetch_add(1, std::memory_order_relaxed);
     local->transfer_status = TRANSFER_UNDER;
@@ -895,6 +935,11 @@ int HipDevice::stage_in(GpuTask* g) {
       any = true;
     } else if (src && src != local) {
       hipMemcpyKind k = src->device_index == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+      hipEvent_t sb = copy_span_begin();
+      struct SpanEnd {
+        HipDevice* dev; hipEvent_t b; uint64_t n; int s, d;
+        ~SpanEnd() { dev->copy_span_end(b, dev->trace_key_in, n, s, d); }
+      } span_end{this, sb, d->nb_elts, src->device_index, device_index};
       if (k == hipMemcpyDeviceToDevice) {
         int src_ord = device_hip_ordinal(src->device_index);
         PARSEC_HIP_CHECK(hipMemcpyPeerAsync(local->device_private, ordinal, src->device_private, src_ord, d->nb_elts, s_copy));
@@ -1018,7 +1063,15 @@ void HipDevice::execute_ready() {
     }
     if (!batches[s].empty()) {
       batches[s].critical = s == 0 && nb_exec_streams >= 2 && wave_priority;
+      if (roctx) {
+        // rocprofv3 --marker-trace: which tasks each launched group carried
+        char label[96];
+        Task* t0 = round_tasks[s][0]->task;
+        std::snprintf(label, sizeof(label), "%s s%d n%zu %s", name.c_str(), s, round_tasks[s].size(), t0->task_class->name.c_str());
+        roctxRangePushA(label);
+      }
       launch_kernel_batch(batches[s], s_exec[s], ordinal, workspace(s, kernel_batch_workspace_bytes(batches[s]) + 64));
+      if (roctx) roctxRangePop();
       stats.kernel_launches.fetch_add(1, std::memory_order_relaxed);
       batches[s].clear();
     }
@@ -1145,6 +1198,7 @@ bool HipDevice::progress() {
     did = true;
   }
   if (!w2r_jobs.empty() && progress_w2r()) did = true;
+  if (!copy_spans.empty()) progress_copy_spans();
   if ((!prefetch_jobs.empty() || !prefetch_requests.empty()) && progress_prefetch()) did = true;
   // stage in
   if (!pending.empty()) {
@@ -1218,7 +1272,9 @@ bool HipDevice::progress() {
               stats.bytes_out.fetch_add(octx.bytes[fi], std::memory_order_relaxed);
               continue;
             }
+            hipEvent_t sb = copy_span_begin();
             PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, g->dev_copy[fi]->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_copy));
+            copy_span_end(sb, trace_key_out, d->nb_elts, device_index, 0);
             stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
           }
           if (octx.flow_mask) {
@@ -1269,6 +1325,9 @@ void HipDevice::manager_main() {
   if (profiling_enabled() && !trace_ref) {
     // GPU spans: one reference event, host time taken once it completed
     profiling_add_dictionary_keyword("GPU_EXEC", "fill:#FF8800", 16, "ntasks{int32_t};stream{int32_t};tc_id{uint32_t};l0{int32_t}", &trace_key_b, &trace_key_e);
+    profiling_add_dictionary_keyword("GPU_MOVEIN", "fill:#0088FF", 16, "bytes{uint64_t};src{int32_t};dst{int32_t}", &trace_key_in, &trace_key_in_e);
+    profiling_add_dictionary_keyword("GPU_MOVEOUT", "fill:#00CC88", 16, "bytes{uint64_t};src{int32_t};dst{int32_t}", &trace_key_out, &trace_key_out_e);
+    profiling_add_dictionary_keyword("GPU_PREFETCH", "fill:#8800FF", 16, "bytes{uint64_t};src{int32_t};dst{int32_t}", &trace_key_pf, &trace_key_pf_e);
     PARSEC_HIP_CHECK(hipEventCreate(&trace_ref));
     PARSEC_HIP_CHECK(hipEventRecord(trace_ref, s_exec[0]));
     PARSEC_HIP_CHECK(hipEventSynchronize(trace_ref));
@@ -1294,10 +1353,15 @@ void HipDevice::manager_main() {
     in_cv.wait_for(lk, std::chrono::milliseconds(2), [&] { return stop.load() || incoming_n.load() > 0; });
     backoff.reset();
   }
+  if (!copy_spans.empty()) {
+    (void)hipStreamSynchronize(s_copy);
+    progress_copy_spans();
+  }
   profiling_thread_fini(es);
   // trace streams belong to this context's profiling session (freed at its fini)
   gpu_trace = false;
   trace_streams.clear();
+  trace_copy_stream = nullptr;
   if (trace_ref) { (void)hipEventDestroy(trace_ref); trace_ref = nullptr; }
 }
 
@@ -1316,7 +1380,8 @@ void hip_devices_init(Context* ctx) {
   int crit = (int)params.reg_int("device", "hip", "critical_threshold", "Task priority at or above which a completed GPU task is released by the manager itself (critical path)", 1 << 29);
   int rcus = (int)params.reg_int("device", "hip", "reserved_cus", "CUs the bulk streams leave free for the critical stream (CU mask on the bulk streams; 0 = none)", 0);
   int rstride = (int)params.reg_int("device", "hip", "reserved_cus_stride", "Spacing of the reserved CU ids in the CU mask", 1);
-  const bool hp_crit = params.reg_int("device", "hip", "hp_on_critical_stream", "High-priority tasks below the critical threshold share the critical stream (1) or go to the least loaded bulk stream (0)", 0) != 0;
+  const bool roctx_on = params.reg_int("device", "hip", "roctx", "roctx range around every launched kernel group (visible with rocprofv3 --marker-trace)", 1) != 0;
+  const bool hp_crit = params.reg_int("device", "hip", "hp_on_critical_stream", "High-priority tasks below the critical threshold share the critical stream (1) or go to the least loaded bulk stream (0; measured 36.0 vs 38.9 TF at 16k, profiles/r3_route_ab.txt)", 1) != 0;
   const bool wprio = params.reg_int("device", "hip", "wave_priority", "Kernels of the critical stream raise their waves' issue priority (s_setprio) over co-resident bulk waves", 1) != 0;
   const bool trace = params.reg_int("device", "hip", "trace_launches", "Print every launched kernel group (stream, tasks, batch sizes) to stderr", 0) != 0;
   const bool cow = params.reg_int("device", "hip", "complete_on_workers", "Release completed GPU tasks (successor activation) on the compute threads instead of the manager (measured no faster on DPOTRF; breaks the multi-rank DTD stencil: off)", 0) != 0;
@@ -1345,6 +1410,7 @@ void hip_devices_init(Context* ctx) {
     d->reserved_stride = rstride;
     d->wave_priority = wprio;
     d->hp_on_critical = hp_crit;
+    d->roctx = roctx_on;
     d->max_inflight_groups = maxg;
     d->sort_pending = sortp != 0;
     d->complete_on_workers = cow;

@@ -136,7 +136,7 @@ struct HipDevice : Device {
   int reserved_cus = 0;
   int reserved_stride = 1;
   bool wave_priority = true;
-  bool hp_on_critical = false;
+  bool hp_on_critical = true;
   bool cu_masked = false;
   bool batching = true;
   bool sort_pending = true;
@@ -168,6 +168,23 @@ struct HipDevice : Device {
   hipEvent_t get_timing_event();
   void trace_group(int stream, const ExecGroup& g);
   bool trace_launches = false;
+  // GPU-side copy spans (profiling on): timing events around every transfer the
+  // engine issues on the copy stream, turned into MOVEIN / MOVEOUT / PREFETCH
+  // events once they completed (reference device_cuda_module.c:1442-1453,
+  // 2317-2321 trace the same transfers)
+  struct CopySpan {
+    hipEvent_t b, e;
+    int key;  // begin key; end = key + 1
+    uint64_t bytes;
+    int32_t src_dev, dst_dev;
+  };
+  std::deque<CopySpan> copy_spans;
+  int trace_key_in = -1, trace_key_in_e = -1, trace_key_out = -1, trace_key_out_e = -1, trace_key_pf = -1, trace_key_pf_e = -1;
+  struct ProfilingStream* trace_copy_stream = nullptr;
+  hipEvent_t copy_span_begin();                                        // nullptr when not tracing
+  void copy_span_end(hipEvent_t b, int key, uint64_t bytes, int src_dev, int dst_dev);
+  void progress_copy_spans();
+  bool roctx = true;  // roctx ranges around every launched group (rocprofv3 --marker-trace)
   uint32_t rr_stream = 0;
   int max_inflight_groups = 2;  // bulk streams: launched groups in flight before new bulk work waits (0 = no limit)
   double us_busy = 0;

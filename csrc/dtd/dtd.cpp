@@ -456,6 +456,13 @@ int DtdTaskpool::wait() {
 
 int DtdTaskpool::data_flush(Tile* tile) {
   if (!tile || !tile->dc) return 0;
+  // reference parsec_dtd_data_flush.c:391,395
+  ExecutionStream* es = my_execution_stream();
+  PARSEC_PINS(es, PINS_DATA_FLUSH_BEGIN, nullptr);
+  struct FlushEnd {
+    ExecutionStream* es;
+    ~FlushEnd() { PARSEC_PINS(es, PINS_DATA_FLUSH_END, nullptr); }
+  } flush_end{es};
   // A no-op CPU task reading the tile on its owner: the CPU staging of the
   // engine brings the newest version home (GPU -> host, or remote -> owner).
   if (tile->dc->home_device() != 0) return 0;

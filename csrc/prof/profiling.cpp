@@ -355,6 +355,7 @@ struct TaskProfiler {
 };
 TaskProfiler& TPf() { static TaskProfiler* t = new TaskProfiler(); return *t; }
 int g_key_release_b = -1, g_key_release_e = -1, g_key_select_b = -1, g_key_select_e = -1;
+int g_key_activate_b = -1, g_key_activate_e = -1, g_key_flush_b = -1, g_key_flush_e = -1;
 }  // namespace
 
 void pins_fire(ExecutionStream* es, int event, Task* t) {
@@ -407,6 +408,21 @@ void pins_init(Context* ctx) {
       });
       pins_register_callback(PINS_COMPLETE_EXEC_END, [](ExecutionStream* es, int, Task*) {
         if (es && es->prof) profiling_trace(es->prof, g_key_release_e, 0, 0, nullptr, 0);
+      });
+      // remote activation callbacks (comm thread) and DTD data flushes
+      profiling_add_dictionary_keyword("ACTIVATE_CB", "fill:#88CC88", 0, "", &g_key_activate_b, &g_key_activate_e);
+      profiling_add_dictionary_keyword("DATA_FLUSH", "fill:#8888CC", 0, "", &g_key_flush_b, &g_key_flush_e);
+      pins_register_callback(PINS_ACTIVATE_CB_BEGIN, [](ExecutionStream* es, int, Task*) {
+        if (es && es->prof) profiling_trace(es->prof, g_key_activate_b, 0, 0, nullptr, 0);
+      });
+      pins_register_callback(PINS_ACTIVATE_CB_END, [](ExecutionStream* es, int, Task*) {
+        if (es && es->prof) profiling_trace(es->prof, g_key_activate_e, 0, 0, nullptr, 0);
+      });
+      pins_register_callback(PINS_DATA_FLUSH_BEGIN, [](ExecutionStream* es, int, Task*) {
+        if (es && es->prof) profiling_trace(es->prof, g_key_flush_b, 0, 0, nullptr, 0);
+      });
+      pins_register_callback(PINS_DATA_FLUSH_END, [](ExecutionStream* es, int, Task*) {
+        if (es && es->prof) profiling_trace(es->prof, g_key_flush_e, 0, 0, nullptr, 0);
       });
     } else if (m == "print_steals") {
       pins_register_callback(PINS_THREAD_FINI, [](ExecutionStream* es, int, Task*) {

@@ -42,6 +42,8 @@ def test_trace_roundtrip(pa, tmp_path):
     summ = profiling.summary([tr])
     assert summ["traced_work"]["count"] == 40
     assert summ["traced_work"]["total_ns"] > 0
+    # PINS DATA_FLUSH events (reference parsec_dtd_data_flush.c:391,395): one per flushed tile
+    assert summ["DATA_FLUSH"]["count"] == 4
     df = profiling.to_dataframe([tr])
     w = df[df["type"] == "traced_work"]
     assert len(w) == 40 and (w["duration"] >= 0).all()
@@ -98,7 +100,7 @@ def test_comm_trace_payload_sizes(pa, tmp_path):
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp", "dist_dpotrf.py")
     base = str(tmp_path / "comm")
     job = "pc" + uuid.uuid4().hex[:10]
-    env = dict(os.environ, PARSEC_MCA_device_hip_enabled="0", PARSEC_MCA_profile_filename=base)
+    env = dict(os.environ, PARSEC_MCA_device_hip_enabled="0", PARSEC_MCA_profile_filename=base, PARSEC_MCA_mca_pins="task_profiler")
     procs = [subprocess.Popen([sys.executable, worker, str(r), "2", job, "256", "32", "2", "1"], stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT, text=True, env=env) for r in range(2)]
     for p in procs:
@@ -111,6 +113,9 @@ def test_comm_trace_payload_sizes(pa, tmp_path):
     assert snd and sorted(snd) == sorted(rcv)
     assert all(b == 32 * 32 * 8 for *_, b in snd)
     assert any(r["type"] == "COMM_ACTIVATE" for r in rows)
+    # PINS ACTIVATE_CB spans (reference remote_dep_mpi.c:1838,1887): every
+    # received activation runs its callback inside one
+    assert any(r["type"] == "ACTIVATE_CB" for r in rows)
 
 
 def test_dagtools_on_recorded_cholesky_dag(pa, tmp_path):
