@@ -97,6 +97,7 @@ class DpotrfTaskpool : public PtgTaskpool {
   // 64x64 diagonal-block inverses kept by POTRF(k) on the GPU so the TRSM(m,k)
   // panel solves skip their own inversion (valid when POTRF(k) ran on that GPU).
   double* invbuf = nullptr;
+  bool inv_from_zone = false;
   size_t inv_stride = 0;
   std::unique_ptr<std::atomic<uint8_t>[]> inv_ready;
   void on_complete_internal() override {
@@ -110,8 +111,11 @@ class DpotrfTaskpool : public PtgTaskpool {
   }
   ~DpotrfTaskpool() override {
     if (info_dev) device_status_release(info_dev_index, info_dev);
-    // the inverse blocks live in the tile-cache zone (no hipMalloc / hipFree per taskpool)
-    if (invbuf && !device_cache_free(info_dev_index, invbuf)) device_free(info_dev_index, invbuf);
+    // the inverse blocks live in the tile-cache zone (no hipMalloc / hipFree per
+    // taskpool); a taskpool freed after its context went away finds the zone gone
+    // with it (nothing left to free)
+    if (invbuf && inv_from_zone) (void)device_cache_free(info_dev_index, invbuf);
+    else if (invbuf) device_free(info_dev_index, invbuf);
   }
 };
 
@@ -128,6 +132,7 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
     tp->inv_stride = (size_t)((A->nb + 63) / 64) * 4096;
     const size_t inv_bytes = tp->inv_stride * A->nt * sizeof(double);
     tp->invbuf = static_cast<double*>(device_cache_alloc(gpu, inv_bytes));
+    tp->inv_from_zone = tp->invbuf != nullptr;
     if (!tp->invbuf) tp->invbuf = static_cast<double*>(device_alloc(gpu, inv_bytes));
     tp->inv_ready.reset(new std::atomic<uint8_t>[A->nt]);
     for (int64_t i = 0; i < A->nt; ++i) tp->inv_ready[i].store(0);

@@ -146,6 +146,7 @@ struct DataCopy : ListItem {  // ListItem: membership in a device LRU
   // set once a view exists: CPU-only runs bump `version` of such copies when a
   // task writes them in place, so a later reshaped read gets a fresh view
   std::atomic<bool> has_reshape_view{false};
+  bool snapshot_from_zone = false;  // DTD send snapshot carved from a device tile-cache zone
   void* ptr() const { return device_private; }
 };
 

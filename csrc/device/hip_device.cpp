@@ -101,7 +101,9 @@ void* device_alloc(int device_index, size_t bytes) {
 void device_free(int device_index, void* p) {
   int ord = device_hip_ordinal(device_index);
   if (ord < 0 || !p) return;
-  (void)hipFree(p);
+  // never leave a failed call in the thread's HIP error state: the caller may be
+  // a user thread whose next library call (torch) would report it as its own
+  if (hipFree(p) != hipSuccess) (void)hipGetLastError();
 }
 
 namespace {

@@ -177,7 +177,8 @@ Tile* DtdTaskpool::tile_new(size_t bytes, int rank) {
 // Private copy of `src` for a pending remote transfer (host or device memory).
 static void snapshot_release(DataCopy* c) {
   if (c->device_index == 0) std::free(c->device_private);
-  else if (!device_cache_free(c->device_index, c->device_private)) device_free(c->device_index, c->device_private);
+  else if (c->snapshot_from_zone) (void)device_cache_free(c->device_index, c->device_private);  // a zone gone with its context freed it already
+  else device_free(c->device_index, c->device_private);
   Data* d = c->original;
   if (d) {
     d->lock.lock();
@@ -194,6 +195,7 @@ static DataCopy* snapshot_copy(DataCopy* src) {
   int dev = src->device_index;
   // from the GPU's tile-cache zone: no hipMalloc (device-synchronising) per send
   if (dev != 0) p = device_cache_alloc(dev, std::max<size_t>(n, 64));
+  const bool from_zone = p != nullptr;
   if (dev != 0 && !p) p = device_alloc(dev, std::max<size_t>(n, 64));
   if (!p) {
     dev = 0;
@@ -210,6 +212,7 @@ static DataCopy* snapshot_copy(DataCopy* src) {
   c->version = src->version;
   c->dtt = src->dtt;
   c->release_fn = snapshot_release;
+  c->snapshot_from_zone = from_zone && dev != 0;
   data_copy_attach(d, c, dev);
   return c;
 }
