@@ -943,3 +943,77 @@ int parsec_ce_gpu_device_index(void) {
   return g >= 0 ? g : 2;
 }
 }
+
+// ------------------------------------------------------- runtime extras (C)
+namespace {
+std::mutex g_info_m;
+std::map<std::pair<const void*, int>, void*> g_info_cb_data;  // (registry, id) -> cb_data
+std::mutex g_rdctx_m;
+std::map<const void*, intptr_t> g_rdctx;
+}  // namespace
+
+extern "C" {
+parsec_info_t* parsec_per_stream_infos = reinterpret_cast<parsec_info_t*>(&gpu_stream_infos());
+
+int parsec_remote_dep_set_ctx(parsec_context_t* context, intptr_t opaque_comm_ctx) {
+  std::lock_guard<std::mutex> g(g_rdctx_m);
+  g_rdctx[context] = opaque_comm_ctx;
+  return PARSEC_SUCCESS;
+}
+intptr_t parsec_remote_dep_get_ctx(parsec_context_t* context) {
+  std::lock_guard<std::mutex> g(g_rdctx_m);
+  auto it = g_rdctx.find(context);
+  return it == g_rdctx.end() ? 0 : it->second;
+}
+
+void parsec_context_at_fini(parsec_context_t* context, parsec_external_fini_cb_t cb, void* data) {
+  if (!context || !cb) return;
+  context->at_fini.push_back([cb](void* d) { (void)cb(d); });
+  context->at_fini_data.push_back(data);
+}
+
+int parsec_taskpool_reserve_id(parsec_taskpool_t* tp) { return taskpool_reserve_id(tp); }
+int parsec_taskpool_register(parsec_taskpool_t* tp) { return taskpool_register(tp); }
+void parsec_taskpool_unregister(parsec_taskpool_t* tp) { taskpool_unregister(tp); }
+void parsec_taskpool_sync_ids(void) { taskpool_sync_ids(); }
+
+int parsec_nb_devices_get(void) { return (int)DeviceRegistry::instance().devices.size(); }
+int parsec_device_get_type(int device_index) {
+  Device* d = DeviceRegistry::instance().get(device_index);
+  return d ? (int)d->type : PARSEC_DEV_NONE;
+}
+int parsec_advise_data_on_device(parsec_data_t* data, int device_index, int advice) { return data_advise_on_device(data, device_index, advice); }
+int parsec_get_best_device(parsec_task_t* task, double ratio) { return get_best_device(task, ratio); }
+
+parsec_info_id_t parsec_info_register(parsec_info_t* nfo, const char* name, parsec_info_destructor_t destructor, void* des_data,
+                                      parsec_info_constructor_t constructor, void* cons_data, void* cb_data) {
+  if (!nfo || !name) return -1;
+  auto* reg = reinterpret_cast<InfoRegistry*>(nfo);
+  const int id = reg->register_info(
+      name, [constructor, cons_data](void* owner) -> void* { return constructor ? constructor(owner, cons_data) : nullptr; },
+      [destructor, des_data](void* elt) { if (destructor) destructor(elt, des_data); });
+  std::lock_guard<std::mutex> g(g_info_m);
+  g_info_cb_data[{nfo, id}] = cb_data;
+  return id;
+}
+parsec_info_id_t parsec_info_unregister(parsec_info_t* nfo, parsec_info_id_t iid, void** pcb_data) {
+  if (!nfo) return -1;
+  const int id = reinterpret_cast<InfoRegistry*>(nfo)->unregister_info(iid);
+  std::lock_guard<std::mutex> g(g_info_m);
+  auto it = g_info_cb_data.find({nfo, iid});
+  if (pcb_data) *pcb_data = it == g_info_cb_data.end() ? nullptr : it->second;
+  if (it != g_info_cb_data.end()) g_info_cb_data.erase(it);
+  return id;
+}
+parsec_info_id_t parsec_info_lookup(parsec_info_t* nfo, const char* name, void** pcb_data) {
+  if (!nfo || !name) return -1;
+  const int id = reinterpret_cast<InfoRegistry*>(nfo)->lookup(name);
+  if (pcb_data) {
+    std::lock_guard<std::mutex> g(g_info_m);
+    auto it = g_info_cb_data.find({nfo, id});
+    *pcb_data = it == g_info_cb_data.end() ? nullptr : it->second;
+  }
+  return id;
+}
+void* parsec_gpu_stream_info_get(parsec_info_id_t iid) { return t_gpu_ctx ? t_gpu_ctx->info(iid) : nullptr; }
+}

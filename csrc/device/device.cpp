@@ -6,6 +6,8 @@
 // parsec_get_best_device :79-189 with load_balance_skew).
 #include "device.hpp"
 
+#include <fstream>
+
 #include <unistd.h>
 
 #include <cmath>
@@ -40,13 +42,51 @@ void DeviceRegistry::registration_complete() {
   frozen = true;
 }
 
+// CPU capability (reference device.c:678-797 parses /proc/cpuinfo for the
+// clock and the widest vector ISA): peak fp64 flops per cycle and core from the
+// ISA flags, the clock from cpufreq (max) or the "cpu MHz" lines.
+CpuCapability cpu_capability() {
+  CpuCapability c;
+  std::ifstream f("/proc/cpuinfo");
+  std::string line;
+  double mhz = 0;
+  while (std::getline(f, line)) {
+    const auto colon = line.find(':');
+    if (colon == std::string::npos) continue;
+    std::string key = line.substr(0, colon);
+    while (!key.empty() && (key.back() == ' ' || key.back() == '\t')) key.pop_back();
+    const std::string val = line.substr(colon + 1);
+    if (key == "model name" && c.model.empty()) c.model = val.substr(val.find_first_not_of(' ') == std::string::npos ? 0 : val.find_first_not_of(' '));
+    else if (key == "cpu MHz") mhz = std::max(mhz, std::atof(val.c_str()));
+    else if (key == "flags" && c.flags_seen == false) {
+      c.flags_seen = true;
+      auto has = [&](const char* fl) { return (" " + val + " ").find(std::string(" ") + fl + " ") != std::string::npos; };
+      c.avx512 = has("avx512f");
+      c.avx2 = has("avx2");
+      c.fma = has("fma");
+      c.sse2 = has("sse2");
+    }
+  }
+  std::ifstream fq("/sys/devices/system/cpu/cpu0/cpufreq/cpuinfo_max_freq");
+  long khz = 0;
+  if (fq >> khz && khz > 0) mhz = std::max(mhz, khz / 1000.0);
+  c.ghz = mhz > 0 ? mhz / 1000.0 : 2.0;
+  // 2 FMA pipes x vector doubles x 2 flops
+  c.dp_flops_per_cycle = c.avx512 ? 32.0 : (c.avx2 && c.fma) ? 16.0 : c.avx2 ? 8.0 : c.sse2 ? 4.0 : 2.0;
+  if (c.isa().empty()) c.model = c.model.empty() ? "unknown" : c.model;
+  return c;
+}
+
+std::string CpuCapability::isa() const { return avx512 ? "AVX512" : (avx2 && fma) ? "AVX2+FMA" : avx2 ? "AVX2" : sse2 ? "SSE2" : "scalar"; }
+
 struct CpuDevice : Device {
-  CpuDevice(int cores) {
+  CpuCapability cap;
+  CpuDevice(int cores) : cap(cpu_capability()) {
     name = "cpu";
     type = DEV_CPU;
-    // 2 FMA pipes x 4 doubles (AVX2) x 2 flops x ~2.4 GHz per core
-    gflops_fp64 = std::max(1, cores) * 2.4 * 16.0;
+    gflops_fp64 = std::max(1, cores) * cap.ghz * cap.dp_flops_per_cycle;
     gflops_fp32 = 2 * gflops_fp64;
+    PARSEC_DEBUG(kVerbInfo, "device", "cpu: %s, %s at %.2f GHz: %.1f GFLOP/s fp64 over %d cores", cap.model.c_str(), cap.isa().c_str(), cap.ghz, gflops_fp64, cores);
   }
 };
 

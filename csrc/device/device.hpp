@@ -20,6 +20,16 @@
 
 namespace parsec {
 
+// CPU capability from /proc/cpuinfo + cpufreq (reference device.c:678-797)
+struct CpuCapability {
+  std::string model;
+  double ghz = 2.0;
+  double dp_flops_per_cycle = 2.0;  // per core
+  bool avx512 = false, avx2 = false, fma = false, sse2 = false, flags_seen = false;
+  std::string isa() const;
+};
+CpuCapability cpu_capability();
+
 void devices_init(Context* ctx);
 void devices_start(Context* ctx);
 void devices_stop(Context* ctx);

@@ -640,6 +640,15 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("kernel_gemm_tile_policy", [](int p) { return parsec_amd_gemm_tile_policy(p); });
   m.def("kernel_gemm_splitk", [](int on) { return parsec_amd_gemm_splitk(on); }, "split-K tail of the 128x128 grouped DGEMM: 1 on, 0 off, -1 query; returns the previous setting");
+  m.def("cpu_capability", []() {
+    const CpuCapability c = cpu_capability();
+    py::dict d;
+    d["model"] = c.model;
+    d["isa"] = c.isa();
+    d["ghz"] = c.ghz;
+    d["dp_flops_per_cycle"] = c.dp_flops_per_cycle;
+    return d;
+  }, "CPU model, widest vector ISA, clock and peak fp64 flops per cycle and core (/proc/cpuinfo, cpufreq)");
   m.def("kernel_potrf_stamps", []() {
     std::vector<long long> v(16, 0);
     if (parsec_amd_potrf_stamps(v.data()) != 0) v.clear();

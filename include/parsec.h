@@ -356,6 +356,50 @@ int parsec_ce_mem_register_device(void* mem, size_t bytes, int device, parsec_ce
 /* runtime device index of this process's GPU (2, the first accelerator, when no context registered devices) */
 int parsec_ce_gpu_device_index(void);
 
+/* ------------------------------------------------------- runtime extras
+ * (reference runtime.h:221,255,448-495; mca/device/device.c:79,987;
+ * class/info.h) */
+/* the communication context of a multi-process job: the reference takes an MPI
+ * communicator; here the job is the shared-memory engine of the launch (see
+ * parsec_amd.launch), and the opaque value is recorded for the application */
+int parsec_remote_dep_set_ctx(parsec_context_t* context, intptr_t opaque_comm_ctx);
+intptr_t parsec_remote_dep_get_ctx(parsec_context_t* context);
+typedef int (*parsec_external_fini_cb_t)(void* data);
+/* run `cb(data)` during parsec_fini, before the runtime is torn down */
+void parsec_context_at_fini(parsec_context_t* context, parsec_external_fini_cb_t cb, void* data);
+int parsec_taskpool_reserve_id(parsec_taskpool_t* tp);
+int parsec_taskpool_register(parsec_taskpool_t* tp);
+void parsec_taskpool_unregister(parsec_taskpool_t* tp);
+/* agree on the next taskpool id with every rank (collective) */
+void parsec_taskpool_sync_ids(void);
+parsec_taskpool_t* parsec_taskpool_lookup(uint32_t taskpool_id);
+
+/* devices: 0 = CPU, 1 = recursive, accelerators from 2 */
+int parsec_nb_devices_get(void);
+int parsec_device_get_type(int device_index); /* PARSEC_DEV_* of a device, PARSEC_DEV_NONE if none */
+#define PARSEC_DEV_DATA_ADVICE_PREFETCH 1
+#define PARSEC_DEV_DATA_ADVICE_PREFERRED_DEVICE 2
+#define PARSEC_DEV_DATA_ADVICE_WARMUP 3
+int parsec_advise_data_on_device(parsec_data_t* data, int device_index, int advice);
+/* device the runtime would run `task` on (load / data-locality balanced) */
+int parsec_get_best_device(parsec_task_t* task, double ratio);
+
+/* info registries: named per-object slots built on first use. parsec_per_stream_infos
+ * is the registry of the GPU execution streams (one object per stream, e.g. a BLAS
+ * handle bound to it); a GPU chore fetches its stream's object with
+ * parsec_gpu_stream_info_get. */
+typedef struct parsec_info_s parsec_info_t;
+typedef int parsec_info_id_t;
+typedef void* (*parsec_info_constructor_t)(void* obj, void* cons_data);
+typedef void (*parsec_info_destructor_t)(void* elt, void* des_data);
+extern parsec_info_t* parsec_per_stream_infos;
+parsec_info_id_t parsec_info_register(parsec_info_t* nfo, const char* name, parsec_info_destructor_t destructor, void* des_data,
+                                      parsec_info_constructor_t constructor, void* cons_data, void* cb_data);
+parsec_info_id_t parsec_info_unregister(parsec_info_t* nfo, parsec_info_id_t iid, void** pcb_data);
+parsec_info_id_t parsec_info_lookup(parsec_info_t* nfo, const char* name, void** pcb_data);
+/* inside a GPU chore: the object of info `iid` for the stream the chore runs on (NULL elsewhere) */
+void* parsec_gpu_stream_info_get(parsec_info_id_t iid);
+
 /* ---------------------------------------------------------------- version */
 int parsec_version(int* version_major, int* version_minor, int* version_release);
 int parsec_version_ex(size_t len, char* version_string);

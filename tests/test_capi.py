@@ -143,3 +143,16 @@ def test_comm_engine_c_program(tmp_path, pa):
     assert rc == 0, outs
     text = "".join(o for o, _ in outs)
     assert text.count("ce ok") == 2 and "[1] GET ok" in text and "[1] PUT ok" in text, text
+
+
+def test_runtime_extras_c_program(tmp_path, pa):
+    """at_fini, taskpool ids, device registry, data advice and info registries
+    from C (reference runtime.h:221,255,448-495, device.c:79,987, class/info.h)."""
+    exe = tmp_path / "runtime_capi"
+    cmd = ["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-O1", f"-I{ROOT}/include", os.path.join(HERE, "capi", "runtime_capi.c"), "-o", str(exe),
+           f"-L{ROOT}/parsec_amd/lib", "-lparsec_amd", f"-Wl,-rpath,{ROOT}/parsec_amd/lib", "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "runtime capi ok" in r.stdout

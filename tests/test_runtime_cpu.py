@@ -557,3 +557,24 @@ def test_topology_cache_levels(pa):
     assert all(len(row) == len(d) for row in d)
     if d:
         assert all(d[i][i] == min(d[i]) for i in range(len(d)))
+
+
+def test_cpu_capability_detection(pa):
+    """CPU device weight from /proc/cpuinfo + cpufreq (reference device.c:678-797):
+    the widest ISA sets the fp64 flops per cycle and core, the CPU device's
+    capability is cores x clock x flops/cycle."""
+    from parsec_amd import _C
+
+    cap = _C.cpu_capability()
+    flags = open("/proc/cpuinfo").read()
+    expect = 32.0 if " avx512f" in flags else 16.0 if (" avx2" in flags and " fma" in flags) else None
+    if expect is not None:
+        assert cap["dp_flops_per_cycle"] == expect
+    assert cap["isa"] in ("AVX512", "AVX2+FMA", "AVX2", "SSE2", "scalar")
+    assert 0.5 < cap["ghz"] < 6.0
+    ctx = pa.init(3)
+    try:
+        cpu = [d for d in pa.devices() if d["name"] == "cpu"][0]
+        assert abs(cpu["gflops_fp64"] - 3 * cap["ghz"] * cap["dp_flops_per_cycle"]) < 1e-6
+    finally:
+        ctx.fini()
