@@ -474,6 +474,60 @@ parsec_data_t* parsec_data_create(parsec_data_t** holder, parsec_data_collection
 void parsec_data_destroy(parsec_data_t* data) { data_destroy(data); }
 parsec_data_copy_t* parsec_data_get_copy(parsec_data_t* data, int device) { return data ? data->copy(device) : nullptr; }
 void* parsec_data_copy_get_ptr(parsec_data_copy_t* copy) { return copy ? copy->device_private : nullptr; }
+parsec_data_copy_t* parsec_data_copy_new(parsec_data_t* data, int device, parsec_datatype_t dtt, uint32_t flags) {
+  if (device < 0 || device >= kMaxDevices) return nullptr;
+  DataCopy* c = new DataCopy();
+  c->device_index = (int8_t)device;
+  c->flags = (uint8_t)(flags & ~(uint32_t)(DATA_FLAG_PARSEC_OWNED | DATA_FLAG_DEVICE_CACHE | DATA_FLAG_ARENA));
+  c->coherency_state = COHERENCY_INVALID;
+  if (dtt != PARSEC_DATATYPE_NULL) c->dtt = type_of(dtt);
+  if (data) {
+    std::lock_guard<SpinLock> g(data->lock);
+    if (dtt == PARSEC_DATATYPE_NULL)
+      for (int i = 0; i < kMaxDevices; ++i)
+        if (DataCopy* o = data->copy(i)) { c->dtt = o->dtt; break; }
+    data_copy_attach(data, c, device);
+  }
+  return c;
+}
+void parsec_data_copy_set_ptr(parsec_data_copy_t* copy, void* ptr) { if (copy) copy->device_private = ptr; }
+int parsec_data_copy_attach(parsec_data_t* data, parsec_data_copy_t* copy, int device) {
+  if (!data || !copy || device < 0 || device >= kMaxDevices) return PARSEC_ERROR;
+  std::lock_guard<SpinLock> g(data->lock);
+  return data_copy_attach(data, copy, device) == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+int parsec_data_copy_detach(parsec_data_t* data, parsec_data_copy_t* copy, int device) {
+  if (!data || !copy || device < 0 || device >= kMaxDevices) return PARSEC_ERROR;
+  std::lock_guard<SpinLock> g(data->lock);
+  if (data_copy_detach(data, copy, device) != 0) return PARSEC_ERROR;
+  copy->original = nullptr;
+  if (data->owner_device == device) {
+    // ownership falls back to the newest remaining valid copy
+    int best = -1;
+    for (int i = 0; i < kMaxDevices; ++i)
+      if (DataCopy* o = data->copy(i); o && o->coherency_state != COHERENCY_INVALID && (best < 0 || o->version > data->copy(best)->version)) best = i;
+    data->owner_device = (int8_t)(best < 0 ? 0 : best);
+  }
+  return PARSEC_SUCCESS;
+}
+void parsec_data_copy_release(parsec_data_copy_t* copy) {
+  if (!copy) return;
+  copy->dev_state = nullptr;  // the device engine's unmanaged marker is static
+  data_copy_release(copy);
+}
+int parsec_data_transfer_ownership_to_copy(parsec_data_t* data, int device, int access) {
+  if (!data || device < 0 || device >= kMaxDevices || !data->copy(device)) return -1;
+  DataCopy* src = data_start_transfer_ownership_to_copy(data, device, (uint8_t)access);
+  const int from = src ? src->device_index : -1;
+  data_end_transfer_ownership_to_copy(data, device, (uint8_t)access);
+  if (access & FLOW_WRITE) {
+    // the new owner is the newest version: other copies are now stale
+    std::lock_guard<SpinLock> g(data->lock);
+    DataCopy* local = data->copy(device);
+    local->version += 1;
+  }
+  return from;
+}
 void* parsec_data_get_ptr(parsec_data_t* data, int device) {
   DataCopy* c = data ? data->copy(device) : nullptr;
   return c ? c->device_private : nullptr;
@@ -683,14 +737,23 @@ int parsec_dtd_task_class_add_chore(parsec_taskpool_t* tp, parsec_dtd_task_class
   return d->add_chore(tc, (uint32_t)device_type, [fn](ExecutionStream* es, Task* t) { return fn(es, t); }, nullptr);
 }
 void parsec_dtd_insert_task_with_task_class(parsec_taskpool_t* tp, parsec_dtd_task_class_t* tcp, int priority, int device_type, ...) {
-  (void)device_type;
+  // arguments are (flags, pointer) pairs: the class signature gives each one's
+  // access mode and size, the flags add PUSHOUT / AFFINITY / ... (reference
+  // insert_function.c:3256-3314)
   auto* d = as_dtd(tp);
+  auto* tc = reinterpret_cast<dtd::DtdTaskClass*>(tcp);
   PendingArgs pa;
   va_list ap;
   va_start(ap, device_type);
-  parse_args(ap, pa);
+  for (size_t i = 0;; ++i) {
+    const int flags = va_arg(ap, int);
+    if (flags == PARSEC_DTD_ARG_END) break;
+    void* ptr = va_arg(ap, void*);
+    if (i >= tc->param_ops.size()) fatal("task class %s takes %zu arguments, inserted with more", tc->name.c_str(), tc->param_ops.size());
+    parse_one(tc->param_sizes[i], ptr, flags | tc->param_ops[i], pa);
+  }
   va_end(ap);
-  d->insert_task(reinterpret_cast<dtd::DtdTaskClass*>(tcp), priority, pa.args);
+  d->insert_task(tc, priority, pa.args, (uint32_t)device_type);
 }
 parsec_dtd_tile_t* parsec_dtd_tile_of(parsec_data_collection_t* dc, parsec_data_key_t key) {
   // tiles are per-taskpool in the runtime; the C API keeps the reference's
@@ -705,6 +768,7 @@ parsec_dtd_tile_t* parsec_dtd_tile_new(parsec_taskpool_t* tp, int rank, size_t s
 }
 void parsec_dtd_data_collection_init(parsec_data_collection_t* dc) { (void)dc; }
 void parsec_dtd_data_collection_fini(parsec_data_collection_t* dc) { (void)dc; }
+parsec_data_t* parsec_dtd_tile_data(parsec_dtd_tile_t* tile) { return tile ? reinterpret_cast<dtd::Tile*>(tile)->data : nullptr; }
 int parsec_dtd_data_flush(parsec_taskpool_t* tp, parsec_dtd_tile_t* tile) { return as_dtd(tp)->data_flush(reinterpret_cast<dtd::Tile*>(tile)); }
 int parsec_dtd_data_flush_all(parsec_taskpool_t* tp, parsec_data_collection_t* dc) { return as_dtd(tp)->data_flush_all(impl_of(dc)); }
 

@@ -304,6 +304,9 @@ struct Chore {
   void* dyld_fn = nullptr;
   std::string dyld;
   double weight = 1.0;  // load-balancing ratio (reference BODY weight=)
+  // per-task weight when BODY weight= names task locals (e.g. weight=m+n+1)
+  std::function<double(const Task*)> weight_fn;
+  double weight_of(const Task* t) const { return weight_fn ? weight_fn(t) : weight; }
 };
 
 enum TaskClassFlags : uint32_t { TC_HIGH_PRIORITY = 0x1, TC_IMMEDIATE = 0x2, TC_NO_PROFILE = 0x4, TC_COUNT_DEPS = 0x8,

@@ -199,7 +199,7 @@ int get_best_device(Task* t, double ratio) {
 
 int gpu_chore_dispatch(ExecutionStream* es, Task* t, int chore) {
   const Chore& ch = t->task_class->chores[chore];
-  int dev = t->selected_device >= 2 ? t->selected_device : get_best_device(t, ch.weight);
+  int dev = t->selected_device >= 2 ? t->selected_device : get_best_device(t, ch.weight_of(t));
   if (dev < 2) return HOOK_NEXT;
   t->selected_device = (int8_t)dev;
   return DeviceRegistry::instance().devices[dev]->submit(es, t, chore);

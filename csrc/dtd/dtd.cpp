@@ -265,13 +265,20 @@ static bool add_edge(DtdTask* pred, DtdTask* succ, int src_flow, int dst_flow, b
   return true;
 }
 
-DtdTask* DtdTaskpool::insert_task(DtdTaskClass* tc, int priority, const std::vector<Arg>& in_args) {
+DtdTask* DtdTaskpool::insert_task(DtdTaskClass* tc, int priority, const std::vector<Arg>& in_args, uint32_t device_types) {
   Context* ctx = context;
   if (!ctx) fatal("insert_task on a DTD taskpool that is not attached to a context");
   const int my = ctx->my_rank;
   auto* t = new DtdTask();
   t->taskpool = this;
   t->task_class = tc;
+  if (device_types && device_types != DEV_ALL) {
+    uint32_t m = 0;
+    for (size_t c = 0; c < tc->chores.size(); ++c)
+      if (tc->chores[c].type & device_types) m |= 1u << c;
+    if (!m) fatal("insert_task: task class %s has no chore for device types 0x%x", tc->name.c_str(), device_types);
+    t->chore_mask = m;
+  }
   t->priority = priority + this->priority;
   t->seq = seq.fetch_add(1);
   t->key = t->seq;

@@ -123,7 +123,9 @@ class DtdTaskpool : public Taskpool {
   // API
   DtdTaskClass* create_task_class(const std::string& name, const std::vector<std::pair<int, int>>& params);
   int add_chore(DtdTaskClass* tc, uint32_t device_type, Hook cpu, std::function<int(GpuExecContext*, Task*)> gpu);
-  DtdTask* insert_task(DtdTaskClass* tc, int priority, const std::vector<Arg>& args);
+  // device_types != 0 (DEV_* bits): only chores of those types may run the task
+  // (reference parsec_dtd_insert_task_with_task_class's device_type argument)
+  DtdTask* insert_task(DtdTaskClass* tc, int priority, const std::vector<Arg>& args, uint32_t device_types = 0);
   Tile* tile_of(DataCollection* dc, uint64_t key);
   Tile* tile_new(size_t bytes, int rank);
   Tile* tile_of_data(Data* d);  // local tile tracking an existing Data (ptg_to_dtd)

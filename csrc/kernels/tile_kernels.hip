@@ -1586,6 +1586,21 @@ int parsec_amd_dgemm_batch(const parsec::GemmDesc* descs, int n, void* stream) {
   parsec::kern::launch_gemm_batch(descs, n, (hipStream_t)stream);
   return (int)hipGetLastError();
 }
+// BLAS-style single DGEMM, C = alpha op(A) op(B) + beta C, column major, on
+// `stream` (the signature a BODY dyld= or a DTD chore calls; reference
+// stress.jdf resolves cublasDgemm the same way). Returns a hipError_t.
+int parsec_amd_dgemm(char transa, char transb, int m, int n, int k, double alpha, const double* A, int lda, const double* B, int ldb, double beta,
+                     double* C, int ldc, void* stream) {
+  parsec::GemmDesc d{};
+  d.A = A; d.B = B; d.C = C;
+  d.m = m; d.n = n; d.k = k;
+  d.lda = lda; d.ldb = ldb; d.ldc = ldc;
+  d.alpha = alpha; d.beta = beta;
+  d.transA = (transa == 'T' || transa == 't' || transa == 'C' || transa == 'c');
+  d.transB = (transb == 'T' || transb == 't' || transb == 'C' || transb == 'c');
+  if (m <= 0 || n <= 0) return 0;
+  return parsec_amd_dgemm_batch(&d, 1, stream);
+}
 int parsec_amd_dtrsm_batch(const parsec::TrsmDesc* descs, int n, void* stream) {
   void* ws = test_ws(parsec::kern::trsm_workspace_bytes(descs, n) + 64);
   parsec::kern::launch_trsm_batch(descs, n, (hipStream_t)stream, static_cast<double*>(ws));

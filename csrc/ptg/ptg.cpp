@@ -426,7 +426,19 @@ int PtgTaskClass::prepare_input(ExecutionStream* es, Task* t) const {
     TaskDataRef& r = t->data[f];
     if (r.data_in) continue;
     const DepTarget* tg = active_input(tp, (int)f, t->locals);
-    if (!tg) continue;
+    if (!tg) {
+      // pure output flow (WRITE with no input dependency): a fresh copy from
+      // the arena of its output datatype (reference jdf2c.c:5690-5719)
+      if (fd.access == FLOW_WRITE && fd.in.empty() && !fd.out.empty()) {
+        const int ai = fd.out[0].then_t.datatype_index;
+        auto& adts = t->taskpool->arenas_datatypes;
+        if (ai >= 0 && ai < (int)adts.size() && adts[ai].arena) {
+          r.data_in = adts[ai].arena->get_copy(nullptr, 0);
+          if (!r.data_in) return HOOK_AGAIN;
+        }
+      }
+      continue;
+    }
     switch (tg->kind) {
       case DEP_DATA: {
         DataCollection* dc = tg->dc(tp);
@@ -784,6 +796,10 @@ void PtgTaskpool::finalize() {
       ch.gpu_hook = b.gpu;
       ch.evaluate = b.evaluate;
       ch.weight = b.weight;
+      if (b.weight_fn) {
+        auto wf = b.weight_fn;
+        ch.weight_fn = [wf](const Task* t) { return wf(t->taskpool, t->locals); };
+      }
       ch.dyld = b.dyld;
       if (!ch.dyld.empty()) {
         // BODY dyld=<symbol> (reference device.c:800-841): resolve the library

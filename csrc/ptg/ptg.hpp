@@ -100,6 +100,7 @@ struct BodyDef {
   std::function<int(GpuExecContext*, Task*)> gpu;
   Evaluate evaluate;
   double weight = 1.0;
+  std::function<double(const Taskpool*, const int32_t*)> weight_fn;  // weight= over task locals
   std::string dyld;
   // BODY stage_in= / stage_out= / F.size= / F.dc= (reference jdf2c.c:6583-6830)
   GpuStageFn stage_in, stage_out;

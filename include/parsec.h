@@ -183,6 +183,23 @@ void* parsec_data_copy_get_ptr(parsec_data_copy_t* copy);
 void* parsec_data_get_ptr(parsec_data_t* data, int device);
 /* Bring the newest version of `data` back to host memory and return it. */
 void* parsec_data_pull_to_host(parsec_data_t* data);
+/* User-managed copies (reference data.h parsec_data_copy_new / attach / detach,
+ * parsec_data_transfer_ownership_to_copy): a copy of `data` on `device` whose
+ * memory the application provides (e.g. hipMalloc on a GPU) and frees after
+ * detaching it. The runtime uses such a device copy in place, never evicts it
+ * and never frees its memory. */
+#define PARSEC_FLOW_ACCESS_NONE 0x0
+#define PARSEC_FLOW_ACCESS_READ 0x1
+#define PARSEC_FLOW_ACCESS_WRITE 0x2
+#define PARSEC_FLOW_ACCESS_RW 0x3
+parsec_data_copy_t* parsec_data_copy_new(parsec_data_t* data, int device, parsec_datatype_t dtt, uint32_t flags);
+void parsec_data_copy_set_ptr(parsec_data_copy_t* copy, void* ptr);
+int parsec_data_copy_attach(parsec_data_t* data, parsec_data_copy_t* copy, int device);
+int parsec_data_copy_detach(parsec_data_t* data, parsec_data_copy_t* copy, int device);
+void parsec_data_copy_release(parsec_data_copy_t* copy);
+/* make the copy on `device` the owner (newest version); returns the device whose
+ * copy holds the bytes to bring over, or -1 when the copy is already current */
+int parsec_data_transfer_ownership_to_copy(parsec_data_t* data, int device, int access);
 #define PARSEC_DATA_COPY_GET_PTR(c) parsec_data_copy_get_ptr(c)
 
 void* parsec_data_allocate(size_t size);
@@ -282,6 +299,8 @@ parsec_dtd_tile_t* parsec_dtd_tile_new(parsec_taskpool_t* tp, int rank, size_t s
 void parsec_dtd_data_collection_init(parsec_data_collection_t* dc);
 void parsec_dtd_data_collection_fini(parsec_data_collection_t* dc);
 int parsec_dtd_data_flush(parsec_taskpool_t* tp, parsec_dtd_tile_t* tile);
+/* the runtime data behind a DTD tile (advice, pull_to_host); valid until the taskpool is freed */
+parsec_data_t* parsec_dtd_tile_data(parsec_dtd_tile_t* tile);
 int parsec_dtd_data_flush_all(parsec_taskpool_t* tp, parsec_data_collection_t* dc);
 void parsec_dtd_unpack_args(parsec_task_t* this_task, ...);
 /* varargs-free forms (used by the Fortran bindings) */
@@ -399,6 +418,12 @@ parsec_info_id_t parsec_info_unregister(parsec_info_t* nfo, parsec_info_id_t iid
 parsec_info_id_t parsec_info_lookup(parsec_info_t* nfo, const char* name, void** pcb_data);
 /* inside a GPU chore: the object of info `iid` for the stream the chore runs on (NULL elsewhere) */
 void* parsec_gpu_stream_info_get(parsec_info_id_t iid);
+
+/* ------------------------------------------------------------ tile kernels
+ * The framework's MFMA DGEMM as a BLAS-style call on a HIP stream (column
+ * major; trans 'N' or 'T'); returns a hipError_t (0 = success). */
+int parsec_amd_dgemm(char transa, char transb, int m, int n, int k, double alpha, const double* A, int lda, const double* B, int ldb, double beta,
+                     double* C, int ldc, void* stream);
 
 /* ---------------------------------------------------------------- version */
 int parsec_version(int* version_major, int* version_minor, int* version_release);

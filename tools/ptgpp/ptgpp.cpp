@@ -1077,7 +1077,7 @@ struct Gen {
         else if (type == "RECURSIVE") c << "b.type = parsec::DEV_RECURSIVE; b.cpu = " << fn << "; ";
         else if (type == "CPU") c << "b.type = parsec::DEV_CPU; b.cpu = " << fn << "; ";
         else die(bd.line, "unsupported BODY type '" + type + "' (CPU, HIP or RECURSIVE)");
-        if (const Prop* w = find_prop(bd.props, "weight")) c << "b.weight = (double)(" << w->val << "); ";
+        if (const Prop* w = find_prop(bd.props, "weight")) c << "b.weight_fn = " << lam(f, w->val, Scope(), "double") << "; ";
         if (const Prop* e = find_prop(bd.props, "evaluate")) c << "b.evaluate = [](const parsec::Task* t) { return " << e->val << "(t); }; ";
         if (const Prop* dy = find_prop(bd.props, "dyld")) c << "b.dyld = \"" << esc(dy->val) << "\"; ";
         // user data movement and per-flow device size / collection
