@@ -37,6 +37,17 @@ ptg::PtgTaskpool* broadcast_new(TiledMatrix* A, int64_t root_m, int64_t root_n, 
 // (disi_dst, disj_dst) of dst (any tile sizes / distributions). Blocking (DTD).
 int redistribute(Context* ctx, TiledMatrix* src, TiledMatrix* dst, int64_t size_row, int64_t size_col, int64_t disi_src, int64_t disj_src, int64_t disi_dst,
                  int64_t disj_dst);
+// The same copy as a PTG taskpool (algos/jdf/redistribute.jdf, or
+// redistribute_reshuffle.jdf when tiles match and the window is tile aligned;
+// reference redistribute_wrapper.c). nullptr on invalid arguments.
+ptg::PtgTaskpool* redistribute_new(TiledMatrix* src, TiledMatrix* dst, int64_t size_row, int64_t size_col, int64_t disi_src, int64_t disj_src, int64_t disi_dst,
+                                   int64_t disj_dst);
+// Blocking form of redistribute_new (0 on success, -1 on invalid arguments).
+int redistribute_ptg(Context* ctx, TiledMatrix* src, TiledMatrix* dst, int64_t size_row, int64_t size_col, int64_t disi_src, int64_t disj_src,
+                     int64_t disi_dst, int64_t disj_dst);
+// Diagonal + sub-diagonal tiles of a lower band matrix to LAPACK band storage in
+// a 1 x (nt+1) row of (mb+1) x (nb+2) tiles (algos/jdf/diag_band_to_rect.jdf).
+ptg::PtgTaskpool* diag_band_to_rect_new(TiledMatrix* A, TiledMatrix* B, int mt, int nt, int mb, int nb, size_t elem_size);
 // Tiled C = alpha A B + beta C inserted as DTD tasks (blocking).
 // Host DGEMM for CPU bodies (packed panels, AVX2/FMA micro-kernel; host_gemm.cpp)
 void host_dgemm(int m, int n, int k, double alpha, const double* A, int lda, const double* B, int ldb, bool transB, double beta, double* C, int ldc);

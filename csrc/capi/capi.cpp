@@ -18,6 +18,7 @@
 #include "../data/collections.hpp"
 #include "../device/device.hpp"
 #include "../dtd/dtd.hpp"
+#include "../algos/linalg.hpp"
 #include "../prof/profiling.hpp"
 // after the runtime headers: the C API defines PASSED_BY_REF & co. as macros
 #include "../../include/parsec.h"
@@ -596,6 +597,61 @@ int parsec_tiled_matrix_data_write(parsec_tiled_matrix_t* tdesc, const char* fil
 int parsec_tiled_matrix_data_read(parsec_tiled_matrix_t* tdesc, const char* filename) {
   auto* tm = dynamic_cast<TiledMatrix*>(impl_of(&tdesc->super));
   return tm && tm->data_read(filename) == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+
+// ------------------------------------------------- matrix operator taskpools
+static TiledMatrix* tm_of(const parsec_tiled_matrix_t* t) {
+  auto* tm = t ? dynamic_cast<TiledMatrix*>(impl_of(const_cast<parsec_data_collection_t*>(&t->super))) : nullptr;
+  if (!tm) fatal("not a tiled matrix of this runtime");
+  return tm;
+}
+parsec_taskpool_t* parsec_apply_New(parsec_matrix_uplo_t uplo, parsec_tiled_matrix_t* A, parsec_tiled_matrix_unary_op_t operation, void* op_args) {
+  const parsec_tiled_matrix_t* cA = A;
+  return algos::apply_new(tm_of(A), (int)uplo, [cA, operation](TiledMatrix*, int64_t m, int64_t n, void* tile, void* arg) {
+    operation(my_execution_stream(), cA, tile, PARSEC_MATRIX_FULL, (int)m, (int)n, arg);
+  }, op_args);
+}
+int parsec_apply(parsec_context_t* parsec, parsec_matrix_uplo_t uplo, parsec_tiled_matrix_t* A, parsec_tiled_matrix_unary_op_t operation, void* op_args) {
+  parsec_taskpool_t* tp = parsec_apply_New(uplo, A, operation, op_args);
+  parsec_context_add_taskpool(parsec, tp);
+  parsec_context_start(parsec);
+  parsec_context_wait(parsec);
+  parsec_taskpool_free(tp);
+  return PARSEC_SUCCESS;
+}
+parsec_taskpool_t* parsec_map_operator_New(const parsec_tiled_matrix_t* src, parsec_tiled_matrix_t* dest, parsec_operator_t op, void* op_data) {
+  return algos::map_operator_new(tm_of(src), tm_of(dest), [op, op_data](const void* s, void* d, int64_t m, int64_t n, int64_t, int64_t) {
+    op(my_execution_stream(), s, d, op_data, (int)m, (int)n);
+  });
+}
+static parsec_taskpool_t* reduce_c(const parsec_tiled_matrix_t* src, parsec_tiled_matrix_t* dest, parsec_operator_t op, void* op_data, bool by_col) {
+  algos::ReduceOp f = [op, op_data](const void* in, void* io, int64_t, int64_t, bool first) { op(my_execution_stream(), in, io, op_data, (int)first); };
+  return by_col ? algos::reduce_col_new(tm_of(src), tm_of(dest), f) : algos::reduce_row_new(tm_of(src), tm_of(dest), f);
+}
+parsec_taskpool_t* parsec_reduce_col_New(const parsec_tiled_matrix_t* src, parsec_tiled_matrix_t* dest, parsec_operator_t op, void* op_data) {
+  return reduce_c(src, dest, op, op_data, true);
+}
+parsec_taskpool_t* parsec_reduce_row_New(const parsec_tiled_matrix_t* src, parsec_tiled_matrix_t* dest, parsec_operator_t op, void* op_data) {
+  return reduce_c(src, dest, op, op_data, false);
+}
+parsec_taskpool_t* parsec_redistribute_New(parsec_tiled_matrix_t* source, parsec_tiled_matrix_t* target, int size_row, int size_col, int disi_source,
+                                           int disj_source, int disi_target, int disj_target) {
+  return algos::redistribute_new(tm_of(source), tm_of(target), size_row, size_col, disi_source, disj_source, disi_target, disj_target);
+}
+int parsec_redistribute(parsec_context_t* parsec, parsec_tiled_matrix_t* source, parsec_tiled_matrix_t* target, int size_row, int size_col, int disi_source,
+                        int disj_source, int disi_target, int disj_target) {
+  return algos::redistribute_ptg(parsec, tm_of(source), tm_of(target), size_row, size_col, disi_source, disj_source, disi_target, disj_target) == 0
+             ? PARSEC_SUCCESS
+             : PARSEC_ERR_NOT_SUPPORTED;
+}
+int parsec_redistribute_dtd(parsec_context_t* parsec, parsec_tiled_matrix_t* source, parsec_tiled_matrix_t* target, int size_row, int size_col,
+                            int disi_source, int disj_source, int disi_target, int disj_target) {
+  return algos::redistribute(parsec, tm_of(source), tm_of(target), size_row, size_col, disi_source, disj_source, disi_target, disj_target) == 0
+             ? PARSEC_SUCCESS
+             : PARSEC_ERROR;
+}
+parsec_taskpool_t* parsec_diag_band_to_rect_New(parsec_tiled_matrix_t* A, parsec_tiled_matrix_t* B, int mt, int nt, int mb, int nb, size_t elem_size) {
+  return algos::diag_band_to_rect_new(tm_of(A), tm_of(B), mt, nt, mb, nb, elem_size);
 }
 
 // --------------------------------------------------------------- arenas

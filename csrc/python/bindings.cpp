@@ -572,10 +572,25 @@ PYBIND11_MODULE(_C, m) {
   m.def("broadcast_new", [](TiledMatrix* A, int64_t rm, int64_t rn, TiledMatrix* dst) { return (Taskpool*)algos::broadcast_new(A, rm, rn, dst); },
         py::return_value_policy::take_ownership);
   m.def("redistribute", [](PxContext& c, TiledMatrix* src, TiledMatrix* dst, int64_t size_row, int64_t size_col, int64_t disi_src, int64_t disj_src, int64_t disi_dst,
-                           int64_t disj_dst) {
+                           int64_t disj_dst, const std::string& method) {
         py::gil_scoped_release rel;
-        return algos::redistribute(c.ctx, src, dst, size_row, size_col, disi_src, disj_src, disi_dst, disj_dst);
-      });
+        if (method == "dtd") return algos::redistribute(c.ctx, src, dst, size_row, size_col, disi_src, disj_src, disi_dst, disj_dst);
+        if (method != "ptg") throw std::invalid_argument("redistribute: method is 'ptg' or 'dtd'");
+        return algos::redistribute_ptg(c.ctx, src, dst, size_row, size_col, disi_src, disj_src, disi_dst, disj_dst);
+      }, py::arg("ctx"), py::arg("src"), py::arg("dst"), py::arg("size_row"), py::arg("size_col"), py::arg("disi_src"), py::arg("disj_src"),
+      py::arg("disi_dst"), py::arg("disj_dst"), py::arg("method") = "ptg",
+      "copy a window between two tiled matrices (PTG redistribute.jdf / redistribute_reshuffle.jdf, or the DTD form)");
+  m.def("redistribute_new", [](TiledMatrix* src, TiledMatrix* dst, int64_t size_row, int64_t size_col, int64_t disi_src, int64_t disj_src, int64_t disi_dst,
+                               int64_t disj_dst) {
+        auto* tp = algos::redistribute_new(src, dst, size_row, size_col, disi_src, disj_src, disi_dst, disj_dst);
+        if (!tp) throw std::invalid_argument("redistribute_new: invalid window");
+        return (Taskpool*)tp;
+      }, py::return_value_policy::take_ownership);
+  m.def("diag_band_to_rect_new", [](TiledMatrix* A, TiledMatrix* B, int mt, int nt, int mb, int nb) {
+        auto* tp = algos::diag_band_to_rect_new(A, B, mt, nt, mb, nb, A->elem_size);
+        if (!tp) throw std::invalid_argument("diag_band_to_rect_new: incompatible shapes");
+        return (Taskpool*)tp;
+      }, py::return_value_policy::take_ownership);
   m.def("dgemm_new", [](double alpha, TiledMatrix* A, TiledMatrix* B, double beta, TiledMatrix* C, int transB) { return (Taskpool*)algos::dgemm_new(alpha, A, B, beta, C, transB); },
         py::arg("alpha"), py::arg("A"), py::arg("B"), py::arg("beta"), py::arg("C"), py::arg("transB") = 0, py::return_value_policy::take_ownership);
   m.def("dtd_dgemm", [](PxContext& c, double alpha, TiledMatrix* A, TiledMatrix* B, double beta, TiledMatrix* C, bool gpu) {

@@ -33,6 +33,7 @@
 
 #define PARSEC_SUCCESS 0
 #define PARSEC_ERROR (-1)
+#define PARSEC_ERR_NOT_SUPPORTED (-2)
 #define PARSEC_ERR_NOT_FOUND (-13)
 
 /* device types (reference mca/device/device.h) */
@@ -245,6 +246,34 @@ int parsec_tiled_matrix_set_storage_device(parsec_tiled_matrix_t* tdesc, int dev
 /* dump / load the local tiles of a matrix to / from a file (one file per process) */
 int parsec_tiled_matrix_data_write(parsec_tiled_matrix_t* tdesc, const char* filename);
 int parsec_tiled_matrix_data_read(parsec_tiled_matrix_t* tdesc, const char* filename);
+
+/* ------------------------------------------------- matrix operator taskpools
+ * (reference data_dist/matrix/matrix.h:143-290: apply.jdf, map_operator.c,
+ * reduce_col/row.jdf, redistribute/redistribute.jdf). Operators run on the owner of the
+ * tile they write. */
+typedef int (*parsec_operator_t)(parsec_execution_stream_t* es, const void* src, void* dst, void* op_data, ...);
+typedef int (*parsec_tiled_matrix_unary_op_t)(parsec_execution_stream_t* es, const parsec_tiled_matrix_t* desc1, void* data1, int uplo, int m, int n,
+                                              void* args);
+/* operation(es, A, tile, PARSEC_MATRIX_FULL, m, n, op_args) on every tile of the uplo part */
+parsec_taskpool_t* parsec_apply_New(parsec_matrix_uplo_t uplo, parsec_tiled_matrix_t* A, parsec_tiled_matrix_unary_op_t operation, void* op_args);
+int parsec_apply(parsec_context_t* parsec, parsec_matrix_uplo_t uplo, parsec_tiled_matrix_t* A, parsec_tiled_matrix_unary_op_t operation, void* op_args);
+/* op(es, src_tile, dest_tile, op_data, m, n) for every tile of dest */
+parsec_taskpool_t* parsec_map_operator_New(const parsec_tiled_matrix_t* src, parsec_tiled_matrix_t* dest, parsec_operator_t op, void* op_data);
+/* chain reduction of the columns (rows) of src into dest(0, n) (dest(m, 0)):
+ * op(es, src_tile, dest_tile, op_data, first) with first = 1 on a chain's first tile */
+parsec_taskpool_t* parsec_reduce_col_New(const parsec_tiled_matrix_t* src, parsec_tiled_matrix_t* dest, parsec_operator_t op, void* op_data);
+parsec_taskpool_t* parsec_reduce_row_New(const parsec_tiled_matrix_t* src, parsec_tiled_matrix_t* dest, parsec_operator_t op, void* op_data);
+/* copy the size_row x size_col window at (disi_source, disj_source) of source to
+ * (disi_target, disj_target) of target, any tile sizes and distributions; NULL /
+ * PARSEC_ERR_NOT_SUPPORTED on an invalid window */
+parsec_taskpool_t* parsec_redistribute_New(parsec_tiled_matrix_t* source, parsec_tiled_matrix_t* target, int size_row, int size_col, int disi_source,
+                                           int disj_source, int disi_target, int disj_target);
+int parsec_redistribute(parsec_context_t* parsec, parsec_tiled_matrix_t* source, parsec_tiled_matrix_t* target, int size_row, int size_col, int disi_source,
+                        int disj_source, int disi_target, int disj_target);
+int parsec_redistribute_dtd(parsec_context_t* parsec, parsec_tiled_matrix_t* source, parsec_tiled_matrix_t* target, int size_row, int size_col,
+                            int disi_source, int disj_source, int disi_target, int disj_target);
+/* diagonal + sub-diagonal tiles of a lower tiled matrix to LAPACK band storage */
+parsec_taskpool_t* parsec_diag_band_to_rect_New(parsec_tiled_matrix_t* A, parsec_tiled_matrix_t* B, int mt, int nt, int mb, int nb, size_t elem_size);
 
 /* ---------------------------------------------------------------- arenas */
 #define PARSEC_ARENA_ALIGNMENT_64b 8

@@ -51,6 +51,7 @@ CORE_SOURCES = [
     "csrc/algos/dtd_builtins.cpp",
     "csrc/capi/capi.cpp",
     "csrc/algos/dpotrf_jdf.cpp",
+    "csrc/algos/redistribute_ptg.cpp",
 ]
 HIP_SOURCES = [
     "csrc/kernels/tile_kernels.hip",
@@ -61,9 +62,14 @@ PY_SOURCES = ["csrc/python/bindings.cpp"]
 PTGPP_SOURCES = ["tools/ptgpp/ptgpp.cpp"]
 # Taskpools written in the JDF language: compiled by parsec-ptgpp into build/gen
 # and linked into the runtime library (reference: DPLASMA ships its *.jdf the same way)
-JDF_SOURCES = ["csrc/algos/jdf/dpotrf_L.jdf"]
+JDF_SOURCES = [
+    "csrc/algos/jdf/dpotrf_L.jdf",
+    "csrc/algos/jdf/redistribute.jdf",
+    "csrc/algos/jdf/redistribute_reshuffle.jdf",
+    "csrc/algos/jdf/diag_band_to_rect.jdf",
+]
 # runtime sources that include generated JDF headers
-JDF_USERS = ["csrc/algos/dpotrf_jdf.cpp"]
+JDF_USERS = ["csrc/algos/dpotrf_jdf.cpp", "csrc/algos/redistribute_ptg.cpp"]
 FORTRAN_SOURCES = ["csrc/fortran/parsecf.F90", "csrc/fortran/parsec_profilef.F90"]
 FLANG = os.path.join(ROCM, "lib", "llvm", "bin", "flang")
 TEST_SOURCES = ["tests/native/test_containers.cpp", "tests/native/test_futures.cpp"]

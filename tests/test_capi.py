@@ -156,3 +156,18 @@ def test_runtime_extras_c_program(tmp_path, pa):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "runtime capi ok" in r.stdout
+
+
+@pytest.mark.parametrize("nranks", [1, 3])
+def test_matrix_operators_c_program(tmp_path, pa, nranks):
+    """parsec_apply / map_operator / reduce_col / redistribute (PTG) from C
+    (reference data_dist/matrix/matrix.h:143-290), 1 and 3 ranks."""
+    exe = tmp_path / "matrix_ops_capi"
+    cmd = ["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-O1", f"-I{ROOT}/include", os.path.join(HERE, "capi", "matrix_ops_capi.c"), "-o", str(exe),
+           f"-L{ROOT}/parsec_amd/lib", "-lparsec_amd", f"-Wl,-rpath,{ROOT}/parsec_amd/lib", "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    rc, outs = launch.launch(nranks, [str(exe)], timeout=90, capture=True, env={"PARSEC_MCA_device_hip_enabled": "0"})
+    text = "".join(o for o, _ in outs)
+    assert rc == 0, text + "".join(e for _, e in outs)
+    assert text.count("bad 0") == nranks

@@ -183,3 +183,42 @@ def test_tiled_matrix_data_write_read(pa, tmp_path):
     assert C.data_read(path) != 0
     assert B.data_read(str(tmp_path / "missing.bin")) != 0
     ctx.fini()
+
+
+@pytest.mark.parametrize("pad", [False, True])
+def test_diag_band_to_rect(pa, pad):
+    """Diagonal + sub-diagonal tiles to LAPACK band storage (reference
+    data_dist/matrix/diag_band_to_rect.jdf), checked against numpy."""
+    ctx = pa.init(2)
+    nb, NT = 6, 5
+    A, S = _mat(pa, nb * NT, nb * NT, nb, seed=7)
+    ncols = (NT + (1 if pad else 0)) * (nb + 2)
+    B = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb + 1, nb + 2, nb + 1, ncols)
+    for n in range(B.nt):
+        B.tile(0, n)[:, :] = 7.0
+    _run(pa, ctx, pa.diag_band_to_rect_new(A, B, NT, NT, nb, nb))
+    for k in range(B.nt):
+        got = B.tile(0, k)
+        want = np.zeros((nb + 1, nb + 2))
+        if k < NT:
+            for j in range(nb):
+                col = k * nb + j
+                for i in range(nb + 1):
+                    r = col + i
+                    # entries below the band's last tile are zero
+                    want[i, j] = S[r, col] if r < nb * NT and (r // nb) <= k + 1 and (k < NT - 1 or r // nb == k) else 0.0
+        assert np.array_equal(got, want), (k, got, want)
+    ctx.fini()
+
+
+def test_redistribute_ptg_and_dtd_agree(pa):
+    """The PTG (default) and DTD forms produce the same target."""
+    outs = []
+    for method in ("ptg", "dtd"):
+        ctx = pa.init(3)
+        Sm, Sd = _mat(pa, 40, 36, 7, seed=1)
+        Dm, Dd = _mat(pa, 44, 40, 5, seed=2)
+        pa.redistribute(ctx, Sm, Dm, 20, 17, 1, 4, 6, 9, method=method)
+        outs.append(_dense(Dm, 44, 40, 5))
+        ctx.fini()
+    assert np.array_equal(outs[0], outs[1])

@@ -123,3 +123,19 @@ def test_distributed_dgeqrf(pa, tmp_path, nranks, P, Q, M, N):
     S = np.random.default_rng(5).standard_normal((M, N))
     G = S.T @ S
     assert np.linalg.norm(R.T @ R - G) / np.linalg.norm(G) < 1e-13
+
+
+@pytest.mark.parametrize("nranks,method,shape", [
+    (2, "ptg", "8 8 5 7 17 13 3 5 9 2"),          # general: different tile sizes, unaligned window
+    (4, "ptg", "7 9 11 6 50 41 2 11 13 20"),
+    (4, "ptg", "8 8 8 8 40 32 8 16 24 0"),        # tile aligned, same tiles: the reshuffle taskpool
+    (3, "ptg", "6 10 10 6 60 50 4 6 1 9"),
+    (4, "dtd", "7 9 11 6 50 41 2 11 13 20"),
+])
+def test_distributed_redistribute(pa, nranks, method, shape):
+    """PTG redistribute.jdf / redistribute_reshuffle.jdf between two different
+    process grids (reference tests/collections/redistribute), and the DTD form."""
+    outs = run_ranks(nranks, method, *shape.split(), worker=os.path.join(HERE, "mp", "dist_redistribute.py"))
+    for rc, out in outs:
+        assert rc == 0 and "bad 0" in out, out
+    assert sum(int(out.split("checked ")[1].split()[0]) for _, out in outs) == int(shape.split()[4]) * int(shape.split()[5])

@@ -67,3 +67,43 @@ def test_dpotrf_host_resident_staged(pa):
         assert gpus[0]["bytes_in"] > 0
     finally:
         ctx.fini()
+
+
+def _gpu_matrix(pa, gpu, M, N, mb, nb, fill):
+    MT, NT = -(-M // mb), -(-N // nb)
+    store = torch.full((NT, MT, nb, mb), float(fill), dtype=torch.float64, device="cuda")
+    A = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, mb, nb, M, N, device=gpu, ptr=store.data_ptr())
+    return A, store
+
+
+def _dense_of(store, M, N, mb, nb):
+    NT, MT = store.shape[0], store.shape[1]
+    return store.permute(1, 3, 0, 2).reshape(MT * mb, NT * nb)[:M, :N]
+
+
+@pytest.mark.parametrize("smb,dmb,win", [(64, 40, (150, 130, 7, 33, 21, 2)), (64, 64, (128, 192, 64, 0, 0, 128))])
+def test_redistribute_hbm_resident(pa, smb, dmb, win):
+    """redistribute.jdf / redistribute_reshuffle.jdf on matrices living in HBM:
+    the HIP bodies (strided device copies) run, nothing is staged to the host."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = pa.init(3)
+    try:
+        gpu = pa.first_gpu_device_index()
+        S, s_store = _gpu_matrix(pa, gpu, 300, 260, smb, smb, 0.0)
+        T, t_store = _gpu_matrix(pa, gpu, 280, 320, dmb, dmb, -1.0)
+        src = torch.arange(300 * 260, dtype=torch.float64, device="cuda").reshape(300, 260)
+        _dense_of(s_store, 300, 260, smb, smb).copy_(src)
+        torch.cuda.synchronize()
+        before = [d for d in pa.devices() if d["type"] == pa.DEV_HIP][0]
+        sr, sc, si, sj, ti, tj = win
+        assert pa.redistribute(ctx, S, T, sr, sc, si, sj, ti, tj) == 0
+        torch.cuda.synchronize()
+        after = [d for d in pa.devices() if d["type"] == pa.DEV_HIP][0]
+        want = torch.full((280, 320), -1.0, dtype=torch.float64, device="cuda")
+        want[ti:ti + sr, tj:tj + sc] = src[si:si + sr, sj:sj + sc]
+        assert torch.equal(_dense_of(t_store, 280, 320, dmb, dmb), want)
+        assert after["executed_tasks"] > before["executed_tasks"]
+        assert after["bytes_in"] == before["bytes_in"]  # device to device only
+    finally:
+        ctx.fini()
