@@ -822,7 +822,12 @@ parsec_dtd_tile_t* parsec_dtd_tile_of(parsec_data_collection_t* dc, parsec_data_
 parsec_dtd_tile_t* parsec_dtd_tile_new(parsec_taskpool_t* tp, int rank, size_t size) {
   return reinterpret_cast<parsec_dtd_tile_t*>(as_dtd(tp)->tile_new(size, rank));
 }
-void parsec_dtd_data_collection_init(parsec_data_collection_t* dc) { (void)dc; }
+// the collection's id names its tiles in remote DTD messages: ids follow the
+// order of registration, identical on every rank (reference insert_function.c:1255)
+void parsec_dtd_data_collection_init(parsec_data_collection_t* dc) {
+  if (!dc) return;
+  dc->dc_id = dc_register_id(impl_of(dc));
+}
 void parsec_dtd_data_collection_fini(parsec_data_collection_t* dc) { (void)dc; }
 parsec_data_t* parsec_dtd_tile_data(parsec_dtd_tile_t* tile) { return tile ? reinterpret_cast<dtd::Tile*>(tile)->data : nullptr; }
 int parsec_dtd_data_flush(parsec_taskpool_t* tp, parsec_dtd_tile_t* tile) { return as_dtd(tp)->data_flush(reinterpret_cast<dtd::Tile*>(tile)); }

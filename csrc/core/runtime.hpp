@@ -389,6 +389,10 @@ struct Taskpool {
   virtual void on_complete_internal() {}
   // Called by context_wait before waiting (DTD: closes insertion).
   virtual void on_context_wait() {}
+  // Called by taskpool_free on a taskpool that has not terminated (DTD: the
+  // application freed it after taskpool_wait, as the reference allows: close
+  // insertion and let it terminate before it is deleted).
+  virtual void on_free_incomplete() {}
   std::function<void()> destructor_hook;
 };
 

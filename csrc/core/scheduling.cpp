@@ -379,6 +379,15 @@ Taskpool::~Taskpool() {
 
 void taskpool_free(Taskpool* tp) {
   if (!tp) return;
+  if (tp->context && !tp->completed.load()) {
+    tp->on_free_incomplete();
+    if (!tp->completed.load()) {
+      // never terminated: at least do not leave a dangling pointer to it
+      std::lock_guard<std::mutex> g(tp->context->tp_m);
+      auto& v = tp->context->taskpools_in_flight;
+      v.erase(std::remove(v.begin(), v.end(), tp), v.end());
+    }
+  }
   if (tp->destructor_hook) tp->destructor_hook();
   for (auto* d : DeviceRegistry::instance().devices) if (d) d->taskpool_unregister(tp);
   delete tp;

@@ -73,6 +73,15 @@ void DtdTaskpool::on_context_wait() {
   release_hold();
 }
 
+void DtdTaskpool::on_free_incomplete() {
+  wait();
+  release_hold();
+  // termination follows the last action (with four-counter detection, after
+  // its waves on the communication thread)
+  Backoff b;
+  while (!completed.load()) b.idle();
+}
+
 DtdTaskClass* DtdTaskpool::create_task_class(const std::string& name, const std::vector<std::pair<int, int>>& params) {
   std::lock_guard<std::mutex> g(classes_m);
   auto it = classes_by_name.find(name);

@@ -120,6 +120,7 @@ class DtdTaskpool : public Taskpool {
   void on_context_wait() override;
   void arm_hold();
   void release_hold();
+  void on_free_incomplete() override;
   // API
   DtdTaskClass* create_task_class(const std::string& name, const std::vector<std::pair<int, int>>& params);
   int add_chore(DtdTaskClass* tc, uint32_t device_type, Hook cpu, std::function<int(GpuExecContext*, Task*)> gpu);

@@ -171,6 +171,7 @@ struct parsec_data_collection_s {
   parsec_datatype_t default_dtt;
   char* key_base;
   void* impl;              /* runtime-side collection object */
+  uint64_t dc_id;          /* set by parsec_dtd_data_collection_init: same value on every rank */
 };
 
 void parsec_data_collection_init(parsec_data_collection_t* dc, int nodes, int myrank);

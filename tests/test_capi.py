@@ -171,3 +171,34 @@ def test_matrix_operators_c_program(tmp_path, pa, nranks):
     text = "".join(o for o, _ in outs)
     assert rc == 0, text + "".join(e for _, e in outs)
     assert text.count("bad 0") == nranks
+
+
+@pytest.fixture(scope="module")
+def dtd_more(tmp_path_factory, pa):
+    exe = tmp_path_factory.mktemp("dtdmore") / "dtd_more"
+    cmd = ["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-O1", "-D_DEFAULT_SOURCE", f"-I{ROOT}/include", os.path.join(HERE, "capi", "dtd_more_capi.c"),
+           "-o", str(exe), f"-L{ROOT}/parsec_amd/lib", "-lparsec_amd", f"-Wl,-rpath,{ROOT}/parsec_amd/lib", "-L/opt/rocm/lib", "-lamdhip64",
+           "-Wl,-rpath,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return str(exe)
+
+
+@pytest.mark.parametrize("args,nranks", [
+    (["interface"], 1),
+    (["hierarchy"], 1), (["hierarchy"], 3),
+    (["template_counter"], 1), (["template_counter"], 4),
+    (["global_id"], 3),
+    (["interleave", ""], 2), (["interleave", "a"], 3), (["interleave", "if"], 4), (["interleave", "afiw"], 2),
+])
+def test_dtd_reference_programs(dtd_more, args, nranks):
+    """dtd_test_insert_task_interface / hierarchy (a task that runs its own DTD
+    taskpool) / template_counter / global_id_for_dc_assumed / interleave_actions
+    (ranks > 0 lag before add / insert / flush / wait), reference tests/dsl/dtd."""
+    rc, outs = launch.launch(nranks, [dtd_more, *args], timeout=90, capture=True, env={"PARSEC_MCA_device_hip_enabled": "0"})
+    text = "".join(o for o, _ in outs)
+    assert rc == 0, text + "".join(e for _, e in outs)
+    assert text.count(f"dtd_more {args[0]} rank") == nranks and "FAILED" not in text
+    if args[0] == "global_id":
+        ids = {line.split("ids ")[1] for line in text.splitlines() if "ids " in line}
+        assert len(ids) == 1, ids  # the same ids on every rank

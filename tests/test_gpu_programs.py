@@ -121,7 +121,7 @@ def test_nvlink_user_device_copies(progs):
     assert r.returncode == 0, r.stdout + r.stderr
     line = [x for x in r.stdout.splitlines() if x.startswith("nvlink ")][-1]
     n = int(line.split("gpus ")[1].split()[0])
-    assert f"gemm1 {8 * n}/{8 * n} gemm2 {8 * n}/{8 * n} user_ptr {n} misplaced 0 cpu 0 bad_c 0 bad_user 0 bad_handle 0" in line, line
+    assert f"gemm1 {8 * n}/{8 * n} gemm2 {8 * n}/{8 * n} user_ptr {8 * n} misplaced 0 cpu 0 bad_c 0 bad_user 0 bad_handle 0" in line, line
 
 
 # ------------------------------------------------------------- write_check
