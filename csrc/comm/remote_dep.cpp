@@ -136,6 +136,7 @@ struct RecvState {
   std::vector<uint8_t> extra;
   DataCopy* data[kMaxFlows] = {};
   uint64_t got[kMaxFlows] = {};
+  char* stage[kMaxFlows] = {};  // pinned landing buffer of host fragments bound for device memory
   int remaining = 0;
 };
 
@@ -182,6 +183,42 @@ std::vector<int> tree_children(int topo, int pos, int n) {
       if (j > pos && pos + j < n) c.push_back(pos + j);
   }
   return c;
+}
+
+// Pinned staging buffers for device tiles sent through host fragments, kept
+// for reuse by size class (comm thread only).
+static std::multimap<size_t, void*> g_pinned_free;
+static size_t pinned_class(size_t bytes) {
+  size_t c = 64 << 10;
+  while (c < bytes) c <<= 1;
+  return c;
+}
+static void* pinned_get(size_t bytes) {
+  const size_t cls = pinned_class(bytes);
+  auto it = g_pinned_free.find(cls);
+  if (it != g_pinned_free.end()) {
+    void* p = it->second;
+    g_pinned_free.erase(it);
+    return p;
+  }
+  void* p = nullptr;
+  if (hipHostMalloc(&p, cls, hipHostMallocDefault) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+  return p;
+}
+static void pinned_put(void* p, size_t bytes) { g_pinned_free.emplace(pinned_class(bytes), p); }
+static void pinned_release_all() {
+  for (auto& kv : g_pinned_free) (void)hipHostFree(kv.second);
+  g_pinned_free.clear();
+}
+// the bytes of one flow as DATA_FRAGMENT messages
+static void send_fragments(int dst, uint64_t recv_id, uint32_t flow, const char* src, size_t bytes) {
+  const size_t frag = g_ce->max_fragment() - sizeof(FragHdr) - 64;
+  for (size_t off = 0; off < bytes || (bytes == 0 && off == 0); off += frag) {
+    FragHdr fh{recv_id, flow, 0, off, bytes};
+    const size_t n = std::min(frag, bytes - off);
+    g_ce->send_am2(TAG_DATA_FRAGMENT, dst, &fh, sizeof(fh), src + off, n);
+    if (bytes == 0) break;
+  }
 }
 
 void release_send(SendState* s) {
@@ -521,23 +558,30 @@ void on_get(int src, int, const void* msg, size_t) {
         continue;
       }
     }
-    const char* src_ptr = static_cast<const char*>(c->device_private);
-    std::vector<char> staged;
-    if (c->device_index != 0) {
-      staged.resize(bytes);
-      device_memcpy(0, staged.data(), c->device_index, c->device_private, bytes);
-      src_ptr = staged.data();
-    }
     CommInfo ci{g.requester, f, (int64_t)bytes, PLANE_HOST, 0};
     comm_trace(k_snd_b, flow_event(g.send_id, f), tpid, &ci);
-    size_t frag = g_ce->max_fragment() - sizeof(FragHdr) - 64;
-    for (size_t off = 0; off < bytes || (bytes == 0 && off == 0); off += frag) {
-      FragHdr fh{g.recv_id, (uint32_t)f, 0, off, bytes};
-      size_t n = std::min(frag, bytes - off);
-      g_ce->send_am2(TAG_DATA_FRAGMENT, g.requester, &fh, sizeof(fh), src_ptr + off, n);
-      if (bytes == 0) break;
+    const int requester = g.requester;
+    const uint64_t recv_id = g.recv_id, ev_id = flow_event(g.send_id, f);
+    if (c->device_index != 0 && bytes) {
+      // device tile without IPC (small allocation, no peer mapping): stage it
+      // through pinned memory on the copy stream; the comm thread keeps serving
+      // and sends the fragments once the copy landed
+      void* pinned = pinned_get(bytes);
+      if (pinned && g_ce->async_copy(pinned, c->device_private, bytes, [=] {
+            send_fragments(requester, recv_id, (uint32_t)f, static_cast<const char*>(pinned), bytes);
+            pinned_put(pinned, bytes);
+            comm_trace(k_snd_e, ev_id, tpid, nullptr);
+            release_send(s);
+          }) == 0)
+        continue;
+      if (pinned) pinned_put(pinned, bytes);
+      std::vector<char> staged(bytes);
+      device_memcpy(0, staged.data(), c->device_index, c->device_private, bytes);
+      send_fragments(requester, recv_id, (uint32_t)f, staged.data(), bytes);
+    } else {
+      send_fragments(requester, recv_id, (uint32_t)f, static_cast<const char*>(c->device_private), bytes);
     }
-    comm_trace(k_snd_e, flow_event(g.send_id, f), tpid, nullptr);
+    comm_trace(k_snd_e, ev_id, tpid, nullptr);
     release_send(s);
   }
 }
@@ -623,17 +667,39 @@ void on_fragment(int src, int, const void* msg, size_t len) {
   }
   size_t n = len - sizeof(FragHdr);
   DataCopy* c = r->data[fh.flow];
-  if (c->device_index == 0) std::memcpy(static_cast<char*>(c->device_private) + fh.offset, (const char*)msg + sizeof(FragHdr), n);
-  else device_memcpy(c->device_index, static_cast<char*>(c->device_private) + fh.offset, 0, (const char*)msg + sizeof(FragHdr), n);
+  const char* payload = (const char*)msg + sizeof(FragHdr);
+  if (c->device_index == 0) {
+    std::memcpy(static_cast<char*>(c->device_private) + fh.offset, payload, n);
+  } else {
+    // device receive buffer: fragments land in pinned memory, one async copy
+    // to the GPU at the end (never a blocking device copy per fragment)
+    if (!r->stage[fh.flow]) r->stage[fh.flow] = static_cast<char*>(pinned_get(std::max<uint64_t>(fh.total, 1)));
+    if (r->stage[fh.flow]) std::memcpy(r->stage[fh.flow] + fh.offset, payload, n);
+    else device_memcpy(c->device_index, static_cast<char*>(c->device_private) + fh.offset, 0, payload, n);
+  }
   r->got[fh.flow] += n;
   if (r->got[fh.flow] < fh.total) return;
-  comm_trace(k_rcv_e, flow_event(fh.recv_id, (int)fh.flow), 0, nullptr);
-  {
-    std::lock_guard<std::mutex> g(g_m);
-    if (--r->remaining > 0) return;
-    g_recvs.erase(r->id);
+  auto flow_landed = [r, recv_id = fh.recv_id, flow = fh.flow] {
+    comm_trace(k_rcv_e, flow_event(recv_id, (int)flow), 0, nullptr);
+    {
+      std::lock_guard<std::mutex> g(g_m);
+      if (--r->remaining > 0) return;
+      g_recvs.erase(r->id);
+    }
+    deliver(r);
+  };
+  if (char* st = r->stage[fh.flow]) {
+    const uint64_t total = fh.total;
+    r->stage[fh.flow] = nullptr;
+    if (g_ce->async_copy(c->device_private, st, total, [st, total, flow_landed] {
+          pinned_put(st, total);
+          flow_landed();
+        }) == 0)
+      return;
+    device_memcpy(c->device_index, c->device_private, 0, st, total);
+    pinned_put(st, total);
   }
-  deliver(r);
+  flow_landed();
 }
 
 void deliver(RecvState* r) {
@@ -808,7 +874,10 @@ void remote_dep_fini(Context* ctx) {
     // owner's hipFree for seconds (2-rank GPU runs, round 2)
     g_ce->release_peer_mappings();
     g_ce->sync();
-    g_ce->post([] { set_my_execution_stream(nullptr); });
+    g_ce->post([] {
+      pinned_release_all();
+      set_my_execution_stream(nullptr);
+    });
   }
   g_comm_es = nullptr;
   if (g_ctx == ctx) g_ctx = nullptr;

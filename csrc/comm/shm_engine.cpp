@@ -606,6 +606,19 @@ int ShmEngine::ipc_copy(int src_rank, void* dst, const void* src, size_t bytes, 
   return 0;
 }
 
+int ShmEngine::async_copy(void* dst, const void* src, size_t bytes, std::function<void()> done) {
+  if (gpu_ < 0 || (int)ipc_q_.size() != size) return -1;
+  hipStream_t st = gpu_copy_stream(gpu_);
+  if (!st) return -1;
+  hipEvent_t ev;
+  if (!ev_pool_.empty()) { ev = ev_pool_.back(); ev_pool_.pop_back(); }
+  else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1;
+  PARSEC_HIP_CHECK_COMM(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st));
+  (void)hipEventRecord(ev, st);
+  ipc_q_[rank].push_back(Xfer{ev, std::move(done)});  // completed by progress() like the pulls
+  return 0;
+}
+
 // ------------------------------------------------------------------ RCCL
 int ShmEngine::init_rccl() {
   if (hipSetDevice(gpu_) != hipSuccess) return -1;

@@ -82,6 +82,10 @@ class ShmEngine : public CommEngine {
   // one copy stream per source rank: pulls from different peers use different
   // xGMI links concurrently instead of queueing behind each other
   int ipc_copy(int src_rank, void* dst, const void* src, size_t bytes, std::function<void()> done);
+  // Copy between this rank's GPU and (pinned) host memory on the GPU's copy
+  // stream; `done` runs on the comm thread once it landed. -1 when there is no
+  // GPU plane (the caller copies synchronously instead).
+  int async_copy(void* dst, const void* src, size_t bytes, std::function<void()> done);
   bool rccl_ok() const { return rccl_ok_; }
   int rccl_send(int peer, const void* buf, size_t bytes, std::function<void()> done);
   int rccl_recv(int peer, void* buf, size_t bytes, std::function<void()> done);

@@ -681,6 +681,74 @@ void DtdTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& ac
   // remote_tasks reference while this thread still installs data
   t->refs.fetch_add(1, std::memory_order_acq_rel);
   lk.unlock();
+  // Installing a received version may copy between a GPU and the host (tile
+  // homes in HBM, receive buffers on the device): that copy and the release
+  // that follows run on a compute thread, not on the communication thread.
+  bool device_copy = false;
+  for (auto& a : t->args) {
+    if (a.flow < 0 || !a.tile || !(act.output_mask & (1u << a.flow)) || !act.data[a.flow]) continue;
+    if ((a.op & OP_MASK) == INPUT || !a.tile->data || act.data[a.flow]->original == a.tile->data) continue;
+    const int home = a.tile->dc ? a.tile->dc->home_device() : 0;
+    if (act.data[a.flow]->device_index != 0 || (!a.tile->is_new && home != 0)) device_copy = true;
+  }
+  if (device_copy && es && es->is_manager && context && !context->simulation && !context->all_es.empty()) {
+    defer_remote_install(t, act);
+    return;
+  }
+  finish_remote_activation(es, t, act);
+}
+
+namespace {
+// A remote activation whose data install copies to / from a GPU, run by a
+// compute thread (internal task; holds a runtime action of the taskpool so it
+// cannot terminate before the successors are released).
+struct RemoteInstall {
+  DtdTaskpool* tp;
+  DtdTask* t;
+  RemoteActivation act;
+};
+struct RemoteInstallClass : TaskClass {
+  RemoteInstallClass() {
+    name = "dtd_remote_install";
+    flags = TC_INTERNAL | TC_NO_PROFILE;
+    Chore ch;
+    ch.type = DEV_CPU;
+    ch.hook = [](ExecutionStream* es, Task* w) {
+      auto* r = static_cast<RemoteInstall*>(w->user);
+      r->tp->finish_remote_activation(es, r->t, r->act);
+      for (DataCopy* c : r->act.data) if (c) data_copy_release(c);
+      r->tp->tdm->taskpool_addto_runtime_actions(r->tp, -1);
+      delete r;
+      return (int)HOOK_DONE;
+    };
+    chores.push_back(std::move(ch));
+  }
+  int complete_execution(ExecutionStream* es, Task* w) const override {
+    (void)es;
+    task_free(w);
+    return 0;
+  }
+};
+const RemoteInstallClass& remote_install_class() {
+  static RemoteInstallClass c;
+  return c;
+}
+}  // namespace
+
+void DtdTaskpool::defer_remote_install(DtdTask* t, RemoteActivation& act) {
+  auto* r = new RemoteInstall{this, t, act};
+  for (DataCopy* c : r->act.data) if (c) data_copy_retain(c);  // the caller releases its references on return
+  tdm->taskpool_addto_runtime_actions(this, 1);
+  ExecutionStream* es = my_execution_stream();
+  Task* w = task_new(es, this, &remote_install_class());
+  w->user = r;
+  w->priority = INT32_MAX / 4;  // data a successor waits for
+  const int nes = (int)context->all_es.size();
+  const int i = (int)(t->seq % (uint64_t)nes);
+  context->scheduler->schedule(context->all_es[i], &w, 1, 0);
+}
+
+void DtdTaskpool::finish_remote_activation(ExecutionStream* es, DtdTask* t, RemoteActivation& act) {
   // install received versions on the tiles the remote task wrote; local
   // consumers then work on the tile's own copy (not the receive buffer), so a
   // local task that is the tile's last writer leaves its result in the tile

@@ -19,6 +19,7 @@
 #include "../core/runtime.hpp"
 
 namespace parsec {
+struct RemoteActivation;
 namespace dtd {
 
 enum Op : int {
@@ -121,6 +122,10 @@ class DtdTaskpool : public Taskpool {
   void arm_hold();
   void release_hold();
   void on_free_incomplete() override;
+  // remote activation, second half: install the received versions on the
+  // tiles, release the local successors (comm thread or a compute thread)
+  void finish_remote_activation(ExecutionStream* es, DtdTask* t, RemoteActivation& act);
+  void defer_remote_install(DtdTask* t, RemoteActivation& act);
   // API
   DtdTaskClass* create_task_class(const std::string& name, const std::vector<std::pair<int, int>>& params);
   int add_chore(DtdTaskClass* tc, uint32_t device_type, Hook cpu, std::function<int(GpuExecContext*, Task*)> gpu);
