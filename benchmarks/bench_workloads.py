@@ -72,6 +72,10 @@ def bench_qr(args):
     storeT = torch.zeros((ln, lm, nb, nb), dtype=torch.float64, device="cuda")
     A = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=Q, device=gpu, ptr=storeA.data_ptr())
     T = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=Q, device=gpu, ptr=storeT.data_ptr())
+    hqr = args.qr_tree == "hqr"
+    if hqr:  # TT-kernel reflectors of the hierarchical tree
+        storeTT = torch.zeros((ln, lm, nb, nb), dtype=torch.float64, device="cuda")
+        TT = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=Q, device=gpu, ptr=storeTT.data_ptr())
     g = torch.Generator(device="cuda").manual_seed(1234 + rank)
     storeA.copy_(torch.rand(storeA.shape, dtype=torch.float64, device="cuda", generator=g) - 0.5)
     backup = storeA.clone()
@@ -80,7 +84,7 @@ def bench_qr(args):
         storeA.copy_(backup)
         storeT.zero_()
         torch.cuda.synchronize()
-        tp = pa.dgeqrf_new(A, T, args.ib)
+        tp = pa.dgeqrf_hqr_new(A, T, TT, args.qr_domain) if hqr else pa.dgeqrf_new(A, T, args.ib)
         ctx.add_taskpool(tp)
         ctx.start()
         ctx.wait()
@@ -104,29 +108,56 @@ def bench_qr(args):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     check = None
-    if args.check and world == 1:
-        # R of the last timed factorization against the input, outside the
-        # timed region: ||R^T R - A^T A||_F / ||A^T A||_F (Q orthogonal =>
-        # A^T A = R^T Q^T Q R = R^T R)
+    if args.check:
+        # R of the last timed factorization against the input, outside the timed
+        # region. Q orthogonal => A^T A = R^T R; probed with a random x from the
+        # local tiles and summed over ranks (4 all-reduces of N-vectors):
+        # ||A^T (A x) - R^T (R x)|| / (||A||_F^2 ||x||)
         torch.cuda.synchronize()
-        Afull = backup.permute(1, 3, 0, 2).reshape(N, N)
-        R = torch.triu(storeA.permute(1, 3, 0, 2).reshape(N, N))
-        AtA = Afull.t() @ Afull
-        del Afull
-        RtR = R.t() @ R
-        del R
-        check = float(torch.linalg.norm(RtR - AtA) / torch.linalg.norm(AtA))
-        del RtR, AtA
-        torch.cuda.empty_cache()
+        gx = torch.Generator(device="cuda").manual_seed(99)
+        x = torch.rand(N, dtype=torch.float64, device="cuda", generator=gx) - 0.5
+        At, Rt = backup.view(-1, nb, nb), storeA.view(-1, nb, nb)
+        loc = [(m, n, A.local_index(m, n)) for n in range(NT) for m in range(NT)]
+        loc = [(m, n, li) for (m, n, li) in loc if li >= 0]
+
+        def allsum(v):
+            if world > 1:
+                dist.all_reduce(v)
+            return v
+
+        def blk(t, m, n):
+            return t.t()[:min(nb, N - m * nb), :min(nb, N - n * nb)]
+
+        def sl(i):
+            return slice(i * nb, min(N, (i + 1) * nb))
+
+        ax, rx = torch.zeros(N, dtype=torch.float64, device="cuda"), torch.zeros(N, dtype=torch.float64, device="cuda")
+        fro = torch.zeros(1, dtype=torch.float64, device="cuda")
+        for m, n, li in loc:
+            a = blk(At[li], m, n)
+            ax[sl(m)] += a @ x[sl(n)]
+            fro += (a * a).sum()
+            if m <= n:
+                r = blk(Rt[li], m, n)
+                rx[sl(m)] += (torch.triu(r) if m == n else r) @ x[sl(n)]
+        allsum(ax), allsum(rx), allsum(fro)
+        ata, rtr = torch.zeros(N, dtype=torch.float64, device="cuda"), torch.zeros(N, dtype=torch.float64, device="cuda")
+        for m, n, li in loc:
+            ata[sl(n)] += blk(At[li], m, n).t() @ ax[sl(m)]
+            if m <= n:
+                r = blk(Rt[li], m, n)
+                rtr[sl(n)] += (torch.triu(r) if m == n else r).t() @ rx[sl(m)]
+        allsum(ata), allsum(rtr)
+        check = float(torch.linalg.norm(ata - rtr) / (fro.item() * torch.linalg.norm(x)))
     ctx.fini()
     if world > 1:
         pa.comm_fini()
     out = {"metric": "GFLOP/s tiled DGEQRF (PTG, HBM-resident)", "value": round(4.0 / 3.0 * N ** 3 / dt / 1e9, 1), "unit": "GFLOP/s",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
-           "dtype": "fp64", "data": "synthetic uniform(-0.5, 0.5)", "config": {"model": "tiled DGEQRF", "N": N, "nb": nb, "ib": args.ib,
+           "dtype": "fp64", "data": "synthetic uniform(-0.5, 0.5)", "config": {"model": "tiled DGEQRF (" + (f"hierarchical, TS domains of {args.qr_domain}, TT binary trees" if hqr else "flat TS tree") + ")", "N": N, "nb": nb, "ib": args.ib,
                                                                              "parallelism": f"2D block-cyclic P{P}xQ{Q}" if Q > 1 else f"1D row-cyclic P{P}x1"}}
     if check is not None:
-        out["residual_RtR_vs_AtA"] = check
+        out["residual_AtAx_vs_RtRx"] = check
     if world > 1:
         dist.destroy_process_group()
     return out, rank
@@ -198,7 +229,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cores", type=int, default=4)
     ap.add_argument("--qr-grid", choices=["1d", "2d"], default="2d", help="qr: process grid over the ranks")
-    ap.add_argument("--check", action="store_true", help="qr: verify R (||R^T R - A^T A|| / ||A^T A||) after the timed steps")
+    ap.add_argument("--check", action="store_true", help="qr: verify R (||A^T A x - R^T R x|| / (||A||_F^2 ||x||), all ranks) after the timed steps")
+    ap.add_argument("--qr-tree", choices=["hqr", "flat"], default="hqr", help="qr: hierarchical (TS domains + TT trees) or flat TS tree")
+    ap.add_argument("--qr-domain", type=int, default=4, help="qr: rows per TS domain of the hierarchical tree")
     args = ap.parse_args()
     if args.n is None:
         args.n = {"qr": 16384, "stencil": 512, "dtd_gemm": 2048}[args.workload]

@@ -140,6 +140,10 @@ static void cpu_apply(const double* V, int ldv, int vrows, bool unit_lower, cons
     }
 }
 
+void cpu_qr_apply(const double* V, int ldv, int vrows, bool unit_lower, const double* T, int ldt, double* A1, int lda1, double* A2, int lda2, int n, int nc) {
+  cpu_apply(V, ldv, vrows, unit_lower, T, ldt, A1, lda1, A2, lda2, n, nc);
+}
+
 // ---------------------------------------------------------------- taskpool
 class DgeqrfTaskpool : public PtgTaskpool {};
 

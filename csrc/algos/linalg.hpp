@@ -21,6 +21,10 @@ ptg::PtgTaskpool* dgemm_new(double alpha, TiledMatrix* A, TiledMatrix* B, double
 // Tiled QR A = QR (Householder, tile algorithm GEQRT/TSQRT/UNMQR/TSMQR). T holds
 // the block reflectors (ib x nb per tile).
 ptg::PtgTaskpool* dgeqrf_new(TiledMatrix* A, TiledMatrix* T, int ib);
+// Hierarchical QR (dgeqrf_hqr.cpp): TS domains of `domain` rows per process row,
+// TT binary trees over domain heads and across the p_rows process rows (<= 0:
+// A's P). TT holds the TT-kernel reflectors (same shape as T).
+ptg::PtgTaskpool* dgeqrf_hqr_new(TiledMatrix* A, TiledMatrix* T, TiledMatrix* TT, int domain, int p_rows);
 // Collection operators (reference data_dist/matrix/apply.jdf, map_operator.c,
 // reduce_col/row.jdf, broadcast.jdf, redistribute/*; see collection_ops.cpp).
 using TileOp = std::function<void(TiledMatrix*, int64_t m, int64_t n, void* tile, void* arg)>;

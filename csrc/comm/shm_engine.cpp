@@ -204,11 +204,56 @@ int ShmEngine::init() {
     std::atomic<bool> done{false};
     post([&] { rc = init_ipc(); done = true; });
     while (!done.load()) std::this_thread::sleep_for(std::chrono::microseconds(200));
-    if (rc.load() == 0) plane_ = PLANE_IPC;
-    else warning("IPC data plane unavailable (rc=%d): device tiles will be staged through host memory", rc.load());
+    // all ranks agree on the plane: a peer mapping that fails (or reads wrong
+    // bytes) anywhere sends every rank to the host plane instead of a fatal
+    // hipIpcOpenMemHandle in the middle of a run
+    const int local = rc.load() == 0 ? probe_ipc() : rc.load();
+    const uint64_t bad = allreduce_max(local != 0 ? 1 : 0);
+    if (bad == 0) plane_ = PLANE_IPC;
+    else warning("IPC data plane unavailable (this rank rc=%d): device tiles will be staged through host memory", local);
   }
   sync();
   return 0;
+}
+
+int ShmEngine::probe_ipc() {
+  if (hipSetDevice(gpu_) != hipSuccess) return -10;
+  const size_t bytes = (size_t)64 << 20;  // far above comm_ipc_min_alloc: a buffer object of its own
+  void* buf = nullptr;
+  int rc = 0;
+  if (hipMalloc(&buf, bytes) != hipSuccess) { (void)hipGetLastError(); rc = -11; }
+  if (rc == 0 && hipMemset(buf, 0x40 + (rank & 0x3f), bytes) != hipSuccess) rc = -12;
+  if (rc == 0 && hipDeviceSynchronize() != hipSuccess) rc = -13;
+  hipIpcMemHandle_t h{};
+  if (rc == 0 && hipIpcGetMemHandle(&h, buf) != hipSuccess) rc = -14;
+  std::memcpy(me_->ipc_probe, &h, sizeof(h));
+  if (allreduce_max(rc != 0 ? 1 : 0) != 0) {  // someone could not even export
+    if (buf) (void)hipFree(buf);
+    (void)hipGetLastError();
+    return rc ? rc : -15;
+  }
+  std::vector<unsigned char> got(4096);
+  for (int r = 0; r < size && rc == 0; ++r) {
+    if (r == rank) continue;
+    hipIpcMemHandle_t ph;
+    std::memcpy(&ph, static_cast<ShmHeader*>(maps_[r])->ipc_probe, sizeof(ph));
+    void* p = nullptr;
+    if (hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess) != hipSuccess) { (void)hipGetLastError(); rc = -20 - r; break; }
+    // the tail of the peer buffer, through the same copy stream the pulls use
+    hipStream_t st = gpu_copy_stream(gpu_);
+    if (hipMemcpyAsync(got.data(), static_cast<char*>(p) + bytes - got.size(), got.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      (void)hipGetLastError();
+      rc = -40 - r;
+    }
+    for (unsigned char c : got)
+      if (rc == 0 && c != (unsigned char)(0x40 + (r & 0x3f))) rc = -60 - r;
+    (void)hipIpcCloseMemHandle(p);
+  }
+  (void)allreduce_max(0);  // every peer is done reading before the buffers go
+  (void)hipFree(buf);
+  if (rc) warning("IPC probe failed on rank %d (rc=%d)", rank, rc);
+  return rc;
 }
 
 ShmRing* ShmEngine::in_ring(int src) {

@@ -28,6 +28,8 @@ struct ShmHeader {
   // RCCL unique ids for the directed pair (this rank -> d), written by this rank
   char nccl_ids[64][128];
   std::atomic<uint32_t> ids_ready;
+  // IPC start-up probe: handle of a device buffer filled with this rank's byte
+  char ipc_probe[64];
 };
 
 class ShmEngine : public CommEngine {
@@ -158,6 +160,7 @@ class ShmEngine : public CommEngine {
   std::mutex ipc_m_;  // ipc_exported_ / ipc_opened_ (exports happen on worker threads too)
   std::map<std::pair<int, std::string>, void*> ipc_opened_;                    // (src, handle) -> base
   int init_ipc();
+  int probe_ipc();  // every rank opens every peer's probe buffer and checks its bytes
   // one-sided: this rank's registrations and the gets waiting for fragments
   struct Region {
     void* ptr;

@@ -125,6 +125,10 @@ struct QrPanelDesc {
   double* Vcopy;   // GEQRT only (optional): clean unit-lower V (m1 x min(m1,n), ld m1)
   int m1;          // GEQRT: rows of the tile (min(m1, n) reflectors)
   int m2, n;       // TSQRT: rows of A2; columns
+  // TTQRT: A2 is a zero-padded scratch copy of the upper trapezoid of `tri`
+  // (m2 x n, ld ldtri), filled before the panel; V2's upper part goes back after
+  double* tri;
+  int ldtri;
 };
 
 // Apply Q^T of a QR panel: UNMQR (A1 == nullptr: C = A2 := Q^T C with C and the

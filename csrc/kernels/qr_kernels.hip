@@ -1036,8 +1036,59 @@ static bool launch_qr_panel_fast(const QrPanelDesc* descs, int n, hipStream_t st
 // j0 of every task of the batch, (1) factor the sub-panel in registers, (2) apply
 // its block reflector to the trailing columns with the grouped MFMA GEMMs, (3)
 // extend the tile's compact-WY T: T(0:j0, j0:j0+jb) = -T11 (V1^T V2) T22.
+// TTQRT staging: dst := the upper trapezoid of src (rows r <= c), and with
+// zero_lower the strictly lower part of dst := 0 (m x n each, one y-block per
+// matrix, 4 columns per 256-thread block).
+constexpr int kMaxCopyBatch = 48;
+struct TriCopyArgs {
+  int count, zero_lower;
+  const double* src[kMaxCopyBatch];
+  double* dst[kMaxCopyBatch];
+  int lds[kMaxCopyBatch], ldd[kMaxCopyBatch], m[kMaxCopyBatch], n[kMaxCopyBatch];
+};
+__global__ __launch_bounds__(256) void tri_copy_kernel(const TriCopyArgs a) {
+  const int i = blockIdx.y;
+  const double* __restrict__ s = a.src[i];
+  double* __restrict__ d = a.dst[i];
+  const int rows = a.m[i], cols = a.n[i];
+  for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cols; c += gridDim.x * 4)
+    for (int r = threadIdx.x & 63; r < rows; r += 64) {
+      if (r <= c) d[(size_t)c * a.ldd[i] + r] = s[(size_t)c * a.lds[i] + r];
+      else if (a.zero_lower) d[(size_t)c * a.ldd[i] + r] = 0.0;
+    }
+}
+static void launch_tri_copies(const QrPanelDesc* descs, int n, bool pre, hipStream_t stream) {
+  TriCopyArgs a{};
+  a.zero_lower = pre ? 1 : 0;
+  int maxc = 1;
+  auto flush = [&]() {
+    if (a.count) hipLaunchKernelGGL(tri_copy_kernel, dim3(std::min(64, (maxc + 3) / 4), a.count), dim3(256), 0, stream, a);
+    a.count = 0;
+  };
+  for (int i = 0; i < n; ++i) {
+    const QrPanelDesc& d = descs[i];
+    if (!d.tri) continue;
+    const int j = a.count++;
+    a.src[j] = pre ? d.tri : d.A2; a.lds[j] = pre ? d.ldtri : d.lda2;
+    a.dst[j] = pre ? d.A2 : d.tri; a.ldd[j] = pre ? d.lda2 : d.ldtri;
+    a.m[j] = d.m2; a.n[j] = d.n;
+    maxc = std::max(maxc, d.n);
+    if (a.count == kMaxCopyBatch) flush();
+  }
+  flush();
+}
+
+static void launch_qr_panel_core(const QrPanelDesc* descs, int n, hipStream_t stream, double* ws);
 void launch_qr_panel_blocked(const QrPanelDesc* descs, int n, hipStream_t stream, double* ws) {
   if (n <= 0) return;
+  bool any_tri = false;
+  for (int i = 0; i < n; ++i) any_tri |= descs[i].tri != nullptr;
+  if (any_tri) launch_tri_copies(descs, n, true, stream);
+  launch_qr_panel_core(descs, n, stream, ws);
+  if (any_tri) launch_tri_copies(descs, n, false, stream);
+}
+
+static void launch_qr_panel_core(const QrPanelDesc* descs, int n, hipStream_t stream, double* ws) {
   static const bool legacy = getenv("PARSEC_QR_LEGACY_PANEL") != nullptr;
   if (!legacy && launch_qr_panel_fast(descs, n, stream, ws)) return;
   struct Task {

@@ -45,6 +45,7 @@ CORE_SOURCES = [
     "csrc/dtd/dtd.cpp",
     "csrc/algos/dpotrf.cpp",
     "csrc/algos/dgeqrf.cpp",
+    "csrc/algos/dgeqrf_hqr.cpp",
     "csrc/algos/stencil3d.cpp",
     "csrc/algos/collection_ops.cpp",
     "csrc/algos/host_gemm.cpp",

@@ -34,7 +34,9 @@ static void* buf_alloc(size_t bytes) {
 #ifdef CE_WITH_HIP
     if (use_gpu) {
         void* p = NULL;
-        if (hipMalloc(&p, bytes < (4u << 20) ? (4u << 20) : bytes) != hipSuccess) return NULL; /* >= 2 MB: IPC-exportable */
+        /* a buffer object of its own (small hipMallocs can be carved out of a shared
+         * one that a peer cannot attach): 64 MB, far above comm_ipc_min_alloc */
+        if (hipMalloc(&p, bytes < (64u << 20) ? (64u << 20) : bytes) != hipSuccess) return NULL;
         return p;
     }
 #endif

@@ -1,6 +1,6 @@
 """Worker: one rank of a distributed PTG DGEQRF on host tiles (CPU bodies),
 2D block-cyclic P x Q; writes this rank's tiles of R (zeros elsewhere).
-argv: rank size job M N nb P Q outdir"""
+argv: rank size job M N nb P Q outdir [hqr_domain]"""
 import os
 import sys
 
@@ -26,7 +26,11 @@ def main():
                 blk = S[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb]
                 A.tile(m, n)[:blk.shape[0], :blk.shape[1]] = blk
                 A.mark_host_modified(m, n)
-    tp = pa.dgeqrf_new(A, T, 32)
+    if len(sys.argv) > 10 and int(sys.argv[10]) > 0:  # hierarchical tree, TS domains of argv[10] rows
+        TT = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, M, N, P=P, Q=Q)
+        tp = pa.dgeqrf_hqr_new(A, T, TT, int(sys.argv[10]))
+    else:
+        tp = pa.dgeqrf_new(A, T, 32)
     ctx.add_taskpool(tp)
     ctx.start()
     ctx.wait()

@@ -5,7 +5,7 @@ tests/test_multirank_gpu.py; each rank validates what it owns.
 
 argv: case rank size job [case args...]
   dpotrf N nb P Q        HBM-resident 2D block-cyclic Cholesky, local tiles vs torch
-  dgeqrf N nb P outdir   1D row-cyclic QR, writes this rank's tiles of R
+  dgeqrf N nb P outdir [Q dom]   P x Q QR (dom > 0: hierarchical tree), writes this rank's tiles of R
   stencil nx ny nz b iters   DTD 7-point stencil on GPU bodies, local blocks vs numpy
 """
 import os
@@ -93,15 +93,21 @@ def case_dpotrf(pa, torch, rank, size, job, N, nb, P, Q):
     return worst < 1e-12 and info_v == 0 and stats["executed_tasks"] > 0
 
 
-def case_dgeqrf(pa, torch, rank, size, job, N, nb, P, outdir):
+def case_dgeqrf(pa, torch, rank, size, job, N, nb, P, outdir, Q=1, dom=0):
+    """P x Q block-cyclic QR; dom > 0 selects the hierarchical tree (TS domains of
+    dom rows, TT trees inside and across process rows)."""
     ctx = _setup(pa, rank, size, job)
     gpu = pa.first_gpu_device_index()
     NT = (N + nb - 1) // nb
-    lm = sum(1 for g in range(NT) if g % P == rank)
-    storeA = torch.zeros((NT, lm, nb, nb), dtype=torch.float64, device="cuda")
-    storeT = torch.zeros((NT, lm, nb, nb), dtype=torch.float64, device="cuda")
-    A = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=1, device=gpu, ptr=storeA.data_ptr())
-    T = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=1, device=gpu, ptr=storeT.data_ptr())
+    myrow, mycol = rank // Q, rank % Q
+    lm = sum(1 for g in range(NT) if g % P == myrow)
+    ln = sum(1 for g in range(NT) if g % Q == mycol)
+    storeA = torch.zeros((ln, lm, nb, nb), dtype=torch.float64, device="cuda")
+    storeT = torch.zeros((ln, lm, nb, nb), dtype=torch.float64, device="cuda")
+    storeTT = torch.zeros((ln, lm, nb, nb), dtype=torch.float64, device="cuda")
+    A = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=Q, device=gpu, ptr=storeA.data_ptr())
+    T = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=Q, device=gpu, ptr=storeT.data_ptr())
+    TT = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=Q, device=gpu, ptr=storeTT.data_ptr())
     g = torch.Generator().manual_seed(77)
     Ahost = torch.rand((N, N), dtype=torch.float64, generator=g) - 0.5
     Afull = Ahost.cuda()
@@ -120,7 +126,7 @@ def case_dgeqrf(pa, torch, rank, size, job, N, nb, P, outdir):
         torch.cuda.synchronize()
         if size > 1:
             pa.comm_barrier()
-        tp = pa.dgeqrf_new(A, T, 32)
+        tp = pa.dgeqrf_hqr_new(A, T, TT, dom) if dom > 0 else pa.dgeqrf_new(A, T, 32)
         ctx.add_taskpool(tp)
         ctx.start()
         ctx.wait()
@@ -140,6 +146,8 @@ def case_dgeqrf(pa, torch, rank, size, job, N, nb, P, outdir):
             rows = slice(m * nb, (m + 1) * nb)
             sg = np.sign(np.diag(part[rows, rows])) * np.sign(np.diag(Rref[rows, rows]))
             for n in range(m, NT):
+                if A.local_index(m, n) < 0:  # 2D grids: another rank's tile of this row
+                    continue
                 cols = slice(n * nb, (n + 1) * nb)
                 e = np.abs(sg[:, None] * part[rows, cols] - Rref[rows, cols]).max() / np.abs(Rref).max()
                 if e > 1e-10:
@@ -191,7 +199,8 @@ def main():
     if case == "dpotrf":
         ok = case_dpotrf(pa, torch, rank, size, job, *map(int, rest))
     elif case == "dgeqrf":
-        ok = case_dgeqrf(pa, torch, rank, size, job, int(rest[0]), int(rest[1]), int(rest[2]), rest[3])
+        extra = [int(x) for x in rest[4:6]]
+        ok = case_dgeqrf(pa, torch, rank, size, job, int(rest[0]), int(rest[1]), int(rest[2]), rest[3], *extra)
     elif case == "stencil":
         ok = case_stencil(pa, torch, rank, size, job, *map(int, rest))
     else:

@@ -125,6 +125,21 @@ def test_distributed_dgeqrf(pa, tmp_path, nranks, P, Q, M, N):
     assert np.linalg.norm(R.T @ R - G) / np.linalg.norm(G) < 1e-13
 
 
+@pytest.mark.parametrize("nranks,P,Q,M,N,dom", [(2, 2, 1, 128, 96, 2), (4, 2, 2, 160, 128, 2), (4, 4, 1, 192, 96, 1), (3, 3, 1, 112, 80, 3)])
+def test_distributed_dgeqrf_hqr(pa, tmp_path, nranks, P, Q, M, N, dom):
+    """Hierarchical QR over P x Q ranks: TS domains and TT trees inside a process
+    row, TT binary tree across the P process rows (the only cross-rank kills)."""
+    import numpy as np
+
+    outs = run_ranks(nranks, M, N, 16, P, Q, str(tmp_path), dom, worker=os.path.join(HERE, "mp", "dist_qr.py"))
+    for rc, out in outs:
+        assert rc == 0, out
+    R = sum(np.load(tmp_path / f"R{r}.npy") for r in range(nranks))
+    S = np.random.default_rng(5).standard_normal((M, N))
+    G = S.T @ S
+    assert np.linalg.norm(R.T @ R - G) / np.linalg.norm(G) < 1e-13
+
+
 @pytest.mark.parametrize("nranks,method,shape", [
     (2, "ptg", "8 8 5 7 17 13 3 5 9 2"),          # general: different tile sizes, unaligned window
     (4, "ptg", "7 9 11 6 50 41 2 11 13 20"),

@@ -77,8 +77,16 @@ def _gpu_matrix(pa, gpu, M, N, mb, nb, fill):
 
 
 def _dense_of(store, M, N, mb, nb):
+    """A dense COPY of the tiled store (the permuted reshape cannot be a view)."""
     NT, MT = store.shape[0], store.shape[1]
     return store.permute(1, 3, 0, 2).reshape(MT * mb, NT * nb)[:M, :N]
+
+
+def _fill_store(store, dense, mb, nb):
+    NT, MT = store.shape[0], store.shape[1]
+    pad = torch.zeros((MT * mb, NT * nb), dtype=store.dtype, device=store.device)
+    pad[:dense.shape[0], :dense.shape[1]] = dense
+    store.copy_(pad.reshape(MT, mb, NT, nb).permute(2, 0, 3, 1))
 
 
 @pytest.mark.parametrize("smb,dmb,win", [(64, 40, (150, 130, 7, 33, 21, 2)), (64, 64, (128, 192, 64, 0, 0, 128))])
@@ -93,7 +101,7 @@ def test_redistribute_hbm_resident(pa, smb, dmb, win):
         S, s_store = _gpu_matrix(pa, gpu, 300, 260, smb, smb, 0.0)
         T, t_store = _gpu_matrix(pa, gpu, 280, 320, dmb, dmb, -1.0)
         src = torch.arange(300 * 260, dtype=torch.float64, device="cuda").reshape(300, 260)
-        _dense_of(s_store, 300, 260, smb, smb).copy_(src)
+        _fill_store(s_store, src, smb, smb)
         torch.cuda.synchronize()
         before = [d for d in pa.devices() if d["type"] == pa.DEV_HIP][0]
         sr, sc, si, sj, ti, tj = win

@@ -91,6 +91,24 @@ def test_dgeqrf_two_ranks_ipc(pa):
     assert np.linalg.norm(R.T @ R - AtA) / np.linalg.norm(AtA) < 1e-12
 
 
+def test_dgeqrf_hqr_2x2_ipc(pa):
+    """Hierarchical QR on a 2 x 2 process grid (4 ranks sharing the GPU): TS
+    domains and TT merges inside each process row on the GPU kernels, the TT
+    kill across the two process rows through the device plane; R^T R = A^T A."""
+    _gpu()
+    import torch
+
+    N, nb = 2048, 256
+    with tempfile.TemporaryDirectory() as d:
+        for rc, out in _run("dgeqrf", 4, N, nb, 2, d, 2, 2):
+            assert rc == 0, out
+        R = sum(np.load(os.path.join(d, f"R{r}.npy")) for r in range(4))
+    g = torch.Generator().manual_seed(77)
+    A = (torch.rand((N, N), dtype=torch.float64, generator=g) - 0.5).numpy()
+    AtA = A.T @ A
+    assert np.linalg.norm(R.T @ R - AtA) / np.linalg.norm(AtA) < 1e-12
+
+
 def test_stencil_four_ranks_ipc(pa):
     """DTD 3D stencil over 4 ranks with GPU bodies: halo faces cross ranks
     through the device plane."""
