@@ -154,7 +154,7 @@ def bench_qr(args):
         pa.comm_fini()
     out = {"metric": "GFLOP/s tiled DGEQRF (PTG, HBM-resident)", "value": round(4.0 / 3.0 * N ** 3 / dt / 1e9, 1), "unit": "GFLOP/s",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
-           "dtype": "fp64", "data": "synthetic uniform(-0.5, 0.5)", "config": {"model": "tiled DGEQRF (" + (f"hierarchical, TS domains of {args.qr_domain}, TT binary trees" if hqr else "flat TS tree") + ")", "N": N, "nb": nb, "ib": args.ib,
+           "dtype": "fp64", "data": "synthetic uniform(-0.5, 0.5)", "config": {"model": "tiled DGEQRF (" + ((f"hierarchical, TS domains of {args.qr_domain}" if args.qr_domain > 0 else "hierarchical, flat TS per process row") + ", TT binary trees" if hqr else "flat TS tree") + ")", "N": N, "nb": nb, "ib": args.ib,
                                                                              "parallelism": f"2D block-cyclic P{P}xQ{Q}" if Q > 1 else f"1D row-cyclic P{P}x1"}}
     if check is not None:
         out["residual_AtAx_vs_RtRx"] = check
@@ -231,7 +231,8 @@ def main():
     ap.add_argument("--qr-grid", choices=["1d", "2d"], default="2d", help="qr: process grid over the ranks")
     ap.add_argument("--check", action="store_true", help="qr: verify R (||A^T A x - R^T R x|| / (||A||_F^2 ||x||), all ranks) after the timed steps")
     ap.add_argument("--qr-tree", choices=["hqr", "flat"], default="hqr", help="qr: hierarchical (TS domains + TT trees) or flat TS tree")
-    ap.add_argument("--qr-domain", type=int, default=4, help="qr: rows per TS domain of the hierarchical tree")
+    ap.add_argument("--qr-domain", type=int, default=0,
+                    help="qr: rows per TS domain of the hierarchical tree (0: one flat TS chain per process row, TT binary tree across process rows; 1 GPU measured fastest flat: profiles/r3_qr_tree_ab.jsonl)")
     args = ap.parse_args()
     if args.n is None:
         args.n = {"qr": 16384, "stencil": 512, "dtd_gemm": 2048}[args.workload]

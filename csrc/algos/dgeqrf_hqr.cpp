@@ -123,7 +123,7 @@ ptg::PtgTaskpool* dgeqrf_hqr_new(TiledMatrix* A, TiledMatrix* T, TiledMatrix* TT
   const int64_t nb = A->nb;
   const int ld = (int)A->mb, ldt = (int)T->mb, ldtt = (int)TT->mb;
   auto tree = std::make_shared<HqrTree>();
-  tree->build((int)MT, (int)KT, p_rows, domain <= 0 ? 4 : domain);
+  tree->build((int)MT, (int)KT, p_rows, domain <= 0 ? (int)MT : domain);  // <= 0: one TS chain per process row
   tp->tree = tree;
   const HqrTree* tr = tree.get();
   auto rows = [A](int64_t m) { return (int)A->tile_rows(m); };

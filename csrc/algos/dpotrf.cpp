@@ -277,11 +277,11 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
     g.type = DEV_HIP;
     g.gpu = [rows, cols, ld](GpuExecContext* c, Task* t) {
       int k = t->locals[0], m = t->locals[1];
-      GemmDesc gd;
+      GemmDesc gd{};
       gd.A = static_cast<double*>(c->ptr(0)); gd.B = gd.A; gd.C = static_cast<double*>(c->ptr(1));
       gd.m = rows(m); gd.n = rows(m); gd.k = cols(k);
       gd.lda = gd.ldb = gd.ldc = (int)ld;
-      gd.alpha = -1.0; gd.beta = 1.0; gd.transA = 0; gd.transB = 1; gd.lower_only = 1; gd.pad = 0;
+      gd.alpha = -1.0; gd.beta = 1.0; gd.transA = 0; gd.transB = 1; gd.lower_only = 1; gd.a_lower = 0;
       c->batch->gemm.push_back(gd);
       return HOOK_DONE;
     };
@@ -323,11 +323,11 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host) {
     g.type = DEV_HIP;
     g.gpu = [rows, cols, ld](GpuExecContext* c, Task* t) {
       int k = t->locals[0], m = t->locals[1], n = t->locals[2];
-      GemmDesc gd;
+      GemmDesc gd{};
       gd.A = static_cast<double*>(c->ptr(0)); gd.B = static_cast<double*>(c->ptr(1)); gd.C = static_cast<double*>(c->ptr(2));
       gd.m = rows(m); gd.n = rows(n); gd.k = cols(k);
       gd.lda = gd.ldb = gd.ldc = (int)ld;
-      gd.alpha = -1.0; gd.beta = 1.0; gd.transA = 0; gd.transB = 1; gd.lower_only = 0; gd.pad = 0;
+      gd.alpha = -1.0; gd.beta = 1.0; gd.transA = 0; gd.transB = 1; gd.lower_only = 0; gd.a_lower = 0;
       c->batch->gemm.push_back(gd);
       return HOOK_DONE;
     };

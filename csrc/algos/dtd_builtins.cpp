@@ -40,11 +40,11 @@ std::function<int(GpuExecContext*, Task*)> builtin_dtd_gpu_body(const std::strin
   if (name == "dgemm")
     return [](GpuExecContext* c, Task* t) {
       Vals v(t);
-      GemmDesc g;
+      GemmDesc g{};
       g.A = dptr(c, t, argidx_of_flow(t, 0)); g.B = dptr(c, t, argidx_of_flow(t, 1)); g.C = dptr(c, t, argidx_of_flow(t, 2));
       g.m = v.i(0); g.n = v.i(1); g.k = v.i(2);
       g.alpha = v.d(3, 1.0); g.beta = v.d(4, 1.0);
-      g.transA = 0; g.transB = (uint8_t)v.i(5, 1); g.lower_only = 0; g.pad = 0;
+      g.transA = 0; g.transB = (uint8_t)v.i(5, 1); g.lower_only = 0; g.a_lower = 0;
       g.lda = g.m; g.ldb = g.transB ? g.n : g.k; g.ldc = g.m;
       c->batch->gemm.push_back(g);
       return (int)HOOK_DONE;
@@ -52,11 +52,11 @@ std::function<int(GpuExecContext*, Task*)> builtin_dtd_gpu_body(const std::strin
   if (name == "dsyrk")
     return [](GpuExecContext* c, Task* t) {
       Vals v(t);
-      GemmDesc g;
+      GemmDesc g{};
       g.A = dptr(c, t, argidx_of_flow(t, 0)); g.B = g.A; g.C = dptr(c, t, argidx_of_flow(t, 1));
       g.m = g.n = v.i(0); g.k = v.i(1);
       g.alpha = v.d(2, -1.0); g.beta = v.d(3, 1.0);
-      g.transA = 0; g.transB = 1; g.lower_only = 1; g.pad = 0;
+      g.transA = 0; g.transB = 1; g.lower_only = 1; g.a_lower = 0;
       g.lda = g.ldb = g.ldc = g.m;
       c->batch->gemm.push_back(g);
       return (int)HOOK_DONE;

@@ -21,7 +21,8 @@ ptg::PtgTaskpool* dgemm_new(double alpha, TiledMatrix* A, TiledMatrix* B, double
 // Tiled QR A = QR (Householder, tile algorithm GEQRT/TSQRT/UNMQR/TSMQR). T holds
 // the block reflectors (ib x nb per tile).
 ptg::PtgTaskpool* dgeqrf_new(TiledMatrix* A, TiledMatrix* T, int ib);
-// Hierarchical QR (dgeqrf_hqr.cpp): TS domains of `domain` rows per process row,
+// Hierarchical QR (dgeqrf_hqr.cpp): TS domains of `domain` rows per process row
+// (<= 0: all of them, i.e. flat inside a process row),
 // TT binary trees over domain heads and across the p_rows process rows (<= 0:
 // A's P). TT holds the TT-kernel reflectors (same shape as T).
 ptg::PtgTaskpool* dgeqrf_hqr_new(TiledMatrix* A, TiledMatrix* T, TiledMatrix* TT, int domain, int p_rows);

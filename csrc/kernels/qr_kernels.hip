@@ -1195,42 +1195,41 @@ size_t qr_apply_workspace_bytes(const QrApplyDesc* descs, int n) {
   return b;
 }
 
-// Q^T application, phase by phase over all descriptors (one grouped launch each).
+// Q^T application over all descriptors in three grouped MFMA launches
+// (Q^T = I - V T^T V^T, T upper with zeros below):
+//   1. W  = V^T C2 (+ A1)                 (TSMQR: A1 enters as the beta operand)
+//   2. W2 = T^T W, A1 -= W2              (T^T lower triangular: the k range of a
+//                                         row block stops at its diagonal; the A1
+//                                         update rides in the epilogue)
+//   3. C2 -= V W2
 void launch_qr_apply(const QrApplyDesc* descs, int n, hipStream_t stream, double* ws) {
   if (n <= 0) return;
-  std::vector<double*> W(n), W2(n);
+  std::vector<GemmDesc> g1, g2, g3;
   size_t off = 0;
   for (int i = 0; i < n; ++i) {
-    const size_t sz = (size_t)descs[i].n * descs[i].ncols;
-    W[i] = ws + off;
-    W2[i] = ws + off + sz;
-    off += 2 * sz;
-  }
-  auto gemm = [](const double* A, const double* B, double* C, int m, int nn, int k, int lda, int ldb, int ldc, double alpha, double beta, int ta) {
-    GemmDesc g{A, B, C, m, nn, k, lda, ldb, ldc, alpha, beta, (uint8_t)ta, 0, 0, 0};
-    return g;
-  };
-  // W = A1 (TSMQR)
-  std::vector<Axpy2D> cp;
-  for (int i = 0; i < n; ++i)
-    if (descs[i].A1) cp.push_back(Axpy2D{descs[i].A1, W[i], descs[i].lda1, descs[i].n, descs[i].n, descs[i].ncols, 1.0, 0.0});
-  launch_axpy(cp, stream);
-  // W (+)= V^T C
-  std::vector<GemmDesc> g1, g2, g3;
-  for (int i = 0; i < n; ++i) {
     const QrApplyDesc& d = descs[i];
-    const int vrows = d.m2;
-    g1.push_back(gemm(d.V, d.A2, W[i], d.n, d.ncols, vrows, d.ldv, d.lda2, d.n, 1.0, d.A1 ? 1.0 : 0.0, 1));
-    g2.push_back(gemm(d.T, W[i], W2[i], d.n, d.ncols, d.n, d.ldt, d.n, d.n, 1.0, 0.0, 1));
-    g3.push_back(gemm(d.V, W2[i], d.A2, vrows, d.ncols, d.n, d.ldv, d.n, d.lda2, -1.0, 1.0, 0));
+    const size_t sz = (size_t)d.n * d.ncols;
+    double* W = ws + off;
+    double* W2 = ws + off + sz;
+    off += 2 * sz;
+    GemmDesc a{};
+    a.A = d.V; a.lda = d.ldv; a.B = d.A2; a.ldb = d.lda2; a.C = W; a.ldc = d.n;
+    a.m = d.n; a.n = d.ncols; a.k = d.m2; a.transA = 1; a.alpha = 1.0;
+    if (d.A1) { a.beta = 1.0; a.Cin = d.A1; a.ldcin = d.lda1; }
+    g1.push_back(a);
+    GemmDesc b{};
+    b.A = d.T; b.lda = d.ldt; b.B = W; b.ldb = d.n; b.C = W2; b.ldc = d.n;
+    b.m = d.n; b.n = d.ncols; b.k = d.n; b.transA = 1; b.a_lower = 1; b.alpha = 1.0; b.beta = 0.0;
+    if (d.A1) { b.C2 = d.A1; b.ldc2 = d.lda1; }
+    g2.push_back(b);
+    GemmDesc c{};
+    c.A = d.V; c.lda = d.ldv; c.B = W2; c.ldb = d.n; c.C = d.A2; c.ldc = d.lda2;
+    c.m = d.m2; c.n = d.ncols; c.k = d.n; c.alpha = -1.0; c.beta = 1.0;
+    g3.push_back(c);
   }
   launch_gemm_batch(g1.data(), (int)g1.size(), stream);
-  launch_gemm_batch(g2.data(), (int)g2.size(), stream);  // W2 = T^T W
-  std::vector<Axpy2D> up;
-  for (int i = 0; i < n; ++i)
-    if (descs[i].A1) up.push_back(Axpy2D{W2[i], descs[i].A1, descs[i].n, descs[i].lda1, descs[i].n, descs[i].ncols, -1.0, 1.0});
-  launch_axpy(up, stream);                                  // A1 -= W2
-  launch_gemm_batch(g3.data(), (int)g3.size(), stream);  // C / A2 -= V W2
+  launch_gemm_batch(g2.data(), (int)g2.size(), stream);
+  launch_gemm_batch(g3.data(), (int)g3.size(), stream);
 }
 
 }  // namespace kern

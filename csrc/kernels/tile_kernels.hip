@@ -126,10 +126,12 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
   const int M = d.m, N = d.n;
   const int lda = d.lda, ldb = d.ldb;
   // K range of this workgroup (whole K unless split); chunks are BK multiples
-  const int kchunk = nsplit > 1 ? (((d.k + nsplit - 1) / nsplit + BK - 1) / BK) * BK : d.k;
+  // op(A) lower triangular: row block m0 needs k < m0 + BM only (never split)
+  const int kfull = d.a_lower ? min(d.k, m0 + BM) : d.k;
+  const int kchunk = nsplit > 1 ? (((kfull + nsplit - 1) / nsplit + BK - 1) / BK) * BK : kfull;
   const int kbeg = ks * kchunk;
-  if (kbeg >= d.k) return;
-  const int K = min(d.k, kbeg + kchunk) - kbeg;
+  if (kbeg >= kfull) return;
+  const int K = min(kfull, kbeg + kchunk) - kbeg;
   const double* __restrict__ A = d.A + (TRANSA ? (size_t)kbeg : (size_t)kbeg * lda);
   const double* __restrict__ B = d.B + (TRANSB ? (size_t)kbeg * ldb : (size_t)kbeg);
   // 16-byte loads when every row pair is aligned and fully inside the tile
@@ -236,6 +238,9 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
   const bool preload = FULL && !split && (d.alpha == 1.0 || d.alpha == -1.0);
   double* __restrict__ C = d.C;
   const int ldc = d.ldc;
+  // beta's operand: C itself or a separate input (Cin)
+  const double* __restrict__ Cr = d.Cin ? d.Cin : C;
+  const int ldcr = d.Cin ? d.ldcin : ldc;
   load_tile(0);
   if (preload && d.beta != 0.0) {
     const double cs = d.beta / d.alpha;
@@ -243,9 +248,9 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
     for (int i = 0; i < FN; ++i)
 #pragma unroll
       for (int j = 0; j < FM; ++j) {
-        const double* p = C + (size_t)(n0 + wn * WTN + i * 16 + fk) * ldc + (m0 + wm * WTM + j * 16 + fr);
+        const double* p = Cr + (size_t)(n0 + wn * WTN + i * 16 + fk) * ldcr + (m0 + wm * WTM + j * 16 + fr);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = cs * p[(size_t)4 * r * ldc];
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = cs * p[(size_t)4 * r * ldcr];
       }
   }
   store_tile(0);
@@ -291,8 +296,9 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
             unsafeAtomicAdd(p, v);  // no-return global f64 add, performed at the memory side
             continue;
           }
-          if (beta != 0.0) v += beta * *p;
+          if (beta != 0.0) v += beta * Cr[(size_t)gn * ldcr + gm];
           *p = v;
+          if (d.C2) d.C2[(size_t)gn * d.ldc2 + gm] -= v;
         }
       }
     }
@@ -611,7 +617,7 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
     int kmin = 1 << 30;
     bool ok = tail > 0 && 2 * tail <= g_gemm_slots;
     for (int i = 0; ok && i < n; ++i) {
-      ok = descs[i].beta == 1.0;
+      ok = descs[i].beta == 1.0 && !descs[i].a_lower && !descs[i].Cin && !descs[i].C2;
       kmin = std::min(kmin, descs[i].k);
     }
     const int s = ok ? std::min({g_gemm_slots / std::max(tail, 1), kmin / 256, 8}) : 1;
@@ -900,10 +906,10 @@ void launch_potrf(const PotrfDesc& p, hipStream_t stream, double* ws) {
     t.m = rest; t.n = jb; t.ldl = p.lda; t.ldb = p.lda; t.trans = 1;
     const double* cinv = inv;
     launch_trsm_inv(&t, &cinv, 1, stream);
-    GemmDesc g;
+    GemmDesc g{};
     g.A = t.B; g.B = t.B; g.C = p.A + (size_t)(j + jb) * p.lda + j + jb;
     g.m = rest; g.n = rest; g.k = jb; g.lda = p.lda; g.ldb = p.lda; g.ldc = p.lda;
-    g.alpha = -1.0; g.beta = 1.0; g.transA = 0; g.transB = 1; g.lower_only = 1; g.pad = 0;
+    g.alpha = -1.0; g.beta = 1.0; g.transA = 0; g.transB = 1; g.lower_only = 1; g.a_lower = 0;
     launch_gemm_batch(&g, 1, stream);
   }
   if (p.W_out) {
@@ -1481,7 +1487,7 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
       e.A = ca.dst[i]; e.B = t.W; e.C = t.B;
       e.m = t.m; e.n = t.n; e.k = t.n;
       e.lda = t.m; e.ldb = t.ldw; e.ldc = t.ldb;
-      e.alpha = 1.0; e.beta = 0.0; e.transA = 0; e.transB = 1; e.lower_only = 0; e.pad = 0;  // copy x (L^-1)^T
+      e.alpha = 1.0; e.beta = 0.0; e.transA = 0; e.transB = 1; e.lower_only = 0; e.a_lower = 0;  // copy x (L^-1)^T
       p += ((size_t)t.m * t.n * sizeof(double) + 255) / 256 * 256;
     }
     hipLaunchKernelGGL(copy_tiles_kernel, dim3(std::min(256, (maxc + 3) / 4), cnt), dim3(256), 0, stream, ca);

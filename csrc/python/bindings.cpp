@@ -497,8 +497,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("dgeqrf_new", [](TiledMatrix* A, TiledMatrix* T, int ib) { return algos::dgeqrf_new(A, T, ib); }, py::arg("A"), py::arg("T"), py::arg("ib") = 0,
         py::return_value_policy::take_ownership);
   m.def("dgeqrf_hqr_new", [](TiledMatrix* A, TiledMatrix* T, TiledMatrix* TT, int domain, int p_rows) { return algos::dgeqrf_hqr_new(A, T, TT, domain, p_rows); },
-        py::arg("A"), py::arg("T"), py::arg("TT"), py::arg("domain") = 4, py::arg("p_rows") = 0, py::return_value_policy::take_ownership,
-        "hierarchical tiled QR: TS domains of `domain` rows per process row, TT binary trees over the domain heads and across process rows");
+        py::arg("A"), py::arg("T"), py::arg("TT"), py::arg("domain") = 0, py::arg("p_rows") = 0, py::return_value_policy::take_ownership,
+        "hierarchical tiled QR: TS domains of `domain` rows per process row (0: one flat TS chain per process row), TT binary trees over the domain heads and across process rows");
   py::class_<algos::StencilGrid, DataCollection>(m, "StencilGrid")
       .def(py::init([](int myrank, int nodes, int64_t nx, int64_t ny, int64_t nz, int bx, int by, int bz, int device) {
              auto* g = new algos::StencilGrid();
