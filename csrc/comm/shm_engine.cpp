@@ -594,8 +594,17 @@ int ShmEngine::ipc_export(const void* ptr, void* handle64, uint64_t* offset) {
   static const size_t min_bytes = ParamRegistry::instance().reg_sizet("comm", "", "ipc_min_alloc", "Smallest device allocation exported through HIP IPC (smaller ones are host-staged)", (size_t)2 << 20);
   if (size < min_bytes) return -3;
   // called by workers (activations with eager IPC descriptors) and the comm thread
+  // the allocator's buffer id joins the key: a freed allocation's (base, size)
+  // comes back for the next hipMalloc of the same size, and its cached handle
+  // would name the freed buffer object (the peer's open then fails)
+  unsigned long long bid = 0;
+  if (hipPointerGetAttribute(&bid, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)base) != hipSuccess) {
+    (void)hipGetLastError();
+    bid = 0;
+  }
   std::lock_guard<std::mutex> g(ipc_m_);
-  auto key = std::make_pair((uintptr_t)base, size);
+  if (bid == 0) ipc_exported_.erase(std::make_tuple((uintptr_t)base, size, bid));  // no identity: never trust a cached handle
+  auto key = std::make_tuple((uintptr_t)base, size, bid);
   auto it = ipc_exported_.find(key);
   if (it == ipc_exported_.end()) {
     hipIpcMemHandle_t h;

@@ -6,6 +6,7 @@
 #include <array>
 #include <deque>
 #include <map>
+#include <tuple>
 #include <thread>
 
 #include "comm.hpp"
@@ -156,7 +157,7 @@ class ShmEngine : public CommEngine {
   int plane_ = PLANE_HOST;
   std::vector<hipStream_t> ipc_stream_;
   std::vector<std::deque<Xfer>> ipc_q_;
-  std::map<std::pair<uintptr_t, size_t>, std::array<char, 64>> ipc_exported_;  // (base, size) -> handle
+  std::map<std::tuple<uintptr_t, size_t, unsigned long long>, std::array<char, 64>> ipc_exported_;  // (base, size, buffer id) -> handle
   std::mutex ipc_m_;  // ipc_exported_ / ipc_opened_ (exports happen on worker threads too)
   std::map<std::pair<int, std::string>, void*> ipc_opened_;                    // (src, handle) -> base
   int init_ipc();

@@ -336,6 +336,13 @@ void HipDevice::start(Context* c) {
       bulk[cu / 32] &= ~(1u << (cu % 32));
       crit[cu / 32] |= 1u << (cu % 32);
     }
+    // reserved_cus_exclusive = 0: the critical stream keeps every CU (the reserved
+    // ones are only guaranteed free of bulk work, so a critical launch never
+    // waits for a bulk workgroup to retire, and spills onto the rest when wide)
+    if (!reserved_exclusive) {
+      std::fill(crit.begin(), crit.end(), ~0u);
+      if (ncu % 32) crit.back() = (1u << (ncu % 32)) - 1;
+    }
     masked = hipExtStreamCreateWithCUMask(&s_exec[0], (uint32_t)crit.size(), crit.data()) == hipSuccess;
     for (int i = 1; masked && i < total_streams; ++i)
       masked = hipExtStreamCreateWithCUMask(&s_exec[i], (uint32_t)bulk.size(), bulk.data()) == hipSuccess;
@@ -978,6 +985,18 @@ void HipDevice::finish_stage_in(GpuTask* g) {
   if (g->ev_in) { put_event(g->ev_in); g->ev_in = nullptr; }
 }
 
+// Work of the open bulk batch of stream s in 128 x 128 output tiles (GEMM) or
+// descriptor-equivalents (the other kernel kinds): the group is closed once it
+// fills group_rounds rounds of resident workgroups, so a panel's bulk update
+// completes (and releases its successors) progressively, highest priority
+// first, instead of as one event at the end of the whole panel.
+static size_t batch_tiles(const KernelBatch& b) {
+  size_t t = 0;
+  for (const GemmDesc& g : b.gemm) t += (size_t)((g.m + 127) / 128) * ((g.n + 127) / 128);
+  for (const QrApplyDesc& q : b.qr_apply) t += (size_t)((q.m2 + 127) / 128) * ((q.n + 127) / 128);
+  return t + 16 * (b.trsm.size() + b.trsm_w.size() + b.stencil.size());
+}
+
 // ------------------------------------------------------------- execution
 void HipDevice::execute_ready() {
   if (ready.empty()) return;
@@ -993,7 +1012,7 @@ void HipDevice::execute_ready() {
     // a CU partition (reserved_cus) it would crowd the few critical CUs, and
     // without one it would queue behind the critical kernels.
     const bool crit = t->priority >= critical_threshold;
-    if (nb_exec_streams == 1 || crit || (hp && hp_on_critical && !cu_masked)) {
+    if (nb_exec_streams == 1 || crit || (hp && hp_on_critical && (!cu_masked || !reserved_exclusive))) {
       s = 0;
     } else if (hp || crit) {
       s = -1;
@@ -1039,6 +1058,7 @@ void HipDevice::execute_ready() {
     if (rc == HOOK_DONE) {
       g->stream = s;
       round_tasks[s].push_back(g);
+      if (s > 0 && group_tiles > 0 && batching && batch_tiles(batches[s]) >= group_tiles) launch_group(s);
     } else if (rc == HOOK_AGAIN) {
       again.push_back(g);
     } else {
@@ -1055,47 +1075,49 @@ void HipDevice::execute_ready() {
     }
   }
   ready.swap(again);
-  for (int s = 0; s < (int)round_tasks.size(); ++s) {
-    if (round_tasks[s].empty()) continue;
-    const size_t ng = batches[s].gemm.size(), nw = batches[s].trsm_w.size(), np = batches[s].potrf.size();
-    hipEvent_t tb = nullptr;
-    if (gpu_trace) {
-      tb = get_timing_event();
-      PARSEC_HIP_CHECK(hipEventRecord(tb, s_exec[s]));
-    }
-    if (!batches[s].empty()) {
-      batches[s].critical = s == 0 && nb_exec_streams >= 2 && wave_priority;
-      if (roctx) {
-        // rocprofv3 --marker-trace: which tasks each launched group carried
-        char label[96];
-        Task* t0 = round_tasks[s][0]->task;
-        std::snprintf(label, sizeof(label), "%s s%d n%zu %s", name.c_str(), s, round_tasks[s].size(), t0->task_class->name.c_str());
-        roctxRangePushA(label);
-      }
-      launch_kernel_batch(batches[s], s_exec[s], ordinal, workspace(s, kernel_batch_workspace_bytes(batches[s]) + 64));
-      if (roctx) roctxRangePop();
-      stats.kernel_launches.fetch_add(1, std::memory_order_relaxed);
-      batches[s].clear();
-    }
-    if (trace_launches) {
-      std::string line = "[engine] stream " + std::to_string(s) + ":";
-      for (GpuTask* g : round_tasks[s]) line += " " + g->task->task_class->describe(g->task);
-      line += " | gemm " + std::to_string(ng) + " trsm_w " + std::to_string(nw) + " potrf " + std::to_string(np);
-      std::fprintf(stderr, "%s\n", line.c_str());
-    }
-    ExecGroup grp;
-    if (tb) {  // end timing event first: complete whenever grp.ev is
-      grp.ts_begin = tb;
-      grp.ts_end = get_timing_event();
-      PARSEC_HIP_CHECK(hipEventRecord(grp.ts_end, s_exec[s]));
-    }
-    grp.ev = get_event();
-    PARSEC_HIP_CHECK(hipEventRecord(grp.ev, s_exec[s]));
-    grp.tasks.swap(round_tasks[s]);
-    grp.t_launch = now_ns();
-    stats.batched_tasks.fetch_add(grp.tasks.size(), std::memory_order_relaxed);
-    executing[s].push_back(std::move(grp));
+  for (int s = 0; s < (int)round_tasks.size(); ++s) launch_group(s);
+}
+
+void HipDevice::launch_group(int s) {
+  if (round_tasks[s].empty()) return;
+  const size_t ng = batches[s].gemm.size(), nw = batches[s].trsm_w.size(), np = batches[s].potrf.size();
+  hipEvent_t tb = nullptr;
+  if (gpu_trace) {
+    tb = get_timing_event();
+    PARSEC_HIP_CHECK(hipEventRecord(tb, s_exec[s]));
   }
+  if (!batches[s].empty()) {
+    batches[s].critical = s == 0 && nb_exec_streams >= 2 && wave_priority;
+    if (roctx) {
+      // rocprofv3 --marker-trace: which tasks each launched group carried
+      char label[96];
+      Task* t0 = round_tasks[s][0]->task;
+      std::snprintf(label, sizeof(label), "%s s%d n%zu %s", name.c_str(), s, round_tasks[s].size(), t0->task_class->name.c_str());
+      roctxRangePushA(label);
+    }
+    launch_kernel_batch(batches[s], s_exec[s], ordinal, workspace(s, kernel_batch_workspace_bytes(batches[s]) + 64));
+    if (roctx) roctxRangePop();
+    stats.kernel_launches.fetch_add(1, std::memory_order_relaxed);
+    batches[s].clear();
+  }
+  if (trace_launches) {
+    std::string line = "[engine] t=" + std::to_string(now_ns() / 1000) + " L stream " + std::to_string(s) + ":";
+    for (GpuTask* g : round_tasks[s]) line += " " + g->task->task_class->describe(g->task);
+    line += " | gemm " + std::to_string(ng) + " trsm_w " + std::to_string(nw) + " potrf " + std::to_string(np);
+    std::fprintf(stderr, "%s\n", line.c_str());
+  }
+  ExecGroup grp;
+  if (tb) {  // end timing event first: complete whenever grp.ev is
+    grp.ts_begin = tb;
+    grp.ts_end = get_timing_event();
+    PARSEC_HIP_CHECK(hipEventRecord(grp.ts_end, s_exec[s]));
+  }
+  grp.ev = get_event();
+  PARSEC_HIP_CHECK(hipEventRecord(grp.ev, s_exec[s]));
+  grp.tasks.swap(round_tasks[s]);
+  grp.t_launch = now_ns();
+  stats.batched_tasks.fetch_add(grp.tasks.size(), std::memory_order_relaxed);
+  executing[s].push_back(std::move(grp));
 }
 
 void HipDevice::epilog(GpuTask* g) {
@@ -1197,6 +1219,7 @@ bool HipDevice::progress() {
       incoming_n.store(0);
     }
     for (GpuTask* g : in) { g->t_submit = now_ns(); pending.push_back(g); }
+    if (trace_launches) std::fprintf(stderr, "[engine] t=%llu I n=%zu\n", (unsigned long long)(now_ns() / 1000), in.size());
     did = true;
   }
   if (!w2r_jobs.empty() && progress_w2r()) did = true;
@@ -1252,6 +1275,7 @@ bool HipDevice::progress() {
       std::vector<GpuTask*> tasks;
       tasks.swap(grp.tasks);
       q.pop_front();
+      const uint64_t tr0 = trace_launches ? now_ns() : 0;
       for (GpuTask* g : tasks) {
         epilog(g);
         const Chore& gch = g->task->task_class->chores[g->chore];
@@ -1293,6 +1317,9 @@ bool HipDevice::progress() {
         }
       }
       flush_completions();
+      if (trace_launches)
+        std::fprintf(stderr, "[engine] t=%llu R stream %d n=%zu release_us=%llu\n", (unsigned long long)(tr0 / 1000), s, tasks.size(),
+                     (unsigned long long)((now_ns() - tr0) / 1000));
       did = true;
       retired = true;
     }
@@ -1382,6 +1409,8 @@ void hip_devices_init(Context* ctx) {
   int crit = (int)params.reg_int("device", "hip", "critical_threshold", "Task priority at or above which a completed GPU task is released by the manager itself (critical path)", 1 << 29);
   int rcus = (int)params.reg_int("device", "hip", "reserved_cus", "CUs the bulk streams leave free for the critical stream (CU mask on the bulk streams; 0 = none)", 0);
   int rstride = (int)params.reg_int("device", "hip", "reserved_cus_stride", "Spacing of the reserved CU ids in the CU mask", 1);
+  const int64_t grounds = params.reg_int("device", "hip", "group_rounds", "Bulk kernel groups close after this many rounds of resident 128x128 GEMM workgroups (2 per CU); their tasks then complete and release successors per group (0 = one group per scheduling round)", 2);
+  int rexcl = (int)params.reg_int("device", "hip", "reserved_cus_exclusive", "With reserved_cus: the critical stream runs on the reserved CUs only (1) or on every CU (0)", 0);
   const bool roctx_on = params.reg_int("device", "hip", "roctx", "roctx range around every launched kernel group (visible with rocprofv3 --marker-trace)", 1) != 0;
   const bool hp_crit = params.reg_int("device", "hip", "hp_on_critical_stream", "High-priority tasks below the critical threshold share the critical stream (1) or go to the least loaded bulk stream (0; measured 36.0 vs 38.9 TF at 16k, profiles/r3_route_ab.txt)", 1) != 0;
   const bool wprio = params.reg_int("device", "hip", "wave_priority", "Kernels of the critical stream raise their waves' issue priority (s_setprio) over co-resident bulk waves", 1) != 0;
@@ -1410,6 +1439,8 @@ void hip_devices_init(Context* ctx) {
     d->critical_threshold = crit;
     d->reserved_cus = rcus;
     d->reserved_stride = rstride;
+    d->reserved_exclusive = rexcl != 0;
+    d->group_tiles = grounds > 0 ? (size_t)grounds * 2 * (size_t)std::max(1, d->props.multiProcessorCount) : 0;
     d->wave_priority = wprio;
     d->hp_on_critical = hp_crit;
     d->roctx = roctx_on;

@@ -135,6 +135,8 @@ struct HipDevice : Device {
   int critical_threshold = 1 << 29;
   int reserved_cus = 0;
   int reserved_stride = 1;
+  bool reserved_exclusive = false;
+  size_t group_tiles = 0;  // close a bulk kernel group at this many 128x128 output tiles (0 = one group per round)
   bool wave_priority = true;
   bool hp_on_critical = true;
   bool cu_masked = false;
@@ -167,6 +169,7 @@ struct HipDevice : Device {
   std::vector<hipEvent_t> timing_pool;
   hipEvent_t get_timing_event();
   void trace_group(int stream, const ExecGroup& g);
+  void launch_group(int stream);
   bool trace_launches = false;
   // GPU-side copy spans (profiling on): timing events around every transfer the
   // engine issues on the copy stream, turned into MOVEIN / MOVEOUT / PREFETCH
