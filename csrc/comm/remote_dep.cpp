@@ -155,11 +155,11 @@ enum : int32_t { PLANE_HOST = 0, PLANE_IPC = 1, PLANE_RCCL = 2 };
 struct CommInfo {
   int32_t peer, flow;
   int64_t bytes;
-  int32_t plane, pad;
+  int32_t plane, send_id;  // send_id: the sender's id of the activation (low 31 bits), links both sides' events
 };
 void comm_trace_init() {
   if (!profiling_enabled() || g_comm_prof) return;
-  const char* desc = "peer{int32_t};flow{int32_t};bytes{int64_t};plane{int32_t};pad{int32_t}";
+  const char* desc = "peer{int32_t};flow{int32_t};bytes{int64_t};plane{int32_t};send_id{int32_t}";
   profiling_add_dictionary_keyword("COMM_DATA_SND", "fill:#0077FF", sizeof(CommInfo), desc, &k_snd_b, &k_snd_e);
   profiling_add_dictionary_keyword("COMM_DATA_RCV", "fill:#00BB44", sizeof(CommInfo), desc, &k_rcv_b, &k_rcv_e);
   profiling_add_dictionary_keyword("COMM_ACTIVATE", "fill:#AA00AA", sizeof(CommInfo), desc, &k_act_b, &k_act_e);
@@ -373,7 +373,7 @@ void send_activations(Taskpool* tp, const ActHdr& base, int my_pos_root_rank, co
     h.termdet_bytes = (uint32_t)tdn;
     if (tdn) put(td, tdn);
     if (g_comm_prof) {
-      CommInfo ci{dst, -1, (int64_t)(sizeof(h) + body.size()), PLANE_HOST, 0};
+      CommInfo ci{dst, -1, (int64_t)(sizeof(h) + body.size()), PLANE_HOST, (int32_t)(h.send_id & 0x7fffffff)};
       const uint64_t ev = g_next_id.fetch_add(1);
       comm_trace(k_act_b, ev, h.tp_id, &ci);
       g_ce->send_am_prio(TAG_REMOTE_DEP_ACTIVATE, dst, &h, sizeof(h), body.data(), body.size(), h.priority);
@@ -456,7 +456,7 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
     if (g_comm_prof)
       for (int f = 0; f < nflows; ++f)
         if (ipc_mask & (1u << f)) {
-          CommInfo ci{src, f, (int64_t)r->fd[f].bytes, PLANE_IPC, 0};
+          CommInfo ci{src, f, (int64_t)r->fd[f].bytes, PLANE_IPC, (int32_t)(r->hdr.send_id & 0x7fffffff)};
           comm_trace(k_rcv_b, flow_event(r->id, f), r->hdr.tp_id, &ci);
         }
     const uint64_t sid = r->hdr.send_id;
@@ -501,7 +501,7 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
       if (!(get_mask & (1u << f))) continue;
       DataCopy* c = r->data[f];
       const int32_t plane = c->device_index != 0 && g_ce->rccl_ok() ? PLANE_RCCL : (c->device_index != 0 && g_ce->ipc_ok() ? PLANE_IPC : PLANE_HOST);
-      CommInfo ci{src, f, (int64_t)r->fd[f].bytes, plane, 0};
+      CommInfo ci{src, f, (int64_t)r->fd[f].bytes, plane, (int32_t)(r->hdr.send_id & 0x7fffffff)};
       comm_trace(k_rcv_b, flow_event(r->id, f), r->hdr.tp_id, &ci);
     }
   GetMsg gm{r->hdr.send_id, r->id, get_mask, g_ce->rank};
@@ -526,7 +526,7 @@ void on_get(int src, int, const void* msg, size_t) {
     size_t bytes = c->original ? c->original->nb_elts : 0;
     const uint32_t tpid = s->tp ? s->tp->taskpool_id : 0;
     if (c->device_index != 0 && g_ce->rccl_ok()) {
-      CommInfo ci{g.requester, f, (int64_t)bytes, PLANE_RCCL, 0};
+      CommInfo ci{g.requester, f, (int64_t)bytes, PLANE_RCCL, (int32_t)(g.send_id & 0x7fffffff)};
       comm_trace(k_snd_b, flow_event(g.send_id, f), tpid, &ci);
       const uint64_t ev = flow_event(g.send_id, f);
       g_ce->rccl_send(g.requester, c->device_private, bytes, [s, ev, tpid] {
@@ -552,13 +552,13 @@ void on_get(int src, int, const void* msg, size_t) {
       m.bytes = bytes;
       if (g_ce->ipc_export(c->device_private, m.handle, &m.offset) == 0) {
         // the receiver pulls the bytes; its IPC_DONE releases this copy
-        CommInfo ci{g.requester, f, (int64_t)bytes, PLANE_IPC, 0};
+        CommInfo ci{g.requester, f, (int64_t)bytes, PLANE_IPC, (int32_t)(g.send_id & 0x7fffffff)};
         comm_trace(k_snd_b, flow_event(g.send_id, f), tpid, &ci);
         g_ce->send_am(TAG_DATA_IPC, g.requester, &m, sizeof(m));
         continue;
       }
     }
-    CommInfo ci{g.requester, f, (int64_t)bytes, PLANE_HOST, 0};
+    CommInfo ci{g.requester, f, (int64_t)bytes, PLANE_HOST, (int32_t)(g.send_id & 0x7fffffff)};
     comm_trace(k_snd_b, flow_event(g.send_id, f), tpid, &ci);
     const int requester = g.requester;
     const uint64_t recv_id = g.recv_id, ev_id = flow_event(g.send_id, f);
@@ -595,7 +595,7 @@ void pull_ipc(int src, RecvState* r, uint32_t f, const char* handle, uint64_t of
   const uint64_t bytes = r->fd[f].bytes;
   const char* srcp = base + offset;
   if (g_comm_prof) {
-    CommInfo ci{src, (int32_t)f, (int64_t)bytes, 1, 0};
+    CommInfo ci{src, (int32_t)f, (int64_t)bytes, 1, (int32_t)(sid & 0x7fffffff)};
     comm_trace(k_pull_b, flow_event(rid, f), r->hdr.tp_id, &ci);
   }
   g_ce->ipc_copy(src, c->device_private, srcp, bytes, [rid, sid, f, src, bytes, want, c, srcp] {

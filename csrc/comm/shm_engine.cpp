@@ -95,6 +95,8 @@ ShmEngine::~ShmEngine() {
   for (auto& kv : ipc_opened_) (void)hipIpcCloseMemHandle(kv.second);
   ipc_opened_.clear();
   ipc_stream_.clear();  // the shared copy stream outlives the engine
+  for (hipStream_t x : own_streams_) (void)hipStreamDestroy(x);
+  own_streams_.clear();
   for (int r = 0; r < size; ++r)
     if (maps_[r]) munmap(maps_[r], map_len_[r]);
   shm_unlink(seg_name(job_, rank).c_str());
@@ -580,8 +582,20 @@ int ShmEngine::init_ipc() {
   // device engine's transfers: no per-peer streams beyond the 4 hardware queues
   hipStream_t st = gpu_copy_stream(gpu_);
   if (!st) return -2;
+  // comm_ipc_streams > 1: extra pull streams (copy engines work in parallel on
+  // distinct queues), peer r on stream r % n; stream 0 is the shared copy stream
+  const int n = (int)std::max<int64_t>(1, ParamRegistry::instance().reg_int("comm", "", "ipc_streams", "Streams the IPC pulls are spread over (peer r -> r % n; 1 = the GPU's shared copy stream only)", 1));
+  std::vector<hipStream_t> pool{st};
+  int lo = 0, hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+  for (int i = 1; i < n; ++i) {
+    hipStream_t x = nullptr;
+    if (hipStreamCreateWithPriority(&x, hipStreamNonBlocking, hi) != hipSuccess) { (void)hipGetLastError(); break; }
+    pool.push_back(x);
+    own_streams_.push_back(x);
+  }
   for (int r = 0; r < size; ++r)
-    if (r != rank) ipc_stream_[r] = st;
+    if (r != rank) ipc_stream_[r] = pool[(size_t)r % pool.size()];
   return 0;
 }
 

@@ -156,6 +156,7 @@ class ShmEngine : public CommEngine {
   // IPC
   int plane_ = PLANE_HOST;
   std::vector<hipStream_t> ipc_stream_;
+  std::vector<hipStream_t> own_streams_;  // extra IPC pull streams (comm_ipc_streams > 1)
   std::vector<std::deque<Xfer>> ipc_q_;
   std::map<std::tuple<uintptr_t, size_t, unsigned long long>, std::array<char, 64>> ipc_exported_;  // (base, size, buffer id) -> handle
   std::mutex ipc_m_;  // ipc_exported_ / ipc_opened_ (exports happen on worker threads too)
