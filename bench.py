@@ -227,8 +227,9 @@ def main():
                     t = (t + t.t()) * 0.5 + N * torch.eye(nb, dtype=torch.float64, device="cuda")
                 full[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb] = t
         S = torch.tril(full) + torch.tril(full, -1).t()
-        # host LAPACK reference: the GPU library Cholesky returned wrong factors
-        # when several processes shared the GPU (--share-gpu validation runs)
+        # host LAPACK reference: torch's GPU Cholesky is intermittently wrong when
+        # several processes share the GPU, with or without this runtime loaded
+        # (profiles/r3_oracle_root_cause.txt)
         Lref = torch.linalg.cholesky(S.cpu()).to(S.device)
         err = 0.0
         for n in range(NT):

@@ -25,8 +25,12 @@ def main():
     ctx = pa.init(4)
     A = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb, nb, N, N)  # host storage
     rng = np.random.default_rng(4)
-    R = rng.standard_normal((N, N))
-    S = R @ R.T / N + np.eye(N)
+    if N <= 8192:
+        R = rng.standard_normal((N, N))
+        S = R @ R.T / N + np.eye(N)
+    else:  # large N: random symmetric + N I (no O(N^3) host product)
+        S = rng.random((N, N)) - 0.5
+        S = (S + S.T) * 0.5 + N * np.eye(N)
     NT = N // nb
     for m in range(NT):
         for n in range(NT):
@@ -47,7 +51,11 @@ def main():
             L[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb] = A.tile(m, n)
     L = np.tril(L)
     ctx.fini()
-    res = np.linalg.norm(L @ L.T - S) / np.linalg.norm(S)
+    if N <= 8192:
+        res = np.linalg.norm(L @ L.T - S) / np.linalg.norm(S)
+    else:  # backward error on random vectors: ||S x - L L^T x|| / (||S|| ||x||)
+        X = rng.random((N, 4)) - 0.5
+        res = np.linalg.norm(S @ X - L @ (L.T @ X)) / (np.linalg.norm(S) * np.linalg.norm(X))
     print(f"evict N={N} nb={nb} cache={frac:.2f} prefetch={pref} info={pa.read_int(info)} residual={res:.3e} "
           f"gpu_tasks={st['executed_tasks']} faults={st['data_faults']} w2r={st['w2r_tasks']} prefetches={st['prefetches']} "
           f"in={st['bytes_in'] >> 20}MiB out={st['bytes_out'] >> 20}MiB", flush=True)

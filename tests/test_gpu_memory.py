@@ -19,7 +19,7 @@ def _gpu():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("N,nb,frac,prefetch", [(4096, 512, 0.25, 0), (4096, 256, 0.3, 1), (4096, 512, 2.0, 1)])
+@pytest.mark.parametrize("N,nb,frac,prefetch", [(4096, 512, 0.25, 0), (4096, 256, 0.3, 1), (4096, 512, 2.0, 1), (16384, 1024, 0.25, 0)])
 def test_dpotrf_forced_eviction(pa, N, nb, frac, prefetch):
     _gpu()
     r = subprocess.run([sys.executable, WORKER, str(N), str(nb), str(frac), str(prefetch)], capture_output=True, text=True, timeout=150)
