@@ -1097,6 +1097,31 @@ __device__ __forceinline__ void inv_tile(const double* Dl, double* Xb, const dou
   __builtin_amdgcn_s_waitcnt(0xc07f);
 }
 
+// X_pp = L_pp^-1 (16 x 16 diagonal block p of the factor in Dl, pivots' 1/L(i,i)
+// in dinv): lane c < 16 owns column c, s_i -= L(i, k) x_k as soon as x_k is known
+__device__ __forceinline__ void diag_block_inverse(const double* Dl, double* Xb, double* Xc, const double* dinv, int p) {
+  const int lane = threadIdx.x & 63;
+  if (lane < 16) {
+    const int b0 = 16 * p;
+    double sv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sv[i] = (i == lane) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      sv[k] *= dinv[b0 + k];
+#pragma unroll
+      for (int i = k + 1; i < 16; ++i) sv[i] = __builtin_fma(-Dl[(b0 + k) * kPL + b0 + i], sv[k], sv[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      Xb[xblk(p, p) + i * 16 + lane] = sv[i];
+      Xc[p * 256 + lane * 16 + i] = sv[i];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+}
+
 __device__ __forceinline__ void diag_factor_inv(double* __restrict__ Dl, double* __restrict__ pool, double* __restrict__ T, int ldt, double* __restrict__ invD, int* info, int info_base, bool stamp) {
   PARSEC_STAMP(1);
   double* Xb = pool;                    // X, block-packed: Xb[xblk(i, j) + m * 16 + n] = X(16i + m, 16j + n)
@@ -1159,25 +1184,6 @@ __device__ __forceinline__ void diag_factor_inv(double* __restrict__ Dl, double*
         if (r >= 16 * p + i) T[(size_t)(16 * p + i) * ldt + r] = a[i];  // L is final: straight out
       }
       if (stamp && lane == 0) g_potrf_stamps[3 + 2 * p] = wall_clock64();
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // this wave's panel / dinv stores are visible to it
-      // X_pp: lane c < 16 owns column c; s_i -= L(i, k) x_k as soon as x_k is known
-      if (lane < 16) {
-        const int b0 = 16 * p;
-        double sv[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sv[i] = (i == lane) ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          sv[k] *= dinv[b0 + k];
-#pragma unroll
-          for (int i = k + 1; i < 16; ++i) sv[i] = __builtin_fma(-Dl[(b0 + k) * kPL + b0 + i], sv[k], sv[i]);
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          Xb[xblk(p, p) + i * 16 + lane] = sv[i];
-          Xc[p * 256 + lane * 16 + i] = sv[i];
-        }
-      }
     } else if (p >= 1) {
       // panel p-1's update of the tiles right of column block p: (R, C), p < C <= R,
       // dealt to the three other waves
@@ -1188,14 +1194,21 @@ __device__ __forceinline__ void diag_factor_inv(double* __restrict__ Dl, double*
         while (u > R - (p + 1)) { u -= R - p; ++R; }
         upd_tile(R, p + 1 + u, p - 1);
       }
-      // row p-1 of the inverse (its diagonal block is done): wave j < p-1 takes X_{p-1,j}
-      if (p >= 2 && v < p - 1) inv_tile(Dl, Xb, Xc, Tw + 256 * v, p - 1, v);
+      // off the panel chain: the wave that factored panel p-1 inverts its
+      // diagonal block X_{p-1,p-1} while wave p factors panel p
+      if (v == p - 1) diag_block_inverse(Dl, Xb, Xc, dinv, p - 1);
+      // row p-2 of the inverse (its diagonal block was inverted one iteration
+      // ago): wave j < p-2 takes X_{p-2,j}
+      if (p >= 3 && v < p - 2) inv_tile(Dl, Xb, Xc, Tw + 256 * v, p - 2, v);
     }
     __syncthreads();
     PARSEC_STAMP(4 + 2 * p);
   }
   if (threadIdx.x == 0 && *bad_s != 0x7fffffff && info) atomicCAS(info, 0, info_base + *bad_s);
-  // row 3 of the inverse
+  // X_33 beside row 2 of the inverse, then row 3
+  if (v == 3) diag_block_inverse(Dl, Xb, Xc, dinv, 3);
+  else if (v < 2) inv_tile(Dl, Xb, Xc, Tw + 256 * v, 2, v);
+  __syncthreads();
   if (v < 3) inv_tile(Dl, Xb, Xc, Tw + 256 * v, 3, v);
   __syncthreads();
   PARSEC_STAMP(11);
@@ -1253,7 +1266,7 @@ __device__ __forceinline__ void blk_put(Blk& S, const BlkRegs& R, bool t) {
 // next to ONE resident 128 x 128 GEMM workgroup (74 KB of LDS), so critical-path
 // work starts as soon as a bulk workgroup retires instead of waiting for a CU to
 // drain completely (the 120 KB version waited 1.2 ms per tile POTRF at 16k).
-__global__ __launch_bounds__(256) void dpotrf_step_kernel(const PotrfStepArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void dpotrf_step_kernel(const PotrfStepArgs a) {
   __shared__ double pool[2 * 64 * kPL];
   static_assert(kDiagPoolDoubles <= 64 * kPL, "diag_factor_inv scratch exceeds one staging block");
   __builtin_amdgcn_s_setprio(2);  // the tile POTRF is the critical path
