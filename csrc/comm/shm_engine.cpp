@@ -209,7 +209,8 @@ int ShmEngine::init() {
     // all ranks agree on the plane: a peer mapping that fails (or reads wrong
     // bytes) anywhere sends every rank to the host plane instead of a fatal
     // hipIpcOpenMemHandle in the middle of a run
-    const int local = rc.load() == 0 ? probe_ipc() : rc.load();
+    const int local = rc.load() == 0 ? probe_ipc() : rc.load();  // probe_ipc syncs: every pci_bus is published
+    detect_same_gpu();
     const uint64_t bad = allreduce_max(local != 0 ? 1 : 0);
     if (bad == 0) plane_ = PLANE_IPC;
     else warning("IPC data plane unavailable (this rank rc=%d): device tiles will be staged through host memory", local);
@@ -576,6 +577,11 @@ uint64_t ShmEngine::allreduce_max(uint64_t v) {
 // ------------------------------------------------------------------- IPC
 int ShmEngine::init_ipc() {
   if (hipSetDevice(gpu_) != hipSuccess) return -1;
+  std::memset(me_->pci_bus, 0, sizeof(me_->pci_bus));
+  if (hipDeviceGetPCIBusId(me_->pci_bus, (int)sizeof(me_->pci_bus) - 1, gpu_) != hipSuccess) {
+    (void)hipGetLastError();
+    me_->pci_bus[0] = 0;
+  }
   ipc_stream_.assign(size, nullptr);
   ipc_q_.resize(size);
   // every pull rides the GPU's one (high-priority) copy stream, shared with the
@@ -597,6 +603,16 @@ int ShmEngine::init_ipc() {
   for (int r = 0; r < size; ++r)
     if (r != rank) ipc_stream_[r] = pool[(size_t)r % pool.size()];
   return 0;
+}
+
+// Which peers share this rank's GPU (PCI bus ids published in the shm headers;
+// called once every rank has run init_ipc)
+void ShmEngine::detect_same_gpu() {
+  same_gpu_.assign(size, 0);
+  for (int r = 0; r < size; ++r) {
+    const char* b = static_cast<ShmHeader*>(maps_[r])->pci_bus;
+    same_gpu_[r] = r == rank || (b[0] != 0 && std::strncmp(b, me_->pci_bus, sizeof(me_->pci_bus)) == 0);
+  }
 }
 
 int ShmEngine::ipc_export(const void* ptr, void* handle64, uint64_t* offset) {
@@ -661,7 +677,12 @@ int ShmEngine::ipc_copy(int src_rank, void* dst, const void* src, size_t bytes, 
   hipEvent_t ev;
   if (!ev_pool_.empty()) { ev = ev_pool_.back(); ev_pool_.pop_back(); }
   else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1;
-  static const int mode = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_copy_mode", "Peer pull: 0 = hipMemcpyAsync (copy engine), 1 = copy kernel (measured 30.7 -> 36.9 TF on 2 ranks of one GPU with comm_ipc_streams=2: profiles/r3_ipc_pull_ab.txt)", 1);
+  // 2 (auto): a copy kernel when the peer shares this GPU (the copy engines
+  // managed 4-11 GB/s for same-device pulls: profiles/r3_ipc_pull_ab.txt), the
+  // copy engines across xGMI (they need no CU, so a pull never waits behind the
+  // bulk GEMM workgroups for a slot)
+  static const int cmode = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_copy_mode", "Peer pull: 0 = hipMemcpyAsync (copy engine), 1 = copy kernel, 2 = kernel for a peer on the same GPU, copy engine otherwise", 2);
+  const int mode = cmode == 2 ? ((size_t)src_rank < same_gpu_.size() && same_gpu_[src_rank] ? 1 : 0) : cmode;
   static const int dbg = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_debug_sync", "Diagnostic: device-synchronize before exporting a tile to a peer", 0);
   if (mode == 1) {
     if (device_copy_kernel(dst, src, bytes, st) != 0) fatal("IPC copy kernel launch failed");

@@ -31,6 +31,9 @@ struct ShmHeader {
   std::atomic<uint32_t> ids_ready;
   // IPC start-up probe: handle of a device buffer filled with this rank's byte
   char ipc_probe[64];
+  // PCI bus id of this rank's GPU: peers on the same device pull with a copy
+  // kernel, peers on another GPU with the copy engines (comm_ipc_copy_mode 2)
+  char pci_bus[32];
 };
 
 class ShmEngine : public CommEngine {
@@ -157,12 +160,14 @@ class ShmEngine : public CommEngine {
   int plane_ = PLANE_HOST;
   std::vector<hipStream_t> ipc_stream_;
   std::vector<hipStream_t> own_streams_;  // extra IPC pull streams (comm_ipc_streams > 1)
+  std::vector<uint8_t> same_gpu_;         // peer r runs on this rank's GPU (shared-GPU validation runs)
   std::vector<std::deque<Xfer>> ipc_q_;
   std::map<std::tuple<uintptr_t, size_t, unsigned long long>, std::array<char, 64>> ipc_exported_;  // (base, size, buffer id) -> handle
   std::mutex ipc_m_;  // ipc_exported_ / ipc_opened_ (exports happen on worker threads too)
   std::map<std::pair<int, std::string>, void*> ipc_opened_;                    // (src, handle) -> base
   int init_ipc();
   int probe_ipc();  // every rank opens every peer's probe buffer and checks its bytes
+  void detect_same_gpu();
   // one-sided: this rank's registrations and the gets waiting for fragments
   struct Region {
     void* ptr;

@@ -663,6 +663,218 @@ __global__ __launch_bounds__(64 * NW) void qr_sub2_kernel(const QrSub2Args args)
     }
 }
 
+// ------------------------------------------- column-owner sub-panel (default)
+// Same contract as qr_sub2_kernel, ONE barrier per column instead of two. Wave w
+// owns columns w, w + 8, w + 16, w + 24 over every row (lane l holds virtual
+// rows l + 64 i), so the column reductions (norm, V^T a) stay inside a wave
+// (DPP row scans + 4 readlanes, no LDS round trip, no barrier). Per column j:
+//   owner(j) forms v_j (scaled, explicit 1 / 0 above) into LDS    | barrier
+//   every wave: a_c -= tau_j (v_j^T a_c) v_j for its columns c > j, and
+//   z_c = V_c^T v_j for its columns c < j (compact-WY T column, formed one step
+//   later by a wave off the critical chain). The owner of column j+1 updates and
+//   factors that column FIRST, so the serial chain per column is one LDS read of
+//   v, one dot + update of one column, one norm and the Householder scalars.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+  const long long b = __builtin_bit_cast(long long, x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, true);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double rl_d(double x, int l) {
+  const long long b = __builtin_bit_cast(long long, x);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
+// sum over the 64 lanes, uniform result: inclusive scans inside the 16-lane rows
+// (DPP row_shr 1, 2, 4, 8 with zero fill), then the four row totals
+__device__ __forceinline__ double wave_sum_dpp(double x) {
+  x += dpp_d<0x111>(x);
+  x += dpp_d<0x112>(x);
+  x += dpp_d<0x114>(x);
+  x += dpp_d<0x118>(x);
+  return (rl_d(x, 15) + rl_d(x, 31)) + (rl_d(x, 47) + rl_d(x, 63));
+}
+
+template <int RPL>
+__global__ __launch_bounds__(512) void qr_sub2c_kernel(const QrSub2Args args) {
+  constexpr int NW = 8, NC = 4;
+  const QrSub2Desc& d = args.d[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bool ts = d.ts != 0;
+  const int jb = d.jb;
+  __shared__ double vbuf[2][64 * RPL];  // v_j with explicit 1 and zeros, by parity of j
+  __shared__ double Tl[32][33];
+  __shared__ double zb[2][32];
+  __shared__ double taus[32], scs[32], betas[32];
+  for (int idx = tid; idx < 32 * 33; idx += 512) (&Tl[0][0])[idx] = 0.0;
+  double a[NC][RPL];
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const int c = w + NW * q;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+      const int vr = lane + 64 * i;
+      double x = 0.0;
+      if (c < jb) {
+        if (ts) {
+          if (vr < 32) {
+            if (vr <= c) x = d.A1[(size_t)c * d.lda1 + vr];  // upper R only (GEQRT's V lies below)
+          } else if (vr - 32 < d.m2) {
+            x = d.A2[(size_t)c * d.lda2 + (vr - 32)];
+          }
+        } else if (vr < d.nR) {
+          x = d.A1[(size_t)c * d.lda1 + vr];
+        }
+      }
+      a[q][i] = x;
+    }
+  }
+  // Householder of column j (local slot q of this wave): v_j -> vbuf[j & 1],
+  // the column itself -> store form (beta on the pivot, v below, R above)
+  auto factor = [&](int j, int q) {
+#pragma unroll
+    for (int qq = 0; qq < NC; ++qq) {
+      if (qq != q) continue;
+      double sg = 0.0;
+#pragma unroll
+      for (int i = 0; i < RPL; ++i) {
+        const int vr = lane + 64 * i;
+        const bool below = ts ? (vr >= 32) : (vr > j);
+        sg = __builtin_fma(below ? a[qq][i] : 0.0, a[qq][i], sg);
+      }
+      const double sigma = wave_sum_dpp(sg);
+      const double alpha = rl_d(a[qq][0], j);  // pivot row j < 32: element 0 of lane j
+      double tau = 0.0, scale = 0.0, beta = alpha;
+      if (sigma != 0.0) {
+        const double norm = sqrt(alpha * alpha + sigma);
+        beta = alpha >= 0.0 ? -norm : norm;
+        tau = (beta - alpha) / beta;
+        scale = 1.0 / (alpha - beta);
+      }
+      double* vb = vbuf[j & 1];
+#pragma unroll
+      for (int i = 0; i < RPL; ++i) {
+        const int vr = lane + 64 * i;
+        const bool below = ts ? (vr >= 32) : (vr > j);
+        double v = 0.0;
+        if (below) {
+          v = a[qq][i] * scale;
+          a[qq][i] = v;
+        } else if (vr == j) {
+          v = 1.0;
+          a[qq][i] = beta;
+        }
+        vb[vr] = v;
+      }
+      if (lane == 0) {
+        taus[j] = tau;
+        scs[j] = scale;
+        betas[j] = beta;
+      }
+    }
+  };
+  // a_c -= tau (v^T a_c) v for slot q
+  auto update = [&](int q, const double* vv, double tau) {
+#pragma unroll
+    for (int qq = 0; qq < NC; ++qq) {
+      if (qq != q) continue;
+      double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+      for (int i = 0; i < RPL; i += 2) {
+        p0 = __builtin_fma(vv[i], a[qq][i], p0);
+        if (i + 1 < RPL) p1 = __builtin_fma(vv[i + 1], a[qq][i + 1], p1);
+      }
+      const double tp = tau * wave_sum_dpp(p0 + p1);
+#pragma unroll
+      for (int i = 0; i < RPL; ++i) a[qq][i] = __builtin_fma(-tp, vv[i], a[qq][i]);
+    }
+  };
+  // T column jp = -tau_jp T(0:jp, 0:jp) z (lane i < jp owns row i), T(jp, jp) = tau_jp
+  auto t_column = [&](int jp, const double* z) {
+    if (lane < jp) {
+      double t0 = 0.0, t1 = 0.0;
+      for (int l = lane; l < jp; l += 2) {
+        t0 = __builtin_fma(Tl[lane][l], z[l], t0);
+        if (l + 1 < jp) t1 = __builtin_fma(Tl[lane][l + 1], z[l + 1], t1);
+      }
+      Tl[lane][jp] = -taus[jp] * (t0 + t1);
+    } else if (lane == jp) {
+      Tl[jp][jp] = taus[jp];
+    }
+  };
+  if (w == 0 && jb > 0) factor(0, 0);
+  __syncthreads();
+  for (int j = 0; j < jb; ++j) {
+    const int par = j & 1;
+    const double tau = taus[j];
+    double vv[RPL];
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) vv[i] = vbuf[par][lane + 64 * i];
+    const int nx = j + 1;
+    const bool own_nx = nx < jb && w == nx % NW;
+    if (own_nx) {  // the critical chain: column j+1 first, then its reflector
+      if (tau != 0.0) update(nx / NW, vv, tau);
+      factor(nx, nx / NW);
+    }
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int c = w + NW * q;
+      if (c >= jb || c == j || (own_nx && c == nx)) continue;
+      if (c > j) {
+        if (tau != 0.0) update(q, vv, tau);
+      } else {
+        // z_c = V_c^T v_j; a TS reflector's R part is e_c (R values sit there)
+        double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < RPL; i += 2) {
+          const double x0 = (ts && i == 0 && lane < 32) ? 0.0 : a[q][i];
+          p0 = __builtin_fma(vv[i], x0, p0);
+          if (i + 1 < RPL) p1 = __builtin_fma(vv[i + 1], a[q][i + 1], p1);
+        }
+        const double z = wave_sum_dpp(p0 + p1);
+        if (lane == 0) zb[par][c] = z;
+      }
+    }
+    // T column j-1 from the z of the previous step, by a wave off the chain
+    if (j >= 1 && w == (j + 4) % NW) t_column(j - 1, zb[par ^ 1]);
+    __syncthreads();
+  }
+  if (w == 0 && jb > 0) t_column(jb - 1, zb[(jb - 1) & 1]);
+  __syncthreads();
+  // ---- write back: R / beta / V per column, T (+ zeros below), zeros above V
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const int c = w + NW * q;
+    if (c >= jb) continue;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+      const int vr = lane + 64 * i;
+      const double x = a[q][i];
+      if (ts) {
+        if (vr < 32) {
+          if (vr <= c) d.A1[(size_t)c * d.lda1 + vr] = x;
+        } else if (vr - 32 < d.m2) {
+          d.A2[(size_t)c * d.lda2 + (vr - 32)] = x;
+        }
+      } else if (vr < d.nR) {
+        d.A1[(size_t)c * d.lda1 + vr] = x;
+        if (d.Vc) d.Vc[(size_t)c * d.ldvc + vr] = vr > c ? x : (vr == c ? 1.0 : 0.0);
+      }
+    }
+  }
+  for (int idx = tid; idx < jb * (jb + d.tzero); idx += 512) {
+    const int col = idx / (jb + d.tzero), r = idx % (jb + d.tzero);
+    d.Tjj[(size_t)col * d.ldt + r] = (r < jb && r <= col) ? Tl[r][col] : 0.0;
+  }
+  if (d.Vc)
+    for (int idx = tid; idx < jb * d.vzero; idx += 512) {
+      const int col = idx / d.vzero, r = idx % d.vzero;
+      d.Vc[(size_t)col * d.ldvc + r - d.vzero] = 0.0;
+    }
+}
+
 struct QrSubApplyTask {
   const double* Vd;  // dense reflector rows of this step (rd x jb, ldv); TS: A2 cols; GEQRT: clean V from row j0
   int ldv, rd, jb;
@@ -889,7 +1101,9 @@ __global__ __launch_bounds__(kSubApplyThreads) void qr_subapply_kernel(const QrS
 }
 
 static void launch_sub2(const std::vector<QrSub2Desc>& v, int rows, hipStream_t stream) {
-  // 8 waves (16 row groups) for tall sub-panels, 4 waves otherwise
+  // column-owner kernel (one barrier per column) unless PARSEC_QR_SUB2=0; the
+  // column-per-lane kernel: 8 waves (16 row groups) for tall sub-panels, 4 otherwise
+  static const int sub2c = getenv("PARSEC_QR_SUB2") ? atoi(getenv("PARSEC_QR_SUB2")) : 1;
   static const int nw_env = getenv("PARSEC_QR_PANEL_WAVES") ? atoi(getenv("PARSEC_QR_PANEL_WAVES")) : 8;
   const int nw = nw_env == 4 ? 4 : 8;
   for (size_t s0 = 0; s0 < v.size(); s0 += kMaxSub2Batch) {
@@ -897,7 +1111,12 @@ static void launch_sub2(const std::vector<QrSub2Desc>& v, int rows, hipStream_t 
     a.count = (int)std::min<size_t>(kMaxSub2Batch, v.size() - s0);
     for (int i = 0; i < a.count; ++i) a.d[i] = v[s0 + i];
     const dim3 grid(a.count);
-    if (nw == 8) {
+    if (sub2c && rows <= 64 * 9) {
+      const int rpl = (rows + 63) / 64;
+      if (rpl <= 2) hipLaunchKernelGGL((qr_sub2c_kernel<2>), grid, dim3(512), 0, stream, a);
+      else if (rpl <= 4) hipLaunchKernelGGL((qr_sub2c_kernel<4>), grid, dim3(512), 0, stream, a);
+      else hipLaunchKernelGGL((qr_sub2c_kernel<9>), grid, dim3(512), 0, stream, a);
+    } else if (nw == 8) {
       const int rpt = (rows + 15) / 16;
       const dim3 block(512);
       if (rpt <= 8) hipLaunchKernelGGL((qr_sub2_kernel<8, 8>), grid, block, 0, stream, a);
