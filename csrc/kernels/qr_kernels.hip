@@ -687,14 +687,25 @@ __device__ __forceinline__ double rl_d(double x, int l) {
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
   return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
 }
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_rows(double x) {  // rows outside ROWS read 0
+  const long long b = __builtin_bit_cast(long long, x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, ROWS, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned int)lo);
+}
 // sum over the 64 lanes, uniform result: inclusive scans inside the 16-lane rows
-// (DPP row_shr 1, 2, 4, 8 with zero fill), then the four row totals
+// (DPP row_shr 1, 2, 4, 8 with zero fill), row totals carried across rows by
+// row_bcast:15 (into rows 1, 3) and row_bcast:31 (into rows 2, 3); lane 63 ends
+// with the total
 __device__ __forceinline__ double wave_sum_dpp(double x) {
   x += dpp_d<0x111>(x);
   x += dpp_d<0x112>(x);
   x += dpp_d<0x114>(x);
   x += dpp_d<0x118>(x);
-  return (rl_d(x, 15) + rl_d(x, 31)) + (rl_d(x, 47) + rl_d(x, 63));
+  x += dpp_rows<0x142, 0xa>(x);
+  x += dpp_rows<0x143, 0xc>(x);
+  return rl_d(x, 63);
 }
 
 template <int RPL>
@@ -775,22 +786,6 @@ __global__ __launch_bounds__(512) void qr_sub2c_kernel(const QrSub2Args args) {
       }
     }
   };
-  // a_c -= tau (v^T a_c) v for slot q
-  auto update = [&](int q, const double* vv, double tau) {
-#pragma unroll
-    for (int qq = 0; qq < NC; ++qq) {
-      if (qq != q) continue;
-      double p0 = 0.0, p1 = 0.0;
-#pragma unroll
-      for (int i = 0; i < RPL; i += 2) {
-        p0 = __builtin_fma(vv[i], a[qq][i], p0);
-        if (i + 1 < RPL) p1 = __builtin_fma(vv[i + 1], a[qq][i + 1], p1);
-      }
-      const double tp = tau * wave_sum_dpp(p0 + p1);
-#pragma unroll
-      for (int i = 0; i < RPL; ++i) a[qq][i] = __builtin_fma(-tp, vv[i], a[qq][i]);
-    }
-  };
   // T column jp = -tau_jp T(0:jp, 0:jp) z (lane i < jp owns row i), T(jp, jp) = tau_jp
   auto t_column = [&](int jp, const double* z) {
     if (lane < jp) {
@@ -804,6 +799,15 @@ __global__ __launch_bounds__(512) void qr_sub2c_kernel(const QrSub2Args args) {
       Tl[jp][jp] = taus[jp];
     }
   };
+  unsigned long long pc_acc[4] = {0, 0, 0, 0};
+  unsigned long long tmark = __builtin_amdgcn_s_memtime();
+  auto mark = [&](int ph) {  // PARSEC_QR_PROFILE: 0 v load, 1 columns, 2 factor + T, 3 barrier
+    if (d.prof) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      pc_acc[ph] += t - tmark;
+      tmark = t;
+    }
+  };
   if (w == 0 && jb > 0) factor(0, 0);
   __syncthreads();
   for (int j = 0; j < jb; ++j) {
@@ -812,35 +816,50 @@ __global__ __launch_bounds__(512) void qr_sub2c_kernel(const QrSub2Args args) {
     double vv[RPL];
 #pragma unroll
     for (int i = 0; i < RPL; ++i) vv[i] = vbuf[par][lane + 64 * i];
+    mark(0);
     const int nx = j + 1;
     const bool own_nx = nx < jb && w == nx % NW;
-    if (own_nx) {  // the critical chain: column j+1 first, then its reflector
-      if (tau != 0.0) update(nx / NW, vv, tau);
-      factor(nx, nx / NW);
-    }
+    // every column of this wave at once (4 independent dots, reductions and
+    // updates interleave instead of queueing behind each other's latency):
+    // c > j: update by v_j; c < j: z_c = V_c^T v_j (a TS reflector's R part is
+    // e_c, R values sit there: the R rows are left out of z)
+    double pr[NC], p0[NC];
 #pragma unroll
     for (int q = 0; q < NC; ++q) {
       const int c = w + NW * q;
-      if (c >= jb || c == j || (own_nx && c == nx)) continue;
-      if (c > j) {
-        if (tau != 0.0) update(q, vv, tau);
-      } else {
-        // z_c = V_c^T v_j; a TS reflector's R part is e_c (R values sit there)
-        double p0 = 0.0, p1 = 0.0;
+      double h = 0.0, t = 0.0;
+      if (c < jb && c != j) {
+        h = vv[0] * a[q][0];
 #pragma unroll
-        for (int i = 0; i < RPL; i += 2) {
-          const double x0 = (ts && i == 0 && lane < 32) ? 0.0 : a[q][i];
-          p0 = __builtin_fma(vv[i], x0, p0);
-          if (i + 1 < RPL) p1 = __builtin_fma(vv[i + 1], a[q][i + 1], p1);
-        }
-        const double z = wave_sum_dpp(p0 + p1);
-        if (lane == 0) zb[par][c] = z;
+        for (int i = 1; i < RPL; ++i) t = __builtin_fma(vv[i], a[q][i], t);
+        if (c < j && ts && lane < 32) h = 0.0;
+      }
+      p0[q] = h + t;
+    }
+#pragma unroll
+    for (int q = 0; q < NC; ++q) pr[q] = wave_sum_dpp(p0[q]);
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int c = w + NW * q;
+      if (c >= jb || c == j) continue;
+      if (c > j) {
+        const double tp = tau * pr[q];
+#pragma unroll
+        for (int i = 0; i < RPL; ++i) a[q][i] = __builtin_fma(-tp, vv[i], a[q][i]);
+      } else if (lane == 0) {
+        zb[par][c] = pr[q];
       }
     }
+    mark(1);
+    if (own_nx) factor(nx, nx / NW);  // the critical chain: the next reflector
     // T column j-1 from the z of the previous step, by a wave off the chain
     if (j >= 1 && w == (j + 4) % NW) t_column(j - 1, zb[par ^ 1]);
+    mark(2);
     __syncthreads();
+    mark(3);
   }
+  if (d.prof && lane == 0)
+    for (int q = 0; q < 4; ++q) atomicAdd(&d.prof[(w & 3) * 8 + (w >> 2) * 4 + q], pc_acc[q]);
   if (w == 0 && jb > 0) t_column(jb - 1, zb[(jb - 1) & 1]);
   __syncthreads();
   // ---- write back: R / beta / V per column, T (+ zeros below), zeros above V
