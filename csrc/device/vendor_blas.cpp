@@ -106,7 +106,7 @@ bool vendor_dgemm_batched(const GemmDesc* d, int n, hipStream_t stream) {
   std::lock_guard<std::mutex> g(g_m);
   if (g_enabled < 0) {
     auto& P = ParamRegistry::instance();
-    g_enabled = (int)P.reg_int("device", "hip", "vendor_gemm", "Uniform tile-GEMM batches (no fused epilogue, no triangle) go to rocblas_dgemm_batched", 1);
+    g_enabled = (int)P.reg_int("device", "hip", "vendor_gemm", "Uniform tile-GEMM batches (no fused epilogue, no triangle) go to rocblas_dgemm_batched", 0);
     g_min_dim = (int)P.reg_int("device", "hip", "vendor_gemm_min_dim", "Smallest m, n and k of a batch sent to rocBLAS", 1024);
     g_min_batch = (int)P.reg_int("device", "hip", "vendor_gemm_min_batch", "Smallest batch sent to rocBLAS", 4);
     if (const char* e = getenv("PARSEC_GEMM_VENDOR")) g_enabled = atoi(e);

@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out/g
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 out=gpurun_out/g/vendor_ab.txt; : > $out
-timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_kernels_gpu.py tests/test_dpotrf_gpu.py > gpurun_out/g/kt.log 2>&1 || { tail -5 gpurun_out/g/kt.log; exit 1; }
+PARSEC_GEMM_VENDOR=1 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_kernels_gpu.py tests/test_dpotrf_gpu.py > gpurun_out/g/kt.log 2>&1 || { tail -5 gpurun_out/g/kt.log; exit 1; }
 tail -1 gpurun_out/g/kt.log
 run() { local n=$1 e=$2; shift 2
   env $e timeout -k 10 240 python3 bench.py "$@" > gpurun_out/g/$n.log 2>&1 || return 1
