@@ -179,6 +179,7 @@ struct KernelBatch {
   std::vector<QrApplyDesc> qr_apply;
   std::vector<std::function<void(hipStream_t)>> generic;  // other kernels, launched in order
   bool critical = false;  // launched on the critical stream: waves at raised issue priority
+  bool one_per_cu = false;  // bulk 128x128 GEMMs padded to one workgroup per CU (room for critical kernels)
   bool empty() const { return gemm.empty() && trsm.empty() && potrf.empty() && trsm_w.empty() && stencil.empty() && qr_panel.empty() && qr_apply.empty() && generic.empty(); }
   void clear() { gemm.clear(); trsm.clear(); potrf.clear(); trsm_w.clear(); stencil.clear(); qr_panel.clear(); qr_apply.clear(); generic.clear(); }
 };

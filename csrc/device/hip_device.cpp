@@ -1088,6 +1088,7 @@ void HipDevice::launch_group(int s) {
   }
   if (!batches[s].empty()) {
     batches[s].critical = s == 0 && nb_exec_streams >= 2 && wave_priority;
+    batches[s].one_per_cu = s > 0 && bulk_one_per_cu;
     if (roctx) {
       // rocprofv3 --marker-trace: which tasks each launched group carried
       char label[96];
@@ -1410,6 +1411,7 @@ void hip_devices_init(Context* ctx) {
   int rcus = (int)params.reg_int("device", "hip", "reserved_cus", "CUs the bulk streams leave free for the critical stream (CU mask on the bulk streams; 0 = none)", 0);
   int rstride = (int)params.reg_int("device", "hip", "reserved_cus_stride", "Spacing of the reserved CU ids in the CU mask", 1);
   const int64_t grounds = params.reg_int("device", "hip", "group_rounds", "Bulk kernel groups close after this many rounds of resident 128x128 GEMM workgroups (2 per CU); their tasks then complete and release successors per group (0 = one group per scheduling round)", 2);
+  const bool bulk1 = params.reg_int("device", "hip", "bulk_gemm_per_cu", "Bulk-stream 128x128 GEMM workgroups per CU: 2 (default) or 1 (padded LDS: every CU keeps room for a critical-path step workgroup; measured >= 2 at configs 2 and 3: profiles/r3_bulk_per_cu_ab.txt)", 1) == 1;
   int rexcl = (int)params.reg_int("device", "hip", "reserved_cus_exclusive", "With reserved_cus: the critical stream runs on the reserved CUs only (1) or on every CU (0)", 0);
   const bool roctx_on = params.reg_int("device", "hip", "roctx", "roctx range around every launched kernel group (visible with rocprofv3 --marker-trace)", 1) != 0;
   const bool hp_crit = params.reg_int("device", "hip", "hp_on_critical_stream", "High-priority tasks below the critical threshold share the critical stream (1) or go to the least loaded bulk stream (0; measured 36.0 vs 38.9 TF at 16k, profiles/r3_route_ab.txt)", 1) != 0;
@@ -1440,6 +1442,7 @@ void hip_devices_init(Context* ctx) {
     d->reserved_cus = rcus;
     d->reserved_stride = rstride;
     d->reserved_exclusive = rexcl != 0;
+    d->bulk_one_per_cu = bulk1;
     d->group_tiles = grounds > 0 ? (size_t)grounds * 2 * (size_t)std::max(1, d->props.multiProcessorCount) : 0;
     d->wave_priority = wprio;
     d->hp_on_critical = hp_crit;

@@ -136,6 +136,7 @@ struct HipDevice : Device {
   int reserved_cus = 0;
   int reserved_stride = 1;
   bool reserved_exclusive = false;
+  bool bulk_one_per_cu = false;  // device_hip_bulk_gemm_per_cu = 1
   size_t group_tiles = 0;  // close a bulk kernel group at this many 128x128 output tiles (0 = one group per round)
   bool wave_priority = true;
   bool hp_on_critical = true;

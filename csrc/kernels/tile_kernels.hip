@@ -55,6 +55,10 @@ static_assert(sizeof(GemmBatchArgs) <= 4096, "GemmBatchArgs exceeds the kernel a
 // pipe and waits behind their instructions (s_setprio: the SIMD arbitrates by
 // priority, then age).
 static thread_local int t_launch_prio = 0;
+// extra dynamic LDS of the 128x128 GEMM launched by this thread right now:
+// 8 KB pads a workgroup to 82 KB, so a CU holds ONE bulk GEMM workgroup and
+// keeps room for a critical-path tile-POTRF step workgroup (78 KB)
+static thread_local int t_launch_pad = 0;
 #define PARSEC_WAVE_PRIO(p) do { if (p) __builtin_amdgcn_s_setprio(2); } while (0)
 
 template <class Args>
@@ -630,10 +634,18 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
   }
   const int mode = (descs[0].transA ? 2 : 0) | (descs[0].transB ? 1 : 0);
   const dim3 grid(grid_size), block(WM * WN * 64);
+  const size_t pad = BM == 128 ? (size_t)t_launch_pad : 0;
+  if (pad) {
+    static bool said = false;
+    if (!said && getenv("PARSEC_GEMM_PAD_DEBUG")) {
+      said = true;
+      std::fprintf(stderr, "[gemm] bulk 128x128 launch with %zu extra LDS bytes (one workgroup per CU)\n", pad);
+    }
+  }
 #define PARSEC_GEMM_LAUNCH(TA, TB)                                                                                    \
   do {                                                                                                                \
-    if (full) hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, OCC>), grid, block, 0, stream, a); \
-    else hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, false, NBUF, OCC>), grid, block, 0, stream, a);    \
+    if (full) hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, OCC>), grid, block, pad, stream, a); \
+    else hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, false, NBUF, OCC>), grid, block, pad, stream, a);    \
   } while (0)
   switch (mode) {
     case 0: PARSEC_GEMM_LAUNCH(false, false); break;
@@ -945,7 +957,14 @@ void launch_potrf(const PotrfDesc& p, hipStream_t stream, double* ws) {
 // and X rows. Every item runs 2-3 64^3 block products on v_mfma_f64_16x16x4f64
 // (4 waves, a 32 x 32 quadrant each) from LDS; DIAG adds the 64 x 64 factor +
 // inverse of diag_factor_inv. Critical path per step: one launch boundary + DIAG.
-constexpr int kPL = 80;  // LDS ld of a staged 64x64 block: 160 dwords = 32 mod 64, conflict-free MFMA operand reads
+#ifndef PARSEC_POTRF_KPL
+#define PARSEC_POTRF_KPL 78
+#endif
+// LDS ld of a staged 64x64 block: 78 (156 dwords) keeps the step kernel at 78 KB,
+// so it fits beside ONE bulk GEMM workgroup padded to 82 KB (device_hip_bulk_gemm_per_cu
+// = 1: at most one bulk workgroup per CU); 80 (160 dwords = 32 mod 64) is the
+// conflict-free stride of round 2 (80 KB)
+constexpr int kPL = PARSEC_POTRF_KPL;
 typedef double Blk[64][kPL];  // operand form: S[k][m] = op(m, k)
 
 // S[k][m] = G(m, k) (col-major, ld) or, transposed, S[k][m] = G(k, m)
@@ -1543,10 +1562,16 @@ size_t kernel_batch_workspace_bytes(const KernelBatch& b) {
 void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal, void* ws) {
   (void)device_ordinal;
   struct PrioScope {
-    int prev;
-    explicit PrioScope(bool on) : prev(kern::t_launch_prio) { kern::t_launch_prio = on ? 1 : 0; }
-    ~PrioScope() { kern::t_launch_prio = prev; }
-  } prio_scope(b.critical);
+    int prev, prev_pad;
+    PrioScope(bool on, int pad) : prev(kern::t_launch_prio), prev_pad(kern::t_launch_pad) {
+      kern::t_launch_prio = on ? 1 : 0;
+      kern::t_launch_pad = pad;
+    }
+    ~PrioScope() {
+      kern::t_launch_prio = prev;
+      kern::t_launch_pad = prev_pad;
+    }
+  } prio_scope(b.critical, b.one_per_cu ? 8192 : 0);
   // critical-path kernels first: POTRF, then TRSM, then the GEMM/SYRK updates
   for (auto& p : b.potrf) {
     if (kern::potrf_steps_eligible(p)) kern::launch_potrf_steps(p, stream, static_cast<double*>(ws));

@@ -28,6 +28,13 @@ step_kernel = any("dpotrf_step_kernel" in n for _, _, n, _ in st)
 per = nb // 64 + 1 if step_kernel else nb // 64
 key = "dpotrf_step_kernel" if step_kernel else "dpotrf_diag_inv"
 pk = [k for k in st if key in k[2]]
+# the silence between factorizations can be short: with N given, keep the last
+# NT tile POTRFs (the last factorization) counted from the end
+if len(sys.argv) > 3:
+    NT = (int(sys.argv[3]) + nb - 1) // nb
+    pk = [k for k in ks if key in k[2]][-NT * per:]
+    t0 = pk[0][0]
+    st = [k for k in ks if k[0] >= t0]
 groups = [pk[i:i + per] for i in range(0, len(pk), per)]
 print(f"factorization span {(max(k[1] for k in st) - t0) / 1e3:.1f} us, {len(groups)} panels, tile POTRF = {per} x {key}")
 print(f"{'k':>3} {'start':>9} {'potrf':>8} {'chain':>8}")
