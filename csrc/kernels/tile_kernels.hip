@@ -593,6 +593,9 @@ static int g_gemm_big_tiles = 384;   // PARSEC_GEMM_BIG_TILES: 128x128 tiles in 
 static int g_gemm_splitk = -1;       // PARSEC_GEMM_SPLITK=0 disables the split-K tail of the 128x128 kernel
 static int g_gemm_slots = 512;       // resident 128x128 workgroups (2 per CU): one round of the big kernel
 static int g_gemm_chunk_fill = -1;   // PARSEC_GEMM_CHUNK_FILL=0: fixed 40-descriptor launches
+// resident 128x128 workgroups of the launch being issued: half when bulk
+// launches are padded to one workgroup per CU (t_launch_pad)
+static inline int gemm_slots() { return t_launch_pad ? std::max(1, g_gemm_slots / 2) : g_gemm_slots; }
 
 template <int BM, int BN, int BK, int WM, int WN, int NBUF, int OCC = WM * WN / 2>
 static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hipStream_t stream) {
@@ -613,19 +616,20 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
   a.ksplit = 1;
   if (total == 0) return;
   int grid_size = total;
-  if (BM == 128 && g_gemm_splitk != 0 && total > g_gemm_slots) {
+  const int slots = gemm_slots();
+  if (BM == 128 && g_gemm_splitk != 0 && total > slots) {
     // the last partial round of workgroups: split its tiles' K range so it
     // finishes in 1/s of a tile time; needs beta == 1 (partials are added into C)
     // and >= 256 of K per chunk (fewer flops per added byte would be bound by
     // the chip's f64 atomic rate)
-    const int tail = total % g_gemm_slots;
+    const int tail = total % slots;
     int kmin = 1 << 30;
-    bool ok = tail > 0 && 2 * tail <= g_gemm_slots;
+    bool ok = tail > 0 && 2 * tail <= slots;
     for (int i = 0; ok && i < n; ++i) {
       ok = descs[i].beta == 1.0 && !descs[i].a_lower && !descs[i].Cin && !descs[i].C2;
       kmin = std::min(kmin, descs[i].k);
     }
-    const int s = ok ? std::min({g_gemm_slots / std::max(tail, 1), kmin / 256, 8}) : 1;
+    const int s = ok ? std::min({slots / std::max(tail, 1), kmin / 256, 8}) : 1;
     if (s >= 2) {
       a.main_tiles = total - tail;
       a.ksplit = s;
@@ -729,9 +733,10 @@ static int gemm_chunk_size(const GemmDesc* d, int n) {
   double best_fill = -1.0;
   for (int c = 1; c <= cap; ++c) {
     tiles += ((d[c - 1].m + 127) / 128) * ((d[c - 1].n + 127) / 128);
-    if (tiles < g_gemm_slots) continue;
-    const int rounds = (tiles + g_gemm_slots - 1) / g_gemm_slots;
-    const double fill = (double)tiles / ((double)rounds * g_gemm_slots);
+    const int slots = gemm_slots();
+    if (tiles < slots) continue;
+    const int rounds = (tiles + slots - 1) / slots;
+    const double fill = (double)tiles / ((double)rounds * slots);
     if (fill >= best_fill - 1e-9) { best_fill = fill; best = c; }  // ties: the larger cut
   }
   return best_fill >= 0.0 ? best : cap;
