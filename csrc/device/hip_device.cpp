@@ -354,7 +354,8 @@ void HipDevice::start(Context* c) {
   }
   if (!masked) {
     PARSEC_HIP_CHECK(hipStreamCreateWithPriority(&s_exec[0], hipStreamNonBlocking, hi));
-    for (int i = 1; i < total_streams; ++i) PARSEC_HIP_CHECK(hipStreamCreateWithPriority(&s_exec[i], hipStreamNonBlocking, lo));
+    for (int i = 1; i < total_streams; ++i)  // the dedicated high-priority lane (hp_route 2) shares the critical priority
+      PARSEC_HIP_CHECK(hipStreamCreateWithPriority(&s_exec[i], hipStreamNonBlocking, (i == 1 && hp_route == 2 && total_streams >= 3) ? hi : lo));
   }
   cu_masked = masked;
   executing.assign(total_streams, {});
@@ -1012,8 +1013,15 @@ void HipDevice::execute_ready() {
     // a CU partition (reserved_cus) it would crowd the few critical CUs, and
     // without one it would queue behind the critical kernels.
     const bool crit = t->priority >= critical_threshold;
-    if (nb_exec_streams == 1 || crit || (hp && hp_on_critical && (!cu_masked || !reserved_exclusive))) {
+    // hp_route 2 with >= 3 streams: stream 1 carries the high-priority tasks
+    // alone (the critical stream then holds only the chain POTRF -> TRSM(k+1) ->
+    // SYRK(k+1), which no longer queues behind a panel's other TRSMs and GEMMs);
+    // the bulk work uses streams 2..
+    const bool hp_lane = hp_route == 2 && nb_exec_streams >= 3;
+    if (nb_exec_streams == 1 || crit || (hp && hp_route == 1 && (!cu_masked || !reserved_exclusive))) {
       s = 0;
+    } else if (hp && hp_lane) {
+      s = 1;
     } else if (hp || crit) {
       s = -1;
       for (int i = 1; i < nb_exec_streams && s < 0; ++i)  // join a batch already open this round
@@ -1027,12 +1035,12 @@ void HipDevice::execute_ready() {
       // Bulk work: pick a bulk stream with fewer than max_inflight_groups launched
       // groups; when every bulk stream is that far ahead, hold the task so the
       // next round launches it in a larger batch (the streams are busy anyway).
-      const int nbulk = nb_exec_streams - 1;
+      const int b0 = hp_lane ? 2 : 1, nbulk = nb_exec_streams - b0;
       s = -1;
       for (int i = 0; i < nbulk && s < 0; ++i)  // join a batch already open this round
-        if (!round_tasks[1 + i].empty()) s = 1 + i;
+        if (!round_tasks[b0 + i].empty()) s = b0 + i;
       for (int i = 0; i < nbulk && s < 0; ++i) {
-        const int c = 1 + (int)((rr_stream + i) % (uint32_t)nbulk);
+        const int c = b0 + (int)((rr_stream + i) % (uint32_t)nbulk);
         if (max_inflight_groups <= 0 || (int)executing[c].size() < max_inflight_groups) s = c;
       }
       if (s < 0) { again.push_back(g); continue; }
@@ -1414,7 +1422,7 @@ void hip_devices_init(Context* ctx) {
   const bool bulk1 = params.reg_int("device", "hip", "bulk_gemm_per_cu", "Bulk-stream 128x128 GEMM workgroups per CU: 2 (default) or 1 (padded LDS: every CU keeps room for a critical-path step workgroup; measured >= 2 at configs 2 and 3: profiles/r3_bulk_per_cu_ab.txt)", 1) == 1;
   int rexcl = (int)params.reg_int("device", "hip", "reserved_cus_exclusive", "With reserved_cus: the critical stream runs on the reserved CUs only (1) or on every CU (0)", 0);
   const bool roctx_on = params.reg_int("device", "hip", "roctx", "roctx range around every launched kernel group (visible with rocprofv3 --marker-trace)", 1) != 0;
-  const bool hp_crit = params.reg_int("device", "hip", "hp_on_critical_stream", "High-priority tasks below the critical threshold share the critical stream (1) or go to the least loaded bulk stream (0; measured 36.0 vs 38.9 TF at 16k, profiles/r3_route_ab.txt)", 1) != 0;
+  const int hp_crit = (int)params.reg_int("device", "hip", "hp_on_critical_stream", "High-priority tasks below the critical threshold share the critical stream (1), go to the least loaded bulk stream (0; measured 36.0 vs 38.9 TF at 16k, profiles/r3_route_ab.txt), or get stream 1 to themselves (2, bulk on streams 2..)", 1);
   const bool wprio = params.reg_int("device", "hip", "wave_priority", "Kernels of the critical stream raise their waves' issue priority (s_setprio) over co-resident bulk waves", 1) != 0;
   const bool trace = params.reg_int("device", "hip", "trace_launches", "Print every launched kernel group (stream, tasks, batch sizes) to stderr", 0) != 0;
   const bool cow = params.reg_int("device", "hip", "complete_on_workers", "Release completed GPU tasks (successor activation) on the compute threads instead of the manager (measured no faster on DPOTRF; breaks the multi-rank DTD stencil: off)", 0) != 0;
@@ -1445,7 +1453,7 @@ void hip_devices_init(Context* ctx) {
     d->bulk_one_per_cu = bulk1;
     d->group_tiles = grounds > 0 ? (size_t)grounds * 2 * (size_t)std::max(1, d->props.multiProcessorCount) : 0;
     d->wave_priority = wprio;
-    d->hp_on_critical = hp_crit;
+    d->hp_route = hp_crit;
     d->roctx = roctx_on;
     d->max_inflight_groups = maxg;
     d->sort_pending = sortp != 0;

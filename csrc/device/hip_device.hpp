@@ -139,7 +139,7 @@ struct HipDevice : Device {
   bool bulk_one_per_cu = false;  // device_hip_bulk_gemm_per_cu = 1
   size_t group_tiles = 0;  // close a bulk kernel group at this many 128x128 output tiles (0 = one group per round)
   bool wave_priority = true;
-  bool hp_on_critical = true;
+  int hp_route = 1;  // device_hip_hp_on_critical_stream: 1 critical stream, 0 bulk streams, 2 stream 1 alone
   bool cu_masked = false;
   bool batching = true;
   bool sort_pending = true;

@@ -6,10 +6,10 @@ Reference: collections/*:mp and dsl/* :mp tests run with mpiexec -n 2|4|8
 (tests/collections/Testings.cmake:5-6, remote_dep.c:454-591).
 
 Oracle note: every rank checks its tiles against a HOST (LAPACK) Cholesky.
-torch.linalg.cholesky on the GPU was measured to return factors off by ~2e-3 in
-about half of the processes when 2-4 processes share one MI355X
-(scripts/gpu_r2_diag.sh history, profiles/r2_multirank_oracle.log); the
-runtime's own factor matched the host reference to 1e-15 in all of them."""
+torch.linalg.cholesky on the GPU returns wrong factors now and then when several
+processes share one MI355X, also with this runtime never imported
+(profiles/r3_oracle_root_cause.txt, scripts/oracle_probe.py); the runtime's own
+factor matched the host reference to 1e-15 every time."""
 import os
 import subprocess
 import sys
@@ -137,3 +137,23 @@ def test_comm_engine_c_program_gpu_memory(tmp_path, pa):
     assert rc == 0, outs
     text = "".join(o for o, _ in outs)
     assert text.count("ce ok") == 2 and "[1] GET ok" in text and "[1] PUT ok" in text, text
+
+
+def test_headline_tile_size_8_ranks_shared_gpu(pa):
+    """The headline tile size (nb=1024) on the 8-rank P4xQ2 grid bench.py uses on
+    8 GPUs, N=16384, all ranks on the box's one GPU: bench.py's distributed
+    backward-error probe (every rank's tiles, two all-reduces) must pass."""
+    _gpu()
+    import json
+
+    port = 29600 + os.getpid() % 300
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.join(os.path.dirname(HERE), "bench.py"), "--gpus", "8", "--size", "16384", "--nb", "1024",
+           "--steps", "1", "--warmup", "0", "--share-gpu", "--cores", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, start_new_session=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    print(line[:200])
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"].startswith("2D block-cyclic P4xQ2")
+    assert out["residual"] < 1e-12
