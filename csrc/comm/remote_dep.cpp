@@ -6,8 +6,10 @@
 // release_incoming (remote_dep_mpi.c:733-1072, 1594-2072), eager short messages
 // (remote_dep_mpi.c:76-79, PARSEC_DIST_SHORT_LIMIT), pending-action accounting
 // for termination detection.
-// Data plane: device-resident copies go GPU->GPU through RCCL (ShmEngine pair
-// communicators); host copies are fragmented through the shm rings.
+// Data plane: device-resident copies go GPU->GPU over HIP IPC (the receiver maps
+// the sender's allocation and pulls it; optional: the IPC descriptor rides in the
+// activation, comm_eager_ipc), or through RCCL pair communicators on request
+// (comm_device_plane=rccl); host copies are fragmented through the shm rings.
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>

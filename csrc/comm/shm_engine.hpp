@@ -1,5 +1,6 @@
-// Shared-memory active-message transport + RCCL data plane (one node, one
-// process per GPU). See comm.hpp for the design rationale.
+// Shared-memory active-message transport + device data planes (HIP IPC pulls by
+// default, RCCL pair communicators on request), one node, one process per GPU.
+// See comm.hpp for the design rationale.
 #pragma once
 #include <hip/hip_runtime_api.h>
 
@@ -85,8 +86,9 @@ class ShmEngine : public CommEngine {
   // handle (cached), and enqueue a device copy with a completion callback.
   int ipc_export(const void* ptr, void* handle64, uint64_t* offset);
   void* ipc_open(int src, const void* handle64);
-  // one copy stream per source rank: pulls from different peers use different
-  // xGMI links concurrently instead of queueing behind each other
+  // pulls spread over comm_ipc_streams streams (peer r on r % n; stream 0 is the
+  // GPU's shared copy stream); a copy kernel for peers on this GPU, the copy
+  // engines across xGMI (comm_ipc_copy_mode 2)
   int ipc_copy(int src_rank, void* dst, const void* src, size_t bytes, std::function<void()> done);
   // Copy between this rank's GPU and (pinned) host memory on the GPU's copy
   // stream; `done` runs on the comm thread once it landed. -1 when there is no
