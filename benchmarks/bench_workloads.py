@@ -43,15 +43,32 @@ def bench_qr(args):
     import torch.distributed as dist
 
     world, rank, local = _dist()
+    if args.share_gpu:  # validation mode: every rank on GPU 0, collectives over gloo
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.share_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import parsec_amd as pa
 
     pa.require_native()
     pa.mca_set("device_hip_mask", str(1 << local))
     _comm(pa, world, rank, local)
     ctx = pa.init(args.cores)
+
+    def allreduce(v, op=None):  # on the GPU (RCCL) or, sharing one GPU, on host copies (gloo)
+        if world == 1:
+            return v
+        kw = {} if op is None else {"op": op}
+        if args.share_gpu:
+            c = v.cpu()
+            dist.all_reduce(c, **kw)
+            v.copy_(c)
+        else:
+            dist.all_reduce(v, **kw)
+        return v
     gpu = pa.first_gpu_device_index()
     N, nb = args.n, args.nb
     # process grid: --qr-grid 1d = P x 1 row-cyclic (the TS chain of a panel
@@ -105,7 +122,7 @@ def bench_qr(args):
     dt = (time.perf_counter() - t0) / args.steps
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        allreduce(tt, dist.ReduceOp.MAX)
         dt = float(tt.item())
     check = None
     if args.check:
@@ -121,9 +138,7 @@ def bench_qr(args):
         loc = [(m, n, li) for (m, n, li) in loc if li >= 0]
 
         def allsum(v):
-            if world > 1:
-                dist.all_reduce(v)
-            return v
+            return allreduce(v)
 
         def blk(t, m, n):
             return t.t()[:min(nb, N - m * nb), :min(nb, N - n * nb)]
@@ -158,6 +173,8 @@ def bench_qr(args):
                                                                              "parallelism": f"2D block-cyclic P{P}xQ{Q}" if Q > 1 else f"1D row-cyclic P{P}x1"}}
     if check is not None:
         out["residual_AtAx_vs_RtRx"] = check
+    if args.share_gpu:
+        out["note"] = "validation mode: all ranks share GPU 0; not a scaling measurement"
     if world > 1:
         dist.destroy_process_group()
     return out, rank
@@ -229,6 +246,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cores", type=int, default=4)
     ap.add_argument("--qr-grid", choices=["1d", "2d"], default="2d", help="qr: process grid over the ranks")
+    ap.add_argument("--share-gpu", action="store_true", help="qr: validation mode, every rank on GPU 0 (gloo collectives); not a scaling measurement")
     ap.add_argument("--check", action="store_true", help="qr: verify R (||A^T A x - R^T R x|| / (||A||_F^2 ||x||), all ranks) after the timed steps")
     ap.add_argument("--qr-tree", choices=["hqr", "flat"], default="hqr", help="qr: hierarchical (TS domains + TT trees) or flat TS tree")
     ap.add_argument("--qr-domain", type=int, default=0,
