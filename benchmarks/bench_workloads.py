@@ -237,7 +237,7 @@ def bench_dtd_gemm(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("workload", choices=["qr", "stencil", "dtd_gemm"])
-    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--n", "--size", dest="n", type=int, default=None, help="matrix order (use --size under torchrun)")
     ap.add_argument("--nb", type=int, default=512)
     ap.add_argument("--ib", type=int, default=32)
     ap.add_argument("--b", type=int, default=128)
