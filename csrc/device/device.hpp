@@ -83,6 +83,7 @@ struct GemmDesc {
   uint8_t transA, transB;  // 0 = N, 1 = T
   uint8_t lower_only;      // 1: only C's lower triangle (SYRK)
   uint8_t a_lower;         // 1: op(A) is lower triangular (zeros above): row block i only reads k < (i+1) BM
+  uint8_t b_upper;         // 1: op(B) is upper triangular (zeros below): column block j only reads k < (j+1) BN
   // optional (zero = off): beta scales Cin (ld ldcin) instead of C, and C2 (ld
   // ldc2) -= every value written to C (fused "W = A1 + V^T A2" / "A1 -= T^T W")
   int ldcin, ldc2;

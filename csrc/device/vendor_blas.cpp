@@ -87,12 +87,12 @@ StreamCtx* ctx_of(hipStream_t s) {
 
 bool uniform(const GemmDesc* d, int n) {
   const GemmDesc& a = d[0];
-  if (a.lower_only || a.a_lower || a.Cin || a.C2) return false;
+  if (a.lower_only || a.a_lower || a.b_upper || a.Cin || a.C2) return false;
   if (a.m < g_min_dim || a.n < g_min_dim || a.k < g_min_dim) return false;
   for (int i = 1; i < n; ++i) {
     const GemmDesc& b = d[i];
     if (b.m != a.m || b.n != a.n || b.k != a.k || b.lda != a.lda || b.ldb != a.ldb || b.ldc != a.ldc || b.alpha != a.alpha || b.beta != a.beta ||
-        b.transA != a.transA || b.transB != a.transB || b.lower_only || b.a_lower || b.Cin || b.C2)
+        b.transA != a.transA || b.transB != a.transB || b.lower_only || b.a_lower || b.b_upper || b.Cin || b.C2)
       return false;
   }
   return true;

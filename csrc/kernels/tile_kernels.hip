@@ -132,7 +132,8 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
   const int lda = d.lda, ldb = d.ldb;
   // K range of this workgroup (whole K unless split); chunks are BK multiples
   // op(A) lower triangular: row block m0 needs k < m0 + BM only (never split)
-  const int kfull = d.a_lower ? min(d.k, m0 + BM) : d.k;
+  int kfull = d.a_lower ? min(d.k, m0 + BM) : d.k;
+  if (d.b_upper) kfull = min(kfull, n0 + BN);  // op(B) upper triangular: column block n0 reads k < n0 + BN
   const int kchunk = nsplit > 1 ? (((kfull + nsplit - 1) / nsplit + BK - 1) / BK) * BK : kfull;
   const int kbeg = ks * kchunk;
   if (kbeg >= kfull) return;
@@ -626,7 +627,7 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
     int kmin = 1 << 30;
     bool ok = tail > 0 && 2 * tail <= slots;
     for (int i = 0; ok && i < n; ++i) {
-      ok = descs[i].beta == 1.0 && !descs[i].a_lower && !descs[i].Cin && !descs[i].C2;
+      ok = descs[i].beta == 1.0 && !descs[i].a_lower && !descs[i].b_upper && !descs[i].Cin && !descs[i].C2;
       kmin = std::min(kmin, descs[i].k);
     }
     const int s = ok ? std::min({slots / std::max(tail, 1), kmin / 256, 8}) : 1;
@@ -1511,6 +1512,7 @@ size_t trsm_w_workspace_bytes(const TrsmGemmDesc* d, int n) {
 
 // B := B W for every descriptor: copy the B tiles into the workspace, then one
 // grouped GEMM writes B from (copy x W).
+static const bool g_trsm_tri = !getenv("PARSEC_TRSM_TRI") || atoi(getenv("PARSEC_TRSM_TRI")) != 0;
 void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, double* ws) {
   for (int s0 = 0; s0 < n; s0 += kMaxCopyBatch) {
     const int cnt = std::min(kMaxCopyBatch, n - s0);
@@ -1530,6 +1532,7 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
       e.m = t.m; e.n = t.n; e.k = t.n;
       e.lda = t.m; e.ldb = t.ldw; e.ldc = t.ldb;
       e.alpha = 1.0; e.beta = 0.0; e.transA = 0; e.transB = 1; e.lower_only = 0; e.a_lower = 0;  // copy x (L^-1)^T
+      e.b_upper = g_trsm_tri ? 1 : 0;  // (L^-1)^T is upper triangular: output column block j needs k < (j+1) BN only
       p += ((size_t)t.m * t.n * sizeof(double) + 255) / 256 * 256;
     }
     hipLaunchKernelGGL(copy_tiles_kernel, dim3(std::min(256, (maxc + 3) / 4), cnt), dim3(256), 0, stream, ca);
