@@ -32,9 +32,12 @@ def grid_of(n):
     return max(p, n // p), min(p, n // p)  # P >= Q
 
 
+_T0 = time.time()
+
+
 def _stage(msg):
     if os.environ.get("PARSEC_BENCH_VERBOSE"):
-        print(f"[bench rank {os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
+        print(f"[bench rank {os.environ.get('RANK', '0')} +{time.time() - _T0:.3f}s] {msg}", file=sys.stderr, flush=True)
 
 
 def residual_probe(torch, dist, world, A, store, backup, nb, N, rank, share_gpu):
