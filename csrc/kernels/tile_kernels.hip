@@ -1180,7 +1180,31 @@ __device__ __forceinline__ void diag_factor_inv(double* __restrict__ Dl, double*
   for (int p = 0; p < 4; ++p) {
     if (v == p) {
       if (p >= 1) {  // lookahead: panel p-1's update of this wave's own column block
-        for (int R = p; R < 4; ++R) upd_tile(R, p, p - 1);
+        // the 4 - p tiles' k-steps interleaved: independent accumulators keep
+        // the MFMA pipe fed instead of one dependent chain per tile
+        double4_t acc[3];
+        const int rr = lane & 15, kq = lane >> 4;
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          if (t >= 4 - p) break;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[t][q] = Dl[(16 * p + (lane >> 4) + 4 * q) * kPL + 16 * (p + t) + rr];
+        }
+#pragma unroll
+        for (int kk = 0; kk < 16; kk += 4) {
+          const double x = -Dl[(16 * (p - 1) + kk + kq) * kPL + 16 * p + rr];  // B: column block p
+#pragma unroll
+          for (int t = 0; t < 3; ++t) {
+            if (t >= 4 - p) break;
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(x, Dl[(16 * (p - 1) + kk + kq) * kPL + 16 * (p + t) + rr], acc[t], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          if (t >= 4 - p) break;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) Dl[(16 * p + (lane >> 4) + 4 * q) * kPL + 16 * (p + t) + rr] = acc[t][q];
+        }
         __builtin_amdgcn_s_waitcnt(0xc07f);
       }
       double a[16];
