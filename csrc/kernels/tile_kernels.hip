@@ -1276,6 +1276,79 @@ __device__ __forceinline__ void diag_factor_inv(double* __restrict__ Dl, double*
   PARSEC_STAMP(13);
 }
 
+// DIAG entry on the triangles: D = A_dd - P P^T with P = A_dj iD^T. iD is lower
+// triangular, so column tile c of P only needs k < 16 (c + 1), and only D's 10
+// lower 16 x 16 tiles are formed (the factorization never reads the others):
+// 40 + 48 MFMAs on the busiest wave instead of 64 + 64 for two full 64^3
+// products. On entry S0 = A_dj, S1 = iD (staged, not yet synchronised); on
+// exit S1[c][r] = D(r, c) on the lower tiles, S0 free.
+#ifndef PARSEC_DIAG_TRI
+#define PARSEC_DIAG_TRI 1
+#endif
+constexpr bool g_diag_tri = PARSEC_DIAG_TRI != 0;
+__device__ __forceinline__ void diag_enter_tri(Blk& S0, Blk& S1, const double* __restrict__ Add, int lda) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 15, kq = lane >> 4;
+  // this wave's D tiles (row tile dm, column tile dn): 3 / 3 / 2 / 2
+  int dm[3], dn[3], nd;
+  if (w == 0) { dm[0] = 3; dn[0] = 0; dm[1] = 3; dn[1] = 1; dm[2] = 3; dn[2] = 2; nd = 3; }
+  else if (w == 1) { dm[0] = 2; dn[0] = 0; dm[1] = 2; dn[1] = 1; dm[2] = 2; dn[2] = 2; nd = 3; }
+  else if (w == 2) { dm[0] = 1; dn[0] = 0; dm[1] = 1; dn[1] = 1; dm[2] = 0; dn[2] = 0; nd = 2; }
+  else { dm[0] = 0; dn[0] = 0; dm[1] = 3; dn[1] = 3; dm[2] = 0; dn[2] = 0; nd = 2; }
+  double4_t dacc[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dacc[t][q] = t < nd ? Add[(size_t)(16 * dn[t] + kq + 4 * q) * lda + 16 * dm[t] + r] : 0.0;
+  __syncthreads();  // S0, S1 staged
+  // P tiles: row tiles 2 (w & 1) + {0, 1}; column tiles {0, 3} (waves 0, 1) or
+  // {1, 2} (waves 2, 3): 4 (1 + 4) or 4 (2 + 3) k-steps x 2 row tiles = 40
+  const int m0 = 32 * (w & 1);
+  const int nc[2] = {(w >> 1) ? 1 : 0, (w >> 1) ? 2 : 3};
+  double4_t p[2][2];
+  acc_zero(p);
+#pragma unroll
+  for (int kk = 0; kk < 64; kk += 4) {
+    double y[2];
+#pragma unroll
+    for (int jm = 0; jm < 2; ++jm) y[jm] = S0[kk + kq][m0 + 16 * jm + r];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (kk < 16 * (nc[i] + 1)) {
+        const double x = S1[kk + kq][16 * nc[i] + r];
+#pragma unroll
+        for (int jm = 0; jm < 2; ++jm) p[i][jm] = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y[jm], p[i][jm], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();  // every wave has read A_dj
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int jm = 0; jm < 2; ++jm)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) S0[16 * nc[i] + kq + 4 * q][m0 + 16 * jm + r] = p[i][jm][q];  // S0[n][m] = P(m, n)
+  __syncthreads();
+#pragma unroll
+  for (int kk = 0; kk < 64; kk += 4) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      if (t < nd) {
+        const double y = S0[kk + kq][16 * dm[t] + r];
+        const double x = -S0[kk + kq][16 * dn[t] + r];
+        dacc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, dacc[t], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+    if (t < nd)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) S1[16 * dn[t] + kq + 4 * q][16 * dm[t] + r] = dacc[t][q];  // S1[c][r] = D(r, c)
+  __syncthreads();
+}
+
 struct PotrfStepArgs {
   double* A;
   double* W;        // optional: W = L^-1 (ldw); also holds the right-hand sides R
@@ -1341,6 +1414,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
     if (j < 0) {          // first launch: D_0 = A_00
       stage_blk(S1, blkA(0, 0), lda, false);  // S1[c][r] = D(r, c)
       __syncthreads();
+    } else if (g_diag_tri) {
+      stage_blk(S0, blkA(d, j), lda, false);
+      stage_blk(S1, iD, 64, false);
+      diag_enter_tri(S0, S1, blkA(d, d), lda);
     } else {
       acc_load(acc, blkA(d, d), lda);
       stage_blk(S0, blkA(d, j), lda, false);
