@@ -1152,6 +1152,46 @@ __device__ __forceinline__ void diag_block_inverse(const double* Dl, double* Xb,
   __builtin_amdgcn_s_waitcnt(0xc07f);
 }
 
+// Row 3 of the inverse, X_3j = -X_33 T_3j with T_3j = sum_{k=j..2} L_3k X_kj,
+// split so the serial tail is short: while X_33 and row 2 are formed, wave 2
+// computes T_32 = L_32 X_22 (B-operand form in its scratch) and the k < 2 parts
+// of T_30 and T_31 (accumulator layout, parked in the X_30 / X_31 slots)
+__device__ __forceinline__ void row3_partials(const double* Dl, double* Xb, double* Tw) {
+  const int lane = threadIdx.x & 63;
+  double4_t t = (double4_t){0.0, 0.0, 0.0, 0.0};
+  mfma16(t, Dl + 32 * kPL + 48, kPL, Xb + xblk(2, 2), 16, 0, 16, 1.0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Tw[((lane >> 4) + 4 * q) + 16 * (lane & 15)] = t[q];
+  double4_t t0 = (double4_t){0.0, 0.0, 0.0, 0.0}, t1 = t0;
+  mfma16(t0, Dl + 48, kPL, Xb + xblk(0, 0), 16, 0, 16, 1.0);
+  mfma16(t1, Dl + 16 * kPL + 48, kPL, Xb + xblk(1, 1), 16, 0, 16, 1.0);
+  mfma16(t0, Dl + 16 * kPL + 48, kPL, Xb + xblk(1, 0), 16, 0, 16, 1.0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    Xb[xblk(3, 0) + q * 64 + lane] = t0[q];
+    Xb[xblk(3, 1) + q * 64 + lane] = t1[q];
+  }
+}
+__device__ __forceinline__ void row3_finish(const double* Dl, double* Xb, const double* Xc, double* Tw, int j) {
+  const int lane = threadIdx.x & 63;
+  if (j < 2) {
+    double4_t t;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = Xb[xblk(3, j) + q * 64 + lane];
+    mfma16(t, Dl + 32 * kPL + 48, kPL, Xb + xblk(2, j), 16, 0, 16, 1.0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Tw[((lane >> 4) + 4 * q) + 16 * (lane & 15)] = t[q];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+  }
+  double4_t x = (double4_t){0.0, 0.0, 0.0, 0.0};
+  mfma16(x, Xc + 256 * 3, 16, Tw, 16, 0, 16, -1.0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Xb[xblk(3, j) + (lane & 15) * 16 + (lane >> 4) + 4 * q] = x[q];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+}
+
 __device__ __forceinline__ void diag_factor_inv(double* __restrict__ Dl, double* __restrict__ pool, double* __restrict__ T, int ldt, double* __restrict__ invD, int* info, int info_base, bool stamp) {
   PARSEC_STAMP(1);
   double* Xb = pool;                    // X, block-packed: Xb[xblk(i, j) + m * 16 + n] = X(16i + m, 16j + n)
@@ -1259,11 +1299,13 @@ __device__ __forceinline__ void diag_factor_inv(double* __restrict__ Dl, double*
     PARSEC_STAMP(4 + 2 * p);
   }
   if (threadIdx.x == 0 && *bad_s != 0x7fffffff && info) atomicCAS(info, 0, info_base + *bad_s);
-  // X_33 beside row 2 of the inverse, then row 3
+  // X_33 beside row 2 of the inverse and the parts of row 3 already known, then
+  // the rest of row 3
   if (v == 3) diag_block_inverse(Dl, Xb, Xc, dinv, 3);
   else if (v < 2) inv_tile(Dl, Xb, Xc, Tw + 256 * v, 2, v);
+  else row3_partials(Dl, Xb, Tw + 512);
   __syncthreads();
-  if (v < 3) inv_tile(Dl, Xb, Xc, Tw + 256 * v, 3, v);
+  if (v < 3) row3_finish(Dl, Xb, Xc, Tw + 256 * v, v);
   __syncthreads();
   PARSEC_STAMP(11);
   PARSEC_STAMP(12);
