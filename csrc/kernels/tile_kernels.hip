@@ -1192,7 +1192,7 @@ __device__ __forceinline__ void row3_finish(const double* Dl, double* Xb, const 
   __builtin_amdgcn_s_waitcnt(0xc07f);
 }
 
-__device__ __forceinline__ void diag_factor_inv(double* __restrict__ Dl, double* __restrict__ pool, double* __restrict__ T, int ldt, double* __restrict__ invD, int* info, int info_base, bool stamp) {
+__device__ __forceinline__ void diag_factor_inv(double* __restrict__ Dl, double* __restrict__ pool, double* __restrict__ T, int ldt, double* __restrict__ invD, int* info, int info_base, bool stamp, bool spread = false) {
   PARSEC_STAMP(1);
   double* Xb = pool;                    // X, block-packed: Xb[xblk(i, j) + m * 16 + n] = X(16i + m, 16j + n)
   double* Xc = pool + 2560;             // 4 diagonal blocks, col-major 16 x 16: Xc[b*256 + k*16 + m] = X(16b+m, 16b+k)
@@ -1218,8 +1218,14 @@ __device__ __forceinline__ void diag_factor_inv(double* __restrict__ Dl, double*
   // unrolled: every v_readlane below gets a constant lane index
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
+    if (spread && p >= 1) {
+      // panel p-1's update of column block p dealt one tile per wave, so the
+      // panel wave starts from a finished block after one barrier
+      if (v < 4 - p) upd_tile(p + v, p, p - 1);
+      __syncthreads();
+    }
     if (v == p) {
-      if (p >= 1) {  // lookahead: panel p-1's update of this wave's own column block
+      if (p >= 1 && !spread) {  // lookahead: panel p-1's update of this wave's own column block
         // the 4 - p tiles' k-steps interleaved: independent accumulators keep
         // the MFMA pipe fed instead of one dependent chain per tile
         double4_t acc[3];
@@ -1450,7 +1456,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
   double4_t acc[2][2];
   // ---------------------------------------------------------------- DIAG
   if (it < a.n_diag) {
-    const bool stamp = a.stamp != 0;
+    const bool stamp = (a.stamp & 1) != 0, spread = (a.stamp & 2) != 0;
     PARSEC_STAMP(0);
     const int d = j + 1;  // block to factor (0 in the first launch)
     if (j < 0) {          // first launch: D_0 = A_00
@@ -1475,7 +1481,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
       acc_to_blk(acc, S1, false);  // S1[c][r] = D(r, c) (S1 = iD no longer read)
       __syncthreads();
     }
-    diag_factor_inv(&S1[0][0], &S0[0][0], blkA(d, d), lda, a.invD + (size_t)d * 4096, a.info, 64 * d, stamp);
+    diag_factor_inv(&S1[0][0], &S0[0][0], blkA(d, d), lda, a.invD + (size_t)d * 4096, a.info, 64 * d, stamp, spread);
     return;
   }
   it -= a.n_diag;
@@ -1613,7 +1619,12 @@ void launch_potrf_steps(const PotrfDesc& p, hipStream_t stream, double* ws) {
     const char* e = getenv("PARSEC_POTRF_STAMPS");
     g_potrf_stamp_mode = e ? atoi(e) : 0;
   }
-  a.stamp = g_potrf_stamp_mode;
+  static int spread = -1;
+  if (spread < 0) {
+    const char* e = getenv("PARSEC_POTRF_SPREAD");
+    spread = e ? atoi(e) : 1;  // profiles/r3_potrf_spread_ab.txt
+  }
+  a.stamp = (g_potrf_stamp_mode ? 1 : 0) | (spread ? 2 : 0);
   const int nb = p.n / 64;
   a.nb = nb;
   const bool w = p.W_out != nullptr;
