@@ -1087,16 +1087,18 @@ __device__ __forceinline__ void mfma16(double4_t& acc, const double* Sa, int lda
 // place and invert the factor: L (lower part) -> T (global, ldt), X = L^-1 ->
 // invD (64 x 64, col-major). Four iterations over 16-column panels with a
 // one-panel lookahead; in iteration q
-//   wave q      applies panel q-1's rank-16 update to its own column block q
-//               (v_mfma_f64_16x16x4f64 from LDS), factors panel q (rows in
-//               lanes; the next pivot column through v_readlane, the other
-//               columns through an LDS broadcast: the only serial chain), stores
-//               it and inverts its 16 x 16 diagonal block X_qq (forward
-//               substitution, lane = column);
+//   all waves   apply panel q-1's rank-16 update to column block q, one 16 x 16
+//               tile each (v_mfma_f64_16x16x4f64 from LDS), then one barrier
+//               (spread = false: wave q updates the whole block itself);
+//   wave q      factors panel q (rows in lanes; the next pivot column through
+//               v_readlane, the other columns through an LDS broadcast: the
+//               only serial chain) and stores it;
 //   the others  apply panel q-1's update to the tiles right of column block q,
-//               and wave j < q-1 computes X_{q-1,j} = -X_{q-1,q-1} sum_k L_{q-1,k} X_kj;
-// then the three X_3j tiles. Only the panel chain and one column update per
-// panel are serial; the rest of the update and the inverse run beside them.
+//               wave q-1 inverts its 16 x 16 diagonal block X_{q-1,q-1} (forward
+//               substitution, lane = column) and wave j < q-2 forms X_{q-2,j};
+// then X_33 beside row 2 and the known parts of row 3, then the rest of row 3.
+// Only the panel chain and one column-block update per panel are serial; the
+// rest of the update and the inverse run beside them.
 // `pool` (kDiagPoolDoubles, not overlapping Dl) holds X block-packed (the 10
 // lower 16 x 16 blocks, row-major), the diagonal blocks of X col-major, per-wave
 // scratch and the broadcast buffers.
