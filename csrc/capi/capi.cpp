@@ -5,6 +5,7 @@
 // two_dim_rectangle_cyclic.c (block-cyclic init / data_of), arena.c,
 // interfaces/dtd/insert_function.c:2978-3300 (variadic insert_task,
 // unpack_args), profiling.h (user dictionary / trace).
+#include <algorithm>
 #include <cstdarg>
 #include <cstring>
 #include <map>
@@ -205,7 +206,18 @@ void parse_args(va_list ap, PendingArgs& pa) {
 // The reference keeps DTD tiles in the collection (parsec_dtd_tile_of takes no
 // taskpool); the runtime keeps them per taskpool, so the C API resolves against
 // the most recently created live DTD taskpool.
-std::atomic<dtd::DtdTaskpool*> g_last_dtd{nullptr};
+// Live DTD taskpools in creation order, and the one each thread created or
+// inserted into last: parsec_dtd_tile_of resolves against the calling thread's
+// taskpool (a task body that runs an inner DTD taskpool -- hierarchy -- must not
+// redirect, or invalidate, its parent thread's tiles).
+std::mutex g_live_dtd_m;
+std::vector<dtd::DtdTaskpool*> g_live_dtd;
+thread_local dtd::DtdTaskpool* t_last_dtd = nullptr;
+dtd::DtdTaskpool* current_dtd() {
+  std::lock_guard<std::mutex> g(g_live_dtd_m);
+  if (t_last_dtd && std::find(g_live_dtd.begin(), g_live_dtd.end(), t_last_dtd) != g_live_dtd.end()) return t_last_dtd;
+  return g_live_dtd.empty() ? nullptr : g_live_dtd.back();
+}
 
 // user profiling stream (per thread)
 thread_local ProfilingStream* t_prof = nullptr;
@@ -695,10 +707,16 @@ int parsec_taskpool_set_arena_datatype(parsec_taskpool_t* tp, int idx, size_t el
 // ------------------------------------------------------------------ DTD
 parsec_taskpool_t* parsec_dtd_taskpool_new(void) {
   auto* tp = new dtd::DtdTaskpool();
-  g_last_dtd.store(tp);
+  {
+    std::lock_guard<std::mutex> g(g_live_dtd_m);
+    g_live_dtd.push_back(tp);
+  }
+  t_last_dtd = tp;
   tp->destructor_hook = [tp] {
-    dtd::DtdTaskpool* e = tp;
-    g_last_dtd.compare_exchange_strong(e, nullptr);
+    {
+      std::lock_guard<std::mutex> g(g_live_dtd_m);
+      g_live_dtd.erase(std::remove(g_live_dtd.begin(), g_live_dtd.end(), tp), g_live_dtd.end());
+    }
     std::lock_guard<std::mutex> g(g_dtd_m);
     for (auto it = g_dtd_classes.begin(); it != g_dtd_classes.end();) it = it->first.first == tp ? g_dtd_classes.erase(it) : std::next(it);
   };
@@ -739,6 +757,7 @@ static void dtd_insert(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, in
       tc = it->second;
     }
   }
+  t_last_dtd = d;
   d->insert_task(tc, priority, pa.args);
 }
 
@@ -809,13 +828,14 @@ void parsec_dtd_insert_task_with_task_class(parsec_taskpool_t* tp, parsec_dtd_ta
     parse_one(tc->param_sizes[i], ptr, flags | tc->param_ops[i], pa);
   }
   va_end(ap);
+  t_last_dtd = d;
   d->insert_task(tc, priority, pa.args, (uint32_t)device_type);
 }
 parsec_dtd_tile_t* parsec_dtd_tile_of(parsec_data_collection_t* dc, parsec_data_key_t key) {
   // tiles are per-taskpool in the runtime; the C API keeps the reference's
   // collection-scoped call by resolving against the most recent DTD taskpool
   DataCollection* impl = impl_of(dc);
-  dtd::DtdTaskpool* tp = g_last_dtd.load();
+  dtd::DtdTaskpool* tp = current_dtd();
   if (!tp) fatal("parsec_dtd_tile_of: no DTD taskpool is active (add one to a context first)");
   return reinterpret_cast<parsec_dtd_tile_t*>(tp->tile_of(impl, key));
 }
@@ -931,7 +951,13 @@ int ce_mem_register(void* mem, parsec_mem_type_t mem_type, size_t count, parsec_
   parsec_datatype_t dtt = datatype;
   int cnt = (int)count;
   if (mem_type == PARSEC_MEM_TYPE_NONCONTIGUOUS) {
-    bytes = (size_t)type_of(datatype).packed_bytes() * count;  // a byte range of the packed size
+    // the engine moves raw byte ranges (supports_noncontiguous_datatype = 0):
+    // a strided / triangular layout would travel as the wrong elements, so only
+    // a datatype whose packed form IS its memory image is accepted (reference
+    // parsec_mpi_funnelled.c:735 lets MPI walk the layout instead)
+    const Datatype& t = type_of(datatype);
+    if (!t.is_contiguous()) return PARSEC_ERROR;
+    bytes = (size_t)t.packed_bytes() * count;
   } else {
     dtt = new_type(Datatype::contiguous(1, (int64_t)mem_size));  // so mem_retrieve + parsec_type_size give the bytes
     cnt = 1;

@@ -8,11 +8,13 @@
 // MI355X-native design (one process per GPU on one node, no MPI):
 //  * control plane: lock-free SPSC shared-memory rings, one per ordered rank pair,
 //    progressed by one comm thread per rank;
-//  * data plane: device tiles travel GPU->GPU over xGMI -- by default the receiver
-//    maps the sender's allocation through HIP IPC and pulls the tile with an async
-//    D2D copy (one IPC_DONE ack releases the sender's copy); optionally with RCCL
-//    send/recv on a communicator + HIP stream per directed rank pair; host tiles
-//    travel through the shm rings in fragments.
+//  * data plane: the one-sided API below, the only payload path of the runtime.
+//    The sender registers a flow's copy (mem_register), the registration rides in
+//    the activation and the receiver get()s it: device tiles travel GPU->GPU over
+//    xGMI (the engine maps the sender's allocation through HIP IPC and pulls it
+//    with an async copy), host tiles -- and device tiles when the ranks could not
+//    map each other's memory -- through the shm rings in fragments. The get's
+//    completion notifies the sender on TAG_PUT_END, which releases its copy.
 #pragma once
 #include <cstdint>
 #include <functional>
@@ -26,7 +28,7 @@ namespace parsec {
 enum CommTag : int {
   TAG_GET_INTERNAL = 0, TAG_PUT_INTERNAL = 1, TAG_REMOTE_DEP_ACTIVATE = 2, TAG_GET_DATA = 3, TAG_PUT_END = 4,
   TAG_TERMDET_FOURCOUNTER = 5, TAG_TERMDET_USER_TRIGGER = 6, TAG_DATA_FRAGMENT = 7, TAG_BARRIER = 8, TAG_ALLREDUCE = 9,
-  TAG_DATA_IPC = 10, TAG_IPC_DONE = 11, TAG_AGGREGATE = 12,
+  TAG_AGGREGATE = 12,
   TAG_USER = 16, TAG_MAX = 32,
 };
 
@@ -132,7 +134,11 @@ int remote_dep_activate(ExecutionStream* es, Taskpool* tp, RemoteDepsMsg& msg);
 CommEngine* comm_engine();
 uint32_t comm_allreduce_max_u32(uint32_t v);
 int comm_barrier();
-const char* comm_device_plane_name();  // "ipc" | "rccl" | "host" | "none"
+const char* comm_device_plane_name();  // "ipc" | "host" | "none"
+// start-up outcome of the IPC plane on this rank: 0, or the first failing step
+// (-1x set-up, -2x open of peer x, -4x copy from peer x, -6x wrong bytes from
+// peer x, -7 another rank failed)
+int comm_plane_status();
 int comm_rank();
 int comm_size();
 // Bring up the engine explicitly (Python / launcher); returns 0 on success.

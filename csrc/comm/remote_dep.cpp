@@ -6,10 +6,14 @@
 // release_incoming (remote_dep_mpi.c:733-1072, 1594-2072), eager short messages
 // (remote_dep_mpi.c:76-79, PARSEC_DIST_SHORT_LIMIT), pending-action accounting
 // for termination detection.
-// Data plane: device-resident copies go GPU->GPU over HIP IPC (the receiver maps
-// the sender's allocation and pulls it; optional: the IPC descriptor rides in the
-// activation, comm_eager_ipc), or through RCCL pair communicators on request
-// (comm_device_plane=rccl); host copies are fragmented through the shm rings.
+// Data plane: every payload moves through the communication engine's
+// one-sided API, as the reference's does (remote_dep_mpi.c:1677-1710 put,
+// 2021-2029 get): the sender registers each flow's copy with mem_register and
+// the registration rides in the activation; the receiver registers its landing
+// buffer and calls get(). The engine pulls device regions GPU -> GPU over xGMI
+// (HIP IPC) and moves host regions (or device regions without an IPC route) in
+// ring fragments; its completion notifies the sender on TAG_PUT_END, which
+// releases the sender's copy. Short host payloads ride in the activation.
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -29,12 +33,10 @@ static ExecutionStream* g_comm_es = nullptr;
 static size_t g_short_limit = 1024;
 static bool g_recv_from_cache = true;
 static int g_recv_pool = 1;  // 0 free after use, 1 recycle by size, 2 never reuse (diagnostic)
-static int g_ipc_debug_sync = 0;  // 1: sender hipDeviceSynchronize before answering a GET (diagnostic)
-static int g_eager_ipc = 0;  // comm_eager_ipc: IPC descriptors ride in the activation (no GET round trip)
-static int g_ipc_verify = 0;      // diagnostic: checksum every IPC payload at the sender and after the pull
 
 CommEngine* comm_engine() { return g_ce; }
 int comm_rank() { return g_ce ? g_ce->rank : 0; }
+int comm_plane_status() { return g_ce ? g_ce->plane_status() : 0; }
 int comm_size() { return g_ce ? g_ce->size : 1; }
 uint32_t comm_allreduce_max_u32(uint32_t v) { return g_ce ? (uint32_t)g_ce->allreduce_max(v) : v; }
 int comm_barrier() { return g_ce ? g_ce->sync() : 0; }
@@ -42,16 +44,15 @@ const char* comm_device_plane_name() {
   if (!g_ce) return "none";
   switch (g_ce->device_plane()) {
     case ShmEngine::PLANE_IPC: return "ipc";
-    case ShmEngine::PLANE_RCCL: return "rccl";
     default: return "host";
   }
 }
 
 // ------------------------------------------------------------- wire format
 namespace {
-// FK_IPC: a device flow whose IPC descriptor rides in the activation itself
-// (the receiver pulls at once: no GET round trip; its IPC_DONE releases)
-enum FlowKind : uint8_t { FK_CTL = 0, FK_HOST = 1, FK_DEVICE = 2, FK_EAGER = 3, FK_IPC = 4 };
+// FK_HOST / FK_DEVICE: a payload the receiver fetches with get() from the
+// registration that follows the flow's rank list; FK_EAGER: the bytes follow
+enum FlowKind : uint8_t { FK_CTL = 0, FK_HOST = 1, FK_DEVICE = 2, FK_EAGER = 3 };
 
 struct ActHdr {
   uint32_t tp_id;
@@ -76,46 +77,8 @@ struct FlowDesc {
   uint64_t bytes;
 };
 
-struct GetMsg {
-  uint64_t send_id;
-  uint64_t recv_id;
-  uint32_t flow_mask;
-  int32_t requester;
-};
-
-struct FragHdr {
-  uint64_t recv_id;
-  uint32_t flow;
-  uint32_t pad;
-  uint64_t offset;
-  uint64_t total;
-};
-
-struct IpcMsg {
-  uint64_t recv_id;
-  uint64_t send_id;
-  uint32_t flow;
-  uint32_t pad;
-  uint64_t offset;
-  uint64_t bytes;
-  uint64_t checksum;  // comm_ipc_verify: sender-side sum of the payload words
-  char handle[64];
-};
-
-uint64_t debug_checksum(int dev, const void* p, size_t bytes) {
-  std::vector<uint64_t> h((bytes + 7) / 8, 0);
-  device_memcpy(0, h.data(), dev, p, bytes);
-  uint64_t s = 0;
-  for (size_t i = 0; i < h.size(); ++i) s = s * 1099511628211ull + h[i];
-  return s;
-}
-
-struct IpcDesc {
-  uint64_t offset;
-  char handle[64];
-};
-
-struct IpcDone {
+// get() completion, receiver -> sender on TAG_PUT_END
+struct PutEnd {
   uint64_t send_id;
   uint32_t flow;
   uint32_t pad;
@@ -125,6 +88,8 @@ struct SendState {
   uint64_t id;
   Taskpool* tp;
   DataCopy* data[kMaxFlows] = {};
+  MemReg reg[kMaxFlows];
+  uint32_t registered = 0;  // flows with a registration in reg[]
   std::atomic<int> pending{1};
 };
 
@@ -137,8 +102,7 @@ struct RecvState {
   std::vector<std::vector<int>> ranks;  // per flow destination list (tree)
   std::vector<uint8_t> extra;
   DataCopy* data[kMaxFlows] = {};
-  uint64_t got[kMaxFlows] = {};
-  char* stage[kMaxFlows] = {};  // pinned landing buffer of host fragments bound for device memory
+  MemReg lreg[kMaxFlows];
   int remaining = 0;
 };
 
@@ -152,8 +116,8 @@ std::atomic<uint64_t> g_next_id{1};
 // (flow, payload) on each side, with peer and byte count (reference
 // remote_dep.h:374-415 MPI_DATA_PLD_SND / RCV, checked by check-comms.py)
 ProfilingStream* g_comm_prof = nullptr;
-int k_snd_b = -1, k_snd_e = -1, k_rcv_b = -1, k_rcv_e = -1, k_act_b = -1, k_act_e = -1, k_pull_b = -1, k_pull_e = -1;
-enum : int32_t { PLANE_HOST = 0, PLANE_IPC = 1, PLANE_RCCL = 2 };
+int k_snd_b = -1, k_snd_e = -1, k_rcv_b = -1, k_rcv_e = -1, k_act_b = -1, k_act_e = -1;
+enum : int32_t { PLANE_HOST = 0, PLANE_IPC = 1 };
 struct CommInfo {
   int32_t peer, flow;
   int64_t bytes;
@@ -165,8 +129,6 @@ void comm_trace_init() {
   profiling_add_dictionary_keyword("COMM_DATA_SND", "fill:#0077FF", sizeof(CommInfo), desc, &k_snd_b, &k_snd_e);
   profiling_add_dictionary_keyword("COMM_DATA_RCV", "fill:#00BB44", sizeof(CommInfo), desc, &k_rcv_b, &k_rcv_e);
   profiling_add_dictionary_keyword("COMM_ACTIVATE", "fill:#AA00AA", sizeof(CommInfo), desc, &k_act_b, &k_act_e);
-  // the device copy of an IPC pull alone: issued on the copy stream -> landed
-  profiling_add_dictionary_keyword("COMM_IPC_PULL", "fill:#FFAA00", sizeof(CommInfo), desc, &k_pull_b, &k_pull_e);
   g_comm_prof = profiling_stream_create("comm");
 }
 inline void comm_trace(int key, uint64_t id, uint32_t tp, const CommInfo* info) {
@@ -174,6 +136,9 @@ inline void comm_trace(int key, uint64_t id, uint32_t tp, const CommInfo* info) 
   if (g_comm_prof) profiling_trace_at(g_comm_prof, key, id, 0, profiling_now(), info, info ? sizeof(CommInfo) : 0);
 }
 inline uint64_t flow_event(uint64_t id, int f) { return id * 32 + (uint64_t)f; }
+// a sender's span is per (flow, destination)
+inline uint64_t send_event(uint64_t id, int f, int dst) { return (flow_event(id, f) << 16) | (uint64_t)(dst & 0xffff); }
+int32_t plane_of(int device_index) { return device_index != 0 && g_ce->device_direct() ? PLANE_IPC : PLANE_HOST; }
 
 // position-based broadcast trees over [root] + ranks
 std::vector<int> tree_children(int topo, int pos, int n) {
@@ -187,48 +152,14 @@ std::vector<int> tree_children(int topo, int pos, int n) {
   return c;
 }
 
-// Pinned staging buffers for device tiles sent through host fragments, kept
-// for reuse by size class (comm thread only).
-static std::multimap<size_t, void*> g_pinned_free;
-static size_t pinned_class(size_t bytes) {
-  size_t c = 64 << 10;
-  while (c < bytes) c <<= 1;
-  return c;
-}
-static void* pinned_get(size_t bytes) {
-  const size_t cls = pinned_class(bytes);
-  auto it = g_pinned_free.find(cls);
-  if (it != g_pinned_free.end()) {
-    void* p = it->second;
-    g_pinned_free.erase(it);
-    return p;
-  }
-  void* p = nullptr;
-  if (hipHostMalloc(&p, cls, hipHostMallocDefault) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
-  return p;
-}
-static void pinned_put(void* p, size_t bytes) { g_pinned_free.emplace(pinned_class(bytes), p); }
-static void pinned_release_all() {
-  for (auto& kv : g_pinned_free) (void)hipHostFree(kv.second);
-  g_pinned_free.clear();
-}
-// the bytes of one flow as DATA_FRAGMENT messages
-static void send_fragments(int dst, uint64_t recv_id, uint32_t flow, const char* src, size_t bytes) {
-  const size_t frag = g_ce->max_fragment() - sizeof(FragHdr) - 64;
-  for (size_t off = 0; off < bytes || (bytes == 0 && off == 0); off += frag) {
-    FragHdr fh{recv_id, flow, 0, off, bytes};
-    const size_t n = std::min(frag, bytes - off);
-    g_ce->send_am2(TAG_DATA_FRAGMENT, dst, &fh, sizeof(fh), src + off, n);
-    if (bytes == 0) break;
-  }
-}
-
 void release_send(SendState* s) {
   if (s->pending.fetch_sub(1) != 1) return;
   {
     std::lock_guard<std::mutex> g(g_m);
     g_sends.erase(s->id);
   }
+  for (int f = 0; f < kMaxFlows; ++f)
+    if (s->registered & (1u << f)) g_ce->mem_unregister(&s->reg[f]);
   for (auto*& c : s->data)
     if (c) {
       if (c->device_index != 0) c->readers.fetch_sub(1);
@@ -303,46 +234,46 @@ DataCopy* new_recv_copy(size_t bytes, bool device) {
 
 void deliver(RecvState* r);
 void start_recv(int src, const char* msg, size_t len, Taskpool* tp);
-void pull_ipc(int src, RecvState* r, uint32_t f, const char* handle, uint64_t offset, uint64_t sid, uint64_t want);
 
 // Build and send activations to the direct children of this rank for every flow.
-void send_activations(Taskpool* tp, const ActHdr& base, int my_pos_root_rank, const std::vector<FlowDesc>& fd_in,
-                      const std::vector<std::vector<int>>& ranks, DataCopy* const* data, const std::vector<uint8_t>& extra) {
+void send_activations(Taskpool* tp, const ActHdr& base, const std::vector<FlowDesc>& fd, const std::vector<std::vector<int>>& ranks, DataCopy* const* data,
+                      const std::vector<uint8_t>& extra) {
   const int me = g_ce->rank;
   const int nflows = (int)ranks.size();
   // destination -> flows for which it is a direct child of me
   std::map<int, uint32_t> dest_flows;
+  uint32_t sent_flows = 0;
   for (int f = 0; f < nflows; ++f) {
     if (!(base.output_mask & (1u << f))) continue;
     const auto& rl = ranks[f];  // [root, d1, d2, ...]
     int pos = (int)(std::find(rl.begin(), rl.end(), me) - rl.begin());
     if (pos >= (int)rl.size()) continue;
-    for (int cpos : tree_children(fd_in[f].topo, pos, (int)rl.size())) dest_flows[rl[cpos]] |= 1u << f;
+    for (int cpos : tree_children(fd[f].topo, pos, (int)rl.size())) {
+      dest_flows[rl[cpos]] |= 1u << f;
+      sent_flows |= 1u << f;
+    }
   }
-  (void)my_pos_root_rank;
   if (dest_flows.empty()) return;
   auto* s = new SendState();
   s->id = g_next_id.fetch_add(1);
   s->tp = tp;
-  for (int f = 0; f < nflows; ++f)
-    if (data[f]) {
-      data_copy_retain(data[f]);
-      if (data[f]->device_index != 0) data[f]->readers.fetch_add(1);  // pinned: a GPU cache must not evict it before the peer read it
-      s->data[f] = data[f];
+  for (int f = 0; f < nflows; ++f) {
+    if (!data[f] || !(sent_flows & (1u << f))) continue;
+    data_copy_retain(data[f]);
+    if (data[f]->device_index != 0) data[f]->readers.fetch_add(1);  // pinned: a GPU cache must not evict it before the peers read it
+    s->data[f] = data[f];
+    // one registration per flow, shared by every destination (released with s)
+    if (fd[f].kind == FK_HOST || fd[f].kind == FK_DEVICE) {
+      if (g_ce->mem_register(data[f]->device_private, fd[f].bytes, data[f]->device_index, 0, 0, &s->reg[f]) != 0)
+        fatal("remote dependency: cannot register the payload of flow %d", f);
+      s->registered |= 1u << f;
     }
+  }
   {
     std::lock_guard<std::mutex> g(g_m);
     g_sends[s->id] = s;
   }
   tp->tdm->taskpool_addto_runtime_actions(tp, 1);
-  // device flows on the IPC plane: export once, every destination pulls
-  std::vector<FlowDesc> fd_eff(fd_in.begin(), fd_in.end());
-  IpcDesc ipc[kMaxFlows];
-  if (g_eager_ipc && g_ce->ipc_ok() && !g_ce->rccl_ok())
-    for (int f = 0; f < nflows; ++f)
-      if ((base.output_mask & (1u << f)) && fd_eff[f].kind == FK_DEVICE && data[f] && data[f]->device_index != 0 &&
-          g_ce->ipc_export(data[f]->device_private, ipc[f].handle, &ipc[f].offset) == 0)
-        fd_eff[f].kind = FK_IPC;
   for (auto& [dst, mask] : dest_flows) {
     ActHdr h = base;
     h.send_id = s->id;
@@ -353,18 +284,20 @@ void send_activations(Taskpool* tp, const ActHdr& base, int my_pos_root_rank, co
     int gets = 0;
     for (int f = 0; f < nflows; ++f) {
       if (!(mask & (1u << f))) continue;
-      FlowDesc d = fd_eff[f];
+      FlowDesc d = fd[f];
       d.nranks = (uint16_t)ranks[f].size();
       put(&d, sizeof(d));
       put(ranks[f].data(), ranks[f].size() * sizeof(int));
       if (d.kind == FK_EAGER) {
         put(data[f]->device_private, d.bytes);
         while (body.size() % 8) body.push_back(0);
-      } else if (d.kind == FK_IPC) {
-        put(&ipc[f], sizeof(IpcDesc));
-        ++gets;  // released by this destination's IPC_DONE
       } else if (d.kind != FK_CTL) {
-        ++gets;
+        put(&s->reg[f], sizeof(MemReg));
+        ++gets;  // released by this destination's PUT_END
+        if (g_comm_prof) {
+          CommInfo ci{dst, f, (int64_t)d.bytes, plane_of(data[f]->device_index), (int32_t)(s->id & 0x7fffffff)};
+          comm_trace(k_snd_b, send_event(s->id, f, dst), h.tp_id, &ci);
+        }
       }
     }
     s->pending.fetch_add(gets);
@@ -401,6 +334,23 @@ void on_activate(int src, int, const void* msg, size_t len) {
   start_recv(src, (const char*)msg, len, tp);
 }
 
+// One flow of receive `rid` landed (comm thread): tell the sender, deliver
+// when it was the last one.
+void flow_landed(uint64_t rid, int f) {
+  comm_trace(k_rcv_e, flow_event(rid, f), 0, nullptr);
+  RecvState* rs = nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_m);
+    auto it = g_recvs.find(rid);
+    if (it == g_recvs.end()) return;
+    rs = it->second;
+    g_ce->mem_unregister(&rs->lreg[f]);
+    if (--rs->remaining > 0) return;
+    g_recvs.erase(it);
+  }
+  deliver(rs);
+}
+
 void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
   auto* r = new RecvState();
   r->id = g_next_id.fetch_add(1);
@@ -412,8 +362,8 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
   for (int f = 0; f < kMaxFlows; ++f) if (r->hdr.output_mask & (1u << f)) nflows = f + 1;
   r->fd.resize(nflows);
   r->ranks.resize(nflows);
-  uint32_t get_mask = 0, ipc_mask = 0;
-  IpcDesc ipc[kMaxFlows];
+  uint32_t get_mask = 0;
+  MemReg rreg[kMaxFlows];
   for (int f = 0; f < nflows; ++f) {
     if (!(r->hdr.output_mask & (1u << f))) continue;
     FlowDesc d;
@@ -429,15 +379,13 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
       off += (d.bytes + 7) / 8 * 8;
       r->data[f] = c;
     } else if (d.kind == FK_HOST || d.kind == FK_DEVICE) {
-      bool dev = d.kind == FK_DEVICE && g_ce->device_direct();
-      r->data[f] = new_recv_copy(d.bytes, dev);
+      std::memcpy(&rreg[f], msg + off, sizeof(MemReg));
+      off += sizeof(MemReg);
+      // device payloads land in device memory when the plane moves them GPU to GPU
+      DataCopy* c = new_recv_copy(d.bytes, d.kind == FK_DEVICE && g_ce->device_direct());
+      if (g_ce->mem_register(c->device_private, d.bytes, c->device_index, 0, 0, &r->lreg[f]) != 0) fatal("remote dependency: cannot register a receive buffer");
+      r->data[f] = c;
       get_mask |= 1u << f;
-      ++r->remaining;
-    } else if (d.kind == FK_IPC) {
-      std::memcpy(&ipc[f], msg + off, sizeof(IpcDesc));
-      off += sizeof(IpcDesc);
-      r->data[f] = new_recv_copy(d.bytes, true);
-      ipc_mask |= 1u << f;
       ++r->remaining;
     }
   }
@@ -446,262 +394,51 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
   off += r->hdr.termdet_bytes;
   (void)len;
   tp->tdm->taskpool_addto_runtime_actions(tp, 1);
-  if (!get_mask && !ipc_mask) { deliver(r); return; }
+  if (!get_mask) { deliver(r); return; }
   {
     std::lock_guard<std::mutex> g(g_m);
     g_recvs[r->id] = r;
   }
-  // flows whose IPC descriptor came with the activation: pull right away
-  // (the last completion may deliver r: nothing below touches r after it
-  // unless GETs are still outstanding, which keep r alive)
-  if (ipc_mask) {
-    if (g_comm_prof)
-      for (int f = 0; f < nflows; ++f)
-        if (ipc_mask & (1u << f)) {
-          CommInfo ci{src, f, (int64_t)r->fd[f].bytes, PLANE_IPC, (int32_t)(r->hdr.send_id & 0x7fffffff)};
-          comm_trace(k_rcv_b, flow_event(r->id, f), r->hdr.tp_id, &ci);
-        }
-    const uint64_t sid = r->hdr.send_id;
-    const uint32_t gm_left = get_mask;
-    // the pulls run on the comm thread (copy queues are its own); a replayed
-    // parked activation arrives here on the thread that added the taskpool
-    for (int f = 0; f < nflows; ++f)
-      if (ipc_mask & (1u << f)) {
-        if (g_ce->on_comm_thread()) {
-          pull_ipc(src, r, (uint32_t)f, ipc[f].handle, ipc[f].offset, sid, 0);
-        } else {
-          IpcDesc d = ipc[f];
-          g_ce->post([src, r, f, d, sid] { pull_ipc(src, r, (uint32_t)f, d.handle, d.offset, sid, 0); });
-        }
-      }
-    if (!gm_left) return;
-  }
-  // post the device receives before asking, in flow order (FIFO-matched by RCCL)
-  for (int f = 0; f < nflows; ++f) {
-    if (!(get_mask & (1u << f))) continue;
-    DataCopy* c = r->data[f];
-    if (c->device_index != 0 && g_ce->rccl_ok()) {
-      uint64_t rid = r->id;
-      g_ce->rccl_recv(src, c->device_private, r->fd[f].bytes, [rid, f] {
-        RecvState* rs = nullptr;
-        comm_trace(k_rcv_e, flow_event(rid, f), 0, nullptr);
-        {
-          std::lock_guard<std::mutex> g(g_m);
-          auto it = g_recvs.find(rid);
-          if (it == g_recvs.end()) return;
-          rs = it->second;
-          rs->got[f] = rs->fd[f].bytes;
-          if (--rs->remaining > 0) return;
-          g_recvs.erase(it);
-        }
-        deliver(rs);
-      });
+  // fetch every payload; the last landing delivers r, so everything the gets
+  // need is copied out of r before the first one is issued
+  struct Fetch {
+    int f;
+    uint64_t bytes;
+    MemReg lreg;
+    int32_t plane;
+  };
+  std::vector<Fetch> todo;
+  for (int f = 0; f < nflows; ++f)
+    if (get_mask & (1u << f)) todo.push_back(Fetch{f, r->fd[f].bytes, r->lreg[f], plane_of(r->data[f]->device_index)});
+  const uint64_t rid = r->id, sid = r->hdr.send_id;
+  const uint32_t tpid = r->hdr.tp_id;
+  for (const Fetch& x : todo) {
+    const int f = x.f;
+    if (g_comm_prof) {
+      CommInfo ci{src, f, (int64_t)x.bytes, x.plane, (int32_t)(sid & 0x7fffffff)};
+      comm_trace(k_rcv_b, flow_event(rid, f), tpid, &ci);
     }
-  }
-  if (g_comm_prof)
-    for (int f = 0; f < nflows; ++f) {
-      if (!(get_mask & (1u << f))) continue;
-      DataCopy* c = r->data[f];
-      const int32_t plane = c->device_index != 0 && g_ce->rccl_ok() ? PLANE_RCCL : (c->device_index != 0 && g_ce->ipc_ok() ? PLANE_IPC : PLANE_HOST);
-      CommInfo ci{src, f, (int64_t)r->fd[f].bytes, plane, (int32_t)(r->hdr.send_id & 0x7fffffff)};
-      comm_trace(k_rcv_b, flow_event(r->id, f), r->hdr.tp_id, &ci);
-    }
-  GetMsg gm{r->hdr.send_id, r->id, get_mask, g_ce->rank};
-  PARSEC_DEBUG(kVerbDebug, "comm", "request data from %d (recv %llu mask %x)", src, (unsigned long long)r->id, get_mask);
-  g_ce->send_am(TAG_GET_DATA, src, &gm, sizeof(gm));
-}
-
-void on_get(int src, int, const void* msg, size_t) {
-  GetMsg g;
-  std::memcpy(&g, msg, sizeof(g));
-  PARSEC_DEBUG(kVerbDebug, "comm", "GET from %d send %llu mask %x", src, (unsigned long long)g.send_id, (unsigned)g.flow_mask);
-  SendState* s = nullptr;
-  {
-    std::lock_guard<std::mutex> lk(g_m);
-    auto it = g_sends.find(g.send_id);
-    if (it == g_sends.end()) fatal("GET for unknown send %llu from rank %d", (unsigned long long)g.send_id, src);
-    s = it->second;
-  }
-  for (int f = 0; f < kMaxFlows; ++f) {
-    if (!(g.flow_mask & (1u << f))) continue;
-    DataCopy* c = s->data[f];
-    size_t bytes = c->original ? c->original->nb_elts : 0;
-    const uint32_t tpid = s->tp ? s->tp->taskpool_id : 0;
-    if (c->device_index != 0 && g_ce->rccl_ok()) {
-      CommInfo ci{g.requester, f, (int64_t)bytes, PLANE_RCCL, (int32_t)(g.send_id & 0x7fffffff)};
-      comm_trace(k_snd_b, flow_event(g.send_id, f), tpid, &ci);
-      const uint64_t ev = flow_event(g.send_id, f);
-      g_ce->rccl_send(g.requester, c->device_private, bytes, [s, ev, tpid] {
-        comm_trace(k_snd_e, ev, tpid, nullptr);
-        release_send(s);
-      });
-      continue;
-    }
-    if (c->device_index != 0 && g_ce->ipc_ok()) {
-      if (g_ipc_debug_sync == 1) (void)hipDeviceSynchronize();
-      IpcMsg m{};
-      if (g_ipc_verify) {
-        m.checksum = debug_checksum(c->device_index, c->device_private, bytes);
-        (void)hipDeviceSynchronize();
-        const uint64_t later = debug_checksum(c->device_index, c->device_private, bytes);
-        if (later != m.checksum)
-          warning("IPC verify: tile of send %llu flow %d (%llu bytes) changed after its producer completed (%016llx -> %016llx)", (unsigned long long)g.send_id, f,
-                  (unsigned long long)bytes, (unsigned long long)m.checksum, (unsigned long long)later);
-      }
-      m.recv_id = g.recv_id;
-      m.send_id = g.send_id;
-      m.flow = (uint32_t)f;
-      m.bytes = bytes;
-      if (g_ce->ipc_export(c->device_private, m.handle, &m.offset) == 0) {
-        // the receiver pulls the bytes; its IPC_DONE releases this copy
-        CommInfo ci{g.requester, f, (int64_t)bytes, PLANE_IPC, (int32_t)(g.send_id & 0x7fffffff)};
-        comm_trace(k_snd_b, flow_event(g.send_id, f), tpid, &ci);
-        g_ce->send_am(TAG_DATA_IPC, g.requester, &m, sizeof(m));
-        continue;
-      }
-    }
-    CommInfo ci{g.requester, f, (int64_t)bytes, PLANE_HOST, (int32_t)(g.send_id & 0x7fffffff)};
-    comm_trace(k_snd_b, flow_event(g.send_id, f), tpid, &ci);
-    const int requester = g.requester;
-    const uint64_t recv_id = g.recv_id, ev_id = flow_event(g.send_id, f);
-    if (c->device_index != 0 && bytes) {
-      // device tile without IPC (small allocation, no peer mapping): stage it
-      // through pinned memory on the copy stream; the comm thread keeps serving
-      // and sends the fragments once the copy landed
-      void* pinned = pinned_get(bytes);
-      if (pinned && g_ce->async_copy(pinned, c->device_private, bytes, [=] {
-            send_fragments(requester, recv_id, (uint32_t)f, static_cast<const char*>(pinned), bytes);
-            pinned_put(pinned, bytes);
-            comm_trace(k_snd_e, ev_id, tpid, nullptr);
-            release_send(s);
-          }) == 0)
-        continue;
-      if (pinned) pinned_put(pinned, bytes);
-      std::vector<char> staged(bytes);
-      device_memcpy(0, staged.data(), c->device_index, c->device_private, bytes);
-      send_fragments(requester, recv_id, (uint32_t)f, staged.data(), bytes);
-    } else {
-      send_fragments(requester, recv_id, (uint32_t)f, static_cast<const char*>(c->device_private), bytes);
-    }
-    comm_trace(k_snd_e, ev_id, tpid, nullptr);
-    release_send(s);
+    const PutEnd pe{sid, (uint32_t)f, 0};
+    PARSEC_DEBUG(kVerbDebug, "comm", "get flow %d (%llu bytes) from %d (recv %llu)", f, (unsigned long long)x.bytes, src, (unsigned long long)rid);
+    if (g_ce->get(x.lreg, 0, rreg[f], 0, x.bytes, src, [rid, f](const MemReg&, ptrdiff_t, const MemReg&, ptrdiff_t, size_t, int) { flow_landed(rid, f); },
+                  TAG_PUT_END, &pe, sizeof(pe)) != 0)
+      fatal("remote dependency: get of flow %d from rank %d failed", f, src);
   }
 }
 
-// Receiver: map the sender's allocation and pull flow f of receive r (comm
-// thread); the completion sends IPC_DONE and delivers when it was the last flow.
-void pull_ipc(int src, RecvState* r, uint32_t f, const char* handle, uint64_t offset, uint64_t sid, uint64_t want) {
-  char* base = static_cast<char*>(g_ce->ipc_open(src, handle));
-  DataCopy* c = r->data[f];
-  const uint64_t rid = r->id;
-  const uint64_t bytes = r->fd[f].bytes;
-  const char* srcp = base + offset;
-  if (g_comm_prof) {
-    CommInfo ci{src, (int32_t)f, (int64_t)bytes, 1, (int32_t)(sid & 0x7fffffff)};
-    comm_trace(k_pull_b, flow_event(rid, f), r->hdr.tp_id, &ci);
-  }
-  g_ce->ipc_copy(src, c->device_private, srcp, bytes, [rid, sid, f, src, bytes, want, c, srcp] {
-    comm_trace(k_pull_e, flow_event(rid, f), 0, nullptr);
-    if (g_ipc_verify && want) {
-      uint64_t got = debug_checksum(c->device_index, c->device_private, bytes);
-      if (got != want) {
-        uint64_t again = debug_checksum(c->device_index, srcp, bytes);
-        warning("IPC verify: flow %u from rank %d (%llu bytes): pulled %016llx, sender had %016llx, source now %016llx", f, src, (unsigned long long)bytes,
-                (unsigned long long)got, (unsigned long long)want, (unsigned long long)again);
-      }
-    }
-    comm_trace(k_rcv_e, flow_event(rid, f), 0, nullptr);
-    IpcDone d{sid, f, 0};
-    g_ce->send_am(TAG_IPC_DONE, src, &d, sizeof(d));
-    RecvState* rs = nullptr;
-    {
-      std::lock_guard<std::mutex> g(g_m);
-      auto it = g_recvs.find(rid);
-      if (it == g_recvs.end()) return;
-      rs = it->second;
-      rs->got[f] = bytes;
-      if (--rs->remaining > 0) return;
-      g_recvs.erase(it);
-    }
-    deliver(rs);
-  });
-}
-
-void on_data_ipc(int src, int, const void* msg, size_t) {
-  IpcMsg m;
-  std::memcpy(&m, msg, sizeof(m));
-  RecvState* r = nullptr;
-  {
-    std::lock_guard<std::mutex> g(g_m);
-    auto it = g_recvs.find(m.recv_id);
-    if (it == g_recvs.end()) fatal("IPC data for unknown receive");
-    r = it->second;
-  }
-  if (r->fd[m.flow].bytes != m.bytes) fatal("IPC data: %llu bytes announced, %llu expected", (unsigned long long)m.bytes, (unsigned long long)r->fd[m.flow].bytes);
-  pull_ipc(src, r, m.flow, m.handle, m.offset, m.send_id, m.checksum);
-}
-
-// Sender: the receiver finished pulling one flow.
-void on_ipc_done(int, int, const void* msg, size_t) {
-  IpcDone d;
+// Sender: a destination has the bytes of one flow.
+void on_put_end(int src, int, const void* msg, size_t) {
+  PutEnd d;
   std::memcpy(&d, msg, sizeof(d));
-  comm_trace(k_snd_e, flow_event(d.send_id, (int)d.flow), 0, nullptr);
+  comm_trace(k_snd_e, send_event(d.send_id, (int)d.flow, src), 0, nullptr);
   SendState* s = nullptr;
   {
     std::lock_guard<std::mutex> g(g_m);
     auto it = g_sends.find(d.send_id);
-    if (it == g_sends.end()) fatal("IPC_DONE for unknown send %llu", (unsigned long long)d.send_id);
+    if (it == g_sends.end()) fatal("PUT_END for unknown send %llu from rank %d", (unsigned long long)d.send_id, src);
     s = it->second;
   }
   release_send(s);
-}
-
-void on_fragment(int src, int, const void* msg, size_t len) {
-  (void)src;
-  FragHdr fh;
-  std::memcpy(&fh, msg, sizeof(fh));
-  RecvState* r = nullptr;
-  {
-    std::lock_guard<std::mutex> g(g_m);
-    auto it = g_recvs.find(fh.recv_id);
-    if (it == g_recvs.end()) fatal("data fragment for unknown receive");
-    r = it->second;
-  }
-  size_t n = len - sizeof(FragHdr);
-  DataCopy* c = r->data[fh.flow];
-  const char* payload = (const char*)msg + sizeof(FragHdr);
-  if (c->device_index == 0) {
-    std::memcpy(static_cast<char*>(c->device_private) + fh.offset, payload, n);
-  } else {
-    // device receive buffer: fragments land in pinned memory, one async copy
-    // to the GPU at the end (never a blocking device copy per fragment)
-    if (!r->stage[fh.flow]) r->stage[fh.flow] = static_cast<char*>(pinned_get(std::max<uint64_t>(fh.total, 1)));
-    if (r->stage[fh.flow]) std::memcpy(r->stage[fh.flow] + fh.offset, payload, n);
-    else device_memcpy(c->device_index, static_cast<char*>(c->device_private) + fh.offset, 0, payload, n);
-  }
-  r->got[fh.flow] += n;
-  if (r->got[fh.flow] < fh.total) return;
-  auto flow_landed = [r, recv_id = fh.recv_id, flow = fh.flow] {
-    comm_trace(k_rcv_e, flow_event(recv_id, (int)flow), 0, nullptr);
-    {
-      std::lock_guard<std::mutex> g(g_m);
-      if (--r->remaining > 0) return;
-      g_recvs.erase(r->id);
-    }
-    deliver(r);
-  };
-  if (char* st = r->stage[fh.flow]) {
-    const uint64_t total = fh.total;
-    r->stage[fh.flow] = nullptr;
-    if (g_ce->async_copy(c->device_private, st, total, [st, total, flow_landed] {
-          pinned_put(st, total);
-          flow_landed();
-        }) == 0)
-      return;
-    device_memcpy(c->device_index, c->device_private, 0, st, total);
-    pinned_put(st, total);
-  }
-  flow_landed();
 }
 
 void deliver(RecvState* r) {
@@ -718,7 +455,7 @@ void deliver(RecvState* r) {
   act.extra = r->extra;
   for (int f = 0; f < kMaxFlows; ++f) act.data[f] = r->data[f];
   // forward down the broadcast trees first (children fetch from us)
-  send_activations(tp, r->hdr, r->hdr.root, r->fd, r->ranks, r->data, r->extra);
+  send_activations(tp, r->hdr, r->fd, r->ranks, r->data, r->extra);
   ExecutionStream* es = g_comm_es ? g_comm_es : (tp->context ? tp->context->all_es[0] : nullptr);
   // reference remote_dep_mpi.c:1838,1887: the activation callback of a received
   // remote dependency, bracketed for PINS modules (task_profiler traces it)
@@ -777,7 +514,7 @@ int remote_dep_activate(ExecutionStream* es, Taskpool* tp, RemoteDepsMsg& m) {
     for (int r : o.ranks) if (r != g_ce->rank) ranks[f].push_back(r);
   }
   if (!h.output_mask) return 0;
-  send_activations(tp, h, g_ce->rank, fd, ranks, data.data(), m.extra);
+  send_activations(tp, h, fd, ranks, data.data(), m.extra);
   return 0;
 }
 
@@ -794,10 +531,7 @@ int comm_init(int rank, int size, const std::string& job_id, int gpu_ordinal) {
   auto* e = new ShmEngine(rank, size, job_id, gpu_ordinal);
   g_ce = e;
   e->tag_register(TAG_REMOTE_DEP_ACTIVATE, on_activate);
-  e->tag_register(TAG_GET_DATA, on_get);
-  e->tag_register(TAG_DATA_FRAGMENT, on_fragment);
-  e->tag_register(TAG_DATA_IPC, on_data_ipc);
-  e->tag_register(TAG_IPC_DONE, on_ipc_done);
+  e->tag_register(TAG_PUT_END, on_put_end);
   e->tag_register(TAG_TERMDET_USER_TRIGGER, on_user_trigger);
   fourcounter_register(e);
   if (e->init() != 0) {
@@ -818,6 +552,10 @@ std::vector<std::pair<std::string, uint64_t>> comm_stats() {
   r.emplace_back("aggregates", st.aggregates.load());
   r.emplace_back("aggregated_msgs", st.aggregated_msgs.load());
   r.emplace_back("max_waiting", st.max_waiting.load());
+  r.emplace_back("get_ipc", st.get_ipc.load());
+  r.emplace_back("get_fragments", st.get_fragments.load());
+  r.emplace_back("put_ipc", st.put_ipc.load());
+  r.emplace_back("put_fragments", st.put_fragments.load());
   return r;
 }
 
@@ -832,9 +570,6 @@ void comm_fini() {
 void remote_dep_init(Context* ctx) {
   g_short_limit = ParamRegistry::instance().reg_sizet("runtime", "comm", "short_limit", "Eager payload limit (bytes) for host data in activations", 1024);
   g_recv_pool = (int)ParamRegistry::instance().reg_int("comm", "", "recv_pool", "Device receive buffers: 1 recycle by size, 0 free after use, 2 never reuse (diagnostic)", 1);
-  g_ipc_debug_sync = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_debug_sync", "Diagnostic: device-synchronize before exporting a tile to a peer", 0);
-  g_ipc_verify = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_verify", "Diagnostic: checksum IPC payloads at the sender and after the pull", 0);
-  g_eager_ipc = (int)ParamRegistry::instance().reg_int("comm", "", "eager_ipc", "Send the IPC descriptor of device flows with the activation (receiver pulls without a GET round trip; off: A/B on shared-GPU ranks inconclusive, profiles/r2_eager_ipc_ab.log)", 0);
   g_recv_from_cache = ParamRegistry::instance().reg_int("comm", "", "recv_from_cache", "Carve device receive buffers from the GPU tile-cache zone (1) or hipMalloc them (0)", 1) != 0;
   ctx->my_rank = comm_rank();
   ctx->nb_nodes = comm_size();
@@ -876,10 +611,7 @@ void remote_dep_fini(Context* ctx) {
     // owner's hipFree for seconds (2-rank GPU runs, round 2)
     g_ce->release_peer_mappings();
     g_ce->sync();
-    g_ce->post([] {
-      pinned_release_all();
-      set_my_execution_stream(nullptr);
-    });
+    g_ce->post([] { set_my_execution_stream(nullptr); });
   }
   g_comm_es = nullptr;
   if (g_ctx == ctx) g_ctx = nullptr;

@@ -1,4 +1,4 @@
-// Shared-memory active messages + RCCL pair communicators.
+// Shared-memory active messages + the HIP-IPC device plane.
 //
 // Every rank owns one POSIX shm segment holding a header and one inbound SPSC
 // ring per peer (ring[src] is written only by rank src, read only by our comm
@@ -7,18 +7,16 @@
 // the comm thread flushes (the reference's funnelled MPI engine keeps a similar
 // per-peer FIFO, parsec_mpi_funnelled.c:1089-1139).
 //
-// RCCL: one 2-rank communicator + one HIP stream per DIRECTED rank pair. A
-// directed pair only ever carries sends from its rank 0 to its rank 1, issued in
-// the order GET requests arrive, and the receiver posts its receives in the order
-// it sent those GETs, so transfers are FIFO-matched and can never cross or
-// deadlock (unlike one shared communicator whose ordered stream would serialize
-// a send behind an unrelated receive).
+// Device plane: at start-up every rank exports a probe buffer, maps every
+// peer's and checks its bytes; the ranks agree (all-reduce) on IPC or on the
+// host plane. Payloads then move only through the one-sided API
+// (shm_onesided.cpp), which pulls device regions over xGMI on this GPU's pull
+// stream(s) and completes them from this comm thread.
 #include "shm_engine.hpp"
 #include "../device/device.hpp"
 
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -97,6 +95,10 @@ ShmEngine::~ShmEngine() {
   ipc_stream_.clear();  // the shared copy stream outlives the engine
   for (hipStream_t x : own_streams_) (void)hipStreamDestroy(x);
   own_streams_.clear();
+  for (auto& kv : pinned_free_) (void)hipHostFree(kv.second);
+  pinned_free_.clear();
+  for (hipEvent_t e : ev_pool_) (void)hipEventDestroy(e);
+  ev_pool_.clear();
   for (int r = 0; r < size; ++r)
     if (maps_[r]) munmap(maps_[r], map_len_[r]);
   shm_unlink(seg_name(job_, rank).c_str());
@@ -191,71 +193,75 @@ int ShmEngine::init() {
   if (gpu_ >= 0 && ParamRegistry::instance().reg_int("runtime", "", "bind_gpu_numa", "Restrict runtime threads to the NUMA node of the (first) GPU", 1))
     bind_thread_to_gpu_numa(gpu_);
   start_thread();
-  // device data plane: ipc (default) | rccl | host
-  const std::string plane = ParamRegistry::instance().reg_string("comm", "", "device_plane", "Data plane for device-resident tiles: ipc, rccl or host", "ipc");
-  if (gpu_ >= 0 && plane == "rccl") {
-    std::atomic<int> rc{1};
-    std::atomic<bool> done{false};
-    post([&] { rc = init_rccl(); done = true; });
-    while (!done.load()) std::this_thread::sleep_for(std::chrono::microseconds(200));
-    rccl_ok_ = rc.load() == 0;
-    if (rccl_ok_) plane_ = PLANE_RCCL;
-    else warning("RCCL data plane unavailable (rc=%d): device tiles will be staged through host memory", rc.load());
-  } else if (gpu_ >= 0 && plane == "ipc") {
+  // device data plane: ipc (default) | host. Every rank runs the same
+  // collective sequence whatever its local outcome (a rank that skips one would
+  // pair unrelated all-reduces of its peers and hang a later barrier): the ranks
+  // agree on IPC only if every one of them mapped every peer's probe buffer and
+  // read the right bytes, else all of them stage device tiles through the host.
+  const std::string plane = ParamRegistry::instance().reg_string("comm", "", "device_plane", "Data plane for device-resident tiles: ipc or host", "ipc");
+  if (plane != "ipc" && plane != "host") warning("comm_device_plane=%s is not a device plane of this engine (ipc | host): using ipc", plane.c_str());
+  if (gpu_ >= 0) copy_q_.resize(size + 1);
+  int local = -1;  // no GPU or host plane requested: this rank does not take part
+  if (gpu_ >= 0 && plane != "host") {
     std::atomic<int> rc{1};
     std::atomic<bool> done{false};
     post([&] { rc = init_ipc(); done = true; });
     while (!done.load()) std::this_thread::sleep_for(std::chrono::microseconds(200));
-    // all ranks agree on the plane: a peer mapping that fails (or reads wrong
-    // bytes) anywhere sends every rank to the host plane instead of a fatal
-    // hipIpcOpenMemHandle in the middle of a run
-    const int local = rc.load() == 0 ? probe_ipc() : rc.load();  // probe_ipc syncs: every pci_bus is published
-    detect_same_gpu();
-    const uint64_t bad = allreduce_max(local != 0 ? 1 : 0);
-    if (bad == 0) plane_ = PLANE_IPC;
-    else warning("IPC data plane unavailable (this rank rc=%d): device tiles will be staged through host memory", local);
+    local = rc.load();
+  }
+  local = probe_ipc(local);  // collectives: every pci_bus is published after its first one
+  detect_same_gpu();
+  const uint64_t bad = allreduce_max(local != 0 ? 1 : 0);
+  ipc_status_ = local != 0 ? local : (bad ? -7 : 0);
+  if (bad == 0) {
+    plane_ = PLANE_IPC;
+    setup_pull_streams();
+  } else if (gpu_ >= 0 && plane != "host") {
+    warning("IPC data plane unavailable (this rank rc=%d): device tiles will be staged through host memory", ipc_status_);
   }
   sync();
   return 0;
 }
 
-int ShmEngine::probe_ipc() {
-  if (hipSetDevice(gpu_) != hipSuccess) return -10;
+// local_rc != 0: this rank cannot (or does not want to) use IPC; it still
+// takes part in both all-reduces so every rank makes the same collective calls.
+int ShmEngine::probe_ipc(int local_rc) {
   const size_t bytes = (size_t)64 << 20;  // far above comm_ipc_min_alloc: a buffer object of its own
   void* buf = nullptr;
-  int rc = 0;
-  if (hipMalloc(&buf, bytes) != hipSuccess) { (void)hipGetLastError(); rc = -11; }
+  int rc = local_rc;
+  if (rc == 0 && hipSetDevice(gpu_) != hipSuccess) { (void)hipGetLastError(); rc = -10; }
+  if (rc == 0 && hipMalloc(&buf, bytes) != hipSuccess) { (void)hipGetLastError(); buf = nullptr; rc = -11; }
   if (rc == 0 && hipMemset(buf, 0x40 + (rank & 0x3f), bytes) != hipSuccess) rc = -12;
   if (rc == 0 && hipDeviceSynchronize() != hipSuccess) rc = -13;
   hipIpcMemHandle_t h{};
   if (rc == 0 && hipIpcGetMemHandle(&h, buf) != hipSuccess) rc = -14;
+  if (rc != 0) (void)hipGetLastError();
   std::memcpy(me_->ipc_probe, &h, sizeof(h));
-  if (allreduce_max(rc != 0 ? 1 : 0) != 0) {  // someone could not even export
-    if (buf) (void)hipFree(buf);
-    (void)hipGetLastError();
-    return rc ? rc : -15;
-  }
-  std::vector<unsigned char> got(4096);
-  for (int r = 0; r < size && rc == 0; ++r) {
-    if (r == rank) continue;
-    hipIpcMemHandle_t ph;
-    std::memcpy(&ph, static_cast<ShmHeader*>(maps_[r])->ipc_probe, sizeof(ph));
-    void* p = nullptr;
-    if (hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess) != hipSuccess) { (void)hipGetLastError(); rc = -20 - r; break; }
-    // the tail of the peer buffer, through the same copy stream the pulls use
+  const bool all_exported = allreduce_max(rc != 0 ? 1 : 0) == 0;  // collective 1: every handle is published
+  if (all_exported) {
+    std::vector<unsigned char> got(4096);
     hipStream_t st = gpu_copy_stream(gpu_);
-    if (hipMemcpyAsync(got.data(), static_cast<char*>(p) + bytes - got.size(), got.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess) {
-      (void)hipGetLastError();
-      rc = -40 - r;
+    for (int r = 0; r < size && rc == 0; ++r) {
+      if (r == rank) continue;
+      hipIpcMemHandle_t ph;
+      std::memcpy(&ph, static_cast<ShmHeader*>(maps_[r])->ipc_probe, sizeof(ph));
+      void* p = nullptr;
+      if (hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess) != hipSuccess) { (void)hipGetLastError(); rc = -20 - r; break; }
+      // the tail of the peer buffer, through the copy stream the pulls use
+      if (!st || hipMemcpyAsync(got.data(), static_cast<char*>(p) + bytes - got.size(), got.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess) {
+        (void)hipGetLastError();
+        rc = -40 - r;
+      }
+      for (unsigned char c : got)
+        if (rc == 0 && c != (unsigned char)(0x40 + (r & 0x3f))) rc = -60 - r;
+      (void)hipIpcCloseMemHandle(p);
     }
-    for (unsigned char c : got)
-      if (rc == 0 && c != (unsigned char)(0x40 + (r & 0x3f))) rc = -60 - r;
-    (void)hipIpcCloseMemHandle(p);
   }
-  (void)allreduce_max(0);  // every peer is done reading before the buffers go
-  (void)hipFree(buf);
-  if (rc) warning("IPC probe failed on rank %d (rc=%d)", rank, rc);
+  (void)allreduce_max(0);  // collective 2: every peer is done reading before the buffers go
+  if (buf) (void)hipFree(buf);
+  if (rc != 0 && local_rc == 0) warning("IPC probe failed on rank %d (rc=%d)", rank, rc);
+  if (rc == 0 && !all_exported) rc = -7;
   return rc;
 }
 
@@ -477,34 +483,17 @@ int ShmEngine::progress() {
       ++n;
     }
   }
-  // IPC copies (per source rank, completed in stream order)
-  for (auto& q : ipc_q_) {
+  // device copies (per pull stream / staging, completed in stream order)
+  for (auto& q : copy_q_) {
     while (!q.empty()) {
       hipError_t e = hipEventQuery(q.front().ev);
       if (e == hipErrorNotReady) break;
-      if (e != hipSuccess) fatal("IPC copy failed: %s", hipGetErrorString(e));
+      if (e != hipSuccess) fatal("device copy of the comm engine failed: %s", hipGetErrorString(e));
       Xfer x = std::move(q.front());
       q.pop_front();
       ev_pool_.push_back(x.ev);
       x.done();
       ++n;
-    }
-  }
-  // RCCL transfers
-  if (rccl_ok_) {
-    for (int p = 0; p < size; ++p) {
-      for (auto* q : {&send_q_[p], &recv_q_[p]}) {
-        while (!q->empty()) {
-          hipError_t e = hipEventQuery(q->front().ev);
-          if (e == hipErrorNotReady) break;
-          if (e != hipSuccess) fatal("RCCL transfer failed: %s", hipGetErrorString(e));
-          Xfer x = std::move(q->front());
-          q->pop_front();
-          ev_pool_.push_back(x.ev);
-          x.done();
-          ++n;
-        }
-      }
     }
   }
   return n;
@@ -576,22 +565,30 @@ uint64_t ShmEngine::allreduce_max(uint64_t v) {
 
 // ------------------------------------------------------------------- IPC
 int ShmEngine::init_ipc() {
-  if (hipSetDevice(gpu_) != hipSuccess) return -1;
+  if (hipSetDevice(gpu_) != hipSuccess) { (void)hipGetLastError(); return -1; }
   std::memset(me_->pci_bus, 0, sizeof(me_->pci_bus));
   if (hipDeviceGetPCIBusId(me_->pci_bus, (int)sizeof(me_->pci_bus) - 1, gpu_) != hipSuccess) {
     (void)hipGetLastError();
     me_->pci_bus[0] = 0;
   }
+  if (!gpu_copy_stream(gpu_)) return -2;
+  return 0;
+}
+
+// Pull streams: every pull rides the GPU's one (high-priority) copy stream,
+// shared with the device engine's transfers, so a process keeps to 4 hardware
+// queues (3 execution streams + this one; GPU_MAX_HW_QUEUES = 4). Across xGMI the
+// copy engines do the pulls, so more queues buy nothing. Only when every peer
+// shares this GPU (validation runs) does a second stream pay: the pulls are
+// copy kernels then, and two queues overlap them (profiles/r3_ipc_pull_ab.txt).
+void ShmEngine::setup_pull_streams() {
   ipc_stream_.assign(size, nullptr);
-  ipc_q_.resize(size);
-  // every pull rides the GPU's one (high-priority) copy stream, shared with the
-  // device engine's transfers: no per-peer streams beyond the 4 hardware queues
-  hipStream_t st = gpu_copy_stream(gpu_);
-  if (!st) return -2;
-  // comm_ipc_streams > 1: extra pull streams (copy engines work in parallel on
-  // distinct queues), peer r on stream r % n; stream 0 is the shared copy stream
-  const int n = (int)std::max<int64_t>(1, ParamRegistry::instance().reg_int("comm", "", "ipc_streams", "Streams the IPC pulls are spread over (peer r -> r % n; 1 = the GPU's shared copy stream only)", 2));
-  std::vector<hipStream_t> pool{st};
+  bool all_same = true;
+  for (int r = 0; r < size; ++r)
+    if (r != rank && !same_gpu_[r]) all_same = false;
+  int n = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_streams", "Streams the IPC pulls are spread over (peer r -> r % n; 1 = the GPU's shared copy stream only; -1 = auto: 2 when every peer shares this GPU, else 1)", -1);
+  if (n < 0) n = all_same ? 2 : 1;
+  std::vector<hipStream_t> pool{gpu_copy_stream(gpu_)};
   int lo = 0, hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
   for (int i = 1; i < n; ++i) {
@@ -602,11 +599,10 @@ int ShmEngine::init_ipc() {
   }
   for (int r = 0; r < size; ++r)
     if (r != rank) ipc_stream_[r] = pool[(size_t)r % pool.size()];
-  return 0;
 }
 
 // Which peers share this rank's GPU (PCI bus ids published in the shm headers;
-// called once every rank has run init_ipc)
+// called after the probe's first collective)
 void ShmEngine::detect_same_gpu() {
   same_gpu_.assign(size, 0);
   for (int r = 0; r < size; ++r) {
@@ -618,13 +614,13 @@ void ShmEngine::detect_same_gpu() {
 int ShmEngine::ipc_export(const void* ptr, void* handle64, uint64_t* offset) {
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
-  if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess || !base) return -1;
+  if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess || !base) { (void)hipGetLastError(); return -1; }
   // small hipMallocs are sub-allocated from shared buffer objects that a peer
   // cannot map at the right offset: such tiles travel through host fragments
   static const size_t min_bytes = ParamRegistry::instance().reg_sizet("comm", "", "ipc_min_alloc", "Smallest device allocation exported through HIP IPC (smaller ones are host-staged)", (size_t)2 << 20);
   if (size < min_bytes) return -3;
-  // called by workers (activations with eager IPC descriptors) and the comm thread
-  // the allocator's buffer id joins the key: a freed allocation's (base, size)
+  // called by workers (registrations of activations) and the comm thread; the
+  // allocator's buffer id joins the key: a freed allocation's (base, size)
   // comes back for the next hipMalloc of the same size, and its cached handle
   // would name the freed buffer object (the peer's open then fails)
   unsigned long long bid = 0;
@@ -639,7 +635,7 @@ int ShmEngine::ipc_export(const void* ptr, void* handle64, uint64_t* offset) {
   if (it == ipc_exported_.end()) {
     hipIpcMemHandle_t h;
     hipError_t e = hipIpcGetMemHandle(&h, (void*)base);
-    if (e != hipSuccess) { warning("hipIpcGetMemHandle failed: %s", hipGetErrorString(e)); return -2; }
+    if (e != hipSuccess) { (void)hipGetLastError(); warning("hipIpcGetMemHandle failed: %s", hipGetErrorString(e)); return -2; }
     std::array<char, 64> a{};
     static_assert(sizeof(h) <= 64, "ipc handle size");
     std::memcpy(a.data(), &h, sizeof(h));
@@ -671,107 +667,67 @@ void ShmEngine::release_peer_mappings() {
   ipc_opened_.clear();
 }
 
-int ShmEngine::ipc_copy(int src_rank, void* dst, const void* src, size_t bytes, std::function<void()> done) {
-  if (src_rank < 0 || src_rank >= size || !ipc_stream_[src_rank]) return -1;
-  hipStream_t st = ipc_stream_[src_rank];
-  hipEvent_t ev;
-  if (!ev_pool_.empty()) { ev = ev_pool_.back(); ev_pool_.pop_back(); }
-  else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1;
-  // 2 (auto): a copy kernel when the peer shares this GPU (the copy engines
-  // managed 4-11 GB/s for same-device pulls: profiles/r3_ipc_pull_ab.txt), the
-  // copy engines across xGMI (they need no CU, so a pull never waits behind the
-  // bulk GEMM workgroups for a slot)
-  static const int cmode = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_copy_mode", "Peer pull: 0 = hipMemcpyAsync (copy engine), 1 = copy kernel, 2 = kernel for a peer on the same GPU, copy engine otherwise", 2);
-  const int mode = cmode == 2 ? ((size_t)src_rank < same_gpu_.size() && same_gpu_[src_rank] ? 1 : 0) : cmode;
-  static const int dbg = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_debug_sync", "Diagnostic: device-synchronize before exporting a tile to a peer", 0);
+hipEvent_t ShmEngine::take_event() {
+  hipEvent_t ev = nullptr;
+  if (!ev_pool_.empty()) { ev = ev_pool_.back(); ev_pool_.pop_back(); return ev; }
+  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+  return ev;
+}
+
+int ShmEngine::ipc_copy(int peer, void* dst, const void* src, size_t bytes, bool kernel_ok, std::function<void()> done) {
+  if (peer < 0 || peer >= size || (size_t)peer >= ipc_stream_.size() || !ipc_stream_[peer]) return -1;
+  hipStream_t st = ipc_stream_[peer];
+  hipEvent_t ev = take_event();
+  if (!ev) return -1;
+  // 2 (auto): a copy kernel when the peer shares this GPU and both ends are
+  // device memory (the copy engines managed 4-11 GB/s for same-device pulls:
+  // profiles/r3_ipc_pull_ab.txt), the copy engines otherwise -- across xGMI they
+  // need no CU, so a pull never waits behind bulk GEMM workgroups for a slot, and
+  // pageable host memory is never touched by a kernel
+  static const int cmode = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_copy_mode", "Peer pull: 0 = hipMemcpyAsync (copy engine), 1 = copy kernel, 2 = kernel for a peer on the same GPU, copy engine otherwise (a kernel only ever moves device-to-device)", 2);
+  const int mode = !kernel_ok ? 0 : cmode == 2 ? ((size_t)peer < same_gpu_.size() && same_gpu_[peer] ? 1 : 0) : cmode;
   if (mode == 1) {
     if (device_copy_kernel(dst, src, bytes, st) != 0) fatal("IPC copy kernel launch failed");
   } else {
     PARSEC_HIP_CHECK_COMM(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st));
   }
-  if (dbg == 2) (void)hipStreamSynchronize(st);
   (void)hipEventRecord(ev, st);
-  ipc_q_[src_rank].push_back(Xfer{ev, std::move(done)});
+  copy_q_[peer].push_back(Xfer{ev, std::move(done)});
   return 0;
 }
 
 int ShmEngine::async_copy(void* dst, const void* src, size_t bytes, std::function<void()> done) {
-  if (gpu_ < 0 || (int)ipc_q_.size() != size) return -1;
+  if (gpu_ < 0 || (int)copy_q_.size() != size + 1) return -1;
   hipStream_t st = gpu_copy_stream(gpu_);
   if (!st) return -1;
-  hipEvent_t ev;
-  if (!ev_pool_.empty()) { ev = ev_pool_.back(); ev_pool_.pop_back(); }
-  else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1;
+  hipEvent_t ev = take_event();
+  if (!ev) return -1;
   PARSEC_HIP_CHECK_COMM(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st));
   (void)hipEventRecord(ev, st);
-  ipc_q_[rank].push_back(Xfer{ev, std::move(done)});  // completed by progress() like the pulls
+  copy_q_[size].push_back(Xfer{ev, std::move(done)});  // completed by progress() like the pulls
   return 0;
 }
 
-// ------------------------------------------------------------------ RCCL
-int ShmEngine::init_rccl() {
-  if (hipSetDevice(gpu_) != hipSuccess) return -1;
-  send_comm_.assign(size, nullptr);
-  recv_comm_.assign(size, nullptr);
-  send_stream_.assign(size, nullptr);
-  recv_stream_.assign(size, nullptr);
-  send_q_.resize(size);
-  recv_q_.resize(size);
-  static_assert(sizeof(ncclUniqueId) <= 128, "id size");
-  for (int d = 0; d < size; ++d) {
-    if (d == rank) continue;
-    ncclUniqueId id;
-    if (ncclGetUniqueId(&id) != ncclSuccess) return -2;
-    std::memcpy(me_->nccl_ids[d], &id, sizeof(id));
+static size_t pinned_class(size_t bytes) {
+  size_t c = 64 << 10;
+  while (c < bytes) c <<= 1;
+  return c;
+}
+void* ShmEngine::pinned_get(size_t bytes) {
+  const size_t cls = pinned_class(bytes);
+  auto it = pinned_free_.find(cls);
+  if (it != pinned_free_.end()) {
+    void* p = it->second;
+    pinned_free_.erase(it);
+    return p;
   }
-  me_->ids_ready.store(1, std::memory_order_release);
-  for (int r = 0; r < size; ++r) {
-    if (r == rank) continue;
-    auto* h = static_cast<ShmHeader*>(maps_[r]);
-    uint64_t t0 = now_ns();
-    while (h->ids_ready.load(std::memory_order_acquire) == 0) {
-      if (now_ns() - t0 > 120ull * 1000000000ull) return -3;
-      std::this_thread::sleep_for(std::chrono::microseconds(200));
-    }
-  }
-  // Ordered init over directed pairs (s -> d) in a global order: deadlock free.
-  for (int s = 0; s < size; ++s)
-    for (int d = 0; d < size; ++d) {
-      if (s == d || (s != rank && d != rank)) continue;
-      ncclUniqueId id;
-      auto* h = static_cast<ShmHeader*>(maps_[s]);
-      std::memcpy(&id, h->nccl_ids[d], sizeof(id));
-      ncclComm_t c;
-      ncclResult_t rc = ncclCommInitRank(&c, 2, id, s == rank ? 0 : 1);
-      if (rc != ncclSuccess) { warning("ncclCommInitRank(%d->%d) failed: %s", s, d, ncclGetErrorString(rc)); return -4; }
-      hipStream_t st;
-      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return -5;
-      if (s == rank) { send_comm_[d] = c; send_stream_[d] = st; }
-      else { recv_comm_[s] = c; recv_stream_[s] = st; }
-    }
-  return 0;
+  if (gpu_ < 0) return nullptr;
+  void* p = nullptr;
+  if (hipHostMalloc(&p, cls, hipHostMallocDefault) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+  return p;
 }
-
-int ShmEngine::rccl_send(int peer, const void* buf, size_t bytes, std::function<void()> done) {
-  hipEvent_t ev;
-  if (!ev_pool_.empty()) { ev = ev_pool_.back(); ev_pool_.pop_back(); }
-  else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1;
-  ncclResult_t rc = ncclSend(buf, bytes, ncclChar, 1, (ncclComm_t)send_comm_[peer], send_stream_[peer]);
-  if (rc != ncclSuccess) fatal("ncclSend to %d failed: %s", peer, ncclGetErrorString(rc));
-  (void)hipEventRecord(ev, send_stream_[peer]);
-  send_q_[peer].push_back(Xfer{ev, std::move(done)});
-  return 0;
-}
-
-int ShmEngine::rccl_recv(int peer, void* buf, size_t bytes, std::function<void()> done) {
-  hipEvent_t ev;
-  if (!ev_pool_.empty()) { ev = ev_pool_.back(); ev_pool_.pop_back(); }
-  else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return -1;
-  ncclResult_t rc = ncclRecv(buf, bytes, ncclChar, 0, (ncclComm_t)recv_comm_[peer], recv_stream_[peer]);
-  if (rc != ncclSuccess) fatal("ncclRecv from %d failed: %s", peer, ncclGetErrorString(rc));
-  (void)hipEventRecord(ev, recv_stream_[peer]);
-  recv_q_[peer].push_back(Xfer{ev, std::move(done)});
-  return 0;
+void ShmEngine::pinned_put(void* p, size_t bytes) {
+  if (p) pinned_free_.emplace(pinned_class(bytes), p);
 }
 
 }  // namespace parsec

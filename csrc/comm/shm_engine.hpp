@@ -1,6 +1,8 @@
-// Shared-memory active-message transport + device data planes (HIP IPC pulls by
-// default, RCCL pair communicators on request), one node, one process per GPU.
-// See comm.hpp for the design rationale.
+// Shared-memory active-message transport + one-sided device data plane (HIP IPC
+// pulls over xGMI), one node, one process per GPU. See comm.hpp for the design
+// rationale. Every payload of the runtime moves through the CommEngine one-sided
+// API (mem_register / get / put): the IPC mapping, the copy queues and the
+// pinned staging below are private to the engine.
 #pragma once
 #include <hip/hip_runtime_api.h>
 
@@ -27,9 +29,6 @@ struct ShmHeader {
   std::atomic<uint32_t> ready;
   int32_t rank, size;
   uint64_t ring_bytes;
-  // RCCL unique ids for the directed pair (this rank -> d), written by this rank
-  char nccl_ids[64][128];
-  std::atomic<uint32_t> ids_ready;
   // IPC start-up probe: handle of a device buffer filled with this rank's byte
   char ipc_probe[64];
   // PCI bus id of this rank's GPU: peers on the same device pull with a copy
@@ -51,15 +50,18 @@ class ShmEngine : public CommEngine {
   struct Stats {
     std::atomic<uint64_t> direct{0}, backlogged{0}, aggregates{0}, aggregated_msgs{0};
     std::atomic<uint64_t> max_waiting{0};
+    std::atomic<uint64_t> get_ipc{0}, get_fragments{0}, put_ipc{0}, put_fragments{0};  // one-sided transfers by route
   } stats;
   int progress() override;
   int sync() override;
   uint64_t allreduce_max(uint64_t v) override;
   void release_peer_mappings() override;
   // one-sided API (shm_onesided.cpp): device regions move GPU <-> GPU over xGMI
-  // through the IPC mapping of the owner's allocation (one async copy on the GPU's
-  // copy stream); host regions move in ring fragments handled by the owner's
-  // comm thread (TAG_GET_INTERNAL request, TAG_PUT_INTERNAL fragments).
+  // through the IPC mapping of the owner's allocation (one async copy on this
+  // GPU's pull stream); host regions, and device regions without an IPC route,
+  // move in ring fragments served by the owner's comm thread (TAG_GET_INTERNAL
+  // request, TAG_PUT_INTERNAL fragments), device ends staged through pinned
+  // memory with async copies (the comm thread never blocks on the GPU).
   int mem_register(void* mem, size_t bytes, int device, int64_t user_dtt, int user_count, MemReg* reg) override;
   int mem_unregister(MemReg* reg) override;
   int mem_retrieve(const MemReg& reg, void** mem, size_t* bytes, int64_t* user_dtt, int* user_count) override;
@@ -75,36 +77,20 @@ class ShmEngine : public CommEngine {
   void set_active(bool on) { active_.store(on, std::memory_order_relaxed); }
   bool thread_running() const { return thread_.joinable(); }
   size_t max_fragment() const { return ring_bytes_ / 4; }
-  // Device data planes (comm thread only). IPC: the sender exports the tile's
-  // allocation (hipIpcGetMemHandle), the receiver maps it once and pulls the
-  // bytes with an async D2D copy (xGMI between GPUs). RCCL: pair communicators.
-  enum DevicePlane { PLANE_HOST = 0, PLANE_IPC = 1, PLANE_RCCL = 2 };
+  // Device data plane, agreed by every rank at start-up: IPC (every rank mapped
+  // every peer's probe buffer and read the right bytes) or host (fragments).
+  enum DevicePlane { PLANE_HOST = 0, PLANE_IPC = 1 };
   int device_plane() const { return plane_; }
   bool device_direct() const { return plane_ != PLANE_HOST; }
-  bool ipc_ok() const { return plane_ == PLANE_IPC; }
-  // IPC: export (handle + offset of `ptr` inside its allocation), open a peer's
-  // handle (cached), and enqueue a device copy with a completion callback.
-  int ipc_export(const void* ptr, void* handle64, uint64_t* offset);
-  void* ipc_open(int src, const void* handle64);
-  // pulls spread over comm_ipc_streams streams (peer r on r % n; stream 0 is the
-  // GPU's shared copy stream); a copy kernel for peers on this GPU, the copy
-  // engines across xGMI (comm_ipc_copy_mode 2)
-  int ipc_copy(int src_rank, void* dst, const void* src, size_t bytes, std::function<void()> done);
-  // Copy between this rank's GPU and (pinned) host memory on the GPU's copy
-  // stream; `done` runs on the comm thread once it landed. -1 when there is no
-  // GPU plane (the caller copies synchronously instead).
-  int async_copy(void* dst, const void* src, size_t bytes, std::function<void()> done);
-  bool rccl_ok() const { return rccl_ok_; }
-  int rccl_send(int peer, const void* buf, size_t bytes, std::function<void()> done);
-  int rccl_recv(int peer, void* buf, size_t bytes, std::function<void()> done);
+  // Start-up report of the IPC plane on this rank: 0, or the first failing
+  // step (-1x set-up, -2x open of peer x, -4x copy from peer x, -6x wrong bytes
+  // from peer x, -7 another rank failed)
+  int plane_status() const { return ipc_status_; }
   int gpu_ordinal() const { return gpu_; }
   void start_thread();
   void stop_thread();
 
  private:
-  struct Pending {
-    std::vector<char> msg;
-  };
   // Per-peer send state. Messages that do not fit the peer's ring wait in
   // `backlog` (FIFO: data / control) or in `prio` (activations, highest task
   // priority first; reference remote_dep_mpi.c:1089-1139 per-peer ordered
@@ -134,7 +120,6 @@ class ShmEngine : public CommEngine {
   ShmRing* in_ring(int src);
   ShmRing* out_ring(int dst);
   void thread_main();
-  int init_rccl();
   std::string job_;
   int gpu_;
   size_t ring_bytes_;
@@ -158,19 +143,36 @@ class ShmEngine : public CommEngine {
   uint64_t coll_result_ = 0;
   int coll_arrived_ = 0;
   uint64_t coll_acc_ = 0;
-  // IPC
+  // ---- device plane (comm thread only, except ipc_export)
   int plane_ = PLANE_HOST;
-  std::vector<hipStream_t> ipc_stream_;
-  std::vector<hipStream_t> own_streams_;  // extra IPC pull streams (comm_ipc_streams > 1)
-  std::vector<uint8_t> same_gpu_;         // peer r runs on this rank's GPU (shared-GPU validation runs)
-  std::vector<std::deque<Xfer>> ipc_q_;
+  int ipc_status_ = 0;
+  std::vector<hipStream_t> ipc_stream_;    // pull stream per peer
+  std::vector<hipStream_t> own_streams_;   // extra pull streams (comm_ipc_streams > 1)
+  std::vector<uint8_t> same_gpu_;          // peer r runs on this rank's GPU (shared-GPU validation runs)
+  std::vector<std::deque<Xfer>> copy_q_;   // per peer (pulls) + [size] (local staging copies), completed in order
+  std::vector<hipEvent_t> ev_pool_;
   std::map<std::tuple<uintptr_t, size_t, unsigned long long>, std::array<char, 64>> ipc_exported_;  // (base, size, buffer id) -> handle
   std::mutex ipc_m_;  // ipc_exported_ / ipc_opened_ (exports happen on worker threads too)
   std::map<std::pair<int, std::string>, void*> ipc_opened_;                    // (src, handle) -> base
   int init_ipc();
-  int probe_ipc();  // every rank opens every peer's probe buffer and checks its bytes
+  void setup_pull_streams();  // after detect_same_gpu: pull streams per peer
+  int probe_ipc(int local_rc);  // every rank opens every peer's probe buffer and checks its bytes
   void detect_same_gpu();
-  // one-sided: this rank's registrations and the gets waiting for fragments
+  // IPC: export (handle + offset of `ptr` inside its allocation), open a peer's
+  // handle (cached), and enqueue a device copy with a completion callback
+  // (kernel_ok: both ends are device memory, so a copy kernel may do it)
+  int ipc_export(const void* ptr, void* handle64, uint64_t* offset);
+  void* ipc_open(int src, const void* handle64);
+  int ipc_copy(int peer, void* dst, const void* src, size_t bytes, bool kernel_ok, std::function<void()> done);
+  // Copy between this rank's GPU and (pinned) host memory on the GPU's copy
+  // stream; `done` runs on the comm thread once it landed. -1 without a GPU.
+  int async_copy(void* dst, const void* src, size_t bytes, std::function<void()> done);
+  hipEvent_t take_event();
+  // pinned staging buffers by size class, reused (comm thread only)
+  std::multimap<size_t, void*> pinned_free_;
+  void* pinned_get(size_t bytes);
+  void pinned_put(void* p, size_t bytes);
+  // ---- one-sided: this rank's registrations and the gets waiting for fragments
   struct Region {
     void* ptr;
     size_t bytes;
@@ -184,26 +186,27 @@ class ShmEngine : public CommEngine {
     size_t size, received;
     char* dst;
     int dst_device;
-    std::vector<char> staging;  // device destination: fragments land here first
+    char* staging;  // device destination: fragments land in pinned memory first
     OneSidedCallback l_cb;
     int r_tag;
     std::vector<char> r_cb_data;
+  };
+  // puts of host fragments into a device region: pinned landing buffer per transfer
+  struct PendingPut {
+    char* staging;
+    uint64_t received;
   };
   std::mutex reg_m_;
   std::map<uint32_t, Region> regions_;
   uint32_t next_region_ = 1;
   std::map<uint64_t, PendingGet> gets_;  // comm thread only
+  std::map<std::tuple<int, uint32_t, uint64_t>, PendingPut> puts_;  // (src, region, start): comm thread only
   uint64_t next_get_ = 1;
   void init_onesided();
   void notify_remote(int remote, int r_tag, const std::vector<char>& data);
   void send_region_fragments(int dst, uint32_t kind, uint32_t region, uint64_t req, const char* src, size_t size, uint64_t dst_off, int r_tag,
                              const std::vector<char>& r_cb_data);
-  // RCCL
-  bool rccl_ok_ = false;
-  std::vector<void*> send_comm_, recv_comm_;  // ncclComm_t per peer
-  std::vector<hipStream_t> send_stream_, recv_stream_;
-  std::vector<std::deque<Xfer>> send_q_, recv_q_;
-  std::vector<hipEvent_t> ev_pool_;
+  void finish_get(int src, uint64_t req);
 };
 
 ShmEngine* shm_engine();

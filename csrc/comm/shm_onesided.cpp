@@ -4,10 +4,16 @@
 // parsec_mpi_funnelled.c:231-382,793-992). MI355X-native transport:
 //  * a device region (GPU memory) is registered by exporting its allocation
 //    through HIP IPC; the peer maps it once and moves the bytes with one async
-//    copy on its GPU's copy stream -- GPU to GPU over xGMI, no host hop;
-//  * a host region is served by its owner's comm thread: a get sends a
-//    TAG_GET_INTERNAL request and the owner answers with TAG_PUT_INTERNAL ring
-//    fragments; a put streams TAG_PUT_INTERNAL fragments into the region.
+//    copy on its GPU's pull stream -- GPU to GPU over xGMI, no host hop (a copy
+//    kernel only when both ends are device memory on one GPU);
+//  * a host region -- or a device region without an IPC route (host plane,
+//    small sub-allocated buffers) -- is served by its owner's comm thread: a get
+//    sends a TAG_GET_INTERNAL request and the owner answers with
+//    TAG_PUT_INTERNAL ring fragments; a put streams TAG_PUT_INTERNAL fragments
+//    into the region. Device ends of such transfers are staged through pinned
+//    buffers with async copies on the copy stream.
+// This is the runtime's only payload path: remote_dep moves every flow with
+// mem_register + get (reference remote_dep_mpi.c:1677-1710, 2021-2029).
 // Completion: the local callback runs on the comm thread, then the remote side
 // receives an active message on r_tag carrying r_cb_data.
 #include <hip/hip_runtime.h>
@@ -136,12 +142,23 @@ void ShmEngine::init_onesided() {
       r = it->second;
     }
     if (q.displ + q.size > r.bytes) fatal("one-sided get from rank %d: [%llu, +%llu) outside region %u (%zu bytes)", src, (unsigned long long)q.displ, (unsigned long long)q.size, q.region, r.bytes);
-    std::vector<char> staged;
     const char* from = static_cast<const char*>(r.ptr) + q.displ;
-    if (r.device != 0) {  // device memory without an IPC route: stage on the host
-      staged.resize(q.size);
-      if (device_memcpy(0, staged.data(), r.device, from, q.size) != 0) fatal("one-sided get: device read failed");
-      from = staged.data();
+    if (r.device != 0 && q.size) {
+      // device memory without an IPC route: staged through pinned memory on the
+      // copy stream; this comm thread keeps serving and sends the fragments
+      // once the copy landed
+      void* pinned = pinned_get(q.size);
+      const uint64_t req = q.req, n = q.size;
+      if (pinned && async_copy(pinned, from, n, [this, src, req, n, pinned] {
+            send_region_fragments(src, FRAG_GET_REPLY, 0, req, static_cast<const char*>(pinned), n, 0, -1, {});
+            pinned_put(pinned, n);
+          }) == 0)
+        return;
+      pinned_put(pinned, n);
+      std::vector<char> staged(n);
+      if (device_memcpy(0, staged.data(), r.device, from, n) != 0) fatal("one-sided get: device read failed");
+      send_region_fragments(src, FRAG_GET_REPLY, 0, q.req, staged.data(), n, 0, -1, {});
+      return;
     }
     send_region_fragments(src, FRAG_GET_REPLY, 0, q.req, from, q.size, 0, -1, {});
   });
@@ -161,29 +178,74 @@ void ShmEngine::init_onesided() {
         r = it->second;
       }
       if (h.offset + h.chunk > r.bytes) fatal("one-sided put from rank %d overflows region %u", src, h.region);
-      char* to = static_cast<char*>(r.ptr) + h.offset;
-      if (r.device == 0) std::memcpy(to, payload, h.chunk);
-      else if (device_memcpy(r.device, to, 0, payload, h.chunk) != 0) fatal("one-sided put: device write failed");
-      if (last && h.r_tag >= 0) {
-        auto cb = (h.r_tag < TAG_MAX) ? cbs_[h.r_tag] : AmCallback();
-        if (cb) cb(src, h.r_tag, payload + h.chunk, h.cbd);
-        else warning("one-sided put completion on unregistered tag %d", h.r_tag);
+      auto notify = [this, src, r_tag = h.r_tag, cbd = std::vector<char>(payload + h.chunk, payload + h.chunk + h.cbd)] {
+        if (r_tag < 0) return;
+        auto cb = (r_tag < TAG_MAX) ? cbs_[r_tag] : AmCallback();
+        if (cb) cb(src, r_tag, cbd.data(), cbd.size());
+        else warning("one-sided put completion on unregistered tag %d", r_tag);
+      };
+      if (r.device == 0) {
+        std::memcpy(static_cast<char*>(r.ptr) + h.offset, payload, h.chunk);
+        if (last) notify();
+        return;
       }
+      // device region: the fragments land in pinned memory, one async copy to
+      // the GPU once the last one arrived (FIFO per peer: it arrives last)
+      const auto key = std::make_tuple(src, h.region, h.start);
+      auto it = puts_.find(key);
+      if (it == puts_.end()) it = puts_.emplace(key, PendingPut{static_cast<char*>(pinned_get(std::max<uint64_t>(h.total, 1))), 0}).first;
+      PendingPut& pp = it->second;
+      char* to = static_cast<char*>(r.ptr) + h.offset;
+      if (pp.staging) std::memcpy(pp.staging + (h.offset - h.start), payload, h.chunk);
+      else if (device_memcpy(r.device, to, 0, payload, h.chunk) != 0) fatal("one-sided put: device write failed");
+      pp.received += h.chunk;
+      if (!last) return;
+      char* st = pp.staging;
+      const uint64_t total = h.total;
+      puts_.erase(it);
+      char* dst = static_cast<char*>(r.ptr) + h.start;
+      if (st && async_copy(dst, st, total, [this, st, total, notify] {
+            pinned_put(st, total);
+            notify();
+          }) == 0)
+        return;
+      if (st) {
+        if (device_memcpy(r.device, dst, 0, st, total) != 0) fatal("one-sided put: device write failed");
+        pinned_put(st, total);
+      }
+      notify();
       return;
     }
     auto it = gets_.find(h.req);
     if (it == gets_.end()) fatal("one-sided get reply for unknown request %llu", (unsigned long long)h.req);
     PendingGet& pg = it->second;
     if (pg.dst_device == 0) std::memcpy(pg.dst + h.offset, payload, h.chunk);
-    else std::memcpy(pg.staging.data() + h.offset, payload, h.chunk);
+    else if (pg.staging) std::memcpy(pg.staging + h.offset, payload, h.chunk);
+    else if (device_memcpy(pg.dst_device, pg.dst + h.offset, 0, payload, h.chunk) != 0) fatal("one-sided get: device write failed");
     pg.received += h.chunk;
     if (pg.received < pg.size) return;
-    if (pg.dst_device != 0 && device_memcpy(pg.dst_device, pg.dst, 0, pg.staging.data(), pg.size) != 0) fatal("one-sided get: device write failed");
-    PendingGet done = std::move(pg);
-    gets_.erase(it);
-    if (done.l_cb) done.l_cb(done.lreg, done.ldispl, done.rreg, done.rdispl, done.size, src);
-    notify_remote(src, done.r_tag, done.r_cb_data);
+    if (pg.dst_device != 0 && pg.staging) {
+      char* st = pg.staging;
+      const uint64_t n = pg.size, req = h.req;
+      if (async_copy(pg.dst, st, n, [this, src, req, st, n] {
+            pinned_put(st, n);
+            finish_get(src, req);
+          }) == 0)
+        return;
+      if (device_memcpy(pg.dst_device, pg.dst, 0, st, n) != 0) fatal("one-sided get: device write failed");
+      pinned_put(st, n);
+    }
+    finish_get(src, h.req);
   });
+}
+
+void ShmEngine::finish_get(int src, uint64_t req) {
+  auto it = gets_.find(req);
+  if (it == gets_.end()) return;
+  PendingGet done = std::move(it->second);
+  gets_.erase(it);
+  if (done.l_cb) done.l_cb(done.lreg, done.ldispl, done.rreg, done.rdispl, done.size, src);
+  notify_remote(src, done.r_tag, done.r_cb_data);
 }
 
 int ShmEngine::get(const MemReg& lreg, ptrdiff_t ldispl, const MemReg& rreg, ptrdiff_t rdispl, size_t size, int remote, OneSidedCallback l_cb, int r_tag,
@@ -196,25 +258,31 @@ int ShmEngine::get(const MemReg& lreg, ptrdiff_t ldispl, const MemReg& rreg, ptr
   if (mem_retrieve(lreg, &lptr, nullptr, nullptr, nullptr) != 0) return -1;
   std::vector<char> cbd(static_cast<const char*>(r_cb_data), static_cast<const char*>(r_cb_data) + (r_cb_data ? r_cb_size : 0));
   char* dst = static_cast<char*>(lptr) + ldispl;
-  post([=, this, cbd = std::move(cbd)]() mutable {
+  auto run = [=, this, cbd = std::move(cbd)]() mutable {
     if (rw.device != 0 && rw.ipc_ok && plane_ == PLANE_IPC) {
       // device region of the peer: map its allocation, pull over xGMI
       char* base = static_cast<char*>(ipc_open(remote, rw.ipc));
       const char* from = base + rw.ipc_offset + rdispl;
-      if (ipc_copy(remote, dst, from, size, [=, this, cbd = std::move(cbd)] {
+      stats.get_ipc.fetch_add(1, std::memory_order_relaxed);
+      if (ipc_copy(remote, dst, from, size, lw.device != 0, [=, this, cbd = std::move(cbd)] {
             if (l_cb) l_cb(lreg, ldispl, rreg, rdispl, size, remote);
             notify_remote(remote, r_tag, cbd);
           }) != 0)
         fatal("one-sided get: IPC copy from rank %d failed", remote);
       return;
     }
-    PendingGet pg{lreg, rreg, ldispl, rdispl, size, 0, dst, lw.device, {}, std::move(l_cb), r_tag, std::move(cbd)};
-    if (lw.device != 0) pg.staging.resize(size);
+    stats.get_fragments.fetch_add(1, std::memory_order_relaxed);
+    char* staging = lw.device != 0 ? static_cast<char*>(pinned_get(size)) : nullptr;
+    PendingGet pg{lreg, rreg, ldispl, rdispl, size, 0, dst, lw.device, staging, std::move(l_cb), r_tag, std::move(cbd)};
     const uint64_t id = next_get_++;
     gets_.emplace(id, std::move(pg));
     GetReq q{id, rw.id, 0, (uint64_t)rdispl, (uint64_t)size};
     send_am(TAG_GET_INTERNAL, remote, &q, sizeof(q));
-  });
+  };
+  // the copy queues and the pending gets belong to the comm thread: a get issued
+  // from one of its callbacks (the runtime's receives) starts right away
+  if (on_comm_thread()) run();
+  else post(std::move(run));
   return 0;
 }
 
@@ -228,29 +296,42 @@ int ShmEngine::put(const MemReg& lreg, ptrdiff_t ldispl, const MemReg& rreg, ptr
   if (mem_retrieve(lreg, &lptr, nullptr, nullptr, nullptr) != 0) return -1;
   std::vector<char> cbd(static_cast<const char*>(r_cb_data), static_cast<const char*>(r_cb_data) + (r_cb_data ? r_cb_size : 0));
   const char* src = static_cast<const char*>(lptr) + ldispl;
-  post([=, this, cbd = std::move(cbd)]() mutable {
+  auto run = [=, this, cbd = std::move(cbd)]() mutable {
     if (rw.device != 0 && rw.ipc_ok && plane_ == PLANE_IPC) {
       // push straight into the peer's device memory over xGMI
       char* base = static_cast<char*>(ipc_open(remote, rw.ipc));
       char* to = base + rw.ipc_offset + rdispl;
-      if (ipc_copy(remote, to, src, size, [=, this, cbd = std::move(cbd)] {
+      stats.put_ipc.fetch_add(1, std::memory_order_relaxed);
+      if (ipc_copy(remote, to, src, size, lw.device != 0, [=, this, cbd = std::move(cbd)] {
             if (l_cb) l_cb(lreg, ldispl, rreg, rdispl, size, remote);
             notify_remote(remote, r_tag, cbd);
           }) != 0)
         fatal("one-sided put: IPC copy to rank %d failed", remote);
       return;
     }
-    std::vector<char> staged;
-    const char* from = src;
+    stats.put_fragments.fetch_add(1, std::memory_order_relaxed);
     if (lw.device != 0) {
-      staged.resize(size);
+      // local device region: staged through pinned memory, fragments once it landed
+      void* pinned = pinned_get(size);
+      if (pinned && async_copy(pinned, src, size, [=, this, cbd = std::move(cbd)] {
+            send_region_fragments(remote, FRAG_PUT, rw.id, 0, static_cast<const char*>(pinned), size, (uint64_t)rdispl, r_tag, cbd);
+            pinned_put(pinned, size);
+            if (l_cb) l_cb(lreg, ldispl, rreg, rdispl, size, remote);
+          }) == 0)
+        return;
+      pinned_put(pinned, size);
+      std::vector<char> staged(size);
       if (device_memcpy(0, staged.data(), lw.device, src, size) != 0) fatal("one-sided put: device read failed");
-      from = staged.data();
+      send_region_fragments(remote, FRAG_PUT, rw.id, 0, staged.data(), size, (uint64_t)rdispl, r_tag, cbd);
+      if (l_cb) l_cb(lreg, ldispl, rreg, rdispl, size, remote);
+      return;
     }
     // the fragments are copies: the local region is free again once they are queued
-    send_region_fragments(remote, FRAG_PUT, rw.id, 0, from, size, (uint64_t)rdispl, r_tag, cbd);
+    send_region_fragments(remote, FRAG_PUT, rw.id, 0, src, size, (uint64_t)rdispl, r_tag, cbd);
     if (l_cb) l_cb(lreg, ldispl, rreg, rdispl, size, remote);
-  });
+  };
+  if (on_comm_thread()) run();
+  else post(std::move(run));
   return 0;
 }
 

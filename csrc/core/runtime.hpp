@@ -109,6 +109,16 @@ struct Datatype {
   void pack(const void* src, void* dst) const;    // gather layout -> contiguous
   void unpack(const void* src, void* dst) const;  // scatter contiguous -> layout
   bool operator==(const Datatype& o) const;
+  // the packed form is the memory image (one gap-free run from offset 0, items
+  // back to back): raw byte copies move such a type correctly
+  bool is_contiguous() const {
+    int64_t at = 0;
+    for (const auto& r : byte_runs()) {
+      if (r.first != at) return false;
+      at += r.second;
+    }
+    return lb == 0 && at == packed_bytes() && extent_bytes() == packed_bytes();
+  }
   static Datatype contiguous(uint32_t esz, int64_t n) { Datatype d; d.kind = CONTIGUOUS; d.elem_size = esz; d.count = n; return d; }
   static Datatype vector(uint32_t esz, int64_t count, int64_t blocklen, int64_t stride) { Datatype d; d.kind = VECTOR; d.elem_size = esz; d.count = count; d.blocklen = blocklen; d.stride = stride; return d; }
   static Datatype lower(uint32_t esz, int64_t n, int64_t ld, bool diag = true) { Datatype d; d.kind = LOWER; d.elem_size = esz; d.count = n; d.stride = ld; d.diag = diag; return d; }

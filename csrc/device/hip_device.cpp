@@ -1020,6 +1020,10 @@ void HipDevice::execute_ready() {
     const bool hp_lane = hp_route == 2 && nb_exec_streams >= 3;
     if (nb_exec_streams == 1 || crit || (hp && hp_route == 1 && (!cu_masked || !reserved_exclusive))) {
       s = 0;
+      // critical_split: the round's critical tasks (sorted first) leave as their
+      // own group, so their completion event -- and the release of the next
+      // link of the chain -- does not wait for the panel's other hp tasks
+      if (critical_split && !crit && !round_tasks[0].empty() && round_tasks[0].back()->task->priority >= critical_threshold) launch_group(0);
     } else if (hp && hp_lane) {
       s = 1;
     } else if (hp || crit) {
@@ -1036,12 +1040,16 @@ void HipDevice::execute_ready() {
       // groups; when every bulk stream is that far ahead, hold the task so the
       // next round launches it in a larger batch (the streams are busy anyway).
       const int b0 = hp_lane ? 2 : 1, nbulk = nb_exec_streams - b0;
+      // while critical-path work runs, bulk streams keep a shallower queue
+      // (critical_bulk_cap): a bulk group launched now would share the CUs with it
+      const int cap = (critical_bulk_cap > 0 && !executing[0].empty()) ? std::min(critical_bulk_cap, max_inflight_groups > 0 ? max_inflight_groups : critical_bulk_cap)
+                                                                        : max_inflight_groups;
       s = -1;
       for (int i = 0; i < nbulk && s < 0; ++i)  // join a batch already open this round
         if (!round_tasks[b0 + i].empty()) s = b0 + i;
       for (int i = 0; i < nbulk && s < 0; ++i) {
         const int c = b0 + (int)((rr_stream + i) % (uint32_t)nbulk);
-        if (max_inflight_groups <= 0 || (int)executing[c].size() < max_inflight_groups) s = c;
+        if (cap <= 0 || (int)executing[c].size() < cap) s = c;
       }
       if (s < 0) { again.push_back(g); continue; }
       if (round_tasks[s].empty()) ++rr_stream;
@@ -1331,7 +1339,11 @@ bool HipDevice::progress() {
                      (unsigned long long)((now_ns() - tr0) / 1000));
       did = true;
       retired = true;
+      // critical_split: the critical stream's successors are dispatched (next
+      // pass) before the bulk streams' completions are released
+      if (s == 0 && critical_split) break;
     }
+    if (s == 0 && retired && critical_split) break;
   }
   if (retired) {
     const uint64_t dt = now_ns() - tc0;
@@ -1427,6 +1439,8 @@ void hip_devices_init(Context* ctx) {
   const bool trace = params.reg_int("device", "hip", "trace_launches", "Print every launched kernel group (stream, tasks, batch sizes) to stderr", 0) != 0;
   const bool cow = params.reg_int("device", "hip", "complete_on_workers", "Release completed GPU tasks (successor activation) on the compute threads instead of the manager (measured no faster on DPOTRF; breaks the multi-rank DTD stencil: off)", 0) != 0;
   int maxg = (int)params.reg_int("device", "hip", "max_inflight_batches", "Launched kernel groups per bulk stream before new bulk tasks wait for a larger batch (0 = no limit)", 2);
+  const int ccap = (int)params.reg_int("device", "hip", "critical_bulk_cap", "Launched kernel groups per bulk stream while the critical stream has work in flight (0 = max_inflight_batches)", 0);
+  const bool csplit = params.reg_int("device", "hip", "critical_split", "Critical-path tasks leave the critical stream as a group of their own and their successors are dispatched before other completions are released", 0) != 0;
   if (enabled == 0) return;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) { (void)hipGetLastError(); return; }
@@ -1456,6 +1470,8 @@ void hip_devices_init(Context* ctx) {
     d->hp_route = hp_crit;
     d->roctx = roctx_on;
     d->max_inflight_groups = maxg;
+    d->critical_bulk_cap = ccap;
+    d->critical_split = csplit;
     d->sort_pending = sortp != 0;
     d->complete_on_workers = cow;
     d->trace_launches = trace;

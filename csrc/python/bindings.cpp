@@ -734,5 +734,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("comm_rank", &comm_rank);
   m.def("comm_size", &comm_size);
   m.def("comm_device_plane", []() { return std::string(comm_device_plane_name()); });
+  m.def("comm_plane_status", &comm_plane_status, "0, or the first failing step of this rank's IPC plane start-up (-1x set-up, -2x open of peer x, -4x copy from peer x, -6x bytes from peer x, -7 another rank failed)");
   m.def("comm_allreduce_max", [](uint32_t v) { py::gil_scoped_release rel; return comm_allreduce_max_u32(v); });
 }

@@ -153,7 +153,7 @@ def generate():
         lines.append(f"build {obj}: hipcc {os.path.join(ROOT, src)}")
         objs.append(obj)
     lib = os.path.join(PKG, "lib", "libparsec_amd.so")
-    libs = f"-L{ROCM}/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -latomic -lpthread -lrt -ldl -Wl,-rpath,{ROCM}/lib"
+    libs = f"-L{ROCM}/lib -lamdhip64 -lrocprofiler-sdk-roctx -latomic -lpthread -lrt -ldl -Wl,-rpath,{ROCM}/lib"
     lines.append(f"build {lib}: solink {' '.join(objs)}")
     lines.append(f"  libs = {libs}")
     pyobjs = []
@@ -221,7 +221,7 @@ def generate_sanitized(kind):
     os.makedirs(os.path.join(out, "obj"), exist_ok=True)
     flags = (f"-std=c++20 -O1 -g -fno-omit-frame-pointer -fPIC -fsanitize={kind} -D__HIP_PLATFORM_AMD__ "
              f"-I{ROCM}/include -I{ROOT}/csrc -I{ROOT}/include -Wno-unused-result")
-    libs = f"-fsanitize={kind} -L{ROCM}/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -latomic -lpthread -lrt -Wl,-rpath,{ROCM}/lib"
+    libs = f"-fsanitize={kind} -L{ROCM}/lib -lamdhip64 -lrocprofiler-sdk-roctx -latomic -lpthread -lrt -Wl,-rpath,{ROCM}/lib"
     lines = [
         "rule cxx",
         f"  command = g++ {flags} $flags_extra -MMD -MF $out.d -c $in -o $out",

@@ -4,8 +4,12 @@
  * plus pack / unpack. Two ranks (parsec_amd.launch -n 2). With "gpu" as the
  * first argument the registered buffers live in GPU memory (hipMalloc) and the
  * one-sided transfers go GPU to GPU through HIP IPC; PARSEC_COMM_GPU selects
- * the device. Differences from the reference: r_tag of get / put is an AM tag
- * (the reference's MPI engine takes a callback address); values are checked. */
+ * the device; the GPU run then repeats both with one end in host memory (a
+ * device-to-host get and a host-to-device put: the engine must use the copy
+ * engines there, never a copy kernel on pageable memory). A non-contiguous
+ * registration (lower triangle) is refused. Differences from the reference:
+ * r_tag of get / put is an AM tag (the reference's MPI engine takes a callback
+ * address); values are checked. */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -27,12 +31,15 @@
 
 static volatile int counter = 0;
 static int my_rank, use_gpu = 0, bad = 0;
+/* where each end of the current phase lives (1: GPU memory) and the label */
+static int get_src_gpu, get_dst_gpu, put_src_gpu, put_dst_gpu;
+static const char* phase = "";
 /* callbacks run on the communication thread, concurrently with main(): counter
  * is reset before each barrier, never after it */
 
-static void* buf_alloc(size_t bytes) {
+static void* buf_alloc(size_t bytes, int gpu) {
 #ifdef CE_WITH_HIP
-    if (use_gpu) {
+    if (gpu) {
         void* p = NULL;
         /* a buffer object of its own (small hipMallocs can be carved out of a shared
          * one that a peer cannot attach): 64 MB, far above comm_ipc_min_alloc */
@@ -40,36 +47,40 @@ static void* buf_alloc(size_t bytes) {
         return p;
     }
 #endif
+    (void)gpu;
     return malloc(bytes);
 }
-static void buf_free(void* p) {
+static void buf_free(void* p, int gpu) {
 #ifdef CE_WITH_HIP
-    if (use_gpu) { hipFree(p); return; }
+    if (gpu) { hipFree(p); return; }
 #endif
+    (void)gpu;
     free(p);
 }
-static void buf_write(void* dst, const int* src, size_t n) {
+static void buf_write(void* dst, const int* src, size_t n, int gpu) {
 #ifdef CE_WITH_HIP
-    if (use_gpu) { hipMemcpy(dst, src, n * sizeof(int), hipMemcpyHostToDevice); return; }
+    if (gpu) { hipMemcpy(dst, src, n * sizeof(int), hipMemcpyHostToDevice); return; }
 #endif
+    (void)gpu;
     memcpy(dst, src, n * sizeof(int));
 }
-static void buf_read(int* dst, const void* src, size_t n) {
+static void buf_read(int* dst, const void* src, size_t n, int gpu) {
 #ifdef CE_WITH_HIP
-    if (use_gpu) { hipMemcpy(dst, src, n * sizeof(int), hipMemcpyDeviceToHost); return; }
+    if (gpu) { hipMemcpy(dst, src, n * sizeof(int), hipMemcpyDeviceToHost); return; }
 #endif
+    (void)gpu;
     memcpy(dst, src, n * sizeof(int));
 }
-static int reg(void* mem, size_t bytes, parsec_ce_mem_reg_handle_t* h, size_t* hs) {
-    if (use_gpu) return parsec_ce_mem_register_device(mem, bytes, parsec_ce_gpu_device_index(), h, hs);
+static int reg(void* mem, size_t bytes, int gpu, parsec_ce_mem_reg_handle_t* h, size_t* hs) {
+    if (gpu) return parsec_ce_mem_register_device(mem, bytes, parsec_ce_gpu_device_index(), h, hs);
     return parsec_ce.mem_register(mem, PARSEC_MEM_TYPE_CONTIGUOUS, 1, PARSEC_DATATYPE_NULL, bytes, h, hs);
 }
-static int check(const void* mem, int mult, const char* what) {
+static int check(const void* mem, int mult, const char* what, int gpu) {
     int* h = malloc(N * sizeof(int));
-    buf_read(h, mem, N);
+    buf_read(h, mem, N, gpu);
     int ok = 1;
     for (int i = 0; i < N; i++) if (h[i] != i * mult) { ok = 0; break; }
-    printf("[%d] %s %s\n", my_rank, what, ok ? "ok" : "WRONG");
+    printf("[%d] %s%s %s\n", my_rank, phase, what, ok ? "ok" : "WRONG");
     free(h);
     if (!ok) bad++;
     return ok;
@@ -100,19 +111,19 @@ static int get_end(parsec_comm_engine_t* ce, parsec_ce_mem_reg_handle_t lreg, pt
     ce->mem_retrieve(lreg, &mem, &dtt, &count);
     parsec_type_size(dtt, &bytes);
     if (size != N * sizeof(int) || bytes != (int)size) bad++;
-    check(mem, 1, "GET");
+    check(mem, 1, "GET", get_dst_gpu);
     ce->mem_unregister(&lreg);
-    buf_free(mem);
+    buf_free(mem, get_dst_gpu);
     counter++;
     return 1;
 }
 static int notify_get(parsec_comm_engine_t* ce, parsec_ce_tag_t tag, void* msg, size_t size, int src, void* cb_data) {
     (void)tag; (void)size; (void)cb_data;
     /* msg = rank 0's handle; register a receive buffer and pull */
-    void* rbuf = buf_alloc(N * sizeof(int));
+    void* rbuf = buf_alloc(N * sizeof(int), get_dst_gpu);
     parsec_ce_mem_reg_handle_t mine;
     size_t hs;
-    reg(rbuf, N * sizeof(int), &mine, &hs);
+    reg(rbuf, N * sizeof(int), get_dst_gpu, &mine, &hs);
     ce->get(ce, mine, 0, (parsec_ce_mem_reg_handle_t)msg, 0, 0, src, get_end, NULL, GET_END_ACK_TAG, msg, (size_t)ce->get_mem_handle_size());
     counter++;
     return 1;
@@ -122,7 +133,7 @@ static int get_end_ack(parsec_comm_engine_t* ce, parsec_ce_tag_t tag, void* msg,
     /* back on rank 0 with its own handle: release the source buffer */
     void* mem;
     ce->mem_retrieve((parsec_ce_mem_reg_handle_t)msg, &mem, NULL, NULL);
-    buf_free(mem);
+    buf_free(mem, get_src_gpu);
     counter++;
     return 1;
 }
@@ -132,10 +143,10 @@ static parsec_ce_mem_reg_handle_t put_src_handle; /* rank 0 */
 static int notify_put(parsec_comm_engine_t* ce, parsec_ce_tag_t tag, void* msg, size_t size, int src, void* cb_data) {
     (void)tag; (void)size; (void)cb_data;
     const int hs0 = ce->get_mem_handle_size();
-    void* rbuf = buf_alloc(N * sizeof(int));
+    void* rbuf = buf_alloc(N * sizeof(int), put_dst_gpu);
     parsec_ce_mem_reg_handle_t mine;
     size_t hs;
-    reg(rbuf, N * sizeof(int), &mine, &hs);
+    reg(rbuf, N * sizeof(int), put_dst_gpu, &mine, &hs);
     char* reply = malloc(2 * (size_t)hs0);
     memcpy(reply, msg, (size_t)hs0);                  /* 0's handle */
     memcpy(reply + hs0, mine, (size_t)hs0);           /* 1's handle */
@@ -151,7 +162,7 @@ static int put_end(parsec_comm_engine_t* ce, parsec_ce_mem_reg_handle_t lreg, pt
     void* mem;
     ce->mem_retrieve(lreg, &mem, NULL, NULL);
     ce->mem_unregister(&put_src_handle);
-    buf_free(mem);
+    buf_free(mem, put_src_gpu);
     counter++;
     return 1;
 }
@@ -168,8 +179,8 @@ static int put_end_ack(parsec_comm_engine_t* ce, parsec_ce_tag_t tag, void* msg,
     void* mem;
     parsec_ce_mem_reg_handle_t h = (parsec_ce_mem_reg_handle_t)msg;
     ce->mem_retrieve(h, &mem, NULL, NULL);
-    check(mem, 2, "PUT");
-    buf_free(mem);
+    check(mem, 2, "PUT", put_dst_gpu);
+    buf_free(mem, put_dst_gpu);
     counter++;
     return 1;
 }
@@ -209,40 +220,49 @@ int main(int argc, char** argv) {
     counter = 0; /* before the barrier: the peer's next messages may arrive right after it */
     ce->sync(ce);
 
-    /* GET: 0 registers, tells 1; 1 pulls (get_end) and acknowledges (get_end_ack on 0) */
-    if (my_rank == 0) {
-        int* h = malloc(N * sizeof(int));
-        for (int i = 0; i < N; i++) h[i] = i;
-        void* sbuf = buf_alloc(N * sizeof(int));
-        buf_write(sbuf, h, N);
-        free(h);
-        parsec_ce_mem_reg_handle_t mine;
-        size_t hs;
-        reg(sbuf, N * sizeof(int), &mine, &hs);
-        ce->send_am(ce, NOTIFY_GET_TAG, 1, mine, hs);
-        wait_for(1);
-        ce->mem_unregister(&mine);
-    } else {
-        wait_for(2);
-    }
-    counter = 0;
-    ce->sync(ce);
+    /* every end in the requested memory, then (GPU runs) one end on the host */
+    for (int round = 0; round < (use_gpu ? 2 : 1); round++) {
+        get_src_gpu = use_gpu;
+        get_dst_gpu = use_gpu && round == 0;
+        put_src_gpu = use_gpu && round == 0;
+        put_dst_gpu = use_gpu;
+        phase = round ? "MIXED " : "";
+        /* GET: 0 registers, tells 1; 1 pulls (get_end) and acknowledges (get_end_ack on 0) */
+        if (my_rank == 0) {
+            int* h = malloc(N * sizeof(int));
+            for (int i = 0; i < N; i++) h[i] = i;
+            void* sbuf = buf_alloc(N * sizeof(int), get_src_gpu);
+            buf_write(sbuf, h, N, get_src_gpu);
+            free(h);
+            parsec_ce_mem_reg_handle_t mine;
+            size_t hs;
+            reg(sbuf, N * sizeof(int), get_src_gpu, &mine, &hs);
+            ce->send_am(ce, NOTIFY_GET_TAG, 1, mine, hs);
+            wait_for(1);
+            ce->mem_unregister(&mine);
+        } else {
+            wait_for(2);
+        }
+        counter = 0;
+        ce->sync(ce);
 
-    /* PUT: 0 tells 1, 1 answers with both handles, 0 pushes (put_end), 1 checks (put_end_ack) */
-    if (my_rank == 0) {
-        int* h = malloc(N * sizeof(int));
-        for (int i = 0; i < N; i++) h[i] = 2 * i;
-        void* sbuf = buf_alloc(N * sizeof(int));
-        buf_write(sbuf, h, N);
-        free(h);
-        size_t hs;
-        reg(sbuf, N * sizeof(int), &put_src_handle, &hs);
-        ce->send_am(ce, NOTIFY_PUT_TAG, 1, put_src_handle, hs);
-        wait_for(2);
-    } else {
-        wait_for(2);
+        /* PUT: 0 tells 1, 1 answers with both handles, 0 pushes (put_end), 1 checks (put_end_ack) */
+        if (my_rank == 0) {
+            int* h = malloc(N * sizeof(int));
+            for (int i = 0; i < N; i++) h[i] = 2 * i;
+            void* sbuf = buf_alloc(N * sizeof(int), put_src_gpu);
+            buf_write(sbuf, h, N, put_src_gpu);
+            free(h);
+            size_t hs;
+            reg(sbuf, N * sizeof(int), put_src_gpu, &put_src_handle, &hs);
+            ce->send_am(ce, NOTIFY_PUT_TAG, 1, put_src_handle, hs);
+            wait_for(2);
+        } else {
+            wait_for(2);
+        }
+        counter = 0;
+        ce->sync(ce);
     }
-    ce->sync(ce);
 
     /* pack / unpack: the lower triangle of a 4 x 4 column-major matrix */
     {
@@ -261,6 +281,19 @@ int main(int argc, char** argv) {
                 if (b[r + 4 * c] != (r >= c ? a[r + 4 * c] : 0.0)) bad++;
         free(packed);
         (void)dbl;
+        /* the engine moves byte ranges: a registration whose layout is not its
+         * packed image must be refused, a contiguous one accepted */
+        parsec_ce_mem_reg_handle_t h;
+        size_t hs;
+        if (ce->mem_register(a, PARSEC_MEM_TYPE_NONCONTIGUOUS, 1, lower, sizeof(a), &h, &hs) == 0) {
+            printf("[%d] non-contiguous registration accepted\n", my_rank);
+            bad++;
+            ce->mem_unregister(&h);
+        }
+        parsec_datatype_t four;
+        parsec_type_create_contiguous(4, parsec_datatype_double_t, &four);
+        if (ce->mem_register(a, PARSEC_MEM_TYPE_NONCONTIGUOUS, 4, four, sizeof(a), &h, &hs) != 0) bad++;
+        else ce->mem_unregister(&h);
     }
     printf("[%d] ce %s (can_serve %d)\n", my_rank, bad ? "FAILED" : "ok", ce->can_serve(ce));
     ce->sync(ce);

@@ -1,6 +1,7 @@
 """Worker: one rank of a multi-process GPU run where every rank drives GPU 0 and
-remote tiles move through the device data plane (HIP IPC: the receiver maps the
-sender's HBM allocation and pulls with an async D2D copy). Used by
+remote tiles move through the communication engine's one-sided get (device
+plane: the engine maps the sender's HBM allocation through HIP IPC and pulls it
+with an async copy). Used by
 tests/test_multirank_gpu.py; each rank validates what it owns.
 
 argv: case rank size job [case args...]
@@ -81,15 +82,17 @@ def case_dpotrf(pa, torch, rank, size, job, N, nb, P, Q):
             print(f"rank {rank} rep {rep} bad tiles {bad[:12]} ({len(bad)} total)", flush=True)
         worst = max(worst, err)
     stats = [d for d in pa.devices() if d["type"] == pa.DEV_HIP][0]
-    plane = pa.comm_device_plane()
+    plane, status = pa.comm_device_plane(), pa.comm_plane_status()
+    cs = pa.comm_stats()
     ctx.fini()
     pa.comm_fini()
     worst /= float(Lref.abs().max())
     want = os.environ.get("EXPECT_PLANE")
     if want and plane != want:
-        print(f"rank {rank}: device plane {plane}, expected {want}", flush=True)
+        print(f"rank {rank}: device plane {plane} (start-up status {status}), expected {want}", flush=True)
         return False
-    print(f"rank {rank} dpotrf err {worst:.3e} info {info_v} gpu_tasks {stats['executed_tasks']} plane {plane} bad_reps {nbad}/{repeat}", flush=True)
+    print(f"rank {rank} dpotrf err {worst:.3e} info {info_v} gpu_tasks {stats['executed_tasks']} plane {plane} "
+          f"gets ipc {cs['get_ipc']} fragments {cs['get_fragments']} bad_reps {nbad}/{repeat}", flush=True)
     return worst < 1e-12 and info_v == 0 and stats["executed_tasks"] > 0
 
 

@@ -1,7 +1,8 @@
 """Multi-rank runs of the distributed device data plane on one MI355X: 2, 4 and
 8 processes (one per "GPU" of a P x Q grid) all drive GPU 0, and every remote
-tile moves HBM -> HBM through HIP IPC (the receiver maps the sender's
-allocation and pulls it on a per-peer stream; IPC_DONE releases the source).
+tile moves HBM -> HBM through the communication engine's one-sided get (the
+engine maps the sender's allocation through HIP IPC and pulls it; the get's
+PUT_END notification releases the source).
 Reference: collections/*:mp and dsl/* :mp tests run with mpiexec -n 2|4|8
 (tests/collections/Testings.cmake:5-6, remote_dep.c:454-591).
 
@@ -59,23 +60,25 @@ def test_dpotrf_multirank_ipc(pa, nranks, P, Q):
     outs = _run("dpotrf", nranks, 8192, 512, P, Q, env_extra={"EXPECT_PLANE": "ipc"})
     # every rank's warnings in the message: the rank whose IPC start-up failed
     # names its own error code
-    notes = "\n".join(f"[{r}] {l}" for r, (_, o) in enumerate(outs) for l in o.splitlines() if "warning" in l or "error" in l.lower())
+    notes = "\n".join(f"[{r}] {l}" for r, (_, o) in enumerate(outs) for l in o.splitlines() if "warning" in l or "error" in l.lower() or "status" in l)
     for rc, out in outs:
         assert rc == 0, out + "\n" + notes
+    # the remote tiles really moved GPU to GPU through the engine's IPC route
+    gets = [int(o.strip().splitlines()[-1].split(" gets ipc ")[-1].split()[0]) for _, o in outs]
+    assert sum(gets) > 0, gets
 
 
-def test_dpotrf_rccl_plane_request(pa):
-    """comm_device_plane=rccl with two ranks on ONE GPU: RCCL refuses two ranks of
-    a communicator on the same device, so the engine must report that and fall
-    back to the host-staged plane with a correct result (the RCCL plane is for
-    ranks on distinct GPUs; IPC is the default either way)."""
+def test_dpotrf_host_plane_request(pa):
+    """comm_device_plane=host: every rank stages device tiles through host
+    fragments (the route a failed IPC start-up falls back to) and the factor is
+    still right; no payload takes the IPC route."""
     _gpu()
-    outs = _run("dpotrf", 2, 2048, 256, 2, 1, env_extra={"PARSEC_MCA_comm_device_plane": "rccl"})
+    outs = _run("dpotrf", 2, 2048, 256, 2, 1, env_extra={"PARSEC_MCA_comm_device_plane": "host", "EXPECT_PLANE": "host"})
     for rc, out in outs:
         assert rc == 0, out
-    planes = {o.strip().splitlines()[-1].split(" plane ")[-1].split()[0] for _, o in outs}
-    print("rccl request ->", planes)
-    assert planes <= {"rccl", "host"}
+    last = [o.strip().splitlines()[-1] for _, o in outs]
+    assert all(" gets ipc 0 " in l for l in last), last
+    assert sum(int(l.split(" fragments ")[-1].split()[0]) for l in last) > 0, last
 
 
 def test_dgeqrf_two_ranks_ipc(pa):
@@ -141,6 +144,7 @@ def test_comm_engine_c_program_gpu_memory(tmp_path, pa):
     assert rc == 0, outs
     text = "".join(o for o, _ in outs)
     assert text.count("ce ok") == 2 and "[1] GET ok" in text and "[1] PUT ok" in text, text
+    assert "[1] MIXED GET ok" in text and "[1] MIXED PUT ok" in text, text
 
 
 def test_headline_tile_size_8_ranks_shared_gpu(pa):
