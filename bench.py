@@ -107,7 +107,9 @@ def main():
     ap.add_argument("--taskpool", choices=["ir", "jdf"], default="jdf",
                     help="jdf (default): the DAG compiled by parsec-ptgpp from csrc/algos/jdf/dpotrf_L.jdf; ir: the same DAG built by hand in C++ (csrc/algos/dpotrf.cpp, a test fixture)")
     ap.add_argument("--share-gpu", action="store_true",
-                    help="validation mode: every rank uses GPU 0 (torch gloo, shm data plane instead of RCCL)")
+                    help="validation mode: every rank uses GPU 0 (torch gloo for the bench's own barriers; the runtime's IPC device plane as always)")
+    ap.add_argument("--allow-host-plane", action="store_true",
+                    help="multi-rank: accept ranks whose device plane fell back to host staging (default: such a run exits non-zero)")
     args = ap.parse_args()
 
     import torch
@@ -141,6 +143,20 @@ def main():
         if rc != 0:
             raise RuntimeError(f"comm_init failed rc={rc}")
     _stage("comm up")
+    # every rank's device plane (ipc: remote tiles move GPU -> GPU over xGMI;
+    # host: staged through host memory), reported in the JSON line; a multi-rank
+    # run on the host plane is not the headline path and fails loudly
+    planes = [{"rank": 0, "plane": "none", "status": 0}]
+    if world > 1:
+        code = {"ipc": 1, "host": 0}.get(pa.comm_device_plane(), -1)
+        mine = torch.tensor([code, pa.comm_plane_status()], dtype=torch.int64, device="cpu" if args.share_gpu else "cuda")
+        got = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(got, mine)
+        planes = [{"rank": r, "plane": {1: "ipc", 0: "host"}.get(int(g[0]), "?"), "status": int(g[1])} for r, g in enumerate(got)]
+        if any(p["plane"] != "ipc" for p in planes) and not args.allow_host_plane:
+            if rank == 0:
+                print(f"error: device plane is not ipc on every rank: {planes}", file=sys.stderr, flush=True)
+            raise SystemExit(3)
     ctx = pa.init(args.cores)
     _stage("context up")
     gpu = pa.first_gpu_device_index()
@@ -278,6 +294,7 @@ def main():
             "config": {"model": "tiled DPOTRF lower (PTG, ptgpp-compiled dpotrf_L.jdf)" if args.taskpool == "jdf" else "tiled DPOTRF lower (PTG, hand-built C++ DAG)", "N": N, "nb": nb, "global_batch": 1, "seq_len": N,
                        "parallelism": f"2D block-cyclic P{P}xQ{Q}, 1 process/GPU", "threads_per_rank": args.cores},
         }
+        out["device_plane"] = planes
         if check is not None:
             out["max_rel_error_vs_torch_cholesky"] = check
         if args.share_gpu:

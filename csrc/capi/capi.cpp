@@ -20,6 +20,7 @@
 #include "../device/device.hpp"
 #include "../dtd/dtd.hpp"
 #include "../algos/linalg.hpp"
+#include "../algos/ptg_ir.hpp"
 #include "../prof/profiling.hpp"
 // after the runtime headers: the C API defines PASSED_BY_REF & co. as macros
 #include "../../include/parsec.h"
@@ -155,6 +156,65 @@ parsec_data_key_t bc_data_key(parsec_data_collection_t* dc, ...) {
 uint32_t bc_rank_of_key(parsec_data_collection_t* dc, parsec_data_key_t k) { return impl_of(dc)->rank_of_key(k); }
 int32_t bc_vpid_of_key(parsec_data_collection_t* dc, parsec_data_key_t k) { return impl_of(dc)->vpid_of_key(k); }
 parsec_data_t* bc_data_of_key(parsec_data_collection_t* dc, parsec_data_key_t k) { return impl_of(dc)->data_of_key(k); }
+// one index (vectors)
+uint32_t v_rank_of(parsec_data_collection_t* dc, ...) {
+  va_list ap;
+  va_start(ap, dc);
+  int64_t idx[1] = {va_arg(ap, int)};
+  va_end(ap);
+  return impl_of(dc)->rank_of(idx, 1);
+}
+int32_t v_vpid_of(parsec_data_collection_t* dc, ...) {
+  va_list ap;
+  va_start(ap, dc);
+  int64_t idx[1] = {va_arg(ap, int)};
+  va_end(ap);
+  return impl_of(dc)->vpid_of(idx, 1);
+}
+parsec_data_t* v_data_of(parsec_data_collection_t* dc, ...) {
+  va_list ap;
+  va_start(ap, dc);
+  int64_t idx[1] = {va_arg(ap, int)};
+  va_end(ap);
+  return impl_of(dc)->data_of(idx, 1);
+}
+parsec_data_key_t v_data_key(parsec_data_collection_t* dc, ...) {
+  va_list ap;
+  va_start(ap, dc);
+  int64_t idx[1] = {va_arg(ap, int)};
+  va_end(ap);
+  return impl_of(dc)->data_key(idx, 1);
+}
+// hash distributions: the one argument IS the key (reference hash_datadist.c)
+uint32_t h_rank_of(parsec_data_collection_t* dc, ...) {
+  va_list ap;
+  va_start(ap, dc);
+  const parsec_data_key_t k = va_arg(ap, parsec_data_key_t);
+  va_end(ap);
+  return impl_of(dc)->rank_of_key(k);
+}
+int32_t h_vpid_of(parsec_data_collection_t* dc, ...) {
+  va_list ap;
+  va_start(ap, dc);
+  const parsec_data_key_t k = va_arg(ap, parsec_data_key_t);
+  va_end(ap);
+  return impl_of(dc)->vpid_of_key(k);
+}
+parsec_data_t* h_data_of(parsec_data_collection_t* dc, ...) {
+  va_list ap;
+  va_start(ap, dc);
+  const parsec_data_key_t k = va_arg(ap, parsec_data_key_t);
+  va_end(ap);
+  return impl_of(dc)->data_of_key(k);
+}
+parsec_data_key_t h_data_key(parsec_data_collection_t* dc, ...) {
+  (void)dc;
+  va_list ap;
+  va_start(ap, dc);
+  const parsec_data_key_t k = va_arg(ap, parsec_data_key_t);
+  va_end(ap);
+  return k;
+}
 
 // ----------------------------------------------------------------- DTD
 thread_local GpuExecContext* t_gpu_ctx = nullptr;
@@ -223,6 +283,50 @@ dtd::DtdTaskpool* current_dtd() {
 thread_local ProfilingStream* t_prof = nullptr;
 
 }  // namespace
+
+template <class Base, class CType>
+struct LazyStorage : Base {
+  CType* c = nullptr;
+  std::mutex sync_m;
+  std::atomic<bool> synced{false};
+  void sync() {
+    if (synced.load(std::memory_order_acquire)) return;
+    std::lock_guard<std::mutex> g(sync_m);
+    if (synced.load(std::memory_order_relaxed)) return;
+    if (!this->mat && c->mat) this->allocate_storage(c->mat);
+    if (this->mat) synced.store(true, std::memory_order_release);
+  }
+  Data* data_of(const int64_t* idx, int n) override { sync(); return Base::data_of(idx, n); }
+  Data* data_of_key(uint64_t key) override { sync(); return Base::data_of_key(key); }
+};
+
+struct CTabular : TabularMatrix {
+  parsec_matrix_tabular_t* c = nullptr;
+  // element data pointers of the local tiles, filled once the storage exists
+  void publish() {
+    if (!c->tiles_table || !mat) return;
+    for (int k = 0; k < c->tiles_table->nbelem && k < (int)local_map.size(); ++k)
+      c->tiles_table->elems[k].data = local_map[k] >= 0 ? static_cast<char*>(mat) + (size_t)local_map[k] * bsiz * elem_size : nullptr;
+  }
+  void apply_table(const parsec_two_dim_td_table_t* t) {
+    std::vector<int> ranks((size_t)(lmt * lnt), 0);
+    for (int k = 0; t && k < t->nbelem && k < (int)ranks.size(); ++k) ranks[k] = (int)t->elems[k].rank;
+    const int64_t keep_m = m, keep_n = n, keep_i = i, keep_j = j;
+    init_tab(mtype, (int)myrank, (int)nodes, mb, nb, lm, ln, ranks);
+    i = keep_i; j = keep_j; m = keep_m; n = keep_n;
+    mt = (i % mb + m + mb - 1) / mb; nt = (j % nb + n + nb - 1) / nb;
+    for (int k = 0; t && k < t->nbelem && k < (int)table_vp.size(); ++k) table_vp[k] = t->elems[k].vpid;
+    if (mat) { if (owns_storage) free_storage(); }
+    allocate_storage(nullptr);
+  }
+  void free_storage() {
+    for (Data*& d : tiles) if (d) { data_destroy(d); d = nullptr; }
+    tiles.clear();
+    if (owns_storage && mat) parsec_data_free(mat);
+    mat = nullptr;
+    owns_storage = false;
+  }
+};
 
 extern "C" {
 
@@ -587,6 +691,141 @@ void parsec_matrix_block_cyclic_init(parsec_matrix_block_cyclic_t* dc, parsec_ma
   t->nb_local_tiles = (int)bc->nb_local_tiles;
   parsec_grid_2Dcyclic_init(&dc->grid, myrank, p, q, kp, kq, ip, jq);
 }
+// ---- the other tiled collections of the reference's C API
+// Storage given by the user through the C struct's `mat` after init (as with
+// parsec_matrix_block_cyclic_t) is picked up on first use.
+static void fill_tiled(parsec_tiled_matrix_t* t, const TiledMatrix* tm, parsec_matrix_type_t mtype, int64_t llm, int64_t lln) {
+  t->mtype = mtype;
+  t->storage = PARSEC_MATRIX_TILE;
+  t->mb = (int)tm->mb; t->nb = (int)tm->nb; t->bsiz = (int)tm->bsiz;
+  t->lm = (int)tm->lm; t->ln = (int)tm->ln; t->lmt = (int)tm->lmt; t->lnt = (int)tm->lnt;
+  t->i = (int)tm->i; t->j = (int)tm->j; t->m = (int)tm->m; t->n = (int)tm->n; t->mt = (int)tm->mt; t->nt = (int)tm->nt;
+  t->llm = (int)llm; t->lln = (int)lln;
+  t->nb_local_tiles = (int)tm->nb_local_tiles;
+}
+static void set_c_callbacks(parsec_data_collection_t* d, DataCollection* impl, int nb_indices) {
+  d->myrank = impl->myrank;
+  d->nodes = impl->nodes;
+  d->rank_of = nb_indices == 1 ? v_rank_of : bc_rank_of;
+  d->vpid_of = nb_indices == 1 ? v_vpid_of : bc_vpid_of;
+  d->data_of = nb_indices == 1 ? v_data_of : bc_data_of;
+  d->data_key = nb_indices == 1 ? v_data_key : bc_data_key;
+  d->rank_of_key = bc_rank_of_key;
+  d->vpid_of_key = bc_vpid_of_key;
+  d->data_of_key = bc_data_of_key;
+  d->nb_indices = nb_indices;
+  d->impl = impl;
+}
+
+void parsec_matrix_sym_block_cyclic_init(parsec_matrix_sym_block_cyclic_t* dc, parsec_matrix_type_t mtype, int myrank, int mb, int nb, int lm, int ln, int i,
+                                         int j, int m, int n, int p, int q, parsec_matrix_uplo_t uplo) {
+  std::memset(dc, 0, sizeof(*dc));
+  auto* sc = new LazyStorage<SymBlockCyclic, parsec_matrix_sym_block_cyclic_t>();
+  sc->c = dc;
+  sc->init_sym((int)mtype, myrank, mb, nb, lm, ln, i, j, m, n, p, q, uplo == PARSEC_MATRIX_UPPER ? MATRIX_UPPER : MATRIX_LOWER);
+  set_c_callbacks(&dc->super.super, sc, 2);
+  fill_tiled(&dc->super, sc, mtype, sc->llm_tiles * mb, sc->lln_tiles * nb);
+  dc->uplo = uplo;
+  parsec_grid_2Dcyclic_init(&dc->grid, myrank, p, q, 1, 1, 0, 0);
+}
+
+
+static parsec_two_dim_td_table_t* new_td_table(int n) {
+  auto* t = static_cast<parsec_two_dim_td_table_t*>(std::calloc(1, sizeof(parsec_two_dim_td_table_t) + sizeof(parsec_two_dim_td_table_elem_t) * (size_t)std::max(0, n - 1)));
+  t->nbelem = n;
+  return t;
+}
+static void tabular_refresh(parsec_matrix_tabular_t* dc) {
+  auto* tc = static_cast<CTabular*>(static_cast<DataCollection*>(dc->super.super.impl));
+  tc->apply_table(dc->tiles_table);
+  int pos = 0;
+  for (int k = 0; dc->tiles_table && k < dc->tiles_table->nbelem; ++k) dc->tiles_table->elems[k].pos = tc->local_map.size() > (size_t)k && tc->local_map[k] >= 0 ? pos++ : -1;
+  tc->publish();
+  fill_tiled(&dc->super, tc, dc->super.mtype, 0, 0);
+}
+void parsec_matrix_tabular_init(parsec_matrix_tabular_t* dc, parsec_matrix_type_t mtype, unsigned int nodes, unsigned int myrank, unsigned int mb, unsigned int nb,
+                                unsigned int lm, unsigned int ln, unsigned int i, unsigned int j, unsigned int m, unsigned int n,
+                                parsec_two_dim_td_table_t* table) {
+  std::memset(dc, 0, sizeof(*dc));
+  auto* tc = new CTabular();
+  tc->c = dc;
+  tc->init_base((int)mtype, (int)myrank, (int)nodes, mb, nb, lm, ln, i, j, m, n);
+  set_c_callbacks(&dc->super.super, tc, 2);
+  dc->super.mtype = mtype;
+  if (table) parsec_matrix_tabular_set_table(dc, table);
+  else tabular_refresh(dc);
+}
+void parsec_matrix_tabular_set_table(parsec_matrix_tabular_t* dc, parsec_two_dim_td_table_t* table) {
+  if (dc->tiles_table && !dc->user_table && dc->tiles_table != table) std::free(dc->tiles_table);
+  dc->tiles_table = table;
+  dc->user_table = 0;
+  tabular_refresh(dc);
+}
+void parsec_matrix_tabular_set_user_table(parsec_matrix_tabular_t* dc, parsec_two_dim_td_table_t* table) {
+  if (dc->tiles_table && !dc->user_table && dc->tiles_table != table) std::free(dc->tiles_table);
+  dc->tiles_table = table;
+  dc->user_table = 1;
+  tabular_refresh(dc);
+}
+void parsec_matrix_tabular_set_random_table(parsec_matrix_tabular_t* dc, unsigned int seed) {
+  const int n = dc->super.lmt * dc->super.lnt;
+  parsec_two_dim_td_table_t* t = new_td_table(n);
+  uint64_t x = 0x9E3779B97F4A7C15ull ^ seed;
+  for (int k = 0; k < n; ++k) {
+    x ^= x << 13; x ^= x >> 7; x ^= x << 17;  // xorshift: the same table on every rank
+    t->elems[k].rank = (uint32_t)(x % std::max<uint32_t>(1, dc->super.super.nodes));
+    t->elems[k].vpid = 0;
+  }
+  parsec_matrix_tabular_set_table(dc, t);
+}
+void parsec_matrix_tabular_destroy(parsec_matrix_tabular_t* dc) {
+  if (auto* tc = dynamic_cast<CTabular*>(static_cast<DataCollection*>(dc->super.super.impl))) tc->free_storage();
+  if (dc->tiles_table && !dc->user_table) std::free(dc->tiles_table);
+  dc->tiles_table = nullptr;
+  parsec_data_collection_destroy(&dc->super.super);
+}
+
+void parsec_vector_two_dim_cyclic_init(parsec_vector_two_dim_cyclic_t* vdesc, parsec_matrix_type_t mtype, enum parsec_vector_two_dim_cyclic_distrib_t distrib, int myrank,
+                                       int mb, int lm, int i, int m, int P, int Q) {
+  std::memset(vdesc, 0, sizeof(*vdesc));
+  auto* vc = new LazyStorage<VectorCyclic, parsec_vector_two_dim_cyclic_t>();
+  vc->c = vdesc;
+  vc->init_vec((int)mtype, myrank, std::max(1, P) * std::max(1, Q), mb, lm, (int)distrib, P, Q);
+  // the window [i, i + m) of the vector (tile-aligned start, as the reference assumes)
+  vc->i = i;
+  vc->m = m;
+  vc->mt = (i % mb + m + mb - 1) / mb;
+  set_c_callbacks(&vdesc->super.super, vc, 1);
+  fill_tiled(&vdesc->super, vc, mtype, vc->nb_local_tiles * mb, 1);
+  vdesc->distrib = distrib;
+  int a = std::max(1, P), b = std::max(1, Q);
+  while (b) { const int r = a % b; a = b; b = r; }
+  vdesc->lcm = std::max(1, P) / a * std::max(1, Q);  // diagonal processes: lcm(P, Q)
+  parsec_grid_2Dcyclic_init(&vdesc->grid, myrank, P, Q, 1, 1, 0, 0);
+}
+
+parsec_hash_datadist_t* parsec_hash_datadist_create(int np, int myrank) {
+  auto* d = static_cast<parsec_hash_datadist_t*>(std::calloc(1, sizeof(parsec_hash_datadist_t)));
+  auto* h = new HashCollection();
+  h->nodes = (uint32_t)np;
+  h->myrank = (uint32_t)myrank;
+  h->key_base = "hash";
+  set_c_callbacks(&d->super, h, 1);
+  d->super.rank_of = h_rank_of;
+  d->super.vpid_of = h_vpid_of;
+  d->super.data_of = h_data_of;
+  d->super.data_key = h_data_key;
+  return d;
+}
+void parsec_hash_datadist_destroy(parsec_hash_datadist_t* d) {
+  if (!d) return;
+  parsec_data_collection_destroy(&d->super);
+  std::free(d);
+}
+void parsec_hash_datadist_set_data(parsec_hash_datadist_t* d, void* actual_data, parsec_data_key_t key, int vpid, int rank, uint32_t size) {
+  static_cast<HashCollection*>(impl_of(&d->super))->set_entry(key, (uint32_t)rank, vpid, actual_data, size);
+}
+
 void parsec_tiled_matrix_destroy(parsec_tiled_matrix_t* tdesc) { parsec_data_collection_destroy(&tdesc->super); }
 parsec_data_key_t parsec_tiled_matrix_data_key(parsec_tiled_matrix_t* tdesc, int m, int n) {
   int64_t idx[2] = {m, n};
@@ -661,6 +900,87 @@ int parsec_redistribute_dtd(parsec_context_t* parsec, parsec_tiled_matrix_t* sou
   return algos::redistribute(parsec, tm_of(source), tm_of(target), size_row, size_col, disi_source, disj_source, disi_target, disj_target) == 0
              ? PARSEC_SUCCESS
              : PARSEC_ERROR;
+}
+// Broadcast of one datum (reference data_dist/matrix/broadcast.jdf): the
+// collection of positions 0 (root) .. sz (ranks[k - 1]) all resolving to *data,
+// SEND(0) on the root and RECV(1 .. sz) on the listed ranks; each RECV's flow
+// goes back into its rank's *data.
+parsec_taskpool_t* parsec_broadcast_New(parsec_data_t** data, int32_t myrank, int32_t world, int root, const int32_t* ranks, int sz, parsec_taskpool_t* master_tp,
+                                        parsec_datatype_t stype, parsec_datatype_t rtype) {
+  using namespace algos::ir;
+  (void)stype;
+  if (!data || sz < 0 || (sz > 0 && !ranks)) return nullptr;
+  std::vector<int32_t> rk(ranks, ranks + sz);
+  const bool listed = std::find(rk.begin(), rk.end(), myrank) != rk.end() && myrank != root;
+  auto* dc = new CallbackCollection();
+  dc->myrank = (uint32_t)myrank;
+  dc->nodes = (uint32_t)world;
+  dc->key_base = "bcast";
+  void* owned = nullptr;
+  if (listed && !*data) {
+    // a receiver without a datum: one of the receive type's extent (the taskpool's)
+    const size_t bytes = (size_t)std::max<int64_t>(1, type_of(rtype).extent_bytes());
+    owned = parsec_data_allocate(bytes);
+    std::memset(owned, 0, bytes);
+    *data = data_create(nullptr, dc, 1, owned, bytes);
+  }
+  Data* mine = *data;
+  dc->f_rank_of = [rk, root](const int64_t* idx, int) { return (uint32_t)(idx[0] == 0 ? root : rk[(size_t)idx[0] - 1]); };
+  dc->f_rank_of_key = [rk, root](uint64_t k) { return (uint32_t)(k == 0 ? root : rk[(size_t)k - 1]); };
+  dc->f_data_key = [](const int64_t* idx, int) { return (uint64_t)idx[0]; };
+  dc->f_data_of = [mine](const int64_t*, int) { return mine; };
+  dc->f_data_of_key = [mine](uint64_t) { return mine; };
+  auto* tp = new ptg::PtgTaskpool();
+  tp->taskpool_name = "broadcast";
+  {
+    TaskClassDef d;
+    d.name = "send";
+    d.locals = {range_local("k", cst(0), cst(0))};
+    d.affinity_dc = [dc](const Taskpool*) { return (DataCollection*)dc; };
+    d.affinity_args = {loc(0)};
+    FlowDef A;
+    A.name = "A"; A.access = FLOW_READ;
+    A.in = {always(data1(dc, loc(0)))};
+    if (sz > 0) A.out = {always(task("recv", "A", {rng(cst(1), cst(sz))}))};
+    d.flows = {A};
+    BodyDef b;
+    b.type = DEV_CPU;
+    b.cpu = [](ExecutionStream*, Task*) { return HOOK_DONE; };
+    d.bodies = {b};
+    tp->add_task_class(std::move(d));
+  }
+  if (sz > 0) {
+    TaskClassDef d;
+    d.name = "recv";
+    d.locals = {range_local("k", cst(1), cst(sz))};
+    d.affinity_dc = [dc](const Taskpool*) { return (DataCollection*)dc; };
+    d.affinity_args = {loc(0)};
+    FlowDef A;
+    A.name = "A"; A.access = FLOW_RW;
+    A.in = {always(task("send", "A", {val(cst(0))}))};
+    A.out = {always(data1(dc, loc(0)))};
+    d.flows = {A};
+    BodyDef b;
+    b.type = DEV_CPU;
+    b.cpu = [](ExecutionStream*, Task*) { return HOOK_DONE; };
+    d.bodies = {b};
+    tp->add_task_class(std::move(d));
+  }
+  tp->finalize();
+  if (master_tp && master_tp->tdm) master_tp->tdm->taskpool_addto_runtime_actions(master_tp, 1);
+  tp->on_complete = [master_tp](Taskpool*) {
+    if (master_tp && master_tp->tdm) master_tp->tdm->taskpool_addto_runtime_actions(master_tp, -1);
+    return 0;
+  };
+  tp->destructor_hook = [dc, owned, data, mine] {
+    if (owned) {
+      if (*data == mine) *data = nullptr;
+      data_destroy(mine);
+      parsec_data_free(owned);
+    }
+    delete dc;
+  };
+  return tp;
 }
 parsec_taskpool_t* parsec_diag_band_to_rect_New(parsec_tiled_matrix_t* A, parsec_tiled_matrix_t* B, int mt, int nt, int mb, int nb, size_t elem_size) {
   return algos::diag_band_to_rect_new(tm_of(A), tm_of(B), mt, nt, mb, nb, elem_size);

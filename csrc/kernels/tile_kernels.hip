@@ -27,7 +27,6 @@
 #include "../device/device.hpp"
 
 namespace parsec {
-bool vendor_dgemm_batched(const GemmDesc* d, int n, hipStream_t stream);  // vendor_blas.cpp
 namespace kern {
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
@@ -743,15 +742,13 @@ static int gemm_chunk_size(const GemmDesc* d, int n) {
   return best_fill >= 0.0 ? best : cap;
 }
 
-// Group descriptors by (transA, transB): one grouped launch per combination;
-// a large uniform plain group goes to the vendor batched DGEMM instead
-// (csrc/device/vendor_blas.cpp).
+// Group descriptors by (transA, transB): one grouped launch per combination
+// (the vendor library is an A/B reference only: scripts/kbench_gemm_vs_vendor.py).
 void launch_gemm_batch(const GemmDesc* descs, int n, hipStream_t stream) {
   gemm_policy_init();
   std::vector<GemmDesc> g[4];
   for (int i = 0; i < n; ++i) g[(descs[i].transA ? 2 : 0) | (descs[i].transB ? 1 : 0)].push_back(descs[i]);
   for (auto& v : g) {
-    if (!v.empty() && vendor_dgemm_batched(v.data(), (int)v.size(), stream)) continue;
     for (size_t s = 0; s < v.size();) {
       const int c = gemm_chunk_size(v.data() + s, (int)(v.size() - s));
       launch_gemm_chunk(v.data() + s, c, stream);

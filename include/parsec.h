@@ -239,6 +239,71 @@ typedef struct parsec_matrix_block_cyclic_s {
 
 void parsec_matrix_block_cyclic_init(parsec_matrix_block_cyclic_t* dc, parsec_matrix_type_t mtype, parsec_matrix_storage_t storage, int myrank, int mb, int nb, int lm, int ln,
                                      int i, int j, int m, int n, int p, int q, int kp, int kq, int ip, int jq);
+/* symmetric 2D block-cyclic: only the `uplo` triangle of tiles exists; a tile of
+ * the other triangle maps to its mirror's owner (reference
+ * data_dist/matrix/sym_two_dim_rectangle_cyclic.c:228) */
+typedef struct parsec_matrix_sym_block_cyclic_s {
+  parsec_tiled_matrix_t super;
+  parsec_grid_2Dcyclic_t grid;
+  void* mat; /* local tile storage (set by the user or parsec_data_allocate) */
+  parsec_matrix_uplo_t uplo;
+} parsec_matrix_sym_block_cyclic_t;
+void parsec_matrix_sym_block_cyclic_init(parsec_matrix_sym_block_cyclic_t* dc, parsec_matrix_type_t mtype, int myrank, int mb, int nb, int lm, int ln, int i,
+                                         int j, int m, int n, int p, int q, parsec_matrix_uplo_t uplo);
+
+/* tabular: an explicit (rank, vpid) per tile, column major (reference
+ * data_dist/matrix/two_dim_tabular.h:55-68); the runtime allocates the local
+ * tiles, `data` of a local element then points at its storage */
+typedef struct parsec_two_dim_td_table_elem_s {
+  uint32_t rank;
+  int32_t vpid;
+  int32_t pos;
+  void* data;
+} parsec_two_dim_td_table_elem_t;
+typedef struct parsec_two_dim_td_table_s {
+  int nbelem;
+  parsec_two_dim_td_table_elem_t elems[1]; /* nbelem elements follow */
+} parsec_two_dim_td_table_t;
+typedef struct parsec_matrix_tabular_s {
+  parsec_tiled_matrix_t super;
+  int user_table;
+  parsec_two_dim_td_table_t* tiles_table;
+} parsec_matrix_tabular_t;
+/* table may be NULL (every tile on rank 0 until a set_*_table call) */
+void parsec_matrix_tabular_init(parsec_matrix_tabular_t* dc, parsec_matrix_type_t mtype, unsigned int nodes, unsigned int myrank, unsigned int mb, unsigned int nb,
+                                unsigned int lm, unsigned int ln, unsigned int i, unsigned int j, unsigned int m, unsigned int n,
+                                parsec_two_dim_td_table_t* table);
+void parsec_matrix_tabular_destroy(parsec_matrix_tabular_t* dc);
+/* the collection takes ownership of `table` (freed at destroy) */
+void parsec_matrix_tabular_set_table(parsec_matrix_tabular_t* dc, parsec_two_dim_td_table_t* table);
+/* `table` stays the caller's */
+void parsec_matrix_tabular_set_user_table(parsec_matrix_tabular_t* dc, parsec_two_dim_td_table_t* table);
+/* every tile on a pseudo-random rank (same seed -> same table on every rank) */
+void parsec_matrix_tabular_set_random_table(parsec_matrix_tabular_t* dc, unsigned int seed);
+
+/* vector of mb-element tiles over a P x Q grid: by process row, column or the
+ * grid diagonal (reference data_dist/matrix/vector_two_dim_cyclic.c:40) */
+typedef enum parsec_vector_two_dim_cyclic_distrib_t { PARSEC_VECTOR_DISTRIB_ROW = 0, PARSEC_VECTOR_DISTRIB_COL, PARSEC_VECTOR_DISTRIB_DIAG } parsec_vector_two_dim_cyclic_distrib_t;
+typedef struct parsec_vector_two_dim_cyclic_s {
+  parsec_tiled_matrix_t super;
+  parsec_grid_2Dcyclic_t grid;
+  parsec_vector_two_dim_cyclic_distrib_t distrib;
+  int lcm; /* processes on the diagonal */
+  void* mat;
+} parsec_vector_two_dim_cyclic_t;
+void parsec_vector_two_dim_cyclic_init(parsec_vector_two_dim_cyclic_t* vdesc, parsec_matrix_type_t mtype, enum parsec_vector_two_dim_cyclic_distrib_t distrib, int myrank,
+                                       int mb, int lm, int i, int m, int P, int Q);
+
+/* hash distribution: arbitrary keys registered one by one with their owner
+ * (reference data_dist/hash_datadist.c:27); rank_of / data_of take the key */
+typedef struct parsec_hash_datadist_s {
+  parsec_data_collection_t super;
+} parsec_hash_datadist_t;
+parsec_hash_datadist_t* parsec_hash_datadist_create(int np, int myrank);
+void parsec_hash_datadist_destroy(parsec_hash_datadist_t* d);
+/* register `key` on `rank` (local keys: `actual_data` holds `size` bytes) */
+void parsec_hash_datadist_set_data(parsec_hash_datadist_t* d, void* actual_data, parsec_data_key_t key, int vpid, int rank, uint32_t size);
+
 void parsec_tiled_matrix_destroy(parsec_tiled_matrix_t* tdesc);
 parsec_data_key_t parsec_tiled_matrix_data_key(parsec_tiled_matrix_t* tdesc, int m, int n);
 size_t parsec_matrix_type_size(parsec_matrix_type_t mtype);
@@ -273,6 +338,13 @@ int parsec_redistribute(parsec_context_t* parsec, parsec_tiled_matrix_t* source,
                         int disj_source, int disi_target, int disj_target);
 int parsec_redistribute_dtd(parsec_context_t* parsec, parsec_tiled_matrix_t* source, parsec_tiled_matrix_t* target, int size_row, int size_col,
                             int disi_source, int disj_source, int disi_target, int disj_target);
+/* broadcast one datum from `root` to the `sz` ranks of `ranks` (reference
+ * data_dist/matrix/broadcast.jdf:160): on the root *data is sent; on every
+ * listed rank *data receives it (when *data is NULL the runtime creates a datum
+ * of the rtype extent, valid until the taskpool is freed). A non-NULL master_tp
+ * counts one runtime action until the broadcast completed. */
+parsec_taskpool_t* parsec_broadcast_New(parsec_data_t** data, int32_t myrank, int32_t world, int root, const int32_t* ranks, int sz, parsec_taskpool_t* master_tp,
+                                        parsec_datatype_t stype, parsec_datatype_t rtype);
 /* diagonal + sub-diagonal tiles of a lower tiled matrix to LAPACK band storage */
 parsec_taskpool_t* parsec_diag_band_to_rect_New(parsec_tiled_matrix_t* A, parsec_tiled_matrix_t* B, int mt, int nt, int mb, int nb, size_t elem_size);
 

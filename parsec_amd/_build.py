@@ -53,7 +53,6 @@ CORE_SOURCES = [
     "csrc/capi/capi.cpp",
     "csrc/algos/dpotrf_jdf.cpp",
     "csrc/algos/redistribute_ptg.cpp",
-    "csrc/device/vendor_blas.cpp",
 ]
 HIP_SOURCES = [
     "csrc/kernels/tile_kernels.hip",

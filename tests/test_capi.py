@@ -173,6 +173,26 @@ def test_matrix_operators_c_program(tmp_path, pa, nranks):
     assert text.count("bad 0") == nranks
 
 
+@pytest.mark.parametrize("nranks", [1, 3])
+def test_collections_c_program(tmp_path, pa, nranks):
+    """parsec_matrix_sym_block_cyclic_init, parsec_matrix_tabular_init (+ random
+    table), parsec_vector_two_dim_cyclic_init, parsec_hash_datadist_create and
+    parsec_broadcast_New from C, 1 and 3 ranks (reference
+    sym_two_dim_rectangle_cyclic.c:228, two_dim_tabular.c:126,
+    vector_two_dim_cyclic.c:40, hash_datadist.c:27, broadcast.jdf:160)."""
+    exe = tmp_path / "collections_capi"
+    cmd = ["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-O1", f"-I{ROOT}/include", os.path.join(HERE, "capi", "collections_capi.c"), "-o", str(exe),
+           f"-L{ROOT}/parsec_amd/lib", "-lparsec_amd", f"-Wl,-rpath,{ROOT}/parsec_amd/lib", "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    rc, outs = launch.launch(nranks, [str(exe)], timeout=90, capture=True, env={"PARSEC_MCA_device_hip_enabled": "0"})
+    text = "".join(o for o, _ in outs)
+    assert rc == 0, text + "".join(e for _, e in outs)
+    assert text.count("collections capi rank") == nranks and text.count(f"/{nranks} bad 0") == nranks, text
+    if nranks > 1:
+        assert text.count("broadcast rank") == nranks
+
+
 @pytest.fixture(scope="module")
 def dtd_more(tmp_path_factory, pa):
     exe = tmp_path_factory.mktemp("dtdmore") / "dtd_more"
