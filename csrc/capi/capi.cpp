@@ -500,8 +500,10 @@ void parsec_fini_f08(parsec_context_t** context, int* ierr) {
   if (ierr) *ierr = rc;
 }
 void parsec_profiling_init_f08(const char* basename, int len, int* ierr) {
+  // the Fortran module keeps the one-call form: init for this rank + dbp_start
   std::string b(basename, (size_t)std::max(len, 0));
-  int rc = parsec_profiling_init(b.c_str());
+  int rc = parsec_profiling_init(comm_rank());
+  if (rc == PARSEC_SUCCESS) rc = parsec_profiling_dbp_start(b.c_str(), "fortran");
   if (ierr) *ierr = rc;
 }
 void parsec_profile_add_dictionary_keyword_f08(const char* name, int name_len, const char* attributes, int attr_len, int info_length, int* key_start, int* key_end, int* ierr) {
@@ -510,7 +512,7 @@ void parsec_profile_add_dictionary_keyword_f08(const char* name, int name_len, c
   if (ierr) *ierr = rc >= 0 ? PARSEC_SUCCESS : rc;
 }
 void parsec_profiling_trace_f08(int key, int64_t event_id, int taskpool_id, int* ierr) {
-  int rc = parsec_profiling_trace(key, (uint64_t)event_id, (uint32_t)taskpool_id, nullptr);
+  int rc = parsec_profiling_ts_trace_flags(key, (uint64_t)event_id, (uint32_t)taskpool_id, nullptr, 0);
   if (ierr) *ierr = rc >= 0 ? PARSEC_SUCCESS : rc;
 }
 int32_t parsec_taskpool_set_priority(parsec_taskpool_t* tp, int32_t p) { return taskpool_set_priority(tp, p); }
@@ -1195,28 +1197,67 @@ void* parsec_dtd_get_dev_ptr(parsec_task_t* this_task, int i) {
 }
 
 // ------------------------------------------------------------ profiling
-int parsec_profiling_init(const char* basename) {
-  ParamRegistry::instance().set_override("profile_filename", basename ? basename : "parsec");
-  return PARSEC_SUCCESS;
+// Standalone interface of the tracing module (reference profiling.h:133-461);
+// inside a runtime context the same streams / dictionary are shared with the
+// runtime's own events.
+int parsec_profiling_init(int rank) { return profiling_standalone_init(rank) == 0 ? PARSEC_SUCCESS : PARSEC_ERROR; }
+void parsec_profiling_start(void) { profiling_start(); }
+int parsec_profiling_fini(void) {
+  t_prof = nullptr;
+  return profiling_standalone_fini() == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
 }
-int parsec_profiling_fini(void) { return PARSEC_SUCCESS; }
 int parsec_profiling_reset(void) { return profiling_reset(); }
+void parsec_profiling_add_information(const char* key, const char* value) { profiling_add_information(key ? key : "", value ? value : ""); }
+void parsec_profiling_stream_add_information(parsec_profiling_stream_t* stream, const char* key, const char* value) {
+  profiling_stream_add_information(reinterpret_cast<ProfilingStream*>(stream), key ? key : "", value ? value : "");
+}
+parsec_profiling_stream_t* parsec_profiling_stream_init(size_t length, const char* format, ...) {
+  (void)length;  // buffers are sized by profile_buffer_events and spilled by the writer thread
+  char name[256] = "stream";
+  if (format) {
+    va_list ap;
+    va_start(ap, format);
+    std::vsnprintf(name, sizeof name, format, ap);
+    va_end(ap);
+  }
+  ProfilingStream* s = profiling_stream_create(name);
+  if (!t_prof) t_prof = s;  // the creating thread's default stream
+  return reinterpret_cast<parsec_profiling_stream_t*>(s);
+}
+parsec_profiling_stream_t* parsec_profiling_set_default_thread(parsec_profiling_stream_t* stream) {
+  ProfilingStream* old = t_prof;
+  t_prof = reinterpret_cast<ProfilingStream*>(stream);
+  return reinterpret_cast<parsec_profiling_stream_t*>(old);
+}
 int parsec_profiling_add_dictionary_keyword(const char* name, const char* attributes, size_t info_length, const char* convertor_code, int* key_start, int* key_end) {
   return profiling_add_dictionary_keyword(name, attributes ? attributes : "", info_length, convertor_code ? convertor_code : "", key_start, key_end);
 }
-int parsec_profiling_trace(int key, uint64_t event_id, uint32_t taskpool_id, const void* info) {
+int parsec_profiling_dictionary_flush(void) { return profiling_dictionary_flush(); }
+int parsec_profiling_trace_flags(parsec_profiling_stream_t* stream, int key, uint64_t event_id, uint32_t taskpool_id, const void* info, uint16_t flags) {
+  auto* s = reinterpret_cast<ProfilingStream*>(stream);
+  if (!s) return PARSEC_ERROR;
+  const size_t n = (info && (flags & PARSEC_PROFILING_EVENT_HAS_INFO)) ? profiling_key_info_length(key) : 0;
+  return profiling_trace(s, key, event_id, taskpool_id, n ? info : nullptr, n) == 0 ? PARSEC_SUCCESS : PARSEC_ERROR;
+}
+int parsec_profiling_ts_trace_flags(int key, uint64_t event_id, uint32_t taskpool_id, const void* info, uint16_t flags) {
   if (!t_prof) {
     char nm[64];
     snprintf(nm, sizeof nm, "user thread %zu", std::hash<std::thread::id>()(std::this_thread::get_id()) % 100000);
     t_prof = profiling_stream_create(nm);
   }
-  return profiling_trace(t_prof, key, event_id, taskpool_id, info, 0);
+  return parsec_profiling_trace_flags(reinterpret_cast<parsec_profiling_stream_t*>(t_prof), key, event_id, taskpool_id, info, flags);
 }
-int parsec_profiling_dump(void) {
-  std::string f;
-  ParamRegistry::instance().lookup("profile_filename", f);
-  return profiling_dump(f.empty() ? "parsec" : f);
+int parsec_profiling_dbp_start(const char* basefile, const char* hr_id) {
+  if (profiling_dbp_start(basefile ? basefile : "", hr_id ? hr_id : "") != 0) return PARSEC_ERROR;
+  ParamRegistry::instance().set_override("profile_filename", basefile);  // a runtime context started later traces too
+  return PARSEC_SUCCESS;
 }
+int parsec_profiling_dbp_dump(void) { return profiling_dbp_dump() == 0 ? PARSEC_SUCCESS : PARSEC_ERROR; }
+int parsec_profiling_dump(void) { return parsec_profiling_dbp_dump(); }
+char* parsec_profiling_strerror(void) { return const_cast<char*>(profiling_last_error()); }
+uint64_t parsec_profiling_get_time(void) { return profiling_now(); }
+void parsec_profiling_enable(void) { profiling_set_recording(true); }
+void parsec_profiling_disable(void) { profiling_set_recording(false); }
 
 }  // extern "C"
 

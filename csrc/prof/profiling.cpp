@@ -46,6 +46,8 @@ struct ProfState {
   bool writer_stop = false;
   size_t jobs_pending = 0;
   std::condition_variable wdone;
+  std::atomic<bool> recording{true};  // parsec_profiling_enable / disable
+  std::string last_error;
 };
 ProfState& P() { static ProfState* s = new ProfState(); return *s; }
 
@@ -174,6 +176,7 @@ int profiling_add_dictionary_keyword(const std::string& name, const std::string&
 }
 
 static void trace_into(ProfilingStream* s, int key, uint64_t event_id, uint32_t taskpool_id, uint64_t ts, const void* info, size_t info_len) {
+  if (!P().recording.load(std::memory_order_relaxed)) return;
   ProfEvent e;
   e.key = (uint16_t)key;
   e.flags = info_len ? 1 : 0;
@@ -256,7 +259,7 @@ int profiling_dump(const std::string& filename) {
   std::lock_guard<std::mutex> g(p.m);
   std::ofstream o(filename, std::ios::binary);
   if (!o) return -1;
-  o.write("PAMDPRF1", 8);
+  o.write("PAMDPRF2", 8);
   uint32_t hdr[4] = {(uint32_t)p.rank, (uint32_t)p.dict.size(), (uint32_t)p.streams.size(), (uint32_t)p.infos.size()};
   o.write((const char*)hdr, sizeof(hdr));
   o.write((const char*)&p.t0, 8);
@@ -270,6 +273,9 @@ int profiling_dump(const std::string& filename) {
     wstr(o, s->name);
     int32_t tid = s->thread_id;
     o.write((const char*)&tid, 4);
+    uint32_t ninfo = (uint32_t)s->infos.size();
+    o.write((const char*)&ninfo, 4);
+    for (auto& kv : s->infos) { wstr(o, kv.first); wstr(o, kv.second); }
     // spilled chunks (in order) + the in-memory tail
     std::vector<uint8_t> sev = read_all(s->spill_ev), sinfo = read_all(s->spill_info);
     uint64_t n = sev.size() / sizeof(ProfEvent) + s->events.size();
@@ -284,6 +290,92 @@ int profiling_dump(const std::string& filename) {
   }
   return o ? 0 : -1;
 }
+
+// ---------------------------------------------------- standalone interface
+int profiling_standalone_init(int rank) {
+  auto& p = P();
+  std::lock_guard<std::mutex> g(p.m);
+  p.rank = rank;
+  if (p.t0 == 0) p.t0 = now_ns();
+  return 0;
+}
+
+int profiling_dbp_start(const std::string& basefile, const std::string& hr_id) {
+  auto& p = P();
+  if (basefile.empty()) {
+    p.last_error = "dbp_start: empty base file name";
+    return -1;
+  }
+  std::lock_guard<std::mutex> g(p.m);
+  p.filename = basefile;
+  p.enabled = true;
+  p.infos.emplace_back("hr_id", hr_id);
+  return 0;
+}
+
+int profiling_dbp_dump() {
+  auto& p = P();
+  writer_drain();
+  if (!p.enabled || p.filename.empty()) {
+    p.last_error = "dbp_dump: no dbp_start";
+    return -1;
+  }
+  const std::string fn = p.filename + "-" + std::to_string(p.rank) + ".prof";
+  if (profiling_dump(fn) != 0) {
+    p.last_error = "dbp_dump: cannot write " + fn;
+    return -1;
+  }
+  return 0;
+}
+
+int profiling_standalone_fini() {
+  auto& p = P();
+  writer_drain();
+  {
+    std::lock_guard<std::mutex> lk(p.wm);
+    p.writer_stop = true;
+  }
+  p.wcv.notify_all();
+  if (p.writer.joinable()) p.writer.join();
+  p.writer_stop = false;
+  std::lock_guard<std::mutex> g(p.m);
+  for (auto* s : p.streams) {
+    std::remove(s->spill_ev.c_str());
+    std::remove(s->spill_info.c_str());
+    delete s;
+  }
+  p.streams.clear();
+  p.infos.clear();
+  p.dict.clear();
+  p.dict_index.clear();
+  p.enabled = false;
+  p.filename.clear();
+  return 0;
+}
+
+void profiling_stream_add_information(ProfilingStream* s, const std::string& key, const std::string& value) {
+  if (!s) return;
+  std::lock_guard<SpinLock> g(s->lock);
+  s->infos.emplace_back(key, value);
+}
+
+int profiling_dictionary_flush() {
+  auto& p = P();
+  std::lock_guard<std::mutex> g(p.m);
+  p.dict.clear();
+  p.dict_index.clear();
+  return 0;
+}
+
+size_t profiling_key_info_length(int key) {
+  auto& p = P();
+  std::lock_guard<std::mutex> g(p.m);
+  const size_t id = (size_t)(key / 2);
+  return key >= 0 && id < p.dict.size() ? p.dict[id].info_length : 0;
+}
+
+void profiling_set_recording(bool on) { P().recording.store(on); }
+const char* profiling_last_error() { return P().last_error.c_str(); }
 
 void profiling_fini(Context* ctx) {
   auto& p = P();

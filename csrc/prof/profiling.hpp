@@ -5,7 +5,7 @@
 // file per rank), PINS callback chains on 16 events (mca/pins/pins.h:26-190) with
 // modules task_profiler / print_steals / alperf / iterators_checker, DOT grapher
 // (parsec_prof_grapher.c:86-266), properties dictionary (dictionary.h:14-60).
-// File format here is our own ("PAMDPRF1", see parsec_amd/profiling.py reader).
+// File format here is our own ("PAMDPRF2", see parsec_amd/profiling.py reader).
 #pragma once
 #include <cstdint>
 #include <string>
@@ -39,6 +39,7 @@ struct ProfilingStream {
   uint64_t spilled_events = 0;  // events already handed to the writer
   std::string spill_ev, spill_info;  // spill file paths
   SpinLock lock;  // only for streams shared by several threads (devices)
+  std::vector<std::pair<std::string, std::string>> infos;  // per-stream key / value pairs
 };
 
 struct DictEntry {
@@ -72,6 +73,18 @@ int profiling_dump(const std::string& filename);
 int profiling_reset();
 void profiling_add_information(const std::string& key, const std::string& value);
 void profiling_start();
+// ---- standalone use without a runtime context (reference profiling.h:133-461:
+// init / dbp_start / stream_init / trace_flags / dbp_dump / fini from any
+// number of application threads, one stream each)
+int profiling_standalone_init(int rank);
+int profiling_dbp_start(const std::string& basefile, const std::string& hr_id);
+int profiling_dbp_dump();  // <basefile>-<rank>.prof
+int profiling_standalone_fini();
+void profiling_stream_add_information(ProfilingStream* s, const std::string& key, const std::string& value);
+int profiling_dictionary_flush();
+size_t profiling_key_info_length(int key);  // info bytes of a begin / end key
+void profiling_set_recording(bool on);      // parsec_profiling_enable / disable
+const char* profiling_last_error();
 
 // PINS
 void pins_init(Context* ctx);

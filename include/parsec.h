@@ -414,13 +414,41 @@ void parsec_dtd_set_window(parsec_taskpool_t* tp, int64_t window, int64_t thresh
 #define PARSEC_DTD_TILE_OF(DC, I, J) parsec_dtd_tile_of((parsec_data_collection_t*)(DC), (DC)->super.super.data_key((parsec_data_collection_t*)(DC), (I), (J)))
 #define PARSEC_DTD_TILE_OF_KEY(DC, KEY) parsec_dtd_tile_of((parsec_data_collection_t*)(DC), (KEY))
 
-/* -------------------------------------------------------------- profiling */
-int parsec_profiling_init(const char* basename);
+/* -------------------------------------------------------------- profiling
+ * (reference parsec/profiling.h:133-461). Usable inside a runtime context
+ * (--mca profile_filename) or standalone from any number of application
+ * threads: init(rank), dbp_start(base, id), one stream per thread
+ * (stream_init), trace_flags, dbp_dump, fini. One file per process:
+ * <base>-<rank>.prof (read with python -m parsec_amd.profiling). */
+typedef struct parsec_profiling_stream_s parsec_profiling_stream_t;
+#define PROFILE_OBJECT_ID_NULL ((uint32_t)-1)
+#define PARSEC_PROFILING_EVENT_HAS_INFO 0x0001
+int parsec_profiling_init(int rank);
+void parsec_profiling_start(void); /* time 0 of the trace */
 int parsec_profiling_fini(void);
-int parsec_profiling_add_dictionary_keyword(const char* name, const char* attributes, size_t info_length, const char* convertor_code, int* key_start, int* key_end);
-int parsec_profiling_trace(int key, uint64_t event_id, uint32_t taskpool_id, const void* info);
-int parsec_profiling_dump(void);
 int parsec_profiling_reset(void);
+void parsec_profiling_add_information(const char* key, const char* value);
+void parsec_profiling_stream_add_information(parsec_profiling_stream_t* stream, const char* key, const char* value);
+/* a stream for the calling thread (not thread safe itself: one writer) */
+parsec_profiling_stream_t* parsec_profiling_stream_init(size_t length, const char* format, ...);
+/* the stream parsec_profiling_ts_trace_flags uses on this thread; returns the previous one */
+parsec_profiling_stream_t* parsec_profiling_set_default_thread(parsec_profiling_stream_t* stream);
+int parsec_profiling_add_dictionary_keyword(const char* name, const char* attributes, size_t info_length, const char* convertor_code, int* key_start, int* key_end);
+int parsec_profiling_dictionary_flush(void);
+/* info (info_length bytes of the key's dictionary entry) is recorded when
+ * flags has PARSEC_PROFILING_EVENT_HAS_INFO */
+int parsec_profiling_trace_flags(parsec_profiling_stream_t* stream, int key, uint64_t event_id, uint32_t taskpool_id, const void* info, uint16_t flags);
+#define parsec_profiling_trace(CTX, KEY, EVENT_ID, TASKPOOL_ID, INFO) parsec_profiling_trace_flags((CTX), (KEY), (EVENT_ID), (TASKPOOL_ID), (INFO), 0)
+/* on the calling thread's default stream (created on first use) */
+int parsec_profiling_ts_trace_flags(int key, uint64_t event_id, uint32_t taskpool_id, const void* info, uint16_t flags);
+#define parsec_profiling_ts_trace(KEY, EVENT_ID, OBJECT_ID, INFO) parsec_profiling_ts_trace_flags((KEY), (EVENT_ID), (OBJECT_ID), (INFO), 0)
+int parsec_profiling_dbp_start(const char* basefile, const char* hr_id);
+int parsec_profiling_dbp_dump(void);
+int parsec_profiling_dump(void); /* = dbp_dump (Fortran binding name) */
+char* parsec_profiling_strerror(void);
+uint64_t parsec_profiling_get_time(void); /* ns since parsec_profiling_start */
+void parsec_profiling_enable(void);
+void parsec_profiling_disable(void);
 
 /* --------------------------------------------------- communication engine
  * (reference parsec/parsec_comm_engine.h:22-186). Active messages on user tags

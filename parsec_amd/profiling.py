@@ -7,10 +7,10 @@ from the ``task_profiler`` PINS module, user events from the C API).
     python -m parsec_amd.profiling chrome out.json trace-*.prof   # chrome://tracing / Perfetto
     python -m parsec_amd.profiling dot-merge out.dot graph-*.dot
 
-File layout (profiling.cpp: profiling_dump): magic ``PAMDPRF1``; u32 rank,
+File layout (profiling.cpp: profiling_dump): magic ``PAMDPRF2``; u32 rank,
 n_dict, n_streams, n_infos; u64 t0; infos (key, value strings); dictionary
 entries (name, attributes, info description, u64 info length); per stream:
-name, i32 thread id, u64 n_events, events (32 B each: u16 key, u16 flags,
+name, i32 thread id, u32 n_infos + that many (key, value) strings, u64 n_events, events (32 B each: u16 key, u16 flags,
 u32 taskpool id, u64 event id, u64 timestamp ns, u32 info offset, u32 info
 length), u64 info blob size + blob. Strings are u32 length + bytes.
 
@@ -51,8 +51,9 @@ def _rstr(buf, off):
 def read_trace(path):
     with open(path, "rb") as f:
         buf = f.read()
-    if buf[:8] != b"PAMDPRF1":
+    if buf[:8] not in (b"PAMDPRF1", b"PAMDPRF2"):
         raise ValueError(f"{path}: not a parsec-amd trace")
+    v2 = buf[:8] == b"PAMDPRF2"  # per-stream key / value infos
     rank, ndict, nstreams, ninfos = struct.unpack_from("<4I", buf, 8)
     (t0,) = struct.unpack_from("<Q", buf, 24)
     off = 32
@@ -74,6 +75,14 @@ def read_trace(path):
         name, off = _rstr(buf, off)
         (tid,) = struct.unpack_from("<i", buf, off)
         off += 4
+        sinfos = {}
+        if v2:
+            (ni,) = struct.unpack_from("<I", buf, off)
+            off += 4
+            for _ in range(ni):
+                k, off = _rstr(buf, off)
+                v, off = _rstr(buf, off)
+                sinfos[k] = v
         (n,) = struct.unpack_from("<Q", buf, off)
         off += 8
         ev = np.frombuffer(buf, dtype=EVENT_DTYPE, count=n, offset=off).copy()
@@ -82,7 +91,7 @@ def read_trace(path):
         off += 8
         info = buf[off:off + isz]
         off += isz
-        streams.append({"name": name, "thread_id": tid, "events": ev, "info": info})
+        streams.append({"name": name, "thread_id": tid, "events": ev, "info": info, "infos": sinfos})
     return Trace(rank, t0, infos, dictionary, streams)
 
 
@@ -97,8 +106,12 @@ def _info_fields(desc):
 
 
 def _decode_info(fields, blob):
+    """Fields laid out as the C struct the convertor describes: each at its
+    natural alignment (an int32_t followed by a double starts the double at 8)."""
     vals, off = {}, 0
     for name, fmt, cnt in fields:
+        align = struct.calcsize("<" + fmt)
+        off = (off + align - 1) // align * align
         sz = struct.calcsize("<" + fmt * cnt)
         if off + sz > len(blob):
             break

@@ -30,7 +30,7 @@ def test_fortran_dtd_program(tmp_path, pa):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "fortran dtd sum 85344 expect 85344 completed 1 enqueued 1" in r.stdout
     assert "fortran ok" in r.stdout
-    trace = tmp_path / "fortran_trace"
+    trace = tmp_path / "fortran_trace-0.prof"  # <base>-<rank>.prof (reference parsec_profiling_dbp_start)
     assert trace.exists()
     from parsec_amd import profiling
 

@@ -199,3 +199,39 @@ def test_live_properties_publisher(pa, tmp_path):
             os.unlink(os.path.join("/dev/shm", name))
         except OSError:
             pass
+
+
+def test_standalone_profiling_c_threads(pa, tmp_path):
+    """Standalone profiling API from C without a runtime context (port of the
+    reference's tests/profiling-standalone/sp-demo.c and sp-perf.c): 4 threads,
+    one stream each (parsec_profiling_stream_init), per-stream and global
+    key / values, 10 begin / end pairs per thread, the B events' info structure
+    {int i; double d} decoded from the trace; the perf mode traces 2 x 20000
+    events per thread."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "sp_demo")
+    cmd = ["gcc", "-std=gnu99", "-Wall", "-Wextra", "-Werror", "-O1", f"-I{root}/include", os.path.join(root, "tests", "capi", "sp_demo.c"), "-o", exe,
+           "-lpthread", f"-L{root}/parsec_amd/lib", "-lparsec_amd", f"-Wl,-rpath,{root}/parsec_amd/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([exe, "demo", str(tmp_path / "sp")], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "sp-demo done" in r.stdout, r.stdout + r.stderr
+    tr = profiling.read_trace(str(tmp_path / "sp-0.prof"))
+    assert tr.infos["This is a global information key"] == "This is the global information value"
+    assert tr.infos["hr_id"] == "Demonstration of basic PaRSEC profiling system"
+    names = sorted(s["name"] for s in tr.streams)
+    assert names == [f"This is the name of thread {i}" for i in range(4)]
+    assert all(s["infos"] == {"This is a thread-specific information key": "This is the corresponding value"} for s in tr.streams)
+    rows = profiling.intervals([tr])
+    assert len(rows) == 40 and {r["type"] for r in rows} <= {"Event A", "Event B"}
+    for r in rows:
+        assert r["end"] >= r["begin"]
+        if r["type"] == "Event B":
+            assert r["i"] == r["event_id"] and r["d"] == float(r["stream"].split()[-1])
+    r = subprocess.run([exe, "perf", str(tmp_path / "spp"), "20000"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "ns per event" in r.stdout, r.stdout + r.stderr
+    print(r.stdout.strip().splitlines()[0])
+    tr = profiling.read_trace(str(tmp_path / "spp-0.prof"))
+    assert sum(len(s["events"]) for s in tr.streams) == 4 * 2 * 20000
