@@ -587,8 +587,20 @@ void parsec_data_collection_set_key(parsec_data_collection_t* dc, const char* na
   dc->key_base = strdup(name);
   impl_of(dc)->key_base = name;
 }
-parsec_data_t* parsec_data_create(parsec_data_t** holder, parsec_data_collection_t* desc, parsec_data_key_t key, void* ptr, size_t size) {
-  return data_create(holder, impl_of(desc), key, ptr, size);
+parsec_data_t* parsec_data_create(parsec_data_t** holder, parsec_data_collection_t* desc, parsec_data_key_t key, void* ptr, size_t size, parsec_data_flag_t flags) {
+  // reference bit positions -> the runtime's copy flags
+  uint8_t f = 0;
+  if (flags & PARSEC_DATA_FLAG_ARENA) f |= DATA_FLAG_ARENA;
+  if (flags & PARSEC_DATA_FLAG_TRANSIT) f |= DATA_FLAG_TRANSIT;
+  if (flags & PARSEC_DATA_FLAG_PARSEC_MANAGED) f |= DATA_FLAG_PARSEC_MANAGED;
+  if (flags & PARSEC_DATA_FLAG_PARSEC_OWNED) f |= DATA_FLAG_PARSEC_OWNED;
+  if (!f) f = DATA_FLAG_PARSEC_MANAGED;
+  return data_create(holder, desc ? impl_of(desc) : nullptr, key, ptr, size, f);
+}
+parsec_data_t* parsec_data_create_with_type(parsec_data_collection_t* desc, parsec_data_key_t key, void* ptr, size_t size, parsec_datatype_t dtt) {
+  Data* d = data_create(nullptr, desc ? impl_of(desc) : nullptr, key, ptr, size, DATA_FLAG_PARSEC_MANAGED);
+  if (d && d->copy(0)) d->copy(0)->dtt = type_of(dtt);
+  return d;
 }
 void parsec_data_destroy(parsec_data_t* data) { data_destroy(data); }
 parsec_data_copy_t* parsec_data_get_copy(parsec_data_t* data, int device) { return data ? data->copy(device) : nullptr; }
@@ -719,6 +731,22 @@ static void set_c_callbacks(parsec_data_collection_t* d, DataCollection* impl, i
   d->impl = impl;
 }
 
+void parsec_matrix_block_cyclic_kview(parsec_matrix_block_cyclic_t* target, parsec_matrix_block_cyclic_t* origin, int kp, int kq) {
+  auto* o = dynamic_cast<BlockCyclic*>(impl_of(&origin->super.super));
+  if (!o) fatal("parsec_matrix_block_cyclic_kview: the origin is not a block-cyclic matrix");
+  if (auto* cb = dynamic_cast<CBlockCyclic*>(o)) cb->sync();  // the user's storage, if given after init
+  std::memset(target, 0, sizeof(*target));
+  auto* v = new KViewMatrix();
+  v->init_view(o, kp, kq);
+  set_c_callbacks(&target->super.super, v, 2);
+  target->super = origin->super;  // sizes, tiles, local counts: the origin's
+  set_c_callbacks(&target->super.super, v, 2);
+  target->super.super.key_base = nullptr;
+  target->grid = origin->grid;
+  target->grid.krows = kp;
+  target->grid.kcols = kq;
+  target->mat = origin->mat;
+}
 void parsec_matrix_sym_block_cyclic_init(parsec_matrix_sym_block_cyclic_t* dc, parsec_matrix_type_t mtype, int myrank, int mb, int nb, int lm, int ln, int i,
                                          int j, int m, int n, int p, int q, parsec_matrix_uplo_t uplo) {
   std::memset(dc, 0, sizeof(*dc));

@@ -19,6 +19,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #define PARSEC_VERSION_MAJOR 4
 #define PARSEC_VERSION_MINOR 0
@@ -33,6 +34,11 @@
 
 #define PARSEC_SUCCESS 0
 #define PARSEC_ERROR (-1)
+/* report a failed call (reference include/parsec/constants.h PARSEC_CHECK_ERROR) */
+#define PARSEC_CHECK_ERROR(rc, WHAT)                                                                   \
+  do {                                                                                             \
+    if ((rc) != PARSEC_SUCCESS) fprintf(stderr, "%s:%d %s failed (%d)\n", __FILE__, __LINE__, (WHAT), (int)(rc)); \
+  } while (0)
 #define PARSEC_ERR_NOT_SUPPORTED (-2)
 #define PARSEC_ERR_NOT_FOUND (-13)
 
@@ -42,6 +48,8 @@
 #define PARSEC_DEV_RECURSIVE 0x02
 #define PARSEC_DEV_HIP 0x40
 #define PARSEC_DEV_ALL 0xff
+
+#include "parsec/sys/atomic.h"
 
 #ifdef __cplusplus
 namespace parsec {
@@ -127,6 +135,8 @@ int parsec_context_rank(const parsec_context_t* context);
 int parsec_context_nb_nodes(const parsec_context_t* context);
 int parsec_context_nb_cores(const parsec_context_t* context);
 int parsec_comm_barrier(void);
+/* deprecated name of parsec_context_add_taskpool (reference include/parsec/deprecated.h:22) */
+static inline int parsec_enqueue(parsec_context_t* context, parsec_taskpool_t* tp) { return parsec_context_add_taskpool(context, tp); }
 
 /* -------------------------------------------------------------- taskpool */
 typedef int (*parsec_event_cb_t)(parsec_taskpool_t* tp, void* cb_data);
@@ -178,7 +188,15 @@ void parsec_data_collection_init(parsec_data_collection_t* dc, int nodes, int my
 void parsec_data_collection_destroy(parsec_data_collection_t* dc);
 void parsec_data_collection_set_key(parsec_data_collection_t* dc, const char* name);
 
-parsec_data_t* parsec_data_create(parsec_data_t** holder, parsec_data_collection_t* desc, parsec_data_key_t key, void* ptr, size_t size);
+/* data copy flags (reference data.h:56-59): MANAGED = the runtime tracks the
+ * bytes the user owns; OWNED = the runtime also frees them */
+typedef uint8_t parsec_data_flag_t;
+#define PARSEC_DATA_FLAG_ARENA ((parsec_data_flag_t)1 << 0)
+#define PARSEC_DATA_FLAG_TRANSIT ((parsec_data_flag_t)1 << 1)
+#define PARSEC_DATA_FLAG_PARSEC_MANAGED ((parsec_data_flag_t)1 << 6)
+#define PARSEC_DATA_FLAG_PARSEC_OWNED ((parsec_data_flag_t)1 << 7)
+parsec_data_t* parsec_data_create(parsec_data_t** holder, parsec_data_collection_t* desc, parsec_data_key_t key, void* ptr, size_t size, parsec_data_flag_t flags);
+parsec_data_t* parsec_data_create_with_type(parsec_data_collection_t* desc, parsec_data_key_t key, void* ptr, size_t size, parsec_datatype_t dtt);
 void parsec_data_destroy(parsec_data_t* data);
 parsec_data_copy_t* parsec_data_get_copy(parsec_data_t* data, int device);
 void* parsec_data_copy_get_ptr(parsec_data_copy_t* copy);
@@ -304,8 +322,37 @@ void parsec_hash_datadist_destroy(parsec_hash_datadist_t* d);
 /* register `key` on `rank` (local keys: `actual_data` holds `size` bytes) */
 void parsec_hash_datadist_set_data(parsec_hash_datadist_t* d, void* actual_data, parsec_data_key_t key, int vpid, int rank, uint32_t size);
 
+/* k-cyclic view of a (non k-cyclic) block-cyclic matrix: view tile (m, n) is
+ * an origin tile permuted so kp consecutive view rows (kq columns) share a
+ * process row (column); data and owners are the origin's (reference
+ * two_dim_rectangle_cyclic.h:128) */
+void parsec_matrix_block_cyclic_kview(parsec_matrix_block_cyclic_t* target, parsec_matrix_block_cyclic_t* origin, int kp, int kq);
 void parsec_tiled_matrix_destroy(parsec_tiled_matrix_t* tdesc);
 parsec_data_key_t parsec_tiled_matrix_data_key(parsec_tiled_matrix_t* tdesc, int m, int n);
+/* element size / element datatype of a matrix type (reference data_dist/matrix/matrix.h:52,75) */
+static inline int parsec_datadist_getsizeoftype(parsec_matrix_type_t type) {
+  switch (type) {
+    case PARSEC_MATRIX_BYTE: return 1;
+    case PARSEC_MATRIX_INTEGER: case PARSEC_MATRIX_FLOAT: return 4;
+    case PARSEC_MATRIX_DOUBLE: case PARSEC_MATRIX_COMPLEX_FLOAT: return 8;
+    case PARSEC_MATRIX_COMPLEX_DOUBLE: return 16;
+  }
+  return 0;
+}
+static inline int parsec_translate_matrix_type(parsec_matrix_type_t mt, parsec_datatype_t* dt) {
+  switch (mt) {
+    case PARSEC_MATRIX_BYTE: *dt = parsec_datatype_int8_t; break;
+    case PARSEC_MATRIX_INTEGER: *dt = parsec_datatype_int32_t; break;
+    case PARSEC_MATRIX_FLOAT: *dt = parsec_datatype_float_t; break;
+    case PARSEC_MATRIX_DOUBLE: *dt = parsec_datatype_double_t; break;
+    case PARSEC_MATRIX_COMPLEX_FLOAT: *dt = parsec_datatype_complex_t; break;
+    case PARSEC_MATRIX_COMPLEX_DOUBLE: *dt = parsec_datatype_double_complex_t; break;
+    default: return PARSEC_ERROR;
+  }
+  return PARSEC_SUCCESS;
+}
+static inline int parsec_imin(int a, int b) { return a < b ? a : b; }
+static inline int parsec_imax(int a, int b) { return a > b ? a : b; }
 size_t parsec_matrix_type_size(parsec_matrix_type_t mtype);
 /* place the local storage in HBM of a GPU device (device index >= 2) */
 int parsec_tiled_matrix_set_storage_device(parsec_tiled_matrix_t* tdesc, int device_index);

@@ -1,0 +1,7 @@
+/* Reference header path -> the parsec_amd C API: symmetric 2D block-cyclic matrices (reference data_dist/matrix/sym_two_dim_rectangle_cyclic.h).
+ * Programs written against the reference's headers include this path; every
+ * declaration lives in parsec.h. */
+#ifndef PARSEC_AMD_COMPAT_DATA_DIST_MATRIX_SYM_TWO_DIM_RECTANGLE_CYCLIC_H
+#define PARSEC_AMD_COMPAT_DATA_DIST_MATRIX_SYM_TWO_DIM_RECTANGLE_CYCLIC_H
+#include "../../../parsec.h"
+#endif

@@ -1,0 +1,9 @@
+/* Reference header path -> the parsec_amd C API: build configuration (reference parsec/parsec_config.h): this runtime has no MPI; HIP is its device module.
+ * Programs written against the reference's headers include this path; every
+ * declaration lives in parsec.h. */
+#ifndef PARSEC_AMD_COMPAT_PARSEC_CONFIG_H
+#define PARSEC_AMD_COMPAT_PARSEC_CONFIG_H
+#include "../parsec.h"
+#define PARSEC_HAVE_HIP 1
+#define PARSEC_DIST_COLLECTIVES 1
+#endif

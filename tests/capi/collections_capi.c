@@ -154,10 +154,10 @@ int main(int argc, char** argv) {
     parsec_data_t* d = NULL;
     if (rank == 0) {
       for (int i = 0; i < 6; ++i) payload[i] = 3.5 * (i + 1);
-      d = parsec_data_create(&d, &holder, 0, payload, sizeof(payload));
+      d = parsec_data_create(&d, &holder, 0, payload, sizeof(payload), PARSEC_DATA_FLAG_PARSEC_MANAGED);
     } else if (rank % 2 == 1) {
       /* an odd rank brings its own (zeroed) landing datum */
-      d = parsec_data_create(&d, &holder, 0, payload, sizeof(payload));
+      d = parsec_data_create(&d, &holder, 0, payload, sizeof(payload), PARSEC_DATA_FLAG_PARSEC_MANAGED);
     }
     int32_t* ranks = malloc(sizeof(int32_t) * (size_t)(nodes - 1));
     for (int r = 1; r < nodes; ++r) ranks[r - 1] = r;

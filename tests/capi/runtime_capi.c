@@ -61,7 +61,7 @@ int main(int argc, char** argv) {
     /* data advice: preferred device = the CPU is accepted, an unknown device is not */
     double v = 1.0;
     parsec_data_t* holder = NULL;
-    parsec_data_t* d = parsec_data_create(&holder, NULL, 7, &v, sizeof(v));
+    parsec_data_t* d = parsec_data_create(&holder, NULL, 7, &v, sizeof(v), PARSEC_DATA_FLAG_PARSEC_MANAGED);
     if (parsec_advise_data_on_device(d, 0, PARSEC_DEV_DATA_ADVICE_PREFERRED_DEVICE) != 0) bad++;
     if (parsec_advise_data_on_device(d, 60, PARSEC_DEV_DATA_ADVICE_PREFETCH) == 0) bad++;
     parsec_data_destroy(d);

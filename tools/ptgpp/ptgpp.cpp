@@ -940,6 +940,10 @@ struct Gen {
     if (gpu) c << "static int " << fn << "(parsec::GpuExecContext* __ctx, parsec::Task* this_task) {\n";
     else c << "static int " << fn << "([[maybe_unused]] parsec::ExecutionStream* es, parsec::Task* this_task) {\n";
     c << "  [[maybe_unused]] auto* __tp = static_cast<parsec_" << fname << "_taskpool_t*>(this_task->taskpool);\n";
+    // reference generated bodies see the internal taskpool as __parsec_tp
+    // (__parsec_tp->super is the public taskpool struct)
+    c << "  [[maybe_unused]] struct { parsec_" << fname << "_taskpool_t& super; } __parsec_tp_ref{*__tp};\n";
+    c << "  [[maybe_unused]] auto* __parsec_tp = &__parsec_tp_ref;\n";
     c << "  " << bind_globals() << "\n";
     c << "  " << bind_locals(f, "this_task->locals") << "\n";
     for (size_t k = 0; k < f.flows.size(); ++k) {
@@ -980,6 +984,9 @@ struct Gen {
     for (size_t i = 0; i < adt_names.size(); ++i) h << "#define PARSEC_" << fname << "_" << adt_names[i] << "_ADT_IDX " << i << "\n";
     h << "#define PARSEC_" << fname << "_ADT_IDX_MAX " << adt_names.size() << "\n\n";
     h << "struct parsec_" << fname << "_taskpool_s : public parsec::ptg::PtgTaskpool {\n";
+    // the reference's C layout starts with `parsec_taskpool_t super`: &tp->super
+    // is the taskpool handle, __parsec_tp->super.super its base
+    h << "  parsec::ptg::PtgTaskpool& super = *this;\n";
     for (auto& g : j.globals) h << "  " << gtype(g) << " _g_" << g.name << "{};\n";
     h << "};\ntypedef struct parsec_" << fname << "_taskpool_s parsec_" << fname << "_taskpool_t;\n\n";
     std::string proto = "parsec_" + fname + "_taskpool_t* parsec_" + fname + "_new(";
@@ -999,6 +1006,15 @@ struct Gen {
       c << j.prologue << "\n";
     }
     c << "#include \"" << base_name(base) << ".h\"\n\n";
+    // reference generated-code helpers a body may use: rank_of_<dc>(...) /
+    // data_of_<dc>(...) on collection globals, PARSEC_<name>_<TYPE>_ADT
+    for (auto& g : j.globals)
+      if (gtype(g).find('*') != std::string::npos) {
+        c << "#define rank_of_" << g.name << "(...) parsec::ptg::rank_of_dc(" << g.name << ", __VA_ARGS__)\n";
+        c << "#define data_of_" << g.name << "(...) parsec::ptg::data_of_dc(" << g.name << ", __VA_ARGS__)\n";
+      }
+    for (auto& kv : adt) c << "#define PARSEC_" << fname << "_" << kv.first << "_ADT (&__tp->arenas_datatypes[PARSEC_" << fname << "_" << kv.first << "_ADT_IDX])\n";
+    c << "\n";
     // bodies
     for (auto& f : j.functions)
       for (size_t b = 0; b < f.bodies.size(); ++b) {
