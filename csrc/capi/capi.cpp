@@ -731,6 +731,31 @@ static void set_c_callbacks(parsec_data_collection_t* d, DataCollection* impl, i
   d->impl = impl;
 }
 
+static void band_init_common(parsec_tiled_matrix_t* super, parsec_data_collection_t* band_dc, parsec_data_collection_t* off_dc, const parsec_tiled_matrix_t* off_t,
+                              int band_size, bool sym) {
+  auto* band = dynamic_cast<BlockCyclic*>(impl_of(band_dc));
+  auto* off = dynamic_cast<BlockCyclic*>(impl_of(off_dc));
+  if (!band || !off) fatal("band matrix: band and off_band must be initialised block-cyclic matrices");
+  if (band_size < 1) fatal("band matrix: band_size must be >= 1");
+  auto* bm = new BandMatrix();
+  bm->init_band(band, off, band_size - 1);  // runtime: |m - n| <= band_size - 1
+  bm->sym = sym;
+  std::memset(super, 0, sizeof(*super));
+  *super = *off_t;
+  set_c_callbacks(&super->super, bm, 2);
+  super->super.key_base = nullptr;
+  super->nb_local_tiles = band_dc ? ((parsec_tiled_matrix_t*)band_dc)->nb_local_tiles + off_t->nb_local_tiles : off_t->nb_local_tiles;
+}
+void parsec_matrix_block_cyclic_band_init(parsec_matrix_block_cyclic_band_t* desc, int nodes, int myrank, int band_size) {
+  (void)nodes; (void)myrank;
+  band_init_common(&desc->super, &desc->band.super.super, &desc->off_band.super.super, &desc->off_band.super, band_size, false);
+  desc->band_size = (unsigned)band_size;
+}
+void parsec_matrix_sym_block_cyclic_band_init(parsec_matrix_sym_block_cyclic_band_t* desc, int nodes, int myrank, int band_size) {
+  (void)nodes; (void)myrank;
+  band_init_common(&desc->super, &desc->band.super.super, &desc->off_band.super.super, &desc->off_band.super, band_size, true);
+  desc->band_size = (unsigned)band_size;
+}
 void parsec_matrix_block_cyclic_kview(parsec_matrix_block_cyclic_t* target, parsec_matrix_block_cyclic_t* origin, int kp, int kq) {
   auto* o = dynamic_cast<BlockCyclic*>(impl_of(&origin->super.super));
   if (!o) fatal("parsec_matrix_block_cyclic_kview: the origin is not a block-cyclic matrix");

@@ -397,6 +397,9 @@ struct Taskpool {
   // Called when a remote activation for this taskpool arrives.
   virtual void on_remote_activation(ExecutionStream* es, struct RemoteActivation& act) { (void)es; (void)act; }
   virtual void on_complete_internal() {}
+  // the task count is discovered while the taskpool runs (PTG %option dynamic):
+  // on several ranks only a distributed detector (fourcounter) can end it
+  virtual bool dynamic_task_count() const { return false; }
   // Called by context_wait before waiting (DTD: closes insertion).
   virtual void on_context_wait() {}
   // Called by taskpool_free on a taskpool that has not terminated (DTD: the

@@ -417,6 +417,10 @@ int context_add_taskpool(Context* ctx, Taskpool* tp) {
   // find tdm and its counters in place (race found by the TSan build)
   taskpool_reserve_id(tp);
   std::string td = tp->termdet_name.empty() ? ctx->default_termdet : tp->termdet_name;
+  // reference: a dynamic PTG taskpool on several ranks runs under the
+  // fourcounter module (termdet_fourcounter_module.c), the local count of a
+  // rank cannot know what its peers will still activate
+  if (tp->termdet_name.empty() && ctx->nb_nodes > 1 && tp->dynamic_task_count() && td == "local") td = "fourcounter";
   tp->tdm = termdet_open_module(td);
   if (!tp->tdm) fatal("termination detection module '%s' not available", td.c_str());
   tp->tdm->monitor_taskpool(tp, [](Taskpool* p) { taskpool_termination_detected(p); });

@@ -349,7 +349,7 @@ void BandMatrix::init_band(BlockCyclic* b, BlockCyclic* off, int bs) {
 uint32_t BandMatrix::rank_of(const int64_t* idx, int n) const {
   int64_t tm = idx[0], tn = n > 1 ? idx[1] : 0;
   if (std::llabs(tm - tn) <= band_size) {
-    int64_t bidx[2] = {tm - tn + band_size, tn};
+    int64_t bidx[2] = {band_row(tm, tn), tn};
     return band->rank_of(bidx, 2);
   }
   return off_band->rank_of(idx, n);
@@ -358,7 +358,7 @@ uint32_t BandMatrix::rank_of(const int64_t* idx, int n) const {
 int32_t BandMatrix::vpid_of(const int64_t* idx, int n) const {
   int64_t tm = idx[0], tn = n > 1 ? idx[1] : 0;
   if (std::llabs(tm - tn) <= band_size) {
-    int64_t bidx[2] = {tm - tn + band_size, tn};
+    int64_t bidx[2] = {band_row(tm, tn), tn};
     return band->vpid_of(bidx, 2);
   }
   return off_band->vpid_of(idx, n);
@@ -367,7 +367,7 @@ int32_t BandMatrix::vpid_of(const int64_t* idx, int n) const {
 Data* BandMatrix::data_of(const int64_t* idx, int n) {
   int64_t tm = idx[0], tn = n > 1 ? idx[1] : 0;
   if (std::llabs(tm - tn) <= band_size) {
-    int64_t bidx[2] = {tm - tn + band_size, tn};
+    int64_t bidx[2] = {band_row(tm, tn), tn};
     return band->data_of(bidx, 2);
   }
   return off_band->data_of(idx, n);

@@ -138,9 +138,12 @@ struct SymBlockCyclic : BlockCyclic {
 };
 
 // Band: tiles with |m - n| <= band_size live in `band` (a 2D block-cyclic of
-// (2*band_size+1) x nt tiles), the rest in `off_band`.
+// (2*band_size+1) x nt tiles, row m - n + band_size; symmetric: band_size+1
+// rows, row |m - n|), the rest in `off_band`.
 struct BandMatrix : TiledMatrix {
   int band_size = 0;
+  bool sym = false;
+  int64_t band_row(int64_t tm, int64_t tn) const { return sym ? std::llabs(tm - tn) : tm - tn + band_size; }
   BlockCyclic* band = nullptr;
   BlockCyclic* off_band = nullptr;
   void init_band(BlockCyclic* band, BlockCyclic* off_band, int band_size);

@@ -181,6 +181,11 @@ struct KernelBatch {
   std::vector<std::function<void(hipStream_t)>> generic;  // other kernels, launched in order
   bool critical = false;  // launched on the critical stream: waves at raised issue priority
   bool one_per_cu = false;  // bulk 128x128 GEMMs padded to one workgroup per CU (room for critical kernels)
+  // critical-path launch (only tasks at or above the critical threshold): its
+  // workgroups claim their CUs, and bulk GEMM waves on a claimed CU pause
+  // (kernels: g_crit_cu, bulk_yield) so the chain runs at idle speed
+  int claim_cus = 0;  // 1: tile-POTRF steps claim, 2: every kernel of the launch
+  bool bulk_yield = false;  // bulk launch: poll the claims
   bool empty() const { return gemm.empty() && trsm.empty() && potrf.empty() && trsm_w.empty() && stencil.empty() && qr_panel.empty() && qr_apply.empty() && generic.empty(); }
   void clear() { gemm.clear(); trsm.clear(); potrf.clear(); trsm_w.clear(); stencil.clear(); qr_panel.clear(); qr_apply.clear(); generic.clear(); }
 };

@@ -1105,6 +1105,11 @@ void HipDevice::launch_group(int s) {
   if (!batches[s].empty()) {
     batches[s].critical = s == 0 && nb_exec_streams >= 2 && wave_priority;
     batches[s].one_per_cu = s > 0 && bulk_one_per_cu;
+    // cooperative CU yield: a critical-stream group headed by a critical-path
+    // task claims its CUs (1: the tile POTRF steps only, 2: every kernel of the
+    // group); bulk GEMMs pause on claimed CUs
+    batches[s].claim_cus = s == 0 && cu_yield > 0 && round_tasks[0][0]->task->priority >= critical_threshold ? cu_yield : 0;
+    batches[s].bulk_yield = s > 0 && cu_yield > 0;
     if (roctx) {
       // rocprofv3 --marker-trace: which tasks each launched group carried
       char label[96];
@@ -1440,6 +1445,7 @@ void hip_devices_init(Context* ctx) {
   const bool cow = params.reg_int("device", "hip", "complete_on_workers", "Release completed GPU tasks (successor activation) on the compute threads instead of the manager (measured no faster on DPOTRF; breaks the multi-rank DTD stencil: off)", 0) != 0;
   int maxg = (int)params.reg_int("device", "hip", "max_inflight_batches", "Launched kernel groups per bulk stream before new bulk tasks wait for a larger batch (0 = no limit)", 2);
   const int ccap = (int)params.reg_int("device", "hip", "critical_bulk_cap", "Launched kernel groups per bulk stream while the critical stream has work in flight (0 = max_inflight_batches)", 0);
+  const int cuy = (int)params.reg_int("device", "hip", "cu_yield", "Cooperative CU yield: critical-path kernels claim their CUs and bulk GEMM workgroups on a claimed CU pause until it is free (0 off, 1 tile-POTRF steps claim, 2 every kernel of a critical group claims)", 0);
   const bool csplit = params.reg_int("device", "hip", "critical_split", "Critical-path tasks leave the critical stream as a group of their own and their successors are dispatched before other completions are released", 0) != 0;
   if (enabled == 0) return;
   int count = 0;
@@ -1472,6 +1478,7 @@ void hip_devices_init(Context* ctx) {
     d->max_inflight_groups = maxg;
     d->critical_bulk_cap = ccap;
     d->critical_split = csplit;
+    d->cu_yield = cuy;
     d->sort_pending = sortp != 0;
     d->complete_on_workers = cow;
     d->trace_launches = trace;

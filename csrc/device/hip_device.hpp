@@ -192,7 +192,8 @@ struct HipDevice : Device {
   uint32_t rr_stream = 0;
   int max_inflight_groups = 2;  // bulk streams: launched groups in flight before new bulk work waits (0 = no limit)
   int critical_bulk_cap = 0;    // the same limit while the critical stream has work in flight (0 = max_inflight_groups)
-  bool critical_split = false;  // critical tasks leave stream 0 as their own group; their release goes first
+  bool critical_split = false;
+  int cu_yield = 0;  // critical tasks leave stream 0 as their own group; their release goes first
   double us_busy = 0;
 
   bool is_gpu() const override { return true; }

@@ -37,6 +37,8 @@ constexpr int kMaxGemmBatch = 40;
 struct GemmBatchArgs {
   int count;
   int prio;  // critical-path launch: raise the waves' issue priority (s_setprio)
+  int claim; // critical-path launch: claim the CUs (bulk waves there pause)
+  int yield; // bulk launch: pause while the CU hosts claimed critical work
   int total_tiles;
   // split-K tail: workgroups [main_tiles, grid) each take 1/ksplit of the K range
   // of one of the last (total_tiles - main_tiles) tiles and add alpha * partial
@@ -59,6 +61,36 @@ static thread_local int t_launch_prio = 0;
 // keeps room for a critical-path tile-POTRF step workgroup (78 KB)
 static thread_local int t_launch_pad = 0;
 #define PARSEC_WAVE_PRIO(p) do { if (p) __builtin_amdgcn_s_setprio(2); } while (0)
+// critical-path launch of this thread: its workgroups claim their CUs
+static thread_local int t_launch_claim = 0;
+// bulk launch of this thread: its GEMM waves yield claimed CUs
+static thread_local int t_launch_yield = 0;
+
+// ---- Cooperative CU yield. A critical-path workgroup (tile POTRF step, the
+// critical TRSM / SYRK GEMMs) counts itself into g_crit_cu[its CU] while it
+// runs; a bulk GEMM workgroup on the same CU polls that count once per k-tile
+// and sleeps while it is non-zero, so the critical workgroup gets the CU's MFMA
+// / LDS / issue bandwidth to itself (beside bulk waves it ran 2-4x slower:
+// profiles/r4_chain16_breakdown.txt). Only the CUs that host critical work
+// pause; a pause is bounded (kYieldMaxPolls) so a stale count can never stall
+// bulk work. One counter per CU: XCC id x (CU, SH, SE) bits of HW_ID.
+__device__ int g_crit_cu[8 * 256];
+__device__ __forceinline__ int cu_key() {
+  // HW_REG_HW_ID (4) bits [15:8] = CU_ID, SH_ID, SE_ID; HW_REG_XCC_ID (20) bits [3:0]
+  const unsigned hw = __builtin_amdgcn_s_getreg((7 << 11) | (8 << 6) | 4);
+  const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
+  return (int)(((xcc & 7u) << 8) | (hw & 0xffu));
+}
+__device__ __forceinline__ void crit_claim(int on) {
+  if (on && threadIdx.x == 0) __hip_atomic_fetch_add(&g_crit_cu[cu_key()], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void crit_release(int on) {
+  if (!on) return;
+  __syncthreads();  // every wave of the workgroup is done
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(&g_crit_cu[cu_key()], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr int kYieldMaxPolls = 2000;  // x ~0.1 us sleep: at most ~0.2 ms of pause per k-tile
+__device__ __forceinline__ int crit_count(int key) { return __hip_atomic_load(&g_crit_cu[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 template <class Args>
 __device__ __forceinline__ int find_desc(const Args& a, const int* starts, int t) {
@@ -124,6 +156,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
   if (d.lower_only && n0 > m0 + BM - 1) return;
 
   const int tid = threadIdx.x;
+  const int ykey = args.yield ? cu_key() : 0;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
@@ -137,6 +170,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
   const int kbeg = ks * kchunk;
   if (kbeg >= kfull) return;
   const int K = min(kfull, kbeg + kchunk) - kbeg;
+  crit_claim(args.claim);
   const double* __restrict__ A = d.A + (TRANSA ? (size_t)kbeg : (size_t)kbeg * lda);
   const double* __restrict__ B = d.B + (TRANSB ? (size_t)kbeg * ldb : (size_t)kbeg);
   // 16-byte loads when every row pair is aligned and fully inside the tile
@@ -262,6 +296,12 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
     const int cur = NBUF == 2 ? (kt & 1) : 0;
+    if (args.yield && tid < 64) {
+      // wave 0 sleeps while this CU hosts critical work; the other waves wait
+      // for it at the k-tile barrier
+      int polls = 0;
+      while (crit_count(ykey) > 0 && polls++ < kYieldMaxPolls) __builtin_amdgcn_s_sleep(4);
+    }
     if (kt + 1 < nkt) load_tile((kt + 1) * BK);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
@@ -307,6 +347,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
         }
       }
     }
+  crit_release(args.claim);
 }
 
 // ========================================================= diag blocks (4 waves)
@@ -600,6 +641,8 @@ static inline int gemm_slots() { return t_launch_pad ? std::max(1, g_gemm_slots 
 template <int BM, int BN, int BK, int WM, int WN, int NBUF, int OCC = WM * WN / 2>
 static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hipStream_t stream) {
   a.prio = t_launch_prio;
+  a.claim = t_launch_claim >= 2;
+  a.yield = t_launch_yield;
   int total = 0;
   bool full = g_gemm_full != 0;
   for (int i = 0; i < n; ++i) {
@@ -1403,6 +1446,7 @@ struct PotrfStepArgs {
   int* info;
   int lda, ldw, nb; // nb = n / 64 blocks
   int stamp;        // record phase clocks of the DIAG item (diagnostics)
+  int claim;        // critical-path launch: claim the CUs
   int j;            // step (-1: first launch, nb - 1: last launch)
   // item ranges: [0, n_diag) DIAG, then TRAIL, RUPD, LW, XW, ZERO
   int n_diag, n_trail, n_rupd, n_lw, n_xw, n_zero;
@@ -1440,8 +1484,14 @@ __device__ __forceinline__ void blk_put(Blk& S, const BlkRegs& R, bool t) {
 // next to ONE resident 128 x 128 GEMM workgroup (74 KB of LDS), so critical-path
 // work starts as soon as a bulk workgroup retires instead of waiting for a CU to
 // drain completely (the 120 KB version waited 1.2 ms per tile POTRF at 16k).
+__device__ __forceinline__ void dpotrf_step(const PotrfStepArgs& a, double* pool);
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void dpotrf_step_kernel(const PotrfStepArgs a) {
   __shared__ double pool[2 * 64 * kPL];
+  crit_claim(a.claim);
+  dpotrf_step(a, pool);
+  crit_release(a.claim);
+}
+__device__ __forceinline__ void dpotrf_step(const PotrfStepArgs& a, double* pool) {
   static_assert(kDiagPoolDoubles <= 64 * kPL, "diag_factor_inv scratch exceeds one staging block");
   __builtin_amdgcn_s_setprio(2);  // the tile POTRF is the critical path
   Blk& S0 = *reinterpret_cast<Blk*>(pool);
@@ -1624,6 +1674,7 @@ void launch_potrf_steps(const PotrfDesc& p, hipStream_t stream, double* ws) {
     spread = e ? atoi(e) : 1;  // profiles/r3_potrf_spread_ab.txt
   }
   a.stamp = (g_potrf_stamp_mode ? 1 : 0) | (spread ? 2 : 0);
+  a.claim = t_launch_claim >= 1;
   const int nb = p.n / 64;
   a.nb = nb;
   const bool w = p.W_out != nullptr;
@@ -1723,16 +1774,21 @@ size_t kernel_batch_workspace_bytes(const KernelBatch& b) {
 void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal, void* ws) {
   (void)device_ordinal;
   struct PrioScope {
-    int prev, prev_pad;
-    PrioScope(bool on, int pad) : prev(kern::t_launch_prio), prev_pad(kern::t_launch_pad) {
+    int prev, prev_pad, prev_claim, prev_yield;
+    PrioScope(bool on, int pad, int claim, bool yield)
+        : prev(kern::t_launch_prio), prev_pad(kern::t_launch_pad), prev_claim(kern::t_launch_claim), prev_yield(kern::t_launch_yield) {
       kern::t_launch_prio = on ? 1 : 0;
       kern::t_launch_pad = pad;
+      kern::t_launch_claim = claim;
+      kern::t_launch_yield = yield ? 1 : 0;
     }
     ~PrioScope() {
       kern::t_launch_prio = prev;
       kern::t_launch_pad = prev_pad;
+      kern::t_launch_claim = prev_claim;
+      kern::t_launch_yield = prev_yield;
     }
-  } prio_scope(b.critical, b.one_per_cu ? 8192 : 0);
+  } prio_scope(b.critical, b.one_per_cu ? 8192 : 0, b.claim_cus, b.bulk_yield);
   // critical-path kernels first: POTRF, then TRSM, then the GEMM/SYRK updates
   for (auto& p : b.potrf) {
     if (kern::potrf_steps_eligible(p)) kern::launch_potrf_steps(p, stream, static_cast<double*>(ws));

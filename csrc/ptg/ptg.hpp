@@ -218,6 +218,7 @@ class PtgTaskpool : public Taskpool {
   // tasks, then each first activation) instead of enumerating the whole local
   // task space at startup (reference jdf2c.c dynamic termination detection).
   bool dynamic_termdet = false;
+  bool dynamic_task_count() const override { return dynamic_termdet; }
   // ptgpp --dep-management: "index-array" (dense per-class slot arrays, the
   // reference default) or "dynamic-hash-table" (sharded hash of pending tasks);
   // MCA ptg_dep_management overrides the compiled choice.

@@ -269,6 +269,25 @@ typedef struct parsec_matrix_sym_block_cyclic_s {
 void parsec_matrix_sym_block_cyclic_init(parsec_matrix_sym_block_cyclic_t* dc, parsec_matrix_type_t mtype, int myrank, int mb, int nb, int lm, int ln, int i,
                                          int j, int m, int n, int p, int q, parsec_matrix_uplo_t uplo);
 
+/* band matrices (reference two_dim_rectangle_cyclic_band.h, sym_..._band.h):
+ * tiles with |m - n| < band_size live in `band` (general: 2 band_size - 1 rows,
+ * row m - n + band_size - 1; symmetric: band_size rows, row |m - n|), the others
+ * in `off_band`. Initialise band and off_band first, then the band structure. */
+typedef struct parsec_matrix_block_cyclic_band_s {
+  parsec_tiled_matrix_t super;
+  parsec_matrix_block_cyclic_t band;
+  parsec_matrix_block_cyclic_t off_band;
+  unsigned int band_size;
+} parsec_matrix_block_cyclic_band_t;
+void parsec_matrix_block_cyclic_band_init(parsec_matrix_block_cyclic_band_t* desc, int nodes, int myrank, int band_size);
+typedef struct parsec_matrix_sym_block_cyclic_band_s {
+  parsec_tiled_matrix_t super;
+  parsec_matrix_block_cyclic_t band;
+  parsec_matrix_sym_block_cyclic_t off_band;
+  unsigned int band_size;
+} parsec_matrix_sym_block_cyclic_band_t;
+void parsec_matrix_sym_block_cyclic_band_init(parsec_matrix_sym_block_cyclic_band_t* desc, int nodes, int myrank, int band_size);
+
 /* tabular: an explicit (rank, vpid) per tile, column major (reference
  * data_dist/matrix/two_dim_tabular.h:55-68); the runtime allocates the local
  * tiles, `data` of a local element then points at its storage */

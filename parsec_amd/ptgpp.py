@@ -62,12 +62,18 @@ def compile_flags(hip=False):
     return ["g++", "-std=c++20", "-O2"] + inc, libs
 
 
-def build_program(jdf, outdir, extra_sources=(), hip=None, name=None, flags=()):
+# JDF bodies written in C (the reference's): compiled as C++ with C's lenient rules
+C_BODIES = ("-fpermissive", "-Drestrict=__restrict__", "-w")
+
+
+def build_program(jdf, outdir, extra_sources=(), hip=None, name=None, flags=(), cxxflags=()):
+    """cxxflags: extra compiler flags, e.g. C_BODIES for JDFs whose C code
+    relies on C rules (implicit void * conversions, `restrict`)."""
     cpp, _ = compile_jdf(jdf, outdir, name, flags=flags)
     hip = _has_hip_body(jdf) if hip is None else hip
     cc, libs = compile_flags(hip)
     exe = os.path.splitext(cpp)[0]
-    cmd = cc + [f"-I{outdir}", cpp] + list(extra_sources) + ["-o", exe] + libs
+    cmd = cc + list(cxxflags) + [f"-I{outdir}", f"-I{os.path.dirname(os.path.abspath(jdf))}", cpp] + list(extra_sources) + ["-o", exe] + libs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise CompileError(" ".join(cmd) + "\n" + r.stderr[-6000:])

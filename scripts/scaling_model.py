@@ -1,0 +1,212 @@
+"""Discrete-event MODEL of tiled DPOTRF (lower) on 1/2/4/8 MI355X ranks.
+
+This is a PREDICTION tool, not a measurement: the driver's 8-GPU node is the
+only place the multi-GPU numbers can be measured (every gpurun box has one
+GPU). It replays the task graph the runtime executes (csrc/algos/jdf/dpotrf_L.jdf,
+reference dplasma zpotrf_L.jdf) on a model of the machine:
+
+  * one rank per GPU, tile (m, n) on rank (m % P) * Q + (n % Q) of a P x Q grid
+    (bench.py grid_of; reference two_dim_rectangle_cyclic.c rank_of);
+  * per GPU a BULK server that runs TRSM / SYRK / GEMM one after another in
+    task-priority order at the measured grouped-GEMM rate (a fluid model of the
+    2 bulk streams: the GPU is throughput-shared, so serial-at-full-rate gives
+    the same completion profile), and a CRITICAL lane for POTRF(k) with the
+    measured tile-POTRF latency under load (it runs beside bulk work on the
+    critical stream, profiles/r4_chain*.txt);
+  * a tile produced on rank r and read by tasks on rank s != r crosses the
+    (r, s) xGMI link ONCE (the runtime's per-rank activation aggregation), after
+    a per-message latency; each directed link carries one transfer at a time.
+
+Calibration: --gemm-tf is the sustained bulk rate; the 1-rank prediction is
+compared with the measured 1-GPU number (BENCH json) so the residual model error
+is visible next to the prediction.
+
+usage: python scripts/scaling_model.py [--n 65536 --nb 1024] [--gemm-tf 66]
+       [--potrf-us 520] [--link-gbs 50] [--lat-us 25] [--ranks 1 2 4 8]
+"""
+import argparse
+import heapq
+import itertools
+
+
+def grid_of(n):
+    # bench.py grid_of: the most square P x Q with P >= Q
+    best = (n, 1)
+    for q in range(1, n + 1):
+        if n % q == 0 and n // q >= q:
+            best = (n // q, q)
+    return best
+
+
+def simulate(NT, nb, P, Q, gemm_tf, potrf_us, link_gbs, lat_us, syrk_eff=0.85, trsm_eff=1.0):
+    R = P * Q
+
+    def owner(m, n):
+        return (m % P) * Q + (n % Q)
+
+    g_us = 2.0 * nb ** 3 / (gemm_tf * 1e12) * 1e6
+    cost = {"POTRF": potrf_us, "TRSM": g_us / trsm_eff, "SYRK": g_us / 2 / syrk_eff, "GEMM": g_us}
+    xfer_us = nb * nb * 8 / (link_gbs * 1e9) * 1e6 + lat_us
+
+    # ---- task graph: name -> (rank, kind, priority, successors); deps counted
+    tasks, nd = {}, {}
+
+    def add(t, rank, kind, prio):
+        tasks[t] = (rank, kind, prio, [])
+        nd.setdefault(t, 0)
+
+    def dep(a, b):
+        tasks[a][3].append(b)
+        nd[b] = nd.get(b, 0) + 1
+
+    for k in range(NT):
+        # priorities of dpotrf_L.jdf: the panel chain first, then by k
+        add(("POTRF", k), owner(k, k), "POTRF", (1 << 30) - k)
+        for m in range(k + 1, NT):
+            add(("TRSM", m, k), owner(m, k), "TRSM", (1 << 29) - k * NT + (NT - m) if m == k + 1 else (1 << 28) - k * NT - m)
+            add(("SYRK", k, m), owner(m, m), "SYRK", (1 << 29) - k if m == k + 1 else (1 << 27) - k * NT - m)
+            for n in range(k + 1, m):
+                add(("GEMM", m, n, k), owner(m, n), "GEMM", ((1 << 27) if n == k + 1 else 0) - k * NT * NT - m * NT - n)
+    for k in range(NT):
+        if k > 0:
+            dep(("SYRK", k - 1, k), ("POTRF", k))
+        for m in range(k + 1, NT):
+            dep(("POTRF", k), ("TRSM", m, k))
+            if k > 0:
+                dep(("GEMM", m, k, k - 1), ("TRSM", m, k))
+            dep(("TRSM", m, k), ("SYRK", k, m))
+            if k > 0:
+                dep(("SYRK", k - 1, m), ("SYRK", k, m))
+            for n in range(k + 1, m):
+                dep(("TRSM", m, k), ("GEMM", m, n, k))
+                dep(("TRSM", n, k), ("GEMM", m, n, k))
+                if k > 0:
+                    dep(("GEMM", m, n, k - 1), ("GEMM", m, n, k))
+
+    # ---- event simulation
+    seq = itertools.count()
+    ev = []  # (time, seq, kind, payload)
+    bulk_q = [[] for _ in range(R)]
+    crit_q = [[] for _ in range(R)]
+    bulk_busy = [False] * R
+    crit_busy = [False] * R
+    link_free = {}  # (src, dst) -> time the link is free
+    arrived = {}  # (producer, dst rank) -> arrival time (None: in flight)
+    waiting = {}  # (producer, dst rank) -> [successors waiting for that tile]
+    busy_us = [0.0] * R
+    bytes_sent = 0
+    now = 0.0
+
+    def ready(t, at):
+        rank, kind, prio, _ = tasks[t]
+        q = crit_q[rank] if kind == "POTRF" else bulk_q[rank]
+        heapq.heappush(q, (-prio, next(seq), t))
+        heapq.heappush(ev, (at, next(seq), "kick", rank))
+
+    def satisfy(t, at):
+        nd[t] -= 1
+        if nd[t] == 0:
+            ready(t, at)
+
+    def kick(rank, at):
+        if not crit_busy[rank] and crit_q[rank]:
+            _, _, t = heapq.heappop(crit_q[rank])
+            crit_busy[rank] = True
+            heapq.heappush(ev, (at + cost["POTRF"], next(seq), "done", (t, "crit")))
+        if not bulk_busy[rank] and bulk_q[rank]:
+            _, _, t = heapq.heappop(bulk_q[rank])
+            bulk_busy[rank] = True
+            c = cost[tasks[t][1]]
+            busy_us[rank] += c
+            heapq.heappush(ev, (at + c, next(seq), "done", (t, "bulk")))
+
+    for t in tasks:
+        if nd[t] == 0:
+            ready(t, 0.0)
+    finish = 0.0
+    while ev:
+        now, _, kind, p = heapq.heappop(ev)
+        if kind == "kick":
+            kick(p, now)
+        elif kind == "done":
+            t, lane = p
+            rank = tasks[t][0]
+            if lane == "crit":
+                crit_busy[rank] = False
+            else:
+                bulk_busy[rank] = False
+            finish = max(finish, now)
+            for s in tasks[t][3]:
+                sr = tasks[s][0]
+                if sr == rank:
+                    satisfy(s, now)
+                    continue
+                key = (t, sr)
+                if key in arrived:
+                    if arrived[key] is None:
+                        waiting[key].append(s)
+                    else:
+                        satisfy(s, now)
+                    continue
+                # one transfer of the tile to that rank
+                arrived[key] = None
+                waiting[key] = [s]
+                start = max(now, link_free.get((rank, sr), 0.0))
+                link_free[(rank, sr)] = start + xfer_us - lat_us
+                bytes_sent += nb * nb * 8
+                heapq.heappush(ev, (start + xfer_us, next(seq), "arrive", key))
+            kick(rank, now)
+        elif kind == "arrive":
+            arrived[p] = now
+            for s in waiting.pop(p):
+                satisfy(s, now)
+    assert all(v == 0 for v in nd.values()), "graph did not drain"
+    n = NT * nb
+    flops = n ** 3 / 3.0
+    return {"ranks": R, "grid": f"P{P}xQ{Q}", "span_ms": finish / 1e3, "tflops": flops / (finish * 1e-6) / 1e12,
+            "bulk_util": sum(busy_us) / (R * finish), "xgmi_GB": bytes_sent / 1e9}
+
+
+def critical_path_us(NT, potrf_us, trsm_us, syrk_us, xfer_us, P, Q):
+    # lower bound of the span ("chain ms"): POTRF(k) -> TRSM(k+1,k) ->
+    # SYRK(k,k+1) -> POTRF(k+1) with infinite GPUs; tile (k,k) -> (k+1,k)
+    # changes grid row (a hop when P > 1), (k+1,k) -> (k+1,k+1) changes grid
+    # column (a hop when Q > 1)
+    hops = (P > 1) + (Q > 1)
+    return NT * potrf_us + (NT - 1) * (trsm_us + syrk_us + hops * xfer_us)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--nb", type=int, default=1024)
+    ap.add_argument("--gemm-tf", type=float, default=66.0, help="sustained bulk GEMM rate per GPU (TF)")
+    ap.add_argument("--potrf-us", type=float, default=520.0, help="tile POTRF latency under load (us)")
+    ap.add_argument("--link-gbs", type=float, nargs="+", default=[50.0], help="effective GB/s per directed xGMI peer link")
+    ap.add_argument("--lat-us", type=float, default=25.0, help="per-message latency (activation + pull setup)")
+    ap.add_argument("--ranks", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--measured-1gpu-tf", type=float, default=None)
+    a = ap.parse_args()
+    NT = a.n // a.nb
+    print(f"MODEL PREDICTION (not a measurement): DPOTRF N={a.n} nb={a.nb} ({NT}x{NT} tiles), bulk GEMM {a.gemm_tf} TF/GPU, "
+          f"tile POTRF {a.potrf_us} us, message latency {a.lat_us} us")
+    for bw in a.link_gbs:
+        print(f"-- xGMI effective {bw} GB/s per directed peer link")
+        print(f"{'ranks':>5} {'grid':>6} {'span ms':>9} {'TF (job)':>9} {'TF/GPU':>7} {'eff':>5} {'bulk util':>9} {'xGMI GB':>8} {'chain ms':>8}")
+        base = None
+        for r in a.ranks:
+            P, Q = grid_of(r)
+            out = simulate(NT, a.nb, P, Q, a.gemm_tf, a.potrf_us, bw, a.lat_us)
+            base = base or out["tflops"]
+            eff = out["tflops"] / (base * r)
+            g_us = 2.0 * a.nb ** 3 / (a.gemm_tf * 1e12) * 1e6
+            chain = critical_path_us(NT, a.potrf_us, g_us, g_us / 2 / 0.85, a.nb * a.nb * 8 / (bw * 1e9) * 1e6 + a.lat_us, P, Q) / 1e3
+            print(f"{r:>5} {out['grid']:>6} {out['span_ms']:>9.1f} {out['tflops']:>9.1f} {out['tflops'] / r:>7.1f} {eff:>5.2f} {out['bulk_util']:>9.2f} {out['xgmi_GB']:>8.1f} {chain:>8.1f}")
+    if a.measured_1gpu_tf:
+        P, Q = grid_of(1)
+        one = simulate(NT, a.nb, P, Q, a.gemm_tf, a.potrf_us, a.link_gbs[0], a.lat_us)
+        print(f"calibration: model 1-GPU {one['tflops']:.1f} TF vs measured {a.measured_1gpu_tf:.1f} TF ({(one['tflops'] / a.measured_1gpu_tf - 1) * 100:+.1f} %)")
+
+
+if __name__ == "__main__":
+    main()

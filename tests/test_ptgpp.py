@@ -270,15 +270,6 @@ _REJECT = {
 }
 
 
-def _ref_jdfs():
-    out = []
-    for root, _, files in os.walk(REF):
-        for f in files:
-            if f.endswith(".jdf"):
-                out.append(os.path.relpath(os.path.join(root, f), REF))
-    return sorted(out)
-
-
 # Generated C++ that does not compile, because the JDF's own C code (prologue,
 # bodies, epilogue) programs against the reference's INTERNAL structures or
 # against MPI, not against the public API: the reason of each
@@ -286,14 +277,14 @@ _NO_COMPILE = {
     "parsec/data_dist/matrix/broadcast.jdf": "builds a collection with the internal object system (PARSEC_OBJ_NEW, parsec_data_t fields); public form: parsec_broadcast_New",
     "parsec/data_dist/matrix/diag_band_to_rect.jdf": "includes parsec/parsec_internal.h",
     "tests/apps/haar_tree/project.jdf": "tree_dist.h uses the internal parsec_hash_table class",
-    "tests/apps/haar_tree/project_dyn.jdf": "tree_dist.h uses the internal parsec_hash_table class",
+    "tests/apps/haar_tree/project_dyn.jdf": "tree_dist.h uses the internal parsec_hash_table class (public-API port: tests/jdf/project_dyn.jdf)",
     "tests/apps/haar_tree/walk.jdf": "tree_dist.h uses the internal parsec_hash_table class",
     "tests/apps/pingpong/bandwidth.jdf": "reads context->virtual_processes (internal)",
     "tests/collections/redistribute/redistribute_bound.jdf": "MPI calls outside PARSEC_HAVE_MPI guards, context->virtual_processes",
     "tests/collections/redistribute/redistribute_check.jdf": "MPI calls outside PARSEC_HAVE_MPI guards",
     "tests/collections/redistribute/redistribute_check2.jdf": "MPI calls outside PARSEC_HAVE_MPI guards",
     "tests/collections/redistribute/redistribute_no_optimization.jdf": "MPI calls outside PARSEC_HAVE_MPI guards",
-    "tests/collections/two_dim_band/two_dim_band.jdf": "reads this_task->data._f_Y (the generated task struct layout)",
+    "tests/collections/two_dim_band/two_dim_band.jdf": "reads this_task->data._f_Y (the generated task struct layout; public-API port: tests/jdf/two_dim_band.jdf)",
     "tests/dsl/ptg/choice/choice.jdf": "reads taskpool->tdm.module (termination detector internals)",
     "tests/dsl/ptg/choice/choice2.jdf": "reads task->parsec_object (object system internals)",
     "tests/dsl/ptg/complex_deps.jdf": "PARSEC_OBJ_RETAIN on a collection (object system)",
@@ -372,6 +363,39 @@ def test_reference_examples_run(tmp_path, name, expect):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=60, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
     assert r.returncode == 0, r.stdout + r.stderr
     assert expect in r.stdout, r.stdout
+
+
+@pytest.mark.parametrize("nranks,args", [(1, ["16", "4", "2", "1", "1"]), (2, ["24", "4", "2", "2", "1"]), (4, ["24", "4", "2", "2", "2"])])
+def test_two_dim_band(tmp_path, nranks, args):
+    """Port of the reference's tests/collections/two_dim_band (main.c:1-160,
+    two_dim_band.jdf): general (2B-1 band rows) and symmetric upper (B band
+    rows) band collections over P x Q grids with their own band grid P_BAND;
+    tasks write every tile through the band collection, each rank checks the
+    values and that band / off-band tiles live in the right storage."""
+    from parsec_amd.launch import launch
+
+    exe = ptgpp.build_program(os.path.join(JDF, "two_dim_band.jdf"), str(tmp_path), cxxflags=ptgpp.C_BODIES)
+    rc, outs = launch(nranks, [exe] + args, timeout=120, capture=True)
+    text = "".join(o or "" for o, _ in outs)
+    assert rc == 0, text + "".join(e or "" for _, e in outs)
+    assert text.count(" ok") == nranks and "bad 0" in text and "FAILED" not in text
+
+
+@pytest.mark.parametrize("nranks", [1, 3])
+def test_project_dyn(tmp_path, nranks):
+    """Port of the reference's tests/apps/haar_tree/project_dyn.jdf: an adaptive
+    wavelet projection whose binary tree (and task count) is only known at run
+    time (%option dynamic, make_key_fn, startup_fn); on several ranks the
+    taskpool runs under the fourcounter detector. Every rank checks the nodes it
+    holds against the sequential recursion (9367 nodes, depth 16)."""
+    from parsec_amd.launch import launch
+
+    exe = ptgpp.build_program(os.path.join(JDF, "project_dyn.jdf"), str(tmp_path), cxxflags=ptgpp.C_BODIES)
+    rc, outs = launch(nranks, [exe, "1e-6", "0.5"], timeout=120, capture=True)
+    text = "".join(o or "" for o, _ in outs)
+    assert rc == 0, text + "".join(e or "" for _, e in outs)
+    held = sum(int(l.split(" nodes ")[1].split()[0]) for l in text.splitlines() if l.startswith("project_dyn rank"))
+    assert held == 9367 and text.count("bad 0") == nranks, text
 
 
 @pytest.mark.parametrize("nranks", [2, 3, 4])

@@ -1,0 +1,37 @@
+"""The DPOTRF scaling model (scripts/scaling_model.py) behind
+profiles/r4_scaling_prediction.txt: the graph drains, one rank moves no bytes,
+and more ranks never predict less than the critical-path bound allows."""
+import importlib.util
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+spec = importlib.util.spec_from_file_location("scaling_model", os.path.join(ROOT, "scripts", "scaling_model.py"))
+sm = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(sm)
+
+
+def test_grid_matches_bench():
+    assert [sm.grid_of(n) for n in (1, 2, 4, 8)] == [(1, 1), (2, 1), (2, 2), (4, 2)]
+
+
+def test_one_rank_is_work_bound():
+    NT, nb = 12, 1024
+    out = sm.simulate(NT, nb, 1, 1, gemm_tf=66.0, potrf_us=0.0, link_gbs=50.0, lat_us=25.0)
+    assert out["xgmi_GB"] == 0
+    # with a free critical lane the bulk server never idles once started
+    g = 2.0 * nb ** 3 / 66e12 * 1e6
+    work = sum((NT - k - 1) * (g + g / 2 / 0.85) + (NT - k - 1) * (NT - k - 2) / 2 * g for k in range(NT))
+    assert abs(out["span_ms"] * 1e3 - work) / work < 0.02
+
+
+def test_more_ranks_more_throughput_and_traffic():
+    NT, nb = 16, 1024
+    prev = None
+    for r in (1, 2, 4, 8):
+        P, Q = sm.grid_of(r)
+        out = sm.simulate(NT, nb, P, Q, gemm_tf=66.0, potrf_us=350.0, link_gbs=50.0, lat_us=25.0)
+        chain = sm.critical_path_us(NT, 350.0, 2.0 * nb ** 3 / 66e12 * 1e6, nb ** 3 / 66e12 * 1e6 / 0.85, nb * nb * 8 / 50e9 * 1e6 + 25.0, P, Q)
+        assert out["span_ms"] * 1e3 >= chain * 0.999
+        if prev:
+            assert out["tflops"] >= prev["tflops"] * 0.99 and out["xgmi_GB"] > prev["xgmi_GB"]
+        prev = out

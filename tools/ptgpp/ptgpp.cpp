@@ -946,6 +946,12 @@ struct Gen {
     c << "  [[maybe_unused]] auto* __parsec_tp = &__parsec_tp_ref;\n";
     c << "  " << bind_globals() << "\n";
     c << "  " << bind_locals(f, "this_task->locals") << "\n";
+    // writable view of the task's locals: `locals.X.value = v` in a body changes
+    // the value the output guards of this task see (reference
+    // this_task->locals.X.value, e.g. haar_tree/project_dyn.jdf)
+    c << "  [[maybe_unused]] struct __locals_view { ";
+    for (auto& l : f.locals) c << "parsec::ptg::LocalSlot " << l.name << "; ";
+    c << "} &locals = *reinterpret_cast<__locals_view*>(this_task->locals);\n";
     for (size_t k = 0; k < f.flows.size(); ++k) {
       const Flow& fl = f.flows[k];
       if (fl.access == "CTL") continue;
@@ -1071,8 +1077,8 @@ struct Gen {
         if (p->val == "off" || p->val == "false" || p->val == "0") c << "    d.flags |= parsec::TC_NO_PROFILE;\n";
       if (const Prop* p = find_prop(f.props, "immediate"))
         if (p->val == "on" || p->val == "true" || p->val == "1") c << "    d.flags |= parsec::TC_IMMEDIATE;\n";
-      if (const Prop* p = find_prop(f.props, "make_key_fn")) c << "    d.make_key_fn = [](const parsec::Taskpool* tp, const int32_t* L) { return (uint64_t)" << p->val << "(tp, L); };\n";
-      if (const Prop* p = find_prop(f.props, "startup_fn")) c << "    d.startup_fn = [](const parsec::Taskpool* tp, std::vector<std::vector<int32_t>>& out) { " << p->val << "(tp, out); };\n";
+      if (const Prop* p = find_prop(f.props, "make_key_fn")) c << "    d.make_key_fn = [](const parsec::Taskpool* __ptp, const int32_t* __plocals) { return (uint64_t)" << p->val << "(__ptp, __plocals); };\n";
+      if (const Prop* p = find_prop(f.props, "startup_fn")) c << "    d.startup_fn = [](const parsec::Taskpool* __ptp, std::vector<std::vector<int32_t>>& __pout) { " << p->val << "(__ptp, __pout); };\n";
       if (const Prop* p = find_prop(f.props, "nb_local_tasks_fn")) c << "    d.nb_local_tasks_fn = [](const parsec::Taskpool* tp) { return (int64_t)" << p->val << "(tp); };\n";
       if (const Prop* p = find_prop(f.props, "flops")) c << "    d.flops = (double)(" << p->val << ");\n";
       auto prop_on = [&](const char* k) { const Prop* p = find_prop(f.props, k); return p && (p->val == "on" || p->val == "true" || p->val == "1"); };
@@ -1131,7 +1137,11 @@ struct Gen {
     for (auto& kv : j.options)
       if (kv.first == "nb_local_tasks_fn")
         c << "  (void)__has_nb_local;\n  __tp->nb_local_tasks_fn = [](const parsec::Taskpool* tp) { return (int64_t)" << kv.second << "(tp); };\n";
-    if (g_dynamic_termdet) c << "  __tp->dynamic_termdet = true;\n";
+    bool dyn = g_dynamic_termdet;
+    for (auto& kv : j.options)  // %option dynamic = ON (reference jdf.h: task counts known only at run time)
+      if ((kv.first == "dynamic" || kv.first == "termdet") && (kv.second == "ON" || kv.second == "on" || kv.second == "true" || kv.second == "1" || kv.second == "dynamic"))
+        dyn = true;
+    if (dyn) c << "  __tp->dynamic_termdet = true;\n";
     if (g_deps_mask) c << "  __tp->deps_mask_default = true;\n";
     c << "  __tp->dep_management = \"" << g_dep_management << "\";\n";
     c << "  __tp->finalize();\n  return __tp;\n}\n";
