@@ -58,6 +58,8 @@ int bind_thread_to_gpu_numa(int ordinal);
 // dst <- src (bytes) as a copy kernel on `stream` (hipStream_t); 0 on success.
 int device_copy_kernel(void* dst, const void* src, size_t bytes, void* stream);
 int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t bytes);
+// bytes moved by device_memcpy since start / the last reset: H2D, D2H, D2D
+void device_memcpy_stats(uint64_t out[3], bool reset);
 // The process-wide copy stream of HIP device `ordinal` (created on first use).
 hipStream_t gpu_copy_stream(int ordinal);
 int device_hip_ordinal(int device_index);  // -1 if not a HIP device

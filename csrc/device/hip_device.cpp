@@ -248,9 +248,16 @@ hipStream_t gpu_copy_stream(int ordinal) {
 // device's copy stream, ordered after earlier work of the null stream (like
 // hipMemcpy: initialisation kernels / memsets launched there), and the caller
 // waits for an event behind it (not for the whole stream's later work).
+static std::atomic<uint64_t> g_memcpy_bytes[3];  // H2D, D2H, D2D through device_memcpy
+
+void device_memcpy_stats(uint64_t out[3], bool reset) {
+  for (int i = 0; i < 3; ++i) out[i] = reset ? g_memcpy_bytes[i].exchange(0) : g_memcpy_bytes[i].load();
+}
+
 int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t bytes) {
   if (dst_dev == 0 && src_dev == 0) { std::memcpy(dst, src, bytes); return 0; }
   hipMemcpyKind k = dst_dev == 0 ? hipMemcpyDeviceToHost : src_dev == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  g_memcpy_bytes[k == hipMemcpyHostToDevice ? 0 : k == hipMemcpyDeviceToHost ? 1 : 2].fetch_add(bytes, std::memory_order_relaxed);
   const int dev = dst_dev != 0 ? dst_dev : src_dev;
   const int ord = device_hip_ordinal(dev);
   hipStream_t s = ord >= 0 ? gpu_copy_stream(ord) : nullptr;
@@ -1165,36 +1172,7 @@ void HipDevice::epilog(GpuTask* g) {
   }
 }
 
-namespace {
-// Internal task that releases a completed GPU task on a compute thread: the
-// dependency release of a finished batch (hundreds of activations when a panel
-// completes) then runs on every compute thread in parallel, by priority,
-// instead of serially on the manager between two launches.
-struct GpuCompleteClass : TaskClass {
-  GpuCompleteClass() {
-    name = "gpu_complete";
-    flags = TC_INTERNAL | TC_NO_PROFILE;
-    Chore ch;
-    ch.type = DEV_CPU;
-    ch.hook = [](ExecutionStream* es, Task* w) {
-      complete_task_execution(es, static_cast<Task*>(w->user));
-      return (int)HOOK_DONE;
-    };
-    chores.push_back(std::move(ch));
-  }
-  int complete_execution(ExecutionStream* es, Task* w) const override {
-    (void)es;
-    task_free(w);
-    return 0;
-  }
-};
-const GpuCompleteClass& gpu_complete_class() {
-  static GpuCompleteClass c;
-  return c;
-}
-}  // namespace
-
-void HipDevice::complete(GpuTask* g, bool small_group) {
+void HipDevice::complete(GpuTask* g) {
   Task* t = g->task;
   PARSEC_DEBUG(kVerbNoisier, "hip", "completed %s", t->task_class->describe(t).c_str());
   for (int fi = 0; fi < kMaxFlows; ++fi) if (g->dev_copy[fi]) lru_touch(g->dev_copy[fi]);
@@ -1203,32 +1181,11 @@ void HipDevice::complete(GpuTask* g, bool small_group) {
   t->gpu = nullptr;
   if (g->ev_out) put_event(g->ev_out);
   delete g;
-  // critical-path work (and tiny groups) is released here: its successors are
-  // few and the manager dispatches them to the GPU at once
-  const bool inline_release = small_group || t->priority >= critical_threshold;
-  if (complete_on_workers && !inline_release && ctx && !ctx->simulation && !ctx->all_es.empty()) {
-    Task* w = task_new(es, t->taskpool, &gpu_complete_class());
-    w->user = t;
-    w->priority = t->priority;
-    completions.push_back(w);
-  } else {
-    complete_task_execution(es, t);
-  }
+  // successors are released by the manager itself: it dispatches the GPU ones
+  // at once (releasing on the compute threads instead was measured no faster
+  // on DPOTRF and raced the multi-rank DTD stencil; removed in round 4)
+  complete_task_execution(es, t);
   inflight.fetch_sub(1, std::memory_order_acq_rel);
-}
-
-void HipDevice::flush_completions() {
-  if (completions.empty()) return;
-  // straight to the compute threads' queues (schedule_tasks from a manager
-  // would try to dispatch GPU work inline)
-  std::stable_sort(completions.begin(), completions.end(), [](Task* a, Task* b) { return a->priority > b->priority; });
-  const int nes = (int)ctx->all_es.size();
-  std::vector<std::vector<Task*>> per(nes);
-  for (size_t i = 0; i < completions.size(); ++i) per[(rr_complete + i) % nes].push_back(completions[i]);
-  rr_complete += (uint32_t)completions.size();
-  for (int i = 0; i < nes; ++i)
-    if (!per[i].empty()) ctx->scheduler->schedule(ctx->all_es[i], per[i].data(), (int)per[i].size(), 0);
-  completions.clear();
 }
 
 bool HipDevice::progress() {
@@ -1335,10 +1292,9 @@ bool HipDevice::progress() {
           PARSEC_HIP_CHECK(hipEventRecord(g->ev_out, s_copy));
           popping.push_back(g);
         } else {
-          complete(g, tasks.size() <= 2);
+          complete(g);
         }
       }
-      flush_completions();
       if (trace_launches)
         std::fprintf(stderr, "[engine] t=%llu R stream %d n=%zu release_us=%llu\n", (unsigned long long)(tr0 / 1000), s, tasks.size(),
                      (unsigned long long)((now_ns() - tr0) / 1000));
@@ -1365,10 +1321,9 @@ bool HipDevice::progress() {
       std::lock_guard<SpinLock> lk(d->lock);
       if (DataCopy* host = d->copy(0)) { host->version = g->dev_copy[fi]->version; host->coherency_state = COHERENCY_SHARED; }
     }
-    complete(g, false);
+    complete(g);
     did = true;
   }
-  flush_completions();
   return did;
 }
 
@@ -1442,7 +1397,6 @@ void hip_devices_init(Context* ctx) {
   const int hp_crit = (int)params.reg_int("device", "hip", "hp_on_critical_stream", "High-priority tasks below the critical threshold share the critical stream (1), go to the least loaded bulk stream (0; measured 36.0 vs 38.9 TF at 16k, profiles/r3_route_ab.txt), or get stream 1 to themselves (2, bulk on streams 2..)", 1);
   const bool wprio = params.reg_int("device", "hip", "wave_priority", "Kernels of the critical stream raise their waves' issue priority (s_setprio) over co-resident bulk waves", 1) != 0;
   const bool trace = params.reg_int("device", "hip", "trace_launches", "Print every launched kernel group (stream, tasks, batch sizes) to stderr", 0) != 0;
-  const bool cow = params.reg_int("device", "hip", "complete_on_workers", "Release completed GPU tasks (successor activation) on the compute threads instead of the manager (measured no faster on DPOTRF; breaks the multi-rank DTD stencil: off)", 0) != 0;
   int maxg = (int)params.reg_int("device", "hip", "max_inflight_batches", "Launched kernel groups per bulk stream before new bulk tasks wait for a larger batch (0 = no limit)", 2);
   const int ccap = (int)params.reg_int("device", "hip", "critical_bulk_cap", "Launched kernel groups per bulk stream while the critical stream has work in flight (0 = max_inflight_batches)", 0);
   const int cuy = (int)params.reg_int("device", "hip", "cu_yield", "Cooperative CU yield: critical-path kernels claim their CUs and bulk GEMM workgroups on a claimed CU pause until it is free (0 off, 1 tile-POTRF steps claim, 2 every kernel of a critical group claims)", 0);
@@ -1480,7 +1434,6 @@ void hip_devices_init(Context* ctx) {
     d->critical_split = csplit;
     d->cu_yield = cuy;
     d->sort_pending = sortp != 0;
-    d->complete_on_workers = cow;
     d->trace_launches = trace;
     reg.add(d);
     g_hip_devices.push_back(d);

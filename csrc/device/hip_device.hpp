@@ -145,10 +145,6 @@ struct HipDevice : Device {
   bool sort_pending = true;
   // completed GPU tasks are released (successor activation) by the compute
   // threads instead of the manager, which keeps launching critical work
-  bool complete_on_workers = false;
-  std::vector<Task*> completions;  // release tasks gathered during one progress pass
-  uint32_t rr_complete = 0;
-  void flush_completions();
   std::deque<W2RJob> w2r_jobs;
   size_t w2r_bytes_inflight = 0;
   bool start_w2r(size_t bytes);
@@ -212,7 +208,7 @@ struct HipDevice : Device {
   int stage_in(GpuTask* g);
   void finish_stage_in(GpuTask* g);
   void execute_ready();
-  void complete(GpuTask* g, bool small_group);
+  void complete(GpuTask* g);
   void epilog(GpuTask* g);
   void* cache_alloc(size_t bytes);
   void ensure_zone();  // zone_m held

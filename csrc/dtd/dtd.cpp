@@ -228,6 +228,42 @@ static DataCopy* snapshot_copy(DataCopy* src) {
 
 static DataCopy* newest_copy(Data* d);
 
+// The copy a remote shadow's received version lives in: same device as the
+// receive buffer (device memory from the tile-cache zone when it has room).
+static void shadow_copy_release(DataCopy* c) {
+  if (c->device_index == 0) std::free(c->device_private);
+  else if (c->snapshot_from_zone) (void)device_cache_free(c->device_index, c->device_private);
+  else device_free(c->device_index, c->device_private);
+  if (Data* d = c->original) {
+    d->lock.lock();
+    data_copy_detach(d, c, c->device_index);
+    d->lock.unlock();
+  }
+  delete c;
+}
+
+static DataCopy* shadow_copy_new(const DataCopy* src, size_t n) {
+  int dev = src->device_index;
+  void* p = dev != 0 ? device_cache_alloc(dev, std::max<size_t>(n, 64)) : nullptr;
+  const bool from_zone = p != nullptr;
+  if (dev != 0 && !p) p = device_alloc(dev, std::max<size_t>(n, 64));
+  if (!p) {
+    dev = 0;
+    if (posix_memalign(&p, 64, std::max<size_t>(n, 64))) fatal("DTD: out of memory for a received version");
+  }
+  if (n) device_memcpy(dev, p, src->device_index, src->device_private, n);
+  auto* nc = new DataCopy();
+  nc->device_private = p;
+  nc->device_index = (int8_t)dev;
+  nc->flags = DATA_FLAG_PARSEC_OWNED;
+  nc->coherency_state = COHERENCY_OWNED;
+  nc->dtt = src->dtt;
+  nc->release_fn = shadow_copy_release;
+  nc->snapshot_from_zone = from_zone && dev != 0;
+  return nc;
+}
+
+
 // A remote consumer was inserted after its local producer `w` completed: send
 // the producer's version of flow `flow` (still the tile's current data -- no
 // later writer can have been inserted before the consumer) unless that rank
@@ -368,7 +404,10 @@ DtdTask* DtdTaskpool::insert_task(DtdTaskClass* tc, int priority, const std::vec
       const bool same = w->rank == t->rank;
       if (same) {
         if (!(w->remote && t->remote)) add_edge(w, t, tl->writer_flow, a.flow, true);
-      } else if (needs_data) {
+      } else if (needs_data && !(w->remote && t->remote)) {
+        // (two shadows of OTHER ranks: the data goes from one to the other
+        // without this rank; an edge here would never be released and held
+        // the reader's shadow forever -- the 3+-rank LeakSanitizer report)
         if (!add_edge(w, t, tl->writer_flow, a.flow, true) && !w->remote && t->remote) {
           task_retain(w);
           late.emplace_back(w, tl->writer_flow);
@@ -771,22 +810,35 @@ void DtdTaskpool::finish_remote_activation(ExecutionStream* es, DtdTask* t, Remo
       d->owner_device = (int8_t)hc->device_index;
       inst[a.flow] = hc;
     } else {
-      // shadow Data: the received buffer becomes its current version
-      std::lock_guard<SpinLock> g(d->lock);
-      uint32_t v = d->newest_version() + 1;
-      for (int i = 0; i < kMaxDevices; ++i) { DataCopy* o = d->copy(i); if (o) o->coherency_state = COHERENCY_INVALID; }
-      DataCopy* nc = new DataCopy();
+      // shadow Data: the received bytes become its current version, in a copy
+      // on the device they arrived on (a halo pulled into HBM stays in HBM: the
+      // GPU tasks reading it stage nothing; round 3 went through host memory)
       size_t n = c->original ? c->original->nb_elts : d->nb_elts;
-      void* p = nullptr;
-      if (posix_memalign(&p, 64, std::max<size_t>(n, 64))) fatal("oom");
-      device_memcpy(0, p, c->device_index, c->device_private, n);
-      nc->device_private = p;
-      nc->flags = DATA_FLAG_PARSEC_OWNED;
-      nc->coherency_state = COHERENCY_OWNED;
-      nc->version = v;
-      if (d->nb_elts == 0) d->nb_elts = n;
-      data_copy_attach(d, nc, 0);
-      d->owner_device = 0;
+      DataCopy* nc = shadow_copy_new(c, n);
+      std::vector<DataCopy*> old;
+      {
+        std::lock_guard<SpinLock> g(d->lock);
+        const uint32_t v = d->newest_version() + 1;
+        // earlier received versions: detached (a task still reading one holds
+        // its own reference); engine cache copies: invalidated
+        for (int i = 0; i < kMaxDevices; ++i)
+          for (DataCopy* o = d->copy(i); o;) {
+            DataCopy* next = o->older;
+            if (o->release_fn == shadow_copy_release) {
+              data_copy_detach(d, o, i);
+              o->original = nullptr;
+              old.push_back(o);
+            } else {
+              o->coherency_state = COHERENCY_INVALID;
+            }
+            o = next;
+          }
+        nc->version = v;
+        if (d->nb_elts == 0) d->nb_elts = n;
+        data_copy_attach(d, nc, nc->device_index);
+        d->owner_device = nc->device_index;
+      }
+      for (DataCopy* o : old) data_copy_release(o);
       inst[a.flow] = nc;
     }
   }

@@ -642,6 +642,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("device_alloc", [](int dev, size_t bytes) { return (uintptr_t)device_alloc(dev, bytes); });
   m.def("device_free", [](int dev, uintptr_t p) { device_free(dev, (void*)p); });
   m.def("device_memcpy", [](int dd, uintptr_t dst, int sd, uintptr_t src, size_t n) { return device_memcpy(dd, (void*)dst, sd, (const void*)src, n); });
+  m.def("device_memcpy_stats", [](bool reset) {
+    uint64_t b[3];
+    device_memcpy_stats(b, reset);
+    py::dict d;
+    d["h2d"] = b[0];
+    d["d2h"] = b[1];
+    d["d2d"] = b[2];
+    return d;
+  }, py::arg("reset") = false, "Bytes moved by the blocking device_memcpy helper (H2D / D2H / D2D), optionally reset");
 
   // raw kernels (tests): descriptors built in python, device pointers as ints
   m.def("kernel_dgemm", [](uintptr_t A, uintptr_t B, uintptr_t C, int mm, int nn, int kk, int lda, int ldb, int ldc, double alpha, double beta, int transB, int lower, uintptr_t stream) {

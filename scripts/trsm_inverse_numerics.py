@@ -27,10 +27,34 @@ def spd_with_cond(n, cond, seed=0, graded=False, nb=None):
     [1, cond^-1/2] inside EVERY nb-tile, so every L(k,k) has cond ~ cond(A)^1/2
     (the adversarial case for the explicit inverse)."""
     rng = np.random.default_rng(seed)
+    if graded == "kahan":
+        # every diagonal tile's factor is a (transposed) Kahan triangle
+        # diag(1, s, s^2..) (I - c * strictly lower ones): ill-conditioned by its
+        # off-diagonal structure, NOT visible in the diagonal ratio; c is set so
+        # that cond(L(k,k)) ~ cond(A)^1/2
+        target = cond ** 0.5
+
+        def kahan(c):
+            sdiag = np.sqrt(1.0 - c * c)
+            K = np.tril(-c * np.ones((nb, nb)), -1) + np.eye(nb)
+            return sdiag ** np.arange(nb)[:, None] * K
+
+        lo, hi = 0.0, 0.5
+        for _ in range(60):
+            mid = 0.5 * (lo + hi)
+            lo, hi = (mid, hi) if np.linalg.cond(kahan(mid)) < target else (lo, mid)
+        K = kahan(lo)
+        L0 = np.zeros((n, n))
+        for t in range(n // nb):
+            L0[t * nb:(t + 1) * nb, t * nb:(t + 1) * nb] = K
+        L0 += np.tril(rng.standard_normal((n, n)) * (1e-3 / np.sqrt(n)), -nb)  # weak coupling below the tile diagonal
+        return L0 @ L0.T
     if graded == "tile":
-        L0 = np.tril(rng.standard_normal((n, n)) / np.sqrt(n), -1)
+        # L0 = D (I + E), E strictly lower and small: cond(L0) ~ cond(D) (an
+        # unscaled random triangle would be exponentially ill-conditioned)
+        E = np.tril(rng.standard_normal((n, n)) * (0.5 / np.sqrt(n)), -1)
         d = np.tile(np.geomspace(1.0, cond ** -0.5, nb), n // nb)
-        L0[np.diag_indices(n)] = d
+        L0 = d[:, None] * (np.eye(n) + E)
         return L0 @ L0.T
     q, _ = np.linalg.qr(rng.standard_normal((n, n)))
     s = np.geomspace(1.0, 1.0 / cond, n)
@@ -89,15 +113,17 @@ def metrics(A, L, Lref):
 def sweep(n, nbs, conds, graded):
     rows = []
     for cond in conds:
-        A = None if graded == "tile" else spd_with_cond(n, cond, graded=graded)
+        A = None if graded in ("tile", "kahan") else spd_with_cond(n, cond, graded=graded)
         for nb in nbs:
-            if graded == "tile":
-                A = spd_with_cond(n, cond, graded="tile", nb=nb)
+            if graded in ("tile", "kahan"):
+                A = spd_with_cond(n, cond, graded=graded, nb=nb)
             Lb = tiled_cholesky(A, nb, "blocked")
             Li = tiled_cholesky(A, nb, "inverse")
             rb, ri = metrics(A, Lb, Lb), metrics(A, Li, Lb)
             kdiag = max(np.linalg.cond(Lb[i * nb:(i + 1) * nb, i * nb:(i + 1) * nb]) for i in range(n // nb))
-            rows.append((cond, nb, kdiag, rb, ri))
+            # the runtime's on-device estimate: max |l_ii| / min |l_ii| per tile
+            dr = max(np.abs(np.diag(Lb)[i * nb:(i + 1) * nb]).max() / np.abs(np.diag(Lb)[i * nb:(i + 1) * nb]).min() for i in range(n // nb))
+            rows.append((cond, nb, kdiag, dr, rb, ri))
     return rows
 
 
@@ -106,13 +132,16 @@ def main():
     ap.add_argument("--n", type=int, default=2048)
     ap.add_argument("--nb", type=int, nargs="+", default=[512, 1024])
     ap.add_argument("--cond", type=float, nargs="+", default=[1e2, 1e4, 1e6, 1e8, 1e10, 1e12])
+    ap.add_argument("--family", nargs="+", default=["plain", "graded", "tile"])
     a = ap.parse_args()
-    names = {False: "Q diag(s) Q^T", True: "graded D A D", "tile": "L0 L0^T, diagonal of L0 swept inside every tile (worst case for the inverse)"}
-    for graded in (False, True, "tile"):
+    names = {False: "Q diag(s) Q^T", True: "graded D A D", "tile": "L0 L0^T, diagonal of L0 swept inside every tile",
+             "kahan": "L0 L0^T, every diagonal tile of L0 a Kahan triangle (ill-conditioned by structure, not by its diagonal)"}
+    fam = {"plain": False, "graded": True, "tile": "tile", "kahan": "kahan"}
+    for graded in [fam[f] for f in a.family]:
         print(f"-- n={a.n} {names[graded]}")
-        print(f"{'cond(A)':>8} {'nb':>5} {'max cond(Lkk)':>13} | {'bwd blk':>9} {'bwd inv':>9} | {'L diff':>9} | {'solv blk':>9} {'solv inv':>9}")
-        for cond, nb, kd, rb, ri in sweep(a.n, a.nb, a.cond, graded):
-            print(f"{cond:8.0e} {nb:5d} {kd:13.2e} | {rb[0]:9.2e} {ri[0]:9.2e} | {ri[1]:9.2e} | {rb[2]:9.2e} {ri[2]:9.2e}")
+        print(f"{'cond(A)':>8} {'nb':>5} {'max cond(Lkk)':>13} {'diag ratio':>10} | {'bwd blk':>9} {'bwd inv':>9} | {'L diff':>9} | {'solv blk':>9} {'solv inv':>9}")
+        for cond, nb, kd, dr, rb, ri in sweep(a.n, a.nb, a.cond, graded):
+            print(f"{cond:8.0e} {nb:5d} {kd:13.2e} {dr:10.2e} | {rb[0]:9.2e} {ri[0]:9.2e} | {ri[1]:9.2e} | {rb[2]:9.2e} {ri[2]:9.2e}")
 
 
 if __name__ == "__main__":

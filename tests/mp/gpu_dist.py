@@ -168,7 +168,15 @@ def case_dgeqrf(pa, torch, rank, size, job, N, nb, P, outdir, Q=1, dom=0):
 def case_stencil(pa, torch, rank, size, job, nx, ny, nz, b, iters):
     ctx = _setup(pa, rank, size, job)
     G = pa.StencilGrid(rank, size, nx, ny, nz, b, b, b, device=pa.first_gpu_device_index())
+    pa.device_memcpy_stats(True)
+    out0 = sum(d["bytes_out"] for d in pa.devices())
     _, _, par = pa.stencil3d_run(ctx, G, iters, 0.4, 0.1, True)
+    # the halo path on the device plane: received faces stay in HBM (no
+    # device -> host copy by the runtime, no engine write-back to host)
+    mc = pa.device_memcpy_stats(True)
+    out1 = sum(d["bytes_out"] for d in pa.devices())
+    cs = pa.comm_stats()
+    print(f"rank {rank} halo d2h {mc['d2h']} h2d {mc['h2d']} d2d {mc['d2d']} writeback {out1 - out0} get_ipc {cs.get('get_ipc', 0)}", flush=True)
     f = lambda v, n: (v + 1) / (n + 1) * (1 - (v + 1) / (n + 1))  # noqa: E731
     U = 64.0 * f(np.arange(nz), nz)[:, None, None] * f(np.arange(ny), ny)[None, :, None] * f(np.arange(nx), nx)[None, None, :]
     for _ in range(iters):

@@ -118,10 +118,18 @@ def test_dgeqrf_hqr_2x2_ipc(pa):
 
 def test_stencil_four_ranks_ipc(pa):
     """DTD 3D stencil over 4 ranks with GPU bodies: halo faces cross ranks
-    through the device plane."""
+    through the device plane and STAY on the device: the receiving rank's
+    shadow version is a device copy (csrc/dtd/dtd.cpp shadow_copy_new), so the
+    runtime copies zero bytes device -> host and writes nothing back to host
+    during the sweeps, while faces did arrive through IPC gets."""
     _gpu()
     for rc, out in _run("stencil", 4, 48, 40, 36, 16, 6):
         assert rc == 0, out
+        line = next(l for l in out.splitlines() if " halo d2h " in l)
+        f = line.split()
+        v = {f[i]: int(f[i + 1]) for i in range(2, len(f) - 1, 2)}
+        assert v["d2h"] == 0 and v["writeback"] == 0, line
+        assert v["get_ipc"] > 0, line
 
 
 def test_comm_engine_c_program_gpu_memory(tmp_path, pa):
