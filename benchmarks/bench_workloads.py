@@ -184,12 +184,13 @@ def bench_stencil(args):
     world, rank, local = _dist()
     import torch
 
-    torch.cuda.set_device(local)
+    dev = 0 if args.share_gpu else local  # --share-gpu: every rank on GPU 0 (halo-path validation, not scaling)
+    torch.cuda.set_device(dev)
     import parsec_amd as pa
 
     pa.require_native()
-    pa.mca_set("device_hip_mask", str(1 << local))
-    _comm(pa, world, rank, local)
+    pa.mca_set("device_hip_mask", str(1 << dev))
+    _comm(pa, world, rank, dev)
     ctx = pa.init(args.cores)
     # grid resident in HBM (the home device of every block and face buffer)
     G = pa.StencilGrid(rank, world, args.n, args.n, args.n, args.b, args.b, args.b, device=pa.first_gpu_device_index())
@@ -204,6 +205,8 @@ def bench_stencil(args):
     out = {"metric": "Gpoint-updates/s DTD 3D 7-point stencil", "value": round(gpts, 2), "unit": "Gpoints/s", "gflops": round(8 * gpts, 1),
            "n_gpus": world, "steps": args.iters, "ms_per_step": round(secs / args.iters * 1e3, 3), "higher_is_better": True, "dtype": "fp64",
            "data": "synthetic smooth field", "config": {"model": "DTD stencil3d", "grid": [args.n] * 3, "block": args.b, "ranks": world}}
+    if args.share_gpu:
+        out["note"] = f"validation mode: all {world} ranks share GPU 0 (halo faces cross ranks over IPC); not a scaling measurement"
     return out, rank
 
 
@@ -246,7 +249,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cores", type=int, default=4)
     ap.add_argument("--qr-grid", choices=["1d", "2d"], default="2d", help="qr: process grid over the ranks")
-    ap.add_argument("--share-gpu", action="store_true", help="qr: validation mode, every rank on GPU 0 (gloo collectives); not a scaling measurement")
+    ap.add_argument("--share-gpu", action="store_true", help="qr / stencil: validation mode, every rank on GPU 0; not a scaling measurement")
     ap.add_argument("--check", action="store_true", help="qr: verify R (||A^T A x - R^T R x|| / (||A||_F^2 ||x||), all ranks) after the timed steps")
     ap.add_argument("--qr-tree", choices=["hqr", "flat"], default="hqr", help="qr: hierarchical (TS domains + TT trees) or flat TS tree")
     ap.add_argument("--qr-domain", type=int, default=0,

@@ -86,6 +86,10 @@ struct GemmDesc {
   uint8_t lower_only;      // 1: only C's lower triangle (SYRK)
   uint8_t a_lower;         // 1: op(A) is lower triangular (zeros above): row block i only reads k < (i+1) BM
   uint8_t b_upper;         // 1: op(B) is upper triangular (zeros below): column block j only reads k < (j+1) BN
+  // 1: panel solve through W = L^-1 under PARSEC_DPOTRF_TRSM=auto: the
+  // workgroups skip when the condition estimate in W's spare slots
+  // (B[(k-1) ldb + 0] = max|L|, + 1 = max|W|) exceeds the launch's limit
+  uint8_t gate;
   // optional (zero = off): beta scales Cin (ld ldcin) instead of C, and C2 (ld
   // ldc2) -= every value written to C (fused "W = A1 + V^T A2" / "A1 -= T^T W")
   int ldcin, ldc2;
@@ -99,9 +103,12 @@ struct TrsmDesc {  // B := B * op(L)^-1 ; right side, lower, (trans), non-unit
   int m, n;  // B is m x n, L is n x n
   int ldl, ldb;
   uint8_t trans;  // 1: B * L^-T (the Cholesky panel)
-  uint8_t pad[7];
+  uint8_t gate = 0;  // 1: run only when the estimate in invD's spare slots exceeds the limit (fallback of a gated W-GEMM)
+  uint8_t pad[2] = {0, 0};
+  int invD_ld = 0;   // 0: invD holds contiguous 64x64 blocks; else the diagonal 64-blocks of an n x n matrix (ld invD_ld), e.g. W = L^-1
   const double* invD = nullptr;  // optional: inverses of L's 64x64 diagonal blocks (from POTRF)
 };
+static_assert(sizeof(GemmDesc) == 96, "GemmDesc grew: the grouped-GEMM kernel argument block is sized for 40 of them");
 
 struct PotrfDesc {
   double* A;
@@ -119,7 +126,17 @@ struct TrsmGemmDesc {
   const double* W;
   int m, n;  // B is m x n, W is n x n lower triangular
   int ldb, ldw;
+  // optional: the factor itself, for the substitution fallback of
+  // PARSEC_DPOTRF_TRSM=auto / blocked (trsm_inverse_mode)
+  const double* L = nullptr;
+  int ldl = 0;
 };
+
+// Panel solve of the tile Cholesky: 0 = always through W = L^-1, 1 = auto (W
+// unless max|L| * max|W| > limit, then blocked substitution), 2 = always
+// blocked substitution. Returns the previous mode; limit <= 0 keeps it.
+int trsm_inverse_mode(int mode, double limit);
+double trsm_inverse_limit();
 
 // Householder QR of a tile (GEQRT: A2 == nullptr) or of a triangle on top of a
 // tile (TSQRT: [R = A1 (upper); A2]), compact WY with a full n x n upper T.

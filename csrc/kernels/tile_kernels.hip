@@ -20,7 +20,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -45,6 +48,7 @@ struct GemmBatchArgs {
   // into C with f64 atomics (beta == 1 for every descriptor of such a launch)
   int main_tiles;
   int ksplit;
+  double gate_limit;  // gated descriptors (GemmDesc::gate) skip above this estimate
   int tile_start[kMaxGemmBatch + 1];
   GemmDesc d[kMaxGemmBatch];
 };
@@ -119,8 +123,13 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // bounds checks and no divergent control flow around its loads.
 // NBUF = 2: double-buffered LDS, one barrier per k-tile; NBUF = 1: one LDS
 // buffer (half the LDS, two barriers per k-tile) for deeper BK.
-template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF = 2, int OCC = WM * WN / 2>
+// PF = 2 (NBUF 2 only): two k-tiles in flight in registers (loaded two compute
+// phases before their LDS store) for the one-workgroup-per-CU regime of the
+// DPOTRF bulk streams, where one k-tile of MFMA work per wave does not cover an
+// HBM miss.
+template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF = 2, int OCC = WM * WN / 2, int PF = 1>
 __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OCC))) void dgemm_batch_kernel(const GemmBatchArgs args) {
+  static_assert(PF == 1 || NBUF == 2, "two tiles in flight need the double-buffered LDS");
   constexpr int NT = WM * WN * 64;
   constexpr int WTM = BM / WM;
   constexpr int WTN = BN / WN;
@@ -154,6 +163,12 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
   const int tm = local % mt, tn = local / mt;
   const int m0 = tm * BM, n0 = tn * BN;
   if (d.lower_only && n0 > m0 + BM - 1) return;
+  if (d.gate) {
+    // panel solve through W = L^-1 whose condition estimate is too large: the
+    // gated substitution kernel launched behind this one solves instead
+    const double* __restrict__ slot = d.B + (size_t)(d.k - 1) * d.ldb;
+    if (slot[0] * slot[1] > args.gate_limit) return;
+  }
 
   const int tid = threadIdx.x;
   const int ykey = args.yield ? cu_key() : 0;
@@ -187,8 +202,9 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
   constexpr int B_PAIRS = BN * BK / 2 / NT;
   static_assert(A_PAIRS >= 1 && B_PAIRS >= 1, "tile too small");
   double2_t ra[A_PAIRS], rb[B_PAIRS];
+  double2_t ra2[PF == 2 ? A_PAIRS : 1], rb2[PF == 2 ? B_PAIRS : 1];
 
-  auto load_tile = [&](int k0) {
+  auto load_tile_to = [&](int k0, double2_t* ra, double2_t* rb) {
 #pragma unroll
     for (int e = 0; e < A_PAIRS; ++e) {
       int idx = tid + NT * e;
@@ -240,7 +256,8 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
       }
     }
   };
-  auto store_tile = [&](int buf) {
+  auto load_tile = [&](int k0) { load_tile_to(k0, ra, rb); };
+  auto store_tile_from = [&](int buf, const double2_t* ra, const double2_t* rb) {
 #pragma unroll
     for (int e = 0; e < A_PAIRS; ++e) {
       int idx = tid + NT * e;
@@ -266,9 +283,30 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
       }
     }
   };
+  auto store_tile = [&](int buf) { store_tile_from(buf, ra, rb); };
+  const int fr = lane & 15, fk = lane >> 4;
+  auto mma_tile = [&](int cur) {
+    if (args.yield && tid < 64) {
+      // wave 0 sleeps while this CU hosts critical work; the other waves wait
+      // for it at the k-tile barrier
+      int polls = 0;
+      while (crit_count(ykey) > 0 && polls++ < kYieldMaxPolls) __builtin_amdgcn_s_sleep(4);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      double bfr[FM], afr[FN];
+#pragma unroll
+      for (int j = 0; j < FM; ++j) bfr[j] = As[cur][kk + fk][wm * WTM + j * 16 + fr];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) afr[i] = Bs[cur][kk + fk][wn * WTN + i * 16 + fr];
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(afr[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
 
   const int nkt = (K + BK - 1) / BK;
-  const int fr = lane & 15, fk = lane >> 4;
   // Full tiles with |alpha| = 1: the accumulators start from (beta/alpha) C (exact),
   // loaded behind the first A/B tile so the C read latency overlaps the prologue
   // and the epilogue is a pure store (no read-modify-write tail when a batch's
@@ -293,28 +331,28 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
       }
   }
   store_tile(0);
+  if (PF == 2) {
+    // slot 1 (ra/rb) carries the odd tiles, slot 2 (ra2/rb2) the even ones
+    if (1 < nkt) load_tile_to(BK, ra, rb);
+    if (2 < nkt) load_tile_to(2 * BK, ra2, rb2);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; kt += 2) {
+      mma_tile(0);                                  // tile kt
+      if (kt + 1 < nkt) store_tile_from(1, ra, rb);  // tile kt + 1 (loaded two phases ago)
+      __syncthreads();
+      if (kt + 3 < nkt) load_tile_to((kt + 3) * BK, ra, rb);
+      if (kt + 1 >= nkt) break;
+      mma_tile(1);                                    // tile kt + 1
+      if (kt + 2 < nkt) store_tile_from(0, ra2, rb2);  // tile kt + 2
+      __syncthreads();
+      if (kt + 4 < nkt) load_tile_to((kt + 4) * BK, ra2, rb2);
+    }
+  } else {
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
     const int cur = NBUF == 2 ? (kt & 1) : 0;
-    if (args.yield && tid < 64) {
-      // wave 0 sleeps while this CU hosts critical work; the other waves wait
-      // for it at the k-tile barrier
-      int polls = 0;
-      while (crit_count(ykey) > 0 && polls++ < kYieldMaxPolls) __builtin_amdgcn_s_sleep(4);
-    }
     if (kt + 1 < nkt) load_tile((kt + 1) * BK);
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 4) {
-      double bfr[FM], afr[FN];
-#pragma unroll
-      for (int j = 0; j < FM; ++j) bfr[j] = As[cur][kk + fk][wm * WTM + j * 16 + fr];
-#pragma unroll
-      for (int i = 0; i < FN; ++i) afr[i] = Bs[cur][kk + fk][wn * WTN + i * 16 + fr];
-#pragma unroll
-      for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int j = 0; j < FM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(afr[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
+    mma_tile(cur);
     if (NBUF == 2) {
       if (kt + 1 < nkt) store_tile(cur ^ 1);
       __syncthreads();
@@ -323,6 +361,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
       store_tile(0);
       __syncthreads();
     }
+  }
   }
 
   const double alpha = d.alpha, beta = preload ? 0.0 : d.beta;
@@ -526,6 +565,7 @@ constexpr int kMaxTrsmBatch = 48;
 struct TrsmInvArgs {
   int count;
   int prio;
+  double gate_limit;  // gated descriptors (TrsmDesc::gate) run only above this estimate
   int block_start[kMaxTrsmBatch + 1];
   TrsmDesc d[kMaxTrsmBatch];
   const double* invD[kMaxTrsmBatch];
@@ -547,6 +587,13 @@ __global__ __launch_bounds__(kTrsmThreads) void dtrsm_inv_kernel(const TrsmInvAr
   const int di = find_desc(args, args.block_start, b);
   const TrsmDesc& d = args.d[di];
   const double* __restrict__ invD = args.invD[di];
+  // invD: contiguous 64x64 blocks, or the diagonal 64-blocks of W = L^-1 (ld invD_ld)
+  const size_t ldD = d.invD_ld ? (size_t)d.invD_ld : 64;
+  const size_t bstride = d.invD_ld ? (size_t)64 * d.invD_ld + 64 : 4096;
+  if (d.gate) {
+    const double* __restrict__ slot = invD + (size_t)(d.n - 1) * ldD;
+    if (!(slot[0] * slot[1] > args.gate_limit)) return;  // the W-GEMM solved this panel
+  }
   const int r0 = (b - args.block_start[di]) * BR;
   const int n = d.n, m = d.m;
   const int nblk = (n + 63) / 64;
@@ -597,10 +644,10 @@ __global__ __launch_bounds__(kTrsmThreads) void dtrsm_inv_kernel(const TrsmInvAr
     __syncthreads();
     // X_j = R_j invD_j^T, reduction over kk split between the two halves
     double4_t t0 = (double4_t){0.0, 0.0, 0.0, 0.0}, t1 = t0;
-    const double* __restrict__ Dj = invD + (size_t)jb * 4096 + 16 * g + fr;
+    const double* __restrict__ Dj = invD + (size_t)jb * bstride + 16 * g + fr;
 #pragma unroll
     for (int kk = 32 * h; kk < 32 * h + 32; kk += 8) {
-      const double a0 = Dj[(kk + fk) * 64], a1 = Dj[(kk + 4 + fk) * 64];
+      const double a0 = Dj[(kk + fk) * ldD], a1 = Dj[(kk + 4 + fk) * ldD];
       const double b0 = P[(c0 + kk + fk) * BR + fr], b1 = P[(c0 + kk + 4 + fk) * BR + fr];
       t0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, t0, 0, 0, 0);
       t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, t1, 0, 0, 0);
@@ -638,11 +685,12 @@ static int g_gemm_chunk_fill = -1;   // PARSEC_GEMM_CHUNK_FILL=0: fixed 40-descr
 // launches are padded to one workgroup per CU (t_launch_pad)
 static inline int gemm_slots() { return t_launch_pad ? std::max(1, g_gemm_slots / 2) : g_gemm_slots; }
 
-template <int BM, int BN, int BK, int WM, int WN, int NBUF, int OCC = WM * WN / 2>
+template <int BM, int BN, int BK, int WM, int WN, int NBUF, int OCC = WM * WN / 2, int PF = 1>
 static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hipStream_t stream) {
   a.prio = t_launch_prio;
   a.claim = t_launch_claim >= 2;
   a.yield = t_launch_yield;
+  a.gate_limit = parsec::trsm_inverse_limit();
   int total = 0;
   bool full = g_gemm_full != 0;
   for (int i = 0; i < n; ++i) {
@@ -691,8 +739,8 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
   }
 #define PARSEC_GEMM_LAUNCH(TA, TB)                                                                                    \
   do {                                                                                                                \
-    if (full) hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, OCC>), grid, block, pad, stream, a); \
-    else hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, false, NBUF, OCC>), grid, block, pad, stream, a);    \
+    if (full) hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, OCC, PF>), grid, block, pad, stream, a); \
+    else hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, false, NBUF, OCC, PF>), grid, block, pad, stream, a);    \
   } while (0)
   switch (mode) {
     case 0: PARSEC_GEMM_LAUNCH(false, false); break;
@@ -756,6 +804,10 @@ static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) 
   switch (g_gemm_variant) {
     case 6: launch_gemm_shape<128, 128, 16, 4, 2, 2>(a, descs, n, stream); break;
     case 8: launch_gemm_shape<128, 128, 16, 2, 2, 2>(a, descs, n, stream); break;
+    // two k-tiles in flight (PF 2), 8 waves, up to 256 VGPRs: one workgroup per CU
+    case 9: launch_gemm_shape<128, 128, 16, 2, 4, 2, 2, 2>(a, descs, n, stream); break;
+    // the same at the default occupancy bound (128 VGPRs)
+    case 10: launch_gemm_shape<128, 128, 16, 2, 4, 2, 4, 2>(a, descs, n, stream); break;
     // default: 8 waves (2 x 4) of 64x32 per 128x128 tile, 126 VGPRs -> 4 waves per
     // SIMD with two workgroups per CU (measured: DPOTRF 64k +4 %, 16k +7 % over
     // the 4-wave 64x64-per-wave kernel = variant 8; profiles/r1_gemm_variants_v8.log;
@@ -815,6 +867,7 @@ void launch_trsm_inv(const TrsmDesc* descs, const double* const* invD, int n, hi
     TrsmInvArgs a;
     a.count = cnt;
     a.prio = t_launch_prio;
+    a.gate_limit = parsec::trsm_inverse_limit();
     int total = 0, maxn = 0;
     for (int i = 0; i < cnt; ++i) {
       a.d[i] = descs[s0 + i];
@@ -870,19 +923,54 @@ __global__ void set_identity_kernel(double* W, int n, int ldw) {
 }
 
 constexpr int kMaxCopyBatch = 48;
+constexpr int kMaxScan = 8;
 struct CopyBatchArgs {
   int count;
   int prio;
   int rows[kMaxCopyBatch], cols[kMaxCopyBatch], ld_src[kMaxCopyBatch], ld_dst[kMaxCopyBatch];
   const double* src[kMaxCopyBatch];
   double* dst[kMaxCopyBatch];
+  // condition estimate of the panel solves (PARSEC_DPOTRF_TRSM=auto): job j
+  // maxes |L| and |W| over the lower triangles into W's spare slots
+  // W[(n-1) ldw + 0 / 1] (strictly upper, zero since POTRF, never read by the
+  // GEMM: its column block 0 reads k < 128 <= n - 1)
+  int nscan;
+  int scan_n[kMaxScan], scan_ldl[kMaxScan], scan_ldw[kMaxScan];
+  const double* scan_L[kMaxScan];
+  double* scan_W[kMaxScan];
 };
 static_assert(sizeof(CopyBatchArgs) <= 4096, "CopyBatchArgs exceeds the kernel argument limit");
 
-// blockIdx.y = tile, blockIdx.x strides over columns; one wave-row per column.
+// blockIdx.y = tile (then the scan jobs), blockIdx.x strides over columns; one
+// wave-row per column.
 __global__ __launch_bounds__(256) void copy_tiles_kernel(const CopyBatchArgs a) {
   PARSEC_WAVE_PRIO(a.prio);
   const int t = blockIdx.y;
+  if (t >= a.count) {
+    const int j = t - a.count;
+    const int n = a.scan_n[j];
+    const double* __restrict__ L = a.scan_L[j];
+    const double* __restrict__ W = a.scan_W[j];
+    const size_t ldl = a.scan_ldl[j], ldw = a.scan_ldw[j];
+    double mL = 0.0, mW = 0.0;
+    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < n; c += gridDim.x * 4)
+      for (int r = c + (threadIdx.x & 63); r < n; r += 64) {
+        mL = fmax(mL, fabs(L[(size_t)c * ldl + r]));
+        mW = fmax(mW, fabs(W[(size_t)c * ldw + r]));
+      }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      mL = fmax(mL, __shfl_xor(mL, o));
+      mW = fmax(mW, __shfl_xor(mW, o));
+    }
+    if ((threadIdx.x & 63) == 0 && (mL > 0.0 || mW > 0.0)) {
+      // non-negative doubles order like their bit patterns: integer max
+      auto* slot = reinterpret_cast<unsigned long long*>(a.scan_W[j] + (size_t)(n - 1) * ldw);
+      __hip_atomic_fetch_max(slot, (unsigned long long)__double_as_longlong(mL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_max(slot + 1, (unsigned long long)__double_as_longlong(mW), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   const int rows = a.rows[t], cols = a.cols[t], lds = a.ld_src[t], ldd = a.ld_dst[t];
   const double* __restrict__ s = a.src[t];
   double* __restrict__ d = a.dst[t];
@@ -1714,15 +1802,44 @@ size_t trsm_w_workspace_bytes(const TrsmGemmDesc* d, int n) {
   return b;
 }
 
-// B := B W for every descriptor: copy the B tiles into the workspace, then one
-// grouped GEMM writes B from (copy x W).
+// B := B W^T for every descriptor: copy the B tiles into the workspace, then one
+// grouped GEMM writes B from (copy x W^T). Under trsm_inverse_mode auto the
+// copy kernel also estimates each W's conditioning (max|L| * max|W|), the GEMM
+// skips the panels above the limit, and a gated substitution kernel behind it
+// solves exactly those (blocked TRSM with W's diagonal 64-blocks as the
+// inverted diagonal blocks); mode blocked solves every panel by substitution.
 static const bool g_trsm_tri = !getenv("PARSEC_TRSM_TRI") || atoi(getenv("PARSEC_TRSM_TRI")) != 0;
+static bool trsm_gateable(const TrsmGemmDesc& t) {
+  // the estimate slots sit at W(0..1, n-1): outside every k range the GEMM reads
+  // only for n >= 256; the substitution kernel keeps a panel of n columns in LDS
+  return t.L && t.ldl > 0 && t.n >= 256 && t.n <= kTrsmMaxCols && t.n % 64 == 0 && t.ldw >= t.n;
+}
 void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, double* ws) {
+  const int mode = parsec::trsm_inverse_mode(-1, 0.0);
   for (int s0 = 0; s0 < n; s0 += kMaxCopyBatch) {
     const int cnt = std::min(kMaxCopyBatch, n - s0);
+    std::vector<TrsmDesc> fb;  // substitution solves of this chunk
+    if (mode == 2) {
+      for (int i = 0; i < cnt; ++i) {
+        const TrsmGemmDesc& t = d[s0 + i];
+        if (!trsm_gateable(t)) continue;
+        TrsmDesc x{};
+        x.L = t.L; x.ldl = t.ldl; x.B = t.B; x.ldb = t.ldb; x.m = t.m; x.n = t.n; x.trans = 1;
+        x.invD = t.W; x.invD_ld = t.ldw;
+        fb.push_back(x);
+      }
+      if ((int)fb.size() == cnt) {  // every panel by substitution: no copy, no GEMM
+        std::vector<const double*> inv(fb.size());
+        for (size_t i = 0; i < fb.size(); ++i) inv[i] = fb[i].invD;
+        launch_trsm_inv(fb.data(), inv.data(), (int)fb.size(), stream);
+        continue;
+      }
+      fb.clear();  // (a panel without its factor: through W like mode 0)
+    }
     CopyBatchArgs ca;
     ca.count = cnt;
     ca.prio = t_launch_prio;
+    ca.nscan = 0;
     std::vector<GemmDesc> g(cnt);
     char* p = reinterpret_cast<char*>(ws);
     int maxc = 1;
@@ -1737,10 +1854,32 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
       e.lda = t.m; e.ldb = t.ldw; e.ldc = t.ldb;
       e.alpha = 1.0; e.beta = 0.0; e.transA = 0; e.transB = 1; e.lower_only = 0; e.a_lower = 0;  // copy x (L^-1)^T
       e.b_upper = g_trsm_tri ? 1 : 0;  // (L^-1)^T is upper triangular: output column block j needs k < (j+1) BN only
+      e.gate = 0;
+      if (mode == 1 && trsm_gateable(t)) {
+        int j = 0;
+        while (j < ca.nscan && ca.scan_W[j] != t.W) ++j;
+        if (j == ca.nscan && ca.nscan < kMaxScan) {
+          ca.scan_n[j] = t.n; ca.scan_ldl[j] = t.ldl; ca.scan_ldw[j] = t.ldw;
+          ca.scan_L[j] = t.L; ca.scan_W[j] = const_cast<double*>(t.W);
+          ++ca.nscan;
+        }
+        if (j < ca.nscan) {
+          e.gate = 1;
+          TrsmDesc x{};
+          x.L = t.L; x.ldl = t.ldl; x.B = t.B; x.ldb = t.ldb; x.m = t.m; x.n = t.n; x.trans = 1;
+          x.invD = t.W; x.invD_ld = t.ldw; x.gate = 1;
+          fb.push_back(x);
+        }
+      }
       p += ((size_t)t.m * t.n * sizeof(double) + 255) / 256 * 256;
     }
-    hipLaunchKernelGGL(copy_tiles_kernel, dim3(std::min(256, (maxc + 3) / 4), cnt), dim3(256), 0, stream, ca);
+    hipLaunchKernelGGL(copy_tiles_kernel, dim3(std::min(256, (maxc + 3) / 4), cnt + ca.nscan), dim3(256), 0, stream, ca);
     launch_gemm_batch(g.data(), cnt, stream);
+    if (!fb.empty()) {
+      std::vector<const double*> inv(fb.size());
+      for (size_t i = 0; i < fb.size(); ++i) inv[i] = fb[i].invD;
+      launch_trsm_inv(fb.data(), inv.data(), (int)fb.size(), stream);
+    }
   }
 }
 
@@ -1826,6 +1965,37 @@ int device_copy_kernel(void* dst, const void* src, size_t bytes, void* stream) {
   return (int)hipGetLastError();
 }
 
+// Panel-solve mode of the tile Cholesky (device.hpp trsm_inverse_mode).
+// PARSEC_DPOTRF_TRSM = inverse | auto | blocked, PARSEC_DPOTRF_TRSM_LIMIT = the
+// estimate above which auto solves by substitution (scripts/trsm_inverse_numerics.py,
+// profiles/r4_trsm_inverse_numerics.txt).
+static std::atomic<int> g_trsm_mode{-1};
+static std::atomic<double> g_trsm_limit{0.0};
+static void trsm_mode_init() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    int m = 1;
+    if (const char* e = getenv("PARSEC_DPOTRF_TRSM")) m = !strcmp(e, "inverse") ? 0 : !strcmp(e, "blocked") ? 2 : 1;
+    double lim = 1e6;
+    if (const char* e = getenv("PARSEC_DPOTRF_TRSM_LIMIT")) lim = atof(e);
+    int exp = -1;
+    g_trsm_mode.compare_exchange_strong(exp, m);
+    double z = 0.0;
+    g_trsm_limit.compare_exchange_strong(z, lim > 0 ? lim : 1e6);
+  });
+}
+int trsm_inverse_mode(int mode, double limit) {
+  trsm_mode_init();
+  const int prev = g_trsm_mode.load();
+  if (mode >= 0) g_trsm_mode.store(mode);
+  if (limit > 0) g_trsm_limit.store(limit);
+  return prev;
+}
+double trsm_inverse_limit() {
+  trsm_mode_init();
+  return g_trsm_limit.load(std::memory_order_relaxed);
+}
+
 }  // namespace parsec
 
 // ------------------------------------------------- C entry points (tests/bench)
@@ -1849,7 +2019,13 @@ extern "C" {
 int parsec_amd_gemm_tile_policy(int p) { return parsec::kern::gemm_tile_policy(p); }
 int parsec_amd_gemm_splitk(int on) { return parsec::kern::gemm_splitk(on); }
 int parsec_amd_dgemm_batch(const parsec::GemmDesc* descs, int n, void* stream) {
+  // PARSEC_GEMM_PAD_TEST=1: launch like a DPOTRF bulk stream (padded LDS: one
+  // 128x128 workgroup per CU) -- kernel benchmarks of the in-DAG regime
+  static const bool pad_test = getenv("PARSEC_GEMM_PAD_TEST") && atoi(getenv("PARSEC_GEMM_PAD_TEST")) != 0;
+  const int prev = parsec::kern::t_launch_pad;
+  if (pad_test) parsec::kern::t_launch_pad = 8192;
   parsec::kern::launch_gemm_batch(descs, n, (hipStream_t)stream);
+  parsec::kern::t_launch_pad = prev;
   return (int)hipGetLastError();
 }
 // BLAS-style single DGEMM, C = alpha op(A) op(B) + beta C, column major, on

@@ -642,6 +642,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("device_alloc", [](int dev, size_t bytes) { return (uintptr_t)device_alloc(dev, bytes); });
   m.def("device_free", [](int dev, uintptr_t p) { device_free(dev, (void*)p); });
   m.def("device_memcpy", [](int dd, uintptr_t dst, int sd, uintptr_t src, size_t n) { return device_memcpy(dd, (void*)dst, sd, (const void*)src, n); });
+  m.def("trsm_inverse_mode", [](int mode, double limit) { return trsm_inverse_mode(mode, limit); }, py::arg("mode") = -1, py::arg("limit") = 0.0,
+        "Tile-Cholesky panel solve: 0 through W = L^-1, 1 auto (substitution when max|L| max|W| > limit), 2 substitution; returns the previous mode");
+  m.def("trsm_inverse_limit", []() { return trsm_inverse_limit(); });
   m.def("device_memcpy_stats", [](bool reset) {
     uint64_t b[3];
     device_memcpy_stats(b, reset);

@@ -10,6 +10,7 @@ tests/test_dpotrf_gpu.py::test_trsm_inverse_vs_blocked_gpu checks the GPU
 points). Printed per (cond, nb):
   bwd  = ||A - L L^T||_F / ||A||_F            (backward error of the factor)
   L diff = ||L_inv - L_blk||_F / ||L_blk||_F  (the two factors)
+  estimate = max over tiles of max|L(k,k)| * max|L(k,k)^-1| (the auto switch)
   solv = ||A x - b|| / (||A|| ||x||)           (solve with the factor)
 usage: python scripts/trsm_inverse_numerics.py [--n 2048] [--nb 512 1024]
        [--cond 1e2 1e4 1e6 1e8 1e10 1e12]
@@ -122,7 +123,10 @@ def sweep(n, nbs, conds, graded):
             rb, ri = metrics(A, Lb, Lb), metrics(A, Li, Lb)
             kdiag = max(np.linalg.cond(Lb[i * nb:(i + 1) * nb, i * nb:(i + 1) * nb]) for i in range(n // nb))
             # the runtime's on-device estimate: max |l_ii| / min |l_ii| per tile
-            dr = max(np.abs(np.diag(Lb)[i * nb:(i + 1) * nb]).max() / np.abs(np.diag(Lb)[i * nb:(i + 1) * nb]).min() for i in range(n // nb))
+            # the runtime's on-device estimate (PARSEC_DPOTRF_TRSM=auto): max |L(k,k)| * max |W|,
+            # W = L(k,k)^-1, elementwise, per tile
+            tiles = [Lb[i * nb:(i + 1) * nb, i * nb:(i + 1) * nb] for i in range(n // nb)]
+            dr = max(np.abs(t).max() * np.abs(lower_inverse(t)).max() for t in tiles)
             rows.append((cond, nb, kdiag, dr, rb, ri))
     return rows
 
@@ -139,7 +143,7 @@ def main():
     fam = {"plain": False, "graded": True, "tile": "tile", "kahan": "kahan"}
     for graded in [fam[f] for f in a.family]:
         print(f"-- n={a.n} {names[graded]}")
-        print(f"{'cond(A)':>8} {'nb':>5} {'max cond(Lkk)':>13} {'diag ratio':>10} | {'bwd blk':>9} {'bwd inv':>9} | {'L diff':>9} | {'solv blk':>9} {'solv inv':>9}")
+        print(f"{'cond(A)':>8} {'nb':>5} {'max cond(Lkk)':>13} {'estimate':>10} | {'bwd blk':>9} {'bwd inv':>9} | {'L diff':>9} | {'solv blk':>9} {'solv inv':>9}")
         for cond, nb, kd, dr, rb, ri in sweep(a.n, a.nb, a.cond, graded):
             print(f"{cond:8.0e} {nb:5d} {kd:13.2e} {dr:10.2e} | {rb[0]:9.2e} {ri[0]:9.2e} | {ri[1]:9.2e} | {rb[2]:9.2e} {ri[2]:9.2e}")
 

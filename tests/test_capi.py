@@ -222,3 +222,20 @@ def test_dtd_reference_programs(dtd_more, args, nranks):
     if args[0] == "global_id":
         ids = {line.split("ids ")[1] for line in text.splitlines() if "ids " in line}
         assert len(ids) == 1, ids  # the same ids on every rank
+
+
+@pytest.mark.parametrize("nranks", [1, 3, 4])
+def test_redistribute_random_c_program(tmp_path, pa, nranks):
+    """Port of the reference's testing_redistribute_random.c: a window between
+    two tabular collections with random tile -> rank tables (seeds 2873 /
+    3872) and different tile sizes, PTG and DTD redistribution, checked in the
+    target and after the round trip back into a zeroed source."""
+    exe = tmp_path / "redistribute_random"
+    cmd = ["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-O1", f"-I{ROOT}/include", os.path.join(HERE, "capi", "redistribute_random.c"), "-o", str(exe),
+           f"-L{ROOT}/parsec_amd/lib", "-lparsec_amd", f"-Wl,-rpath,{ROOT}/parsec_amd/lib", "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    rc, outs = launch.launch(nranks, [str(exe)], timeout=120, capture=True, env={"PARSEC_MCA_device_hip_enabled": "0"})
+    text = "".join(o for o, _ in outs)
+    assert rc == 0, text + "".join(e for _, e in outs)
+    assert "Redistribute Result is CORRECT" in text and text.count("bad 0, round trip bad 0") == 2 * nranks, text

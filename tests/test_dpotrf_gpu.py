@@ -115,3 +115,55 @@ def test_redistribute_hbm_resident(pa, smb, dmb, win):
         assert after["bytes_in"] == before["bytes_in"]  # device to device only
     finally:
         ctx.fini()
+
+
+def _factor_gpu(pa, S, N, nb, mode, limit=0.0):
+    """JDF Cholesky of S (torch, cuda) in panel-solve mode `mode`; returns L."""
+    prev_limit = pa.trsm_inverse_limit()
+    prev = pa.trsm_inverse_mode(mode, limit)
+    ctx = pa.init(3)
+    try:
+        gpu = pa.first_gpu_device_index()
+        NT = N // nb
+        store = torch.empty((NT, NT, nb, nb), dtype=torch.float64, device="cuda")
+        A = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb, nb, N, N, device=gpu, ptr=store.data_ptr())
+        store.copy_(S.reshape(NT, nb, NT, nb).permute(2, 0, 3, 1))
+        torch.cuda.synchronize()
+        tp, info = pa.dpotrf_jdf_new(A)
+        ctx.add_taskpool(tp)
+        ctx.start()
+        ctx.wait()
+        assert pa.read_int(info) == 0
+        return torch.tril(store.permute(1, 3, 0, 2).reshape(N, N)).clone()
+    finally:
+        ctx.fini()
+        pa.trsm_inverse_mode(prev, prev_limit)
+
+
+@pytest.mark.parametrize("nb", [512, 1024])
+def test_trsm_inverse_modes_gpu(pa, nb):
+    """Panel solve through W = L^-1 (mode 0), by the gated substitution kernel
+    (mode 2) and auto (mode 1: the copy kernel estimates max|L| max|W| into W's
+    spare slots, the W-GEMM skips and the substitution kernel solves above the
+    limit). On an SPD matrix with cond 1e12 (numerics sweep:
+    profiles/r4_trsm_inverse_numerics.txt) every mode is backward stable; auto
+    with its default limit takes the inverse path (same factor as mode 0) and
+    auto with limit 1 takes the substitution path (same factor as mode 2)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    N = 2048
+    g = torch.Generator(device="cpu").manual_seed(11)
+    q, _ = torch.linalg.qr(torch.randn((N, N), dtype=torch.float64, generator=g))
+    S = ((q * torch.logspace(0, -12, N, dtype=torch.float64)) @ q.t())
+    S = (0.5 * (S + S.t())).cuda()
+    L0 = _factor_gpu(pa, S, N, nb, 0)
+    L2 = _factor_gpu(pa, S, N, nb, 2)
+    L1 = _factor_gpu(pa, S, N, nb, 1)
+    L1s = _factor_gpu(pa, S, N, nb, 1, 1.0)
+    nS = torch.linalg.norm(S)
+    for L in (L0, L1, L2, L1s):
+        assert (torch.linalg.norm(L @ L.t() - S) / nS).item() < 1e-14
+    d02 = torch.linalg.norm(L0 - L2).item()
+    assert d02 > 0  # the two solves differ (by ~cond(L(k,k)) eps)
+    assert torch.linalg.norm(L1 - L0).item() < 1e-3 * d02   # auto below the limit = the inverse path
+    assert torch.linalg.norm(L1s - L2).item() < 1e-3 * d02  # auto above it = the substitution path

@@ -127,9 +127,10 @@ def test_stencil_four_ranks_ipc(pa):
         assert rc == 0, out
         line = next(l for l in out.splitlines() if " halo d2h " in l)
         f = line.split()
-        v = {f[i]: int(f[i + 1]) for i in range(2, len(f) - 1, 2)}
+        v = {f[i]: int(f[i + 1]) for i in range(3, len(f) - 1, 2)}
         assert v["d2h"] == 0 and v["writeback"] == 0, line
         assert v["get_ipc"] > 0, line
+        print(line)
 
 
 def test_comm_engine_c_program_gpu_memory(tmp_path, pa):

@@ -398,6 +398,24 @@ def test_project_dyn(tmp_path, nranks):
     assert held == 9367 and text.count("bad 0") == nranks, text
 
 
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("nranks,nt", [(1, 7), (1, 13), (2, 13), (3, 21)])
+def test_reference_bt_reduction(tmp_path, nranks, nt):
+    """The reference's tests/apps/generalized_reduction/BT_reduction.jdf,
+    compiled unmodified, driven by tests/capi/bt_reduction_main.cpp (public API
+    in place of the reference's main.c / wrapper / reduc_data.c): binary trees
+    per set bit of NT + a linear chain; rank 0 prints NT (NT - 1) / 2."""
+    from parsec_amd.launch import launch
+
+    exe = ptgpp.build_program(os.path.join(REF, "tests/apps/generalized_reduction/BT_reduction.jdf"), str(tmp_path),
+                              extra_sources=[os.path.join(os.path.dirname(JDF), "capi", "bt_reduction_main.cpp")], cxxflags=ptgpp.C_BODIES)
+    rc, outs = launch(nranks, [exe, str(nt)], timeout=120, capture=True)
+    text = "".join(o or "" for o, _ in outs)
+    assert rc == 0, text + "".join(e or "" for _, e in outs)
+    lines = text.split()
+    assert lines[0] == str(nt * (nt - 1) // 2) and f"expected {nt * (nt - 1) // 2}" in text, text
+
+
 @pytest.mark.parametrize("nranks", [2, 3, 4])
 def test_stencil_1d_remote_reshape(tmp_path, nranks):
     """Neighbours on other ranks receive only the halo columns of a tile
