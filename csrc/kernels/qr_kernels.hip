@@ -439,12 +439,14 @@ struct QrSub2Desc {
 };
 struct QrSub2Args {
   int count;
+  int prio;  // wave issue priority (s_setprio) of the sub-panel: the TS chain's critical path
   QrSub2Desc d[kMaxSub2Batch];
 };
 static_assert(sizeof(QrSub2Args) <= 4096, "QrSub2Args exceeds the kernel argument limit");
 
 template <int RPT, int NW>
 __global__ __launch_bounds__(64 * NW) void qr_sub2_kernel(const QrSub2Args args) {
+  if (args.prio) __builtin_amdgcn_s_setprio(2);
   constexpr int G = 2 * NW, RB = 32 / G, NTH = 64 * NW;
   // Two barriers per column. Loops over a thread's rows run in chunks of 8 with
   // ONE uniform test per chunk (chunks entirely above the pivot are skipped).
@@ -710,6 +712,7 @@ __device__ __forceinline__ double wave_sum_dpp(double x) {
 
 template <int RPL>
 __global__ __launch_bounds__(512) void qr_sub2c_kernel(const QrSub2Args args) {
+  if (args.prio) __builtin_amdgcn_s_setprio(2);
   constexpr int NW = 8, NC = 4;
   const QrSub2Desc& d = args.d[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -913,6 +916,7 @@ struct QrSubApplyTask {
 constexpr int kMaxSubApplyBatch = 24;
 struct QrSubApplyArgs {
   int count;
+  int prio;
   int start[kMaxSubApplyBatch + 1];  // first item of each task
   int ntr[kMaxSubApplyBatch];        // trailing column blocks per task
   QrSubApplyTask t[kMaxSubApplyBatch];
@@ -960,6 +964,7 @@ __device__ __forceinline__ double4_t mfma_atb(const double* __restrict__ A, int 
 constexpr int kSubApplyThreads = 512;
 
 __global__ __launch_bounds__(kSubApplyThreads) void qr_subapply_kernel(const QrSubApplyArgs args) {
+  if (args.prio) __builtin_amdgcn_s_setprio(2);
   int ti = 0;
   while (ti + 1 < args.count && (int)blockIdx.x >= args.start[ti + 1]) ++ti;
   const QrSubApplyTask& t = args.t[ti];
@@ -1119,6 +1124,14 @@ __global__ __launch_bounds__(kSubApplyThreads) void qr_subapply_kernel(const QrS
   }
 }
 
+// PARSEC_QR_PRIO=1: the sub-panel factor and its in-tile apply -- the serial
+// chain of a TS panel -- raise their waves' issue priority over co-resident
+// bulk GEMM waves (as the tile POTRF steps do)
+static int qr_prio() {
+  static const int p = getenv("PARSEC_QR_PRIO") ? atoi(getenv("PARSEC_QR_PRIO")) : 0;
+  return p;
+}
+
 static void launch_sub2(const std::vector<QrSub2Desc>& v, int rows, hipStream_t stream) {
   // column-owner kernel (one barrier per column) unless PARSEC_QR_SUB2=0; the
   // column-per-lane kernel: 8 waves (16 row groups) for tall sub-panels, 4 otherwise
@@ -1128,6 +1141,7 @@ static void launch_sub2(const std::vector<QrSub2Desc>& v, int rows, hipStream_t 
   for (size_t s0 = 0; s0 < v.size(); s0 += kMaxSub2Batch) {
     QrSub2Args a;
     a.count = (int)std::min<size_t>(kMaxSub2Batch, v.size() - s0);
+    a.prio = qr_prio();
     for (int i = 0; i < a.count; ++i) a.d[i] = v[s0 + i];
     const dim3 grid(a.count);
     if (sub2c && rows <= 64 * 9) {
@@ -1156,6 +1170,7 @@ static void launch_subapply(const std::vector<QrSubApplyTask>& v, hipStream_t st
   for (size_t s0 = 0; s0 < v.size(); s0 += kMaxSubApplyBatch) {
     QrSubApplyArgs a;
     a.count = (int)std::min<size_t>(kMaxSubApplyBatch, v.size() - s0);
+    a.prio = qr_prio();
     int items = 0;
     for (int i = 0; i < a.count; ++i) {
       const QrSubApplyTask& t = v[s0 + i];
