@@ -43,6 +43,11 @@ struct GemmBatchArgs {
   int claim; // critical-path launch: claim the CUs (bulk waves there pause)
   int yield; // bulk launch: pause while the CU hosts claimed critical work
   int total_tiles;
+  // staggered start (> 0): tiles [0, stagger) run as two K-halves, the first
+  // halves interleaved with whole tiles in the first round, the second halves
+  // last, both added into C (beta 1) -- workgroups then finish out of phase, so
+  // the C read / write bursts of a round overlap other workgroups' MFMA work
+  int stagger;
   // split-K tail: workgroups [main_tiles, grid) each take 1/ksplit of the K range
   // of one of the last (total_tiles - main_tiles) tiles and add alpha * partial
   // into C with f64 atomics (beta == 1 for every descriptor of such a launch)
@@ -147,7 +152,24 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
   // dispatched last split the K range of the tail tiles (wave quantisation:
   // a 606-tile launch on 512 slots would otherwise run a 94-tile second round)
   int tile, ks = 0, nsplit = 1;
-  if ((int)blockIdx.x < args.main_tiles) {
+  if (args.stagger > 0) {
+    const int S = args.stagger, total = args.total_tiles;
+    const int p = xcd_remap(blockIdx.x, total + S);
+    if (p < 2 * S) {
+      if (p & 1) {
+        tile = S + (p >> 1);
+      } else {
+        tile = p >> 1;
+        nsplit = 2;
+      }
+    } else if (p < total) {
+      tile = p;
+    } else {
+      tile = p - total;
+      nsplit = 2;
+      ks = 1;
+    }
+  } else if ((int)blockIdx.x < args.main_tiles) {
     tile = xcd_remap(blockIdx.x, args.main_tiles);
   } else {
     const int u = blockIdx.x - args.main_tiles;
@@ -705,10 +727,21 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
   a.total_tiles = total;
   a.main_tiles = total;
   a.ksplit = 1;
+  a.stagger = 0;
   if (total == 0) return;
   int grid_size = total;
   const int slots = gemm_slots();
-  if (BM == 128 && g_gemm_splitk != 0 && total > slots) {
+  static const int stagger_env = getenv("PARSEC_GEMM_STAGGER") ? atoi(getenv("PARSEC_GEMM_STAGGER")) : 0;
+  if (BM == 128 && stagger_env > 0 && total >= 2 * slots) {
+    bool ok = true;
+    for (int i = 0; ok && i < n; ++i)
+      ok = descs[i].beta == 1.0 && !descs[i].a_lower && !descs[i].b_upper && !descs[i].Cin && !descs[i].C2 && !descs[i].gate && descs[i].k >= 2 * BK;
+    if (ok) {
+      a.stagger = slots / 2;
+      grid_size = total + a.stagger;
+    }
+  }
+  if (BM == 128 && g_gemm_splitk != 0 && total > slots && a.stagger == 0) {
     // the last partial round of workgroups: split its tiles' K range so it
     // finishes in 1/s of a tile time; needs beta == 1 (partials are added into C)
     // and >= 256 of K per chunk (fewer flops per added byte would be bound by
