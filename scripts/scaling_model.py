@@ -167,6 +167,32 @@ def simulate(NT, nb, P, Q, gemm_tf, potrf_us, link_gbs, lat_us, syrk_eff=0.85, t
             "bulk_util": sum(busy_us) / (R * finish), "xgmi_GB": bytes_sent / 1e9}
 
 
+def critical_path_exact_ns(NT, costs_ns):
+    """Longest path of the DPOTRF DAG with per-kind task costs (ns; no
+    communication, infinite GPUs): what the runtime's simulation mode computes
+    for csrc/algos/jdf/dpotrf_L.jdf with its SIMCOST (runtime_simulation=1)."""
+    done = {}
+    for k in range(NT):
+        p_in = done.get(("SYRK", k - 1, k), 0)
+        done[("POTRF", k)] = p_in + costs_ns["POTRF"]
+        for m in range(k + 1, NT):
+            t_in = max(done[("POTRF", k)], done.get(("GEMM", m, k, k - 1), 0))
+            done[("TRSM", m, k)] = t_in + costs_ns["TRSM"]
+        for m in range(k + 1, NT):
+            s_in = max(done[("TRSM", m, k)], done.get(("SYRK", k - 1, m), 0))
+            done[("SYRK", k, m)] = s_in + costs_ns["SYRK"]
+            for n in range(k + 1, m):
+                g_in = max(done[("TRSM", m, k)], done[("TRSM", n, k)], done.get(("GEMM", m, n, k - 1), 0))
+                done[("GEMM", m, n, k)] = g_in + costs_ns["GEMM"]
+    return max(done.values())
+
+
+def simcost_ns(nb, gemm_tf=66.0, potrf_us=None):
+    """The per-kind costs of dpotrf_L.jdf's SIMCOST (jdf_simcost), integer ns."""
+    g = 2.0 * nb ** 3 / (gemm_tf * 1e3)
+    return {"POTRF": int((potrf_us if potrf_us else 520.0 * nb / 1024.0) * 1e3), "TRSM": int(g), "SYRK": int(g / 2 / 0.85), "GEMM": int(g)}
+
+
 def critical_path_us(NT, potrf_us, trsm_us, syrk_us, xfer_us, P, Q):
     # lower bound of the span ("chain ms"): POTRF(k) -> TRSM(k+1,k) ->
     # SYRK(k,k+1) -> POTRF(k+1) with infinite GPUs; tile (k,k) -> (k+1,k)

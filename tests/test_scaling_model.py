@@ -35,3 +35,35 @@ def test_more_ranks_more_throughput_and_traffic():
         if prev:
             assert out["tflops"] >= prev["tflops"] * 0.99 and out["xgmi_GB"] > prev["xgmi_GB"]
         prev = out
+
+
+def test_model_dag_matches_runtime_simulation(tmp_path):
+    """The runtime's own simulation mode (runtime_simulation=1) on the
+    ptgpp-compiled dpotrf_L.jdf with its SIMCOST (costs of a 1024-tile run,
+    PARSEC_SIMCOST_NB, on small real tiles) yields exactly the longest path the
+    model computes for the same DAG and costs."""
+    import subprocess
+    import sys
+
+    NT = 12
+    code = f"""
+import numpy as np, parsec_amd as pa
+pa.mca_set("runtime_simulation", "1")
+ctx = pa.init(4)
+nb = 8
+N = {NT} * nb
+A = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb, nb, N, N)
+S = np.random.default_rng(1).standard_normal((N, N)); S = S @ S.T + N * np.eye(N)
+for m in range(A.mt):
+    for n in range(A.nt):
+        A.tile(m, n)[:, :] = S[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb]
+tp, info = pa.dpotrf_jdf_new(A)
+ctx.add_taskpool(tp); ctx.start(); ctx.wait()
+print("SIMDATE", tp.simulation_date)
+ctx.fini()
+"""
+    env = dict(__import__("os").environ, PARSEC_SIMCOST_NB="1024", PARSEC_MCA_device_hip_enabled="0")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout + r.stderr
+    date = int(next(l for l in r.stdout.splitlines() if l.startswith("SIMDATE")).split()[1])
+    assert date == sm.critical_path_exact_ns(NT, sm.simcost_ns(1024))
