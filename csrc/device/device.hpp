@@ -137,6 +137,11 @@ struct TrsmGemmDesc {
 // blocked substitution. Returns the previous mode; limit <= 0 keeps it.
 int trsm_inverse_mode(int mode, double limit);
 double trsm_inverse_limit();
+namespace kern {
+// device_hip_cu_yield as the kernels see it (QR sub-panel kernels claim their CUs when > 0)
+void set_cu_yield_mode(int m);
+int cu_yield_mode();
+}  // namespace kern
 
 // Householder QR of a tile (GEQRT: A2 == nullptr) or of a triangle on top of a
 // tile (TSQRT: [R = A1 (upper); A2]), compact WY with a full n x n upper T.

@@ -1433,6 +1433,7 @@ void hip_devices_init(Context* ctx) {
     d->critical_bulk_cap = ccap;
     d->critical_split = csplit;
     d->cu_yield = cuy;
+    kern::set_cu_yield_mode(cuy);
     d->sort_pending = sortp != 0;
     d->trace_launches = trace;
     reg.add(d);

@@ -20,6 +20,24 @@
 
 namespace parsec {
 namespace kern {
+// Cooperative CU claim (device_hip_cu_yield, tile_kernels.hip g_crit_cu): the
+// TS chain's sub-panel kernels count themselves into the per-CU table so bulk
+// GEMM workgroups on their CU pause (vector atomics; table null = off).
+__device__ __forceinline__ int qr_cu_key() {
+  const unsigned hw = __builtin_amdgcn_s_getreg((7 << 11) | (8 << 6) | 4);   // HW_ID bits [15:8]
+  const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // XCC_ID bits [3:0]
+  return (int)(((xcc & 7u) << 8) | (hw & 0xffu));
+}
+__device__ __forceinline__ void qr_claim(int* table) {
+  if (table && threadIdx.x == 0) __hip_atomic_fetch_add(&table[qr_cu_key()], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void qr_release(int* table) {
+  if (!table) return;
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(&table[qr_cu_key()], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+int* crit_cu_table();
+int cu_yield_mode();
 
 void launch_gemm_batch(const GemmDesc* descs, int n, hipStream_t stream);  // tile_kernels.hip
 
@@ -440,6 +458,7 @@ struct QrSub2Desc {
 struct QrSub2Args {
   int count;
   int prio;  // wave issue priority (s_setprio) of the sub-panel: the TS chain's critical path
+  int* crit; // per-CU claim table (device_hip_cu_yield) or null
   QrSub2Desc d[kMaxSub2Batch];
 };
 static_assert(sizeof(QrSub2Args) <= 4096, "QrSub2Args exceeds the kernel argument limit");
@@ -713,6 +732,7 @@ __device__ __forceinline__ double wave_sum_dpp(double x) {
 template <int RPL>
 __global__ __launch_bounds__(512) void qr_sub2c_kernel(const QrSub2Args args) {
   if (args.prio) __builtin_amdgcn_s_setprio(2);
+  qr_claim(args.crit);
   constexpr int NW = 8, NC = 4;
   const QrSub2Desc& d = args.d[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -895,6 +915,7 @@ __global__ __launch_bounds__(512) void qr_sub2c_kernel(const QrSub2Args args) {
       const int col = idx / d.vzero, r = idx % d.vzero;
       d.Vc[(size_t)col * d.ldvc + r - d.vzero] = 0.0;
     }
+  qr_release(args.crit);
 }
 
 struct QrSubApplyTask {
@@ -917,6 +938,7 @@ constexpr int kMaxSubApplyBatch = 24;
 struct QrSubApplyArgs {
   int count;
   int prio;
+  int* crit;
   int start[kMaxSubApplyBatch + 1];  // first item of each task
   int ntr[kMaxSubApplyBatch];        // trailing column blocks per task
   QrSubApplyTask t[kMaxSubApplyBatch];
@@ -963,8 +985,14 @@ __device__ __forceinline__ double4_t mfma_atb(const double* __restrict__ A, int 
 
 constexpr int kSubApplyThreads = 512;
 
+__device__ __forceinline__ void qr_subapply_body(const QrSubApplyArgs& args);
 __global__ __launch_bounds__(kSubApplyThreads) void qr_subapply_kernel(const QrSubApplyArgs args) {
   if (args.prio) __builtin_amdgcn_s_setprio(2);
+  qr_claim(args.crit);
+  qr_subapply_body(args);
+  qr_release(args.crit);
+}
+__device__ __forceinline__ void qr_subapply_body(const QrSubApplyArgs& args) {
   int ti = 0;
   while (ti + 1 < args.count && (int)blockIdx.x >= args.start[ti + 1]) ++ti;
   const QrSubApplyTask& t = args.t[ti];
@@ -1142,6 +1170,7 @@ static void launch_sub2(const std::vector<QrSub2Desc>& v, int rows, hipStream_t 
     QrSub2Args a;
     a.count = (int)std::min<size_t>(kMaxSub2Batch, v.size() - s0);
     a.prio = qr_prio();
+    a.crit = cu_yield_mode() > 0 ? crit_cu_table() : nullptr;
     for (int i = 0; i < a.count; ++i) a.d[i] = v[s0 + i];
     const dim3 grid(a.count);
     if (sub2c && rows <= 64 * 9) {
@@ -1171,6 +1200,7 @@ static void launch_subapply(const std::vector<QrSubApplyTask>& v, hipStream_t st
     QrSubApplyArgs a;
     a.count = (int)std::min<size_t>(kMaxSubApplyBatch, v.size() - s0);
     a.prio = qr_prio();
+    a.crit = cu_yield_mode() > 0 ? crit_cu_table() : nullptr;
     int items = 0;
     for (int i = 0; i < a.count; ++i) {
       const QrSubApplyTask& t = v[s0 + i];

@@ -98,6 +98,19 @@ __device__ __forceinline__ void crit_release(int on) {
   __syncthreads();  // every wave of the workgroup is done
   if (threadIdx.x == 0) __hip_atomic_fetch_add(&g_crit_cu[cu_key()], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// host side: the table's device address (for kernels of other translation
+// units) and the engine's cu_yield mode (HipDevice init)
+static std::atomic<int> g_cu_yield_mode{0};
+void set_cu_yield_mode(int m) { g_cu_yield_mode.store(m); }
+int cu_yield_mode() { return g_cu_yield_mode.load(std::memory_order_relaxed); }
+int* crit_cu_table() {
+  static int* p = [] {
+    void* q = nullptr;
+    if (hipGetSymbolAddress(&q, HIP_SYMBOL(g_crit_cu)) != hipSuccess) { (void)hipGetLastError(); q = nullptr; }
+    return static_cast<int*>(q);
+  }();
+  return p;
+}
 constexpr int kYieldMaxPolls = 2000;  // x ~0.1 us sleep: at most ~0.2 ms of pause per k-tile
 __device__ __forceinline__ int crit_count(int key) { return __hip_atomic_load(&g_crit_cu[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
