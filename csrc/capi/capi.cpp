@@ -437,6 +437,9 @@ int parsec_context_start(parsec_context_t* context) { return context_start(conte
 int parsec_context_test(parsec_context_t* context) { return context_test(context); }
 int parsec_context_wait(parsec_context_t* context) { return context_wait(context); }
 int parsec_context_rank(const parsec_context_t* context) { return context->my_rank; }
+int parsec_debug_rank(void) { return parsec::comm_rank(); }
+int parsec_debug_level(void) { return parsec::debug_verbosity(); }
+int parsec_debug_output = 0;
 int parsec_context_nb_nodes(const parsec_context_t* context) { return context->nb_nodes; }
 int parsec_context_nb_cores(const parsec_context_t* context) { return context->nb_cores; }
 int parsec_comm_barrier(void) { return comm_size() > 1 ? comm_barrier() : 0; }

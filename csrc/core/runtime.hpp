@@ -202,6 +202,9 @@ struct Arena {
   Arena(size_t esz, size_t align, const Datatype& d);
   ~Arena();
   DataCopy* get_copy(Data* data, int device);   // host memory copy (device 0)
+  // count elements in one contiguous allocation (count <= 1: get_copy); freed,
+  // not recycled, when the copy is released
+  DataCopy* get_copy_count(Data* data, int device, int64_t count);
   void* allocate();
   void release_chunk(void* p);
 };

@@ -347,6 +347,42 @@ DataCopy* Arena::get_copy(Data* data, int device) {
   return c;  // refcount 1 owned by the caller
 }
 
+static void arena_multi_release(DataCopy* c) {
+  Data* d = c->original;
+  if (d) {
+    d->lock.lock();
+    data_copy_detach(d, c, c->device_index);
+    d->lock.unlock();
+  }
+  std::free(c->device_private);
+  delete c;
+  if (d) data_release(d);
+}
+
+DataCopy* Arena::get_copy_count(Data* data, int device, int64_t count) {
+  if (count <= 1) return get_copy(data, device);
+  void* p = nullptr;
+  const size_t bytes = elem_size * (size_t)count;
+  if (posix_memalign(&p, std::max<size_t>(alignment, sizeof(void*)), std::max<size_t>(bytes, 64)) != 0) return nullptr;
+  if (data == nullptr) {
+    data = data_new();
+    data->nb_elts = bytes;
+    data->owner_device = (int8_t)device;
+  } else {
+    data_retain(data);
+  }
+  DataCopy* c = new DataCopy();
+  c->device_private = p;
+  c->dtt = dtt;
+  c->coherency_state = COHERENCY_OWNED;
+  c->release_fn = arena_multi_release;
+  {
+    std::lock_guard<SpinLock> g(data->lock);
+    data_copy_attach(data, c, device);
+  }
+  return c;
+}
+
 void add2arena_rect(ArenaDatatype& adt, uint32_t esz, int64_t mb, int64_t nb, int64_t ld) {
   Datatype d = ld == mb ? Datatype::contiguous(esz, mb * nb) : Datatype::vector(esz, nb, mb, ld);
   add2arena(adt, d, 64);

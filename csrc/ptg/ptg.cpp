@@ -430,10 +430,18 @@ int PtgTaskClass::prepare_input(ExecutionStream* es, Task* t) const {
       // pure output flow (WRITE with no input dependency): a fresh copy from
       // the arena of its output datatype (reference jdf2c.c:5690-5719)
       if (fd.access == FLOW_WRITE && fd.in.empty() && !fd.out.empty()) {
-        const int ai = fd.out[0].then_t.datatype_index;
+        // the shape of the first active output dependency: its arena, and
+        // [count = ...] elements of it
+        const DepTarget* ot = &fd.out[0].then_t;
+        for (const Dep& d : fd.out) {
+          if (!d.guard || d.guard(tp, t->locals)) { ot = &d.then_t; break; }
+          if (d.has_else) { ot = &d.else_t; break; }
+        }
+        const int ai = ot->datatype_index;
         auto& adts = t->taskpool->arenas_datatypes;
         if (ai >= 0 && ai < (int)adts.size() && adts[ai].arena) {
-          r.data_in = adts[ai].arena->get_copy(nullptr, 0);
+          const int64_t count = ot->count ? ot->count(tp, t->locals) : 1;
+          r.data_in = adts[ai].arena->get_copy_count(nullptr, 0, count);
           if (!r.data_in) return HOOK_AGAIN;
         }
       }

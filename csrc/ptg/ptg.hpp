@@ -76,6 +76,10 @@ struct DepTarget {
   // type_remote starting displ_remote bytes into the producer's copy. -1: as `type`.
   int remote_datatype_index = -1;
   Expr displ_remote, count_remote;
+  // [count = ...] of the local shape: a pure output flow (WRITE without input)
+  // is allocated as count elements of its arena (reference jdf2c.c:5690-5719,
+  // parsec_arena_get_copy(arena, count, ...)); null: 1
+  Expr count;
   bool has_remote_shape() const { return remote_datatype_index >= 0 || (bool)displ_remote || (bool)count_remote; }
   std::vector<IterDef> iters;  // iterators local to this branch (`? [ j = .. ] T(..) : ..`)
 };

@@ -20,6 +20,10 @@
 #include <stddef.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
+#if !defined(_WIN32)
+#include <unistd.h> /* getopt / getpid: the reference's headers bring them in */
+#endif
 
 #define PARSEC_VERSION_MAJOR 4
 #define PARSEC_VERSION_MINOR 0
@@ -80,6 +84,11 @@ typedef struct parsec_arena_datatype_s parsec_arena_datatype_t;
 #endif
 
 typedef uint64_t parsec_data_key_t;
+
+/* diagnostics (reference parsec/utils/debug.h): this process' rank and the
+ * runtime's debug verbosity (MCA debug_verbose) */
+int parsec_debug_rank(void);
+int parsec_debug_level(void);
 
 /* Compile-time limits of the PTG runtime (reference parsec_config.h / jdf2c
  * checks): locals per task class, flows per class, dependencies per flow. */

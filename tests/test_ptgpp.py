@@ -416,6 +416,30 @@ def test_reference_bt_reduction(tmp_path, nranks, nt):
     assert lines[0] == str(nt * (nt - 1) // 2) and f"expected {nt * (nt - 1) // 2}" in text, text
 
 
+# Reference test programs compiled UNMODIFIED (their JDF and their own C
+# drivers, from /root/reference, read in place) against include/parsec.h:
+# (jdf, driver sources, args, check on stdout)
+REF_PROGRAMS = [
+    ("tests/api/touch.jdf", ["tests/api/touch_ex.c"], [], lambda out: out.count("STARTUP(") == 10 and "TASKS2(9)" in out),
+    ("tests/runtime/dtt_bug_replicator.jdf", ["tests/runtime/dtt_bug_replicator_ex.c"], [],
+     lambda out: out.count("PING") == 4 and out.count("PONG") == 3 and "A[DTT2] 6 7 8" in out),
+    # WRITE C [count = data_size]: pure-output flows sized by the dependency's count
+    ("tests/apps/merge_sort/merge_sort.jdf", ["tests/apps/merge_sort/main.c", "tests/apps/merge_sort/merge_sort_wrapper.c", "tests/apps/merge_sort/sort_data.c"],
+     ["100"], lambda out: len(out.split()) == 500 and all(a >= b for a, b in zip(list(map(int, out.split())), list(map(int, out.split()))[1:]))),
+]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("jdf,srcs,args,check", REF_PROGRAMS, ids=[os.path.basename(p[0]) for p in REF_PROGRAMS])
+def test_reference_programs_unmodified(tmp_path, jdf, srcs, args, check):
+    d = os.path.dirname(os.path.join(REF, jdf))
+    exe = ptgpp.build_program(os.path.join(REF, jdf), str(tmp_path), extra_sources=[os.path.join(REF, x) for x in srcs],
+                              cxxflags=ptgpp.C_BODIES + (f"-I{d}", f"-I{REF}/tests", f"-I{REF}"))
+    r = subprocess.run([exe] + args, capture_output=True, text=True, timeout=120, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert check(r.stdout), r.stdout[-2000:]
+
+
 @pytest.mark.parametrize("nranks", [2, 3, 4])
 def test_stencil_1d_remote_reshape(tmp_path, nranks):
     """Neighbours on other ranks receive only the halo columns of a tile

@@ -910,6 +910,7 @@ struct Gen {
     if (const Prop* tr = find_prop(dprops, "type_remote")) o << "__t.remote_datatype_index = " << adt_index(tr->val) << "; ";
     if (const Prop* d = find_prop(dprops, "displ_remote")) o << "__t.displ_remote = " << lam(f, prop_expr(*d), sc) << "; ";
     if (const Prop* d = find_prop(dprops, "count_remote")) o << "__t.count_remote = " << lam(f, prop_expr(*d), sc) << "; ";
+    if (const Prop* d = find_prop(dprops, "count")) o << "__t.count = " << lam(f, prop_expr(*d), sc) << "; ";
     o << "return __t; }()";
     return o.str();
   }
