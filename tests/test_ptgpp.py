@@ -423,6 +423,11 @@ REF_PROGRAMS = [
     ("tests/api/touch.jdf", ["tests/api/touch_ex.c"], [], lambda out: out.count("STARTUP(") == 10 and "TASKS2(9)" in out),
     ("tests/runtime/dtt_bug_replicator.jdf", ["tests/runtime/dtt_bug_replicator_ex.c"], [],
      lambda out: out.count("PING") == 4 and out.count("PONG") == 3 and "A[DTT2] 6 7 8" in out),
+    # JDFs that carry their own main
+    ("tests/dsl/ptg/ptgpp/forward_RW_NULL.jdf", [], [], lambda out: "I'm the task 20" in out),
+    ("tests/dsl/ptg/ptgpp/forward_READ_NULL.jdf", [], [], lambda out: "I'm the task 20" in out),
+    ("tests/dsl/ptg/local-indices/local_indices.jdf", [], [], lambda out: True),
+    ("tests/collections/kcyclic.jdf", [], [], lambda out: "M=02, N=08" in out),
     # WRITE C [count = data_size]: pure-output flows sized by the dependency's count
     ("tests/apps/merge_sort/merge_sort.jdf", ["tests/apps/merge_sort/main.c", "tests/apps/merge_sort/merge_sort_wrapper.c", "tests/apps/merge_sort/sort_data.c"],
      ["100"], lambda out: len(out.split()) == 500 and all(a >= b for a, b in zip(list(map(int, out.split())), list(map(int, out.split()))[1:]))),
@@ -437,7 +442,7 @@ def test_reference_programs_unmodified(tmp_path, jdf, srcs, args, check):
                               cxxflags=ptgpp.C_BODIES + (f"-I{d}", f"-I{REF}/tests", f"-I{REF}"))
     r = subprocess.run([exe] + args, capture_output=True, text=True, timeout=120, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    assert check(r.stdout), r.stdout[-2000:]
+    assert check(r.stdout + r.stderr), (r.stdout + r.stderr)[-2000:]
 
 
 @pytest.mark.parametrize("nranks", [2, 3, 4])
