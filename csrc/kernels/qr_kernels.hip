@@ -39,6 +39,22 @@ __device__ __forceinline__ void qr_release(int* table) {
 int* crit_cu_table();
 int cu_yield_mode();
 
+// The TS chain's sub-panel kernels (qr_sub2c, qr_subapply: 512 threads = 2
+// waves per SIMD) are held at <= 128 VGPRs so a workgroup fits on a CU beside
+// the one padded bulk GEMM workgroup (128 VGPRs x 2 waves per SIMD, 82 KB LDS,
+// device_hip_bulk_gemm_per_cu = 1). At 136 / 159 VGPRs they needed 272 / 320
+// of a SIMD's 512 and could only start on a CU with no bulk workgroup: under
+// load the launches averaged 269 / 222 us for ~60 us of work
+// (profiles/r4_qr32_kernels.txt). PARSEC_QR_VGPR_CAP=0 at build time lifts it.
+#ifndef PARSEC_QR_VGPR_CAP
+#define PARSEC_QR_VGPR_CAP 1
+#endif
+#if PARSEC_QR_VGPR_CAP
+#define QR_CHAIN_VGPR_CAP __attribute__((amdgpu_waves_per_eu(4)))
+#else
+#define QR_CHAIN_VGPR_CAP
+#endif
+
 void launch_gemm_batch(const GemmDesc* descs, int n, hipStream_t stream);  // tile_kernels.hip
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
@@ -730,7 +746,7 @@ __device__ __forceinline__ double wave_sum_dpp(double x) {
 }
 
 template <int RPL>
-__global__ __launch_bounds__(512) void qr_sub2c_kernel(const QrSub2Args args) {
+__global__ __launch_bounds__(512) QR_CHAIN_VGPR_CAP void qr_sub2c_kernel(const QrSub2Args args) {
   if (args.prio) __builtin_amdgcn_s_setprio(2);
   qr_claim(args.crit);
   constexpr int NW = 8, NC = 4;
@@ -948,7 +964,9 @@ static_assert(sizeof(QrSubApplyArgs) <= 4096, "QrSubApplyArgs exceeds the kernel
 // D(16x16) = A^T B over rows [rb, re): A (16 cols, lda), B (16 cols, ldb).
 // Lanes: m = lane & 15 is A's column, n = lane & 15 B's column, and MFMA u of
 // a 16-row step takes rows 4 (lane >> 4) + u, so each lane reads 4 consecutive
-// doubles per operand. 64 rows per group, the next group prefetched.
+// doubles per operand. 16 kS rows per group, the next group prefetched (kS = 2
+// under the VGPR cap: 4 x 16 doubles of operands in flight spilled at 128).
+constexpr int kAtbS = PARSEC_QR_VGPR_CAP ? 2 : 4;
 __device__ __forceinline__ double4_t mfma_atb(const double* __restrict__ A, int lda, int acols, const double* __restrict__ B, int ldb, int bcols,
                                               int rb, int re, int lane) {
   double4_t acc = {0.0, 0.0, 0.0, 0.0};
@@ -956,10 +974,11 @@ __device__ __forceinline__ double4_t mfma_atb(const double* __restrict__ A, int 
   const bool av = col < acols, bv = col < bcols;
   const double* ap = A + (size_t)(av ? col : 0) * lda;
   const double* bp = B + (size_t)(bv ? col : 0) * ldb;
-  double xa[16], ya[16];
+  constexpr int S = kAtbS, G = 16 * S;
+  double xa[4 * S], ya[4 * S];
   auto load = [&](int r0, double* x, double* y) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+    for (int s = 0; s < S; ++s)
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int r = r0 + 16 * s + kq + u;
@@ -969,15 +988,15 @@ __device__ __forceinline__ double4_t mfma_atb(const double* __restrict__ A, int 
       }
   };
   if (rb < re) load(rb, xa, ya);
-  for (int r0 = rb; r0 < re; r0 += 64) {
-    double xn[16], yn[16];
-    const bool more = r0 + 64 < re;
-    if (more) load(r0 + 64, xn, yn);
+  for (int r0 = rb; r0 < re; r0 += G) {
+    double xn[4 * S], yn[4 * S];
+    const bool more = r0 + G < re;
+    if (more) load(r0 + G, xn, yn);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[q], ya[q], acc, 0, 0, 0);
+    for (int q = 0; q < 4 * S; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[q], ya[q], acc, 0, 0, 0);
     if (more) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) { xa[q] = xn[q]; ya[q] = yn[q]; }
+      for (int q = 0; q < 4 * S; ++q) { xa[q] = xn[q]; ya[q] = yn[q]; }
     }
   }
   return acc;
@@ -986,7 +1005,7 @@ __device__ __forceinline__ double4_t mfma_atb(const double* __restrict__ A, int 
 constexpr int kSubApplyThreads = 512;
 
 __device__ __forceinline__ void qr_subapply_body(const QrSubApplyArgs& args);
-__global__ __launch_bounds__(kSubApplyThreads) void qr_subapply_kernel(const QrSubApplyArgs args) {
+__global__ __launch_bounds__(kSubApplyThreads) QR_CHAIN_VGPR_CAP void qr_subapply_kernel(const QrSubApplyArgs args) {
   if (args.prio) __builtin_amdgcn_s_setprio(2);
   qr_claim(args.crit);
   qr_subapply_body(args);
