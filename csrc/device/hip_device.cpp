@@ -1397,7 +1397,7 @@ void hip_devices_init(Context* ctx) {
   const int hp_crit = (int)params.reg_int("device", "hip", "hp_on_critical_stream", "High-priority tasks below the critical threshold share the critical stream (1), go to the least loaded bulk stream (0; measured 36.0 vs 38.9 TF at 16k, profiles/r3_route_ab.txt), or get stream 1 to themselves (2, bulk on streams 2..)", 1);
   const bool wprio = params.reg_int("device", "hip", "wave_priority", "Kernels of the critical stream raise their waves' issue priority (s_setprio) over co-resident bulk waves", 1) != 0;
   const bool trace = params.reg_int("device", "hip", "trace_launches", "Print every launched kernel group (stream, tasks, batch sizes) to stderr", 0) != 0;
-  int maxg = (int)params.reg_int("device", "hip", "max_inflight_batches", "Launched kernel groups per bulk stream before new bulk tasks wait for a larger batch (0 = no limit)", 2);
+  int maxg = (int)params.reg_int("device", "hip", "max_inflight_batches", "Launched kernel groups per bulk stream before new bulk tasks wait for a larger batch (0 = no limit; 1: +1-3 % at 16k / nb 512 over 2 in five A/B pairs, 64k within noise: profiles/r4_inflight_ab.txt)", 1);
   const int ccap = (int)params.reg_int("device", "hip", "critical_bulk_cap", "Launched kernel groups per bulk stream while the critical stream has work in flight (0 = max_inflight_batches)", 0);
   const int cuy = (int)params.reg_int("device", "hip", "cu_yield", "Cooperative CU yield: critical-path kernels claim their CUs and bulk GEMM workgroups on a claimed CU pause until it is free (0 off, 1 tile-POTRF steps claim, 2 every kernel of a critical group claims)", 0);
   const bool csplit = params.reg_int("device", "hip", "critical_split", "Critical-path tasks leave the critical stream as a group of their own and their successors are dispatched before other completions are released", 0) != 0;
