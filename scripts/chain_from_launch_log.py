@@ -14,7 +14,7 @@ for l in lines:
     if m: ev.append((int(m.group(1)), m.group(2), m.group(3)))
 t0 = ev[0][0]
 # per panel k: POTRF(k) launch, its R, TRSM group launch with TRSM(k, k+1), its R, SYRK(k,k+1) launch, R, POTRF(k+1) launch
-open_groups = {0: [], 1: [], 2: []}
+open_groups = {i: [] for i in range(8)}
 pl = {}
 def note(k, what, t):
     pl.setdefault(k, {})[what] = t - t0
