@@ -26,6 +26,7 @@ constexpr int kMaxStencilBatch = 24;
 struct StencilBatchArgs {
   int count;
   int xcd;  // remap workgroups so each XCD runs a contiguous range (g_stencil_xcd)
+  int kc;   // planes per workgroup of the vector kernel (g_stencil_kc)
   int start[kMaxStencilBatch + 1];  // first workgroup of each block update
   StencilDesc d[kMaxStencilBatch];
 };
@@ -85,8 +86,8 @@ __device__ __forceinline__ void st2_nt(double* p, double2 v) {
 }
 static int g_stencil_nt = -1;  // PARSEC_STENCIL_NT=0: plain stores for the block output
 
-template <bool NT>
-__device__ __forceinline__ void stencil7v_tile(const StencilArgs& a, int tx, int ty, int tz) {
+template <bool NT, int UNR>
+__device__ __forceinline__ void stencil7v_tile(const StencilArgs& a, int tx, int ty, int tz, int kc) {
   const int lane = threadIdx.x & 63;
   const int i = tx * 128 + lane * 2;
   const int j = ty * 4 + (threadIdx.x >> 6);
@@ -95,13 +96,16 @@ __device__ __forceinline__ void stencil7v_tile(const StencilArgs& a, int tx, int
   const size_t plane = (size_t)bx * by;
   const size_t row = (size_t)j * bx + i;
   const double* __restrict__ u = a.u;
-  const int k0 = tz * kStencilKc2, k1 = min(bz, k0 + kStencilKc2);
+  double* __restrict__ out = a.out;
+  const int k0 = tz * kc, k1 = min(bz, k0 + kc);
   const double2 zero = make_double2(0.0, 0.0);
   double2 zm = zero, c = zero;
   if (in) {
     zm = k0 > 0 ? ld2(u + (size_t)(k0 - 1) * plane + row) : (a.fin[4] ? ld2(a.fin[4] + row) : zero);
     c = ld2(u + (size_t)k0 * plane + row);
   }
+  // UNR > 1: the loads of UNR planes may be issued ahead (out is restrict)
+#pragma unroll UNR
   for (int k = k0; k < k1; ++k) {
     const size_t idx = (size_t)k * plane + row;
     double2 zp = zero, ym = zero, yp = zero;
@@ -120,8 +124,8 @@ __device__ __forceinline__ void stencil7v_tile(const StencilArgs& a, int tx, int
       double2 v;
       v.x = a.c0 * c.x + a.c1 * (left + c.y + ym.x + yp.x + zm.x + zp.x);
       v.y = a.c0 * c.y + a.c1 * (c.x + right + ym.y + yp.y + zm.y + zp.y);
-      if (NT) st2_nt(a.out + idx, v);
-      else st2(a.out + idx, v);
+      if (NT) st2_nt(out + idx, v);
+      else st2(out + idx, v);
       if (i == 0 && a.fout[0]) a.fout[0][(size_t)k * by + j] = v.x;
       if (i + 2 == bx && a.fout[1]) a.fout[1][(size_t)k * by + j] = v.y;
       if (j == 0 && a.fout[2]) st2(a.fout[2] + (size_t)k * bx + i, v);
@@ -134,7 +138,7 @@ __device__ __forceinline__ void stencil7v_tile(const StencilArgs& a, int tx, int
   }
 }
 
-static int stencil_wgs_v(const StencilArgs& a) { return ((a.bx + 127) / 128) * ((a.by + 3) / 4) * ((a.bz + kStencilKc2 - 1) / kStencilKc2); }
+static int stencil_wgs_v(const StencilArgs& a, int kc) { return ((a.bx + 127) / 128) * ((a.by + 3) / 4) * ((a.bz + kc - 1) / kc); }
 
 static bool stencil_vec_ok(const StencilArgs& a) {
   auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
@@ -155,7 +159,7 @@ __device__ __forceinline__ int xcd_contiguous(int b, int total) {
   return x * q + min(x, r) + (b >> 3);
 }
 
-template <bool NT>
+template <bool NT, int UNR>
 __global__ __launch_bounds__(256) void stencil7v_batch_kernel(const StencilBatchArgs args) {
   const int w = args.xcd ? xcd_contiguous((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
   int lo = 0, hi = args.count - 1;
@@ -167,7 +171,7 @@ __global__ __launch_bounds__(256) void stencil7v_batch_kernel(const StencilBatch
   const StencilArgs& a = args.d[lo];
   const int local = w - args.start[lo];
   const int nx = (a.bx + 127) / 128, ny = (a.by + 3) / 4;
-  stencil7v_tile<NT>(a, local % nx, (local / nx) % ny, local / (nx * ny));
+  stencil7v_tile<NT, UNR>(a, local % nx, (local / nx) % ny, local / (nx * ny), args.kc);
 }
 
 // Initial condition of a block (the same smooth bump as the host
@@ -222,6 +226,8 @@ void launch_stencil7(const StencilArgs& a, hipStream_t stream) {
 
 static int g_stencil_vec = -1;  // PARSEC_STENCIL_VEC=0 forces the scalar kernel
 static int g_stencil_xcd = 1;   // PARSEC_STENCIL_XCD=0: workgroups in dispatch order
+static int g_stencil_kc = kStencilKc2;  // PARSEC_STENCIL_KC: planes per workgroup (vector kernel)
+static int g_stencil_unr = 1;           // PARSEC_STENCIL_UNR=4: k loop unrolled 4x
 
 void launch_stencil7_batch(const StencilDesc* d, int n, hipStream_t stream) {
   if (g_stencil_vec < 0) {
@@ -231,23 +237,29 @@ void launch_stencil7_batch(const StencilDesc* d, int n, hipStream_t stream) {
     g_stencil_nt = n ? std::atoi(n) : 1;
     const char* x = std::getenv("PARSEC_STENCIL_XCD");
     g_stencil_xcd = x ? std::atoi(x) : 1;
+    const char* kc = std::getenv("PARSEC_STENCIL_KC");
+    g_stencil_kc = kc && std::atoi(kc) > 0 ? std::atoi(kc) : kStencilKc2;
+    const char* un = std::getenv("PARSEC_STENCIL_UNR");
+    g_stencil_unr = un ? std::atoi(un) : 1;
   }
   for (int s0 = 0; s0 < n; s0 += kMaxStencilBatch) {
     StencilBatchArgs a;
     a.count = std::min(kMaxStencilBatch, n - s0);
     a.xcd = g_stencil_xcd;
+    a.kc = g_stencil_kc;
     bool vec = g_stencil_vec != 0;
     for (int i = 0; i < a.count; ++i) vec = vec && stencil_vec_ok(d[s0 + i]);
     int total = 0;
     for (int i = 0; i < a.count; ++i) {
       a.d[i] = d[s0 + i];
       a.start[i] = total;
-      total += vec ? stencil_wgs_v(a.d[i]) : stencil_wgs(a.d[i]);
+      total += vec ? stencil_wgs_v(a.d[i], a.kc) : stencil_wgs(a.d[i]);
     }
     a.start[a.count] = total;
     if (total <= 0) continue;
-    if (vec && g_stencil_nt) hipLaunchKernelGGL(stencil7v_batch_kernel<true>, dim3(total), dim3(256), 0, stream, a);
-    else if (vec) hipLaunchKernelGGL(stencil7v_batch_kernel<false>, dim3(total), dim3(256), 0, stream, a);
+    if (vec && g_stencil_nt && g_stencil_unr > 1) hipLaunchKernelGGL((stencil7v_batch_kernel<true, 4>), dim3(total), dim3(256), 0, stream, a);
+    else if (vec && g_stencil_nt) hipLaunchKernelGGL((stencil7v_batch_kernel<true, 1>), dim3(total), dim3(256), 0, stream, a);
+    else if (vec) hipLaunchKernelGGL((stencil7v_batch_kernel<false, 1>), dim3(total), dim3(256), 0, stream, a);
     else hipLaunchKernelGGL(stencil7_batch_kernel, dim3(total), dim3(256), 0, stream, a);
   }
 }
