@@ -110,13 +110,23 @@ void devices_init(Context* ctx) {
   auto& reg = DeviceRegistry::instance();
   auto& params = ParamRegistry::instance();
   g_load_balance_skew = (double)params.reg_int("device", "", "load_balance_skew", "Allowed load imbalance (percent) before moving work off the data-owner device", 20);
+  const double cpu_g = (double)params.reg_int("device", "cpu", "gflops", "Override the CPU device fp64 GFLOP/s estimate (0 = estimate)", 0);
   if (reg.devices.empty()) {
-    double cpu_g = (double)params.reg_int("device", "cpu", "gflops", "Override the CPU device fp64 GFLOP/s estimate (0 = estimate)", 0);
     auto* cpu = new CpuDevice(ctx->nb_cores);
     if (cpu_g > 0) cpu->gflops_fp64 = cpu_g;
     reg.add(cpu);
     reg.add(new RecursiveDevice());
     hip_devices_init(ctx);
+    reg.registration_complete();
+  } else {
+    // the registry outlives a context: a later context's core count sets the
+    // CPU device's capability (and so the weights) again
+    for (auto* d : reg.devices)
+      if (d && d->type == DEV_CPU) {
+        auto* cpu = static_cast<CpuDevice*>(d);
+        cpu->gflops_fp64 = cpu_g > 0 ? cpu_g : std::max(1, ctx->nb_cores) * cpu->cap.ghz * cpu->cap.dp_flops_per_cycle;
+        cpu->gflops_fp32 = 2 * cpu->gflops_fp64;
+      }
     reg.registration_complete();
   }
   // the template device can be enabled by a later context of the same process
