@@ -482,17 +482,26 @@ int PtgTaskClass::prepare_input(ExecutionStream* es, Task* t) const {
 // share the reshaped copy through a DatacopyFuture kept on the source copy
 // (one per source version, one nested future per target datatype): the first
 // successor produces it, the others wait for and retain it, like the
-// reference's reshape promises. Writable inputs get a private copy. Host
-// copies only; device-resident inputs are passed unchanged.
+// reference's reshape promises. Writable inputs share it too: the reference
+// makes one reshaped copy per source copy and type for every successor,
+// whatever their access (tests/collections/reshape/
+// input_dep_single_copy_reshape.jdf checks that a write by one RW successor
+// is seen by the others). Host copies only; device-resident inputs are
+// passed unchanged.
 static SpinLock g_reshape_locks[64];
 
+// The elements travel in the source copy's own layout when it has as many as
+// the target (a type conversion, e.g. a LOWER_TILE copy read as UPPER_TILE:
+// reference local_input_LU_LL.jdf), otherwise the target layout selects them
+// from the source (a full tile read as LOWER_TILE).
 static DataCopy* reshape_produce(const ArenaDatatype* adt, const DataCopy* c) {
   const Datatype& want = adt->opaque_dtt;
   DataCopy* nc = adt->arena->get_copy(nullptr, 0);
   if (!nc) return nullptr;
   std::memset(nc->device_private, 0, adt->arena->elem_size);
   std::vector<uint8_t> tmp((size_t)want.packed_bytes());
-  want.pack(c->device_private, tmp.data());
+  const bool convert = c->dtt.kind != Datatype::NONE && c->dtt.packed_bytes() == want.packed_bytes();
+  (convert ? c->dtt : want).pack(c->device_private, tmp.data());
   want.unpack(tmp.data(), nc->device_private);
   nc->dtt = want;
   return nc;
@@ -542,6 +551,22 @@ void PtgTaskpool::drop_reshape_views() {
   }
 }
 
+// Reshape on output (reference parsec_reshape.c, `-> A T(..) [type = X]`): a
+// local successor reached through a typed output dependency receives the
+// producer's copy in layout X, one reshaped copy per source version and type
+// shared by every successor (the same future as the input-side reshape); the
+// successor's input dependency then finds the layout it names and does not
+// reshape again. Host copies only.
+static DataCopy* output_reshape(PtgTaskpool* tp, const DepTarget* tg, DataCopy* c) {
+  if (!c || !tg || tg->datatype_index <= 0 || c->device_index != 0) return c;
+  const auto& adts = tp->arenas_datatypes;
+  if (tg->datatype_index >= (int)adts.size()) return c;
+  const ArenaDatatype& adt = adts[tg->datatype_index];
+  if (!adt.arena || adt.opaque_dtt.kind == Datatype::NONE || adt.opaque_dtt == c->dtt) return c;
+  DataCopy* nc = static_cast<DataCopy*>(reshape_future_of(tp, c)->get_or_trigger(&adt));
+  return nc ? nc : c;
+}
+
 void PtgTaskClass::reshape_inputs(Task* t) const {
   auto& adts = t->taskpool->arenas_datatypes;
   for (size_t f = 0; f < def.flows.size(); ++f) {
@@ -549,17 +574,16 @@ void PtgTaskClass::reshape_inputs(Task* t) const {
     DataCopy* c = r.data_in;
     if (!c || c->device_index != 0 || def.flows[f].access == FLOW_CTL) continue;
     const DepTarget* tg = active_input(t->taskpool, (int)f, t->locals);
-    if (!tg || tg->datatype_index <= 0 || tg->datatype_index >= (int)adts.size()) continue;
-    const ArenaDatatype& adt = adts[tg->datatype_index];
+    if (!tg) continue;
+    // a collection read names its tile layout with [type_data = X] (reference
+    // remote_read_reshape.jdf): the task gets a copy of those elements
+    const int di = tg->kind == DEP_DATA && tg->data_datatype_index > 0 ? tg->data_datatype_index : tg->datatype_index;
+    if (di <= 0 || di >= (int)adts.size()) continue;
+    const ArenaDatatype& adt = adts[di];
     if (!adt.arena || adt.opaque_dtt.kind == Datatype::NONE || adt.opaque_dtt == c->dtt) continue;
-    DataCopy* nc = nullptr;
-    if (def.flows[f].access == FLOW_READ) {
-      std::shared_ptr<DatacopyFuture> fut = reshape_future_of(static_cast<PtgTaskpool*>(t->taskpool), c);
-      nc = static_cast<DataCopy*>(fut->get_or_trigger(&adt));
-      if (nc) data_copy_retain(nc);
-    } else {
-      nc = reshape_produce(&adt, c);
-    }
+    std::shared_ptr<DatacopyFuture> fut = reshape_future_of(static_cast<PtgTaskpool*>(t->taskpool), c);
+    DataCopy* nc = static_cast<DataCopy*>(fut->get_or_trigger(&adt));
+    if (nc) data_copy_retain(nc);
     if (!nc) continue;
     data_copy_release(c);
     r.data_in = nc;
@@ -603,8 +627,30 @@ DataCopy* PtgTaskClass::remote_reshape(const Taskpool* tp, const int32_t* PL, co
 
 // Copy `src` into the collection's own copy of `home` (final write of a flow
 // into a collection position it did not come from).
+// A typed dependency (`-> descA(m, k) [type = X type_data = Y]`, reference
+// jdf2c output-to-collection reshape) moves only the elements of the layout:
+// the flow's copy is read through X and written into the tile through Y (Y
+// defaults to X); host copies, equal packed sizes. Untyped: the whole tile.
 static int g_trace_writeback = -1;
-static void write_back(Data* home, DataCopy* src) {
+static bool typed_write_back(const Taskpool* tp, const DepTarget* tg, DataCopy* dst, const DataCopy* src) {
+  if (!tp || !tg || dst->device_index != 0 || src->device_index != 0) return false;
+  const auto& adts = tp->arenas_datatypes;
+  auto dtt_of = [&](int i) -> const Datatype* {
+    if (i <= 0 || i >= (int)adts.size() || adts[i].opaque_dtt.kind == Datatype::NONE) return nullptr;
+    return &adts[i].opaque_dtt;
+  };
+  const Datatype* a = dtt_of(tg->datatype_index);
+  const Datatype* b = dtt_of(tg->data_datatype_index);
+  if (!a && !b) return false;
+  if (!a) a = b;
+  if (!b) b = a;
+  if (a->packed_bytes() != b->packed_bytes()) return false;
+  std::vector<uint8_t> tmp((size_t)a->packed_bytes());
+  a->pack(src->device_private, tmp.data());
+  b->unpack(tmp.data(), dst->device_private);
+  return true;
+}
+static void write_back(Data* home, DataCopy* src, const Taskpool* tp = nullptr, const DepTarget* tg = nullptr) {
   if (g_trace_writeback < 0) g_trace_writeback = (int)ParamRegistry::instance().reg_int("ptg", "", "trace_writeback", "Log every final write of a flow into a collection tile (debug)", 0);
   if (g_trace_writeback)
     std::fprintf(stderr, "[writeback] home key %llu owner_dev %d src %p dev %d orig==home %d home copies:%s%s\n", (unsigned long long)(home ? home->key : 0),
@@ -617,7 +663,7 @@ static void write_back(Data* home, DataCopy* src) {
   if (!dst) return;
   size_t n = std::min(home->nb_elts, src->original ? src->original->nb_elts : home->nb_elts);
   if (g_trace_writeback) std::fprintf(stderr, "[writeback]   -> dst %p dev %d bytes %zu\n", dst->device_private, dst->device_index, n);
-  device_memcpy(dst->device_index, dst->device_private, src->device_index, src->device_private, n);
+  if (!typed_write_back(tp, tg, dst, src)) device_memcpy(dst->device_index, dst->device_private, src->device_index, src->device_private, n);
   std::lock_guard<SpinLock> g(home->lock);
   dst->version = home->newest_version() + 1;
 }
@@ -654,7 +700,7 @@ int PtgTaskClass::complete_execution(ExecutionStream* es, Task* t) const {
           uint32_t r = dst->rank_of(tp, TL);
           grapher_dep(es, t, dst, TL, dst->nb_params, (int)f, tg->dst_flow);
           if (r == my) {
-            tp->activate(es, dst, TL, tg->dst_flow, data, ready);
+            tp->activate(es, dst, TL, tg->dst_flow, output_reshape(tp, tg, data), ready);
           } else {
             if (!msg) {
               msg = new RemoteDepsMsg();
@@ -672,7 +718,7 @@ int PtgTaskClass::complete_execution(ExecutionStream* es, Task* t) const {
         collection_index(tp, X, tg->args, idx);
         const uint32_t r = dc->rank_of(idx, (int)tg->args.size());
         if (r == my) {
-          if (data) write_back(dc->data_of(idx, (int)tg->args.size()), data);
+          if (data) write_back(dc->data_of(idx, (int)tg->args.size()), data, tp, tg);
         } else if (fd.access != FLOW_CTL) {
           // final version of a tile owned by another rank (e.g. the R of a QR
           // TS chain): ship it; the owner writes it back in on_remote_activation.
@@ -1167,7 +1213,7 @@ void PtgTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& ac
         DataCollection* dc = tg->dc(this);
         int64_t idx[kMaxLocals];
         collection_index(this, X, tg->args, idx);
-        if (dc->rank_of(idx, (int)tg->args.size()) == my) write_back(dc->data_of(idx, (int)tg->args.size()), data);
+        if (dc->rank_of(idx, (int)tg->args.size()) == my) write_back(dc->data_of(idx, (int)tg->args.size()), data, this, tg);
       }
     });
   }

@@ -71,6 +71,7 @@ struct DepTarget {
   std::vector<CallArg> args;  // target parameters (TASK) or collection indices (DATA)
   std::function<DataCollection*(const Taskpool*)> dc;  // DEP_DATA
   int datatype_index = 0;     // arena / datatype slot ([type = ...]: NEW, local reshape)
+  int data_datatype_index = 0;  // [type_data = ...]: layout of a write into a collection tile
   // [type_remote / displ_remote / count_remote] (reference remote_dep_mpi.c:594-731):
   // what a successor on ANOTHER rank receives: count_remote elements of
   // type_remote starting displ_remote bytes into the producer's copy. -1: as `type`.

@@ -46,6 +46,15 @@
 #define PARSEC_ERR_NOT_SUPPORTED (-2)
 #define PARSEC_ERR_NOT_FOUND (-13)
 
+/* Object-system reference counts (reference parsec/class/parsec_object.h).
+ * Objects of this API are kept alive by the runtime's own reference counts
+ * (an arena is shared by every copy of its parsec_arena_datatype_t, a
+ * taskpool's arenas_datatypes hold their own references) or released by the
+ * explicit *_destroy / *_free calls, so a program's RETAIN / RELEASE pairs
+ * have nothing to balance: accepted for source compatibility. */
+#define PARSEC_OBJ_RETAIN(obj) ((void)(obj))
+#define PARSEC_OBJ_RELEASE(obj) ((void)(obj))
+
 /* device types (reference mca/device/device.h) */
 #define PARSEC_DEV_NONE 0x00
 #define PARSEC_DEV_CPU 0x01

@@ -287,8 +287,6 @@ _NO_COMPILE = {
     "tests/collections/two_dim_band/two_dim_band.jdf": "reads this_task->data._f_Y (the generated task struct layout; public-API port: tests/jdf/two_dim_band.jdf)",
     "tests/dsl/ptg/choice/choice.jdf": "reads taskpool->tdm.module (termination detector internals)",
     "tests/dsl/ptg/choice/choice2.jdf": "reads task->parsec_object (object system internals)",
-    "tests/dsl/ptg/complex_deps.jdf": "PARSEC_OBJ_RETAIN on a collection (object system)",
-    "tests/dsl/ptg/startup.jdf": "PARSEC_OBJ_RETAIN / RELEASE on a collection (object system)",
     "tests/dsl/ptg/ptgpp/too_many_local_vars.jdf": "includes a compiler-check header of the reference build tree",
     "tests/dsl/ptg/ptgpp/write_check.jdf": "MPI_Reduce outside PARSEC_HAVE_MPI guards",
     "tests/dsl/ptg/user-defined-functions/udf.jdf": "implements the internal parsec_key_fn_t hash-key interface",
@@ -419,6 +417,13 @@ def test_reference_bt_reduction(tmp_path, nranks, nt):
 # Reference test programs compiled UNMODIFIED (their JDF and their own C
 # drivers, from /root/reference, read in place) against include/parsec.h:
 # (jdf, driver sources, args, check on stdout)
+_RS = "tests/collections/reshape/"
+
+
+def _reshape_ok(n):
+    return lambda out: out.count(" PASSED") == n and "FAILED" not in out
+
+
 REF_PROGRAMS = [
     ("tests/api/touch.jdf", ["tests/api/touch_ex.c"], [], lambda out: out.count("STARTUP(") == 10 and "TASKS2(9)" in out),
     ("tests/runtime/dtt_bug_replicator.jdf", ["tests/runtime/dtt_bug_replicator_ex.c"], [],
@@ -429,6 +434,16 @@ REF_PROGRAMS = [
     ("tests/dsl/ptg/local-indices/local_indices.jdf", [], [], lambda out: True),
     ("tests/collections/kcyclic.jdf", [], [], lambda out: "M=02, N=08" in out),
     # WRITE C [count = data_size]: pure-output flows sized by the dependency's count
+    # reshape family (reference tests/collections/reshape, drivers + common.c unmodified, 1 rank):
+    # reshape on output / input / collection read (type_data) / write-back (type + type_data),
+    # one reshaped copy shared by every successor, LOWER -> UPPER type conversion
+    ("tests/collections/reshape/avoidable_reshape.jdf", [_RS + "testing_avoidable_reshape.c", _RS + "common.c"], [], _reshape_ok(1)),
+    ("tests/collections/reshape/input_dep_single_copy_reshape.jdf", [_RS + "testing_input_dep_reshape_single_copy.c", _RS + "common.c"], [], _reshape_ok(1)),
+    ("tests/collections/reshape/remote_multiple_outs_same_pred_flow.jdf",
+     [_RS + "remote_multiple_outs_same_pred_flow_multiple_deps.jdf", _RS + "testing_remote_multiple_outs_same_pred_flow.c", _RS + "common.c"], [], _reshape_ok(2)),
+    ("tests/collections/reshape/local_no_reshape.jdf",
+     [_RS + j + ".jdf" for j in ("local_read_reshape", "local_output_reshape", "local_input_reshape", "local_input_LU_LL", "remote_read_reshape", "remote_no_re_reshape")]
+     + [_RS + "testing_reshape.c", _RS + "common.c"], [], _reshape_ok(7)),
     ("tests/apps/merge_sort/merge_sort.jdf", ["tests/apps/merge_sort/main.c", "tests/apps/merge_sort/merge_sort_wrapper.c", "tests/apps/merge_sort/sort_data.c"],
      ["100"], lambda out: len(out.split()) == 500 and all(a >= b for a, b in zip(list(map(int, out.split())), list(map(int, out.split()))[1:]))),
 ]
@@ -438,7 +453,9 @@ REF_PROGRAMS = [
 @pytest.mark.parametrize("jdf,srcs,args,check", REF_PROGRAMS, ids=[os.path.basename(p[0]) for p in REF_PROGRAMS])
 def test_reference_programs_unmodified(tmp_path, jdf, srcs, args, check):
     d = os.path.dirname(os.path.join(REF, jdf))
-    exe = ptgpp.build_program(os.path.join(REF, jdf), str(tmp_path), extra_sources=[os.path.join(REF, x) for x in srcs],
+    # further JDFs of a multi-taskpool program are compiled next to the first
+    extra = [ptgpp.compile_jdf(os.path.join(REF, x), str(tmp_path), None)[0] if x.endswith(".jdf") else os.path.join(REF, x) for x in srcs]
+    exe = ptgpp.build_program(os.path.join(REF, jdf), str(tmp_path), extra_sources=extra,
                               cxxflags=ptgpp.C_BODIES + (f"-I{d}", f"-I{REF}/tests", f"-I{REF}"))
     r = subprocess.run([exe] + args, capture_output=True, text=True, timeout=120, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]

@@ -908,6 +908,7 @@ struct Gen {
     if (!ty) ty = find_prop(fprops, "type");
     if (ty) o << "__t.datatype_index = " << adt_index(ty->val) << "; ";
     if (const Prop* tr = find_prop(dprops, "type_remote")) o << "__t.remote_datatype_index = " << adt_index(tr->val) << "; ";
+    if (const Prop* td = find_prop(dprops, "type_data")) o << "__t.data_datatype_index = " << adt_index(td->val) << "; ";
     if (const Prop* d = find_prop(dprops, "displ_remote")) o << "__t.displ_remote = " << lam(f, prop_expr(*d), sc) << "; ";
     if (const Prop* d = find_prop(dprops, "count_remote")) o << "__t.count_remote = " << lam(f, prop_expr(*d), sc) << "; ";
     if (const Prop* d = find_prop(dprops, "count")) o << "__t.count = " << lam(f, prop_expr(*d), sc) << "; ";
@@ -978,7 +979,7 @@ struct Gen {
       for (auto& fl : f.flows) {
         if (const Prop* p = find_prop(fl.props, "type")) adt_index(p->val);
         for (auto& d : fl.deps)
-          for (const char* k : {"type", "type_remote"})
+          for (const char* k : {"type", "type_remote", "type_data"})
             if (const Prop* p = find_prop(d.props, k)) adt_index(p->val);
       }
     std::vector<std::string> adt_names(adt.size());
