@@ -119,9 +119,25 @@ struct CBlockCyclic : BlockCyclic {
   Data* data_of_key(uint64_t key) override { sync(); return BlockCyclic::data_of_key(key); }
 };
 
+// A collection the program filled in by hand (zeroed memory, myrank / nodes
+// and its callbacks assigned, no parsec_data_collection_init: the reference's
+// tests/dsl/ptg/branching/branching_data.c) gets its runtime side on first use.
+static std::mutex g_lazy_dc_m;
 DataCollection* impl_of(parsec_data_collection_t* dc) {
   if (!dc) return nullptr;
-  if (!dc->impl) fatal("data collection %p was not initialized (parsec_data_collection_init / parsec_matrix_block_cyclic_init)", (void*)dc);
+  if (!dc->impl) {
+    std::lock_guard<std::mutex> g(g_lazy_dc_m);
+    if (!dc->impl) {
+      if (!dc->rank_of && !dc->rank_of_key && !dc->data_of && !dc->data_of_key)
+        fatal("data collection %p was not initialized (parsec_data_collection_init / parsec_matrix_block_cyclic_init)", (void*)dc);
+      if (dc->nb_indices == 0) dc->nb_indices = 2;
+      auto* impl = new CCollection();
+      impl->c = dc;
+      impl->nodes = dc->nodes ? dc->nodes : 1;
+      impl->myrank = dc->myrank;
+      dc->impl = impl;
+    }
+  }
   return static_cast<DataCollection*>(dc->impl);
 }
 

@@ -17,10 +17,12 @@
 #ifndef PARSEC_AMD_PARSEC_H
 #define PARSEC_AMD_PARSEC_H
 
+#include <assert.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 #if !defined(_WIN32)
 #include <unistd.h> /* getopt / getpid: the reference's headers bring them in */
 #endif
@@ -54,6 +56,11 @@
  * have nothing to balance: accepted for source compatibility. */
 #define PARSEC_OBJ_RETAIN(obj) ((void)(obj))
 #define PARSEC_OBJ_RELEASE(obj) ((void)(obj))
+/* A class instance names a taskpool type's constructor / destructor (e.g. a
+ * wrapper's destructor that frees the datatypes of its arenas). The runtime
+ * releases a taskpool's arenas and datatypes itself when it is freed, so the
+ * declaration only has to compile. */
+#define PARSEC_OBJ_CLASS_INSTANCE(NAME, PARENT, CTOR, DTOR) struct parsec_obj_class_instance_##NAME##_s
 
 /* device types (reference mca/device/device.h) */
 #define PARSEC_DEV_NONE 0x00
@@ -73,6 +80,7 @@ struct ExecutionStream;
 struct Data;
 struct DataCopy;
 struct ArenaDatatype;
+struct Datatype;
 }  // namespace parsec
 typedef parsec::Context parsec_context_t;
 typedef parsec::Taskpool parsec_taskpool_t;
@@ -656,6 +664,10 @@ void parsec_profiling_trace_f08(int key, int64_t event_id, int taskpool_id, int*
 
 #ifdef __cplusplus
 }
+/* C++ view of a taskpool's arenas_datatypes[i].opaque_dtt (a parsec::Datatype,
+ * not a handle): the reference's wrappers free it in their destructors. The
+ * datatype belongs to its arena datatype, which the runtime releases. */
+inline int parsec_type_free(parsec::Datatype*) { return PARSEC_SUCCESS; }
 #endif
 
 #endif /* PARSEC_AMD_PARSEC_H */

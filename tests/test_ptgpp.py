@@ -444,6 +444,12 @@ REF_PROGRAMS = [
     ("tests/collections/reshape/local_no_reshape.jdf",
      [_RS + j + ".jdf" for j in ("local_read_reshape", "local_output_reshape", "local_input_reshape", "local_input_LU_LL", "remote_read_reshape", "remote_no_re_reshape")]
      + [_RS + "testing_reshape.c", _RS + "common.c"], [], _reshape_ok(7)),
+    # the reference's own drivers: BT_reduction (main.c + wrapper with its class-instance
+    # destructor + reduc_data.c), branching (a collection filled in by hand, no init call)
+    ("tests/apps/generalized_reduction/BT_reduction.jdf",
+     ["tests/apps/generalized_reduction/" + x for x in ("BT_reduction_wrapper.c", "reduc_data.c", "main.c")], [], lambda out: "21" in out.split()),
+    ("tests/dsl/ptg/branching/branching.jdf", ["tests/dsl/ptg/branching/" + x for x in ("branching_data.c", "branching_wrapper.c", "main.c")], [],
+     lambda out: "nb_taskA = 10, nb_taskB = 20, nb_taskC = 10" in out),
     ("tests/apps/merge_sort/merge_sort.jdf", ["tests/apps/merge_sort/main.c", "tests/apps/merge_sort/merge_sort_wrapper.c", "tests/apps/merge_sort/sort_data.c"],
      ["100"], lambda out: len(out.split()) == 500 and all(a >= b for a, b in zip(list(map(int, out.split())), list(map(int, out.split()))[1:]))),
 ]
