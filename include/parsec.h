@@ -89,6 +89,10 @@ typedef parsec::ExecutionStream parsec_execution_stream_t;
 typedef parsec::Data parsec_data_t;
 typedef parsec::DataCopy parsec_data_copy_t;
 typedef parsec::ArenaDatatype parsec_arena_datatype_t;
+/* programs that spell the C struct tags (`struct parsec_data_s *d;`, reference
+ * tests/apps/pingpong/rtt_data.c) name the same classes when compiled as C++ */
+#define parsec_data_s parsec::Data
+#define parsec_data_copy_s parsec::DataCopy
 extern "C" {
 #else
 typedef struct parsec_context_s parsec_context_t;

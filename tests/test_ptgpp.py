@@ -450,6 +450,9 @@ REF_PROGRAMS = [
      ["tests/apps/generalized_reduction/" + x for x in ("BT_reduction_wrapper.c", "reduc_data.c", "main.c")], [], lambda out: "21" in out.split()),
     ("tests/dsl/ptg/branching/branching.jdf", ["tests/dsl/ptg/branching/" + x for x in ("branching_data.c", "branching_wrapper.c", "main.c")], [],
      lambda out: "nb_taskA = 10, nb_taskB = 20, nb_taskC = 10" in out),
+    # pingpong round trip (main.c + rtt_wrapper.c + rtt_data.c: a hand-filled collection whose
+    # data handle is declared as `struct parsec_data_s *`); success = clean exit
+    ("tests/apps/pingpong/rtt.jdf", ["tests/apps/pingpong/" + x for x in ("rtt_data.c", "rtt_wrapper.c", "main.c")], [], lambda out: True),
     ("tests/apps/merge_sort/merge_sort.jdf", ["tests/apps/merge_sort/main.c", "tests/apps/merge_sort/merge_sort_wrapper.c", "tests/apps/merge_sort/sort_data.c"],
      ["100"], lambda out: len(out.split()) == 500 and all(a >= b for a, b in zip(list(map(int, out.split())), list(map(int, out.split()))[1:]))),
 ]
