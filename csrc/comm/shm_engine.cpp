@@ -246,7 +246,25 @@ int ShmEngine::probe_ipc(int local_rc) {
       hipIpcMemHandle_t ph;
       std::memcpy(&ph, static_cast<ShmHeader*>(maps_[r])->ipc_probe, sizeof(ph));
       void* p = nullptr;
-      if (hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess) != hipSuccess) { (void)hipGetLastError(); rc = -20 - r; break; }
+      // 8 processes mapping each other's buffers on one GPU: an open has been
+      // seen to fail once and succeed on the next try (round-3/4 validation,
+      // rank 4 -> rank 1); a few spaced attempts before giving the plane up
+      hipError_t oe = hipSuccess;
+      for (int attempt = 0; attempt < 5; ++attempt) {
+        oe = hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess);
+        if (oe == hipSuccess) {
+          if (attempt > 0) warning("IPC probe: rank %d mapped rank %d's buffer at attempt %d", rank, r, attempt + 1);
+          break;
+        }
+        (void)hipGetLastError();
+        p = nullptr;
+        std::this_thread::sleep_for(std::chrono::milliseconds(5 * (attempt + 1)));
+      }
+      if (oe != hipSuccess) {
+        warning("IPC probe: rank %d cannot map rank %d's buffer: %s", rank, r, hipGetErrorString(oe));
+        rc = -20 - r;
+        break;
+      }
       // the tail of the peer buffer, through the copy stream the pulls use
       if (!st || hipMemcpyAsync(got.data(), static_cast<char*>(p) + bytes - got.size(), got.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
           hipStreamSynchronize(st) != hipSuccess) {
@@ -655,7 +673,14 @@ void* ShmEngine::ipc_open(int src, const void* handle64) {
   hipIpcMemHandle_t h;
   std::memcpy(&h, handle64, sizeof(h));
   void* p = nullptr;
-  hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+  hipError_t e = hipSuccess;
+  for (int attempt = 0; attempt < 5; ++attempt) {  // see probe_ipc: transient open failures
+    e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+    if (e == hipSuccess) break;
+    (void)hipGetLastError();
+    p = nullptr;
+    std::this_thread::sleep_for(std::chrono::milliseconds(5 * (attempt + 1)));
+  }
   if (e != hipSuccess) fatal("hipIpcOpenMemHandle (from rank %d) failed: %s", src, hipGetErrorString(e));
   ipc_opened_[key] = p;
   return p;
