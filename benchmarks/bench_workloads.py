@@ -55,11 +55,6 @@ def bench_qr(args):
 
     pa.require_native()
     pa.mca_set("device_hip_mask", str(1 << local))
-    # two bulk groups in flight per bulk stream: the engine default (1) is tuned on
-    # DPOTRF's critical chain; DGEQRF's TS chain does better with a deeper bulk
-    # queue (profiles/r4_qr_knobs.txt). An explicit PARSEC_MCA_ setting wins.
-    if "PARSEC_MCA_device_hip_max_inflight_batches" not in os.environ:
-        pa.mca_set("device_hip_max_inflight_batches", "2")
     _comm(pa, world, rank, local)
     ctx = pa.init(args.cores)
 

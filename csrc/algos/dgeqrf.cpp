@@ -152,6 +152,7 @@ ptg::PtgTaskpool* dgeqrf_new(TiledMatrix* A, TiledMatrix* T, int ib) {
   if (A->mb != A->nb || T->mb < A->nb || T->nb < A->nb) fatal("dgeqrf: square tiles required and T tiles must be at least nb x nb");
   auto* tp = new DgeqrfTaskpool();
   tp->taskpool_name = "dgeqrf";
+  tp->bulk_inflight_hint = 2;  // the TS chain prefers a deeper bulk queue (profiles/r4_qr_knobs.txt)
   const int64_t MT = A->mt, NT = A->nt, KT = std::min(MT, NT);
   const int64_t nb = A->nb;
   const int ld = (int)A->mb, ldt = (int)T->mb;

@@ -119,6 +119,7 @@ ptg::PtgTaskpool* dgeqrf_hqr_new(TiledMatrix* A, TiledMatrix* T, TiledMatrix* TT
   }
   auto* tp = new DgeqrfHqrTaskpool();
   tp->taskpool_name = "dgeqrf_hqr";
+  tp->bulk_inflight_hint = 2;  // the TS chain prefers a deeper bulk queue (profiles/r4_qr_knobs.txt)
   const int64_t MT = A->mt, NT = A->nt, KT = std::min(MT, NT);
   const int64_t nb = A->nb;
   const int ld = (int)A->mb, ldt = (int)T->mb, ldtt = (int)TT->mb;

@@ -137,6 +137,12 @@ bool ParamRegistry::lookup(const std::string& full, std::string& value) {
   return src != "default";
 }
 
+std::string ParamRegistry::source(const std::string& full) {
+  std::lock_guard<std::mutex> g(m_);
+  auto it = params_.find(full);
+  return it != params_.end() ? it->second.source : std::string();
+}
+
 std::vector<ParamInfo> ParamRegistry::dump() {
   std::lock_guard<std::mutex> g(m_);
   std::vector<ParamInfo> out;

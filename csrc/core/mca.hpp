@@ -36,6 +36,8 @@ class ParamRegistry {
   void set_override(const std::string& full_name, const std::string& value);
   void clear_override(const std::string& full_name);
   bool lookup(const std::string& full_name, std::string& value);
+  // where a registered parameter's value came from ("default", "env", ...; "" if unknown)
+  std::string source(const std::string& full_name);
   std::vector<ParamInfo> dump();
   void load_files();  // $HOME/.parsec/mca-params.conf, $PARSEC_MCA_PARAM_FILES
   // Parse argv: consumes "--mca k v" and "-mca k v" pairs, returns remaining args.

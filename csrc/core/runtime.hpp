@@ -389,6 +389,9 @@ struct Taskpool {
   std::string termdet_name;          // "" = context default
   std::atomic<bool> completed{false};
   std::vector<ArenaDatatype> arenas_datatypes;
+  // GPU engine hint: launched bulk kernel groups per bulk stream for this
+  // taskpool's tasks (0 = device_hip_max_inflight_batches). DGEQRF asks for 2.
+  int bulk_inflight_hint = 0;
   // distributed
   bool registered = false;
   bool is_dtd = false;

@@ -1049,8 +1049,10 @@ void HipDevice::execute_ready() {
       const int b0 = hp_lane ? 2 : 1, nbulk = nb_exec_streams - b0;
       // while critical-path work runs, bulk streams keep a shallower queue
       // (critical_bulk_cap): a bulk group launched now would share the CUs with it
-      const int cap = (critical_bulk_cap > 0 && !executing[0].empty()) ? std::min(critical_bulk_cap, max_inflight_groups > 0 ? max_inflight_groups : critical_bulk_cap)
-                                                                        : max_inflight_groups;
+      // a taskpool can ask for its own depth (Taskpool::bulk_inflight_hint), unless
+      // the parameter was set explicitly
+      const int maxg = (t->taskpool && t->taskpool->bulk_inflight_hint > 0 && !max_inflight_explicit) ? t->taskpool->bulk_inflight_hint : max_inflight_groups;
+      const int cap = (critical_bulk_cap > 0 && !executing[0].empty()) ? std::min(critical_bulk_cap, maxg > 0 ? maxg : critical_bulk_cap) : maxg;
       s = -1;
       for (int i = 0; i < nbulk && s < 0; ++i)  // join a batch already open this round
         if (!round_tasks[b0 + i].empty()) s = b0 + i;
@@ -1430,6 +1432,7 @@ void hip_devices_init(Context* ctx) {
     d->hp_route = hp_crit;
     d->roctx = roctx_on;
     d->max_inflight_groups = maxg;
+    d->max_inflight_explicit = params.source(ParamRegistry::join("device", "hip", "max_inflight_batches")) != "default";
     d->critical_bulk_cap = ccap;
     d->critical_split = csplit;
     d->cu_yield = cuy;

@@ -187,6 +187,7 @@ struct HipDevice : Device {
   bool roctx = true;  // roctx ranges around every launched group (rocprofv3 --marker-trace)
   uint32_t rr_stream = 0;
   int max_inflight_groups = 2;  // bulk streams: launched groups in flight before new bulk work waits (0 = no limit)
+  bool max_inflight_explicit = false;  // set by the user: taskpool hints do not override it
   int critical_bulk_cap = 0;    // the same limit while the critical stream has work in flight (0 = max_inflight_groups)
   bool critical_split = false;
   int cu_yield = 0;  // critical tasks leave stream 0 as their own group; their release goes first
