@@ -18,6 +18,7 @@
 #define PARSEC_AMD_PARSEC_H
 
 #include <assert.h>
+#include <stdarg.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <stdio.h>

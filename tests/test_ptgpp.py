@@ -533,3 +533,22 @@ def test_stage_properties_diagnostics(tmp_path, props, msg):
     r = subprocess.run([ptgpp.PTGPP, "-i", str(p), "-o", str(tmp_path / "bad")], capture_output=True, text=True)
     assert r.returncode != 0
     assert msg in r.stderr + r.stdout
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+def test_reference_reduce_program(tmp_path):
+    """The reference's tests/collections/reduce.c with the library JDF it was
+    written for (parsec/data_dist/matrix/reduce.jdf, compiled by parsec-ptgpp
+    into the header path the driver includes): a binary reduction tree over
+    the tiles of a 1 x NT matrix, both files unmodified."""
+    inc = tmp_path / "parsec" / "data_dist" / "matrix"
+    cpp, _ = ptgpp.compile_jdf(os.path.join(REF, "parsec/data_dist/matrix/reduce.jdf"), str(inc), None)
+    cc, libs = ptgpp.compile_flags(False)
+    exe = str(tmp_path / "reduce")
+    r = subprocess.run(cc + list(ptgpp.C_BODIES) + [f"-I{tmp_path}", f"-I{inc}", f"-I{REF}/tests", f"-I{REF}", cpp, "-x", "c++",
+                                                    os.path.join(REF, "tests/collections/reduce.c"), "-o", exe] + libs, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    # the root of the tree combines the two halves last
+    assert "reduce(level = 5, process = 0) 0 16" in r.stdout, r.stdout[-2000:]
