@@ -68,6 +68,27 @@ ptg::PtgTaskpool* map_operator_new(TiledMatrix* src, TiledMatrix* dst, MapOp op)
   tp->taskpool_name = "map_operator";
   TaskClassDef d;
   d.name = "MAP";
+  if (!dst) {  // in place on src: one RW flow, the operator's destination is NULL
+    d.locals = {range_local("m", cst(0), cst(src->mt - 1)), range_local("n", cst(0), cst(src->nt - 1))};
+    d.affinity_dc = [src](const Taskpool*) { return (DataCollection*)src; };
+    d.affinity_args = {loc(0), loc(1)};
+    FlowDef S;
+    S.name = "S"; S.access = FLOW_RW;
+    S.in = {always(data(src, loc(0), loc(1)))};
+    S.out = {always(data(src, loc(0), loc(1)))};
+    d.flows = {S};
+    BodyDef b;
+    b.type = DEV_CPU;
+    b.cpu = [op, src](ExecutionStream*, Task* t) {
+      const int64_t m = t->locals[0], n = t->locals[1];
+      op(fptr(t, 0), nullptr, m, n, src->tile_rows(m), src->tile_cols(n));
+      return HOOK_DONE;
+    };
+    d.bodies = {b};
+    tp->add_task_class(std::move(d));
+    tp->finalize();
+    return tp;
+  }
   d.locals = {range_local("m", cst(0), cst(dst->mt - 1)), range_local("n", cst(0), cst(dst->nt - 1))};
   d.affinity_dc = [dst](const Taskpool*) { return (DataCollection*)dst; };
   d.affinity_args = {loc(0), loc(1)};

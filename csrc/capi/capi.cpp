@@ -945,7 +945,9 @@ int parsec_apply(parsec_context_t* parsec, parsec_matrix_uplo_t uplo, parsec_til
   return PARSEC_SUCCESS;
 }
 parsec_taskpool_t* parsec_map_operator_New(const parsec_tiled_matrix_t* src, parsec_tiled_matrix_t* dest, parsec_operator_t op, void* op_data) {
-  return algos::map_operator_new(tm_of(src), tm_of(dest), [op, op_data](const void* s, void* d, int64_t m, int64_t n, int64_t, int64_t) {
+  // dest NULL: the operator runs on the source tiles alone (reference
+  // map_operator.c; tests/api/operator.c prints every tile this way)
+  return algos::map_operator_new(tm_of(src), dest ? tm_of(dest) : nullptr, [op, op_data](const void* s, void* d, int64_t m, int64_t n, int64_t, int64_t) {
     op(my_execution_stream(), s, d, op_data, (int)m, (int)n);
   });
 }

@@ -580,7 +580,7 @@ void remote_dep_init(Context* ctx) {
     ctx->comm = g_ce;
     auto* es = new ExecutionStream();
     es->ctx = ctx;
-    es->vp = ctx->vps[0];
+    es->virtual_process = ctx->vps[0];
     es->is_manager = true;
     es->th_id = 2000;
     es->slot = -1;

@@ -232,7 +232,7 @@ Context* context_init(int nb_cores, std::vector<std::string>& args) {
     for (int tid : vps[v]) {
       auto* es = new ExecutionStream();
       es->th_id = tid;
-      es->vp = vp;
+      es->virtual_process = vp;
       es->ctx = ctx;
       es->rand_seed = 1234567u + 7919u * tid;
       if (!cpus.empty()) {

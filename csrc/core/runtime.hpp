@@ -469,7 +469,7 @@ struct alignas(64) ExecutionStream {  // one thread writes it per task: keep it 
   int core_id = -1;
   int socket_id = 0;
   int slot = 0;           // mempool slot
-  VirtualProcess* vp = nullptr;
+  VirtualProcess* virtual_process = nullptr;
   Context* ctx = nullptr;
   Task* next_task = nullptr;
   void* sched_obj = nullptr;

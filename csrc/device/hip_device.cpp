@@ -374,7 +374,7 @@ void HipDevice::start(Context* c) {
   for (int i = 0; i < total_streams; ++i) stream_infos.emplace_back(new InfoArray(&gpu_stream_infos(), (void*)s_exec[i]));
   es = new ExecutionStream();
   es->ctx = c;
-  es->vp = c->vps[0];
+  es->virtual_process = c->vps[0];
   es->is_manager = true;
   es->th_id = 1000 + device_index;
   c->aux_es.push_back(es);

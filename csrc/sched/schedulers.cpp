@@ -190,7 +190,7 @@ struct VpSystemQueue {
   SortedQueue q;
 };
 
-static VpSystemQueue* vpq(ExecutionStream* es) { return static_cast<VpSystemQueue*>(es->vp->sched_obj); }
+static VpSystemQueue* vpq(ExecutionStream* es) { return static_cast<VpSystemQueue*>(es->virtual_process->sched_obj); }
 
 static void install_vp_queues(Context* ctx) {
   for (auto* vp : ctx->vps) vp->sched_obj = new VpSystemQueue();
@@ -334,7 +334,7 @@ class LhqScheduler : public Scheduler {
     remove_vp_queues(ctx);
   }
  private:
-  static int key(ExecutionStream* es) { return es->vp->vp_id * 4096 + es->socket_id; }
+  static int key(ExecutionStream* es) { return es->virtual_process->vp_id * 4096 + es->socket_id; }
   std::map<int, HBBuffer*> socket_buf_;
 };
 
@@ -350,7 +350,7 @@ class VpListScheduler : public Scheduler {
     return 0;
   }
   int schedule(ExecutionStream* es, Task** tasks, int n, int32_t) override {
-    Q* q = static_cast<Q*>(es->vp->sched_obj);
+    Q* q = static_cast<Q*>(es->virtual_process->sched_obj);
     std::lock_guard<SpinLock> g(q->lock);
     for (int i = 0; i < n; ++i) {
       int32_t key = tasks[i]->priority;
@@ -363,7 +363,7 @@ class VpListScheduler : public Scheduler {
   }
   Task* select(ExecutionStream* es, int32_t* distance) override {
     *distance = 0;
-    Q* q = static_cast<Q*>(es->vp->sched_obj);
+    Q* q = static_cast<Q*>(es->virtual_process->sched_obj);
     if (q->count.load(std::memory_order_acquire) == 0) return nullptr;  // unlocked fast path: atomic count only
     std::lock_guard<SpinLock> g(q->lock);
     if (q->items.empty()) return nullptr;
@@ -399,7 +399,7 @@ class SpqScheduler : public Scheduler {
     return 0;
   }
   int schedule(ExecutionStream* es, Task** tasks, int n, int32_t distance) override {
-    Q* q = static_cast<Q*>(es->vp->sched_obj);
+    Q* q = static_cast<Q*>(es->virtual_process->sched_obj);
     SortedQueue* lvl;
     {
       std::lock_guard<SpinLock> g(q->lock);
@@ -410,7 +410,7 @@ class SpqScheduler : public Scheduler {
     return 0;
   }
   Task* select(ExecutionStream* es, int32_t* distance) override {
-    Q* q = static_cast<Q*>(es->vp->sched_obj);
+    Q* q = static_cast<Q*>(es->virtual_process->sched_obj);
     std::vector<SortedQueue*> lv;
     {
       std::lock_guard<SpinLock> g(q->lock);
@@ -440,7 +440,7 @@ class GdScheduler : public Scheduler {
     return 0;
   }
   int schedule(ExecutionStream* es, Task** tasks, int n, int32_t) override {
-    auto* q = static_cast<Dequeue<Task>*>(es->vp->sched_obj);
+    auto* q = static_cast<Dequeue<Task>*>(es->virtual_process->sched_obj);
     std::lock_guard<SpinLock> g(q->lock());
     List& l = q->raw();
     for (int i = n - 1; i >= 0; --i) {  // reverse: the highest priority ends at the front
@@ -453,7 +453,7 @@ class GdScheduler : public Scheduler {
   }
   Task* select(ExecutionStream* es, int32_t* distance) override {
     *distance = 0;
-    return static_cast<Dequeue<Task>*>(es->vp->sched_obj)->pop_front();
+    return static_cast<Dequeue<Task>*>(es->virtual_process->sched_obj)->pop_front();
   }
   void remove(Context* ctx) override {
     for (auto* vp : ctx->vps) { delete static_cast<Dequeue<Task>*>(vp->sched_obj); vp->sched_obj = nullptr; }

@@ -552,3 +552,22 @@ def test_reference_reduce_program(tmp_path):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     # the root of the tree combines the two halves last
     assert "reduce(level = 5, process = 0) 0 16" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("name,check", [
+    ("operator", lambda out: sum(l.startswith("tile (") for l in out.splitlines()) == 100),   # map operator, NULL destination
+    ("compose", lambda out: sum(l.startswith("tp1:") for l in out.splitlines()) == 10 and sum(l.startswith("tp2:") for l in out.splitlines()) == 10),
+])
+def test_reference_api_programs(tmp_path, name, check):
+    """The reference's tests/api/{operator,compose}.c (C programs over the public
+    API, no JDF), compiled as C++ against this runtime's headers, unmodified:
+    the operator callbacks read es->th_id and es->virtual_process->vp_id."""
+    cc, libs = ptgpp.compile_flags(False)
+    exe = str(tmp_path / name)
+    r = subprocess.run(cc + list(ptgpp.C_BODIES) + [f"-I{REF}/tests", f"-I{REF}", "-x", "c++", os.path.join(REF, "tests/api", name + ".c"), "-o", exe] + libs,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert check(r.stdout), r.stdout[-2000:]
