@@ -243,6 +243,7 @@ Context* context_init(int nb_cores, std::vector<std::string>& args) {
         es->l3_id = ct.l3;
       }
       vp->es.push_back(es);
+      vp->nb_cores = (int)vp->es.size();
       ctx->all_es.push_back(es);
     }
     ctx->vps.push_back(vp);

@@ -485,6 +485,7 @@ struct alignas(64) ExecutionStream {  // one thread writes it per task: keep it 
 
 struct VirtualProcess {
   int vp_id = 0;
+  int nb_cores = 0;  // compute streams of this VP (reference field name)
   std::vector<ExecutionStream*> es;
   void* sched_obj = nullptr;
 };
@@ -556,6 +557,7 @@ struct Context {
   int my_rank = 0;
   int nb_nodes = 1;
   std::vector<VirtualProcess*> vps;
+  std::vector<VirtualProcess*>& virtual_processes = vps;  // the reference's name for programs that read it
   std::vector<ExecutionStream*> all_es;  // compute threads, th_id order
   std::vector<ExecutionStream*> aux_es;  // managers / comm thread
   Scheduler* scheduler = nullptr;

@@ -571,3 +571,19 @@ def test_reference_api_programs(tmp_path, name, check):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert check(r.stdout), r.stdout[-2000:]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+def test_reference_stencil_1d_program(tmp_path):
+    """The reference's 1D stencil application (tests/apps/stencil: stencil_1D.jdf,
+    stencil_internal.c, testing_stencil_1D.c, unmodified). Its loop body is the
+    output of the reference's loop_gen_1D script for radius 1, written here;
+    the driver reads the context's VP core counts (parsec->virtual_processes)."""
+    d = os.path.join(REF, "tests/apps/stencil")
+    (tmp_path / "loop_body_1D.in").write_text("      OUT(i,j) = WEIGHT_1D(0)*IN(i,j)\n        +WEIGHT_1D(-1)*IN(i,j-1)+WEIGHT_1D(1)*IN(i,j+1)\n        ;\n")
+    exe = ptgpp.build_program(os.path.join(d, "stencil_1D.jdf"), str(tmp_path), extra_sources=[os.path.join(d, "stencil_internal.c"), os.path.join(d, "testing_stencil_1D.c")],
+                              cxxflags=ptgpp.C_BODIES + (f"-I{tmp_path}", f"-I{d}", f"-I{REF}/tests", f"-I{REF}"))
+    r = subprocess.run([exe, "-M", "64", "-N", "64", "-t", "8", "-T", "8", "-I", "20"], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "Stencil\tN= 64" in r.stdout and "Iteration= 20" in r.stdout, r.stdout[-2000:]
