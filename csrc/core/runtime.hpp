@@ -378,7 +378,14 @@ struct Taskpool {
   uint32_t devices_index_mask = 0xffffffffu;
   Context* context = nullptr;
   std::vector<TaskClass*> task_classes;
-  TermdetModule* tdm = nullptr;
+  // termination detector; `tdm.module` is the reference's spelling (tests/dsl/ptg/
+  // user-defined-functions/utt.jdf calls tdm.module->taskpool_set_nb_tasks)
+  struct TermdetRef {
+    TermdetModule* module = nullptr;
+    TermdetModule* operator->() const { return module; }
+    operator TermdetModule*() const { return module; }
+    TermdetRef& operator=(TermdetModule* m) { module = m; return *this; }
+  } tdm;
   // termdet bookkeeping (interpreted by the module)
   std::atomic<int64_t> nb_tasks{0};
   std::atomic<int64_t> nb_pending_actions{0};

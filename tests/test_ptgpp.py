@@ -279,18 +279,15 @@ _NO_COMPILE = {
     "tests/apps/haar_tree/project.jdf": "tree_dist.h uses the internal parsec_hash_table class",
     "tests/apps/haar_tree/project_dyn.jdf": "tree_dist.h uses the internal parsec_hash_table class (public-API port: tests/jdf/project_dyn.jdf)",
     "tests/apps/haar_tree/walk.jdf": "tree_dist.h uses the internal parsec_hash_table class",
-    "tests/apps/pingpong/bandwidth.jdf": "reads context->virtual_processes (internal)",
     "tests/collections/redistribute/redistribute_bound.jdf": "MPI calls outside PARSEC_HAVE_MPI guards, context->virtual_processes",
     "tests/collections/redistribute/redistribute_check.jdf": "MPI calls outside PARSEC_HAVE_MPI guards",
     "tests/collections/redistribute/redistribute_check2.jdf": "MPI calls outside PARSEC_HAVE_MPI guards",
     "tests/collections/redistribute/redistribute_no_optimization.jdf": "MPI calls outside PARSEC_HAVE_MPI guards",
     "tests/collections/two_dim_band/two_dim_band.jdf": "reads this_task->data._f_Y (the generated task struct layout; public-API port: tests/jdf/two_dim_band.jdf)",
-    "tests/dsl/ptg/choice/choice.jdf": "reads taskpool->tdm.module (termination detector internals)",
     "tests/dsl/ptg/choice/choice2.jdf": "reads task->parsec_object (object system internals)",
     "tests/dsl/ptg/ptgpp/too_many_local_vars.jdf": "includes a compiler-check header of the reference build tree",
     "tests/dsl/ptg/ptgpp/write_check.jdf": "MPI_Reduce outside PARSEC_HAVE_MPI guards",
     "tests/dsl/ptg/user-defined-functions/udf.jdf": "implements the internal parsec_key_fn_t hash-key interface",
-    "tests/dsl/ptg/user-defined-functions/utt.jdf": "reads taskpool->tdm.module (termination detector internals)",
     "tests/profiling/async.jdf": "calls __parsec_schedule and the internal list classes",
     "tests/runtime/multichain.jdf": "MPI communicators, tp->super.nb_tasks of the C taskpool layout",
 }
@@ -453,6 +450,8 @@ REF_PROGRAMS = [
     # pingpong round trip (main.c + rtt_wrapper.c + rtt_data.c: a hand-filled collection whose
     # data handle is declared as `struct parsec_data_s *`); success = clean exit
     ("tests/apps/pingpong/rtt.jdf", ["tests/apps/pingpong/" + x for x in ("rtt_data.c", "rtt_wrapper.c", "main.c")], [], lambda out: True),
+    # pingpong bandwidth (own main; reads the context's VPs): one rank, prints its rate
+    ("tests/apps/pingpong/bandwidth.jdf", [], [], lambda out: "GB/s" in out),
     ("tests/apps/merge_sort/merge_sort.jdf", ["tests/apps/merge_sort/main.c", "tests/apps/merge_sort/merge_sort_wrapper.c", "tests/apps/merge_sort/sort_data.c"],
      ["100"], lambda out: len(out.split()) == 500 and all(a >= b for a, b in zip(list(map(int, out.split())), list(map(int, out.split()))[1:]))),
 ]
@@ -587,3 +586,23 @@ def test_reference_stencil_1d_program(tmp_path):
                        env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "Stencil\tN= 64" in r.stdout and "Iteration= 20" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+def test_reference_utt_program(tmp_path):
+    """The reference's tests/dsl/ptg/user-defined-functions/utt.jdf (its own
+    main, unmodified): %option termdet = "user-triggered", a fan-out / fan-in
+    tree whose END task ends the taskpool through
+    this_task->taskpool->tdm.module->taskpool_set_nb_tasks(tp, 0). All 14 tasks
+    of the tree (nt = 2 on one rank: STARTUP, 2 + 4 FANOUT, 2 + 4 FANIN, END)
+    run and the context terminates. The program's own final check expects 25
+    tasks, a count this DAG never has on one rank; the reference builds utt but
+    does not run it (user-defined-functions/Testings.cmake), so that check's
+    verdict (exit 1, "found 14 total") is asserted as is."""
+    d = os.path.join(REF, "tests/dsl/ptg/user-defined-functions")
+    exe = ptgpp.build_program(os.path.join(d, "utt.jdf"), str(tmp_path), cxxflags=ptgpp.C_BODIES + (f"-I{d}", f"-I{REF}/tests", f"-I{REF}"))
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    lines = r.stdout.splitlines()
+    assert sum(l.startswith(("STARTUP(", "FANOUT(", "FANIN(", "END(")) for l in lines) == 14, r.stdout[-2000:]
+    assert "END(0) on rank 0" in lines
+    assert r.returncode == 1 and "found 14 total" in r.stderr, r.stderr[-2000:]
