@@ -279,8 +279,15 @@ def build_sanitized(kind, jobs=None):
     need += [os.path.join(BUILD, "gen", os.path.splitext(os.path.basename(s))[0] + ".cpp") for s in _exists(JDF_SOURCES)]
     if not all(os.path.exists(p) for p in need):
         build(jobs)
-    out = generate_sanitized(kind)
-    r = subprocess.run(["ninja", "-C", out, f"-j{jobs or min(8, os.cpu_count() or 4)}"])
+    # one builder at a time per tree: parallel test workers (pytest -n) that
+    # ran ninja in the same directory together corrupted its log and linked a
+    # half-written library
+    import fcntl
+    os.makedirs(sanitize_dir(kind), exist_ok=True)
+    with open(os.path.join(sanitize_dir(kind), ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        out = generate_sanitized(kind)
+        r = subprocess.run(["ninja", "-C", out, f"-j{jobs or min(8, os.cpu_count() or 4)}"])
     if r.returncode != 0:
         raise RuntimeError(f"sanitized ({kind}) build failed")
     return out
