@@ -114,6 +114,9 @@ struct CBlockCyclic : BlockCyclic {
     if (synced.load(std::memory_order_relaxed)) return;
     if (!mat && c->mat) allocate_storage(c->mat);
     if (mat) synced.store(true, std::memory_order_release);
+    // no storage at all (reference tests_data.c create_and_distribute_empty_data:
+    // tiles that only carry dependencies): a tile table of storage-less tiles
+    else if (tiles.empty()) tiles.assign((size_t)nb_local_tiles, nullptr);
   }
   Data* data_of(const int64_t* idx, int n) override { sync(); return BlockCyclic::data_of(idx, n); }
   Data* data_of_key(uint64_t key) override { sync(); return BlockCyclic::data_of_key(key); }
@@ -417,6 +420,7 @@ int parsec_type_free(parsec_datatype_t* type) {
 }
 
 // -------------------------------------------------------------- context
+extern int parsec_dtd_window_size, parsec_dtd_threshold_size;
 parsec_context_t* parsec_init(int nb_cores, int* pargc, char** pargv[]) {
   std::vector<std::string> args;
   if (pargc && pargv && *pargv)
@@ -433,6 +437,11 @@ parsec_context_t* parsec_init(int nb_cores, int* pargc, char** pargv[]) {
     comm_init(atoi(r), atoi(s), j, g ? atoi(g) : -1);
   }
   Context* ctx = context_init(nb_cores, args);
+  {
+    auto& reg = ParamRegistry::instance();
+    parsec_dtd_window_size = (int)reg.reg_int("dtd", "", "window_size", "Tasks in flight before the inserting thread starts executing", 8000);
+    parsec_dtd_threshold_size = (int)reg.reg_int("dtd", "", "threshold_size", "Tasks in flight at which the inserting thread resumes inserting", 4000);
+  }
   if (pargc && pargv && *pargv) {  // hand back the arguments the runtime did not consume
     int n = 1;
     for (auto& a : args)
@@ -901,6 +910,9 @@ void parsec_hash_datadist_set_data(parsec_hash_datadist_t* d, void* actual_data,
 }
 
 void parsec_tiled_matrix_destroy(parsec_tiled_matrix_t* tdesc) { parsec_data_collection_destroy(&tdesc->super); }
+// the reference releases the matrix's data handles here, before the collection;
+// this runtime's collection owns them and parsec_data_collection_destroy frees both
+void parsec_tiled_matrix_destroy_data(parsec_tiled_matrix_t* tdesc) { (void)tdesc; }
 parsec_data_key_t parsec_tiled_matrix_data_key(parsec_tiled_matrix_t* tdesc, int m, int n) {
   int64_t idx[2] = {m, n};
   return impl_of(&tdesc->super)->data_key(idx, 2);
@@ -1075,6 +1087,42 @@ parsec_arena_datatype_t* parsec_arena_datatype_new(size_t elem_size, size_t alig
   return a;
 }
 void parsec_arena_datatype_free(parsec_arena_datatype_t* adt) { delete adt; }
+// Context-wide DTD arena datatypes (reference insert_function.c
+// parsec_dtd_create_arena_datatype): the id is what programs OR into an
+// argument's flags (the REGION bits). This runtime moves whole tiles, so the id
+// only names the datatype for parsec_dtd_get_arena_datatype.
+static std::mutex g_dtd_adt_m;
+static std::map<int, std::unique_ptr<ArenaDatatype>> g_dtd_adts;
+parsec_arena_datatype_t* parsec_dtd_create_arena_datatype(parsec_context_t* ctx, int* id) {
+  (void)ctx;
+  std::lock_guard<std::mutex> g(g_dtd_adt_m);
+  int i = 1;
+  while (g_dtd_adts.count(i)) ++i;
+  if (i > 0xffff) return nullptr;
+  auto& slot = g_dtd_adts[i];
+  slot = std::make_unique<ArenaDatatype>();
+  if (id) *id = i;
+  return slot.get();
+}
+parsec_arena_datatype_t* parsec_dtd_get_arena_datatype(parsec_context_t* ctx, int id) {
+  (void)ctx;
+  std::lock_guard<std::mutex> g(g_dtd_adt_m);
+  auto it = g_dtd_adts.find(id);
+  return it == g_dtd_adts.end() ? nullptr : it->second.get();
+}
+int parsec_dtd_destroy_arena_datatype(parsec_context_t* ctx, int id) {
+  (void)ctx;
+  std::lock_guard<std::mutex> g(g_dtd_adt_m);
+  return g_dtd_adts.erase(id) ? PARSEC_SUCCESS : PARSEC_ERR_NOT_FOUND;
+}
+void parsec_output(int output_id, const char* fmt, ...) {
+  (void)output_id;
+  va_list ap;
+  va_start(ap, fmt);
+  std::vfprintf(stdout, fmt, ap);
+  va_end(ap);
+  std::fflush(stdout);
+}
 int parsec_add2arena_rect(parsec_arena_datatype_t* adt, parsec_datatype_t oldtype, int tile_mb, int tile_nb, int resized) {
   (void)resized;
   add2arena_rect(*adt, type_of(oldtype).elem_size, tile_mb, tile_nb, tile_mb);
@@ -1101,8 +1149,15 @@ int parsec_taskpool_set_arena_datatype(parsec_taskpool_t* tp, int idx, size_t el
 }
 
 // ------------------------------------------------------------------ DTD
+// the DTD sliding window as the reference's globals: a program may change them
+// while its taskpools run (tests/dsl/dtd/dtd_test_task_insertion.c); set from
+// the dtd_window_size / dtd_threshold_size MCA parameters by parsec_init
+int parsec_dtd_window_size = 8000;
+int parsec_dtd_threshold_size = 4000;
 parsec_taskpool_t* parsec_dtd_taskpool_new(void) {
   auto* tp = new dtd::DtdTaskpool();
+  tp->window_src = &parsec_dtd_window_size;
+  tp->threshold_src = &parsec_dtd_threshold_size;
   {
     std::lock_guard<std::mutex> g(g_live_dtd_m);
     g_live_dtd.push_back(tp);
@@ -1239,10 +1294,15 @@ parsec_dtd_tile_t* parsec_dtd_tile_new(parsec_taskpool_t* tp, int rank, size_t s
   return reinterpret_cast<parsec_dtd_tile_t*>(as_dtd(tp)->tile_new(size, rank));
 }
 // the collection's id names its tiles in remote DTD messages: ids follow the
-// order of registration, identical on every rank (reference insert_function.c:1255)
+// order of registration, identical on every rank (reference insert_function.c:1255).
+// The C-visible dc_id is the DTD registration number (0, 1, 2, ... as the
+// reference's dtd_test_global_id_for_dc_assumed.c expects); the runtime's
+// own id, registered here too, is what the messages carry.
+static std::atomic<uint64_t> g_dtd_dc_seq{0};
 void parsec_dtd_data_collection_init(parsec_data_collection_t* dc) {
   if (!dc) return;
-  dc->dc_id = dc_register_id(impl_of(dc));
+  (void)dc_register_id(impl_of(dc));
+  dc->dc_id = g_dtd_dc_seq.fetch_add(1);
 }
 void parsec_dtd_data_collection_fini(parsec_data_collection_t* dc) { (void)dc; }
 parsec_data_t* parsec_dtd_tile_data(parsec_dtd_tile_t* tile) { return tile ? reinterpret_cast<dtd::Tile*>(tile)->data : nullptr; }

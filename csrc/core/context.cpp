@@ -228,6 +228,7 @@ Context* context_init(int nb_cores, std::vector<std::string>& args) {
   ctx->nb_vp = (int)vps.size();
   for (int v = 0; v < ctx->nb_vp; ++v) {
     auto* vp = new VirtualProcess();
+    vp->parsec_context = ctx;
     vp->vp_id = v;
     for (int tid : vps[v]) {
       auto* es = new ExecutionStream();

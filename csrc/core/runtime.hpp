@@ -493,6 +493,7 @@ struct alignas(64) ExecutionStream {  // one thread writes it per task: keep it 
 struct VirtualProcess {
   int vp_id = 0;
   int nb_cores = 0;  // compute streams of this VP (reference field name)
+  Context* parsec_context = nullptr;  // owning context (reference field name)
   std::vector<ExecutionStream*> es;
   void* sched_obj = nullptr;
 };

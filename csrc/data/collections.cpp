@@ -77,12 +77,12 @@ void* TiledMatrix::tile_ptr(int64_t tm, int64_t tn) {
 
 Data* TiledMatrix::tile_data(int64_t tm, int64_t tn) {
   int64_t li = local_index(tm, tn);
-  if (li < 0) return nullptr;
+  if (li < 0 || (size_t)li >= tiles.size()) return nullptr;  // no tile table: the storage was never set up
   Data* d = __atomic_load_n(&tiles[li], __ATOMIC_ACQUIRE);
   if (d) return d;
   int64_t idx[2] = {tm, tn};
   uint64_t key = data_key(idx, 2);
-  void* p = static_cast<char*>(mat) + (size_t)li * (size_t)bsiz * elem_size;
+  void* p = mat ? static_cast<char*>(mat) + (size_t)li * (size_t)bsiz * elem_size : nullptr;  // storage-less tile
   d = data_create(&tiles[li], this, key, p, (size_t)bsiz * elem_size, DATA_FLAG_PARSEC_MANAGED, storage_device);
   d->copy(storage_device)->dtt = default_dtt;
   return d;

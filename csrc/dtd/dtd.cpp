@@ -467,7 +467,8 @@ DtdTask* DtdTaskpool::insert_task(DtdTaskClass* tc, int priority, const std::vec
     ctx->scheduler->schedule(es, &tt, 1, 0);
   }
   // sliding window
-  if (!t->remote && nb_tasks.load(std::memory_order_relaxed) > window) execute_and_come_back(threshold);
+  const int64_t win = window_src ? (int64_t)*window_src : window;
+  if (!t->remote && nb_tasks.load(std::memory_order_relaxed) > win) execute_and_come_back(threshold_src ? (int64_t)*threshold_src : threshold);
   if (t->remote) {
     // a remote shadow never completes here: drop the insertion reference; the
     // shadow lives on through remote_tasks and the edges that reference it

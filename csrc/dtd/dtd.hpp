@@ -111,6 +111,8 @@ class DtdTaskpool : public Taskpool {
   ShardedMap<RemoteActivation*> early{6}; // activations that arrived before the insert
   std::atomic<uint64_t> seq{0};
   int64_t window = 8000, threshold = 4000;
+  const int* window_src = nullptr;     // C API: the program's parsec_dtd_window_size / threshold_size
+  const int* threshold_src = nullptr;
   std::atomic<bool> hold{false};
   std::vector<Tile*> new_tiles;
   std::mutex new_tiles_m;

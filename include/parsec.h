@@ -18,6 +18,7 @@
 #define PARSEC_AMD_PARSEC_H
 
 #include <assert.h>
+#include <inttypes.h>
 #include <stdarg.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -38,6 +39,16 @@
 #define PARSEC_HOOK_RETURN_DISABLE (-3)
 #define PARSEC_HOOK_RETURN_ASYNC (-4)
 #define PARSEC_HOOK_RETURN_ERROR (-5)
+
+#ifndef BEGIN_C_DECLS /* reference parsec_config.h */
+#ifdef __cplusplus
+#define BEGIN_C_DECLS extern "C" {
+#define END_C_DECLS }
+#else
+#define BEGIN_C_DECLS
+#define END_C_DECLS
+#endif
+#endif
 
 #define PARSEC_SUCCESS 0
 #define PARSEC_ERROR (-1)
@@ -458,6 +469,13 @@ void parsec_arena_datatype_free(parsec_arena_datatype_t* adt);
 int parsec_add2arena_rect(parsec_arena_datatype_t* adt, parsec_datatype_t oldtype, int tile_mb, int tile_nb, int resized);
 int parsec_add2arena(parsec_arena_datatype_t* adt, parsec_datatype_t oldtype, parsec_matrix_uplo_t uplo, int diag, int m, int n, int ld, size_t alignment, int resized);
 void parsec_del2arena(parsec_arena_datatype_t* adt);
+/* context-wide DTD arena datatypes; the id goes into an argument's flags
+ * (reference insert_function.h parsec_dtd_create_arena_datatype) */
+parsec_arena_datatype_t* parsec_dtd_create_arena_datatype(parsec_context_t* ctx, int* id);
+parsec_arena_datatype_t* parsec_dtd_get_arena_datatype(parsec_context_t* ctx, int id);
+int parsec_dtd_destroy_arena_datatype(parsec_context_t* ctx, int id);
+/* printf-style line on an output stream (reference utils/output.h; one stream: stdout) */
+void parsec_output(int output_id, const char* fmt, ...);
 /* Set arena slot `idx` of a taskpool (generated PARSEC_<name>_<TYPE>_ADT_IDX). */
 int parsec_taskpool_set_arena_datatype(parsec_taskpool_t* tp, int idx, size_t elem_size, size_t alignment, parsec_datatype_t opaque_dtt);
 
@@ -488,6 +506,12 @@ typedef int(parsec_dtd_funcptr_t)(parsec_execution_stream_t* es, parsec_task_t* 
 typedef int(parsec_dtd_gpu_funcptr_t)(void* stream, parsec_task_t* this_task);
 
 parsec_taskpool_t* parsec_dtd_taskpool_new(void);
+/* sliding window of DTD insertion (reference insert_function.h): above
+ * window_size tasks in flight the inserting thread executes tasks until
+ * threshold_size remain; read on every insertion */
+extern int parsec_dtd_window_size;
+extern int parsec_dtd_threshold_size;
+void parsec_tiled_matrix_destroy_data(parsec_tiled_matrix_t* tdesc);
 int parsec_dtd_taskpool_wait(parsec_taskpool_t* tp);
 void parsec_dtd_insert_task(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, int priority, int device_type, const char* name_of_kernel, ...);
 parsec_dtd_task_class_t* parsec_dtd_create_task_class(parsec_taskpool_t* tp, const char* name, ...);

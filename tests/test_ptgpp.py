@@ -606,3 +606,29 @@ def test_reference_utt_program(tmp_path):
     assert sum(l.startswith(("STARTUP(", "FANOUT(", "FANIN(", "END(")) for l in lines) == 14, r.stdout[-2000:]
     assert "END(0) on rank 0" in lines
     assert r.returncode == 1 and "found 14 total" in r.stderr, r.stderr[-2000:]
+
+
+REF_DTD_PROGRAMS = ["allreduce", "broadcast", "data_flush", "flag_dont_track", "global_id_for_dc_assumed", "hierarchy", "insert_task_interface",
+                    "multiple_handle_wait", "null_as_tile", "reduce", "task_generation", "task_inserting_task", "task_insertion",
+                    "template_counter", "untie", "war"]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("name", REF_DTD_PROGRAMS)
+def test_reference_dtd_programs_unmodified(tmp_path, name):
+    """The reference's DTD test programs (tests/dsl/dtd/dtd_test_<name>.c with
+    tests/tests_data.c, unmodified) compiled as C++ against this runtime's
+    headers and run on one process; each checks itself (parsec_fatal / assert
+    on a wrong result, non-zero exit). Not here: the two-process ones
+    (pingpong, task_placement, interleave_actions), the CUDA / MPI-only ones,
+    and those that reach the reference's internal task classes or
+    __parsec_complete_execution (new_tile, tp_enqueue_dequeue,
+    explicit_task_creation)."""
+    cc, libs = ptgpp.compile_flags(False)
+    exe = str(tmp_path / name)
+    src = os.path.join(REF, "tests/dsl/dtd", f"dtd_test_{name}.c")
+    r = subprocess.run(cc + list(ptgpp.C_BODIES) + [f"-I{REF}/tests", f"-I{REF}", f"-I{REF}/tests/dsl/dtd", "-x", "c++", src, os.path.join(REF, "tests/tests_data.c"),
+                                                    "-o", exe] + libs, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
