@@ -632,3 +632,20 @@ def test_reference_dtd_programs_unmodified(tmp_path, name):
     assert r.returncode == 0, r.stderr[-3000:]
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("src,expect", [("examples/Ex00_StartStop.c", None),
+                                        ("examples/interfaces/dtd/dtd_example_hello_world.c", "Hello World my rank is: 0")])
+def test_reference_c_examples(tmp_path, src, expect):
+    """The reference's C examples without a JDF (Ex00 start / stop of a context,
+    the DTD hello world), unmodified."""
+    cc, libs = ptgpp.compile_flags(False)
+    exe = str(tmp_path / "ex")
+    r = subprocess.run(cc + list(ptgpp.C_BODIES) + [f"-I{REF}/tests", f"-I{REF}", "-x", "c++", os.path.join(REF, src), "-o", exe] + libs,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    if expect:
+        assert expect in r.stdout, r.stdout[-2000:]
