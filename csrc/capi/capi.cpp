@@ -10,6 +10,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <atomic>
 #include <thread>
 
@@ -1210,6 +1211,46 @@ static void dtd_insert(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, in
   }
   t_last_dtd = d;
   d->insert_task(tc, priority, pa.args);
+}
+
+// Explicit task creation (reference insert_function.h parsec_dtd_create_task /
+// parsec_insert_dtd_task): the task is described now and inserted later. The
+// handle carries the parsed arguments; insertion is exactly
+// parsec_dtd_insert_task's (dependencies are discovered at insertion, in
+// insertion order, which is what the reference's creation order gives too).
+struct DeferredDtdTask : Task {
+  parsec_taskpool_t* dtp = nullptr;
+  parsec_dtd_funcptr_t* fpointer = nullptr;
+  int priority = 0, device_type = 0;
+  std::string name;
+  PendingArgs pa;
+};
+static std::mutex g_deferred_m;
+static std::set<Task*> g_deferred;
+parsec_task_t* parsec_dtd_create_task(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, int priority, int device_type, const char* name, ...) {
+  auto* t = new DeferredDtdTask();
+  t->dtp = tp;
+  t->taskpool = tp;
+  t->fpointer = fpointer;
+  t->priority = priority;
+  t->device_type = device_type;
+  t->name = name ? name : "dtd_task";
+  va_list ap;
+  va_start(ap, name);
+  parse_args(ap, t->pa);
+  va_end(ap);
+  std::lock_guard<std::mutex> g(g_deferred_m);
+  g_deferred.insert(t);
+  return t;
+}
+void parsec_insert_dtd_task(parsec_task_t* this_task) {
+  {
+    std::lock_guard<std::mutex> g(g_deferred_m);
+    if (!g_deferred.erase(this_task)) fatal("parsec_insert_dtd_task: %p was not made by parsec_dtd_create_task (or was inserted already)", (void*)this_task);
+  }
+  auto* t = static_cast<DeferredDtdTask*>(this_task);
+  dtd_insert(t->dtp, t->fpointer, t->priority, t->device_type, t->name.c_str(), t->pa);
+  delete t;
 }
 
 void parsec_dtd_insert_task(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, int priority, int device_type, const char* name, ...) {

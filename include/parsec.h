@@ -515,6 +515,10 @@ void parsec_tiled_matrix_destroy_data(parsec_tiled_matrix_t* tdesc);
 int parsec_dtd_taskpool_wait(parsec_taskpool_t* tp);
 void parsec_dtd_insert_task(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, int priority, int device_type, const char* name_of_kernel, ...);
 parsec_dtd_task_class_t* parsec_dtd_create_task_class(parsec_taskpool_t* tp, const char* name, ...);
+/* explicit task creation: described now (same arguments as
+ * parsec_dtd_insert_task), inserted by parsec_insert_dtd_task */
+parsec_task_t* parsec_dtd_create_task(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, int priority, int device_type, const char* name, ...);
+void parsec_insert_dtd_task(parsec_task_t* this_task);
 int parsec_dtd_task_class_add_chore(parsec_taskpool_t* tp, parsec_dtd_task_class_t* tc, int device_type, void* function);
 void parsec_dtd_insert_task_with_task_class(parsec_taskpool_t* tp, parsec_dtd_task_class_t* tc, int priority, int device_type, ...);
 parsec_dtd_tile_t* parsec_dtd_tile_of(parsec_data_collection_t* dc, parsec_data_key_t key);

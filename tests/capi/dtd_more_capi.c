@@ -252,6 +252,47 @@ static int run_interface(parsec_context_t* ctx, int rank, int world) {
   return 0;
 }
 
+/* explicit task creation (reference dtd_test_explicit_task_creation.c, without
+ * its MPI datatype): tasks are created first, then inserted, each one
+ * incrementing the shared tile; ranks > 0 own nothing and run nothing */
+static int bump(parsec_execution_stream_t* es, parsec_task_t* t) {
+  (void)es;
+  int* a;
+  int expect;
+  parsec_dtd_unpack_args(t, &a, &expect);
+  if (*a != expect) BAD("explicit: tile %d before task %d\n", *a, expect);
+  *a += 1;
+  __atomic_add_fetch(&g_count, 1, __ATOMIC_RELAXED);
+  return PARSEC_HOOK_RETURN_DONE;
+}
+static int run_explicit(parsec_context_t* ctx, int rank, int world) {
+  enum { N = 50 };
+  parsec_matrix_block_cyclic_t A;
+  make_vector(&A, rank, world, 0);
+  parsec_dtd_data_collection_init(&A.super.super);
+  parsec_taskpool_t* tp = parsec_dtd_taskpool_new();
+  parsec_context_add_taskpool(ctx, tp);
+  parsec_context_start(ctx);
+  static int order[N];
+  parsec_task_t* tasks[N];
+  for (int i = 0; i < N; ++i) {
+    order[i] = i;
+    tasks[i] = parsec_dtd_create_task(tp, bump, 0, PARSEC_DEV_CPU, "Bump", PASSED_BY_REF, PARSEC_DTD_TILE_OF(&A, 0, 0), PARSEC_INOUT | PARSEC_AFFINITY,
+                                      (int)sizeof(int), &order[i], PARSEC_VALUE, PARSEC_DTD_ARG_END);
+  }
+  if (g_count != 0) BAD("explicit rank %d: %d tasks ran before insertion\n", rank, g_count);
+  for (int i = 0; i < N; ++i) parsec_insert_dtd_task(tasks[i]);
+  parsec_dtd_data_flush_all(tp, &A.super.super);
+  parsec_dtd_taskpool_wait(tp);
+  parsec_context_wait(ctx);
+  parsec_taskpool_free(tp);
+  parsec_dtd_data_collection_fini(&A.super.super);
+  free_vector(&A);
+  if (rank == 0 && g_count != N) BAD("explicit: %d tasks ran, expected %d\n", g_count, N);
+  printf("explicit rank %d ran %d\n", rank, g_count);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const char* mode = argc > 1 ? argv[1] : "interleave";
   const char* opt = argc > 2 ? argv[2] : "";
@@ -262,6 +303,7 @@ int main(int argc, char** argv) {
   else if (!strcmp(mode, "template_counter")) run_template_counter(ctx, rank, world);
   else if (!strcmp(mode, "global_id")) run_global_id(rank, world);
   else if (!strcmp(mode, "interface")) run_interface(ctx, rank, world);
+  else if (!strcmp(mode, "explicit")) run_explicit(ctx, rank, world);
   else BAD("unknown mode %s\n", mode);
   parsec_fini(&ctx);
   printf("dtd_more %s rank %d %s\n", mode, rank, g_bad ? "FAILED" : "ok");

@@ -209,10 +209,11 @@ def dtd_more(tmp_path_factory, pa):
     (["hierarchy"], 1), (["hierarchy"], 3),
     (["template_counter"], 1), (["template_counter"], 4),
     (["global_id"], 3),
+    (["explicit"], 1), (["explicit"], 2),
     (["interleave", ""], 2), (["interleave", "a"], 3), (["interleave", "if"], 4), (["interleave", "afiw"], 2),
 ])
 def test_dtd_reference_programs(dtd_more, args, nranks):
-    """dtd_test_insert_task_interface / hierarchy (a task that runs its own DTD
+    """dtd_test_insert_task_interface / explicit_task_creation / hierarchy (a task that runs its own DTD
     taskpool) / template_counter / global_id_for_dc_assumed / interleave_actions
     (ranks > 0 lag before add / insert / flush / wait), reference tests/dsl/dtd."""
     rc, outs = launch.launch(nranks, [dtd_more, *args], timeout=90, capture=True, env={"PARSEC_MCA_device_hip_enabled": "0"})
