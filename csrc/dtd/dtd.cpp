@@ -459,8 +459,12 @@ DtdTask* DtdTaskpool::insert_task(DtdTaskClass* tc, int priority, const std::vec
       delete act;
     }
   }
-  // drop the insertion guard
-  if (t->deps.fetch_sub(1) == 1 && !t->remote) {
+  // drop the insertion guard; a local task may run and be freed by a worker as
+  // soon as the guard is gone, so nothing below reads it (the remote flag is
+  // taken first: reading it after the schedule was a use-after-free found by
+  // the ASan build on the reference's dtd_test_multiple_handle_wait)
+  const bool remote = t->remote;
+  if (t->deps.fetch_sub(1) == 1 && !remote) {
     ExecutionStream* es = my_execution_stream();
     if (!es || es->ctx != ctx) es = ctx->all_es[0];
     Task* tt = t;
@@ -468,8 +472,8 @@ DtdTask* DtdTaskpool::insert_task(DtdTaskClass* tc, int priority, const std::vec
   }
   // sliding window
   const int64_t win = window_src ? (int64_t)*window_src : window;
-  if (!t->remote && nb_tasks.load(std::memory_order_relaxed) > win) execute_and_come_back(threshold_src ? (int64_t)*threshold_src : threshold);
-  if (t->remote) {
+  if (!remote && nb_tasks.load(std::memory_order_relaxed) > win) execute_and_come_back(threshold_src ? (int64_t)*threshold_src : threshold);
+  if (remote) {
     // a remote shadow never completes here: drop the insertion reference; the
     // shadow lives on through remote_tasks and the edges that reference it
     // (leak found by the ASan build)

@@ -20,13 +20,21 @@ namespace parsec {
 
 // ================================================================ hbbuffer
 // Bounded buffer of CAS'd slots; overflow is pushed to a parent callback.
+// Each slot's task priority is kept beside it: a scan must not read a task
+// through a slot pointer, since another thread may have popped, run and freed
+// that task in the meantime (use-after-free found by the ASan build); the CAS
+// on the pointer is what decides ownership, the priority only steers the pick.
 class HBBuffer {
  public:
   using Parent = std::function<void(Task**, int, int32_t)>;
-  HBBuffer(int size, Parent parent) : size_(std::max(size, 1)), slots_(new std::atomic<Task*>[size_]), parent_(std::move(parent)) {
-    for (int i = 0; i < size_; ++i) slots_[i].store(nullptr, std::memory_order_relaxed);
+  HBBuffer(int size, Parent parent)
+      : size_(std::max(size, 1)), slots_(new std::atomic<Task*>[size_]), prio_(new std::atomic<int32_t>[size_]), parent_(std::move(parent)) {
+    for (int i = 0; i < size_; ++i) {
+      slots_[i].store(nullptr, std::memory_order_relaxed);
+      prio_[i].store(INT32_MIN, std::memory_order_relaxed);
+    }
   }
-  ~HBBuffer() { delete[] slots_; }
+  ~HBBuffer() { delete[] slots_; delete[] prio_; }
   // Push each task into a free slot; spill the rest (already priority sorted) to the parent.
   void push_all(Task** tasks, int n, int32_t distance) {
     std::vector<Task*> spill;
@@ -35,7 +43,9 @@ class HBBuffer {
       bool placed = false;
       for (int j = start; j < size_; ++j) {
         Task* exp = nullptr;
+        const int32_t pr = tasks[i]->priority;  // read while the task is still ours
         if (slots_[j].load(std::memory_order_relaxed) == nullptr && slots_[j].compare_exchange_strong(exp, tasks[i], std::memory_order_release)) {
+          prio_[j].store(pr, std::memory_order_relaxed);
           placed = true;
           start = j + 1;
           break;
@@ -52,6 +62,7 @@ class HBBuffer {
     std::vector<Task*> spill;
     for (int i = 0; i < n; ++i) {
       Task* t = tasks[i];
+      const int32_t tp = t->priority;
       bool placed = false;
       for (int attempt = 0; attempt < 4 && !placed; ++attempt) {
         int lowest = -1;
@@ -60,15 +71,22 @@ class HBBuffer {
           Task* cur = slots_[j].load(std::memory_order_relaxed);
           if (cur == nullptr) {
             Task* exp = nullptr;
-            if (slots_[j].compare_exchange_strong(exp, t, std::memory_order_release)) { placed = true; break; }
+            if (slots_[j].compare_exchange_strong(exp, t, std::memory_order_release)) {
+              prio_[j].store(tp, std::memory_order_relaxed);
+              placed = true;
+              break;
+            }
             continue;
           }
-          if (cur->priority < lowest_prio) { lowest_prio = cur->priority; lowest = j; }
+          const int32_t cp = prio_[j].load(std::memory_order_relaxed);
+          if (cp < lowest_prio) { lowest_prio = cp; lowest = j; }
         }
         if (placed) break;
-        if (lowest < 0 || lowest_prio >= t->priority) break;
+        if (lowest < 0 || lowest_prio >= tp) break;
         Task* victim = slots_[lowest].load(std::memory_order_relaxed);
-        if (victim && victim->priority < t->priority && slots_[lowest].compare_exchange_strong(victim, t, std::memory_order_acq_rel)) {
+        // the ejected task is ours once the CAS succeeds; until then only its slot's priority is read
+        if (victim && prio_[lowest].load(std::memory_order_relaxed) < tp && slots_[lowest].compare_exchange_strong(victim, t, std::memory_order_acq_rel)) {
+          prio_[lowest].store(tp, std::memory_order_relaxed);
           placed = true;
           spill.push_back(victim);  // ejected to parent
         }
@@ -85,9 +103,12 @@ class HBBuffer {
     for (int attempt = 0; attempt < 8; ++attempt) {
       int best = -1;
       Task* bt = nullptr;
+      int32_t bp = INT32_MIN;
       for (int j = 0; j < size_; ++j) {
         Task* cur = slots_[j].load(std::memory_order_acquire);
-        if (cur && (!bt || cur->priority > bt->priority)) { bt = cur; best = j; }
+        if (!cur) continue;
+        const int32_t cp = prio_[j].load(std::memory_order_relaxed);
+        if (!bt || cp > bp) { bt = cur; bp = cp; best = j; }
       }
       if (!bt) return nullptr;
       if (slots_[best].compare_exchange_strong(bt, nullptr, std::memory_order_acq_rel)) {
@@ -102,6 +123,7 @@ class HBBuffer {
  private:
   int size_;
   std::atomic<Task*>* slots_;
+  std::atomic<int32_t>* prio_;
   Parent parent_;
   std::atomic<int> count_hint_{0};
 };
