@@ -295,6 +295,9 @@ def main():
                        "parallelism": f"2D block-cyclic P{P}xQ{Q}, 1 process/GPU", "threads_per_rank": args.cores},
         }
         out["device_plane"] = planes
+        est = pa.trsm_estimate_stats(False)
+        out["panel_solve"] = {"mode": {0: "inverse", 1: "auto", 2: "blocked"}.get(pa.trsm_inverse_mode(), "?"),
+                              "estimates_published": est[0], "decided_on_host": est[1], "device_gate": est[2]}
         if check is not None:
             out["max_rel_error_vs_torch_cholesky"] = check
         if args.share_gpu:

@@ -23,6 +23,7 @@
 
 #include "../device/device.hpp"
 #include "../prof/profiling.hpp"
+#include "fetch_queue.hpp"
 #include "shm_engine.hpp"
 
 namespace parsec {
@@ -33,6 +34,8 @@ static ExecutionStream* g_comm_es = nullptr;
 static size_t g_short_limit = 1024;
 static bool g_recv_from_cache = true;
 static int g_recv_pool = 1;  // 0 free after use, 1 recycle by size, 2 never reuse (diagnostic)
+// payload gets of incoming activations, highest priority first, comm_gets_max in flight
+static FetchQueue g_fetch;
 
 CommEngine* comm_engine() { return g_ce; }
 int comm_rank() { return g_ce ? g_ce->rank : 0; }
@@ -337,6 +340,7 @@ void on_activate(int src, int, const void* msg, size_t len) {
 // One flow of receive `rid` landed (comm thread): tell the sender, deliver
 // when it was the last one.
 void flow_landed(uint64_t rid, int f) {
+  g_fetch.done();  // the next queued get (by priority) may start
   comm_trace(k_rcv_e, flow_event(rid, f), 0, nullptr);
   RecvState* rs = nullptr;
   {
@@ -383,7 +387,8 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
       off += sizeof(MemReg);
       // device payloads land in device memory when the plane moves them GPU to GPU
       DataCopy* c = new_recv_copy(d.bytes, d.kind == FK_DEVICE && g_ce->device_direct());
-      if (g_ce->mem_register(c->device_private, d.bytes, c->device_index, 0, 0, &r->lreg[f]) != 0) fatal("remote dependency: cannot register a receive buffer");
+      // the local end of a get: no peer ever reads it, so no IPC export
+      if (g_ce->mem_register_local(c->device_private, d.bytes, c->device_index, &r->lreg[f]) != 0) fatal("remote dependency: cannot register a receive buffer");
       r->data[f] = c;
       get_mask |= 1u << f;
       ++r->remaining;
@@ -399,8 +404,9 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
     std::lock_guard<std::mutex> g(g_m);
     g_recvs[r->id] = r;
   }
-  // fetch every payload; the last landing delivers r, so everything the gets
-  // need is copied out of r before the first one is issued
+  // queue every payload's get by the activation's priority (FetchQueue: at most
+  // comm_gets_max in flight); the last landing delivers r, so everything the
+  // gets need is copied out of r before the first one is queued
   struct Fetch {
     int f;
     uint64_t bytes;
@@ -412,17 +418,21 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
     if (get_mask & (1u << f)) todo.push_back(Fetch{f, r->fd[f].bytes, r->lreg[f], plane_of(r->data[f]->device_index)});
   const uint64_t rid = r->id, sid = r->hdr.send_id;
   const uint32_t tpid = r->hdr.tp_id;
+  const int32_t prio = r->hdr.priority;
   for (const Fetch& x : todo) {
     const int f = x.f;
     if (g_comm_prof) {
       CommInfo ci{src, f, (int64_t)x.bytes, x.plane, (int32_t)(sid & 0x7fffffff)};
       comm_trace(k_rcv_b, flow_event(rid, f), tpid, &ci);
     }
-    const PutEnd pe{sid, (uint32_t)f, 0};
-    PARSEC_DEBUG(kVerbDebug, "comm", "get flow %d (%llu bytes) from %d (recv %llu)", f, (unsigned long long)x.bytes, src, (unsigned long long)rid);
-    if (g_ce->get(x.lreg, 0, rreg[f], 0, x.bytes, src, [rid, f](const MemReg&, ptrdiff_t, const MemReg&, ptrdiff_t, size_t, int) { flow_landed(rid, f); },
-                  TAG_PUT_END, &pe, sizeof(pe)) != 0)
-      fatal("remote dependency: get of flow %d from rank %d failed", f, src);
+    const MemReg remote = rreg[f];
+    g_fetch.submit(prio, [x, remote, src, rid, sid, f] {
+      const PutEnd pe{sid, (uint32_t)f, 0};
+      PARSEC_DEBUG(kVerbDebug, "comm", "get flow %d (%llu bytes) from %d (recv %llu)", f, (unsigned long long)x.bytes, src, (unsigned long long)rid);
+      if (g_ce->get(x.lreg, 0, remote, 0, x.bytes, src, [rid, f](const MemReg&, ptrdiff_t, const MemReg&, ptrdiff_t, size_t, int) { flow_landed(rid, f); },
+                    TAG_PUT_END, &pe, sizeof(pe)) != 0)
+        fatal("remote dependency: get of flow %d from rank %d failed", f, src);
+    });
   }
 }
 
@@ -556,6 +566,12 @@ std::vector<std::pair<std::string, uint64_t>> comm_stats() {
   r.emplace_back("get_fragments", st.get_fragments.load());
   r.emplace_back("put_ipc", st.put_ipc.load());
   r.emplace_back("put_fragments", st.put_fragments.load());
+  r.emplace_back("bytes_pulled_ipc", st.bytes_ipc.load());
+  r.emplace_back("bytes_fragments", st.bytes_fragments.load());
+  const FetchQueue::Stats fq = g_fetch.stats();
+  r.emplace_back("gets_max", (uint64_t)std::max(0, g_fetch.max_inflight()));
+  r.emplace_back("gets_queued_max", fq.max_queued);
+  r.emplace_back("gets_submitted", fq.submitted);
   return r;
 }
 
@@ -571,6 +587,13 @@ void remote_dep_init(Context* ctx) {
   g_short_limit = ParamRegistry::instance().reg_sizet("runtime", "comm", "short_limit", "Eager payload limit (bytes) for host data in activations", 1024);
   g_recv_pool = (int)ParamRegistry::instance().reg_int("comm", "", "recv_pool", "Device receive buffers: 1 recycle by size, 0 free after use, 2 never reuse (diagnostic)", 1);
   g_recv_from_cache = ParamRegistry::instance().reg_int("comm", "", "recv_from_cache", "Carve device receive buffers from the GPU tile-cache zone (1) or hipMalloc them (0)", 1) != 0;
+  if (g_ce) {
+    // reference parsec_comm_gets_max (remote_dep_mpi.c:26): pulls on one copy
+    // stream run in order, so a small bound keeps a critical flow near the head
+    const int gm = (int)ParamRegistry::instance().reg_int("comm", "", "gets_max",
+        "Payload gets of incoming activations in flight at once, highest activation priority first; -1 = auto (2 per IPC pull stream, 4 on the host plane), 0 = unbounded", -1);
+    g_fetch.set_max_inflight(gm >= 0 ? gm : g_ce->device_direct() ? 2 * g_ce->pull_streams() : 4);
+  }
   ctx->my_rank = comm_rank();
   ctx->nb_nodes = comm_size();
   set_debug_rank(ctx->my_rank);

@@ -51,6 +51,7 @@ class ShmEngine : public CommEngine {
     std::atomic<uint64_t> direct{0}, backlogged{0}, aggregates{0}, aggregated_msgs{0};
     std::atomic<uint64_t> max_waiting{0};
     std::atomic<uint64_t> get_ipc{0}, get_fragments{0}, put_ipc{0}, put_fragments{0};  // one-sided transfers by route
+    std::atomic<uint64_t> bytes_ipc{0}, bytes_fragments{0};  // payload bytes of gets by route
   } stats;
   int progress() override;
   int sync() override;
@@ -64,6 +65,11 @@ class ShmEngine : public CommEngine {
   // memory with async copies (the comm thread never blocks on the GPU).
   int mem_register(void* mem, size_t bytes, int device, int64_t user_dtt, int user_count, MemReg* reg) override;
   int mem_unregister(MemReg* reg) override;
+  // a registration that is only ever the local end of this rank's own get / put:
+  // never exported through IPC (no peer maps it)
+  int mem_register_local(void* mem, size_t bytes, int device, MemReg* reg);
+  // distinct streams the IPC pulls are spread over (comm_ipc_streams)
+  int pull_streams() const { return 1 + (int)own_streams_.size(); }
   int mem_retrieve(const MemReg& reg, void** mem, size_t* bytes, int64_t* user_dtt, int* user_count) override;
   int get(const MemReg& lreg, ptrdiff_t ldispl, const MemReg& rreg, ptrdiff_t rdispl, size_t size, int remote, OneSidedCallback l_cb, int r_tag,
           const void* r_cb_data, size_t r_cb_size) override;

@@ -84,6 +84,23 @@ int ShmEngine::mem_register(void* mem, size_t bytes, int device, int64_t user_dt
   return 0;
 }
 
+int ShmEngine::mem_register_local(void* mem, size_t bytes, int device, MemReg* reg) {
+  if (!reg) return -1;
+  RegWire w{};
+  w.magic = kRegMagic;
+  w.owner = rank;
+  w.device = device;
+  w.bytes = bytes;
+  {
+    std::lock_guard<std::mutex> g(reg_m_);
+    w.id = next_region_++;
+    regions_[w.id] = Region{mem, bytes, device, 0, 0};
+  }
+  std::memset(reg->b, 0, sizeof(reg->b));
+  std::memcpy(reg->b, &w, sizeof(w));
+  return 0;
+}
+
 int ShmEngine::mem_unregister(MemReg* reg) {
   if (!reg) return -1;
   const RegWire w = wire_of(*reg);
@@ -264,6 +281,7 @@ int ShmEngine::get(const MemReg& lreg, ptrdiff_t ldispl, const MemReg& rreg, ptr
       char* base = static_cast<char*>(ipc_open(remote, rw.ipc));
       const char* from = base + rw.ipc_offset + rdispl;
       stats.get_ipc.fetch_add(1, std::memory_order_relaxed);
+      stats.bytes_ipc.fetch_add(size, std::memory_order_relaxed);
       if (ipc_copy(remote, dst, from, size, lw.device != 0, [=, this, cbd = std::move(cbd)] {
             if (l_cb) l_cb(lreg, ldispl, rreg, rdispl, size, remote);
             notify_remote(remote, r_tag, cbd);
@@ -272,6 +290,7 @@ int ShmEngine::get(const MemReg& lreg, ptrdiff_t ldispl, const MemReg& rreg, ptr
       return;
     }
     stats.get_fragments.fetch_add(1, std::memory_order_relaxed);
+    stats.bytes_fragments.fetch_add(size, std::memory_order_relaxed);
     char* staging = lw.device != 0 ? static_cast<char*>(pinned_get(size)) : nullptr;
     PendingGet pg{lreg, rreg, ldispl, rdispl, size, 0, dst, lw.device, staging, std::move(l_cb), r_tag, std::move(cbd)};
     const uint64_t id = next_get_++;

@@ -141,6 +141,13 @@ namespace kern {
 // device_hip_cu_yield as the kernels see it (QR sub-panel kernels claim their CUs when > 0)
 void set_cu_yield_mode(int m);
 int cu_yield_mode();
+// auto panel solve: 1 = the TRSM launch decides from the estimate the local
+// POTRF published to pinned host memory (default), 0 = always the device-side
+// gate; < 0 queries. Returns the previous setting.
+int trsm_estimate_route(int on);
+// [0] estimates published by tile POTRFs, [1] panel decisions taken on the
+// host, [2] panels left to the device-side gate
+void trsm_estimate_stats(uint64_t out[3], bool reset);
 }  // namespace kern
 
 // Householder QR of a tile (GEQRT: A2 == nullptr) or of a triangle on top of a

@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "../device/device.hpp"
@@ -612,11 +613,18 @@ static_assert(sizeof(TrsmInvArgs) <= 4096, "TrsmInvArgs exceeds the kernel argum
 // conflict-free MFMA operand reads). 8 waves: wave (g, h) computes columns
 // 16g..16g+15 of the block over half h of the reduction, with four independent
 // MFMA accumulator chains; the two halves are summed through LDS.
+// kGlobal: the row panel stays in B itself (solved in place, 8 KB of LDS for the
+// reduction only), so the launch fits on a CU beside a resident bulk GEMM
+// workgroup: the gated fallback of the auto panel solve, whose workgroups nearly
+// always return at once (the 139 KB LDS version waited for whole CUs at
+// nb = 1024: 6.3 ms per launch on the critical stream, profiles/r4_kernel_stats_final.txt).
+// Needs n % 64 == 0. Waves of a workgroup share the CU's L1, so the in-place
+// writes of one block are visible to the next block's reads after the barrier.
 constexpr int kTrsmThreads = 512;
-template <int BR>
+template <int BR, bool kGlobal>
 __global__ __launch_bounds__(kTrsmThreads) void dtrsm_inv_kernel(const TrsmInvArgs args) {
   static_assert(BR == 16, "MFMA operand layout assumes 16-row panels");
-  extern __shared__ double P[];  // [ncols_padded][BR], then red[16][64]
+  extern __shared__ double P[];  // [ncols_padded][BR], then red[16][64] (kGlobal: red only)
   PARSEC_WAVE_PRIO(args.prio);
   const int b = blockIdx.x;
   const int di = find_desc(args, args.block_start, b);
@@ -632,17 +640,33 @@ __global__ __launch_bounds__(kTrsmThreads) void dtrsm_inv_kernel(const TrsmInvAr
   const int r0 = (b - args.block_start[di]) * BR;
   const int n = d.n, m = d.m;
   const int nblk = (n + 63) / 64;
-  double* red = P + nblk * 64 * BR;
+  double* red = kGlobal ? P : P + nblk * 64 * BR;
+  double* Bp = d.B;
+  const size_t ldb = d.ldb;
+  // element (row rr of the panel, column c)
+  auto pget = [&](int c, int rr) -> double {
+    if (kGlobal) return r0 + rr < m ? Bp[(size_t)c * ldb + r0 + rr] : 0.0;
+    return P[c * BR + rr];
+  };
+  auto pset = [&](int c, int rr, double v) {
+    if (kGlobal) {
+      if (r0 + rr < m) Bp[(size_t)c * ldb + r0 + rr] = v;
+    } else {
+      P[c * BR + rr] = v;
+    }
+  };
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = wv & 3, h = wv >> 2;
   const int fr = lane & 15, fk = lane >> 4;
   const double* __restrict__ L = d.L;
   const size_t ldl = d.ldl;
-  for (int idx = tid; idx < nblk * 64 * BR; idx += kTrsmThreads) {
-    int c = idx / BR, rr = idx % BR;
-    P[idx] = (c < n && r0 + rr < m) ? d.B[(size_t)c * d.ldb + r0 + rr] : 0.0;
+  if (!kGlobal) {
+    for (int idx = tid; idx < nblk * 64 * BR; idx += kTrsmThreads) {
+      int c = idx / BR, rr = idx % BR;
+      P[idx] = (c < n && r0 + rr < m) ? Bp[(size_t)c * ldb + r0 + rr] : 0.0;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   for (int jb = 0; jb < nblk; ++jb) {
     const int c0 = jb * 64;
     const int cw = c0 + 16 * g + fr;  // L row this lane feeds as the MFMA A-operand
@@ -658,7 +682,7 @@ __global__ __launch_bounds__(kTrsmThreads) void dtrsm_inv_kernel(const TrsmInvAr
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         av[u] = valid ? Lp[(size_t)(k + 4 * u + fk) * ldl] : 0.0;
-        bv[u] = P[(k + 4 * u + fk) * BR + fr];
+        bv[u] = pget(k + 4 * u + fk, fr);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc[u], 0, 0, 0);
@@ -673,7 +697,7 @@ __global__ __launch_bounds__(kTrsmThreads) void dtrsm_inv_kernel(const TrsmInvAr
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int c = c0 + 16 * g + fk + 4 * q;
-        P[c * BR + fr] -= s[q] + red[(g * 4 + q) * 64 + lane];
+        pset(c, fr, pget(c, fr) - (s[q] + red[(g * 4 + q) * 64 + lane]));
       }
     }
     __syncthreads();
@@ -683,7 +707,7 @@ __global__ __launch_bounds__(kTrsmThreads) void dtrsm_inv_kernel(const TrsmInvAr
 #pragma unroll
     for (int kk = 32 * h; kk < 32 * h + 32; kk += 8) {
       const double a0 = Dj[(kk + fk) * ldD], a1 = Dj[(kk + 4 + fk) * ldD];
-      const double b0 = P[(c0 + kk + fk) * BR + fr], b1 = P[(c0 + kk + 4 + fk) * BR + fr];
+      const double b0 = pget(c0 + kk + fk, fr), b1 = pget(c0 + kk + 4 + fk, fr);
       t0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, t0, 0, 0, 0);
       t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, t1, 0, 0, 0);
     }
@@ -697,14 +721,16 @@ __global__ __launch_bounds__(kTrsmThreads) void dtrsm_inv_kernel(const TrsmInvAr
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int c = c0 + 16 * g + fk + 4 * q;
-        P[c * BR + fr] = t[q] + red[(g * 4 + q) * 64 + lane];
+        pset(c, fr, t[q] + red[(g * 4 + q) * 64 + lane]);
       }
     }
     __syncthreads();
   }
-  for (int idx = tid; idx < n * BR; idx += kTrsmThreads) {
-    int c = idx / BR, rr = idx % BR;
-    if (r0 + rr < m) d.B[(size_t)c * d.ldb + r0 + rr] = P[idx];
+  if (!kGlobal) {
+    for (int idx = tid; idx < n * BR; idx += kTrsmThreads) {
+      int c = idx / BR, rr = idx % BR;
+      if (r0 + rr < m) Bp[(size_t)c * ldb + r0 + rr] = P[idx];
+    }
   }
 }
 
@@ -901,11 +927,12 @@ void launch_gemm_batch(const GemmDesc* descs, int n, hipStream_t stream) {
 static constexpr int kTrsmRows = 16;
 static constexpr int kTrsmMaxCols = 18 * 64;  // LDS bound: (18*64*16 + 1024) doubles < 160 KiB
 
-// invD[i] must already hold the inverted diagonal blocks of descs[i].L
-void launch_trsm_inv(const TrsmDesc* descs, const double* const* invD, int n, hipStream_t stream) {
+// invD[i] must already hold the inverted diagonal blocks of descs[i].L.
+// in_place: the small-LDS variant (every n a multiple of 64; see dtrsm_inv_kernel)
+void launch_trsm_inv(const TrsmDesc* descs, const double* const* invD, int n, hipStream_t stream, bool in_place = false) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)dtrsm_inv_kernel<kTrsmRows>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)dtrsm_inv_kernel<kTrsmRows, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   for (int s0 = 0; s0 < n; s0 += kMaxTrsmBatch) {
@@ -921,12 +948,17 @@ void launch_trsm_inv(const TrsmDesc* descs, const double* const* invD, int n, hi
       a.block_start[i] = total;
       total += (a.d[i].m + kTrsmRows - 1) / kTrsmRows;
       maxn = std::max(maxn, a.d[i].n);
+      if (in_place && a.d[i].n % 64 != 0) fatal("dtrsm in-place kernel: n=%d is not a multiple of 64", a.d[i].n);
     }
     a.block_start[cnt] = total;
     if (total == 0) continue;
+    if (in_place) {
+      hipLaunchKernelGGL((dtrsm_inv_kernel<kTrsmRows, true>), dim3(total), dim3(kTrsmThreads), 1024 * sizeof(double), stream, a);
+      continue;
+    }
     if (maxn > kTrsmMaxCols) fatal("dtrsm tile kernel: n=%d exceeds the LDS-resident panel limit %d", maxn, kTrsmMaxCols);
     size_t lds = ((size_t)((maxn + 63) / 64) * 64 * kTrsmRows + 1024) * sizeof(double);
-    hipLaunchKernelGGL((dtrsm_inv_kernel<kTrsmRows>), dim3(total), dim3(kTrsmThreads), lds, stream, a);
+    hipLaunchKernelGGL((dtrsm_inv_kernel<kTrsmRows, false>), dim3(total), dim3(kTrsmThreads), lds, stream, a);
   }
 }
 
@@ -1086,7 +1118,7 @@ static void launch_lower_inverse(const double* L, int lda, int n, const double* 
 // Blocked tile Cholesky (lower). ws needs 4096 doubles unless p.invD_out keeps
 // every diagonal-block inverse (then the panel TRSMs can reuse them); with W_out
 // and no invD_out it needs every block inverse (potrf_workspace_bytes).
-void launch_trsm_inv(const TrsmDesc* descs, const double* const* invD, int n, hipStream_t stream);
+void launch_trsm_inv(const TrsmDesc* descs, const double* const* invD, int n, hipStream_t stream, bool in_place);
 void launch_potrf(const PotrfDesc& p, hipStream_t stream, double* ws) {
   const int JB = 64;
   const bool keep_all = p.invD_out || p.W_out;
@@ -1584,7 +1616,50 @@ struct PotrfStepArgs {
   int j;            // step (-1: first launch, nb - 1: last launch)
   // item ranges: [0, n_diag) DIAG, then TRAIL, RUPD, LW, XW, ZERO
   int n_diag, n_trail, n_rupd, n_lw, n_xw, n_zero;
+  // auto panel solve (optional): the items that finalize blocks of L and W fold
+  // their max |.| into est[0] / est[1] (bit patterns), the last launch counts its
+  // workgroups in est[2] and the last one publishes max|L| max|W| to est_host
+  unsigned long long* est;
+  double* est_host;
 };
+
+// max |v| of the workgroup folded into est[slot]: non-negative doubles order
+// like their bit patterns (integer max); one atomic per wave
+__device__ __forceinline__ void est_fold(unsigned long long* est, int slot, double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0 && v > 0.0)
+    __hip_atomic_fetch_max(est + slot, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double acc_absmax(const double4_t (&acc)[2][2]) {
+  double v = 0.0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v = fmax(v, fabs(acc[i][j][q]));
+  return v;
+}
+// Last launch of a tile POTRF: the workgroup that retires last publishes the
+// estimate (system scope: the host reads it once the launch's event completed)
+// and clears the device slots for the next factorization using them.
+__device__ __forceinline__ void est_publish(const PotrfStepArgs& a) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  unsigned long long* e = a.est;
+  const unsigned long long old = __hip_atomic_fetch_add(e + 2, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (old != (unsigned long long)gridDim.x - 1) return;
+  const double mL = __longlong_as_double((long long)__hip_atomic_load(e + 0, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT));
+  const double mW = __longlong_as_double((long long)__hip_atomic_load(e + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT));
+  __hip_atomic_store(e + 0, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(e + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(e + 2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double v = mL * mW;
+  if (!(v > 0.0)) v = v != v ? __builtin_huge_val() : 2.2250738585072014e-308;  // 0 means "not published"
+  __hip_atomic_store(a.est_host, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // Prefetch of a 64 x 64 block into registers (8 x 16 B per thread), so its
 // global latency overlaps the MFMA work on the LDS buffers, then the LDS store.
@@ -1623,6 +1698,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
   __shared__ double pool[2 * 64 * kPL];
   crit_claim(a.claim);
   dpotrf_step(a, pool);
+  if (a.est && a.j == a.nb - 1) est_publish(a);
   crit_release(a.claim);
 }
 __device__ __forceinline__ void dpotrf_step(const PotrfStepArgs& a, double* pool) {
@@ -1743,6 +1819,7 @@ __device__ __forceinline__ void dpotrf_step(const PotrfStepArgs& a, double* pool
     mma_blk(acc, S0, S1, 1.0);
     __syncthreads();  // every wave has read S0 (a copy of the block being overwritten)
     acc_store(acc, blkA(r, p), lda, false);
+    if (a.est) est_fold(a.est, 0, acc_absmax(acc));  // L(r, p) is final
     return;
   }
   it -= a.n_lw;
@@ -1754,7 +1831,20 @@ __device__ __forceinline__ void dpotrf_step(const PotrfStepArgs& a, double* pool
     const double* iDr = a.invD + (size_t)row * 4096;
     if (c == row) {  // diagonal block: iD itself
       double* Wd = blkW(row, row);
-      for (int e = threadIdx.x; e < 4096; e += 256) Wd[(size_t)(e >> 6) * ldw + (e & 63)] = iDr[e];
+      double mw = 0.0, ml = 0.0;
+      const double* Ld = blkA(row, row);
+      for (int e = threadIdx.x; e < 4096; e += 256) {
+        const double v = iDr[e];
+        Wd[(size_t)(e >> 6) * ldw + (e & 63)] = v;
+        if (a.est) {
+          mw = fmax(mw, fabs(v));
+          if ((e & 63) >= (e >> 6)) ml = fmax(ml, fabs(Ld[(size_t)(e >> 6) * lda + (e & 63)]));  // L(row, row), lower
+        }
+      }
+      if (a.est) {
+        est_fold(a.est, 0, ml);
+        est_fold(a.est, 1, mw);
+      }
       return;
     }
     stage_blk(S1, iDr, 64, false);
@@ -1764,6 +1854,7 @@ __device__ __forceinline__ void dpotrf_step(const PotrfStepArgs& a, double* pool
     mma_blk(acc, S1, S0, 1.0);
     __syncthreads();
     acc_store(acc, blkW(row, c), ldw, false);
+    if (a.est) est_fold(a.est, 1, acc_absmax(acc));  // W(row, c) is final
     return;
   }
   it -= a.n_xw;
@@ -1794,6 +1885,97 @@ bool potrf_steps_eligible(const PotrfDesc& p) {
 
 size_t potrf_steps_workspace_bytes(const PotrfDesc& p) { return p.invD_out ? 0 : (size_t)(p.n / 64) * 4096 * sizeof(double); }
 
+// ---------------------------------------------- host-published panel estimates
+// Under PARSEC_DPOTRF_TRSM=auto the tile POTRF that writes W = L^-1 publishes
+// max|L| max|W| into pinned host memory when its last step launch retires. The
+// engine dispatches TRSM(m, k) only after POTRF(k)'s completion event, so the
+// TRSM launch reads the estimate on the host and launches the substitution
+// kernel only for the panels above the limit: no gated kernel rides the
+// critical stream behind every panel GEMM. A W whose estimate is unknown here
+// (factored by another process, or not yet published) takes the device-side
+// gate (scan in the copy kernel, in-place gated substitution kernel).
+namespace {
+constexpr uint32_t kEstSlots = 4096;
+struct EstimateSlots {
+  std::mutex m;
+  bool tried = false;
+  double* host = nullptr;              // [kEstSlots], pinned; 0 = not published
+  unsigned long long* dev = nullptr;   // [kEstSlots][4]: max|L|, max|W|, arrivals, pad
+  const double* owner[kEstSlots] = {};
+  uint32_t next = 0;
+  std::unordered_map<const double*, uint32_t> of_w;
+};
+EstimateSlots g_est[16];
+int g_est_route = -1;  // PARSEC_DPOTRF_TRSM_ESTIMATE: 1 = host-published (default), 0 = device gate only
+EstimateSlots* est_slots() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  return &g_est[dev];
+}
+}  // namespace
+
+int trsm_estimate_route(int on) {
+  if (g_est_route < 0) {
+    const char* e = getenv("PARSEC_DPOTRF_TRSM_ESTIMATE");
+    g_est_route = e ? (atoi(e) != 0) : 1;
+  }
+  const int prev = g_est_route;
+  if (on >= 0) g_est_route = on != 0;
+  return prev;
+}
+
+// A slot for the POTRF writing W (device / host halves), or false.
+static bool est_acquire(const double* W, unsigned long long** dev, double** host) {
+  if (trsm_estimate_route(-1) == 0 || parsec::trsm_inverse_mode(-1, 0.0) != 1) return false;
+  EstimateSlots* e = est_slots();
+  if (!e) return false;
+  std::lock_guard<std::mutex> lk(e->m);
+  if (!e->tried) {
+    e->tried = true;
+    void* h = nullptr;
+    void* d = nullptr;
+    if (hipHostMalloc(&h, kEstSlots * sizeof(double), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) { (void)hipGetLastError(); h = nullptr; }
+    if (h && hipMalloc(&d, kEstSlots * 4 * sizeof(unsigned long long)) != hipSuccess) { (void)hipGetLastError(); d = nullptr; }
+    if (h && d && hipMemset(d, 0, kEstSlots * 4 * sizeof(unsigned long long)) == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
+      std::memset(h, 0, kEstSlots * sizeof(double));
+      e->host = static_cast<double*>(h);
+      e->dev = static_cast<unsigned long long*>(d);
+    } else {
+      (void)hipGetLastError();
+      if (h) (void)hipHostFree(h);
+      if (d) (void)hipFree(d);
+    }
+  }
+  if (!e->host) return false;
+  const uint32_t slot = e->next++ % kEstSlots;
+  if (e->owner[slot]) {
+    auto it = e->of_w.find(e->owner[slot]);
+    if (it != e->of_w.end() && it->second == slot) e->of_w.erase(it);
+  }
+  e->owner[slot] = W;
+  e->of_w[W] = slot;
+  *reinterpret_cast<volatile double*>(&e->host[slot]) = 0.0;
+  *dev = e->dev + (size_t)slot * 4;
+  *host = e->host + slot;
+  return true;
+}
+
+// The published estimate of the POTRF that wrote W (> 0), or 0 when unknown.
+static double est_lookup(const double* W) {
+  if (trsm_estimate_route(-1) == 0) return 0.0;
+  EstimateSlots* e = est_slots();
+  if (!e || !e->host) return 0.0;
+  std::lock_guard<std::mutex> lk(e->m);
+  auto it = e->of_w.find(W);
+  if (it == e->of_w.end() || e->owner[it->second] != W) return 0.0;
+  const double v = *reinterpret_cast<volatile const double*>(&e->host[it->second]);
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return v;
+}
+
+// Estimates published / taken on the host / left to the device gate (tests, bench)
+static std::atomic<uint64_t> g_est_stats[3];
+
 void launch_potrf_steps(const PotrfDesc& p, hipStream_t stream, double* ws) {
   PotrfStepArgs a{};
   a.A = p.A; a.lda = p.lda; a.W = p.W_out; a.ldw = p.ldw; a.info = p.info;
@@ -1809,6 +1991,9 @@ void launch_potrf_steps(const PotrfDesc& p, hipStream_t stream, double* ws) {
   }
   a.stamp = (g_potrf_stamp_mode ? 1 : 0) | (spread ? 2 : 0);
   a.claim = t_launch_claim >= 1;
+  a.est = nullptr;
+  a.est_host = nullptr;
+  if (p.W_out && est_acquire(p.W_out, &a.est, &a.est_host)) g_est_stats[0].fetch_add(1, std::memory_order_relaxed);
   const int nb = p.n / 64;
   a.nb = nb;
   const bool w = p.W_out != nullptr;
@@ -1849,39 +2034,62 @@ size_t trsm_w_workspace_bytes(const TrsmGemmDesc* d, int n) {
 }
 
 // B := B W^T for every descriptor: copy the B tiles into the workspace, then one
-// grouped GEMM writes B from (copy x W^T). Under trsm_inverse_mode auto the
-// copy kernel also estimates each W's conditioning (max|L| * max|W|), the GEMM
-// skips the panels above the limit, and a gated substitution kernel behind it
-// solves exactly those (blocked TRSM with W's diagonal 64-blocks as the
-// inverted diagonal blocks); mode blocked solves every panel by substitution.
+// grouped GEMM writes B from (copy x W^T). Panel-solve modes:
+//  * blocked: every panel with its factor by substitution (blocked TRSM with W's
+//    diagonal 64-blocks as the inverted diagonal blocks);
+//  * auto, estimate published by the local POTRF (est_lookup): the panels above
+//    the limit by substitution, the others through W -- decided here, no gate;
+//  * auto, estimate unknown (W from another process): the copy kernel estimates
+//    each W's conditioning (max|L| * max|W|) into W's spare slots, the GEMM skips
+//    the panels above the limit and the in-place gated substitution kernel behind
+//    it solves exactly those.
 static const bool g_trsm_tri = !getenv("PARSEC_TRSM_TRI") || atoi(getenv("PARSEC_TRSM_TRI")) != 0;
+static bool trsm_substitutable(const TrsmGemmDesc& t) {
+  // the substitution kernel keeps a panel of n columns in LDS
+  return t.L && t.ldl > 0 && t.n <= kTrsmMaxCols && t.n % 64 == 0 && t.ldw >= t.n;
+}
 static bool trsm_gateable(const TrsmGemmDesc& t) {
-  // the estimate slots sit at W(0..1, n-1): outside every k range the GEMM reads
-  // only for n >= 256; the substitution kernel keeps a panel of n columns in LDS
-  return t.L && t.ldl > 0 && t.n >= 256 && t.n <= kTrsmMaxCols && t.n % 64 == 0 && t.ldw >= t.n;
+  // the estimate slots sit at W(0..1, n-1): outside every k range the
+  // triangular (b_upper) GEMM reads only for n >= 256
+  return trsm_substitutable(t) && t.n >= 256 && g_trsm_tri;
+}
+static TrsmDesc subst_desc(const TrsmGemmDesc& t, bool gate) {
+  TrsmDesc x{};
+  x.L = t.L; x.ldl = t.ldl; x.B = t.B; x.ldb = t.ldb; x.m = t.m; x.n = t.n; x.trans = 1;
+  x.invD = t.W; x.invD_ld = t.ldw; x.gate = gate ? 1 : 0;
+  return x;
 }
 void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, double* ws) {
   const int mode = parsec::trsm_inverse_mode(-1, 0.0);
-  for (int s0 = 0; s0 < n; s0 += kMaxCopyBatch) {
-    const int cnt = std::min(kMaxCopyBatch, n - s0);
-    std::vector<TrsmDesc> fb;  // substitution solves of this chunk
-    if (mode == 2) {
-      for (int i = 0; i < cnt; ++i) {
-        const TrsmGemmDesc& t = d[s0 + i];
-        if (!trsm_gateable(t)) continue;
-        TrsmDesc x{};
-        x.L = t.L; x.ldl = t.ldl; x.B = t.B; x.ldb = t.ldb; x.m = t.m; x.n = t.n; x.trans = 1;
-        x.invD = t.W; x.invD_ld = t.ldw;
-        fb.push_back(x);
+  const double limit = parsec::trsm_inverse_limit();
+  std::vector<TrsmDesc> subst;          // solved by substitution, decided on the host
+  std::vector<TrsmGemmDesc> via_w;      // through W
+  std::vector<uint8_t> gated;           // ... with the device-side gate
+  for (int i = 0; i < n; ++i) {
+    const TrsmGemmDesc& t = d[i];
+    int route = 0;  // 0 W, 1 substitution, 2 W gated on the device
+    if (mode == 2 && trsm_substitutable(t)) {
+      route = 1;
+    } else if (mode == 1 && trsm_substitutable(t)) {
+      const double e = est_lookup(t.W);
+      if (e > 0.0) {
+        route = e > limit ? 1 : 0;
+        g_est_stats[1].fetch_add(1, std::memory_order_relaxed);
+      } else if (trsm_gateable(t)) {
+        route = 2;
+        g_est_stats[2].fetch_add(1, std::memory_order_relaxed);
       }
-      if ((int)fb.size() == cnt) {  // every panel by substitution: no copy, no GEMM
-        std::vector<const double*> inv(fb.size());
-        for (size_t i = 0; i < fb.size(); ++i) inv[i] = fb[i].invD;
-        launch_trsm_inv(fb.data(), inv.data(), (int)fb.size(), stream);
-        continue;
-      }
-      fb.clear();  // (a panel without its factor: through W like mode 0)
     }
+    if (route == 1) {
+      subst.push_back(subst_desc(t, false));
+    } else {
+      via_w.push_back(t);
+      gated.push_back(route == 2);
+    }
+  }
+  for (size_t s0 = 0; s0 < via_w.size(); s0 += kMaxCopyBatch) {
+    const int cnt = (int)std::min<size_t>(kMaxCopyBatch, via_w.size() - s0);
+    std::vector<TrsmDesc> fb;  // gated substitution solves of this chunk
     CopyBatchArgs ca;
     ca.count = cnt;
     ca.prio = t_launch_prio;
@@ -1890,7 +2098,7 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
     char* p = reinterpret_cast<char*>(ws);
     int maxc = 1;
     for (int i = 0; i < cnt; ++i) {
-      const TrsmGemmDesc& t = d[s0 + i];
+      const TrsmGemmDesc& t = via_w[s0 + i];
       ca.rows[i] = t.m; ca.cols[i] = t.n; ca.ld_src[i] = t.ldb; ca.ld_dst[i] = t.m;
       ca.src[i] = t.B; ca.dst[i] = reinterpret_cast<double*>(p);
       maxc = std::max(maxc, t.n);
@@ -1901,7 +2109,7 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
       e.alpha = 1.0; e.beta = 0.0; e.transA = 0; e.transB = 1; e.lower_only = 0; e.a_lower = 0;  // copy x (L^-1)^T
       e.b_upper = g_trsm_tri ? 1 : 0;  // (L^-1)^T is upper triangular: output column block j needs k < (j+1) BN only
       e.gate = 0;
-      if (mode == 1 && trsm_gateable(t)) {
+      if (gated[s0 + i]) {
         int j = 0;
         while (j < ca.nscan && ca.scan_W[j] != t.W) ++j;
         if (j == ca.nscan && ca.nscan < kMaxScan) {
@@ -1911,10 +2119,7 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
         }
         if (j < ca.nscan) {
           e.gate = 1;
-          TrsmDesc x{};
-          x.L = t.L; x.ldl = t.ldl; x.B = t.B; x.ldb = t.ldb; x.m = t.m; x.n = t.n; x.trans = 1;
-          x.invD = t.W; x.invD_ld = t.ldw; x.gate = 1;
-          fb.push_back(x);
+          fb.push_back(subst_desc(t, true));
         }
       }
       p += ((size_t)t.m * t.n * sizeof(double) + 255) / 256 * 256;
@@ -1924,9 +2129,20 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
     if (!fb.empty()) {
       std::vector<const double*> inv(fb.size());
       for (size_t i = 0; i < fb.size(); ++i) inv[i] = fb[i].invD;
-      launch_trsm_inv(fb.data(), inv.data(), (int)fb.size(), stream);
+      launch_trsm_inv(fb.data(), inv.data(), (int)fb.size(), stream, true);
     }
   }
+  if (!subst.empty()) {
+    std::vector<const double*> inv(subst.size());
+    for (size_t i = 0; i < subst.size(); ++i) inv[i] = subst[i].invD;
+    launch_trsm_inv(subst.data(), inv.data(), (int)subst.size(), stream);
+  }
+}
+
+// counters: [0] estimates published by POTRF, [1] panel decisions taken on the
+// host, [2] panels left to the device gate
+void trsm_estimate_stats(uint64_t out[3], bool reset) {
+  for (int i = 0; i < 3; ++i) out[i] = reset ? g_est_stats[i].exchange(0) : g_est_stats[i].load();
 }
 
 }  // namespace kern

@@ -645,6 +645,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("trsm_inverse_mode", [](int mode, double limit) { return trsm_inverse_mode(mode, limit); }, py::arg("mode") = -1, py::arg("limit") = 0.0,
         "Tile-Cholesky panel solve: 0 through W = L^-1, 1 auto (substitution when max|L| max|W| > limit), 2 substitution; returns the previous mode");
   m.def("trsm_inverse_limit", []() { return trsm_inverse_limit(); });
+  m.def("trsm_estimate_route", [](int on) { return kern::trsm_estimate_route(on); }, py::arg("on") = -1,
+        "Auto panel solve: 1 decide on the host from the estimate the local POTRF published, 0 device-side gate only; returns the previous setting");
+  m.def("trsm_estimate_stats", [](bool reset) {
+    uint64_t v[3];
+    kern::trsm_estimate_stats(v, reset);
+    return py::make_tuple(v[0], v[1], v[2]);
+  }, py::arg("reset") = false, "(published by POTRF, decided on the host, left to the device gate)");
   m.def("device_memcpy_stats", [](bool reset) {
     uint64_t b[3];
     device_memcpy_stats(b, reset);

@@ -73,7 +73,7 @@ JDF_SOURCES = [
 JDF_USERS = ["csrc/algos/dpotrf_jdf.cpp", "csrc/algos/redistribute_ptg.cpp"]
 FORTRAN_SOURCES = ["csrc/fortran/parsecf.F90", "csrc/fortran/parsec_profilef.F90"]
 FLANG = os.path.join(ROCM, "lib", "llvm", "bin", "flang")
-TEST_SOURCES = ["tests/native/test_containers.cpp", "tests/native/test_futures.cpp"]
+TEST_SOURCES = ["tests/native/test_containers.cpp", "tests/native/test_futures.cpp", "tests/native/test_fetch_queue.cpp"]
 
 
 def _exists(paths):

@@ -140,15 +140,18 @@ def _factor_gpu(pa, S, N, nb, mode, limit=0.0):
         pa.trsm_inverse_mode(prev, prev_limit)
 
 
-@pytest.mark.parametrize("nb", [512, 1024])
+@pytest.mark.parametrize("nb", [256, 512, 1024])
 def test_trsm_inverse_modes_gpu(pa, nb):
-    """Panel solve through W = L^-1 (mode 0), by the gated substitution kernel
-    (mode 2) and auto (mode 1: the copy kernel estimates max|L| max|W| into W's
-    spare slots, the W-GEMM skips and the substitution kernel solves above the
-    limit). On an SPD matrix with cond 1e12 (numerics sweep:
-    profiles/r4_trsm_inverse_numerics.txt) every mode is backward stable; auto
-    with its default limit takes the inverse path (same factor as mode 0) and
-    auto with limit 1 takes the substitution path (same factor as mode 2)."""
+    """Panel solve through W = L^-1 (mode 0), by substitution (mode 2) and auto
+    (mode 1). Auto decides per panel from max|L| max|W|: by default the tile
+    POTRF publishes it to pinned host memory and the TRSM launch picks the
+    route on the host (no gated kernel); with trsm_estimate_route(0) the copy
+    kernel estimates into W's spare slots, the W-GEMM skips and the in-place
+    gated substitution kernel solves above the limit. On an SPD matrix with
+    cond 1e12 (numerics sweep: profiles/r4_trsm_inverse_numerics.txt) every mode
+    is backward stable; auto with its default limit takes the inverse path (same
+    factor as mode 0) and auto with limit 1 takes the substitution path (same
+    factor as mode 2), through either estimate route."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     N = 2048
@@ -158,12 +161,29 @@ def test_trsm_inverse_modes_gpu(pa, nb):
     S = (0.5 * (S + S.t())).cuda()
     L0 = _factor_gpu(pa, S, N, nb, 0)
     L2 = _factor_gpu(pa, S, N, nb, 2)
+    pa.trsm_estimate_stats(True)
     L1 = _factor_gpu(pa, S, N, nb, 1)
     L1s = _factor_gpu(pa, S, N, nb, 1, 1.0)
+    published, host, device = pa.trsm_estimate_stats(True)
+    NT = N // nb
+    assert published == 2 * (NT - 1)           # every POTRF with a W published its estimate
+    assert host == 2 * NT * (NT - 1) // 2      # every TRSM decided on the host
+    assert device == 0
+    prev_route = pa.trsm_estimate_route(0)
+    try:
+        L1d = _factor_gpu(pa, S, N, nb, 1)
+        L1ds = _factor_gpu(pa, S, N, nb, 1, 1.0)
+    finally:
+        pa.trsm_estimate_route(prev_route)
+    published, host, device = pa.trsm_estimate_stats(True)
+    assert published == 0 and host == 0
+    assert device == (2 * NT * (NT - 1) // 2 if nb >= 256 else 0)
     nS = torch.linalg.norm(S)
-    for L in (L0, L1, L2, L1s):
+    for L in (L0, L1, L2, L1s, L1d, L1ds):
         assert (torch.linalg.norm(L @ L.t() - S) / nS).item() < 1e-14
     d02 = torch.linalg.norm(L0 - L2).item()
     assert d02 > 0  # the two solves differ (by ~cond(L(k,k)) eps)
-    assert torch.linalg.norm(L1 - L0).item() < 1e-3 * d02   # auto below the limit = the inverse path
-    assert torch.linalg.norm(L1s - L2).item() < 1e-3 * d02  # auto above it = the substitution path
+    for La, Lb in ((L1, L0), (L1d, L0)):  # auto below the limit = the inverse path
+        assert torch.linalg.norm(La - Lb).item() < 1e-3 * d02
+    for La, Lb in ((L1s, L2), (L1ds, L2)):  # auto above it = the substitution path
+        assert torch.linalg.norm(La - Lb).item() < 1e-3 * d02

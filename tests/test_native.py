@@ -1,5 +1,6 @@
 """Runs the native C++ unit-test programs built by parsec_amd._build
-(build/tests/*): lock-free containers, mempool, sharded hash map, barrier, futures, rwlock."""
+(build/tests/*): lock-free containers, mempool, sharded hash map, barrier, futures, rwlock,
+the priority-ordered bounded fetch queue of the remote dependency engine."""
 import os
 import subprocess
 
@@ -9,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "build", "tests")
 
 
-@pytest.mark.parametrize("prog", ["test_containers", "test_futures"])
+@pytest.mark.parametrize("prog", ["test_containers", "test_futures", "test_fetch_queue"])
 def test_native_program(pa, prog):
     exe = os.path.join(BIN, prog)
     if not os.path.exists(exe):
