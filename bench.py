@@ -269,6 +269,22 @@ def main():
         check = err
         _stage("check done")
 
+    # every rank's one-sided transfers by route (IPC pull over xGMI / host
+    # fragments) and payload bytes, gathered for the JSON line; a multi-rank run
+    # whose payloads went through host fragments is not the headline path
+    comm = []
+    if world > 1:
+        cs = pa.comm_stats()
+        keys = ("get_ipc", "get_fragments", "bytes_pulled_ipc", "bytes_fragments", "gets_queued_max")
+        mine = torch.tensor([int(cs.get(k, 0)) for k in keys], dtype=torch.int64, device="cpu" if args.share_gpu else "cuda")
+        got = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(got, mine)
+        comm = [dict(rank=r, **{k: int(v) for k, v in zip(keys, g.tolist())}) for r, g in enumerate(got)]
+        frag = [c["rank"] for c in comm if c["get_fragments"] > 0]
+        if frag and not args.allow_host_plane:
+            if rank == 0:
+                print(f"error: payloads took the host-fragment route on ranks {frag}: {comm}", file=sys.stderr, flush=True)
+            raise SystemExit(4)
     devs = pa.devices()
     _stage("fini context")
     ctx.fini()
@@ -295,6 +311,8 @@ def main():
                        "parallelism": f"2D block-cyclic P{P}xQ{Q}, 1 process/GPU", "threads_per_rank": args.cores},
         }
         out["device_plane"] = planes
+        if comm:
+            out["comm"] = comm
         est = pa.trsm_estimate_stats(False)
         out["panel_solve"] = {"mode": {0: "inverse", 1: "auto", 2: "blocked"}.get(pa.trsm_inverse_mode(), "?"),
                               "estimates_published": est[0], "decided_on_host": est[1], "device_gate": est[2]}

@@ -250,6 +250,18 @@ dtd::DtdTaskpool* as_dtd(parsec_taskpool_t* tp) {
 struct PendingArgs {
   std::vector<dtd::Arg> args;
   std::vector<std::pair<int, int>> sig;
+  // bytes of the VALUE arguments, owned (parsec_dtd_create_task: the caller's
+  // variables may change or go out of scope before the task is inserted;
+  // reference insert_function.c:2812 copies them into the task at creation)
+  std::vector<std::vector<char>> values;
+  void own_values() {
+    for (dtd::Arg& a : args) {
+      if ((a.op & dtd::OP_MASK) != dtd::VALUE || !a.ptr || a.size <= 0) continue;
+      const char* p = static_cast<const char*>(a.ptr);
+      values.emplace_back(p, p + a.size);  // a moved vector keeps its buffer: earlier pointers stay valid
+      a.ptr = values.back().data();
+    }
+  }
 };
 
 void parse_one(int size, void* ptr, int flags, PendingArgs& pa) {
@@ -1239,6 +1251,7 @@ parsec_task_t* parsec_dtd_create_task(parsec_taskpool_t* tp, parsec_dtd_funcptr_
   va_start(ap, name);
   parse_args(ap, t->pa);
   va_end(ap);
+  t->pa.own_values();
   std::lock_guard<std::mutex> g(g_deferred_m);
   g_deferred.insert(t);
   return t;

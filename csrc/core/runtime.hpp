@@ -83,6 +83,7 @@ enum TransferStatus : uint8_t { TRANSFER_NOT = 0, TRANSFER_UNDER = 1, TRANSFER_C
 enum DataFlags : uint8_t {
   DATA_FLAG_ARENA = 0x1, DATA_FLAG_TRANSIT = 0x2, DATA_FLAG_PARSEC_MANAGED = 0x4, DATA_FLAG_PARSEC_OWNED = 0x8,
   DATA_FLAG_DEVICE_CACHE = 0x10,  // a device engine's cache copy: the engine owns its lifetime (LRU, eviction)
+  DATA_FLAG_OWNS_DATA = 0x20,     // the copy's `original` is a private Data made for it: released with the copy
 };
 
 // Datatype: a typed, possibly strided layout. Replaces MPI datatypes of the

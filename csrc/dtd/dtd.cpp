@@ -234,12 +234,15 @@ static void shadow_copy_release(DataCopy* c) {
   if (c->device_index == 0) std::free(c->device_private);
   else if (c->snapshot_from_zone) (void)device_cache_free(c->device_index, c->device_private);
   else device_free(c->device_index, c->device_private);
-  if (Data* d = c->original) {
+  Data* d = c->original;
+  if (d) {
     d->lock.lock();
     data_copy_detach(d, c, c->device_index);
     d->lock.unlock();
   }
+  const bool owns = (c->flags & DATA_FLAG_OWNS_DATA) != 0;
   delete c;
+  if (d && owns) data_release(d);
 }
 
 static DataCopy* shadow_copy_new(const DataCopy* src, size_t n) {
@@ -825,13 +828,21 @@ void DtdTaskpool::finish_remote_activation(ExecutionStream* es, DtdTask* t, Remo
         std::lock_guard<SpinLock> g(d->lock);
         const uint32_t v = d->newest_version() + 1;
         // earlier received versions: detached (a task still reading one holds
-        // its own reference); engine cache copies: invalidated
+        // its own reference) onto a private Data of their own, so CPU and GPU
+        // stage-in of a local reader that got such a version as its input --
+        // a remote writer's next version can land before that reader runs --
+        // still find its bytes (pulled to the host / used in place); engine
+        // cache copies: invalidated
         for (int i = 0; i < kMaxDevices; ++i)
           for (DataCopy* o = d->copy(i); o;) {
             DataCopy* next = o->older;
             if (o->release_fn == shadow_copy_release) {
               data_copy_detach(d, o, i);
-              o->original = nullptr;
+              Data* own = data_new();
+              own->nb_elts = d->nb_elts;
+              own->owner_device = o->device_index;
+              o->flags |= DATA_FLAG_OWNS_DATA;
+              data_copy_attach(own, o, i);
               old.push_back(o);
             } else {
               o->coherency_state = COHERENCY_INVALID;

@@ -16,10 +16,12 @@
  * Compiled as C99 (gcc) against include/parsec.h and the HIP runtime API;
  * the kernels live in dtd_gpu_kernels.hip (hipcc). Without GPUs every case runs
  * its CPU chores. */
+#define _POSIX_C_SOURCE 200809L
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <hip/hip_runtime_api.h>
 
@@ -513,6 +515,87 @@ static int test_multiple_devices(parsec_context_t* ctx, int rank, int world) {
   return g_errors - e0;
 }
 
+/* superseded: rank 1 writes tile T (its own) with a GPU chore, a slow CPU
+ * reader on rank 0 reads it, then rank 1 writes T again. The second version
+ * can land on rank 0 before the first reader ran (a remote writer is not
+ * ordered after a local reader); the reader must still see the FIRST version,
+ * in host memory, although the received versions live in device memory (the
+ * superseded one moves to a private Data: csrc/dtd/dtd.cpp). Needs 2 ranks. */
+static int fill_chore_cpu(parsec_execution_stream_t* es, parsec_task_t* t) {
+  (void)es;
+  int *data, nb, value, r;
+  parsec_dtd_unpack_args(t, &data, &nb, &value, &r);
+  for (int j = 0; j < nb; j++) data[j] = value;
+  COUNT(g_cpu_chores);
+  return PARSEC_HOOK_RETURN_DONE;
+}
+static int fill_chore_gpu(void* stream, parsec_task_t* t) {
+  int *data, nb, value, r;
+  parsec_dtd_unpack_args(t, &data, &nb, &value, &r);
+  COUNT(g_gpu_chores);
+  return hipMemsetD32Async((hipDeviceptr_t)parsec_dtd_get_dev_ptr(t, 0), value, (size_t)nb, (hipStream_t)stream) == hipSuccess ? PARSEC_HOOK_RETURN_DONE
+                                                                                                                              : PARSEC_HOOK_RETURN_ERROR;
+}
+static int slow_cpu(parsec_execution_stream_t* es, parsec_task_t* t) {
+  (void)es;
+  int *s, r;
+  parsec_dtd_unpack_args(t, &s, &r);
+  struct timespec ts = {0, 400 * 1000 * 1000};
+  nanosleep(&ts, NULL);
+  return PARSEC_HOOK_RETURN_DONE;
+}
+static int check_cpu(parsec_execution_stream_t* es, parsec_task_t* t) {
+  (void)es;
+  int *s, *src, nb, expect, r;
+  parsec_dtd_unpack_args(t, &s, &src, &nb, &expect, &r);
+  for (int j = 0; j < nb; j++)
+    if (src[j] != expect) { ERR("superseded: reader saw T[%d] = %d, expected %d\n", j, src[j], expect); break; }
+  s[0] += 1;
+  return PARSEC_HOOK_RETURN_DONE;
+}
+static int test_superseded(parsec_context_t* ctx, int rank, int world) {
+  if (world < 2) return -1;
+  const int e0 = g_errors;
+  int nb = 1 << 15, one = 1, zero = 0, v1 = 11, v2 = 22;
+  coll_t A;
+  coll_init(&A, rank, world, nb, 1);
+  parsec_taskpool_t* tp = parsec_dtd_taskpool_new();
+  parsec_context_start(ctx);
+  parsec_context_add_taskpool(ctx, tp);
+  parsec_dtd_task_class_t* ftc = parsec_dtd_create_task_class(tp, "fill", PASSED_BY_REF, PARSEC_INOUT, (int)sizeof(int), PARSEC_VALUE,
+                                                              (int)sizeof(int), PARSEC_VALUE, (int)sizeof(int), PARSEC_VALUE, PARSEC_DTD_ARG_END);
+  if (g_nb_gpus) parsec_dtd_task_class_add_chore(tp, ftc, PARSEC_DEV_HIP, (void*)fill_chore_gpu);
+  parsec_dtd_task_class_add_chore(tp, ftc, PARSEC_DEV_CPU, (void*)fill_chore_cpu);
+  const int dev = g_nb_gpus ? PARSEC_DEV_HIP : PARSEC_DEV_CPU;
+  parsec_dtd_tile_t* T = PARSEC_DTD_TILE_OF(&A.dc, 0, 1);
+  parsec_dtd_tile_t* S = PARSEC_DTD_TILE_OF(&A.dc, 0, 0);
+  parsec_dtd_insert_task_with_task_class(tp, ftc, 1, dev, PARSEC_INOUT, T, PARSEC_DTD_EMPTY_FLAG, &nb, PARSEC_DTD_EMPTY_FLAG, &v1, PARSEC_AFFINITY, &one,
+                                         PARSEC_DTD_ARG_END);
+  parsec_dtd_insert_task(tp, slow_cpu, 1, PARSEC_DEV_CPU, "Slow", PASSED_BY_REF, S, PARSEC_INOUT, (int)sizeof(int), &zero, PARSEC_VALUE | PARSEC_AFFINITY,
+                         PARSEC_DTD_ARG_END);
+  parsec_dtd_insert_task(tp, check_cpu, 1, PARSEC_DEV_CPU, "Check1", PASSED_BY_REF, S, PARSEC_INOUT, PASSED_BY_REF, T, PARSEC_INPUT, (int)sizeof(int),
+                         &nb, PARSEC_VALUE, (int)sizeof(int), &v1, PARSEC_VALUE, (int)sizeof(int), &zero, PARSEC_VALUE | PARSEC_AFFINITY, PARSEC_DTD_ARG_END);
+  parsec_dtd_insert_task_with_task_class(tp, ftc, 1, dev, PARSEC_INOUT, T, PARSEC_DTD_EMPTY_FLAG, &nb, PARSEC_DTD_EMPTY_FLAG, &v2, PARSEC_AFFINITY, &one,
+                                         PARSEC_DTD_ARG_END);
+  parsec_dtd_insert_task(tp, check_cpu, 1, PARSEC_DEV_CPU, "Check2", PASSED_BY_REF, S, PARSEC_INOUT, PASSED_BY_REF, T, PARSEC_INPUT, (int)sizeof(int),
+                         &nb, PARSEC_VALUE, (int)sizeof(int), &v2, PARSEC_VALUE, (int)sizeof(int), &zero, PARSEC_VALUE | PARSEC_AFFINITY, PARSEC_DTD_ARG_END);
+  parsec_dtd_data_flush_all(tp, &A.dc.super.super);
+  parsec_dtd_taskpool_wait(tp);
+  parsec_context_wait(ctx);
+  if (rank == 0) {
+    const unsigned* p = tile_host(&A, 0, 0);
+    const unsigned want = unique_id(0, 0, 1, 0, nb) + 2u;
+    if (p[0] != want) ERR("superseded: S[0] = %u, expected %u (both readers ran)\n", p[0], want);
+  }
+  if (rank == 1) {
+    const unsigned* p = tile_host(&A, 0, 1);
+    if (p[0] != (unsigned)v2) ERR("superseded: T[0] = %u on its owner, expected %d\n", p[0], v2);
+  }
+  parsec_taskpool_free(tp);
+  coll_fini(&A);
+  return g_errors - e0;
+}
+
 static int report(const char* name, int rc) {
   printf("%s: %s\n", name, rc < 0 ? "skipped" : rc == 0 ? "ok" : "FAILED");
   return rc > 0;
@@ -543,6 +626,7 @@ int main(int argc, char** argv) {
   failed += report("write_read (both)", test_write_read(ctx, rank, world, WITH_CPU | (g_nb_gpus ? WITH_GPU : 0)));
   failed += report("gemm_handle", test_gemm_handle(ctx, rank, world));
   failed += report("multiple_devices", test_multiple_devices(ctx, rank, world));
+  failed += report("superseded", test_superseded(ctx, rank, world));
   for (int g = 0; g < MAX_GPUS; ++g)
     if (g_gpu_acc[g]) { (void)hipSetDevice(g); (void)hipFree(g_gpu_acc[g]); }
   printf("dtd gpu capi rank %d chores gpu %d cpu %d errors %d\n", rank, g_gpu_chores, g_cpu_chores, g_errors);

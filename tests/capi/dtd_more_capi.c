@@ -273,12 +273,12 @@ static int run_explicit(parsec_context_t* ctx, int rank, int world) {
   parsec_taskpool_t* tp = parsec_dtd_taskpool_new();
   parsec_context_add_taskpool(ctx, tp);
   parsec_context_start(ctx);
-  static int order[N];
   parsec_task_t* tasks[N];
   for (int i = 0; i < N; ++i) {
-    order[i] = i;
+    /* &i of the creation loop: the value is copied when the task is created
+     * (reference insert_function.c:2812), not read at insertion */
     tasks[i] = parsec_dtd_create_task(tp, bump, 0, PARSEC_DEV_CPU, "Bump", PASSED_BY_REF, PARSEC_DTD_TILE_OF(&A, 0, 0), PARSEC_INOUT | PARSEC_AFFINITY,
-                                      (int)sizeof(int), &order[i], PARSEC_VALUE, PARSEC_DTD_ARG_END);
+                                      (int)sizeof(int), &i, PARSEC_VALUE, PARSEC_DTD_ARG_END);
   }
   if (g_count != 0) BAD("explicit rank %d: %d tasks ran before insertion\n", rank, g_count);
   for (int i = 0; i < N; ++i) parsec_insert_dtd_task(tasks[i]);

@@ -169,6 +169,21 @@ def test_dtd_gpu_chores_two_ranks_cpu(progs):
     text = "".join(o for o, _ in outs)
     assert rc == 0, text + "".join(e for _, e in outs)
     assert "FAILED" not in text and text.count("errors 0") == 2
+    assert text.count("superseded: ok") == 2, text
+
+
+@pytest.mark.gpu
+def test_dtd_gpu_chores_two_ranks_gpu(progs):
+    """The same program on 2 ranks sharing the GPU: GPU chores, remote tiles
+    over the IPC device plane. `superseded`: a remote GPU writer's version of a
+    tile lands in device memory, a slow local CPU reader reads it, and the
+    writer's NEXT version lands before that reader ran -- the reader still sees
+    the first version (pulled to the host from its own, superseded copy)."""
+    rc, outs = launch.launch(2, [progs("dtd_gpu_capi")], timeout=120, capture=True, env={"PARSEC_COMM_GPU": "0"})
+    text = "".join(o for o, _ in outs)
+    assert rc == 0, text + "".join(e for _, e in outs)
+    assert "FAILED" not in text and text.count("errors 0") == 2, text
+    assert text.count("superseded: ok") == 2, text
 
 
 @pytest.mark.gpu

@@ -52,20 +52,35 @@ def _run(case, nranks, *args, timeout=100, env_extra=None):
     return outs
 
 
+# The IPC pull routes. "auto" on this 1-GPU box: every peer shares the GPU, so
+# pulls are copy kernels spread over 2 streams. "copy-engine": the exact route a
+# peer on ANOTHER GPU takes (comm_ipc_copy_mode 2 picks it for distinct GPUs):
+# hipMemcpyAsync on the GPU's one shared copy stream.
+ROUTES = {
+    "auto": {},
+    "copy-engine": {"PARSEC_MCA_comm_ipc_copy_mode": "0", "PARSEC_MCA_comm_ipc_streams": "1"},
+}
+
+
+@pytest.mark.parametrize("route", list(ROUTES))
 @pytest.mark.parametrize("nranks,P,Q", [(2, 2, 1), (4, 2, 2), (8, 4, 2)])
-def test_dpotrf_multirank_ipc(pa, nranks, P, Q):
+def test_dpotrf_multirank_ipc(pa, nranks, P, Q, route):
     """N=8192, nb=512 Cholesky over P x Q ranks (the 8-rank grid is the one
-    bench.py uses on 8 GPUs), every rank checking its tiles of L."""
+    bench.py uses on 8 GPUs), every rank checking its tiles of L, through both
+    IPC pull routes."""
     _gpu()
-    outs = _run("dpotrf", nranks, 8192, 512, P, Q, env_extra={"EXPECT_PLANE": "ipc"})
+    outs = _run("dpotrf", nranks, 8192, 512, P, Q, env_extra={"EXPECT_PLANE": "ipc", **ROUTES[route]})
     # every rank's warnings in the message: the rank whose IPC start-up failed
     # names its own error code
     notes = "\n".join(f"[{r}] {l}" for r, (_, o) in enumerate(outs) for l in o.splitlines() if "warning" in l or "error" in l.lower() or "status" in l)
     for rc, out in outs:
         assert rc == 0, out + "\n" + notes
-    # the remote tiles really moved GPU to GPU through the engine's IPC route
-    gets = [int(o.strip().splitlines()[-1].split(" gets ipc ")[-1].split()[0]) for _, o in outs]
-    assert sum(gets) > 0, gets
+    # the remote tiles really moved GPU to GPU through the engine's IPC route,
+    # none through host fragments
+    last = [o.strip().splitlines()[-1] for _, o in outs]
+    gets = [int(l.split(" gets ipc ")[-1].split()[0]) for l in last]
+    frags = [int(l.split(" fragments ")[-1].split()[0]) for l in last]
+    assert sum(gets) > 0 and sum(frags) == 0, last
 
 
 def test_dpotrf_host_plane_request(pa):
@@ -116,14 +131,15 @@ def test_dgeqrf_hqr_2x2_ipc(pa):
     assert np.linalg.norm(R.T @ R - AtA) / np.linalg.norm(AtA) < 1e-12
 
 
-def test_stencil_four_ranks_ipc(pa):
+@pytest.mark.parametrize("route", list(ROUTES))
+def test_stencil_four_ranks_ipc(pa, route):
     """DTD 3D stencil over 4 ranks with GPU bodies: halo faces cross ranks
     through the device plane and STAY on the device: the receiving rank's
     shadow version is a device copy (csrc/dtd/dtd.cpp shadow_copy_new), so the
     runtime copies zero bytes device -> host and writes nothing back to host
     during the sweeps, while faces did arrive through IPC gets."""
     _gpu()
-    for rc, out in _run("stencil", 4, 48, 40, 36, 16, 6):
+    for rc, out in _run("stencil", 4, 48, 40, 36, 16, 6, env_extra=ROUTES[route]):
         assert rc == 0, out
         line = next(l for l in out.splitlines() if " halo d2h " in l)
         f = line.split()
@@ -133,7 +149,8 @@ def test_stencil_four_ranks_ipc(pa):
         print(line)
 
 
-def test_comm_engine_c_program_gpu_memory(tmp_path, pa):
+@pytest.mark.parametrize("route", list(ROUTES))
+def test_comm_engine_c_program_gpu_memory(tmp_path, pa, route):
     """CE get / put between GPU buffers of two processes (both on GPU 0): the
     registrations export the allocations through HIP IPC and every transfer is
     one device copy on the copy stream (ports dtd_test_ce.c to device memory)."""
@@ -149,28 +166,34 @@ def test_comm_engine_c_program_gpu_memory(tmp_path, pa):
            f"-Wl,-rpath,{root}/parsec_amd/lib", "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
-    rc, outs = launch.launch(2, [exe, "gpu"], timeout=120, capture=True, env={"PARSEC_COMM_GPU": "0"})
+    rc, outs = launch.launch(2, [exe, "gpu"], timeout=120, capture=True, env={"PARSEC_COMM_GPU": "0", **ROUTES[route]})
     assert rc == 0, outs
     text = "".join(o for o, _ in outs)
     assert text.count("ce ok") == 2 and "[1] GET ok" in text and "[1] PUT ok" in text, text
     assert "[1] MIXED GET ok" in text and "[1] MIXED PUT ok" in text, text
 
 
-def test_headline_tile_size_8_ranks_shared_gpu(pa):
+@pytest.mark.parametrize("route", list(ROUTES))
+def test_headline_tile_size_8_ranks_shared_gpu(pa, route):
     """The headline tile size (nb=1024) on the 8-rank P4xQ2 grid bench.py uses on
     8 GPUs, N=16384, all ranks on the box's one GPU: bench.py's distributed
-    backward-error probe (every rank's tiles, two all-reduces) must pass."""
+    backward-error probe (every rank's tiles, two all-reduces) must pass, and
+    its JSON line carries every rank's transfers by route (bench.py exits
+    non-zero if any payload took the host-fragment route)."""
     _gpu()
     import json
 
-    port = 29600 + os.getpid() % 300
+    port = 29600 + (os.getpid() + (7 if route != "auto" else 0)) % 300
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr", "127.0.0.1",
            "--master-port", str(port), os.path.join(os.path.dirname(HERE), "bench.py"), "--gpus", "8", "--size", "16384", "--nb", "1024",
            "--steps", "1", "--warmup", "0", "--share-gpu", "--cores", "1"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, start_new_session=True)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, start_new_session=True, env=dict(os.environ, **ROUTES[route]))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
     print(line[:200])
     assert out["n_gpus"] == 8 and out["config"]["parallelism"].startswith("2D block-cyclic P4xQ2")
     assert out["residual"] < 1e-12
+    comm = out["comm"]
+    assert len(comm) == 8 and all(c["get_fragments"] == 0 for c in comm), comm
+    assert sum(c["get_ipc"] for c in comm) > 0 and sum(c["bytes_pulled_ipc"] for c in comm) > 0, comm
