@@ -957,9 +957,24 @@ static TiledMatrix* tm_of(const parsec_tiled_matrix_t* t) {
 }
 parsec_taskpool_t* parsec_apply_New(parsec_matrix_uplo_t uplo, parsec_tiled_matrix_t* A, parsec_tiled_matrix_unary_op_t operation, void* op_args) {
   const parsec_tiled_matrix_t* cA = A;
-  return algos::apply_new(tm_of(A), (int)uplo, [cA, operation](TiledMatrix*, int64_t m, int64_t n, void* tile, void* arg) {
+  auto* tp = algos::apply_new(tm_of(A), (int)uplo, [cA, operation](TiledMatrix*, int64_t m, int64_t n, void* tile, void* arg) {
     operation(my_execution_stream(), cA, tile, PARSEC_MATRIX_FULL, (int)m, (int)n, arg);
   }, op_args);
+  // the taskpool owns op_args (malloc'ed by the caller) and frees it when it is
+  // destroyed (reference parsec_apply_Destruct, apply_wrapper.c:111-121)
+  if (op_args) {
+    auto prev = tp->destructor_hook;
+    tp->destructor_hook = [op_args, prev] {
+      if (prev) prev();
+      std::free(op_args);
+    };
+  }
+  return tp;
+}
+parsec_taskpool_t* parsec_dpotrf_New(parsec_matrix_uplo_t uplo, parsec_tiled_matrix_t* A, int* info) {
+  if (uplo != PARSEC_MATRIX_LOWER) fatal("parsec_dpotrf_New: only PARSEC_MATRIX_LOWER is implemented");
+  if (A->mtype != PARSEC_MATRIX_DOUBLE) fatal("parsec_dpotrf_New: the matrix must hold doubles");
+  return algos::dpotrf_jdf_new(tm_of(A), info);
 }
 int parsec_apply(parsec_context_t* parsec, parsec_matrix_uplo_t uplo, parsec_tiled_matrix_t* A, parsec_tiled_matrix_unary_op_t operation, void* op_args) {
   parsec_taskpool_t* tp = parsec_apply_New(uplo, A, operation, op_args);

@@ -133,6 +133,21 @@ struct Datatype {
 };
 
 class DatacopyFuture;
+// Version counter of a copy: read by threads that only inspect coherency while
+// the owner of a write bumps it (reshape views, write-backs, stage-in), so every
+// access is a relaxed atomic; ordering comes from the data locks and the DAG.
+struct CopyVersion {
+  std::atomic<uint32_t> v{0};
+  operator uint32_t() const { return v.load(std::memory_order_relaxed); }
+  CopyVersion& operator=(uint32_t x) {
+    v.store(x, std::memory_order_relaxed);
+    return *this;
+  }
+  CopyVersion& operator=(const CopyVersion& o) { return *this = (uint32_t)o; }
+  uint32_t operator++() { return v.fetch_add(1, std::memory_order_relaxed) + 1; }
+  uint32_t operator+=(uint32_t d) { return v.fetch_add(d, std::memory_order_relaxed) + d; }
+};
+
 struct DataCopy : ListItem {  // ListItem: membership in a device LRU
   std::atomic<int32_t> refcount{1};
   Data* original = nullptr;
@@ -142,7 +157,7 @@ struct DataCopy : ListItem {  // ListItem: membership in a device LRU
   uint8_t coherency_state = COHERENCY_INVALID;
   uint8_t transfer_status = TRANSFER_NOT;
   std::atomic<int32_t> readers{0};
-  uint32_t version = 0;
+  CopyVersion version;
   void* device_private = nullptr;  // pointer to the bytes on device_index
   Arena* arena = nullptr;          // set when allocated from an arena
   Datatype dtt;
@@ -391,6 +406,9 @@ struct Taskpool {
   std::atomic<int64_t> nb_tasks{0};
   std::atomic<int64_t> nb_pending_actions{0};
   std::atomic<int> termdet_state{TERMDET_NOT_READY};
+  // local / user-trigger detectors: both counters and the state in one word, so
+  // the update that completes termination is also the decision (termdet.cpp)
+  std::atomic<uint64_t> termdet_word{0};
   void* termdet_private = nullptr;
   std::function<int(Taskpool*)> on_complete;
   std::function<int(Taskpool*)> on_enqueue;

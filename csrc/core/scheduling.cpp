@@ -218,7 +218,7 @@ int execute_task(ExecutionStream* es, Task* t) {
           for (auto& f : tc->flows) {
             if (!(f.access & FLOW_WRITE)) continue;
             DataCopy* c = t->data[f.index].data_in;
-            if (c && c->has_reshape_view.load(std::memory_order_acquire)) __atomic_add_fetch(&c->version, 1, __ATOMIC_ACQ_REL);
+            if (c && c->has_reshape_view.load(std::memory_order_acquire)) ++c->version;
           }
         }
       }

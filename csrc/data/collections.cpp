@@ -150,7 +150,7 @@ int TiledMatrix::data_read(const std::string& filename) {
     // the loaded copy becomes the only valid version
     std::lock_guard<SpinLock> g(d->lock);
     uint32_t newest = 0;
-    for (int i = 0; i < kMaxDevices; ++i) if (DataCopy* o = d->copy(i)) newest = std::max(newest, o->version);
+    for (int i = 0; i < kMaxDevices; ++i) if (DataCopy* o = d->copy(i)) newest = std::max<uint32_t>(newest, o->version);
     for (int i = 0; i < kMaxDevices; ++i) if (DataCopy* o = d->copy(i); o && o != home) o->coherency_state = COHERENCY_INVALID;
     home->version = newest + 1;
     home->coherency_state = COHERENCY_OWNED;

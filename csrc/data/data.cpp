@@ -126,7 +126,7 @@ uint32_t Data::newest_version() const {
   uint32_t v = 0;
   for (int i = 0; i < kMaxDevices; ++i) {
     DataCopy* c = copy(i);
-    if (c && c->coherency_state != COHERENCY_INVALID) v = std::max(v, c->version);
+    if (c && c->coherency_state != COHERENCY_INVALID) v = std::max<uint32_t>(v, c->version);
   }
   return v;
 }
@@ -270,9 +270,9 @@ void data_end_transfer_ownership_to_copy(Data* d, int device, uint8_t access) {
   uint32_t newest = 0;
   for (int i = 0; i < kMaxDevices; ++i) {
     DataCopy* c = d->copy(i);
-    if (c && c != local && c->coherency_state != COHERENCY_INVALID) newest = std::max(newest, c->version);
+    if (c && c != local && c->coherency_state != COHERENCY_INVALID) newest = std::max<uint32_t>(newest, c->version);
   }
-  local->version = std::max(local->version, newest);
+  local->version = std::max<uint32_t>(local->version, newest);
   local->transfer_status = TRANSFER_COMPLETE;
   if (access & FLOW_WRITE) {
     local->coherency_state = COHERENCY_OWNED;

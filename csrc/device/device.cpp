@@ -255,7 +255,7 @@ void cpu_stage_in(ExecutionStream* es, Task* t) {
       // host copy present: is it current?
       std::lock_guard<SpinLock> g(d->lock);
       uint32_t newest = 0;
-      for (int i = 1; i < kMaxDevices; ++i) { DataCopy* o = d->copy(i); if (o && o->coherency_state != COHERENCY_INVALID) newest = std::max(newest, o->version); }
+      for (int i = 1; i < kMaxDevices; ++i) { DataCopy* o = d->copy(i); if (o && o->coherency_state != COHERENCY_INVALID) newest = std::max<uint32_t>(newest, o->version); }
       needs = newest > c->version && (f.access & FLOW_READ);
     }
     if (!needs) continue;
@@ -276,7 +276,7 @@ void cpu_write_epilog(Task* t) {
     Data* d = c->original;
     std::lock_guard<SpinLock> g(d->lock);
     uint32_t v = 0;
-    for (int i = 0; i < kMaxDevices; ++i) { DataCopy* o = d->copy(i); if (o && o->coherency_state != COHERENCY_INVALID) v = std::max(v, o->version); }
+    for (int i = 0; i < kMaxDevices; ++i) { DataCopy* o = d->copy(i); if (o && o->coherency_state != COHERENCY_INVALID) v = std::max<uint32_t>(v, o->version); }
     c->version = v + 1;
     c->coherency_state = COHERENCY_OWNED;
     d->owner_device = 0;

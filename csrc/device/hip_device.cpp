@@ -1160,7 +1160,7 @@ void HipDevice::epilog(GpuTask* g) {
     if (g->access[fi] & FLOW_WRITE) {
       std::lock_guard<SpinLock> lk(d->lock);
       uint32_t v = 0;
-      for (int i = 0; i < kMaxDevices; ++i) { DataCopy* o = d->copy(i); if (o && o->coherency_state != COHERENCY_INVALID) v = std::max(v, o->version); }
+      for (int i = 0; i < kMaxDevices; ++i) { DataCopy* o = d->copy(i); if (o && o->coherency_state != COHERENCY_INVALID) v = std::max<uint32_t>(v, o->version); }
       local->version = v + 1;
       local->coherency_state = COHERENCY_OWNED;
       d->owner_device = (int8_t)device_index;

@@ -631,7 +631,6 @@ DataCopy* PtgTaskClass::remote_reshape(const Taskpool* tp, const int32_t* PL, co
 // jdf2c output-to-collection reshape) moves only the elements of the layout:
 // the flow's copy is read through X and written into the tile through Y (Y
 // defaults to X); host copies, equal packed sizes. Untyped: the whole tile.
-static int g_trace_writeback = -1;
 static bool typed_write_back(const Taskpool* tp, const DepTarget* tg, DataCopy* dst, const DataCopy* src) {
   if (!tp || !tg || dst->device_index != 0 || src->device_index != 0) return false;
   const auto& adts = tp->arenas_datatypes;
@@ -651,7 +650,7 @@ static bool typed_write_back(const Taskpool* tp, const DepTarget* tg, DataCopy* 
   return true;
 }
 static void write_back(Data* home, DataCopy* src, const Taskpool* tp = nullptr, const DepTarget* tg = nullptr) {
-  if (g_trace_writeback < 0) g_trace_writeback = (int)ParamRegistry::instance().reg_int("ptg", "", "trace_writeback", "Log every final write of a flow into a collection tile (debug)", 0);
+  static const int g_trace_writeback = (int)ParamRegistry::instance().reg_int("ptg", "", "trace_writeback", "Log every final write of a flow into a collection tile (debug)", 0);
   if (g_trace_writeback)
     std::fprintf(stderr, "[writeback] home key %llu owner_dev %d src %p dev %d orig==home %d home copies:%s%s\n", (unsigned long long)(home ? home->key : 0),
                  home ? home->owner_device : -9, src ? src->device_private : nullptr, src ? src->device_index : -9, (int)(home && src && src->original == home),

@@ -22,21 +22,54 @@ static void fire(Taskpool* tp) {
   if (c && c->cb) c->cb(tp);
 }
 
-// ------------------------------------------------------------------- local
-class LocalTermdet : public TermdetModule {
+// Packed termination word (Taskpool::termdet_word) of the local and
+// user-trigger detectors: nb_tasks and nb_pending_actions as biased 30-bit
+// fields plus the state bits, so the update that completes termination and the
+// termination decision are ONE atomic operation. A thread whose update does not
+// terminate the taskpool never touches it again -- it may be freed the moment
+// another thread fires. (The previous separate counters were re-read after the
+// decrement; ThreadSanitizer caught a comm thread reading a taskpool the main
+// thread had already freed, round 5.) nb_tasks / nb_pending_actions stay
+// updated for readers, BEFORE the packed update.
+namespace {
+constexpr uint64_t kField = 30;
+constexpr uint64_t kMask = (1ull << kField) - 1;
+constexpr uint64_t kBias = 1ull << (kField - 1);
+constexpr uint64_t kTasksShift = 0, kActionsShift = kField;
+constexpr uint64_t kReady = 1ull << 60, kTriggered = 1ull << 61, kDone = 1ull << 62;
+constexpr uint64_t kZero = (kBias << kTasksShift) | (kBias << kActionsShift);
+
+inline uint64_t fresh_word() { return kZero; }
+inline int64_t field(uint64_t w, uint64_t shift) { return (int64_t)((w >> shift) & kMask) - (int64_t)kBias; }
+inline uint64_t delta(int64_t d, uint64_t shift) { return (uint64_t)d << shift; }  // two's complement: a borrow stays in the biased field
+
+// Terminated by this update? `need_tasks`: the tasks field counts (local);
+// user-trigger needs the trigger bit instead.
+inline bool finished(uint64_t w, bool need_tasks) {
+  if ((w & kDone) || !(w & kReady)) return false;
+  if (need_tasks ? field(w, kTasksShift) != 0 : !(w & kTriggered)) return false;
+  return field(w, kActionsShift) == 0;
+}
+
+// The unique thread whose update produced a finished word claims it.
+inline bool claim(Taskpool* tp, uint64_t w) {
+  return tp->termdet_word.compare_exchange_strong(w, w | kDone, std::memory_order_acq_rel);
+}
+
+void monitor(Taskpool* tp, std::function<void(Taskpool*)> cb) {
+  tp->nb_tasks.store(0);
+  tp->nb_pending_actions.store(0);
+  tp->termdet_state.store(TERMDET_NOT_READY);
+  tp->termdet_word.store(fresh_word());
+  delete static_cast<TermdetCallback*>(tp->termdet_private);  // re-monitoring replaces the callback
+  tp->termdet_private = new TermdetCallback{std::move(cb)};
+}
+
+class PackedTermdet : public TermdetModule {
  public:
-  const char* name() const override { return "local"; }
-  void monitor_taskpool(Taskpool* tp, std::function<void(Taskpool*)> cb) override {
-    tp->nb_tasks.store(0);
-    tp->nb_pending_actions.store(0);
-    tp->termdet_state.store(TERMDET_NOT_READY);
-    delete static_cast<TermdetCallback*>(tp->termdet_private);
-    tp->termdet_private = new TermdetCallback{std::move(cb)};
-  }
-  void unmonitor_taskpool(Taskpool* tp) override {
-    // keep the callback object alive until the taskpool dies; it is tiny.
-    (void)tp;
-  }
+  explicit PackedTermdet(bool count_tasks) : count_tasks_(count_tasks) {}
+  void monitor_taskpool(Taskpool* tp, std::function<void(Taskpool*)> cb) override { monitor(tp, std::move(cb)); }
+  void unmonitor_taskpool(Taskpool* tp) override { (void)tp; }  // the callback object lives until release
   void release_taskpool(Taskpool* tp) override {
     delete static_cast<TermdetCallback*>(tp->termdet_private);
     tp->termdet_private = nullptr;
@@ -44,86 +77,76 @@ class LocalTermdet : public TermdetModule {
   void taskpool_ready(Taskpool* tp) override {
     int exp = TERMDET_NOT_READY;
     tp->termdet_state.compare_exchange_strong(exp, TERMDET_BUSY);
-    check(tp);
+    settle(tp, tp->termdet_word.fetch_or(kReady, std::memory_order_acq_rel) | kReady);
   }
-  void taskpool_set_nb_tasks(Taskpool* tp, int64_t v) override { tp->nb_tasks.store(v, std::memory_order_seq_cst); check(tp); }
+  void taskpool_set_nb_tasks(Taskpool* tp, int64_t v) override {
+    tp->nb_tasks.store(v, std::memory_order_seq_cst);
+    settle(tp, set_field(tp, kTasksShift, v));
+  }
   int64_t taskpool_addto_nb_tasks(Taskpool* tp, int64_t d) override {
-    int64_t v = tp->nb_tasks.fetch_add(d, std::memory_order_seq_cst) + d;
-    if (v == 0) check(tp);
+    const int64_t v = tp->nb_tasks.fetch_add(d, std::memory_order_seq_cst) + d;
+    settle(tp, tp->termdet_word.fetch_add(delta(d, kTasksShift), std::memory_order_acq_rel) + delta(d, kTasksShift));
     return v;
   }
-  void taskpool_set_runtime_actions(Taskpool* tp, int64_t v) override { tp->nb_pending_actions.store(v, std::memory_order_seq_cst); check(tp); }
+  void taskpool_set_runtime_actions(Taskpool* tp, int64_t v) override {
+    tp->nb_pending_actions.store(v, std::memory_order_seq_cst);
+    settle(tp, set_field(tp, kActionsShift, v));
+  }
   int64_t taskpool_addto_runtime_actions(Taskpool* tp, int64_t d) override {
-    int64_t v = tp->nb_pending_actions.fetch_add(d, std::memory_order_seq_cst) + d;
-    if (v == 0) check(tp);
+    const int64_t v = tp->nb_pending_actions.fetch_add(d, std::memory_order_seq_cst) + d;
+    settle(tp, tp->termdet_word.fetch_add(delta(d, kActionsShift), std::memory_order_acq_rel) + delta(d, kActionsShift));
     return v;
   }
- private:
-  void check(Taskpool* tp) {
-    if (tp->termdet_state.load(std::memory_order_seq_cst) != TERMDET_BUSY) return;
-    if (tp->nb_tasks.load(std::memory_order_seq_cst) != 0 || tp->nb_pending_actions.load(std::memory_order_seq_cst) != 0) return;
-    int exp = TERMDET_BUSY;
-    if (tp->termdet_state.compare_exchange_strong(exp, TERMDET_TERMINATED)) fire(tp);
+
+ protected:
+  // w: the word this thread's update produced; tp is touched again only when
+  // that update finished the taskpool (then this thread is the only one left)
+  void settle(Taskpool* tp, uint64_t w) {
+    if (!finished(w, count_tasks_) || !claim(tp, w)) return;
+    tp->termdet_state.store(TERMDET_TERMINATED, std::memory_order_seq_cst);
+    fire(tp);
   }
+  static uint64_t set_field(Taskpool* tp, uint64_t shift, int64_t v) {
+    uint64_t w = tp->termdet_word.load(std::memory_order_acquire), n;
+    do {
+      n = (w & ~(kMask << shift)) | ((((uint64_t)(v + (int64_t)kBias)) & kMask) << shift);
+    } while (!tp->termdet_word.compare_exchange_weak(w, n, std::memory_order_acq_rel));
+    return n;
+  }
+  bool count_tasks_;
+};
+}  // namespace
+
+// ------------------------------------------------------------------- local
+// CAS state machine NOT_READY -> BUSY -> TERMINATED once nb_tasks and
+// nb_pending_actions reach zero (reference termdet_local_module.c:110-193).
+class LocalTermdet : public PackedTermdet {
+ public:
+  LocalTermdet() : PackedTermdet(true) {}
+  const char* name() const override { return "local"; }
 };
 
 // ------------------------------------------------------------ user_trigger
 // Termination is declared by the application (one task calls
 // parsec_termdet_user_trigger); in distributed runs the declaration is
 // broadcast to every rank. Pending runtime actions still delay termination.
-class UserTriggerTermdet : public TermdetModule {
+class UserTriggerTermdet : public PackedTermdet {
  public:
+  UserTriggerTermdet() : PackedTermdet(false) {}
   const char* name() const override { return "user_trigger"; }
-  void monitor_taskpool(Taskpool* tp, std::function<void(Taskpool*)> cb) override {
-    tp->nb_tasks.store(0);
-    tp->nb_pending_actions.store(0);
-    tp->termdet_state.store(TERMDET_NOT_READY);
-    delete static_cast<TermdetCallback*>(tp->termdet_private);  // re-monitoring replaces the callback
-    tp->termdet_private = new TermdetCallback{std::move(cb)};
-    std::lock_guard<std::mutex> g(m_);
-    triggered_.erase(tp);
-  }
-  void release_taskpool(Taskpool* tp) override {
-    delete static_cast<TermdetCallback*>(tp->termdet_private);
-    tp->termdet_private = nullptr;
-    std::lock_guard<std::mutex> g(m_);
-    triggered_.erase(tp);
-  }
-  void taskpool_ready(Taskpool* tp) override {
-    int exp = TERMDET_NOT_READY;
-    tp->termdet_state.compare_exchange_strong(exp, TERMDET_BUSY);
-    check(tp);
-  }
-  void taskpool_set_nb_tasks(Taskpool* tp, int64_t v) override { tp->nb_tasks.store(v); }
-  int64_t taskpool_addto_nb_tasks(Taskpool* tp, int64_t d) override { return tp->nb_tasks.fetch_add(d) + d; }
-  void taskpool_set_runtime_actions(Taskpool* tp, int64_t v) override { tp->nb_pending_actions.store(v); check(tp); }
-  int64_t taskpool_addto_runtime_actions(Taskpool* tp, int64_t d) override {
-    int64_t v = tp->nb_pending_actions.fetch_add(d) + d;
-    if (v == 0) check(tp);
-    return v;
-  }
   void user_trigger(Taskpool* tp) override {
-    bool first;
-    {
-      std::lock_guard<std::mutex> g(m_);
-      first = triggered_.insert(tp).second;
-    }
-    if (!first) return;
-    if (tp->context && tp->context->nb_nodes > 1) termdet_user_trigger_broadcast(tp);
-    check(tp);
+    const uint64_t prev = tp->termdet_word.load(std::memory_order_acquire);
+    if (prev & kTriggered) return;
+    // the broadcast precedes the local trigger: tp stays alive until it is set
+    if (tp->context && tp->context->nb_nodes > 1 && !(tp->termdet_word.fetch_or(kBroadcast, std::memory_order_acq_rel) & kBroadcast))
+      termdet_user_trigger_broadcast(tp);
+    const uint64_t w = tp->termdet_word.fetch_or(kTriggered, std::memory_order_acq_rel);
+    if (w & kTriggered) return;
+    settle(tp, w | kTriggered);
   }
+
  private:
-  void check(Taskpool* tp) {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      if (!triggered_.count(tp)) return;
-    }
-    if (tp->termdet_state.load() != TERMDET_BUSY || tp->nb_pending_actions.load() != 0) return;
-    int exp = TERMDET_BUSY;
-    if (tp->termdet_state.compare_exchange_strong(exp, TERMDET_TERMINATED)) fire(tp);
-  }
-  std::mutex m_;
-  std::set<Taskpool*> triggered_;
+  static constexpr uint64_t kBroadcast = 1ull << 63;
 };
 
 TermdetModule* termdet_open_module(const std::string& name) {

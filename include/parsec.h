@@ -428,8 +428,14 @@ int parsec_tiled_matrix_data_read(parsec_tiled_matrix_t* tdesc, const char* file
 typedef int (*parsec_operator_t)(parsec_execution_stream_t* es, const void* src, void* dst, void* op_data, ...);
 typedef int (*parsec_tiled_matrix_unary_op_t)(parsec_execution_stream_t* es, const parsec_tiled_matrix_t* desc1, void* data1, int uplo, int m, int n,
                                               void* args);
-/* operation(es, A, tile, PARSEC_MATRIX_FULL, m, n, op_args) on every tile of the uplo part */
+/* operation(es, A, tile, PARSEC_MATRIX_FULL, m, n, op_args) on every tile of the uplo part;
+ * the taskpool takes ownership of op_args (malloc'ed, freed with the taskpool, or NULL) */
 parsec_taskpool_t* parsec_apply_New(parsec_matrix_uplo_t uplo, parsec_tiled_matrix_t* A, parsec_tiled_matrix_unary_op_t operation, void* op_args);
+/* Tiled Cholesky A = L L^T of a double matrix (PARSEC_MATRIX_LOWER only), the
+ * ptgpp-compiled dpotrf_L.jdf taskpool of the BASELINE configs (DPLASMA's
+ * dplasma_dpotrf_New role): HIP bodies on GPUs, CPU bodies otherwise. *info
+ * holds the LAPACK info once the taskpool completed (0: success). */
+parsec_taskpool_t* parsec_dpotrf_New(parsec_matrix_uplo_t uplo, parsec_tiled_matrix_t* A, int* info);
 int parsec_apply(parsec_context_t* parsec, parsec_matrix_uplo_t uplo, parsec_tiled_matrix_t* A, parsec_tiled_matrix_unary_op_t operation, void* op_args);
 /* op(es, src_tile, dest_tile, op_data, m, n) for every tile of dest */
 parsec_taskpool_t* parsec_map_operator_New(const parsec_tiled_matrix_t* src, parsec_tiled_matrix_t* dest, parsec_operator_t op, void* op_data);

@@ -228,7 +228,7 @@ def generate_sanitized(kind):
         "  deps = gcc",
         "  description = CXX[" + kind + "] $out",
         "rule cc",
-        f"  command = gcc -std=c99 -O1 -g -fno-omit-frame-pointer -fsanitize={kind} -I{ROOT}/include -c $in -o $out",
+        f"  command = gcc -std=c99 -D_DEFAULT_SOURCE -O1 -g -fno-omit-frame-pointer -fsanitize={kind} -I{ROOT}/include -c $in -o $out",
         "  description = CC[" + kind + "] $out",
         "rule solink",
         "  command = g++ -shared -o $out $in $libs",
@@ -263,11 +263,15 @@ def generate_sanitized(kind):
         lines.append(f"build {obj}: cxx {os.path.join(ROOT, src)}")
         lines.append(f"build {exe}: exelink {obj} | {lib}")
         lines.append(f"  libs = -L{out} -lparsec_amd -Wl,-rpath,{out} {libs}")
-    capi = "tests/capi/dtd_capi.c"
-    if os.path.exists(os.path.join(ROOT, capi)):
-        lines.append(f"build {os.path.join(out, 'obj', 'dtd_capi.o')}: cc {os.path.join(ROOT, capi)}")
-        lines.append(f"build {os.path.join(out, 'dtd_capi')}: exelink {os.path.join(out, 'obj', 'dtd_capi.o')} | {lib}")
-        lines.append(f"  libs = -L{out} -lparsec_amd -Wl,-rpath,{out} {libs}")
+    # C API programs run instrumented: the DTD program and the distributed PTG
+    # Cholesky (ptgpp-compiled dpotrf_L.jdf, CPU bodies on 1..4 ranks)
+    for capi in ("tests/capi/dtd_capi.c", "tests/capi/dpotrf_capi.c"):
+        if not os.path.exists(os.path.join(ROOT, capi)):
+            continue
+        name = os.path.splitext(os.path.basename(capi))[0]
+        lines.append(f"build {os.path.join(out, 'obj', name + '.o')}: cc {os.path.join(ROOT, capi)}")
+        lines.append(f"build {os.path.join(out, name)}: exelink {os.path.join(out, 'obj', name + '.o')} | {lib}")
+        lines.append(f"  libs = -L{out} -lparsec_amd -Wl,-rpath,{out} {libs} -lm")
     with open(os.path.join(out, "build.ninja"), "w") as f:
         f.write("\n".join(lines) + "\n")
     return out

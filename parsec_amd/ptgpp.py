@@ -54,9 +54,16 @@ def _has_hip_body(jdf):
     return "type=HIP" in src.replace(" ", "")
 
 
-def compile_flags(hip=False):
+def compile_flags(hip=False, sanitize=None):
+    """sanitize: "thread" / "address": instrumented host code linked against the
+    sanitized runtime of build-<kind>/ (parsec_amd._build.build_sanitized)."""
     inc = [f"-I{ROOT}/include", f"-I{ROOT}/csrc", f"-I{ROCM}/include", "-D__HIP_PLATFORM_AMD__"]
-    libs = [f"-L{PKG}/lib", "-lparsec_amd", f"-Wl,-rpath,{PKG}/lib", f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib", "-lpthread"]
+    lib = os.path.join(ROOT, "build-" + sanitize) if sanitize else os.path.join(PKG, "lib")
+    libs = [f"-L{lib}", "-lparsec_amd", f"-Wl,-rpath,{lib}", f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib", "-lpthread"]
+    if sanitize:
+        if hip:
+            raise CompileError("sanitized builds are host-only (no HIP bodies)")
+        return ["g++", "-std=c++20", "-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={sanitize}"] + inc, [f"-fsanitize={sanitize}"] + libs
     if hip:
         return [f"{ROCM}/bin/hipcc", "-std=c++20", "-O2", f"--offload-arch={ARCH}"] + inc, libs
     return ["g++", "-std=c++20", "-O2"] + inc, libs
@@ -66,12 +73,13 @@ def compile_flags(hip=False):
 C_BODIES = ("-fpermissive", "-Drestrict=__restrict__", "-w")
 
 
-def build_program(jdf, outdir, extra_sources=(), hip=None, name=None, flags=(), cxxflags=()):
+def build_program(jdf, outdir, extra_sources=(), hip=None, name=None, flags=(), cxxflags=(), sanitize=None):
     """cxxflags: extra compiler flags, e.g. C_BODIES for JDFs whose C code
-    relies on C rules (implicit void * conversions, `restrict`)."""
+    relies on C rules (implicit void * conversions, `restrict`); sanitize: see
+    compile_flags."""
     cpp, _ = compile_jdf(jdf, outdir, name, flags=flags)
-    hip = _has_hip_body(jdf) if hip is None else hip
-    cc, libs = compile_flags(hip)
+    hip = (_has_hip_body(jdf) if hip is None else hip) and not sanitize
+    cc, libs = compile_flags(hip, sanitize)
     exe = os.path.splitext(cpp)[0]
     cmd = cc + list(cxxflags) + [f"-I{outdir}", f"-I{os.path.dirname(os.path.abspath(jdf))}", cpp] + list(extra_sources) + ["-o", exe] + libs
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -66,7 +66,9 @@ int main(int argc, char** argv) {
   init_bc(&T, rank, nodes, 4, 7, 30, 30);
 
   /* apply: A(i, j) = 100 i + j */
-  parsec_apply(ctx, PARSEC_MATRIX_FULL, &A.super, set_pos, &scale);
+  double* scale_arg = (double*)malloc(sizeof(double)); /* owned (freed) by the apply taskpool */
+  *scale_arg = scale;
+  parsec_apply(ctx, PARSEC_MATRIX_FULL, &A.super, set_pos, scale_arg);
   /* map: B = -A */
   parsec_taskpool_t* tp = parsec_map_operator_New(&A.super, &B.super, negate, NULL);
   parsec_context_add_taskpool(ctx, tp);

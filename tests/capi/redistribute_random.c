@@ -14,6 +14,11 @@
 #include "parsec.h"
 
 static double value_of(int i, int j) { return 1000.0 * i + j + 0.5; }
+static int* int_arg(int v) {
+  int* p = (int*)malloc(sizeof(int));
+  *p = v;
+  return p;
+}
 
 /* op_args: 1 -> every element = value_of(global row, global col); 0 -> zero */
 static int init_ops(parsec_execution_stream_t* es, const parsec_tiled_matrix_t* d, void* data, int uplo, int m, int n, void* args) {
@@ -67,15 +72,15 @@ int main(int argc, char** argv) {
     parsec_matrix_tabular_set_random_table(&Y, 2873);
     parsec_matrix_tabular_init(&T, PARSEC_MATRIX_DOUBLE, nodes, rank, MBR, NBR, MR, NR, 0, 0, MR, NR, NULL);
     parsec_matrix_tabular_set_random_table(&T, 3872);
-    int one = 1, zero = 0;
-    parsec_apply(parsec, PARSEC_MATRIX_FULL, &Y.super, init_ops, &one);
-    parsec_apply(parsec, PARSEC_MATRIX_FULL, &T.super, init_ops, &zero);
+    /* parsec_apply owns (frees) its op_args, as in the reference */
+    parsec_apply(parsec, PARSEC_MATRIX_FULL, &Y.super, init_ops, int_arg(1));
+    parsec_apply(parsec, PARSEC_MATRIX_FULL, &T.super, init_ops, int_arg(0));
     int rc = variant == 0 ? parsec_redistribute(parsec, &Y.super, &T.super, rows, cols, diY, djY, diT, djT)
                           : parsec_redistribute_dtd(parsec, &Y.super, &T.super, rows, cols, diY, djY, diT, djT);
     if (rc != 0) { fprintf(stderr, "redistribute rc %d\n", rc); bad++; }
     const int b1 = check_window(&T.super, diT, djT, rows, cols, diY, djY, 0.0);
     /* back into a zeroed Y */
-    parsec_apply(parsec, PARSEC_MATRIX_FULL, &Y.super, init_ops, &zero);
+    parsec_apply(parsec, PARSEC_MATRIX_FULL, &Y.super, init_ops, int_arg(0));
     rc = variant == 0 ? parsec_redistribute(parsec, &T.super, &Y.super, rows, cols, diT, djT, diY, djY)
                       : parsec_redistribute_dtd(parsec, &T.super, &Y.super, rows, cols, diT, djT, diY, djY);
     if (rc != 0) bad++;

@@ -3,7 +3,9 @@ PARSEC_DEBUG_MEM_LEAK, PARSEC_DEBUG_MEM_RACE, CMakeLists.txt:195-200,320-360):
 `python -m parsec_amd._build --sanitize KIND` rebuilds the host code with
 -fsanitize=KIND into build-KIND/, and these tests run the lock-free container
 test and the C99 DTD program (1..4 processes over the shared-memory engine)
-under ThreadSanitizer and AddressSanitizer + LeakSanitizer. Races these runs
+under ThreadSanitizer and AddressSanitizer + LeakSanitizer, plus (round 5)
+the distributed PTG Cholesky with CPU bodies on 1 / 2 / 4 ranks, the
+reference's dtd_test_multiple_handle_wait.c and its reshape family. Races these runs
 found and that are fixed: unlocked emptiness checks of the dequeue / sorted
 queue / max-heap / VP queues (now atomic counts), termination detection set
 up after the taskpool was published to the comm thread, remote DTD shadows
@@ -16,7 +18,10 @@ import subprocess
 
 import pytest
 
-from parsec_amd import _build, launch
+from parsec_amd import _build, launch, ptgpp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
 
 pytestmark = pytest.mark.skipif(subprocess.run(["which", "ninja"], capture_output=True).returncode != 0, reason="ninja missing")
 
@@ -56,3 +61,88 @@ def test_dtd_program_sanitized(sanitized, nranks):
     assert rc == 0, errs[first:first + 6000] if first >= 0 else errs[-4000:]
     assert "Sanitizer" not in errs
     assert sum("ok" in o for o, _ in outs) == nranks
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 4])
+def test_dpotrf_program_sanitized(sanitized, nranks):
+    """The distributed PTG Cholesky (ptgpp-compiled dpotrf_L.jdf through
+    parsec_dpotrf_New, CPU bodies) on 1 / 2 / 4 ranks: the PTG engine, the
+    remote-dependency send / receive / deliver path and the priority fetch
+    queue, instrumented."""
+    kind, out = sanitized
+    old = dict(os.environ)
+    os.environ.update(_env(kind))
+    os.environ["PARSEC_MCA_device_hip_enabled"] = "0"
+    try:
+        rc, outs = launch.launch(nranks, [os.path.join(out, "dpotrf_capi"), "512", "64"], timeout=600, capture=True)
+    finally:
+        os.environ.clear()
+        os.environ.update(old)
+    errs = "\n".join(e for _, e in outs)
+    first = errs.find("WARNING: ")
+    assert rc == 0, errs[first:first + 6000] if first >= 0 else errs[-4000:]
+    assert "Sanitizer" not in errs
+    assert sum(" ok" in o for o, _ in outs) == nranks, [o for o, _ in outs]
+
+
+def _run_sanitized(kind, exe, args=(), timeout=300):
+    env = _env(kind)
+    env["PARSEC_MCA_device_hip_enabled"] = "0"
+    r = subprocess.run([exe, *args], capture_output=True, text=True, timeout=timeout, env=env)
+    first = r.stderr.find("WARNING: ")
+    assert r.returncode == 0, r.stdout[-2000:] + (r.stderr[first:first + 6000] if first >= 0 else r.stderr[-4000:])
+    assert "Sanitizer" not in r.stderr
+    return r
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+def test_reference_multiple_handle_wait_sanitized(sanitized, tmp_path):
+    """The reference's dtd_test_multiple_handle_wait.c (unmodified), which found
+    round 4's two use-after-frees under a manual ASan run, now in the suite."""
+    kind, _ = sanitized
+    cc, libs = ptgpp.compile_flags(False, kind)
+    exe = str(tmp_path / "mhw")
+    r = subprocess.run(cc + list(ptgpp.C_BODIES) + [f"-I{REF}/tests", f"-I{REF}", f"-I{REF}/tests/dsl/dtd", "-x", "c++",
+                                                    os.path.join(REF, "tests/dsl/dtd/dtd_test_multiple_handle_wait.c"),
+                                                    os.path.join(REF, "tests/tests_data.c"), "-o", exe] + libs, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for _ in range(3):
+        _run_sanitized(kind, exe)
+
+
+_RS = "tests/collections/reshape/"
+RESHAPE = [
+    ("avoidable_reshape.jdf", ["testing_avoidable_reshape.c", "common.c"], 1),
+    ("input_dep_single_copy_reshape.jdf", ["testing_input_dep_reshape_single_copy.c", "common.c"], 1),
+    ("remote_multiple_outs_same_pred_flow.jdf", ["remote_multiple_outs_same_pred_flow_multiple_deps.jdf", "testing_remote_multiple_outs_same_pred_flow.c", "common.c"], 2),
+    ("local_no_reshape.jdf", [j + ".jdf" for j in ("local_read_reshape", "local_output_reshape", "local_input_reshape", "local_input_LU_LL",
+                                                   "remote_read_reshape", "remote_no_re_reshape")] + ["testing_reshape.c", "common.c"], 7),
+]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("jdf,srcs,npass", RESHAPE, ids=[r[0] for r in RESHAPE])
+def test_reference_reshape_sanitized(sanitized, tmp_path, jdf, srcs, npass):
+    """The reference's reshape family (JDFs + drivers unmodified, as in
+    tests/test_ptgpp.py) against the instrumented runtime: reshape futures,
+    shared reshaped copies, typed write-backs."""
+    kind, _ = sanitized
+    if kind == "thread" and jdf == "input_dep_single_copy_reshape.jdf":
+        # its BODY spins on a plain global (`do {} while (set == 0)`,
+        # input_dep_single_copy_reshape.jdf:64-73): a race in the program itself
+        pytest.skip("the reference program's body races on its own global by design")
+    if kind == "thread" and jdf == "local_no_reshape.jdf":
+        # this driver also runs remote_no_re_reshape.jdf, whose TASK_A(m, k)
+        # writes descA(m, k) from READ_A(k, m)'s data while READ_A(m, k) may
+        # still read descA(m, k): the DAG orders neither (lines 30-48), a race in
+        # the test program that ThreadSanitizer reports in the runtime's copy
+        # code (an early-termination probe over 30 runs found the runtime's
+        # taskpool boundaries intact); AddressSanitizer runs it
+        pytest.skip("remote_no_re_reshape.jdf leaves a read and a write of one tile unordered")
+    d = os.path.join(REF, _RS)
+    extra = [ptgpp.compile_jdf(os.path.join(d, x), str(tmp_path), None)[0] if x.endswith(".jdf") else os.path.join(d, x) for x in srcs]
+    exe = ptgpp.build_program(os.path.join(d, jdf), str(tmp_path), extra_sources=extra, sanitize=kind,
+                              cxxflags=ptgpp.C_BODIES + (f"-I{d}", f"-I{REF}/tests", f"-I{REF}"))
+    r = _run_sanitized(kind, exe)
+    out = r.stdout + r.stderr
+    assert out.count(" PASSED") == npass and "FAILED" not in out, out[-2000:]
