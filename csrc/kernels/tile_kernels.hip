@@ -146,52 +146,21 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // phases before their LDS store) for the one-workgroup-per-CU regime of the
 // DPOTRF bulk streams, where one k-tile of MFMA work per wave does not cover an
 // HBM miss.
-template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF = 2, int OCC = WM * WN / 2, int PF = 1>
-__global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OCC))) void dgemm_batch_kernel(const GemmBatchArgs args) {
+// EPI = 1: the epilogue adds alpha * acc into C with no-return f64 atomics
+// performed at the memory side (beta == 1 for every descriptor of the launch):
+// the accumulators start from zero (no C preload), nothing of C is read by the
+// waves, and the wave does not wait for the update -- C traffic leaves the MFMA
+// timeline of the workgroup. Each element gets one add per tile (or per K chunk
+// of a split tile), so the result does not depend on timing.
+template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF, int PF, int EPI>
+__device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, int ks, int nsplit, double (&As)[NBUF][BK][BM + (((BM % 32) == 16) ? 0 : 16)],
+                                          double (&Bs)[NBUF][BK][BN + (((BN % 32) == 16) ? 0 : 16)]) {
   static_assert(PF == 1 || NBUF == 2, "two tiles in flight need the double-buffered LDS");
   constexpr int NT = WM * WN * 64;
   constexpr int WTM = BM / WM;
   constexpr int WTN = BN / WN;
   constexpr int FM = WTM / 16;
   constexpr int FN = WTN / 16;
-  constexpr int PADM = ((BM % 32) == 16) ? 0 : 16;
-  constexpr int PADN = ((BN % 32) == 16) ? 0 : 16;
-  constexpr int LDA_S = BM + PADM;
-  constexpr int LDB_S = BN + PADN;
-  __shared__ double As[NBUF][BK][LDA_S];
-  __shared__ double Bs[NBUF][BK][LDB_S];
-  PARSEC_WAVE_PRIO(args.prio);
-
-  // Workgroups [0, main_tiles) own whole tiles (XCD-aware order); the ones
-  // dispatched last split the K range of the tail tiles (wave quantisation:
-  // a 606-tile launch on 512 slots would otherwise run a 94-tile second round)
-  int tile, ks = 0, nsplit = 1;
-  if (args.stagger > 0) {
-    const int S = args.stagger, total = args.total_tiles;
-    const int p = xcd_remap(blockIdx.x, total + S);
-    if (p < 2 * S) {
-      if (p & 1) {
-        tile = S + (p >> 1);
-      } else {
-        tile = p >> 1;
-        nsplit = 2;
-      }
-    } else if (p < total) {
-      tile = p;
-    } else {
-      tile = p - total;
-      nsplit = 2;
-      ks = 1;
-    }
-  } else if ((int)blockIdx.x < args.main_tiles) {
-    tile = xcd_remap(blockIdx.x, args.main_tiles);
-  } else {
-    const int u = blockIdx.x - args.main_tiles;
-    nsplit = args.ksplit;
-    tile = args.main_tiles + u / nsplit;
-    ks = u % nsplit;
-  }
-  if (tile >= args.total_tiles) return;
   const int di = find_desc(args, args.tile_start, tile);
   const GemmDesc& d = args.d[di];
   const int local = tile - args.tile_start[di];
@@ -348,7 +317,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
   // and the epilogue is a pure store (no read-modify-write tail when a batch's
   // workgroups all finish together).
   const bool split = nsplit > 1;
-  const bool preload = FULL && !split && (d.alpha == 1.0 || d.alpha == -1.0);
+  const bool preload = EPI == 0 && FULL && !split && (d.alpha == 1.0 || d.alpha == -1.0);
   double* __restrict__ C = d.C;
   const int ldc = d.ldc;
   // beta's operand: C itself or a separate input (Cin)
@@ -412,7 +381,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
         if ((FULL || (gm < M && gn < N)) && (!d.lower_only || gm >= gn)) {
           double* p = C + (size_t)gn * ldc + gm;
           double v = alpha * acc[i][j][r];
-          if (split) {
+          if (split || EPI == 1) {
             unsafeAtomicAdd(p, v);  // no-return global f64 add, performed at the memory side
             continue;
           }
@@ -423,6 +392,66 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
       }
     }
   crit_release(args.claim);
+}
+
+template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF = 2, int OCC = WM * WN / 2, int PF = 1, int EPI = 0>
+__global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OCC))) void dgemm_batch_kernel(const GemmBatchArgs args) {
+  constexpr int PADM = ((BM % 32) == 16) ? 0 : 16;
+  constexpr int PADN = ((BN % 32) == 16) ? 0 : 16;
+  __shared__ double As[NBUF][BK][BM + PADM];
+  __shared__ double Bs[NBUF][BK][BN + PADN];
+  PARSEC_WAVE_PRIO(args.prio);
+  // Workgroups [0, main_tiles) own whole tiles (XCD-aware order); the ones
+  // dispatched last split the K range of the tail tiles (wave quantisation:
+  // a 606-tile launch on 512 slots would otherwise run a 94-tile second round)
+  int tile, ks = 0, nsplit = 1;
+  if (args.stagger > 0) {
+    const int S = args.stagger, total = args.total_tiles;
+    const int p = xcd_remap(blockIdx.x, total + S);
+    if (p < 2 * S) {
+      if (p & 1) {
+        tile = S + (p >> 1);
+      } else {
+        tile = p >> 1;
+        nsplit = 2;
+      }
+    } else if (p < total) {
+      tile = p;
+    } else {
+      tile = p - total;
+      nsplit = 2;
+      ks = 1;
+    }
+  } else if ((int)blockIdx.x < args.main_tiles) {
+    tile = xcd_remap(blockIdx.x, args.main_tiles);
+  } else {
+    const int u = blockIdx.x - args.main_tiles;
+    nsplit = args.ksplit;
+    tile = args.main_tiles + u / nsplit;
+    ks = u % nsplit;
+  }
+  if (tile >= args.total_tiles) return;
+  gemm_tile<BM, BN, BK, WM, WN, TRANSA, TRANSB, FULL, NBUF, PF, EPI>(args, tile, ks, nsplit, As, Bs);
+}
+
+// Persistent form: a grid of (at most) one round of resident workgroups walks
+// the launch's tiles, workgroup b taking every G-th tile of its XCD's
+// contiguous range, so a workgroup's next tile starts without a new dispatch
+// and, with the atomic epilogue, without waiting for its C update to land.
+template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF = 2, int OCC = WM * WN / 2, int PF = 1, int EPI = 0>
+__global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OCC))) void dgemm_persist_kernel(const GemmBatchArgs args) {
+  constexpr int PADM = ((BM % 32) == 16) ? 0 : 16;
+  constexpr int PADN = ((BN % 32) == 16) ? 0 : 16;
+  __shared__ double As[NBUF][BK][BM + PADM];
+  __shared__ double Bs[NBUF][BK][BN + PADN];
+  PARSEC_WAVE_PRIO(args.prio);
+  const int G = gridDim.x, b = blockIdx.x, T = args.total_tiles;
+  const int x = b % 8, nx = G / 8 + (x < G % 8 ? 1 : 0), i = b / 8;  // workgroups b = x, x + 8, ... share XCD x
+  const int t0 = (int)((long long)T * x / 8), t1 = (int)((long long)T * (x + 1) / 8);
+  for (int tile = t0 + i; tile < t1; tile += nx) {
+    gemm_tile<BM, BN, BK, WM, WN, TRANSA, TRANSB, FULL, NBUF, PF, EPI>(args, tile, 0, 1, As, Bs);
+    __syncthreads();  // the LDS tiles are reused by the next tile's prologue
+  }
 }
 
 // ========================================================= diag blocks (4 waves)
@@ -800,6 +829,23 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
     }
   }
   const int mode = (descs[0].transA ? 2 : 0) | (descs[0].transB ? 1 : 0);
+  // atomic epilogue: every descriptor accumulates into C (beta 1, no separate
+  // Cin / C2). PARSEC_GEMM_EPI = 1 always, 0 never, -1 (default) when every
+  // descriptor has K >= 1024: 40 x 1024^3 61.6 -> 63.9 TF, 16 x 1024^3 57.9 ->
+  // 58.9 TF, but 32 x 512^3 51.3 -> 47.5 TF (half the flops per memory-side
+  // add) -- profiles/r5_gemm_epilogue.txt. Persistent grid (PARSEC_GEMM_PERSIST=1,
+  // off: -5..-8 % with one workgroup per CU): one round of resident workgroups
+  // walks the tiles (no split-K tail, no stagger).
+  static const int epi_env = getenv("PARSEC_GEMM_EPI") ? atoi(getenv("PARSEC_GEMM_EPI")) : -1;
+  static const int persist_env = getenv("PARSEC_GEMM_PERSIST") ? atoi(getenv("PARSEC_GEMM_PERSIST")) : 0;
+  bool epi = epi_env != 0 && full;
+  for (int i = 0; epi && i < n; ++i) epi = descs[i].beta == 1.0 && !descs[i].Cin && !descs[i].C2 && (epi_env > 0 || descs[i].k >= 1024);
+  const bool persist = persist_env != 0 && full && BM == 128 && a.stagger == 0 && total > slots;
+  if (persist) {
+    a.main_tiles = total;
+    a.ksplit = 1;
+    grid_size = slots;
+  }
   const dim3 grid(grid_size), block(WM * WN * 64);
   const size_t pad = BM == 128 ? (size_t)t_launch_pad : 0;
   if (pad) {
@@ -809,10 +855,16 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
       std::fprintf(stderr, "[gemm] bulk 128x128 launch with %zu extra LDS bytes (one workgroup per CU)\n", pad);
     }
   }
-#define PARSEC_GEMM_LAUNCH(TA, TB)                                                                                    \
-  do {                                                                                                                \
-    if (full) hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, OCC, PF>), grid, block, pad, stream, a); \
-    else hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, false, NBUF, OCC, PF>), grid, block, pad, stream, a);    \
+#define PARSEC_GEMM_LAUNCH_E(TA, TB, E)                                                                                                      \
+  do {                                                                                                                                      \
+    if (persist) hipLaunchKernelGGL((dgemm_persist_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, OCC, PF, E>), grid, block, pad, stream, a);  \
+    else if (full) hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, OCC, PF, E>), grid, block, pad, stream, a);  \
+    else hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, false, NBUF, OCC, PF, 0>), grid, block, pad, stream, a);          \
+  } while (0)
+#define PARSEC_GEMM_LAUNCH(TA, TB)               \
+  do {                                            \
+    if (epi) PARSEC_GEMM_LAUNCH_E(TA, TB, 1);     \
+    else PARSEC_GEMM_LAUNCH_E(TA, TB, 0);         \
   } while (0)
   switch (mode) {
     case 0: PARSEC_GEMM_LAUNCH(false, false); break;
@@ -821,6 +873,7 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
     default: PARSEC_GEMM_LAUNCH(true, true); break;
   }
 #undef PARSEC_GEMM_LAUNCH
+#undef PARSEC_GEMM_LAUNCH_E
 }
 
 static void gemm_policy_init() {
