@@ -173,6 +173,12 @@ struct DataCopy : ListItem {  // ListItem: membership in a device LRU
   // task writes them in place, so a later reshaped read gets a fresh view
   std::atomic<bool> has_reshape_view{false};
   bool snapshot_from_zone = false;  // DTD send snapshot carved from a device tile-cache zone
+  // early release (HIP engine): the copy is read or written by a kernel group
+  // on execution stream pending_stream whose completion event is pending_event
+  // (hipEvent_t) and whose tasks were already released; users on other streams,
+  // the copy stream or a CPU wait for it (hip_device.cpp early_release_group)
+  std::atomic<void*> pending_event{nullptr};
+  int8_t pending_stream = -1;
   void* ptr() const { return device_private; }
 };
 
@@ -526,6 +532,7 @@ struct DeviceStats {
   std::atomic<uint64_t> data_faults{0};
   std::atomic<uint64_t> kernel_launches{0}, batched_tasks{0};
   std::atomic<uint64_t> w2r_tasks{0}, prefetches{0};
+  std::atomic<uint64_t> early_released{0};  // HIP: tasks completed at launch (device_hip_early_release)
   // GPU manager thread: time (ns) spent retiring completed kernel groups
   // (epilog + dependency release) and the longest single retirement pass
   std::atomic<uint64_t> ns_complete{0}, ns_complete_max{0}, ns_launch{0};

@@ -248,6 +248,9 @@ void cpu_stage_in(ExecutionStream* es, Task* t) {
     if (f.access == FLOW_CTL || f.access == FLOW_NONE) continue;
     TaskDataRef& r = t->data[f.index];
     DataCopy* c = r.data_in;
+    // an early-released GPU group may still be writing (or reading) this copy
+    if (c)
+      if (void* ev = c->pending_event.load(std::memory_order_acquire)) (void)hipEventSynchronize((hipEvent_t)ev);
     if (!c || !c->original) continue;
     Data* d = c->original;
     bool needs = c->device_index != 0;

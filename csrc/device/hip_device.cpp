@@ -313,6 +313,14 @@ int HipDevice::detach(Context* c) {
 
 void HipDevice::start(Context* c) {
   ctx = c;
+  {
+    // routing knobs a later context of the process may change (the device
+    // registry, and this engine, outlive a context)
+    auto& params = ParamRegistry::instance();
+    early_release = (int)params.reg_int("device", "hip", "early_release", "Critical-stream groups release their tasks' successors when launched (1) or when their kernels completed (0); single-process runs", early_release);
+    hp_route = (int)params.reg_int("device", "hip", "hp_on_critical_stream", "High-priority tasks below the critical threshold share the critical stream (1), go to the least loaded bulk stream (0), or get stream 1 to themselves (2, bulk on streams 2..)", hp_route);
+    critical_split = params.reg_int("device", "hip", "critical_split", "Critical-path tasks leave the critical stream as a group of their own", critical_split ? 1 : 0) != 0;
+  }
   if (manager.joinable()) return;
   PARSEC_HIP_CHECK(hipSetDevice(ordinal));
   int lo = 0, hi = 0;
@@ -449,9 +457,8 @@ void HipDevice::trace_group(int s, const ExecGroup& g) {
   }
   if ((size_t)s >= trace_streams.size()) trace_streams.resize(s + 1, nullptr);
   if (!trace_streams[s]) trace_streams[s] = profiling_stream_create(name + " stream " + std::to_string(s));
-  struct { int32_t ntasks, stream; uint32_t tc; int32_t l0; } info{(int32_t)g.tasks.size(), s, g.tasks.empty() ? 0u : g.tasks[0]->task->task_class->task_class_id,
-                                                                   g.tasks.empty() ? 0 : g.tasks[0]->task->locals[0]};
-  const uint32_t tp = g.tasks.empty() ? 0 : g.tasks[0]->task->taskpool->taskpool_id;
+  struct { int32_t ntasks, stream; uint32_t tc; int32_t l0; } info{(int32_t)g.tasks.size(), s, g.trace_tc, g.trace_l0};
+  const uint32_t tp = g.trace_tp;
   const uint64_t id = (uint64_t)(uintptr_t)g.ev;
   profiling_trace_at(trace_streams[s], trace_key_b, id, tp, trace_ref_ns + (uint64_t)((double)b * 1e6), &info, sizeof(info));
   profiling_trace_at(trace_streams[s], trace_key_e, id, tp, trace_ref_ns + (uint64_t)((double)e * 1e6), nullptr, 0);
@@ -1008,6 +1015,7 @@ static size_t batch_tiles(const KernelBatch& b) {
 // ------------------------------------------------------------- execution
 void HipDevice::execute_ready() {
   if (ready.empty()) return;
+  pending_seen.clear();
   std::stable_sort(ready.begin(), ready.end(), [](GpuTask* a, GpuTask* b) { return a->task->priority > b->task->priority; });
   std::vector<GpuTask*> again;
   for (GpuTask* g : ready) {
@@ -1062,6 +1070,10 @@ void HipDevice::execute_ready() {
       }
       if (s < 0) { again.push_back(g); continue; }
       if (round_tasks[s].empty()) ++rr_stream;
+    }
+    if (early_release > 0 && copies_pending(g, s)) {  // an input is still in use by an early-released group on another stream
+      again.push_back(g);
+      continue;
     }
     GpuExecContext ctxg;
     ctxg.dev = this;
@@ -1147,8 +1159,100 @@ void HipDevice::launch_group(int s) {
   PARSEC_HIP_CHECK(hipEventRecord(grp.ev, s_exec[s]));
   grp.tasks.swap(round_tasks[s]);
   grp.t_launch = now_ns();
+  if (!grp.tasks.empty() && grp.tasks[0]->task) {
+    Task* t0 = grp.tasks[0]->task;
+    grp.trace_tc = t0->task_class->task_class_id;
+    grp.trace_l0 = t0->locals[0];
+    grp.trace_tp = t0->taskpool ? t0->taskpool->taskpool_id : 0;
+  }
   stats.batched_tasks.fetch_add(grp.tasks.size(), std::memory_order_relaxed);
   executing[s].push_back(std::move(grp));
+  if (early_release > 0 && s == 0 && ctx && ctx->nb_nodes <= 1) early_release_group(executing[s].back(), s);
+}
+
+// Early release (device_hip_early_release): the tasks of a critical-stream group
+// are completed as soon as the group is queued. Their successors become ready
+// while the kernels run: the ones routed to the critical stream are launched
+// behind them in stream order (the chain POTRF -> TRSM -> SYRK -> POTRF no
+// longer pays a completion poll + dispatch + launch per hop); the others wait in
+// execute_ready until the group's event fired (copies_pending), a CPU reader
+// waits in cpu_stage_in, and the taskpool holds one runtime action per task
+// until its kernels retired (a factorization never terminates before them).
+// Every copy the group reads or writes carries the group's event meanwhile.
+// Single-process runs only: remote sends of a released output would not wait.
+void HipDevice::early_release_group(ExecGroup& grp, int s) {
+  for (GpuTask* g : grp.tasks) {
+    Task* t = g->task;
+    if (!t || g->kind != GPU_TASK_KERNEL || g->pushout || !t->taskpool || t->taskpool->is_dtd) continue;
+    if (early_release == 1 && t->priority < critical_threshold) continue;  // 1: critical-path tasks only; 2: every task of the stream
+    const Chore& ch = t->task_class->chores[g->chore];
+    if (ch.stage_in || ch.stage_out) continue;
+    for (int fi = 0; fi < kMaxFlows; ++fi) {
+      DataCopy* c = g->dev_copy[fi];
+      if (!c) continue;
+      c->pending_stream = (int8_t)s;
+      c->pending_event.store((void*)grp.ev, std::memory_order_release);
+    }
+    // the written copies become the newest versions now (epilog without unpinning)
+    for (int fi = 0; fi < kMaxFlows; ++fi) {
+      DataCopy* local = g->dev_copy[fi];
+      if (!local || !(g->access[fi] & FLOW_WRITE)) continue;
+      Data* d = local->original;
+      std::lock_guard<SpinLock> lk(d->lock);
+      uint32_t v = 0;
+      for (int i = 0; i < kMaxDevices; ++i) { DataCopy* o = d->copy(i); if (o && o->coherency_state != COHERENCY_INVALID) v = std::max<uint32_t>(v, o->version); }
+      local->version = v + 1;
+      local->coherency_state = COHERENCY_OWNED;
+      d->owner_device = (int8_t)device_index;
+      if (t->data[fi].data_out != local) {
+        if (t->data[fi].data_out && t->data[fi].data_out != t->data[fi].data_in) data_copy_release(t->data[fi].data_out);
+        data_copy_retain(local);
+        t->data[fi].data_out = local;
+      }
+    }
+    g->early = true;
+    g->hold_tp = t->taskpool;
+    g->hold_tp->tdm->taskpool_addto_runtime_actions(g->hold_tp, 1);
+    t->gpu = nullptr;
+    g->task = nullptr;
+    stats.early_released.fetch_add(1, std::memory_order_relaxed);
+    complete_task_execution(es, t);
+  }
+}
+
+// The kernels of an early-released task retired: unpin its copies.
+void HipDevice::late_complete(GpuTask* g, hipEvent_t ev) {
+  for (int fi = 0; fi < kMaxFlows; ++fi) {
+    DataCopy* c = g->dev_copy[fi];
+    if (!c) continue;
+    void* exp = (void*)ev;
+    c->pending_event.compare_exchange_strong(exp, nullptr, std::memory_order_acq_rel);
+    c->readers.fetch_sub(1);
+    lru_touch(c);
+  }
+  load.fetch_sub((int64_t)g->load, std::memory_order_relaxed);
+  stats.executed_tasks.fetch_add(1, std::memory_order_relaxed);
+  Taskpool* tp = g->hold_tp;
+  delete g;
+  inflight.fetch_sub(1, std::memory_order_acq_rel);
+  tp->tdm->taskpool_addto_runtime_actions(tp, -1);
+}
+
+bool HipDevice::copies_pending(GpuTask* g, int stream) {
+  for (int fi = 0; fi < kMaxFlows; ++fi) {
+    DataCopy* c = g->dev_copy[fi];
+    if (!c) continue;
+    void* ev = c->pending_event.load(std::memory_order_acquire);
+    if (!ev || c->pending_stream == stream) continue;  // same stream: ordered behind it
+    // one query per event and round (a panel releases many bulk tasks at once)
+    auto it = std::find_if(pending_seen.begin(), pending_seen.end(), [&](const std::pair<void*, bool>& e) { return e.first == ev; });
+    if (it == pending_seen.end()) {
+      pending_seen.emplace_back(ev, hipEventQuery((hipEvent_t)ev) == hipErrorNotReady);
+      it = pending_seen.end() - 1;
+    }
+    if (it->second) return true;
+  }
+  return false;
 }
 
 void HipDevice::epilog(GpuTask* g) {
@@ -1252,12 +1356,16 @@ bool HipDevice::progress() {
         timing_pool.push_back(grp.ts_begin);
         timing_pool.push_back(grp.ts_end);
       }
-      put_event(grp.ev);
+      const hipEvent_t grp_ev = grp.ev;
       std::vector<GpuTask*> tasks;
       tasks.swap(grp.tasks);
       q.pop_front();
       const uint64_t tr0 = trace_launches ? now_ns() : 0;
       for (GpuTask* g : tasks) {
+        if (g->early) {
+          late_complete(g, grp_ev);
+          continue;
+        }
         epilog(g);
         const Chore& gch = g->task->task_class->chores[g->chore];
         if (gch.stage_in || gch.stage_out)  // custom layouts go home through the chore, right after the task
@@ -1297,6 +1405,7 @@ bool HipDevice::progress() {
           complete(g);
         }
       }
+      put_event(grp_ev);  // after late_complete cleared the copies that named it
       if (trace_launches)
         std::fprintf(stderr, "[engine] t=%llu R stream %d n=%zu release_us=%llu\n", (unsigned long long)(tr0 / 1000), s, tasks.size(),
                      (unsigned long long)((now_ns() - tr0) / 1000));
@@ -1403,6 +1512,7 @@ void hip_devices_init(Context* ctx) {
   const int ccap = (int)params.reg_int("device", "hip", "critical_bulk_cap", "Launched kernel groups per bulk stream while the critical stream has work in flight (0 = max_inflight_batches)", 0);
   const int cuy = (int)params.reg_int("device", "hip", "cu_yield", "Cooperative CU yield: critical-path kernels claim their CUs and bulk GEMM workgroups on a claimed CU pause until it is free (0 off, 1 tile-POTRF steps claim, 2 every kernel of a critical group claims)", 0);
   const bool csplit = params.reg_int("device", "hip", "critical_split", "Critical-path tasks leave the critical stream as a group of their own and their successors are dispatched before other completions are released", 0) != 0;
+  const int early = (int)params.reg_int("device", "hip", "early_release", "Critical-stream groups release their tasks' successors when launched (1) or when their kernels completed (0); single-process runs", 0);
   if (enabled == 0) return;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) { (void)hipGetLastError(); return; }
@@ -1435,6 +1545,7 @@ void hip_devices_init(Context* ctx) {
     d->max_inflight_explicit = params.source(ParamRegistry::join("device", "hip", "max_inflight_batches")) != "default";
     d->critical_bulk_cap = ccap;
     d->critical_split = csplit;
+    d->early_release = early;
     d->cu_yield = cuy;
     kern::set_cu_yield_mode(cuy);
     d->sort_pending = sortp != 0;

@@ -64,6 +64,10 @@ struct GpuTask {
   int stream = -1;
   double load = 0;
   uint64_t t_submit = 0, t_exec = 0;
+  // early release: the task was completed (successors released) when its group
+  // was launched; the group's retirement only unpins its copies
+  bool early = false;
+  Taskpool* hold_tp = nullptr;  // runtime action held until the kernels retired
 };
 
 struct DevCopyState {  // DataCopy::dev_state for engine-managed copies
@@ -98,6 +102,9 @@ struct ExecGroup {
   uint64_t t_launch = 0;
   // profiling: timing events around the group's kernels (GPU-side span)
   hipEvent_t ts_begin = nullptr, ts_end = nullptr;
+  // first task's identity, kept for the trace (its task may be released early)
+  uint32_t trace_tc = 0, trace_tp = 0;
+  int32_t trace_l0 = 0;
 };
 
 struct HipDevice : Device {
@@ -190,6 +197,13 @@ struct HipDevice : Device {
   bool max_inflight_explicit = false;  // set by the user: taskpool hints do not override it
   int critical_bulk_cap = 0;    // the same limit while the critical stream has work in flight (0 = max_inflight_groups)
   bool critical_split = false;
+  // device_hip_early_release: groups of the critical stream complete their
+  // tasks (release successors) when launched, not when their event fires
+  int early_release = 0;
+  void early_release_group(ExecGroup& grp, int s);
+  void late_complete(GpuTask* g, hipEvent_t ev);
+  bool copies_pending(GpuTask* g, int stream);  // an input still written / read by a stream-0 group in flight
+  std::vector<std::pair<void*, bool>> pending_seen;  // events queried this round (still running?)
   int cu_yield = 0;  // critical tasks leave stream 0 as their own group; their release goes first
   double us_busy = 0;
 

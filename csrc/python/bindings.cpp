@@ -626,6 +626,7 @@ PYBIND11_MODULE(_C, m) {
       e["ms_complete_max"] = d->stats.ns_complete_max.load() / 1e6;
       e["ms_launch"] = d->stats.ns_launch.load() / 1e6;
       e["kernel_launches"] = d->stats.kernel_launches.load();
+      e["early_released"] = d->stats.early_released.load();
       e["batched_tasks"] = d->stats.batched_tasks.load();
       e["bytes_in"] = d->stats.bytes_in.load();
       e["bytes_out"] = d->stats.bytes_out.load();

@@ -187,3 +187,41 @@ def test_trsm_inverse_modes_gpu(pa, nb):
         assert torch.linalg.norm(La - Lb).item() < 1e-3 * d02
     for La, Lb in ((L1s, L2), (L1ds, L2)):  # auto above it = the substitution path
         assert torch.linalg.norm(La - Lb).item() < 1e-3 * d02
+
+
+@pytest.mark.parametrize("hp_route", [1, 2])
+@pytest.mark.parametrize("N,nb", [(4096, 256), (4096, 512)])
+def test_dpotrf_early_release(pa, N, nb, hp_route):
+    """device_hip_early_release=1: critical-stream groups release their tasks'
+    successors when launched (the chain POTRF -> TRSM -> SYRK -> POTRF queues
+    in stream order; successors on other streams wait for the group's event);
+    hp_route 2 puts the non-critical high-priority tasks on their own stream.
+    The factor matches and tasks were released early."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    pa.mca_set("device_hip_early_release", "1")
+    pa.mca_set("device_hip_hp_on_critical_stream", str(hp_route))
+    ctx = pa.init(3)
+    try:
+        gpu = pa.first_gpu_device_index()
+        NT = N // nb
+        store = torch.empty((NT, NT, nb, nb), dtype=torch.float64, device="cuda")
+        A = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb, nb, N, N, device=gpu, ptr=store.data_ptr())
+        S = _spd(N, "cuda", 5)
+        for rep in range(2):
+            store.copy_(S.reshape(NT, nb, NT, nb).permute(2, 0, 3, 1))
+            torch.cuda.synchronize()
+            tp, info = pa.dpotrf_jdf_new(A)
+            ctx.add_taskpool(tp)
+            ctx.start()
+            ctx.wait()
+            assert pa.read_int(info) == 0
+            torch.cuda.synchronize()
+            L = torch.tril(store.permute(1, 3, 0, 2).reshape(N, N))
+            assert (torch.linalg.norm(L @ L.t() - S) / torch.linalg.norm(S)).item() < 1e-13, rep
+        gpus = [d for d in pa.devices() if d["type"] == pa.DEV_HIP]
+        assert gpus[0]["early_released"] >= 2 * NT, gpus[0]
+    finally:
+        ctx.fini()
+        pa.mca_set("device_hip_early_release", "0")
+        pa.mca_set("device_hip_hp_on_critical_stream", "1")
