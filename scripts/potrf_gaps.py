@@ -11,8 +11,8 @@ rows = list(csv.DictReader(open(path)))
 per = nb // 64 + 1
 NT = (N + nb - 1) // nb
 ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows if "dpotrf_step_kernel" in r["Kernel_Name"])
-pk = ks[-(NT - 1) * per - 1:]  # the last POTRF (k = NT - 1) has no W: nb/64 + 1 launches too
-groups = [pk[i:i + per] for i in range(0, len(pk) - per + 1, per)]
+pk = ks[-NT * per:]  # every tile POTRF is nb/64 + 1 step launches (the last one too)
+groups = [pk[i:i + per] for i in range(0, len(pk), per)]
 print(f"{len(groups)} tile POTRFs x {per} step kernels (last factorization)")
 print(f"{'k':>3} {'span':>8} {'run':>8} {'gaps':>8} {'max_gap':>8}")
 ts = tr = 0.0
