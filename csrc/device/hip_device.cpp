@@ -320,6 +320,7 @@ void HipDevice::start(Context* c) {
     early_release = (int)params.reg_int("device", "hip", "early_release", "Critical-stream groups release their tasks' successors when launched (1) or when their kernels completed (0); single-process runs", early_release);
     hp_route = (int)params.reg_int("device", "hip", "hp_on_critical_stream", "High-priority tasks below the critical threshold share the critical stream (1), go to the least loaded bulk stream (0), or get stream 1 to themselves (2, bulk on streams 2..)", hp_route);
     critical_split = params.reg_int("device", "hip", "critical_split", "Critical-path tasks leave the critical stream as a group of their own", critical_split ? 1 : 0) != 0;
+    sort_pending = (int)params.reg_int("device", "hip", "sort_pending_tasks", "Order of the pending GPU tasks: 0 arrival, 1 priority, 2 data already on the device first, then priority", sort_pending);
   }
   if (manager.joinable()) return;
   PARSEC_HIP_CHECK(hipSetDevice(ordinal));
@@ -990,6 +991,22 @@ int HipDevice::stage_in(GpuTask* g) {
   return 1;
 }
 
+// Flows of a pending task whose newest version is not on this device yet
+// (each would need a transfer before the task can run).
+int HipDevice::missing_on_device(GpuTask* g) const {
+  const Task* t = g->task;
+  int n = 0;
+  for (auto& f : t->task_class->flows) {
+    if (f.access == FLOW_CTL || f.access == FLOW_NONE) continue;
+    const DataCopy* c = t->data[f.index].data_in;
+    if (!c || !c->original) continue;
+    const Data* d = c->original;
+    const DataCopy* local = d->copy(device_index);
+    if (!local || local->coherency_state == COHERENCY_INVALID || local->version < d->newest_version()) ++n;
+  }
+  return n;
+}
+
 void HipDevice::finish_stage_in(GpuTask* g) {
   for (int fi = 0; fi < kMaxFlows; ++fi) {
     if (!g->issued_copy[fi]) continue;
@@ -1312,8 +1329,20 @@ bool HipDevice::progress() {
   if ((!prefetch_jobs.empty() || !prefetch_requests.empty()) && progress_prefetch()) did = true;
   // stage in
   if (!pending.empty()) {
-    if (sort_pending && pending.size() > 1)
+    if (sort_pending == 2 && pending.size() > 1) {
+      // reference parsec_gpu_sort_pending_list (device_gpu.c): tasks whose data
+      // is already on this device first, so a task that can run now is not
+      // queued behind one waiting for transfers; priority among equals
+      std::vector<std::pair<int, GpuTask*>> keyed;
+      keyed.reserve(pending.size());
+      for (GpuTask* g : pending) keyed.emplace_back(missing_on_device(g), g);
+      std::stable_sort(keyed.begin(), keyed.end(), [](const auto& a, const auto& b) {
+        return a.first != b.first ? a.first < b.first : a.second->task->priority > b.second->task->priority;
+      });
+      for (size_t i = 0; i < keyed.size(); ++i) pending[i] = keyed[i].second;
+    } else if (sort_pending && pending.size() > 1) {
       std::stable_sort(pending.begin(), pending.end(), [](GpuTask* a, GpuTask* b) { return a->task->priority > b->task->priority; });
+    }
     std::vector<GpuTask*> keep;
     for (GpuTask* g : pending) {
       int rc = stage_in(g);
@@ -1497,7 +1526,7 @@ void hip_devices_init(Context* ctx) {
   g_nb_exec_streams = (int)params.reg_int("device", "hip", "max_streams", "Execution streams per GPU: stream 0 (high priority) takes critical-path and high-priority tasks, the others the bulk (with the copy stream: 4 hardware queues)", 3);
   int batching = (int)params.reg_int("device", "hip", "batching", "Group ready tile kernels of one kind into one launch", 1);
   int hp = (int)params.reg_int("device", "hip", "high_priority_threshold", "Task priority at or above which the high-priority stream is used", 1 << 27);
-  int sortp = (int)params.reg_int("device", "hip", "sort_pending_tasks", "Sort pending GPU tasks by priority", 1);
+  int sortp = (int)params.reg_int("device", "hip", "sort_pending_tasks", "Order of the pending GPU tasks: 0 arrival, 1 priority, 2 data already on the device first, then priority (reference parsec_gpu_sort_pending_list)", 1);
   int crit = (int)params.reg_int("device", "hip", "critical_threshold", "Task priority at or above which a completed GPU task is released by the manager itself (critical path)", 1 << 29);
   int rcus = (int)params.reg_int("device", "hip", "reserved_cus", "CUs the bulk streams leave free for the critical stream (CU mask on the bulk streams; 0 = none)", 0);
   int rstride = (int)params.reg_int("device", "hip", "reserved_cus_stride", "Spacing of the reserved CU ids in the CU mask", 1);
@@ -1548,7 +1577,7 @@ void hip_devices_init(Context* ctx) {
     d->early_release = early;
     d->cu_yield = cuy;
     kern::set_cu_yield_mode(cuy);
-    d->sort_pending = sortp != 0;
+    d->sort_pending = sortp;
     d->trace_launches = trace;
     reg.add(d);
     g_hip_devices.push_back(d);

@@ -149,7 +149,8 @@ struct HipDevice : Device {
   int hp_route = 1;  // device_hip_hp_on_critical_stream: 1 critical stream, 0 bulk streams, 2 stream 1 alone
   bool cu_masked = false;
   bool batching = true;
-  bool sort_pending = true;
+  int sort_pending = 1;  // 0 arrival order, 1 priority, 2 data availability then priority
+  int missing_on_device(GpuTask* g) const;
   // completed GPU tasks are released (successor activation) by the compute
   // threads instead of the manager, which keeps launching critical work
   std::deque<W2RJob> w2r_jobs;

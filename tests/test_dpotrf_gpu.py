@@ -38,14 +38,18 @@ def test_dpotrf_hbm_resident(pa, N, nb):
         ctx.fini()
 
 
-def test_dpotrf_host_resident_staged(pa):
+@pytest.mark.parametrize("sort_pending", [1, 2])
+def test_dpotrf_host_resident_staged(pa, sort_pending):
     """Tiles live on the host: the engine stages them into its HBM tile cache
-    and pushes final tiles back (collection write-back)."""
+    and pushes final tiles back (collection write-back). sort_pending 2: the
+    pending GPU tasks whose data is already on the device go first (reference
+    parsec_gpu_sort_pending_list), priority among equals."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import numpy as np
 
     N, nb = 1024, 256
+    pa.mca_set("device_hip_sort_pending_tasks", str(sort_pending))
     ctx = pa.init(3)
     try:
         A = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb, nb, N, N)
@@ -67,6 +71,7 @@ def test_dpotrf_host_resident_staged(pa):
         assert gpus[0]["bytes_in"] > 0
     finally:
         ctx.fini()
+        pa.mca_set("device_hip_sort_pending_tasks", "1")
 
 
 def _gpu_matrix(pa, gpu, M, N, mb, nb, fill):
