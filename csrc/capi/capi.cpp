@@ -99,6 +99,12 @@ struct CCollection : DataCollection {
     int64_t idx[1] = {(int64_t)key};
     return c->data_of ? call_varargs<Data*>(c->data_of, c, idx, 1) : nullptr;
   }
+  std::string key_to_string(uint64_t key) const override {
+    if (!c->key_to_string) return DataCollection::key_to_string(key);
+    char buf[128] = {0};
+    c->key_to_string(c, (parsec_data_key_t)key, buf, sizeof(buf));
+    return buf;
+  }
 };
 
 // Block-cyclic matrix behind parsec_matrix_block_cyclic_t: picks up the
@@ -434,6 +440,23 @@ int parsec_type_free(parsec_datatype_t* type) {
 
 // -------------------------------------------------------------- context
 extern int parsec_dtd_window_size, parsec_dtd_threshold_size;
+// the context vpmap queries refer to: the calling worker's, else the last
+// one parsec_init created
+static Context* g_capi_ctx = nullptr;
+static Context* vpmap_ctx() {
+  ExecutionStream* es = my_execution_stream();
+  return es && es->ctx ? es->ctx : g_capi_ctx;
+}
+int vpmap_get_nb_vp(void) {
+  Context* c = vpmap_ctx();
+  return c ? std::max<int>(1, (int)c->vps.size()) : 1;
+}
+int vpmap_get_nb_threads_in_vp(int vp) {
+  Context* c = vpmap_ctx();
+  if (!c || vp < 0 || vp >= (int)c->vps.size()) return 0;
+  return (int)c->vps[vp]->es.size();
+}
+
 parsec_context_t* parsec_init(int nb_cores, int* pargc, char** pargv[]) {
   std::vector<std::string> args;
   if (pargc && pargv && *pargv)
@@ -450,6 +473,7 @@ parsec_context_t* parsec_init(int nb_cores, int* pargc, char** pargv[]) {
     comm_init(atoi(r), atoi(s), j, g ? atoi(g) : -1);
   }
   Context* ctx = context_init(nb_cores, args);
+  g_capi_ctx = ctx;
   {
     auto& reg = ParamRegistry::instance();
     parsec_dtd_window_size = (int)reg.reg_int("dtd", "", "window_size", "Tasks in flight before the inserting thread starts executing", 8000);
@@ -465,6 +489,7 @@ parsec_context_t* parsec_init(int nb_cores, int* pargc, char** pargv[]) {
   return ctx;
 }
 int parsec_fini(parsec_context_t** pcontext) {
+  if (pcontext && *pcontext == g_capi_ctx) g_capi_ctx = nullptr;
   int rc = context_fini(pcontext);
   if (comm_size() > 1) comm_fini();
   return rc;

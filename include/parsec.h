@@ -209,6 +209,7 @@ int parsec_mca_param_get_int(const char* name, int64_t* value);
 typedef struct parsec_data_collection_s parsec_data_collection_t;
 /* user callbacks take the collection followed by the indices as ints; the
  * runtime passes `nb_indices` of them (reference data_distribution.h:26-66) */
+struct parsec_device_module_s; /* include/parsec/mca/device/device.h */
 struct parsec_data_collection_s {
   uint32_t myrank;
   uint32_t nodes;
@@ -224,7 +225,17 @@ struct parsec_data_collection_s {
   char* key_base;
   void* impl;              /* runtime-side collection object */
   uint64_t dc_id;          /* set by parsec_dtd_data_collection_init: same value on every rank */
+  /* optional hooks of user collections (reference data_distribution.h:45-66):
+   * device memory registration (pinning for transfers) and key printing */
+  int (*register_memory)(parsec_data_collection_t* dc, struct parsec_device_module_s* device);
+  int (*unregister_memory)(parsec_data_collection_t* dc, struct parsec_device_module_s* device);
+  int memory_registration_status;
+  int (*key_to_string)(parsec_data_collection_t* dc, parsec_data_key_t key, char* buffer, uint32_t buffer_size);
+  char* key_dim;
+  char* key;
 };
+#define PARSEC_MEMORY_STATUS_UNREGISTERED 0
+#define PARSEC_MEMORY_STATUS_REGISTERED 1
 
 void parsec_data_collection_init(parsec_data_collection_t* dc, int nodes, int myrank);
 void parsec_data_collection_destroy(parsec_data_collection_t* dc);

@@ -240,3 +240,41 @@ def test_redistribute_random_c_program(tmp_path, pa, nranks):
     text = "".join(o for o, _ in outs)
     assert rc == 0, text + "".join(e for _, e in outs)
     assert "Redistribute Result is CORRECT" in text and text.count("bad 0, round trip bad 0") == 2 * nranks, text
+
+
+_LINK = [f"-L{ROOT}/parsec_amd/lib", "-lparsec_amd", f"-Wl,-rpath,{ROOT}/parsec_amd/lib", "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+HAAR = "/root/reference/tests/apps/haar_tree"
+
+
+def test_hash_table_c_program(tmp_path, pa):
+    """Public parsec_hash_table (include/parsec/class/parsec_hash_table.h):
+    8 threads racing find-then-insert under bucket handles, growth from 16
+    buckets, for_all with removal, user key functions (reference
+    tests/class/hash.c)."""
+    exe = tmp_path / "hash_table"
+    cmd = ["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-O1", "-pthread", f"-I{ROOT}/include", os.path.join(HERE, "capi", "hash_table_capi.c"),
+           "-o", str(exe), *_LINK]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "hash table ok" in r.stdout and "40000 items" in r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(HAAR, "tree_dist.c")), reason="reference tree not present")
+def test_reference_tree_dist_collection(tmp_path, pa):
+    """The reference's haar-tree collection (tests/apps/haar_tree/tree_dist.c),
+    compiled unmodified with -Werror against include/ (hash table, vpmap,
+    device module, register_memory / key_to_string hooks) and driven by
+    tests/capi/tree_dist_driver.c."""
+    exe = tmp_path / "tree_dist"
+    cmd = ["gcc", "-std=gnu99", "-Wall", "-Wextra", "-Werror", "-O1", "-pthread", f"-I{ROOT}/include", f"-I{HAAR}",
+           os.path.join(HERE, "capi", "tree_dist_driver.c"), os.path.join(HAAR, "tree_dist.c"), "-o", str(exe), *_LINK]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    dot = tmp_path / "tree.dot"
+    r = subprocess.run([str(exe), str(dot)], capture_output=True, text=True, timeout=60, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "tree_dist ok" in r.stdout
+    text = dot.read_text()
+    assert text.startswith("digraph G {") and text.count("->") == 62

@@ -146,3 +146,17 @@ def test_reference_reshape_sanitized(sanitized, tmp_path, jdf, srcs, npass):
     r = _run_sanitized(kind, exe)
     out = r.stdout + r.stderr
     assert out.count(" PASSED") == npass and "FAILED" not in out, out[-2000:]
+
+
+def test_hash_table_sanitized(sanitized, tmp_path):
+    """The public hash table under 8 racing threads (tests/capi/hash_table_capi.c):
+    bucket handles held across find-then-insert, growth while other threads
+    hold no bucket, for_all with removal."""
+    kind, _ = sanitized
+    cc, libs = ptgpp.compile_flags(False, kind)
+    exe = str(tmp_path / "ht")
+    cmd = ["gcc", "-std=c99", "-O1", "-g", "-pthread", f"-fsanitize={kind}", f"-I{ROOT}/include", os.path.join(ROOT, "tests/capi/hash_table_capi.c"), "-o", exe] + libs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = _run_sanitized(kind, exe)
+    assert "hash table ok" in r.stdout
