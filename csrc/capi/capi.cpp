@@ -7,6 +7,7 @@
 // unpack_args), profiling.h (user dictionary / trace).
 #include <algorithm>
 #include <cstdarg>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -613,6 +614,11 @@ int32_t parsec_task_local(const parsec_task_t* task, int i) { return task->local
 const char* parsec_task_class_name(const parsec_task_t* task) { return task->task_class->name.c_str(); }
 parsec_taskpool_t* parsec_task_taskpool(const parsec_task_t* task) { return task->taskpool; }
 int parsec_execution_stream_id(const parsec_execution_stream_t* es) { return es->th_id; }
+int __parsec_schedule(parsec_execution_stream_t* es, parsec_task_t* task, int32_t distance) {
+  if (!es) es = my_execution_stream();
+  if (!es || !task) return PARSEC_ERROR;
+  return schedule_async_task(es, task, distance);
+}
 
 // ------------------------------------------------------------ MCA params
 int parsec_mca_param_set_string(const char* name, const char* value) {
@@ -1486,6 +1492,14 @@ char* parsec_profiling_strerror(void) { return const_cast<char*>(profiling_last_
 uint64_t parsec_profiling_get_time(void) { return profiling_now(); }
 void parsec_profiling_enable(void) { profiling_set_recording(true); }
 void parsec_profiling_disable(void) { profiling_set_recording(false); }
+void profiling_save_dinfo(const char* key, double value) {
+  char buf[64];
+  std::snprintf(buf, sizeof(buf), "%g", value);
+  profiling_add_information(key ? key : "", buf);
+}
+void profiling_save_iinfo(const char* key, int value) { profiling_add_information(key ? key : "", std::to_string(value)); }
+void profiling_save_uint64info(const char* key, unsigned long long value) { profiling_add_information(key ? key : "", std::to_string(value)); }
+void profiling_save_sinfo(const char* key, char* svalue) { profiling_add_information(key ? key : "", svalue ? svalue : ""); }
 
 }  // extern "C"
 

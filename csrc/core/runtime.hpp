@@ -296,6 +296,9 @@ struct Task : PoolElt {
   TaskDataRef data[kMaxFlows];
   GpuTask* gpu = nullptr;        // GPU bookkeeping while owned by a device
   int8_t selected_device = -1;
+  // CPU body in flight / parked after returning ASYNC / put back while in
+  // flight (the handshake of execute_task and parsec_schedule_async)
+  uint8_t async_state = 0;
   uint64_t sim_exec_date = 0;    // simulation mode (critical path)
   uint64_t prof_event_id = 0;
   void* user = nullptr;          // front-end private (DTD task, recursive parent, ...)
@@ -648,6 +651,12 @@ extern bool g_paranoid;  // debug_paranoid (set at init)
 // Push a set of ready tasks (sorted internally by priority).
 int schedule_tasks(ExecutionStream* es, Task** tasks, int n, int32_t distance);
 int schedule_task(ExecutionStream* es, Task* t, int32_t distance);
+enum TaskAsyncState : uint8_t { ASYNC_NONE = 0, ASYNC_RUNNING = 1, ASYNC_PARKED = 2, ASYNC_REQUESTED = 3 };
+// Put back a task whose CPU body returned HOOK_ASYNC (reference
+// __parsec_schedule on such a task): if the body has not returned yet, the
+// executing thread schedules it itself once it has (so the task is never run
+// again, nor freed, while its first run is still being traced).
+int schedule_async_task(ExecutionStream* es, Task* t, int32_t distance);
 int reschedule(ExecutionStream* es, Task* t);
 // Execute a task's body selecting among its chores (reference __parsec_execute).
 int execute_task(ExecutionStream* es, Task* t);

@@ -177,6 +177,14 @@ int schedule_task(ExecutionStream* es, Task* t, int32_t distance) { return sched
 
 int reschedule(ExecutionStream* es, Task* t) { return schedule_tasks(es, &t, 1, 1); }
 
+int schedule_async_task(ExecutionStream* es, Task* t, int32_t distance) {
+  uint8_t s = __atomic_load_n(&t->async_state, __ATOMIC_ACQUIRE);
+  while (s == ASYNC_RUNNING)
+    if (__atomic_compare_exchange_n(&t->async_state, &s, (uint8_t)ASYNC_REQUESTED, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) return 0;
+  t->async_state = ASYNC_NONE;
+  return schedule_task(es, t, distance);
+}
+
 // ============================================================= execution
 int execute_task(ExecutionStream* es, Task* t) {
   const TaskClass* tc = t->task_class;
@@ -195,8 +203,20 @@ int execute_task(ExecutionStream* es, Task* t) {
       const bool gpus = DeviceRegistry::instance().nb_gpus() > 0;
       if (gpus) cpu_stage_in(es, t);  // device-resident inputs come home first
       PARSEC_PINS(es, PINS_EXEC_BEGIN, t);
+      t->async_state = ASYNC_RUNNING;
       rc = ch.hook(es, t);
       PARSEC_PINS(es, PINS_EXEC_END, t);
+      if (rc == HOOK_ASYNC) {
+        // the body handed the task to someone who will put it back: park it,
+        // or reschedule it now if that already happened
+        uint8_t expect = ASYNC_RUNNING;
+        if (!__atomic_compare_exchange_n(&t->async_state, &expect, (uint8_t)ASYNC_PARKED, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+          t->async_state = ASYNC_NONE;
+          schedule_task(es, t, 0);
+        }
+        return rc;
+      }
+      t->async_state = ASYNC_NONE;
       if (rc == HOOK_DONE && !(tc->flags & TC_INTERNAL)) {
         Device* dev = DeviceRegistry::instance().devices[0];
         if (ch.type == DEV_TEMPLATE)

@@ -5,6 +5,8 @@
 #include <sys/resource.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <cctype>
 #include <cstdio>
 #include <cstring>
 #include <condition_variable>
@@ -432,6 +434,17 @@ std::atomic<int64_t>* counter(const std::string& n) {
 }
 
 // task_profiler: one begin/end key per task class
+constexpr int kProfiledLocals = 8;
+int named_locals(const TaskClass* tc) {
+  int n = std::min<int>({tc->nb_locals, (int)tc->local_names.size(), kProfiledLocals});
+  for (int i = 0; i < n; ++i) {
+    const std::string& nm = tc->local_names[i];
+    bool ok = !nm.empty() && nm != "tp_id" && nm != "tc_id" && nm != "locals";
+    for (char ch : nm) ok = ok && (std::isalnum((unsigned char)ch) || ch == '_');
+    if (!ok) return i;
+  }
+  return n;
+}
 struct TaskProfiler {
   std::mutex m;
   std::map<const TaskClass*, std::pair<int, int>> keys;
@@ -440,7 +453,13 @@ struct TaskProfiler {
     auto it = keys.find(tc);
     if (it != keys.end()) return it->second;
     int b, e;
-    profiling_add_dictionary_keyword(tc->name, "fill:#" + std::to_string(0x100000 + (tc->task_class_id * 2654435761u) % 0xEFFFFF), 16, "tp_id{uint32_t};tc_id{uint32_t};locals{int32_t[2]}", &b, &e);
+    // the first two locals as an array, then every named local by its name
+    // (what the reference's generated profiling convertors record: a column
+    // per task parameter, e.g. "k" for ASYNC(k))
+    std::string desc = "tp_id{uint32_t};tc_id{uint32_t};locals{int32_t[2]}";
+    const int named = named_locals(tc);
+    for (int i = 0; i < named; ++i) desc += ";" + tc->local_names[i] + "{int32_t}";
+    profiling_add_dictionary_keyword(tc->name, "fill:#" + std::to_string(0x100000 + (tc->task_class_id * 2654435761u) % 0xEFFFFF), 16 + 4 * (size_t)named, desc, &b, &e);
     keys[tc] = {b, e};
     return {b, e};
   }
@@ -477,8 +496,11 @@ std::vector<std::pair<std::string, int64_t>> pins_counters() {
 static void trace_task(ExecutionStream* es, Task* t, bool begin) {
   if (!es || !es->prof || !t) return;
   auto k = TPf().key_of(t->task_class);
-  struct { uint32_t tp, tc; int32_t l[2]; } info{t->taskpool->taskpool_id, t->task_class->task_class_id, {t->locals[0], t->task_class->nb_locals > 1 ? t->locals[1] : 0}};
-  profiling_trace(es->prof, begin ? k.first : k.second, t->key, t->taskpool->taskpool_id, &info, sizeof(info));
+  struct { uint32_t tp, tc; int32_t l[2]; int32_t named[kProfiledLocals]; } info{t->taskpool->taskpool_id, t->task_class->task_class_id,
+                                                                               {t->locals[0], t->task_class->nb_locals > 1 ? t->locals[1] : 0}, {}};
+  const int named = named_locals(t->task_class);
+  for (int i = 0; i < named; ++i) info.named[i] = t->locals[i];
+  profiling_trace(es->prof, begin ? k.first : k.second, t->key, t->taskpool->taskpool_id, &info, 16 + 4 * (size_t)named);
 }
 
 void pins_init(Context* ctx) {

@@ -199,6 +199,14 @@ int32_t parsec_task_local(const parsec_task_t* task, int i);
 const char* parsec_task_class_name(const parsec_task_t* task);
 parsec_taskpool_t* parsec_task_taskpool(const parsec_task_t* task);
 int parsec_execution_stream_id(const parsec_execution_stream_t* es);
+/* Put a task back into the scheduler (reference scheduling.h __parsec_schedule):
+ * a task whose body returned PARSEC_HOOK_RETURN_ASYNC is parked until someone
+ * calls this on it; its body then runs again (DONE completes it, ASYNC parks it
+ * again). distance: 0 = the calling stream's own queue, > 0 further away. */
+int __parsec_schedule(parsec_execution_stream_t* es, parsec_task_t* task, int32_t distance);
+/* Tasks are not list items in this API (the scheduler queues them through its
+ * own links): the reference's reset of a task's list links is a no-op here. */
+#define PARSEC_LIST_ITEM_SINGLETON(item) ((void)(item))
 
 /* --------------------------------------------------------- MCA params */
 int parsec_mca_param_set_string(const char* name, const char* value);
@@ -591,6 +599,20 @@ char* parsec_profiling_strerror(void);
 uint64_t parsec_profiling_get_time(void); /* ns since parsec_profiling_start */
 void parsec_profiling_enable(void);
 void parsec_profiling_disable(void);
+/* global key / value information of the trace (reference profiling.h:486-513) */
+void profiling_save_dinfo(const char* key, double value);
+void profiling_save_iinfo(const char* key, int value);
+void profiling_save_uint64info(const char* key, unsigned long long value);
+void profiling_save_sinfo(const char* key, char* svalue);
+#define PROFILING_SAVE_dINFO(key, v) profiling_save_dinfo((key), (v))
+#define PROFILING_SAVE_iINFO(key, v) profiling_save_iinfo((key), (v))
+#define PROFILING_SAVE_uint64INFO(key, v) profiling_save_uint64info((key), (v))
+#define PROFILING_SAVE_sINFO(key, v) profiling_save_sinfo((key), (v))
+/* tracing is always compiled into this runtime (enabled at run time by
+ * --mca profile_filename): programs' PARSEC_PROF_TRACE blocks are built */
+#ifndef PARSEC_PROF_TRACE
+#define PARSEC_PROF_TRACE 1
+#endif
 
 /* --------------------------------------------------- communication engine
  * (reference parsec/parsec_comm_engine.h:22-186). Active messages on user tags

@@ -8,8 +8,8 @@
  * locked one by one (lock_bucket / the _handle variants hold a bucket across a
  * find-then-insert); the nolock_ calls assume the caller holds that lock. The
  * table grows (doubling the buckets) when its load exceeds 4 items per bucket;
- * a resize takes every bucket lock, so it never runs under a caller's bucket
- * lock (the growth is deferred to the next locked insert that holds none).
+ * a resize needs the table to itself (no bucket held by anyone), so it is
+ * attempted, without waiting, by the next bucket lock taken while loaded.
  * Implementation: csrc/capi/hash_table.cpp. */
 #ifndef PARSEC_CLASS_HASH_TABLE_H
 #define PARSEC_CLASS_HASH_TABLE_H

@@ -122,33 +122,61 @@ def _decode_info(fields, blob):
 
 
 def intervals(traces):
-    """Match begin (even key) / end (odd key) events per stream into rows."""
+    """Match begin (even key) / end (odd key) events into rows: within each
+    stream first, then the begins and ends left over are matched across the
+    streams of a rank (an event a task begins on one thread and ends on
+    another, e.g. a body that returned ASYNC and ran again elsewhere;
+    reference dbpreader.c matches across threads the same way)."""
     rows = []
     for tr in traces:
         fields = [_info_fields(d["info_desc"]) for d in tr.dictionary]
+
+        def row(sb, b, se, e):
+            d = int(e["key"]) // 2
+            r = {"rank": tr.rank, "stream": sb["name"], "thread": sb["thread_id"],
+                 "type": tr.dictionary[d]["name"] if d < len(tr.dictionary) else str(d),
+                 "taskpool_id": int(e["taskpool_id"]), "event_id": int(e["event_id"]),
+                 "begin": int(b["timestamp"]), "end": int(e["timestamp"]),
+                 "duration": int(e["timestamp"]) - int(b["timestamp"])}
+            if se is not sb:
+                r["end_stream"] = se["name"]
+            for st, src in ((sb, b), (se, e)):
+                if src["flags"] & 1 and d < len(fields):
+                    blob = st["info"][int(src["info_off"]):int(src["info_off"]) + int(src["info_len"])]
+                    r.update(_decode_info(fields[d], blob))
+            return r
+
+        left_b, left_e = {}, []
         for s in tr.streams:
-            ev = s["events"]
             open_ = {}
-            for e in ev:
+            for e in s["events"]:
                 k = int(e["key"])
                 ident = (k // 2, int(e["taskpool_id"]), int(e["event_id"]))
                 if k % 2 == 0:
+                    if ident in open_:  # an earlier begin of this id never ended here
+                        left_b.setdefault(ident, []).append((s, open_[ident]))
                     open_[ident] = e
                     continue
                 b = open_.pop(ident, None)
                 if b is None:
+                    left_e.append((ident, s, e))
                     continue
-                d = k // 2
-                row = {"rank": tr.rank, "stream": s["name"], "thread": s["thread_id"],
-                       "type": tr.dictionary[d]["name"] if d < len(tr.dictionary) else str(d),
-                       "taskpool_id": int(e["taskpool_id"]), "event_id": int(e["event_id"]),
-                       "begin": int(b["timestamp"]), "end": int(e["timestamp"]),
-                       "duration": int(e["timestamp"]) - int(b["timestamp"])}
-                for src in (b, e):
-                    if src["flags"] & 1 and d < len(fields):
-                        blob = s["info"][int(src["info_off"]):int(src["info_off"]) + int(src["info_len"])]
-                        row.update(_decode_info(fields[d], blob))
-                rows.append(row)
+                rows.append(row(s, b, s, e))
+            for ident, b in open_.items():
+                left_b.setdefault(ident, []).append((s, b))
+        for lst in left_b.values():
+            lst.sort(key=lambda x: int(x[1]["timestamp"]))
+        left_e.sort(key=lambda x: int(x[2]["timestamp"]))
+        for ident, se, e in left_e:
+            cands = left_b.get(ident)
+            if not cands:
+                continue
+            # the latest begin before this end
+            i = max((j for j, (_, b) in enumerate(cands) if int(b["timestamp"]) <= int(e["timestamp"])), default=None)
+            if i is None:
+                continue
+            sb, b = cands.pop(i)
+            rows.append(row(sb, b, se, e))
     return rows
 
 

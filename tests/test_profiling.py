@@ -6,6 +6,7 @@ import json
 import os
 
 import numpy as np
+import pytest
 
 from parsec_amd import profiling
 
@@ -235,3 +236,65 @@ def test_standalone_profiling_c_threads(pa, tmp_path):
     print(r.stdout.strip().splitlines()[0])
     tr = profiling.read_trace(str(tmp_path / "spp-0.prof"))
     assert sum(len(s["events"]) for s in tr.streams) == 4 * 2 * 20000
+
+
+def _check_async(traces, nb):
+    """tests/profiling/check-async.py of the reference, over parsec_amd.profiling
+    intervals instead of its HDF5 tables: one STARTUP, one FULL_RESCHED, NB
+    FULL_ASYNC, 2*NB ASYNC (each body runs twice), RESCHED executions mutually
+    exclusive and inside FULL_RESCHED (except the first one's begin and the
+    last one's end), ASYNC(k)'s first run ending and second run beginning inside
+    FULL_ASYNC(k)."""
+    import pandas as pd
+
+    ev = pd.DataFrame(profiling.intervals(traces))
+    assert int(traces[0].infos["NB"]) == nb
+    cnt = ev.type.value_counts()
+    assert cnt.get("STARTUP", 0) == 1 and cnt.get("FULL_RESCHED", 0) == 1, cnt
+    assert cnt.get("FULL_ASYNC", 0) == nb and cnt.get("ASYNC", 0) == 2 * nb, cnt
+    full = ev[ev.type == "FULL_RESCHED"].iloc[0]
+    res = ev[ev.type == "RESCHED"].sort_values("begin")
+    assert len(res) >= 1
+    before = res[res.begin < full.begin]
+    after = res[res.end > full.end]
+    assert len(before) <= 1 and len(after) <= 1, (before, after)
+    for _, e in before.iterrows():
+        assert full.begin <= e.end <= full.end
+    for _, e in after.iterrows():
+        assert full.begin <= e.begin <= full.end
+    b, e = res.begin.to_numpy(), res.end.to_numpy()
+    assert (b[1:] > e[:-1]).all(), "two RESCHED executions overlap"
+    fa = ev[ev.type == "FULL_ASYNC"].set_index("event_id")
+    asy = ev[ev.type == "ASYNC"].sort_values("begin")
+    for k, g in asy.groupby("k"):
+        assert len(g) == 2, (k, g)
+        ref = fa.loc[k]
+        first, second = g.iloc[0], g.iloc[1]
+        assert ref.begin <= first.end <= ref.end, k
+        assert ref.begin <= second.begin <= ref.end, k
+    assert sorted(asy.k.unique()) == list(range(nb))
+
+
+REF = "/root/reference"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("nb,cores", [(100, 4), (1000, 8), (300, 1)])
+def test_reference_async_profile(pa, tmp_path, nb, cores):
+    """The reference's tests/profiling/async.jdf, unmodified: bodies that return
+    PARSEC_HOOK_RETURN_ASYNC and are put back by another task's
+    __parsec_schedule, a body that returns AGAIN until they all ran once, user
+    streams per thread (parsec_profiling_stream_init) with begin / end events
+    that cross threads, profiling_save_iinfo, and the task_profiler's per-local
+    columns; traced with --mca profile_filename / mca_pins task_profiler, as
+    Testings.cmake:20 runs it, and checked as check-async.py does."""
+    import subprocess
+
+    from parsec_amd import ptgpp
+
+    exe = ptgpp.build_program(os.path.join(REF, "tests/profiling/async.jdf"), str(tmp_path), cxxflags=ptgpp.C_BODIES + (f"-I{REF}",))
+    r = subprocess.run([exe, str(nb), "--", "--mca", "profile_filename", str(tmp_path / "async"), "--mca", "mca_pins", "task_profiler",
+                        "--mca", "runtime_num_cores", str(cores)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    _check_async([profiling.read_trace(str(tmp_path / "async-0.prof"))], nb)

@@ -288,7 +288,6 @@ _NO_COMPILE = {
     "tests/dsl/ptg/ptgpp/too_many_local_vars.jdf": "includes a compiler-check header of the reference build tree",
     "tests/dsl/ptg/ptgpp/write_check.jdf": "MPI_Reduce outside PARSEC_HAVE_MPI guards",
     "tests/dsl/ptg/user-defined-functions/udf.jdf": "implements the internal parsec_key_fn_t hash-key interface",
-    "tests/profiling/async.jdf": "calls __parsec_schedule and the internal list classes",
     "tests/runtime/multichain.jdf": "MPI communicators, tp->super.nb_tasks of the C taskpool layout",
 }
 
