@@ -614,10 +614,39 @@ int32_t parsec_task_local(const parsec_task_t* task, int i) { return task->local
 const char* parsec_task_class_name(const parsec_task_t* task) { return task->task_class->name.c_str(); }
 parsec_taskpool_t* parsec_task_taskpool(const parsec_task_t* task) { return task->taskpool; }
 int parsec_execution_stream_id(const parsec_execution_stream_t* es) { return es->th_id; }
+void parsec_obj_retain_data(parsec_data_t* d) { if (d) data_retain(d); }
+void parsec_obj_release_data(parsec_data_t* d) { if (d) data_release(d); }
+void parsec_obj_retain_copy(parsec_data_copy_t* c) { if (c) data_copy_retain(c); }
+void parsec_obj_release_copy(parsec_data_copy_t* c) { if (c) data_copy_release(c); }
+
+void* parsec_thread_mempool_allocate(parsec_thread_mempool_t* mempool) {
+  ExecutionStream* es = mempool ? mempool->es : nullptr;
+  Context* ctx = es ? es->ctx : g_capi_ctx;
+  if (!ctx) fatal("parsec_thread_mempool_allocate: no context");
+  PoolElt* e = ctx->task_mempool->allocate(es && my_execution_stream() == es ? es->slot : thread_slot());
+  PoolCache* owner = e->owner;
+  Task* t = new (e) Task();
+  t->owner = owner;
+  return t;
+}
+
+int parsec_dependencies_mark_task_as_startup(parsec_task_t* task, parsec_execution_stream_t* es) {
+  (void)es;
+  if (!task || !task->taskpool || !task->task_class) return PARSEC_ERROR;
+  // the hand-built record: ready now (no pending inputs), keyed by its locals;
+  // the repository fields the caller reset have no storage here
+  task->flags |= TASK_FLAG_STARTUP;
+  task->key = task->task_class->make_key(task->taskpool, task->locals);
+  task->deps_remaining = 0;
+  task->status = STATUS_NONE;
+  for (auto& r : task->data.v) r.data_in = r.data_out = nullptr;
+  __atomic_fetch_add(&task->taskpool->initial_number_tasks, 1, __ATOMIC_RELAXED);
+  return PARSEC_SUCCESS;
+}
+
 int __parsec_schedule(parsec_execution_stream_t* es, parsec_task_t* task, int32_t distance) {
-  if (!es) es = my_execution_stream();
-  if (!es || !task) return PARSEC_ERROR;
-  return schedule_async_task(es, task, distance);
+  if (!task) return PARSEC_ERROR;
+  return schedule_async_task(es ? es : my_execution_stream(), task, distance);
 }
 
 // ------------------------------------------------------------ MCA params
@@ -1770,4 +1799,17 @@ parsec_info_id_t parsec_info_lookup(parsec_info_t* nfo, const char* name, void**
   return id;
 }
 void* parsec_gpu_stream_info_get(parsec_info_id_t iid) { return t_gpu_ctx ? t_gpu_ctx->info(iid) : nullptr; }
+}
+
+// C++ overloads (include/parsec.h): opaque_dtt is a parsec::Datatype here
+parsec_data_copy_t* parsec_data_copy_new(parsec_data_t* data, int device, const parsec::Datatype& dtt, uint32_t flags) {
+  parsec_data_copy_t* c = parsec_data_copy_new(data, device, PARSEC_DATATYPE_NULL, flags);
+  if (c) c->dtt = dtt;
+  return c;
+}
+parsec_data_copy_t* parsec_arena_get_copy(const std::shared_ptr<parsec::Arena>& arena, size_t count, int device, const parsec::Datatype& dtt) {
+  if (!arena || device < 0 || device >= kMaxDevices) return nullptr;
+  DataCopy* c = arena->get_copy_count(nullptr, device, (int64_t)std::max<size_t>(count, 1));
+  if (c) c->dtt = dtt;
+  return c;
 }

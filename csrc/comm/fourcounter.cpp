@@ -73,7 +73,12 @@ class FourCounter : public TermdetModule {
     tp->termdet_state.compare_exchange_strong(exp, TERMDET_BUSY);
     idle_check(tp);
   }
-  void taskpool_set_nb_tasks(Taskpool* tp, int64_t v) override { tp->nb_tasks.store(v); idle_check(tp); }
+  void taskpool_set_nb_tasks(Taskpool* tp, int64_t v) override {
+    // set from a body of tp: its own completion is still to come (termdet.cpp)
+    if (Task* t = current_task(); t && t->taskpool == tp && !(t->task_class->flags & TC_INTERNAL)) ++v;
+    tp->nb_tasks.store(v);
+    idle_check(tp);
+  }
   int64_t taskpool_addto_nb_tasks(Taskpool* tp, int64_t d) override {
     int64_t v = tp->nb_tasks.fetch_add(d) + d;
     if (v == 0) idle_check(tp);

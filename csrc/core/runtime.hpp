@@ -280,30 +280,64 @@ enum TaskFlags : uint32_t { TASK_FLAG_REMOTE_SHADOW = 0x1, TASK_FLAG_STARTUP = 0
 // Freed-task marker written by task_free when debug_paranoid is set (use-after-release detection).
 constexpr uint8_t STATUS_FREED = 0xFF;
 
-struct Task : PoolElt {
-  Taskpool* taskpool = nullptr;
-  const TaskClass* task_class = nullptr;
-  uint64_t key = 0;
-  int32_t priority = 0;
-  uint8_t status = STATUS_NONE;
-  int8_t chore_id = 0;
-  uint16_t nb_remote_targets = 0;
-  int32_t deps_remaining = 0;    // activations still expected (PTG counter mode)
-  uint32_t deps_mask = 0;        // flows satisfied so far (PTG mask mode)
-  uint32_t chore_mask = 0xffffffffu;
-  uint32_t flags = 0;
-  int32_t locals[kMaxLocals];
-  TaskDataRef data[kMaxFlows];
-  GpuTask* gpu = nullptr;        // GPU bookkeeping while owned by a device
-  int8_t selected_device = -1;
-  // CPU body in flight / parked after returning ASYNC / put back while in
-  // flight (the handshake of execute_task and parsec_schedule_async)
-  uint8_t async_state = 0;
-  uint64_t sim_exec_date = 0;    // simulation mode (critical path)
-  uint64_t prof_event_id = 0;
-  void* user = nullptr;          // front-end private (DTD task, recursive parent, ...)
-  void* pending_events[4] = {};  // device events this task must wait on (stream-ordered release)
+// One task local as the reference's generated code sees it (parsec_assignment_t:
+// `task->locals[i].value`); converts to / from int32_t for the runtime.
+struct TaskLocal {
+  int32_t value;
+  operator int32_t&() { return value; }
+  operator int32_t() const { return value; }
+  TaskLocal& operator=(int32_t v) { value = v; return *this; }
+};
+// A task's locals: indexable as int32_t (runtime) or TaskLocal (`.value`), and
+// usable wherever the runtime takes `const int32_t*`.
+struct TaskLocals {
+  TaskLocal v[kMaxLocals];
+  TaskLocal& operator[](int i) { return v[i]; }
+  const TaskLocal& operator[](int i) const { return v[i]; }
+  int32_t* data() { return &v[0].value; }
+  const int32_t* data() const { return &v[0].value; }
+  operator int32_t*() { return data(); }
+  operator const int32_t*() const { return data(); }
+};
+static_assert(sizeof(TaskLocals) == sizeof(int32_t) * kMaxLocals, "task locals layout");
+
+// The task record's members. Task spells them with the runtime's types; the
+// per-class task views parsec-ptgpp generates (__parsec_<tp>_<class>_task_t,
+// the reference's generated task structs) spell `locals` / `data` as structs of
+// named members, so the layout is the same by construction.
+#define PARSEC_TASK_MEMBERS(LOCALS_T, DATA_T)                                                                           \
+  parsec::Taskpool* taskpool = nullptr;                                                                                 \
+  const parsec::TaskClass* task_class = nullptr;                                                                        \
+  uint64_t key = 0;                                                                                                     \
+  int32_t priority = 0;                                                                                                 \
+  uint8_t status = parsec::STATUS_NONE;                                                                                 \
+  int8_t chore_id = 0;                                                                                                  \
+  uint16_t nb_remote_targets = 0;                                                                                       \
+  int32_t deps_remaining = 0;    /* activations still expected (PTG counter mode) */                                   \
+  uint32_t deps_mask = 0;        /* flows satisfied so far (PTG mask mode) */                                          \
+  uint32_t chore_mask = 0xffffffffu;                                                                                    \
+  uint32_t flags = 0;                                                                                                   \
+  LOCALS_T locals;                                                                                                      \
+  DATA_T data;                                                                                                          \
+  parsec::GpuTask* gpu = nullptr; /* GPU bookkeeping while owned by a device */                                        \
+  int8_t selected_device = -1;                                                                                          \
+  /* CPU body in flight / parked after returning ASYNC / put back while in flight */                                   \
+  /* (the handshake of execute_task and schedule_async_task) */                                                        \
+  uint8_t async_state = 0;                                                                                              \
+  uint64_t sim_exec_date = 0;    /* simulation mode (critical path) */                                                 \
+  uint64_t prof_event_id = 0;                                                                                           \
+  void* user = nullptr;          /* front-end private (DTD task, recursive parent, ...) */                             \
+  void* pending_events[4] = {};  /* device events this task must wait on (stream-ordered release) */                   \
   int nb_pending_events = 0;
+
+struct TaskDataRefs {
+  TaskDataRef v[kMaxFlows];
+  TaskDataRef& operator[](int i) { return v[i]; }
+  const TaskDataRef& operator[](int i) const { return v[i]; }
+};
+
+struct Task : PoolElt {
+  PARSEC_TASK_MEMBERS(TaskLocals, TaskDataRefs)
 };
 
 struct Flow {
@@ -403,6 +437,14 @@ struct Taskpool {
   uint32_t devices_index_mask = 0xffffffffu;
   Context* context = nullptr;
   std::vector<TaskClass*> task_classes;
+  std::vector<TaskClass*>& task_classes_array = task_classes;  // the reference's name (generated code reads it)
+  // per-class state of a user alloc_deps_fn (reference tp->dependencies_array:
+  // JDF find_deps_fn / alloc_deps_fn / free_deps_fn, e.g. haar_tree/project.jdf)
+  std::vector<void*> dependencies_array;
+  // tasks a user startup_fn created (reference internal taskpool field: the
+  // user adds to it, or parsec_dependencies_mark_task_as_startup does); counted
+  // into nb_tasks when the task count is dynamic
+  int32_t initial_number_tasks = 0;
   // termination detector; `tdm.module` is the reference's spelling (tests/dsl/ptg/
   // user-defined-functions/utt.jdf calls tdm.module->taskpool_set_nb_tasks)
   struct TermdetRef {
@@ -499,6 +541,13 @@ const std::vector<SchedulerComponent>& scheduler_components();
 struct PinsChain;
 struct ProfilingStream;
 
+// A stream's task allocator as the reference's generated code reaches it
+// (es->context_mempool, parsec_thread_mempool_allocate: a task a startup_fn
+// builds by hand).
+struct ThreadMempool {
+  ExecutionStream* es;
+};
+
 struct alignas(64) ExecutionStream {  // one thread writes it per task: keep it off its neighbours' lines
   int th_id = 0;          // global id in the context
   int core_id = -1;
@@ -516,6 +565,8 @@ struct alignas(64) ExecutionStream {  // one thread writes it per task: keep it 
   uint32_t cpu_exec_pending = 0;
   int l2_id = -1, l3_id = -1;  // caches this thread's core shares (lowest CPU id sharing them)  // executed CPU tasks not yet added to the CPU device's shared counter
   std::vector<int> steal_order;  // other th_ids by distance (filled by vpmap)
+  ThreadMempool mempool_handle{this};
+  ThreadMempool* context_mempool = &mempool_handle;
 };
 
 struct VirtualProcess {
@@ -523,6 +574,7 @@ struct VirtualProcess {
   int nb_cores = 0;  // compute streams of this VP (reference field name)
   Context* parsec_context = nullptr;  // owning context (reference field name)
   std::vector<ExecutionStream*> es;
+  std::vector<ExecutionStream*>& execution_streams = es;  // the reference's name
   void* sched_obj = nullptr;
 };
 
@@ -657,6 +709,8 @@ enum TaskAsyncState : uint8_t { ASYNC_NONE = 0, ASYNC_RUNNING = 1, ASYNC_PARKED 
 // executing thread schedules it itself once it has (so the task is never run
 // again, nor freed, while its first run is still being traced).
 int schedule_async_task(ExecutionStream* es, Task* t, int32_t distance);
+// the task whose CPU body the calling thread is running (nullptr outside one)
+Task* current_task();
 int reschedule(ExecutionStream* es, Task* t);
 // Execute a task's body selecting among its chores (reference __parsec_execute).
 int execute_task(ExecutionStream* es, Task* t);

@@ -186,6 +186,9 @@ int schedule_async_task(ExecutionStream* es, Task* t, int32_t distance) {
 }
 
 // ============================================================= execution
+static thread_local Task* t_current_task = nullptr;
+Task* current_task() { return t_current_task; }
+
 int execute_task(ExecutionStream* es, Task* t) {
   const TaskClass* tc = t->task_class;
   Taskpool* tp = t->taskpool;
@@ -204,7 +207,10 @@ int execute_task(ExecutionStream* es, Task* t) {
       if (gpus) cpu_stage_in(es, t);  // device-resident inputs come home first
       PARSEC_PINS(es, PINS_EXEC_BEGIN, t);
       t->async_state = ASYNC_RUNNING;
+      Task* const outer = t_current_task;
+      t_current_task = t;
       rc = ch.hook(es, t);
+      t_current_task = outer;
       PARSEC_PINS(es, PINS_EXEC_END, t);
       if (rc == HOOK_ASYNC) {
         // the body handed the task to someone who will put it back: park it,

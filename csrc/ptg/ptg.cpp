@@ -279,7 +279,7 @@ uint32_t PtgTaskClass::direct_mask(const Taskpool* tp, const int32_t* L) const {
 void PtgTaskClass::build_index_store(const Taskpool* tp) {
   IndexStore& st = istore;
   st.ok = false;
-  if (def.startup_fn || def.nb_local_tasks_fn || def.make_key_fn || nb_params == 0) return;
+  if (def.startup_fn || def.startup_task_fn || def.nb_local_tasks_fn || def.make_key_fn || nb_params == 0) return;
   const uint32_t my = tp->context ? (uint32_t)tp->context->my_rank : 0;
   std::vector<int64_t> mn(nb_params, INT64_MAX), mx(nb_params, INT64_MIN);
   int64_t n = 0;
@@ -328,6 +328,13 @@ bool PtgTaskClass::is_startup_instance(const Taskpool* tp, const int32_t* L) con
     if (data_flow && !any) return false;
   }
   return true;
+}
+
+bool PtgTaskClass::always_from_task() const {
+  for (const FlowDef& f : def.flows)
+    for (const Dep& d : f.in)
+      if (d.iters.empty() && d.then_t.kind == DEP_TASK && (!d.guard || (d.has_else && d.else_t.kind == DEP_TASK))) return true;
+  return false;
 }
 
 int64_t PtgTaskClass::sim_cost(const Task* t) const { return def.sim_cost ? def.sim_cost(t->taskpool, t->locals) : 1; }
@@ -784,6 +791,8 @@ PtgTaskpool::PtgTaskpool() { taskpool_name = "ptg"; }
 
 PtgTaskpool::~PtgTaskpool() {
   drop_reshape_views();
+  for (size_t i = 0; i < classes.size() && i < dependencies_array.size(); ++i)
+    if (classes[i]->def.free_deps_fn && dependencies_array[i]) classes[i]->def.free_deps_fn(this, dependencies_array[i]);
   pending.for_each([](uint64_t, Task* t) {
     for (int f = 0; f < kMaxFlows; ++f) if (t->data[f].data_in) data_copy_release(t->data[f].data_in);
     task_free(t);
@@ -1011,6 +1020,9 @@ int PtgTaskpool::startup_step(ExecutionStream* es, StartupGen* g) {
 
 void PtgTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
   if (!finalized) finalize();
+  dependencies_array.assign(classes.size(), nullptr);
+  for (size_t i = 0; i < classes.size(); ++i)
+    if (classes[i]->def.alloc_deps_fn) dependencies_array[i] = classes[i]->def.alloc_deps_fn(this);
   ExecutionStream* es = my_execution_stream();
   uint32_t my = (uint32_t)ctx->my_rank;
   int64_t nb_local = nb_local_tasks_fn ? nb_local_tasks_fn(this) : 0;
@@ -1024,12 +1036,23 @@ void PtgTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
       for_each_task(this, tc, [&](const int32_t* L) {
         if (tc->rank_of(this, L) == my) ++nb_local;
       });
+    if (tc->def.startup_task_fn) {
+      // the user builds and schedules the startup tasks (counted by the
+      // taskpool's nb_local_tasks_fn, or as they are marked when dynamic)
+      Task tmpl;
+      tmpl.taskpool = this;
+      tmpl.task_class = tc;
+      initial_number_tasks = 0;
+      tc->def.startup_task_fn(es, &tmpl);
+      nb_startup += __atomic_exchange_n(&initial_number_tasks, 0, __ATOMIC_ACQ_REL);
+      continue;
+    }
     if (tc->def.startup_fn) {
       std::vector<std::vector<int32_t>> st;
       tc->def.startup_fn(this, st);
       for (auto& L : st) {
         Task* t = task_new(es, this, tc);
-        std::copy(L.begin(), L.end(), t->locals);
+        std::copy(L.begin(), L.end(), t->locals.data());
         t->key = tc->make_key(this, t->locals);
         t->priority = tc->priority_of(this, t->locals);
         t->flags |= TASK_FLAG_STARTUP;
@@ -1038,6 +1061,11 @@ void PtgTaskpool::startup(Context* ctx, std::vector<Task*>& ready) {
       }
       continue;
     }
+    // a class keyed by a user make_key_fn spans a space that is not meant to
+    // be enumerated (haar_tree: l = 0 .. 1<<n, n < 32); as in the reference's
+    // generated code, a class whose inputs always come from tasks has no
+    // startup tasks to look for
+    if (tc->def.make_key_fn && tc->always_from_task()) continue;
     // the first chunk is produced here; a generator task continues the rest
     auto* g = new StartupGen(this, tc);
     const size_t before = ready.size();
@@ -1138,8 +1166,9 @@ void PtgTaskpool::activate(ExecutionStream* es, PtgTaskClass* tc, const int32_t*
       // reference's persistent dependency words): an extra activation is a DAG
       // error, fatal in mask mode / paranoid, otherwise reported and dropped
       if (tc->use_mask || g_paranoid)
-        fatal("%s: flow %s activated after the task became ready (double activation of an already satisfied dependency)",
-              tc->name.c_str(), flow >= 0 ? tc->def.flows[flow].name.c_str() : "?");
+        fatal("%s key %s: flow %s activated after the task became ready (double activation of an already satisfied dependency)",
+              tc->name.c_str(), tc->def.key_print ? tc->def.key_print(key).c_str() : std::to_string(key).c_str(),
+              flow >= 0 ? tc->def.flows[flow].name.c_str() : "?");
       if (!tc->warned_extra_activation.exchange(true))
         warning("%s: extra activation of flow %s after the task became ready ignored", tc->name.c_str(), flow >= 0 ? tc->def.flows[flow].name.c_str() : "?");
       return nullptr;

@@ -129,6 +129,15 @@ struct TaskClassDef {
   std::function<uint64_t(const Taskpool*, const int32_t*)> make_key_fn;
   std::function<int64_t(const Taskpool*)> nb_local_tasks_fn;
   std::function<void(const Taskpool*, std::vector<std::vector<int32_t>>&)> startup_fn;  // returns startup locals
+  // a startup_fn in the reference's form: called once with a template task of
+  // the class (taskpool set), it builds its tasks (parsec_thread_mempool_allocate,
+  // parsec_dependencies_mark_task_as_startup) and schedules them itself
+  std::function<int(ExecutionStream*, Task*)> startup_task_fn;
+  // alloc_deps_fn / free_deps_fn: per-class user state in tp->dependencies_array
+  std::function<void*(Taskpool*)> alloc_deps_fn;
+  std::function<void(Taskpool*, void*)> free_deps_fn;
+  // hash_struct: the user's key printer (keys in diagnostics)
+  std::function<std::string(uint64_t)> key_print;
   // dependency tracking: -1 = taskpool default, 0 = counter, 1 = mask
   // (reference class properties count_deps / mask_deps, jdf2c.c:4171-4206)
   int deps_mode = -1;
@@ -158,6 +167,9 @@ class PtgTaskClass : public TaskClass {
   // active (memory / NULL / NEW) input: the startup rule of the reference
   // compiler (jdf2c.c:2775-2815 has_ready_input_dependency, 2870-2965).
   bool is_startup_instance(const Taskpool* tp, const int32_t* L) const;
+  // some flow always takes its input from a task (unguarded, or a ternary
+  // whose both branches are tasks): no instance can be a startup task
+  bool always_from_task() const;
   const DepTarget* active_input(const Taskpool* tp, int flow, const int32_t* L) const;
   // Every active input instance of `flow` (one for data flows, all for CTL gathers).
   void for_each_input(const Taskpool* tp, int flow, const int32_t* L, const std::function<void(const int32_t* Lx, const DepTarget*)>& f) const;

@@ -80,6 +80,10 @@ class PackedTermdet : public TermdetModule {
     settle(tp, tp->termdet_word.fetch_or(kReady, std::memory_order_acq_rel) | kReady);
   }
   void taskpool_set_nb_tasks(Taskpool* tp, int64_t v) override {
+    // from a body of this taskpool (e.g. haar_tree's "we are now DONE"
+    // nb_tasks = 0): that task's own completion is still to come, so it stays
+    // counted -- the taskpool ends when it has finished, not while it runs
+    if (Task* t = current_task(); t && t->taskpool == tp && !(t->task_class->flags & TC_INTERNAL)) ++v;
     tp->nb_tasks.store(v, std::memory_order_seq_cst);
     settle(tp, set_field(tp, kTasksShift, v));
   }

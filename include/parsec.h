@@ -60,14 +60,6 @@
 #define PARSEC_ERR_NOT_SUPPORTED (-2)
 #define PARSEC_ERR_NOT_FOUND (-13)
 
-/* Object-system reference counts (reference parsec/class/parsec_object.h).
- * Objects of this API are kept alive by the runtime's own reference counts
- * (an arena is shared by every copy of its parsec_arena_datatype_t, a
- * taskpool's arenas_datatypes hold their own references) or released by the
- * explicit *_destroy / *_free calls, so a program's RETAIN / RELEASE pairs
- * have nothing to balance: accepted for source compatibility. */
-#define PARSEC_OBJ_RETAIN(obj) ((void)(obj))
-#define PARSEC_OBJ_RELEASE(obj) ((void)(obj))
 /* A class instance names a taskpool type's constructor / destructor (e.g. a
  * wrapper's destructor that frees the datatypes of its arenas). The runtime
  * releases a taskpool's arenas and datatypes itself when it is freed, so the
@@ -93,6 +85,7 @@ struct Data;
 struct DataCopy;
 struct ArenaDatatype;
 struct Datatype;
+struct ThreadMempool;
 }  // namespace parsec
 typedef parsec::Context parsec_context_t;
 typedef parsec::Taskpool parsec_taskpool_t;
@@ -101,6 +94,7 @@ typedef parsec::ExecutionStream parsec_execution_stream_t;
 typedef parsec::Data parsec_data_t;
 typedef parsec::DataCopy parsec_data_copy_t;
 typedef parsec::ArenaDatatype parsec_arena_datatype_t;
+typedef parsec::ThreadMempool parsec_thread_mempool_t;
 /* programs that spell the C struct tags (`struct parsec_data_s *d;`, reference
  * tests/apps/pingpong/rtt_data.c) name the same classes when compiled as C++ */
 #define parsec_data_s parsec::Data
@@ -114,9 +108,42 @@ typedef struct parsec_execution_stream_s parsec_execution_stream_t;
 typedef struct parsec_data_s parsec_data_t;
 typedef struct parsec_data_copy_s parsec_data_copy_t;
 typedef struct parsec_arena_datatype_s parsec_arena_datatype_t;
+typedef struct parsec_thread_mempool_s parsec_thread_mempool_t;
 #endif
 
 typedef uint64_t parsec_data_key_t;
+
+/* Object-system reference counts (reference parsec/class/parsec_object.h).
+ * Data and data copies are reference counted by the runtime: RETAIN / RELEASE
+ * on a parsec_data_t* or parsec_data_copy_t* take / drop a reference (a body
+ * that keeps a NEW tile past its task, haar_tree/project.jdf:199 +
+ * tree_dist.c:168). Every other object of this API is kept alive by the
+ * runtime's own counts (an arena is shared by every copy of its
+ * parsec_arena_datatype_t, a taskpool's arenas_datatypes hold their own
+ * references) or released by the explicit *_destroy / *_free calls: for them
+ * the macros accept the pair and do nothing. */
+void parsec_obj_retain_data(parsec_data_t* d);
+void parsec_obj_release_data(parsec_data_t* d);
+void parsec_obj_retain_copy(parsec_data_copy_t* c);
+void parsec_obj_release_copy(parsec_data_copy_t* c);
+static inline void parsec_obj_keep_none(const volatile void* o) { (void)o; }
+#ifdef __cplusplus
+}  /* extern "C" */
+inline void parsec_obj_retain(parsec_data_t* d) { parsec_obj_retain_data(d); }
+inline void parsec_obj_retain(parsec_data_copy_t* c) { parsec_obj_retain_copy(c); }
+template <class T> inline void parsec_obj_retain(T&&) {}
+inline void parsec_obj_release(parsec_data_t* d) { parsec_obj_release_data(d); }
+inline void parsec_obj_release(parsec_data_copy_t* c) { parsec_obj_release_copy(c); }
+template <class T> inline void parsec_obj_release(T&&) {}
+#define PARSEC_OBJ_RETAIN(obj) parsec_obj_retain(obj)
+#define PARSEC_OBJ_RELEASE(obj) parsec_obj_release(obj)
+extern "C" {
+#else
+#define PARSEC_OBJ_RETAIN(obj) \
+  _Generic((obj), parsec_data_t*: parsec_obj_retain_data, parsec_data_copy_t*: parsec_obj_retain_copy, default: parsec_obj_keep_none)(obj)
+#define PARSEC_OBJ_RELEASE(obj) \
+  _Generic((obj), parsec_data_t*: parsec_obj_release_data, parsec_data_copy_t*: parsec_obj_release_copy, default: parsec_obj_keep_none)(obj)
+#endif
 
 /* diagnostics (reference parsec/utils/debug.h): this process' rank and the
  * runtime's debug verbosity (MCA debug_verbose) */
@@ -207,6 +234,33 @@ int __parsec_schedule(parsec_execution_stream_t* es, parsec_task_t* task, int32_
 /* Tasks are not list items in this API (the scheduler queues them through its
  * own links): the reference's reset of a task's list links is a no-op here. */
 #define PARSEC_LIST_ITEM_SINGLETON(item) ((void)(item))
+
+/* The vocabulary of the reference's generated code that user functions of a
+ * JDF program against (jdf2c output: tests/apps/haar_tree/project.jdf,
+ * walk.jdf, tests/dsl/ptg/user-defined-functions/udf.jdf). parsec-ptgpp emits
+ * per-class views __parsec_<tp>_<class>_task_t / _assignment_s and the
+ * internal taskpool type over the runtime's task and taskpool. */
+typedef struct parsec_assignment_s {
+  int32_t value;
+} parsec_assignment_t;
+/* dependency word of a user find_deps_fn (this runtime tracks dependencies in
+ * its own pending-task table: alloc / free_deps_fn state is kept per class in
+ * tp->dependencies_array, find_deps_fn is accepted and not consulted) */
+typedef uint32_t parsec_dependency_t;
+/* nb_local_tasks_fn result: the taskpool ends when a body sets nb_tasks to 0 */
+#define PARSEC_UNDETERMINED_NB_TASKS (0x0fffffff)
+#define PARSEC_TASK_STATUS_NONE 0
+#define PARSEC_TASK_STATUS_PREPARE_INPUT 1
+#define PARSEC_TASK_STATUS_EVAL 2
+#define PARSEC_TASK_STATUS_HOOK 3
+#define PARSEC_TASK_STATUS_PREPARE_OUTPUT 4
+#define PARSEC_TASK_STATUS_COMPLETE 5
+/* a task record from a stream's allocator (es->context_mempool); the caller
+ * fills taskpool / task_class / locals / priority and hands it to
+ * parsec_dependencies_mark_task_as_startup, then __parsec_schedule */
+void* parsec_thread_mempool_allocate(parsec_thread_mempool_t* mempool);
+/* finish a hand-built startup task: key from its locals, no pending inputs */
+int parsec_dependencies_mark_task_as_startup(parsec_task_t* task, parsec_execution_stream_t* es);
 
 /* --------------------------------------------------------- MCA params */
 int parsec_mca_param_set_string(const char* name, const char* value);
@@ -740,6 +794,13 @@ void parsec_profiling_trace_f08(int key, int64_t event_id, int taskpool_id, int*
  * not a handle): the reference's wrappers free it in their destructors. The
  * datatype belongs to its arena datatype, which the runtime releases. */
 inline int parsec_type_free(parsec::Datatype*) { return PARSEC_SUCCESS; }
+/* the same datatype where the reference passes opaque_dtt by value */
+parsec_data_copy_t* parsec_data_copy_new(parsec_data_t* data, int device, const parsec::Datatype& dtt, uint32_t flags);
+#include <memory>
+namespace parsec { struct Arena; }
+/* a fresh copy (and its Data) from a taskpool arena (reference arena.h
+ * parsec_arena_get_copy): `count` elements of the arena's size, on `device` */
+parsec_data_copy_t* parsec_arena_get_copy(const std::shared_ptr<parsec::Arena>& arena, size_t count, int device, const parsec::Datatype& dtt);
 #endif
 
 #endif /* PARSEC_AMD_PARSEC_H */

@@ -276,18 +276,13 @@ _REJECT = {
 _NO_COMPILE = {
     "parsec/data_dist/matrix/broadcast.jdf": "builds a collection with the internal object system (PARSEC_OBJ_NEW, parsec_data_t fields); public form: parsec_broadcast_New",
     "parsec/data_dist/matrix/diag_band_to_rect.jdf": "includes parsec/parsec_internal.h",
-    "tests/apps/haar_tree/project.jdf": "tree_dist.h uses the internal parsec_hash_table class",
-    "tests/apps/haar_tree/project_dyn.jdf": "tree_dist.h uses the internal parsec_hash_table class (public-API port: tests/jdf/project_dyn.jdf)",
-    "tests/apps/haar_tree/walk.jdf": "tree_dist.h uses the internal parsec_hash_table class",
     "tests/collections/redistribute/redistribute_bound.jdf": "MPI calls outside PARSEC_HAVE_MPI guards, context->virtual_processes",
     "tests/collections/redistribute/redistribute_check.jdf": "MPI calls outside PARSEC_HAVE_MPI guards",
     "tests/collections/redistribute/redistribute_check2.jdf": "MPI calls outside PARSEC_HAVE_MPI guards",
     "tests/collections/redistribute/redistribute_no_optimization.jdf": "MPI calls outside PARSEC_HAVE_MPI guards",
-    "tests/collections/two_dim_band/two_dim_band.jdf": "reads this_task->data._f_Y (the generated task struct layout; public-API port: tests/jdf/two_dim_band.jdf)",
     "tests/dsl/ptg/choice/choice2.jdf": "reads task->parsec_object (object system internals)",
     "tests/dsl/ptg/ptgpp/too_many_local_vars.jdf": "includes a compiler-check header of the reference build tree",
     "tests/dsl/ptg/ptgpp/write_check.jdf": "MPI_Reduce outside PARSEC_HAVE_MPI guards",
-    "tests/dsl/ptg/user-defined-functions/udf.jdf": "implements the internal parsec_key_fn_t hash-key interface",
     "tests/runtime/multichain.jdf": "MPI communicators, tp->super.nb_tasks of the C taskpool layout",
 }
 
@@ -648,3 +643,124 @@ def test_reference_c_examples(tmp_path, src, expect):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     if expect:
         assert expect in r.stdout, r.stdout[-2000:]
+
+
+# ------------------------------------------- reference programs on generated-code internals
+HAAR = os.path.join(REF, "tests/apps/haar_tree")
+SUM_VALUE = 0xbdae8a4ea45fc32e  # reference tests/apps/haar_tree/main.c:23
+
+
+def _build_haar(tmp_path, dyn, main=None):
+    """project(_dyn).jdf + walk.jdf + tree_dist.c of the reference, unmodified;
+    the driver is tests/capi/haar_tree_driver.cpp (prints each rank's
+    checksum) or the reference's own main.c."""
+    proj = "project_dyn" if dyn else "project"
+    srcs = [ptgpp.compile_jdf(os.path.join(HAAR, j + ".jdf"), str(tmp_path))[0] for j in (proj, "walk")]
+    cc, libs = ptgpp.compile_flags(False)
+    exe = str(tmp_path / ("haar_dyn" if dyn else "haar"))
+    drv = main or os.path.join(HERE, "capi", "haar_tree_driver.cpp")
+    defs = (["-DHAAR_DYN"] if dyn else []) + (["-Dparsec_project_new=parsec_project_dyn_new"] if dyn and main else [])
+    cmd = cc + list(ptgpp.C_BODIES) + defs + [f"-I{HAAR}", f"-I{tmp_path}", f"-I{REF}", "-x", "c++", drv, os.path.join(HAAR, "tree_dist.c"), "-x", "none"] + srcs + ["-o", exe] + libs + ["-lm"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return exe
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("dyn", [False, True], ids=["project", "project_dyn"])
+@pytest.mark.parametrize("nranks", [1, 2, 4])
+def test_reference_haar_tree(tmp_path, dyn, nranks):
+    """The reference's haar-tree application (tests/apps/haar_tree, Testings.cmake:1-5,
+    `project -x` on 1 and 4 ranks): a tree refined until the local error is
+    below a threshold, with a user startup_fn that builds and schedules the root
+    task by hand, make_key_fn / hash_struct / find_deps / alloc_deps on a
+    2^32-wide space, writable locals (this_task->locals.larger_than_thresh),
+    NEW tiles kept past their task (PARSEC_OBJ_RETAIN) and a body that ends the
+    taskpool (tdm.module->taskpool_set_nb_tasks(tp, 0)); then walk.jdf visits the
+    tree. The XOR of the ranks' checksums is the reference's SUM_VALUE."""
+    from parsec_amd import launch
+
+    exe = _build_haar(tmp_path, dyn)
+    rc, outs = launch.launch(nranks, [exe], timeout=120, capture=True, env={"PARSEC_MCA_device_hip_enabled": "0"})
+    text = "".join(o for o, _ in outs)
+    assert rc == 0, text + "".join(e for _, e in outs)
+    lines = [l.split() for l in text.splitlines() if l.startswith("haar rank")]
+    assert len(lines) == nranks, text
+    ck = keys = nodes = 0
+    for w in lines:
+        ck ^= int(w[w.index("cksum") + 1], 16)
+        keys ^= int(w[w.index("keys") + 1], 16)
+        nodes += int(w[w.index("nodes_up") + 1])
+    m_ck, m_keys, m_internal, m_leaves = _haar_model(dyn)
+    if dyn:
+        # the leaves' NEW tiles go back into the tree too, with unset contents
+        assert (nodes, keys) == (m_internal + m_leaves, m_keys), (nodes, hex(keys), text)
+    else:
+        assert m_ck == SUM_VALUE and nodes == m_internal  # the model reproduces main.c's constant
+        assert ck == SUM_VALUE, (hex(ck), text)
+
+
+def _haar_model(dyn, thresh=1e-3, alpha=1.0):
+    """The tree project(_dyn).jdf builds, recomputed: checksum of the created
+    nodes (main.c cksum_node_fn), XOR of all keys written (nodes, plus the
+    leaves for project_dyn), node and leaf counts."""
+    import math
+    import struct
+
+    def bits(x):
+        return struct.unpack("<Q", struct.pack("<d", x))[0]
+
+    def key_to_x(n, l):
+        return -10.0 + (2.0 * 10.0) * math.pow(2.0, -n) * (0.5 + l)
+
+    f = (lambda x: math.exp(-(x / alpha) * (x / alpha))) if dyn else (lambda x: math.exp(-x * x))
+    ck = keys = internal = leaves = 0
+    stack = [(0, 0)]
+    while stack:
+        n, l = stack.pop()
+        sl, sr = f(key_to_x(n + 1, 2 * l)), f(key_to_x(n + 1, 2 * l + 1))
+        d = 0.5 * (sl - sr)
+        if n >= (8 if dyn else 3) and abs(d) * math.pow(2.0, -0.5 * n) <= thresh:
+            leaves += 1
+            if dyn:
+                keys ^= (l << 32) | n
+            continue
+        ck ^= bits(0.5 * (sl + sr)) ^ bits(0.5 * (sl - sr)) ^ ((l << 32) | n)
+        keys ^= (l << 32) | n
+        internal += 1
+        stack += [(n + 1, 2 * l), (n + 1, 2 * l + 1)]
+    return ck, keys, internal, leaves
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("args", [["-x"], []], ids=["check", "dot"])
+def test_reference_haar_tree_main(tmp_path, args):
+    """The reference's own main.c (compiled unmodified; without MPI it builds
+    and walks the tree and exits 0, its checksum comparison is under HAVE_MPI)."""
+    exe = _build_haar(tmp_path, False, main=os.path.join(HAAR, "main.c"))
+    r = subprocess.run([exe, *args], capture_output=True, text=True, timeout=120, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+def test_reference_udf(tmp_path):
+    """The reference's user-defined-functions test (tests/dsl/ptg/user-defined-functions,
+    Testings.cmake: `udf -N 100 -n 10`), JDF, wrapper and main unmodified:
+    nb_local_tasks_fn over the internal taskpool type, make_key_fn on
+    parsec_assignment_t locals, hash_struct key functions, startup_fn that
+    allocates (parsec_thread_mempool_allocate), marks
+    (parsec_dependencies_mark_task_as_startup) and schedules its tasks. Every
+    class's range probe is counted per local tile; the taskpool must end with
+    exactly its nb_local_tasks_fn count of tasks."""
+    d = os.path.join(REF, "tests/dsl/ptg/user-defined-functions")
+    cpp = ptgpp.compile_jdf(os.path.join(d, "udf.jdf"), str(tmp_path))[0]
+    cc, libs = ptgpp.compile_flags(False)
+    exe = str(tmp_path / "udf")
+    cmd = cc + list(ptgpp.C_BODIES) + [f"-I{d}", f"-I{tmp_path}", f"-I{REF}", "-x", "c++", os.path.join(d, "main.c"), os.path.join(d, "udf_wrapper.c"),
+                                       "-x", "none", cpp, "-o", exe] + libs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    r = subprocess.run([exe, "-N", "100", "-n", "10"], capture_output=True, text=True, timeout=60, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Rank 0 - 100 local tiles" in r.stdout, r.stdout
+    assert r.stdout.count("iterator is called") == 5, r.stdout

@@ -936,36 +936,66 @@ struct Gen {
     return o.str();
   }
 
+  std::string view_name(const Function& f) const { return "__parsec_" + fname + "_" + f.name + "_task_t"; }
+
+  // The reference's generated-code types, over this runtime's records (the
+  // user functions of a JDF program against them, haar_tree/project.jdf,
+  // user-defined-functions/udf.jdf): the internal taskpool type, and per class
+  // the assignment struct (locals by name), the task view (the task record
+  // with `locals` / `data` spelled by name, same layout by construction:
+  // PARSEC_TASK_MEMBERS) and `<name>_<class>.task_class_id`.
+  void emit_views() {
+    const std::string itp = "__parsec_" + fname + "_internal_taskpool_s";
+    c << "struct " << itp << " : parsec_" << fname << "_taskpool_s {\n  parsec_" << fname << "_taskpool_t& super = *this;\n};\n";
+    c << "typedef struct " << itp << " __parsec_" << fname << "_internal_taskpool_t;\n";
+    int id = 0;
+    for (auto& f : j.functions) {
+      const std::string pre = "__parsec_" + fname + "_" + f.name;
+      c << "struct " << pre << "_assignment_s { ";
+      for (auto& l : f.locals) c << "parsec_assignment_t " << l.name << "; ";
+      if ((int)f.locals.size() < kMaxLocals) c << "parsec_assignment_t __unused[" << kMaxLocals - (int)f.locals.size() << "]; ";
+      c << "};\ntypedef struct " << pre << "_assignment_s " << pre << "_parsec_assignment_t;\n";
+      c << "struct " << pre << "_data_s { ";
+      for (auto& fl : f.flows) c << "parsec::ptg::FlowRef _f_" << fl.name << "; ";
+      if ((int)f.flows.size() < kMaxFlows) c << "parsec::ptg::FlowRef __unused[" << kMaxFlows - (int)f.flows.size() << "]; ";
+      c << "};\n";
+      c << "struct " << pre << "_task_s : parsec::PoolElt {\n  PARSEC_TASK_MEMBERS(" << pre << "_assignment_s, " << pre << "_data_s)\n";
+      c << "  static inline thread_local void* repo_entry = nullptr;  // no data repositories: a per-thread sink\n};\n";
+      c << "typedef struct " << pre << "_task_s " << pre << "_task_t;\n";
+      c << "static_assert(sizeof(" << pre << "_task_t) == sizeof(parsec::Task), \"task view layout\");\n";
+      c << "[[maybe_unused]] static const parsec::ptg::ClassHandle " << fname << "_" << f.name << "{" << id++ << "};\n";
+    }
+    c << "\n";
+  }
+
   void body_fn(const Function& f, const Body& b, int idx, const std::string& type) {
     const std::string fn = "__ptg_" + fname + "_" + f.name + "_body" + std::to_string(idx);
     const bool gpu = type == "HIP";
-    if (gpu) c << "static int " << fn << "(parsec::GpuExecContext* __ctx, parsec::Task* this_task) {\n";
-    else c << "static int " << fn << "([[maybe_unused]] parsec::ExecutionStream* es, parsec::Task* this_task) {\n";
-    c << "  [[maybe_unused]] auto* __tp = static_cast<parsec_" << fname << "_taskpool_t*>(this_task->taskpool);\n";
-    // reference generated bodies see the internal taskpool as __parsec_tp
-    // (__parsec_tp->super is the public taskpool struct)
-    c << "  [[maybe_unused]] struct { parsec_" << fname << "_taskpool_t& super; } __parsec_tp_ref{*__tp};\n";
-    c << "  [[maybe_unused]] auto* __parsec_tp = &__parsec_tp_ref;\n";
+    // the body sees the task through its class view (this_task->locals.X.value,
+    // this_task->data._f_X: the reference's generated task struct) and the
+    // taskpool as the internal type (__parsec_tp->super._g_X)
+    if (gpu) c << "static int " << fn << "(parsec::GpuExecContext* __ctx, parsec::Task* __ptask) {\n";
+    else c << "static int " << fn << "([[maybe_unused]] parsec::ExecutionStream* es, parsec::Task* __ptask) {\n";
+    c << "  [[maybe_unused]] auto* this_task = reinterpret_cast<" << view_name(f) << "*>(__ptask);\n";
+    c << "  [[maybe_unused]] auto* __tp = static_cast<parsec_" << fname << "_taskpool_t*>(__ptask->taskpool);\n";
+    c << "  [[maybe_unused]] auto* __parsec_tp = static_cast<__parsec_" << fname << "_internal_taskpool_t*>(__tp);\n";
     c << "  " << bind_globals() << "\n";
-    c << "  " << bind_locals(f, "this_task->locals") << "\n";
-    // writable view of the task's locals: `locals.X.value = v` in a body changes
-    // the value the output guards of this task see (reference
-    // this_task->locals.X.value, e.g. haar_tree/project_dyn.jdf)
-    c << "  [[maybe_unused]] struct __locals_view { ";
-    for (auto& l : f.locals) c << "parsec::ptg::LocalSlot " << l.name << "; ";
-    c << "} &locals = *reinterpret_cast<__locals_view*>(this_task->locals);\n";
+    c << "  " << bind_locals(f, "__ptask->locals") << "\n";
+    // writable locals: `locals.X.value = v` changes the value the output guards
+    // of this task see (reference this_task->locals.X.value, haar_tree/project.jdf)
+    c << "  [[maybe_unused]] auto& locals = this_task->locals;\n";
     for (size_t k = 0; k < f.flows.size(); ++k) {
       const Flow& fl = f.flows[k];
       if (fl.access == "CTL") continue;
-      c << "  [[maybe_unused]] parsec::DataCopy* _f_" << fl.name << " = parsec::ptg::flow_copy(this_task, " << k << ");\n";
+      c << "  [[maybe_unused]] parsec::DataCopy* _f_" << fl.name << " = parsec::ptg::flow_copy(__ptask, " << k << ");\n";
       if (gpu) c << "  [[maybe_unused]] void* " << fl.name << " = __ctx->ptr(" << k << ");\n";
-      else c << "  [[maybe_unused]] void* " << fl.name << " = parsec::ptg::flow_ptr(this_task, " << k << ");\n";
+      else c << "  [[maybe_unused]] void* " << fl.name << " = parsec::ptg::flow_ptr(__ptask, " << k << ");\n";
     }
     // parsec_body: stream / context of a GPU body, and the resolved BODY dyld=
     // symbol typed by dyldtype= (reference jdf2c.c parsec_body.dyld_fn)
     const Prop* dyt = find_prop(b.props, "dyldtype");
     const std::string fnty = dyt ? dyt->val : "void*";
-    const std::string dyld_expr = "(" + fnty + ")this_task->task_class->chores[this_task->chore_id].dyld_fn";
+    const std::string dyld_expr = "(" + fnty + ")__ptask->task_class->chores[__ptask->chore_id].dyld_fn";
     if (gpu) c << "  [[maybe_unused]] struct { hipStream_t stream; parsec::GpuExecContext* ctx; " << fnty << " dyld_fn; } parsec_body{__ctx->stream, __ctx, " << dyld_expr << "};\n";
     else c << "  [[maybe_unused]] struct { " << fnty << " dyld_fn; } parsec_body{" << dyld_expr << "};\n";
     if (!g_noline) c << "#line " << b.line + 1 << " \"" << g_file << "\"\n";
@@ -1014,6 +1044,7 @@ struct Gen {
       c << j.prologue << "\n";
     }
     c << "#include \"" << base_name(base) << ".h\"\n\n";
+    emit_views();
     // reference generated-code helpers a body may use: rank_of_<dc>(...) /
     // data_of_<dc>(...) on collection globals, PARSEC_<name>_<TYPE>_ADT
     for (auto& g : j.globals)
@@ -1030,7 +1061,7 @@ struct Gen {
         body_fn(f, f.bodies[b], (int)b, ty ? ty->val : "CPU");
       }
     c << proto << " {\n";
-    c << "  auto* __tp = new parsec_" << fname << "_taskpool_t();\n";
+    c << "  parsec_" << fname << "_taskpool_t* __tp = new __parsec_" << fname << "_internal_taskpool_t();\n";
     c << "  __tp->taskpool_name = \"" << fname << "\";\n";
     for (auto& g : j.globals)
       if (!hidden(g)) c << "  __tp->_g_" << g.name << " = " << g.name << ";\n";
@@ -1079,9 +1110,19 @@ struct Gen {
         if (p->val == "off" || p->val == "false" || p->val == "0") c << "    d.flags |= parsec::TC_NO_PROFILE;\n";
       if (const Prop* p = find_prop(f.props, "immediate"))
         if (p->val == "on" || p->val == "true" || p->val == "1") c << "    d.flags |= parsec::TC_IMMEDIATE;\n";
-      if (const Prop* p = find_prop(f.props, "make_key_fn")) c << "    d.make_key_fn = [](const parsec::Taskpool* __ptp, const int32_t* __plocals) { return (uint64_t)" << p->val << "(__ptp, __plocals); };\n";
-      if (const Prop* p = find_prop(f.props, "startup_fn")) c << "    d.startup_fn = [](const parsec::Taskpool* __ptp, std::vector<std::vector<int32_t>>& __pout) { " << p->val << "(__ptp, __pout); };\n";
-      if (const Prop* p = find_prop(f.props, "nb_local_tasks_fn")) c << "    d.nb_local_tasks_fn = [](const parsec::Taskpool* tp) { return (int64_t)" << p->val << "(tp); };\n";
+      // user functions: this runtime's signatures or the reference's (locals as
+      // parsec_assignment_t, the class view, the internal taskpool)
+      if (const Prop* p = find_prop(f.props, "make_key_fn"))
+        c << "    d.make_key_fn = [](const parsec::Taskpool* __ptp, const int32_t* __plocals) { return parsec::ptg::call_make_key(&" << p->val << ", __ptp, __plocals); };\n";
+      if (const Prop* p = find_prop(f.props, "startup_fn")) c << "    parsec::ptg::set_startup<" << view_name(f) << ">(d, &" << p->val << ");\n";
+      if (const Prop* p = find_prop(f.props, "nb_local_tasks_fn"))
+        c << "    d.nb_local_tasks_fn = [](const parsec::Taskpool* tp) { return parsec::ptg::call_nb_local<__parsec_" << fname << "_internal_taskpool_t>(&" << p->val << ", tp); };\n";
+      if (const Prop* p = find_prop(f.props, "hash_struct")) c << "    parsec::ptg::set_key_functions(d, " << p->val << ");\n";
+      if (const Prop* p = find_prop(f.props, "alloc_deps_fn"))
+        c << "    d.alloc_deps_fn = [](parsec::Taskpool* tp) { return (void*)" << p->val << "(static_cast<__parsec_" << fname << "_internal_taskpool_t*>(tp)); };\n";
+      if (const Prop* p = find_prop(f.props, "free_deps_fn"))
+        c << "    d.free_deps_fn = [](parsec::Taskpool* tp, void* deps) { " << p->val << "(static_cast<__parsec_" << fname << "_internal_taskpool_t*>(tp), deps); };\n";
+      if (const Prop* p = find_prop(f.props, "find_deps_fn")) c << "    (void)&" << p->val << ";  // dependencies live in the engine's pending table\n";
       if (const Prop* p = find_prop(f.props, "flops")) c << "    d.flops = (double)(" << p->val << ");\n";
       auto prop_on = [&](const char* k) { const Prop* p = find_prop(f.props, k); return p && (p->val == "on" || p->val == "true" || p->val == "1"); };
       if (prop_on("count_deps")) c << "    d.deps_mode = 0;\n";
@@ -1138,7 +1179,8 @@ struct Gen {
     }
     for (auto& kv : j.options)
       if (kv.first == "nb_local_tasks_fn")
-        c << "  (void)__has_nb_local;\n  __tp->nb_local_tasks_fn = [](const parsec::Taskpool* tp) { return (int64_t)" << kv.second << "(tp); };\n";
+        c << "  (void)__has_nb_local;\n  __tp->nb_local_tasks_fn = [](const parsec::Taskpool* tp) { return parsec::ptg::call_nb_local<__parsec_" << fname
+          << "_internal_taskpool_t>(&" << kv.second << ", tp); };\n";
     bool dyn = g_dynamic_termdet;
     for (auto& kv : j.options)  // %option dynamic = ON (reference jdf.h: task counts known only at run time)
       if ((kv.first == "dynamic" || kv.first == "termdet") && (kv.second == "ON" || kv.second == "on" || kv.second == "true" || kv.second == "1" || kv.second == "dynamic"))
