@@ -334,6 +334,9 @@ struct LazyStorage : Base {
     if (synced.load(std::memory_order_relaxed)) return;
     if (!this->mat && c->mat) this->allocate_storage(c->mat);
     if (this->mat) synced.store(true, std::memory_order_release);
+    // no storage (tiles a program allocates itself, reference
+    // tests/collections/two_dim_band): storage-less tiles, as CBlockCyclic
+    else if (this->tiles.empty()) this->tiles.assign((size_t)this->nb_local_tiles, nullptr);
   }
   Data* data_of(const int64_t* idx, int n) override { sync(); return Base::data_of(idx, n); }
   Data* data_of_key(uint64_t key) override { sync(); return Base::data_of_key(key); }

@@ -278,6 +278,19 @@ def generate_sanitized(kind):
     return out
 
 
+def _headers_fingerprint():
+    import hashlib
+
+    h = hashlib.sha1()
+    for top in ("csrc", "include"):
+        for root, _, files in sorted(os.walk(os.path.join(ROOT, top))):
+            for f in sorted(files):
+                if f.endswith((".h", ".hpp")):
+                    st = os.stat(os.path.join(root, f))
+                    h.update(f"{root}/{f}:{st.st_mtime_ns}:{st.st_size};".encode())
+    return h.hexdigest()
+
+
 def build_sanitized(kind, jobs=None):
     """Build the instrumented runtime (needs the main build's kernel objects)."""
     need = [os.path.join(BUILD, "obj", s.replace("/", "_") + ".o") for s in _exists(HIP_SOURCES)]
@@ -292,7 +305,22 @@ def build_sanitized(kind, jobs=None):
     with open(os.path.join(sanitize_dir(kind), ".build.lock"), "w") as lk:
         fcntl.flock(lk, fcntl.LOCK_EX)
         out = generate_sanitized(kind)
+        # ninja's header dependencies live in its deps log; a log cut short (an
+        # interrupted build) forgets them and left objects compiled against an
+        # older runtime.hpp linked into the instrumented library. A changed
+        # header set rebuilds everything.
+        stamp = os.path.join(out, ".headers")
+        fp = _headers_fingerprint()
+        if not os.path.exists(stamp) or open(stamp).read() != fp:
+            import shutil
+            shutil.rmtree(os.path.join(out, "obj"), ignore_errors=True)
+            for f in (".ninja_deps", ".ninja_log"):
+                if os.path.exists(os.path.join(out, f)):
+                    os.remove(os.path.join(out, f))
         r = subprocess.run(["ninja", "-C", out, f"-j{jobs or min(8, os.cpu_count() or 4)}"])
+        if r.returncode == 0:
+            with open(stamp, "w") as f:
+                f.write(fp)
     if r.returncode != 0:
         raise RuntimeError(f"sanitized ({kind}) build failed")
     return out

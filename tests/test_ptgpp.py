@@ -764,3 +764,23 @@ def test_reference_udf(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Rank 0 - 100 local tiles" in r.stdout, r.stdout
     assert r.stdout.count("iterator is called") == 5, r.stdout
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("args", [[], ["-N", "40", "-T", "4", "-b", "3"]], ids=["default", "band3"])
+def test_reference_two_dim_band(tmp_path, args):
+    """The reference's tests/collections/two_dim_band (main.c, two_dim_band.jdf,
+    two_dim_band_free.jdf unmodified): band and symmetric-band collections
+    whose tiles have no storage until tasks allocate it
+    (this_task->data._f_Y.data_out = parsec_data_copy_new(...)), initialise it
+    and free it again."""
+    d = os.path.join(REF, "tests/collections/two_dim_band")
+    srcs = [ptgpp.compile_jdf(os.path.join(d, j + ".jdf"), str(tmp_path))[0] for j in ("two_dim_band", "two_dim_band_free")]
+    cc, libs = ptgpp.compile_flags(False)
+    exe = str(tmp_path / "band")
+    cmd = cc + list(ptgpp.C_BODIES) + [f"-I{d}", f"-I{tmp_path}", f"-I{REF}", "-x", "c++", os.path.join(d, "main.c"), "-x", "none"] + srcs + ["-o", exe] + libs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    r = subprocess.run([exe, *args], capture_output=True, text=True, timeout=60, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    assert r.stdout.count("Init") == 2, r.stdout

@@ -998,6 +998,18 @@ struct Gen {
     const std::string dyld_expr = "(" + fnty + ")__ptask->task_class->chores[__ptask->chore_id].dyld_fn";
     if (gpu) c << "  [[maybe_unused]] struct { hipStream_t stream; parsec::GpuExecContext* ctx; " << fnty << " dyld_fn; } parsec_body{__ctx->stream, __ctx, " << dyld_expr << "};\n";
     else c << "  [[maybe_unused]] struct { " << fnty << " dyld_fn; } parsec_body{" << dyld_expr << "};\n";
+    // a body that sets a flow's copy itself (this_task->data._f_X.data_out =
+    // parsec_data_copy_new(...), two_dim_band.jdf) hands the task a copy the
+    // collection's Data already owns: the task takes its own reference, which
+    // its release drops (on every return path)
+    if (b.code.find("data_out") != std::string::npos && !f.flows.empty()) {
+      c << "  struct __out_guard { parsec::Task* t; parsec::DataCopy* before[" << f.flows.size() << "];\n"
+        << "    ~__out_guard() { for (int k = 0; k < " << f.flows.size() << "; ++k) "
+        << "if (t->data[k].data_out && t->data[k].data_out != before[k] && t->data[k].data_out != t->data[k].data_in) parsec::data_copy_retain(t->data[k].data_out); }\n"
+        << "  } __og{__ptask, {";
+      for (size_t k = 0; k < f.flows.size(); ++k) c << (k ? ", " : "") << "__ptask->data[" << k << "].data_out";
+      c << "}};\n";
+    }
     if (!g_noline) c << "#line " << b.line + 1 << " \"" << g_file << "\"\n";
     c << "  {" << b.code << "}\n";
     c << "  return PARSEC_HOOK_RETURN_DONE;\n}\n\n";
