@@ -152,6 +152,11 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // waves, and the wave does not wait for the update -- C traffic leaves the MFMA
 // timeline of the workgroup. Each element gets one add per tile (or per K chunk
 // of a split tile), so the result does not depend on timing.
+// EPI = 2: late C. The accumulators start from zero and C is read into its own
+// registers right behind the first A / B tile; the loads retire under the first
+// k-tile's MFMA work instead of in front of it, and the epilogue forms
+// alpha AB + beta C from registers (a pure store). Needs the register budget of
+// two waves per SIMD (launched with one workgroup per CU).
 template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF, int PF, int EPI>
 __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, int ks, int nsplit, double (&As)[NBUF][BK][BM + (((BM % 32) == 16) ? 0 : 16)],
                                           double (&Bs)[NBUF][BK][BN + (((BN % 32) == 16) ? 0 : 16)]) {
@@ -323,7 +328,20 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
   // beta's operand: C itself or a separate input (Cin)
   const double* __restrict__ Cr = d.Cin ? d.Cin : C;
   const int ldcr = d.Cin ? d.ldcin : ldc;
+  constexpr bool LATE = EPI == 2;
+  const bool late = LATE && FULL && !split && d.beta != 0.0;
+  double4_t cr[LATE ? FN : 1][LATE ? FM : 1];
   load_tile(0);
+  if (LATE && late) {
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const double* p = Cr + (size_t)(n0 + wn * WTN + i * 16 + fk) * ldcr + (m0 + wm * WTM + j * 16 + fr);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cr[i][j][r] = p[(size_t)4 * r * ldcr];
+      }
+  }
   if (preload && d.beta != 0.0) {
     const double cs = d.beta / d.alpha;
 #pragma unroll
@@ -369,7 +387,7 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
   }
   }
 
-  const double alpha = d.alpha, beta = preload ? 0.0 : d.beta;
+  const double alpha = d.alpha, beta = (preload || late) ? 0.0 : d.beta;
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -381,6 +399,7 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
         if ((FULL || (gm < M && gn < N)) && (!d.lower_only || gm >= gn)) {
           double* p = C + (size_t)gn * ldc + gm;
           double v = alpha * acc[i][j][r];
+          if (LATE && late) v = fma(d.beta, cr[LATE ? i : 0][LATE ? j : 0][r], v);
           if (split || EPI == 1) {
             unsafeAtomicAdd(p, v);  // no-return global f64 add, performed at the memory side
             continue;
@@ -836,10 +855,15 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
   // add) -- profiles/r5_gemm_epilogue.txt. Persistent grid (PARSEC_GEMM_PERSIST=1,
   // off: -5..-8 % with one workgroup per CU): one round of resident workgroups
   // walks the tiles (no split-K tail, no stagger).
+  const size_t pad = BM == 128 ? (size_t)t_launch_pad : 0;
   static const int epi_env = getenv("PARSEC_GEMM_EPI") ? atoi(getenv("PARSEC_GEMM_EPI")) : -1;
   static const int persist_env = getenv("PARSEC_GEMM_PERSIST") ? atoi(getenv("PARSEC_GEMM_PERSIST")) : 0;
-  bool epi = epi_env != 0 && full;
+  bool epi = epi_env != 0 && epi_env != 2 && full;
   for (int i = 0; epi && i < n; ++i) epi = descs[i].beta == 1.0 && !descs[i].Cin && !descs[i].C2 && (epi_env > 0 || descs[i].k >= 1024);
+  // late C (EPI 2) on the one-workgroup-per-CU bulk launches that do not take
+  // the atomic epilogue: PARSEC_GEMM_LATE_C = 1 (default 0 until measured)
+  static const int late_env = getenv("PARSEC_GEMM_LATE_C") ? atoi(getenv("PARSEC_GEMM_LATE_C")) : 0;
+  const bool late = BM == 128 && full && !epi && (epi_env == 2 || late_env > 0) && pad;
   const bool persist = persist_env != 0 && full && BM == 128 && a.stagger == 0 && total > slots;
   if (persist) {
     a.main_tiles = total;
@@ -847,7 +871,6 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
     grid_size = slots;
   }
   const dim3 grid(grid_size), block(WM * WN * 64);
-  const size_t pad = BM == 128 ? (size_t)t_launch_pad : 0;
   if (pad) {
     static bool said = false;
     if (!said && getenv("PARSEC_GEMM_PAD_DEBUG")) {
@@ -861,10 +884,16 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
     else if (full) hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, OCC, PF, E>), grid, block, pad, stream, a);  \
     else hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, false, NBUF, OCC, PF, 0>), grid, block, pad, stream, a);          \
   } while (0)
-#define PARSEC_GEMM_LAUNCH(TA, TB)               \
-  do {                                            \
-    if (epi) PARSEC_GEMM_LAUNCH_E(TA, TB, 1);     \
-    else PARSEC_GEMM_LAUNCH_E(TA, TB, 0);         \
+#define PARSEC_GEMM_LAUNCH(TA, TB)                                                                                   \
+  do {                                                                                                              \
+    if constexpr (BM == 128) {                                                                                      \
+      if (late && !persist) {                                                                                       \
+        hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, 2, PF, 2>), grid, block, pad, stream, a); \
+        break;                                                                                                      \
+      }                                                                                                             \
+    }                                                                                                               \
+    if (epi) PARSEC_GEMM_LAUNCH_E(TA, TB, 1);                                                                       \
+    else PARSEC_GEMM_LAUNCH_E(TA, TB, 0);                                                                           \
   } while (0)
   switch (mode) {
     case 0: PARSEC_GEMM_LAUNCH(false, false); break;
