@@ -15,7 +15,15 @@ reference dplasma zpotrf_L.jdf) on a model of the machine:
     critical stream, profiles/r4_chain*.txt);
   * a tile produced on rank r and read by tasks on rank s != r crosses the
     (r, s) xGMI link ONCE (the runtime's per-rank activation aggregation), after
-    a per-message latency; each directed link carries one transfer at a time.
+    a per-message latency. Round 5 (what the code does): every rank pulls its
+    inbound tiles through ONE serial receive queue (csrc/comm/fetch_queue.hpp:
+    priority ordered by the consuming task's priority, one copy-engine pull
+    stream between distinct GPUs), so all of a rank's inbound transfers run one
+    after another (`--recv per-link` restores the round-4 assumption of one
+    transfer at a time per directed link);
+  * the panel chain's TRSM(k+1, k) / SYRK(k, k+1) run on the critical stream
+    with a measured latency (`--trsm-us`: the critical 64x64 grouped TRSM
+    W-GEMM averages 265 us under load at config 3, profiles/r5_kernel_stats_c3_v1.csv).
 
 Calibration: --gemm-tf is the sustained bulk rate; the 1-rank prediction is
 compared with the measured 1-GPU number (BENCH json) so the residual model error
@@ -38,7 +46,7 @@ def grid_of(n):
     return best
 
 
-def simulate(NT, nb, P, Q, gemm_tf, potrf_us, link_gbs, lat_us, syrk_eff=0.85, trsm_eff=1.0):
+def simulate(NT, nb, P, Q, gemm_tf, potrf_us, link_gbs, lat_us, syrk_eff=0.85, trsm_eff=1.0, recv="per-link", trsm_us=None):
     R = P * Q
 
     def owner(m, n):
@@ -97,9 +105,33 @@ def simulate(NT, nb, P, Q, gemm_tf, potrf_us, link_gbs, lat_us, syrk_eff=0.85, t
     bytes_sent = 0
     now = 0.0
 
+    def on_crit(t):
+        # the panel chain on the critical stream: POTRF, and with a measured
+        # chain latency also TRSM(k+1, k) and SYRK(k, k+1)
+        kind = tasks[t][1]
+        if kind == "POTRF":
+            return True
+        if trsm_us is None:
+            return False
+        return (kind == "TRSM" and t[1] == t[2] + 1) or (kind == "SYRK" and t[2] == t[1] + 1)
+
+    def crit_cost(t):
+        kind = tasks[t][1]
+        return cost["POTRF"] if kind == "POTRF" else trsm_us if kind == "TRSM" else cost["SYRK"]
+
+    recv_q = [[] for _ in range(R)]  # serial receive: (-prio, seq, key)
+    recv_busy = [False] * R
+
+    def recv_kick(r, at):
+        if recv_busy[r] or not recv_q[r]:
+            return
+        _, _, key = heapq.heappop(recv_q[r])
+        recv_busy[r] = True
+        heapq.heappush(ev, (at + xfer_us - lat_us, next(seq), "arrive", key))
+
     def ready(t, at):
         rank, kind, prio, _ = tasks[t]
-        q = crit_q[rank] if kind == "POTRF" else bulk_q[rank]
+        q = crit_q[rank] if on_crit(t) else bulk_q[rank]
         heapq.heappush(q, (-prio, next(seq), t))
         heapq.heappush(ev, (at, next(seq), "kick", rank))
 
@@ -112,7 +144,7 @@ def simulate(NT, nb, P, Q, gemm_tf, potrf_us, link_gbs, lat_us, syrk_eff=0.85, t
         if not crit_busy[rank] and crit_q[rank]:
             _, _, t = heapq.heappop(crit_q[rank])
             crit_busy[rank] = True
-            heapq.heappush(ev, (at + cost["POTRF"], next(seq), "done", (t, "crit")))
+            heapq.heappush(ev, (at + crit_cost(t), next(seq), "done", (t, "crit")))
         if not bulk_busy[rank] and bulk_q[rank]:
             _, _, t = heapq.heappop(bulk_q[rank])
             bulk_busy[rank] = True
@@ -151,13 +183,25 @@ def simulate(NT, nb, P, Q, gemm_tf, potrf_us, link_gbs, lat_us, syrk_eff=0.85, t
                 # one transfer of the tile to that rank
                 arrived[key] = None
                 waiting[key] = [s]
+                bytes_sent += nb * nb * 8
+                if recv == "serial":
+                    # the activation reaches the receiver after the message
+                    # latency; its pull then queues behind the rank's other pulls
+                    heapq.heappush(ev, (now + lat_us, next(seq), "request", (key, tasks[s][2])))
+                    continue
                 start = max(now, link_free.get((rank, sr), 0.0))
                 link_free[(rank, sr)] = start + xfer_us - lat_us
-                bytes_sent += nb * nb * 8
                 heapq.heappush(ev, (start + xfer_us, next(seq), "arrive", key))
             kick(rank, now)
+        elif kind == "request":
+            key, prio = p
+            heapq.heappush(recv_q[key[1]], (-prio, next(seq), key))
+            recv_kick(key[1], now)
         elif kind == "arrive":
             arrived[p] = now
+            if recv == "serial":
+                recv_busy[p[1]] = False
+                recv_kick(p[1], now)
             for s in waiting.pop(p):
                 satisfy(s, now)
     assert all(v == 0 for v in nd.values()), "graph did not drain"
@@ -212,25 +256,28 @@ def main():
     ap.add_argument("--lat-us", type=float, default=25.0, help="per-message latency (activation + pull setup)")
     ap.add_argument("--ranks", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--measured-1gpu-tf", type=float, default=None)
+    ap.add_argument("--recv", choices=["serial", "per-link"], default="serial", help="inbound transfers: one serial queue per rank (the code) or one per directed link (round 4)")
+    ap.add_argument("--trsm-us", type=float, default=265.0, help="TRSM(k+1,k) latency on the critical stream (us); <0: in the bulk at the GEMM rate")
     a = ap.parse_args()
     NT = a.n // a.nb
+    trsm = a.trsm_us if a.trsm_us >= 0 else None
     print(f"MODEL PREDICTION (not a measurement): DPOTRF N={a.n} nb={a.nb} ({NT}x{NT} tiles), bulk GEMM {a.gemm_tf} TF/GPU, "
-          f"tile POTRF {a.potrf_us} us, message latency {a.lat_us} us")
+          f"tile POTRF {a.potrf_us} us, TRSM(k+1,k) {a.trsm_us} us, message latency {a.lat_us} us, receive {a.recv}")
     for bw in a.link_gbs:
         print(f"-- xGMI effective {bw} GB/s per directed peer link")
         print(f"{'ranks':>5} {'grid':>6} {'span ms':>9} {'TF (job)':>9} {'TF/GPU':>7} {'eff':>5} {'bulk util':>9} {'xGMI GB':>8} {'chain ms':>8}")
         base = None
         for r in a.ranks:
             P, Q = grid_of(r)
-            out = simulate(NT, a.nb, P, Q, a.gemm_tf, a.potrf_us, bw, a.lat_us)
+            out = simulate(NT, a.nb, P, Q, a.gemm_tf, a.potrf_us, bw, a.lat_us, recv=a.recv, trsm_us=trsm)
             base = base or out["tflops"]
             eff = out["tflops"] / (base * r)
             g_us = 2.0 * a.nb ** 3 / (a.gemm_tf * 1e12) * 1e6
-            chain = critical_path_us(NT, a.potrf_us, g_us, g_us / 2 / 0.85, a.nb * a.nb * 8 / (bw * 1e9) * 1e6 + a.lat_us, P, Q) / 1e3
+            chain = critical_path_us(NT, a.potrf_us, trsm if trsm is not None else g_us, g_us / 2 / 0.85, a.nb * a.nb * 8 / (bw * 1e9) * 1e6 + a.lat_us, P, Q) / 1e3
             print(f"{r:>5} {out['grid']:>6} {out['span_ms']:>9.1f} {out['tflops']:>9.1f} {out['tflops'] / r:>7.1f} {eff:>5.2f} {out['bulk_util']:>9.2f} {out['xgmi_GB']:>8.1f} {chain:>8.1f}")
     if a.measured_1gpu_tf:
         P, Q = grid_of(1)
-        one = simulate(NT, a.nb, P, Q, a.gemm_tf, a.potrf_us, a.link_gbs[0], a.lat_us)
+        one = simulate(NT, a.nb, P, Q, a.gemm_tf, a.potrf_us, a.link_gbs[0], a.lat_us, recv=a.recv, trsm_us=trsm)
         print(f"calibration: model 1-GPU {one['tflops']:.1f} TF vs measured {a.measured_1gpu_tf:.1f} TF ({(one['tflops'] / a.measured_1gpu_tf - 1) * 100:+.1f} %)")
 
 

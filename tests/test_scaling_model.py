@@ -67,3 +67,16 @@ ctx.fini()
     assert r.returncode == 0, r.stdout + r.stderr
     date = int(next(l for l in r.stdout.splitlines() if l.startswith("SIMDATE")).split()[1])
     assert date == sm.critical_path_exact_ns(NT, sm.simcost_ns(1024))
+
+
+def test_serial_receive_queue_never_beats_per_link():
+    """Round 5: one serial receive queue per rank (the code's fetch queue over one
+    copy-engine pull stream) can only lengthen the span against one transfer per
+    directed link; the critical-stream TRSM keeps the graph draining."""
+    NT, nb = 16, 1024
+    for r in (2, 4, 8):
+        P, Q = sm.grid_of(r)
+        link = sm.simulate(NT, nb, P, Q, gemm_tf=66.0, potrf_us=350.0, link_gbs=50.0, lat_us=25.0, recv="per-link", trsm_us=265.0)
+        ser = sm.simulate(NT, nb, P, Q, gemm_tf=66.0, potrf_us=350.0, link_gbs=50.0, lat_us=25.0, recv="serial", trsm_us=265.0)
+        assert ser["span_ms"] >= link["span_ms"] * 0.999
+        assert ser["xgmi_GB"] == link["xgmi_GB"]
