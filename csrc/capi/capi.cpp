@@ -8,6 +8,8 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <pthread.h>
+#include <sched.h>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -617,6 +619,69 @@ int32_t parsec_task_local(const parsec_task_t* task, int i) { return task->local
 const char* parsec_task_class_name(const parsec_task_t* task) { return task->task_class->name.c_str(); }
 parsec_taskpool_t* parsec_task_taskpool(const parsec_task_t* task) { return task->taskpool; }
 int parsec_execution_stream_id(const parsec_execution_stream_t* es) { return es->th_id; }
+// ----------------------------------- MCA parameters by index, topology, debug
+static std::mutex g_param_index_m;
+static std::vector<std::string> g_param_index;  // index -> full name
+int parsec_mca_param_init(void) { return PARSEC_SUCCESS; }
+int parsec_mca_param_find(const char* type, const char* component, const char* param) {
+  const std::string full = ParamRegistry::join(type ? type : "", component ? component : "", param ? param : "");
+  std::string v;
+  if (!ParamRegistry::instance().lookup(full, v)) return PARSEC_ERROR;
+  std::lock_guard<std::mutex> g(g_param_index_m);
+  for (size_t i = 0; i < g_param_index.size(); ++i)
+    if (g_param_index[i] == full) return (int)i;
+  g_param_index.push_back(full);
+  return (int)g_param_index.size() - 1;
+}
+static bool param_name(int index, std::string& full) {
+  std::lock_guard<std::mutex> g(g_param_index_m);
+  if (index < 0 || index >= (int)g_param_index.size()) return false;
+  full = g_param_index[(size_t)index];
+  return true;
+}
+int parsec_mca_param_lookup_int(int index, int* value) {
+  std::string full, v;
+  if (!value || !param_name(index, full) || !ParamRegistry::instance().lookup(full, v)) return PARSEC_ERROR;
+  *value = (int)std::strtoll(v.c_str(), nullptr, 0);
+  return PARSEC_SUCCESS;
+}
+int parsec_mca_param_set_int_index(int index, int value) {
+  std::string full;
+  if (!param_name(index, full)) return PARSEC_ERROR;
+  ParamRegistry::instance().set_override(full, std::to_string(value));
+  return PARSEC_SUCCESS;
+}
+
+int parsec_hwloc_init(void) { return PARSEC_SUCCESS; }
+int parsec_hwloc_fini(void) { return PARSEC_SUCCESS; }
+// physical cores among the allowed CPUs: a CPU counts when it is the first of
+// its SMT siblings
+static std::vector<int> physical_cpus() {
+  std::vector<int> out;
+  for (auto& c : topology_cpus()) {
+    int first = c[0];
+    if (FILE* f = std::fopen(("/sys/devices/system/cpu/cpu" + std::to_string(c[0]) + "/topology/thread_siblings_list").c_str(), "r")) {
+      if (std::fscanf(f, "%d", &first) != 1) first = c[0];
+      std::fclose(f);
+    }
+    if (first == c[0]) out.push_back(c[0]);
+  }
+  if (out.empty()) out.push_back(0);
+  return out;
+}
+int parsec_hwloc_nb_real_cores(void) { return (int)physical_cpus().size(); }
+int parsec_bindthread(int cpu, int ht) {
+  (void)ht;
+  static const std::vector<int> cpus = physical_cpus();
+  if (cpu < 0) return -1;
+  const int target = cpus[(size_t)cpu % cpus.size()];
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  CPU_SET(target, &set);
+  return pthread_setaffinity_np(pthread_self(), sizeof(set), &set) == 0 ? target : -1;
+}
+void parsec_debug_init(void) {}
+
 void parsec_obj_retain_data(parsec_data_t* d) { if (d) data_retain(d); }
 void parsec_obj_release_data(parsec_data_t* d) { if (d) data_release(d); }
 void parsec_obj_retain_copy(parsec_data_copy_t* c) { if (c) data_copy_retain(c); }

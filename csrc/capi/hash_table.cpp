@@ -2,15 +2,16 @@
 // Parity: the reference's parsec_hash_table interface (parsec/class/
 // parsec_hash_table.h:132-434) -- bucket locks held across find-then-insert,
 // handles, for_all with removal, user key functions -- over a different
-// structure: one bucket array behind a reader/writer lock, buckets with their
-// own spin locks, growth by rehashing into twice the buckets when a locked
-// insert finds the table loaded above 4 items per bucket and no bucket is held
-// (the reference chains older, smaller tables instead).
+// structure: one bucket array, buckets with their own spin locks, and a
+// holder count instead of a table lock. A thread that finds the table loaded
+// above 4 items per bucket while it holds no bucket raises the resize flag,
+// waits for the holders to drain (new entries wait; a thread already holding a
+// bucket never waits, so nested locking cannot deadlock) and rehashes into
+// twice the buckets (the reference chains older, smaller tables instead).
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <mutex>
-#include <shared_mutex>
 #include <vector>
 
 #include "../core/base.hpp"
@@ -25,14 +26,37 @@ struct Bucket {
 };
 
 struct HtImpl {
-  std::shared_mutex resize_m;  // shared: any bucket operation; exclusive: growth
+  std::atomic<int> holders{0};   // threads inside a bucket operation
+  std::atomic<int> resizing{0};  // a resize waits for holders == 0
   std::vector<Bucket> buckets;
   uint32_t nb_bits = 0;
   std::atomic<int64_t> count{0};
-  std::atomic<int64_t> capacity;  // buckets.size(): read without the lock by the growth check
+  std::atomic<int64_t> capacity;  // buckets.size(): read without entering by the growth check
   explicit HtImpl(uint32_t bits) : buckets((size_t)1 << bits), nb_bits(bits), capacity((int64_t)1 << bits) {}
   bool loaded() const { return count.load(std::memory_order_relaxed) > 4 * capacity.load(std::memory_order_relaxed); }
 };
+
+// buckets this thread holds (any table): a holder never waits for a resize
+thread_local int t_held = 0;
+
+void enter(HtImpl* h) {
+  if (t_held > 0) {
+    h->holders.fetch_add(1, std::memory_order_seq_cst);
+    ++t_held;
+    return;
+  }
+  for (;;) {
+    while (h->resizing.load(std::memory_order_acquire)) PARSEC_CPU_RELAX();
+    h->holders.fetch_add(1, std::memory_order_seq_cst);
+    if (!h->resizing.load(std::memory_order_seq_cst)) break;
+    h->holders.fetch_sub(1, std::memory_order_release);
+  }
+  ++t_held;
+}
+void leave(HtImpl* h) {
+  h->holders.fetch_sub(1, std::memory_order_release);
+  --t_held;
+}
 
 HtImpl* impl(parsec_hash_table_t* ht) { return static_cast<HtImpl*>(ht->impl); }
 
@@ -69,25 +93,29 @@ parsec_hash_table_item_t* remove_in(parsec_hash_table_t* ht, HtImpl* h, Bucket& 
   return nullptr;
 }
 
-// Grow when loaded and nobody holds a bucket (exclusive lock taken without waiting).
+// Grow when loaded, from a thread that holds no bucket.
 void maybe_grow(HtImpl* h) {
-  if (!h->loaded() || h->capacity.load(std::memory_order_relaxed) >= ((int64_t)1 << 26)) return;
-  std::unique_lock<std::shared_mutex> g(h->resize_m, std::try_to_lock);
-  if (!g.owns_lock() || !h->loaded()) return;
-  const uint32_t bits = h->nb_bits + 1;
-  std::vector<Bucket> nb((size_t)1 << bits);
-  for (Bucket& b : h->buckets)
-    for (parsec_hash_table_item_t* it = b.head; it;) {
-      parsec_hash_table_item_t* next = it->next_item;
-      Bucket& d = nb[it->hash64 & ((1ull << bits) - 1)];
-      it->next_item = d.head;
-      d.head = it;
-      ++d.n;
-      it = next;
-    }
-  h->buckets.swap(nb);
-  h->nb_bits = bits;
-  h->capacity.store((int64_t)1 << bits, std::memory_order_relaxed);
+  if (t_held > 0 || !h->loaded() || h->capacity.load(std::memory_order_relaxed) >= ((int64_t)1 << 26)) return;
+  int idle = 0;
+  if (!h->resizing.compare_exchange_strong(idle, 1, std::memory_order_seq_cst)) return;  // another thread resizes
+  while (h->holders.load(std::memory_order_seq_cst) != 0) PARSEC_CPU_RELAX();
+  if (h->loaded()) {
+    const uint32_t bits = h->nb_bits + 1;
+    std::vector<Bucket> nb((size_t)1 << bits);
+    for (Bucket& b : h->buckets)
+      for (parsec_hash_table_item_t* it = b.head; it;) {
+        parsec_hash_table_item_t* next = it->next_item;
+        Bucket& d = nb[it->hash64 & ((1ull << bits) - 1)];
+        it->next_item = d.head;
+        d.head = it;
+        ++d.n;
+        it = next;
+      }
+    h->buckets.swap(nb);
+    h->nb_bits = bits;
+    h->capacity.store((int64_t)1 << bits, std::memory_order_relaxed);
+  }
+  h->resizing.store(0, std::memory_order_release);
 }
 
 }  // namespace
@@ -112,7 +140,7 @@ void parsec_hash_table_fini(parsec_hash_table_t* ht) {
 void parsec_hash_table_lock_bucket(parsec_hash_table_t* ht, parsec_key_t key) {
   HtImpl* h = impl(ht);
   maybe_grow(h);
-  h->resize_m.lock_shared();
+  enter(h);
   bucket_of(h, hash_of(ht, key)).m.lock();
 }
 
@@ -121,13 +149,13 @@ void parsec_hash_table_unlock_bucket_impl(parsec_hash_table_t* ht, parsec_key_t 
   (void)line;
   HtImpl* h = impl(ht);
   bucket_of(h, hash_of(ht, key)).m.unlock();
-  h->resize_m.unlock_shared();
+  leave(h);
 }
 
 void parsec_hash_table_lock_bucket_handle(parsec_hash_table_t* ht, parsec_key_t key, parsec_key_handle_t* handle) {
   HtImpl* h = impl(ht);
   maybe_grow(h);
-  h->resize_m.lock_shared();
+  enter(h);
   handle->key = key;
   handle->hash64 = hash_of(ht, key);
   Bucket& b = bucket_of(h, handle->hash64);
@@ -139,7 +167,7 @@ void parsec_hash_table_unlock_bucket_handle_impl(parsec_hash_table_t* ht, parsec
   (void)file;
   (void)line;
   static_cast<Bucket*>(handle->bucket)->m.unlock();
-  impl(ht)->resize_m.unlock_shared();
+  leave(impl(ht));
 }
 
 void parsec_hash_table_nolock_insert(parsec_hash_table_t* ht, parsec_hash_table_item_t* item) {
@@ -207,24 +235,27 @@ void* parsec_hash_table_item_lookup(parsec_hash_table_t* ht, parsec_hash_table_i
 
 void parsec_hash_table_for_all(parsec_hash_table_t* ht, parsec_hash_elem_fct_t fct, void* cb_data) {
   HtImpl* h = impl(ht);
-  std::shared_lock<std::shared_mutex> g(h->resize_m);
+  enter(h);
   for (Bucket& b : h->buckets)
     for (parsec_hash_table_item_t* it = b.head; it;) {
       parsec_hash_table_item_t* next = it->next_item;  // fct may remove (and free) it
       fct(object_of(ht, it), cb_data);
       it = next;
     }
+  leave(h);
 }
 
 void parsec_hash_table_stat(parsec_hash_table_t* ht) {
   HtImpl* h = impl(ht);
-  std::shared_lock<std::shared_mutex> g(h->resize_m);
+  enter(h);
   int32_t longest = 0, used = 0;
   for (Bucket& b : h->buckets) {
     longest = std::max(longest, b.n);
     used += b.n > 0;
   }
-  std::printf("hash table %p: %lld items in %zu buckets (%d used, longest chain %d)\n", (void*)ht, (long long)h->count.load(), h->buckets.size(), used,
+  const size_t nbuckets = h->buckets.size();
+  leave(h);
+  std::printf("hash table %p: %lld items in %zu buckets (%d used, longest chain %d)\n", (void*)ht, (long long)h->count.load(), nbuckets, used,
               longest);
 }
 

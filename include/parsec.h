@@ -266,6 +266,22 @@ int parsec_dependencies_mark_task_as_startup(parsec_task_t* task, parsec_executi
 int parsec_mca_param_set_string(const char* name, const char* value);
 int parsec_mca_param_set_int(const char* name, int64_t value);
 int parsec_mca_param_get_int(const char* name, int64_t* value);
+/* by index, as the reference's utils/mca_param.h: find returns the index of a
+ * registered parameter type_component_name (component may be NULL) or
+ * PARSEC_ERROR; lookup_int reads it */
+int parsec_mca_param_init(void);
+int parsec_mca_param_find(const char* type, const char* component, const char* param);
+int parsec_mca_param_lookup_int(int index, int* value);
+int parsec_mca_param_set_int_index(int index, int value);
+
+/* ------------------------------------------------ topology / threads / debug
+ * (reference parsec_hwloc.h, bindthread.h, utils/debug.h): the runtime's own
+ * /sys topology discovery, no hwloc */
+int parsec_hwloc_init(void);
+int parsec_hwloc_fini(void);
+int parsec_hwloc_nb_real_cores(void);       /* allowed CPUs, one per physical core */
+int parsec_bindthread(int cpu, int ht);      /* pin the calling thread; returns the CPU id or -1 */
+void parsec_debug_init(void);
 
 /* ---------------------------------------------------- data collections */
 typedef struct parsec_data_collection_s parsec_data_collection_t;
@@ -794,6 +810,8 @@ void parsec_profiling_trace_f08(int key, int64_t event_id, int taskpool_id, int*
  * not a handle): the reference's wrappers free it in their destructors. The
  * datatype belongs to its arena datatype, which the runtime releases. */
 inline int parsec_type_free(parsec::Datatype*) { return PARSEC_SUCCESS; }
+/* the reference's index form of parsec_mca_param_set_int */
+inline int parsec_mca_param_set_int(int index, int value) { return parsec_mca_param_set_int_index(index, value); }
 /* the same datatype where the reference passes opaque_dtt by value */
 parsec_data_copy_t* parsec_data_copy_new(parsec_data_t* data, int device, const parsec::Datatype& dtt, uint32_t flags);
 #include <memory>

@@ -15,6 +15,9 @@ static inline int32_t parsec_atomic_fetch_dec_int32(volatile int32_t* l) { retur
 static inline int32_t parsec_atomic_fetch_or_int32(volatile int32_t* l, int32_t v) { return __atomic_fetch_or(l, v, __ATOMIC_SEQ_CST); }
 static inline int32_t parsec_atomic_fetch_and_int32(volatile int32_t* l, int32_t v) { return __atomic_fetch_and(l, v, __ATOMIC_SEQ_CST); }
 static inline int64_t parsec_atomic_fetch_add_int64(volatile int64_t* l, int64_t v) { return __atomic_fetch_add(l, v, __ATOMIC_SEQ_CST); }
+static inline int64_t parsec_atomic_fetch_sub_int64(volatile int64_t* l, int64_t v) { return __atomic_fetch_sub(l, v, __ATOMIC_SEQ_CST); }
+static inline int64_t parsec_atomic_fetch_or_int64(volatile int64_t* l, int64_t v) { return __atomic_fetch_or(l, v, __ATOMIC_SEQ_CST); }
+static inline int64_t parsec_atomic_fetch_and_int64(volatile int64_t* l, int64_t v) { return __atomic_fetch_and(l, v, __ATOMIC_SEQ_CST); }
 static inline int64_t parsec_atomic_fetch_inc_int64(volatile int64_t* l) { return __atomic_fetch_add(l, 1, __ATOMIC_SEQ_CST); }
 static inline int64_t parsec_atomic_fetch_dec_int64(volatile int64_t* l) { return __atomic_fetch_sub(l, 1, __ATOMIC_SEQ_CST); }
 static inline int parsec_atomic_cas_int32(volatile int32_t* l, int32_t o, int32_t n) {

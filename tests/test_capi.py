@@ -278,3 +278,30 @@ def test_reference_tree_dist_collection(tmp_path, pa):
     assert "tree_dist ok" in r.stdout
     text = dot.read_text()
     assert text.startswith("digraph G {") and text.count("->") == 62
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/tests/class"), reason="reference tree not present")
+@pytest.mark.parametrize("prog,args,check", [
+    ("hash", ["-#", "65536", "-r", "4", "-n"], "threads"),
+    ("hash", ["-#", "65536", "-r", "4", "-n", "-H"], "threads"),
+    ("atomics", ["-c", "4"], "No error in integer operation on 64 bits"),
+    ("rwlock", ["-c", "4"], None),
+], ids=["hash", "hash-handles", "atomics", "rwlock"])
+def test_reference_class_programs(tmp_path, pa, prog, args, check):
+    """The reference's tests/class programs (Testings.cmake: hash -# 65536 -r 4 -n,
+    atomics -c 4, rwlock -c 4), compiled unmodified against include/: the
+    public hash table under concurrent find-then-insert / remove with and
+    without bucket handles (every inconsistency is printed as 'Error in
+    implementation'), the C atomics and the reader / writer lock, with the
+    barrier / bindthread / timing / hwloc / MCA-index helpers they use."""
+    ref = "/root/reference"
+    exe = tmp_path / prog
+    cmd = ["g++", "-x", "c++", "-std=c++20", "-fpermissive", "-w", "-O1", "-pthread", f"-I{ROOT}/include", f"-I{ref}",
+           os.path.join(ref, "tests/class", prog + ".c"), "-o", str(exe), *_LINK]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([str(exe), *args], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "Error in implementation" not in r.stdout + r.stderr
+    if check:
+        assert check in r.stdout + r.stderr, r.stdout[-2000:]
