@@ -60,11 +60,6 @@
 #define PARSEC_ERR_NOT_SUPPORTED (-2)
 #define PARSEC_ERR_NOT_FOUND (-13)
 
-/* A class instance names a taskpool type's constructor / destructor (e.g. a
- * wrapper's destructor that frees the datatypes of its arenas). The runtime
- * releases a taskpool's arenas and datatypes itself when it is freed, so the
- * declaration only has to compile. */
-#define PARSEC_OBJ_CLASS_INSTANCE(NAME, PARENT, CTOR, DTOR) struct parsec_obj_class_instance_##NAME##_s
 
 /* device types (reference mca/device/device.h) */
 #define PARSEC_DEV_NONE 0x00
@@ -113,36 +108,125 @@ typedef struct parsec_thread_mempool_s parsec_thread_mempool_t;
 
 typedef uint64_t parsec_data_key_t;
 
-/* Object-system reference counts (reference parsec/class/parsec_object.h).
- * Data and data copies are reference counted by the runtime: RETAIN / RELEASE
- * on a parsec_data_t* or parsec_data_copy_t* take / drop a reference (a body
- * that keeps a NEW tile past its task, haar_tree/project.jdf:199 +
- * tree_dist.c:168). Every other object of this API is kept alive by the
- * runtime's own counts (an arena is shared by every copy of its
- * parsec_arena_datatype_t, a taskpool's arenas_datatypes hold their own
- * references) or released by the explicit *_destroy / *_free calls: for them
- * the macros accept the pair and do nothing. */
+/* ---------------------------------------------------------- object system
+ * (reference parsec/class/parsec_object.h: classes with a parent, constructor
+ * and destructor; objects start with a parsec_object_t and carry a reference
+ * count). PARSEC_OBJ_NEW allocates and constructs (parents' constructors
+ * first), PARSEC_OBJ_CONSTRUCT / DESTRUCT work in place, RETAIN / RELEASE
+ * count references and RELEASE to zero destructs and frees.
+ * The runtime's own objects are not parsec_object_t: data and data copies keep
+ * their runtime reference counts (RETAIN / RELEASE on a parsec_data_t* or
+ * parsec_data_copy_t* take / drop one, e.g. a body keeping a NEW tile past its
+ * task: haar_tree/project.jdf:199, tree_dist.c:168; PARSEC_OBJ_NEW of either
+ * makes a runtime object), and for every other runtime handle (taskpools,
+ * arenas) the macros do nothing -- those are released by their *_free calls.
+ * Implementation: csrc/capi/object.cpp; containers: class/list.h, lifo.h,
+ * fifo.h, dequeue.h. */
+typedef struct parsec_object_t parsec_object_t;
+typedef struct parsec_class_t parsec_class_t;
+typedef void (*parsec_construct_t)(parsec_object_t* obj);
+typedef void (*parsec_destruct_t)(parsec_object_t* obj);
+#define PARSEC_OBJ_MAX_DEPTH 16
+struct parsec_class_t {
+  const char* cls_name;
+  parsec_class_t* cls_parent;
+  parsec_construct_t cls_construct;
+  parsec_destruct_t cls_destruct;
+  volatile int32_t cls_initialized;  /* 0 no, 1 in progress, 2 done */
+  int32_t cls_depth;
+  parsec_construct_t cls_construct_array[PARSEC_OBJ_MAX_DEPTH + 1];  /* root first, NULL-terminated */
+  parsec_destruct_t cls_destruct_array[PARSEC_OBJ_MAX_DEPTH + 1];    /* leaf first, NULL-terminated */
+  size_t cls_sizeof;
+};
+struct parsec_object_t {
+  parsec_class_t* obj_class;
+  volatile int32_t obj_reference_count;
+};
+/* containers of class/ (forward: the RETAIN / RELEASE dispatch names them) */
+typedef struct parsec_list_item_s parsec_list_item_t;
+typedef struct parsec_list_s parsec_list_t;
+typedef struct parsec_lifo_s parsec_lifo_t;
+typedef parsec_list_t parsec_fifo_t;
+typedef parsec_list_t parsec_dequeue_t;
+
+#define PARSEC_OBJ_CLASS(NAME) (&(NAME##_class))
+#define PARSEC_OBJ_CLASS_DECLARATION(NAME) extern parsec_class_t NAME##_class
+#define PARSEC_OBJ_CLASS_INSTANCE(NAME, PARENT, CONSTRUCTOR, DESTRUCTOR) \
+  parsec_class_t NAME##_class = {#NAME, PARSEC_OBJ_CLASS(PARENT), (parsec_construct_t)(CONSTRUCTOR), (parsec_destruct_t)(DESTRUCTOR), 0, 0, {0}, {0}, sizeof(NAME)}
+PARSEC_OBJ_CLASS_DECLARATION(parsec_object_t);
+PARSEC_OBJ_CLASS_DECLARATION(parsec_taskpool_t);   /* parent of the reference's taskpool wrapper classes */
+PARSEC_OBJ_CLASS_DECLARATION(parsec_data_t);       /* PARSEC_OBJ_NEW: a runtime Data */
+PARSEC_OBJ_CLASS_DECLARATION(parsec_data_copy_t);  /* PARSEC_OBJ_NEW: a runtime DataCopy */
+PARSEC_OBJ_CLASS_DECLARATION(parsec_list_item_t);
+PARSEC_OBJ_CLASS_DECLARATION(parsec_list_t);
+PARSEC_OBJ_CLASS_DECLARATION(parsec_lifo_t);
+PARSEC_OBJ_CLASS_DECLARATION(parsec_fifo_t);
+PARSEC_OBJ_CLASS_DECLARATION(parsec_dequeue_t);
+
+void* parsec_obj_new_of(parsec_class_t* cls);
+void parsec_obj_construct_as(parsec_object_t* obj, parsec_class_t* cls);
+void parsec_obj_destruct_obj(parsec_object_t* obj);
+void parsec_obj_retain_object(parsec_object_t* obj);
+int parsec_obj_release_object(parsec_object_t* obj);  /* 1 when this release destroyed it */
 void parsec_obj_retain_data(parsec_data_t* d);
 void parsec_obj_release_data(parsec_data_t* d);
 void parsec_obj_retain_copy(parsec_data_copy_t* c);
 void parsec_obj_release_copy(parsec_data_copy_t* c);
 static inline void parsec_obj_keep_none(const volatile void* o) { (void)o; }
+static inline void parsec_obj_retain_item(parsec_list_item_t* o) { parsec_obj_retain_object((parsec_object_t*)o); }
+static inline void parsec_obj_release_item(parsec_list_item_t* o) { parsec_obj_release_object((parsec_object_t*)o); }
+static inline void parsec_obj_retain_list(parsec_list_t* o) { parsec_obj_retain_object((parsec_object_t*)o); }
+static inline void parsec_obj_release_list(parsec_list_t* o) { parsec_obj_release_object((parsec_object_t*)o); }
+static inline void parsec_obj_retain_lifo(parsec_lifo_t* o) { parsec_obj_retain_object((parsec_object_t*)o); }
+static inline void parsec_obj_release_lifo(parsec_lifo_t* o) { parsec_obj_release_object((parsec_object_t*)o); }
+static inline void parsec_obj_release_pobj(parsec_object_t* o) { parsec_obj_release_object(o); }
+
+#define PARSEC_OBJ_NEW(type) ((type*)parsec_obj_new_of(PARSEC_OBJ_CLASS(type)))
+#define PARSEC_OBJ_CONSTRUCT(obj, type) parsec_obj_construct_as((parsec_object_t*)(obj), PARSEC_OBJ_CLASS(type))
+#define PARSEC_OBJ_DESTRUCT(obj) parsec_obj_destruct_obj((parsec_object_t*)(obj))
 #ifdef __cplusplus
 }  /* extern "C" */
+#include <type_traits>
+#include <utility>
+namespace parsec_obj_detail {
+/* a C "subclass": its first member `super` is (a subclass of) parsec_object_t */
+template <class T, class = void>
+struct is_object : std::false_type {};
+template <>
+struct is_object<parsec_object_t> : std::true_type {};
+template <class T>
+struct is_object<T, std::void_t<decltype(std::declval<T&>().super)>>
+    : is_object<std::remove_cv_t<std::remove_reference_t<decltype(std::declval<T&>().super)>>> {};
+}  // namespace parsec_obj_detail
 inline void parsec_obj_retain(parsec_data_t* d) { parsec_obj_retain_data(d); }
 inline void parsec_obj_retain(parsec_data_copy_t* c) { parsec_obj_retain_copy(c); }
-template <class T> inline void parsec_obj_retain(T&&) {}
+template <class T>
+inline void parsec_obj_retain(T* o) {
+  if constexpr (parsec_obj_detail::is_object<std::remove_cv_t<T>>::value) parsec_obj_retain_object((parsec_object_t*)o);
+}
+template <class T>
+inline void parsec_obj_retain(T&&) {}
 inline void parsec_obj_release(parsec_data_t* d) { parsec_obj_release_data(d); }
 inline void parsec_obj_release(parsec_data_copy_t* c) { parsec_obj_release_copy(c); }
-template <class T> inline void parsec_obj_release(T&&) {}
+template <class T>
+inline void parsec_obj_release(T* o) {
+  if constexpr (parsec_obj_detail::is_object<std::remove_cv_t<T>>::value) parsec_obj_release_object((parsec_object_t*)o);
+}
+template <class T>
+inline void parsec_obj_release(T&&) {}
 #define PARSEC_OBJ_RETAIN(obj) parsec_obj_retain(obj)
+/* as the reference's: the pointer is NULL afterwards when it named an object */
 #define PARSEC_OBJ_RELEASE(obj) parsec_obj_release(obj)
 extern "C" {
 #else
-#define PARSEC_OBJ_RETAIN(obj) \
-  _Generic((obj), parsec_data_t*: parsec_obj_retain_data, parsec_data_copy_t*: parsec_obj_retain_copy, default: parsec_obj_keep_none)(obj)
-#define PARSEC_OBJ_RELEASE(obj) \
-  _Generic((obj), parsec_data_t*: parsec_obj_release_data, parsec_data_copy_t*: parsec_obj_release_copy, default: parsec_obj_keep_none)(obj)
+#define PARSEC_OBJ_RETAIN(obj)                                                                                       \
+  _Generic((obj), parsec_data_t*: parsec_obj_retain_data, parsec_data_copy_t*: parsec_obj_retain_copy,             \
+           parsec_object_t*: parsec_obj_retain_object, parsec_list_item_t*: parsec_obj_retain_item,                \
+           parsec_list_t*: parsec_obj_retain_list, parsec_lifo_t*: parsec_obj_retain_lifo, default: parsec_obj_keep_none)(obj)
+#define PARSEC_OBJ_RELEASE(obj)                                                                                      \
+  _Generic((obj), parsec_data_t*: parsec_obj_release_data, parsec_data_copy_t*: parsec_obj_release_copy,           \
+           parsec_object_t*: parsec_obj_release_pobj, parsec_list_item_t*: parsec_obj_release_item,                \
+           parsec_list_t*: parsec_obj_release_list, parsec_lifo_t*: parsec_obj_release_lifo, default: parsec_obj_keep_none)(obj)
 #endif
 
 /* diagnostics (reference parsec/utils/debug.h): this process' rank and the
@@ -231,9 +315,22 @@ int parsec_execution_stream_id(const parsec_execution_stream_t* es);
  * calls this on it; its body then runs again (DONE completes it, ASYNC parks it
  * again). distance: 0 = the calling stream's own queue, > 0 further away. */
 int __parsec_schedule(parsec_execution_stream_t* es, parsec_task_t* task, int32_t distance);
-/* Tasks are not list items in this API (the scheduler queues them through its
- * own links): the reference's reset of a task's list links is a no-op here. */
-#define PARSEC_LIST_ITEM_SINGLETON(item) ((void)(item))
+/* Reset an item's list links to itself (class/list_item.h). Tasks are not list
+ * items in this API (the scheduler queues them through its own links): on a
+ * task, as the reference's bodies apply it, it does nothing. */
+void parsec_list_item_singleton(parsec_list_item_t* item);
+#ifdef __cplusplus
+}  /* extern "C" */
+inline void parsec_list_item_singleton_any(parsec_list_item_t* item) { parsec_list_item_singleton(item); }
+template <class T>
+inline void parsec_list_item_singleton_any(T* item) {
+  if constexpr (std::is_same_v<std::remove_cv_t<T>, parsec_list_item_t>) parsec_list_item_singleton((parsec_list_item_t*)item);
+}
+#define PARSEC_LIST_ITEM_SINGLETON(item) parsec_list_item_singleton_any(item)
+extern "C" {
+#else
+#define PARSEC_LIST_ITEM_SINGLETON(item) _Generic((item), parsec_list_item_t*: parsec_list_item_singleton, default: parsec_obj_keep_none)(item)
+#endif
 
 /* The vocabulary of the reference's generated code that user functions of a
  * JDF program against (jdf2c output: tests/apps/haar_tree/project.jdf,

@@ -286,14 +286,18 @@ def test_reference_tree_dist_collection(tmp_path, pa):
     ("hash", ["-#", "65536", "-r", "4", "-n", "-H"], "threads"),
     ("atomics", ["-c", "4"], "No error in integer operation on 64 bits"),
     ("rwlock", ["-c", "4"], None),
-], ids=["hash", "hash-handles", "atomics", "rwlock"])
+    ("lifo", ["-c", "4"], "all tests passed"),
+    ("list", ["-c", "4"], "all tests passed"),
+], ids=["hash", "hash-handles", "atomics", "rwlock", "lifo", "list"])
 def test_reference_class_programs(tmp_path, pa, prog, args, check):
     """The reference's tests/class programs (Testings.cmake: hash -# 65536 -r 4 -n,
-    atomics -c 4, rwlock -c 4), compiled unmodified against include/: the
-    public hash table under concurrent find-then-insert / remove with and
+    atomics / rwlock / lifo / list -c 4), compiled unmodified against include/:
+    the public hash table under concurrent find-then-insert / remove with and
     without bucket handles (every inconsistency is printed as 'Error in
-    implementation'), the C atomics and the reader / writer lock, with the
-    barrier / bindthread / timing / hwloc / MCA-index helpers they use."""
+    implementation'), the C atomics, the reader / writer lock, the object
+    system (PARSEC_OBJ_CONSTRUCT) with the lock-free LIFO (tagged head, aligned
+    items) and the locked list (sort by priority offset), with the barrier /
+    bindthread / timing / hwloc / MCA-index helpers they use."""
     ref = "/root/reference"
     exe = tmp_path / prog
     cmd = ["g++", "-x", "c++", "-std=c++20", "-fpermissive", "-w", "-O1", "-pthread", f"-I{ROOT}/include", f"-I{ref}",
