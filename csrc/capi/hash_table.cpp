@@ -249,9 +249,12 @@ void parsec_hash_table_stat(parsec_hash_table_t* ht) {
   HtImpl* h = impl(ht);
   enter(h);
   int32_t longest = 0, used = 0;
-  for (Bucket& b : h->buckets) {
-    longest = std::max(longest, b.n);
-    used += b.n > 0;
+  for (Bucket& b : h->buckets) {  // other threads may be inserting: read each count under its lock
+    b.m.lock();
+    const int32_t n = b.n;
+    b.m.unlock();
+    longest = std::max(longest, n);
+    used += n > 0;
   }
   const size_t nbuckets = h->buckets.size();
   leave(h);

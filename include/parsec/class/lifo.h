@@ -26,7 +26,7 @@ static inline int parsec_lifo_nolock_is_empty(parsec_lifo_t* l) { return parsec_
 static inline void parsec_lifo_push(parsec_lifo_t* l, parsec_list_item_t* it) {
   uint64_t old = __atomic_load_n(&l->lifo_head, __ATOMIC_RELAXED), nw;
   do {
-    it->list_next = parsec_lifo_head_item(old);
+    __atomic_store_n(&it->list_next, parsec_lifo_head_item(old), __ATOMIC_RELAXED);
     nw = ((old & ~PARSEC_LIFO_PTR_MASK) + PARSEC_LIFO_TAG_ONE) | ((uint64_t)(uintptr_t)it & PARSEC_LIFO_PTR_MASK);
   } while (!__atomic_compare_exchange_n(&l->lifo_head, &old, nw, 1, __ATOMIC_RELEASE, __ATOMIC_RELAXED));
 }
@@ -34,7 +34,7 @@ static inline void parsec_lifo_push(parsec_lifo_t* l, parsec_list_item_t* it) {
 static inline void parsec_lifo_chain(parsec_lifo_t* l, parsec_list_item_t* first, parsec_list_item_t* last) {
   uint64_t old = __atomic_load_n(&l->lifo_head, __ATOMIC_RELAXED), nw;
   do {
-    last->list_next = parsec_lifo_head_item(old);
+    __atomic_store_n(&last->list_next, parsec_lifo_head_item(old), __ATOMIC_RELAXED);
     nw = ((old & ~PARSEC_LIFO_PTR_MASK) + PARSEC_LIFO_TAG_ONE) | ((uint64_t)(uintptr_t)first & PARSEC_LIFO_PTR_MASK);
   } while (!__atomic_compare_exchange_n(&l->lifo_head, &old, nw, 1, __ATOMIC_RELEASE, __ATOMIC_RELAXED));
 }
@@ -44,9 +44,12 @@ static inline parsec_list_item_t* parsec_lifo_pop(parsec_lifo_t* l) {
   do {
     it = parsec_lifo_head_item(old);
     if (!it) return NULL;
-    nw = ((old & ~PARSEC_LIFO_PTR_MASK) + PARSEC_LIFO_TAG_ONE) | ((uint64_t)(uintptr_t)it->list_next & PARSEC_LIFO_PTR_MASK);
+    /* `it` may be popped and pushed again meanwhile: the read races by design,
+       the counter in the head makes the swap below fail then */
+    nw = ((old & ~PARSEC_LIFO_PTR_MASK) + PARSEC_LIFO_TAG_ONE) |
+         ((uint64_t)(uintptr_t)__atomic_load_n(&it->list_next, __ATOMIC_RELAXED) & PARSEC_LIFO_PTR_MASK);
   } while (!__atomic_compare_exchange_n(&l->lifo_head, &old, nw, 1, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE));
-  it->list_next = it;
+  __atomic_store_n(&it->list_next, it, __ATOMIC_RELAXED);
   return it;
 }
 static inline parsec_list_item_t* parsec_lifo_try_pop(parsec_lifo_t* l) { return parsec_lifo_pop(l); }
