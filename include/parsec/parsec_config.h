@@ -5,5 +5,8 @@
 #define PARSEC_AMD_COMPAT_PARSEC_CONFIG_H
 #include "../parsec.h"
 #define PARSEC_HAVE_HIP 1
+#ifndef PARSEC_DECLSPEC
+#define PARSEC_DECLSPEC /* symbols are exported by default */
+#endif
 #define PARSEC_DIST_COLLECTIVES 1
 #endif

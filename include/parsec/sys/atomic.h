@@ -29,6 +29,17 @@ static inline int parsec_atomic_cas_int64(volatile int64_t* l, int64_t o, int64_
 static inline int parsec_atomic_cas_ptr(volatile void* l, void* o, void* n) {
   return __atomic_compare_exchange_n((void* volatile*)l, &o, n, 0, __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST);
 }
+/* spin lock on one word (reference parsec_atomic_lock_t) */
+typedef volatile int32_t parsec_atomic_lock_t;
+#define PARSEC_ATOMIC_UNLOCKED 0
+#define PARSEC_ATOMIC_LOCKED 1
+static inline void parsec_atomic_lock_init(parsec_atomic_lock_t* l) { __atomic_store_n(l, 0, __ATOMIC_RELEASE); }
+static inline int parsec_atomic_trylock(parsec_atomic_lock_t* l) { return __atomic_exchange_n(l, 1, __ATOMIC_ACQUIRE) == 0; }
+static inline void parsec_atomic_lock(parsec_atomic_lock_t* l) {
+  while (__atomic_exchange_n(l, 1, __ATOMIC_ACQUIRE))
+    while (__atomic_load_n(l, __ATOMIC_RELAXED)) {}
+}
+static inline void parsec_atomic_unlock(parsec_atomic_lock_t* l) { __atomic_store_n(l, 0, __ATOMIC_RELEASE); }
 static inline void parsec_atomic_wmb(void) { __atomic_thread_fence(__ATOMIC_RELEASE); }
 static inline void parsec_atomic_rmb(void) { __atomic_thread_fence(__ATOMIC_ACQUIRE); }
 static inline void parsec_mfence(void) { __atomic_thread_fence(__ATOMIC_SEQ_CST); }

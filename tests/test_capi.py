@@ -288,7 +288,9 @@ def test_reference_tree_dist_collection(tmp_path, pa):
     ("rwlock", ["-c", "4"], None),
     ("lifo", ["-c", "4"], "all tests passed"),
     ("list", ["-c", "4"], "all tests passed"),
-], ids=["hash", "hash-handles", "atomics", "rwlock", "lifo", "list"])
+    ("future", ["-c", "4"], "countable future successfully triggered"),
+    ("future_datacopy", [], "Nested parsec_datacopy_future validated"),
+], ids=["hash", "hash-handles", "atomics", "rwlock", "lifo", "list", "future", "future_datacopy"])
 def test_reference_class_programs(tmp_path, pa, prog, args, check):
     """The reference's tests/class programs (Testings.cmake: hash -# 65536 -r 4 -n,
     atomics / rwlock / lifo / list -c 4), compiled unmodified against include/:
@@ -296,7 +298,8 @@ def test_reference_class_programs(tmp_path, pa, prog, args, check):
     without bucket handles (every inconsistency is printed as 'Error in
     implementation'), the C atomics, the reader / writer lock, the object
     system (PARSEC_OBJ_CONSTRUCT) with the lock-free LIFO (tagged head, aligned
-    items) and the locked list (sort by priority offset), with the barrier /
+    items) and the locked list (sort by priority offset), base / countable /
+    datacopy futures with nested futures (future / future_datacopy), with the barrier /
     bindthread / timing / hwloc / MCA-index helpers they use."""
     ref = "/root/reference"
     exe = tmp_path / prog

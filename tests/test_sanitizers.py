@@ -165,7 +165,8 @@ def test_hash_table_sanitized(sanitized, tmp_path):
 
 
 @pytest.mark.skipif(not os.path.isdir(REF + "/tests/class"), reason="reference tree not present")
-@pytest.mark.parametrize("prog,args", [("hash", ["-#", "16384", "-r", "2", "-n", "-c", "4"]), ("lifo", ["-c", "4"]), ("list", ["-c", "4"])])
+@pytest.mark.parametrize("prog,args", [("hash", ["-#", "16384", "-r", "2", "-n", "-c", "4"]), ("lifo", ["-c", "4"]), ("list", ["-c", "4"]),
+                                       ("future", ["-c", "4"]), ("future_datacopy", [])])
 def test_reference_class_programs_sanitized(sanitized, tmp_path, prog, args):
     """The reference's tests/class hash / lifo / list (unmodified) against the
     instrumented library: bucket locking and growth, the tagged-head LIFO, the
