@@ -256,6 +256,12 @@ dtd::DtdTaskpool* as_dtd(parsec_taskpool_t* tp) {
   return d;
 }
 
+dtd::DtdTaskClass* as_dtd_class(dtd::DtdTaskpool* d, parsec_task_class_t* tc) {
+  auto* c = dynamic_cast<dtd::DtdTaskClass*>(tc);
+  if (!c || c->owner != d) fatal("task class %s is not a task class of this DTD taskpool", tc ? tc->name.c_str() : "(null)");
+  return c;
+}
+
 struct PendingArgs {
   std::vector<dtd::Arg> args;
   std::vector<std::pair<int, int>> sig;
@@ -712,6 +718,7 @@ int parsec_dependencies_mark_task_as_startup(parsec_task_t* task, parsec_executi
   return PARSEC_SUCCESS;
 }
 
+int __parsec_complete_execution(parsec_execution_stream_t* es, parsec_task_t* task) { return complete_async_task(es ? es : my_execution_stream(), task); }
 int __parsec_schedule(parsec_execution_stream_t* es, parsec_task_t* task, int32_t distance) {
   if (!task) return PARSEC_ERROR;
   return schedule_async_task(es ? es : my_execution_stream(), task, distance);
@@ -1271,6 +1278,23 @@ int parsec_dtd_destroy_arena_datatype(parsec_context_t* ctx, int id) {
   std::lock_guard<std::mutex> g(g_dtd_adt_m);
   return g_dtd_adts.erase(id) ? PARSEC_SUCCESS : PARSEC_ERR_NOT_FOUND;
 }
+// Tiles of parsec_dtd_tile_new(tp, rank) get their storage at their first
+// insertion: the size of the arena datatype that argument names (REGION bits).
+static void size_new_tiles(dtd::DtdTaskpool* d, const PendingArgs& pa) {
+  for (const dtd::Arg& a : pa.args) {
+    if (!a.tile || !a.tile->unsized) continue;
+    const int id = a.op & dtd::REGION_MASK;
+    size_t bytes = 0;
+    {
+      std::lock_guard<std::mutex> g(g_dtd_adt_m);
+      auto it = g_dtd_adts.find(id);
+      if (it != g_dtd_adts.end() && it->second->arena) bytes = it->second->arena->elem_size;
+    }
+    if (!bytes) fatal("a tile of parsec_dtd_tile_new is first used without an arena datatype in its flags (region %d): its size is unknown", id);
+    d->tile_materialize(a.tile, bytes);
+  }
+}
+
 void parsec_output(int output_id, const char* fmt, ...) {
   (void)output_id;
   va_list ap;
@@ -1364,6 +1388,7 @@ static void dtd_insert(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, in
       tc = it->second;
     }
   }
+  size_new_tiles(d, pa);
   t_last_dtd = d;
   d->insert_task(tc, priority, pa.args);
 }
@@ -1430,7 +1455,7 @@ void parsec_dtd_insert_task_array(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* f
 // Pointer to argument i of a running DTD task (value, scratch or tile data).
 void* parsec_dtd_task_arg(parsec_task_t* this_task, int i) { return dtd::task_arg(this_task, i); }
 
-parsec_dtd_task_class_t* parsec_dtd_create_task_class(parsec_taskpool_t* tp, const char* name, ...) {
+parsec_task_class_t* parsec_dtd_create_task_class(parsec_taskpool_t* tp, const char* name, ...) {
   auto* d = as_dtd(tp);
   std::vector<std::pair<int, int>> sig;
   va_list ap;
@@ -1442,11 +1467,27 @@ parsec_dtd_task_class_t* parsec_dtd_create_task_class(parsec_taskpool_t* tp, con
     sig.push_back({flags, size});
   }
   va_end(ap);
-  return reinterpret_cast<parsec_dtd_task_class_t*>(d->create_task_class(name, sig));
+  return d->create_task_class(name, sig);
 }
-int parsec_dtd_task_class_add_chore(parsec_taskpool_t* tp, parsec_dtd_task_class_t* tcp, int device_type, void* function) {
+void parsec_dtd_task_class_release(parsec_taskpool_t* tp, parsec_task_class_t* tc) {
+  // the class belongs to its taskpool (freed with it); the program's handle
+  // needs no bookkeeping of its own
+  (void)as_dtd(tp);
+  (void)tc;
+}
+parsec_taskpool_t* parsec_dtd_get_taskpool(parsec_task_t* this_task) { return this_task ? this_task->taskpool : nullptr; }
+// detach from the context (reference insert_function.c:215-237): the program
+// gives up inserting; the taskpool terminates once its tasks are done, without
+// waiting here
+int parsec_dtd_dequeue_taskpool(parsec_taskpool_t* tp) {
   auto* d = as_dtd(tp);
-  auto* tc = reinterpret_cast<dtd::DtdTaskClass*>(tcp);
+  if (!d->context) return PARSEC_ERR_NOT_SUPPORTED;
+  d->release_hold();
+  return PARSEC_SUCCESS;
+}
+int parsec_dtd_task_class_add_chore(parsec_taskpool_t* tp, parsec_task_class_t* tcp, int device_type, void* function) {
+  auto* d = as_dtd(tp);
+  auto* tc = as_dtd_class(d, tcp);
   if (device_type == PARSEC_DEV_HIP) {
     auto* gfn = reinterpret_cast<parsec_dtd_gpu_funcptr_t*>(function);
     return d->add_chore(tc, DEV_HIP, nullptr, [gfn](GpuExecContext* c, Task* t) {
@@ -1459,12 +1500,12 @@ int parsec_dtd_task_class_add_chore(parsec_taskpool_t* tp, parsec_dtd_task_class
   auto* fn = reinterpret_cast<parsec_dtd_funcptr_t*>(function);
   return d->add_chore(tc, (uint32_t)device_type, [fn](ExecutionStream* es, Task* t) { return fn(es, t); }, nullptr);
 }
-void parsec_dtd_insert_task_with_task_class(parsec_taskpool_t* tp, parsec_dtd_task_class_t* tcp, int priority, int device_type, ...) {
+void parsec_dtd_insert_task_with_task_class(parsec_taskpool_t* tp, parsec_task_class_t* tcp, int priority, int device_type, ...) {
   // arguments are (flags, pointer) pairs: the class signature gives each one's
   // access mode and size, the flags add PUSHOUT / AFFINITY / ... (reference
   // insert_function.c:3256-3314)
   auto* d = as_dtd(tp);
-  auto* tc = reinterpret_cast<dtd::DtdTaskClass*>(tcp);
+  auto* tc = as_dtd_class(d, tcp);
   PendingArgs pa;
   va_list ap;
   va_start(ap, device_type);
@@ -1476,6 +1517,7 @@ void parsec_dtd_insert_task_with_task_class(parsec_taskpool_t* tp, parsec_dtd_ta
     parse_one(tc->param_sizes[i], ptr, flags | tc->param_ops[i], pa);
   }
   va_end(ap);
+  size_new_tiles(d, pa);
   t_last_dtd = d;
   d->insert_task(tc, priority, pa.args, (uint32_t)device_type);
 }
@@ -1487,8 +1529,14 @@ parsec_dtd_tile_t* parsec_dtd_tile_of(parsec_data_collection_t* dc, parsec_data_
   if (!tp) fatal("parsec_dtd_tile_of: no DTD taskpool is active (add one to a context first)");
   return reinterpret_cast<parsec_dtd_tile_t*>(tp->tile_of(impl, key));
 }
-parsec_dtd_tile_t* parsec_dtd_tile_new(parsec_taskpool_t* tp, int rank, size_t size) {
-  return reinterpret_cast<parsec_dtd_tile_t*>(as_dtd(tp)->tile_new(size, rank));
+parsec_dtd_tile_t* parsec_dtd_tile_new(parsec_taskpool_t* tp, int rank) { return as_dtd(tp)->tile_new(0, rank); }
+parsec_dtd_tile_t* parsec_dtd_tile_new_sized(parsec_taskpool_t* tp, int rank, size_t size) { return as_dtd(tp)->tile_new(size, rank); }
+parsec_data_copy_t* parsec_dtd_tile_data_copy(parsec_dtd_tile_t* tile) { return tile ? tile->data_copy : nullptr; }
+void parsec_dtd_tile_retain(parsec_dtd_tile_t* tile) {
+  if (tile) tile->refcount.fetch_add(1);
+}
+void parsec_dtd_tile_release(parsec_dtd_tile_t* tile) {
+  if (tile) dtd::tile_release(tile);
 }
 // the collection's id names its tiles in remote DTD messages: ids follow the
 // order of registration, identical on every rank (reference insert_function.c:1255).

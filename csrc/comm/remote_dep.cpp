@@ -179,7 +179,7 @@ struct DevPool {
   std::map<size_t, std::vector<void*>> free;
 };
 DevPool& dev_pool() { static DevPool* p = new DevPool(); return *p; }
-int g_gpu_index = -1;
+std::atomic<int> g_gpu_index{-1};  // set by every context_add_taskpool (bodies may add taskpools concurrently)
 
 void recv_copy_release(DataCopy* c) {
   Data* d = c->original;
@@ -216,7 +216,7 @@ DataCopy* new_recv_copy(size_t bytes, bool device) {
     // thread); recycled by size through the pool, returned at remote_dep_fini
     if (!p && g_recv_from_cache) p = device_cache_alloc(g_gpu_index, bytes);
     if (!p) p = device_alloc(g_gpu_index, bytes);
-    dev = p ? g_gpu_index : 0;
+    dev = p ? g_gpu_index.load(std::memory_order_relaxed) : 0;
   }
   if (!p) {
     if (posix_memalign(&p, 4096, std::max<size_t>(bytes, 64))) fatal("out of host memory for a remote tile");
@@ -660,7 +660,7 @@ void remote_dep_progress_inline(Context* ctx) {
 
 void remote_dep_new_taskpool(Context* ctx, Taskpool* tp) {
   (void)ctx;
-  g_gpu_index = first_gpu_device_index();
+  g_gpu_index.store(first_gpu_device_index(), std::memory_order_relaxed);
   if (!g_ce) return;
   std::vector<std::pair<int, std::vector<char>>> parked;
   {

@@ -322,6 +322,7 @@ int context_fini(Context** pctx) {
   Context* ctx = *pctx;
   if (!ctx) return 0;
   if (ctx->active_taskpools.load() > 0) context_wait(ctx);
+  context_drain_zombies(ctx);
   PARSEC_DEBUG(kVerbDebug, "fini", "at_fini hooks (%zu)", ctx->at_fini.size());
   for (size_t i = 0; i < ctx->at_fini.size(); ++i) ctx->at_fini[i](ctx->at_fini_data[i]);
   PARSEC_DEBUG(kVerbDebug, "fini", "remote deps");
@@ -399,6 +400,7 @@ int context_wait(Context* ctx) {
   }
   for (Taskpool* tp : tps) tp->on_context_wait();
   worker_loop(es, true);
+  context_drain_zombies(ctx);
   set_my_execution_stream(prev);
   {
     std::lock_guard<std::mutex> g(ctx->wake_m);

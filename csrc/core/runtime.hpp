@@ -417,6 +417,12 @@ struct TaskClass {
   // Called once the body finished: release successors, write back data, free.
   virtual int complete_execution(ExecutionStream* es, Task* t) const = 0;
   virtual void release_task(ExecutionStream* es, Task* t) const;
+  // Keep a task's memory valid past its completion (a program may read the
+  // task it just completed, reference tests/dsl/dtd/dtd_test_tp_enqueue_dequeue.c:44-48,
+  // harmless there because tasks come from mempools): take a reference and
+  // return the function that drops it, or nullptr when the memory stays valid
+  // anyway (mempool-allocated tasks).
+  virtual void (*hold_task(Task* t) const)(Task*) { (void)t; return nullptr; }
   virtual void iterate_successors(ExecutionStream* es, const Task* t, uint32_t action_mask, const DepVisitor& v) const { (void)es; (void)t; (void)action_mask; (void)v; }
   virtual void iterate_predecessors(ExecutionStream* es, const Task* t, uint32_t action_mask, const DepVisitor& v) const { (void)es; (void)t; (void)action_mask; (void)v; }
   virtual int64_t sim_cost(const Task* t) const { (void)t; return 1; }
@@ -489,6 +495,13 @@ struct Taskpool {
   // application freed it after taskpool_wait, as the reference allows: close
   // insertion and let it terminate before it is deleted).
   virtual void on_free_incomplete() {}
+  // taskpool_free from a task body on a taskpool still running (reference
+  // parsec_taskpool_free = release of the program's reference,
+  // parsec.c:2173): DTD closes insertion; the runtime deletes the taskpool
+  // once it terminated (Context::zombies, drained by context_wait)
+  virtual void on_free_in_body() {}
+  // 0 live, 1 freed by the program while running, 2 terminated
+  std::atomic<int> free_state{0};
   std::function<void()> destructor_hook;
 };
 
@@ -676,6 +689,7 @@ struct Context {
   void* grapher = nullptr;
   std::mutex tp_m;
   std::vector<Taskpool*> taskpools_in_flight;
+  std::vector<Taskpool*> zombies;  // freed from a body while running, deleted after termination (tp_m)
   std::atomic<uint64_t> sim_date{0};
   bool simulation = false;
 };
@@ -703,12 +717,19 @@ extern bool g_paranoid;  // debug_paranoid (set at init)
 // Push a set of ready tasks (sorted internally by priority).
 int schedule_tasks(ExecutionStream* es, Task** tasks, int n, int32_t distance);
 int schedule_task(ExecutionStream* es, Task* t, int32_t distance);
-enum TaskAsyncState : uint8_t { ASYNC_NONE = 0, ASYNC_RUNNING = 1, ASYNC_PARKED = 2, ASYNC_REQUESTED = 3 };
+enum TaskAsyncState : uint8_t { ASYNC_NONE = 0, ASYNC_RUNNING = 1, ASYNC_PARKED = 2, ASYNC_REQUESTED = 3, ASYNC_COMPLETE_REQUESTED = 4 };
 // Put back a task whose CPU body returned HOOK_ASYNC (reference
 // __parsec_schedule on such a task): if the body has not returned yet, the
 // executing thread schedules it itself once it has (so the task is never run
 // again, nor freed, while its first run is still being traced).
 int schedule_async_task(ExecutionStream* es, Task* t, int32_t distance);
+// Complete a task whose CPU body returned HOOK_ASYNC without running it again
+// (reference __parsec_complete_execution, e.g. from the completion callback of
+// a taskpool the body started): same handshake, the executing thread completes
+// it itself when the body has not returned yet.
+int complete_async_task(ExecutionStream* es, Task* t);
+// delete the taskpools freed from bodies that have terminated since
+void context_drain_zombies(Context* ctx);
 // the task whose CPU body the calling thread is running (nullptr outside one)
 Task* current_task();
 int reschedule(ExecutionStream* es, Task* t);

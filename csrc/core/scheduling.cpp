@@ -185,6 +185,27 @@ int schedule_async_task(ExecutionStream* es, Task* t, int32_t distance) {
   return schedule_task(es, t, distance);
 }
 
+// tasks completed by complete_async_task on this thread, kept readable until
+// its next scheduling step (TaskClass::hold_task)
+static thread_local std::vector<std::pair<void (*)(Task*), Task*>> t_held;
+static void drain_held_tasks() {
+  while (!t_held.empty()) {
+    std::vector<std::pair<void (*)(Task*), Task*>> v;
+    v.swap(t_held);
+    for (auto& h : v) h.first(h.second);
+  }
+}
+
+int complete_async_task(ExecutionStream* es, Task* t) {
+  uint8_t s = __atomic_load_n(&t->async_state, __ATOMIC_ACQUIRE);
+  while (s == ASYNC_RUNNING)
+    if (__atomic_compare_exchange_n(&t->async_state, &s, (uint8_t)ASYNC_COMPLETE_REQUESTED, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) return 0;
+  t->async_state = ASYNC_NONE;
+  // the caller may still read the task (e.g. t->taskpool) after this returns
+  if (auto rel = t->task_class->hold_task(t)) t_held.push_back({rel, t});
+  return complete_task_execution(es ? es : my_execution_stream(), t);
+}
+
 // ============================================================= execution
 static thread_local Task* t_current_task = nullptr;
 Task* current_task() { return t_current_task; }
@@ -218,6 +239,7 @@ int execute_task(ExecutionStream* es, Task* t) {
         uint8_t expect = ASYNC_RUNNING;
         if (!__atomic_compare_exchange_n(&t->async_state, &expect, (uint8_t)ASYNC_PARKED, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
           t->async_state = ASYNC_NONE;
+          if (expect == ASYNC_COMPLETE_REQUESTED) return HOOK_DONE;  // task_progress completes it
           schedule_task(es, t, 0);
         }
         return rc;
@@ -333,6 +355,7 @@ void worker_loop(ExecutionStream* es, bool master) {
       t = s->select(es, &dist);
       PARSEC_PINS(es, PINS_SELECT_END, t);
     }
+    if (!t_held.empty()) drain_held_tasks();
     if (t) {
       backoff.reset();
       ++es->nb_selected;
@@ -344,6 +367,7 @@ void worker_loop(ExecutionStream* es, bool master) {
     }
   }
   flush_exec_counter(es);
+  drain_held_tasks();
   // drain the bypass slot so a later epoch does not lose it
   if (es->next_task) {
     Task* t = es->next_task;
@@ -403,8 +427,32 @@ Taskpool::~Taskpool() {
   if (tdm && termdet_private) tdm->release_taskpool(this);
 }
 
+static void taskpool_destroy(Taskpool* tp) {
+  if (tp->destructor_hook) tp->destructor_hook();
+  for (auto* d : DeviceRegistry::instance().devices) if (d) d->taskpool_unregister(tp);
+  delete tp;
+}
+
+void context_drain_zombies(Context* ctx) {
+  std::vector<Taskpool*> z;
+  {
+    std::lock_guard<std::mutex> g(ctx->tp_m);
+    z.swap(ctx->zombies);
+  }
+  for (Taskpool* tp : z) taskpool_destroy(tp);
+}
+
 void taskpool_free(Taskpool* tp) {
   if (!tp) return;
+  if (tp->context && !tp->completed.load() && current_task()) {
+    // freed by a task body while it runs: it cannot be waited for here (the
+    // body may be what completes it); termination hands it to context_wait
+    int expect = 0;
+    if (tp->free_state.compare_exchange_strong(expect, 1)) {
+      tp->on_free_in_body();
+      return;
+    }
+  }
   if (tp->context && !tp->completed.load()) {
     tp->on_free_incomplete();
     if (!tp->completed.load()) {
@@ -414,9 +462,7 @@ void taskpool_free(Taskpool* tp) {
       v.erase(std::remove(v.begin(), v.end(), tp), v.end());
     }
   }
-  if (tp->destructor_hook) tp->destructor_hook();
-  for (auto* d : DeviceRegistry::instance().devices) if (d) d->taskpool_unregister(tp);
-  delete tp;
+  taskpool_destroy(tp);
 }
 
 int taskpool_termination_detected(Taskpool* tp) {
@@ -430,6 +476,8 @@ int taskpool_termination_detected(Taskpool* tp) {
     std::lock_guard<std::mutex> g(ctx->tp_m);
     auto& v = ctx->taskpools_in_flight;
     v.erase(std::remove(v.begin(), v.end(), tp), v.end());
+    // freed by a body while running: deleted by context_wait from now on
+    if (tp->free_state.exchange(2) == 1) ctx->zombies.push_back(tp);
   }
   ctx->active_taskpools.fetch_sub(1, std::memory_order_acq_rel);
   return 1;

@@ -42,7 +42,13 @@ DtdTaskpool::~DtdTaskpool() {
   tiles.clear();
   remote_tasks.for_each([](uint64_t, DtdTask* t) { task_unref(t); });
   remote_tasks.clear();
-  for (Tile* t : new_tiles) tile_release(t);
+  for (Tile* t : new_tiles) {
+    if (t->writer) task_unref(t->writer);
+    for (auto& r : t->readers) task_unref(r.first);
+    t->writer = nullptr;
+    t->readers.clear();
+    tile_release(t);
+  }
   for (auto* c : classes) delete c;
 }
 
@@ -140,6 +146,8 @@ Tile* DtdTaskpool::tile_of(DataCollection* dc, uint64_t key) {
       t->data->key = key;
       t->data->nb_elts = dc->data_size_of_key(key);
       t->is_new = true;
+    } else {
+      t->data_copy = t->data->copy(0);
     }
     m[k] = t;
     return t;
@@ -168,7 +176,22 @@ Tile* DtdTaskpool::tile_new(size_t bytes, int rank) {
   Tile* t = new Tile();
   t->rank = rank;
   t->is_new = true;
-  if (rank == (context ? context->my_rank : 0)) {
+  t->unsized = true;
+  if (bytes) tile_materialize(t, bytes);
+  // the taskpool's reference (released with it); a program keeping the tile
+  // past parsec_taskpool_free takes its own (parsec_dtd_tile_retain)
+  std::lock_guard<std::mutex> g(new_tiles_m);
+  new_tiles.push_back(t);
+  return t;
+}
+
+// Storage of a new tile: zeroed host memory on its owner, a shadow Data of that
+// size elsewhere (remote versions land in it). Called by the inserting thread
+// before the tile's first task is inserted, so no task sees it unsized.
+void DtdTaskpool::tile_materialize(Tile* t, size_t bytes) {
+  std::lock_guard<SpinLock> g(t->lock);
+  if (!t->unsized) return;
+  if (t->rank == (context ? context->my_rank : 0)) {
     void* p = nullptr;
     if (posix_memalign(&p, 64, std::max<size_t>(bytes, 64))) fatal("tile_new: out of memory");
     std::memset(p, 0, bytes);
@@ -177,10 +200,7 @@ Tile* DtdTaskpool::tile_new(size_t bytes, int rank) {
     t->data = data_new();
     t->data->nb_elts = bytes;
   }
-  std::lock_guard<std::mutex> g(new_tiles_m);
-  new_tiles.push_back(t);
-  t->refcount.fetch_add(1);
-  return t;
+  t->unsized = false;
 }
 
 // Private copy of `src` for a pending remote transfer (host or device memory).
@@ -521,7 +541,10 @@ int DtdTaskpool::wait() {
 }
 
 int DtdTaskpool::data_flush(Tile* tile) {
-  if (!tile || !tile->dc) return 0;
+  // a collection tile, or a new tile once it has storage (parsec_dtd_tile_new:
+  // the flush brings its last version to the owner, whose tile->data_copy then
+  // names it -- reference tests/dsl/dtd/dtd_test_new_tile.c:415-454)
+  if (!tile || (!tile->dc && !(tile->is_new && !tile->unsized && tile->data))) return 0;
   // reference parsec_dtd_data_flush.c:391,395
   ExecutionStream* es = my_execution_stream();
   PARSEC_PINS(es, PINS_DATA_FLUSH_BEGIN, nullptr);
@@ -531,9 +554,14 @@ int DtdTaskpool::data_flush(Tile* tile) {
   } flush_end{es};
   // A no-op CPU task reading the tile on its owner: the CPU staging of the
   // engine brings the newest version home (GPU -> host, or remote -> owner).
-  if (tile->dc->home_device() != 0) return 0;
+  if (tile->dc && tile->dc->home_device() != 0) return 0;
   DtdTaskClass* tc = create_task_class("parsec_dtd_data_flush", {{INPUT | AFFINITY, (int)PASSED_BY_REF}});
-  if (tc->chores.empty()) add_chore(tc, DEV_CPU, [](ExecutionStream*, Task*) { return HOOK_DONE; }, nullptr);
+  if (tc->chores.empty())
+    add_chore(tc, DEV_CPU, [](ExecutionStream*, Task* t) {
+      Tile* ft = static_cast<DtdTask*>(t)->args[0].tile;
+      if (ft && ft->data) ft->data_copy = ft->data->copy(0);
+      return HOOK_DONE;
+    }, nullptr);
   Arg a;
   a.op = INPUT | AFFINITY;
   a.size = PASSED_BY_REF;
@@ -705,6 +733,12 @@ static void task_unref(DtdTask* t) {
   if (t->refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
   for (auto& a : t->args) if (a.tile) tile_release(a.tile);
   delete t;
+}
+
+static void task_unhold(Task* t) { task_unref(static_cast<DtdTask*>(t)); }
+void (*DtdTaskClass::hold_task(Task* t) const)(Task*) {
+  task_retain(static_cast<DtdTask*>(t));
+  return &task_unhold;
 }
 
 void DtdTaskpool::on_remote_activation(ExecutionStream* es, RemoteActivation& act) {

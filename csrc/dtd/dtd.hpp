@@ -41,7 +41,11 @@ struct Tile {
   uint64_t key = 0;
   int rank = 0;
   bool is_new = false;  // parsec_dtd_tile_new
+  bool unsized = false;   // parsec_dtd_tile_new without a size: storage at its first insertion (tile_materialize)
   bool data_ref = false;  // holds a reference on an existing Data (tile_of_data)
+  // host copy with the tile's last version (reference parsec_dtd_tile_t::data_copy):
+  // a collection tile's home copy; a new tile's once a flush brought it home
+  DataCopy* data_copy = nullptr;
   SpinLock lock;
   DtdTask* writer = nullptr;
   int writer_flow = -1;
@@ -98,6 +102,7 @@ class DtdTaskClass : public TaskClass {
   void iterate_successors(ExecutionStream* es, const Task* t, uint32_t mask, const DepVisitor& v) const override;
   // flows inserted with PUSHOUT: copied back to the host when a GPU chore ran
   uint32_t gpu_pushout_mask(const Task* t, int device) const override;
+  void (*hold_task(Task* t) const)(Task*) override;
 };
 
 class DtdTaskpool : public Taskpool {
@@ -124,6 +129,7 @@ class DtdTaskpool : public Taskpool {
   void arm_hold();
   void release_hold();
   void on_free_incomplete() override;
+  void on_free_in_body() override { release_hold(); }
   // remote activation, second half: install the received versions on the
   // tiles, release the local successors (comm thread or a compute thread)
   void finish_remote_activation(ExecutionStream* es, DtdTask* t, RemoteActivation& act);
@@ -135,7 +141,8 @@ class DtdTaskpool : public Taskpool {
   // (reference parsec_dtd_insert_task_with_task_class's device_type argument)
   DtdTask* insert_task(DtdTaskClass* tc, int priority, const std::vector<Arg>& args, uint32_t device_types = 0);
   Tile* tile_of(DataCollection* dc, uint64_t key);
-  Tile* tile_new(size_t bytes, int rank);
+  Tile* tile_new(size_t bytes, int rank);  // bytes 0: unsized until tile_materialize
+  void tile_materialize(Tile* t, size_t bytes);
   Tile* tile_of_data(Data* d);  // local tile tracking an existing Data (ptg_to_dtd)
   int data_flush(Tile* tile);
   int data_flush_all(DataCollection* dc);

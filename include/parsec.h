@@ -67,6 +67,9 @@
 #define PARSEC_DEV_RECURSIVE 0x02
 #define PARSEC_DEV_HIP 0x40
 #define PARSEC_DEV_ALL 0xff
+/* the reference's CUDA device type: no device of this runtime has it (programs
+ * that pick it only when they counted CUDA devices take their CPU path) */
+#define PARSEC_DEV_CUDA 0x04
 
 #include "parsec/sys/atomic.h"
 
@@ -81,6 +84,10 @@ struct DataCopy;
 struct ArenaDatatype;
 struct Datatype;
 struct ThreadMempool;
+struct TaskClass;
+namespace dtd {
+struct Tile;
+}
 }  // namespace parsec
 typedef parsec::Context parsec_context_t;
 typedef parsec::Taskpool parsec_taskpool_t;
@@ -90,6 +97,10 @@ typedef parsec::Data parsec_data_t;
 typedef parsec::DataCopy parsec_data_copy_t;
 typedef parsec::ArenaDatatype parsec_arena_datatype_t;
 typedef parsec::ThreadMempool parsec_thread_mempool_t;
+/* task classes (PTG and DTD alike) and DTD tiles: the runtime's own */
+typedef parsec::TaskClass parsec_task_class_t;
+typedef parsec::TaskClass parsec_dtd_task_class_t;
+typedef parsec::dtd::Tile parsec_dtd_tile_t;
 /* programs that spell the C struct tags (`struct parsec_data_s *d;`, reference
  * tests/apps/pingpong/rtt_data.c) name the same classes when compiled as C++ */
 #define parsec_data_s parsec::Data
@@ -104,6 +115,9 @@ typedef struct parsec_data_s parsec_data_t;
 typedef struct parsec_data_copy_s parsec_data_copy_t;
 typedef struct parsec_arena_datatype_s parsec_arena_datatype_t;
 typedef struct parsec_thread_mempool_s parsec_thread_mempool_t;
+typedef struct parsec_task_class_s parsec_task_class_t;
+typedef struct parsec_task_class_s parsec_dtd_task_class_t;
+typedef struct parsec_dtd_tile_s parsec_dtd_tile_t;
 #endif
 
 typedef uint64_t parsec_data_key_t;
@@ -180,6 +194,8 @@ static inline void parsec_obj_release_list(parsec_list_t* o) { parsec_obj_releas
 static inline void parsec_obj_retain_lifo(parsec_lifo_t* o) { parsec_obj_retain_object((parsec_object_t*)o); }
 static inline void parsec_obj_release_lifo(parsec_lifo_t* o) { parsec_obj_release_object((parsec_object_t*)o); }
 static inline void parsec_obj_release_pobj(parsec_object_t* o) { parsec_obj_release_object(o); }
+void parsec_dtd_tile_retain(parsec_dtd_tile_t* tile);
+void parsec_dtd_tile_release(parsec_dtd_tile_t* tile);
 
 #define PARSEC_OBJ_NEW(type) ((type*)parsec_obj_new_of(PARSEC_OBJ_CLASS(type)))
 #define PARSEC_OBJ_CONSTRUCT(obj, type) parsec_obj_construct_as((parsec_object_t*)(obj), PARSEC_OBJ_CLASS(type))
@@ -200,6 +216,7 @@ struct is_object<T, std::void_t<decltype(std::declval<T&>().super)>>
 }  // namespace parsec_obj_detail
 inline void parsec_obj_retain(parsec_data_t* d) { parsec_obj_retain_data(d); }
 inline void parsec_obj_retain(parsec_data_copy_t* c) { parsec_obj_retain_copy(c); }
+inline void parsec_obj_retain(parsec_dtd_tile_t* t) { parsec_dtd_tile_retain(t); }
 template <class T>
 inline void parsec_obj_retain(T* o) {
   if constexpr (parsec_obj_detail::is_object<std::remove_cv_t<T>>::value) parsec_obj_retain_object((parsec_object_t*)o);
@@ -208,6 +225,7 @@ template <class T>
 inline void parsec_obj_retain(T&&) {}
 inline void parsec_obj_release(parsec_data_t* d) { parsec_obj_release_data(d); }
 inline void parsec_obj_release(parsec_data_copy_t* c) { parsec_obj_release_copy(c); }
+inline void parsec_obj_release(parsec_dtd_tile_t* t) { parsec_dtd_tile_release(t); }
 template <class T>
 inline void parsec_obj_release(T* o) {
   if constexpr (parsec_obj_detail::is_object<std::remove_cv_t<T>>::value) parsec_obj_release_object((parsec_object_t*)o);
@@ -222,11 +240,13 @@ extern "C" {
 #define PARSEC_OBJ_RETAIN(obj)                                                                                       \
   _Generic((obj), parsec_data_t*: parsec_obj_retain_data, parsec_data_copy_t*: parsec_obj_retain_copy,             \
            parsec_object_t*: parsec_obj_retain_object, parsec_list_item_t*: parsec_obj_retain_item,                \
-           parsec_list_t*: parsec_obj_retain_list, parsec_lifo_t*: parsec_obj_retain_lifo, default: parsec_obj_keep_none)(obj)
+           parsec_list_t*: parsec_obj_retain_list, parsec_lifo_t*: parsec_obj_retain_lifo,                         \
+           parsec_dtd_tile_t*: parsec_dtd_tile_retain, default: parsec_obj_keep_none)(obj)
 #define PARSEC_OBJ_RELEASE(obj)                                                                                      \
   _Generic((obj), parsec_data_t*: parsec_obj_release_data, parsec_data_copy_t*: parsec_obj_release_copy,           \
            parsec_object_t*: parsec_obj_release_pobj, parsec_list_item_t*: parsec_obj_release_item,                \
-           parsec_list_t*: parsec_obj_release_list, parsec_lifo_t*: parsec_obj_release_lifo, default: parsec_obj_keep_none)(obj)
+           parsec_list_t*: parsec_obj_release_list, parsec_lifo_t*: parsec_obj_release_lifo,                       \
+           parsec_dtd_tile_t*: parsec_dtd_tile_release, default: parsec_obj_keep_none)(obj)
 #endif
 
 /* diagnostics (reference parsec/utils/debug.h): this process' rank and the
@@ -315,6 +335,12 @@ int parsec_execution_stream_id(const parsec_execution_stream_t* es);
  * calls this on it; its body then runs again (DONE completes it, ASYNC parks it
  * again). distance: 0 = the calling stream's own queue, > 0 further away. */
 int __parsec_schedule(parsec_execution_stream_t* es, parsec_task_t* task, int32_t distance);
+/* Complete a task whose body returned PARSEC_HOOK_RETURN_ASYNC, without running
+ * it again: its outputs are released to its successors (reference scheduling.h
+ * __parsec_complete_execution; e.g. from the completion callback of a taskpool
+ * the body started, tests/dsl/dtd/dtd_test_tp_enqueue_dequeue.c:39-51). Safe
+ * before the body has returned: the executing thread then completes it. */
+int __parsec_complete_execution(parsec_execution_stream_t* es, parsec_task_t* task);
 /* Reset an item's list links to itself (class/list_item.h). Tasks are not list
  * items in this API (the scheduler queues them through its own links): on a
  * task, as the reference's bodies apply it, it does nothing. */
@@ -691,8 +717,6 @@ int parsec_taskpool_set_arena_datatype(parsec_taskpool_t* tp, int idx, size_t el
 #define PARSEC_DTD_EMPTY_FLAG 0
 #define PARSEC_DTD_MAX_PARAMS 64
 
-typedef struct parsec_dtd_tile_s parsec_dtd_tile_t;
-typedef struct parsec_dtd_task_class_s parsec_dtd_task_class_t;
 typedef int(parsec_dtd_funcptr_t)(parsec_execution_stream_t* es, parsec_task_t* this_task);
 /* GPU chore: launches on `stream` (a hipStream_t); device pointers via parsec_dtd_get_dev_ptr */
 typedef int(parsec_dtd_gpu_funcptr_t)(void* stream, parsec_task_t* this_task);
@@ -706,15 +730,37 @@ extern int parsec_dtd_threshold_size;
 void parsec_tiled_matrix_destroy_data(parsec_tiled_matrix_t* tdesc);
 int parsec_dtd_taskpool_wait(parsec_taskpool_t* tp);
 void parsec_dtd_insert_task(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, int priority, int device_type, const char* name_of_kernel, ...);
-parsec_dtd_task_class_t* parsec_dtd_create_task_class(parsec_taskpool_t* tp, const char* name, ...);
+/* a task class from (size, flags) pairs ending with PARSEC_DTD_ARG_END; add
+ * its chores, insert instances with parsec_dtd_insert_task_with_task_class
+ * (reference insert_function.h:389-412). Classes live until the taskpool is
+ * freed; _release only drops the program's handle. */
+parsec_task_class_t* parsec_dtd_create_task_class(parsec_taskpool_t* tp, const char* name, ...);
+void parsec_dtd_task_class_release(parsec_taskpool_t* tp, parsec_task_class_t* tc);
+/* the taskpool of a running DTD task; explicit dequeue of a DTD taskpool from
+ * its context: no more insertions, it terminates once its tasks are done
+ * (context_wait does the same for every DTD taskpool still attached) */
+parsec_taskpool_t* parsec_dtd_get_taskpool(parsec_task_t* this_task);
+int parsec_dtd_dequeue_taskpool(parsec_taskpool_t* tp);
 /* explicit task creation: described now (same arguments as
  * parsec_dtd_insert_task), inserted by parsec_insert_dtd_task */
 parsec_task_t* parsec_dtd_create_task(parsec_taskpool_t* tp, parsec_dtd_funcptr_t* fpointer, int priority, int device_type, const char* name, ...);
 void parsec_insert_dtd_task(parsec_task_t* this_task);
-int parsec_dtd_task_class_add_chore(parsec_taskpool_t* tp, parsec_dtd_task_class_t* tc, int device_type, void* function);
-void parsec_dtd_insert_task_with_task_class(parsec_taskpool_t* tp, parsec_dtd_task_class_t* tc, int priority, int device_type, ...);
+int parsec_dtd_task_class_add_chore(parsec_taskpool_t* tp, parsec_task_class_t* tc, int device_type, void* function);
+void parsec_dtd_insert_task_with_task_class(parsec_taskpool_t* tp, parsec_task_class_t* tc, int priority, int device_type, ...);
 parsec_dtd_tile_t* parsec_dtd_tile_of(parsec_data_collection_t* dc, parsec_data_key_t key);
-parsec_dtd_tile_t* parsec_dtd_tile_new(parsec_taskpool_t* tp, int rank, size_t size);
+/* a new tile owned by `rank`, without storage until its first writer: sized
+ * then from the arena datatype named in that argument's flags (the REGION bits,
+ * parsec_dtd_create_arena_datatype); reference insert_function.h:224 */
+parsec_dtd_tile_t* parsec_dtd_tile_new(parsec_taskpool_t* tp, int rank);
+/* same, with its byte size given now (arguments need no arena datatype) */
+parsec_dtd_tile_t* parsec_dtd_tile_new_sized(parsec_taskpool_t* tp, int rank, size_t size);
+/* the host copy holding a tile's last version: set for collection tiles, and
+ * for new tiles once a flush brought the last version home (the reference's
+ * tile->data_copy; in C++ builds with the runtime's headers the field itself) */
+parsec_data_copy_t* parsec_dtd_tile_data_copy(parsec_dtd_tile_t* tile);
+/* a program's own reference on a tile (PARSEC_OBJ_RETAIN / RELEASE) */
+void parsec_dtd_tile_retain(parsec_dtd_tile_t* tile);
+void parsec_dtd_tile_release(parsec_dtd_tile_t* tile);
 void parsec_dtd_data_collection_init(parsec_data_collection_t* dc);
 void parsec_dtd_data_collection_fini(parsec_data_collection_t* dc);
 int parsec_dtd_data_flush(parsec_taskpool_t* tp, parsec_dtd_tile_t* tile);

@@ -137,7 +137,7 @@ static int test_new_tile(parsec_context_t* ctx, int rank, int world) {
   for (int t = 0; t < NCASE * world; t++) {
     int r = t % world, tcase = t / world;
     if (r == rank) expected += 2 * (nb * (nb - 1)) / 2;
-    tiles[t] = parsec_dtd_tile_new(tp, r, (size_t)nb * sizeof(int));
+    tiles[t] = parsec_dtd_tile_new_sized(tp, r, (size_t)nb * sizeof(int));
     const int on1 = g_nb_gpus > 0 && !(tcase & 1), on2 = g_nb_gpus > 0 && !(tcase & 2), on3 = g_nb_gpus > 0 && !(tcase & 4);
     const int push1 = on1 && !on2 ? PARSEC_PUSHOUT : 0, push2 = on2 && !on3 ? PARSEC_PUSHOUT : 0, push3 = on3 ? PARSEC_PUSHOUT : 0;
     parsec_dtd_insert_task_with_task_class(tp, set_tc, 0, on1 ? PARSEC_DEV_HIP : PARSEC_DEV_CPU, PARSEC_AFFINITY, &r, push1, tiles[t],

@@ -603,8 +603,8 @@ def test_reference_utt_program(tmp_path):
 
 
 REF_DTD_PROGRAMS = ["allreduce", "broadcast", "data_flush", "flag_dont_track", "global_id_for_dc_assumed", "hierarchy", "insert_task_interface",
-                    "multiple_handle_wait", "null_as_tile", "reduce", "task_generation", "task_inserting_task", "task_insertion",
-                    "template_counter", "untie", "war"]
+                    "multiple_handle_wait", "new_tile", "null_as_tile", "reduce", "task_generation", "task_inserting_task", "task_insertion",
+                    "template_counter", "tp_enqueue_dequeue", "untie", "war"]
 
 
 @pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
@@ -613,11 +613,15 @@ def test_reference_dtd_programs_unmodified(tmp_path, name):
     """The reference's DTD test programs (tests/dsl/dtd/dtd_test_<name>.c with
     tests/tests_data.c, unmodified) compiled as C++ against this runtime's
     headers and run on one process; each checks itself (parsec_fatal / assert
-    on a wrong result, non-zero exit). Not here: the two-process ones
-    (pingpong, task_placement, interleave_actions), the CUDA / MPI-only ones,
-    and those that reach the reference's internal task classes or
-    __parsec_complete_execution (new_tile, tp_enqueue_dequeue,
-    explicit_task_creation)."""
+    on a wrong result, non-zero exit). new_tile: tiles without storage until
+    their first writer, sized from the arena datatype in the flags, task-class
+    handles, a flush bringing the last version home (tile->data_copy);
+    tp_enqueue_dequeue: taskpools created and freed inside bodies, a body
+    returning ASYNC completed by an inner taskpool's completion callback
+    (__parsec_complete_execution) and explicit dequeue. Not here: the
+    two-process ones (pingpong, task_placement, interleave_actions), the CUDA
+    ones (cuda_task_insert, simple_gemm: ported in tests/capi/dtd_gpu_capi.c)
+    and explicit_task_creation (MPI_INT outside its MPI guard)."""
     cc, libs = ptgpp.compile_flags(False)
     exe = str(tmp_path / name)
     src = os.path.join(REF, "tests/dsl/dtd", f"dtd_test_{name}.c")

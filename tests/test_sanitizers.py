@@ -98,18 +98,22 @@ def _run_sanitized(kind, exe, args=(), timeout=300, leaks=True):
 
 
 @pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
-def test_reference_multiple_handle_wait_sanitized(sanitized, tmp_path):
-    """The reference's dtd_test_multiple_handle_wait.c (unmodified), which found
-    round 4's two use-after-frees under a manual ASan run, now in the suite."""
+@pytest.mark.parametrize("prog,runs,args", [("multiple_handle_wait", 3, []), ("tp_enqueue_dequeue", 2, ["4"]), ("new_tile", 2, [])])
+def test_reference_dtd_programs_sanitized(sanitized, tmp_path, prog, runs, args):
+    """Reference DTD programs (tests/dsl/dtd/dtd_test_<prog>.c, unmodified):
+    multiple_handle_wait found round 4's two use-after-frees under a manual ASan
+    run; tp_enqueue_dequeue frees taskpools from bodies (deferred deletion) and
+    completes an ASYNC task from another taskpool's completion callback;
+    new_tile sizes tiles at their first insertion and flushes them home."""
     kind, _ = sanitized
     cc, libs = ptgpp.compile_flags(False, kind)
-    exe = str(tmp_path / "mhw")
+    exe = str(tmp_path / prog)
     r = subprocess.run(cc + list(ptgpp.C_BODIES) + [f"-I{REF}/tests", f"-I{REF}", f"-I{REF}/tests/dsl/dtd", "-x", "c++",
-                                                    os.path.join(REF, "tests/dsl/dtd/dtd_test_multiple_handle_wait.c"),
+                                                    os.path.join(REF, f"tests/dsl/dtd/dtd_test_{prog}.c"),
                                                     os.path.join(REF, "tests/tests_data.c"), "-o", exe] + libs, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-3000:]
-    for _ in range(3):
-        _run_sanitized(kind, exe)
+    for _ in range(runs):
+        _run_sanitized(kind, exe, args)
 
 
 _RS = "tests/collections/reshape/"
