@@ -809,7 +809,7 @@ void HipDevice::ensure_zone() {
     size_t seg = ParamRegistry::instance().reg_sizet("device", "hip", "memory_block_size", "Tile-cache segment size (bytes)", (size_t)1 << 30);
     size_t unit = ParamRegistry::instance().reg_sizet("device", "hip", "memory_unit", "Tile-cache allocation granule (bytes)", 4096);
     size_t maxb = ParamRegistry::instance().reg_sizet("device", "hip", "memory_max", "Hard cap of the tile cache (bytes, 0 = percent rule)", 0);
-    zone_max = maxb ? maxb : (size_t)(freeb * pct / 100.0);
+    zone_max = maxb ? maxb : (size_t)(freeb * pct / 100.0 / std::max(1, replicas));
     zone = std::make_unique<ZoneAllocator>(ordinal, zone_max, seg, unit);
   }
 }
@@ -959,6 +959,14 @@ int HipDevice::stage_in(GpuTask* g) {
       g->issued_copy[fi] = true;
       any = true;
     } else if (src && src != local) {
+      // read-only flow whose source is the host copy: a GPU of this process
+      // holding the same version is the faster source (device-to-device over
+      // xGMI; reference device_cuda_module.c:1308-1360)
+      if (src->device_index == 0 && !(g->access[fi] & FLOW_WRITE) && peer_stage_in)
+        if (DataCopy* alt = peer_source(d, src->version)) {
+          src = alt;
+          g->peer_src[fi] = alt;
+        }
       hipMemcpyKind k = src->device_index == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
       hipEvent_t sb = copy_span_begin();
       struct SpanEnd {
@@ -1007,8 +1015,43 @@ int HipDevice::missing_on_device(GpuTask* g) const {
   return n;
 }
 
+DataCopy* HipDevice::peer_source(Data* d, uint32_t version) {
+  auto& reg = DeviceRegistry::instance();
+  std::lock_guard<SpinLock> lk(d->lock);  // the owner evicts under this lock after checking readers
+  for (int i = 0; i < kMaxDevices && i < (int)reg.devices.size(); ++i) {
+    if (i == device_index || !reg.devices[i] || reg.devices[i]->type != DEV_HIP) continue;
+    auto* peer = static_cast<HipDevice*>(reg.devices[i]);
+    if (!peer_accessible(peer)) continue;
+    DataCopy* c = d->copy(i);
+    if (!c || c->version != version || c->coherency_state == COHERENCY_INVALID || c->transfer_status == TRANSFER_UNDER || !c->device_private) continue;
+    c->readers.fetch_add(1);
+    return c;
+  }
+  return nullptr;
+}
+
+void HipDevice::peer_release(DataCopy* c) {
+  auto* owner = static_cast<HipDevice*>(DeviceRegistry::instance().devices[c->device_index]);
+  {
+    std::lock_guard<std::mutex> lk(owner->in_m);
+    owner->peer_done.push_back(c);
+    owner->peer_done_n.fetch_add(1, std::memory_order_release);
+  }
+  owner->in_cv.notify_one();
+}
+
+bool HipDevice::peer_accessible(const HipDevice* peer) const {
+  if (peer->ordinal == ordinal) return true;  // logical devices of one GPU (device_hip_replicas)
+  int can = 0;
+  return hipDeviceCanAccessPeer(&can, ordinal, peer->ordinal) == hipSuccess && can;
+}
+
 void HipDevice::finish_stage_in(GpuTask* g) {
   for (int fi = 0; fi < kMaxFlows; ++fi) {
+    if (g->peer_src[fi]) {
+      peer_release(g->peer_src[fi]);
+      g->peer_src[fi] = nullptr;
+    }
     if (!g->issued_copy[fi]) continue;
     DataCopy* local = g->dev_copy[fi];
     data_end_transfer_ownership_to_copy(local->original, device_index, g->access[fi]);
@@ -1324,6 +1367,17 @@ bool HipDevice::progress() {
     if (trace_launches) std::fprintf(stderr, "[engine] t=%llu I n=%zu\n", (unsigned long long)(now_ns() / 1000), in.size());
     did = true;
   }
+  if (peer_done_n.load(std::memory_order_acquire) > 0) {
+    std::vector<DataCopy*> done;
+    {
+      std::lock_guard<std::mutex> lk(in_m);
+      done.swap(peer_done);
+      peer_done_n.store(0);
+    }
+    for (DataCopy* c : done)
+      if (c->readers.fetch_sub(1) == 1) lru_touch(c);
+    did = true;
+  }
   if (!w2r_jobs.empty() && progress_w2r()) did = true;
   if (!copy_spans.empty()) progress_copy_spans();
   if ((!prefetch_jobs.empty() || !prefetch_requests.empty()) && progress_prefetch()) did = true;
@@ -1500,7 +1554,7 @@ void HipDevice::manager_main() {
     }
     if (stop.load()) break;
     std::unique_lock<std::mutex> lk(in_m);
-    in_cv.wait_for(lk, std::chrono::milliseconds(2), [&] { return stop.load() || incoming_n.load() > 0; });
+    in_cv.wait_for(lk, std::chrono::milliseconds(2), [&] { return stop.load() || incoming_n.load() > 0 || peer_done_n.load() > 0; });
     backoff.reset();
   }
   if (!copy_spans.empty()) {
@@ -1546,13 +1600,23 @@ void hip_devices_init(Context* ctx) {
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) { (void)hipGetLastError(); return; }
   auto& reg = DeviceRegistry::instance();
-  for (int o = 0; o < count; ++o) {
+  // replicas > 1: every GPU is registered that many times, as distinct devices
+  // (own streams, manager, tile cache, data copies): tiles then move between
+  // devices through the device-to-device path (hipMemcpyPeerAsync, same
+  // physical GPU) -- how the multi-GPU paths of one process are exercised on a
+  // one-GPU machine
+  const bool peer_in = params.reg_int("device", "hip", "peer_stage_in", "Read-only flows whose newest copy is also on another GPU of this process are staged in from that GPU (device to device) instead of the host", 1) != 0;
+  const int replicas = std::max(1, (int)params.reg_int("device", "hip", "replicas", "Devices registered per GPU (> 1: logical devices sharing one GPU, for testing the multi-device paths)", 1));
+  for (int o = 0; o < count; ++o)
+   for (int rep = 0; rep < replicas; ++rep) {
     if (mask >= 0 && !(mask & (1LL << o))) continue;
     if (enabled > 0 && (int)g_hip_devices.size() >= enabled) break;
     auto* d = new HipDevice();
     d->ordinal = o;
+    d->replicas = replicas;
+    d->peer_stage_in = peer_in;
     (void)hipGetDeviceProperties(&d->props, o);
-    d->name = "hip" + std::to_string(o);
+    d->name = "hip" + std::to_string(o) + (replicas > 1 ? "." + std::to_string(rep) : std::string());
     d->type = DEV_HIP;
     // fp64 MFMA: 2048 flop / 64 cycles per SIMD -> 32 flop/clk/SIMD (measured 77.6 TF on MI355X)
     double ghz = d->props.clockRate > 0 ? d->props.clockRate / 1e6 : 2.4;
@@ -1585,7 +1649,7 @@ void hip_devices_init(Context* ctx) {
   // peer access between the GPUs this process drives (xGMI)
   for (auto* a : g_hip_devices)
     for (auto* b : g_hip_devices) {
-      if (a == b) continue;
+      if (a == b || a->ordinal == b->ordinal) continue;
       int can = 0;
       if (hipDeviceCanAccessPeer(&can, a->ordinal, b->ordinal) == hipSuccess && can) {
         (void)hipSetDevice(a->ordinal);

@@ -59,6 +59,7 @@ struct GpuTask {
   uint8_t access[kMaxFlows] = {};
   DataCopy* dev_copy[kMaxFlows] = {};
   bool issued_copy[kMaxFlows] = {};
+  DataCopy* peer_src[kMaxFlows] = {};  // read-only flow pulled from another GPU's copy (one reader held on it)
   hipEvent_t ev_in = nullptr;
   hipEvent_t ev_out = nullptr;
   int stream = -1;
@@ -124,6 +125,16 @@ struct HipDevice : Device {
   std::condition_variable in_cv;
   std::vector<GpuTask*> incoming;
   std::atomic<int> incoming_n{0};
+  // copies of this device another device read from (peer stage-in) and is done
+  // with: this manager drops that reader and re-files the copy in its LRU
+  std::vector<DataCopy*> peer_done;
+  std::atomic<int> peer_done_n{0};
+  // another GPU's valid copy of d at `version` to stage a read-only flow from
+  // instead of the host (one reader taken on it), or nullptr
+  DataCopy* peer_source(Data* d, uint32_t version);
+  void peer_release(DataCopy* c);  // called by the reading device
+  bool peer_accessible(const HipDevice* peer) const;
+  bool peer_stage_in = true;  // device_hip_peer_stage_in
   // manager-thread private state
   std::vector<GpuTask*> pending, staging, ready;
   std::vector<std::deque<ExecGroup>> executing;
@@ -148,6 +159,7 @@ struct HipDevice : Device {
   bool wave_priority = true;
   int hp_route = 1;  // device_hip_hp_on_critical_stream: 1 critical stream, 0 bulk streams, 2 stream 1 alone
   bool cu_masked = false;
+  int replicas = 1;  // devices registered on this GPU (device_hip_replicas)
   bool batching = true;
   int sort_pending = 1;  // 0 arrival order, 1 priority, 2 data availability then priority
   int missing_on_device(GpuTask* g) const;

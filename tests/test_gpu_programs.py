@@ -124,6 +124,47 @@ def test_nvlink_user_device_copies(progs):
     assert f"gemm1 {8 * n}/{8 * n} gemm2 {8 * n}/{8 * n} user_ptr {8 * n} misplaced 0 cpu 0 bad_c 0 bad_user 0 bad_handle 0" in line, line
 
 
+def _d2d_bytes(stderr):
+    """Summed d2d bytes of device_show_statistics lines, and the HIP device names."""
+    tot, names = 0, []
+    for line in stderr.splitlines():
+        if line.startswith("[parsec] device ") and " d2d=" in line:
+            names.append(line.split()[3])
+            tot += int(line.split(" d2d=")[1].split()[0])
+    return tot, names
+
+
+TWO_LOGICAL = {"PARSEC_MCA_device_hip_replicas": "2", "PARSEC_MCA_device_show_statistics": "1"}
+
+
+@pytest.mark.gpu
+def test_nvlink_two_logical_devices(progs):
+    """The GPU registered twice (device_hip_replicas 2): nvlink's GEMM1 chains
+    move A from one device to the next, so the device-to-device stage-in
+    (hipMemcpyPeerAsync between two devices of the process) really runs --
+    the route two distinct GPUs of one process take, here on one GPU."""
+    r = _run([progs("nvlink_hip"), "8", "256"], env=TWO_LOGICAL)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = [x for x in r.stdout.splitlines() if x.startswith("nvlink ")][-1]
+    assert "gpus 2 " in line, line
+    assert "gemm1 16/16 gemm2 16/16 user_ptr 16 misplaced 0 cpu 0 bad_c 0 bad_user 0 bad_handle 0" in line, line
+    d2d, names = _d2d_bytes(r.stderr)
+    assert "hip0.0" in names and "hip0.1" in names, r.stderr[-2000:]
+    assert d2d > 0, r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+def test_dtd_gpu_chores_two_logical_devices(progs):
+    """The DTD GPU-chore programs over two devices of one process (the
+    reference's dtd_test_cuda_task_insert multi-device cases)."""
+    r = _run([progs("dtd_gpu_capi")], env=TWO_LOGICAL)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for name in ("new_tile", "memset (GPU)", "memset (alternating)", "memset_read (GPU)", "write_read (GPU)", "gemm_handle"):
+        assert f"{name}: ok" in r.stdout, r.stdout
+    _, names = _d2d_bytes(r.stderr)
+    assert [n for n in names if n.startswith("hip")] == ["hip0.0", "hip0.1"], r.stderr[-2000:]
+
+
 # ------------------------------------------------------------- write_check
 @pytest.mark.skipif(shutil.which("cmake") is None, reason="cmake not available")
 def test_write_check_out_of_tree_cmake(tmp_path, pa):
