@@ -145,7 +145,7 @@ def _factor_gpu(pa, S, N, nb, mode, limit=0.0):
         pa.trsm_inverse_mode(prev, prev_limit)
 
 
-@pytest.mark.parametrize("nb", [256, 512, 1024])
+@pytest.mark.parametrize("nb", [128, 256, 512, 1024])
 def test_trsm_inverse_modes_gpu(pa, nb):
     """Panel solve through W = L^-1 (mode 0), by substitution (mode 2) and auto
     (mode 1). Auto decides per panel from max|L| max|W|: by default the tile
@@ -156,7 +156,9 @@ def test_trsm_inverse_modes_gpu(pa, nb):
     cond 1e12 (numerics sweep: profiles/r4_trsm_inverse_numerics.txt) every mode
     is backward stable; auto with its default limit takes the inverse path (same
     factor as mode 0) and auto with limit 1 takes the substitution path (same
-    factor as mode 2), through either estimate route."""
+    factor as mode 2), through either estimate route -- below nb 256 through
+    the host route only (W has no spare slots for the device gate there: a W
+    factored by another process takes the inverse path unguarded)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     N = 2048
@@ -190,7 +192,7 @@ def test_trsm_inverse_modes_gpu(pa, nb):
     assert d02 > 0  # the two solves differ (by ~cond(L(k,k)) eps)
     for La, Lb in ((L1, L0), (L1d, L0)):  # auto below the limit = the inverse path
         assert torch.linalg.norm(La - Lb).item() < 1e-3 * d02
-    for La, Lb in ((L1s, L2), (L1ds, L2)):  # auto above it = the substitution path
+    for La, Lb in ((L1s, L2), (L1ds, L2 if nb >= 256 else L0)):  # auto above it = the substitution path
         assert torch.linalg.norm(La - Lb).item() < 1e-3 * d02
 
 
