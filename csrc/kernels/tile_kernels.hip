@@ -157,7 +157,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // k-tile's MFMA work instead of in front of it, and the epilogue forms
 // alpha AB + beta C from registers (a pure store). Needs the register budget of
 // two waves per SIMD (launched with one workgroup per CU).
-template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF, int PF, int EPI>
+template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF, int PF, int EPI, bool DL = false>
 __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, int ks, int nsplit, double (&As)[NBUF][BK][BM + (((BM % 32) == 16) ? 0 : 16)],
                                           double (&Bs)[NBUF][BK][BN + (((BN % 32) == 16) ? 0 : 16)]) {
   static_assert(PF == 1 || NBUF == 2, "two tiles in flight need the double-buffered LDS");
@@ -331,6 +331,45 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
   constexpr bool LATE = EPI == 2;
   const bool late = LATE && FULL && !split && d.beta != 0.0;
   double4_t cr[LATE ? FN : 1][LATE ? FM : 1];
+  if constexpr (DL) {
+    // Direct-to-LDS k-tiles (global_load_lds_dwordx4): for op(A) = A and
+    // op(B) = B^T a k-row of the A (B) tile is 128 contiguous doubles in memory
+    // and in LDS, i.e. exactly one wave-wide 16-byte-per-lane DMA, so the tiles
+    // skip the VGPR staging and the ds_write pass; the DMA of k-tile kt + 1
+    // runs under the MFMAs of k-tile kt (one barrier per k-tile).
+    static_assert(!TRANSA && TRANSB && FULL && NBUF == 2 && PF == 1 && BM == 128 && BN == 128 && !LATE, "direct-LDS tiles: NT operands, full 128x128 tiles");
+    constexpr int NW = NT / 64;
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    auto dl_tile = [&](int k0, int buf) {
+#pragma unroll
+      for (int e = 0; e < BK / NW; ++e) {
+        const int kk = wave_u + NW * e;
+        __builtin_amdgcn_global_load_lds((const void*)(A + (size_t)(k0 + kk) * lda + m0 + 2 * lane),
+                                         (__attribute__((address_space(3))) void*)&As[buf][kk][0], 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(B + (size_t)(k0 + kk) * ldb + n0 + 2 * lane),
+                                         (__attribute__((address_space(3))) void*)&Bs[buf][kk][0], 16, 0, 0);
+      }
+    };
+    dl_tile(0, 0);
+    if (preload && d.beta != 0.0) {
+      const double cs = d.beta / d.alpha;
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) {
+          const double* p = Cr + (size_t)(n0 + wn * WTN + i * 16 + fk) * ldcr + (m0 + wm * WTM + j * 16 + fr);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = cs * p[(size_t)4 * r * ldcr];
+        }
+    }
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int cur = kt & 1;
+      __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA of k-tile kt has landed
+      __syncthreads();                 // ... every wave's; and buffer cur ^ 1 is free again
+      if (kt + 1 < nkt) dl_tile((kt + 1) * BK, cur ^ 1);
+      mma_tile(cur);
+    }
+  } else {
   load_tile(0);
   if (LATE && late) {
 #pragma unroll
@@ -386,6 +425,7 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
     }
   }
   }
+  }  // DL
 
   const double alpha = d.alpha, beta = (preload || late) ? 0.0 : d.beta;
 #pragma unroll
@@ -413,12 +453,12 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
   crit_release(args.claim);
 }
 
-template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF = 2, int OCC = WM * WN / 2, int PF = 1, int EPI = 0>
+template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF = 2, int OCC = WM * WN / 2, int PF = 1, int EPI = 0, bool DL = false>
 __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OCC))) void dgemm_batch_kernel(const GemmBatchArgs args) {
   constexpr int PADM = ((BM % 32) == 16) ? 0 : 16;
   constexpr int PADN = ((BN % 32) == 16) ? 0 : 16;
-  __shared__ double As[NBUF][BK][BM + PADM];
-  __shared__ double Bs[NBUF][BK][BN + PADN];
+  __shared__ __attribute__((aligned(16))) double As[NBUF][BK][BM + PADM];
+  __shared__ __attribute__((aligned(16))) double Bs[NBUF][BK][BN + PADN];
   PARSEC_WAVE_PRIO(args.prio);
   // Workgroups [0, main_tiles) own whole tiles (XCD-aware order); the ones
   // dispatched last split the K range of the tail tiles (wave quantisation:
@@ -450,7 +490,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
     ks = u % nsplit;
   }
   if (tile >= args.total_tiles) return;
-  gemm_tile<BM, BN, BK, WM, WN, TRANSA, TRANSB, FULL, NBUF, PF, EPI>(args, tile, ks, nsplit, As, Bs);
+  gemm_tile<BM, BN, BK, WM, WN, TRANSA, TRANSB, FULL, NBUF, PF, EPI, DL>(args, tile, ks, nsplit, As, Bs);
 }
 
 // Persistent form: a grid of (at most) one round of resident workgroups walks
@@ -865,6 +905,9 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
   static const int late_env = getenv("PARSEC_GEMM_LATE_C") ? atoi(getenv("PARSEC_GEMM_LATE_C")) : 0;
   const bool late = BM == 128 && full && !epi && (epi_env == 2 || late_env > 0) && pad;
   const bool persist = persist_env != 0 && full && BM == 128 && a.stagger == 0 && total > slots;
+  // direct-to-LDS k-tiles for the NT bulk GEMM (PARSEC_GEMM_DLDS=1; off until measured)
+  static const int dl_env = getenv("PARSEC_GEMM_DLDS") ? atoi(getenv("PARSEC_GEMM_DLDS")) : 0;
+  const bool dl = dl_env != 0 && !late && a.stagger == 0;
   if (persist) {
     a.main_tiles = total;
     a.ksplit = 1;
@@ -880,6 +923,11 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
   }
 #define PARSEC_GEMM_LAUNCH_E(TA, TB, E)                                                                                                      \
   do {                                                                                                                                      \
+    if constexpr (!(TA) && (TB) && BM == 128 && BN == 128 && NBUF == 2 && PF == 1)                                                          \
+      if (dl && full && !persist) {                                                                                                          \
+        hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, OCC, PF, E, true>), grid, block, pad, stream, a);     \
+        break;                                                                                                                               \
+      }                                                                                                                                      \
     if (persist) hipLaunchKernelGGL((dgemm_persist_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, OCC, PF, E>), grid, block, pad, stream, a);  \
     else if (full) hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, OCC, PF, E>), grid, block, pad, stream, a);  \
     else hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, false, NBUF, OCC, PF, 0>), grid, block, pad, stream, a);          \
@@ -962,6 +1010,9 @@ static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) 
     case 9: launch_gemm_shape<128, 128, 16, 2, 4, 2, 2, 2>(a, descs, n, stream); break;
     // the same at the default occupancy bound (128 VGPRs)
     case 10: launch_gemm_shape<128, 128, 16, 2, 4, 2, 4, 2>(a, descs, n, stream); break;
+    // k-tiles of 32 (144 KB of LDS: one workgroup per CU, half the barriers per
+    // flop; with PARSEC_GEMM_DLDS the k-tiles go straight to LDS)
+    case 11: launch_gemm_shape<128, 128, 32, 2, 4, 2>(a, descs, n, stream); break;
     // default: 8 waves (2 x 4) of 64x32 per 128x128 tile, 126 VGPRs -> 4 waves per
     // SIMD with two workgroups per CU (measured: DPOTRF 64k +4 %, 16k +7 % over
     // the 4-wave 64x64-per-wave kernel = variant 8; profiles/r1_gemm_variants_v8.log;
