@@ -337,7 +337,7 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
     // and in LDS, i.e. exactly one wave-wide 16-byte-per-lane DMA, so the tiles
     // skip the VGPR staging and the ds_write pass; the DMA of k-tile kt + 1
     // runs under the MFMAs of k-tile kt (one barrier per k-tile).
-    static_assert(!TRANSA && TRANSB && FULL && NBUF == 2 && PF == 1 && BM == 128 && BN == 128 && !LATE, "direct-LDS tiles: NT operands, full 128x128 tiles");
+    static_assert(!TRANSA && TRANSB && FULL && (NBUF == 2 || NBUF == 3) && PF == 1 && BM == 128 && BN == 128 && !LATE, "direct-LDS tiles: NT operands, full 128x128 tiles");
     constexpr int NW = NT / 64;
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     auto dl_tile = [&](int k0, int buf) {
@@ -362,12 +362,30 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
           for (int r = 0; r < 4; ++r) acc[i][j][r] = cs * p[(size_t)4 * r * ldcr];
         }
     }
-    for (int kt = 0; kt < nkt; ++kt) {
-      const int cur = kt & 1;
-      __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA of k-tile kt has landed
-      __syncthreads();                 // ... every wave's; and buffer cur ^ 1 is free again
-      if (kt + 1 < nkt) dl_tile((kt + 1) * BK, cur ^ 1);
-      mma_tile(cur);
+    if constexpr (NBUF == 2) {
+      for (int kt = 0; kt < nkt; ++kt) {
+        const int cur = kt & 1;
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA of k-tile kt has landed
+        __syncthreads();                 // ... every wave's; and buffer cur ^ 1 is free again
+        if (kt + 1 < nkt) dl_tile((kt + 1) * BK, cur ^ 1);
+        mma_tile(cur);
+      }
+    } else {
+      // three buffers: k-tile kt + 2 is requested while kt is multiplied (two
+      // k-tiles of DMA in flight to cover the memory latency under load)
+      constexpr int PER_TILE = 2 * (BK / NW);  // DMA instructions per wave per k-tile
+      static_assert(PER_TILE < 16, "vmcnt field");
+      if (nkt > 1) dl_tile(BK, 1);
+      int cur = 0, nxt = 2;
+      for (int kt = 0; kt < nkt; ++kt) {
+        if (kt + 1 < nkt) __builtin_amdgcn_s_waitcnt(PER_TILE | (7 << 4) | (15 << 8));  // only k-tile kt + 1 may still be in flight
+        else __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();  // every wave's k-tile kt landed; buffer (kt + 2) % 3 = (kt - 1) % 3 is free again
+        if (kt + 2 < nkt) dl_tile((kt + 2) * BK, nxt);
+        mma_tile(cur);
+        cur = cur == 2 ? 0 : cur + 1;
+        nxt = nxt == 2 ? 0 : nxt + 1;
+      }
     }
   } else {
   load_tile(0);
@@ -923,7 +941,7 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
   }
 #define PARSEC_GEMM_LAUNCH_E(TA, TB, E)                                                                                                      \
   do {                                                                                                                                      \
-    if constexpr (!(TA) && (TB) && BM == 128 && BN == 128 && NBUF == 2 && PF == 1)                                                          \
+    if constexpr (!(TA) && (TB) && BM == 128 && BN == 128 && (NBUF == 2 || NBUF == 3) && PF == 1)                                          \
       if (dl && full && !persist) {                                                                                                          \
         hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, TA, TB, true, NBUF, OCC, PF, E, true>), grid, block, pad, stream, a);     \
         break;                                                                                                                               \
@@ -1013,6 +1031,8 @@ static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) 
     // k-tiles of 32 (144 KB of LDS: one workgroup per CU, half the barriers per
     // flop; with PARSEC_GEMM_DLDS the k-tiles go straight to LDS)
     case 11: launch_gemm_shape<128, 128, 32, 2, 4, 2>(a, descs, n, stream); break;
+    // three LDS k-tile buffers (110 KB), only with PARSEC_GEMM_DLDS=1: two k-tiles of DMA in flight
+    case 12: launch_gemm_shape<128, 128, 16, 2, 4, 3>(a, descs, n, stream); break;
     // default: 8 waves (2 x 4) of 64x32 per 128x128 tile, 126 VGPRs -> 4 waves per
     // SIMD with two workgroups per CU (measured: DPOTRF 64k +4 %, 16k +7 % over
     // the 4-wave 64x64-per-wave kernel = variant 8; profiles/r1_gemm_variants_v8.log;
