@@ -1029,9 +1029,10 @@ static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) 
     // the same at the default occupancy bound (128 VGPRs)
     case 10: launch_gemm_shape<128, 128, 16, 2, 4, 2, 4, 2>(a, descs, n, stream); break;
     // k-tiles of 32 (144 KB of LDS: one workgroup per CU, half the barriers per
-    // flop; with PARSEC_GEMM_DLDS the k-tiles go straight to LDS)
+    // flop; with PARSEC_GEMM_DLDS the k-tiles go straight to LDS); measured 10 % slower
     case 11: launch_gemm_shape<128, 128, 32, 2, 4, 2>(a, descs, n, stream); break;
-    // three LDS k-tile buffers (110 KB), only with PARSEC_GEMM_DLDS=1: two k-tiles of DMA in flight
+    // three LDS k-tile buffers (110 KB), only with PARSEC_GEMM_DLDS=1: two k-tiles of DMA in
+    // flight; measured 15 % slower than variant 0 (profiles/r5_gemm_direct_lds.txt)
     case 12: launch_gemm_shape<128, 128, 16, 2, 4, 3>(a, descs, n, stream); break;
     // default: 8 waves (2 x 4) of 64x32 per 128x128 tile, 126 VGPRs -> 4 waves per
     // SIMD with two workgroups per CU (measured: DPOTRF 64k +4 %, 16k +7 % over
