@@ -233,11 +233,14 @@ DataCopy* data_pull_to_host(Data* d) {
     host = d->copy(0);
   }
   DataCopy* src = data_start_transfer_ownership_to_copy(d, 0, FLOW_READ);
+  bool pinned = false;
+  if (src && src != host && src->device_index != 0) src = pin_gpu_source(d, 0, host, src, FLOW_READ, &pinned);
   if (src && src != host) {
     device_memcpy(0, host->device_private, src->device_index, src->device_private, d->nb_elts);
     auto* dev = DeviceRegistry::instance().get(src->device_index);
     if (dev) dev->stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
   }
+  if (pinned) unpin_gpu_copy(src);
   data_end_transfer_ownership_to_copy(d, 0, FLOW_READ);
   return host;
 }

@@ -62,6 +62,13 @@ int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t b
 void device_memcpy_stats(uint64_t out[3], bool reset);
 // The process-wide copy stream of HIP device `ordinal` (created on first use).
 hipStream_t gpu_copy_stream(int ordinal);
+// A GPU copy chosen as the source of a transfer to `dst_device` (by
+// data_start_transfer_ownership_to_copy), pinned with one reader under the data
+// lock so its device cannot evict it before the transfer ran (re-chosen when it
+// was evicted in between); *pinned says whether the returned copy is held.
+// unpin_gpu_copy hands the reader back to the owning device's manager.
+DataCopy* pin_gpu_source(Data* d, int dst_device, DataCopy* local, DataCopy* src, uint8_t access, bool* pinned);
+void unpin_gpu_copy(DataCopy* c);
 int device_hip_ordinal(int device_index);  // -1 if not a HIP device
 int first_gpu_device_index();
 // Bring the newest version of `d` to the host (device 0), synchronously.

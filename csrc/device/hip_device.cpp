@@ -767,6 +767,8 @@ bool HipDevice::progress_prefetch() {
     }
     if (local->transfer_status == TRANSFER_UNDER) { data_release(d); continue; }
     DataCopy* src = data_start_transfer_ownership_to_copy(d, device_index, FLOW_READ);
+    bool pinned = false;
+    if (src && src != local && src->device_index != 0) src = pin_source(d, local, src, FLOW_READ, &pinned);
     if (!src || src == local) {
       data_end_transfer_ownership_to_copy(d, device_index, FLOW_READ);
       data_release(d);
@@ -781,6 +783,7 @@ bool HipDevice::progress_prefetch() {
     local->transfer_status = TRANSFER_UNDER;
     local->readers.fetch_add(1);
     PrefetchJob j;
+    j.src_pin = pinned ? src : nullptr;
     j.ev = get_event();
     PARSEC_HIP_CHECK(hipEventRecord(j.ev, s_copy));
     j.local = local;
@@ -794,6 +797,7 @@ bool HipDevice::progress_prefetch() {
     j.local->readers.fetch_sub(1);
     lru_touch(j.local);
     put_event(j.ev);
+    if (j.src_pin) peer_release(j.src_pin);
     data_release(j.d);
     prefetch_jobs.pop_front();
     did = true;
@@ -946,6 +950,9 @@ int HipDevice::stage_in(GpuTask* g) {
     g->dev_copy[fi] = local;
     if (local->transfer_status == TRANSFER_UNDER) { any = true; continue; }  // ordered behind the in-flight copy on s_copy
     DataCopy* src = data_start_transfer_ownership_to_copy(d, device_index, g->access[fi]);
+    bool pinned = false;
+    if (src && src != local && src->device_index != 0) src = pin_source(d, local, src, g->access[fi], &pinned);
+    if (pinned) g->peer_src[fi] = src;
     if (src && src != local && custom_in && src->device_index == 0) {
       // the chore moves this flow itself (one stage_in call for all of them below)
       sctx.flow_mask |= 1u << fi;
@@ -962,7 +969,7 @@ int HipDevice::stage_in(GpuTask* g) {
       // read-only flow whose source is the host copy: a GPU of this process
       // holding the same version is the faster source (device-to-device over
       // xGMI; reference device_cuda_module.c:1308-1360)
-      if (src->device_index == 0 && !(g->access[fi] & FLOW_WRITE) && peer_stage_in)
+      if (src->device_index == 0 && !pinned && !(g->access[fi] & FLOW_WRITE) && peer_stage_in)
         if (DataCopy* alt = peer_source(d, src->version)) {
           src = alt;
           g->peer_src[fi] = alt;
@@ -1030,7 +1037,31 @@ DataCopy* HipDevice::peer_source(Data* d, uint32_t version) {
   return nullptr;
 }
 
-void HipDevice::peer_release(DataCopy* c) {
+DataCopy* HipDevice::pin_source(Data* d, DataCopy* local, DataCopy* src, uint8_t access, bool* pinned) {
+  return pin_gpu_source(d, device_index, local, src, access, pinned);
+}
+
+DataCopy* pin_gpu_source(Data* d, int dst_device, DataCopy* local, DataCopy* src, uint8_t access, bool* pinned) {
+  *pinned = false;
+  for (int tries = 0; src && src != local && src->device_index != 0; ++tries) {
+    {
+      std::lock_guard<SpinLock> lk(d->lock);  // the owner evicts under this lock after checking readers
+      if (d->copy(src->device_index) == src && src->coherency_state != COHERENCY_INVALID && src->device_private) {
+        src->readers.fetch_add(1);
+        *pinned = true;
+        return src;
+      }
+    }
+    // evicted since it was chosen (only clean copies are: an equally new one exists)
+    if (tries >= 8) fatal("device %d: the source copy of a transfer keeps being evicted", dst_device);
+    src = data_start_transfer_ownership_to_copy(d, dst_device, access);
+  }
+  return src;
+}
+
+void HipDevice::peer_release(DataCopy* c) { unpin_gpu_copy(c); }
+
+void unpin_gpu_copy(DataCopy* c) {
   auto* owner = static_cast<HipDevice*>(DeviceRegistry::instance().devices[c->device_index]);
   {
     std::lock_guard<std::mutex> lk(owner->in_m);

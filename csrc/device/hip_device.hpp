@@ -95,6 +95,7 @@ struct PrefetchJob {
   hipEvent_t ev = nullptr;
   DataCopy* local = nullptr;
   Data* d = nullptr;
+  DataCopy* src_pin = nullptr;  // another GPU's copy read by the transfer (one reader held)
 };
 
 struct ExecGroup {
@@ -133,6 +134,10 @@ struct HipDevice : Device {
   // instead of the host (one reader taken on it), or nullptr
   DataCopy* peer_source(Data* d, uint32_t version);
   void peer_release(DataCopy* c);  // called by the reading device
+  // the source data_start_transfer_ownership_to_copy chose, pinned (one reader,
+  // taken under the data lock) when it is another GPU's copy, so that GPU cannot
+  // evict it before this device's copy from it ran; *pinned tells which
+  DataCopy* pin_source(Data* d, DataCopy* local, DataCopy* src, uint8_t access, bool* pinned);
   bool peer_accessible(const HipDevice* peer) const;
   bool peer_stage_in = true;  // device_hip_peer_stage_in
   // manager-thread private state

@@ -25,3 +25,18 @@ def test_dpotrf_forced_eviction(pa, N, nb, frac, prefetch):
     r = subprocess.run([sys.executable, WORKER, str(N), str(nb), str(frac), str(prefetch)], capture_output=True, text=True, timeout=150)
     print(r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr[-2000:])
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+
+
+TWO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp", "gpu_two_devices.py")
+
+
+@pytest.mark.parametrize("N,nb,frac", [(4096, 512, 0.0), (4096, 256, 0.3)])
+def test_dpotrf_two_logical_devices(pa, N, nb, frac):
+    """DPOTRF on host tiles with the GPU registered as two devices
+    (device_hip_replicas 2): both devices run tasks, tiles move between them
+    device to device (newest version on the other device, or a read-only input
+    staged from the other device's copy), with and without a capped tile cache."""
+    _gpu()
+    r = subprocess.run([sys.executable, TWO, str(N), str(nb), str(frac)], capture_output=True, text=True, timeout=150)
+    print(r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr[-2000:])
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
