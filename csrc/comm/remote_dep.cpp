@@ -165,7 +165,7 @@ void release_send(SendState* s) {
     if (s->registered & (1u << f)) g_ce->mem_unregister(&s->reg[f]);
   for (auto*& c : s->data)
     if (c) {
-      if (c->device_index != 0) c->readers.fetch_sub(1);
+      if (c->device_index != 0) unpin_gpu_copy(c);  // its device re-files it in its LRU when the last reader left
       data_copy_release(c);
       c = nullptr;
     }

@@ -1062,7 +1062,13 @@ DataCopy* pin_gpu_source(Data* d, int dst_device, DataCopy* local, DataCopy* src
 void HipDevice::peer_release(DataCopy* c) { unpin_gpu_copy(c); }
 
 void unpin_gpu_copy(DataCopy* c) {
-  auto* owner = static_cast<HipDevice*>(DeviceRegistry::instance().devices[c->device_index]);
+  Device* dev = DeviceRegistry::instance().get(c->device_index);
+  if (!dev || dev->type != DEV_HIP) {  // not an engine-managed GPU copy (template device memory)
+    c->readers.fetch_sub(1);
+    return;
+  }
+  auto* owner = static_cast<HipDevice*>(dev);
+  data_copy_retain(c);  // the caller may drop its own reference right away
   {
     std::lock_guard<std::mutex> lk(owner->in_m);
     owner->peer_done.push_back(c);
@@ -1405,8 +1411,10 @@ bool HipDevice::progress() {
       done.swap(peer_done);
       peer_done_n.store(0);
     }
-    for (DataCopy* c : done)
+    for (DataCopy* c : done) {
       if (c->readers.fetch_sub(1) == 1) lru_touch(c);
+      data_copy_release(c);
+    }
     did = true;
   }
   if (!w2r_jobs.empty() && progress_w2r()) did = true;
