@@ -201,8 +201,12 @@ int complete_async_task(ExecutionStream* es, Task* t) {
   while (s == ASYNC_RUNNING)
     if (__atomic_compare_exchange_n(&t->async_state, &s, (uint8_t)ASYNC_COMPLETE_REQUESTED, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) return 0;
   t->async_state = ASYNC_NONE;
-  // the caller may still read the task (e.g. t->taskpool) after this returns
-  if (auto rel = t->task_class->hold_task(t)) t_held.push_back({rel, t});
+  // the caller may still read the task (e.g. t->taskpool) after this returns;
+  // held until this thread's next scheduling step (compute threads only: the
+  // comm thread and GPU managers never come back to worker_loop)
+  ExecutionStream* me = my_execution_stream();
+  if (me && !me->is_manager)
+    if (auto rel = t->task_class->hold_task(t)) t_held.push_back({rel, t});
   return complete_task_execution(es ? es : my_execution_stream(), t);
 }
 
