@@ -199,6 +199,7 @@ Context* context_init(int nb_cores, std::vector<std::string>& args) {
   args = reg.parse_cmdline(args);
   output_init();
   Context* ctx = new Context();
+  context_set_live(ctx, true);
 
   int param_cores = (int)reg.reg_int("runtime", "", "num_cores", "Number of compute threads (0 = all allowed cores)", 0);
   auto cpus = allowed_cpus();
@@ -361,6 +362,7 @@ int context_fini(Context** pctx) {
   }
   delete ctx->barrier;
   set_my_execution_stream(nullptr);
+  context_set_live(ctx, false);
   delete ctx;
   *pctx = nullptr;
   PARSEC_DEBUG(kVerbDebug, "fini", "context released");

@@ -573,6 +573,12 @@ struct alignas(64) ExecutionStream {  // one thread writes it per task: keep it 
   ProfilingStream* prof = nullptr;
   uint32_t rand_seed = 1;
   bool is_manager = false;  // GPU manager / comm thread (does not select tasks)
+  // the taskpool whose task this thread is completing (complete_task_execution):
+  // taskpool deletion waits until no thread is inside one of its completions
+  // (a body ending the taskpool -- set_nb_tasks(tp, 0), reference
+  // tests/apps/haar_tree/walk.jdf:47 -- can let context_wait return while the
+  // task that activated it still walks its successors)
+  std::atomic<Taskpool*> completing_tp{nullptr};
   // statistics
   uint64_t nb_executed = 0, nb_selected = 0, nb_stolen = 0;
   uint32_t cpu_exec_pending = 0;
@@ -730,6 +736,10 @@ int schedule_async_task(ExecutionStream* es, Task* t, int32_t distance);
 int complete_async_task(ExecutionStream* es, Task* t);
 // delete the taskpools freed from bodies that have terminated since
 void context_drain_zombies(Context* ctx);
+// contexts between context_init and context_fini (a taskpool freed after its
+// context's fini must not look at the context's streams)
+void context_set_live(Context* ctx, bool live);
+bool context_is_live(Context* ctx);
 // the task whose CPU body the calling thread is running (nullptr outside one)
 Task* current_task();
 int reschedule(ExecutionStream* es, Task* t);

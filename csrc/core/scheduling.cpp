@@ -284,6 +284,13 @@ int execute_task(ExecutionStream* es, Task* t) {
 }
 
 int complete_task_execution(ExecutionStream* es, Task* t) {
+  Taskpool* const prev_tp = es ? es->completing_tp.load(std::memory_order_relaxed) : nullptr;
+  if (es) es->completing_tp.store(t->taskpool, std::memory_order_release);
+  struct Done {
+    ExecutionStream* es;
+    Taskpool* prev;
+    ~Done() { if (es) es->completing_tp.store(prev, std::memory_order_release); }
+  } done{es, prev_tp};
   PARSEC_PINS(es, PINS_COMPLETE_EXEC_BEGIN, t);
   if (g_paranoid && t->status == STATUS_COMPLETE) fatal("paranoid: task %s completed twice", t->task_class->describe(t).c_str());
   t->status = STATUS_PREPARE_OUTPUT;
@@ -431,7 +438,34 @@ Taskpool::~Taskpool() {
   if (tdm && termdet_private) tdm->release_taskpool(this);
 }
 
+static std::mutex g_live_ctx_m;
+static std::vector<Context*> g_live_ctx;
+void context_set_live(Context* ctx, bool live) {
+  std::lock_guard<std::mutex> g(g_live_ctx_m);
+  if (live) g_live_ctx.push_back(ctx);
+  else g_live_ctx.erase(std::remove(g_live_ctx.begin(), g_live_ctx.end(), ctx), g_live_ctx.end());
+}
+bool context_is_live(Context* ctx) {
+  std::lock_guard<std::mutex> g(g_live_ctx_m);
+  return std::find(g_live_ctx.begin(), g_live_ctx.end(), ctx) != g_live_ctx.end();
+}
+
+// No thread may still be inside a completion of one of tp's tasks (the calling
+// thread excepted: a completion callback freeing its own taskpool).
+static void wait_completions_drained(Taskpool* tp) {
+  Context* ctx = tp->context;
+  if (!ctx || !context_is_live(ctx)) return;
+  ExecutionStream* me = my_execution_stream();
+  auto drain = [tp, me](ExecutionStream* es) {
+    Backoff b;
+    while (es && es != me && es->completing_tp.load(std::memory_order_acquire) == tp) b.idle();
+  };
+  for (ExecutionStream* es : ctx->all_es) drain(es);
+  for (ExecutionStream* es : ctx->aux_es) drain(es);
+}
+
 static void taskpool_destroy(Taskpool* tp) {
+  wait_completions_drained(tp);
   if (tp->destructor_hook) tp->destructor_hook();
   for (auto* d : DeviceRegistry::instance().devices) if (d) d->taskpool_unregister(tp);
   delete tp;

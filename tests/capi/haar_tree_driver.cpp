@@ -35,7 +35,7 @@ static void cksum_node(tree_dist_t* tree, node_t* node, int n, int l, void* para
   up ^= (((int64_t)l) << 32) | (int64_t)n;
   int64_t ov, nv;
   do {
-    ov = *cksum;
+    ov = __atomic_load_n(cksum, __ATOMIC_RELAXED);
     nv = ov ^ up;
   } while (!parsec_atomic_cas_int64(cksum, ov, nv));
   (void)tree;
@@ -50,7 +50,7 @@ static void count_node(tree_dist_t*, node_t*, int n, int l, void*) {
   parsec_atomic_fetch_add_int32(&nodes_up, 1);
   int64_t ov, nv;
   do {
-    ov = keys_up;
+    ov = __atomic_load_n(&keys_up, __ATOMIC_RELAXED);
     nv = ov ^ ((((int64_t)l) << 32) | (int64_t)n);
   } while (!parsec_atomic_cas_int64(&keys_up, ov, nv));
 }

@@ -185,3 +185,32 @@ def test_reference_class_programs_sanitized(sanitized, tmp_path, prog, args):
     # checking would report the test, not the containers
     r = _run_sanitized(kind, exe, args, timeout=600, leaks=False)
     assert "Error in implementation" not in r.stdout + r.stderr
+
+
+HAAR = os.path.join(REF, "tests/apps/haar_tree")
+SUM_VALUE = 0xbdae8a4ea45fc32e  # reference tests/apps/haar_tree/main.c:23
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("dyn", [False, True], ids=["project", "project_dyn"])
+def test_reference_haar_tree_sanitized(sanitized, tmp_path, dyn):
+    """The reference's haar-tree application (project(_dyn).jdf + walk.jdf over
+    tree_dist.c, unmodified) under TSan / ASan: generated per-class task views,
+    a user startup_fn building the root task by hand, make_key / hash_struct /
+    find_deps / alloc_deps hooks on a 2^32-wide space, the concurrent hash table
+    and a body ending the taskpool (set_nb_tasks from a body)."""
+    kind, _ = sanitized
+    proj = "project_dyn" if dyn else "project"
+    srcs = [ptgpp.compile_jdf(os.path.join(HAAR, j + ".jdf"), str(tmp_path))[0] for j in (proj, "walk")]
+    cc, libs = ptgpp.compile_flags(False, kind)
+    exe = str(tmp_path / proj)
+    drv = os.path.join(ROOT, "tests", "capi", "haar_tree_driver.cpp")
+    r = subprocess.run(cc + list(ptgpp.C_BODIES) + (["-DHAAR_DYN"] if dyn else []) +
+                       [f"-I{HAAR}", f"-I{tmp_path}", f"-I{REF}", "-x", "c++", drv, os.path.join(HAAR, "tree_dist.c"), "-x", "none"] + srcs +
+                       ["-o", exe] + libs + ["-lm"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = _run_sanitized(kind, exe, ["--"], leaks=False)
+    line = [l.split() for l in r.stdout.splitlines() if l.startswith("haar rank")]
+    assert len(line) == 1, r.stdout[-2000:]
+    if not dyn:
+        assert int(line[0][line[0].index("cksum") + 1], 16) == SUM_VALUE, r.stdout[-2000:]
