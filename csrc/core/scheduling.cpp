@@ -284,13 +284,16 @@ int execute_task(ExecutionStream* es, Task* t) {
 }
 
 int complete_task_execution(ExecutionStream* es, Task* t) {
-  Taskpool* const prev_tp = es ? es->completing_tp.load(std::memory_order_relaxed) : nullptr;
-  if (es) es->completing_tp.store(t->taskpool, std::memory_order_release);
+  // flagged on the calling thread's own stream (`es` may be another thread's:
+  // __parsec_complete_execution callers pass an arbitrary stream)
+  ExecutionStream* const me = my_execution_stream();
+  Taskpool* const prev_tp = me ? me->completing_tp.load(std::memory_order_relaxed) : nullptr;
+  if (me) me->completing_tp.store(t->taskpool, std::memory_order_release);
   struct Done {
     ExecutionStream* es;
     Taskpool* prev;
     ~Done() { if (es) es->completing_tp.store(prev, std::memory_order_release); }
-  } done{es, prev_tp};
+  } done{me, prev_tp};
   PARSEC_PINS(es, PINS_COMPLETE_EXEC_BEGIN, t);
   if (g_paranoid && t->status == STATUS_COMPLETE) fatal("paranoid: task %s completed twice", t->task_class->describe(t).c_str());
   t->status = STATUS_PREPARE_OUTPUT;
