@@ -6,7 +6,7 @@
 // holder count instead of a table lock. A thread that finds the table loaded
 // above 4 items per bucket while it holds no bucket raises the resize flag,
 // waits for the holders to drain (new entries wait; a thread already holding a
-// bucket never waits, so nested locking cannot deadlock) and rehashes into
+// bucket of that table never waits, so nested locking cannot deadlock) and rehashes into
 // twice the buckets (the reference chains older, smaller tables instead).
 #include <atomic>
 #include <cstdint>
@@ -36,12 +36,31 @@ struct HtImpl {
   bool loaded() const { return count.load(std::memory_order_relaxed) > 4 * capacity.load(std::memory_order_relaxed); }
 };
 
-// buckets this thread holds (any table): a holder never waits for a resize
+// Buckets this thread holds: per table, and in total. A thread that already
+// holds a bucket of THIS table never waits for its resize (the resizer waits
+// for it to leave: nested find-then-insert would deadlock). A bucket of
+// another table is no pass: the resize of this table could be draining its
+// holders, and entering without waiting would read buckets being rehashed.
+// A thread holding any bucket never starts a resize (maybe_grow).
+struct Held {
+  const HtImpl* table;
+  int n;
+};
+thread_local std::vector<Held> t_held_tables;
 thread_local int t_held = 0;
 
+int& held_of(const HtImpl* h) {
+  for (Held& e : t_held_tables)
+    if (e.table == h) return e.n;
+  t_held_tables.push_back(Held{h, 0});
+  return t_held_tables.back().n;
+}
+
 void enter(HtImpl* h) {
-  if (t_held > 0) {
+  int& mine = held_of(h);
+  if (mine > 0) {
     h->holders.fetch_add(1, std::memory_order_seq_cst);
+    ++mine;
     ++t_held;
     return;
   }
@@ -51,11 +70,20 @@ void enter(HtImpl* h) {
     if (!h->resizing.load(std::memory_order_seq_cst)) break;
     h->holders.fetch_sub(1, std::memory_order_release);
   }
+  ++mine;
   ++t_held;
 }
 void leave(HtImpl* h) {
   h->holders.fetch_sub(1, std::memory_order_release);
   --t_held;
+  for (size_t i = 0; i < t_held_tables.size(); ++i)
+    if (t_held_tables[i].table == h) {
+      if (--t_held_tables[i].n == 0) {  // keep the list short: drop tables no longer held
+        t_held_tables[i] = t_held_tables.back();
+        t_held_tables.pop_back();
+      }
+      break;
+    }
 }
 
 HtImpl* impl(parsec_hash_table_t* ht) { return static_cast<HtImpl*>(ht->impl); }

@@ -139,6 +139,11 @@ const char* comm_device_plane_name();  // "ipc" | "host" | "none"
 // (-1x set-up, -2x open of peer x, -4x copy from peer x, -6x wrong bytes from
 // peer x, -7 another rank failed)
 int comm_plane_status();
+// this rank's IPC start-up probe, per peer: (outcome bits, open attempts)
+std::vector<std::pair<int, int>> comm_probe_table();
+// IPC payload bytes this rank pulled from each peer; pull route per peer
+std::vector<uint64_t> comm_bytes_by_peer();
+std::vector<int> comm_pull_routes();
 int comm_rank();
 int comm_size();
 // Bring up the engine explicitly (Python / launcher); returns 0 on success.

@@ -40,6 +40,9 @@ static FetchQueue g_fetch;
 CommEngine* comm_engine() { return g_ce; }
 int comm_rank() { return g_ce ? g_ce->rank : 0; }
 int comm_plane_status() { return g_ce ? g_ce->plane_status() : 0; }
+std::vector<std::pair<int, int>> comm_probe_table() { return g_ce ? g_ce->probe_table() : std::vector<std::pair<int, int>>{}; }
+std::vector<uint64_t> comm_bytes_by_peer() { return g_ce ? g_ce->bytes_by_peer() : std::vector<uint64_t>{}; }
+std::vector<int> comm_pull_routes() { return g_ce ? g_ce->pull_routes() : std::vector<int>{}; }
 int comm_size() { return g_ce ? g_ce->size : 1; }
 uint32_t comm_allreduce_max_u32(uint32_t v) { return g_ce ? (uint32_t)g_ce->allreduce_max(v) : v; }
 int comm_barrier() { return g_ce ? g_ce->sync() : 0; }
@@ -212,6 +215,7 @@ DataCopy* new_recv_copy(size_t bytes, bool device) {
       auto& v = pool.free[bytes];
       if (!v.empty()) { p = v.back(); v.pop_back(); }
     }
+    if (p) kern::trsm_estimate_forget(p);  // a recycled buffer: not the W it held before
     // carved from the GPU's tile-cache zone (no hipMalloc / memset on the comm
     // thread); recycled by size through the pool, returned at remote_dep_fini
     if (!p && g_recv_from_cache) p = device_cache_alloc(g_gpu_index, bytes);
@@ -339,8 +343,8 @@ void on_activate(int src, int, const void* msg, size_t len) {
 
 // One flow of receive `rid` landed (comm thread): tell the sender, deliver
 // when it was the last one.
-void flow_landed(uint64_t rid, int f) {
-  g_fetch.done();  // the next queued get (by priority) may start
+void flow_landed(uint64_t rid, int f, int src) {
+  g_fetch.done(src);  // the next queued get (by priority, on a lane with room) may start
   comm_trace(k_rcv_e, flow_event(rid, f), 0, nullptr);
   RecvState* rs = nullptr;
   {
@@ -426,10 +430,11 @@ void start_recv(int src, const char* msg, size_t len, Taskpool* tp) {
       comm_trace(k_rcv_b, flow_event(rid, f), tpid, &ci);
     }
     const MemReg remote = rreg[f];
-    g_fetch.submit(prio, [x, remote, src, rid, sid, f] {
+    // lane = the source rank: its own xGMI link
+    g_fetch.submit(prio, src, [x, remote, src, rid, sid, f] {
       const PutEnd pe{sid, (uint32_t)f, 0};
       PARSEC_DEBUG(kVerbDebug, "comm", "get flow %d (%llu bytes) from %d (recv %llu)", f, (unsigned long long)x.bytes, src, (unsigned long long)rid);
-      if (g_ce->get(x.lreg, 0, remote, 0, x.bytes, src, [rid, f](const MemReg&, ptrdiff_t, const MemReg&, ptrdiff_t, size_t, int) { flow_landed(rid, f); },
+      if (g_ce->get(x.lreg, 0, remote, 0, x.bytes, src, [rid, f, src](const MemReg&, ptrdiff_t, const MemReg&, ptrdiff_t, size_t, int) { flow_landed(rid, f, src); },
                     TAG_PUT_END, &pe, sizeof(pe)) != 0)
         fatal("remote dependency: get of flow %d from rank %d failed", f, src);
     });
@@ -570,8 +575,13 @@ std::vector<std::pair<std::string, uint64_t>> comm_stats() {
   r.emplace_back("bytes_fragments", st.bytes_fragments.load());
   const FetchQueue::Stats fq = g_fetch.stats();
   r.emplace_back("gets_max", (uint64_t)std::max(0, g_fetch.max_inflight()));
+  r.emplace_back("gets_per_peer", (uint64_t)std::max(0, g_fetch.per_lane()));
   r.emplace_back("gets_queued_max", fq.max_queued);
   r.emplace_back("gets_submitted", fq.submitted);
+  r.emplace_back("gets_inflight_max", (uint64_t)fq.max_inflight_seen);
+  r.emplace_back("gets_lanes_busy_max", (uint64_t)fq.max_lanes_busy);
+  r.emplace_back("gather_launches", st.gathers.load());
+  r.emplace_back("gather_max_pulls", st.gather_max.load());
   return r;
 }
 
@@ -588,11 +598,19 @@ void remote_dep_init(Context* ctx) {
   g_recv_pool = (int)ParamRegistry::instance().reg_int("comm", "", "recv_pool", "Device receive buffers: 1 recycle by size, 0 free after use, 2 never reuse (diagnostic)", 1);
   g_recv_from_cache = ParamRegistry::instance().reg_int("comm", "", "recv_from_cache", "Carve device receive buffers from the GPU tile-cache zone (1) or hipMalloc them (0)", 1) != 0;
   if (g_ce) {
-    // reference parsec_comm_gets_max (remote_dep_mpi.c:26): pulls on one copy
-    // stream run in order, so a small bound keeps a critical flow near the head
+    // reference parsec_comm_gets_max (remote_dep_mpi.c:26): an issued pull
+    // cannot be overtaken, so small bounds keep a critical flow near the head.
+    // Per source peer (its own xGMI link): 2 on the IPC plane -- one pulling,
+    // one in the next gather launch -- so every link stays busy while a
+    // critical tile still waits behind at most two of its link's transfers.
     const int gm = (int)ParamRegistry::instance().reg_int("comm", "", "gets_max",
-        "Payload gets of incoming activations in flight at once, highest activation priority first; -1 = auto (2 per IPC pull stream, 4 on the host plane), 0 = unbounded", -1);
-    g_fetch.set_max_inflight(gm >= 0 ? gm : g_ce->device_direct() ? 2 * g_ce->pull_streams() : 4);
+        "Payload gets of incoming activations in flight at once, highest activation priority first; -1 = auto (comm_gets_per_peer x peers on the IPC plane, 4 on the host plane), 0 = unbounded", -1);
+    const int gp = (int)ParamRegistry::instance().reg_int("comm", "", "gets_per_peer",
+        "Payload gets in flight per source rank (its own xGMI link); -1 = auto (2 on the IPC plane, unbounded on the host plane), 0 = unbounded", -1);
+    const bool ipc = g_ce->device_direct();
+    const int per = gp >= 0 ? gp : ipc ? 2 : 0;
+    const int peers = std::max(1, g_ce->size - 1);
+    g_fetch.configure(gm >= 0 ? gm : ipc ? std::max(2, per * peers) : 4, per);
   }
   ctx->my_rank = comm_rank();
   ctx->nb_nodes = comm_size();

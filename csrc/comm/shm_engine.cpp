@@ -21,6 +21,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstring>
 
 #define PARSEC_HIP_CHECK_COMM(x)                                                    \
@@ -84,6 +85,9 @@ ShmEngine::ShmEngine(int rank_, int size_, const std::string& job, int gpu) : jo
     }
   };
   for (int i = 0; i < size; ++i) out_.emplace_back(new Out());
+  bytes_from_.reset(new std::atomic<uint64_t>[size]);
+  for (int i = 0; i < size; ++i) bytes_from_[i].store(0);
+  route_.assign(size, 0);
   maps_.assign(size, nullptr);
   map_len_.assign(size, 0);
 }
@@ -225,59 +229,123 @@ int ShmEngine::init() {
 
 // local_rc != 0: this rank cannot (or does not want to) use IPC; it still
 // takes part in both all-reduces so every rank makes the same collective calls.
+//
+// Every rank maps every peer's probe buffer and reads it through each route a
+// payload pull can take (reference comm bring-up: remote_dep_mpi.c:250-338):
+//   * a device <- peer hipMemcpyAsync on this GPU's copy stream (the copy-engine
+//     pull between distinct GPUs),
+//   * the copy kernel reading the peer mapping (the pull between ranks sharing
+//     a GPU, and the device-to-device kernel route of comm_ipc_copy_mode 1),
+//   * a device -> host read of the mapping (host-staged gets / puts).
+// The bytes of each route are checked. The per-peer outcome goes to
+// probe_table() (bench.py reports it as a rank x peer table): bit 1 open failed,
+// 2 copy-engine pull, 4 copy kernel, 8 host read; `attempts` = opens needed.
+// comm_ipc_probe_fail = "r:p,..." makes rank r's open of peer p fail (tests of
+// the fall-back and of the report).
+//
+// Retries of hipIpcOpenMemHandle: one open in the round-3 8-rank shared-GPU
+// validation failed once and succeeded on the next call (rank 4 -> rank 1, no
+// HIP error recorded then); the cause was not identified and no later run
+// (rounds 4-6) needed a second attempt. The retries stay, each logged with its
+// HIP error and counted in the table, so a failing pair is visible instead of
+// silently moving the job to the host plane.
 int ShmEngine::probe_ipc(int local_rc) {
   const size_t bytes = (size_t)64 << 20;  // far above comm_ipc_min_alloc: a buffer object of its own
+  constexpr size_t kChunk = 4096;
   void* buf = nullptr;
+  void* land = nullptr;  // local device landing buffer of the pulls
   int rc = local_rc;
+  probe_code_.assign(size, 0);
+  probe_attempts_.assign(size, 0);
   if (rc == 0 && hipSetDevice(gpu_) != hipSuccess) { (void)hipGetLastError(); rc = -10; }
   if (rc == 0 && hipMalloc(&buf, bytes) != hipSuccess) { (void)hipGetLastError(); buf = nullptr; rc = -11; }
+  if (rc == 0 && hipMalloc(&land, 2 * kChunk) != hipSuccess) { (void)hipGetLastError(); land = nullptr; rc = -11; }
   if (rc == 0 && hipMemset(buf, 0x40 + (rank & 0x3f), bytes) != hipSuccess) rc = -12;
   if (rc == 0 && hipDeviceSynchronize() != hipSuccess) rc = -13;
   hipIpcMemHandle_t h{};
   if (rc == 0 && hipIpcGetMemHandle(&h, buf) != hipSuccess) rc = -14;
   if (rc != 0) (void)hipGetLastError();
   std::memcpy(me_->ipc_probe, &h, sizeof(h));
+  // injected failures: "r:p" pairs
+  std::vector<int> forced;
+  {
+    const std::string spec = ParamRegistry::instance().reg_string("comm", "", "ipc_probe_fail", "Test hook: rank:peer pairs (comma separated) whose IPC probe open fails", "");
+    size_t i = 0;
+    while (i < spec.size()) {
+      size_t j = spec.find(',', i);
+      const std::string part = spec.substr(i, j == std::string::npos ? std::string::npos : j - i);
+      const size_t c = part.find(':');
+      if (c != std::string::npos && std::atoi(part.substr(0, c).c_str()) == rank) forced.push_back(std::atoi(part.substr(c + 1).c_str()));
+      if (j == std::string::npos) break;
+      i = j + 1;
+    }
+  }
   const bool all_exported = allreduce_max(rc != 0 ? 1 : 0) == 0;  // collective 1: every handle is published
   if (all_exported) {
-    std::vector<unsigned char> got(4096);
+    std::vector<unsigned char> got(kChunk);
     hipStream_t st = gpu_copy_stream(gpu_);
-    for (int r = 0; r < size && rc == 0; ++r) {
+    for (int r = 0; r < size; ++r) {
       if (r == rank) continue;
+      const unsigned char want = (unsigned char)(0x40 + (r & 0x3f));
       hipIpcMemHandle_t ph;
       std::memcpy(&ph, static_cast<ShmHeader*>(maps_[r])->ipc_probe, sizeof(ph));
       void* p = nullptr;
-      // 8 processes mapping each other's buffers on one GPU: an open has been
-      // seen to fail once and succeed on the next try (round-3/4 validation,
-      // rank 4 -> rank 1); a few spaced attempts before giving the plane up
-      hipError_t oe = hipSuccess;
-      for (int attempt = 0; attempt < 5; ++attempt) {
+      hipError_t oe = hipErrorInvalidValue;
+      const bool fail = std::find(forced.begin(), forced.end(), r) != forced.end();
+      for (int attempt = 0; attempt < 5 && !fail; ++attempt) {
+        probe_attempts_[r] = attempt + 1;
         oe = hipIpcOpenMemHandle(&p, ph, hipIpcMemLazyEnablePeerAccess);
         if (oe == hipSuccess) {
           if (attempt > 0) warning("IPC probe: rank %d mapped rank %d's buffer at attempt %d", rank, r, attempt + 1);
           break;
         }
+        warning("IPC probe: rank %d, open of rank %d's buffer, attempt %d: %s", rank, r, attempt + 1, hipGetErrorString(oe));
         (void)hipGetLastError();
         p = nullptr;
         std::this_thread::sleep_for(std::chrono::milliseconds(5 * (attempt + 1)));
       }
       if (oe != hipSuccess) {
-        warning("IPC probe: rank %d cannot map rank %d's buffer: %s", rank, r, hipGetErrorString(oe));
-        rc = -20 - r;
-        break;
+        warning("IPC probe: rank %d cannot map rank %d's buffer%s", rank, r, fail ? " (comm_ipc_probe_fail)" : "");
+        probe_code_[r] = 1;
+        if (rc == 0) rc = -20 - r;
+        continue;
       }
-      // the tail of the peer buffer, through the copy stream the pulls use
-      if (!st || hipMemcpyAsync(got.data(), static_cast<char*>(p) + bytes - got.size(), got.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
-          hipStreamSynchronize(st) != hipSuccess) {
-        (void)hipGetLastError();
-        rc = -40 - r;
-      }
-      for (unsigned char c : got)
-        if (rc == 0 && c != (unsigned char)(0x40 + (r & 0x3f))) rc = -60 - r;
+      const char* tail = static_cast<char*>(p) + bytes - kChunk;
+      auto check = [&](int bit, int err) {
+        for (unsigned char c : got)
+          if (c != want) {
+            probe_code_[r] |= bit;
+            if (rc == 0) rc = err - r;
+            return;
+          }
+      };
+      auto fetch_land = [&](size_t off) {
+        std::fill(got.begin(), got.end(), 0);
+        return hipMemcpyAsync(got.data(), static_cast<char*>(land) + off, kChunk, hipMemcpyDeviceToHost, st) == hipSuccess &&
+               hipStreamSynchronize(st) == hipSuccess;
+      };
+      // (1) copy engine: device <- peer, then the landed bytes to the host
+      bool ok = st && hipMemsetAsync(land, 0, 2 * kChunk, st) == hipSuccess &&
+                hipMemcpyAsync(land, tail, kChunk, hipMemcpyDefault, st) == hipSuccess && fetch_land(0);
+      if (!ok) { (void)hipGetLastError(); probe_code_[r] |= 2; if (rc == 0) rc = -40 - r; }
+      else check(2, -60);
+      // (2) copy kernel reading the mapping
+      ok = st && device_copy_kernel(static_cast<char*>(land) + kChunk, tail, kChunk, st) == 0 && fetch_land(kChunk);
+      if (!ok) { (void)hipGetLastError(); probe_code_[r] |= 4; if (rc == 0) rc = -40 - r; }
+      else check(4, -60);
+      // (3) host read of the mapping
+      std::fill(got.begin(), got.end(), 0);
+      ok = st && hipMemcpyAsync(got.data(), tail, kChunk, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
+      if (!ok) { (void)hipGetLastError(); probe_code_[r] |= 8; if (rc == 0) rc = -40 - r; }
+      else check(8, -60);
       (void)hipIpcCloseMemHandle(p);
     }
   }
+  else
+    for (int r = 0; r < size; ++r) probe_code_[r] = r == rank ? 0 : -1;  // not probed: some rank has no exportable buffer
   (void)allreduce_max(0);  // collective 2: every peer is done reading before the buffers go
   if (buf) (void)hipFree(buf);
+  if (land) (void)hipFree(land);
   if (rc != 0 && local_rc == 0) warning("IPC probe failed on rank %d (rc=%d)", rank, rc);
   if (rc == 0 && !all_exported) rc = -7;
   return rc;
@@ -501,6 +569,17 @@ int ShmEngine::progress() {
       ++n;
     }
   }
+  // gather batches (each on its own event; a batch's pulls land together)
+  for (auto it = gather_q_.begin(); it != gather_q_.end();) {
+    hipError_t e = hipEventQuery(it->ev);
+    if (e == hipErrorNotReady) { ++it; continue; }
+    if (e != hipSuccess) fatal("gather pull of the comm engine failed: %s", hipGetErrorString(e));
+    GatherBatch b = std::move(*it);
+    it = gather_q_.erase(it);
+    ev_pool_.push_back(b.ev);
+    for (auto& d : b.done) d();  // may issue the next pulls (flushed below)
+    ++n;
+  }
   // device copies (per pull stream / staging, completed in stream order)
   for (auto& q : copy_q_) {
     while (!q.empty()) {
@@ -514,7 +593,36 @@ int ShmEngine::progress() {
       ++n;
     }
   }
+  // the pulls issued during this pass (activations received, completions that
+  // freed a lane) leave as one gather launch
+  flush_gather();
   return n;
+}
+
+void ShmEngine::flush_gather() {
+  if (gather_pending_.empty()) return;
+  std::vector<void*> dst;
+  std::vector<const void*> src;
+  std::vector<size_t> bytes;
+  GatherBatch b{take_event(), {}};
+  if (!b.ev) fatal("gather pull: no event");
+  for (auto& g : gather_pending_) {
+    dst.push_back(g.dst);
+    src.push_back(g.src);
+    bytes.push_back(g.bytes);
+    b.done.push_back(std::move(g.done));
+  }
+  // alternate over the pull streams (one unless comm_ipc_streams > 1)
+  std::vector<hipStream_t> pool{gpu_copy_stream(gpu_)};
+  for (hipStream_t x : own_streams_) pool.push_back(x);
+  hipStream_t st = pool[gather_rr_++ % pool.size()];
+  if (device_gather_kernel(dst.data(), src.data(), bytes.data(), (int)dst.size(), st) != 0) fatal("IPC gather kernel launch failed");
+  (void)hipEventRecord(b.ev, st);
+  stats.gathers.fetch_add(1, std::memory_order_relaxed);
+  uint64_t m = stats.gather_max.load(std::memory_order_relaxed);
+  while (dst.size() > m && !stats.gather_max.compare_exchange_weak(m, dst.size(), std::memory_order_relaxed)) {}
+  gather_pending_.clear();
+  gather_q_.push_back(std::move(b));
 }
 
 void ShmEngine::thread_main() {
@@ -617,6 +725,22 @@ void ShmEngine::setup_pull_streams() {
   }
   for (int r = 0; r < size; ++r)
     if (r != rank) ipc_stream_[r] = pool[(size_t)r % pool.size()];
+  // pull route per peer (comm_ipc_copy_mode):
+  //  3 (default) gather: the pulls of a progress pass leave in one multi-source
+  //    kernel -- pulls from distinct peers (distinct xGMI links) move at the same
+  //    time on the one copy stream; a peer whose mapping failed the probe's
+  //    kernel read takes the copy engine instead (and one that failed that too
+  //    made the whole job fall back to the host plane at start-up);
+  //  2 kernel per pull for a peer on this GPU, copy engine otherwise (rounds 3-5);
+  //  1 copy kernel per pull; 0 copy engine (hipMemcpyAsync) per pull.
+  const int cmode = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_copy_mode", "Peer pull: 0 = hipMemcpyAsync (copy engine), 1 = copy kernel, 2 = kernel for a peer on the same GPU, copy engine otherwise, 3 = multi-source gather kernel (the pulls of one progress pass in one launch; copy engine for a peer whose probe kernel read failed)", 3);
+  for (int r = 0; r < size; ++r) {
+    if (r == rank) continue;
+    const int probe = (size_t)r < probe_code_.size() ? probe_code_[r] : 0;
+    int route = cmode == 2 ? (same_gpu_[r] ? 1 : 0) : cmode;
+    if ((route == 1 || route == 3) && probe > 0 && (probe & 4)) route = 0;  // the kernel could not read this peer
+    route_[r] = (int8_t)route;
+  }
 }
 
 // Which peers share this rank's GPU (PCI bus ids published in the shm headers;
@@ -701,16 +825,16 @@ hipEvent_t ShmEngine::take_event() {
 
 int ShmEngine::ipc_copy(int peer, void* dst, const void* src, size_t bytes, bool kernel_ok, std::function<void()> done) {
   if (peer < 0 || peer >= size || (size_t)peer >= ipc_stream_.size() || !ipc_stream_[peer]) return -1;
+  // route per peer (setup_pull_streams); a kernel only ever moves device to
+  // device: pageable host memory is never touched by one
+  const int mode = !kernel_ok ? 0 : (size_t)peer < route_.size() ? route_[peer] : 0;
+  if (mode == 3) {
+    gather_pending_.push_back(GatherItem{dst, src, bytes, std::move(done)});
+    return 0;
+  }
   hipStream_t st = ipc_stream_[peer];
   hipEvent_t ev = take_event();
   if (!ev) return -1;
-  // 2 (auto): a copy kernel when the peer shares this GPU and both ends are
-  // device memory (the copy engines managed 4-11 GB/s for same-device pulls:
-  // profiles/r3_ipc_pull_ab.txt), the copy engines otherwise -- across xGMI they
-  // need no CU, so a pull never waits behind bulk GEMM workgroups for a slot, and
-  // pageable host memory is never touched by a kernel
-  static const int cmode = (int)ParamRegistry::instance().reg_int("comm", "", "ipc_copy_mode", "Peer pull: 0 = hipMemcpyAsync (copy engine), 1 = copy kernel, 2 = kernel for a peer on the same GPU, copy engine otherwise (a kernel only ever moves device-to-device)", 2);
-  const int mode = !kernel_ok ? 0 : cmode == 2 ? ((size_t)peer < same_gpu_.size() && same_gpu_[peer] ? 1 : 0) : cmode;
   if (mode == 1) {
     if (device_copy_kernel(dst, src, bytes, st) != 0) fatal("IPC copy kernel launch failed");
   } else {

@@ -52,7 +52,16 @@ class ShmEngine : public CommEngine {
     std::atomic<uint64_t> max_waiting{0};
     std::atomic<uint64_t> get_ipc{0}, get_fragments{0}, put_ipc{0}, put_fragments{0};  // one-sided transfers by route
     std::atomic<uint64_t> bytes_ipc{0}, bytes_fragments{0};  // payload bytes of gets by route
+    std::atomic<uint64_t> gathers{0}, gather_max{0};         // multi-source gather launches, most pulls in one
   } stats;
+  // payload bytes this rank fetched from each peer (gets, either route): per xGMI link
+  std::vector<uint64_t> bytes_by_peer() const {
+    std::vector<uint64_t> v(size, 0);
+    for (int r = 0; r < size && bytes_from_; ++r) v[r] = bytes_from_[r].load(std::memory_order_relaxed);
+    return v;
+  }
+  // pull route per peer: 0 copy engine (hipMemcpyAsync), 1 copy kernel, 3 gather
+  std::vector<int> pull_routes() const { return std::vector<int>(route_.begin(), route_.end()); }
   int progress() override;
   int sync() override;
   uint64_t allreduce_max(uint64_t v) override;
@@ -92,6 +101,13 @@ class ShmEngine : public CommEngine {
   // step (-1x set-up, -2x open of peer x, -4x copy from peer x, -6x wrong bytes
   // from peer x, -7 another rank failed)
   int plane_status() const { return ipc_status_; }
+  // per peer: IPC probe outcome bits (1 open, 2 copy-engine pull, 4 copy kernel,
+  // 8 host read; 0 = every route moved the right bytes) and open attempts
+  std::vector<std::pair<int, int>> probe_table() const {
+    std::vector<std::pair<int, int>> t;
+    for (size_t r = 0; r < probe_code_.size(); ++r) t.emplace_back(probe_code_[r], probe_attempts_[r]);
+    return t;
+  }
   int gpu_ordinal() const { return gpu_; }
   void start_thread();
   void stop_thread();
@@ -152,10 +168,30 @@ class ShmEngine : public CommEngine {
   // ---- device plane (comm thread only, except ipc_export)
   int plane_ = PLANE_HOST;
   int ipc_status_ = 0;
+  std::vector<int> probe_code_, probe_attempts_;
   std::vector<hipStream_t> ipc_stream_;    // pull stream per peer
   std::vector<hipStream_t> own_streams_;   // extra pull streams (comm_ipc_streams > 1)
   std::vector<uint8_t> same_gpu_;          // peer r runs on this rank's GPU (shared-GPU validation runs)
   std::vector<std::deque<Xfer>> copy_q_;   // per peer (pulls) + [size] (local staging copies), completed in order
+  // multi-source gather (comm_ipc_copy_mode 3): the pulls issued during one
+  // progress pass leave together in ONE kernel launch (flush_gather), one per
+  // source peer's link; a batch completes on one event
+  struct GatherItem {
+    void* dst;
+    const void* src;
+    size_t bytes;
+    std::function<void()> done;
+  };
+  struct GatherBatch {
+    hipEvent_t ev;
+    std::vector<std::function<void()>> done;
+  };
+  std::vector<GatherItem> gather_pending_;
+  std::deque<GatherBatch> gather_q_;
+  uint32_t gather_rr_ = 0;
+  void flush_gather();
+  std::vector<int8_t> route_;  // pull route per peer (pull_routes())
+  std::unique_ptr<std::atomic<uint64_t>[]> bytes_from_;
   std::vector<hipEvent_t> ev_pool_;
   std::map<std::tuple<uintptr_t, size_t, unsigned long long>, std::array<char, 64>> ipc_exported_;  // (base, size, buffer id) -> handle
   std::mutex ipc_m_;  // ipc_exported_ / ipc_opened_ (exports happen on worker threads too)

@@ -276,6 +276,7 @@ int ShmEngine::get(const MemReg& lreg, ptrdiff_t ldispl, const MemReg& rreg, ptr
   std::vector<char> cbd(static_cast<const char*>(r_cb_data), static_cast<const char*>(r_cb_data) + (r_cb_data ? r_cb_size : 0));
   char* dst = static_cast<char*>(lptr) + ldispl;
   auto run = [=, this, cbd = std::move(cbd)]() mutable {
+    if (bytes_from_ && remote >= 0 && remote < this->size) bytes_from_[remote].fetch_add(size, std::memory_order_relaxed);
     if (rw.device != 0 && rw.ipc_ok && plane_ == PLANE_IPC) {
       // device region of the peer: map its allocation, pull over xGMI
       char* base = static_cast<char*>(ipc_open(remote, rw.ipc));

@@ -57,6 +57,8 @@ bool device_cache_free(int device_index, void* p);
 int bind_thread_to_gpu_numa(int ordinal);
 // dst <- src (bytes) as a copy kernel on `stream` (hipStream_t); 0 on success.
 int device_copy_kernel(void* dst, const void* src, size_t bytes, void* stream);
+// n device-to-device transfers in one launch (multi-source gather of IPC pulls)
+int device_gather_kernel(void* const* dst, const void* const* src, const size_t* bytes, int n, void* stream);
 int device_memcpy(int dst_dev, void* dst, int src_dev, const void* src, size_t bytes);
 // bytes moved by device_memcpy since start / the last reset: H2D, D2H, D2D
 void device_memcpy_stats(uint64_t out[3], bool reset);
@@ -155,6 +157,10 @@ int trsm_estimate_route(int on);
 // [0] estimates published by tile POTRFs, [1] panel decisions taken on the
 // host, [2] panels left to the device-side gate
 void trsm_estimate_stats(uint64_t out[3], bool reset);
+// a device buffer was (re)allocated: drop a panel estimate keyed by its address
+void trsm_estimate_forget(const void* p);
+double trsm_estimate_lookup(const void* p);
+std::vector<uintptr_t> trsm_estimate_known();
 }  // namespace kern
 
 // Householder QR of a tile (GEQRT: A2 == nullptr) or of a triangle on top of a

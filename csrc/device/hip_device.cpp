@@ -39,6 +39,7 @@ void* ZoneAllocator::alloc(size_t bytes) {
       void* p = s.base + off;
       live_[p] = {si, sz};
       used_ += sz;
+      kern::trsm_estimate_forget(p);
       return p;
     }
   }
@@ -61,6 +62,7 @@ void* ZoneAllocator::alloc(size_t bytes) {
   if (seg > sz) s.free_[sz] = seg - sz;
   live_[base] = {segs_.size() - 1, sz};
   used_ += sz;
+  kern::trsm_estimate_forget(base);
   return base;
 }
 
@@ -95,6 +97,7 @@ void* device_alloc(int device_index, size_t bytes) {
   hipError_t e = hipMalloc(&p, bytes);
   if (e == hipSuccess) (void)hipMemset(p, 0, bytes);
   (void)hipSetDevice(prev);
+  if (e == hipSuccess) kern::trsm_estimate_forget(p);
   return e == hipSuccess ? p : nullptr;
 }
 
@@ -299,6 +302,8 @@ void* GpuExecContext::info(int id) {
 
 // ================================================================ device
 static int g_nb_exec_streams = 3;
+static std::vector<HipDevice*> g_hip_devices;
+static size_t hip_device_count() { return g_hip_devices.size(); }
 
 int HipDevice::attach(Context* c) {
   ctx = c;
@@ -318,6 +323,14 @@ void HipDevice::start(Context* c) {
     // registry, and this engine, outlive a context)
     auto& params = ParamRegistry::instance();
     early_release = (int)params.reg_int("device", "hip", "early_release", "Critical-stream groups release their tasks' successors when launched (1) or when their kernels completed (0); single-process runs", early_release);
+    // an early-released output is published before its kernel ran; only this
+    // device's own streams and CPU readers wait for it -- a peer stage-in or a
+    // host pull issued by ANOTHER device's manager would not, so early release
+    // is a single-device mode
+    if (early_release > 0 && hip_device_count() > 1) {
+      warning("device_hip_early_release ignored: %zu HIP devices in this process", hip_device_count());
+      early_release = 0;
+    }
     hp_route = (int)params.reg_int("device", "hip", "hp_on_critical_stream", "High-priority tasks below the critical threshold share the critical stream (1), go to the least loaded bulk stream (0), or get stream 1 to themselves (2, bulk on streams 2..)", hp_route);
     critical_split = params.reg_int("device", "hip", "critical_split", "Critical-path tasks leave the critical stream as a group of their own", critical_split ? 1 : 0) != 0;
     sort_pending = (int)params.reg_int("device", "hip", "sort_pending_tasks", "Order of the pending GPU tasks: 0 arrival, 1 priority, 2 data already on the device first, then priority", sort_pending);
@@ -1609,7 +1622,6 @@ void HipDevice::manager_main() {
 }
 
 // ================================================================ module
-static std::vector<HipDevice*> g_hip_devices;
 
 void hip_devices_init(Context* ctx) {
   (void)ctx;

@@ -2060,6 +2060,7 @@ struct EstimateSlots {
   std::unordered_map<const double*, uint32_t> of_w;
 };
 EstimateSlots g_est[16];
+std::atomic<bool> g_est_any{false};  // some device has estimate slots (forget() is a no-op before)
 int g_est_route = -1;  // PARSEC_DPOTRF_TRSM_ESTIMATE: 1 = host-published (default), 0 = device gate only
 EstimateSlots* est_slots() {
   int dev = 0;
@@ -2094,6 +2095,7 @@ static bool est_acquire(const double* W, unsigned long long** dev, double** host
       std::memset(h, 0, kEstSlots * sizeof(double));
       e->host = static_cast<double*>(h);
       e->dev = static_cast<unsigned long long*>(d);
+      g_est_any.store(true, std::memory_order_release);
     } else {
       (void)hipGetLastError();
       if (h) (void)hipHostFree(h);
@@ -2114,6 +2116,23 @@ static bool est_acquire(const double* W, unsigned long long** dev, double** host
   return true;
 }
 
+// A device buffer was (re)allocated: whatever W it held is gone, so an estimate
+// keyed by its address must not be found for the next tile living there (a
+// receive buffer recycled from the pool or the zone, a tile re-staged after
+// eviction). Called by the zone allocator, device_alloc and the comm engine's
+// receive-buffer pool.
+void trsm_estimate_forget(const void* p) {
+  if (!p || !g_est_any.load(std::memory_order_acquire)) return;
+  for (EstimateSlots& e : g_est) {
+    std::lock_guard<std::mutex> lk(e.m);
+    if (!e.host) continue;
+    auto it = e.of_w.find(static_cast<const double*>(p));
+    if (it == e.of_w.end()) continue;
+    if (e.owner[it->second] == p) e.owner[it->second] = nullptr;
+    e.of_w.erase(it);
+  }
+}
+
 // The published estimate of the POTRF that wrote W (> 0), or 0 when unknown.
 static double est_lookup(const double* W) {
   if (trsm_estimate_route(-1) == 0) return 0.0;
@@ -2125,6 +2144,20 @@ static double est_lookup(const double* W) {
   const double v = *reinterpret_cast<volatile const double*>(&e->host[it->second]);
   std::atomic_thread_fence(std::memory_order_acquire);
   return v;
+}
+
+// tests: the estimate keyed by p on the current device, and every W address
+// holding a published one
+double trsm_estimate_lookup(const void* p) { return est_lookup(static_cast<const double*>(p)); }
+std::vector<uintptr_t> trsm_estimate_known() {
+  std::vector<uintptr_t> out;
+  EstimateSlots* e = est_slots();
+  if (!e) return out;
+  std::lock_guard<std::mutex> lk(e->m);
+  if (!e->host) return out;
+  for (const auto& kv : e->of_w)
+    if (e->owner[kv.second] == kv.first && *reinterpret_cast<volatile const double*>(&e->host[kv.second]) > 0.0) out.push_back((uintptr_t)kv.first);
+  return out;
 }
 
 // Estimates published / taken on the host / left to the device gate (tests, bench)
@@ -2378,6 +2411,64 @@ int device_copy_kernel(void* dst, const void* src, size_t bytes, void* stream) {
   }
   const size_t done = n16 * 16;
   if (bytes > done) hipLaunchKernelGGL(copy_tail_kernel, dim3(1), dim3(256), 0, s, static_cast<char*>(dst) + done, static_cast<const char*>(src) + done, bytes - done);
+  return (int)hipGetLastError();
+}
+
+// Multi-source gather: ONE launch moves up to kMaxGather transfers, each from
+// another peer's IPC mapping. Across xGMI every peer GPU sits behind its own
+// link, so the transfers of one launch pull over up to 7 links at once while
+// the process keeps one copy stream (one hardware queue). Workgroups are split
+// between the transfers in proportion to their size (at most 64 per transfer,
+// 4 x 16-byte loads in flight per thread: ~1 MiB in flight per link).
+constexpr int kMaxGather = 16;
+struct GatherArgs {
+  int count;
+  int wg_start[kMaxGather + 1];
+  uint4* dst[kMaxGather];
+  const uint4* src[kMaxGather];
+  unsigned long long n16[kMaxGather];
+};
+static_assert(sizeof(GatherArgs) <= 4096, "GatherArgs exceeds the kernel argument limit");
+__global__ __launch_bounds__(256) void gather_kernel(const GatherArgs a) {
+  int t = 0;
+  while (t + 1 < a.count && (int)blockIdx.x >= a.wg_start[t + 1]) ++t;
+  const int w = (int)blockIdx.x - a.wg_start[t], nw = a.wg_start[t + 1] - a.wg_start[t];
+  uint4* __restrict__ d = a.dst[t];
+  const uint4* __restrict__ s = a.src[t];
+  const size_t n = a.n16[t], stride = (size_t)nw * 256;
+  size_t i = (size_t)w * 256 + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const uint4 v0 = s[i], v1 = s[i + stride], v2 = s[i + 2 * stride], v3 = s[i + 3 * stride];
+    d[i] = v0;
+    d[i + stride] = v1;
+    d[i + 2 * stride] = v2;
+    d[i + 3 * stride] = v3;
+  }
+  for (; i < n; i += stride) d[i] = s[i];
+}
+
+int device_gather_kernel(void* const* dst, const void* const* src, const size_t* bytes, int n, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  for (int b = 0; b < n; b += kMaxGather) {
+    GatherArgs a{};
+    int wg = 0;
+    for (int i = b; i < n && a.count < kMaxGather; ++i) {
+      const bool aligned = ((uintptr_t)dst[i] % 16 == 0) && ((uintptr_t)src[i] % 16 == 0) && bytes[i] % 16 == 0;
+      if (!aligned || bytes[i] == 0) {  // odd sizes / offsets: a copy kernel of its own, same stream
+        if (bytes[i] && device_copy_kernel(dst[i], src[i], bytes[i], stream) != 0) return -1;
+        continue;
+      }
+      const int k = a.count++;
+      a.dst[k] = static_cast<uint4*>(dst[i]);
+      a.src[k] = static_cast<const uint4*>(src[i]);
+      a.n16[k] = bytes[i] / 16;
+      a.wg_start[k] = wg;
+      wg += (int)std::min<size_t>(64, std::max<size_t>(1, a.n16[k] / (256 * 16)));
+    }
+    if (!a.count) continue;
+    a.wg_start[a.count] = wg;
+    hipLaunchKernelGGL(gather_kernel, dim3(wg), dim3(256), 0, st, a);
+  }
   return (int)hipGetLastError();
 }
 

@@ -213,6 +213,10 @@ PYBIND11_MODULE(_C, m) {
       .def_property("termdet", [](Taskpool& t) { return t.termdet_name; }, [](Taskpool& t, const std::string& n) { t.termdet_name = n; })
       .def_property_readonly("nb_tasks", [](Taskpool& t) { return t.nb_tasks.load(); })
       .def_property_readonly("nb_pending_actions", [](Taskpool& t) { return t.nb_pending_actions.load(); })
+      // termination-detector counters (reference parsec_taskpool_update_nbtask /
+      // runtime_actions); only meaningful on a monitored taskpool
+      .def("addto_nb_tasks", [](Taskpool& t, int64_t d) { return t.tdm ? t.tdm->taskpool_addto_nb_tasks(&t, d) : (int64_t)0; })
+      .def("addto_runtime_actions", [](Taskpool& t, int64_t d) { return t.tdm ? t.tdm->taskpool_addto_runtime_actions(&t, d) : (int64_t)0; })
       .def_property_readonly("completed", [](Taskpool& t) { return t.completed.load(); })
       .def_property_readonly("simulation_date", [](Taskpool& t) { return t.largest_simulation_date.load(); })
       .def("set_complete_callback", [](Taskpool& t, py::function f) {
@@ -648,6 +652,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("trsm_inverse_limit", []() { return trsm_inverse_limit(); });
   m.def("trsm_estimate_route", [](int on) { return kern::trsm_estimate_route(on); }, py::arg("on") = -1,
         "Auto panel solve: 1 decide on the host from the estimate the local POTRF published, 0 device-side gate only; returns the previous setting");
+  m.def("trsm_estimate_lookup", [](uintptr_t p) { return kern::trsm_estimate_lookup((const void*)p); },
+        "Published panel estimate keyed by the W address p on the current device (0 = unknown)");
+  m.def("trsm_estimate_known", []() { return kern::trsm_estimate_known(); }, "W addresses with a published panel estimate (current device)");
+  m.def("device_cache_alloc", [](int dev, size_t bytes) { return (uintptr_t)device_cache_alloc(dev, bytes); }, "Carve a buffer from a GPU's tile-cache zone");
+  m.def("device_cache_free", [](int dev, uintptr_t p) { return device_cache_free(dev, (void*)p); });
   m.def("trsm_estimate_stats", [](bool reset) {
     uint64_t v[3];
     kern::trsm_estimate_stats(v, reset);
@@ -754,6 +763,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("comm_rank", &comm_rank);
   m.def("comm_size", &comm_size);
   m.def("comm_device_plane", []() { return std::string(comm_device_plane_name()); });
+  m.def("comm_bytes_by_peer", &comm_bytes_by_peer, "IPC payload bytes this rank pulled from each peer (xGMI link by link)");
+  m.def("comm_pull_routes", &comm_pull_routes, "Pull route per peer: 0 copy engine, 1 copy kernel, 3 multi-source gather kernel");
+  m.def("comm_probe_table", &comm_probe_table, "This rank's IPC start-up probe per peer: (bits: 1 open, 2 copy-engine pull, 4 copy kernel, 8 host read; 0 = ok, open attempts)");
   m.def("comm_plane_status", &comm_plane_status, "0, or the first failing step of this rank's IPC plane start-up (-1x set-up, -2x open of peer x, -4x copy from peer x, -6x bytes from peer x, -7 another rank failed)");
   m.def("comm_allreduce_max", [](uint32_t v) { py::gil_scoped_release rel; return comm_allreduce_max_u32(v); });
 }

@@ -23,24 +23,38 @@ static void fire(Taskpool* tp) {
 }
 
 // Packed termination word (Taskpool::termdet_word) of the local and
-// user-trigger detectors: nb_tasks and nb_pending_actions as biased 30-bit
-// fields plus the state bits, so the update that completes termination and the
-// termination decision are ONE atomic operation. A thread whose update does not
-// terminate the taskpool never touches it again -- it may be freed the moment
-// another thread fires. (The previous separate counters were re-read after the
+// user-trigger detectors: nb_tasks and nb_pending_actions as biased fields plus
+// the state bits, so the update that completes termination and the termination
+// decision are ONE atomic operation. A thread whose update does not terminate
+// the taskpool never touches it again -- it may be freed the moment another
+// thread fires. (The previous separate counters were re-read after the
 // decrement; ThreadSanitizer caught a comm thread reading a taskpool the main
 // thread had already freed, round 5.) nb_tasks / nb_pending_actions stay
 // updated for readers, BEFORE the packed update.
+// Widths: nb_tasks 32 bits (+-2^31, the reference's int32 nb_tasks range),
+// nb_pending_actions 28 bits (+-2^27 runtime actions in flight), state bits
+// 60..63. A value outside its field is fatal: it would carry into the
+// neighbouring field and terminate early or never (checked on the exact int64
+// counters, which are updated first).
 namespace {
-constexpr uint64_t kField = 30;
-constexpr uint64_t kMask = (1ull << kField) - 1;
-constexpr uint64_t kBias = 1ull << (kField - 1);
-constexpr uint64_t kTasksShift = 0, kActionsShift = kField;
+constexpr uint64_t kTasksBits = 32, kActionsBits = 28;
+constexpr uint64_t kTasksShift = 0, kActionsShift = kTasksBits;
+constexpr uint64_t bits_of(uint64_t shift) { return shift == kTasksShift ? kTasksBits : kActionsBits; }
+constexpr uint64_t mask_of(uint64_t shift) { return (1ull << bits_of(shift)) - 1; }
+constexpr uint64_t bias_of(uint64_t shift) { return 1ull << (bits_of(shift) - 1); }
 constexpr uint64_t kReady = 1ull << 60, kTriggered = 1ull << 61, kDone = 1ull << 62;
-constexpr uint64_t kZero = (kBias << kTasksShift) | (kBias << kActionsShift);
+constexpr uint64_t kZero = (bias_of(kTasksShift) << kTasksShift) | (bias_of(kActionsShift) << kActionsShift);
+static_assert(kActionsShift + kActionsBits <= 60, "counter fields overlap the state bits");
+
+inline void check_range(const Taskpool* tp, uint64_t shift, int64_t v) {
+  const int64_t b = (int64_t)bias_of(shift);
+  if (v < -b || v >= b)
+    fatal("termination detection of taskpool %u: %s = %lld leaves the packed field (+-%lld)", tp->taskpool_id,
+          shift == kTasksShift ? "nb_tasks" : "nb_pending_actions", (long long)v, (long long)b);
+}
 
 inline uint64_t fresh_word() { return kZero; }
-inline int64_t field(uint64_t w, uint64_t shift) { return (int64_t)((w >> shift) & kMask) - (int64_t)kBias; }
+inline int64_t field(uint64_t w, uint64_t shift) { return (int64_t)((w >> shift) & mask_of(shift)) - (int64_t)bias_of(shift); }
 inline uint64_t delta(int64_t d, uint64_t shift) { return (uint64_t)d << shift; }  // two's complement: a borrow stays in the biased field
 
 // Terminated by this update? `need_tasks`: the tasks field counts (local);
@@ -84,20 +98,24 @@ class PackedTermdet : public TermdetModule {
     // nb_tasks = 0): that task's own completion is still to come, so it stays
     // counted -- the taskpool ends when it has finished, not while it runs
     if (Task* t = current_task(); t && t->taskpool == tp && !(t->task_class->flags & TC_INTERNAL)) ++v;
+    check_range(tp, kTasksShift, v);
     tp->nb_tasks.store(v, std::memory_order_seq_cst);
     settle(tp, set_field(tp, kTasksShift, v));
   }
   int64_t taskpool_addto_nb_tasks(Taskpool* tp, int64_t d) override {
     const int64_t v = tp->nb_tasks.fetch_add(d, std::memory_order_seq_cst) + d;
+    check_range(tp, kTasksShift, v);
     settle(tp, tp->termdet_word.fetch_add(delta(d, kTasksShift), std::memory_order_acq_rel) + delta(d, kTasksShift));
     return v;
   }
   void taskpool_set_runtime_actions(Taskpool* tp, int64_t v) override {
+    check_range(tp, kActionsShift, v);
     tp->nb_pending_actions.store(v, std::memory_order_seq_cst);
     settle(tp, set_field(tp, kActionsShift, v));
   }
   int64_t taskpool_addto_runtime_actions(Taskpool* tp, int64_t d) override {
     const int64_t v = tp->nb_pending_actions.fetch_add(d, std::memory_order_seq_cst) + d;
+    check_range(tp, kActionsShift, v);
     settle(tp, tp->termdet_word.fetch_add(delta(d, kActionsShift), std::memory_order_acq_rel) + delta(d, kActionsShift));
     return v;
   }
@@ -113,7 +131,7 @@ class PackedTermdet : public TermdetModule {
   static uint64_t set_field(Taskpool* tp, uint64_t shift, int64_t v) {
     uint64_t w = tp->termdet_word.load(std::memory_order_acquire), n;
     do {
-      n = (w & ~(kMask << shift)) | ((((uint64_t)(v + (int64_t)kBias)) & kMask) << shift);
+      n = (w & ~(mask_of(shift) << shift)) | ((((uint64_t)(v + (int64_t)bias_of(shift))) & mask_of(shift)) << shift);
     } while (!tp->termdet_word.compare_exchange_weak(w, n, std::memory_order_acq_rel));
     return n;
   }
@@ -138,12 +156,18 @@ class UserTriggerTermdet : public PackedTermdet {
  public:
   UserTriggerTermdet() : PackedTermdet(false) {}
   const char* name() const override { return "user_trigger"; }
+  // Exactly one caller settles, and only after its last use of tp: on several
+  // ranks the caller that wins kBroadcast (the application's trigger, or the
+  // comm thread relaying a peer's) broadcasts, then sets kTriggered and
+  // settles; every later caller returns without touching tp again (a caller
+  // that settled while the winner was still broadcasting could free tp under
+  // it). On one rank the first caller to set kTriggered settles.
   void user_trigger(Taskpool* tp) override {
-    const uint64_t prev = tp->termdet_word.load(std::memory_order_acquire);
-    if (prev & kTriggered) return;
-    // the broadcast precedes the local trigger: tp stays alive until it is set
-    if (tp->context && tp->context->nb_nodes > 1 && !(tp->termdet_word.fetch_or(kBroadcast, std::memory_order_acq_rel) & kBroadcast))
+    if (tp->termdet_word.load(std::memory_order_acquire) & kTriggered) return;
+    if (tp->context && tp->context->nb_nodes > 1) {
+      if (tp->termdet_word.fetch_or(kBroadcast, std::memory_order_acq_rel) & kBroadcast) return;
       termdet_user_trigger_broadcast(tp);
+    }
     const uint64_t w = tp->termdet_word.fetch_or(kTriggered, std::memory_order_acq_rel);
     if (w & kTriggered) return;
     settle(tp, w | kTriggered);

@@ -154,3 +154,59 @@ def test_distributed_redistribute(pa, nranks, method, shape):
     for rc, out in outs:
         assert rc == 0 and "bad 0" in out, out
     assert sum(int(out.split("checked ")[1].split()[0]) for _, out in outs) == int(shape.split()[4]) * int(shape.split()[5])
+
+
+def _bench_ranks(nranks, extra, timeout=240):
+    """bench.py --device cpu as `nranks` processes (the env torchrun would give
+    them): returns [(returncode, stdout, stderr)] in rank order."""
+    import random
+
+    port = str(29700 + random.randint(0, 250))
+    bench = os.path.join(os.path.dirname(HERE), "bench.py")
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks), MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
+                   PARSEC_MCA_device_hip_enabled="0", TORCHELASTIC_RUN_ID="t" + uuid.uuid4().hex[:6] if r == 0 else "")
+        procs.append(env)
+    rid = procs[0]["TORCHELASTIC_RUN_ID"]
+    run = []
+    for env in procs:
+        env["TORCHELASTIC_RUN_ID"] = rid
+        run.append(subprocess.Popen([sys.executable, bench, "--gpus", str(nranks), "--size", "768", "--nb", "128", "--steps", "1",
+                                     "--warmup", "0", "--device", "cpu", "--cores", "2", *extra],
+                                    stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
+    outs = []
+    try:
+        for p in run:
+            o, e = p.communicate(timeout=timeout)
+            outs.append((p.returncode, o, e))
+    finally:
+        for p in run:
+            if p.poll() is None:
+                p.kill()
+    return outs
+
+
+def test_bench_json_before_failing_exit(pa):
+    """bench.py on a multi-rank job whose device plane is not IPC (here: CPU
+    ranks, every peer unprobed) prints its JSON line -- device plane and the
+    rank x peer probe table -- BEFORE exiting 3, so a failed 8-GPU run still
+    reports which pair failed; with --allow-host-plane the same job runs, and
+    the line carries the per-peer payload bytes."""
+    import json
+
+    outs = _bench_ranks(2, [])
+    assert [rc for rc, _, _ in outs] == [3, 3], [(rc, e[-800:]) for rc, _, e in outs]
+    line = [l for l in outs[0][1].splitlines() if l.startswith("{")]
+    assert line, outs[0]
+    out = json.loads(line[-1])
+    assert out["value"] is None and "device plane is not ipc" in out["error"]
+    assert [p["plane"] for p in out["device_plane"]] == ["host", "host"]
+    assert out["ipc_probe"]["codes"] == [[0, -1], [-1, 0]]
+    outs = _bench_ranks(2, ["--allow-host-plane"])
+    assert [rc for rc, _, _ in outs] == [0, 0], [(rc, e[-800:]) for rc, _, e in outs]
+    out = json.loads([l for l in outs[0][1].splitlines() if l.startswith("{")][-1])
+    assert out["value"] > 0 and out["residual"] < 1e-12
+    for r, c in enumerate(out["comm"]):
+        assert c["get_fragments"] > 0 and sum(c["bytes_from_peer"]) == c["bytes_fragments"], c
+        assert c["bytes_from_peer"][r] == 0

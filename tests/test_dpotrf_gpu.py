@@ -196,6 +196,57 @@ def test_trsm_inverse_modes_gpu(pa, nb):
         assert torch.linalg.norm(La - Lb).item() < 1e-3 * d02
 
 
+def test_trsm_estimate_forgotten_on_reuse(pa):
+    """A panel estimate is keyed by the address of the W its POTRF wrote. Once
+    that W is gone, a buffer carved at the same address (a receive buffer, a
+    re-staged tile) is a different tile: the lookup must not return the old
+    estimate (it would skip the guard of an ill-conditioned panel that arrived
+    from another rank). Every tile-cache allocation drops the key of its
+    address. Here the first context's zone (and its W tiles) is released at
+    fini; the next context's zone is carved from the same device memory."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    N, nb = 2048, 256
+    NT = N // nb
+    ctx = pa.init(3)
+    try:
+        gpu = pa.first_gpu_device_index()
+        store = torch.empty((NT, NT, nb, nb), dtype=torch.float64, device="cuda")
+        A = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb, nb, N, N, device=gpu, ptr=store.data_ptr())
+        S = _spd(N, "cuda", 7)
+        store.copy_(S.reshape(NT, nb, NT, nb).permute(2, 0, 3, 1))
+        torch.cuda.synchronize()
+        tp, info = pa.dpotrf_jdf_new(A)
+        ctx.add_taskpool(tp)
+        ctx.start()
+        ctx.wait()
+        assert pa.read_int(info) == 0
+        known = set(pa.trsm_estimate_known())
+        assert len(known) >= NT - 1, known
+        assert all(pa.trsm_estimate_lookup(p) > 0 for p in known)
+    finally:
+        ctx.fini()
+    ctx = pa.init(3)
+    try:
+        gpu = pa.first_gpu_device_index()
+        got, hits = [], []
+        for _ in range(4 * NT):
+            p = pa.device_cache_alloc(gpu, nb * nb * 8)
+            if not p:
+                break
+            got.append(p)
+            if p in known:
+                hits.append(p)
+        for p in got:
+            pa.device_cache_free(gpu, p)
+        if not hits:
+            pytest.skip("the new zone did not reuse a W address")
+        assert all(pa.trsm_estimate_lookup(p) == 0.0 for p in hits)
+        assert all(pa.trsm_estimate_lookup(p) > 0 for p in known - set(hits))  # only the reused keys went
+    finally:
+        ctx.fini()
+
+
 @pytest.mark.parametrize("hp_route", [1, 2])
 @pytest.mark.parametrize("N,nb", [(4096, 256), (4096, 512)])
 def test_dpotrf_early_release(pa, N, nb, hp_route):

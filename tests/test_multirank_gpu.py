@@ -52,12 +52,14 @@ def _run(case, nranks, *args, timeout=100, env_extra=None):
     return outs
 
 
-# The IPC pull routes. "auto" on this 1-GPU box: every peer shares the GPU, so
-# pulls are copy kernels spread over 2 streams. "copy-engine": the exact route a
-# peer on ANOTHER GPU takes (comm_ipc_copy_mode 2 picks it for distinct GPUs):
-# hipMemcpyAsync on the GPU's one shared copy stream.
+# The IPC pull routes. "gather" (the default, comm_ipc_copy_mode 3, the route
+# of peers on distinct GPUs too): the pulls of a progress pass leave in ONE
+# multi-source gather kernel, one transfer per source peer; on this 1-GPU box
+# every peer shares the GPU and the gathers alternate over 2 streams.
+# "copy-engine": hipMemcpyAsync per pull on the GPU's one shared copy stream
+# (the fall-back of a peer whose probe kernel read failed).
 ROUTES = {
-    "auto": {},
+    "gather": {},
     "copy-engine": {"PARSEC_MCA_comm_ipc_copy_mode": "0", "PARSEC_MCA_comm_ipc_streams": "1"},
 }
 
@@ -183,7 +185,7 @@ def test_headline_tile_size_8_ranks_shared_gpu(pa, route):
     _gpu()
     import json
 
-    port = 29600 + (os.getpid() + (7 if route != "auto" else 0)) % 300
+    port = 29600 + (os.getpid() + (7 if route != "gather" else 0)) % 300
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr", "127.0.0.1",
            "--master-port", str(port), os.path.join(os.path.dirname(HERE), "bench.py"), "--gpus", "8", "--size", "16384", "--nb", "1024",
            "--steps", "1", "--warmup", "0", "--share-gpu", "--cores", "1"]
@@ -197,3 +199,34 @@ def test_headline_tile_size_8_ranks_shared_gpu(pa, route):
     comm = out["comm"]
     assert len(comm) == 8 and all(c["get_fragments"] == 0 for c in comm), comm
     assert sum(c["get_ipc"] for c in comm) > 0 and sum(c["bytes_pulled_ipc"] for c in comm) > 0, comm
+    # every pair passed every probe route; bytes by source peer add up
+    assert out["ipc_probe"]["codes"] == [[0] * 8 for _ in range(8)], out["ipc_probe"]
+    for r, c in enumerate(comm):
+        assert sum(c["bytes_from_peer"]) == c["bytes_pulled_ipc"] and c["bytes_from_peer"][r] == 0, c
+    # pulls from distinct source ranks were in flight together (lanes)
+    assert max(c["gets_lanes_busy_max"] for c in comm) >= 2, comm
+
+
+def test_bench_probe_failure_reported(pa):
+    """comm_ipc_probe_fail=2:1: rank 2's open of rank 1's probe buffer fails,
+    so every rank falls back to the host plane; bench.py prints its JSON line
+    (device plane per rank, the rank x peer probe table with the failed pair)
+    before exiting non-zero."""
+    _gpu()
+    import json
+
+    port = 29600 + (os.getpid() + 13) % 300
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.join(os.path.dirname(HERE), "bench.py"), "--gpus", "4", "--size", "4096", "--nb", "512",
+           "--steps", "1", "--warmup", "0", "--share-gpu", "--cores", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, start_new_session=True,
+                       env=dict(os.environ, PARSEC_MCA_comm_ipc_probe_fail="2:1"))
+    assert r.returncode != 0, r.stdout[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert lines, r.stdout[-2000:] + r.stderr[-2000:]
+    out = json.loads(lines[-1])
+    assert out["value"] is None and "not ipc" in out["error"], out
+    codes = out["ipc_probe"]["codes"]
+    assert codes[2][1] == 1, codes  # open failed
+    assert all(codes[a][b] == 0 for a in range(4) for b in range(4) if (a, b) != (2, 1)), codes
+    assert all(p["plane"] == "host" for p in out["device_plane"]), out["device_plane"]

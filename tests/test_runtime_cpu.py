@@ -12,6 +12,7 @@ import threading
 import numpy as np
 import pytest
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCHEDULERS = ["lfq", "pbq", "ltq", "lhq", "ap", "spq", "gd", "ll", "llp", "rnd", "ip"]
 
 
@@ -465,6 +466,43 @@ def test_user_trigger_termdet(pa):
     ctx.wait()
     assert tp.completed
     ctx.fini()
+
+
+def test_termdet_packed_field_bounds(pa, tmp_path):
+    """The local detector packs nb_tasks (32 bits, the reference's int32 range)
+    and nb_pending_actions (28 bits) into one atomic word: values up to the
+    bound count exactly and terminate normally; one past it is a fatal error
+    instead of a silent carry into the neighbouring field."""
+    import subprocess
+    import sys
+
+    ctx = _ctx(pa, 1)
+    tp = pa._C.DtdTaskpool()
+    ctx.add_taskpool(tp)
+    ctx.start()
+    big = 2**31 - 2  # + the taskpool's own bookkeeping stays below 2^31
+    assert tp.addto_nb_tasks(big) >= big
+    assert not tp.completed
+    tp.addto_nb_tasks(-big)
+    acts = 2**27 - 2
+    tp.addto_runtime_actions(acts)
+    tp.addto_runtime_actions(-acts)
+    ctx.wait()
+    assert tp.completed
+    ctx.fini()
+    code = (
+        "import parsec_amd as pa\n"
+        "ctx = pa.init(1)\n"
+        "tp = pa._C.DtdTaskpool()\n"
+        "ctx.add_taskpool(tp)\n"
+        "ctx.start()\n"
+        f"tp.{{}}(2**{{}})\n"
+    )
+    for fn, bits in (("addto_nb_tasks", 31), ("addto_runtime_actions", 27)):
+        r = subprocess.run([sys.executable, "-c", code.format(fn, bits)], capture_output=True, text=True, timeout=120,
+                           cwd=str(tmp_path), env=dict(os.environ, PYTHONPATH=REPO))
+        assert r.returncode != 0, (fn, r.stdout, r.stderr)
+        assert "leaves the packed field" in r.stderr, r.stderr[-2000:]
 
 
 # ------------------------------------------------- PINS: checkers / steals
