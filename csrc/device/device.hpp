@@ -96,8 +96,9 @@ struct GemmDesc {
   uint8_t a_lower;         // 1: op(A) is lower triangular (zeros above): row block i only reads k < (i+1) BM
   uint8_t b_upper;         // 1: op(B) is upper triangular (zeros below): column block j only reads k < (j+1) BN
   // 1: panel solve through W = L^-1 under PARSEC_DPOTRF_TRSM=auto: the
-  // workgroups skip when the condition estimate in W's spare slots
-  // (B[(k-1) ldb + 0] = max|L|, + 1 = max|W|) exceeds the launch's limit
+  // workgroups skip when the condition estimate (Cin[0] = max|L|, Cin[1] =
+  // max|W|: a gated descriptor has beta 0 and never reads Cin as C) exceeds
+  // the launch's limit
   uint8_t gate;
   // optional (zero = off): beta scales Cin (ld ldcin) instead of C, and C2 (ld
   // ldc2) -= every value written to C (fused "W = A1 + V^T A2" / "A1 -= T^T W")
@@ -112,10 +113,12 @@ struct TrsmDesc {  // B := B * op(L)^-1 ; right side, lower, (trans), non-unit
   int m, n;  // B is m x n, L is n x n
   int ldl, ldb;
   uint8_t trans;  // 1: B * L^-T (the Cholesky panel)
-  uint8_t gate = 0;  // 1: run only when the estimate in invD's spare slots exceeds the limit (fallback of a gated W-GEMM)
-  uint8_t pad[2] = {0, 0};
+  uint8_t gate = 0;  // 1: run only when the estimate at gate_slot exceeds the limit (fallback of a gated W-GEMM)
+  uint8_t packed = 0;  // 1: L is a packed panel tile: L(i, k) = L[i * ldl + k] for i > k (its strict upper part)
+  uint8_t pad = 0;
   int invD_ld = 0;   // 0: invD holds contiguous 64x64 blocks; else the diagonal 64-blocks of an n x n matrix (ld invD_ld), e.g. W = L^-1
   const double* invD = nullptr;  // optional: inverses of L's 64x64 diagonal blocks (from POTRF)
+  const double* gate_slot = nullptr;  // gate: max|L|, max|W| of the panel (workspace)
 };
 static_assert(sizeof(GemmDesc) == 96, "GemmDesc grew: the grouped-GEMM kernel argument block is sized for 40 of them");
 
@@ -126,6 +129,10 @@ struct PotrfDesc {
   double* invD_out = nullptr;  // optional: keep the 64x64 diagonal-block inverses (ceil(n/64) x 4096 doubles)
   double* W_out = nullptr;     // optional: also write W = L^-1 (n x n, lower triangular, zero above, ld ldw)
   int ldw = 0;
+  // packed panel tile: W_out's strict upper triangle holds L^T instead of
+  // zeros (W lower incl. the diagonal, L(i, j) = W_out(j, i) for i > j), so the
+  // panel solve needs this ONE tile (TrsmGemmDesc::packed)
+  uint8_t pack_w = 0;
 };
 
 // Panel solve through the explicit inverse: B := B * W^T with W = L^-1 from
@@ -139,6 +146,9 @@ struct TrsmGemmDesc {
   // PARSEC_DPOTRF_TRSM=auto / blocked (trsm_inverse_mode)
   const double* L = nullptr;
   int ldl = 0;
+  // 1: W is a packed panel tile (PotrfDesc::pack_w): W below and on the
+  // diagonal, L^T above; L = W, ldl = ldw
+  uint8_t packed = 0;
 };
 
 // Panel solve of the tile Cholesky: 0 = always through W = L^-1, 1 = auto (W

@@ -175,8 +175,9 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
   if (d.lower_only && n0 > m0 + BM - 1) return;
   if (d.gate) {
     // panel solve through W = L^-1 whose condition estimate is too large: the
-    // gated substitution kernel launched behind this one solves instead
-    const double* __restrict__ slot = d.B + (size_t)(d.k - 1) * d.ldb;
+    // gated substitution kernel launched behind this one solves instead (the
+    // estimate slots: Cin, which a gated descriptor (beta 0) never reads as C)
+    const double* __restrict__ slot = d.Cin;
     if (slot[0] * slot[1] > args.gate_limit) return;
   }
 
@@ -740,9 +741,10 @@ __global__ __launch_bounds__(kTrsmThreads) void dtrsm_inv_kernel(const TrsmInvAr
   const size_t ldD = d.invD_ld ? (size_t)d.invD_ld : 64;
   const size_t bstride = d.invD_ld ? (size_t)64 * d.invD_ld + 64 : 4096;
   if (d.gate) {
-    const double* __restrict__ slot = invD + (size_t)(d.n - 1) * ldD;
+    const double* __restrict__ slot = d.gate_slot;
     if (!(slot[0] * slot[1] > args.gate_limit)) return;  // the W-GEMM solved this panel
   }
+  const bool packed = d.packed != 0;  // L(i, k) = d.L(k, i) for i > k (packed panel tile)
   const int r0 = (b - args.block_start[di]) * BR;
   const int n = d.n, m = d.m;
   const int nblk = (n + 63) / 64;
@@ -777,7 +779,8 @@ __global__ __launch_bounds__(kTrsmThreads) void dtrsm_inv_kernel(const TrsmInvAr
     const int c0 = jb * 64;
     const int cw = c0 + 16 * g + fr;  // L row this lane feeds as the MFMA A-operand
     const bool valid = cw < n;
-    const double* __restrict__ Lp = L + (valid ? cw : 0);
+    const double* __restrict__ Lp = packed ? L + (size_t)(valid ? cw : 0) * ldl : L + (valid ? cw : 0);
+    const size_t lstride = packed ? 1 : ldl;
     double4_t acc[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) acc[u] = (double4_t){0.0, 0.0, 0.0, 0.0};
@@ -787,7 +790,7 @@ __global__ __launch_bounds__(kTrsmThreads) void dtrsm_inv_kernel(const TrsmInvAr
       double av[4], bv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        av[u] = valid ? Lp[(size_t)(k + 4 * u + fk) * ldl] : 0.0;
+        av[u] = valid ? Lp[(size_t)(k + 4 * u + fk) * lstride] : 0.0;
         bv[u] = pget(k + 4 * u + fk, fr);
       }
 #pragma unroll
@@ -1163,21 +1166,40 @@ struct CopyBatchArgs {
   const double* src[kMaxCopyBatch];
   double* dst[kMaxCopyBatch];
   // condition estimate of the panel solves (PARSEC_DPOTRF_TRSM=auto): job j
-  // maxes |L| and |W| over the lower triangles into W's spare slots
-  // W[(n-1) ldw + 0 / 1] (strictly upper, zero since POTRF, never read by the
-  // GEMM: its column block 0 reads k < 128 <= n - 1)
+  // maxes |L| and |W| into scan_slot[j][0 / 1] (workspace, zeroed before the
+  // launch). Unpacked: L lower (scan_L), W lower (scan_W). Packed panel tile
+  // (scan_packed): W = its lower part incl. the diagonal, L = its strict upper
+  // part transposed with the diagonal 1 / W(i, i).
   int nscan;
-  int scan_n[kMaxScan], scan_ldl[kMaxScan], scan_ldw[kMaxScan];
+  int scan_n[kMaxScan], scan_ldl[kMaxScan], scan_ldw[kMaxScan], scan_packed[kMaxScan];
   const double* scan_L[kMaxScan];
-  double* scan_W[kMaxScan];
+  const double* scan_W[kMaxScan];
+  unsigned long long* scan_slot[kMaxScan];
+  // unpack jobs: Wu (n x n, ld n) = the lower part incl. the diagonal of a
+  // packed panel tile, zeros above: what the W-GEMM and the substitution's
+  // diagonal blocks read
+  int nunpack;
+  int up_n[kMaxScan], up_ld[kMaxScan];
+  const double* up_src[kMaxScan];
+  double* up_dst[kMaxScan];
 };
 static_assert(sizeof(CopyBatchArgs) <= 4096, "CopyBatchArgs exceeds the kernel argument limit");
 
-// blockIdx.y = tile (then the scan jobs), blockIdx.x strides over columns; one
-// wave-row per column.
+// blockIdx.y = tile, then the scan jobs, then the unpack jobs; blockIdx.x
+// strides over columns; one wave-row per column.
 __global__ __launch_bounds__(256) void copy_tiles_kernel(const CopyBatchArgs a) {
   PARSEC_WAVE_PRIO(a.prio);
   const int t = blockIdx.y;
+  if (t >= a.count + a.nscan) {
+    const int j = t - a.count - a.nscan;
+    const int n = a.up_n[j];
+    const size_t ld = a.up_ld[j];
+    const double* __restrict__ P = a.up_src[j];
+    double* __restrict__ W = a.up_dst[j];
+    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < n; c += gridDim.x * 4)
+      for (int r = threadIdx.x & 63; r < n; r += 64) W[(size_t)c * n + r] = r >= c ? P[(size_t)c * ld + r] : 0.0;
+    return;
+  }
   if (t >= a.count) {
     const int j = t - a.count;
     const int n = a.scan_n[j];
@@ -1185,11 +1207,21 @@ __global__ __launch_bounds__(256) void copy_tiles_kernel(const CopyBatchArgs a) 
     const double* __restrict__ W = a.scan_W[j];
     const size_t ldl = a.scan_ldl[j], ldw = a.scan_ldw[j];
     double mL = 0.0, mW = 0.0;
-    for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < n; c += gridDim.x * 4)
-      for (int r = c + (threadIdx.x & 63); r < n; r += 64) {
-        mL = fmax(mL, fabs(L[(size_t)c * ldl + r]));
-        mW = fmax(mW, fabs(W[(size_t)c * ldw + r]));
-      }
+    if (a.scan_packed[j]) {
+      for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < n; c += gridDim.x * 4)
+        for (int r = threadIdx.x & 63; r < n; r += 64) {
+          const double v = fabs(W[(size_t)c * ldw + r]);
+          if (r >= c) mW = fmax(mW, v);
+          if (r < c) mL = fmax(mL, v);
+          if (r == c && v > 0.0) mL = fmax(mL, 1.0 / v);
+        }
+    } else {
+      for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < n; c += gridDim.x * 4)
+        for (int r = c + (threadIdx.x & 63); r < n; r += 64) {
+          mL = fmax(mL, fabs(L[(size_t)c * ldl + r]));
+          mW = fmax(mW, fabs(W[(size_t)c * ldw + r]));
+        }
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       mL = fmax(mL, __shfl_xor(mL, o));
@@ -1197,7 +1229,7 @@ __global__ __launch_bounds__(256) void copy_tiles_kernel(const CopyBatchArgs a) 
     }
     if ((threadIdx.x & 63) == 0 && (mL > 0.0 || mW > 0.0)) {
       // non-negative doubles order like their bit patterns: integer max
-      auto* slot = reinterpret_cast<unsigned long long*>(a.scan_W[j] + (size_t)(n - 1) * ldw);
+      unsigned long long* slot = a.scan_slot[j];
       __hip_atomic_fetch_max(slot, (unsigned long long)__double_as_longlong(mL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_fetch_max(slot + 1, (unsigned long long)__double_as_longlong(mW), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1208,6 +1240,26 @@ __global__ __launch_bounds__(256) void copy_tiles_kernel(const CopyBatchArgs a) 
   double* __restrict__ d = a.dst[t];
   for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cols; c += gridDim.x * 4)
     for (int r = threadIdx.x & 63; r < rows; r += 64) d[(size_t)c * ldd + r] = s[(size_t)c * lds + r];
+}
+
+// Packed panel tile (PotrfDesc::pack_w): P(r, c) = L(c, r) for r < c, through
+// a 64 x 64 LDS tile (coalesced on both sides); blocks below the diagonal exit.
+__global__ __launch_bounds__(256) void pack_upper_lt_kernel(double* __restrict__ P, int ldp, const double* __restrict__ L, int ldl, int n) {
+  __shared__ double t[64][65];
+  const int br = blockIdx.x, bc = blockIdx.y;  // P block (br, bc), br <= bc
+  if (br > bc) return;
+  const int r0 = br * 64, c0 = bc * 64;
+  for (int e = threadIdx.x; e < 4096; e += 256) {
+    const int cc = e >> 6, rr = e & 63;  // read L(c0 + rr, r0 + cc): column r0 + cc of L, contiguous in rr
+    const int lr = c0 + rr, lc = r0 + cc;
+    t[cc][rr] = (lr < n && lc < n) ? L[(size_t)lc * ldl + lr] : 0.0;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 4096; e += 256) {
+    const int cc = e >> 6, rr = e & 63;  // write P(r0 + rr, c0 + cc) = L(c0 + cc, r0 + rr) = t[rr][cc]
+    const int pr = r0 + rr, pc = c0 + cc;
+    if (pr < n && pc < n && pr < pc) P[(size_t)pc * ldp + pr] = t[rr][cc];
+  }
 }
 
 size_t potrf_workspace_bytes(const PotrfDesc& p) {
@@ -1229,6 +1281,8 @@ static void launch_lower_inverse(const double* L, int lda, int n, const double* 
     CopyBatchArgs ca;
     ca.count = std::min(kMaxCopyBatch, nblk - b0);
     ca.prio = t_launch_prio;
+    ca.nscan = 0;
+    ca.nunpack = 0;
     for (int i = 0; i < ca.count; ++i) {
       const int b = b0 + i, w = std::min(64, n - 64 * b);
       ca.rows[i] = w; ca.cols[i] = w; ca.ld_src[i] = 64; ca.ld_dst[i] = ldx;
@@ -1299,6 +1353,10 @@ void launch_potrf(const PotrfDesc& p, hipStream_t stream, double* ws) {
     // W = L^-1 from the diagonal-block inverses just computed
     double* tmp = ws + (p.invD_out ? 0 : (size_t)((p.n + 63) / 64) * 4096);
     launch_lower_inverse(p.A, p.lda, p.n, inv_base, p.W_out, p.ldw, tmp, stream);
+    if (p.pack_w) {
+      const int nblk = (p.n + 63) / 64;
+      hipLaunchKernelGGL(pack_upper_lt_kernel, dim3(nblk, nblk), dim3(256), 0, stream, p.W_out, p.ldw, p.A, p.lda, p.n);
+    }
   }
 }
 
@@ -1768,6 +1826,7 @@ struct PotrfStepArgs {
   int stamp;        // record phase clocks of the DIAG item (diagnostics)
   int claim;        // critical-path launch: claim the CUs
   int j;            // step (-1: first launch, nb - 1: last launch)
+  int pack;         // packed panel tile: W's strict upper triangle receives L^T (PotrfDesc::pack_w)
   // item ranges: [0, n_diag) DIAG, then TRAIL, RUPD, LW, XW, ZERO
   int n_diag, n_trail, n_rupd, n_lw, n_xw, n_zero;
   // auto panel solve (optional): the items that finalize blocks of L and W fold
@@ -1840,6 +1899,18 @@ __device__ __forceinline__ void blk_put(Blk& S, const BlkRegs& R, bool t) {
       S[lo][hi] = R.v[e].x;
       S[lo + 1][hi] = R.v[e].y;
     }
+  }
+}
+
+// S[n][m] = C(m, n) (acc_to_blk operand form) -> G(n, m) = C(m, n): the block
+// transposed into global memory, 16-byte stores along G's columns
+__device__ __forceinline__ void blk_store_t(const Blk& S, double* __restrict__ G, int ld) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int p = tid + 256 * e;
+    const int col = p >> 5, lo = (p & 31) * 2;  // G column col = C row m; G rows lo, lo + 1 = C columns
+    *reinterpret_cast<double2_t*>(G + (size_t)col * ld + lo) = (double2_t){S[lo][col], S[lo + 1][col]};
   }
 }
 
@@ -1974,6 +2045,11 @@ __device__ __forceinline__ void dpotrf_step(const PotrfStepArgs& a, double* pool
     __syncthreads();  // every wave has read S0 (a copy of the block being overwritten)
     acc_store(acc, blkA(r, p), lda, false);
     if (a.est) est_fold(a.est, 0, acc_absmax(acc));  // L(r, p) is final
+    if (a.pack) {  // packed panel tile: L(r, p)^T into W's upper block (p, r)
+      acc_to_blk(acc, S0, false);
+      __syncthreads();
+      blk_store_t(S0, blkW(p, r), ldw);
+    }
     return;
   }
   it -= a.n_lw;
@@ -1988,11 +2064,13 @@ __device__ __forceinline__ void dpotrf_step(const PotrfStepArgs& a, double* pool
       double mw = 0.0, ml = 0.0;
       const double* Ld = blkA(row, row);
       for (int e = threadIdx.x; e < 4096; e += 256) {
+        const int rr = e & 63, cc = e >> 6;  // element (rr, cc) of the diagonal block
         const double v = iDr[e];
-        Wd[(size_t)(e >> 6) * ldw + (e & 63)] = v;
+        // packed panel tile: the strict upper part holds L(row, row)^T
+        Wd[(size_t)cc * ldw + rr] = (a.pack && rr < cc) ? Ld[(size_t)rr * lda + cc] : v;
         if (a.est) {
           mw = fmax(mw, fabs(v));
-          if ((e & 63) >= (e >> 6)) ml = fmax(ml, fabs(Ld[(size_t)(e >> 6) * lda + (e & 63)]));  // L(row, row), lower
+          if (rr >= cc) ml = fmax(ml, fabs(Ld[(size_t)cc * lda + rr]));  // L(row, row), lower
         }
       }
       if (a.est) {
@@ -2178,6 +2256,7 @@ void launch_potrf_steps(const PotrfDesc& p, hipStream_t stream, double* ws) {
   }
   a.stamp = (g_potrf_stamp_mode ? 1 : 0) | (spread ? 2 : 0);
   a.claim = t_launch_claim >= 1;
+  a.pack = p.pack_w && p.W_out ? 1 : 0;
   a.est = nullptr;
   a.est_host = nullptr;
   if (p.W_out && est_acquire(p.W_out, &a.est, &a.est_host)) g_est_stats[0].fetch_add(1, std::memory_order_relaxed);
@@ -2214,10 +2293,28 @@ void launch_potrf_steps(const PotrfDesc& p, hipStream_t stream, double* ws) {
   launch(nb - 1);
 }
 
+// Workspace of a TRSM-W batch: estimate slots (2 doubles per descriptor), the
+// unpacked W of every distinct packed panel tile, then the copies of the B
+// tiles (reused chunk after chunk).
+struct TrsmWLayout {
+  size_t slots = 0, unpack = 0, copies = 0;
+};
+static size_t al256(size_t b) { return (b + 255) / 256 * 256; }
+static TrsmWLayout trsm_w_layout(const TrsmGemmDesc* d, int n) {
+  TrsmWLayout l;
+  l.slots = al256((size_t)n * 2 * sizeof(double));
+  std::vector<const double*> seen;
+  for (int i = 0; i < n; ++i) {
+    l.copies += al256((size_t)d[i].m * d[i].n * sizeof(double));
+    if (!d[i].packed || std::find(seen.begin(), seen.end(), d[i].W) != seen.end()) continue;
+    seen.push_back(d[i].W);
+    l.unpack += al256((size_t)d[i].n * d[i].n * sizeof(double));
+  }
+  return l;
+}
 size_t trsm_w_workspace_bytes(const TrsmGemmDesc* d, int n) {
-  size_t b = 0;
-  for (int i = 0; i < n; ++i) b += ((size_t)d[i].m * d[i].n * sizeof(double) + 255) / 256 * 256;
-  return b;
+  const TrsmWLayout l = trsm_w_layout(d, n);
+  return l.slots + l.unpack + l.copies;
 }
 
 // B := B W^T for every descriptor: copy the B tiles into the workspace, then one
@@ -2227,31 +2324,53 @@ size_t trsm_w_workspace_bytes(const TrsmGemmDesc* d, int n) {
 //  * auto, estimate published by the local POTRF (est_lookup): the panels above
 //    the limit by substitution, the others through W -- decided here, no gate;
 //  * auto, estimate unknown (W from another process): the copy kernel estimates
-//    each W's conditioning (max|L| * max|W|) into W's spare slots, the GEMM skips
+//    each W's conditioning (max|L| * max|W|) into workspace slots, the GEMM skips
 //    the panels above the limit and the in-place gated substitution kernel behind
 //    it solves exactly those.
+// A packed panel tile (TrsmGemmDesc::packed: W below and on the diagonal, L^T
+// above -- the one tile POTRF sends) is unpacked into the workspace by the first
+// copy launch: the GEMM reads W from there, the substitution reads L from the
+// tile's upper part and its diagonal blocks from the unpacked W.
 static const bool g_trsm_tri = !getenv("PARSEC_TRSM_TRI") || atoi(getenv("PARSEC_TRSM_TRI")) != 0;
 static bool trsm_substitutable(const TrsmGemmDesc& t) {
   // the substitution kernel keeps a panel of n columns in LDS
   return t.L && t.ldl > 0 && t.n <= kTrsmMaxCols && t.n % 64 == 0 && t.ldw >= t.n;
 }
-static bool trsm_gateable(const TrsmGemmDesc& t) {
-  // the estimate slots sit at W(0..1, n-1): outside every k range the
-  // triangular (b_upper) GEMM reads only for n >= 256
-  return trsm_substitutable(t) && t.n >= 256 && g_trsm_tri;
-}
-static TrsmDesc subst_desc(const TrsmGemmDesc& t, bool gate) {
-  TrsmDesc x{};
-  x.L = t.L; x.ldl = t.ldl; x.B = t.B; x.ldb = t.ldb; x.m = t.m; x.n = t.n; x.trans = 1;
-  x.invD = t.W; x.invD_ld = t.ldw; x.gate = gate ? 1 : 0;
-  return x;
-}
+static bool trsm_gateable(const TrsmGemmDesc& t) { return trsm_substitutable(t); }
 void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, double* ws) {
   const int mode = parsec::trsm_inverse_mode(-1, 0.0);
   const double limit = parsec::trsm_inverse_limit();
+  const TrsmWLayout lay = trsm_w_layout(d, n);
+  char* const base = reinterpret_cast<char*>(ws);
+  auto* slots = reinterpret_cast<unsigned long long*>(base);
+  char* up_next = base + lay.slots;
+  char* const copies = base + lay.slots + lay.unpack;
+  // distinct W tiles of the batch: unpacked copy (packed tiles), gate slot
+  struct WInfo {
+    const double* W;
+    const double* Wu;  // what the GEMM / substitution read as W
+    int ldu;
+    unsigned long long* slot = nullptr;
+    bool unpack = false;
+  };
+  std::vector<WInfo> wi;
+  auto info_of = [&](const TrsmGemmDesc& t) -> WInfo& {
+    for (WInfo& w : wi)
+      if (w.W == t.W) return w;
+    WInfo w{t.W, t.W, t.ldw};
+    if (t.packed) {
+      w.Wu = reinterpret_cast<const double*>(up_next);
+      w.ldu = t.n;
+      w.unpack = true;
+      up_next += al256((size_t)t.n * t.n * sizeof(double));
+    }
+    wi.push_back(w);
+    return wi.back();
+  };
   std::vector<TrsmDesc> subst;          // solved by substitution, decided on the host
   std::vector<TrsmGemmDesc> via_w;      // through W
   std::vector<uint8_t> gated;           // ... with the device-side gate
+  std::vector<int> slot_of;             // via_w index -> wi index
   for (int i = 0; i < n; ++i) {
     const TrsmGemmDesc& t = d[i];
     int route = 0;  // 0 W, 1 substitution, 2 W gated on the device
@@ -2267,12 +2386,61 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
         g_est_stats[2].fetch_add(1, std::memory_order_relaxed);
       }
     }
+    WInfo& w = info_of(t);
+    if (route == 2 && !w.slot) w.slot = slots + 2 * (&w - wi.data());
+    const int wix = (int)(&w - wi.data());
     if (route == 1) {
-      subst.push_back(subst_desc(t, false));
+      TrsmDesc x{};
+      x.L = t.L; x.ldl = t.ldl; x.B = t.B; x.ldb = t.ldb; x.m = t.m; x.n = t.n; x.trans = 1;
+      x.invD = w.Wu; x.invD_ld = w.ldu; x.packed = t.packed;
+      subst.push_back(x);
     } else {
       via_w.push_back(t);
       gated.push_back(route == 2);
+      slot_of.push_back(wix);
     }
+  }
+  // estimate slots start from zero (the scan jobs max into them)
+  int nslots = 0;
+  for (const WInfo& w : wi) nslots += w.slot ? 1 : 0;
+  if (nslots) (void)hipMemsetAsync(slots, 0, wi.size() * 2 * sizeof(unsigned long long), stream);
+  // scan / unpack jobs ride the first copy launch (extra launches beyond kMaxScan)
+  std::vector<int> pend_scan, pend_unpack;
+  for (int j = 0; j < (int)wi.size(); ++j) {
+    if (wi[j].slot) pend_scan.push_back(j);
+    if (wi[j].unpack) pend_unpack.push_back(j);
+  }
+  auto add_jobs = [&](CopyBatchArgs& ca, int& maxc) {
+    ca.nscan = 0;
+    ca.nunpack = 0;
+    while (!pend_scan.empty() && ca.nscan < kMaxScan) {
+      const WInfo& w = wi[pend_scan.back()];
+      // the descriptor data of this W (any descriptor naming it)
+      const TrsmGemmDesc* t = nullptr;
+      for (int i = 0; i < n && !t; ++i) if (d[i].W == w.W) t = &d[i];
+      const int j = ca.nscan++;
+      ca.scan_n[j] = t->n; ca.scan_ldl[j] = t->ldl; ca.scan_ldw[j] = t->ldw; ca.scan_packed[j] = t->packed;
+      ca.scan_L[j] = t->L; ca.scan_W[j] = t->W; ca.scan_slot[j] = w.slot;
+      maxc = std::max(maxc, t->n);
+      pend_scan.pop_back();
+    }
+    while (!pend_unpack.empty() && ca.nunpack < kMaxScan) {
+      const WInfo& w = wi[pend_unpack.back()];
+      const TrsmGemmDesc* t = nullptr;
+      for (int i = 0; i < n && !t; ++i) if (d[i].W == w.W) t = &d[i];
+      const int j = ca.nunpack++;
+      ca.up_n[j] = t->n; ca.up_ld[j] = t->ldw; ca.up_src[j] = t->W; ca.up_dst[j] = const_cast<double*>(w.Wu);
+      maxc = std::max(maxc, t->n);
+      pend_unpack.pop_back();
+    }
+  };
+  while (pend_scan.size() > (size_t)kMaxScan || pend_unpack.size() > (size_t)kMaxScan || (via_w.empty() && (!pend_scan.empty() || !pend_unpack.empty()))) {
+    CopyBatchArgs ca;
+    ca.count = 0;
+    ca.prio = t_launch_prio;
+    int maxc = 1;
+    add_jobs(ca, maxc);
+    hipLaunchKernelGGL(copy_tiles_kernel, dim3(std::min(256, (maxc + 3) / 4), ca.nscan + ca.nunpack), dim3(256), 0, stream, ca);
   }
   for (size_t s0 = 0; s0 < via_w.size(); s0 += kMaxCopyBatch) {
     const int cnt = (int)std::min<size_t>(kMaxCopyBatch, via_w.size() - s0);
@@ -2280,38 +2448,36 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
     CopyBatchArgs ca;
     ca.count = cnt;
     ca.prio = t_launch_prio;
-    ca.nscan = 0;
     std::vector<GemmDesc> g(cnt);
-    char* p = reinterpret_cast<char*>(ws);
+    char* p = copies;
     int maxc = 1;
+    add_jobs(ca, maxc);
     for (int i = 0; i < cnt; ++i) {
       const TrsmGemmDesc& t = via_w[s0 + i];
+      const WInfo& w = wi[slot_of[s0 + i]];
       ca.rows[i] = t.m; ca.cols[i] = t.n; ca.ld_src[i] = t.ldb; ca.ld_dst[i] = t.m;
       ca.src[i] = t.B; ca.dst[i] = reinterpret_cast<double*>(p);
       maxc = std::max(maxc, t.n);
       GemmDesc& e = g[i];
-      e.A = ca.dst[i]; e.B = t.W; e.C = t.B;
+      e.A = ca.dst[i]; e.B = w.Wu; e.C = t.B;
       e.m = t.m; e.n = t.n; e.k = t.n;
-      e.lda = t.m; e.ldb = t.ldw; e.ldc = t.ldb;
+      e.lda = t.m; e.ldb = w.ldu; e.ldc = t.ldb;
       e.alpha = 1.0; e.beta = 0.0; e.transA = 0; e.transB = 1; e.lower_only = 0; e.a_lower = 0;  // copy x (L^-1)^T
       e.b_upper = g_trsm_tri ? 1 : 0;  // (L^-1)^T is upper triangular: output column block j needs k < (j+1) BN only
       e.gate = 0;
       if (gated[s0 + i]) {
-        int j = 0;
-        while (j < ca.nscan && ca.scan_W[j] != t.W) ++j;
-        if (j == ca.nscan && ca.nscan < kMaxScan) {
-          ca.scan_n[j] = t.n; ca.scan_ldl[j] = t.ldl; ca.scan_ldw[j] = t.ldw;
-          ca.scan_L[j] = t.L; ca.scan_W[j] = const_cast<double*>(t.W);
-          ++ca.nscan;
-        }
-        if (j < ca.nscan) {
-          e.gate = 1;
-          fb.push_back(subst_desc(t, true));
-        }
+        e.gate = 1;
+        e.Cin = reinterpret_cast<const double*>(w.slot);  // the estimate slots (beta 0: never read as C)
+        TrsmDesc x{};
+        x.L = t.L; x.ldl = t.ldl; x.B = t.B; x.ldb = t.ldb; x.m = t.m; x.n = t.n; x.trans = 1;
+        x.invD = w.Wu; x.invD_ld = w.ldu; x.packed = t.packed;
+        x.gate = 1;
+        x.gate_slot = reinterpret_cast<const double*>(w.slot);
+        fb.push_back(x);
       }
-      p += ((size_t)t.m * t.n * sizeof(double) + 255) / 256 * 256;
+      p += al256((size_t)t.m * t.n * sizeof(double));
     }
-    hipLaunchKernelGGL(copy_tiles_kernel, dim3(std::min(256, (maxc + 3) / 4), cnt + ca.nscan), dim3(256), 0, stream, ca);
+    hipLaunchKernelGGL(copy_tiles_kernel, dim3(std::min(256, (maxc + 3) / 4), cnt + ca.nscan + ca.nunpack), dim3(256), 0, stream, ca);
     launch_gemm_batch(g.data(), cnt, stream);
     if (!fb.empty()) {
       std::vector<const double*> inv(fb.size());
@@ -2567,10 +2733,11 @@ int parsec_amd_dpotrf_tile(double* A, int n, int lda, int* info, void* stream) {
   return (int)hipGetLastError();
 }
 // Tile Cholesky that also writes W = L^-1 (ld ldw)
-int parsec_amd_dpotrf_tile_w(double* A, int n, int lda, int* info, double* W, int ldw, void* stream) {
+int parsec_amd_dpotrf_tile_w(double* A, int n, int lda, int* info, double* W, int ldw, void* stream, int pack) {
   parsec::PotrfDesc p{A, n, lda, info};
   p.W_out = W;
   p.ldw = ldw;
+  p.pack_w = pack ? 1 : 0;
   if (parsec::kern::potrf_steps_eligible(p)) {
     void* ws = test_ws(parsec::kern::potrf_steps_workspace_bytes(p) + 64);
     parsec::kern::launch_potrf_steps(p, (hipStream_t)stream, static_cast<double*>(ws));

@@ -30,8 +30,8 @@ extern "C" int parsec_amd_potrf_steps(int on);
 extern "C" int parsec_amd_potrf_stamps(long long* out);
 extern "C" int parsec_amd_dtrsm_batch(const TrsmDesc* descs, int n, void* stream);
 extern "C" int parsec_amd_dpotrf_tile(double* A, int n, int lda, int* info, void* stream);
-extern "C" int parsec_amd_dpotrf_tile_w(double* A, int n, int lda, int* info, double* W, int ldw, void* stream);
 extern "C" int parsec_amd_trsm_w_batch(const parsec::TrsmGemmDesc* d, int n, void* stream);
+extern "C" int parsec_amd_dpotrf_tile_w(double* A, int n, int lda, int* info, double* W, int ldw, void* stream, int pack);
 extern "C" int parsec_amd_qr_panel(const parsec::QrPanelDesc* d, int n, void* stream);
 extern "C" int parsec_amd_qr_profile(unsigned long long* out);
 extern "C" int parsec_amd_qr_apply(const parsec::QrApplyDesc* d, int n, void* ws, void* stream);
@@ -725,12 +725,23 @@ PYBIND11_MODULE(_C, m) {
     return parsec_amd_qr_apply(&q, 1, (void*)ws, (void*)stream);
   });
   m.def("kernel_dpotrf", [](uintptr_t A, int n, int lda, uintptr_t info, uintptr_t stream) { return parsec_amd_dpotrf_tile((double*)A, n, lda, (int*)info, (void*)stream); });
-  m.def("kernel_dpotrf_w", [](uintptr_t A, int n, int lda, uintptr_t info, uintptr_t W, int ldw, uintptr_t stream) {
-    return parsec_amd_dpotrf_tile_w((double*)A, n, lda, (int*)info, (double*)W, ldw, (void*)stream);
-  });
-  m.def("kernel_trsm_w_batch", [](std::vector<std::tuple<uintptr_t, uintptr_t, int, int, int, int>> ds, uintptr_t stream) {
+  m.def("kernel_dpotrf_w", [](uintptr_t A, int n, int lda, uintptr_t info, uintptr_t W, int ldw, uintptr_t stream, bool pack) {
+    return parsec_amd_dpotrf_tile_w((double*)A, n, lda, (int*)info, (double*)W, ldw, (void*)stream, pack ? 1 : 0);
+  }, py::arg("A"), py::arg("n"), py::arg("lda"), py::arg("info"), py::arg("W"), py::arg("ldw"), py::arg("stream"), py::arg("pack") = false,
+     "Tile POTRF writing W = L^-1 (pack: W's strict upper triangle holds L^T, the packed panel tile)");
+  // descriptors (B, W, m, n, ldb, ldw[, packed]): packed W = the packed panel
+  // tile, which also provides L for the substitution routes
+  m.def("kernel_trsm_w_batch", [](std::vector<py::tuple> ds, uintptr_t stream) {
     std::vector<TrsmGemmDesc> v;
-    for (auto& d : ds) v.push_back(TrsmGemmDesc{(double*)std::get<0>(d), (const double*)std::get<1>(d), std::get<2>(d), std::get<3>(d), std::get<4>(d), std::get<5>(d)});
+    for (auto& d : ds) {
+      TrsmGemmDesc t{(double*)d[0].cast<uintptr_t>(), (const double*)d[1].cast<uintptr_t>(), d[2].cast<int>(), d[3].cast<int>(), d[4].cast<int>(), d[5].cast<int>()};
+      if (d.size() > 6 && d[6].cast<bool>()) {
+        t.packed = 1;
+        t.L = t.W;
+        t.ldl = t.ldw;
+      }
+      v.push_back(t);
+    }
     return parsec_amd_trsm_w_batch(v.data(), (int)v.size(), (void*)stream);
   });
 

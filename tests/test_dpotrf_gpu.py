@@ -151,14 +151,15 @@ def test_trsm_inverse_modes_gpu(pa, nb):
     (mode 1). Auto decides per panel from max|L| max|W|: by default the tile
     POTRF publishes it to pinned host memory and the TRSM launch picks the
     route on the host (no gated kernel); with trsm_estimate_route(0) the copy
-    kernel estimates into W's spare slots, the W-GEMM skips and the in-place
-    gated substitution kernel solves above the limit. On an SPD matrix with
-    cond 1e12 (numerics sweep: profiles/r4_trsm_inverse_numerics.txt) every mode
-    is backward stable; auto with its default limit takes the inverse path (same
-    factor as mode 0) and auto with limit 1 takes the substitution path (same
-    factor as mode 2), through either estimate route -- below nb 256 through
-    the host route only (W has no spare slots for the device gate there: a W
-    factored by another process takes the inverse path unguarded)."""
+    kernel estimates into workspace slots, the W-GEMM skips and the in-place
+    gated substitution kernel solves above the limit. The panel tile is the
+    packed one POTRF sends (W below, L(k,k)^T above the diagonal): the W-GEMM
+    reads W unpacked in the workspace, the substitution reads L from the tile.
+    On an SPD matrix with cond 1e12 (numerics sweep:
+    profiles/r4_trsm_inverse_numerics.txt) every mode is backward stable; auto
+    with its default limit takes the inverse path (same factor as mode 0) and
+    auto with limit 1 takes the substitution path (same factor as mode 2),
+    through either estimate route, at every tile size."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     N = 2048
@@ -184,7 +185,7 @@ def test_trsm_inverse_modes_gpu(pa, nb):
         pa.trsm_estimate_route(prev_route)
     published, host, device = pa.trsm_estimate_stats(True)
     assert published == 0 and host == 0
-    assert device == (2 * NT * (NT - 1) // 2 if nb >= 256 else 0)
+    assert device == 2 * NT * (NT - 1) // 2
     nS = torch.linalg.norm(S)
     for L in (L0, L1, L2, L1s, L1d, L1ds):
         assert (torch.linalg.norm(L @ L.t() - S) / nS).item() < 1e-14
@@ -192,7 +193,7 @@ def test_trsm_inverse_modes_gpu(pa, nb):
     assert d02 > 0  # the two solves differ (by ~cond(L(k,k)) eps)
     for La, Lb in ((L1, L0), (L1d, L0)):  # auto below the limit = the inverse path
         assert torch.linalg.norm(La - Lb).item() < 1e-3 * d02
-    for La, Lb in ((L1s, L2), (L1ds, L2 if nb >= 256 else L0)):  # auto above it = the substitution path
+    for La, Lb in ((L1s, L2), (L1ds, L2)):  # auto above it = the substitution path
         assert torch.linalg.norm(La - Lb).item() < 1e-3 * d02
 
 

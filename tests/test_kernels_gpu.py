@@ -133,6 +133,69 @@ def test_dpotrf_tile_inverse(pa, dev, n):
     assert torch.triu(W, 1).abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("n,steps", [(512, 1), (1024, 1), (256, 0)])
+def test_dpotrf_packed_panel_tile(pa, dev, n, steps):
+    """The packed panel tile POTRF(k) sends to its TRSMs: W = L^-1 below and on
+    the diagonal, L^T strictly above (written by the step kernel's LW / XW
+    items; by a transpose kernel on the 3-launches-per-64-columns path)."""
+    prev = pa.kernel_potrf_steps(steps)
+    try:
+        R = torch.randn((n, n), dtype=torch.float64, device=dev)
+        S = R @ R.t() + n * torch.eye(n, dtype=torch.float64, device=dev)
+        A = S.t().contiguous().t().clone()
+        W = _colmajor(n)
+        W.fill_(7.0)
+        info = torch.zeros(1, dtype=torch.int32, device=dev)
+        pa.kernel_dpotrf_w(A.data_ptr(), n, n, info.data_ptr(), W.data_ptr(), n, _stream(), pack=True)
+        torch.cuda.synchronize()
+    finally:
+        pa.kernel_potrf_steps(prev)
+    assert info.item() == 0
+    L = torch.tril(A)
+    assert ((L @ L.t() - S).norm() / S.norm()).item() < 1e-13
+    eye = torch.eye(n, dtype=torch.float64, device=dev)
+    assert (torch.tril(W) @ L - eye).abs().max().item() < 1e-12
+    assert torch.equal(torch.triu(W, 1), torch.triu(L.t(), 1))
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("n", [512, 128])
+def test_trsm_packed_panel_tile(pa, dev, mode, n):
+    """Panel solve from the packed tile alone (the one tile a panel broadcast
+    sends): through W (mode 0), by substitution with the L held in the tile's
+    upper part (mode 2), and auto with an unknown estimate -- the device gate:
+    the copy kernel estimates from the tile into workspace slots -- with the
+    limit 1 (every panel by substitution); vs torch in fp64."""
+    m, tasks = 384, 3
+    R = torch.randn((n, n), dtype=torch.float64, device=dev)
+    S = R @ R.t() + n * torch.eye(n, dtype=torch.float64, device=dev)
+    A = S.t().contiguous().t().clone()
+    P = _colmajor(n)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+    pa.kernel_dpotrf_w(A.data_ptr(), n, n, info.data_ptr(), P.data_ptr(), n, _stream(), pack=True)
+    torch.cuda.synchronize()
+    L = torch.tril(A)
+    Bs = [_colmajor(m, n) for _ in range(tasks)]
+    refs = []
+    for B in Bs:
+        B.copy_(torch.randn((m, n), dtype=torch.float64, device=dev))
+        refs.append(torch.linalg.solve_triangular(L, B.t(), upper=False).t())
+    prev_limit = pa.trsm_inverse_limit()
+    prev = pa.trsm_inverse_mode(mode, 1.0 if mode == 1 else 0.0)
+    prev_route = pa.trsm_estimate_route(0)
+    pa.trsm_estimate_stats(True)
+    try:
+        pa.kernel_trsm_w_batch([(B.data_ptr(), P.data_ptr(), m, n, m, n, True) for B in Bs], _stream())
+        torch.cuda.synchronize()
+    finally:
+        pa.trsm_inverse_mode(prev, prev_limit)
+        pa.trsm_estimate_route(prev_route)
+    _, _, gated = pa.trsm_estimate_stats(True)
+    assert gated == (tasks if mode == 1 else 0)
+    for B, ref in zip(Bs, refs):
+        assert ((B - ref).abs().max() / ref.abs().max()).item() < 1e-12
+
+
 @pytest.mark.parametrize("m,n,tasks", [(1024, 1024, 3), (512, 512, 5), (300, 200, 2)])
 def test_trsm_through_inverse(pa, dev, m, n, tasks):
     """Panel solve B := B L^-T as copy + grouped GEMM with W = L^-1 (the
