@@ -89,7 +89,11 @@ def bench_qr(args):
     storeT = torch.zeros((ln, lm, nb, nb), dtype=torch.float64, device="cuda")
     A = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=Q, device=gpu, ptr=storeA.data_ptr())
     T = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=Q, device=gpu, ptr=storeT.data_ptr())
-    hqr = args.qr_tree == "hqr"
+    # auto: one process row -> the flat TS tree from the ptgpp-compiled
+    # dgeqrf.jdf (what the hierarchical tree reduces to there); several process
+    # rows -> the hierarchical tree (TT merges across the rows)
+    hqr = args.qr_tree == "hqr" or (args.qr_tree == "auto" and P > 1)
+    use_jdf = not hqr and args.taskpool == "jdf"
     if hqr:  # TT-kernel reflectors of the hierarchical tree
         storeTT = torch.zeros((ln, lm, nb, nb), dtype=torch.float64, device="cuda")
         TT = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, N, N, P=P, Q=Q, device=gpu, ptr=storeTT.data_ptr())
@@ -101,7 +105,7 @@ def bench_qr(args):
         storeA.copy_(backup)
         storeT.zero_()
         torch.cuda.synchronize()
-        tp = pa.dgeqrf_hqr_new(A, T, TT, args.qr_domain) if hqr else pa.dgeqrf_new(A, T, args.ib)
+        tp = pa.dgeqrf_hqr_new(A, T, TT, args.qr_domain) if hqr else pa.dgeqrf_jdf_new(A, T) if use_jdf else pa.dgeqrf_new(A, T, args.ib)
         ctx.add_taskpool(tp)
         ctx.start()
         ctx.wait()
@@ -169,7 +173,7 @@ def bench_qr(args):
         pa.comm_fini()
     out = {"metric": "GFLOP/s tiled DGEQRF (PTG, HBM-resident)", "value": round(4.0 / 3.0 * N ** 3 / dt / 1e9, 1), "unit": "GFLOP/s",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
-           "dtype": "fp64", "data": "synthetic uniform(-0.5, 0.5)", "config": {"model": "tiled DGEQRF (" + ((f"hierarchical, TS domains of {args.qr_domain}" if args.qr_domain > 0 else "hierarchical, flat TS per process row") + ", TT binary trees" if hqr else "flat TS tree") + ")", "N": N, "nb": nb, "ib": 32,
+           "dtype": "fp64", "data": "synthetic uniform(-0.5, 0.5)", "config": {"model": "tiled DGEQRF (" + ((f"hierarchical, TS domains of {args.qr_domain}" if args.qr_domain > 0 else "hierarchical, flat TS per process row") + ", TT binary trees" if hqr else "flat TS tree") + (", ptgpp-compiled dgeqrf.jdf" if use_jdf else ", hand-built C++ DAG") + ")", "N": N, "nb": nb, "ib": 32,
                                                                              "parallelism": f"2D block-cyclic P{P}xQ{Q}" if Q > 1 else f"1D row-cyclic P{P}x1"}}
     if check is not None:
         out["residual_AtAx_vs_RtRx"] = check
@@ -251,7 +255,8 @@ def main():
     ap.add_argument("--qr-grid", choices=["1d", "2d"], default="2d", help="qr: process grid over the ranks")
     ap.add_argument("--share-gpu", action="store_true", help="qr / stencil: validation mode, every rank on GPU 0; not a scaling measurement")
     ap.add_argument("--check", action="store_true", help="qr: verify R (||A^T A x - R^T R x|| / (||A||_F^2 ||x||), all ranks) after the timed steps")
-    ap.add_argument("--qr-tree", choices=["hqr", "flat"], default="hqr", help="qr: hierarchical (TS domains + TT trees) or flat TS tree")
+    ap.add_argument("--qr-tree", choices=["auto", "hqr", "flat"], default="auto", help="qr: hierarchical (TS domains + TT trees), flat TS tree, or auto (flat on one process row, hierarchical otherwise)")
+    ap.add_argument("--taskpool", choices=["jdf", "ir"], default="jdf", help="qr flat tree: the ptgpp-compiled dgeqrf.jdf (default) or the hand-built C++ DAG (dgeqrf.cpp)")
     ap.add_argument("--qr-domain", type=int, default=0,
                     help="qr: rows per TS domain of the hierarchical tree (0: one flat TS chain per process row, TT binary tree across process rows; 1 GPU measured fastest flat: profiles/r3_qr_tree_ab.jsonl)")
     args = ap.parse_args()

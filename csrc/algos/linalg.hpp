@@ -21,6 +21,9 @@ ptg::PtgTaskpool* dgemm_new(double alpha, TiledMatrix* A, TiledMatrix* B, double
 // Tiled QR A = QR (Householder, tile algorithm GEQRT/TSQRT/UNMQR/TSMQR). T holds
 // the block reflectors (ib x nb per tile).
 ptg::PtgTaskpool* dgeqrf_new(TiledMatrix* A, TiledMatrix* T, int ib);
+// The same factorization from the JDF source algos/jdf/dgeqrf.jdf, compiled by
+// parsec-ptgpp at build time (the benchmark's taskpool).
+ptg::PtgTaskpool* dgeqrf_jdf_new(TiledMatrix* A, TiledMatrix* T);
 // Hierarchical QR (dgeqrf_hqr.cpp): TS domains of `domain` rows per process row
 // (<= 0: all of them, i.e. flat inside a process row),
 // TT binary trees over domain heads and across the p_rows process rows (<= 0:

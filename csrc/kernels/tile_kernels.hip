@@ -2256,7 +2256,10 @@ void launch_potrf_steps(const PotrfDesc& p, hipStream_t stream, double* ws) {
   }
   a.stamp = (g_potrf_stamp_mode ? 1 : 0) | (spread ? 2 : 0);
   a.claim = t_launch_claim >= 1;
-  a.pack = p.pack_w && p.W_out ? 1 : 0;
+  // PARSEC_POTRF_PACK=0 (measurement only): skip the L^T half of the packed
+  // tile -- the substitution routes would then read garbage
+  static const bool pack_env = !getenv("PARSEC_POTRF_PACK") || atoi(getenv("PARSEC_POTRF_PACK")) != 0;
+  a.pack = p.pack_w && p.W_out && pack_env ? 1 : 0;
   a.est = nullptr;
   a.est_host = nullptr;
   if (p.W_out && est_acquire(p.W_out, &a.est, &a.est_host)) g_est_stats[0].fetch_add(1, std::memory_order_relaxed);

@@ -498,6 +498,8 @@ PYBIND11_MODULE(_C, m) {
         tp->destructor_hook = [info, prev]() { if (prev) prev(); delete info; };
         return py::make_tuple(py::cast(tp, py::return_value_policy::take_ownership), (uintptr_t)info);
       }, "tiled Cholesky (lower) from the ptgpp-compiled algos/jdf/dpotrf_L.jdf; returns (taskpool, info address)");
+  m.def("dgeqrf_jdf_new", [](TiledMatrix* A, TiledMatrix* T) { return algos::dgeqrf_jdf_new(A, T); }, py::arg("A"), py::arg("T"),
+        py::return_value_policy::take_ownership, "Tiled QR from the ptgpp-compiled dgeqrf.jdf (GEQRT / TSQRT / UNMQR / TSMQR)");
   m.def("dgeqrf_new", [](TiledMatrix* A, TiledMatrix* T, int ib) { return algos::dgeqrf_new(A, T, ib); }, py::arg("A"), py::arg("T"), py::arg("ib") = 0,
         py::return_value_policy::take_ownership);
   m.def("dgeqrf_hqr_new", [](TiledMatrix* A, TiledMatrix* T, TiledMatrix* TT, int domain, int p_rows) { return algos::dgeqrf_hqr_new(A, T, TT, domain, p_rows); },

@@ -53,6 +53,7 @@ CORE_SOURCES = [
     "csrc/capi/capi.cpp",
     "csrc/capi/hash_table.cpp", "csrc/capi/object.cpp", "csrc/capi/future_c.cpp",
     "csrc/algos/dpotrf_jdf.cpp",
+    "csrc/algos/dgeqrf_jdf.cpp",
     "csrc/algos/redistribute_ptg.cpp",
 ]
 HIP_SOURCES = [
@@ -66,12 +67,13 @@ PTGPP_SOURCES = ["tools/ptgpp/ptgpp.cpp"]
 # and linked into the runtime library (reference: DPLASMA ships its *.jdf the same way)
 JDF_SOURCES = [
     "csrc/algos/jdf/dpotrf_L.jdf",
+    "csrc/algos/jdf/dgeqrf.jdf",
     "csrc/algos/jdf/redistribute.jdf",
     "csrc/algos/jdf/redistribute_reshuffle.jdf",
     "csrc/algos/jdf/diag_band_to_rect.jdf",
 ]
 # runtime sources that include generated JDF headers
-JDF_USERS = ["csrc/algos/dpotrf_jdf.cpp", "csrc/algos/redistribute_ptg.cpp"]
+JDF_USERS = ["csrc/algos/dpotrf_jdf.cpp", "csrc/algos/dgeqrf_jdf.cpp", "csrc/algos/redistribute_ptg.cpp"]
 FORTRAN_SOURCES = ["csrc/fortran/parsecf.F90", "csrc/fortran/parsec_profilef.F90"]
 FLANG = os.path.join(ROCM, "lib", "llvm", "bin", "flang")
 TEST_SOURCES = ["tests/native/test_containers.cpp", "tests/native/test_futures.cpp", "tests/native/test_fetch_queue.cpp"]

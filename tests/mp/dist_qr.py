@@ -30,7 +30,7 @@ def main():
         TT = pa.BlockCyclic(pa.MATRIX_DOUBLE, rank, nb, nb, M, N, P=P, Q=Q)
         tp = pa.dgeqrf_hqr_new(A, T, TT, int(sys.argv[10]))
     else:
-        tp = pa.dgeqrf_new(A, T, 32)
+        tp = (pa.dgeqrf_jdf_new(A, T) if os.environ.get("QR_TASKPOOL", "jdf") == "jdf" else pa.dgeqrf_new(A, T, 32))
     ctx.add_taskpool(tp)
     ctx.start()
     ctx.wait()

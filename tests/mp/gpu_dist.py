@@ -129,7 +129,7 @@ def case_dgeqrf(pa, torch, rank, size, job, N, nb, P, outdir, Q=1, dom=0):
         torch.cuda.synchronize()
         if size > 1:
             pa.comm_barrier()
-        tp = pa.dgeqrf_hqr_new(A, T, TT, dom) if dom > 0 else pa.dgeqrf_new(A, T, 32)
+        tp = pa.dgeqrf_hqr_new(A, T, TT, dom) if dom > 0 else (pa.dgeqrf_jdf_new(A, T) if os.environ.get("QR_TASKPOOL", "jdf") == "jdf" else pa.dgeqrf_new(A, T, 32))
         ctx.add_taskpool(tp)
         ctx.start()
         ctx.wait()

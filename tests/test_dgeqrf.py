@@ -1,11 +1,13 @@
-"""Tiled Householder QR (DGEQRF PTG taskpool): R^T R == A^T A on square, tall,
+"""Tiled Householder QR (DGEQRF PTG taskpools): R^T R == A^T A on square, tall,
 wide and ragged matrices, CPU bodies and (gpu) HIP bodies; distributed over
-2 ranks on CPU. Reference workload: BASELINE.json config 4 (DPLASMA dgeqrf)."""
+2 ranks on CPU. Both taskpools run: the ptgpp-compiled dgeqrf.jdf (the
+benchmark's) and the hand-built C++ IR (dgeqrf.cpp, same DAG). Reference
+workload: BASELINE.json config 4 (DPLASMA dgeqrf)."""
 import numpy as np
 import pytest
 
 
-def _run_qr(pa, M, N, nb, cores=4, gpu=False, seed=0, domain=None):
+def _run_qr(pa, M, N, nb, cores=4, gpu=False, seed=0, domain=None, taskpool="jdf"):
     ctx = pa.init(cores)
     dev = pa.first_gpu_device_index() if gpu else 0
     if gpu and dev < 0:
@@ -18,7 +20,7 @@ def _run_qr(pa, M, N, nb, cores=4, gpu=False, seed=0, domain=None):
             blk = S[m * nb:(m + 1) * nb, n * nb:(n + 1) * nb]
             A.tile(m, n)[:blk.shape[0], :blk.shape[1]] = blk
     if domain is None:
-        tp = pa.dgeqrf_new(A, T, 32)
+        tp = pa.dgeqrf_jdf_new(A, T) if taskpool == "jdf" else pa.dgeqrf_new(A, T, 32)
     else:  # hierarchical tree: TS domains of `domain` rows, TT binary trees
         TT = pa.BlockCyclic(pa.MATRIX_DOUBLE, 0, nb, nb, M, N)
         tp = pa.dgeqrf_hqr_new(A, T, TT, domain)
@@ -38,15 +40,17 @@ def _run_qr(pa, M, N, nb, cores=4, gpu=False, seed=0, domain=None):
     return np.linalg.norm(R.T @ R - G) / np.linalg.norm(G)
 
 
+@pytest.mark.parametrize("taskpool", ["jdf", "ir"])
 @pytest.mark.parametrize("M,N,nb", [(64, 64, 16), (80, 48, 16), (48, 80, 16), (70, 50, 16), (50, 70, 16), (96, 96, 32)])
-def test_dgeqrf_cpu(pa, M, N, nb):
-    assert _run_qr(pa, M, N, nb) < 1e-13
+def test_dgeqrf_cpu(pa, M, N, nb, taskpool):
+    assert _run_qr(pa, M, N, nb, taskpool=taskpool) < 1e-13
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("taskpool", ["jdf", "ir"])
 @pytest.mark.parametrize("M,N,nb", [(1024, 1024, 256), (1280, 768, 256), (1000, 1000, 256), (2048, 2048, 512)])
-def test_dgeqrf_gpu(pa, M, N, nb):
-    assert _run_qr(pa, M, N, nb, gpu=True) < 1e-12
+def test_dgeqrf_gpu(pa, M, N, nb, taskpool):
+    assert _run_qr(pa, M, N, nb, gpu=True, taskpool=taskpool) < 1e-12
 
 
 @pytest.mark.parametrize("M,N,nb,domain", [(64, 64, 16, 1), (64, 64, 16, 2), (160, 96, 16, 3), (70, 50, 16, 2), (50, 70, 16, 2), (256, 128, 16, 4)])

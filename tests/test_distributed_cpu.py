@@ -110,13 +110,15 @@ def test_launcher_kills_survivors_on_failure():
     assert time.monotonic() - t0 < 20
 
 
+@pytest.mark.parametrize("taskpool", ["jdf", "ir"])
 @pytest.mark.parametrize("nranks,P,Q,M,N", [(2, 2, 1, 96, 96), (3, 3, 1, 112, 80), (4, 2, 2, 96, 128)])
-def test_distributed_dgeqrf(pa, tmp_path, nranks, P, Q, M, N):
-    """QR over P x Q ranks: the TS chains write R(k,k) / A(k,n) from remote ranks,
-    so the final versions must travel back to the owning rank."""
+def test_distributed_dgeqrf(pa, tmp_path, nranks, P, Q, M, N, taskpool):
+    """QR over P x Q ranks (the ptgpp-compiled dgeqrf.jdf and the hand-built IR):
+    the TS chains write R(k,k) / A(k,n) from remote ranks, so the final versions
+    must travel back to the owning rank."""
     import numpy as np
 
-    outs = run_ranks(nranks, M, N, 16, P, Q, str(tmp_path), worker=os.path.join(HERE, "mp", "dist_qr.py"))
+    outs = run_ranks(nranks, M, N, 16, P, Q, str(tmp_path), worker=os.path.join(HERE, "mp", "dist_qr.py"), env_extra={"QR_TASKPOOL": taskpool})
     for rc, out in outs:
         assert rc == 0, out
     R = sum(np.load(tmp_path / f"R{r}.npy") for r in range(nranks))
