@@ -29,6 +29,9 @@
 // after the runtime headers: the C API defines PASSED_BY_REF & co. as macros
 #include "../../include/parsec.h"
 
+namespace parsec {
+bool& comm_owned_by_mpi();  // mpi_shim.cpp
+}
 using namespace parsec;
 
 namespace {
@@ -503,7 +506,9 @@ parsec_context_t* parsec_init(int nb_cores, int* pargc, char** pargv[]) {
 int parsec_fini(parsec_context_t** pcontext) {
   if (pcontext && *pcontext == g_capi_ctx) g_capi_ctx = nullptr;
   int rc = context_fini(pcontext);
-  if (comm_size() > 1) comm_fini();
+  // an engine the program brought up through MPI_Init (include/mpi/mpi.h)
+  // lives until MPI_Finalize, like the application's MPI under PaRSEC
+  if (comm_size() > 1 && !comm_owned_by_mpi()) comm_fini();
   return rc;
 }
 void parsec_abort(parsec_context_t* context, int status) { context_abort(context, status); }
@@ -879,6 +884,7 @@ void parsec_matrix_block_cyclic_init(parsec_matrix_block_cyclic_t* dc, parsec_ma
   t->i = i; t->j = j; t->m = (int)bc->m; t->n = (int)bc->n; t->mt = (int)bc->mt; t->nt = (int)bc->nt;
   t->llm = (int)(bc->llm_tiles * mb); t->lln = (int)(bc->lln_tiles * nb);
   t->nb_local_tiles = (int)bc->nb_local_tiles;
+  t->dtype = parsec_matrix_type | parsec_matrix_block_cyclic_type;
   parsec_grid_2Dcyclic_init(&dc->grid, myrank, p, q, kp, kq, ip, jq);
 }
 // ---- the other tiled collections of the reference's C API
@@ -956,6 +962,7 @@ void parsec_matrix_sym_block_cyclic_init(parsec_matrix_sym_block_cyclic_t* dc, p
   sc->init_sym((int)mtype, myrank, mb, nb, lm, ln, i, j, m, n, p, q, uplo == PARSEC_MATRIX_UPPER ? MATRIX_UPPER : MATRIX_LOWER);
   set_c_callbacks(&dc->super.super, sc, 2);
   fill_tiled(&dc->super, sc, mtype, sc->llm_tiles * mb, sc->lln_tiles * nb);
+  dc->super.dtype = parsec_matrix_type | parsec_matrix_sym_block_cyclic_type;
   dc->uplo = uplo;
   parsec_grid_2Dcyclic_init(&dc->grid, myrank, p, q, 1, 1, 0, 0);
 }
@@ -973,6 +980,7 @@ static void tabular_refresh(parsec_matrix_tabular_t* dc) {
   for (int k = 0; dc->tiles_table && k < dc->tiles_table->nbelem; ++k) dc->tiles_table->elems[k].pos = tc->local_map.size() > (size_t)k && tc->local_map[k] >= 0 ? pos++ : -1;
   tc->publish();
   fill_tiled(&dc->super, tc, dc->super.mtype, 0, 0);
+  dc->super.dtype = parsec_matrix_type | parsec_matrix_tabular_type;
 }
 void parsec_matrix_tabular_init(parsec_matrix_tabular_t* dc, parsec_matrix_type_t mtype, unsigned int nodes, unsigned int myrank, unsigned int mb, unsigned int nb,
                                 unsigned int lm, unsigned int ln, unsigned int i, unsigned int j, unsigned int m, unsigned int n,

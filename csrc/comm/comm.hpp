@@ -28,7 +28,7 @@ namespace parsec {
 enum CommTag : int {
   TAG_GET_INTERNAL = 0, TAG_PUT_INTERNAL = 1, TAG_REMOTE_DEP_ACTIVATE = 2, TAG_GET_DATA = 3, TAG_PUT_END = 4,
   TAG_TERMDET_FOURCOUNTER = 5, TAG_TERMDET_USER_TRIGGER = 6, TAG_DATA_FRAGMENT = 7, TAG_BARRIER = 8, TAG_ALLREDUCE = 9,
-  TAG_AGGREGATE = 12,
+  TAG_AGGREGATE = 12, TAG_MPI_SHIM = 13,
   TAG_USER = 16, TAG_MAX = 32,
 };
 

@@ -1828,7 +1828,7 @@ struct PotrfStepArgs {
   int j;            // step (-1: first launch, nb - 1: last launch)
   int pack;         // packed panel tile: W's strict upper triangle receives L^T (PotrfDesc::pack_w)
   // item ranges: [0, n_diag) DIAG, then TRAIL, RUPD, LW, XW, ZERO
-  int n_diag, n_trail, n_rupd, n_lw, n_xw, n_zero;
+  int n_diag, n_trail, n_rupd, n_lw, n_xw, n_zero, n_pack;
   // auto panel solve (optional): the items that finalize blocks of L and W fold
   // their max |.| into est[0] / est[1] (bit patterns), the last launch counts its
   // workgroups in est[2] and the last one publishes max|L| max|W| to est_host
@@ -2045,7 +2045,7 @@ __device__ __forceinline__ void dpotrf_step(const PotrfStepArgs& a, double* pool
     __syncthreads();  // every wave has read S0 (a copy of the block being overwritten)
     acc_store(acc, blkA(r, p), lda, false);
     if (a.est) est_fold(a.est, 0, acc_absmax(acc));  // L(r, p) is final
-    if (a.pack) {  // packed panel tile: L(r, p)^T into W's upper block (p, r)
+    if (a.pack && j == nb - 1) {  // packed panel tile: the last panel's L(r, p)^T into W's upper block (p, r)
       acc_to_blk(acc, S0, false);
       __syncthreads();
       blk_store_t(S0, blkW(p, r), ldw);
@@ -2095,6 +2095,21 @@ __device__ __forceinline__ void dpotrf_step(const PotrfStepArgs& a, double* pool
     const size_t nn = (size_t)64 * nb;
     for (size_t c = (size_t)it; c < nn; c += (size_t)a.n_zero)
       for (size_t r = threadIdx.x * 2; r < nn; r += 512) *reinterpret_cast<double2_t*>(a.W + c * ldw + r) = (double2_t){0.0, 0.0};
+    return;
+  }
+  it -= a.n_zero;
+  // ---------------------------------------------------------------- PACK
+  // last launch of a packed panel tile: the L blocks final before it (panels
+  // 0 .. nb - 3) go transposed into W's upper blocks, beside the launch's own
+  // work -- off the step launches of the critical path (the last panel's block
+  // is written by its LW item, the diagonal blocks by the XW items)
+  if (it < a.n_pack) {
+    int p = 0, rem = it;
+    while (rem >= nb - 1 - p) { rem -= nb - 1 - p; ++p; }
+    const int r = p + 1 + rem;
+    stage_blk(S0, blkA(r, p), lda, false);
+    __syncthreads();
+    blk_store_t(S0, blkW(p, r), ldw);
   }
 }
 
@@ -2288,7 +2303,9 @@ void launch_potrf_steps(const PotrfDesc& p, hipStream_t stream, double* ws) {
     if (j == nb - 1 && nb == 1) {  // a single block: X row 0 only
       a.n_lw = 0;
     }
-    const int grid = a.n_diag + a.n_trail + a.n_rupd + a.n_lw + a.n_xw + a.n_zero;
+    // packed tile: blocks (r, p), p <= nb - 3, r > p, in the last launch
+    a.n_pack = (a.pack && j == nb - 1 && nb >= 3) ? (nb - 2) * (nb - 1) - (nb - 3) * (nb - 2) / 2 : 0;
+    const int grid = a.n_diag + a.n_trail + a.n_rupd + a.n_lw + a.n_xw + a.n_zero + a.n_pack;
     if (grid > 0) hipLaunchKernelGGL(dpotrf_step_kernel, dim3(grid), dim3(256), 0, stream, a);
   };
   launch(-1);

@@ -16,6 +16,12 @@
  */
 #ifndef PARSEC_AMD_PARSEC_H
 #define PARSEC_AMD_PARSEC_H
+/* Programs built with -DPARSEC_HAVE_MPI (and -I include/mpi: the minimal MPI
+ * over this runtime's engine) see MPI through the runtime header, as the
+ * reference's parsec.h gives it to them. */
+#if defined(PARSEC_HAVE_MPI)
+#include <mpi.h>
+#endif
 
 #include <assert.h>
 #include <inttypes.h>
@@ -493,7 +499,10 @@ typedef struct parsec_tiled_matrix_s {
   int i, j, m, n, mt, nt;  /* submatrix */
   int llm, lln;            /* local rows / columns */
   int nb_local_tiles;
+  int dtype;               /* distribution type: parsec_matrix_*_type bits (set by the init functions) */
 } parsec_tiled_matrix_t;
+/* distribution-type bits of parsec_tiled_matrix_t::dtype (reference matrix.h) */
+enum { parsec_matrix_type = 0x01, parsec_matrix_block_cyclic_type = 0x02, parsec_matrix_sym_block_cyclic_type = 0x04, parsec_matrix_tabular_type = 0x08 };
 
 typedef struct parsec_grid_2Dcyclic_s {
   int rank, rows, cols, krows, kcols, ip, jq, rrank, crank;

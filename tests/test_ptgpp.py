@@ -10,6 +10,7 @@ import pytest
 from parsec_amd import ptgpp
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
 JDF = os.path.join(HERE, "jdf")
 
 pytestmark = pytest.mark.skipif(not os.path.exists(ptgpp.PTGPP), reason="parsec-ptgpp not built")
@@ -275,15 +276,20 @@ _REJECT = {
 # against MPI, not against the public API: the reason of each
 _NO_COMPILE = {
     "parsec/data_dist/matrix/broadcast.jdf": "builds a collection with the internal object system (PARSEC_OBJ_NEW, parsec_data_t fields); public form: parsec_broadcast_New",
-    "parsec/data_dist/matrix/diag_band_to_rect.jdf": "includes parsec/parsec_internal.h",
-    "tests/collections/redistribute/redistribute_bound.jdf": "MPI calls outside PARSEC_HAVE_MPI guards, context->virtual_processes",
-    "tests/collections/redistribute/redistribute_check.jdf": "MPI calls outside PARSEC_HAVE_MPI guards",
-    "tests/collections/redistribute/redistribute_check2.jdf": "MPI calls outside PARSEC_HAVE_MPI guards",
-    "tests/collections/redistribute/redistribute_no_optimization.jdf": "MPI calls outside PARSEC_HAVE_MPI guards",
     "tests/dsl/ptg/choice/choice2.jdf": "reads task->parsec_object (object system internals)",
     "tests/dsl/ptg/ptgpp/too_many_local_vars.jdf": "includes a compiler-check header of the reference build tree",
-    "tests/dsl/ptg/ptgpp/write_check.jdf": "MPI_Reduce outside PARSEC_HAVE_MPI guards",
-    "tests/runtime/multichain.jdf": "MPI communicators, tp->super.nb_tasks of the C taskpool layout",
+    "tests/runtime/multichain.jdf": "tp->super.nb_tasks printed as an int (an atomic counter here); runs the DAG on MPI sub-communicators (parsec_remote_dep_set_ctx)",
+}
+# JDFs whose C code calls MPI outside PARSEC_HAVE_MPI guards (the reference
+# builds every test with MPI): compiled with the minimal MPI of include/mpi
+# (csrc/capi/mpi_shim.cpp over this runtime's engine)
+MPI_FLAGS = [f"-I{os.path.join(ROOT, 'include', 'mpi')}", "-DPARSEC_HAVE_MPI"]
+_MPI_JDFS = {
+    "tests/collections/redistribute/redistribute_bound.jdf",
+    "tests/collections/redistribute/redistribute_check.jdf",
+    "tests/collections/redistribute/redistribute_check2.jdf",
+    "tests/collections/redistribute/redistribute_no_optimization.jdf",
+    "tests/dsl/ptg/ptgpp/write_check.jdf",
 }
 
 
@@ -320,7 +326,7 @@ def test_reference_jdf_corpus(tmp_path):
             return None
         if r.returncode != 0:
             return f"{rel}: {r.stderr[-400:]}"
-        r = subprocess.run(cc + ["-fpermissive", "-Drestrict=__restrict__", f"-I{out}", f"-I{os.path.dirname(os.path.join(REF, rel))}", f"-I{REF}", "-c",
+        r = subprocess.run(cc + (MPI_FLAGS if rel in _MPI_JDFS else []) + ["-fpermissive", "-Drestrict=__restrict__", f"-I{out}", f"-I{os.path.dirname(os.path.join(REF, rel))}", f"-I{REF}", "-c",
                                  str(out / (base + ".cpp")), "-o", str(out / (base + ".o"))], capture_output=True, text=True, timeout=300)
         if rel in _NO_COMPILE:
             return None if r.returncode != 0 else f"{rel}: compiles now, remove it from _NO_COMPILE"
@@ -630,6 +636,51 @@ def test_reference_dtd_programs_unmodified(tmp_path, name):
     assert r.returncode == 0, r.stderr[-3000:]
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=dict(os.environ, PARSEC_MCA_device_hip_enabled="0"))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("name,nranks,expect", [("pingpong", 2, "Pingpong is behaving correctly"), ("task_placement", 2, "Task placed in"),
+                                                ("interleave_actions", 2, "recv_data_kernel"), ("explicit_task_creation", 1, None)])
+def test_reference_mpi_dtd_programs_unmodified(tmp_path, name, nranks, expect):
+    """The reference's DTD programs that need MPI (dtd_test_<name>.c with
+    tests/tests_data.c, unmodified), built with -DPARSEC_HAVE_MPI against the
+    minimal MPI of include/mpi (MPI_Init_thread, communicator queries, barrier
+    and reductions over this runtime's engine) and started as `nranks` processes
+    by parsec_amd.launch, mpiexec-style; each checks itself."""
+    from parsec_amd import launch
+
+    cc, libs = ptgpp.compile_flags(False)
+    exe = str(tmp_path / name)
+    src = os.path.join(REF, "tests/dsl/dtd", f"dtd_test_{name}.c")
+    r = subprocess.run(cc + list(ptgpp.C_BODIES) + MPI_FLAGS + [f"-I{REF}/tests", f"-I{REF}", f"-I{REF}/tests/dsl/dtd", "-x", "c++", src,
+                                                              os.path.join(REF, "tests/tests_data.c"), "-o", exe] + libs, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rc, outs = launch.launch(nranks, [exe], timeout=240, capture=True, env={"PARSEC_MCA_device_hip_enabled": "0"})
+    text = "".join(o + e for o, e in outs)
+    assert rc == 0, text[-3000:]
+    if expect:
+        assert expect in text, text[-2000:]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("nranks", [1, 2, 4])
+def test_reference_write_check_mpi(tmp_path, nranks):
+    """tests/dsl/ptg/ptgpp/write_check.jdf + vector.c, unmodified, with MPI
+    (its result check is an MPI_Reduce MAXLOC outside the MPI guards), on 1, 2
+    and 4 processes (reference Testings.cmake: write_check and write_check:mp
+    with 4 ranks)."""
+    from parsec_amd import launch
+
+    wc = os.path.join(REF, "tests/dsl/ptg/ptgpp")
+    cpp, _ = ptgpp.compile_jdf(os.path.join(wc, "write_check.jdf"), str(tmp_path))
+    cc, libs = ptgpp.compile_flags(False)
+    exe = str(tmp_path / "write_check")
+    r = subprocess.run(cc + list(ptgpp.C_BODIES) + MPI_FLAGS + [f"-I{tmp_path}", f"-I{wc}", cpp, "-x", "c++", os.path.join(wc, "vector.c"), "-x", "none",
+                                                              "-o", exe] + libs, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rc, outs = launch.launch(nranks, [exe], timeout=240, capture=True, env={"PARSEC_MCA_device_hip_enabled": "0"})
+    text = "".join(o + e for o, e in outs)
+    assert rc == 0 and "TEST SUCCESS" in text, text[-3000:]
 
 
 @pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
