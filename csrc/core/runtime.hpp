@@ -610,6 +610,9 @@ struct DeviceStats {
   // GPU manager thread: time (ns) spent retiring completed kernel groups
   // (epilog + dependency release) and the longest single retirement pass
   std::atomic<uint64_t> ns_complete{0}, ns_complete_max{0}, ns_launch{0};
+  // tasks that waited for stage-in copies (on the shared copy stream) and
+  // their summed wait from the first copy issued to the last one completed
+  std::atomic<uint64_t> staged_tasks{0}, ns_stage_wait{0};
 };
 
 // data_advise (reference device.c parsec_advise_data_on_device, PARSEC_DEV_DATA_ADVICE_*)

@@ -1453,7 +1453,7 @@ bool HipDevice::progress() {
     for (GpuTask* g : pending) {
       int rc = stage_in(g);
       if (rc == 0) ready.push_back(g);
-      else if (rc == 1) staging.push_back(g);
+      else if (rc == 1) { g->t_stage = now_ns(); staging.push_back(g); }
       else keep.push_back(g);
     }
     pending.swap(keep);
@@ -1464,6 +1464,10 @@ bool HipDevice::progress() {
     std::vector<GpuTask*> keep;
     for (GpuTask* g : staging) {
       if (g->ev_in && hipEventQuery(g->ev_in) == hipErrorNotReady) { keep.push_back(g); continue; }
+      if (g->t_stage) {
+        stats.ns_stage_wait.fetch_add(now_ns() - g->t_stage, std::memory_order_relaxed);
+        stats.staged_tasks.fetch_add(1, std::memory_order_relaxed);
+      }
       finish_stage_in(g);
       ready.push_back(g);
       did = true;

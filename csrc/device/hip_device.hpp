@@ -64,7 +64,7 @@ struct GpuTask {
   hipEvent_t ev_out = nullptr;
   int stream = -1;
   double load = 0;
-  uint64_t t_submit = 0, t_exec = 0;
+  uint64_t t_submit = 0, t_exec = 0, t_stage = 0;
   // early release: the task was completed (successors released) when its group
   // was launched; the group's retirement only unpins its copies
   bool early = false;

@@ -640,6 +640,8 @@ PYBIND11_MODULE(_C, m) {
       e["data_faults"] = d->stats.data_faults.load();
       e["w2r_tasks"] = d->stats.w2r_tasks.load();
       e["prefetches"] = d->stats.prefetches.load();
+      e["staged_tasks"] = d->stats.staged_tasks.load();
+      e["ms_stage_wait"] = d->stats.ns_stage_wait.load() / 1e6;
       out.append(e);
     }
     return out;

@@ -15,12 +15,14 @@ reference dplasma zpotrf_L.jdf) on a model of the machine:
     critical stream, profiles/r4_chain*.txt);
   * a tile produced on rank r and read by tasks on rank s != r crosses the
     (r, s) xGMI link ONCE (the runtime's per-rank activation aggregation), after
-    a per-message latency. Round 5 (what the code does): every rank pulls its
-    inbound tiles through ONE serial receive queue (csrc/comm/fetch_queue.hpp:
-    priority ordered by the consuming task's priority, one copy-engine pull
-    stream between distinct GPUs), so all of a rank's inbound transfers run one
-    after another (`--recv per-link` restores the round-4 assumption of one
-    transfer at a time per directed link);
+    a per-message latency. Round 6 (what the code does, `--recv lanes`): every
+    rank queues its inbound pulls per SOURCE rank (csrc/comm/fetch_queue.hpp
+    lanes, priority ordered by the consuming task's priority) and issues them in
+    multi-source gather launches on its one copy stream (shm_engine.cpp
+    flush_gather): a launch moves the head tile of every source with work at
+    once, one per xGMI link, and the next launch follows it. `--recv serial` is
+    round 5 (one pull at a time per rank), `--recv per-link` round 4 (one
+    transfer at a time per directed link, no wave synchronization);
   * the panel chain's TRSM(k+1, k) / SYRK(k, k+1) run on the critical stream
     with a measured latency (`--trsm-us`: the critical 64x64 grouped TRSM
     W-GEMM averages 265 us under load at config 3, profiles/r5_kernel_stats_c3_v1.csv).
@@ -120,10 +122,22 @@ def simulate(NT, nb, P, Q, gemm_tf, potrf_us, link_gbs, lat_us, syrk_eff=0.85, t
         return cost["POTRF"] if kind == "POTRF" else trsm_us if kind == "TRSM" else cost["SYRK"]
 
     recv_q = [[] for _ in range(R)]  # serial receive: (-prio, seq, key)
+    lane_q = [{} for _ in range(R)]  # lanes: source rank -> [(-prio, seq, key)]
     recv_busy = [False] * R
+    max_wave = [0] * R
 
     def recv_kick(r, at):
-        if recv_busy[r] or not recv_q[r]:
+        if recv_busy[r]:
+            return
+        if recv == "lanes":
+            wave = [heapq.heappop(q)[2] for q in lane_q[r].values() if q]
+            if not wave:
+                return
+            recv_busy[r] = True
+            max_wave[r] = max(max_wave[r], len(wave))
+            heapq.heappush(ev, (at + xfer_us - lat_us, next(seq), "wave", (r, wave)))
+            return
+        if not recv_q[r]:
             return
         _, _, key = heapq.heappop(recv_q[r])
         recv_busy[r] = True
@@ -184,7 +198,7 @@ def simulate(NT, nb, P, Q, gemm_tf, potrf_us, link_gbs, lat_us, syrk_eff=0.85, t
                 arrived[key] = None
                 waiting[key] = [s]
                 bytes_sent += nb * nb * 8
-                if recv == "serial":
+                if recv in ("serial", "lanes"):
                     # the activation reaches the receiver after the message
                     # latency; its pull then queues behind the rank's other pulls
                     heapq.heappush(ev, (now + lat_us, next(seq), "request", (key, tasks[s][2])))
@@ -195,8 +209,19 @@ def simulate(NT, nb, P, Q, gemm_tf, potrf_us, link_gbs, lat_us, syrk_eff=0.85, t
             kick(rank, now)
         elif kind == "request":
             key, prio = p
-            heapq.heappush(recv_q[key[1]], (-prio, next(seq), key))
+            if recv == "lanes":
+                heapq.heappush(lane_q[key[1]].setdefault(tasks[key[0]][0], []), (-prio, next(seq), key))
+            else:
+                heapq.heappush(recv_q[key[1]], (-prio, next(seq), key))
             recv_kick(key[1], now)
+        elif kind == "wave":
+            r, wave = p
+            recv_busy[r] = False
+            for key in wave:
+                arrived[key] = now
+                for s in waiting.pop(key):
+                    satisfy(s, now)
+            recv_kick(r, now)
         elif kind == "arrive":
             arrived[p] = now
             if recv == "serial":
@@ -208,7 +233,7 @@ def simulate(NT, nb, P, Q, gemm_tf, potrf_us, link_gbs, lat_us, syrk_eff=0.85, t
     n = NT * nb
     flops = n ** 3 / 3.0
     return {"ranks": R, "grid": f"P{P}xQ{Q}", "span_ms": finish / 1e3, "tflops": flops / (finish * 1e-6) / 1e12,
-            "bulk_util": sum(busy_us) / (R * finish), "xgmi_GB": bytes_sent / 1e9}
+            "bulk_util": sum(busy_us) / (R * finish), "xgmi_GB": bytes_sent / 1e9, "max_wave": max(max_wave)}
 
 
 def critical_path_exact_ns(NT, costs_ns):
@@ -256,7 +281,7 @@ def main():
     ap.add_argument("--lat-us", type=float, default=25.0, help="per-message latency (activation + pull setup)")
     ap.add_argument("--ranks", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--measured-1gpu-tf", type=float, default=None)
-    ap.add_argument("--recv", choices=["serial", "per-link"], default="serial", help="inbound transfers: one serial queue per rank (the code) or one per directed link (round 4)")
+    ap.add_argument("--recv", choices=["lanes", "serial", "per-link"], default="lanes", help="inbound transfers: per-source lanes in gather waves (the code, round 6), one serial queue per rank (round 5) or one per directed link (round 4)")
     ap.add_argument("--trsm-us", type=float, default=265.0, help="TRSM(k+1,k) latency on the critical stream (us); <0: in the bulk at the GEMM rate")
     a = ap.parse_args()
     NT = a.n // a.nb
@@ -265,7 +290,7 @@ def main():
           f"tile POTRF {a.potrf_us} us, TRSM(k+1,k) {a.trsm_us} us, message latency {a.lat_us} us, receive {a.recv}")
     for bw in a.link_gbs:
         print(f"-- xGMI effective {bw} GB/s per directed peer link")
-        print(f"{'ranks':>5} {'grid':>6} {'span ms':>9} {'TF (job)':>9} {'TF/GPU':>7} {'eff':>5} {'bulk util':>9} {'xGMI GB':>8} {'chain ms':>8}")
+        print(f"{'ranks':>5} {'grid':>6} {'span ms':>9} {'TF (job)':>9} {'TF/GPU':>7} {'eff':>5} {'bulk util':>9} {'xGMI GB':>8} {'chain ms':>8} {'max wave':>8}")
         base = None
         for r in a.ranks:
             P, Q = grid_of(r)
@@ -274,7 +299,7 @@ def main():
             eff = out["tflops"] / (base * r)
             g_us = 2.0 * a.nb ** 3 / (a.gemm_tf * 1e12) * 1e6
             chain = critical_path_us(NT, a.potrf_us, trsm if trsm is not None else g_us, g_us / 2 / 0.85, a.nb * a.nb * 8 / (bw * 1e9) * 1e6 + a.lat_us, P, Q) / 1e3
-            print(f"{r:>5} {out['grid']:>6} {out['span_ms']:>9.1f} {out['tflops']:>9.1f} {out['tflops'] / r:>7.1f} {eff:>5.2f} {out['bulk_util']:>9.2f} {out['xgmi_GB']:>8.1f} {chain:>8.1f}")
+            print(f"{r:>5} {out['grid']:>6} {out['span_ms']:>9.1f} {out['tflops']:>9.1f} {out['tflops'] / r:>7.1f} {eff:>5.2f} {out['bulk_util']:>9.2f} {out['xgmi_GB']:>8.1f} {chain:>8.1f} {out['max_wave']:>8}")
     if a.measured_1gpu_tf:
         P, Q = grid_of(1)
         one = simulate(NT, a.nb, P, Q, a.gemm_tf, a.potrf_us, a.link_gbs[0], a.lat_us, recv=a.recv, trsm_us=trsm)

@@ -87,3 +87,23 @@ def test_serial_receive_queue():
         assert ser["span_ms"] * 1e3 >= chain * 0.999
         per_rank_tiles = ser["xgmi_GB"] * 1e9 / (nb * nb * 8) / r
         assert ser["span_ms"] * 1e3 >= per_rank_tiles * xfer_us * 0.999
+
+
+def test_receive_lanes():
+    """Round 6: per-source receive lanes issued in multi-source gather waves
+    (one tile per source link per wave, the code's fetch-queue lanes and
+    flush_gather): same bytes as the other receive models, several sources in
+    one wave at 4+ ranks, never slower than one serial receive queue, and the
+    receive bound becomes a per-link one."""
+    NT, nb = 16, 1024
+    xfer_us = nb * nb * 8 / 50e9 * 1e6
+    for r in (2, 4, 8):
+        P, Q = sm.grid_of(r)
+        ser = sm.simulate(NT, nb, P, Q, gemm_tf=66.0, potrf_us=350.0, link_gbs=50.0, lat_us=25.0, recv="serial", trsm_us=265.0)
+        lan = sm.simulate(NT, nb, P, Q, gemm_tf=66.0, potrf_us=350.0, link_gbs=50.0, lat_us=25.0, recv="lanes", trsm_us=265.0)
+        assert lan["xgmi_GB"] == ser["xgmi_GB"]
+        assert lan["span_ms"] <= ser["span_ms"] * 1.001
+        chain = sm.critical_path_us(NT, 350.0, 265.0, nb ** 3 / 66e12 * 1e6 / 0.85, xfer_us + 25.0, P, Q)
+        assert lan["span_ms"] * 1e3 >= chain * 0.999
+        if r >= 4:
+            assert lan["max_wave"] >= 2
