@@ -1037,6 +1037,12 @@ static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) 
     // three LDS k-tile buffers (110 KB), only with PARSEC_GEMM_DLDS=1: two k-tiles of DMA in
     // flight; measured 15 % slower than variant 0 (profiles/r5_gemm_direct_lds.txt)
     case 12: launch_gemm_shape<128, 128, 16, 2, 4, 3>(a, descs, n, stream); break;
+    // 256 x 128 macro tiles, 8 waves of 64 x 64 (16 accumulators each, up to 256
+    // VGPRs + AGPRs: one workgroup per CU): a quarter fewer L2 -> LDS bytes per
+    // flop and twice the MFMA work between barriers; BK 16 (106 KB of LDS) or 8
+    // (53 KB). No room for a co-resident critical-path workgroup.
+    case 13: launch_gemm_shape<256, 128, 16, 4, 2, 2, 2>(a, descs, n, stream); break;
+    case 14: launch_gemm_shape<256, 128, 8, 4, 2, 2, 2>(a, descs, n, stream); break;
     // default: 8 waves (2 x 4) of 64x32 per 128x128 tile, 126 VGPRs -> 4 waves per
     // SIMD with two workgroups per CU (measured: DPOTRF 64k +4 %, 16k +7 % over
     // the 4-wave 64x64-per-wave kernel = variant 8; profiles/r1_gemm_variants_v8.log;

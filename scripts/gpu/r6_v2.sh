@@ -34,3 +34,10 @@ for spec in "evict;16384 512 0.25" "fit;16384 512 2.0" "two;16384 512 0.0 2"; do
   rm -rf $O/p_$name
   cat $O/${name}_occupancy.txt 2>/dev/null | head -12
 done
+# 256 x 128 GEMM macro tiles: kernel rate, then config 3
+O=gpurun_out/r6gemm; mkdir -p $O
+for v in 0 13 14; do
+  PARSEC_GEMM_PAD_TEST=1 PARSEC_GEMM_VARIANT=$v timeout -k 10 200 python3 scripts/kbench_gemm.py > $O/k$v.txt 2>&1 || { echo "kbench $v failed"; tail -5 $O/k$v.txt; exit 1; }
+  cat $O/k$v.txt
+done
+AB_TAG=r6_gemm bash scripts/gpu/bench_ab.sh "c3v0;;--steps 3 --warmup 1" "c3v13;PARSEC_GEMM_VARIANT=13;--steps 3 --warmup 1" "c3v14;PARSEC_GEMM_VARIANT=14;--steps 3 --warmup 1" || exit 1
