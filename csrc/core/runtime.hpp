@@ -613,6 +613,10 @@ struct DeviceStats {
   // tasks that waited for stage-in copies (on the shared copy stream) and
   // their summed wait from the first copy issued to the last one completed
   std::atomic<uint64_t> staged_tasks{0}, ns_stage_wait{0};
+  // copy stream, from the engine's timed copy spans (profiling on): busy time
+  // (in-order stream: the spans do not overlap), first start / last end (ns
+  // since the device's reference event), copies timed
+  std::atomic<uint64_t> ns_copy_busy{0}, ns_copy_first{0}, ns_copy_last{0}, copies_timed{0};
 };
 
 // data_advise (reference device.c parsec_advise_data_on_device, PARSEC_DEV_DATA_ADVICE_*)

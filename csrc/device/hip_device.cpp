@@ -503,6 +503,11 @@ void HipDevice::progress_copy_spans() {
       const uint64_t id = (uint64_t)(uintptr_t)c.e;
       profiling_trace_at(trace_copy_stream, c.key, id, 0, trace_ref_ns + (uint64_t)((double)tb * 1e6), &info, sizeof(info));
       profiling_trace_at(trace_copy_stream, c.key + 1, id, 0, trace_ref_ns + (uint64_t)((double)te * 1e6), nullptr, 0);
+      const uint64_t b = (uint64_t)((double)tb * 1e6), e = (uint64_t)((double)te * 1e6);
+      if (e > b) stats.ns_copy_busy.fetch_add(e - b, std::memory_order_relaxed);
+      if (!stats.copies_timed.load(std::memory_order_relaxed) || b < stats.ns_copy_first.load(std::memory_order_relaxed)) stats.ns_copy_first.store(b, std::memory_order_relaxed);
+      if (e > stats.ns_copy_last.load(std::memory_order_relaxed)) stats.ns_copy_last.store(e, std::memory_order_relaxed);
+      stats.copies_timed.fetch_add(1, std::memory_order_relaxed);
     } else {
       (void)hipGetLastError();
     }

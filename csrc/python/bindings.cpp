@@ -642,6 +642,9 @@ PYBIND11_MODULE(_C, m) {
       e["prefetches"] = d->stats.prefetches.load();
       e["staged_tasks"] = d->stats.staged_tasks.load();
       e["ms_stage_wait"] = d->stats.ns_stage_wait.load() / 1e6;
+      e["copies_timed"] = d->stats.copies_timed.load();
+      e["ms_copy_busy"] = d->stats.ns_copy_busy.load() / 1e6;
+      e["ms_copy_window"] = (d->stats.ns_copy_last.load() - d->stats.ns_copy_first.load()) / 1e6;
       out.append(e);
     }
     return out;

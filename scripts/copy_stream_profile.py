@@ -28,6 +28,10 @@ def main():
 
     pa.require_native()
     pa.mca_set("device_hip_memory_max", str(int(frac * N * N * 8)))
+    # the engine times every copy it issues on the copy stream when profiling is
+    # on (GPU_MOVEIN / MOVEOUT / PREFETCH spans): busy time and window below
+    trace = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"copyprof{os.getpid()}")
+    pa.mca_set("profile_filename", trace)
     if reps > 1:
         pa.mca_set("device_hip_replicas", str(reps))
     ctx = pa.init(4)
@@ -53,11 +57,18 @@ def main():
     ctx.fini()
     X = rng.random((N, 4)) - 0.5
     res = np.linalg.norm(S @ X - np.tril(L) @ (np.tril(L).T @ X)) / (np.linalg.norm(S) * np.linalg.norm(X))
-    tot = {k: sum(g[k] for g in gpus) for k in ("executed_tasks", "bytes_in", "bytes_out", "bytes_d2d", "data_faults", "w2r_tasks", "staged_tasks", "ms_stage_wait")}
+    tot = {k: sum(g[k] for g in gpus) for k in ("executed_tasks", "bytes_in", "bytes_out", "bytes_d2d", "data_faults", "w2r_tasks", "staged_tasks", "ms_stage_wait",
+                                                 "copies_timed", "ms_copy_busy")}
+    window = max(g["ms_copy_window"] for g in gpus)
     print(f"copy-stream N={N} nb={nb} cache={frac:.2f} devices={len(gpus)} info={pa.read_int(info)} residual={res:.2e} span_ms={dt * 1e3:.1f} "
           f"GF={N ** 3 / 3 / dt / 1e9:.0f} tasks={tot['executed_tasks']} in_MiB={tot['bytes_in'] >> 20} out_MiB={tot['bytes_out'] >> 20} "
           f"d2d_MiB={tot['bytes_d2d'] >> 20} faults={tot['data_faults']} w2r={tot['w2r_tasks']} staged_tasks={tot['staged_tasks']} "
-          f"stage_wait_ms_sum={tot['ms_stage_wait']:.1f} stage_wait_ms_per_task={tot['ms_stage_wait'] / max(1, tot['staged_tasks']):.3f}", flush=True)
+          f"stage_wait_ms_sum={tot['ms_stage_wait']:.1f} stage_wait_ms_per_task={tot['ms_stage_wait'] / max(1, tot['staged_tasks']):.3f} "
+          f"copies_timed={tot['copies_timed']} copy_busy_ms={tot['ms_copy_busy']:.1f} copy_window_ms={window:.1f} "
+          f"copy_occupancy={tot['ms_copy_busy'] / max(window, 1e-9) / max(1, len(gpus)):.2f} copy_GBps={(tot['bytes_in'] + tot['bytes_out'] + tot['bytes_d2d']) / max(tot['ms_copy_busy'], 1e-9) / 1e6:.1f}", flush=True)
+    for f in os.listdir(os.path.dirname(trace)):
+        if f.startswith(os.path.basename(trace)):
+            os.unlink(os.path.join(os.path.dirname(trace), f))
     sys.exit(0 if pa.read_int(info) == 0 and res < 1e-12 else 1)
 
 
