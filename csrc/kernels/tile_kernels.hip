@@ -2641,10 +2641,10 @@ __global__ __launch_bounds__(256) void gather_kernel(const GatherArgs a) {
 
 int device_gather_kernel(void* const* dst, const void* const* src, const size_t* bytes, int n, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  for (int b = 0; b < n; b += kMaxGather) {
+  for (int i = 0; i < n;) {
     GatherArgs a{};
     int wg = 0;
-    for (int i = b; i < n && a.count < kMaxGather; ++i) {
+    for (; i < n && a.count < kMaxGather; ++i) {
       const bool aligned = ((uintptr_t)dst[i] % 16 == 0) && ((uintptr_t)src[i] % 16 == 0) && bytes[i] % 16 == 0;
       if (!aligned || bytes[i] == 0) {  // odd sizes / offsets: a copy kernel of its own, same stream
         if (bytes[i] && device_copy_kernel(dst[i], src[i], bytes[i], stream) != 0) return -1;
