@@ -16,6 +16,7 @@ ptg::PtgTaskpool* dpotrf_new(TiledMatrix* A, int uplo, int* info_host);
 // The same factorization from the JDF source algos/jdf/dpotrf_L.jdf, compiled by
 // parsec-ptgpp at build time (lower only, W = L^-1 panel solves).
 ptg::PtgTaskpool* dpotrf_jdf_new(TiledMatrix* A, int* info_host);
+int dpotrf_fuse_syrk(int set);  // SYRK(k-1,k) fused into POTRF(k) in new dpotrf_L.jdf taskpools; set < 0 queries
 // Tiled GEMM C = alpha op(A) op(B) + beta C (PTG; B transposed if transB).
 ptg::PtgTaskpool* dgemm_new(double alpha, TiledMatrix* A, TiledMatrix* B, double beta, TiledMatrix* C, int transB);
 // Tiled QR A = QR (Householder, tile algorithm GEQRT/TSQRT/UNMQR/TSMQR). T holds

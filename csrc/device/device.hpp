@@ -225,6 +225,7 @@ struct StencilInitDesc {
 };
 
 struct KernelBatch {
+  std::vector<GemmDesc> pre_gemm;  // launched before everything else (a POTRF's fused last update)
   std::vector<GemmDesc> gemm;
   std::vector<TrsmDesc> trsm;
   std::vector<PotrfDesc> potrf;
@@ -240,8 +241,8 @@ struct KernelBatch {
   // (kernels: g_crit_cu, bulk_yield) so the chain runs at idle speed
   int claim_cus = 0;  // 1: tile-POTRF steps claim, 2: every kernel of the launch
   bool bulk_yield = false;  // bulk launch: poll the claims
-  bool empty() const { return gemm.empty() && trsm.empty() && potrf.empty() && trsm_w.empty() && stencil.empty() && qr_panel.empty() && qr_apply.empty() && generic.empty(); }
-  void clear() { gemm.clear(); trsm.clear(); potrf.clear(); trsm_w.clear(); stencil.clear(); qr_panel.clear(); qr_apply.clear(); generic.clear(); }
+  bool empty() const { return pre_gemm.empty() && gemm.empty() && trsm.empty() && potrf.empty() && trsm_w.empty() && stencil.empty() && qr_panel.empty() && qr_apply.empty() && generic.empty(); }
+  void clear() { pre_gemm.clear(); gemm.clear(); trsm.clear(); potrf.clear(); trsm_w.clear(); stencil.clear(); qr_panel.clear(); qr_apply.clear(); generic.clear(); }
 };
 
 struct HipDevice;

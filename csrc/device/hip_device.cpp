@@ -1409,6 +1409,42 @@ void HipDevice::complete(GpuTask* g) {
   inflight.fetch_sub(1, std::memory_order_acq_rel);
 }
 
+// critical_release: a retired critical-stream group completes its critical-path
+// tasks first and launches what they made ready (the next link of the chain)
+// before it releases the successors of the group's other tasks -- a panel's
+// TRSM group releases hundreds of GEMMs, which took 50-380 us at config 2
+// (profiles/r6_chain2.txt) while SYRK(k,k+1) waited to be dispatched.
+void HipDevice::dispatch_critical_now() {
+  if (incoming_n.load(std::memory_order_acquire) == 0) return;
+  std::vector<GpuTask*> in;
+  {
+    std::lock_guard<std::mutex> lk(in_m);
+    in.swap(incoming);
+    incoming_n.store(0);
+  }
+  std::vector<GpuTask*> later;
+  for (GpuTask* g : in) {
+    g->t_submit = now_ns();
+    if (g->task->priority < critical_threshold) { later.push_back(g); continue; }
+    const int rc = stage_in(g);
+    if (rc == 0) ready.push_back(g);
+    else if (rc == 1) { g->t_stage = now_ns(); staging.push_back(g); }
+    else later.push_back(g);
+  }
+  for (GpuTask* g : later) pending.push_back(g);
+  if (ready.empty()) return;
+  // launch only the critical tasks now; other ready tasks wait for the next pass
+  std::vector<GpuTask*> rest;
+  std::vector<GpuTask*> crit;
+  for (GpuTask* g : ready) (g->task->priority >= critical_threshold ? crit : rest).push_back(g);
+  if (crit.empty()) return;
+  ready.swap(crit);
+  const uint64_t t0 = now_ns();
+  execute_ready();
+  stats.ns_launch.fetch_add(now_ns() - t0, std::memory_order_relaxed);
+  for (GpuTask* g : rest) ready.push_back(g);
+}
+
 bool HipDevice::progress() {
   bool did = false;
   if (incoming_n.load(std::memory_order_acquire) > 0) {
@@ -1505,7 +1541,16 @@ bool HipDevice::progress() {
       tasks.swap(grp.tasks);
       q.pop_front();
       const uint64_t tr0 = trace_launches ? now_ns() : 0;
+      if (s == 0 && critical_release && tasks.size() > 1) {
+        // critical-path tasks first (stable: the group is priority ordered already)
+        std::stable_partition(tasks.begin(), tasks.end(), [&](GpuTask* g) { return !g->early && !g->pushout && g->task->priority >= critical_threshold; });
+      }
+      bool crit_done = !(s == 0 && critical_release);
       for (GpuTask* g : tasks) {
+        if (!crit_done && (g->early || g->pushout || g->task->priority < critical_threshold)) {
+          crit_done = true;
+          dispatch_critical_now();
+        }
         if (g->early) {
           late_complete(g, grp_ev);
           continue;
@@ -1557,9 +1602,9 @@ bool HipDevice::progress() {
       retired = true;
       // critical_split: the critical stream's successors are dispatched (next
       // pass) before the bulk streams' completions are released
-      if (s == 0 && critical_split) break;
+      if (s == 0 && (critical_split || critical_first)) break;
     }
-    if (s == 0 && retired && critical_split) break;
+    if (s == 0 && retired && (critical_split || critical_first)) break;
   }
   if (retired) {
     const uint64_t dt = now_ns() - tc0;
@@ -1655,6 +1700,8 @@ void hip_devices_init(Context* ctx) {
   const int ccap = (int)params.reg_int("device", "hip", "critical_bulk_cap", "Launched kernel groups per bulk stream while the critical stream has work in flight (0 = max_inflight_batches)", 0);
   const int cuy = (int)params.reg_int("device", "hip", "cu_yield", "Cooperative CU yield: critical-path kernels claim their CUs and bulk GEMM workgroups on a claimed CU pause until it is free (0 off, 1 tile-POTRF steps claim, 2 every kernel of a critical group claims)", 0);
   const bool csplit = params.reg_int("device", "hip", "critical_split", "Critical-path tasks leave the critical stream as a group of their own and their successors are dispatched before other completions are released", 0) != 0;
+  const bool crel = params.reg_int("device", "hip", "critical_release", "A retired critical-stream group completes its critical-path tasks first and launches their critical successors before releasing its other tasks' successors", 0) != 0;
+  const bool cfirst = params.reg_int("device", "hip", "critical_first", "A retired critical-stream group's successors are dispatched before the bulk streams' completions are released (the groups themselves are not split)", 0) != 0;
   const int early = (int)params.reg_int("device", "hip", "early_release", "Critical-stream groups release their tasks' successors when launched (1) or when their kernels completed (0); single-process runs", 0);
   if (enabled == 0) return;
   int count = 0;
@@ -1698,6 +1745,8 @@ void hip_devices_init(Context* ctx) {
     d->max_inflight_explicit = params.source(ParamRegistry::join("device", "hip", "max_inflight_batches")) != "default";
     d->critical_bulk_cap = ccap;
     d->critical_split = csplit;
+    d->critical_first = cfirst;
+    d->critical_release = crel;
     d->early_release = early;
     d->cu_yield = cuy;
     kern::set_cu_yield_mode(cuy);

@@ -215,6 +215,8 @@ struct HipDevice : Device {
   bool max_inflight_explicit = false;  // set by the user: taskpool hints do not override it
   int critical_bulk_cap = 0;    // the same limit while the critical stream has work in flight (0 = max_inflight_groups)
   bool critical_split = false;
+  bool critical_first = false;
+  bool critical_release = false;
   // device_hip_early_release: groups of the critical stream complete their
   // tasks (release successors) when launched, not when their event fires
   int early_release = 0;
@@ -241,6 +243,7 @@ struct HipDevice : Device {
   int stage_in(GpuTask* g);
   void finish_stage_in(GpuTask* g);
   void execute_ready();
+  void dispatch_critical_now();
   void complete(GpuTask* g);
   void epilog(GpuTask* g);
   void* cache_alloc(size_t bytes);

@@ -1022,7 +1022,11 @@ static void launch_gemm_chunk(const GemmDesc* descs, int n, hipStream_t stream) 
     t128 += ((descs[i].m + 127) / 128) * ((descs[i].n + 127) / 128);
     if (descs[i].m < 128 || descs[i].n < 128) big = false;
   }
-  const bool use_big = g_gemm_tile_policy == 128 || (g_gemm_tile_policy == 0 && big && t128 >= g_gemm_big_tiles);
+  // PARSEC_CRIT_TILE=64 (measurement): critical-stream groups (the chain's
+  // TRSM / SYRK / column GEMMs) on 64x64 tiles -- four times the workgroups,
+  // each a quarter of the work, spread over more CUs beside the bulk kernels
+  static const int crit_tile = getenv("PARSEC_CRIT_TILE") ? atoi(getenv("PARSEC_CRIT_TILE")) : 0;
+  const bool use_big = (g_gemm_tile_policy == 128 || (g_gemm_tile_policy == 0 && big && t128 >= g_gemm_big_tiles)) && !(crit_tile == 64 && t_launch_prio);
   if (!use_big) { launch_gemm_shape<64, 64, 16, 2, 2, 2>(a, descs, n, stream); return; }
   switch (g_gemm_variant) {
     case 6: launch_gemm_shape<128, 128, 16, 4, 2, 2>(a, descs, n, stream); break;
@@ -2569,7 +2573,8 @@ void launch_kernel_batch(KernelBatch& b, hipStream_t stream, int device_ordinal,
       kern::t_launch_yield = prev_yield;
     }
   } prio_scope(b.critical, b.one_per_cu ? 8192 : 0, b.claim_cus, b.bulk_yield);
-  // critical-path kernels first: POTRF, then TRSM, then the GEMM/SYRK updates
+  // critical-path kernels first: a POTRF's fused update, POTRF, then TRSM, then the GEMM/SYRK updates
+  if (!b.pre_gemm.empty()) kern::launch_gemm_batch(b.pre_gemm.data(), (int)b.pre_gemm.size(), stream);
   for (auto& p : b.potrf) {
     if (kern::potrf_steps_eligible(p)) kern::launch_potrf_steps(p, stream, static_cast<double*>(ws));
     else kern::launch_potrf(p, stream, static_cast<double*>(ws));

@@ -47,6 +47,7 @@ def test_distributed_dpotrf(pa, nranks, P, Q, topo, termdet):
     (2, 2, 1, {}),
     (4, 2, 2, {"PARSEC_MCA_ptg_deps_mask": "1"}),
     (3, 3, 1, {"PARSEC_MCA_ptg_dep_management": "dynamic-hash-table"}),
+    (4, 2, 2, {"PARSEC_DPOTRF_FUSE_SYRK": "1"}),  # SYRK(k-1,k) inside POTRF(k): TRSM(k,k-1) -> POTRF(k) crosses ranks
 ])
 def test_distributed_dpotrf_jdf(pa, nranks, P, Q, mode):
     """The ptgpp-compiled dpotrf_L.jdf over several ranks (remote activations

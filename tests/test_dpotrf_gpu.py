@@ -12,11 +12,15 @@ def _spd(N, dev, seed=0):
     return (R + R.t()) / 2 + N * torch.eye(N, dtype=torch.float64, device=dev)
 
 
+@pytest.mark.parametrize("fuse", [0, 1])
 @pytest.mark.parametrize("N,nb", [(1024, 256), (2048, 512), (1536, 384)])
-def test_dpotrf_hbm_resident(pa, N, nb):
+def test_dpotrf_hbm_resident(pa, N, nb, fuse):
+    """fuse = 1: POTRF(k) applies SYRK(k-1,k) itself (pre-GEMM in its launch on
+    the critical stream); the factor is checked against torch's fp64 Cholesky."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ctx = pa.init(3)
+    prev = pa.dpotrf_fuse_syrk(fuse)
     try:
         gpu = pa.first_gpu_device_index()
         NT = N // nb
@@ -32,9 +36,12 @@ def test_dpotrf_hbm_resident(pa, N, nb):
         assert pa.read_int(info) == 0
         L = torch.tril(store.permute(1, 3, 0, 2).reshape(N, N))
         assert (torch.linalg.norm(L @ L.t() - S) / torch.linalg.norm(S)).item() < 1e-13
+        Lref = torch.linalg.cholesky(S)
+        assert (torch.linalg.norm(L - Lref) / torch.linalg.norm(Lref)).item() < 1e-12
         gpus = [d for d in pa.devices() if d["type"] == pa.DEV_HIP]
         assert gpus and gpus[0]["executed_tasks"] > 0
     finally:
+        pa.dpotrf_fuse_syrk(prev)
         ctx.fini()
 
 

@@ -549,14 +549,20 @@ def test_pins_print_steals(pa):
 
 
 # ------------------------------------------------ JDF-compiled DPOTRF (CPU)
-@pytest.mark.parametrize("NT,nb", [(1, 16), (6, 16), (9, 8)])
-def test_dpotrf_jdf_cpu(pa, NT, nb):
+@pytest.mark.parametrize("fuse", [0, 1])
+@pytest.mark.parametrize("NT,nb", [(1, 16), (2, 16), (6, 16), (9, 8)])
+def test_dpotrf_jdf_cpu(pa, NT, nb, fuse):
     """algos/jdf/dpotrf_L.jdf, compiled by parsec-ptgpp into the runtime at build
-    time, factors like the hand-built IR (CPU bodies; W = L^-1 panel solves)."""
+    time, factors like the hand-built IR (CPU bodies; W = L^-1 panel solves);
+    fuse = 1: SYRK(k-1,k) applied by POTRF(k) itself (FUSE global)."""
     ctx = _ctx(pa, 4)
     N = NT * nb
     A, S = _spd_matrix(pa, N, nb, 5)
-    tp, info = pa.dpotrf_jdf_new(A)
+    prev = pa.dpotrf_fuse_syrk(fuse)
+    try:
+        tp, info = pa.dpotrf_jdf_new(A)
+    finally:
+        pa.dpotrf_fuse_syrk(prev)
     assert tp.name == "dpotrf_L.jdf"
     ctx.add_taskpool(tp)
     ctx.start()
