@@ -67,6 +67,10 @@ ShmEngine::ShmEngine(int rank_, int size_, const std::string& job, int gpu) : jo
   size = size_;
   ring_bytes_ = ParamRegistry::instance().reg_sizet("comm", "shm", "ring_bytes", "Bytes of each inbound shared-memory ring", (size_t)8 << 20);
   cbs_.resize(TAG_MAX);
+  reg_.reset(new std::atomic<bool>[TAG_MAX]);
+  stash_n_.reset(new std::atomic<int>[TAG_MAX]);
+  for (int t = 0; t < TAG_MAX; ++t) { reg_[t].store(false); stash_n_[t].store(0); }
+  stash_.resize(TAG_MAX);
   aggregate_ = ParamRegistry::instance().reg_int("runtime", "comm", "aggregate", "Pack activations waiting for the same peer into one message (reference runtime_comm_aggregate)", 1) != 0;
   // an aggregate: [u32 count] then per message [i32 tag][u32 len][bytes, 8-aligned]
   cbs_[TAG_AGGREGATE] = [this](int src, int, const void* msg, size_t len) {
@@ -80,10 +84,11 @@ ShmEngine::ShmEngine(int rank_, int size_, const std::string& job, int gpu) : jo
       std::memcpy(&tag, p + off, 4);
       std::memcpy(&n, p + off + 4, 4);
       off += 8;
-      if (tag >= 0 && tag < TAG_MAX && cbs_[tag]) cbs_[tag](src, tag, p + off, n);
+      deliver(src, tag, p + off, n);
       off += (n + 7) & ~(size_t)7;
     }
   };
+  reg_[TAG_AGGREGATE].store(true, std::memory_order_release);
   for (int i = 0; i < size; ++i) out_.emplace_back(new Out());
   bytes_from_.reset(new std::atomic<uint64_t>[size]);
   for (int i = 0; i < size; ++i) bytes_from_[i].store(0);
@@ -362,13 +367,53 @@ ShmRing* ShmEngine::out_ring(int dst) {
 
 int ShmEngine::tag_register(int tag, AmCallback cb) {
   if (tag < 0 || tag >= TAG_MAX) return -1;
+  std::lock_guard<std::mutex> g(stash_m_);
   cbs_[tag] = std::move(cb);
+  reg_[tag].store(cbs_[tag] != nullptr, std::memory_order_release);
   return 0;
 }
 int ShmEngine::tag_unregister(int tag) {
   if (tag < 0 || tag >= TAG_MAX) return -1;
+  std::lock_guard<std::mutex> g(stash_m_);
+  reg_[tag].store(false, std::memory_order_release);
   cbs_[tag] = nullptr;
   return 0;
+}
+
+// Progress thread: hand a message to its tag's callback, or keep it (in order)
+// until the tag is registered.
+void ShmEngine::deliver(int src, int tag, const void* msg, size_t len) {
+  if (tag < 0 || tag >= TAG_MAX) {
+    warning("dropping active message with invalid tag %d from %d", tag, src);
+    return;
+  }
+  if (reg_[tag].load(std::memory_order_acquire) && stash_n_[tag].load(std::memory_order_acquire) == 0) {
+    cbs_[tag](src, tag, msg, len);
+    return;
+  }
+  std::lock_guard<std::mutex> g(stash_m_);
+  const char* p = static_cast<const char*>(msg);
+  stash_[tag].push_back(Stashed{src, std::vector<char>(p, p + len)});
+  stash_n_[tag].fetch_add(1, std::memory_order_release);
+  stash_any_.fetch_add(1, std::memory_order_release);
+}
+
+// Progress thread: deliver the kept messages of tags registered since.
+int ShmEngine::replay_stash() {
+  int n = 0;
+  for (int t = 0; t < TAG_MAX; ++t) {
+    if (stash_n_[t].load(std::memory_order_acquire) == 0 || !reg_[t].load(std::memory_order_acquire)) continue;
+    std::vector<Stashed> v;
+    {
+      std::lock_guard<std::mutex> g(stash_m_);
+      v.swap(stash_[t]);
+      stash_any_.fetch_sub((int)v.size(), std::memory_order_acq_rel);
+      stash_n_[t].store(0, std::memory_order_release);
+    }
+    for (const Stashed& m : v) cbs_[t](m.src, t, m.msg.data(), m.msg.size());
+    n += (int)v.size();
+  }
+  return n;
 }
 
 bool ShmEngine::ring_write(ShmRing* r, const void* hdr, size_t hlen, const void* payload, size_t plen, int tag, int src) {
@@ -402,7 +447,7 @@ int ShmEngine::send_am2(int tag, int dst, const void* hdr, size_t hlen, const vo
     std::vector<char> m(hlen + plen);
     if (hlen) std::memcpy(m.data(), hdr, hlen);
     if (plen) std::memcpy(m.data() + hlen, payload, plen);
-    post([this, tag, m = std::move(m)] { if (cbs_[tag]) cbs_[tag](rank, tag, m.data(), m.size()); });
+    post([this, tag, m = std::move(m)] { deliver(rank, tag, m.data(), m.size()); });
     return 0;
   }
   Out& o = *out_[dst];
@@ -529,6 +574,7 @@ void ShmEngine::post(std::function<void()> fn) {
 
 int ShmEngine::progress() {
   int n = 0;
+  if (stash_any_.load(std::memory_order_acquire) > 0) n += replay_stash();
   if (posted_n_.load(std::memory_order_acquire) > 0) {
     std::vector<std::function<void()>> fns;
     {
@@ -563,8 +609,7 @@ int ShmEngine::progress() {
       }
       if (h.magic != 0xA11C0DE5u) fatal("corrupted shm message from rank %d", s);
       const char* payload = r->data + pos + sizeof(h);
-      if (h.tag >= 0 && h.tag < TAG_MAX && cbs_[h.tag]) cbs_[h.tag](h.src, h.tag, payload, h.plen);
-      else warning("dropping active message with unregistered tag %d from %d", h.tag, s);
+      deliver(h.src, h.tag, payload, h.plen);
       r->tail.store(tail + h.len, std::memory_order_release);
       ++n;
     }

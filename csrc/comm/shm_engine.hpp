@@ -149,6 +149,21 @@ class ShmEngine : public CommEngine {
   std::vector<size_t> map_len_;
   ShmHeader* me_ = nullptr;
   std::vector<AmCallback> cbs_;
+  // Messages for a tag nobody registered yet (a peer ran ahead: e.g. its MPI
+  // shim collective reached this rank before this rank's shim registered the
+  // tag) wait here, in arrival order, and are delivered once the tag is
+  // registered -- the unexpected-message queue of an MPI library.
+  struct Stashed {
+    int src;
+    std::vector<char> msg;
+  };
+  std::unique_ptr<std::atomic<bool>[]> reg_;
+  std::unique_ptr<std::atomic<int>[]> stash_n_;
+  std::vector<std::vector<Stashed>> stash_;
+  std::mutex stash_m_;
+  std::atomic<int> stash_any_{0};
+  void deliver(int src, int tag, const void* msg, size_t len);
+  int replay_stash();
   std::vector<std::unique_ptr<Out>> out_;
   std::mutex post_m_;
   std::vector<std::function<void()>> posted_;

@@ -9,4 +9,7 @@
 #define PARSEC_DECLSPEC /* symbols are exported by default */
 #endif
 #define PARSEC_DIST_COLLECTIVES 1
+/* glibc provides getopt.h and getopt_long (reference CMake checks PARSEC_HAVE_GETOPT_H / _LONG) */
+#define PARSEC_HAVE_GETOPT_H 1
+#define PARSEC_HAVE_GETOPT_LONG 1
 #endif

@@ -51,7 +51,7 @@ CORE_SOURCES = [
     "csrc/algos/host_gemm.cpp",
     "csrc/algos/dtd_builtins.cpp",
     "csrc/capi/capi.cpp",
-    "csrc/capi/hash_table.cpp", "csrc/capi/object.cpp", "csrc/capi/future_c.cpp", "csrc/capi/mpi_shim.cpp",
+    "csrc/capi/hash_table.cpp", "csrc/capi/object.cpp", "csrc/capi/future_c.cpp", "csrc/capi/mpi_shim.cpp", "csrc/capi/redistribute_core.cpp",
     "csrc/algos/dpotrf_jdf.cpp",
     "csrc/algos/dgeqrf_jdf.cpp",
     "csrc/algos/redistribute_ptg.cpp",

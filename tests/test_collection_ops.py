@@ -129,6 +129,25 @@ def test_ptg_dgemm(pa, transB):
     ctx.fini()
 
 
+@pytest.mark.parametrize("transB", [0, 1])
+@pytest.mark.parametrize("b", [50, 300])
+def test_ptg_dgemm_host_kernel_edges(pa, b, transB):
+    """Tiles large enough for the packed host GEMM (csrc/algos/host_gemm.cpp:
+    24 x 8 AVX-512 / 8 x 4 AVX2 register tiles): b = 50 leaves 2-row / 2-column
+    edge tiles, b = 300 spans two k blocks (KC 256) and three row blocks."""
+    ctx = pa.init(4)
+    M, N, K = 2 * b, b, 2 * b
+    A, SA = _mat(pa, M, K, b, seed=13)
+    B, SB = _mat(pa, N, K, b, seed=14) if transB else _mat(pa, K, N, b, seed=14)
+    C, SC = _mat(pa, M, N, b, seed=15)
+    tp = pa.dgemm_new(-0.75, A, B, 1.0, C, transB)
+    tp.devices_mask = 1
+    _run(pa, ctx, tp)
+    ref = -0.75 * SA @ (SB.T if transB else SB) + SC
+    assert np.allclose(_dense(C, M, N, b), ref, rtol=1e-12, atol=1e-11)
+    ctx.fini()
+
+
 def test_dtd_dgemm_4x4_tiles(pa):
     """BASELINE config 1: DTD tiled DGEMM, 4x4 tiles, one CPU process."""
     ctx = pa.init(4)

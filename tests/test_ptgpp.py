@@ -683,6 +683,44 @@ def test_reference_write_check_mpi(tmp_path, nranks):
     assert rc == 0 and "TEST SUCCESS" in text, text[-3000:]
 
 
+REDIST = os.path.join(REF, "tests/collections/redistribute")
+# reference tests/collections/Testings.cmake:5-9 (collections/redistribute[:mp])
+REDIST_ARGS = "-M 2400 -N 2400 -a 2400 -A 2400 -t 300 -T 300 -b 200 -B 200 -m 2000 -n 2000 -I 30 -J 40 -i 100 -j 121 -v -z -x".split()
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
+@pytest.mark.parametrize("prog,nranks,extra", [
+    ("testing_redistribute", 1, ["-c", "2"]),
+    ("testing_redistribute", 4, ["-c", "2"]),
+    ("testing_redistribute", 8, ["-P", "2", "-Q", "4", "-p", "4", "-q", "2", "-c", "1"]),  # the :mp case
+    ("testing_redistribute_random", 2, ["-c", "2"]),
+    ("testing_redistribute_random", 4, ["-c", "2"]),
+])
+def test_reference_redistribute_mpi(tmp_path, prog, nranks, extra):
+    """tests/collections/redistribute: testing_redistribute(_random).c + common.c
+    + the four check / bound JDFs, unmodified, with the minimal MPI: PTG and DTD
+    redistribution of a 2000 x 2000 window between two block-cyclic layouts with
+    different tile sizes and displacements, each checked by redistributing back
+    (redistribute_check2.jdf: "Redistribute Result is CORRECT!" for PTG and
+    DTD). The 4-rank run hung one time in three before the comm engine kept
+    messages that arrive for a tag not registered yet (a peer's MPI-shim
+    collective reaching a rank before its own shim registered the tag)."""
+    from parsec_amd import launch
+
+    cpps = [ptgpp.compile_jdf(os.path.join(REDIST, j + ".jdf"), str(tmp_path))[0]
+            for j in ("redistribute_check", "redistribute_check2", "redistribute_bound", "redistribute_no_optimization")]
+    cc, libs = ptgpp.compile_flags(False)
+    exe = str(tmp_path / prog)
+    r = subprocess.run(cc + list(ptgpp.C_BODIES) + MPI_FLAGS + [f"-I{tmp_path}", f"-I{REDIST}", f"-I{REF}"] + cpps +
+                       ["-x", "c++", os.path.join(REDIST, prog + ".c"), os.path.join(REDIST, "common.c"), "-x", "none", "-o", exe] + libs,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rc, outs = launch.launch(nranks, [exe] + REDIST_ARGS + extra, timeout=180, capture=True, env={"PARSEC_MCA_device_hip_enabled": "0"})
+    text = "".join(o + e for o, e in outs)
+    assert rc == 0, text[-3000:]
+    assert text.count("Redistribute Result is CORRECT!") == 2 and "NOT correct" not in text, text[-3000:]
+
+
 @pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present")
 @pytest.mark.parametrize("src,expect", [("examples/Ex00_StartStop.c", None),
                                         ("examples/interfaces/dtd/dtd_example_hello_world.c", "Hello World my rank is: 0")])
