@@ -100,6 +100,13 @@ struct GemmDesc {
   // max|W|: a gated descriptor has beta 0 and never reads Cin as C) exceeds
   // the launch's limit
   uint8_t gate;
+  // 1: C is also the A operand (B := B op(W), the panel solve in place, op(B)
+  // upper triangular): the column blocks of a row run right to left in
+  // dispatch order, and a workgroup writes its block only after the ones to
+  // its right (which read it) finished; C2 then points to the per-row-block
+  // counters of this descriptor (unsigned, zero between launches), not a
+  // second output
+  uint8_t inplace;
   // optional (zero = off): beta scales Cin (ld ldcin) instead of C, and C2 (ld
   // ldc2) -= every value written to C (fused "W = A1 + V^T A2" / "A1 -= T^T W")
   int ldcin, ldc2;

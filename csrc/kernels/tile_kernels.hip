@@ -170,7 +170,8 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
   const GemmDesc& d = args.d[di];
   const int local = tile - args.tile_start[di];
   const int mt = (d.m + BM - 1) / BM;
-  const int tm = local % mt, tn = local / mt;
+  const int nt = (d.n + BN - 1) / BN;
+  const int tm = local % mt, tn = d.inplace ? nt - 1 - local / mt : local / mt;
   const int m0 = tm * BM, n0 = tn * BN;
   if (d.lower_only && n0 > m0 + BM - 1) return;
   if (d.gate) {
@@ -447,6 +448,19 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
   }  // DL
 
   const double alpha = d.alpha, beta = (preload || late) ? 0.0 : d.beta;
+  // in place: the blocks to the right of this one in its row block (lower
+  // blockIdx: dispatched earlier, so waiting on them cannot deadlock) read it;
+  // write only after all of them finished. The wait is bounded: a lost
+  // signal degrades to a wrong result a test catches, never to a hung GPU.
+  unsigned* const rsync = d.inplace ? reinterpret_cast<unsigned*>(d.C2) + tm : nullptr;
+  if (rsync) {
+    if (tid == 0) {
+      const unsigned want = (unsigned)(nt - 1 - tn);
+      int spins = 0;
+      while (__hip_atomic_load(rsync, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < want && spins++ < (1 << 19)) __builtin_amdgcn_s_sleep(8);
+    }
+    __syncthreads();
+  }
 #pragma unroll
   for (int i = 0; i < FN; ++i)
 #pragma unroll
@@ -465,10 +479,20 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
           }
           if (beta != 0.0) v += beta * Cr[(size_t)gn * ldcr + gm];
           *p = v;
-          if (d.C2) d.C2[(size_t)gn * d.ldc2 + gm] -= v;
+          if (d.C2 && !rsync) d.C2[(size_t)gn * d.ldc2 + gm] -= v;
         }
       }
     }
+  if (rsync) {
+    // signal the blocks to the left; the leftmost one (the last of its row)
+    // leaves the counter at zero for the next launch
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) {
+      if (tn == 0) __hip_atomic_store(rsync, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      else __hip_atomic_fetch_add(rsync, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   crit_release(args.claim);
 }
 
@@ -501,7 +525,8 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
       ks = 1;
     }
   } else if ((int)blockIdx.x < args.main_tiles) {
-    tile = xcd_remap(blockIdx.x, args.main_tiles);
+    // stagger < 0: tiles in dispatch order (in-place descriptors wait on lower blockIdx)
+    tile = args.stagger < 0 ? (int)blockIdx.x : xcd_remap(blockIdx.x, args.main_tiles);
   } else {
     const int u = blockIdx.x - args.main_tiles;
     nsplit = args.ksplit;
@@ -880,7 +905,10 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
   int grid_size = total;
   const int slots = gemm_slots();
   static const int stagger_env = getenv("PARSEC_GEMM_STAGGER") ? atoi(getenv("PARSEC_GEMM_STAGGER")) : 0;
-  if (BM == 128 && stagger_env > 0 && total >= 2 * slots) {
+  bool ordered = false;  // in-place descriptors: tiles in dispatch order, no remap / stagger / split / persistent / direct-LDS
+  for (int i = 0; i < n; ++i) ordered = ordered || descs[i].inplace;
+  if (ordered) a.stagger = -1;
+  if (!ordered && BM == 128 && stagger_env > 0 && total >= 2 * slots) {
     bool ok = true;
     for (int i = 0; ok && i < n; ++i)
       ok = descs[i].beta == 1.0 && !descs[i].a_lower && !descs[i].b_upper && !descs[i].Cin && !descs[i].C2 && !descs[i].gate && descs[i].k >= 2 * BK;
@@ -2367,6 +2395,35 @@ static bool trsm_substitutable(const TrsmGemmDesc& t) {
   return t.L && t.ldl > 0 && t.n <= kTrsmMaxCols && t.n % 64 == 0 && t.ldw >= t.n;
 }
 static bool trsm_gateable(const TrsmGemmDesc& t) { return trsm_substitutable(t); }
+// Per-stream row-block counters of the in-place W-GEMM (GemmDesc::inplace):
+// zero between launches (the last workgroup of each row block resets its
+// counter), so one zeroed allocation per stream serves every launch on it.
+static unsigned* trsm_row_counters(hipStream_t stream, size_t need) {
+  static std::mutex m;
+  static std::vector<std::pair<hipStream_t, std::pair<unsigned*, size_t>>> bufs;
+  std::lock_guard<std::mutex> g(m);
+  for (auto& b : bufs)
+    if (b.first == stream) {
+      if (b.second.second >= need) return b.second.first;
+      return nullptr;  // larger than the first allocation: the caller copies instead
+    }
+  const size_t cap = std::max<size_t>(need, 1 << 16);
+  void* p = nullptr;
+  if (hipMalloc(&p, cap * sizeof(unsigned)) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+  if (hipMemset(p, 0, cap * sizeof(unsigned)) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+  bufs.push_back({stream, {static_cast<unsigned*>(p), cap}});
+  return static_cast<unsigned*>(p);
+}
+
+// PARSEC_TRSM_INPLACE=1 (measurement, off): the W-GEMM runs in place (no B
+// copies). Correct, but 22 % slower
+// at config 2 and 8 % at config 3 (profiles/r6_trsm_inplace.txt): a block
+// waiting for the blocks to its right keeps its CU slot, and beside the bulk
+// GEMMs the critical stream has about one slot per CU. Default: every B tile
+// copied into the workspace first, W unpacked there, the GEMM reading both.
+static const bool g_trsm_inplace = getenv("PARSEC_TRSM_INPLACE") && atoi(getenv("PARSEC_TRSM_INPLACE")) != 0;
+static constexpr int kRowSlots = 64;  // row-block counters per descriptor (m / 64)
+
 void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, double* ws) {
   const int mode = parsec::trsm_inverse_mode(-1, 0.0);
   const double limit = parsec::trsm_inverse_limit();
@@ -2375,29 +2432,26 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
   auto* slots = reinterpret_cast<unsigned long long*>(base);
   char* up_next = base + lay.slots;
   char* const copies = base + lay.slots + lay.unpack;
-  // distinct W tiles of the batch: unpacked copy (packed tiles), gate slot
+  // distinct W tiles of the batch: unpacked copy (packed tiles that a
+  // substitution needs), gate slot
   struct WInfo {
     const double* W;
-    const double* Wu;  // what the GEMM / substitution read as W
-    int ldu;
+    int ldw;
+    bool packed;
+    const double* Wu = nullptr;  // unpacked W (lower, zeros above): the substitution's diagonal blocks
+    int ldu = 0;
     unsigned long long* slot = nullptr;
     bool unpack = false;
   };
   std::vector<WInfo> wi;
-  auto info_of = [&](const TrsmGemmDesc& t) -> WInfo& {
-    for (WInfo& w : wi)
-      if (w.W == t.W) return w;
-    WInfo w{t.W, t.W, t.ldw};
-    if (t.packed) {
-      w.Wu = reinterpret_cast<const double*>(up_next);
-      w.ldu = t.n;
-      w.unpack = true;
-      up_next += al256((size_t)t.n * t.n * sizeof(double));
-    }
-    wi.push_back(w);
-    return wi.back();
+  auto info_of = [&](const TrsmGemmDesc& t) -> int {
+    for (size_t i = 0; i < wi.size(); ++i)
+      if (wi[i].W == t.W) return (int)i;
+    wi.push_back(WInfo{t.W, t.ldw, t.packed != 0});
+    if (!t.packed) { wi.back().Wu = t.W; wi.back().ldu = t.ldw; }
+    return (int)wi.size() - 1;
   };
-  std::vector<TrsmDesc> subst;          // solved by substitution, decided on the host
+  std::vector<int> subst_i, subst_w;    // solved by substitution, decided on the host (desc, W)
   std::vector<TrsmGemmDesc> via_w;      // through W
   std::vector<uint8_t> gated;           // ... with the device-side gate
   std::vector<int> slot_of;             // via_w index -> wi index
@@ -2416,20 +2470,39 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
         g_est_stats[2].fetch_add(1, std::memory_order_relaxed);
       }
     }
-    WInfo& w = info_of(t);
-    if (route == 2 && !w.slot) w.slot = slots + 2 * (&w - wi.data());
-    const int wix = (int)(&w - wi.data());
+    const int wix = info_of(t);
+    WInfo& w = wi[wix];
+    if (route == 2 && !w.slot) w.slot = slots + 2 * wix;
+    if (route != 0 && w.packed && !w.unpack) {  // the substitution reads W's diagonal blocks unpacked
+      w.unpack = true;
+      w.Wu = reinterpret_cast<const double*>(up_next);
+      w.ldu = t.n;
+      up_next += al256((size_t)t.n * t.n * sizeof(double));
+    }
     if (route == 1) {
-      TrsmDesc x{};
-      x.L = t.L; x.ldl = t.ldl; x.B = t.B; x.ldb = t.ldb; x.m = t.m; x.n = t.n; x.trans = 1;
-      x.invD = w.Wu; x.invD_ld = w.ldu; x.packed = t.packed;
-      subst.push_back(x);
+      subst_i.push_back(i);
+      subst_w.push_back(wix);
     } else {
       via_w.push_back(t);
       gated.push_back(route == 2);
       slot_of.push_back(wix);
     }
   }
+  // in place (no B copies): every descriptor of a chunk gets kRowSlots counters
+  unsigned* rows = nullptr;
+  if (g_trsm_inplace && g_trsm_tri && !via_w.empty()) {  // in place needs the triangular k bound (a block never reads columns right of it)
+    bool fits = true;
+    for (const TrsmGemmDesc& t : via_w) fits = fits && (t.m + 63) / 64 <= kRowSlots;
+    if (fits) rows = trsm_row_counters(stream, (size_t)kMaxCopyBatch * kRowSlots);
+  }
+  // the GEMM reads W unpacked (lower, zeros above)
+  for (WInfo& w : wi)
+      if (w.packed && !w.unpack) {
+        w.unpack = true;
+        w.Wu = reinterpret_cast<const double*>(up_next);
+        for (int i = 0; i < n; ++i)
+          if (d[i].W == w.W) { w.ldu = d[i].n; up_next += al256((size_t)d[i].n * d[i].n * sizeof(double)); break; }
+      }
   // estimate slots start from zero (the scan jobs max into them)
   int nslots = 0;
   for (const WInfo& w : wi) nslots += w.slot ? 1 : 0;
@@ -2464,35 +2537,51 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
       pend_unpack.pop_back();
     }
   };
-  while (pend_scan.size() > (size_t)kMaxScan || pend_unpack.size() > (size_t)kMaxScan || (via_w.empty() && (!pend_scan.empty() || !pend_unpack.empty()))) {
+  // jobs that cannot wait for a chunk's copy launch: before everything else
+  while (pend_scan.size() > (size_t)kMaxScan || pend_unpack.size() > (size_t)kMaxScan ||
+         ((rows || via_w.empty()) && (!pend_scan.empty() || !pend_unpack.empty()))) {
     CopyBatchArgs ca;
     ca.count = 0;
     ca.prio = t_launch_prio;
     int maxc = 1;
     add_jobs(ca, maxc);
-    hipLaunchKernelGGL(copy_tiles_kernel, dim3(std::min(256, (maxc + 3) / 4), ca.nscan + ca.nunpack), dim3(256), 0, stream, ca);
+    if (ca.nscan + ca.nunpack > 0)
+      hipLaunchKernelGGL(copy_tiles_kernel, dim3(std::min(256, (maxc + 3) / 4), ca.nscan + ca.nunpack), dim3(256), 0, stream, ca);
   }
   for (size_t s0 = 0; s0 < via_w.size(); s0 += kMaxCopyBatch) {
     const int cnt = (int)std::min<size_t>(kMaxCopyBatch, via_w.size() - s0);
     std::vector<TrsmDesc> fb;  // gated substitution solves of this chunk
     CopyBatchArgs ca;
-    ca.count = cnt;
+    ca.count = 0;
+    ca.nscan = 0;
+    ca.nunpack = 0;
     ca.prio = t_launch_prio;
     std::vector<GemmDesc> g(cnt);
     char* p = copies;
     int maxc = 1;
-    add_jobs(ca, maxc);
+    if (!rows) add_jobs(ca, maxc);
     for (int i = 0; i < cnt; ++i) {
       const TrsmGemmDesc& t = via_w[s0 + i];
       const WInfo& w = wi[slot_of[s0 + i]];
-      ca.rows[i] = t.m; ca.cols[i] = t.n; ca.ld_src[i] = t.ldb; ca.ld_dst[i] = t.m;
-      ca.src[i] = t.B; ca.dst[i] = reinterpret_cast<double*>(p);
-      maxc = std::max(maxc, t.n);
       GemmDesc& e = g[i];
-      e.A = ca.dst[i]; e.B = w.Wu; e.C = t.B;
+      if (rows) {
+        // B := B W^T in place: column blocks right to left, each written after
+        // the blocks to its right (its readers) finished
+        e.A = t.B; e.lda = t.ldb;
+        e.inplace = 1;
+        e.C2 = reinterpret_cast<double*>(rows + (size_t)i * kRowSlots);
+      } else {
+        const int c = ca.count++;
+        ca.rows[c] = t.m; ca.cols[c] = t.n; ca.ld_src[c] = t.ldb; ca.ld_dst[c] = t.m;
+        ca.src[c] = t.B; ca.dst[c] = reinterpret_cast<double*>(p);
+        maxc = std::max(maxc, t.n);
+        e.A = ca.dst[c]; e.lda = t.m;
+        p += al256((size_t)t.m * t.n * sizeof(double));
+      }
+      e.B = w.Wu; e.ldb = w.ldu;  // W unpacked (lower, zeros above)
+      e.C = t.B; e.ldc = t.ldb;
       e.m = t.m; e.n = t.n; e.k = t.n;
-      e.lda = t.m; e.ldb = w.ldu; e.ldc = t.ldb;
-      e.alpha = 1.0; e.beta = 0.0; e.transA = 0; e.transB = 1; e.lower_only = 0; e.a_lower = 0;  // copy x (L^-1)^T
+      e.alpha = 1.0; e.beta = 0.0; e.transA = 0; e.transB = 1; e.lower_only = 0; e.a_lower = 0;  // B (L^-1)^T
       e.b_upper = g_trsm_tri ? 1 : 0;  // (L^-1)^T is upper triangular: output column block j needs k < (j+1) BN only
       e.gate = 0;
       if (gated[s0 + i]) {
@@ -2505,9 +2594,9 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
         x.gate_slot = reinterpret_cast<const double*>(w.slot);
         fb.push_back(x);
       }
-      p += al256((size_t)t.m * t.n * sizeof(double));
     }
-    hipLaunchKernelGGL(copy_tiles_kernel, dim3(std::min(256, (maxc + 3) / 4), cnt + ca.nscan + ca.nunpack), dim3(256), 0, stream, ca);
+    if (ca.count + ca.nscan + ca.nunpack > 0)
+      hipLaunchKernelGGL(copy_tiles_kernel, dim3(std::min(256, (maxc + 3) / 4), ca.count + ca.nscan + ca.nunpack), dim3(256), 0, stream, ca);
     launch_gemm_batch(g.data(), cnt, stream);
     if (!fb.empty()) {
       std::vector<const double*> inv(fb.size());
@@ -2515,9 +2604,18 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
       launch_trsm_inv(fb.data(), inv.data(), (int)fb.size(), stream, true);
     }
   }
-  if (!subst.empty()) {
-    std::vector<const double*> inv(subst.size());
-    for (size_t i = 0; i < subst.size(); ++i) inv[i] = subst[i].invD;
+  if (!subst_i.empty()) {
+    std::vector<TrsmDesc> subst;
+    std::vector<const double*> inv;
+    for (size_t k = 0; k < subst_i.size(); ++k) {
+      const TrsmGemmDesc& t = d[subst_i[k]];
+      const WInfo& w = wi[subst_w[k]];
+      TrsmDesc x{};
+      x.L = t.L; x.ldl = t.ldl; x.B = t.B; x.ldb = t.ldb; x.m = t.m; x.n = t.n; x.trans = 1;
+      x.invD = w.Wu; x.invD_ld = w.ldu; x.packed = t.packed;
+      subst.push_back(x);
+      inv.push_back(w.Wu);
+    }
     launch_trsm_inv(subst.data(), inv.data(), (int)subst.size(), stream);
   }
 }
