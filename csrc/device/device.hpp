@@ -174,6 +174,8 @@ int trsm_estimate_route(int on);
 // [0] estimates published by tile POTRFs, [1] panel decisions taken on the
 // host, [2] panels left to the device-side gate
 void trsm_estimate_stats(uint64_t out[3], bool reset);
+// in-place panel-solve W-GEMM (PARSEC_TRSM_INPLACE): on (1) / off (0), < 0 queries; returns the previous setting
+int trsm_inplace(int set);
 // a device buffer was (re)allocated: drop a panel estimate keyed by its address
 void trsm_estimate_forget(const void* p);
 double trsm_estimate_lookup(const void* p);

@@ -2421,7 +2421,16 @@ static unsigned* trsm_row_counters(hipStream_t stream, size_t need) {
 // waiting for the blocks to its right keeps its CU slot, and beside the bulk
 // GEMMs the critical stream has about one slot per CU. Default: every B tile
 // copied into the workspace first, W unpacked there, the GEMM reading both.
-static const bool g_trsm_inplace = getenv("PARSEC_TRSM_INPLACE") && atoi(getenv("PARSEC_TRSM_INPLACE")) != 0;
+static std::atomic<int> g_trsm_inplace_v{-1};
+static bool trsm_inplace_on() {
+  int v = g_trsm_inplace_v.load(std::memory_order_relaxed);
+  if (v < 0) {
+    v = getenv("PARSEC_TRSM_INPLACE") && atoi(getenv("PARSEC_TRSM_INPLACE")) != 0 ? 1 : 0;
+    int expected = -1;
+    if (!g_trsm_inplace_v.compare_exchange_strong(expected, v)) v = expected;
+  }
+  return v != 0;
+}
 static constexpr int kRowSlots = 64;  // row-block counters per descriptor (m / 64)
 
 void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, double* ws) {
@@ -2490,7 +2499,7 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
   }
   // in place (no B copies): every descriptor of a chunk gets kRowSlots counters
   unsigned* rows = nullptr;
-  if (g_trsm_inplace && g_trsm_tri && !via_w.empty()) {  // in place needs the triangular k bound (a block never reads columns right of it)
+  if (trsm_inplace_on() && g_trsm_tri && !via_w.empty()) {  // in place needs the triangular k bound (a block never reads columns right of it)
     bool fits = true;
     for (const TrsmGemmDesc& t : via_w) fits = fits && (t.m + 63) / 64 <= kRowSlots;
     if (fits) rows = trsm_row_counters(stream, (size_t)kMaxCopyBatch * kRowSlots);
@@ -2618,6 +2627,13 @@ void launch_trsm_w_batch(const TrsmGemmDesc* d, int n, hipStream_t stream, doubl
     }
     launch_trsm_inv(subst.data(), inv.data(), (int)subst.size(), stream);
   }
+}
+
+// In-place W-GEMM on (1) / off (0) for later launches; < 0 queries. Returns the previous setting.
+int trsm_inplace(int set) {
+  const int prev = trsm_inplace_on() ? 1 : 0;
+  if (set >= 0) g_trsm_inplace_v.store(set ? 1 : 0);
+  return prev;
 }
 
 // counters: [0] estimates published by POTRF, [1] panel decisions taken on the

@@ -491,6 +491,8 @@ PYBIND11_MODULE(_C, m) {
         tp->destructor_hook = [info]() { delete info; };
         return py::make_tuple(py::cast(tp, py::return_value_policy::take_ownership), (uintptr_t)info);
       });
+  m.def("trsm_inplace", [](int set) { return kern::trsm_inplace(set); }, py::arg("set") = -1,
+        "Panel-solve W-GEMM in place (no B-tile copies; PARSEC_TRSM_INPLACE): 1 on, 0 off, < 0 query; returns the previous setting");
   m.def("dpotrf_fuse_syrk", [](int set) { return algos::dpotrf_fuse_syrk(set); }, py::arg("set") = -1,
         "SYRK(k-1,k) fused into POTRF(k) for new dpotrf_L.jdf taskpools (PARSEC_DPOTRF_FUSE_SYRK); returns the previous value");
   m.def("dpotrf_jdf_new", [](TiledMatrix* A) {

@@ -12,15 +12,18 @@ def _spd(N, dev, seed=0):
     return (R + R.t()) / 2 + N * torch.eye(N, dtype=torch.float64, device=dev)
 
 
-@pytest.mark.parametrize("fuse", [0, 1])
+@pytest.mark.parametrize("fuse,inplace", [(0, 0), (1, 0), (0, 1)])
 @pytest.mark.parametrize("N,nb", [(1024, 256), (2048, 512), (1536, 384)])
-def test_dpotrf_hbm_resident(pa, N, nb, fuse):
+def test_dpotrf_hbm_resident(pa, N, nb, fuse, inplace):
     """fuse = 1: POTRF(k) applies SYRK(k-1,k) itself (pre-GEMM in its launch on
-    the critical stream); the factor is checked against torch's fp64 Cholesky."""
+    the critical stream); inplace = 1: the panel-solve W-GEMM runs in place
+    (ordered row-block signalling, no B-tile copies). The factor is checked
+    against torch's fp64 Cholesky."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     ctx = pa.init(3)
     prev = pa.dpotrf_fuse_syrk(fuse)
+    prev_ip = pa.trsm_inplace(inplace)
     try:
         gpu = pa.first_gpu_device_index()
         NT = N // nb
@@ -42,6 +45,7 @@ def test_dpotrf_hbm_resident(pa, N, nb, fuse):
         assert gpus and gpus[0]["executed_tasks"] > 0
     finally:
         pa.dpotrf_fuse_syrk(prev)
+        pa.trsm_inplace(prev_ip)
         ctx.fini()
 
 
