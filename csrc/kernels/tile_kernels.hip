@@ -1276,6 +1276,23 @@ __global__ __launch_bounds__(256) void copy_tiles_kernel(const CopyBatchArgs a) 
   const int rows = a.rows[t], cols = a.cols[t], lds = a.ld_src[t], ldd = a.ld_dst[t];
   const double* __restrict__ s = a.src[t];
   double* __restrict__ d = a.dst[t];
+  if (lds == rows && ldd == rows && (((uintptr_t)s | (uintptr_t)d) % 16) == 0 && ((size_t)rows * cols) % 2 == 0) {
+    // a whole contiguous tile (the panel solve's B tiles): 16-byte vectors,
+    // four loads in flight per thread before the stores
+    const uint4* __restrict__ s4 = reinterpret_cast<const uint4*>(s);
+    uint4* __restrict__ d4 = reinterpret_cast<uint4*>(d);
+    const size_t n = (size_t)rows * cols / 2, stride = (size_t)gridDim.x * 256;
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+      const uint4 v0 = s4[i], v1 = s4[i + stride], v2 = s4[i + 2 * stride], v3 = s4[i + 3 * stride];
+      d4[i] = v0;
+      d4[i + stride] = v1;
+      d4[i + 2 * stride] = v2;
+      d4[i + 3 * stride] = v3;
+    }
+    for (; i < n; i += stride) d4[i] = s4[i];
+    return;
+  }
   for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < cols; c += gridDim.x * 4)
     for (int r = threadIdx.x & 63; r < rows; r += 64) d[(size_t)c * ldd + r] = s[(size_t)c * lds + r];
 }

@@ -205,6 +205,26 @@ def test_headline_tile_size_8_ranks_shared_gpu(pa, route):
         assert sum(c["bytes_from_peer"]) == c["bytes_pulled_ipc"] and c["bytes_from_peer"][r] == 0, c
     # pulls from distinct source ranks were in flight together (lanes)
     assert max(c["gets_lanes_busy_max"] for c in comm) >= 2, comm
+    # exactly one pull per (tile, receiving rank): the POTRF(k) panel is ONE
+    # packed tile (W with L(k,k)^T above the diagonal), so the panel volume is
+    # 42 tiles here where the round-5 DAG (W and L(k,k) apart) pulled 84
+    w_tiles, c_tiles = _dpotrf_remote_tiles(16, lambda m, n: (m % 4) * 2 + (n % 2))
+    assert (w_tiles, c_tiles) == (42, 394)
+    assert sum(c["bytes_pulled_ipc"] for c in comm) == (w_tiles + c_tiles) * 1024 * 1024 * 8, comm
+
+
+def _dpotrf_remote_tiles(NT, owner):
+    """Remote tile transfers of dpotrf_L.jdf (FUSE 0) under the owner map: the
+    panel tile of POTRF(k) to every other rank owning a TRSM(m, k), and each
+    TRSM(m, k) output to every other rank owning one of its SYRK / GEMM
+    consumers; a rank receives a datum once whatever the number of its readers."""
+    w = c = 0
+    for k in range(NT):
+        w += len({owner(m, k) for m in range(k + 1, NT)} - {owner(k, k)})
+        for m in range(k + 1, NT):
+            readers = {owner(m, m)} | {owner(m, n) for n in range(k + 1, m)} | {owner(r, m) for r in range(m + 1, NT)}
+            c += len(readers - {owner(m, k)})
+    return w, c
 
 
 def test_bench_probe_failure_reported(pa):
