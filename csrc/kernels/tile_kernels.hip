@@ -269,11 +269,26 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
     }
   };
   auto load_tile = [&](int k0) { load_tile_to(k0, ra, rb); };
+  // Operands loaded as k-pairs (op(A) = A^T, op(B) = B): LDS holds them
+  // m- / n-major with k contiguous, rows of BK + 2 doubles inside the same
+  // buffer, so a pair is one 16-byte store (eight lanes of a store group write
+  // one 128-byte row: no bank conflict) and the MFMA fragment reads of 16
+  // consecutive rows land on distinct banks (36 r mod 64 for r < 16, the k + 1
+  // lanes 2 banks over). The k-major layout made those stores 8-way conflicts.
+  constexpr int KS = BK + 2;
+  // (tile shapes whose k-contiguous rows would not fit the buffer keep the k-major layout)
+  constexpr bool KA = TRANSA && BM * KS <= BK * (BM + (((BM % 32) == 16) ? 0 : 16));
+  constexpr bool KB = !TRANSB && BN * KS <= BK * (BN + (((BN % 32) == 16) ? 0 : 16));
+  auto a_km = [&](int buf) { return &As[buf][0][0]; };
+  auto b_km = [&](int buf) { return &Bs[buf][0][0]; };
   auto store_tile_from = [&](int buf, const double2_t* ra, const double2_t* rb) {
 #pragma unroll
     for (int e = 0; e < A_PAIRS; ++e) {
       int idx = tid + NT * e;
-      if (TRANSA) {
+      if (KA) {
+        int kk = (idx % (BK / 2)) * 2, mm = idx / (BK / 2);
+        *reinterpret_cast<double2_t*>(a_km(buf) + mm * KS + kk) = ra[e];
+      } else if (TRANSA) {
         int kk = (idx % (BK / 2)) * 2, mm = idx / (BK / 2);
         As[buf][kk][mm] = ra[e].x;
         As[buf][kk + 1][mm] = ra[e].y;
@@ -288,6 +303,9 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
       if (TRANSB) {
         int nn = (idx % (BN / 2)) * 2, kk = idx / (BN / 2);
         *reinterpret_cast<double2_t*>(&Bs[buf][kk][nn]) = rb[e];
+      } else if (KB) {
+        int kk = (idx % (BK / 2)) * 2, nn = idx / (BK / 2);
+        *reinterpret_cast<double2_t*>(b_km(buf) + nn * KS + kk) = rb[e];
       } else {
         int kk = (idx % (BK / 2)) * 2, nn = idx / (BK / 2);
         Bs[buf][kk][nn] = rb[e].x;
@@ -308,9 +326,9 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
     for (int kk = 0; kk < BK; kk += 4) {
       double bfr[FM], afr[FN];
 #pragma unroll
-      for (int j = 0; j < FM; ++j) bfr[j] = As[cur][kk + fk][wm * WTM + j * 16 + fr];
+      for (int j = 0; j < FM; ++j) bfr[j] = KA ? a_km(cur)[(wm * WTM + j * 16 + fr) * KS + kk + fk] : As[cur][kk + fk][wm * WTM + j * 16 + fr];
 #pragma unroll
-      for (int i = 0; i < FN; ++i) afr[i] = Bs[cur][kk + fk][wn * WTN + i * 16 + fr];
+      for (int i = 0; i < FN; ++i) afr[i] = KB ? b_km(cur)[(wn * WTN + i * 16 + fr) * KS + kk + fk] : Bs[cur][kk + fk][wn * WTN + i * 16 + fr];
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll

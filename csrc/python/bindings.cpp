@@ -735,6 +735,24 @@ PYBIND11_MODULE(_C, m) {
     q.m2 = m2; q.n = n; q.ncols = ncols;
     return parsec_amd_qr_apply(&q, 1, (void*)ws, (void*)stream);
   });
+  // batched block-reflector applications (one grouped launch per GEMM phase):
+  // tuples (V, ldv, T, ldt, A1, lda1, A2, lda2, m2, n, ncols); ws sized by kernel_qr_apply_ws
+  m.def("kernel_qr_apply_batch", [](const std::vector<std::tuple<uintptr_t, int, uintptr_t, int, uintptr_t, int, uintptr_t, int, int, int, int>>& ds, uintptr_t ws, uintptr_t stream) {
+    std::vector<QrApplyDesc> v;
+    for (const auto& d : ds) {
+      QrApplyDesc q{};
+      q.V = (const double*)std::get<0>(d); q.ldv = std::get<1>(d); q.T = (const double*)std::get<2>(d); q.ldt = std::get<3>(d);
+      q.A1 = (double*)std::get<4>(d); q.lda1 = std::get<5>(d); q.A2 = (double*)std::get<6>(d); q.lda2 = std::get<7>(d);
+      q.m2 = std::get<8>(d); q.n = std::get<9>(d); q.ncols = std::get<10>(d);
+      v.push_back(q);
+    }
+    return parsec_amd_qr_apply(v.data(), (int)v.size(), (void*)ws, (void*)stream);
+  });
+  m.def("kernel_qr_apply_ws", [](int count, int n, int ncols) {
+    std::vector<QrApplyDesc> v(count);
+    for (auto& q : v) { q.n = n; q.ncols = ncols; }
+    return parsec_amd_qr_apply_ws(v.data(), count);
+  });
   m.def("kernel_dpotrf", [](uintptr_t A, int n, int lda, uintptr_t info, uintptr_t stream) { return parsec_amd_dpotrf_tile((double*)A, n, lda, (int*)info, (void*)stream); });
   m.def("kernel_dpotrf_w", [](uintptr_t A, int n, int lda, uintptr_t info, uintptr_t W, int ldw, uintptr_t stream, bool pack) {
     return parsec_amd_dpotrf_tile_w((double*)A, n, lda, (int*)info, (double*)W, ldw, (void*)stream, pack ? 1 : 0);
