@@ -270,12 +270,14 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
   };
   auto load_tile = [&](int k0) { load_tile_to(k0, ra, rb); };
   // Operands loaded as k-pairs (op(A) = A^T, op(B) = B): LDS holds them
-  // m- / n-major with k contiguous, rows of BK + 2 doubles inside the same
-  // buffer, so a pair is one 16-byte store (eight lanes of a store group write
-  // one 128-byte row: no bank conflict) and the MFMA fragment reads of 16
-  // consecutive rows land on distinct banks (36 r mod 64 for r < 16, the k + 1
-  // lanes 2 banks over). The k-major layout made those stores 8-way conflicts.
-  constexpr int KS = BK + 2;
+  // m- / n-major with k contiguous, rows of BK + 1 doubles inside the same
+  // buffer. The fragment reads (ds_read2_b64: 16-lane groups, banks mod 32)
+  // of 16 consecutive rows then start 34 r mod 32 = 2 r banks apart, and the
+  // two 8-byte stores of a pair (ds_write_b64, 16-lane groups) hit 2 kk + 34 m
+  // mod 32: both conflict-free. The k-major layout made the stores 8-way
+  // conflicts; even rows (BK + 2, one 16-byte store) still left the reads
+  // 2-way (SQ_LDS_BANK_CONFLICT 40 % of the TN kernels' LDS cycles).
+  constexpr int KS = BK + 1;
   // (tile shapes whose k-contiguous rows would not fit the buffer keep the k-major layout)
   constexpr bool KA = TRANSA && BM * KS <= BK * (BM + (((BM % 32) == 16) ? 0 : 16));
   constexpr bool KB = !TRANSB && BN * KS <= BK * (BN + (((BN % 32) == 16) ? 0 : 16));
@@ -287,7 +289,8 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
       int idx = tid + NT * e;
       if (KA) {
         int kk = (idx % (BK / 2)) * 2, mm = idx / (BK / 2);
-        *reinterpret_cast<double2_t*>(a_km(buf) + mm * KS + kk) = ra[e];
+        a_km(buf)[mm * KS + kk] = ra[e].x;
+        a_km(buf)[mm * KS + kk + 1] = ra[e].y;
       } else if (TRANSA) {
         int kk = (idx % (BK / 2)) * 2, mm = idx / (BK / 2);
         As[buf][kk][mm] = ra[e].x;
@@ -305,7 +308,8 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
         *reinterpret_cast<double2_t*>(&Bs[buf][kk][nn]) = rb[e];
       } else if (KB) {
         int kk = (idx % (BK / 2)) * 2, nn = idx / (BK / 2);
-        *reinterpret_cast<double2_t*>(b_km(buf) + nn * KS + kk) = rb[e];
+        b_km(buf)[nn * KS + kk] = rb[e].x;
+        b_km(buf)[nn * KS + kk + 1] = rb[e].y;
       } else {
         int kk = (idx % (BK / 2)) * 2, nn = idx / (BK / 2);
         Bs[buf][kk][nn] = rb[e].x;
