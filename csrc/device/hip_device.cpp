@@ -1445,6 +1445,52 @@ void HipDevice::dispatch_critical_now() {
   for (GpuTask* g : rest) ready.push_back(g);
 }
 
+// One task of a retired group: epilogue, then completion (or the push-out copy).
+void HipDevice::retire_task(GpuTask* g, hipEvent_t grp_ev) {
+  if (g->early) {
+    late_complete(g, grp_ev);
+    return;
+  }
+  epilog(g);
+  const Chore& gch = g->task->task_class->chores[g->chore];
+  if (gch.stage_in || gch.stage_out)  // custom layouts go home through the chore, right after the task
+    for (int fi = 0; fi < kMaxFlows; ++fi)
+      if (g->dev_copy[fi] && (g->access[fi] & FLOW_WRITE)) g->pushout |= 1u << fi;
+  if (g->pushout) {
+    GpuStageContext octx;
+    for (int fi = 0; fi < kMaxFlows; ++fi) {
+      if (!(g->pushout & (1u << fi)) || !g->dev_copy[fi]) continue;
+      Data* d = g->dev_copy[fi]->original;
+      DataCopy* host = d->copy(0);
+      if (!host) { host = data_pull_to_host(d); continue; }
+      if (gch.stage_out) {
+        octx.flow_mask |= 1u << fi;
+        octx.src[fi] = g->dev_copy[fi];
+        octx.dst[fi] = host;
+        octx.dc[fi] = fi < (int)gch.flow_dc.size() && gch.flow_dc[fi] ? gch.flow_dc[fi](g->task) : d->dc;
+        octx.bytes[fi] = fi < (int)gch.flow_size.size() && gch.flow_size[fi] ? gch.flow_size[fi](g->task) : d->nb_elts;
+        stats.bytes_out.fetch_add(octx.bytes[fi], std::memory_order_relaxed);
+        continue;
+      }
+      hipEvent_t sb = copy_span_begin();
+      PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, g->dev_copy[fi]->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_copy));
+      copy_span_end(sb, trace_key_out, d->nb_elts, device_index, 0);
+      stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
+    }
+    if (octx.flow_mask) {
+      octx.task = g->task;
+      octx.stream = s_copy;
+      octx.device_index = device_index;
+      if (gch.stage_out(octx) != 0) fatal("%s: user stage_out failed", g->task->task_class->name.c_str());
+    }
+    g->ev_out = get_event();
+    PARSEC_HIP_CHECK(hipEventRecord(g->ev_out, s_copy));
+    popping.push_back(g);
+  } else {
+    complete(g);
+  }
+}
+
 bool HipDevice::progress() {
   bool did = false;
   if (incoming_n.load(std::memory_order_acquire) > 0) {
@@ -1546,53 +1592,17 @@ bool HipDevice::progress() {
         std::stable_partition(tasks.begin(), tasks.end(), [&](GpuTask* g) { return !g->early && !g->pushout && g->task->priority >= critical_threshold; });
       }
       bool crit_done = !(s == 0 && critical_release);
-      for (GpuTask* g : tasks) {
+      for (size_t ti = 0; ti < tasks.size(); ++ti) {
+        GpuTask* g = tasks[ti];
         if (!crit_done && (g->early || g->pushout || g->task->priority < critical_threshold)) {
           crit_done = true;
           dispatch_critical_now();
         }
-        if (g->early) {
-          late_complete(g, grp_ev);
+        if (s > 0 && retire_slice > 0 && !g->early) {  // bulk: complete in slices (below)
+          retiring.push_back(g);
           continue;
         }
-        epilog(g);
-        const Chore& gch = g->task->task_class->chores[g->chore];
-        if (gch.stage_in || gch.stage_out)  // custom layouts go home through the chore, right after the task
-          for (int fi = 0; fi < kMaxFlows; ++fi)
-            if (g->dev_copy[fi] && (g->access[fi] & FLOW_WRITE)) g->pushout |= 1u << fi;
-        if (g->pushout) {
-          GpuStageContext octx;
-          for (int fi = 0; fi < kMaxFlows; ++fi) {
-            if (!(g->pushout & (1u << fi)) || !g->dev_copy[fi]) continue;
-            Data* d = g->dev_copy[fi]->original;
-            DataCopy* host = d->copy(0);
-            if (!host) { host = data_pull_to_host(d); continue; }
-            if (gch.stage_out) {
-              octx.flow_mask |= 1u << fi;
-              octx.src[fi] = g->dev_copy[fi];
-              octx.dst[fi] = host;
-              octx.dc[fi] = fi < (int)gch.flow_dc.size() && gch.flow_dc[fi] ? gch.flow_dc[fi](g->task) : d->dc;
-              octx.bytes[fi] = fi < (int)gch.flow_size.size() && gch.flow_size[fi] ? gch.flow_size[fi](g->task) : d->nb_elts;
-              stats.bytes_out.fetch_add(octx.bytes[fi], std::memory_order_relaxed);
-              continue;
-            }
-            hipEvent_t sb = copy_span_begin();
-            PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, g->dev_copy[fi]->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_copy));
-            copy_span_end(sb, trace_key_out, d->nb_elts, device_index, 0);
-            stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
-          }
-          if (octx.flow_mask) {
-            octx.task = g->task;
-            octx.stream = s_copy;
-            octx.device_index = device_index;
-            if (gch.stage_out(octx) != 0) fatal("%s: user stage_out failed", g->task->task_class->name.c_str());
-          }
-          g->ev_out = get_event();
-          PARSEC_HIP_CHECK(hipEventRecord(g->ev_out, s_copy));
-          popping.push_back(g);
-        } else {
-          complete(g);
-        }
+        retire_task(g, grp_ev);
       }
       put_event(grp_ev);  // after late_complete cleared the copies that named it
       if (trace_launches)
@@ -1605,6 +1615,15 @@ bool HipDevice::progress() {
       if (s == 0 && (critical_split || critical_first)) break;
     }
     if (s == 0 && retired && (critical_split || critical_first)) break;
+  }
+  if (!retiring.empty()) {
+    for (int i = 0; i < retire_slice && !retiring.empty(); ++i) {
+      GpuTask* g = retiring.front();
+      retiring.pop_front();
+      retire_task(g, nullptr);
+    }
+    did = true;
+    retired = true;
   }
   if (retired) {
     const uint64_t dt = now_ns() - tc0;
@@ -1700,6 +1719,7 @@ void hip_devices_init(Context* ctx) {
   const int ccap = (int)params.reg_int("device", "hip", "critical_bulk_cap", "Launched kernel groups per bulk stream while the critical stream has work in flight (0 = max_inflight_batches)", 0);
   const int cuy = (int)params.reg_int("device", "hip", "cu_yield", "Cooperative CU yield: critical-path kernels claim their CUs and bulk GEMM workgroups on a claimed CU pause until it is free (0 off, 1 tile-POTRF steps claim, 2 every kernel of a critical group claims)", 0);
   const bool csplit = params.reg_int("device", "hip", "critical_split", "Critical-path tasks leave the critical stream as a group of their own and their successors are dispatched before other completions are released", 0) != 0;
+  const int rslice = (int)params.reg_int("device", "hip", "retire_slice", "Tasks of a retired bulk group completed per progress pass (0 = the whole group at once): a critical group's completion is then noticed between slices", 0);
   const bool crel = params.reg_int("device", "hip", "critical_release", "A retired critical-stream group completes its critical-path tasks first and launches their critical successors before releasing its other tasks' successors", 0) != 0;
   const bool cfirst = params.reg_int("device", "hip", "critical_first", "A retired critical-stream group's successors are dispatched before the bulk streams' completions are released (the groups themselves are not split)", 0) != 0;
   const int early = (int)params.reg_int("device", "hip", "early_release", "Critical-stream groups release their tasks' successors when launched (1) or when their kernels completed (0); single-process runs", 0);
@@ -1747,6 +1767,7 @@ void hip_devices_init(Context* ctx) {
     d->critical_split = csplit;
     d->critical_first = cfirst;
     d->critical_release = crel;
+    d->retire_slice = rslice;
     d->early_release = early;
     d->cu_yield = cuy;
     kern::set_cu_yield_mode(cuy);

@@ -144,6 +144,11 @@ struct HipDevice : Device {
   std::vector<GpuTask*> pending, staging, ready;
   std::vector<std::deque<ExecGroup>> executing;
   std::deque<GpuTask*> popping;
+  // retire_slice > 0: tasks of retired bulk groups still to complete (at most
+  // retire_slice per progress pass, so a critical group's completion is noticed
+  // between slices)
+  std::deque<GpuTask*> retiring;
+  int retire_slice = 0;
   std::vector<hipEvent_t> event_pool;
   std::vector<KernelBatch> batches;
   std::vector<std::vector<GpuTask*>> round_tasks;
@@ -217,6 +222,7 @@ struct HipDevice : Device {
   bool critical_split = false;
   bool critical_first = false;
   bool critical_release = false;
+  void retire_task(GpuTask* g, hipEvent_t grp_ev);
   // device_hip_early_release: groups of the critical stream complete their
   // tasks (release successors) when launched, not when their event fires
   int early_release = 0;
