@@ -157,7 +157,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 // k-tile's MFMA work instead of in front of it, and the epilogue forms
 // alpha AB + beta C from registers (a pure store). Needs the register budget of
 // two waves per SIMD (launched with one workgroup per CU).
-template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF, int PF, int EPI, bool DL = false>
+template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF, int PF, int EPI, bool DL = false, bool INPL = false>
 __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, int ks, int nsplit, double (&As)[NBUF][BK][BM + (((BM % 32) == 16) ? 0 : 16)],
                                           double (&Bs)[NBUF][BK][BN + (((BN % 32) == 16) ? 0 : 16)]) {
   static_assert(PF == 1 || NBUF == 2, "two tiles in flight need the double-buffered LDS");
@@ -171,7 +171,7 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
   const int local = tile - args.tile_start[di];
   const int mt = (d.m + BM - 1) / BM;
   const int nt = (d.n + BN - 1) / BN;
-  const int tm = local % mt, tn = d.inplace ? nt - 1 - local / mt : local / mt;
+  const int tm = local % mt, tn = (INPL && d.inplace) ? nt - 1 - local / mt : local / mt;
   const int m0 = tm * BM, n0 = tn * BN;
   if (d.lower_only && n0 > m0 + BM - 1) return;
   if (d.gate) {
@@ -474,7 +474,7 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
   // blockIdx: dispatched earlier, so waiting on them cannot deadlock) read it;
   // write only after all of them finished. The wait is bounded: a lost
   // signal degrades to a wrong result a test catches, never to a hung GPU.
-  unsigned* const rsync = d.inplace ? reinterpret_cast<unsigned*>(d.C2) + tm : nullptr;
+  unsigned* const rsync = (INPL && d.inplace) ? reinterpret_cast<unsigned*>(d.C2) + tm : nullptr;
   if (rsync) {
     if (tid == 0) {
       const unsigned want = (unsigned)(nt - 1 - tn);
@@ -518,7 +518,7 @@ __device__ __forceinline__ void gemm_tile(const GemmBatchArgs& args, int tile, i
   crit_release(args.claim);
 }
 
-template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF = 2, int OCC = WM * WN / 2, int PF = 1, int EPI = 0, bool DL = false>
+template <int BM, int BN, int BK, int WM, int WN, bool TRANSA, bool TRANSB, bool FULL, int NBUF = 2, int OCC = WM * WN / 2, int PF = 1, int EPI = 0, bool DL = false, bool INPL = false>
 __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OCC))) void dgemm_batch_kernel(const GemmBatchArgs args) {
   constexpr int PADM = ((BM % 32) == 16) ? 0 : 16;
   constexpr int PADN = ((BN % 32) == 16) ? 0 : 16;
@@ -547,8 +547,8 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
       ks = 1;
     }
   } else if ((int)blockIdx.x < args.main_tiles) {
-    // stagger < 0: tiles in dispatch order (in-place descriptors wait on lower blockIdx)
-    tile = args.stagger < 0 ? (int)blockIdx.x : xcd_remap(blockIdx.x, args.main_tiles);
+    // INPL: tiles in dispatch order (in-place descriptors wait on lower blockIdx)
+    tile = INPL ? (int)blockIdx.x : xcd_remap(blockIdx.x, args.main_tiles);
   } else {
     const int u = blockIdx.x - args.main_tiles;
     nsplit = args.ksplit;
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(OC
     ks = u % nsplit;
   }
   if (tile >= args.total_tiles) return;
-  gemm_tile<BM, BN, BK, WM, WN, TRANSA, TRANSB, FULL, NBUF, PF, EPI, DL>(args, tile, ks, nsplit, As, Bs);
+  gemm_tile<BM, BN, BK, WM, WN, TRANSA, TRANSB, FULL, NBUF, PF, EPI, DL, INPL>(args, tile, ks, nsplit, As, Bs);
 }
 
 // Persistent form: a grid of (at most) one round of resident workgroups walks
@@ -1014,6 +1014,13 @@ static void launch_gemm_shape(GemmBatchArgs& a, const GemmDesc* descs, int n, hi
     if (epi) PARSEC_GEMM_LAUNCH_E(TA, TB, 1);                                                                       \
     else PARSEC_GEMM_LAUNCH_E(TA, TB, 0);                                                                           \
   } while (0)
+  if (ordered) {
+    // in-place panel solve (launch_trsm_w_batch): NT descriptors, plain epilogue
+    if (mode != 1 || epi || late) fatal("in-place GEMM launch: NT descriptors with the plain epilogue only");
+    if (full) hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, false, true, true, NBUF, OCC, PF, 0, false, true>), grid, block, pad, stream, a);
+    else hipLaunchKernelGGL((dgemm_batch_kernel<BM, BN, BK, WM, WN, false, true, false, NBUF, OCC, PF, 0, false, true>), grid, block, pad, stream, a);
+    return;
+  }
   switch (mode) {
     case 0: PARSEC_GEMM_LAUNCH(false, false); break;
     case 1: PARSEC_GEMM_LAUNCH(false, true); break;
