@@ -27,6 +27,7 @@
 #define MEM_HANDLE_FROM_1_TAG 6
 #define GET_END_ACK_TAG 7
 #define PUT_END_ACK_TAG 8
+#define LATE_TAG 9 /* registered on rank 0 only after rank 1's messages arrived */
 #define N 4096 /* ints per buffer: 16 KB, several ring fragments at most */
 
 static volatile int counter = 0;
@@ -189,6 +190,21 @@ static void wait_for(int n) {
     while (counter < n) parsec_ce.progress(&parsec_ce);
 }
 
+/* messages on a tag registered late: delivered once it is, in send order */
+static int late_next = 0;
+static int late_am(parsec_comm_engine_t* ce, parsec_ce_tag_t tag, void* msg, size_t size, int src, void* cb_data) {
+    (void)ce; (void)tag; (void)cb_data;
+    int v;
+    memcpy(&v, msg, sizeof(v));
+    if (size != sizeof(int) || src != 1 || v != late_next) {
+        printf("[%d] late message %d from %d, expected %d\n", my_rank, v, src, late_next);
+        bad++;
+    }
+    late_next++;
+    counter++;
+    return 1;
+}
+
 int main(int argc, char** argv) {
     use_gpu = argc > 1 && strcmp(argv[1], "gpu") == 0;
     parsec_comm_engine_t* ce = parsec_comm_engine_init(NULL);
@@ -263,6 +279,22 @@ int main(int argc, char** argv) {
         counter = 0;
         ce->sync(ce);
     }
+
+    /* a tag rank 0 registers only after rank 1's messages on it arrived (an MPI
+     * unexpected-message queue: kept in order, not dropped) */
+    if (my_rank == 1)
+        for (int i = 0; i < 5; i++) ce->send_am(ce, LATE_TAG, 0, &i, sizeof(i));
+    ce->sync(ce); /* rank 1's messages precede its barrier message on the same ring */
+    if (my_rank == 0) {
+        ce->tag_register(LATE_TAG, late_am, ce, 64);
+        for (long spins = 0; counter < 5 && spins < 200000000L; spins++) parsec_ce.progress(&parsec_ce);
+        if (counter != 5) {
+            printf("[0] %d of 5 late-tag messages delivered\n", counter);
+            bad++;
+        }
+    }
+    counter = 0;
+    ce->sync(ce);
 
     /* pack / unpack: the lower triangle of a 4 x 4 column-major matrix */
     {

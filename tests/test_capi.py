@@ -137,7 +137,9 @@ def _build_ce(tmp_path, gpu=False):
 def test_comm_engine_c_program(tmp_path, pa):
     """The communication-engine vtable from C (port of the reference's
     tests/dsl/dtd/dtd_test_ce.c): active messages both ways, a GET and a PUT on
-    registered host memory with AM completion notices, pack / unpack."""
+    registered host memory with AM completion notices, pack / unpack, and five
+    messages on a tag rank 0 registers only after they arrived (kept in order
+    by the engine's unexpected-message queue, not dropped)."""
     exe = _build_ce(tmp_path)
     rc, outs = launch.launch(2, [exe], timeout=120, capture=True)
     assert rc == 0, outs
