@@ -57,6 +57,15 @@ def test_distributed_dpotrf_jdf(pa, nranks, P, Q, mode):
         assert rc == 0, out
 
 
+@pytest.mark.parametrize("nranks,pad", [(2, 0), (3, 1)])
+def test_distributed_diag_band_to_rect(pa, nranks, pad):
+    """diag_band_to_rect.jdf with the band on a P x 1 grid and the target row on
+    a 1 x Q grid: the source tiles travel to the target tiles' owners."""
+    outs = run_ranks(nranks, 6, 5, pad, worker=os.path.join(HERE, "mp", "dist_band.py"))
+    for rc, out in outs:
+        assert rc == 0 and "band ok" in out, out
+
+
 @pytest.mark.parametrize("aggregate", ["1", "0"])
 def test_distributed_backpressure_aggregation(pa, aggregate):
     """Tiny shared-memory rings and a slow receiver (comm_shm_debug_delay_us)
