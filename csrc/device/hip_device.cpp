@@ -341,6 +341,13 @@ void HipDevice::start(Context* c) {
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
   s_copy = gpu_copy_stream(ordinal);
   if (!s_copy) fatal("hip%d: cannot create the copy stream", ordinal);
+  s_copy_out = s_copy;
+  if (copy_out_stream) {
+    // a queue of its own for device-to-host traffic (out-of-core runs): with
+    // the default 4 hardware queues it shares one with another stream, so give
+    // the process GPU_MAX_HW_QUEUES >= 5 when using it
+    PARSEC_HIP_CHECK(hipStreamCreateWithFlags(&s_copy_out, hipStreamNonBlocking));
+  }
   const int total_streams = std::max(1, nb_exec_streams);
   s_exec.assign(total_streams, nullptr);
   // Stream 0 carries the critical path at high priority. A critical kernel that
@@ -417,6 +424,8 @@ void HipDevice::shutdown() {
   stream_infos.clear();  // per-stream objects die before their streams
   for (auto s : s_exec) (void)hipStreamDestroy(s);
   s_exec.clear();
+  if (s_copy_out && s_copy_out != s_copy) (void)hipStreamDestroy(s_copy_out);
+  s_copy_out = nullptr;
   s_copy = nullptr;  // the process-wide copy stream outlives the engine
   // drop cached copies
   for (List* l : {&lru_clean, &lru_owned}) {
@@ -478,17 +487,17 @@ void HipDevice::trace_group(int s, const ExecGroup& g) {
   profiling_trace_at(trace_streams[s], trace_key_e, id, tp, trace_ref_ns + (uint64_t)((double)e * 1e6), nullptr, 0);
 }
 
-hipEvent_t HipDevice::copy_span_begin() {
+hipEvent_t HipDevice::copy_span_begin(hipStream_t st) {
   if (!gpu_trace) return nullptr;
   hipEvent_t b = get_timing_event();
-  PARSEC_HIP_CHECK(hipEventRecord(b, s_copy));
+  PARSEC_HIP_CHECK(hipEventRecord(b, st ? st : s_copy));
   return b;
 }
 
-void HipDevice::copy_span_end(hipEvent_t b, int key, uint64_t bytes, int src_dev, int dst_dev) {
+void HipDevice::copy_span_end(hipEvent_t b, int key, uint64_t bytes, int src_dev, int dst_dev, hipStream_t st) {
   if (!b) return;
   hipEvent_t e = get_timing_event();
-  PARSEC_HIP_CHECK(hipEventRecord(e, s_copy));
+  PARSEC_HIP_CHECK(hipEventRecord(e, st ? st : s_copy));
   copy_spans.push_back(CopySpan{b, e, key, bytes, src_dev, dst_dev});
 }
 
@@ -685,9 +694,9 @@ bool HipDevice::start_w2r(size_t bytes) {
     lru_remove(c);
     st->w2r = true;
     c->readers.fetch_add(1);  // pinned: not dropped while the copy is in flight
-    hipEvent_t sb = copy_span_begin();
-    PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, c->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_copy));
-    copy_span_end(sb, trace_key_out, d->nb_elts, device_index, 0);
+    hipEvent_t sb = copy_span_begin(s_copy_out);
+    PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, c->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_copy_out));
+    copy_span_end(sb, trace_key_out, d->nb_elts, device_index, 0, s_copy_out);
     stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
     job.copies.push_back(c);
     job.versions.push_back(c->version);
@@ -697,7 +706,7 @@ bool HipDevice::start_w2r(size_t bytes) {
   }
   if (job.copies.empty()) return false;
   job.ev = get_event();
-  PARSEC_HIP_CHECK(hipEventRecord(job.ev, s_copy));
+  PARSEC_HIP_CHECK(hipEventRecord(job.ev, s_copy_out));
   w2r_bytes_inflight += queued;
   stats.w2r_tasks.fetch_add(1, std::memory_order_relaxed);
   w2r_jobs.push_back(std::move(job));
@@ -1463,6 +1472,10 @@ void HipDevice::retire_task(GpuTask* g, hipEvent_t grp_ev) {
       Data* d = g->dev_copy[fi]->original;
       DataCopy* host = d->copy(0);
       if (!host) { host = data_pull_to_host(d); continue; }
+      if (copy_out_stream) {  // the buffer must not be reused before its D2H ran (no stream order with stage-ins)
+        g->dev_copy[fi]->readers.fetch_add(1);
+        g->out_pinned |= 1u << fi;
+      }
       if (gch.stage_out) {
         octx.flow_mask |= 1u << fi;
         octx.src[fi] = g->dev_copy[fi];
@@ -1472,19 +1485,19 @@ void HipDevice::retire_task(GpuTask* g, hipEvent_t grp_ev) {
         stats.bytes_out.fetch_add(octx.bytes[fi], std::memory_order_relaxed);
         continue;
       }
-      hipEvent_t sb = copy_span_begin();
-      PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, g->dev_copy[fi]->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_copy));
-      copy_span_end(sb, trace_key_out, d->nb_elts, device_index, 0);
+      hipEvent_t sb = copy_span_begin(s_copy_out);
+      PARSEC_HIP_CHECK(hipMemcpyAsync(host->device_private, g->dev_copy[fi]->device_private, d->nb_elts, hipMemcpyDeviceToHost, s_copy_out));
+      copy_span_end(sb, trace_key_out, d->nb_elts, device_index, 0, s_copy_out);
       stats.bytes_out.fetch_add(d->nb_elts, std::memory_order_relaxed);
     }
     if (octx.flow_mask) {
       octx.task = g->task;
-      octx.stream = s_copy;
+      octx.stream = s_copy_out;
       octx.device_index = device_index;
       if (gch.stage_out(octx) != 0) fatal("%s: user stage_out failed", g->task->task_class->name.c_str());
     }
     g->ev_out = get_event();
-    PARSEC_HIP_CHECK(hipEventRecord(g->ev_out, s_copy));
+    PARSEC_HIP_CHECK(hipEventRecord(g->ev_out, s_copy_out));
     popping.push_back(g);
   } else {
     complete(g);
@@ -1640,6 +1653,12 @@ bool HipDevice::progress() {
       std::lock_guard<SpinLock> lk(d->lock);
       if (DataCopy* host = d->copy(0)) { host->version = g->dev_copy[fi]->version; host->coherency_state = COHERENCY_SHARED; }
     }
+    for (int fi = 0; fi < kMaxFlows; ++fi)
+      if ((g->out_pinned & (1u << fi)) && g->dev_copy[fi]) {
+        g->dev_copy[fi]->readers.fetch_sub(1);
+        lru_touch(g->dev_copy[fi]);
+      }
+    g->out_pinned = 0;
     complete(g);
     did = true;
   }
@@ -1684,6 +1703,7 @@ void HipDevice::manager_main() {
   }
   if (!copy_spans.empty()) {
     (void)hipStreamSynchronize(s_copy);
+    if (s_copy_out && s_copy_out != s_copy) (void)hipStreamSynchronize(s_copy_out);
     progress_copy_spans();
   }
   profiling_thread_fini(es);
@@ -1719,6 +1739,7 @@ void hip_devices_init(Context* ctx) {
   const int ccap = (int)params.reg_int("device", "hip", "critical_bulk_cap", "Launched kernel groups per bulk stream while the critical stream has work in flight (0 = max_inflight_batches)", 0);
   const int cuy = (int)params.reg_int("device", "hip", "cu_yield", "Cooperative CU yield: critical-path kernels claim their CUs and bulk GEMM workgroups on a claimed CU pause until it is free (0 off, 1 tile-POTRF steps claim, 2 every kernel of a critical group claims)", 0);
   const bool csplit = params.reg_int("device", "hip", "critical_split", "Critical-path tasks leave the critical stream as a group of their own and their successors are dispatched before other completions are released", 0) != 0;
+  const bool cout = params.reg_int("device", "hip", "copy_out_stream", "Device-to-host write-back and W2R on a copy stream of their own (1) or on the one copy stream (0); with 1 give the process GPU_MAX_HW_QUEUES >= 5", 0) != 0;
   const int rslice = (int)params.reg_int("device", "hip", "retire_slice", "Tasks of a retired bulk group completed per progress pass (0 = the whole group at once): a critical group's completion is then noticed between slices", 0);
   const bool crel = params.reg_int("device", "hip", "critical_release", "A retired critical-stream group completes its critical-path tasks first and launches their critical successors before releasing its other tasks' successors", 0) != 0;
   const bool cfirst = params.reg_int("device", "hip", "critical_first", "A retired critical-stream group's successors are dispatched before the bulk streams' completions are released (the groups themselves are not split)", 0) != 0;
@@ -1768,6 +1789,7 @@ void hip_devices_init(Context* ctx) {
     d->critical_first = cfirst;
     d->critical_release = crel;
     d->retire_slice = rslice;
+    d->copy_out_stream = cout;
     d->early_release = early;
     d->cu_yield = cuy;
     kern::set_cu_yield_mode(cuy);

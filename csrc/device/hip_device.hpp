@@ -56,6 +56,7 @@ struct GpuTask {
   int kind = GPU_TASK_KERNEL;
   uint32_t flows = 0;        // data flows handled by the engine
   uint32_t pushout = 0;      // flows copied back to the host after execution
+  uint32_t out_pinned = 0;   // of those, device copies held (readers) until the write-back completed (separate D2H stream)
   uint8_t access[kMaxFlows] = {};
   DataCopy* dev_copy[kMaxFlows] = {};
   bool issued_copy[kMaxFlows] = {};
@@ -114,6 +115,10 @@ struct HipDevice : Device {
   hipDeviceProp_t props{};
   int nb_exec_streams = 3;
   hipStream_t s_copy = nullptr;  // gpu_copy_stream(ordinal): stage-in, write-back, prefetch
+  // device-to-host write-back / W2R: s_copy, or a stream of its own with
+  // device_hip_copy_out_stream (H2D and D2H on separate copy queues)
+  hipStream_t s_copy_out = nullptr;
+  bool copy_out_stream = false;
   std::vector<hipStream_t> s_exec;
   std::vector<std::unique_ptr<InfoArray>> stream_infos;  // one per s_exec stream (gpu_stream_infos())
   std::unique_ptr<ZoneAllocator> zone;
@@ -211,8 +216,8 @@ struct HipDevice : Device {
   std::deque<CopySpan> copy_spans;
   int trace_key_in = -1, trace_key_in_e = -1, trace_key_out = -1, trace_key_out_e = -1, trace_key_pf = -1, trace_key_pf_e = -1;
   struct ProfilingStream* trace_copy_stream = nullptr;
-  hipEvent_t copy_span_begin();                                        // nullptr when not tracing
-  void copy_span_end(hipEvent_t b, int key, uint64_t bytes, int src_dev, int dst_dev);
+  hipEvent_t copy_span_begin(hipStream_t st = nullptr);                // nullptr when not tracing
+  void copy_span_end(hipEvent_t b, int key, uint64_t bytes, int src_dev, int dst_dev, hipStream_t st = nullptr);
   void progress_copy_spans();
   bool roctx = true;  // roctx ranges around every launched group (rocprofv3 --marker-trace)
   uint32_t rr_stream = 0;
